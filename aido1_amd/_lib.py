@@ -1,0 +1,135 @@
+"""ctypes binding of libdtsim.so (include/dtsim.h) and its in-tree build.
+
+The product path has exactly one implementation — the gfx950 kernels in
+aido1_amd/csrc.  If the library is missing it is built in-tree with hipcc (the
+same command as __graft_entry__.build()); if that fails, or no gfx950 device
+is present when a handle is created, this module raises.  There is no CPU
+fallback.
+"""
+import ctypes
+import os
+import subprocess
+import threading
+
+from aido1_amd.config import DtConfig
+
+PKG_DIR = os.path.dirname(os.path.abspath(__file__))
+REPO_DIR = os.path.dirname(PKG_DIR)
+LIB_PATH = os.path.join(PKG_DIR, 'libdtsim.so')
+CSRC = os.path.join(PKG_DIR, 'csrc')
+SOURCES = ['dtsim.hip', 'dtrender.hip']
+HEADERS = ['dtsim_common.h', 'dtrender.h']
+HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
+ABI_VERSION = 1
+
+HIP_FLAGS = ['--offload-arch=gfx950', '-O3', '-fPIC', '-shared', '-std=c++17',
+             '-ffp-contract=off', '-munsafe-fp-atomics']
+
+
+class DtError(RuntimeError):
+    pass
+
+
+class DtMap(ctypes.Structure):
+    _fields_ = [('width', ctypes.c_int32), ('height', ctypes.c_int32),
+                ('kind', ctypes.c_void_p), ('curves', ctypes.c_void_p),
+                ('headings', ctypes.c_void_p)]
+
+
+def _sources():
+    return [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
+
+
+def _stale():
+    if not os.path.exists(LIB_PATH):
+        return True
+    t = os.path.getmtime(LIB_PATH)
+    deps = _sources() + [os.path.join(CSRC, h) for h in HEADERS] + \
+        [os.path.join(REPO_DIR, 'include', 'dtsim.h')]
+    return any(os.path.exists(d) and os.path.getmtime(d) > t for d in deps)
+
+
+def build(force=False, verbose=False):
+    """Compile libdtsim.so for gfx950 in-tree."""
+    if not force and not _stale():
+        return LIB_PATH
+    tmp = LIB_PATH + '.tmp%d' % os.getpid()
+    cmd = [HIPCC] + HIP_FLAGS + ['-o', tmp] + _sources()
+    if verbose:
+        print(' '.join(cmd))
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise DtError('hipcc failed building libdtsim.so:\n' + r.stderr[-4000:])
+    os.replace(tmp, LIB_PATH)
+    return LIB_PATH
+
+
+# symbols whose kernels are still being brought up
+_OPTIONAL = {'dt_render'}
+
+_lib = None
+_lock = threading.Lock()
+
+
+def lib():
+    """Load (building first if needed) libdtsim.so; raises DtError if impossible."""
+    global _lib
+    with _lock:
+        if _lib is not None:
+            return _lib
+        # torch (if importable) must own the HIP runtime first: both it and this
+        # library NEED libamdhip64.so.7, and loading torch first makes the
+        # dynamic linker bind ours to torch's copy (one runtime per process).
+        try:
+            import torch  # noqa: F401
+        except ImportError:
+            pass
+        if _stale():
+            build()
+        L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        vp, i32, u32, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64
+        sig = {
+            'dt_abi_version': (i32, []),
+            'dt_create': (ctypes.c_int, [ctypes.POINTER(DtConfig), ctypes.POINTER(DtMap), u64, i32,
+                                         i32, ctypes.POINTER(vp)]),
+            'dt_destroy': (ctypes.c_int, [vp]),
+            'dt_n_envs': (i32, [vp]),
+            'dt_last_error': (ctypes.c_char_p, [vp]),
+            'dt_seed': (ctypes.c_int, [vp, vp, u64, u32]),
+            'dt_reset': (ctypes.c_int, [vp, vp, vp]),
+            'dt_step': (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+            'dt_lane_pos': (ctypes.c_int, [vp, vp, vp, vp]),
+            'dt_render': (ctypes.c_int, [vp, vp, vp, vp, vp]),
+            'dt_get_state': (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp]),
+            'dt_set_state': (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp]),
+            'dt_check': (ctypes.c_int, [vp, ctypes.POINTER(u32)]),
+            'dt_stats': (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), i32]),
+        }
+        for name, (res, args) in sig.items():
+            if not hasattr(L, name):
+                if name in _OPTIONAL:
+                    continue
+                raise DtError('libdtsim.so lacks %s (stale build?)' % name)
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        v = L.dt_abi_version()
+        if v != ABI_VERSION:
+            raise DtError('libdtsim ABI %d != expected %d (rebuild)' % (v, ABI_VERSION))
+        _lib = L
+        return L
+
+
+def exported_symbols():
+    """Names declared in include/dtsim.h (checked against the .so by tests)."""
+    import re
+    with open(os.path.join(REPO_DIR, 'include', 'dtsim.h')) as f:
+        src = f.read()
+    return sorted(set(re.findall(r'^\s*(?:int|int32_t|const char\*)\s+(dt_\w+)\s*\(', src,
+                                 re.M)))
+
+
+def check(L, handle, rc, what):
+    if rc != 0:
+        msg = L.dt_last_error(handle)
+        raise DtError('%s failed (%d): %s' % (what, rc, msg.decode() if msg else ''))

@@ -1,0 +1,534 @@
+// libdtsim: MI355X-native batched Duckietown environment — step/reset kernels
+// and the C ABI declared in include/dtsim.h.
+//
+// One wavefront lane per environment; 64-thread workgroups (one wave each) so
+// a 4096-env batch spreads over 64 CUs instead of piling onto 16; the map's
+// tile kinds, Bezier control points and headings are staged in LDS per block;
+// pose state is float64 SoA in HBM (coalesced 8-B lanes); done/reset masks are
+// wave ballots; resets are wave-cooperative rejection sampling (see
+// dtsim_common.h wave_spawn).
+#include <math.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <string>
+#include <vector>
+
+#include "dtsim_common.h"
+
+struct StepCfg {
+  int32_t repeat, frame_skip, action_mode, clip, speed_measured, auto_reset;
+  uint32_t max_steps, max_env_steps, max_spawn_attempts;
+  double reward_scale;
+};
+
+struct dt_handle {
+  int device = 0;
+  int n = 0;
+  dt_config cfg{};
+  dt::Geo geo{};
+  StepCfg sc{};
+  dt::MapDev map{};
+  void* map_buf = nullptr;
+  dt::State st{};
+  void* st_buf = nullptr;
+  size_t lds_bytes = 0;
+  uint32_t env_base = 0;
+  std::string err;
+};
+
+static std::string g_create_err;
+
+namespace {
+
+using dt::MapLds;
+
+__device__ inline void map_action(int mode, float a0, float a1, double& vl, double& vr) {
+  if (mode == DT_ACTION_TANH) {
+    // utils/env_wrappers.py:214-216: in-place float32 `action /= 2; action += 0.5`
+    a0 = a0 / 2.0f;
+    a0 = a0 + 0.5f;
+    a1 = a1 / 2.0f;
+    a1 = a1 + 0.5f;
+    vl = (double)a0;
+    vr = (double)a1;
+  } else if (mode == DT_ACTION_STEERING) {
+    // duckietown_rl/wrappers.py:138-161 then ActionWrapper :99-101 (left wheel x0.8)
+    const double vel = (double)a0, ang = (double)a1;
+    const double kinv_r = (1.0 + 0.0) / 27.0, kinv_l = (1.0 - 0.0) / 27.0;
+    const double om_r = (vel + 0.5 * ang * 0.102) / 0.0318;
+    const double om_l = (vel - 0.5 * ang * 0.102) / 0.0318;
+    double ur = om_r * kinv_r, ul = om_l * kinv_l;
+    ur = ur < 1.0 ? ur : 1.0;
+    ur = ur > -1.0 ? ur : -1.0;
+    ul = ul < 1.0 ? ul : 1.0;
+    ul = ul > -1.0 ? ul : -1.0;
+    vl = ul * 0.8;
+    vr = ur;
+  } else {
+    vl = (double)a0;
+    vr = (double)a1;
+  }
+}
+
+// EnvironmentWrapper.step (utils/env_wrappers.py:213-253) x repeat Simulator.step.
+__global__ __launch_bounds__(64) void step_kernel(dt::State st, dt::MapDev md, dt::Geo g,
+                                                  StepCfg sc, int n, uint32_t env_base,
+                                                  const float2* __restrict__ act,
+                                                  double* __restrict__ rew,
+                                                  double* __restrict__ rewm,
+                                                  uint8_t* __restrict__ done_out,
+                                                  float2* __restrict__ obs,
+                                                  double* __restrict__ lanepos,
+                                                  int32_t* __restrict__ tile_out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const MapLds M = dt::stage_map(md, lds);
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = e < n;
+  const int ei = active ? e : 0;
+
+  double x = st.x[ei], z = st.z[ei], ang = st.angle[ei];
+  uint32_t step_count = st.step_count[ei], env_step = st.env_step[ei];
+  const float2 a = act[ei];
+
+  double vl, vr;
+  map_action(sc.action_mode, a.x, a.y, vl, vr);
+  if (sc.clip) {  // Simulator.step: np.clip(action, -1, 1)
+    vl = vl < -1.0 ? -1.0 : (vl > 1.0 ? 1.0 : vl);
+    vr = vr < -1.0 ? -1.0 : (vr > 1.0 ? 1.0 : vr);
+  }
+  const double wl = vl * g.robot_speed * 1.0, wr = vr * g.robot_speed * 1.0;
+  const bool straight = (wl == wr);
+  double w_rot = 0.0, r_icc = 0.0, rot = 0.0, cr = 1.0, sr = 0.0;
+  if (!straight) {  // _update_pos terms that do not depend on the pose (A4)
+    const double l = g.wheel_dist;
+    w_rot = (wr - wl) / l;
+    r_icc = (l * (wl + wr)) / (2.0 * (wl - wr));
+    rot = w_rot * g.dt;
+    sincos(rot, &sr, &cr);
+  }
+  const double kstraight = g.dt * wl;
+
+  double tr = 0.0, trm = 0.0;
+  bool dn = !active;
+  unsigned nsim = 0;
+  double c = 0.0, s = 0.0;
+  sincos(ang, &s, &c);
+  for (int rep = 0; rep < sc.repeat; ++rep) {
+    if (!dn) {
+      double speed = 0.0;
+      for (int f = 0; f < sc.frame_skip; ++f) {
+        const double ox = x, oz = z;
+        if (straight) {
+          x = x + kstraight * c;
+          z = z + kstraight * (-s);
+        } else {
+          const double cx = x + r_icc * s;
+          const double cz = z + r_icc * c;
+          const double ddx = x - cx, ddz = z - cz;
+          const double ndx = ddx * cr + ddz * sr;
+          const double ndz = ddz * cr - ddx * sr;
+          x = cx + ndx;
+          z = cz + ndz;
+          ang = ang + rot;
+          sincos(ang, &s, &c);
+        }
+        step_count += 1u;
+        nsim += 1u;
+        if (sc.speed_measured) {
+          const double a1 = x - ox, a3 = z - oz;
+          speed = sqrt((a1 * a1 + 0.0 * 0.0) + a3 * a3) / g.dt;
+        }
+      }
+      // _compute_done_reward (A11)
+      double r;
+      bool sd = false;
+      if (!dt::valid_pose(M, g, x, z, c, s, 1.0)) {
+        r = -1000.0;
+        sd = true;
+      } else if (step_count >= sc.max_steps) {
+        r = 0.0;
+        sd = true;
+      } else {
+        double lp[4];
+        const double sp = sc.speed_measured ? speed : g.robot_speed;
+        if (dt::lane_pos(M, g, x, z, c, s, lp)) {
+          const double ad = fabs(lp[0]);
+          r = ((1.0 * sp) * lp[1] + (-10.0) * ad) + 40.0 * 0.0;
+        } else {
+          r = 40.0 * 0.0;
+        }
+      }
+      // BaselineAggregationFunction (aggregation_functions.py:25-32)
+      const double rm = (r == -1000.0) ? -10.0 : (r > 0.0 ? r + 10.0 : r + 4.0);
+      tr = tr + r;
+      trm = trm + rm;
+      env_step += 1u;
+      dn = sd || env_step > sc.max_env_steps;
+    }
+  }
+  trm = trm * sc.reward_scale;
+
+  double lp[4];
+  bool inl = active && dt::lane_pos(M, g, x, z, c, s, lp);
+  if (active) {
+    rew[e] = tr;
+    rewm[e] = trm;
+    done_out[e] = (uint8_t)dn;
+    if (lanepos) {
+      const double nan = __longlong_as_double(0x7ff8000000000000LL);
+      double* o = lanepos + 4 * (size_t)e;
+      o[0] = inl ? lp[0] : nan;
+      o[1] = inl ? lp[1] : nan;
+      o[2] = inl ? lp[2] : nan;
+      o[3] = inl ? lp[3] : nan;
+    }
+    if (tile_out) tile_out[e] = dt::tile_of(M, g, x, z);
+  }
+
+  dt::wave_add(st.stats + 0, nsim);
+  dt::wave_add(st.stats + 1, active ? 1u : 0u);
+  dt::wave_add(st.stats + 3, (active && dn) ? 1u : 0u);
+  uint32_t episode = st.episode[ei];
+  if (sc.auto_reset) {
+    const bool need = active && dn;
+    if (__ballot(need)) {  // wave-uniform
+      bool failed = false;
+      double nx = x, nz = z, na = ang;
+      dt::wave_spawn(M, g, sc.max_spawn_attempts, need, env_base + (uint32_t)e, st.seed[ei],
+                     episode, nx, nz, na, failed);
+      dt::wave_add(st.stats + 2, (need && !failed) ? 1u : 0u);
+      if (need) {
+        if (failed) {
+          atomicOr(st.err, dt::kErrSpawn);
+        } else {
+          x = nx;
+          z = nz;
+          ang = na;
+          step_count = 0u;
+          env_step = 0u;
+          episode += 1u;
+          sincos(ang, &s, &c);
+          inl = dt::lane_pos(M, g, x, z, c, s, lp);
+        }
+      }
+    }
+  }
+  if (active) {
+    if (obs) obs[e] = inl ? make_float2((float)lp[0], (float)lp[3]) : make_float2(0.0f, 0.0f);
+    st.x[e] = x;
+    st.z[e] = z;
+    st.angle[e] = ang;
+    st.step_count[e] = step_count;
+    st.env_step[e] = env_step;
+    st.episode[e] = episode;
+  }
+}
+
+// Simulator.reset + EnvironmentWrapper.reset counters for masked envs (A13).
+__global__ __launch_bounds__(64) void reset_kernel(dt::State st, dt::MapDev md, dt::Geo g,
+                                                   uint32_t max_attempts, int n, uint32_t env_base,
+                                                   const uint8_t* __restrict__ mask) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const MapLds M = dt::stage_map(md, lds);
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const bool active = e < n;
+  const int ei = active ? e : 0;
+  const bool need = active && (mask == nullptr || mask[e] != 0);
+  if (!__ballot(need)) return;  // wave-uniform exit
+  double x = st.x[ei], z = st.z[ei], ang = st.angle[ei];
+  const uint32_t episode = st.episode[ei];
+  bool failed = false;
+  dt::wave_spawn(M, g, max_attempts, need, env_base + (uint32_t)e, st.seed[ei], episode, x, z, ang,
+                 failed);
+  dt::wave_add(st.stats + 2, (need && !failed) ? 1u : 0u);
+  if (need) {
+    if (failed) {
+      atomicOr(st.err, dt::kErrSpawn);
+    } else {
+      st.x[e] = x;
+      st.z[e] = z;
+      st.angle[e] = ang;
+      st.step_count[e] = 0u;
+      st.env_step[e] = 0u;
+      st.episode[e] = episode + 1u;
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void lane_pos_kernel(dt::State st, dt::MapDev md, dt::Geo g,
+                                                      int n, double* __restrict__ lanepos,
+                                                      int32_t* __restrict__ tile_out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const MapLds M = dt::stage_map(md, lds);
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n) return;
+  const double x = st.x[e], z = st.z[e], ang = st.angle[e];
+  double s, c;
+  sincos(ang, &s, &c);
+  double lp[4];
+  const bool inl = dt::lane_pos(M, g, x, z, c, s, lp);
+  const double nan = __longlong_as_double(0x7ff8000000000000LL);
+  if (lanepos) {
+    for (int q = 0; q < 4; ++q) lanepos[4 * (size_t)e + q] = inl ? lp[q] : nan;
+  }
+  if (tile_out) tile_out[e] = dt::tile_of(M, g, x, z);
+}
+
+#define HIP_OR_FAIL(h, expr)                                                   \
+  do {                                                                         \
+    hipError_t _e = (expr);                                                    \
+    if (_e != hipSuccess) {                                                    \
+      (h)->err = std::string(#expr) + ": " + hipGetErrorString(_e);             \
+      return DT_E_HIP;                                                         \
+    }                                                                          \
+  } while (0)
+
+int grid_of(int n) { return (n + dt::kWave - 1) / dt::kWave; }
+
+}  // namespace
+
+extern "C" {
+
+int32_t dt_abi_version(void) { return DT_ABI_VERSION; }
+
+int32_t dt_n_envs(const dt_handle* h) { return h ? h->n : -1; }
+
+const char* dt_last_error(const dt_handle* h) {
+  return h ? h->err.c_str() : g_create_err.c_str();
+}
+
+int dt_create(const dt_config* cfg, const dt_map* map, uint64_t seed, int32_t n_envs,
+              int32_t device, dt_handle** out) {
+  g_create_err.clear();
+  if (!cfg || !map || !out || n_envs <= 0 || !map->kind || !map->curves || !map->headings ||
+      map->width <= 0 || map->height <= 0) {
+    g_create_err = "dt_create: bad argument";
+    return DT_E_ARG;
+  }
+  const int T = map->width * map->height;
+  if (T > dt::kMaxLdsTiles) {
+    g_create_err = "dt_create: map larger than the LDS staging limit (256 tiles)";
+    return DT_E_ARG;
+  }
+  if (cfg->repeat_actions < 1 || cfg->frame_skip < 1 || cfg->road_tile_size <= 0) {
+    g_create_err = "dt_create: bad config";
+    return DT_E_ARG;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) {
+    g_create_err = "dt_create: no HIP device " + std::to_string(device);
+    return DT_E_NODEV;
+  }
+  hipDeviceProp_t prop;
+  if (hipGetDeviceProperties(&prop, device) != hipSuccess) {
+    g_create_err = "dt_create: hipGetDeviceProperties failed";
+    return DT_E_NODEV;
+  }
+  if (strncmp(prop.gcnArchName, "gfx950", 6) != 0) {
+    g_create_err = std::string("dt_create: device is ") + prop.gcnArchName + ", need gfx950";
+    return DT_E_NODEV;
+  }
+  std::vector<int16_t> drv;
+  for (int t = 0; t < T; ++t)
+    if (map->kind[t] > 0) drv.push_back((int16_t)t);
+  if (drv.empty()) {
+    g_create_err = "dt_create: map has no drivable tile";
+    return DT_E_ARG;
+  }
+
+  dt_handle* h = new dt_handle();
+  h->device = device;
+  h->n = n_envs;
+  h->cfg = *cfg;
+  dt::Geo& g = h->geo;
+  g.ts = cfg->road_tile_size;
+  g.wheel_dist = cfg->wheel_dist;
+  g.dt = cfg->delta_time;
+  g.off = cfg->camera_forward_dist - (cfg->robot_length / 2);
+  g.robot_width = cfg->robot_width;
+  g.front = cfg->front_probe_length ? cfg->robot_length : cfg->robot_width;
+  g.rad2deg = cfg->rad2deg;
+  g.two_pi = cfg->two_pi;
+  g.accept_deg = cfg->accept_start_angle_deg;
+  g.reset_safety = cfg->reset_safety;
+  g.robot_speed = cfg->robot_speed;
+  StepCfg& sc = h->sc;
+  sc.repeat = cfg->repeat_actions;
+  sc.frame_skip = cfg->frame_skip;
+  sc.action_mode = cfg->action_mode;
+  sc.clip = cfg->clip_action;
+  sc.speed_measured = cfg->reward_speed_measured;
+  sc.auto_reset = cfg->auto_reset;
+  sc.max_steps = cfg->max_steps;
+  sc.max_env_steps = cfg->max_env_steps;
+  sc.max_spawn_attempts = cfg->max_spawn_attempts;
+  sc.reward_scale = cfg->reward_scale;
+
+  int rc = 0;
+  auto fail = [&](const std::string& m) {
+    g_create_err = m;
+    if (h->map_buf) (void)hipFree(h->map_buf);
+    if (h->st_buf) (void)hipFree(h->st_buf);
+    delete h;
+    return DT_E_HIP;
+  };
+  if (hipSetDevice(device) != hipSuccess) return fail("hipSetDevice failed");
+  // map image: curves | headings | kind | drivable
+  const size_t cb = (size_t)T * 24 * 8, hb = (size_t)T * 6 * 8, kb = ((size_t)T + 15) & ~15ul,
+               db = (drv.size() * 2 + 15) & ~15ul;
+  if (hipMalloc(&h->map_buf, cb + hb + kb + db) != hipSuccess) return fail("hipMalloc(map)");
+  char* mb = (char*)h->map_buf;
+  if (hipMemcpy(mb, map->curves, cb, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(mb + cb, map->headings, hb, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(mb + cb + hb, map->kind, (size_t)T, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(mb + cb + hb + kb, drv.data(), drv.size() * 2, hipMemcpyHostToDevice) !=
+          hipSuccess)
+    return fail("hipMemcpy(map)");
+  h->map.width = map->width;
+  h->map.height = map->height;
+  h->map.n_tiles = T;
+  h->map.n_drivable = (int)drv.size();
+  h->map.curves = (const double*)mb;
+  h->map.headings = (const double*)(mb + cb);
+  h->map.kind = (const int8_t*)(mb + cb + hb);
+  h->map.drivable = (const int16_t*)(mb + cb + hb + kb);
+  h->lds_bytes = dt::map_lds_bytes(T, (int)drv.size());
+
+  // state: x z angle seed (8 B) | step_count env_step episode (4 B) | err
+  const size_t N = (size_t)n_envs, N8 = N * 8, N4 = (N * 4 + 255) & ~255ul;
+  const size_t total = 4 * N8 + 3 * N4 + 256 + 256;
+  if (hipMalloc(&h->st_buf, total) != hipSuccess) return fail("hipMalloc(state)");
+  if (hipMemset(h->st_buf, 0, total) != hipSuccess) return fail("hipMemset(state)");
+  char* sb = (char*)h->st_buf;
+  h->st.x = (double*)sb;
+  h->st.z = (double*)(sb + N8);
+  h->st.angle = (double*)(sb + 2 * N8);
+  h->st.seed = (uint64_t*)(sb + 3 * N8);
+  h->st.step_count = (uint32_t*)(sb + 4 * N8);
+  h->st.env_step = (uint32_t*)(sb + 4 * N8 + N4);
+  h->st.episode = (uint32_t*)(sb + 4 * N8 + 2 * N4);
+  h->st.err = (uint32_t*)(sb + 4 * N8 + 3 * N4);
+  h->st.stats = (unsigned long long*)(sb + 4 * N8 + 3 * N4 + 256);
+  *out = h;
+  rc = dt_seed(h, nullptr, seed, 0);
+  if (rc) {
+    std::string m = h->err;
+    dt_destroy(h);
+    *out = nullptr;
+    g_create_err = m;
+    return rc;
+  }
+  return DT_OK;
+}
+
+int dt_destroy(dt_handle* h) {
+  if (!h) return DT_E_ARG;
+  (void)hipSetDevice(h->device);
+  if (h->map_buf) (void)hipFree(h->map_buf);
+  if (h->st_buf) (void)hipFree(h->st_buf);
+  delete h;
+  return DT_OK;
+}
+
+int dt_seed(dt_handle* h, const uint64_t* seeds, uint64_t base, uint32_t env_id_base) {
+  if (!h) return DT_E_ARG;
+  h->env_base = env_id_base;
+  HIP_OR_FAIL(h, hipSetDevice(h->device));
+  std::vector<uint64_t> s(h->n);
+  for (int i = 0; i < h->n; ++i) s[i] = seeds ? seeds[i] : base;
+  HIP_OR_FAIL(h, hipMemcpy(h->st.seed, s.data(), s.size() * 8, hipMemcpyHostToDevice));
+  HIP_OR_FAIL(h, hipMemset(h->st.episode, 0, (size_t)h->n * 4));
+  return DT_OK;
+}
+
+int dt_reset(dt_handle* h, const uint8_t* mask, void* stream) {
+  if (!h) return DT_E_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(reset_kernel, dim3(grid_of(h->n)), dim3(dt::kWave), h->lds_bytes, s, h->st,
+                     h->map, h->geo, h->sc.max_spawn_attempts, h->n, h->env_base, mask);
+  HIP_OR_FAIL(h, hipGetLastError());
+  return DT_OK;
+}
+
+int dt_step(dt_handle* h, const float* actions, double* reward, double* reward_mod,
+            uint8_t* done, float* obs, double* lanepos, int32_t* tile, void* stream) {
+  if (!h) return DT_E_ARG;
+  if (!actions || !reward || !reward_mod || !done) {
+    h->err = "dt_step: actions, reward, reward_mod and done are required";
+    return DT_E_ARG;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(step_kernel, dim3(grid_of(h->n)), dim3(dt::kWave), h->lds_bytes, s, h->st,
+                     h->map, h->geo, h->sc, h->n, h->env_base, (const float2*)actions, reward, reward_mod,
+                     done, (float2*)obs, lanepos, tile);
+  HIP_OR_FAIL(h, hipGetLastError());
+  return DT_OK;
+}
+
+int dt_lane_pos(dt_handle* h, double* lanepos, int32_t* tile, void* stream) {
+  if (!h) return DT_E_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(lane_pos_kernel, dim3(grid_of(h->n)), dim3(dt::kWave), h->lds_bytes, s,
+                     h->st, h->map, h->geo, h->n, lanepos, tile);
+  HIP_OR_FAIL(h, hipGetLastError());
+  return DT_OK;
+}
+
+int dt_get_state(dt_handle* h, double* x, double* z, double* angle, uint32_t* step_count,
+                 uint32_t* env_step, uint32_t* episode) {
+  if (!h) return DT_E_ARG;
+  HIP_OR_FAIL(h, hipSetDevice(h->device));
+  HIP_OR_FAIL(h, hipDeviceSynchronize());
+  const size_t N = (size_t)h->n;
+  if (x) HIP_OR_FAIL(h, hipMemcpy(x, h->st.x, N * 8, hipMemcpyDeviceToHost));
+  if (z) HIP_OR_FAIL(h, hipMemcpy(z, h->st.z, N * 8, hipMemcpyDeviceToHost));
+  if (angle) HIP_OR_FAIL(h, hipMemcpy(angle, h->st.angle, N * 8, hipMemcpyDeviceToHost));
+  if (step_count)
+    HIP_OR_FAIL(h, hipMemcpy(step_count, h->st.step_count, N * 4, hipMemcpyDeviceToHost));
+  if (env_step) HIP_OR_FAIL(h, hipMemcpy(env_step, h->st.env_step, N * 4, hipMemcpyDeviceToHost));
+  if (episode) HIP_OR_FAIL(h, hipMemcpy(episode, h->st.episode, N * 4, hipMemcpyDeviceToHost));
+  return DT_OK;
+}
+
+int dt_set_state(dt_handle* h, const double* x, const double* z, const double* angle,
+                 const uint32_t* step_count, const uint32_t* env_step, const uint32_t* episode) {
+  if (!h) return DT_E_ARG;
+  HIP_OR_FAIL(h, hipSetDevice(h->device));
+  HIP_OR_FAIL(h, hipDeviceSynchronize());
+  const size_t N = (size_t)h->n;
+  if (x) HIP_OR_FAIL(h, hipMemcpy(h->st.x, x, N * 8, hipMemcpyHostToDevice));
+  if (z) HIP_OR_FAIL(h, hipMemcpy(h->st.z, z, N * 8, hipMemcpyHostToDevice));
+  if (angle) HIP_OR_FAIL(h, hipMemcpy(h->st.angle, angle, N * 8, hipMemcpyHostToDevice));
+  if (step_count)
+    HIP_OR_FAIL(h, hipMemcpy(h->st.step_count, step_count, N * 4, hipMemcpyHostToDevice));
+  if (env_step) HIP_OR_FAIL(h, hipMemcpy(h->st.env_step, env_step, N * 4, hipMemcpyHostToDevice));
+  if (episode) HIP_OR_FAIL(h, hipMemcpy(h->st.episode, episode, N * 4, hipMemcpyHostToDevice));
+  return DT_OK;
+}
+
+int dt_stats(dt_handle* h, uint64_t out[4], int32_t reset) {
+  if (!h || !out) return DT_E_ARG;
+  HIP_OR_FAIL(h, hipSetDevice(h->device));
+  HIP_OR_FAIL(h, hipDeviceSynchronize());
+  HIP_OR_FAIL(h, hipMemcpy(out, h->st.stats, 32, hipMemcpyDeviceToHost));
+  if (reset) HIP_OR_FAIL(h, hipMemset(h->st.stats, 0, 32));
+  return DT_OK;
+}
+
+int dt_check(dt_handle* h, uint32_t* flags) {
+  if (!h) return DT_E_ARG;
+  HIP_OR_FAIL(h, hipSetDevice(h->device));
+  HIP_OR_FAIL(h, hipDeviceSynchronize());
+  uint32_t f = 0;
+  HIP_OR_FAIL(h, hipMemcpy(&f, h->st.err, 4, hipMemcpyDeviceToHost));
+  HIP_OR_FAIL(h, hipMemset(h->st.err, 0, 4));
+  if (flags) *flags = f;
+  if (f & dt::kErrSpawn) {
+    h->err = "reset: could not find a valid starting pose after max_spawn_attempts";
+    return DT_E_SPAWN;
+  }
+  return DT_OK;
+}
+
+}  // extern "C"

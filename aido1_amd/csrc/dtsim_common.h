@@ -1,0 +1,334 @@
+// Shared device-side definitions of libdtsim: handle layout, map staging, the
+// Philox stream, and the float64 Simulator step math (one wavefront lane per
+// environment).  gfx950 only.
+//
+// Float semantics: every kernel TU is compiled with -ffp-contract=off (and the
+// pragma below) so no multiply-add is fused.  The reference (numpy float64)
+// never fuses, and the spec demands <=1e-5 on pose/reward and bit-exact
+// tile/done; keeping numpy's rounding sequence makes the GPU agree with the
+// CPU oracle to the last ulp except where libm and ocml transcendentals differ.
+#pragma once
+#pragma clang fp contract(off)
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "../../include/dtsim.h"
+
+namespace dt {
+
+constexpr int kWave = 64;
+constexpr int kMaxTiles = 1024;  // LDS staging: 24+6 doubles + 1 kind byte per tile (<= 246 KB
+                                 // worst case is over budget; dt_create enforces kMaxLdsTiles)
+constexpr int kMaxLdsTiles = 256;
+
+constexpr uint32_t kTagTile = 0x54494C45u;    // 'TILE'
+constexpr uint32_t kTagSpawnA = 0x53504E41u;  // 'SPNA'
+constexpr uint32_t kTagSpawnB = 0x53504E42u;  // 'SPNB'
+
+constexpr uint32_t kErrSpawn = 1u;   // a reset exhausted max_spawn_attempts
+constexpr uint32_t kErrNonFinite = 2u;
+
+// SoA environment state, all device pointers (one allocation).
+struct State {
+  double* x;
+  double* z;
+  double* angle;
+  uint64_t* seed;
+  uint32_t* step_count;
+  uint32_t* env_step;
+  uint32_t* episode;
+  uint32_t* err;  // one word, OR of kErr*
+  unsigned long long* stats;  // [4] sim steps, decisions, resets, episodes done
+};
+
+// One atomic per wave: lane-sum through the 64-wide reduction, lane 0 adds.
+__device__ inline void wave_add(unsigned long long* p, unsigned v) {
+  unsigned long long s = v;
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  if ((threadIdx.x & 63) == 0 && s) atomicAdd(p, s);
+}
+
+// Map image in device memory; staged into LDS by each block.
+struct MapDev {
+  int32_t width, height, n_tiles, n_drivable;
+  const double* curves;     // [T,2,4,3]
+  const double* headings;   // [T,2,3]
+  const int8_t* kind;       // [T]
+  const int16_t* drivable;  // [n_drivable] tile index of the k-th drivable tile (load order)
+};
+
+// LDS view of the map.
+struct MapLds {
+  const double* curves;
+  const double* headings;
+  const int8_t* kind;
+  const int16_t* drivable;
+  int32_t width, height, n_drivable;
+};
+
+__host__ __device__ inline size_t map_lds_bytes(int n_tiles, int n_drivable) {
+  size_t b = (size_t)n_tiles * (24 + 6) * sizeof(double);
+  b += ((size_t)n_tiles + 15) & ~(size_t)15;
+  b += ((size_t)n_drivable * 2 + 15) & ~(size_t)15;
+  return b;
+}
+
+// Cooperative copy of the map into LDS; every thread of the block calls it.
+__device__ inline MapLds stage_map(const MapDev& m, unsigned char* lds) {
+  double* cv = reinterpret_cast<double*>(lds);
+  double* hd = cv + (size_t)m.n_tiles * 24;
+  int8_t* kd = reinterpret_cast<int8_t*>(hd + (size_t)m.n_tiles * 6);
+  int16_t* dv = reinterpret_cast<int16_t*>(kd + (((size_t)m.n_tiles + 15) & ~(size_t)15));
+  const int tid = threadIdx.x, nt = blockDim.x;
+  for (int i = tid; i < m.n_tiles * 24; i += nt) cv[i] = m.curves[i];
+  for (int i = tid; i < m.n_tiles * 6; i += nt) hd[i] = m.headings[i];
+  for (int i = tid; i < m.n_tiles; i += nt) kd[i] = m.kind[i];
+  for (int i = tid; i < m.n_drivable; i += nt) dv[i] = m.drivable[i];
+  __syncthreads();
+  MapLds r;
+  r.curves = cv;
+  r.headings = hd;
+  r.kind = kd;
+  r.drivable = dv;
+  r.width = m.width;
+  r.height = m.height;
+  r.n_drivable = m.n_drivable;
+  return r;
+}
+
+// ---- Philox4x32-10 ----------------------------------------------------------
+struct U4 {
+  uint32_t a, b, c, d;
+};
+
+__device__ inline U4 philox(uint32_t c0, uint32_t c1, uint32_t c2, uint32_t c3, uint32_t k0,
+                            uint32_t k1) {
+#pragma unroll
+  for (int r = 0; r < 10; ++r) {
+    if (r) {
+      k0 += 0x9E3779B9u;
+      k1 += 0xBB67AE85u;
+    }
+    const uint32_t lo0 = 0xD2511F53u * c0, hi0 = __umulhi(0xD2511F53u, c0);
+    const uint32_t lo1 = 0xCD9E8D57u * c2, hi1 = __umulhi(0xCD9E8D57u, c2);
+    const uint32_t n0 = hi1 ^ c1 ^ k0, n2 = hi0 ^ c3 ^ k1;
+    c0 = n0;
+    c1 = lo1;
+    c2 = n2;
+    c3 = lo0;
+  }
+  return U4{c0, c1, c2, c3};
+}
+
+__device__ inline double u01(uint32_t a, uint32_t b) {
+  return (double)(((((uint64_t)a) << 32) | b) >> 11) * (1.0 / 9007199254740992.0);
+}
+
+// ---- wave helpers -------------------------------------------------------------
+__device__ inline uint32_t bcast(uint32_t v, int lane) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, lane);
+}
+__device__ inline double bcast(double v, int lane) {
+  const uint64_t u = __double_as_longlong(v);
+  const uint32_t lo = bcast((uint32_t)u, lane), hi = bcast((uint32_t)(u >> 32), lane);
+  return __longlong_as_double((long long)(((uint64_t)hi << 32) | lo));
+}
+__device__ inline uint64_t bcast(uint64_t v, int lane) {
+  const uint32_t lo = bcast((uint32_t)v, lane), hi = bcast((uint32_t)(v >> 32), lane);
+  return ((uint64_t)hi << 32) | lo;
+}
+
+// ---- Simulator math -----------------------------------
+struct Geo {  // constants hoisted per launch
+  double ts, wheel_dist, dt, off, robot_width, front, rad2deg, two_pi, accept_deg, reset_safety;
+  double robot_speed;
+};
+
+// get_grid_coords + _get_tile: tile index or -1 (A5)
+__device__ inline int tile_of(const MapLds& M, const Geo& g, double x, double z) {
+  const double fi = floor(x / g.ts), fj = floor(z / g.ts);
+  if (fi < 0.0 || fj < 0.0 || fi >= (double)M.width || fj >= (double)M.height) return -1;
+  return (int)fj * M.width + (int)fi;
+}
+
+__device__ inline bool drivable(const MapLds& M, const Geo& g, double x, double z) {
+  const int t = tile_of(M, g, x, z);
+  return t >= 0 && M.kind[t] > 0;
+}
+
+// _valid_pose with precomputed (c, s) = (cos, sin)(angle) (A6)
+__device__ inline bool valid_pose(const MapLds& M, const Geo& g, double x, double z, double c,
+                                  double s, double safety) {
+  const double px = x + g.off * c;
+  const double pz = z + g.off * (-s);
+  const double kw = (safety * 0.5) * g.robot_width;
+  const double kf = (safety * 0.5) * g.front;
+  bool ok = drivable(M, g, px, pz);
+  ok = ok && drivable(M, g, px - kw * s, pz - kw * c);
+  ok = ok && drivable(M, g, px + kw * s, pz + kw * c);
+  ok = ok && drivable(M, g, px + kf * c, pz + kf * (-s));
+  return ok;
+}
+
+// bezier_point (A9): coefficients are exact dyadics for the bisection's t values
+__device__ inline void bez_xz(const double* __restrict__ cp, double t, double& ox, double& oy,
+                              double& oz) {
+  const double u = 1.0 - t;
+  const double c0 = u * u * u, c1 = 3.0 * t * (u * u), c2 = 3.0 * (t * t) * u, c3 = t * t * t;
+  double px = c0 * cp[0], py = c0 * cp[1], pz = c0 * cp[2];
+  px = px + c1 * cp[3];
+  py = py + c1 * cp[4];
+  pz = pz + c1 * cp[5];
+  px = px + c2 * cp[6];
+  py = py + c2 * cp[7];
+  pz = pz + c2 * cp[8];
+  px = px + c3 * cp[9];
+  py = py + c3 * cp[10];
+  pz = pz + c3 * cp[11];
+  ox = px;
+  oy = py;
+  oz = pz;
+}
+
+__device__ inline double dist_to(const double* __restrict__ cp, double t, double x, double z) {
+  double bx, by, bz;
+  bez_xz(cp, t, bx, by, bz);
+  const double a = bx - x, b = by - 0.0, c = bz - z;
+  return sqrt((a * a + b * b) + c * c);
+}
+
+// get_lane_pos2 (A8-A10).  Returns false when NotInLane.
+// lp = {dist, dot_dir, angle_deg, angle_rad}
+__device__ inline bool lane_pos(const MapLds& M, const Geo& g, double x, double z, double c,
+                                double s, double lp[4]) {
+  const int t = tile_of(M, g, x, z);
+  if (t < 0 || M.kind[t] <= 0) return false;
+  const double dx = c, dz = -s;
+  const double* hd = M.headings + t * 6;
+  const double d0 = (hd[0] * dx + hd[1] * 0.0) + hd[2] * dz;
+  const double d1 = (hd[3] * dx + hd[4] * 0.0) + hd[5] * dz;
+  const double* cp = M.curves + t * 24 + ((d1 > d0) ? 12 : 0);
+  // bezier_closest, 8 levels.  One endpoint distance is carried between levels:
+  // the kept half's end was evaluated at the same t one level earlier, and the
+  // function is deterministic, so the result is bit-identical to re-evaluating.
+  double tb = 0.0, tt = 1.0;
+  double db = dist_to(cp, tb, x, z), dtp = dist_to(cp, tt, x, z);
+#pragma unroll
+  for (int n = 8; n > 0; --n) {
+    const double mid = (tb + tt) * 0.5;
+    if (db < dtp) {
+      tt = mid;
+      if (n > 1) dtp = dist_to(cp, tt, x, z);
+    } else {
+      tb = mid;
+      if (n > 1) db = dist_to(cp, tb, x, z);
+    }
+  }
+  const double tm = (tb + tt) * 0.5;
+  double qx, qy, qz;
+  bez_xz(cp, tm, qx, qy, qz);
+  const double u = 1.0 - tm;
+  const double a0 = 3.0 * (u * u), a1 = 6.0 * u * tm, a2 = 3.0 * (tm * tm);
+  double tx = a0 * (cp[3] - cp[0]), ty = a0 * (cp[4] - cp[1]), tz = a0 * (cp[5] - cp[2]);
+  tx = tx + a1 * (cp[6] - cp[3]);
+  ty = ty + a1 * (cp[7] - cp[4]);
+  tz = tz + a1 * (cp[8] - cp[5]);
+  tx = tx + a2 * (cp[9] - cp[6]);
+  ty = ty + a2 * (cp[10] - cp[7]);
+  tz = tz + a2 * (cp[11] - cp[8]);
+  const double nn = sqrt((tx * tx + ty * ty) + tz * tz);
+  tx = tx / nn;
+  ty = ty / nn;
+  tz = tz / nn;
+  double dot = (dx * tx + 0.0 * ty) + dz * tz;
+  dot = dot > 1.0 ? 1.0 : dot;
+  dot = dot < -1.0 ? -1.0 : dot;
+  const double rx = 0.0 - tz, rz = tx;
+  const double px = x - qx, pz = z - qz;
+  const double dist = (px * rx + (0.0 - qy) * 0.0) + pz * rz;
+  double ang = acos(dot);
+  if ((dx * rx + 0.0) + dz * rz < 0.0) ang = -ang;
+  lp[0] = dist;
+  lp[1] = dot;
+  lp[2] = ang * g.rad2deg;
+  lp[3] = ang;
+  return true;
+}
+
+// One spawn proposal (A13): returns true if accepted.
+__device__ inline bool spawn_try(const MapLds& M, const Geo& g, uint32_t k0, uint32_t k1,
+                                 uint32_t env, uint32_t episode, uint32_t k, double fi,
+                                 double fj, double& ox, double& oz, double& oa) {
+  const U4 a = philox(k, episode, env, kTagSpawnA, k0, k1);
+  const U4 b = philox(k, episode, env, kTagSpawnB, k0, k1);
+  const double px = (fi + u01(a.a, a.b)) * g.ts;
+  const double pz = (fj + u01(a.c, a.d)) * g.ts;
+  const double pa = g.two_pi * u01(b.a, b.b);
+  double s, c;
+  sincos(pa, &s, &c);
+  ox = px;
+  oz = pz;
+  oa = pa;
+  if (!valid_pose(M, g, px, pz, c, s, g.reset_safety)) return false;
+  double lp[4];
+  if (!lane_pos(M, g, px, pz, c, s, lp)) return false;
+  return -g.accept_deg < lp[2] && lp[2] < g.accept_deg;
+}
+
+// Wave-cooperative Simulator.reset for every lane whose `need` is set.
+// For env e the 64 lanes test proposals k = 64*round + lane in parallel; the
+// lowest accepting lane of the first round with any acceptance wins, which is
+// exactly the first accepted k of a sequential rejection loop over the same
+// i.i.d. stream — so the spawn distribution is upstream's and the result is
+// bit-reproducible by the sequential CPU oracle.
+// All 64 lanes of the wave must call this (uniform control flow).
+__device__ inline void wave_spawn(const MapLds& M, const Geo& g, uint32_t max_attempts,
+                                  bool need, uint32_t env, uint64_t seed, uint32_t episode,
+                                  double& x, double& z, double& ang, bool& failed) {
+  const int lane = threadIdx.x & 63;
+  uint64_t pending = __ballot(need);
+  failed = false;
+  while (pending) {
+    const int owner = __ffsll((unsigned long long)pending) - 1;
+    pending &= pending - 1;
+    const uint32_t e = bcast(env, owner);
+    const uint64_t sd = bcast(seed, owner);
+    const uint32_t ep = bcast(episode, owner);
+    const uint32_t k0 = (uint32_t)sd, k1 = (uint32_t)(sd >> 32);
+    const U4 tw = philox(0u, ep, e, kTagTile, k0, k1);
+    int pick = (int)(u01(tw.a, tw.b) * (double)M.n_drivable);
+    pick = pick > M.n_drivable - 1 ? M.n_drivable - 1 : pick;
+    const int ti = M.drivable[pick];
+    const double fi = (double)(ti % M.width), fj = (double)(ti / M.width);
+    bool got = false;
+    double wx = 0, wz = 0, wa = 0;
+    for (uint32_t base = 0; base < max_attempts; base += kWave) {
+      const uint32_t k = base + (uint32_t)lane;
+      double px, pz, pa;
+      const bool ok = (k < max_attempts) &&
+                      spawn_try(M, g, k0, k1, e, ep, k, fi, fj, px, pz, pa);
+      const uint64_t acc = __ballot(ok);
+      if (acc) {
+        const int w = __ffsll((unsigned long long)acc) - 1;
+        wx = bcast(px, w);
+        wz = bcast(pz, w);
+        wa = bcast(pa, w);
+        got = true;
+        break;
+      }
+    }
+    if (lane == owner) {
+      if (got) {
+        x = wx;
+        z = wz;
+        ang = wa;
+      } else {
+        failed = true;
+      }
+    }
+  }
+}
+
+}  // namespace dt

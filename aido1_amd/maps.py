@@ -1,0 +1,120 @@
+"""Tile maps -> the C ABI's ``dt_map`` arrays.
+
+Follows upstream Simulator._load_map / _get_curve (un-vendored gym-duckietown,
+aido1 era): tiles "kind/orient" are drivable with
+orient index ['S','E','N','W'], anything else without a slash is an off-road
+tile, 'empty' is no tile at all; each drivable tile gets two cubic Bezier lane
+curves, the unit-tile template scaled by the tile size, rotated by
+``pts @ R_y(angle * pi / 2)`` (quaternion-form matrix) and translated to the
+tile centre.  The computation is done once per map on the host in float64 with
+the same numpy expressions, so the control points are the reference's.
+"""
+import math
+import os
+from dataclasses import dataclass
+
+import numpy as np
+import yaml
+
+MAP_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'maps')
+
+TILE_EMPTY, TILE_OFFROAD, TILE_STRAIGHT, TILE_CURVE_LEFT, TILE_CURVE_RIGHT = -1, 0, 1, 2, 3
+KIND_CODES = {'straight': TILE_STRAIGHT, 'curve_left': TILE_CURVE_LEFT,
+              'curve_right': TILE_CURVE_RIGHT}
+
+# unit-tile lane templates (two lanes per tile, right-hand traffic)
+LANE_TEMPLATES = {
+    TILE_STRAIGHT: np.array([
+        [[-0.20, 0, -0.50], [-0.20, 0, -0.25], [-0.20, 0, 0.25], [-0.20, 0, 0.50]],
+        [[0.20, 0, 0.50], [0.20, 0, 0.25], [0.20, 0, -0.25], [0.20, 0, -0.50]],
+    ]),
+    TILE_CURVE_LEFT: np.array([
+        [[-0.20, 0, -0.50], [-0.20, 0, 0.00], [0.00, 0, 0.20], [0.50, 0, 0.20]],
+        [[0.50, 0, -0.20], [0.30, 0, -0.20], [0.20, 0, -0.30], [0.20, 0, -0.50]],
+    ]),
+    TILE_CURVE_RIGHT: np.array([
+        [[-0.20, 0, -0.50], [-0.20, 0, -0.20], [-0.30, 0, -0.20], [-0.50, 0, -0.20]],
+        [[-0.50, 0, 0.20], [-0.30, 0, 0.20], [0.30, 0, 0.00], [0.20, 0, -0.50]],
+    ]),
+}
+
+
+def rotation_y(angle):
+    """Counter-clockwise rotation about +y, upstream gen_rot_matrix form."""
+    axis = np.array([0, 1, 0])
+    axis = axis / math.sqrt(np.dot(axis, axis))
+    a = math.cos(angle / 2.0)
+    b, c, d = -axis * math.sin(angle / 2.0)
+    return np.array([
+        [a * a + b * b - c * c - d * d, 2 * (b * c - a * d), 2 * (b * d + a * c)],
+        [2 * (b * c + a * d), a * a + c * c - b * b - d * d, 2 * (c * d - a * b)],
+        [2 * (b * d - a * c), 2 * (c * d + a * b), a * a + d * d - b * b - c * c],
+    ])
+
+
+@dataclass
+class TileMap:
+    name: str
+    width: int
+    height: int
+    tile_size: float
+    kind: np.ndarray       # [H*W] int8
+    orient: np.ndarray     # [H*W] int8
+    curves: np.ndarray     # [H*W, 2, 4, 3] float64 (zeros off-road)
+    headings: np.ndarray   # [H*W, 2, 3] float64
+    rows: list
+
+    @property
+    def drivable(self):
+        return np.nonzero(self.kind > 0)[0]
+
+
+def parse_rows(rows, name='custom', tile_size=0.61):
+    H, W = len(rows), len(rows[0])
+    kind = np.full(H * W, TILE_EMPTY, np.int8)
+    orient = np.zeros(H * W, np.int8)
+    curves = np.zeros((H * W, 2, 4, 3), np.float64)
+    headings = np.zeros((H * W, 2, 3), np.float64)
+    for j, row in enumerate(rows):
+        if len(row) != W:
+            raise ValueError('each row of tiles must have the same length')
+        for i, tile in enumerate(row):
+            tile = tile.strip()
+            t = j * W + i
+            if tile == 'empty':
+                continue
+            if '/' in tile:
+                k, o = (s.strip(' ') for s in tile.split('/'))
+                if k not in KIND_CODES:
+                    raise NotImplementedError('tile kind %r (intersections: SURVEY §8f item 3)' % k)
+                kind[t] = KIND_CODES[k]
+                orient[t] = ['S', 'E', 'N', 'W'].index(o)
+                pts = LANE_TEMPLATES[kind[t]] * tile_size
+                pts = np.matmul(pts, rotation_y(int(orient[t]) * math.pi / 2))
+                pts += np.array([(i + .5) * tile_size, 0, (j + .5) * tile_size])
+                curves[t] = pts
+                h = pts[:, -1, :] - pts[:, 0, :]
+                headings[t] = h / np.linalg.norm(h).reshape(1, -1)
+            elif '4' in tile:
+                raise NotImplementedError('4-way intersections: SURVEY §8f item 3')
+            else:
+                kind[t] = TILE_OFFROAD
+    return TileMap(name, W, H, tile_size, kind, orient, curves, headings,
+                   [list(r) for r in rows])
+
+
+def load_map(name_or_path, tile_size=0.61):
+    path = name_or_path
+    if not os.path.exists(path):
+        path = os.path.join(MAP_DIR, name_or_path + '.yaml')
+    with open(path) as f:
+        doc = yaml.safe_load(f)
+    if doc.get('objects'):
+        raise NotImplementedError('maps with objects (collision / proximity penalty) are '
+                                  'SURVEY §8f item 3')
+    name = os.path.splitext(os.path.basename(path))[0]
+    return parse_rows(doc['tiles'], name, tile_size)
+
+
+def available_maps():
+    return sorted(os.path.splitext(f)[0] for f in os.listdir(MAP_DIR) if f.endswith('.yaml'))

@@ -1,0 +1,246 @@
+#!/usr/bin/env python
+"""bench.py — BASELINE.json's metric: env-steps/s (whole node) at 4096 envs/GPU.
+
+Workload (BASELINE.json configs[1]): 4096 envs per GPU
+on loop_empty, lane-pose (dist, angle) observation, i.i.d. U[0,1)^2 wheel
+actions (the train.py contract after utils/env_wrappers.py:214-216), Philox
+spawn streams keyed by seed 1234, auto-reset on done or at the 2000-step wrapper
+cap.  One bench "step" = one VecEnv.step = one EnvironmentWrapper.step for every
+env = up to repeat_actions (3) Simulator steps each; the unit counted is the
+Simulator step (env-step), read back exactly from the device counters (envs
+that finish mid-repeat run fewer).  Actions for every step are generated and
+resident in HBM before the timed region.
+
+  python bench.py [--gpus N --steps K --warmup W] [--config lane|render]
+
+N > 1: launched by torch.distributed.run, one rank per GPU; envs shard by
+env_id_base = rank * envs (disjoint spawn streams), no data-path collective;
+timing = barrier + synchronize on both sides, max over ranks; value = all
+ranks' env-steps / that time.  Rank 0 prints one JSON line.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+METRIC = 'env-steps/sec (whole node) at 4096 envs/GPU; pose/reward max-abs-err vs CPU ref'
+HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
+
+# Algorithmic HBM bytes per env per dt_step launch (DESIGN.md "step kernel"):
+# reads  x,z,angle 24 + step_count,env_step,episode 12 + action 8           = 44
+# writes x,z,angle 24 + counters 12 + reward 8 + reward_mod 8 + done 1 + obs 8 = 61
+STEP_BYTES_PER_ENV = 44 + 61
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument('--gpus', type=int, default=1)
+    p.add_argument('--steps', type=int, default=300)
+    p.add_argument('--warmup', type=int, default=30)
+    p.add_argument('--envs', type=int, default=4096)
+    p.add_argument('--map', default='loop_empty')
+    p.add_argument('--config', default='lane', choices=['lane', 'render'])
+    p.add_argument('--seed', type=int, default=1234)
+    p.add_argument('--cpu-seconds', type=float, default=1.5,
+                   help='per-process seconds of the CPU baseline sample (0 = skip)')
+    p.add_argument('--cpu-procs', type=int, default=0)
+    return p.parse_args()
+
+
+# ---- CPU baseline: the oracle's numpy restatement of step(), one env/process ----
+def _cpu_worker(args):
+    idx, seconds, map_name = args
+    import yaml
+    from oracle import dtsim_ref as R
+    with open(os.path.join(REPO, 'aido1_amd', 'maps', map_name + '.yaml')) as f:
+        rows = yaml.safe_load(f)['tiles']
+    env = R.EnvironmentWrapperRef(R.SimulatorRef(rows, seed=1234, env_id=idx))
+    env.reset()
+    rng = np.random.default_rng(1234 + idx)
+    steps = 0
+    t0 = time.perf_counter()
+    while time.perf_counter() - t0 < seconds:
+        for _ in range(20):
+            a = rng.random(2, dtype=np.float32)
+            before = env.sim.step_count
+            _, _, d = env.step(a)
+            steps += env.sim.step_count - before
+            if d:
+                env.reset()
+    return steps, time.perf_counter() - t0
+
+
+def cpu_baseline(seconds, procs, map_name):
+    import multiprocessing as mp
+    if procs <= 0:
+        try:
+            avail = len(os.sched_getaffinity(0))
+        except AttributeError:
+            avail = os.cpu_count() or 1
+        procs = max(1, min(16, avail))
+    ctx = mp.get_context('spawn')
+    with ctx.Pool(procs) as pool:
+        res = pool.map(_cpu_worker, [(i, seconds, map_name) for i in range(procs)])
+    steps = sum(r[0] for r in res)
+    wall = max(r[1] for r in res)
+    model = ''
+    try:
+        with open('/proc/cpuinfo') as f:
+            for line in f:
+                if line.startswith('model name'):
+                    model = line.split(':', 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {'value': steps / wall, 'unit': 'env-steps/s', 'cores': procs, 'kind': 'port',
+            'sample': '%d processes x %.1f s, one env each: oracle/dtsim_ref.py numpy-float64 '
+                      'restatement of Simulator.step + EnvironmentWrapper.step (no render), '
+                      '%s, U[0,1)^2 wheel actions, auto-reset; %d env-steps; host CPU: %s'
+                      % (procs, seconds, map_name, steps, model)}
+
+
+def load_traffic(kernel):
+    """Per-launch HBM bytes from a committed rocprofv3 PMC summary (or None)."""
+    path = os.path.join(REPO, 'profiles', 'pmc_traffic.json')
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        d = json.load(f)
+    v = d.get(kernel)
+    return v.get('hbm_bytes_per_launch') if isinstance(v, dict) else None
+
+
+def main():
+    args = parse()
+    import torch
+    import torch.distributed as dist
+    world = int(os.environ.get('WORLD_SIZE', '1'))
+    rank = int(os.environ.get('RANK', '0'))
+    local = int(os.environ.get('LOCAL_RANK', '0'))
+    if world > 1:
+        torch.cuda.set_device(local)
+        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
+    else:
+        torch.cuda.set_device(0)
+    dev = torch.device('cuda', local if world > 1 else 0)
+
+    from aido1_amd.config import EnvConfig
+    from aido1_amd.vec_env import StepOutput, VecEnv
+
+    n = args.envs
+    env = VecEnv(n, seed=args.seed, device=dev.index,
+                 config=EnvConfig(map_name=args.map), env_id_base=rank * n)
+    out = StepOutput(n, dev, lanepos=False, tile=False)
+    g = torch.Generator(device=dev)
+    g.manual_seed(args.seed + 7919 * rank)
+    total = args.warmup + args.steps
+    actions = torch.rand(total, n, 2, generator=g, device=dev, dtype=torch.float32)
+    render = None
+    if args.config == 'render':
+        from aido1_amd.render import RenderOutput
+        render = RenderOutput(n, dev)
+    env.reset()
+    torch.cuda.synchronize(dev)
+
+    def one(i):
+        env.step_into(actions[i], out)
+        if render is not None:
+            env.render_into(render)
+
+    for i in range(args.warmup):
+        one(i)
+    torch.cuda.synchronize(dev)
+    env.stats(reset=True)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    rev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)] if render is not None else None
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        i = args.warmup + k
+        ev[k][0].record()
+        env.step_into(actions[i], out)
+        ev[k][1].record()
+        if render is not None:
+            rev[k][0].record()
+            env.render_into(render)
+            rev[k][1].record()
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    st = env.stats()
+    env.check()
+    step_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    render_ms = float(np.mean([a.elapsed_time(b) for a, b in rev])) if rev else None
+
+    sims = torch.tensor([st['sim_steps'], st['decisions'], st['resets']], dtype=torch.float64,
+                        device=dev)
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(sims, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    sim_steps, decisions, resets = (float(v) for v in sims.tolist())
+    tmax = float(tmax.item())
+
+    if rank == 0:
+        if render is None:
+            kname, kms = 'step_kernel', step_ms
+            bytes_per_launch = STEP_BYTES_PER_ENV * n
+        else:
+            from aido1_amd.render import RENDER_BYTES_PER_ENV
+            kname, kms = 'render_kernel', render_ms
+            bytes_per_launch = RENDER_BYTES_PER_ENV * n
+        achieved = bytes_per_launch / (kms * 1e-3) / 1e9
+        line = {
+            'metric': METRIC,
+            'value': sim_steps / tmax,
+            'unit': 'env-steps/s',
+            'n_gpus': world,
+            'steps': args.steps,
+            'warmup': args.warmup,
+            'ms_per_step': tmax / args.steps * 1e3,
+            'higher_is_better': True,
+            'scaling': 'weak',
+            'vs_baseline': None,
+            'dtype': 'f64',
+            'data': 'synthetic',
+            'config': {
+                'workload': ('config2: %d envs/GPU, lane-pose (dist, angle) obs' % n
+                             if render is None else
+                             'config3: %d envs/GPU, lane-pose + 120x160 top-down render + '
+                             'line_detector1 HSV/edge obs' % n),
+                'map': args.map, 'envs_per_gpu': n, 'repeat_actions': 3,
+                'actions': 'U[0,1)^2 wheel velocities, resident in HBM',
+                'auto_reset': True, 'global_envs': n * world,
+                'parallelism': 'env shards (%d x %d), no collective' % (world, n)},
+            'counts': {'env_steps': sim_steps, 'decisions': decisions, 'resets': resets,
+                       'elapsed_s': tmax},
+            'roofline': {'bound': 'hbm', 'kernel': kname, 'achieved': achieved,
+                         'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
+                         'traffic': load_traffic(kname), 'avg_kernel_ms': kms,
+                         'algorithmic_bytes_per_launch': bytes_per_launch},
+        }
+        if render_ms is not None:
+            line['step_kernel_ms'] = step_ms
+        if world == 1 and args.cpu_seconds > 0:
+            line['cpu_baseline'] = cpu_baseline(args.cpu_seconds, args.cpu_procs, args.map)
+        else:
+            line['cpu_baseline'] = None
+        print(json.dumps(line), flush=True)
+    env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == '__main__':
+    main()

@@ -1,0 +1,229 @@
+/*
+ * dtsim.h — C ABI of libdtsim.so, the MI355X-native batched Duckietown
+ * lane-following environment (aido1_amd).
+ *
+ * The reference (niksaz/aido1) drives ONE gym-duckietown `Simulator` per
+ * process through `launch_env()` (duckietown_rl/env.py:4-20) and the
+ * `EnvironmentWrapper.step` repeat loop (utils/env_wrappers.py:213-253).
+ * This library replaces that per-env Python object with N environments whose
+ * state lives in HBM and whose step/reset run as gfx950 kernels.  Every entry
+ * point below names the reference call it replaces.
+ *
+ * Conventions
+ *   - Every call returns int: 0 = ok, <0 = error (DT_E_*).  No C++ exception
+ *     crosses the ABI.  dt_last_error(h) returns a human-readable message.
+ *   - Pointers documented "device" must be device memory of the handle's GPU
+ *     (e.g. torch tensors' data_ptr()), contiguous, in the documented layout.
+ *     Pointers documented "host" are ordinary host memory.
+ *   - All device work is enqueued on the given stream (hipStream_t passed as
+ *     void*; NULL = the default stream).  Only dt_get_state / dt_set_state /
+ *     dt_seed synchronise.
+ *   - One handle per (process, GPU).  Calls on one handle are not thread-safe.
+ */
+#ifndef AIDO1_AMD_DTSIM_H
+#define AIDO1_AMD_DTSIM_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define DT_ABI_VERSION 1
+
+/* error codes */
+#define DT_OK 0
+#define DT_E_ARG (-1)      /* bad argument (null handle, bad size, bad map) */
+#define DT_E_HIP (-2)      /* HIP runtime error (see dt_last_error) */
+#define DT_E_SPAWN (-3)    /* reset exhausted max_spawn_attempts (upstream raises) */
+#define DT_E_NODEV (-4)    /* no usable gfx950 device */
+
+/* action contracts (how the [N,2] f32 action is turned into wheel velocities) */
+#define DT_ACTION_WHEELS 0   /* (left, right) wheel velocities, as the Simulator takes them */
+#define DT_ACTION_TANH 1     /* EnvironmentWrapper.step: a = a/2 + 0.5 in f32, in place
+                                (utils/env_wrappers.py:214-216, config.json:88 tanh head) */
+#define DT_ACTION_STEERING 2 /* (vel, steer) -> SteeringToWheelVelWrapper -> ActionWrapper
+                                (duckietown_rl/wrappers.py:138-161, :99-101; order
+                                train-ddpg-cnn.py:48-50: the x0.8 lands on the LEFT wheel) */
+
+/* Kinds of a map tile (upstream Simulator._load_map tile dict). */
+#define DT_TILE_EMPTY (-1)       /* 'empty' -> no tile; _get_tile returns None */
+#define DT_TILE_OFFROAD 0        /* grass / asphalt / floor: drivable False */
+#define DT_TILE_STRAIGHT 1
+#define DT_TILE_CURVE_LEFT 2
+#define DT_TILE_CURVE_RIGHT 3
+
+/* Simulator + EnvironmentWrapper constants.  Every value mirrors an upstream
+ * gym-duckietown constant or a reference config key; the host fills them from
+ * the same Python expressions (aido1_amd/config.py) so the doubles are
+ * bit-identical to the ones the reference computes. */
+typedef struct dt_config {
+  double road_tile_size;      /* ROAD_TILE_SIZE 0.61 */
+  double robot_speed;         /* DEFAULT_ROBOT_SPEED 1.20 (wheelVels = a * speed) */
+  double wheel_dist;          /* WHEEL_DIST 0.102 */
+  double delta_time;          /* 1.0 / DEFAULT_FRAMERATE (30) */
+  double robot_width;         /* ROBOT_WIDTH 0.13 + 0.02 */
+  double robot_length;        /* ROBOT_LENGTH 0.18 */
+  double camera_forward_dist; /* CAMERA_FORWARD_DIST 0.066 */
+  double accept_start_angle_deg; /* env.py:14 -> 4 */
+  double reset_safety;        /* _valid_pose safety factor in reset: 1.3 */
+  double reward_scale;        /* config.json:7 environment.wrapper.reward_scale */
+  double two_pi;              /* 2 * math.pi */
+  double rad2deg;             /* numpy rad2deg factor 180/pi */
+  uint32_t max_steps;         /* Simulator max_steps (env.py:10 -> 500001) */
+  uint32_t max_env_steps;     /* config.json:5 wrapper.max_env_steps (2000); done |= env_step > it */
+  uint32_t max_spawn_attempts;/* MAX_SPAWN_ATTEMPTS 5000 */
+  int32_t repeat_actions;     /* config.json:6 wrapper.repeat_actions (3) */
+  int32_t frame_skip;         /* DEFAULT_FRAME_SKIP 1 (update_physics per Simulator.step) */
+  int32_t action_mode;        /* DT_ACTION_* */
+  int32_t clip_action;        /* 1: Simulator.step clips the action to [-1, 1] */
+  int32_t reward_speed_measured; /* 0: compute_reward(.., self.robot_speed); 1: measured |dpos|/dt */
+  int32_t front_probe_length; /* 1: _valid_pose front probe uses ROBOT_LENGTH, 0: ROBOT_WIDTH */
+  int32_t auto_reset;         /* 1: dt_step resets done envs in the same launch (VectorEnv) */
+} dt_config;
+
+/* A tile map.  Tile (i, j) is grid[j * width + i]; i follows +x, j follows +z
+ * (upstream get_grid_coords / _get_tile). */
+typedef struct dt_map {
+  int32_t width;
+  int32_t height;
+  const int8_t* kind;      /* host [height*width] DT_TILE_* */
+  const double* curves;    /* host [height*width, 2, 4, 3] world-frame Bezier control points
+                              (upstream _get_curve: template * tile_size @ R_y + centre);
+                              ignored for non-drivable tiles */
+  const double* headings;  /* host [height*width, 2, 3] curve headings (P3 - P0) divided by the
+                              Frobenius norm of the tile's heading matrix (the
+                              closest_curve_point np.linalg.norm quirk) */
+} dt_map;
+
+typedef struct dt_handle dt_handle;
+
+/* ---- lifecycle ------------------------------------------------------- */
+
+/* Replaces: Simulator(...) construction in launch_env() (duckietown_rl/env.py:6-17)
+ * for n_envs environments on GPU `device`.  Every env is seeded with `seed`
+ * (per-env Philox streams are keyed by (seed, env id)) and left un-reset:
+ * call dt_reset before the first dt_step. */
+int dt_create(const dt_config* cfg, const dt_map* map, uint64_t seed, int32_t n_envs,
+              int32_t device, dt_handle** out);
+int dt_destroy(dt_handle* h);
+int32_t dt_n_envs(const dt_handle* h);
+const char* dt_last_error(const dt_handle* h); /* h may be NULL: last create error */
+int32_t dt_abi_version(void);
+
+/* Replaces: Simulator.seed(s) / DuckietownEnvironmentWrapper.change_model(seed)
+ * (utils/env_wrappers.py:126-130).  seeds: host [n_envs] or NULL (all = base).
+ * env_id_base: global id of this handle's env 0 — the spawn stream of env e is
+ * Philox(key = seed[e], counter = (k, episode, env_id_base + e, tag)), so shards
+ * of one job on different GPUs draw disjoint streams.
+ * Also zeroes every env's episode counter.  Synchronous. */
+int dt_seed(dt_handle* h, const uint64_t* seeds, uint64_t base, uint32_t env_id_base);
+
+/* ---- hot path -------------------------------------------------------- */
+
+/* Replaces: Simulator.reset() (spawn by rejection sampling, MAX_SPAWN_ATTEMPTS,
+ * _valid_pose(safety 1.3), |angle_deg| < accept_start_angle_deg) and the
+ * EnvironmentWrapper.reset counters (utils/env_wrappers.py:182-204).
+ * mask: device [n_envs] u8 (nonzero = reset) or NULL = reset all. */
+int dt_reset(dt_handle* h, const uint8_t* mask, void* stream);
+
+/* Replaces: EnvironmentWrapper.step(action) (utils/env_wrappers.py:213-253) ->
+ * repeat_actions x Simulator.step (update_physics, _compute_done_reward,
+ * compute_reward, get_lane_pos2) -> BaselineAggregationFunction
+ * (utils/reward_shaping/aggregation_functions.py:25-32), for all envs at once.
+ *   actions    device [n,2] f32 (interpreted per cfg.action_mode)          required
+ *   reward     device [n] f64  sum of raw Simulator rewards                required
+ *   reward_mod device [n] f64  sum of aggregated rewards * reward_scale    required
+ *   done       device [n] u8                                               required
+ *   obs        device [n,2] f32 (dist, angle_rad) of the returned pose: the reset
+ *              pose for envs that auto-reset; 0 when not in a lane        nullable
+ *   lanepos    device [n,4] f64 terminal LanePosition (dist, dot_dir, angle_deg,
+ *              angle_rad) before any auto-reset; NaN when not in a lane    nullable
+ *   tile       device [n] i32 terminal tile index j*W+i, -1 off the grid   nullable
+ */
+int dt_step(dt_handle* h, const float* actions, double* reward, double* reward_mod,
+            uint8_t* done, float* obs, double* lanepos, int32_t* tile, void* stream);
+
+/* Replaces: Simulator.get_lane_pos2(cur_pos, cur_angle) for every env (no step).
+ * lanepos device [n,4] f64 (NaN if NotInLane); tile device [n] i32 (nullable). */
+int dt_lane_pos(dt_handle* h, double* lanepos, int32_t* tile, void* stream);
+
+/* ---- observation path (config 3) --------------------------------------- */
+
+#define DT_OBS_H 120
+#define DT_OBS_W 160
+#define DT_MASK_WHITE 0
+#define DT_MASK_YELLOW 1
+#define DT_MASK_RED 2
+#define DT_MASK_EDGES 3
+
+/* features/line_detector1.py LineDetectorHSV parameters (dtu.Configurable,
+ * :18-34).  The values are not in the reference repo; dt_default_line_params
+ * gives the Duckietown defaults (white [0,0,150]-[180,60,255], yellow
+ * [25,140,100]-[45,255,255], red [0,140,100]-[15,255,255] U
+ * [165,140,100]-[180,255,255], dilation 3, Canny [80,200]).  HSV is OpenCV's
+ * 8-bit convention (H in [0,180)). */
+typedef struct dt_line_params {
+  uint8_t hsv_white1[3], hsv_white2[3];
+  uint8_t hsv_yellow1[3], hsv_yellow2[3];
+  uint8_t hsv_red1[3], hsv_red2[3], hsv_red3[3], hsv_red4[3];
+  int32_t dilation_kernel_size; /* odd, 1..7, MORPH_ELLIPSE */
+  double canny_lo, canny_hi;    /* Canny thresholds (apertureSize 3, L1 gradient) */
+} dt_line_params;
+
+int dt_default_line_params(dt_line_params* p);
+
+/* Where dt_render writes. */
+typedef struct dt_render_io {
+  float* gray;          /* device [n, gray_slots, 120, 160] f32 rgb2gray in [0,1], or NULL */
+  int32_t gray_slots;   /* frames per env in `gray` (3: a Transformer stack ring; 1: one frame) */
+  int32_t gray_slot;    /* slot written by this call */
+  const uint8_t* fresh; /* device [n] u8 or NULL: nonzero -> the frame goes to EVERY slot
+                           (Transformer.reset fills the stack with copies,
+                           utils/reward_shaping/env_utils.py:60-63) */
+  uint8_t* masks;       /* device [n, 4, 120, 160] u8 255/0 {white, yellow, red, edges}, or NULL */
+  uint8_t* rgb;         /* device [n, 120, 160, 3] u8 RGB raster, or NULL */
+} dt_render_io;
+
+/* Replaces, per env and fused in one launch (one workgroup per env, the frame
+ * kept in LDS): Simulator.render_obs (build-defined 120x160 ego-centric
+ * top-down raster: tile background + lane markings drawn as Bresenham
+ * polylines, utils/bresenham.py:6-34), PreliminaryTransformer's rgb2gray
+ * (utils/reward_shaping/env_utils.py:48-51) and LineDetectorHSV.setImage +
+ * _colorFilter (features/line_detector1.py:134-141, :36-57): HSV inRange,
+ * ellipse dilation, Canny(bgr, lo, hi, 3).  Renders the CURRENT pose (call it
+ * after dt_step). */
+int dt_render(dt_handle* h, const dt_render_io* io, void* stream);
+int dt_set_line_params(dt_handle* h, const dt_line_params* p);
+
+/* LineDetectorHSV on caller images (no environment): bgr device [n, height,
+ * width, 3] u8 (height*width <= 19200, e.g. 120x160); masks device [n, 4,
+ * height, width] u8 as above; hsv device [n, height, width, 3] u8 or NULL
+ * (cvtColor BGR2HSV).  Runs on the current device. */
+int dt_line_detect(const dt_line_params* p, const uint8_t* bgr, int32_t n, int32_t height,
+                   int32_t width, uint8_t* masks, uint8_t* hsv, void* stream);
+
+/* ---- state access (parity injection; synchronous) ---------------------- */
+/* x, z, angle: host [n] f64; step_count (Simulator), env_step (wrapper),
+ * episode (resets so far, keys the Philox spawn stream): host [n] u32.
+ * Any pointer may be NULL (that field is skipped). */
+int dt_get_state(dt_handle* h, double* x, double* z, double* angle, uint32_t* step_count,
+                 uint32_t* env_step, uint32_t* episode);
+int dt_set_state(dt_handle* h, const double* x, const double* z, const double* angle,
+                 const uint32_t* step_count, const uint32_t* env_step, const uint32_t* episode);
+
+/* Counters accumulated on the device since dt_create (synchronous read):
+ * out[0] Simulator steps executed (each repeat that ran, x frame_skip = 1 env-step),
+ * out[1] EnvironmentWrapper steps (agent decisions x envs), out[2] resets done,
+ * out[3] episodes finished (done flags raised).  reset != 0 zeroes them after reading.
+ * Replaces the "step per second" bookkeeping of training/explorers.py:215-240. */
+int dt_stats(dt_handle* h, uint64_t out[4], int32_t reset);
+
+/* Device-side error word (DT_E_SPAWN bit etc.) accumulated by kernels since the
+ * last call; synchronous; clears it. */
+int dt_check(dt_handle* h, uint32_t* flags);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

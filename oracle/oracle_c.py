@@ -1,0 +1,179 @@
+"""TEST INFRASTRUCTURE ONLY — ctypes front-end of oracle/_build/liboracle.so
+(the C restatement, dtsim_oracle.c).  Used by tests/ and bench.py's
+cpu_baseline leg; never by the product.
+
+The oracle takes the same ``dt_config`` / ``dt_map`` structs as the product's
+ABI (include/dtsim.h) — they are the contract's data, not its implementation —
+but builds them itself from the map rows and its own constants.
+"""
+import ctypes
+import math
+import os
+import subprocess
+
+import numpy as np
+
+from oracle import dtsim_ref as R
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+SO = os.path.join(HERE, '_build', 'liboracle.so')
+
+
+def build():
+    r = subprocess.run(['make', '-s', '-C', HERE], capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError('oracle build failed:\n' + r.stdout + r.stderr)
+    return SO
+
+
+class _Cfg(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_double) for n in (
+        'road_tile_size', 'robot_speed', 'wheel_dist', 'delta_time', 'robot_width',
+        'robot_length', 'camera_forward_dist', 'accept_start_angle_deg', 'reset_safety',
+        'reward_scale', 'two_pi', 'rad2deg')] + \
+        [(n, ctypes.c_uint32) for n in ('max_steps', 'max_env_steps', 'max_spawn_attempts')] + \
+        [(n, ctypes.c_int32) for n in ('repeat_actions', 'frame_skip', 'action_mode',
+                                       'clip_action', 'reward_speed_measured',
+                                       'front_probe_length', 'auto_reset')]
+
+
+class _Map(ctypes.Structure):
+    _fields_ = [('width', ctypes.c_int32), ('height', ctypes.c_int32),
+                ('kind', ctypes.c_void_p), ('curves', ctypes.c_void_p),
+                ('headings', ctypes.c_void_p)]
+
+
+_MODES = {'wheels': 0, 'tanh': 1, 'steering': 2}
+_KINDS = {'straight': 1, 'curve_left': 2, 'curve_right': 3}
+
+
+def make_cfg(sc: 'R.SimConfig', auto_reset=True):
+    c = _Cfg()
+    c.road_tile_size = sc.road_tile_size
+    c.robot_speed = sc.robot_speed
+    c.wheel_dist = R.WHEEL_DIST
+    c.delta_time = 1.0 / sc.frame_rate
+    c.robot_width = R.ROBOT_WIDTH
+    c.robot_length = R.ROBOT_LENGTH
+    c.camera_forward_dist = R.CAMERA_FORWARD_DIST
+    c.accept_start_angle_deg = sc.accept_start_angle_deg
+    c.reset_safety = sc.reset_safety
+    c.reward_scale = sc.reward_scale
+    c.two_pi = 2 * math.pi
+    c.rad2deg = float(np.rad2deg(1.0))
+    c.max_steps = sc.max_steps
+    c.max_env_steps = sc.max_env_steps
+    c.max_spawn_attempts = sc.max_spawn_attempts
+    c.repeat_actions = sc.repeat_actions
+    c.frame_skip = sc.frame_skip
+    c.action_mode = _MODES[sc.action_mode]
+    c.clip_action = int(sc.clip_action)
+    c.reward_speed_measured = int(sc.reward_speed_measured)
+    c.front_probe_length = int(sc.front_probe_length)
+    c.auto_reset = int(auto_reset)
+    return c
+
+
+class OracleMap:
+    """Map arrays built by the oracle's own MapRef (restated _load_map/_get_curve)."""
+
+    def __init__(self, rows, road_tile_size=R.ROAD_TILE_SIZE):
+        m = R.MapRef(rows, road_tile_size)
+        T = m.grid_width * m.grid_height
+        self.width, self.height = m.grid_width, m.grid_height
+        self.kind = np.full(T, -1, np.int8)
+        self.curves = np.zeros((T, 2, 4, 3))
+        self.headings = np.zeros((T, 2, 3))
+        for t, tile in enumerate(m.grid):
+            if tile is None:
+                continue
+            if tile['drivable']:
+                self.kind[t] = _KINDS[tile['kind']]
+                self.curves[t] = tile['curves']
+                self.headings[t] = R.tile_headings(tile['curves'])
+            else:
+                self.kind[t] = 0
+        self.c = _Map(self.width, self.height, self.kind.ctypes.data, self.curves.ctypes.data,
+                      self.headings.ctypes.data)
+
+
+def _p(a):
+    return a.ctypes.data_as(ctypes.c_void_p) if a is not None else None
+
+
+class OracleBatch:
+    """N envs stepped by the C oracle with the product's batch semantics."""
+
+    def __init__(self, rows, n, seed=123, sim_config=None, auto_reset=True, env_base=0):
+        if not os.path.exists(SO) or os.path.getmtime(SO) < max(
+                os.path.getmtime(os.path.join(HERE, f)) for f in os.listdir(HERE)
+                if f.endswith('.c')):
+            build()
+        self.L = ctypes.CDLL(SO)
+        self.sc = sim_config or R.SimConfig()
+        self.cfg = make_cfg(self.sc, auto_reset)
+        self.map = OracleMap(rows, self.sc.road_tile_size)
+        self.n = n
+        self.env_base = env_base
+        self.seed = np.full(n, seed, np.uint64)
+        self.x = np.zeros(n)
+        self.z = np.zeros(n)
+        self.angle = np.zeros(n)
+        self.step_count = np.zeros(n, np.uint32)
+        self.env_step = np.zeros(n, np.uint32)
+        self.episode = np.zeros(n, np.uint32)
+        self.spawn_k = np.full(n, -1, np.int32)
+
+    def _state(self):
+        return [_p(a) for a in (self.x, self.z, self.angle, self.step_count, self.env_step,
+                                self.episode)]
+
+    def reset(self, mask=None):
+        m = None if mask is None else np.ascontiguousarray(mask, np.uint8)
+        rc = self.L.oracle_reset(ctypes.byref(self.cfg), ctypes.byref(self.map.c), self.n,
+                                 ctypes.c_uint32(self.env_base), _p(self.seed), _p(m),
+                                 *self._state(), _p(self.spawn_k))
+        if rc:
+            raise R.SpawnError('oracle_reset rc=%d' % rc)
+
+    def step(self, actions):
+        a = np.ascontiguousarray(actions, np.float32)
+        assert a.shape == (self.n, 2)
+        out = dict(reward=np.zeros(self.n), reward_mod=np.zeros(self.n),
+                   done=np.zeros(self.n, np.uint8), obs=np.zeros((self.n, 2), np.float32),
+                   lanepos=np.zeros((self.n, 4)), tile=np.zeros(self.n, np.int32))
+        rc = self.L.oracle_step(ctypes.byref(self.cfg), ctypes.byref(self.map.c), self.n,
+                                ctypes.c_uint32(self.env_base), _p(self.seed), _p(a),
+                                *self._state(), _p(out['reward']), _p(out['reward_mod']),
+                                _p(out['done']), _p(out['obs']), _p(out['lanepos']),
+                                _p(out['tile']))
+        if rc:
+            raise R.SpawnError('oracle_step rc=%d' % rc)
+        return out
+
+    def lane_pos(self):
+        lp = np.zeros((self.n, 4))
+        tile = np.zeros(self.n, np.int32)
+        self.L.oracle_lane_pos(ctypes.byref(self.cfg), ctypes.byref(self.map.c), self.n,
+                               _p(self.x), _p(self.z), _p(self.angle), _p(lp), _p(tile))
+        return lp, tile
+
+    def state(self):
+        return dict(x=self.x.copy(), z=self.z.copy(), angle=self.angle.copy(),
+                    step_count=self.step_count.copy(), env_step=self.env_step.copy(),
+                    episode=self.episode.copy())
+
+    def set_state(self, **kw):
+        for k, v in kw.items():
+            getattr(self, k)[...] = v
+
+
+def philox(ctr, key):
+    if not os.path.exists(SO):
+        build()
+    L = ctypes.CDLL(SO)
+    c = (ctypes.c_uint32 * 4)(*ctr)
+    k = (ctypes.c_uint32 * 2)(*key)
+    o = (ctypes.c_uint32 * 4)()
+    L.oracle_philox(c, k, o)
+    return tuple(o)

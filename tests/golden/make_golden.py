@@ -1,0 +1,368 @@
+"""Generate the golden fixtures in tests/golden/ by importing the reference.
+
+Run in the build container (where /root/reference exists):
+    python tests/golden/make_golden.py [/root/reference]
+
+The reference is pure Python; the pieces on this path that import without its
+absent dependencies are imported directly.  Minimal in-process stand-ins are
+installed for the modules the reference imports but that are not installed and
+that the captured code paths never exercise in a way that matters:
+  - ``gym`` (Wrapper base classes + spaces.Box): the wrappers only call
+    ``__init__(env)`` and read ``observation_space``;
+  - ``scipy.misc.imresize`` (removed from scipy) and ``skimage.color`` (absent):
+    only needed so utils/reward_shaping/env_utils.py imports; the captured
+    Transformer stacking never calls them on meaningful data;
+  - ``tensorboardX``/``requests`` are not needed by the modules imported here.
+The gym-duckietown Simulator is absent, so EnvironmentWrapper fixtures drive the
+reference's own EnvironmentWrapper code over the oracle's SimulatorRef: they pin
+the wrapper's repeat / break / reward-shaping / in-place action mapping, not the
+Simulator.
+
+Outputs are JSON (small) and .npz (arrays); nothing here is reference source.
+"""
+import json
+import math
+import os
+import random
+import sys
+import types
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = sys.argv[1] if len(sys.argv) > 1 else '/root/reference'
+
+
+def install_stubs():
+    gym = types.ModuleType('gym')
+
+    class Wrapper:
+        def __init__(self, env=None):
+            self.env = env
+            self.observation_space = getattr(env, 'observation_space', None)
+            self.action_space = getattr(env, 'action_space', None)
+
+        def reset(self):
+            return self.observation(self.env.reset()) if hasattr(self, 'observation') \
+                else self.env.reset()
+
+    class Box:
+        def __init__(self, low, high, shape=None, dtype=np.float32):
+            self.shape = tuple(shape) if shape is not None else np.shape(low)
+            self.low = np.full(self.shape, low, dtype) if np.isscalar(low) else low
+            self.high = np.full(self.shape, high, dtype) if np.isscalar(high) else high
+            self.dtype = dtype
+
+    gym.Wrapper = Wrapper
+    gym.ObservationWrapper = type('ObservationWrapper', (Wrapper,), {})
+    gym.ActionWrapper = type('ActionWrapper', (Wrapper,), {})
+    gym.RewardWrapper = type('RewardWrapper', (Wrapper,), {})
+    gym.make = lambda *a, **k: None
+    spaces = types.ModuleType('gym.spaces')
+    spaces.Box = Box
+    gym.spaces = spaces
+    sys.modules['gym'] = gym
+    sys.modules['gym.spaces'] = spaces
+
+    import scipy.misc
+    from PIL import Image
+
+    def imresize(arr, size):
+        h, w = size[:2]
+        return np.asarray(Image.fromarray(np.asarray(arr, np.uint8)).resize((w, h),
+                                                                              Image.BILINEAR))
+    scipy.misc.imresize = imresize
+    sk = types.ModuleType('skimage')
+    color = types.ModuleType('skimage.color')
+    color.rgb2gray = lambda rgb: (np.asarray(rgb, np.float64) / 255.0) @ \
+        np.array([0.2125, 0.7154, 0.0721])
+    sk.color = color
+    sys.modules['skimage'] = sk
+    sys.modules['skimage.color'] = color
+    tb = types.ModuleType('tensorboardX')
+    tb.SummaryWriter = object
+    sys.modules.setdefault('tensorboardX', tb)
+
+
+def dump(name, obj):
+    with open(os.path.join(HERE, name), 'w') as f:
+        json.dump(obj, f, indent=None, separators=(',', ':'))
+    print('wrote', name)
+
+
+def gen_bresenham():
+    from utils.bresenham import bresenham
+    rng = random.Random(1234)
+    cases = [(0, 0, 0, 0), (0, 0, 5, 0), (0, 0, 0, 5), (0, 0, -5, 0), (0, 0, 0, -5),
+             (0, 0, 5, 3), (0, 0, 3, 5), (0, 0, -5, 3), (0, 0, -3, 5), (0, 0, 5, -3),
+             (0, 0, 3, -5), (0, 0, -5, -3), (0, 0, -3, -5), (0, 0, 4, 4), (0, 0, -4, 4),
+             (2, 3, 2, 3), (10, 7, -6, 7), (159, 119, 0, 0), (0, 119, 159, 0)]
+    for _ in range(150):
+        cases.append(tuple(rng.randint(-40, 170) for _ in range(4)))
+    dump('bresenham.json', [{'line': list(c), 'points': [list(p) for p in bresenham(*c)]}
+                            for c in cases])
+
+
+def gen_aggregation():
+    from utils.reward_shaping.aggregation_functions import BaselineAggregationFunction
+    from duckietown_rl.wrappers import DtRewardWrapper
+    f = BaselineAggregationFunction({})
+    rng = np.random.default_rng(5)
+    xs = [-1000, -1000.0, 0, 0.0, -0.0, 1e-300, -1e-300, 0.5, -0.5, 1.2, -999.999999, -1000.0001,
+          5e-324] + [float(v) for v in rng.normal(0, 5, 200)]
+    w = DtRewardWrapper(None)
+    dump('aggregation.json', [{'r': x, 'baseline': f(None, None, x), 'dt_reward_wrapper':
+                               w.reward(x)} for x in xs])
+
+
+def gen_steering():
+    from duckietown_rl.wrappers import ActionWrapper, SteeringToWheelVelWrapper
+
+    class Dummy:
+        observation_space = None
+        action_space = None
+    # wrapper order of train-ddpg-cnn.py:48-50 / solution.py:35-36:
+    # env = ActionWrapper(env); env = SteeringToWheelVelWrapper(env)
+    # -> the agent's action goes through SteeringToWheelVel.action first, then
+    #    ActionWrapper.action (x0.8 on element 0 = the LEFT wheel).
+    inner = ActionWrapper(Dummy())
+    outer = SteeringToWheelVelWrapper(inner)
+    rng = np.random.default_rng(6)
+    acts = [(0.5, 0.0), (0.4, 0.3), (1.0, 1.0), (-1.0, -1.0), (0.0, 0.0), (1.0, -8.0), (0.2, 20.0),
+            (0.05, -0.5)] + [tuple(float(v) for v in rng.uniform(-1.5, 1.5, 2)) for _ in range(200)]
+    out = []
+    for a in acts:
+        wheels = outer.action(np.array(a))
+        final = inner.action(wheels)
+        out.append({'action': list(a), 'wheels': [float(v) for v in wheels],
+                    'sim_action': [float(v) for v in final]})
+    # float32 inputs (the actor emits float32)
+    acts32 = rng.uniform(-1, 1, (100, 2)).astype(np.float32)
+    for a in acts32:
+        wheels = outer.action(a)
+        final = inner.action(wheels)
+        out.append({'action32': [float(v) for v in a], 'wheels': [float(v) for v in wheels],
+                    'sim_action': [float(v) for v in final]})
+    dump('steering.json', out)
+
+
+def gen_stacking():
+    from duckietown_rl.wrappers import ImgStacker
+    from utils.reward_shaping.env_utils import Transformer
+
+    class Env:
+        def __init__(self):
+            self.k = 0
+            self.observation_space = sys.modules['gym'].spaces.Box(0.0, 1.0, (1, 2, 2))
+
+        def reset(self):
+            self.k = 100
+            return np.full((1, 2, 2), self.k, np.float64)
+
+    # ImgStacker: newest first, reset pre-fills copies
+    env = Env()
+    st = ImgStacker(env)
+    seq = []
+    o = st.observation(env.reset())
+    seq.append(o[:, 0, 0].tolist())
+    for k in range(1, 6):
+        o = st.observation(np.full((1, 2, 2), k, np.float64))
+        seq.append(o[:, 0, 0].tolist())
+    st.reset()
+    o = st.observation(np.full((1, 2, 2), 200, np.float64))
+    seq.append(o[:, 0, 0].tolist())
+    # Transformer: oldest first; reset fills three copies, then the wrapper's
+    # reset() calls transform once more (utils/env_wrappers.py:198-201)
+    tr = Transformer()
+    tseq = []
+    first = np.full((1, 2, 2), 100, np.float64)
+    tr.reset(first)
+    tseq.append(tr.transform(first)[:, 0, 0].tolist())
+    for k in range(1, 6):
+        tseq.append(tr.transform(np.full((1, 2, 2), k, np.float64))[:, 0, 0].tolist())
+    dump('stacking.json', {'img_stacker': seq, 'transformer': tseq})
+
+
+def gen_env_wrapper():
+    """Drive the reference's EnvironmentWrapper over the oracle SimulatorRef."""
+    import utils.env_wrappers as ew
+    sys.path.insert(0, REPO)
+    from oracle import dtsim_ref as R
+    with open(os.path.join(REF, 'config.json')) as f:
+        config = json.load(f)
+    rows = [['curve_left/W', 'straight/W', 'curve_left/N'],
+            ['straight/S', 'grass', 'straight/N'],
+            ['curve_left/S', 'straight/E', 'curve_left/E']]
+    fixtures = []
+    for mode, seed in (('tanh', 11), ('wheels', 12)):
+        head = config['model']['actor'][-1]['modules'][-1][-1]
+        head['name'] = 'tanh' if mode == 'tanh' else 'sigmoid'
+        log = {'raw': []}
+
+        class OracleDT(ew.BaseEnvironment):
+            def __init__(self):
+                self.sim = R.SimulatorRef(rows, seed=seed, env_id=0,
+                                          cfg=R.SimConfig(max_env_steps=40))
+                self.obs = [[[0.0, 0.0], [0.0, 0.0]]]  # from_numpy'd, as the reference's env returns
+
+            def step(self, action):
+                _, r, d, info = self.sim.step(np.array(action, np.float64))
+                log['raw'].append([float(r), bool(d)])
+                return [self.obs, r, d, None]
+
+            def reset(self):
+                self.sim.reset()
+                return self.obs
+
+            def get_observation(self):
+                return self.obs
+
+            def change_model(self, seed):
+                return 'ok'
+
+            def collect_garbage(self):
+                pass
+
+        ew.DuckietownEnvironmentWrapper = lambda **kw: OracleDT()
+        cfg = json.loads(json.dumps(config))
+        cfg['environment']['wrapper']['max_env_steps'] = 40
+        env = ew.EnvironmentWrapper(cfg, {'env_type': 'normal', 'env_init_args': {},
+                                          'env_config': {'seed': seed}}, transfer=False)
+        rng = np.random.default_rng(seed)
+        steps = []
+        env.reset()
+        for t in range(120):
+            if mode == 'tanh':
+                a = rng.uniform(-1, 1, 2).astype(np.float32)
+            else:
+                a = rng.uniform(0, 1, 2).astype(np.float32)
+            a_in = a.copy()
+            log['raw'] = []
+            _, (r, rm), done, _ = env.step(a)
+            steps.append({'action_in': [float(v) for v in a_in],
+                          'action_after': [float(v) for v in a],
+                          'raw': log['raw'], 'reward': float(r), 'reward_mod': float(rm),
+                          'done': bool(done), 'env_step': env.env_step})
+            if done:
+                env.reset()
+        fixtures.append({'mode': mode, 'seed': seed, 'max_env_steps': 40, 'steps': steps})
+    dump('env_wrapper.json', fixtures)
+
+
+def gen_segment_tree():
+    from utils.segment_tree import MinSegmentTree, SumSegmentTree
+    rng = np.random.default_rng(7)
+    out = []
+    for cap in (1, 2, 16, 64):
+        s, m = SumSegmentTree(cap), MinSegmentTree(cap)
+        ops = []
+        for _ in range(200):
+            i = int(rng.integers(0, cap))
+            v = float(rng.random() ** 2)
+            s[i] = v
+            m[i] = v
+            a = int(rng.integers(0, cap))
+            b = int(rng.integers(a + 1, cap + 1))
+            total = s.sum()
+            p = float(rng.random()) * total
+            ops.append({'set': [i, v], 'range': [a, b], 'sum': s.sum(a, b), 'min': m.min(a, b),
+                        'total': total, 'prefix': p, 'idx': s.find_prefixsum_idx(p)})
+        out.append({'capacity': cap, 'ops': ops})
+    dump('segment_tree.json', out)
+
+
+def gen_random_process_and_decay():
+    from utils.random_process import OrnsteinUhlenbeckProcess
+    from utils.util import create_decay_fn
+    np.random.seed(42)
+    ou = OrnsteinUhlenbeckProcess(size=2, theta=0.15, mu=0.0, sigma=0.3, sigma_min=0.15)
+    # record the normals too: the reference draws them from numpy's global RNG
+    np.random.seed(42)
+    normals = np.random.normal(size=(300, 2)).tolist()
+    np.random.seed(42)
+    samples = [ou.sample().tolist() for _ in range(300)]
+    ou.reset_states()
+    decays = {}
+    steps = [0, 1, 7, 31, 32, 33, 100, 1000, 23999, 24000]
+    decays['cycle'] = [create_decay_fn('cycle', initial_value=0.5, final_value=0.025,
+                                       cycle_len=32, num_cycles=24000 // 32)(s) for s in steps]
+    decays['linear'] = [create_decay_fn('linear', initial_value=0.002, final_value=1e-5,
+                                        max_step=4000000)(s) for s in steps]
+    decays['exponential'] = [create_decay_fn('exponential', initial_value=1.0,
+                                             final_value=0.01, max_step=1000,
+                                             updates=10)(s) for s in steps]
+    decays['cyclic_cosine'] = [create_decay_fn('cyclic_cosine', initial_value=1.0,
+                                               final_value=0.1, period_base=10,
+                                               period_modifier=2)(s) for s in steps]
+    dump('random_process.json', {'normals': normals, 'ou': samples, 'decay_steps': steps,
+                                 'decay': decays})
+
+
+def formula_state_dict(model):
+    """Deterministic, torch-version-independent weights for the actor fixtures."""
+    import torch
+    sd = {}
+    for k, (name, t) in enumerate(model.state_dict().items()):
+        n = t.numel()
+        idx = torch.arange(n, dtype=torch.float64)
+        if name.endswith('num_batches_tracked'):
+            sd[name] = t.clone()
+        elif name.endswith('running_var'):
+            sd[name] = (1.0 + 0.25 * torch.sin(0.7 * idx + k)).reshape(t.shape).float()
+        elif name.endswith('running_mean'):
+            sd[name] = (0.1 * torch.cos(0.3 * idx + k)).reshape(t.shape).float()
+        else:
+            fan = max(1, n // t.shape[0]) if t.dim() > 1 else 16
+            sd[name] = (math.sqrt(2.0 / fan) * torch.sin(0.37 * idx + 1.3 * k)).reshape(
+                t.shape).float()
+    return sd
+
+
+def formula_input(n):
+    """Deterministic [n,3,120,160] float32 frames in [0,1] (tests rebuild it)."""
+    import torch
+    idx = torch.arange(n * 3 * 120 * 160, dtype=torch.float64)
+    return (0.5 + 0.5 * torch.sin(0.013 * idx) * torch.cos(0.0007 * idx)).reshape(
+        n, 3, 120, 160).float()
+
+
+def gen_actor():
+    import torch
+    from duckietown_rl.ddpg import ActorCNN
+    from models.ddpg.modules import Actor
+    with open(os.path.join(REF, 'config.json')) as f:
+        config = json.load(f)
+    x = formula_input(4)
+    out = {}
+    a = ActorCNN(2, 1.0)
+    a.load_state_dict(formula_state_dict(a))
+    a.eval()
+    with torch.no_grad():
+        out['actor_cnn'] = a(x).numpy()
+    c = Actor(config['model']['actor'])
+    c.load_state_dict(formula_state_dict(c))
+    c.eval()
+    with torch.no_grad():
+        out['config_actor'] = c(x).numpy()
+    out['config_actor_keys'] = np.array(list(c.state_dict().keys()))
+    out['actor_cnn_keys'] = np.array(list(a.state_dict().keys()))
+    np.savez_compressed(os.path.join(HERE, 'actor.npz'), **out)
+    print('wrote actor.npz')
+
+
+def main():
+    sys.path.insert(0, REF)
+    install_stubs()
+    gen_bresenham()
+    gen_aggregation()
+    gen_steering()
+    gen_stacking()
+    gen_env_wrapper()
+    gen_segment_tree()
+    gen_random_process_and_decay()
+    gen_actor()
+
+
+if __name__ == '__main__':
+    main()

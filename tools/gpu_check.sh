@@ -1,0 +1,25 @@
+#!/bin/bash
+# One GPU session: parity tests, bench, rocprofv3 kernel-trace summary.
+# Each GPU step has its own time limit; a crash/timeout/abort stops the script.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd)
+mkdir -p gpurun_out
+TESTS=${TESTS:-tests}
+STEPS=${STEPS:-300}
+run() {  # run <name> <timeout> cmd...; stop on fault-like exit codes
+  local name=$1 t=$2; shift 2
+  echo "=== $name: $*"
+  timeout -k 10 "$t" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "=== $name rc=$rc"; tail -n 25 "gpurun_out/$name.log"
+  case $rc in 0|1|5) return 0;; *) echo "fatal rc=$rc, stopping"; exit $rc;; esac
+}
+run smi 60 rocm-smi --showproductname
+run pytest_gpu 900 python -m pytest $TESTS -x -q -m gpu
+run bench 600 python bench.py --steps $STEPS --warmup 30 ${BENCH_ARGS}
+if [ -n "$PROFILE" ]; then
+  export TMPDIR=/tmp
+  run rocprof 600 rocprofv3 --kernel-trace --stats -d "$ROOT/gpurun_out/prof" -o run \
+      --output-format csv -- python3 "$ROOT/bench.py" --steps $STEPS --warmup 30 --cpu-seconds 0 ${BENCH_ARGS}
+fi
+echo done
