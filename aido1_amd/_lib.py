@@ -64,8 +64,7 @@ def build(force=False, verbose=False):
     return LIB_PATH
 
 
-# symbols whose kernels are still being brought up
-_OPTIONAL = {'dt_render'}
+_OPTIONAL = set()
 
 _lib = None
 _lock = threading.Lock()
@@ -99,7 +98,10 @@ def lib():
             'dt_reset': (ctypes.c_int, [vp, vp, vp]),
             'dt_step': (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp]),
             'dt_lane_pos': (ctypes.c_int, [vp, vp, vp, vp]),
-            'dt_render': (ctypes.c_int, [vp, vp, vp, vp, vp]),
+            'dt_render': (ctypes.c_int, [vp, vp, vp]),
+            'dt_default_line_params': (ctypes.c_int, [vp]),
+            'dt_set_line_params': (ctypes.c_int, [vp, vp]),
+            'dt_line_detect': (ctypes.c_int, [vp, vp, i32, i32, i32, vp, vp, vp]),
             'dt_get_state': (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp]),
             'dt_set_state': (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp]),
             'dt_check': (ctypes.c_int, [vp, ctypes.POINTER(u32)]),

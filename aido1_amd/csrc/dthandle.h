@@ -1,0 +1,39 @@
+// Internal: the opaque dt_handle behind include/dtsim.h, shared by the step
+// (dtsim.hip) and observation (dtrender.hip) translation units.
+#pragma once
+#include <string>
+
+#include "dtrender.h"
+#include "dtsim_common.h"
+
+struct StepCfg {
+  int32_t repeat, frame_skip, action_mode, clip, speed_measured, auto_reset;
+  uint32_t max_steps, max_env_steps, max_spawn_attempts;
+  double reward_scale;
+};
+
+struct dt_handle {
+  int device = 0;
+  int n = 0;
+  dt_config cfg{};
+  dt::Geo geo{};
+  StepCfg sc{};
+  dt::MapDev map{};
+  void* map_buf = nullptr;
+  dt::State st{};
+  void* st_buf = nullptr;
+  size_t lds_bytes = 0;
+  uint32_t env_base = 0;
+  // observation path (dtrender.hip)
+  dt_line_params line_params{};
+  dr::LineDev line{};
+  void* mark_buf = nullptr;   // float4 segments (x0, z0, x1, z1): yellow then white
+  int32_t n_yellow = 0, n_white = 0;
+  std::string err;
+};
+
+// dtrender.hip: lane-marking polylines of the map + default line params
+int dt_render_init(dt_handle* h, const dt_map* map);
+void dt_render_free(dt_handle* h);
+
+

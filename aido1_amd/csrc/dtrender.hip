@@ -1,0 +1,795 @@
+// Observation path: build-defined 120x160 ego-centric top-down raster of the
+// lane markings fused with the features/line_detector1.py colour/edge filter
+// and PreliminaryTransformer's grey conversion.  One 256-thread workgroup per
+// environment; the frame never leaves LDS until its outputs are written:
+//
+//   raster:  tile background per pixel (get_grid_coords of the pixel's world
+//            point) + lane markings as Bresenham polylines (utils/bresenham.py
+//            semantics: both endpoints, major-axis swap, D = 2dy - dx)
+//   pass A:  Sobel 3x3 (max-|dx|+|dy| channel), NMS direction, HSV inRange
+//            bits, rgb2gray -> gray (f32, written here: 16 B per lane)
+//   pass B:  Canny non-maximum suppression + double threshold
+//   hyst:    Canny hysteresis to a fixed point (__syncthreads_or)
+//   pass C:  ellipse dilation of the colour masks + edges -> 4 u8 masks
+//            (16 B per lane stores)
+//
+// LDS: palette image 19.2 KB + magnitudes 38.4 KB + work bits 19.2 KB ~ 78 KB
+// -> two workgroups per CU.
+#include <math.h>
+#include <string.h>
+
+#include <vector>
+
+#include "dthandle.h"
+
+namespace {
+
+using namespace dr;
+
+constexpr HsvTables kHsvHost = make_hsv_tables();
+__constant__ HsvTables c_hsv = make_hsv_tables();
+
+// ---- marking polylines (host, once per map) ----------------------------------
+// Build-defined lane markings from the map's lane curves: per drivable tile and
+// lane curve, 9 samples t = k/8 of the Bezier, offset along the curve's right
+// normal: a white edge line (5 px wide, centred 0.26 tile to the lane's right)
+// and, for curve 0 only, a dashed yellow centre line (0.20 tile to its left,
+// every other of the 8 segments).  A line of width w is kW parallel polylines
+// 0.7 px apart (closer than 1 px so curved thick lines have no holes): white 7
+// (4.2 cm), yellow 4 (2.1 cm).  oracle/render_oracle.c restates this.
+constexpr int kSegs = 8, kWhiteW = 7, kYellowW = 4;
+constexpr double kWhiteOff = 0.26, kYellowOff = -0.20, kHalfStep = 0.0035;
+
+void bez_host(const double* cp, double t, double& x, double& z, double& dx, double& dz) {
+  const double u = 1.0 - t;
+  const double c0 = u * u * u, c1 = 3.0 * t * (u * u), c2 = 3.0 * (t * t) * u, c3 = t * t * t;
+  x = c0 * cp[0];
+  z = c0 * cp[2];
+  x = x + c1 * cp[3];
+  z = z + c1 * cp[5];
+  x = x + c2 * cp[6];
+  z = z + c2 * cp[8];
+  x = x + c3 * cp[9];
+  z = z + c3 * cp[11];
+  const double a0 = 3.0 * (u * u), a1 = 6.0 * u * t, a2 = 3.0 * (t * t);
+  dx = a0 * (cp[3] - cp[0]);
+  dz = a0 * (cp[5] - cp[2]);
+  dx = dx + a1 * (cp[6] - cp[3]);
+  dz = dz + a1 * (cp[8] - cp[5]);
+  dx = dx + a2 * (cp[9] - cp[6]);
+  dz = dz + a2 * (cp[11] - cp[8]);
+}
+
+void build_marks(const dt_map* m, double ts, std::vector<float4>& yellow,
+                 std::vector<float4>& white) {
+  const int T = m->width * m->height;
+  for (int t = 0; t < T; ++t) {
+    if (m->kind[t] <= 0) continue;
+    for (int c = 0; c < 2; ++c) {
+      const double* cp = m->curves + (size_t)t * 24 + c * 12;
+      double px[kSegs + 1], pz[kSegs + 1], rx[kSegs + 1], rz[kSegs + 1];
+      for (int k = 0; k <= kSegs; ++k) {
+        double dx, dz;
+        bez_host(cp, (double)k / kSegs, px[k], pz[k], dx, dz);
+        const double n = sqrt(dx * dx + dz * dz);
+        rx[k] = (0.0 - dz) / n;  // right of the tangent: cross(tangent, up) = (-tz, tx)
+        rz[k] = dx / n;
+      }
+      for (int w = 0; w < kWhiteW; ++w) {
+        const double o = kWhiteOff * ts + (2 * w - (kWhiteW - 1)) * kHalfStep;
+        for (int k = 0; k < kSegs; ++k)
+          white.push_back(make_float4((float)(px[k] + o * rx[k]), (float)(pz[k] + o * rz[k]),
+                                      (float)(px[k + 1] + o * rx[k + 1]),
+                                      (float)(pz[k + 1] + o * rz[k + 1])));
+      }
+      if (c != 0) continue;
+      for (int w = 0; w < kYellowW; ++w) {
+        const double o = kYellowOff * ts + (2 * w - (kYellowW - 1)) * kHalfStep;
+        for (int k = 0; k < kSegs; k += 2)
+          yellow.push_back(make_float4((float)(px[k] + o * rx[k]), (float)(pz[k] + o * rz[k]),
+                                       (float)(px[k + 1] + o * rx[k + 1]),
+                                       (float)(pz[k + 1] + o * rz[k + 1])));
+      }
+    }
+  }
+}
+
+LineDev to_line_dev(const dt_line_params& p) {
+  LineDev L{};
+  memcpy(L.lo[0], p.hsv_white1, 3);
+  memcpy(L.hi[0], p.hsv_white2, 3);
+  memcpy(L.lo[1], p.hsv_yellow1, 3);
+  memcpy(L.hi[1], p.hsv_yellow2, 3);
+  memcpy(L.lo[2], p.hsv_red1, 3);
+  memcpy(L.hi[2], p.hsv_red2, 3);
+  memcpy(L.lo[3], p.hsv_red3, 3);
+  memcpy(L.hi[3], p.hsv_red4, 3);
+  // getStructuringElement(MORPH_ELLIPSE, (k, k))
+  const int k = p.dilation_kernel_size;
+  const int r = k / 2;
+  L.dil_r = r;
+  L.dil_mask = 0;
+  if (r == 0) {
+    L.dil_mask = 1ull << (3 * 7 + 3);
+  } else {
+    const double inv_r2 = 1.0 / ((double)r * r);
+    for (int i = 0; i < k; ++i) {
+      const int dy = i - r;
+      const int dxm = (int)lrint(r * sqrt((double)(r * r - dy * dy) * inv_r2));
+      const int j1 = r - dxm < 0 ? 0 : r - dxm, j2 = r + dxm + 1 > k ? k : r + dxm + 1;
+      for (int j = j1; j < j2; ++j) L.dil_mask |= 1ull << ((dy + 3) * 7 + (j - r + 3));
+    }
+  }
+  double lo = p.canny_lo, hi = p.canny_hi;
+  if (lo > hi) {
+    const double t = lo;
+    lo = hi;
+    hi = t;
+  }
+  L.canny_lo = (int)floor(lo);
+  L.canny_hi = (int)floor(hi);
+  return L;
+}
+
+// ---- device passes -----------------------------------------------------------------
+struct Lds {
+  int16_t mag[NPIX];
+  uint8_t work[NPIX];
+  int sdiv[256];
+  int hdiv[256];
+};
+
+__device__ inline void load_tables(Lds& S) {
+  for (int i = threadIdx.x; i < 256; i += blockDim.x) {
+    S.sdiv[i] = c_hsv.sdiv[i];
+    S.hdiv[i] = c_hsv.hdiv[i];
+  }
+}
+
+// Bresenham (utils/bresenham.py:6-34) into the palette image.
+__device__ inline void draw_line(uint8_t* img, int x0, int y0, int x1, int y1, uint8_t col) {
+  int dx = x1 - x0, dy = y1 - y0;
+  const int xsign = dx > 0 ? 1 : -1, ysign = dy > 0 ? 1 : -1;
+  dx = dx < 0 ? -dx : dx;
+  dy = dy < 0 ? -dy : dy;
+  int xx, xy, yx, yy;
+  if (dx > dy) {
+    xx = xsign; xy = 0; yx = 0; yy = ysign;
+  } else {
+    const int t = dx; dx = dy; dy = t;
+    xx = 0; xy = ysign; yx = xsign; yy = 0;
+  }
+  int D = 2 * dy - dx, y = 0;
+  for (int x = 0; x <= dx; ++x) {
+    const int px = x0 + x * xx + y * yx, py = y0 + x * xy + y * yy;
+    if ((unsigned)px < (unsigned)W && (unsigned)py < (unsigned)H) img[py * W + px] = col;
+    if (D >= 0) {
+      y += 1;
+      D -= 2 * dx;
+    }
+    D += 2 * dy;
+  }
+}
+
+struct View {  // f32 camera frame of one env
+  float cx, cz, dirx, dirz, rx, rz;
+};
+
+__device__ inline int proj(float v) {  // round-to-nearest pixel, clamped far off-screen
+  v = floorf(v + 0.5f);
+  v = v < -100000.0f ? -100000.0f : (v > 100000.0f ? 100000.0f : v);
+  return (int)v;
+}
+
+__device__ inline void draw_segments(uint8_t* img, const View& V, const float4* __restrict__ seg,
+                                     int nseg, uint8_t col) {
+  for (int s = threadIdx.x; s < nseg; s += blockDim.x) {
+    const float4 q = seg[s];
+    const float ax = q.x - V.cx, az = q.y - V.cz, bx = q.z - V.cx, bz = q.w - V.cz;
+    const float fa = ax * V.dirx + az * V.dirz, la = ax * V.rx + az * V.rz;
+    const float fb = bx * V.dirx + bz * V.dirz, lb = bx * V.rx + bz * V.rz;
+    const int c0 = proj(la * kInvRes + 79.5f), r0 = proj(119.5f - fa * kInvRes);
+    const int c1 = proj(lb * kInvRes + 79.5f), r1 = proj(119.5f - fb * kInvRes);
+    if ((c0 < 0 && c1 < 0) || (c0 >= W && c1 >= W) || (r0 < 0 && r1 < 0) ||
+        (r0 >= H && r1 >= H))
+      continue;
+    const int len = (c1 > c0 ? c1 - c0 : c0 - c1) + (r1 > r0 ? r1 - r0 : r0 - r1);
+    if (len > 400) continue;  // degenerate (a segment is <= ~10 px at 1 cm/px)
+    draw_line(img, c0, r0, c1, r1, col);
+  }
+}
+
+// pass A for one pixel: Sobel/NMS dir + colour bits into work, magnitude into mag
+template <class Fetch>
+__device__ inline void pass_a_pixel(const Fetch& fetch, Lds& S, const LineDev& L, int hgt,
+                                    int wid, int r, int c) {
+  int dx, dy, m;
+  sobel_max(fetch, r, c, hgt, wid, dx, dy, m);
+  const uint32_t p = fetch(r, c);
+  int h, s, v;
+  bgr_to_hsv(S.sdiv, S.hdiv, p & 255, (p >> 8) & 255, (p >> 16) & 255, h, s, v);
+  const int idx = r * wid + c;
+  S.mag[idx] = (int16_t)m;
+  S.work[idx] = color_bits(L, h, s, v) | (uint8_t)(nms_dir(dx, dy) << B_DIR_SHIFT);
+}
+
+__device__ inline int mag_at(const Lds& S, int hgt, int wid, int r, int c) {
+  return ((unsigned)r < (unsigned)hgt && (unsigned)c < (unsigned)wid) ? S.mag[r * wid + c] : 0;
+}
+
+// pass B: Canny NMS + thresholds
+__device__ inline void pass_b(Lds& S, const LineDev& L, int hgt, int wid) {
+  const int np = hgt * wid;
+  for (int idx = threadIdx.x; idx < np; idx += blockDim.x) {
+    const int m = S.mag[idx];
+    if (m <= L.canny_lo) continue;
+    const int r = idx / wid, c = idx - r * wid;
+    const int dir = (S.work[idx] >> B_DIR_SHIFT) & 3;
+    bool keep;
+    if (dir == 0) {
+      keep = m > mag_at(S, hgt, wid, r, c - 1) && m >= mag_at(S, hgt, wid, r, c + 1);
+    } else if (dir == 1) {
+      keep = m > mag_at(S, hgt, wid, r - 1, c) && m >= mag_at(S, hgt, wid, r + 1, c);
+    } else {
+      const int s = dir == 2 ? 1 : -1;
+      keep = m > mag_at(S, hgt, wid, r - 1, c - s) && m > mag_at(S, hgt, wid, r + 1, c + s);
+    }
+    if (keep) S.work[idx] |= (uint8_t)(B_CAND | (m > L.canny_hi ? B_EDGE : 0));
+  }
+}
+
+// Canny hysteresis: candidates 8-connected to a strong pixel become edges.
+__device__ inline void hysteresis(Lds& S, int hgt, int wid) {
+  const int np = hgt * wid;
+  for (;;) {
+    int changed = 0;
+    for (int idx = threadIdx.x; idx < np; idx += blockDim.x) {
+      const uint8_t b = S.work[idx];
+      if ((b & (B_CAND | B_EDGE)) != B_CAND) continue;
+      const int r = idx / wid, c = idx - r * wid;
+      bool hit = false;
+      for (int dy = -1; dy <= 1 && !hit; ++dy) {
+        const int rr = r + dy;
+        if ((unsigned)rr >= (unsigned)hgt) continue;
+        for (int dx = -1; dx <= 1; ++dx) {
+          const int cc = c + dx;
+          if ((unsigned)cc >= (unsigned)wid) continue;
+          if (S.work[rr * wid + cc] & B_EDGE) {
+            hit = true;
+            break;
+          }
+        }
+      }
+      if (hit) {
+        S.work[idx] = b | B_EDGE;
+        changed = 1;
+      }
+    }
+    if (!__syncthreads_or(changed)) break;
+  }
+}
+
+// pass C for one pixel: dilated colour bits | edge bit (bit 3)
+__device__ inline uint8_t pass_c_pixel(const Lds& S, const LineDev& L, int hgt, int wid, int r,
+                                       int c) {
+  uint8_t bits = 0;
+  const int R = L.dil_r;
+  for (int dy = -R; dy <= R; ++dy) {
+    const int rr = r + dy;
+    if ((unsigned)rr >= (unsigned)hgt) continue;
+    for (int dx = -R; dx <= R; ++dx) {
+      const int cc = c + dx;
+      if ((unsigned)cc >= (unsigned)wid) continue;
+      if (!((L.dil_mask >> ((dy + 3) * 7 + (dx + 3))) & 1ull)) continue;
+      bits |= S.work[rr * wid + cc] & 7;
+    }
+  }
+  if (S.work[r * wid + c] & B_EDGE) bits |= 8;
+  return bits;
+}
+
+struct RenderArgs {
+  const double* x;
+  const double* z;
+  const double* angle;
+  const int8_t* kind;
+  int32_t width, height;
+  float inv_ts;
+  double cam_fwd;
+  const float4* marks;
+  int32_t n_yellow, n_white;
+  float* gray;
+  int32_t slots, slot;
+  const uint8_t* fresh;
+  uint8_t* masks;
+  uint8_t* rgb;
+  LineDev line;
+  int32_t n;
+};
+
+// ---- fused render kernel ----------------------------------------------------------
+// Works on 4-pixel words (u32 of palette indices / work bytes, row-major,
+// 40 words per row).  Phases, each a barrier apart:
+//   0  background words + Bresenham markings into img
+//   1  every word: 3x3-word neighbourhood uniform?  yes -> colour bits and grey
+//      from the palette LUTs, no gradient (Sobel of a constant patch is 0);
+//      no -> grey from the LUT, word index appended to `list` (wave-aggregated
+//      LDS atomic).  Grey is stored here (float4 per lane).
+//   2  listed words only: SWAR 3-channel Sobel, Canny NMS (neighbour
+//      magnitudes recomputed, so no magnitude image is kept), double
+//      threshold; weak pixels appended to `weak`
+//   3  hysteresis over the weak list to a fixed point
+//   4  masks: SWAR ellipse dilation of the colour bits + edge bit, 16 px per
+//      lane, four uint4 stores per lane
+// LDS ~52 KB -> three workgroups per CU.
+constexpr int WPR = W / 4;          // words per row
+constexpr int NW = NPIX / 4;        // words per image
+constexpr int kWeakCap = 2048;
+
+struct FusedLds {
+  uint32_t img[NW];
+  uint32_t work[NW];
+  uint16_t list[NW];
+  uint16_t weak[kWeakCap];
+  uint32_t pal_swar[PAL_N];
+  float pal_gray[PAL_N];
+  uint32_t pal_bits[PAL_N];  // colour bits replicated into the 4 bytes
+  int32_t nlist, nweak;
+  int8_t kind[dt::kMaxLdsTiles];
+};
+
+__device__ inline uint32_t swar_of(uint32_t bgr) {  // B | G << 10 | R << 20
+  return (bgr & 255u) | (((bgr >> 8) & 255u) << 10) | (((bgr >> 16) & 255u) << 20);
+}
+
+// Sobel of one pixel from its 3x3 SWAR neighbourhood; returns max-channel m
+// (first max in B, G, R order) and that channel's (dx, dy).
+__device__ inline int sobel_swar(uint32_t a00, uint32_t a01, uint32_t a02, uint32_t a10,
+                                 uint32_t a12, uint32_t a20, uint32_t a21, uint32_t a22,
+                                 int& dx, int& dy) {
+  const uint32_t px = a02 + (a12 << 1) + a22, nx = a00 + (a10 << 1) + a20;
+  const uint32_t py = a20 + (a21 << 1) + a22, ny = a00 + (a01 << 1) + a02;
+  int best = -1;
+#pragma unroll
+  for (int ch = 0; ch < 3; ++ch) {
+    const int sh = 10 * ch;
+    const int gx = (int)((px >> sh) & 1023u) - (int)((nx >> sh) & 1023u);
+    const int gy = (int)((py >> sh) & 1023u) - (int)((ny >> sh) & 1023u);
+    const int m = (gx < 0 ? -gx : gx) + (gy < 0 ? -gy : gy);
+    if (m > best) {
+      best = m;
+      dx = gx;
+      dy = gy;
+    }
+  }
+  return best;
+}
+
+// Sobel magnitude at (r, c) read from the LDS palette image; 0 outside the image
+// (the zero border of OpenCV's magnitude buffer).
+__device__ inline int mag_at(const FusedLds& S, int r, int c) {
+  if ((unsigned)r >= (unsigned)H || (unsigned)c >= (unsigned)W) return 0;
+  const uint8_t* im = reinterpret_cast<const uint8_t*>(S.img);
+  const int r0 = r > 0 ? r - 1 : 0, r2 = r < H - 1 ? r + 1 : H - 1;
+  const int c0 = c > 0 ? c - 1 : 0, c2 = c < W - 1 ? c + 1 : W - 1;
+  int dx, dy;
+  return sobel_swar(S.pal_swar[im[r0 * W + c0]], S.pal_swar[im[r0 * W + c]],
+                    S.pal_swar[im[r0 * W + c2]], S.pal_swar[im[r * W + c0]],
+                    S.pal_swar[im[r * W + c2]], S.pal_swar[im[r2 * W + c0]],
+                    S.pal_swar[im[r2 * W + c]], S.pal_swar[im[r2 * W + c2]], dx, dy);
+}
+
+// byte-lane shift of a row of words: result byte i = pixel (i + d) (0 outside)
+__device__ inline uint32_t shift_bytes(uint32_t prev, uint32_t cur, uint32_t next, int d) {
+  if (d == 0) return cur;
+  if (d > 0) return (cur >> (8 * d)) | (next << (32 - 8 * d));
+  return (cur << (-8 * d)) | (prev >> (32 + 8 * d));
+}
+
+__device__ inline void wave_push(int32_t* counter, uint16_t* list, int cap, bool want,
+                                 uint16_t value) {
+  const uint64_t m = __ballot(want);
+  if (!m) return;
+  const int lane = threadIdx.x & 63;
+  const int leader = __ffsll((unsigned long long)m) - 1;
+  int base = 0;
+  if (lane == leader) base = atomicAdd(counter, __popcll(m));
+  base = __shfl(base, leader);
+  if (want) {
+    const int slot = base + __popcll(m & ((1ull << lane) - 1ull));
+    if (slot < cap) list[slot] = value;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void render_kernel(RenderArgs a) {
+  __shared__ __attribute__((aligned(16))) FusedLds S;
+  const int e = blockIdx.x;
+  const int tid = threadIdx.x;
+  const LineDev& L = a.line;
+  if (tid < PAL_N) {
+    const uint32_t p = kPalette[tid];
+    S.pal_swar[tid] = swar_of(p);
+    const double inv = 1.0 / 255.0;
+    const double rr = (double)((p >> 16) & 255) * inv, gg = (double)((p >> 8) & 255) * inv,
+                 bb = (double)(p & 255) * inv;
+    S.pal_gray[tid] = (float)((rr * 0.2125 + gg * 0.7154) + bb * 0.0721);
+    int h, sat, v;
+    const HsvTables& T = c_hsv;
+    bgr_to_hsv(T.sdiv, T.hdiv, p & 255, (p >> 8) & 255, (p >> 16) & 255, h, sat, v);
+    S.pal_bits[tid] = (uint32_t)color_bits(L, h, sat, v) * 0x01010101u;
+  }
+  if (tid == 0) {
+    S.nlist = 0;
+    S.nweak = 0;
+  }
+  for (int i = tid; i < a.width * a.height; i += blockDim.x) S.kind[i] = a.kind[i];
+
+  const double ang = a.angle[e];
+  double sd, cd;
+  sincos(ang, &sd, &cd);
+  View V;
+  V.cx = (float)(a.x[e] + a.cam_fwd * cd);
+  V.cz = (float)(a.z[e] + a.cam_fwd * (-sd));
+  V.dirx = (float)cd;
+  V.dirz = -(float)sd;
+  V.rx = (float)sd;
+  V.rz = (float)cd;
+  __syncthreads();
+
+  // phase 0: background, one word (4 pixels) per lane
+  for (int w = tid; w < NW; w += blockDim.x) {
+    const int r = w / WPR, c0 = 4 * (w - r * WPR);
+    const float f = (119.5f - (float)r) * kRes;
+    const float bx = V.cx + f * V.dirx, bz = V.cz + f * V.dirz;
+    uint32_t word = 0;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const float l = ((float)(c0 + i) - 79.5f) * kRes;
+      const float wx = bx + l * V.rx, wz = bz + l * V.rz;
+      const float fi = floorf(wx * a.inv_ts), fj = floorf(wz * a.inv_ts);
+      uint32_t col = PAL_FLOOR;
+      if (fi >= 0.0f && fj >= 0.0f && fi < (float)a.width && fj < (float)a.height) {
+        const int k = S.kind[(int)fj * a.width + (int)fi];
+        col = k > 0 ? PAL_ROAD : (k == 0 ? PAL_OFFROAD : PAL_FLOOR);
+      }
+      word |= col << (8 * i);
+    }
+    S.img[w] = word;
+  }
+  __syncthreads();
+  uint8_t* img8 = reinterpret_cast<uint8_t*>(S.img);
+  draw_segments(img8, V, a.marks, a.n_yellow, PAL_YELLOW);
+  __syncthreads();
+  draw_segments(img8, V, a.marks + a.n_yellow, a.n_white, PAL_WHITE);
+  __syncthreads();
+
+  // phase 1: uniform test, LUT colour bits, grey
+  const bool fresh = a.fresh != nullptr && a.fresh[e] != 0;
+  float* gbase = a.gray ? a.gray + (size_t)e * a.slots * NPIX : nullptr;
+  for (int w0 = 0; w0 < NW; w0 += blockDim.x) {
+    const int w = w0 + tid;
+    const bool act = w < NW;
+    bool uni = false;
+    uint32_t mid = 0;
+    if (act) {
+      const int r = w / WPR, cw = w - r * WPR;
+      const int ru = r > 0 ? r - 1 : 0, rd = r < H - 1 ? r + 1 : H - 1;
+      const int cl = cw > 0 ? cw - 1 : 0, cr = cw < WPR - 1 ? cw + 1 : WPR - 1;
+      mid = S.img[w];
+      const uint32_t rep = (mid & 255u) * 0x01010101u;
+      uni = mid == rep && S.img[ru * WPR + cl] == rep && S.img[ru * WPR + cw] == rep &&
+            S.img[ru * WPR + cr] == rep && S.img[r * WPR + cl] == rep &&
+            S.img[r * WPR + cr] == rep && S.img[rd * WPR + cl] == rep &&
+            S.img[rd * WPR + cw] == rep && S.img[rd * WPR + cr] == rep;
+      if (uni) S.work[w] = S.pal_bits[mid & 255u];
+      if (gbase) {
+        float4 g;
+        g.x = S.pal_gray[mid & 255u];
+        g.y = S.pal_gray[(mid >> 8) & 255u];
+        g.z = S.pal_gray[(mid >> 16) & 255u];
+        g.w = S.pal_gray[mid >> 24];
+        if (fresh) {
+          for (int sl = 0; sl < a.slots; ++sl)
+            *reinterpret_cast<float4*>(gbase + sl * NPIX + 4 * w) = g;
+        } else {
+          *reinterpret_cast<float4*>(gbase + a.slot * NPIX + 4 * w) = g;
+        }
+      }
+      if (a.rgb) {
+        uint8_t* o = a.rgb + ((size_t)e * NPIX + 4 * w) * 3;
+        for (int i = 0; i < 4; ++i) {
+          const uint32_t p = kPalette[(mid >> (8 * i)) & 255u];
+          o[3 * i + 0] = (p >> 16) & 255;
+          o[3 * i + 1] = (p >> 8) & 255;
+          o[3 * i + 2] = p & 255;
+        }
+      }
+    }
+    wave_push(&S.nlist, S.list, NW, act && !uni, (uint16_t)w);
+  }
+  __syncthreads();
+
+  // phase 2: gradients + NMS + thresholds on the listed words
+  const int nlist = S.nlist;
+  for (int i0 = 0; i0 < nlist; i0 += blockDim.x) {
+    const int li = i0 + tid;
+    uint16_t wk[4] = {0, 0, 0, 0};
+    bool want[4] = {false, false, false, false};
+    if (li < nlist) {
+      const int w = S.list[li];
+      const int r = w / WPR, c0 = 4 * (w - r * WPR);
+      const int ru = r > 0 ? r - 1 : 0, rd = r < H - 1 ? r + 1 : H - 1;
+      uint32_t nb[3][6];
+      const int rows[3] = {ru, r, rd};
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        const uint8_t* rowp = img8 + rows[k] * W;
+#pragma unroll
+        for (int j = 0; j < 6; ++j) {
+          int cc = c0 - 1 + j;
+          cc = cc < 0 ? 0 : (cc > W - 1 ? W - 1 : cc);
+          nb[k][j] = S.pal_swar[rowp[cc]];
+        }
+      }
+      uint32_t word = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int c = c0 + i;
+        int dx, dy;
+        const int m = sobel_swar(nb[0][i], nb[0][i + 1], nb[0][i + 2], nb[1][i], nb[1][i + 2],
+                                 nb[2][i], nb[2][i + 1], nb[2][i + 2], dx, dy);
+        uint32_t b = S.pal_bits[img8[r * W + c]] & 7u;
+        if (m > L.canny_lo) {
+          bool keep;
+          const uint8_t dir = nms_dir(dx, dy);
+          if (dir == 0) {
+            keep = m > mag_at(S, r, c - 1) && m >= mag_at(S, r, c + 1);
+          } else if (dir == 1) {
+            keep = m > mag_at(S, r - 1, c) && m >= mag_at(S, r + 1, c);
+          } else {
+            const int sg = dir == 2 ? 1 : -1;
+            keep = m > mag_at(S, r - 1, c - sg) && m > mag_at(S, r + 1, c + sg);
+          }
+          if (keep) {
+            if (m > L.canny_hi) {
+              b |= B_CAND | B_EDGE;
+            } else {
+              b |= B_CAND;
+              want[i] = true;
+              wk[i] = (uint16_t)(r * W + c);
+            }
+          }
+        }
+        word |= b << (8 * i);
+      }
+      S.work[w] = word;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) wave_push(&S.nweak, S.weak, kWeakCap, want[i], wk[i]);
+  }
+  __syncthreads();
+
+  // phase 3: hysteresis (weak candidates 8-connected to an edge become edges)
+  uint8_t* work8 = reinterpret_cast<uint8_t*>(S.work);
+  const int nweak = S.nweak;
+  if (nweak > 0) {
+    const bool overflow = nweak > kWeakCap;
+    const int cnt = overflow ? NPIX : nweak;
+    for (;;) {
+      int changed = 0;
+      for (int i = tid; i < cnt; i += blockDim.x) {
+        const int idx = overflow ? i : S.weak[i];
+        const uint8_t b = work8[idx];
+        if ((b & (B_CAND | B_EDGE)) != B_CAND) continue;
+        const int r = idx / W, c = idx - r * W;
+        bool hit = false;
+        for (int dy = -1; dy <= 1 && !hit; ++dy) {
+          const int rr = r + dy;
+          if ((unsigned)rr >= (unsigned)H) continue;
+          for (int dx = -1; dx <= 1; ++dx) {
+            const int cc = c + dx;
+            if ((unsigned)cc < (unsigned)W && (work8[rr * W + cc] & B_EDGE)) {
+              hit = true;
+              break;
+            }
+          }
+        }
+        if (hit) {
+          work8[idx] = b | B_EDGE;
+          changed = 1;
+        }
+      }
+      if (!__syncthreads_or(changed)) break;
+    }
+  }
+
+  // phase 4: masks, 16 pixels (4 words) per lane
+  if (a.masks) {
+    uint8_t* mb = a.masks + (size_t)e * 4 * NPIX;
+    const int R = L.dil_r;
+    for (int q = tid; q < NW / 4; q += blockDim.x) {
+      const int r = q / (WPR / 4), cw0 = 4 * (q - r * (WPR / 4));
+      uint32_t dil[4] = {0, 0, 0, 0};
+      for (int dy = -R; dy <= R; ++dy) {
+        const int rr = r + dy;
+        if ((unsigned)rr >= (unsigned)H) continue;
+        const uint32_t* row = S.work + rr * WPR;
+        const uint32_t prev = cw0 > 0 ? row[cw0 - 1] : 0u;
+        const uint32_t next = cw0 + 4 < WPR ? row[cw0 + 4] : 0u;
+        const uint4 cur = *reinterpret_cast<const uint4*>(row + cw0);
+        const uint32_t wv[6] = {prev, cur.x, cur.y, cur.z, cur.w, next};
+        for (int dx = -R; dx <= R; ++dx) {
+          if (!((L.dil_mask >> ((dy + 3) * 7 + (dx + 3))) & 1ull)) continue;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) dil[j] |= shift_bytes(wv[j], wv[j + 1], wv[j + 2], dx);
+        }
+      }
+      const uint4 own = *reinterpret_cast<const uint4*>(S.work + r * WPR + cw0);
+      const uint32_t ow[4] = {own.x, own.y, own.z, own.w};
+      uint32_t o[4][4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        o[0][j] = (dil[j] & 0x01010101u) * 255u;
+        o[1][j] = ((dil[j] >> 1) & 0x01010101u) * 255u;
+        o[2][j] = ((dil[j] >> 2) & 0x01010101u) * 255u;
+        o[3][j] = ((ow[j] >> 6) & 0x01010101u) * 255u;
+      }
+      const int p0 = r * W + 4 * cw0;
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+        *reinterpret_cast<uint4*>(mb + k * NPIX + p0) = make_uint4(o[k][0], o[k][1], o[k][2],
+                                                                    o[k][3]);
+    }
+  }
+}
+
+// LineDetectorHSV on caller BGR images (one workgroup per image, <= 19200 px).
+__global__ __launch_bounds__(kThreads) void line_detect_kernel(LineDev L, const uint8_t* bgr,
+                                                               int hgt, int wid, uint8_t* masks,
+                                                               uint8_t* hsv) {
+  __shared__ __attribute__((aligned(16))) uint32_t src[NPIX];
+  __shared__ __attribute__((aligned(16))) Lds S;
+  const int e = blockIdx.x, np = hgt * wid;
+  const uint8_t* in = bgr + (size_t)e * np * 3;
+  for (int p = threadIdx.x; p < np; p += blockDim.x)
+    src[p] = (uint32_t)in[3 * p] | ((uint32_t)in[3 * p + 1] << 8) | ((uint32_t)in[3 * p + 2] << 16);
+  load_tables(S);
+  __syncthreads();
+  const auto fetch = [&](int r, int c) -> uint32_t { return src[r * wid + c]; };
+  for (int p = threadIdx.x; p < np; p += blockDim.x) {
+    const int r = p / wid, c = p - r * wid;
+    pass_a_pixel(fetch, S, L, hgt, wid, r, c);
+    if (hsv) {
+      int h, s, v;
+      const uint32_t q = src[p];
+      bgr_to_hsv(S.sdiv, S.hdiv, q & 255, (q >> 8) & 255, (q >> 16) & 255, h, s, v);
+      uint8_t* o = hsv + ((size_t)e * np + p) * 3;
+      o[0] = (uint8_t)h;
+      o[1] = (uint8_t)s;
+      o[2] = (uint8_t)v;
+    }
+  }
+  __syncthreads();
+  pass_b(S, L, hgt, wid);
+  __syncthreads();
+  hysteresis(S, hgt, wid);
+  uint8_t* mb = masks + (size_t)e * 4 * np;
+  for (int p = threadIdx.x; p < np; p += blockDim.x) {
+    const int r = p / wid, c = p - r * wid;
+    const uint8_t b = pass_c_pixel(S, L, hgt, wid, r, c);
+    mb[p] = b & 1 ? 255 : 0;
+    mb[np + p] = b & 2 ? 255 : 0;
+    mb[2 * np + p] = b & 4 ? 255 : 0;
+    mb[3 * np + p] = b & 8 ? 255 : 0;
+  }
+}
+
+}  // namespace
+
+int dt_render_init(dt_handle* h, const dt_map* map) {
+  std::vector<float4> yellow, white;
+  build_marks(map, h->cfg.road_tile_size, yellow, white);
+  h->n_yellow = (int)yellow.size();
+  h->n_white = (int)white.size();
+  std::vector<float4> all(yellow);
+  all.insert(all.end(), white.begin(), white.end());
+  if (!all.empty()) {
+    if (hipMalloc(&h->mark_buf, all.size() * sizeof(float4)) != hipSuccess) {
+      h->err = "hipMalloc(markings) failed";
+      return DT_E_HIP;
+    }
+    if (hipMemcpy(h->mark_buf, all.data(), all.size() * sizeof(float4), hipMemcpyHostToDevice) !=
+        hipSuccess) {
+      h->err = "hipMemcpy(markings) failed";
+      return DT_E_HIP;
+    }
+  }
+  dt_default_line_params(&h->line_params);
+  h->line = to_line_dev(h->line_params);
+  return DT_OK;
+}
+
+void dt_render_free(dt_handle* h) {
+  if (h->mark_buf) (void)hipFree(h->mark_buf);
+  h->mark_buf = nullptr;
+}
+
+extern "C" {
+
+int dt_default_line_params(dt_line_params* p) {
+  if (!p) return DT_E_ARG;
+  const uint8_t v[8][3] = {{0, 0, 150},    {180, 60, 255},  {25, 140, 100}, {45, 255, 255},
+                           {0, 140, 100},  {15, 255, 255},  {165, 140, 100}, {180, 255, 255}};
+  memcpy(p->hsv_white1, v[0], 3);
+  memcpy(p->hsv_white2, v[1], 3);
+  memcpy(p->hsv_yellow1, v[2], 3);
+  memcpy(p->hsv_yellow2, v[3], 3);
+  memcpy(p->hsv_red1, v[4], 3);
+  memcpy(p->hsv_red2, v[5], 3);
+  memcpy(p->hsv_red3, v[6], 3);
+  memcpy(p->hsv_red4, v[7], 3);
+  p->dilation_kernel_size = 3;
+  p->canny_lo = 80;
+  p->canny_hi = 200;
+  return DT_OK;
+}
+
+int dt_set_line_params(dt_handle* h, const dt_line_params* p) {
+  if (!h || !p) return DT_E_ARG;
+  if (p->dilation_kernel_size < 1 || p->dilation_kernel_size > 7 ||
+      (p->dilation_kernel_size & 1) == 0) {
+    h->err = "dilation_kernel_size must be odd, 1..7";
+    return DT_E_ARG;
+  }
+  h->line_params = *p;
+  h->line = to_line_dev(*p);
+  return DT_OK;
+}
+
+int dt_render(dt_handle* h, const dt_render_io* io, void* stream) {
+  if (!h || !io) return DT_E_ARG;
+  if (io->gray && (io->gray_slots < 1 || io->gray_slot < 0 || io->gray_slot >= io->gray_slots)) {
+    h->err = "dt_render: gray_slot out of range";
+    return DT_E_ARG;
+  }
+  RenderArgs a{};
+  a.x = h->st.x;
+  a.z = h->st.z;
+  a.angle = h->st.angle;
+  a.kind = h->map.kind;
+  a.width = h->map.width;
+  a.height = h->map.height;
+  a.inv_ts = (float)(1.0 / h->cfg.road_tile_size);
+  a.cam_fwd = h->cfg.camera_forward_dist;
+  a.marks = (const float4*)h->mark_buf;
+  a.n_yellow = h->n_yellow;
+  a.n_white = h->n_white;
+  a.gray = io->gray;
+  a.slots = io->gray_slots < 1 ? 1 : io->gray_slots;
+  a.slot = io->gray_slot;
+  a.fresh = io->fresh;
+  a.masks = io->masks;
+  a.rgb = io->rgb;
+  a.line = h->line;
+  a.n = h->n;
+  hipLaunchKernelGGL(render_kernel, dim3(h->n), dim3(kThreads), 0, (hipStream_t)stream, a);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) {
+    h->err = std::string("dt_render launch: ") + hipGetErrorString(e);
+    return DT_E_HIP;
+  }
+  return DT_OK;
+}
+
+int dt_line_detect(const dt_line_params* p, const uint8_t* bgr, int32_t n, int32_t height,
+                   int32_t width, uint8_t* masks, uint8_t* hsv, void* stream) {
+  if (!p || !bgr || !masks || n <= 0 || height <= 0 || width <= 0 || height * width > NPIX ||
+      p->dilation_kernel_size < 1 || p->dilation_kernel_size > 7 ||
+      (p->dilation_kernel_size & 1) == 0)
+    return DT_E_ARG;
+  hipLaunchKernelGGL(line_detect_kernel, dim3(n), dim3(kThreads), 0, (hipStream_t)stream,
+                     to_line_dev(*p), bgr, height, width, masks, hsv);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
+}  // extern "C"

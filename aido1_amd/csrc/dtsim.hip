@@ -14,28 +14,7 @@
 #include <string>
 #include <vector>
 
-#include "dtsim_common.h"
-
-struct StepCfg {
-  int32_t repeat, frame_skip, action_mode, clip, speed_measured, auto_reset;
-  uint32_t max_steps, max_env_steps, max_spawn_attempts;
-  double reward_scale;
-};
-
-struct dt_handle {
-  int device = 0;
-  int n = 0;
-  dt_config cfg{};
-  dt::Geo geo{};
-  StepCfg sc{};
-  dt::MapDev map{};
-  void* map_buf = nullptr;
-  dt::State st{};
-  void* st_buf = nullptr;
-  size_t lds_bytes = 0;
-  uint32_t env_base = 0;
-  std::string err;
-};
+#include "dthandle.h"
 
 static std::string g_create_err;
 
@@ -411,7 +390,8 @@ int dt_create(const dt_config* cfg, const dt_map* map, uint64_t seed, int32_t n_
   h->st.err = (uint32_t*)(sb + 4 * N8 + 3 * N4);
   h->st.stats = (unsigned long long*)(sb + 4 * N8 + 3 * N4 + 256);
   *out = h;
-  rc = dt_seed(h, nullptr, seed, 0);
+  rc = dt_render_init(h, map);
+  if (rc == DT_OK) rc = dt_seed(h, nullptr, seed, 0);
   if (rc) {
     std::string m = h->err;
     dt_destroy(h);
@@ -425,6 +405,7 @@ int dt_create(const dt_config* cfg, const dt_map* map, uint64_t seed, int32_t n_
 int dt_destroy(dt_handle* h) {
   if (!h) return DT_E_ARG;
   (void)hipSetDevice(h->device);
+  dt_render_free(h);
   if (h->map_buf) (void)hipFree(h->map_buf);
   if (h->st_buf) (void)hipFree(h->st_buf);
   delete h;

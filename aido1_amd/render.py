@@ -1,0 +1,133 @@
+"""Observation path host API (BASELINE.json configs[2]).
+
+- ``RenderOutput`` + ``VecEnv.render_into``: the fused gfx950 kernel that draws
+  each env's 120x160 ego-centric top-down frame (build-defined replacement of
+  Simulator.render_obs), converts it to grey (PreliminaryTransformer,
+  utils/reward_shaping/env_utils.py:48-51) straight into a 3-slot frame ring
+  (the Transformer stack, env_utils.py:54-70) and runs the
+  features/line_detector1.py colour/edge filter on it.
+- ``line_detect``: LineDetectorHSV (setImage + _colorFilter for white, yellow,
+  red + the Canny edge map) on caller-supplied BGR images.
+- ``stack_view``: the Transformer's oldest-first [N,3,120,160] view of the ring.
+"""
+import ctypes
+
+import torch
+
+from aido1_amd import _lib
+
+H, W = 120, 160
+NPIX = H * W
+MASK_WHITE, MASK_YELLOW, MASK_RED, MASK_EDGES = range(4)
+
+# Algorithmic HBM bytes per env per render launch (DESIGN.md "render kernel"):
+# writes: grey frame f32 76,800 + 4 u8 masks 76,800; reads: pose 24.
+RENDER_BYTES_PER_ENV = 4 * NPIX + 4 * NPIX + 24
+
+
+class LineParams(ctypes.Structure):
+    """Mirror of dt_line_params (include/dtsim.h)."""
+    _fields_ = [('hsv_white1', ctypes.c_uint8 * 3), ('hsv_white2', ctypes.c_uint8 * 3),
+                ('hsv_yellow1', ctypes.c_uint8 * 3), ('hsv_yellow2', ctypes.c_uint8 * 3),
+                ('hsv_red1', ctypes.c_uint8 * 3), ('hsv_red2', ctypes.c_uint8 * 3),
+                ('hsv_red3', ctypes.c_uint8 * 3), ('hsv_red4', ctypes.c_uint8 * 3),
+                ('dilation_kernel_size', ctypes.c_int32),
+                ('canny_lo', ctypes.c_double), ('canny_hi', ctypes.c_double)]
+
+    @classmethod
+    def default(cls):
+        p = cls()
+        _lib.lib().dt_default_line_params(ctypes.byref(p))
+        return p
+
+    @classmethod
+    def from_config(cls, cfg):
+        """From a LineDetectorHSV configuration dict (features/line_detector1.py:18-34 keys)."""
+        p = cls.default()
+        for k in ('hsv_white1', 'hsv_white2', 'hsv_yellow1', 'hsv_yellow2', 'hsv_red1',
+                  'hsv_red2', 'hsv_red3', 'hsv_red4'):
+            if k in cfg:
+                getattr(p, k)[:] = [int(v) for v in cfg[k]]
+        if 'dilation_kernel_size' in cfg:
+            p.dilation_kernel_size = int(cfg['dilation_kernel_size'])
+        if 'canny_thresholds' in cfg:
+            p.canny_lo, p.canny_hi = (float(v) for v in cfg['canny_thresholds'])
+        return p
+
+
+class RenderIO(ctypes.Structure):
+    _fields_ = [('gray', ctypes.c_void_p), ('gray_slots', ctypes.c_int32),
+                ('gray_slot', ctypes.c_int32), ('fresh', ctypes.c_void_p),
+                ('masks', ctypes.c_void_p), ('rgb', ctypes.c_void_p)]
+
+
+class RenderOutput:
+    """Device buffers of the observation path for n envs: a 3-slot grey frame
+    ring (the Transformer's stack, see stack_view), the 4 line masks of the
+    latest frame, optionally the RGB raster."""
+
+    def __init__(self, n, device, slots=3, rgb=False, masks=True):
+        self.n = n
+        self.slots = slots
+        self.slot = -1  # slot of the newest frame
+        self._all = torch.ones(n, dtype=torch.uint8, device=device)
+        self.ring = torch.zeros(n, slots, H, W, dtype=torch.float32, device=device)
+        self.masks = torch.zeros(n, 4, H, W, dtype=torch.uint8, device=device) if masks else None
+        self.rgb = torch.zeros(n, H, W, 3, dtype=torch.uint8, device=device) if rgb else None
+
+    def restart(self):
+        """Next render fills every slot (after VecEnv.reset(): Transformer.reset)."""
+        self.slot = -1
+
+    def advance(self):
+        self.slot = (self.slot + 1) % self.slots
+        return self.slot
+
+    def order(self):
+        """Ring slots oldest -> newest (the Transformer's concatenation order)."""
+        return [(self.slot + 1 + k) % self.slots for k in range(self.slots)]
+
+    def stack_view(self):
+        """[n, 3, 120, 160] oldest-first stack (a gather copy; the actor consumes the
+        ring zero-copy by permuting its first conv's input channels instead)."""
+        return self.ring[:, self.order()]
+
+
+def render_into(env, out, fresh=None):
+    """Render every env's current pose into `out` (advancing the frame ring).
+    fresh: optional [n] u8 device tensor; nonzero -> the frame fills every slot
+    (Transformer.reset semantics): pass the done flags of an auto-resetting
+    step.  The first render after RenderOutput creation / restart() fills every
+    slot of every env."""
+    if out.slot < 0:
+        fresh = out._all
+    slot = out.advance()
+    io = RenderIO(ctypes.c_void_p(out.ring.data_ptr()), out.slots, slot,
+                  ctypes.c_void_p(fresh.data_ptr()) if fresh is not None else None,
+                  ctypes.c_void_p(out.masks.data_ptr()) if out.masks is not None else None,
+                  ctypes.c_void_p(out.rgb.data_ptr()) if out.rgb is not None else None)
+    rc = env._L.dt_render(env._h, ctypes.byref(io), env._stream())
+    env._check(rc, 'dt_render')
+    return out
+
+
+def line_detect(bgr, params=None, hsv=False, stream=None):
+    """LineDetectorHSV on a [n, h, w, 3] uint8 BGR CUDA tensor (h*w <= 19200).
+    Returns masks [n, 4, h, w] u8 ({white, yellow, red, edges}) and, if hsv,
+    the cvtColor(BGR2HSV) image [n, h, w, 3]."""
+    L = _lib.lib()
+    if bgr.dtype != torch.uint8 or bgr.dim() != 4 or bgr.shape[3] != 3 or not bgr.is_cuda:
+        raise ValueError('bgr must be a [n,h,w,3] uint8 CUDA tensor')
+    bgr = bgr.contiguous()
+    n, h, w, _ = bgr.shape
+    p = params or LineParams.default()
+    masks = torch.empty(n, 4, h, w, dtype=torch.uint8, device=bgr.device)
+    hsv_t = torch.empty(n, h, w, 3, dtype=torch.uint8, device=bgr.device) if hsv else None
+    s = stream if stream is not None else torch.cuda.current_stream(bgr.device).cuda_stream
+    rc = L.dt_line_detect(ctypes.byref(p), ctypes.c_void_p(bgr.data_ptr()), n, h, w,
+                          ctypes.c_void_p(masks.data_ptr()),
+                          ctypes.c_void_p(hsv_t.data_ptr()) if hsv else None,
+                          ctypes.c_void_p(s))
+    if rc != 0:
+        raise _lib.DtError('dt_line_detect failed (%d)' % rc)
+    return (masks, hsv_t) if hsv else masks

@@ -157,6 +157,17 @@ class VecEnv:
                     'dt_lane_pos')
         return lp, tile
 
+    # ---- observation path (config 3) ----------------------------------------------------
+    def render_into(self, out, fresh=None):
+        """Top-down raster + grey + line masks of every env's current pose into a
+        RenderOutput (see aido1_amd/render.py)."""
+        from aido1_amd.render import render_into
+        return render_into(self, out, fresh)
+
+    def set_line_params(self, params):
+        self._check(self._L.dt_set_line_params(self._h, ctypes.byref(params)),
+                    'dt_set_line_params')
+
     def stats(self, reset=False):
         """{'sim_steps', 'decisions', 'resets', 'episodes'} counted on the device."""
         o = (ctypes.c_uint64 * 4)()

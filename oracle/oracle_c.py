@@ -37,6 +37,13 @@ class _Cfg(ctypes.Structure):
                                        'front_probe_length', 'auto_reset')]
 
 
+class _LineParams(ctypes.Structure):
+    _fields_ = [(k, ctypes.c_uint8 * 3) for k in (
+        'hsv_white1', 'hsv_white2', 'hsv_yellow1', 'hsv_yellow2', 'hsv_red1', 'hsv_red2',
+        'hsv_red3', 'hsv_red4')] + [('dilation_kernel_size', ctypes.c_int32),
+                                    ('canny_lo', ctypes.c_double), ('canny_hi', ctypes.c_double)]
+
+
 class _Map(ctypes.Structure):
     _fields_ = [('width', ctypes.c_int32), ('height', ctypes.c_int32),
                 ('kind', ctypes.c_void_p), ('curves', ctypes.c_void_p),
@@ -177,3 +184,67 @@ def philox(ctr, key):
     o = (ctypes.c_uint32 * 4)()
     L.oracle_philox(c, k, o)
     return tuple(o)
+
+
+def line_params_default():
+    """Duckietown defaults (same values as dt_default_line_params)."""
+    p = _LineParams()
+    vals = [(0, 0, 150), (180, 60, 255), (25, 140, 100), (45, 255, 255), (0, 140, 100),
+            (15, 255, 255), (165, 140, 100), (180, 255, 255)]
+    for k, v in zip(('hsv_white1', 'hsv_white2', 'hsv_yellow1', 'hsv_yellow2', 'hsv_red1',
+                     'hsv_red2', 'hsv_red3', 'hsv_red4'), vals):
+        getattr(p, k)[:] = v
+    p.dilation_kernel_size = 3
+    p.canny_lo, p.canny_hi = 80.0, 200.0
+    return p
+
+
+class OracleRender:
+    """Observation-path oracle (render_oracle.c)."""
+
+    def __init__(self, rows, sim_config=None, params=None):
+        if not os.path.exists(SO):
+            build()
+        self.L = ctypes.CDLL(SO)
+        self.sc = sim_config or R.SimConfig()
+        self.cfg = make_cfg(self.sc)
+        self.map = OracleMap(rows, self.sc.road_tile_size)
+        self.params = params or line_params_default()
+
+    def render(self, x, z, angle):
+        x, z, angle = (np.ascontiguousarray(v, np.float64) for v in (x, z, angle))
+        n = len(x)
+        gray = np.zeros((n, 120, 160), np.float32)
+        masks = np.zeros((n, 4, 120, 160), np.uint8)
+        rgb = np.zeros((n, 120, 160, 3), np.uint8)
+        rc = self.L.oracle_render(ctypes.byref(self.cfg), ctypes.byref(self.map.c),
+                                  ctypes.byref(self.params), n, _p(x), _p(z), _p(angle),
+                                  _p(gray), _p(masks), _p(rgb))
+        assert rc == 0
+        return gray, masks, rgb
+
+    def marks(self):
+        cap = 1 << 16
+        out = np.zeros((cap, 4), np.float32)
+        ny = ctypes.c_int(0)
+        n = self.L.oracle_marks(ctypes.byref(self.cfg), ctypes.byref(self.map.c), _p(out), cap,
+                                ctypes.byref(ny))
+        return out[:n], ny.value
+
+    def line_detect(self, bgr, hsv=False):
+        bgr = np.ascontiguousarray(bgr, np.uint8)
+        n, h, w, _ = bgr.shape
+        masks = np.zeros((n, 4, h, w), np.uint8)
+        hs = np.zeros((n, h, w, 3), np.uint8) if hsv else None
+        self.L.oracle_line_detect(ctypes.byref(self.params), _p(bgr), n, h, w, _p(masks), _p(hs))
+        return (masks, hs) if hsv else masks
+
+
+def bresenham(x0, y0, x1, y1):
+    if not os.path.exists(SO):
+        build()
+    L = ctypes.CDLL(SO)
+    cap = 4096
+    buf = (ctypes.c_int * (2 * cap))()
+    n = L.oracle_bresenham(x0, y0, x1, y1, buf, cap)
+    return [(buf[2 * i], buf[2 * i + 1]) for i in range(min(n, cap))]

@@ -1,0 +1,101 @@
+"""GPU parity of the observation path: the fused raster + grey + line-detector
+kernel and the standalone LineDetectorHSV kernel vs the C oracle
+(oracle/render_oracle.c).  Integer/byte outputs (raster, masks) must match bit
+for bit; grey is float32 of the same expression (bit-exact expected)."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import map_rows
+from oracle import oracle_c as OC
+
+pytestmark = pytest.mark.gpu
+
+
+def poses(n, rng, env=None):
+    ts = 0.61
+    x = rng.uniform(-0.2, 3 * ts + 0.2, n)
+    z = rng.uniform(-0.2, 3 * ts + 0.2, n)
+    a = rng.uniform(-math.pi, 3 * math.pi, n)
+    x[:4] = [(0.5 - 0.2) * ts, 1.5 * ts, -40.0, 1e3]
+    z[:4] = [0.7, 1.5 * ts, 7.0, -1e3]
+    a[:4] = [-math.pi / 2, 0.0, 1.0, 2.0]
+    return x, z, a
+
+
+@pytest.mark.parametrize('map_name', ['loop_empty', 'zigzag'])
+def test_render_parity(gpu, map_name):
+    from aido1_amd.config import EnvConfig
+    from aido1_amd.render import RenderOutput
+    from aido1_amd.vec_env import VecEnv
+    n = 384
+    env = VecEnv(n, seed=3, config=EnvConfig(map_name=map_name))
+    env.reset()
+    rng = np.random.default_rng(4)
+    x, z, a = poses(n, rng)
+    s = env.get_state()   # keep half the envs at their spawn poses
+    x[n // 2:], z[n // 2:], a[n // 2:] = s['x'][n // 2:], s['z'][n // 2:], s['angle'][n // 2:]
+    env.set_state(x=x, z=z, angle=a)
+    out = RenderOutput(n, gpu, slots=1, rgb=True)
+    env.render_into(out)
+    torch.cuda.synchronize()
+    g, m, rgb = OC.OracleRender(map_rows(map_name)).render(x, z, a)
+    assert np.array_equal(out.rgb.cpu().numpy(), rgb)
+    assert np.array_equal(out.masks.cpu().numpy(), m)
+    assert np.array_equal(out.ring[:, 0].cpu().numpy(), g)
+    # the pipeline is exercised: lines visible, edges found
+    assert (m[:, 0] > 0).any() and (m[:, 1] > 0).any() and (m[:, 3] > 0).any()
+
+
+def test_ring_and_fresh(gpu):
+    from aido1_amd.render import RenderOutput
+    from aido1_amd.vec_env import VecEnv
+    n = 64
+    env = VecEnv(n, seed=5)
+    env.reset()
+    out = RenderOutput(n, gpu, slots=3, masks=False)
+    env.render_into(out)                     # first frame: fills every slot
+    f0 = out.ring[:, 0].clone()
+    assert torch.equal(out.ring[:, 1], f0) and torch.equal(out.ring[:, 2], f0)
+    acts = torch.full((n, 2), 0.6, device=gpu)
+    o = env.step_into(acts)
+    fresh = o.done.clone()
+    env.render_into(out, fresh=fresh)        # slot 1 (or all slots for reset envs)
+    f1 = out.ring[:, 1].clone()
+    st = out.stack_view()
+    assert torch.equal(st[:, 2], f1)         # newest last, as Transformer.transform
+    keep = (fresh == 0)
+    assert torch.equal(out.ring[keep, 0], f0[keep]) and torch.equal(out.ring[keep, 2], f0[keep])
+    if (~keep).any():
+        r = out.ring[~keep]
+        assert torch.equal(r[:, 0], r[:, 1]) and torch.equal(r[:, 2], r[:, 1])
+
+
+@pytest.mark.parametrize('shape', [(120, 160), (37, 53), (1, 1), (96, 200)])
+def test_line_detect_parity(gpu, shape):
+    from aido1_amd.render import LineParams, line_detect
+    h, w = shape
+    rng = np.random.default_rng(h * w)
+    n = 12
+    img = rng.integers(0, 256, (n, h, w, 3), dtype=np.uint8)
+    # blocky content with real edges and colours in the HSV ranges
+    for i in range(n // 2):
+        img[i] = 40
+        r0, c0 = rng.integers(0, max(1, h - 5)), rng.integers(0, max(1, w - 5))
+        img[i, r0:r0 + 20, c0:c0 + 7] = [0, 230, 255]   # yellow (BGR)
+        img[i, r0:r0 + 5, c0:] = [250, 250, 250]         # white
+        img[i, :, :3] = [30, 30, 220]                   # red
+    dev = torch.from_numpy(img).to(gpu)
+    for params in (None, 'custom'):
+        p = OC.line_params_default()
+        lp = LineParams.default()
+        if params:
+            p.dilation_kernel_size = lp.dilation_kernel_size = 5
+            p.canny_lo, p.canny_hi = lp.canny_lo, lp.canny_hi = 40.0, 120.0
+        masks, hsv = line_detect(dev, lp, hsv=True)
+        torch.cuda.synchronize()
+        rm, rh = OC.OracleRender(map_rows('loop_empty'), params=p).line_detect(img, hsv=True)
+        assert np.array_equal(hsv.cpu().numpy(), rh)
+        assert np.array_equal(masks.cpu().numpy(), rm)

@@ -17,9 +17,16 @@ run() {  # run <name> <timeout> cmd...; stop on fault-like exit codes
 run smi 60 rocm-smi --showproductname
 run pytest_gpu 900 python -m pytest $TESTS -x -q -m gpu
 run bench 600 python bench.py --steps $STEPS --warmup 30 ${BENCH_ARGS}
+if [ -n "$RENDER" ]; then
+  run bench_render 600 python bench.py --config render --steps $STEPS --warmup 30 --cpu-seconds 0
+fi
 if [ -n "$PROFILE" ]; then
   export TMPDIR=/tmp
   run rocprof 600 rocprofv3 --kernel-trace --stats -d "$ROOT/gpurun_out/prof" -o run \
       --output-format csv -- python3 "$ROOT/bench.py" --steps $STEPS --warmup 30 --cpu-seconds 0 ${BENCH_ARGS}
+  if [ -n "$RENDER" ]; then
+    run rocprof_render 600 rocprofv3 --kernel-trace --stats -d "$ROOT/gpurun_out/prof_render" -o run \
+        --output-format csv -- python3 "$ROOT/bench.py" --config render --steps $STEPS --warmup 30 --cpu-seconds 0
+  fi
 fi
 echo done
