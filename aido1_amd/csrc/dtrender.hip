@@ -16,6 +16,7 @@
 // LDS: palette image 19.2 KB + magnitudes 38.4 KB + work bits 19.2 KB ~ 78 KB
 // -> two workgroups per CU.
 #include <math.h>
+#include <stdlib.h>
 #include <string.h>
 
 #include <vector>
@@ -181,21 +182,34 @@ __device__ inline int proj(float v) {  // round-to-nearest pixel, clamped far of
   return (int)v;
 }
 
+__device__ inline void draw_one(uint8_t* img, const View& V, float4 q, uint8_t col) {
+  const float ax = q.x - V.cx, az = q.y - V.cz, bx = q.z - V.cx, bz = q.w - V.cz;
+  const float fa = ax * V.dirx + az * V.dirz, la = ax * V.rx + az * V.rz;
+  const float fb = bx * V.dirx + bz * V.dirz, lb = bx * V.rx + bz * V.rz;
+  const int c0 = proj(la * kInvRes + 79.5f), r0 = proj(119.5f - fa * kInvRes);
+  const int c1 = proj(lb * kInvRes + 79.5f), r1 = proj(119.5f - fb * kInvRes);
+  if ((c0 < 0 && c1 < 0) || (c0 >= W && c1 >= W) || (r0 < 0 && r1 < 0) || (r0 >= H && r1 >= H))
+    return;
+  const int len = (c1 > c0 ? c1 - c0 : c0 - c1) + (r1 > r0 ? r1 - r0 : r0 - r1);
+  if (len > 400) return;  // degenerate (a segment is <= ~10 px at 1 cm/px)
+  draw_line(img, c0, r0, c1, r1, col);
+}
+
+// Every thread draws segments tid, tid + T, ...; the (L2-resident) segment
+// loads of a thread are issued together, four at a time, before any is drawn.
 __device__ inline void draw_segments(uint8_t* img, const View& V, const float4* __restrict__ seg,
                                      int nseg, uint8_t col) {
-  for (int s = threadIdx.x; s < nseg; s += blockDim.x) {
-    const float4 q = seg[s];
-    const float ax = q.x - V.cx, az = q.y - V.cz, bx = q.z - V.cx, bz = q.w - V.cz;
-    const float fa = ax * V.dirx + az * V.dirz, la = ax * V.rx + az * V.rz;
-    const float fb = bx * V.dirx + bz * V.dirz, lb = bx * V.rx + bz * V.rz;
-    const int c0 = proj(la * kInvRes + 79.5f), r0 = proj(119.5f - fa * kInvRes);
-    const int c1 = proj(lb * kInvRes + 79.5f), r1 = proj(119.5f - fb * kInvRes);
-    if ((c0 < 0 && c1 < 0) || (c0 >= W && c1 >= W) || (r0 < 0 && r1 < 0) ||
-        (r0 >= H && r1 >= H))
-      continue;
-    const int len = (c1 > c0 ? c1 - c0 : c0 - c1) + (r1 > r0 ? r1 - r0 : r0 - r1);
-    if (len > 400) continue;  // degenerate (a segment is <= ~10 px at 1 cm/px)
-    draw_line(img, c0, r0, c1, r1, col);
+  const int T = blockDim.x;
+  for (int s0 = threadIdx.x; s0 < nseg; s0 += 4 * T) {
+    float4 q[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int s = s0 + k * T;
+      q[k] = s < nseg ? seg[s] : make_float4(-1e9f, -1e9f, -1e9f, -1e9f);
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      if (s0 + k * T < nseg) draw_one(img, V, q[k], col);
   }
 }
 
@@ -305,35 +319,38 @@ struct RenderArgs {
   uint8_t* rgb;
   LineDev line;
   int32_t n;
+  int32_t skip;  // diagnostics only (DTSIM_RENDER_SKIP): bit k skips phase k; outputs invalid
 };
 
 // ---- fused render kernel ----------------------------------------------------------
-// Works on 4-pixel words (u32 of palette indices / work bytes, row-major,
-// 40 words per row).  Phases, each a barrier apart:
+// Works on 4-pixel words (u32 of palette indices, row-major, 40 words per row)
+// and a 16-bit work image  [mag 11 b | NMS dir 2 b | CAND | EDGE].  Phases,
+// each a barrier apart:
 //   0  background words + Bresenham markings into img
-//   1  every word: 3x3-word neighbourhood uniform?  yes -> colour bits and grey
-//      from the palette LUTs, no gradient (Sobel of a constant patch is 0);
-//      no -> grey from the LUT, word index appended to `list` (wave-aggregated
-//      LDS atomic).  Grey is stored here (float4 per lane).
-//   2  listed words only: SWAR 3-channel Sobel, Canny NMS (neighbour
-//      magnitudes recomputed, so no magnitude image is kept), double
-//      threshold; weak pixels appended to `weak`
+//   1  every word: 3x3-pixel neighbourhood of all 4 pixels one colour?  yes ->
+//      Sobel = 0 (work 0); no -> word index appended to `list`
+//      (wave-aggregated LDS atomic).  Grey from the palette LUT, stored here
+//      (float4 per lane).
+//   2a listed words: SWAR 3-channel Sobel -> mag + dir into work
+//   2b listed words: Canny NMS (branch-free neighbour select) + thresholds;
+//      weak pixels appended to `weak`
 //   3  hysteresis over the weak list to a fixed point
-//   4  masks: SWAR ellipse dilation of the colour bits + edge bit, 16 px per
-//      lane, four uint4 stores per lane
-// LDS ~52 KB -> three workgroups per CU.
+//   4  masks: colour bits from img through a v_perm LUT, SWAR ellipse
+//      dilation, edge bits from work; 16 px per lane, four uint4 stores
+// LDS ~71 KB -> two workgroups per CU.
 constexpr int WPR = W / 4;          // words per row
 constexpr int NW = NPIX / 4;        // words per image
 constexpr int kWeakCap = 2048;
+constexpr uint16_t WK_MAG = 0x7FF, WK_DIR_SHIFT = 11, WK_CAND = 1 << 13, WK_EDGE = 1 << 14;
 
 struct FusedLds {
   uint32_t img[NW];
-  uint32_t work[NW];
+  uint16_t work[NPIX];
   uint16_t list[NW];
   uint16_t weak[kWeakCap];
   uint32_t pal_swar[PAL_N];
   float pal_gray[PAL_N];
-  uint32_t pal_bits[PAL_N];  // colour bits replicated into the 4 bytes
+  uint32_t bits_lo, bits_hi;  // colour bits of palette entries 0-3 / 4-7 (one byte each)
   int32_t nlist, nweak;
   int8_t kind[dt::kMaxLdsTiles];
 };
@@ -365,20 +382,6 @@ __device__ inline int sobel_swar(uint32_t a00, uint32_t a01, uint32_t a02, uint3
   return best;
 }
 
-// Sobel magnitude at (r, c) read from the LDS palette image; 0 outside the image
-// (the zero border of OpenCV's magnitude buffer).
-__device__ inline int mag_at(const FusedLds& S, int r, int c) {
-  if ((unsigned)r >= (unsigned)H || (unsigned)c >= (unsigned)W) return 0;
-  const uint8_t* im = reinterpret_cast<const uint8_t*>(S.img);
-  const int r0 = r > 0 ? r - 1 : 0, r2 = r < H - 1 ? r + 1 : H - 1;
-  const int c0 = c > 0 ? c - 1 : 0, c2 = c < W - 1 ? c + 1 : W - 1;
-  int dx, dy;
-  return sobel_swar(S.pal_swar[im[r0 * W + c0]], S.pal_swar[im[r0 * W + c]],
-                    S.pal_swar[im[r0 * W + c2]], S.pal_swar[im[r * W + c0]],
-                    S.pal_swar[im[r * W + c2]], S.pal_swar[im[r2 * W + c0]],
-                    S.pal_swar[im[r2 * W + c]], S.pal_swar[im[r2 * W + c2]], dx, dy);
-}
-
 // byte-lane shift of a row of words: result byte i = pixel (i + d) (0 outside)
 __device__ inline uint32_t shift_bytes(uint32_t prev, uint32_t cur, uint32_t next, int d) {
   if (d == 0) return cur;
@@ -401,6 +404,11 @@ __device__ inline void wave_push(int32_t* counter, uint16_t* list, int cap, bool
   }
 }
 
+__device__ inline int mag16(const FusedLds& S, int r, int c) {
+  return ((unsigned)r < (unsigned)H && (unsigned)c < (unsigned)W) ? (S.work[r * W + c] & WK_MAG)
+                                                                  : 0;
+}
+
 __global__ __launch_bounds__(kThreads) void render_kernel(RenderArgs a) {
   __shared__ __attribute__((aligned(16))) FusedLds S;
   const int e = blockIdx.x;
@@ -413,12 +421,19 @@ __global__ __launch_bounds__(kThreads) void render_kernel(RenderArgs a) {
     const double rr = (double)((p >> 16) & 255) * inv, gg = (double)((p >> 8) & 255) * inv,
                  bb = (double)(p & 255) * inv;
     S.pal_gray[tid] = (float)((rr * 0.2125 + gg * 0.7154) + bb * 0.0721);
-    int h, sat, v;
-    const HsvTables& T = c_hsv;
-    bgr_to_hsv(T.sdiv, T.hdiv, p & 255, (p >> 8) & 255, (p >> 16) & 255, h, sat, v);
-    S.pal_bits[tid] = (uint32_t)color_bits(L, h, sat, v) * 0x01010101u;
   }
   if (tid == 0) {
+    uint32_t lo = 0, hi = 0;
+    const HsvTables& T = c_hsv;
+    for (int i = 0; i < PAL_N; ++i) {
+      const uint32_t p = kPalette[i];
+      int h, sat, v;
+      bgr_to_hsv(T.sdiv, T.hdiv, p & 255, (p >> 8) & 255, (p >> 16) & 255, h, sat, v);
+      const uint32_t b = color_bits(L, h, sat, v);
+      if (i < 4) lo |= b << (8 * i); else hi |= b << (8 * (i - 4));
+    }
+    S.bits_lo = lo;
+    S.bits_hi = hi;
     S.nlist = 0;
     S.nweak = 0;
   }
@@ -437,7 +452,7 @@ __global__ __launch_bounds__(kThreads) void render_kernel(RenderArgs a) {
   __syncthreads();
 
   // phase 0: background, one word (4 pixels) per lane
-  for (int w = tid; w < NW; w += blockDim.x) {
+  for (int w = tid; w < NW && !(a.skip & 1); w += blockDim.x) {
     const int r = w / WPR, c0 = 4 * (w - r * WPR);
     const float f = (119.5f - (float)r) * kRes;
     const float bx = V.cx + f * V.dirx, bz = V.cz + f * V.dirz;
@@ -458,30 +473,40 @@ __global__ __launch_bounds__(kThreads) void render_kernel(RenderArgs a) {
   }
   __syncthreads();
   uint8_t* img8 = reinterpret_cast<uint8_t*>(S.img);
-  draw_segments(img8, V, a.marks, a.n_yellow, PAL_YELLOW);
-  __syncthreads();
-  draw_segments(img8, V, a.marks + a.n_yellow, a.n_white, PAL_WHITE);
+  if (!(a.skip & 2)) {
+    draw_segments(img8, V, a.marks, a.n_yellow, PAL_YELLOW);
+    __syncthreads();
+    draw_segments(img8, V, a.marks + a.n_yellow, a.n_white, PAL_WHITE);
+  }
   __syncthreads();
 
-  // phase 1: uniform test, LUT colour bits, grey
+  // phase 1: exact uniformity test of the 3 x 6 byte neighbourhood, grey
   const bool fresh = a.fresh != nullptr && a.fresh[e] != 0;
   float* gbase = a.gray ? a.gray + (size_t)e * a.slots * NPIX : nullptr;
-  for (int w0 = 0; w0 < NW; w0 += blockDim.x) {
+  for (int w0 = 0; w0 < NW && !(a.skip & 4); w0 += blockDim.x) {
     const int w = w0 + tid;
     const bool act = w < NW;
     bool uni = false;
-    uint32_t mid = 0;
     if (act) {
       const int r = w / WPR, cw = w - r * WPR;
       const int ru = r > 0 ? r - 1 : 0, rd = r < H - 1 ? r + 1 : H - 1;
-      const int cl = cw > 0 ? cw - 1 : 0, cr = cw < WPR - 1 ? cw + 1 : WPR - 1;
-      mid = S.img[w];
+      const uint32_t mid = S.img[w];
       const uint32_t rep = (mid & 255u) * 0x01010101u;
-      uni = mid == rep && S.img[ru * WPR + cl] == rep && S.img[ru * WPR + cw] == rep &&
-            S.img[ru * WPR + cr] == rep && S.img[r * WPR + cl] == rep &&
-            S.img[r * WPR + cr] == rep && S.img[rd * WPR + cl] == rep &&
-            S.img[rd * WPR + cw] == rep && S.img[rd * WPR + cr] == rep;
-      if (uni) S.work[w] = S.pal_bits[mid & 255u];
+      // side bytes (BORDER_REPLICATE: an edge column repeats itself)
+      const uint32_t lm = cw > 0 ? 1u : 0u, rm = cw < WPR - 1 ? 1u : 0u;
+      bool u = mid == rep && S.img[ru * WPR + cw] == rep && S.img[rd * WPR + cw] == rep;
+      if (lm) {
+        u = u && (S.img[ru * WPR + cw - 1] >> 24) == (mid & 255u) &&
+            (S.img[r * WPR + cw - 1] >> 24) == (mid & 255u) &&
+            (S.img[rd * WPR + cw - 1] >> 24) == (mid & 255u);
+      }
+      if (rm) {
+        u = u && (S.img[ru * WPR + cw + 1] & 255u) == (mid & 255u) &&
+            (S.img[r * WPR + cw + 1] & 255u) == (mid & 255u) &&
+            (S.img[rd * WPR + cw + 1] & 255u) == (mid & 255u);
+      }
+      uni = u;
+      if (uni) *reinterpret_cast<uint2*>(S.work + 4 * w) = make_uint2(0u, 0u);
       if (gbase) {
         float4 g;
         g.x = S.pal_gray[mid & 255u];
@@ -509,8 +534,37 @@ __global__ __launch_bounds__(kThreads) void render_kernel(RenderArgs a) {
   }
   __syncthreads();
 
-  // phase 2: gradients + NMS + thresholds on the listed words
-  const int nlist = S.nlist;
+  // phase 2a: gradients of the listed words
+  const int nlist = (a.skip & 8) ? 0 : S.nlist;
+  for (int li = tid; li < nlist; li += blockDim.x) {
+    const int w = S.list[li];
+    const int r = w / WPR, c0 = 4 * (w - r * WPR);
+    const int rows[3] = {r > 0 ? r - 1 : 0, r, r < H - 1 ? r + 1 : H - 1};
+    uint32_t nb[3][6];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+      const uint8_t* rowp = img8 + rows[k] * W;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        int cc = c0 - 1 + j;
+        cc = cc < 0 ? 0 : (cc > W - 1 ? W - 1 : cc);
+        nb[k][j] = S.pal_swar[rowp[cc]];
+      }
+    }
+    uint32_t out[2] = {0u, 0u};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      int dx, dy;
+      const int m = sobel_swar(nb[0][i], nb[0][i + 1], nb[0][i + 2], nb[1][i], nb[1][i + 2],
+                               nb[2][i], nb[2][i + 1], nb[2][i + 2], dx, dy);
+      const uint32_t v = (uint32_t)m | ((uint32_t)nms_dir(dx, dy) << WK_DIR_SHIFT);
+      out[i >> 1] |= v << (16 * (i & 1));
+    }
+    *reinterpret_cast<uint2*>(S.work + 4 * w) = make_uint2(out[0], out[1]);
+  }
+  __syncthreads();
+
+  // phase 2b: NMS + double threshold on the listed words
   for (int i0 = 0; i0 < nlist; i0 += blockDim.x) {
     const int li = i0 + tid;
     uint16_t wk[4] = {0, 0, 0, 0};
@@ -518,51 +572,37 @@ __global__ __launch_bounds__(kThreads) void render_kernel(RenderArgs a) {
     if (li < nlist) {
       const int w = S.list[li];
       const int r = w / WPR, c0 = 4 * (w - r * WPR);
-      const int ru = r > 0 ? r - 1 : 0, rd = r < H - 1 ? r + 1 : H - 1;
-      uint32_t nb[3][6];
-      const int rows[3] = {ru, r, rd};
-#pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        const uint8_t* rowp = img8 + rows[k] * W;
-#pragma unroll
-        for (int j = 0; j < 6; ++j) {
-          int cc = c0 - 1 + j;
-          cc = cc < 0 ? 0 : (cc > W - 1 ? W - 1 : cc);
-          nb[k][j] = S.pal_swar[rowp[cc]];
-        }
-      }
-      uint32_t word = 0;
+      const uint2 cur = *reinterpret_cast<const uint2*>(S.work + 4 * w);
+      const uint32_t vv[4] = {cur.x & 0xFFFFu, cur.x >> 16, cur.y & 0xFFFFu, cur.y >> 16};
+      uint32_t setb[4] = {0, 0, 0, 0};
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
-        const int c = c0 + i;
-        int dx, dy;
-        const int m = sobel_swar(nb[0][i], nb[0][i + 1], nb[0][i + 2], nb[1][i], nb[1][i + 2],
-                                 nb[2][i], nb[2][i + 1], nb[2][i + 2], dx, dy);
-        uint32_t b = S.pal_bits[img8[r * W + c]] & 7u;
+        const int m = (int)(vv[i] & WK_MAG);
         if (m > L.canny_lo) {
-          bool keep;
-          const uint8_t dir = nms_dir(dx, dy);
-          if (dir == 0) {
-            keep = m > mag_at(S, r, c - 1) && m >= mag_at(S, r, c + 1);
-          } else if (dir == 1) {
-            keep = m > mag_at(S, r - 1, c) && m >= mag_at(S, r + 1, c);
-          } else {
-            const int sg = dir == 2 ? 1 : -1;
-            keep = m > mag_at(S, r - 1, c - sg) && m > mag_at(S, r + 1, c + sg);
-          }
+          const int dir = (int)(vv[i] >> WK_DIR_SHIFT) & 3;
+          const int c = c0 + i;
+          // dir 0: (0,-1)/(0,+1); 1: (-1,0)/(+1,0); 2: (-1,-1)/(+1,+1); 3: (-1,+1)/(+1,-1)
+          const int dy1 = dir == 0 ? 0 : -1;
+          const int dx1 = dir == 0 ? -1 : (dir == 1 ? 0 : (dir == 2 ? -1 : 1));
+          const int n1 = mag16(S, r + dy1, c + dx1);
+          const int n2 = mag16(S, r - dy1, c - dx1);
+          const bool keep = m > n1 && (dir >= 2 ? m > n2 : m >= n2);
           if (keep) {
             if (m > L.canny_hi) {
-              b |= B_CAND | B_EDGE;
+              setb[i] = WK_CAND | WK_EDGE;
             } else {
-              b |= B_CAND;
+              setb[i] = WK_CAND;
               want[i] = true;
               wk[i] = (uint16_t)(r * W + c);
             }
           }
         }
-        word |= b << (8 * i);
       }
-      S.work[w] = word;
+      // only this lane writes these four entries; neighbours read only the
+      // magnitude bits, which do not change
+      if (setb[0] | setb[1] | setb[2] | setb[3])
+        *reinterpret_cast<uint2*>(S.work + 4 * w) =
+            make_uint2(cur.x | setb[0] | (setb[1] << 16), cur.y | setb[2] | (setb[3] << 16));
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) wave_push(&S.nweak, S.weak, kWeakCap, want[i], wk[i]);
@@ -570,8 +610,7 @@ __global__ __launch_bounds__(kThreads) void render_kernel(RenderArgs a) {
   __syncthreads();
 
   // phase 3: hysteresis (weak candidates 8-connected to an edge become edges)
-  uint8_t* work8 = reinterpret_cast<uint8_t*>(S.work);
-  const int nweak = S.nweak;
+  const int nweak = (a.skip & 16) ? 0 : S.nweak;
   if (nweak > 0) {
     const bool overflow = nweak > kWeakCap;
     const int cnt = overflow ? NPIX : nweak;
@@ -579,8 +618,8 @@ __global__ __launch_bounds__(kThreads) void render_kernel(RenderArgs a) {
       int changed = 0;
       for (int i = tid; i < cnt; i += blockDim.x) {
         const int idx = overflow ? i : S.weak[i];
-        const uint8_t b = work8[idx];
-        if ((b & (B_CAND | B_EDGE)) != B_CAND) continue;
+        const uint16_t b = S.work[idx];
+        if ((b & (WK_CAND | WK_EDGE)) != WK_CAND) continue;
         const int r = idx / W, c = idx - r * W;
         bool hit = false;
         for (int dy = -1; dy <= 1 && !hit; ++dy) {
@@ -588,14 +627,14 @@ __global__ __launch_bounds__(kThreads) void render_kernel(RenderArgs a) {
           if ((unsigned)rr >= (unsigned)H) continue;
           for (int dx = -1; dx <= 1; ++dx) {
             const int cc = c + dx;
-            if ((unsigned)cc < (unsigned)W && (work8[rr * W + cc] & B_EDGE)) {
+            if ((unsigned)cc < (unsigned)W && (S.work[rr * W + cc] & WK_EDGE)) {
               hit = true;
               break;
             }
           }
         }
         if (hit) {
-          work8[idx] = b | B_EDGE;
+          S.work[idx] = b | WK_EDGE;
           changed = 1;
         }
       }
@@ -604,35 +643,46 @@ __global__ __launch_bounds__(kThreads) void render_kernel(RenderArgs a) {
   }
 
   // phase 4: masks, 16 pixels (4 words) per lane
-  if (a.masks) {
+  if (a.masks && !(a.skip & 32)) {
     uint8_t* mb = a.masks + (size_t)e * 4 * NPIX;
     const int R = L.dil_r;
+    const uint32_t blo = S.bits_lo, bhi = S.bits_hi;
     for (int q = tid; q < NW / 4; q += blockDim.x) {
       const int r = q / (WPR / 4), cw0 = 4 * (q - r * (WPR / 4));
       uint32_t dil[4] = {0, 0, 0, 0};
       for (int dy = -R; dy <= R; ++dy) {
         const int rr = r + dy;
         if ((unsigned)rr >= (unsigned)H) continue;
-        const uint32_t* row = S.work + rr * WPR;
-        const uint32_t prev = cw0 > 0 ? row[cw0 - 1] : 0u;
-        const uint32_t next = cw0 + 4 < WPR ? row[cw0 + 4] : 0u;
+        const uint32_t* row = S.img + rr * WPR;
         const uint4 cur = *reinterpret_cast<const uint4*>(row + cw0);
-        const uint32_t wv[6] = {prev, cur.x, cur.y, cur.z, cur.w, next};
+        // palette index bytes -> colour-bit bytes (v_perm LUT); 0 outside the image
+        const uint32_t wv[6] = {
+            cw0 > 0 ? __builtin_amdgcn_perm(bhi, blo, row[cw0 - 1]) : 0u,
+            __builtin_amdgcn_perm(bhi, blo, cur.x), __builtin_amdgcn_perm(bhi, blo, cur.y),
+            __builtin_amdgcn_perm(bhi, blo, cur.z), __builtin_amdgcn_perm(bhi, blo, cur.w),
+            cw0 + 4 < WPR ? __builtin_amdgcn_perm(bhi, blo, row[cw0 + 4]) : 0u};
         for (int dx = -R; dx <= R; ++dx) {
           if (!((L.dil_mask >> ((dy + 3) * 7 + (dx + 3))) & 1ull)) continue;
 #pragma unroll
           for (int j = 0; j < 4; ++j) dil[j] |= shift_bytes(wv[j], wv[j + 1], wv[j + 2], dx);
         }
       }
-      const uint4 own = *reinterpret_cast<const uint4*>(S.work + r * WPR + cw0);
-      const uint32_t ow[4] = {own.x, own.y, own.z, own.w};
+      // edge bytes from the 16 work entries of this chunk
+      const uint16_t* wk = S.work + r * W + 4 * cw0;
+      uint32_t edg[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint2 v = *reinterpret_cast<const uint2*>(wk + 4 * j);
+        edg[j] = ((v.x >> 14) & 1u) | ((v.x >> 30) & 1u) << 8 | ((v.y >> 14) & 1u) << 16 |
+                 ((v.y >> 30) & 1u) << 24;
+      }
       uint32_t o[4][4];
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         o[0][j] = (dil[j] & 0x01010101u) * 255u;
         o[1][j] = ((dil[j] >> 1) & 0x01010101u) * 255u;
         o[2][j] = ((dil[j] >> 2) & 0x01010101u) * 255u;
-        o[3][j] = ((ow[j] >> 6) & 0x01010101u) * 255u;
+        o[3][j] = edg[j] * 255u;
       }
       const int p0 = r * W + 4 * cw0;
 #pragma unroll
@@ -706,6 +756,8 @@ int dt_render_init(dt_handle* h, const dt_map* map) {
   }
   dt_default_line_params(&h->line_params);
   h->line = to_line_dev(h->line_params);
+  const char* sk = getenv("DTSIM_RENDER_SKIP");  // diagnostics: phase ablation
+  h->render_skip = sk ? atoi(sk) : 0;
   return DT_OK;
 }
 
@@ -772,6 +824,7 @@ int dt_render(dt_handle* h, const dt_render_io* io, void* stream) {
   a.rgb = io->rgb;
   a.line = h->line;
   a.n = h->n;
+  a.skip = h->render_skip;
   hipLaunchKernelGGL(render_kernel, dim3(h->n), dim3(kThreads), 0, (hipStream_t)stream, a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {

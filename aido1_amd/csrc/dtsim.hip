@@ -91,10 +91,15 @@ __global__ __launch_bounds__(64) void step_kernel(dt::State st, dt::MapDev md, d
   double tr = 0.0, trm = 0.0;
   bool dn = !active;
   unsigned nsim = 0;
+  // lane position of the last reward computation; valid while the pose has not
+  // moved since (reused for the terminal output instead of a 4th bisection)
+  double lp[4];
+  bool lp_fresh = false, lp_inl = false;
   double c = 0.0, s = 0.0;
   sincos(ang, &s, &c);
   for (int rep = 0; rep < sc.repeat; ++rep) {
     if (!dn) {
+      lp_fresh = false;
       double speed = 0.0;
       for (int f = 0; f < sc.frame_skip; ++f) {
         const double ox = x, oz = z;
@@ -129,9 +134,10 @@ __global__ __launch_bounds__(64) void step_kernel(dt::State st, dt::MapDev md, d
         r = 0.0;
         sd = true;
       } else {
-        double lp[4];
         const double sp = sc.speed_measured ? speed : g.robot_speed;
-        if (dt::lane_pos(M, g, x, z, c, s, lp)) {
+        lp_fresh = true;
+        lp_inl = dt::lane_pos<false>(M, g, x, z, c, s, lp);
+        if (lp_inl) {
           const double ad = fabs(lp[0]);
           r = ((1.0 * sp) * lp[1] + (-10.0) * ad) + 40.0 * 0.0;
         } else {
@@ -148,8 +154,13 @@ __global__ __launch_bounds__(64) void step_kernel(dt::State st, dt::MapDev md, d
   }
   trm = trm * sc.reward_scale;
 
-  double lp[4];
-  bool inl = active && dt::lane_pos(M, g, x, z, c, s, lp);
+  bool inl;
+  if (lp_fresh) {  // same pose as the last reward: only the angle is missing
+    inl = lp_inl;
+    if (inl) dt::finish_angle(g, lp);
+  } else {
+    inl = active && dt::lane_pos<true>(M, g, x, z, c, s, lp);
+  }
   if (active) {
     rew[e] = tr;
     rewm[e] = trm;
@@ -168,31 +179,6 @@ __global__ __launch_bounds__(64) void step_kernel(dt::State st, dt::MapDev md, d
   dt::wave_add(st.stats + 0, nsim);
   dt::wave_add(st.stats + 1, active ? 1u : 0u);
   dt::wave_add(st.stats + 3, (active && dn) ? 1u : 0u);
-  uint32_t episode = st.episode[ei];
-  if (sc.auto_reset) {
-    const bool need = active && dn;
-    if (__ballot(need)) {  // wave-uniform
-      bool failed = false;
-      double nx = x, nz = z, na = ang;
-      dt::wave_spawn(M, g, sc.max_spawn_attempts, need, env_base + (uint32_t)e, st.seed[ei],
-                     episode, nx, nz, na, failed);
-      dt::wave_add(st.stats + 2, (need && !failed) ? 1u : 0u);
-      if (need) {
-        if (failed) {
-          atomicOr(st.err, dt::kErrSpawn);
-        } else {
-          x = nx;
-          z = nz;
-          ang = na;
-          step_count = 0u;
-          env_step = 0u;
-          episode += 1u;
-          sincos(ang, &s, &c);
-          inl = dt::lane_pos(M, g, x, z, c, s, lp);
-        }
-      }
-    }
-  }
   if (active) {
     if (obs) obs[e] = inl ? make_float2((float)lp[0], (float)lp[3]) : make_float2(0.0f, 0.0f);
     st.x[e] = x;
@@ -200,38 +186,43 @@ __global__ __launch_bounds__(64) void step_kernel(dt::State st, dt::MapDev md, d
     st.angle[e] = ang;
     st.step_count[e] = step_count;
     st.env_step[e] = env_step;
-    st.episode[e] = episode;
   }
 }
 
-// Simulator.reset + EnvironmentWrapper.reset counters for masked envs (A13).
-__global__ __launch_bounds__(64) void reset_kernel(dt::State st, dt::MapDev md, dt::Geo g,
-                                                   uint32_t max_attempts, int n, uint32_t env_base,
-                                                   const uint8_t* __restrict__ mask) {
+// Simulator.reset + EnvironmentWrapper.reset counters (A13): one wave per env,
+// so the envs that finished in a step respawn in parallel across the chip
+// instead of one after another inside their step wave.  flags: NULL = every
+// env, else envs with flags[e] != 0 (the reset mask, or dt_step's done flags
+// for the auto-reset).  obs (nullable) receives the new (dist, angle_rad).
+__global__ __launch_bounds__(64) void spawn_kernel(dt::State st, dt::MapDev md, dt::Geo g,
+                                                   uint32_t max_attempts, uint32_t env_base,
+                                                   const uint8_t* __restrict__ flags,
+                                                   float2* __restrict__ obs) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const int e = blockIdx.x;
+  if (flags != nullptr && flags[e] == 0) return;  // block-uniform
   const MapLds M = dt::stage_map(md, lds);
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool active = e < n;
-  const int ei = active ? e : 0;
-  const bool need = active && (mask == nullptr || mask[e] != 0);
-  if (!__ballot(need)) return;  // wave-uniform exit
-  double x = st.x[ei], z = st.z[ei], ang = st.angle[ei];
-  const uint32_t episode = st.episode[ei];
-  bool failed = false;
-  dt::wave_spawn(M, g, max_attempts, need, env_base + (uint32_t)e, st.seed[ei], episode, x, z, ang,
-                 failed);
-  dt::wave_add(st.stats + 2, (need && !failed) ? 1u : 0u);
-  if (need) {
-    if (failed) {
-      atomicOr(st.err, dt::kErrSpawn);
-    } else {
-      st.x[e] = x;
-      st.z[e] = z;
-      st.angle[e] = ang;
-      st.step_count[e] = 0u;
-      st.env_step[e] = 0u;
-      st.episode[e] = episode + 1u;
-    }
+  double x = 0.0, z = 0.0, ang = 0.0;
+  const uint32_t episode = st.episode[e];
+  const bool ok = dt::spawn_one(M, g, max_attempts, env_base + (uint32_t)e, st.seed[e], episode,
+                                x, z, ang);
+  if (threadIdx.x != 0) return;
+  if (!ok) {
+    atomicOr(st.err, dt::kErrSpawn);
+    return;
+  }
+  st.x[e] = x;
+  st.z[e] = z;
+  st.angle[e] = ang;
+  st.step_count[e] = 0u;
+  st.env_step[e] = 0u;
+  st.episode[e] = episode + 1u;
+  atomicAdd(st.stats + 2, 1ull);
+  if (obs) {
+    double s, c, lp[4];
+    sincos(ang, &s, &c);
+    const bool inl = dt::lane_pos<true>(M, g, x, z, c, s, lp);
+    obs[e] = inl ? make_float2((float)lp[0], (float)lp[3]) : make_float2(0.0f, 0.0f);
   }
 }
 
@@ -322,6 +313,7 @@ int dt_create(const dt_config* cfg, const dt_map* map, uint64_t seed, int32_t n_
   h->cfg = *cfg;
   dt::Geo& g = h->geo;
   g.ts = cfg->road_tile_size;
+  g.inv_ts = 1.0 / cfg->road_tile_size;
   g.wheel_dist = cfg->wheel_dist;
   g.dt = cfg->delta_time;
   g.off = cfg->camera_forward_dist - (cfg->robot_length / 2);
@@ -426,8 +418,8 @@ int dt_seed(dt_handle* h, const uint64_t* seeds, uint64_t base, uint32_t env_id_
 int dt_reset(dt_handle* h, const uint8_t* mask, void* stream) {
   if (!h) return DT_E_ARG;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(reset_kernel, dim3(grid_of(h->n)), dim3(dt::kWave), h->lds_bytes, s, h->st,
-                     h->map, h->geo, h->sc.max_spawn_attempts, h->n, h->env_base, mask);
+  hipLaunchKernelGGL(spawn_kernel, dim3(h->n), dim3(dt::kWave), h->lds_bytes, s, h->st, h->map,
+                     h->geo, h->sc.max_spawn_attempts, h->env_base, mask, (float2*)nullptr);
   HIP_OR_FAIL(h, hipGetLastError());
   return DT_OK;
 }
@@ -444,6 +436,12 @@ int dt_step(dt_handle* h, const float* actions, double* reward, double* reward_m
                      h->map, h->geo, h->sc, h->n, h->env_base, (const float2*)actions, reward, reward_mod,
                      done, (float2*)obs, lanepos, tile);
   HIP_OR_FAIL(h, hipGetLastError());
+  if (h->sc.auto_reset) {
+    hipLaunchKernelGGL(spawn_kernel, dim3(h->n), dim3(dt::kWave), h->lds_bytes, s, h->st, h->map,
+                       h->geo, h->sc.max_spawn_attempts, h->env_base, (const uint8_t*)done,
+                       (float2*)obs);
+    HIP_OR_FAIL(h, hipGetLastError());
+  }
   return DT_OK;
 }
 

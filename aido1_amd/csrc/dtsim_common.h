@@ -142,13 +142,26 @@ __device__ inline uint64_t bcast(uint64_t v, int lane) {
 
 // ---- Simulator math -----------------------------------
 struct Geo {  // constants hoisted per launch
-  double ts, wheel_dist, dt, off, robot_width, front, rad2deg, two_pi, accept_deg, reset_safety;
+  double ts, inv_ts, wheel_dist, dt, off, robot_width, front, rad2deg, two_pi, accept_deg,
+      reset_safety;
   double robot_speed;
 };
 
+// floor(v / ts) exactly as numpy computes it (correctly rounded division, then
+// floor), via the reciprocal: RN(v * inv_ts) is within 2 ulp of RN(v / ts), so
+// their floors can only differ when the quotient is within a few ulp of an
+// integer — only then is the real division done.
+__device__ inline double floor_div_ts(double v, const Geo& g) {
+  const double q = v * g.inv_ts;
+  const double f = floor(q);
+  const double tol = 1e-12 * (fabs(q) + 1.0);
+  if (q - f < tol || (f + 1.0) - q < tol) return floor(v / g.ts);
+  return f;
+}
+
 // get_grid_coords + _get_tile: tile index or -1 (A5)
 __device__ inline int tile_of(const MapLds& M, const Geo& g, double x, double z) {
-  const double fi = floor(x / g.ts), fj = floor(z / g.ts);
+  const double fi = floor_div_ts(x, g), fj = floor_div_ts(z, g);
   if (fi < 0.0 || fj < 0.0 || fi >= (double)M.width || fj >= (double)M.height) return -1;
   return (int)fj * M.width + (int)fi;
 }
@@ -192,15 +205,36 @@ __device__ inline void bez_xz(const double* __restrict__ cp, double t, double& o
   oz = pz;
 }
 
-__device__ inline double dist_to(const double* __restrict__ cp, double t, double x, double z) {
+// squared distance |B(t) - p|^2, summed as np.linalg.norm's dot (unfused, in order)
+__device__ inline double dist2_to(const double* __restrict__ cp, double t, double x, double z) {
   double bx, by, bz;
   bez_xz(cp, t, bx, by, bz);
   const double a = bx - x, b = by - 0.0, c = bz - z;
-  return sqrt((a * a + b * b) + c * c);
+  return (a * a + b * b) + c * c;
+}
+
+// sqrt(a) < sqrt(b), the comparison bezier_closest makes, decided on the
+// squares: sqrt is monotone, so only when a and b are within a few ulp (where
+// rounding could make the roots equal) are the roots taken.
+__device__ inline bool root_less(double a, double b) {
+  const double d = b - a;
+  if (fabs(d) > 8.0 * 2.220446049250313e-16 * fmax(a, b)) return a < b;
+  return sqrt(a) < sqrt(b);
+}
+
+// angle_rad = acos(dot_dir), negated right of the tangent (get_lane_pos2);
+// lp[2] holds the side value on entry, angle_deg on exit.
+__device__ inline void finish_angle(const Geo& g, double lp[4]) {
+  double ang = acos(lp[1]);
+  if (lp[2] < 0.0) ang = -ang;
+  lp[2] = ang * g.rad2deg;
+  lp[3] = ang;
 }
 
 // get_lane_pos2 (A8-A10).  Returns false when NotInLane.
-// lp = {dist, dot_dir, angle_deg, angle_rad}
+// lp = {dist, dot_dir, angle_deg, angle_rad}; without kAngle the acos is left
+// out and lp[2] holds the side value for finish_angle.
+template <bool kAngle = true>
 __device__ inline bool lane_pos(const MapLds& M, const Geo& g, double x, double z, double c,
                                 double s, double lp[4]) {
   const int t = tile_of(M, g, x, z);
@@ -214,16 +248,16 @@ __device__ inline bool lane_pos(const MapLds& M, const Geo& g, double x, double 
   // the kept half's end was evaluated at the same t one level earlier, and the
   // function is deterministic, so the result is bit-identical to re-evaluating.
   double tb = 0.0, tt = 1.0;
-  double db = dist_to(cp, tb, x, z), dtp = dist_to(cp, tt, x, z);
+  double db = dist2_to(cp, tb, x, z), dtp = dist2_to(cp, tt, x, z);
 #pragma unroll
   for (int n = 8; n > 0; --n) {
     const double mid = (tb + tt) * 0.5;
-    if (db < dtp) {
+    if (root_less(db, dtp)) {
       tt = mid;
-      if (n > 1) dtp = dist_to(cp, tt, x, z);
+      if (n > 1) dtp = dist2_to(cp, tt, x, z);
     } else {
       tb = mid;
-      if (n > 1) db = dist_to(cp, tb, x, z);
+      if (n > 1) db = dist2_to(cp, tb, x, z);
     }
   }
   const double tm = (tb + tt) * 0.5;
@@ -248,12 +282,10 @@ __device__ inline bool lane_pos(const MapLds& M, const Geo& g, double x, double 
   const double rx = 0.0 - tz, rz = tx;
   const double px = x - qx, pz = z - qz;
   const double dist = (px * rx + (0.0 - qy) * 0.0) + pz * rz;
-  double ang = acos(dot);
-  if ((dx * rx + 0.0) + dz * rz < 0.0) ang = -ang;
   lp[0] = dist;
   lp[1] = dot;
-  lp[2] = ang * g.rad2deg;
-  lp[3] = ang;
+  lp[2] = (dx * rx + 0.0) + dz * rz;  // side of the tangent (sign of the angle)
+  if (kAngle) finish_angle(g, lp);
   return true;
 }
 
@@ -277,58 +309,38 @@ __device__ inline bool spawn_try(const MapLds& M, const Geo& g, uint32_t k0, uin
   return -g.accept_deg < lp[2] && lp[2] < g.accept_deg;
 }
 
-// Wave-cooperative Simulator.reset for every lane whose `need` is set.
-// For env e the 64 lanes test proposals k = 64*round + lane in parallel; the
-// lowest accepting lane of the first round with any acceptance wins, which is
-// exactly the first accepted k of a sequential rejection loop over the same
-// i.i.d. stream — so the spawn distribution is upstream's and the result is
-// bit-reproducible by the sequential CPU oracle.
-// All 64 lanes of the wave must call this (uniform control flow).
-__device__ inline void wave_spawn(const MapLds& M, const Geo& g, uint32_t max_attempts,
-                                  bool need, uint32_t env, uint64_t seed, uint32_t episode,
-                                  double& x, double& z, double& ang, bool& failed) {
+// Wave-cooperative Simulator.reset of ONE env (every argument wave-uniform;
+// all 64 lanes must call).  The 64 lanes test proposals k = 64*round + lane in
+// parallel; the lowest accepting lane of the first round with any acceptance
+// wins, which is exactly the first accepted k of a sequential rejection loop
+// over the same i.i.d. stream — so the spawn distribution is upstream's and the
+// result is bit-reproducible by the sequential CPU oracle.  Returns false if
+// max_attempts proposals were all rejected (upstream raises).
+__device__ inline bool spawn_one(const MapLds& M, const Geo& g, uint32_t max_attempts,
+                                 uint32_t env, uint64_t seed, uint32_t episode, double& x,
+                                 double& z, double& ang) {
   const int lane = threadIdx.x & 63;
-  uint64_t pending = __ballot(need);
-  failed = false;
-  while (pending) {
-    const int owner = __ffsll((unsigned long long)pending) - 1;
-    pending &= pending - 1;
-    const uint32_t e = bcast(env, owner);
-    const uint64_t sd = bcast(seed, owner);
-    const uint32_t ep = bcast(episode, owner);
-    const uint32_t k0 = (uint32_t)sd, k1 = (uint32_t)(sd >> 32);
-    const U4 tw = philox(0u, ep, e, kTagTile, k0, k1);
-    int pick = (int)(u01(tw.a, tw.b) * (double)M.n_drivable);
-    pick = pick > M.n_drivable - 1 ? M.n_drivable - 1 : pick;
-    const int ti = M.drivable[pick];
-    const double fi = (double)(ti % M.width), fj = (double)(ti / M.width);
-    bool got = false;
-    double wx = 0, wz = 0, wa = 0;
-    for (uint32_t base = 0; base < max_attempts; base += kWave) {
-      const uint32_t k = base + (uint32_t)lane;
-      double px, pz, pa;
-      const bool ok = (k < max_attempts) &&
-                      spawn_try(M, g, k0, k1, e, ep, k, fi, fj, px, pz, pa);
-      const uint64_t acc = __ballot(ok);
-      if (acc) {
-        const int w = __ffsll((unsigned long long)acc) - 1;
-        wx = bcast(px, w);
-        wz = bcast(pz, w);
-        wa = bcast(pa, w);
-        got = true;
-        break;
-      }
-    }
-    if (lane == owner) {
-      if (got) {
-        x = wx;
-        z = wz;
-        ang = wa;
-      } else {
-        failed = true;
-      }
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  const U4 tw = philox(0u, episode, env, kTagTile, k0, k1);
+  int pick = (int)(u01(tw.a, tw.b) * (double)M.n_drivable);
+  pick = pick > M.n_drivable - 1 ? M.n_drivable - 1 : pick;
+  const int ti = M.drivable[pick];
+  const double fi = (double)(ti % M.width), fj = (double)(ti / M.width);
+  for (uint32_t base = 0; base < max_attempts; base += kWave) {
+    const uint32_t k = base + (uint32_t)lane;
+    double px, pz, pa;
+    const bool ok = (k < max_attempts) && spawn_try(M, g, k0, k1, env, episode, k, fi, fj, px,
+                                                    pz, pa);
+    const uint64_t acc = __ballot(ok);
+    if (acc) {
+      const int w = __ffsll((unsigned long long)acc) - 1;
+      x = bcast(px, w);
+      z = bcast(pz, w);
+      ang = bcast(pa, w);
+      return true;
     }
   }
+  return false;
 }
 
 }  // namespace dt

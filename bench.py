@@ -32,10 +32,13 @@ sys.path.insert(0, REPO)
 METRIC = 'env-steps/sec (whole node) at 4096 envs/GPU; pose/reward max-abs-err vs CPU ref'
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
 
-# Algorithmic HBM bytes per env per dt_step launch (DESIGN.md "step kernel"):
-# reads  x,z,angle 24 + step_count,env_step,episode 12 + action 8           = 44
-# writes x,z,angle 24 + counters 12 + reward 8 + reward_mod 8 + done 1 + obs 8 = 61
-STEP_BYTES_PER_ENV = 44 + 61
+# Algorithmic HBM bytes of one dt_step (step_kernel + spawn_kernel), DESIGN.md §3.1:
+# step, per env:   reads pose 24 + step_count,env_step 8 + action 8             = 40
+#                  writes pose 24 + counters 8 + reward 8 + reward_mod 8 + done 1 + obs 8 = 57
+# spawn, per env:  reads its done flag 1
+#        per reset: reads seed 8 + episode 4; writes pose 24 + counters 12 + obs 8 = 56
+STEP_BYTES_PER_ENV = 40 + 57 + 1
+SPAWN_BYTES_PER_RESET = 56
 
 
 def parse():
@@ -151,7 +154,7 @@ def main():
     def one(i):
         env.step_into(actions[i], out)
         if render is not None:
-            env.render_into(render)
+            env.render_into(render, fresh=out.done)
 
     for i in range(args.warmup):
         one(i)
@@ -172,7 +175,7 @@ def main():
         ev[k][1].record()
         if render is not None:
             rev[k][0].record()
-            env.render_into(render)
+            env.render_into(render, fresh=out.done)
             rev[k][1].record()
     torch.cuda.synchronize(dev)
     if world > 1:
@@ -194,8 +197,9 @@ def main():
 
     if rank == 0:
         if render is None:
-            kname, kms = 'step_kernel', step_ms
-            bytes_per_launch = STEP_BYTES_PER_ENV * n
+            kname, kms = 'step_kernel+spawn_kernel', step_ms
+            bytes_per_launch = STEP_BYTES_PER_ENV * n + SPAWN_BYTES_PER_RESET * resets / max(
+                1.0, decisions / n)
         else:
             from aido1_amd.render import RENDER_BYTES_PER_ENV
             kname, kms = 'render_kernel', render_ms
