@@ -338,6 +338,7 @@ struct RenderArgs {
 //   4  masks: colour bits from img through a v_perm LUT, SWAR ellipse
 //      dilation, edge bits from work; 16 px per lane, four uint4 stores
 // LDS ~71 KB -> two workgroups per CU.
+constexpr int kRenderThreads = 768;  // 12 waves (measured best of 256-1024); LDS per workgroup is fixed (~71 KB)
 constexpr int WPR = W / 4;          // words per row
 constexpr int NW = NPIX / 4;        // words per image
 constexpr int kWeakCap = 2048;
@@ -409,7 +410,7 @@ __device__ inline int mag16(const FusedLds& S, int r, int c) {
                                                                   : 0;
 }
 
-__global__ __launch_bounds__(kThreads) void render_kernel(RenderArgs a) {
+__global__ __launch_bounds__(1024) void render_kernel(RenderArgs a) {
   __shared__ __attribute__((aligned(16))) FusedLds S;
   const int e = blockIdx.x;
   const int tid = threadIdx.x;
@@ -758,6 +759,10 @@ int dt_render_init(dt_handle* h, const dt_map* map) {
   h->line = to_line_dev(h->line_params);
   const char* sk = getenv("DTSIM_RENDER_SKIP");  // diagnostics: phase ablation
   h->render_skip = sk ? atoi(sk) : 0;
+  const char* th = getenv("DTSIM_RENDER_THREADS");  // tuning: workgroup size
+  h->render_threads = th ? atoi(th) : kRenderThreads;
+  if (h->render_threads < 64 || h->render_threads > 1024 || (h->render_threads & 63))
+    h->render_threads = kRenderThreads;
   return DT_OK;
 }
 
@@ -825,7 +830,8 @@ int dt_render(dt_handle* h, const dt_render_io* io, void* stream) {
   a.line = h->line;
   a.n = h->n;
   a.skip = h->render_skip;
-  hipLaunchKernelGGL(render_kernel, dim3(h->n), dim3(kThreads), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(render_kernel, dim3(h->n), dim3(h->render_threads), 0, (hipStream_t)stream,
+                     a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     h->err = std::string("dt_render launch: ") + hipGetErrorString(e);

@@ -194,18 +194,21 @@ __global__ __launch_bounds__(64) void step_kernel(dt::State st, dt::MapDev md, d
 // instead of one after another inside their step wave.  flags: NULL = every
 // env, else envs with flags[e] != 0 (the reset mask, or dt_step's done flags
 // for the auto-reset).  obs (nullable) receives the new (dist, angle_rad).
-__global__ __launch_bounds__(64) void spawn_kernel(dt::State st, dt::MapDev md, dt::Geo g,
+constexpr int kSpawnThreads = 256;  // proposals per round: one accept in ~37, so ~1 round
+
+__global__ __launch_bounds__(kSpawnThreads) void spawn_kernel(dt::State st, dt::MapDev md, dt::Geo g,
                                                    uint32_t max_attempts, uint32_t env_base,
                                                    const uint8_t* __restrict__ flags,
                                                    float2* __restrict__ obs) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const int e = blockIdx.x;
   if (flags != nullptr && flags[e] == 0) return;  // block-uniform
+  __shared__ double scratch[6 * (kSpawnThreads / 64)];
   const MapLds M = dt::stage_map(md, lds);
-  double x = 0.0, z = 0.0, ang = 0.0;
+  double x = 0.0, z = 0.0, ang = 0.0, dist = 0.0, arad = 0.0;
   const uint32_t episode = st.episode[e];
-  const bool ok = dt::spawn_one(M, g, max_attempts, env_base + (uint32_t)e, st.seed[e], episode,
-                                x, z, ang);
+  const bool ok = dt::spawn_block(M, g, max_attempts, env_base + (uint32_t)e, st.seed[e],
+                                  episode, scratch, x, z, ang, dist, arad);
   if (threadIdx.x != 0) return;
   if (!ok) {
     atomicOr(st.err, dt::kErrSpawn);
@@ -218,12 +221,7 @@ __global__ __launch_bounds__(64) void spawn_kernel(dt::State st, dt::MapDev md, 
   st.env_step[e] = 0u;
   st.episode[e] = episode + 1u;
   atomicAdd(st.stats + 2, 1ull);
-  if (obs) {
-    double s, c, lp[4];
-    sincos(ang, &s, &c);
-    const bool inl = dt::lane_pos<true>(M, g, x, z, c, s, lp);
-    obs[e] = inl ? make_float2((float)lp[0], (float)lp[3]) : make_float2(0.0f, 0.0f);
-  }
+  if (obs) obs[e] = make_float2((float)dist, (float)arad);  // accepted => in a lane
 }
 
 __global__ __launch_bounds__(64) void lane_pos_kernel(dt::State st, dt::MapDev md, dt::Geo g,
@@ -418,8 +416,9 @@ int dt_seed(dt_handle* h, const uint64_t* seeds, uint64_t base, uint32_t env_id_
 int dt_reset(dt_handle* h, const uint8_t* mask, void* stream) {
   if (!h) return DT_E_ARG;
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(spawn_kernel, dim3(h->n), dim3(dt::kWave), h->lds_bytes, s, h->st, h->map,
-                     h->geo, h->sc.max_spawn_attempts, h->env_base, mask, (float2*)nullptr);
+  hipLaunchKernelGGL(spawn_kernel, dim3(h->n), dim3(kSpawnThreads), h->lds_bytes, s, h->st,
+                     h->map, h->geo, h->sc.max_spawn_attempts, h->env_base, mask,
+                     (float2*)nullptr);
   HIP_OR_FAIL(h, hipGetLastError());
   return DT_OK;
 }
@@ -437,9 +436,9 @@ int dt_step(dt_handle* h, const float* actions, double* reward, double* reward_m
                      done, (float2*)obs, lanepos, tile);
   HIP_OR_FAIL(h, hipGetLastError());
   if (h->sc.auto_reset) {
-    hipLaunchKernelGGL(spawn_kernel, dim3(h->n), dim3(dt::kWave), h->lds_bytes, s, h->st, h->map,
-                       h->geo, h->sc.max_spawn_attempts, h->env_base, (const uint8_t*)done,
-                       (float2*)obs);
+    hipLaunchKernelGGL(spawn_kernel, dim3(h->n), dim3(kSpawnThreads), h->lds_bytes, s, h->st,
+                       h->map, h->geo, h->sc.max_spawn_attempts, h->env_base,
+                       (const uint8_t*)done, (float2*)obs);
     HIP_OR_FAIL(h, hipGetLastError());
   }
   return DT_OK;

@@ -292,7 +292,8 @@ __device__ inline bool lane_pos(const MapLds& M, const Geo& g, double x, double 
 // One spawn proposal (A13): returns true if accepted.
 __device__ inline bool spawn_try(const MapLds& M, const Geo& g, uint32_t k0, uint32_t k1,
                                  uint32_t env, uint32_t episode, uint32_t k, double fi,
-                                 double fj, double& ox, double& oz, double& oa) {
+                                 double fj, double& ox, double& oz, double& oa,
+                                 double* lp_out = nullptr) {
   const U4 a = philox(k, episode, env, kTagSpawnA, k0, k1);
   const U4 b = philox(k, episode, env, kTagSpawnB, k0, k1);
   const double px = (fi + u01(a.a, a.b)) * g.ts;
@@ -306,6 +307,10 @@ __device__ inline bool spawn_try(const MapLds& M, const Geo& g, uint32_t k0, uin
   if (!valid_pose(M, g, px, pz, c, s, g.reset_safety)) return false;
   double lp[4];
   if (!lane_pos(M, g, px, pz, c, s, lp)) return false;
+  if (lp_out) {
+    lp_out[0] = lp[0];
+    lp_out[1] = lp[3];
+  }
   return -g.accept_deg < lp[2] && lp[2] < g.accept_deg;
 }
 
@@ -339,6 +344,63 @@ __device__ inline bool spawn_one(const MapLds& M, const Geo& g, uint32_t max_att
       ang = bcast(pa, w);
       return true;
     }
+  }
+  return false;
+}
+
+// The same over a whole workgroup (every thread calls; nthreads = blockDim.x, a
+// multiple of 64): proposals k = nthreads*round + tid; per round each wave
+// publishes its lowest accepting lane in LDS, and the lowest accepting wave
+// wins -- again the first accepted k of the sequential loop.  `scratch` is 48 B
+// per wave of LDS.  The winner's lane position (dist, angle_rad) comes back too.
+__device__ inline bool spawn_block(const MapLds& M, const Geo& g, uint32_t max_attempts,
+                                   uint32_t env, uint64_t seed, uint32_t episode,
+                                   double* scratch, double& x, double& z, double& ang,
+                                   double& dist, double& angle_rad) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
+  const U4 tw = philox(0u, episode, env, kTagTile, k0, k1);
+  int pick = (int)(u01(tw.a, tw.b) * (double)M.n_drivable);
+  pick = pick > M.n_drivable - 1 ? M.n_drivable - 1 : pick;
+  const int ti = M.drivable[pick];
+  const double fi = (double)(ti % M.width), fj = (double)(ti / M.width);
+  double* wx = scratch;              // [nw]
+  double* wz = scratch + nw;         // [nw]
+  double* wa = scratch + 2 * nw;     // [nw]
+  double* wd = scratch + 3 * nw;     // [nw] lane dist of the winner
+  double* wr = scratch + 4 * nw;     // [nw] lane angle_rad of the winner
+  int* flag = reinterpret_cast<int*>(scratch + 5 * nw);  // [nw]
+  for (uint32_t base = 0; base < max_attempts; base += blockDim.x) {
+    const uint32_t k = base + (uint32_t)tid;
+    double px, pz, pa, lpo[2] = {0.0, 0.0};
+    const bool ok = (k < max_attempts) && spawn_try(M, g, k0, k1, env, episode, k, fi, fj, px,
+                                                    pz, pa, lpo);
+    const uint64_t acc = __ballot(ok);
+    const int first = acc ? __ffsll((unsigned long long)acc) - 1 : -1;
+    if (lane == 0) flag[wave] = first;
+    if (first >= 0 && lane == first) {
+      wx[wave] = px;
+      wz[wave] = pz;
+      wa[wave] = pa;
+      wd[wave] = lpo[0];
+      wr[wave] = lpo[1];
+    }
+    __syncthreads();
+    int win = -1;
+    for (int w = 0; w < nw; ++w)
+      if (flag[w] >= 0) {
+        win = w;
+        break;
+      }
+    if (win >= 0) {
+      x = wx[win];
+      z = wz[win];
+      ang = wa[win];
+      dist = wd[win];
+      angle_rad = wr[win];
+    }
+    __syncthreads();
+    if (win >= 0) return true;
   }
   return false;
 }

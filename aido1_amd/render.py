@@ -66,12 +66,16 @@ class RenderOutput:
     ring (the Transformer's stack, see stack_view), the 4 line masks of the
     latest frame, optionally the RGB raster."""
 
-    def __init__(self, n, device, slots=3, rgb=False, masks=True):
+    def __init__(self, n, device, slots=3, rgb=False, masks=True, ring=None):
         self.n = n
         self.slots = slots
         self.slot = -1  # slot of the newest frame
         self._all = torch.ones(n, dtype=torch.uint8, device=device)
-        self.ring = torch.zeros(n, slots, H, W, dtype=torch.float32, device=device)
+        if ring is not None:  # a contiguous [n, slots, 120, 160] f32 view (e.g. a slice)
+            assert ring.is_contiguous() and tuple(ring.shape) == (n, slots, H, W)
+            assert ring.dtype == torch.float32
+        self.ring = ring if ring is not None else torch.zeros(n, slots, H, W,
+                                                              dtype=torch.float32, device=device)
         self.masks = torch.zeros(n, 4, H, W, dtype=torch.uint8, device=device) if masks else None
         self.rgb = torch.zeros(n, H, W, 3, dtype=torch.uint8, device=device) if rgb else None
 

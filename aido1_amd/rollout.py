@@ -1,0 +1,131 @@
+"""Actor-in-loop batched rollout (BASELINE configs[3]).
+
+One GPU runs `n_envs` environments split over maps (mixed small_loop /
+zigzag), all rendering into ONE shared frame ring so a single actor forward
+covers every env.  Per decision:
+
+  actor (bf16, BN folded, ring read zero-copy)  -> DDPG.act noise / every-
+  second-random (explore.py)  -> dt_step per map handle (tanh head mapping,
+  repeat 3, reward shaping, respawn) -> dt_render per handle into the ring
+  (+ line masks) -> OU reset for finished envs
+
+which is SingleThreadExplorer._explore_episode's loop body
+(training/explorers.py:177-211) for thousands of explorers at once.
+"""
+import math
+
+import numpy as np
+import torch
+
+from aido1_amd.actor import ConfigActor, FusedActor
+from aido1_amd.config import EnvConfig
+from aido1_amd.explore import OUNoise, explore_actions
+from aido1_amd.render import H, W, RenderOutput
+from aido1_amd.vec_env import StepOutput, VecEnv
+
+
+class CycleEpsilon:
+    """Vectorised EpsilonSchedule: per-env cycle length in [L/2, 2L]
+    (explorers.py:92-99), epsilon = clip(cycle_decay(episode), final, initial)."""
+
+    def __init__(self, config, n, device, generator=None):
+        t = config['training']
+        L = t['epsilon_cycle_len']
+        self.i, self.f = t['initial_epsilon'], t['final_epsilon']
+        self.cl = torch.randint(L // 2, 2 * L + 1, (n,), device=device,
+                                generator=generator).double()
+        self.max_step = self.cl * torch.floor(t['max_episodes'] / self.cl)
+
+    def __call__(self, episodes):
+        ep = episodes.double()
+        rel = 1.0 - ep / self.max_step
+        cosv = 0.5 * (torch.cos(math.pi * torch.remainder(ep, self.cl) / self.cl) + 1.0)
+        return (cosv * (self.i - self.f) * rel + self.f).clamp(self.f, self.i)
+
+
+class ActorRollout:
+    def __init__(self, config, n_envs=4096, maps=('small_loop', 'zigzag'), device=0, seed=1234,
+                 env_id_base=0, actor=None, dtype=torch.bfloat16, masks=True):
+        self.config = config
+        self.device = torch.device('cuda', device)
+        self.n = n_envs
+        k = len(maps)
+        sizes = [n_envs // k + (1 if i < n_envs % k else 0) for i in range(k)]
+        self.ring = torch.zeros(n_envs, 3, H, W, dtype=torch.float32, device=self.device)
+        self.masks = torch.zeros(n_envs, 4, H, W, dtype=torch.uint8, device=self.device) \
+            if masks else None
+        self.actions = torch.zeros(n_envs, 2, dtype=torch.float32, device=self.device)
+        self.reward = torch.zeros(n_envs, dtype=torch.float64, device=self.device)
+        self.reward_mod = torch.zeros(n_envs, dtype=torch.float64, device=self.device)
+        self.done = torch.zeros(n_envs, dtype=torch.uint8, device=self.device)
+        self.envs, self.outs, self.renders, self.slices = [], [], [], []
+        head = config['model']['actor'][-1]['modules'][-1][-1]['name']
+        self.head = head
+        off = 0
+        for m, sz in zip(maps, sizes):
+            ec = EnvConfig.from_reference_config(config, map_name=m)
+            env = VecEnv(sz, seed=seed, device=device, config=ec, env_id_base=env_id_base + off)
+            sl = slice(off, off + sz)
+            out = StepOutput(sz, self.device, lanepos=False, tile=False)
+            out.reward, out.reward_mod, out.done = self.reward[sl], self.reward_mod[sl], \
+                self.done[sl]
+            ro = RenderOutput(sz, self.device, slots=3, ring=self.ring[sl],
+                              masks=False)
+            if masks:
+                ro.masks = self.masks[sl]
+            self.envs.append(env)
+            self.outs.append(out)
+            self.renders.append(ro)
+            self.slices.append(sl)
+            off += sz
+        if actor is None:
+            actor = ConfigActor(config['model']['actor'])
+            actor.eval()
+        self.actor = FusedActor(actor, dtype=dtype).to(self.device)
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(seed + 17 * env_id_base)
+        self.ou = OUNoise.from_config(config, n_envs, device=self.device, generator=self.gen)
+        self.eps = CycleEpsilon(config, n_envs, self.device, generator=self.gen)
+        self.episode = torch.zeros(n_envs, dtype=torch.int64, device=self.device)
+        self.explorer_id = torch.arange(env_id_base, env_id_base + n_envs, device=self.device)
+        self.actor_events = None
+
+    def reset(self):
+        for env, ro in zip(self.envs, self.renders):
+            env.reset()
+            ro.restart()
+            env.render_into(ro)
+        self.ou.reset_states()
+        self.episode.zero_()
+
+    def order(self):
+        return self.renders[0].order()
+
+    def step(self, timing=None):
+        """One decision for every env; returns (reward, reward_mod, done) views."""
+        if timing is not None:
+            timing[0].record()
+        out = self.actor(self.ring, self.order())
+        if timing is not None:
+            timing[1].record()
+        eps = self.eps(self.episode)
+        self.actions.copy_(explore_actions(out, self.ou, eps, self.explorer_id, self.config,
+                                           generator=self.gen, head=self.head))
+        for env, o, ro, sl in zip(self.envs, self.outs, self.renders, self.slices):
+            env.step_into(self.actions[sl], o)
+            env.render_into(ro, fresh=o.done)
+        d = self.done.bool()
+        self.ou.reset_states(d)
+        self.episode += d.long()
+        return self.reward, self.reward_mod, self.done
+
+    def stats(self, reset=False):
+        tot = {}
+        for env in self.envs:
+            for k, v in env.stats(reset).items():
+                tot[k] = tot.get(k, 0) + v
+        return tot
+
+    def close(self):
+        for env in self.envs:
+            env.close()

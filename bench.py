@@ -48,7 +48,7 @@ def parse():
     p.add_argument('--warmup', type=int, default=30)
     p.add_argument('--envs', type=int, default=4096)
     p.add_argument('--map', default='loop_empty')
-    p.add_argument('--config', default='lane', choices=['lane', 'render'])
+    p.add_argument('--config', default='lane', choices=['lane', 'render', 'actor'])
     p.add_argument('--seed', type=int, default=1234)
     p.add_argument('--cpu-seconds', type=float, default=1.5,
                    help='per-process seconds of the CPU baseline sample (0 = skip)')
@@ -137,6 +137,8 @@ def main():
     from aido1_amd.vec_env import StepOutput, VecEnv
 
     n = args.envs
+    if args.config == 'actor':
+        return bench_actor(args, dev, rank, world, dist)
     env = VecEnv(n, seed=args.seed, device=dev.index,
                  config=EnvConfig(map_name=args.map), env_id_base=rank * n)
     out = StepOutput(n, dev, lanepos=False, tile=False)
@@ -242,6 +244,72 @@ def main():
             line['cpu_baseline'] = None
         print(json.dumps(line), flush=True)
     env.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 MFMA (spec)
+
+
+def bench_actor(args, dev, rank, world, dist):
+    """BASELINE configs[3]: 4096 envs/GPU, mixed small_loop/zigzag, actor in the loop."""
+    import torch
+    from aido1_amd.actor import flops_per_sample
+    from aido1_amd.rollout import ActorRollout
+    with open(os.path.join(REPO, 'aido1_amd', 'configs', 'reference_config.json')) as f:
+        cfg = json.load(f)
+    n = args.envs
+    torch.manual_seed(args.seed)
+    roll = ActorRollout(cfg, n, maps=('small_loop', 'zigzag'), device=dev.index, seed=args.seed,
+                        env_id_base=rank * n)
+    roll.reset()
+    for _ in range(args.warmup):
+        roll.step()
+    torch.cuda.synchronize(dev)
+    roll.stats(reset=True)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        roll.step(timing=ev[k])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    st = roll.stats()
+    actor_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    sims = torch.tensor([st['sim_steps'], st['decisions'], st['resets']], dtype=torch.float64,
+                        device=dev)
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(sims, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    sim_steps, decisions, resets = (float(v) for v in sims.tolist())
+    tmax = float(tmax.item())
+    if rank == 0:
+        tflops = n * flops_per_sample() / (actor_ms * 1e-3) / 1e12
+        print(json.dumps({
+            'metric': METRIC, 'value': sim_steps / tmax, 'unit': 'env-steps/s', 'n_gpus': world,
+            'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': tmax / args.steps * 1e3,
+            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+            'dtype': 'f64 env / bf16 actor', 'data': 'synthetic',
+            'config': {'workload': 'config4: %d envs/GPU, actor in the loop (ConfigActor, '
+                                   'config.json), mixed small_loop/zigzag' % n,
+                       'envs_per_gpu': n, 'global_envs': n * world, 'repeat_actions': 3,
+                       'weights': 'random init (no checkpoint offline)',
+                       'parallelism': 'env shards (%d x %d), no collective' % (world, n)},
+            'counts': {'env_steps': sim_steps, 'decisions': decisions, 'resets': resets,
+                       'elapsed_s': tmax},
+            'roofline': {'bound': 'mfma', 'kernel': 'actor forward (bf16 convs + linears)',
+                         'achieved': tflops, 'peak': BF16_DENSE_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                         'frac': tflops / BF16_DENSE_PEAK_TFLOPS, 'traffic': None,
+                         'avg_kernel_ms': actor_ms,
+                         'algorithmic_flops_per_launch': n * flops_per_sample()},
+            'cpu_baseline': None}), flush=True)
+    roll.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -299,49 +299,23 @@ def gen_random_process_and_decay():
                                  'decay': decays})
 
 
-def formula_state_dict(model):
-    """Deterministic, torch-version-independent weights for the actor fixtures."""
-    import torch
-    sd = {}
-    for k, (name, t) in enumerate(model.state_dict().items()):
-        n = t.numel()
-        idx = torch.arange(n, dtype=torch.float64)
-        if name.endswith('num_batches_tracked'):
-            sd[name] = t.clone()
-        elif name.endswith('running_var'):
-            sd[name] = (1.0 + 0.25 * torch.sin(0.7 * idx + k)).reshape(t.shape).float()
-        elif name.endswith('running_mean'):
-            sd[name] = (0.1 * torch.cos(0.3 * idx + k)).reshape(t.shape).float()
-        else:
-            fan = max(1, n // t.shape[0]) if t.dim() > 1 else 16
-            sd[name] = (math.sqrt(2.0 / fan) * torch.sin(0.37 * idx + 1.3 * k)).reshape(
-                t.shape).float()
-    return sd
-
-
-def formula_input(n):
-    """Deterministic [n,3,120,160] float32 frames in [0,1] (tests rebuild it)."""
-    import torch
-    idx = torch.arange(n * 3 * 120 * 160, dtype=torch.float64)
-    return (0.5 + 0.5 * torch.sin(0.013 * idx) * torch.cos(0.0007 * idx)).reshape(
-        n, 3, 120, 160).float()
-
-
 def gen_actor():
     import torch
     from duckietown_rl.ddpg import ActorCNN
     from models.ddpg.modules import Actor
+    sys.path.insert(0, HERE)
+    from formulas import formula_input, formula_state_dict
     with open(os.path.join(REF, 'config.json')) as f:
         config = json.load(f)
     x = formula_input(4)
     out = {}
     a = ActorCNN(2, 1.0)
-    a.load_state_dict(formula_state_dict(a))
+    a.load_state_dict(formula_state_dict(a.state_dict()))
     a.eval()
     with torch.no_grad():
         out['actor_cnn'] = a(x).numpy()
     c = Actor(config['model']['actor'])
-    c.load_state_dict(formula_state_dict(c))
+    c.load_state_dict(formula_state_dict(c.state_dict()))
     c.eval()
     with torch.no_grad():
         out['config_actor'] = c(x).numpy()
@@ -351,8 +325,28 @@ def gen_actor():
     print('wrote actor.npz')
 
 
+def gen_config_keys():
+    """The config.json keys the env path reads (wrapper section, actor head, the
+    explorer's noise/epsilon keys) — a data extract, not the file."""
+    with open(os.path.join(REF, 'config.json')) as f:
+        cfg = json.load(f)
+    head = cfg['model']['actor'][-1]['modules'][-1][-1]['name']
+    keys = ('global_seed', 'rp_theta', 'rp_mu', 'rp_sigma', 'rp_sigma_min', 'epsilon_cycle_len',
+            'initial_epsilon', 'final_epsilon', 'epsilon_ratio', 'max_episodes',
+            'every_second_random', 'alpha', 'beta', 'batch_size', 'buffer_size', 'gamma', 'tau')
+    mini = {'environment': {'wrapper': cfg['environment']['wrapper']},
+            'model': {'num_action': cfg['model']['num_action'], 'actor': cfg['model']['actor'],
+                      'critic': cfg['model']['critic']},
+            'training': {k: cfg['training'][k] for k in keys}}
+    assert mini['model']['actor'][-1]['modules'][-1][-1]['name'] == head
+    with open(os.path.join(HERE, 'reference_config.json'), 'w') as f:
+        json.dump(mini, f, indent=1)
+    print('wrote reference_config.json')
+
+
 def main():
     sys.path.insert(0, REF)
+    gen_config_keys()
     install_stubs()
     gen_bresenham()
     gen_aggregation()

@@ -1,0 +1,65 @@
+"""Actor: the reference's two actor layouts reproduced with
+identical parameter names, against golden outputs of the reference's own
+modules (tests/golden/actor.npz, formula weights from tests/golden/formulas.py),
+and the BN-folded inference copy against the eval-mode actor."""
+import os
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, golden
+
+sys.path.insert(0, GOLDEN)
+from formulas import formula_input, formula_state_dict  # noqa: E402
+
+
+def test_actor_cnn_golden():
+    from aido1_amd.actor import ActorCNN
+    g = golden('actor.npz')
+    a = ActorCNN(2, 1.0)
+    assert list(a.state_dict().keys()) == [str(k) for k in g['actor_cnn_keys']]
+    a.load_state_dict(formula_state_dict(a.state_dict()))
+    a.eval()
+    with torch.no_grad():
+        y = a(formula_input(4)).numpy()
+    assert np.max(np.abs(y - g['actor_cnn'])) < 1e-5
+
+
+def test_config_actor_golden():
+    from aido1_amd.actor import ConfigActor
+    g = golden('actor.npz')
+    cfg = golden('reference_config.json')
+    a = ConfigActor(cfg['model']['actor'])
+    assert list(a.state_dict().keys()) == [str(k) for k in g['config_actor_keys']]
+    a.load_state_dict(formula_state_dict(a.state_dict()))
+    a.eval()
+    with torch.no_grad():
+        y = a(formula_input(4)).numpy()
+    assert np.max(np.abs(y - g['config_actor'])) < 1e-5
+
+
+@pytest.mark.parametrize('kind', ['cnn', 'config'])
+def test_fused_actor_matches_eval_fp32(kind):
+    from aido1_amd.actor import ActorCNN, ConfigActor, FusedActor
+    a = ActorCNN(2, 1.0) if kind == 'cnn' else ConfigActor(golden('reference_config.json')['model']['actor'])
+    a.load_state_dict(formula_state_dict(a.state_dict()))
+    a.eval()
+    f = FusedActor(a, dtype=torch.float32)
+    x = formula_input(4)
+    with torch.no_grad():
+        ref = a(x)
+    assert torch.max(torch.abs(f(x) - ref)) < 1e-4
+    # ring order: feeding the slots in ring order with `order` == feeding the stack
+    order = [2, 0, 1]
+    ring = torch.empty_like(x)
+    for c, sl in enumerate(order):
+        ring[:, sl] = x[:, c]
+    assert torch.max(torch.abs(f(ring, order) - ref)) < 1e-4
+
+
+def test_flops_figure():
+    from aido1_amd.actor import flops_per_sample
+    # 50.8 M MAC = 101.6 MFLOP per env per decision
+    assert abs(flops_per_sample() / 1e6 - 101.6) < 0.2

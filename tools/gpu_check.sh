@@ -20,6 +20,9 @@ run bench 600 python bench.py --steps $STEPS --warmup 30 ${BENCH_ARGS}
 if [ -n "$RENDER" ]; then
   run bench_render 600 python bench.py --config render --steps $STEPS --warmup 30 --cpu-seconds 0
 fi
+if [ -n "$ACTOR" ]; then
+  run bench_actor 600 python bench.py --config actor --steps 100 --warmup 10 --cpu-seconds 0
+fi
 if [ -n "$PROFILE" ]; then
   export TMPDIR=/tmp
   run rocprof 600 rocprofv3 --kernel-trace --stats -d "$ROOT/gpurun_out/prof" -o run \
