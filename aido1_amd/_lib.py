@@ -17,8 +17,9 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_PATH = os.path.join(PKG_DIR, 'libdtsim.so')
 CSRC = os.path.join(PKG_DIR, 'csrc')
-SOURCES = ['dtsim.hip', 'dtrender.hip']
+SOURCES = ['dtsim.hip', 'dtrender.hip', 'dtreplay.hip']
 HEADERS = ['dtsim_common.h', 'dtrender.h']
+PUBLIC_HEADERS = ['dtsim.h', 'dtreplay.h']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ABI_VERSION = 1
 
@@ -45,7 +46,7 @@ def _stale():
         return True
     t = os.path.getmtime(LIB_PATH)
     deps = _sources() + [os.path.join(CSRC, h) for h in HEADERS] + \
-        [os.path.join(REPO_DIR, 'include', 'dtsim.h')]
+        [os.path.join(REPO_DIR, 'include', h) for h in PUBLIC_HEADERS]
     return any(os.path.exists(d) and os.path.getmtime(d) > t for d in deps)
 
 
@@ -87,6 +88,7 @@ def lib():
             build()
         L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
         vp, i32, u32, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64
+        i64, f64 = ctypes.c_int64, ctypes.c_double
         sig = {
             'dt_abi_version': (i32, []),
             'dt_create': (ctypes.c_int, [ctypes.POINTER(DtConfig), ctypes.POINTER(DtMap), u64, i32,
@@ -106,6 +108,18 @@ def lib():
             'dt_set_state': (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp]),
             'dt_check': (ctypes.c_int, [vp, ctypes.POINTER(u32)]),
             'dt_stats': (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), i32]),
+            # dtreplay.h
+            'dt_per_create': (ctypes.c_int, [i64, f64, i32, ctypes.POINTER(vp)]),
+            'dt_per_destroy': (None, [vp]),
+            'dt_per_last_error': (ctypes.c_char_p, [vp]),
+            'dt_per_capacity': (i64, [vp]),
+            'dt_per_len': (i64, [vp]),
+            'dt_per_next_idx': (i64, [vp]),
+            'dt_per_add': (ctypes.c_int, [vp, i64, vp, vp]),
+            'dt_per_sample': (ctypes.c_int, [vp, i32, vp, f64, vp, vp, vp]),
+            'dt_per_update': (ctypes.c_int, [vp, i32, vp, vp, vp]),
+            'dt_per_read': (ctypes.c_int, [vp, vp, vp, vp, vp]),
+            'dt_per_check': (ctypes.c_int, [vp]),
         }
         for name, (res, args) in sig.items():
             if not hasattr(L, name):
@@ -123,12 +137,15 @@ def lib():
 
 
 def exported_symbols():
-    """Names declared in include/dtsim.h (checked against the .so by tests)."""
+    """Names declared in include/*.h (checked against the .so by tests)."""
     import re
-    with open(os.path.join(REPO_DIR, 'include', 'dtsim.h')) as f:
-        src = f.read()
-    return sorted(set(re.findall(r'^\s*(?:int|int32_t|const char\*)\s+(dt_\w+)\s*\(', src,
-                                 re.M)))
+    names = set()
+    for h in PUBLIC_HEADERS:
+        with open(os.path.join(REPO_DIR, 'include', h)) as f:
+            src = f.read()
+        names |= set(re.findall(r'^\s*(?:int|int32_t|int64_t|void|const char\*)\s+(dt_\w+)\s*\(',
+                                src, re.M))
+    return sorted(names)
 
 
 def check(L, handle, rc, what):

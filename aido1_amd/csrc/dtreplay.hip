@@ -1,0 +1,350 @@
+// GPU prioritized replay: the sum/min segment trees of utils/segment_tree.py
+// and the index logic of utils/buffers.py:140-259 (PrioritizedReplayBuffer),
+// batched.  See include/dtreplay.h for the contract.
+//
+// Exactness: every tree node is combined from its two children exactly as
+// SegmentTree.__setitem__ does (segment_tree.py:77-87), so after a batch of
+// leaf writes the bottom-up recompute of the touched paths leaves the same
+// float64 values the reference's one-at-a-time loop leaves; the prefix-sum
+// descent and the range sum use the reference's comparison / subtraction /
+// nesting order, so sampled indices are bit-identical for the same uniforms.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+
+#include "../../include/dtreplay.h"
+
+struct dt_per {
+  int device = 0;
+  int64_t size = 0, cap = 0, len = 0, next = 0;
+  int log2cap = 0;
+  double alpha = 0.0;
+  double* sum = nullptr;   // [2*cap]
+  double* mn = nullptr;    // [2*cap]
+  double* maxp = nullptr;  // [1]
+  int32_t* winner = nullptr;  // [cap], -1 when idle
+  int32_t* err = nullptr;     // [1] bit 0: bad priority, bit 1: bad index
+  void* buf = nullptr;
+  std::string msg;
+};
+
+namespace {
+
+constexpr int kTreeThreads = 1024;
+constexpr int kSampleThreads = 256;
+constexpr int kMaxDepth = 40;
+
+// Python's min(a, b): the first argument unless the second is smaller.
+__device__ __forceinline__ double py_min(double a, double b) { return b < a ? b : a; }
+
+__device__ __forceinline__ void recompute(double* sum, double* mn, int64_t node) {
+  sum[node] = sum[2 * node] + sum[2 * node + 1];
+  mn[node] = py_min(mn[2 * node], mn[2 * node + 1]);
+}
+
+__global__ void fill_kernel(double* sum, double* mn, double* maxp, int32_t* winner, int64_t cap) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < 2 * cap;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    sum[i] = 0.0;
+    mn[i] = INFINITY;
+    if (i < cap) winner[i] = -1;
+  }
+  if (blockIdx.x == 0 && threadIdx.x == 0) *maxp = 1.0;
+}
+
+// n adds starting at slot `next`; one workgroup walks the touched leaf ranges
+// (at most two: the batch may wrap at `size`) up to the root level by level.
+__global__ void __launch_bounds__(kTreeThreads)
+add_kernel(double* sum, double* mn, const double* maxp, int64_t cap, int log2cap, int64_t size,
+           int64_t next, int64_t n, double alpha, int64_t* slots) {
+  const double v = pow(*maxp, alpha);  // buffers.py:173-174
+  for (int64_t k = threadIdx.x; k < n; k += blockDim.x) {
+    const int64_t s = (next + k) % size;
+    if (slots) slots[k] = s;
+  }
+  const int64_t m = n < size ? n : size;  // distinct slots written
+  int64_t lo[2], hi[2];
+  const int64_t end = next + m;
+  lo[0] = cap + next;
+  hi[0] = cap + (end < size ? end : size);
+  lo[1] = cap;
+  hi[1] = cap + (end > size ? end - size : 0);
+  for (int r = 0; r < 2; ++r)
+    for (int64_t i = lo[r] + threadIdx.x; i < hi[r]; i += blockDim.x) {
+      sum[i] = v;
+      mn[i] = v;
+    }
+  for (int l = 0; l < log2cap; ++l) {
+    __syncthreads();
+    for (int r = 0; r < 2; ++r) {
+      if (hi[r] <= lo[r]) continue;
+      lo[r] >>= 1;
+      hi[r] = ((hi[r] - 1) >> 1) + 1;
+      for (int64_t i = lo[r] + threadIdx.x; i < hi[r]; i += blockDim.x) recompute(sum, mn, i);
+    }
+  }
+}
+
+__device__ double block_max(double v, double* scratch) {
+  for (int o = 32; o > 0; o >>= 1) v = fmax(v, __shfl_xor(v, o));
+  const int w = threadIdx.x / 64, nw = blockDim.x / 64;
+  if ((threadIdx.x & 63) == 0) scratch[w] = v;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double r = scratch[0];
+    for (int i = 1; i < nw; ++i) r = fmax(r, scratch[i]);
+    scratch[0] = r;
+  }
+  __syncthreads();
+  return scratch[0];
+}
+
+__global__ void __launch_bounds__(kTreeThreads)
+update_kernel(double* sum, double* mn, double* maxp, int32_t* winner, int32_t* err, int64_t cap,
+              int log2cap, int64_t len, int32_t n, const int64_t* idx, const double* prio,
+              double alpha) {
+  __shared__ double scratch[kTreeThreads / 64];
+  double pmax = 0.0;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int64_t j = idx[i];
+    const double p = prio[i];
+    const bool ok_p = p > 0.0;  // false for NaN too
+    const bool ok_i = j >= 0 && j < len;
+    if (!ok_p) atomicOr(err, 1);
+    if (!ok_i) atomicOr(err, 2);
+    if (ok_p && ok_i) {
+      atomicMax(&winner[j], i);  // the sequential loop's last write wins
+      pmax = fmax(pmax, p);
+    }
+  }
+  pmax = block_max(pmax, scratch);  // also the barrier after the atomics
+  if (threadIdx.x == 0 && pmax > *maxp) *maxp = pmax;
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int64_t j = idx[i];
+    if (j >= 0 && j < len && prio[i] > 0.0 && winner[j] == i) {
+      const double v = pow(prio[i], alpha);
+      sum[cap + j] = v;
+      mn[cap + j] = v;
+    }
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < n; i += blockDim.x) {
+    const int64_t j = idx[i];
+    if (j >= 0 && j < len) winner[j] = -1;
+  }
+  // the ancestors of every written leaf, level by level; a node shared by
+  // several leaves is recomputed redundantly to the same value
+  for (int l = 1; l <= log2cap; ++l) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      const int64_t j = idx[i];
+      if (j >= 0 && j < len && prio[i] > 0.0) recompute(sum, mn, (cap + j) >> l);
+    }
+  }
+}
+
+// reduce(0, len - 1) of segment_tree.py:37-74 for the sum tree: the recursion
+// with start == node_start peels exact left children, combined right-nested:
+// a1 + (a2 + (... + ak)).
+__device__ double prefix_range_sum(const double* sum, int64_t cap, int64_t end) {
+  double vals[kMaxDepth];
+  int k = 0;
+  int64_t node = 1, ns = 0, ne = cap - 1;
+  while (true) {
+    if (end == ne) {
+      vals[k++] = sum[node];
+      break;
+    }
+    const int64_t mid = (ns + ne) / 2;
+    if (end <= mid) {
+      node = 2 * node;
+      ne = mid;
+    } else {
+      vals[k++] = sum[2 * node];
+      node = 2 * node + 1;
+      ns = mid + 1;
+    }
+  }
+  double acc = vals[k - 1];
+  for (int q = k - 2; q >= 0; --q) acc = vals[q] + acc;
+  return acc;
+}
+
+__global__ void __launch_bounds__(kSampleThreads)
+sample_kernel(const double* sum, const double* mn, int64_t cap, int64_t len, int32_t batch,
+              const double* u, double beta, int64_t* idx_out, double* w_out) {
+  __shared__ double s_range, s_total, s_maxw;
+  if (threadIdx.x == 0) {
+    s_range = prefix_range_sum(sum, cap, len - 2);
+    s_total = sum[1];
+    const double p_min = mn[1] / s_total;                         // buffers.py:226
+    s_maxw = pow(p_min * (double)len, -beta);                      // :227
+  }
+  __syncthreads();
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= batch) return;
+  double mass = u[i] * s_range;                                    // :180
+  int64_t node = 1;
+  while (node < cap) {                                             // segment_tree.py:125-131
+    const double l = sum[2 * node];
+    if (l > mass) {
+      node = 2 * node;
+    } else {
+      mass -= l;
+      node = 2 * node + 1;
+    }
+  }
+  const int64_t j = node - cap;
+  idx_out[i] = j;
+  const double p_sample = sum[node] / s_total;                     // :230
+  w_out[i] = pow(p_sample * (double)len, -beta) / s_maxw;          // :231-232
+}
+
+#define PER_HIP(h, expr)                                                       \
+  do {                                                                         \
+    hipError_t _e = (expr);                                                    \
+    if (_e != hipSuccess) {                                                    \
+      (h)->msg = std::string(#expr) + ": " + hipGetErrorString(_e);             \
+      return DT_E_HIP;                                                         \
+    }                                                                          \
+  } while (0)
+
+std::string g_per_create_err;
+
+}  // namespace
+
+extern "C" {
+
+int dt_per_create(int64_t size, double alpha, int32_t device, dt_per** out) {
+  g_per_create_err.clear();
+  if (!out || size < 1 || !(alpha > 0.0) || size > (int64_t(1) << 31)) {
+    g_per_create_err = "dt_per_create: need 1 <= size <= 2^31 and alpha > 0";
+    return DT_E_ARG;
+  }
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || device < 0 || device >= ndev) {
+    g_per_create_err = "dt_per_create: no HIP device " + std::to_string(device);
+    return DT_E_NODEV;
+  }
+  dt_per* h = new dt_per();
+  h->device = device;
+  h->size = size;
+  h->alpha = alpha;
+  h->cap = 1;
+  while (h->cap < size) {
+    h->cap *= 2;
+    ++h->log2cap;
+  }
+  const size_t tb = (size_t)(2 * h->cap) * sizeof(double);
+  const size_t wb = (((size_t)h->cap * 4) + 255) & ~size_t(255);
+  if (hipSetDevice(device) != hipSuccess || hipMalloc(&h->buf, 2 * tb + wb + 256) != hipSuccess) {
+    g_per_create_err = "dt_per_create: hipMalloc failed";
+    delete h;
+    return DT_E_HIP;
+  }
+  char* b = (char*)h->buf;
+  h->sum = (double*)b;
+  h->mn = (double*)(b + tb);
+  h->winner = (int32_t*)(b + 2 * tb);
+  h->maxp = (double*)(b + 2 * tb + wb);
+  h->err = (int32_t*)(b + 2 * tb + wb + 64);
+  const int grid = (int)std::min<int64_t>((2 * h->cap + 255) / 256, 4096);
+  fill_kernel<<<grid, 256>>>(h->sum, h->mn, h->maxp, h->winner, h->cap);
+  if (hipMemset(h->err, 0, 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+    g_per_create_err = "dt_per_create: init failed";
+    (void)hipFree(h->buf);
+    delete h;
+    return DT_E_HIP;
+  }
+  *out = h;
+  return DT_OK;
+}
+
+void dt_per_destroy(dt_per* h) {
+  if (!h) return;
+  (void)hipSetDevice(h->device);
+  (void)hipFree(h->buf);
+  delete h;
+}
+
+const char* dt_per_last_error(const dt_per* h) { return h ? h->msg.c_str() : g_per_create_err.c_str(); }
+int64_t dt_per_capacity(const dt_per* h) { return h ? h->cap : -1; }
+int64_t dt_per_len(const dt_per* h) { return h ? h->len : -1; }
+int64_t dt_per_next_idx(const dt_per* h) { return h ? h->next : -1; }
+
+int dt_per_add(dt_per* h, int64_t n, int64_t* slots_dev, void* stream) {
+  if (!h || n < 0) return DT_E_ARG;
+  if (n == 0) return DT_OK;
+  PER_HIP(h, hipSetDevice(h->device));
+  add_kernel<<<1, kTreeThreads, 0, (hipStream_t)stream>>>(h->sum, h->mn, h->maxp, h->cap, h->log2cap,
+                                                          h->size, h->next, n, h->alpha, slots_dev);
+  PER_HIP(h, hipGetLastError());
+  h->next = (h->next + n) % h->size;
+  h->len = std::min(h->len + n, h->size);
+  return DT_OK;
+}
+
+int dt_per_sample(dt_per* h, int32_t batch, const double* u_dev, double beta, int64_t* idx_dev,
+                  double* weights_dev, void* stream) {
+  if (!h || batch < 0 || !(beta > 0.0) || (batch > 0 && (!u_dev || !idx_dev || !weights_dev))) {
+    if (h) h->msg = "dt_per_sample: bad argument (beta must be > 0)";
+    return DT_E_ARG;
+  }
+  if (h->len < 2) {
+    h->msg = "dt_per_sample: need at least 2 stored transitions";
+    return DT_E_ARG;
+  }
+  if (batch == 0) return DT_OK;
+  PER_HIP(h, hipSetDevice(h->device));
+  const int grid = (batch + kSampleThreads - 1) / kSampleThreads;
+  sample_kernel<<<grid, kSampleThreads, 0, (hipStream_t)stream>>>(h->sum, h->mn, h->cap, h->len,
+                                                                  batch, u_dev, beta, idx_dev,
+                                                                  weights_dev);
+  PER_HIP(h, hipGetLastError());
+  return DT_OK;
+}
+
+int dt_per_update(dt_per* h, int32_t n, const int64_t* idx_dev, const double* priorities_dev,
+                  void* stream) {
+  if (!h || n < 0 || (n > 0 && (!idx_dev || !priorities_dev))) return DT_E_ARG;
+  if (n == 0) return DT_OK;
+  PER_HIP(h, hipSetDevice(h->device));
+  update_kernel<<<1, kTreeThreads, 0, (hipStream_t)stream>>>(h->sum, h->mn, h->maxp, h->winner,
+                                                             h->err, h->cap, h->log2cap, h->len, n,
+                                                             idx_dev, priorities_dev, h->alpha);
+  PER_HIP(h, hipGetLastError());
+  return DT_OK;
+}
+
+int dt_per_read(dt_per* h, double* sum_dev, double* min_dev, double* max_priority_dev,
+                void* stream) {
+  if (!h) return DT_E_ARG;
+  PER_HIP(h, hipSetDevice(h->device));
+  const size_t tb = (size_t)(2 * h->cap) * sizeof(double);
+  hipStream_t s = (hipStream_t)stream;
+  if (sum_dev) PER_HIP(h, hipMemcpyAsync(sum_dev, h->sum, tb, hipMemcpyDeviceToDevice, s));
+  if (min_dev) PER_HIP(h, hipMemcpyAsync(min_dev, h->mn, tb, hipMemcpyDeviceToDevice, s));
+  if (max_priority_dev)
+    PER_HIP(h, hipMemcpyAsync(max_priority_dev, h->maxp, 8, hipMemcpyDeviceToDevice, s));
+  return DT_OK;
+}
+
+int dt_per_check(dt_per* h) {
+  if (!h) return DT_E_ARG;
+  PER_HIP(h, hipSetDevice(h->device));
+  PER_HIP(h, hipDeviceSynchronize());
+  int32_t e = 0;
+  PER_HIP(h, hipMemcpy(&e, h->err, 4, hipMemcpyDeviceToHost));
+  if (!e) return DT_OK;
+  PER_HIP(h, hipMemset(h->err, 0, 4));
+  h->msg = "update_priorities: ";
+  if (e & 1) h->msg += "priority must be > 0; ";
+  if (e & 2) h->msg += "index outside [0, len); ";
+  h->msg += "offending entries were skipped";
+  return DT_E_ARG;
+}
+
+}  // extern "C"

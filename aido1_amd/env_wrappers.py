@@ -5,7 +5,10 @@ collect_garbage, get_observation) whose arguments and results carry a leading
 env dimension and live on the GPU.
 
 EnvironmentWrapper.step (utils/env_wrappers.py:213-253) semantics kept:
-  - tanh actor head (config.json:88): action/2 + 0.5 in float32 (in-kernel);
+  - tanh actor head (config.json:88): action/2 + 0.5 in float32 (in-kernel),
+    and, as the reference's ``action /= 2; action += 0.5``, the caller's
+    action array is left holding the mapped values (what the explorer then
+    stores in its replay, explorers.py:209);
   - repeat_actions Simulator steps, break on done (per env);
   - reward = sum of raw rewards, reward_mod = sum of BaselineAggregation
     rewards x reward_scale;
@@ -35,6 +38,16 @@ def create_env(config, internal_env_args=None, transfer=False, **kw):
     if seed is not None:
         env.change_model(seed)
     return env
+
+
+def map_tanh_in_place(action):
+    """utils/env_wrappers.py:214-216 on the caller's array (float32 ops, the
+    values the kernel used).  Stream-ordered after the step that read it."""
+    if isinstance(action, torch.Tensor):
+        action.div_(2).add_(0.5)
+    else:
+        action /= 2
+        action += 0.5
 
 
 class EnvironmentWrapper:
@@ -73,6 +86,8 @@ class EnvironmentWrapper:
 
     def step(self, action):
         out = self.env.step_into(self._actions(action))
+        if self.env.config.action_mode == 'tanh':
+            map_tanh_in_place(action)
         if self.render is not None:
             self.env.render_into(self.render, fresh=out.done)
             obs = self.render.stack_view()

@@ -19,6 +19,7 @@ import torch
 
 from aido1_amd.actor import ConfigActor, FusedActor
 from aido1_amd.config import EnvConfig
+from aido1_amd.env_wrappers import map_tanh_in_place
 from aido1_amd.explore import OUNoise, explore_actions
 from aido1_amd.render import H, W, RenderOutput
 from aido1_amd.vec_env import StepOutput, VecEnv
@@ -114,6 +115,8 @@ class ActorRollout:
         for env, o, ro, sl in zip(self.envs, self.outs, self.renders, self.slices):
             env.step_into(self.actions[sl], o)
             env.render_into(ro, fresh=o.done)
+        if self.head == 'tanh':   # the wrapper's in-place a/2 + 0.5 (env_wrappers.py:214-216)
+            map_tanh_in_place(self.actions)
         d = self.done.bool()
         self.ou.reset_states(d)
         self.episode += d.long()

@@ -1,0 +1,77 @@
+/* dtreplay.h — C-ABI of the GPU prioritized replay.
+ *
+ * Replaces, for the batched DDPG path, the index side of
+ *   utils/buffers.py:140-259   PrioritizedReplayBuffer (add / sample / update_priorities)
+ *   utils/segment_tree.py:94-146 SumSegmentTree + MinSegmentTree
+ * The payload (observations, actions, ...) lives in caller-owned device tensors
+ * indexed by the slots these calls return (aido1_amd/replay.py).
+ *
+ * Layout in HBM: two float64 trees of 2*capacity nodes each (node 1 = root,
+ * leaf i at capacity + i, as segment_tree.py:34), an int32[capacity] scratch
+ * used to resolve duplicate indices in one update, and the float64 running
+ * max priority.  All state stays on the device: add / sample / update are
+ * stream-ordered and never synchronise.
+ *
+ * Conventions as dtsim.h: every call returns 0 or a negative DT_E_* code,
+ * device pointers belong to the handle's GPU, work goes on `stream`
+ * (a hipStream_t, NULL = default stream).
+ */
+#ifndef AIDO1_AMD_DTREPLAY_H
+#define AIDO1_AMD_DTREPLAY_H
+
+#include <stdint.h>
+
+#include "dtsim.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct dt_per dt_per;
+
+/* PrioritizedReplayBuffer(size, alpha) — buffers.py:141-167: capacity = next
+ * power of two >= size, sum tree 0, min tree +inf, max_priority 1. */
+int dt_per_create(int64_t size, double alpha, int32_t device, dt_per** out);
+void dt_per_destroy(dt_per* h);
+const char* dt_per_last_error(const dt_per* h);
+int64_t dt_per_capacity(const dt_per* h);
+int64_t dt_per_len(const dt_per* h);      /* len(buffer._storage) */
+int64_t dt_per_next_idx(const dt_per* h); /* buffer._next_idx */
+
+/* n consecutive add() calls — buffers.py:169-174 + ReplayBuffer.add :29-36:
+ * slot k = (next_idx + k) % size gets leaf max_priority**alpha in both trees.
+ * slots_dev (int64[n], may be NULL) receives each add's slot; when n > size
+ * later adds overwrite earlier ones, so the payload of add k belongs in
+ * slots[k] only if k >= n - size. */
+int dt_per_add(dt_per* h, int64_t n, int64_t* slots_dev, void* stream);
+
+/* sample(batch, beta) — buffers.py:176-235 with random.random() replaced by
+ * u_dev[batch] (float64 in [0,1)): mass = u * sum(0, len - 1) (leaves
+ * 0..len-2, the reference's reduce() end quirk), idx = find_prefixsum_idx(mass)
+ * (segment_tree.py:106-132), weight = (p_idx * len)^-beta / (p_min * len)^-beta.
+ * Needs len >= 2 (the reference recurses forever at len 1). */
+int dt_per_sample(dt_per* h, int32_t batch, const double* u_dev, double beta, int64_t* idx_dev,
+                  double* weights_dev, void* stream);
+
+/* update_priorities(idx, priorities) — buffers.py:237-259: leaf = p**alpha
+ * (the last occurrence of a duplicated index wins, as the sequential loop),
+ * max_priority = max(max_priority, p).  Entries the reference would reject
+ * (p <= 0 or NaN, idx outside [0, len)) are skipped and flagged for
+ * dt_per_check. */
+int dt_per_update(dt_per* h, int32_t n, const int64_t* idx_dev, const double* priorities_dev,
+                  void* stream);
+
+/* Copy out the trees (float64[2*capacity] each; NULL to skip) and the max
+ * priority (float64[1]) — tests and checkpointing. */
+int dt_per_read(dt_per* h, double* sum_dev, double* min_dev, double* max_priority_dev,
+                void* stream);
+
+/* Synchronises; DT_E_ARG if an update since the last check held an entry the
+ * reference's asserts reject (message in dt_per_last_error). */
+int dt_per_check(dt_per* h);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* AIDO1_AMD_DTREPLAY_H */

@@ -272,6 +272,54 @@ def gen_segment_tree():
     dump('segment_tree.json', out)
 
 
+def gen_prioritized_replay():
+    """Drive utils/buffers.py PrioritizedReplayBuffer through adds (with wrap),
+    proportional samples and priority updates (with duplicate indices).  The
+    uniforms random.random() returns are scripted and recorded, so a GPU run fed
+    the same uniforms must return the same indices."""
+    import utils.buffers as buffers
+    rng = np.random.default_rng(11)
+    out = []
+    for size, alpha, beta in ((100, 0.6, 0.4), (37, 0.5, 1.0), (16, 0.6, 0.4)):
+        buf = buffers.PrioritizedReplayBuffer(size, alpha)
+        cap = buf._it_sum._capacity
+        ops = []
+        counter = 0
+        for step in range(12):
+            n_add = int(rng.integers(1, 2 * size // 3 + 2))
+            items = list(range(counter, counter + n_add))
+            counter += n_add
+            for k in items:
+                # ndarray items: numpy 2's np.array(x, copy=False) refuses to copy
+                buf.add(np.array([k]), np.array([k, -k]), float(k), np.array([k + 1]), k % 5 == 0)
+            op = {'add': items}
+            if len(buf) >= 2:
+                batch = int(rng.integers(1, 33))
+                us = [float(u) for u in rng.random(batch)]
+                it = iter(us)
+                saved = buffers.random.random
+                buffers.random.random = lambda: next(it)
+                try:
+                    obs, act, rew, nxt, done, w, idx = buf.sample(batch, beta=beta)
+                finally:
+                    buffers.random.random = saved
+                op['sample'] = {'batch': batch, 'beta': beta, 'u': us, 'idx': [int(i) for i in idx],
+                                'weights': [float(x) for x in w], 'obs': [int(o) for o in obs.reshape(-1)]}
+                n_up = int(rng.integers(1, batch + 1))
+                up_idx = [int(idx[int(j)]) for j in rng.integers(0, batch, n_up)]
+                pr = [float(x) for x in rng.random(n_up) * 3 + 1e-3]
+                buf.update_priorities(up_idx, pr)
+                op['update'] = {'idx': up_idx, 'priorities': pr}
+            op['len'] = len(buf)
+            op['next_idx'] = buf._next_idx
+            op['max_priority'] = buf._max_priority
+            op['sum_tree'] = [float(v) for v in buf._it_sum._value]
+            op['min_tree'] = [float(v) if v != float('inf') else None for v in buf._it_min._value]
+            ops.append(op)
+        out.append({'size': size, 'alpha': alpha, 'capacity': cap, 'ops': ops})
+    dump('prioritized_replay.json', out)
+
+
 def gen_random_process_and_decay():
     from utils.random_process import OrnsteinUhlenbeckProcess
     from utils.util import create_decay_fn
@@ -333,14 +381,21 @@ def gen_config_keys():
     head = cfg['model']['actor'][-1]['modules'][-1][-1]['name']
     keys = ('global_seed', 'rp_theta', 'rp_mu', 'rp_sigma', 'rp_sigma_min', 'epsilon_cycle_len',
             'initial_epsilon', 'final_epsilon', 'epsilon_ratio', 'max_episodes',
-            'every_second_random', 'alpha', 'beta', 'batch_size', 'buffer_size', 'gamma', 'tau')
+            'every_second_random', 'alpha', 'beta', 'batch_size', 'buffer_size', 'gamma', 'tau',
+            'optimizer', 'critic_loss', 'actor_train_decay', 'critic_train_decay',
+            'num_threads_training', 'update_steps_between_update')
     mini = {'environment': {'wrapper': cfg['environment']['wrapper']},
             'model': {'num_action': cfg['model']['num_action'], 'actor': cfg['model']['actor'],
                       'critic': cfg['model']['critic']},
             'training': {k: cfg['training'][k] for k in keys}}
     assert mini['model']['actor'][-1]['modules'][-1][-1]['name'] == head
-    with open(os.path.join(HERE, 'reference_config.json'), 'w') as f:
-        json.dump(mini, f, indent=1)
+    for path in (os.path.join(HERE, 'reference_config.json'),
+                 os.path.join(REPO, 'aido1_amd', 'configs', 'reference_config.json')):
+        if os.path.exists(path):
+            os.chmod(path, 0o644)
+        with open(path, 'w') as f:
+            json.dump(mini, f, indent=1)
+        os.chmod(path, 0o444)
     print('wrote reference_config.json')
 
 
@@ -354,6 +409,7 @@ def main():
     gen_stacking()
     gen_env_wrapper()
     gen_segment_tree()
+    gen_prioritized_replay()
     gen_random_process_and_decay()
     gen_actor()
 

@@ -68,7 +68,9 @@ def test_env_wrappers_batched(gpu):
     prev_newest = obs[:, 2].clone()
     for t in range(20):
         a = torch.from_numpy(rng.uniform(-1, 1, (256, 2)).astype(np.float32))
+        a0 = a.clone()
         obs, (r, rm), done, info = env.step(a)
+        assert torch.equal(a, a0 / 2 + 0.5)             # env_wrappers.py:214-216, in place
         keep = ~done
         # the previous newest frame is now the middle one (Transformer shift)
         assert torch.equal(obs[keep, 1], prev_newest[keep])

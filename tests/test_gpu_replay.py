@@ -1,0 +1,113 @@
+"""GPU prioritized replay (csrc/dtreplay.hip through include/dtreplay.h) against
+the reference's PrioritizedReplayBuffer (golden op sequences) and the oracle
+at full size.  Sampled indices must be identical for the same uniforms; the
+trees are compared bit for bit."""
+import math
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle.per_ref import PrioritizedReplayRef
+
+pytestmark = pytest.mark.gpu
+
+
+def _payload(items, dev):
+    k = torch.tensor(items, dtype=torch.float32, device=dev)
+    n = k.numel()
+    return k.view(n, 1), torch.stack([k, -k], 1), k.double(), (k + 1).view(n, 1), \
+        (k.long() % 5 == 0)
+
+
+def _inf(v):
+    return math.inf if v is None else v
+
+
+def assert_trees(st, mt, ref_sum, ref_min):
+    st, mt = st.cpu().numpy(), mt.cpu().numpy()
+    ref_sum = np.asarray(ref_sum, np.float64)
+    ref_min = np.asarray([_inf(v) for v in ref_min], np.float64)
+    cap = st.size // 2
+    leaf = slice(cap, 2 * cap)
+    np.testing.assert_allclose(st[leaf], ref_sum[leaf], rtol=4.5e-16, atol=0)
+    np.testing.assert_allclose(mt[leaf], ref_min[leaf], rtol=4.5e-16, atol=0)
+    node = np.arange(1, cap)
+    assert np.array_equal(st[node], st[2 * node] + st[2 * node + 1])          # exact recurrence
+    l, r = mt[2 * node], mt[2 * node + 1]
+    assert np.array_equal(mt[node], np.where(r < l, r, l))                    # Python min(l, r)
+    np.testing.assert_allclose(st[1:cap], ref_sum[1:cap], rtol=1e-15)
+    np.testing.assert_allclose(mt[1:cap], ref_min[1:cap], rtol=4.5e-16)
+
+
+def test_per_matches_reference_op_sequences(gpu):
+    from aido1_amd.replay import PrioritizedReplayBuffer
+    for case in golden('prioritized_replay.json'):
+        rb = PrioritizedReplayBuffer(case['size'], case['alpha'], device=gpu)
+        assert rb.capacity == case['capacity']
+        for op in case['ops']:
+            rb.add_batch(*_payload(op['add'], gpu))
+            if 'sample' in op:
+                s = op['sample']
+                obs, act, rew, nxt, done, w, idx = rb.sample(s['batch'], beta=s['beta'], u=s['u'])
+                assert idx.tolist() == s['idx']
+                assert obs.view(-1).long().tolist() == s['obs']
+                np.testing.assert_allclose(w.cpu().numpy(), s['weights'], rtol=1e-13, atol=0)
+                rb.update_priorities(op['update']['idx'], op['update']['priorities'])
+            rb.check()
+            st, mt, mp = rb.trees()
+            assert len(rb) == op['len'] and rb._next_idx == op['next_idx']
+            assert mp.item() == op['max_priority']
+            assert_trees(st, mt, op['sum_tree'], op['min_tree'])
+        rb.close()
+
+
+def test_per_full_size_against_oracle(gpu):
+    """BASELINE config 5 shape: 4096 transitions per add, batched updates with
+    duplicate indices, 4096-wide samples; capacity 2^17."""
+    from aido1_amd.replay import PrioritizedReplayBuffer
+    size, alpha, beta, n = 100_000, 0.6, 0.4, 4096
+    rb = PrioritizedReplayBuffer(size, alpha, device=gpu)
+    ref = PrioritizedReplayRef(size, alpha)
+    rng = np.random.default_rng(5)
+    obs = torch.zeros(n, 1, device=gpu)
+    act = torch.zeros(n, 2, device=gpu)
+    rew = torch.zeros(n, dtype=torch.float64, device=gpu)
+    done = torch.zeros(n, dtype=torch.bool, device=gpu)
+    for it in range(30):                      # 122880 adds: wraps the 100000 ring
+        rb.add_batch(obs, act, rew, obs, done)
+        ref.add(n)
+        u = rng.random(n)
+        *_, w, idx = rb.sample(n, beta=beta, u=u)
+        ridx, rw = ref.sample(u.tolist(), beta)
+        assert idx.tolist() == ridx, it
+        np.testing.assert_allclose(w.cpu().numpy(), rw, rtol=1e-13)
+        upd = idx[torch.from_numpy(rng.integers(0, n, n)).to(gpu)]   # duplicates included
+        pr = rng.random(n) * (2.0 + it) + 1e-6
+        rb.update_priorities(upd, pr)
+        ref.update_priorities(upd.tolist(), pr.tolist())
+    rb.check()
+    st, mt, mp = rb.trees()
+    assert mp.item() == ref.max_priority
+    assert_trees(st, mt, ref.it_sum.value, [None if v == math.inf else v for v in ref.it_min.value])
+    rb.close()
+
+
+def test_per_rejects_like_reference_asserts(gpu):
+    from aido1_amd._lib import DtError
+    from aido1_amd.replay import PrioritizedReplayBuffer
+    rb = PrioritizedReplayBuffer(16, 0.6, device=gpu)
+    rb.add_batch(*_payload(list(range(4)), gpu))
+    rb.update_priorities([1, 2], [0.5, -1.0])          # p <= 0: buffers.py:254
+    with pytest.raises(DtError, match='priority'):
+        rb.check()
+    rb.update_priorities([7], [0.5])                   # idx >= len: buffers.py:255
+    with pytest.raises(DtError, match='index'):
+        rb.check()
+    st, _, _ = rb.trees()
+    assert st[16 + 1].item() == pytest.approx(0.5 ** 0.6, rel=1e-15)   # valid entry applied
+    one = PrioritizedReplayBuffer(16, 0.6, device=gpu)
+    one.add_batch(*_payload([0], gpu))
+    with pytest.raises(DtError, match='at least 2'):
+        one.sample(4, beta=0.4)

@@ -1,0 +1,54 @@
+"""Host logic of the replay buffers on CPU tensors (uniform ReplayBuffer:
+utils/buffers.py:12-137), checked against the oracle's index restatement."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+from oracle.per_ref import uniform_indices
+
+
+def _batch(k0, n):
+    k = torch.arange(k0, k0 + n, dtype=torch.float32)
+    return k.view(n, 1, 1).expand(n, 3, 4).contiguous(), torch.stack([k, -k], 1), k.double(), \
+        k.view(n, 1, 1).expand(n, 3, 4) + 1, (k.long() % 5 == 0)
+
+
+def test_uniform_buffer_add_wrap_and_sample():
+    from aido1_amd.replay import ReplayBuffer
+    rb = ReplayBuffer(10, device='cpu')
+    rb.add_batch(*_batch(0, 4))
+    rb.add(*[t[0] for t in _batch(4, 1)])       # single add, reference signature
+    assert len(rb) == 5 and rb._next_idx == 5
+    rb.add_batch(*_batch(5, 23))                 # wraps twice, later adds win
+    assert len(rb) == 10 and rb._next_idx == 8
+    # slot s holds the last item k with k % 10 == s among 0..27
+    expect = {s: max(k for k in range(28) if k % 10 == s) for s in range(10)}
+    assert [int(v) for v in rb.storage['reward']] == [expect[s] for s in range(10)]
+    u = np.random.default_rng(0).random(64)
+    obs, act, rew, nxt, done = rb.sample(64, u=u)
+    idx = uniform_indices(u, len(rb))
+    assert [int(v) for v in rew] == [expect[i] for i in idx]
+    assert torch.equal(nxt, obs + 1) and torch.equal(act[:, 1], -act[:, 0])
+    assert torch.equal(done, rew.long() % 5 == 0)
+    assert obs.shape == (64, 3, 4)
+
+
+def test_obs_dtype_narrowing():
+    from aido1_amd.replay import ReplayBuffer
+    rb = ReplayBuffer(8, device='cpu', obs_dtype=torch.bfloat16)
+    rb.add_batch(*_batch(0, 3))
+    assert rb.storage['obs'].dtype == torch.bfloat16 and rb.storage['action'].dtype == torch.float32
+
+
+def test_create_buffer_reads_config():
+    from aido1_amd.replay import ReplayBuffer, create_buffer
+    cfg = golden('reference_config.json')
+    rb = create_buffer(cfg, device='cpu')
+    assert isinstance(rb, ReplayBuffer) and rb._maxsize == cfg['training']['buffer_size']
+
+
+def test_sample_empty_raises():
+    from aido1_amd.replay import ReplayBuffer
+    with pytest.raises(ValueError):
+        ReplayBuffer(4, device='cpu').sample(2)
