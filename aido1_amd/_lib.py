@@ -17,9 +17,9 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_PATH = os.path.join(PKG_DIR, 'libdtsim.so')
 CSRC = os.path.join(PKG_DIR, 'csrc')
-SOURCES = ['dtsim.hip', 'dtrender.hip', 'dtreplay.hip']
+SOURCES = ['dtsim.hip', 'dtrender.hip', 'dtreplay.hip', 'dtactor.hip']
 HEADERS = ['dtsim_common.h', 'dtrender.h']
-PUBLIC_HEADERS = ['dtsim.h', 'dtreplay.h']
+PUBLIC_HEADERS = ['dtsim.h', 'dtreplay.h', 'dtactor.h']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ABI_VERSION = 1
 
@@ -120,6 +120,9 @@ def lib():
             'dt_per_update': (ctypes.c_int, [vp, i32, vp, vp, vp]),
             'dt_per_read': (ctypes.c_int, [vp, vp, vp, vp, vp]),
             'dt_per_check': (ctypes.c_int, [vp]),
+            # dtactor.h
+            'dt_sample_norm': (ctypes.c_int, [vp, vp, i32, i32, i32, vp, vp, ctypes.c_float,
+                                              ctypes.c_float, i32, vp]),
         }
         for name, (res, args) in sig.items():
             if not hasattr(L, name):

@@ -60,15 +60,42 @@ class ActorCNN(nn.Module):
 
 
 class _Conv(nn.Module):      # Conv2dWrapper: parameter path ".kernel"
-    def __init__(self, cin, cout, k, s):
+    def __init__(self, cin, cout, k, s, weight_init=None):
         super().__init__()
         self.kernel = nn.Conv2d(cin, cout, k, stride=s)
+        _init_weight(self.kernel.weight, weight_init, conv=True)
+
+    def forward(self, x):
+        return self.kernel(x)
 
 
 class _Lin(nn.Module):       # LinearWrapper: parameter path ".linear"
-    def __init__(self, fin, fout):
+    def __init__(self, fin, fout, weight_init=None):
         super().__init__()
         self.linear = nn.Linear(fin, fout)
+        _init_weight(self.linear.weight, weight_init, conv=False)
+
+    def forward(self, x):
+        return self.linear(x)
+
+
+def _init_weight(w, mode, conv):
+    """LinearWrapper / Conv2dWrapper.init_weights (models/ddpg/modules.py:36-78);
+    fanin_init's fan-in is size[0] (the OUTPUT dim, a reference quirk)."""
+    with torch.no_grad():
+        if mode == 'fanin':
+            v = 1.0 / float(w.shape[0]) ** 0.5
+            w.uniform_(-v, v)
+        elif mode == 'uniform':
+            w.uniform_(-3e-3, 3e-3)
+        elif mode == 'xavier_normal':
+            nn.init.xavier_normal_(w)
+        elif mode == 'xavier_uniform':
+            nn.init.xavier_uniform_(w)
+        elif mode == 'kaiming_normal' and not conv:
+            nn.init.kaiming_normal_(w)
+        elif mode == 'kaiming_uniform' and not conv:
+            nn.init.kaiming_uniform_(w)
 
 
 class _Seq(nn.Module):       # MetaNet: ".internal_modules.<i>"
@@ -76,17 +103,26 @@ class _Seq(nn.Module):       # MetaNet: ".internal_modules.<i>"
         super().__init__()
         self.internal_modules = nn.ModuleList(mods)
 
+    def forward(self, x):
+        for m in self.internal_modules:
+            x = m(x)
+        return x
 
-class _Net(nn.Module):
+
+class _Net(nn.Module):       # Net: input_nets / output_nets (modules.py:86-109)
     def __init__(self, inputs, outputs):
         super().__init__()
         self.input_nets = nn.ModuleList(inputs)
         self.output_nets = nn.ModuleList(outputs)
 
+    def forward(self, *inputs):
+        x = torch.cat([net(v) for net, v in zip(self.input_nets, inputs)], dim=1)
+        return [net(x) for net in self.output_nets]
+
 
 def _build_branch(spec):
     """One branch of config.json's module list -> list of modules (index-aligned
-    with the reference's MetaNet so state_dict keys match)."""
+    with the reference's MetaNet so state_dict keys match; modules.py:111-142)."""
     mods = []
     last = None
     for m in spec:
@@ -99,9 +135,10 @@ def _build_branch(spec):
             last = m['in_channels']
             continue
         if name == 'conv_2d':
-            mods.append(_Conv(last, a['out_channels'], a['kernel_size'], a['stride']))
             if a.get('padding', 0) != 0:
                 raise NotImplementedError('padding')
+            mods.append(_Conv(last, a['out_channels'], a['kernel_size'], a['stride'],
+                              a.get('weight_init')))
             last = a['out_channels']
         elif name == 'batch_norm_2d':
             mods.append(nn.BatchNorm2d(last))
@@ -113,7 +150,7 @@ def _build_branch(spec):
         elif name == 'dropout':
             mods.append(nn.Dropout(a['p']))
         elif name == 'linear':
-            mods.append(_Lin(last, a['out_features']))
+            mods.append(_Lin(last, a['out_features'], a.get('weight_init')))
             last = a['out_features']
         elif name == 'tanh':
             mods.append(nn.Tanh())
@@ -124,27 +161,36 @@ def _build_branch(spec):
     return mods
 
 
-class ConfigActor(nn.Module):
+def _branches(config, kind):
+    return [s for m in config if m['name'] == kind for s in m['modules']]
+
+
+class ConfigNet(nn.Module):
+    """models/ddpg/modules.py Actor / Critic: a Net from a config.json module
+    list; forward(*inputs) concatenates the input branches and returns the
+    first output branch (modules.py:168-194)."""
+
+    def __init__(self, net_config):
+        super().__init__()
+        self.net = _Net([_Seq(_build_branch(b)) for b in _branches(net_config, 'inputs')],
+                        [_Seq(_build_branch(b)) for b in _branches(net_config, 'outputs')])
+
+    def forward(self, *inputs):
+        return self.net(*inputs)[0]
+
+
+class ConfigActor(ConfigNet):
     """models/ddpg/modules.py Actor built from config.json's "actor" list
     (single input branch, single output branch, as config.json:19-91)."""
 
     def __init__(self, actor_config):
-        super().__init__()
-        ins = [s for m in actor_config if m['name'] == 'inputs' for s in m['modules']]
-        outs = [s for m in actor_config if m['name'] == 'outputs' for s in m['modules']]
+        super().__init__(actor_config)
+        ins, outs = _branches(actor_config, 'inputs'), _branches(actor_config, 'outputs')
         if len(ins) != 1 or len(outs) != 1:
             raise NotImplementedError('one input and one output branch')
-        self.net = _Net([_Seq(_build_branch(ins[0]))], [_Seq(_build_branch(outs[0]))])
         last = outs[0][-1]['name']
         self.head = {'tanh': 'tanh', 'sigmoid': 'sigmoid'}.get(last, 'none')
         self.max_action = 1.0
-
-    def forward(self, x):
-        for m in self.net.input_nets[0].internal_modules:
-            x = m.kernel(x) if isinstance(m, _Conv) else (m.linear(x) if isinstance(m, _Lin) else m(x))
-        for m in self.net.output_nets[0].internal_modules:
-            x = m.kernel(x) if isinstance(m, _Conv) else (m.linear(x) if isinstance(m, _Lin) else m(x))
-        return x
 
     def layers(self):
         mods = list(self.net.input_nets[0].internal_modules)
@@ -155,6 +201,12 @@ class ConfigActor(nn.Module):
         if len(convs) != 4 or len(bns) != 4 or len(lins) != 2:
             raise NotImplementedError('fused path expects 4 conv/bn pairs and 2 linears')
         return convs, bns, lins[0], lins[1]
+
+
+class ConfigCritic(ConfigNet):
+    """models/ddpg/modules.py Critic from config.json's "critic" list: conv
+    trunk -> linear 256 on the observation, the action passed through, both
+    concatenated (258) -> linear 128 -> linear 1 (config.json:93-170)."""
 
 
 def apply_head(x, head, max_action=1.0):
@@ -168,49 +220,114 @@ def apply_head(x, head, max_action=1.0):
 
 
 class FusedActor(nn.Module):
-    """Inference copy of an actor for the batched rollout: eval-mode BatchNorm
-    (applied after LeakyReLU) folded into the NEXT conv / the first linear
-    (an affine map of that layer's input), weights in `dtype`, and the first
-    conv's input channels re-ordered per call to read the frame ring directly.
-    Mathematically equal to the source actor in eval mode; numerically within
-    bf16 rounding (tests/test_gpu_actor.py).  Convolutions run channels_last."""
+    """Inference copy of an actor for the batched rollout, weights in `dtype`
+    (fp16 by default in the rollout: under per-sample normalisation bf16's
+    8-bit mantissa costs ~5e-2 in the actions vs ~6e-3 for fp16 on rendered
+    frames, tools/actor_precision.py; both run on MFMA at the same rate), convolutions channels_last (MIOpen's NHWC bf16 kernels are
+    ~1.75x its NCHW ones on these shapes, tools/actor_micro.py), the first
+    conv's input channels re-ordered per call so it reads the frame ring in
+    place.  Two modes:
 
-    def __init__(self, actor, dtype=torch.bfloat16):
+    * ``'reference'`` — what the reference's explorers compute: every model is
+      in train mode (managers.py:264-268, explorers.py:46) and acts on a batch
+      of ONE observation (models/ddpg/model.py:74-88), so each BatchNorm
+      normalises a sample with that sample's own per-channel mean and biased
+      variance over H x W, and the 0.5 dropout is live.  Batched here as
+      per-sample statistics (float32 accumulation) + affine.
+    * ``'eval'`` — eval-mode BatchNorm (running statistics) folded into the
+      next conv / the first linear: the checkpoint-evaluation policy
+      (test-ddpg-cnn.py, DDPG.act after .eval()).
+
+    Numerically within bf16 rounding of the float32 modules
+    (tests/test_gpu_actor.py).  ``refresh(actor)`` re-derives the weights in
+    place (the acting copy follows the trainer's target actor)."""
+
+    def __init__(self, actor, dtype=torch.bfloat16, mode='eval'):
         super().__init__()
+        if mode not in ('eval', 'reference'):
+            raise ValueError(mode)
         convs, bns, lin1, lin2 = actor.layers()
+        self.mode = mode
         self.head = actor.head
         self.max_action = getattr(actor, 'max_action', 1.0)
         self.dtype = dtype
-        ws, bs = [], []
-        scale = shift = None
-        for conv, bn in zip(convs, bns):
-            w = conv.weight.detach().double()
-            b = conv.bias.detach().double()
-            if scale is not None:   # fold previous BN: conv(s*x + t)
-                b = b + (w * shift.view(1, -1, 1, 1)).sum((1, 2, 3))
-                w = w * scale.view(1, -1, 1, 1)
-            ws.append(w)
-            bs.append(b)
-            scale = bn.weight.detach().double() / torch.sqrt(bn.running_var.detach().double() +
-                                                             bn.eps)
-            shift = bn.bias.detach().double() - bn.running_mean.detach().double() * scale
-        w1 = lin1.weight.detach().double()
-        b1 = lin1.bias.detach().double()
-        s_flat = scale.repeat_interleave(FLAT // scale.numel())
-        t_flat = shift.repeat_interleave(FLAT // shift.numel())
-        b1 = b1 + w1 @ t_flat
-        w1 = w1 * s_flat.view(1, -1)
         self.strides = [conv.stride for conv in convs]
-        # NHWC (channels_last) convolutions: MIOpen's bf16 kernels are ~1.75x
-        # faster on these shapes than NCHW (tools/actor_micro.py)
-        self.w = nn.ParameterList([nn.Parameter(
-            w.to(dtype).contiguous(memory_format=torch.channels_last), requires_grad=False)
-            for w in ws])
-        self.b = nn.ParameterList([nn.Parameter(b.to(dtype), requires_grad=False) for b in bs])
-        self.w1 = nn.Parameter(w1.to(dtype), requires_grad=False)
-        self.b1 = nn.Parameter(b1.to(dtype), requires_grad=False)
-        self.w2 = nn.Parameter(lin2.weight.detach().to(dtype), requires_grad=False)
-        self.b2 = nn.Parameter(lin2.bias.detach().to(dtype), requires_grad=False)
+        self.eps = [bn.eps for bn in bns]
+        drops = [m for m in actor.modules() if isinstance(m, nn.Dropout)]
+        self.p_drop = drops[0].p if drops else 0.0
+        cl = torch.channels_last
+        dev = convs[0].weight.device
+        self.w = nn.ParameterList([nn.Parameter(torch.empty_like(c.weight, dtype=dtype)
+                                                .contiguous(memory_format=cl), requires_grad=False)
+                                   for c in convs])
+        self.b = nn.ParameterList([nn.Parameter(torch.empty_like(c.bias, dtype=dtype),
+                                                requires_grad=False) for c in convs])
+        self.gamma = nn.ParameterList([nn.Parameter(torch.empty(bn.num_features, device=dev),
+                                                    requires_grad=False) for bn in bns])
+        self.beta = nn.ParameterList([nn.Parameter(torch.empty(bn.num_features, device=dev),
+                                                   requires_grad=False) for bn in bns])
+        self.w1 = nn.Parameter(torch.empty_like(lin1.weight, dtype=dtype), requires_grad=False)
+        self.b1 = nn.Parameter(torch.empty_like(lin1.bias, dtype=dtype), requires_grad=False)
+        self.w2 = nn.Parameter(torch.empty_like(lin2.weight, dtype=dtype), requires_grad=False)
+        self.b2 = nn.Parameter(torch.empty_like(lin2.bias, dtype=dtype), requires_grad=False)
+        self.refresh(actor)
+
+    @torch.no_grad()
+    def refresh(self, actor):
+        convs, bns, lin1, lin2 = actor.layers()
+        if self.mode == 'reference':
+            for i, (conv, bn) in enumerate(zip(convs, bns)):
+                self.w[i].copy_(conv.weight)
+                self.b[i].copy_(conv.bias)
+                self.gamma[i].copy_(bn.weight)
+                self.beta[i].copy_(bn.bias)
+            self.w1.copy_(lin1.weight)
+            self.b1.copy_(lin1.bias)
+        else:
+            scale = shift = None
+            for i, (conv, bn) in enumerate(zip(convs, bns)):
+                w = conv.weight.detach().double()
+                b = conv.bias.detach().double()
+                if scale is not None:   # fold previous BN: conv(s*x + t)
+                    b = b + (w * shift.view(1, -1, 1, 1)).sum((1, 2, 3))
+                    w = w * scale.view(1, -1, 1, 1)
+                self.w[i].copy_(w)
+                self.b[i].copy_(b)
+                scale = bn.weight.detach().double() / torch.sqrt(
+                    bn.running_var.detach().double() + bn.eps)
+                shift = bn.bias.detach().double() - bn.running_mean.detach().double() * scale
+            w1 = lin1.weight.detach().double()
+            b1 = lin1.bias.detach().double()
+            s_flat = scale.repeat_interleave(FLAT // scale.numel())
+            t_flat = shift.repeat_interleave(FLAT // shift.numel())
+            self.w1.copy_(w1 * s_flat.view(1, -1))
+            self.b1.copy_(b1 + w1 @ t_flat)
+        self.w2.copy_(lin2.weight)
+        self.b2.copy_(lin2.bias)
+
+    def _lrelu_sample_norm(self, x, i):
+        """LeakyReLU then BatchNorm2d in train mode on a batch of one, for every
+        sample at once: the dt_sample_norm HIP kernel (include/dtactor.h) on
+        the GPU, in place; a two-pass torch restatement on CPU (tests)."""
+        if x.is_cuda:
+            from aido1_amd import _lib
+            n, c, h, w = x.shape
+            assert x.is_contiguous(memory_format=torch.channels_last)
+            dt = {torch.bfloat16: 0, torch.float32: 1, torch.float16: 2}[x.dtype]
+            L = _lib.lib()
+            rc = L.dt_sample_norm(x.data_ptr(), x.data_ptr(), n, h * w, c,
+                                  self.gamma[i].data_ptr(), self.beta[i].data_ptr(),
+                                  self.eps[i], 0.01, dt,
+                                  torch.cuda.current_stream(x.device).cuda_stream)
+            if rc != 0:
+                raise _lib.DtError('dt_sample_norm failed (%d)' % rc)
+            return x
+        x = F.leaky_relu(x).float()
+        mean = x.mean((2, 3), keepdim=True)
+        var = (x - mean).square().mean((2, 3), keepdim=True)
+        g = self.gamma[i].view(1, -1, 1, 1)
+        b = self.beta[i].view(1, -1, 1, 1)
+        return ((x - mean) / torch.sqrt(var + self.eps[i]) * g + b).to(self.dtype)
 
     @torch.no_grad()
     def forward(self, x, order=None):
@@ -221,11 +338,15 @@ class FusedActor(nn.Module):
             inv = sorted(range(len(order)), key=lambda c: order[c])
             w0 = w0[:, inv].contiguous(memory_format=torch.channels_last)
         x = x.to(self.dtype, memory_format=torch.channels_last)
-        x = F.leaky_relu(F.conv2d(x, w0, self.b[0], stride=self.strides[0]))
-        for i in range(1, 4):
-            x = F.leaky_relu(F.conv2d(x, self.w[i], self.b[i], stride=self.strides[i]))
+        ref = self.mode == 'reference'
+        for i in range(4):
+            x = F.conv2d(x, w0 if i == 0 else self.w[i], self.b[i], stride=self.strides[i])
+            x = self._lrelu_sample_norm(x, i) if ref else F.leaky_relu(x)
         # flatten in NCHW order, as the reference's view(x.size(0), -1)
-        x = F.leaky_relu(F.linear(x.contiguous().flatten(1), self.w1, self.b1))
+        x = x.contiguous().flatten(1)
+        if ref and self.p_drop > 0:
+            x = F.dropout(x, self.p_drop, training=True)
+        x = F.leaky_relu(F.linear(x, self.w1, self.b1))
         x = F.linear(x, self.w2, self.b2).float()
         return apply_head(x, self.head, self.max_action)
 

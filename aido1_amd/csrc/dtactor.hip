@@ -1,0 +1,192 @@
+// Per-sample (batch-of-one, train-mode) LeakyReLU + BatchNorm2d over NHWC
+// activations — see include/dtactor.h.  One workgroup per sample: the sample's
+// [hw, c] slab is read three times (sum, squared deviations, normalise) — the
+// first read from HBM, the next two mostly from L2 / MALL — and written once.
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/dtactor.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kVec = 8;  // channels per thread per pixel (16 B of bf16)
+
+__device__ __forceinline__ float bf16_to_f32(uint32_t h) { return __uint_as_float(h << 16); }
+
+__device__ __forceinline__ uint32_t f32_to_bf16(float f) {
+  uint32_t u = __float_as_uint(f);
+  u += 0x7FFFu + ((u >> 16) & 1u);  // round to nearest even
+  return u >> 16;
+}
+
+template <typename T>
+struct Io;
+
+template <>
+struct Io<uint16_t> {  // bf16
+  static __device__ __forceinline__ void load(const uint16_t* p, float* f) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      f[2 * k] = bf16_to_f32(w[k] & 0xFFFFu);
+      f[2 * k + 1] = bf16_to_f32(w[k] >> 16);
+    }
+  }
+  static __device__ __forceinline__ void store(uint16_t* p, const float* f) {
+    uint4 v;
+    v.x = f32_to_bf16(f[0]) | (f32_to_bf16(f[1]) << 16);
+    v.y = f32_to_bf16(f[2]) | (f32_to_bf16(f[3]) << 16);
+    v.z = f32_to_bf16(f[4]) | (f32_to_bf16(f[5]) << 16);
+    v.w = f32_to_bf16(f[6]) | (f32_to_bf16(f[7]) << 16);
+    *reinterpret_cast<uint4*>(p) = v;
+  }
+};
+
+template <>
+struct Io<__half> {
+  static __device__ __forceinline__ void load(const __half* p, float* f) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p);
+    const __half2* h = reinterpret_cast<const __half2*>(&v);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float2 t = __half22float2(h[k]);
+      f[2 * k] = t.x;
+      f[2 * k + 1] = t.y;
+    }
+  }
+  static __device__ __forceinline__ void store(__half* p, const float* f) {
+    uint4 v;
+    __half2* h = reinterpret_cast<__half2*>(&v);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) h[k] = __floats2half2_rn(f[2 * k], f[2 * k + 1]);
+    *reinterpret_cast<uint4*>(p) = v;
+  }
+};
+
+template <>
+struct Io<float> {
+  static __device__ __forceinline__ void load(const float* p, float* f) {
+    const float4 a = reinterpret_cast<const float4*>(p)[0];
+    const float4 b = reinterpret_cast<const float4*>(p)[1];
+    f[0] = a.x; f[1] = a.y; f[2] = a.z; f[3] = a.w;
+    f[4] = b.x; f[5] = b.y; f[6] = b.z; f[7] = b.w;
+  }
+  static __device__ __forceinline__ void store(float* p, const float* f) {
+    reinterpret_cast<float4*>(p)[0] = make_float4(f[0], f[1], f[2], f[3]);
+    reinterpret_cast<float4*>(p)[1] = make_float4(f[4], f[5], f[6], f[7]);
+  }
+};
+
+__device__ __forceinline__ float lrelu(float v, float slope) { return v > 0.0f ? v : v * slope; }
+
+// Sum over the threads that own the same channel group (t % groups) of
+// acc[kVec] (idle threads hold zeros); returns, in s_out[c], the per-channel
+// totals.
+__device__ void reduce_channels(const float* acc, float (*s_part)[kVec], float* s_out, int groups,
+                                int c) {
+  const int t = threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < kVec; ++k) s_part[t][k] = acc[k];
+  __syncthreads();
+  if (t < c) {
+    const int g = t / kVec, k = t % kVec;
+    float s = 0.0f;
+    for (int u = g; u < kThreads; u += groups) s += s_part[u][k];
+    s_out[t] = s;
+  }
+  __syncthreads();
+}
+
+template <typename T>
+__global__ void __launch_bounds__(kThreads)
+sample_norm_kernel(const T* x, T* y, int hw, int c,  // y may alias x
+                   const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+                   float slope) {
+  __shared__ float s_part[kThreads][kVec];
+  __shared__ float s_mean[64], s_scale[64], s_shift[64];
+  const int groups = c / kVec;          // threads per pixel
+  const int per_iter = kThreads / groups;
+  const int t = threadIdx.x;
+  const int g = t % groups;
+  const size_t base = (size_t)blockIdx.x * hw * c;
+  const T* xs = x + base;
+  T* ys = y + base;
+  const int active = per_iter * groups;  // threads beyond this idle (c not dividing 256)
+  float v[kVec], acc[kVec];
+
+#pragma unroll
+  for (int k = 0; k < kVec; ++k) acc[k] = 0.0f;
+  if (t < active)
+    for (int p = t / groups; p < hw; p += per_iter) {
+      Io<T>::load(xs + (size_t)p * c + g * kVec, v);
+#pragma unroll
+      for (int k = 0; k < kVec; ++k) acc[k] += lrelu(v[k], slope);
+    }
+  reduce_channels(acc, s_part, s_mean, groups, c);
+  if (t < c) s_mean[t] = s_mean[t] / (float)hw;
+  __syncthreads();
+
+  float mu[kVec];
+#pragma unroll
+  for (int k = 0; k < kVec; ++k) {
+    mu[k] = s_mean[g * kVec + k];
+    acc[k] = 0.0f;
+  }
+  if (t < active)
+    for (int p = t / groups; p < hw; p += per_iter) {
+      Io<T>::load(xs + (size_t)p * c + g * kVec, v);
+#pragma unroll
+      for (int k = 0; k < kVec; ++k) {
+        const float d = lrelu(v[k], slope) - mu[k];
+        acc[k] += d * d;
+      }
+    }
+  reduce_channels(acc, s_part, s_scale, groups, c);
+  if (t < c) {
+    const float var = s_scale[t] / (float)hw;
+    const float sc = gamma[t] / sqrtf(var + eps);
+    s_scale[t] = sc;
+    s_shift[t] = beta[t] - s_mean[t] * sc;
+  }
+  __syncthreads();
+
+  float sc[kVec], sh[kVec];
+#pragma unroll
+  for (int k = 0; k < kVec; ++k) {
+    sc[k] = s_scale[g * kVec + k];
+    sh[k] = s_shift[g * kVec + k];
+  }
+  if (t < active)
+    for (int p = t / groups; p < hw; p += per_iter) {
+      Io<T>::load(xs + (size_t)p * c + g * kVec, v);
+#pragma unroll
+      for (int k = 0; k < kVec; ++k) v[k] = lrelu(v[k], slope) * sc[k] + sh[k];
+      Io<T>::store(ys + (size_t)p * c + g * kVec, v);
+    }
+}
+
+}  // namespace
+
+extern "C" int dt_sample_norm(const void* x, void* y, int32_t n, int32_t hw, int32_t c,
+                              const float* gamma, const float* beta, float eps, float slope,
+                              int32_t dtype, void* stream) {
+  if (!x || !y || !gamma || !beta || n < 0 || hw <= 0 || c <= 0 || c % kVec || c > 64 ||
+      dtype < 0 || dtype > 2)
+    return DT_E_ARG;
+  if (n == 0) return DT_OK;
+  hipStream_t s = (hipStream_t)stream;
+  if (dtype == 0)
+    sample_norm_kernel<uint16_t><<<n, kThreads, 0, s>>>((const uint16_t*)x, (uint16_t*)y, hw, c,
+                                                        gamma, beta, eps, slope);
+  else if (dtype == 1)
+    sample_norm_kernel<float><<<n, kThreads, 0, s>>>((const float*)x, (float*)y, hw, c, gamma,
+                                                     beta, eps, slope);
+  else
+    sample_norm_kernel<__half><<<n, kThreads, 0, s>>>((const __half*)x, (__half*)y, hw, c, gamma,
+                                                      beta, eps, slope);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}

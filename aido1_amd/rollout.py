@@ -4,7 +4,8 @@ One GPU runs `n_envs` environments split over maps (mixed small_loop /
 zigzag), all rendering into ONE shared frame ring so a single actor forward
 covers every env.  Per decision:
 
-  actor (bf16, BN folded, ring read zero-copy)  -> DDPG.act noise / every-
+  actor (fp16 MFMA, ring read zero-copy; actor_mode 'reference' = the reference's
+  train-mode batch-of-one BatchNorm + live dropout, 'eval' = BN folded)  -> DDPG.act noise / every-
   second-random (explore.py)  -> dt_step per map handle (tanh head mapping,
   repeat 3, reward shaping, respawn) -> dt_render per handle into the ring
   (+ line masks) -> OU reset for finished envs
@@ -46,7 +47,8 @@ class CycleEpsilon:
 
 class ActorRollout:
     def __init__(self, config, n_envs=4096, maps=('small_loop', 'zigzag'), device=0, seed=1234,
-                 env_id_base=0, actor=None, dtype=torch.bfloat16, masks=True):
+                 env_id_base=0, actor=None, dtype=torch.float16, masks=True,
+                 actor_mode='reference'):
         self.config = config
         self.device = torch.device('cuda', device)
         self.n = n_envs
@@ -81,8 +83,8 @@ class ActorRollout:
             off += sz
         if actor is None:
             actor = ConfigActor(config['model']['actor'])
-            actor.eval()
-        self.actor = FusedActor(actor, dtype=dtype).to(self.device)
+        self.actor_mode = actor_mode
+        self.actor = FusedActor(actor.to(self.device), dtype=dtype, mode=actor_mode)
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed + 17 * env_id_base)
         self.ou = OUNoise.from_config(config, n_envs, device=self.device, generator=self.gen)
@@ -101,6 +103,14 @@ class ActorRollout:
 
     def order(self):
         return self.renders[0].order()
+
+    def stack(self):
+        """[n, 3, 120, 160] oldest-first observation (a copy of the ring)."""
+        return self.ring[:, self.order()]
+
+    def load_actor(self, actor):
+        """Act with `actor`'s current weights from the next decision on."""
+        self.actor.refresh(actor)
 
     def step(self, timing=None):
         """One decision for every env; returns (reward, reward_mod, done) views."""

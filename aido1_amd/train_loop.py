@@ -1,0 +1,96 @@
+"""Full DDPG training on the GPU (BASELINE configs[4]).
+
+The reference splits this over processes and HTTP: explorers step envs and
+push episodes (training/explorers.py:164-211), a sampling worker fills a
+replay buffer and hands batches to the trainer through a queue
+(training/workers_client.py:16-60), the trainer updates and soft-updates the
+shared target model the explorers act with (training/trainers.py:143-237).
+Here one process per GPU runs, per iteration:
+
+  ActorRollout.step          one decision for n envs (actor on the frame ring,
+                             exploration noise, 3 sim steps, render)
+  replay.add_batch           n transitions (obs, mapped action, reward_mod,
+                             next_obs, done), HBM-resident
+  replay.sample              batch_size transitions (proportional, GPU trees)
+  DDPGTrainer.update         critic + actor + soft target update (grads
+                             all-reduced over ranks with RCCL)
+  replay.update_priorities   |td_error| + eps
+  rollout actor refresh      the acting copy follows the target actor, which
+                             is what the reference's explorers act with
+
+Nothing in the loop synchronises with the host.  Transition semantics: the
+stored next_obs of a finished env is its respawn stack (auto-reset), harmless
+because notdone = 0 removes Q(s') from its target.
+"""
+import torch
+
+from aido1_amd.actor import ConfigActor, ConfigCritic
+from aido1_amd.replay import PrioritizedReplayBuffer, ReplayBuffer
+from aido1_amd.rollout import ActorRollout
+from aido1_amd.trainer import DDPGTrainer
+
+PRIORITY_EPS = 1e-6
+
+
+class TrainLoop:
+    def __init__(self, config, n_envs=4096, maps=('small_loop', 'zigzag'), device=0, seed=1234,
+                 env_id_base=0, buffer_size=None, prioritized=True, batch_size=None,
+                 updates_per_step=1, refresh_every=1, obs_dtype=None, actor_dtype=torch.float16,
+                 actor_mode='reference', masks=False, graph=True):
+        t = config['training']
+        self.config = config
+        self.device = torch.device('cuda', device)
+        self.batch_size = int(batch_size or t['batch_size'])
+        self.beta = t['beta']
+        self.reward_modified = t.get('reward_modified', True)
+        self.updates_per_step = updates_per_step
+        self.refresh_every = refresh_every
+        torch.manual_seed(seed)                         # identical init on every rank
+        actor = ConfigActor(config['model']['actor'])
+        critic = ConfigCritic(config['model']['critic'])
+        self.trainer = DDPGTrainer(config, actor, critic, device=self.device, graph=graph)
+        self.rollout = ActorRollout(config, n_envs, maps=maps, device=device, seed=seed,
+                                    env_id_base=env_id_base, actor=self.trainer.target_actor,
+                                    dtype=actor_dtype, masks=masks, actor_mode=actor_mode)
+        size = int(buffer_size or t['buffer_size'])
+        gen = torch.Generator(device=self.device)
+        gen.manual_seed(seed * 7919 + env_id_base)
+        if prioritized:
+            self.replay = PrioritizedReplayBuffer(size, t['alpha'], device=self.device,
+                                                  obs_dtype=obs_dtype, generator=gen)
+        else:
+            self.replay = ReplayBuffer(size, device=self.device, obs_dtype=obs_dtype, generator=gen)
+        self.prioritized = prioritized
+        self.obs = None
+        self.updates = 0
+        self.decisions = 0
+        self.metrics = None
+
+    def reset(self):
+        self.rollout.reset()
+        self.obs = self.rollout.stack()
+
+    def step(self, timing=None):
+        r, rm, done = self.rollout.step(timing)
+        nxt = self.rollout.stack()
+        rew = rm if self.reward_modified else r        # explorers.py:205-206
+        self.replay.add_batch(self.obs, self.rollout.actions, rew, nxt, done)
+        self.obs = nxt
+        self.decisions += 1
+        if len(self.replay) >= max(self.batch_size, 2):
+            for _ in range(self.updates_per_step):
+                self._update()
+        return r, rm, done
+
+    def _update(self):
+        if self.prioritized:
+            obs, act, rew, nxt, done, _w, idx = self.replay.sample(self.batch_size, self.beta)
+        else:
+            obs, act, rew, nxt, done = self.replay.sample(self.batch_size)
+        self.metrics, info = self.trainer.update((obs, act, rew, nxt, done))
+        if self.prioritized:
+            pr = info['td_error'].detach().abs().reshape(-1).double() + PRIORITY_EPS
+            self.replay.update_priorities(idx, pr)
+        self.updates += 1
+        if self.updates % self.refresh_every == 0:
+            self.rollout.load_actor(self.trainer.target_actor)

@@ -1,0 +1,226 @@
+"""DDPG update on the GPU (BASELINE config 5).
+
+``DDPGTrainer.update`` follows training/trainers.py:143-237 step for step:
+
+  1. lr of both optimisers from TrainingDecay at the global update step
+     (utils/util.py:77-90, linear decay in config.json);
+  2. target actor -> target critic on next_obs (train mode: BatchNorm on batch
+     statistics, running stats updated — all reference models are .train());
+  3. y = r + notdone * gamma * Q'(s', pi'(s'));
+  4. critic MSE (or smooth-L1) backward, Adam step;
+  5. actor loss -mean Q(s, pi(s)) backward, Adam step;
+  6. soft update of both targets, tau (models/torch_utils.py:5-9);
+  7. td_error = y - Q(s, a) under no_grad (trainers.py:223-229), returned for
+     the prioritized replay's update_priorities.
+
+Multi-GPU: the reference's periodic barrier + parameter averaging
+across trainer processes (trainers.py:206-213) becomes an RCCL all-reduce of
+the gradients before each optimiser step (distributed.GradAllReduce), which
+keeps every rank's replica identical.
+
+Layout: modules and image batches are channels_last.  Besides being MIOpen's
+faster convolution layout, it selects MIOpen's NHWC BatchNorm: its NCHW
+train-mode BatchNorm loses precision on large H x W planes (5.8e-3 max error
+on a 57x77 N(3, 2) plane vs ~1e-6 for NHWC or torch's native kernel,
+tools/bn_probe.py), which the train-mode networks here hit every update.
+
+Metrics stay on the device (no .item() inside update) so the update can run
+back to back with the rollout without host synchronisation.
+
+HIP graphs (``graph=True``, GPU only): a batch-64 update is ~400 small
+kernels, so it is launch-bound.  The update is split in three stages at the
+two gradient all-reduces (critic: targets + critic loss + backward; critic
+step + actor loss + backward; actor step + soft updates + TD error).  The
+first ``warmup`` updates run eagerly (MIOpen algorithm selection, optimiser
+state creation), then each stage is captured once and replayed: one graph
+when there is nothing to all-reduce, three with the RCCL all-reduces run
+between them otherwise.  Inputs are copied into static buffers; Adam is the
+capturable variant with a device-tensor learning rate set by fill_ before
+each replay.  Dropout draws stay fresh per replay (graph-safe Philox offsets).
+"""
+import copy
+
+import torch
+import torch.nn.functional as F
+
+from aido1_amd.distributed import GradAllReduce, world
+from aido1_amd.explore import create_decay_fn
+from aido1_amd.optim import make_optimizer
+
+
+class TrainingDecay:
+    """utils/util.py:77-90: per-hyperparameter decay functions applied to an
+    optimiser param group."""
+
+    def __init__(self, config):
+        self.decays = {name: create_decay_fn(c['type'], **c['args']) for name, c in config.items()}
+        self.realization = {}
+
+    def __call__(self, params):
+        for name, v in self.realization.items():
+            if isinstance(params[name], torch.Tensor):
+                params[name].fill_(v)           # capturable optimiser: lr lives on the device
+            else:
+                params[name] = v
+
+    def update_step(self, step):
+        for name, fn in self.decays.items():
+            self.realization[name] = fn(step)
+
+
+def soft_update(target, source, tau):
+    """models/torch_utils.py:5-9: t <- t * (1 - tau) + p * tau (two products
+    rounded separately, as the reference's expression)."""
+    tp = [p.data for p in target.parameters()]
+    sp = [p.data for p in source.parameters()]
+    a = torch._foreach_mul(tp, 1.0 - tau)
+    b = torch._foreach_mul(sp, tau)
+    torch._foreach_add_(a, b)
+    torch._foreach_copy_(tp, a)
+
+
+def hard_update(target, source):
+    """models/torch_utils.py:12-14."""
+    torch._foreach_copy_([p.data for p in target.parameters()],
+                         [p.data for p in source.parameters()])
+
+
+class DDPGTrainer:
+    def __init__(self, config, actor, critic, target_actor=None, target_critic=None,
+                 device=None, sync_grads=None, bucket_mb=16, graph=False, warmup=3):
+        t = config['training']
+        self.config = config
+        self.gamma, self.tau = float(t['gamma']), float(t['tau'])
+        self.critic_loss_kind = t.get('critic_loss', 'mse_loss')
+        if self.critic_loss_kind not in ('mse_loss', 'smooth_l1_loss'):
+            raise NotImplementedError(self.critic_loss_kind)
+        self.device = torch.device(device) if device is not None else \
+            next(actor.parameters()).device
+        self.dtype = next(actor.parameters()).dtype      # float32 (float64 for parity tests)
+        self.actor, self.critic = actor.to(self.device), critic.to(self.device)
+        self.target_actor = (target_actor if target_actor is not None
+                             else copy.deepcopy(actor)).to(self.device)
+        self.target_critic = (target_critic if target_critic is not None
+                              else copy.deepcopy(critic)).to(self.device)
+        for m in (self.actor, self.critic, self.target_actor, self.target_critic):
+            m.to(memory_format=torch.channels_last)
+            m.train()                           # managers.py:264-268 _prime_model
+        self.graph = bool(graph) and self.device.type == 'cuda'
+        if self.graph and t['optimizer'] != 'adam':
+            raise NotImplementedError('graph capture needs the capturable Adam')
+        self.actor_optim = make_optimizer(t['optimizer'], self.actor.parameters(), self.graph,
+                                          self.device)
+        self.critic_optim = make_optimizer(t['optimizer'], self.critic.parameters(), self.graph,
+                                           self.device)
+        self.warmup = warmup
+        self._graphs = None
+        self._in = None
+        self.actor_decay = TrainingDecay(t['actor_train_decay'])
+        self.critic_decay = TrainingDecay(t['critic_train_decay'])
+        self.global_update_step = 0
+        if sync_grads is None:
+            sync_grads = world()[1] > 1
+        self.sync_actor = GradAllReduce(self.actor.parameters(), bucket_mb) if sync_grads else None
+        self.sync_critic = GradAllReduce(self.critic.parameters(), bucket_mb) if sync_grads \
+            else None
+
+    def _tensor(self, x, dtype=None):
+        return torch.as_tensor(x, device=self.device).to(dtype or self.dtype)
+
+    def _inputs(self, train_data):
+        observations, actions, rewards, next_observations, dones = train_data
+        cl = torch.channels_last
+        x = {'obs': self._tensor(observations).contiguous(memory_format=cl),
+             'nxt': self._tensor(next_observations).contiguous(memory_format=cl),
+             'act': self._tensor(actions),
+             'rew': self._tensor(rewards).reshape(-1, 1),
+             'notdone': (~self._tensor(dones, torch.bool).reshape(-1, 1)).to(self.dtype)}
+        if not self.graph:
+            self._in = x
+        elif self._in is None:
+            self._in = {k: v.clone(memory_format=torch.preserve_format) for k, v in x.items()}
+        else:
+            for k, v in x.items():
+                if v.shape != self._in[k].shape:
+                    raise ValueError('graph mode needs a fixed batch shape')
+                self._in[k].copy_(v)
+
+    # ---- the three stages (trainers.py:156-229) ------------------------------------
+    def _stage_critic(self):
+        x = self._in
+        with torch.no_grad():
+            next_actions = self.target_actor(x['nxt'])
+            next_v = self.target_critic(x['nxt'], next_actions)
+            self._y = x['rew'] + x['notdone'] * self.gamma * next_v
+        y_predicted = self.critic(x['obs'], x['act'])
+        if self.critic_loss_kind == 'mse_loss':
+            critic_loss = F.mse_loss(y_predicted, self._y)
+        else:
+            critic_loss = F.smooth_l1_loss(y_predicted, self._y)
+        self.critic_optim.zero_grad(set_to_none=not self.graph)
+        critic_loss.backward()
+        # keep no autograd graph alive past backward (a live graph pins the
+        # AccumulateGrad nodes to the eager stream and breaks graph capture)
+        self._critic_loss = critic_loss.detach()
+
+    def _stage_actor(self):
+        x = self._in
+        self.critic_optim.step()
+        pred_actions = self.actor(x['obs'])
+        actor_loss = -1.0 * torch.mean(self.critic(x['obs'], pred_actions))
+        self.actor_optim.zero_grad(set_to_none=not self.graph)
+        actor_loss.backward()
+        self._actor_loss = actor_loss.detach()
+
+    def _stage_targets(self):
+        x = self._in
+        self.actor_optim.step()
+        soft_update(self.target_actor, self.actor, self.tau)       # trainers.py:215-216
+        soft_update(self.target_critic, self.critic, self.tau)
+        with torch.no_grad():                                        # trainers.py:223-229
+            self._td = self._y - self.critic(x['obs'], x['act'])
+            self._metrics = (torch.sqrt(self._critic_loss), self._actor_loss)
+
+    def _capture(self):
+        stages = [self._stage_critic, self._stage_actor, self._stage_targets]
+        groups = [stages] if self.sync_actor is None else [[st] for st in stages]
+        self._graphs = []
+        for group in groups:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                for st in group:
+                    st()
+            self._graphs.append(g)
+
+    def update(self, train_data):
+        """train_data = (obs, actions, rewards, next_obs, dones), leading batch
+        dimension (numpy or tensors).  Returns (metrics, info) like the
+        reference; metric values are 0-dim device tensors (valid until the
+        next update in graph mode)."""
+        self._inputs(train_data)
+        self.critic_decay.update_step(self.global_update_step)
+        self.actor_decay.update_step(self.global_update_step)
+        for group in self.critic_optim.param_groups:
+            self.critic_decay(group)
+        for group in self.actor_optim.param_groups:
+            self.actor_decay(group)
+        syncs = [self.sync_critic, self.sync_actor, None]
+        if self.graph and self.global_update_step >= self.warmup:
+            if self._graphs is None:
+                self._capture()
+            if len(self._graphs) == 1:
+                self._graphs[0].replay()
+            else:
+                for g, sync in zip(self._graphs, syncs):
+                    g.replay()
+                    if sync is not None:
+                        sync()
+        else:
+            for st, sync in zip((self._stage_critic, self._stage_actor, self._stage_targets),
+                                syncs):
+                st()
+                if sync is not None:
+                    sync()
+        self.global_update_step += 1
+        metrics = {'critic_loss': self._metrics[0], 'actor_loss': self._metrics[1]}
+        return metrics, {'td_error': self._td}

@@ -11,7 +11,11 @@ Simulator step (env-step), read back exactly from the device counters (envs
 that finish mid-repeat run fewer).  Actions for every step are generated and
 resident in HBM before the timed region.
 
-  python bench.py [--gpus N --steps K --warmup W] [--config lane|render]
+  python bench.py [--gpus N --steps K --warmup W] [--config lane|render|actor|train]
+
+Other configs (not the headline line): render = configs[2] (obs pipeline),
+actor = configs[3] (actor in the loop), train = configs[4] (full DDPG: rollout +
+GPU prioritized replay + update + RCCL gradient all-reduce).
 
 N > 1: launched by torch.distributed.run, one rank per GPU; envs shard by
 env_id_base = rank * envs (disjoint spawn streams), no data-path collective;
@@ -48,7 +52,13 @@ def parse():
     p.add_argument('--warmup', type=int, default=30)
     p.add_argument('--envs', type=int, default=4096)
     p.add_argument('--map', default='loop_empty')
-    p.add_argument('--config', default='lane', choices=['lane', 'render', 'actor'])
+    p.add_argument('--config', default='lane', choices=['lane', 'render', 'actor', 'train'])
+    p.add_argument('--actor-mode', default='reference', choices=['reference', 'eval'],
+                   help="actor/train: 'reference' = train-mode batch-of-one BatchNorm + live "
+                        "dropout as the reference's explorers act; 'eval' = BN folded")
+    p.add_argument('--batch-size', type=int, default=0, help='train: 0 = config.json (64)')
+    p.add_argument('--buffer-size', type=int, default=131072)
+    p.add_argument('--updates-per-step', type=int, default=1)
     p.add_argument('--seed', type=int, default=1234)
     p.add_argument('--cpu-seconds', type=float, default=1.5,
                    help='per-process seconds of the CPU baseline sample (0 = skip)')
@@ -139,6 +149,8 @@ def main():
     n = args.envs
     if args.config == 'actor':
         return bench_actor(args, dev, rank, world, dist)
+    if args.config == 'train':
+        return bench_train(args, dev, rank, world, dist)
     env = VecEnv(n, seed=args.seed, device=dev.index,
                  config=EnvConfig(map_name=args.map), env_id_base=rank * n)
     out = StepOutput(n, dev, lanepos=False, tile=False)
@@ -261,7 +273,7 @@ def bench_actor(args, dev, rank, world, dist):
     n = args.envs
     torch.manual_seed(args.seed)
     roll = ActorRollout(cfg, n, maps=('small_loop', 'zigzag'), device=dev.index, seed=args.seed,
-                        env_id_base=rank * n)
+                        env_id_base=rank * n, actor_mode=args.actor_mode)
     roll.reset()
     for _ in range(args.warmup):
         roll.step()
@@ -295,21 +307,99 @@ def bench_actor(args, dev, rank, world, dist):
             'metric': METRIC, 'value': sim_steps / tmax, 'unit': 'env-steps/s', 'n_gpus': world,
             'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': tmax / args.steps * 1e3,
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
-            'dtype': 'f64 env / bf16 actor', 'data': 'synthetic',
+            'dtype': 'f64 env / %s actor' % str(roll.actor.dtype).replace('torch.', ''),
+            'data': 'synthetic',
             'config': {'workload': 'config4: %d envs/GPU, actor in the loop (ConfigActor, '
                                    'config.json), mixed small_loop/zigzag' % n,
-                       'envs_per_gpu': n, 'global_envs': n * world, 'repeat_actions': 3,
+                       'actor_mode': args.actor_mode, 'envs_per_gpu': n, 'global_envs': n * world, 'repeat_actions': 3,
                        'weights': 'random init (no checkpoint offline)',
                        'parallelism': 'env shards (%d x %d), no collective' % (world, n)},
             'counts': {'env_steps': sim_steps, 'decisions': decisions, 'resets': resets,
                        'elapsed_s': tmax},
-            'roofline': {'bound': 'mfma', 'kernel': 'actor forward (bf16 convs + linears)',
+            'roofline': {'bound': 'mfma', 'kernel': 'actor forward (fp16 MFMA convs + linears)',
                          'achieved': tflops, 'peak': BF16_DENSE_PEAK_TFLOPS, 'unit': 'TFLOP/s',
                          'frac': tflops / BF16_DENSE_PEAK_TFLOPS, 'traffic': None,
                          'avg_kernel_ms': actor_ms,
                          'algorithmic_flops_per_launch': n * flops_per_sample()},
             'cpu_baseline': None}), flush=True)
     roll.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def bench_train(args, dev, rank, world, dist):
+    """BASELINE configs[4]: full DDPG on every GPU — actor-in-loop rollout of
+    4096 envs, GPU prioritized replay, one update per decision, gradients
+    all-reduced over RCCL (world > 1).  value = env-steps/s; updates/s beside."""
+    import torch
+    from aido1_amd.actor import flops_per_sample
+    from aido1_amd.train_loop import TrainLoop
+    with open(os.path.join(REPO, 'aido1_amd', 'configs', 'reference_config.json')) as f:
+        cfg = json.load(f)
+    n = args.envs
+    loop = TrainLoop(cfg, n, device=dev.index, seed=args.seed, env_id_base=rank * n,
+                     buffer_size=args.buffer_size, batch_size=args.batch_size or None,
+                     updates_per_step=args.updates_per_step, actor_mode=args.actor_mode)
+    loop.reset()
+    for _ in range(max(args.warmup, 2)):
+        loop.step()
+    torch.cuda.synchronize(dev)
+    loop.rollout.stats(reset=True)
+    u0 = loop.updates
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        loop.step(timing=ev[k])
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    st = loop.rollout.stats()
+    actor_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    sims = torch.tensor([st['sim_steps'], st['decisions'], st['resets'], loop.updates - u0],
+                        dtype=torch.float64, device=dev)
+    tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(sims, op=dist.ReduceOp.SUM)
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+    sim_steps, decisions, resets, updates = (float(v) for v in sims.tolist())
+    tmax = float(tmax.item())
+    if rank == 0:
+        tflops = n * flops_per_sample() / (actor_ms * 1e-3) / 1e12
+        print(json.dumps({
+            'metric': METRIC, 'value': sim_steps / tmax, 'unit': 'env-steps/s', 'n_gpus': world,
+            'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': tmax / args.steps * 1e3,
+            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+            'dtype': 'f64 env / %s actor / f32 update' % str(
+                loop.rollout.actor.dtype).replace('torch.', ''), 'data': 'synthetic',
+            'config': {'workload': 'config5: %d envs/GPU full DDPG (rollout + GPU prioritized '
+                                   'replay + update + grad all-reduce)' % n,
+                       'actor_mode': args.actor_mode, 'envs_per_gpu': n,
+                       'global_envs': n * world, 'batch_size_per_gpu': loop.batch_size,
+                       'buffer_size_per_gpu': args.buffer_size,
+                       'updates_per_step': args.updates_per_step,
+                       'weights': 'random init (config.json xavier_normal)',
+                       'parallelism': 'env shards (%d x %d) + data-parallel update, RCCL '
+                                      'all-reduce of %d gradients' % (
+                                          world, n, sum(p.numel() for p in
+                                                        loop.trainer.actor.parameters()) +
+                                          sum(p.numel() for p in
+                                              loop.trainer.critic.parameters()))},
+            'counts': {'env_steps': sim_steps, 'decisions': decisions, 'resets': resets,
+                       'updates_all_ranks': updates, 'elapsed_s': tmax,
+                       'synchronous_updates_per_s': args.steps / tmax,
+                       'samples_per_s': loop.batch_size * updates / tmax},
+            'roofline': {'bound': 'mfma', 'kernel': 'actor forward (fp16 MFMA convs + linears)',
+                         'achieved': tflops, 'peak': BF16_DENSE_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                         'frac': tflops / BF16_DENSE_PEAK_TFLOPS, 'traffic': None,
+                         'avg_kernel_ms': actor_ms,
+                         'algorithmic_flops_per_launch': n * flops_per_sample()},
+            'cpu_baseline': None}), flush=True)
+    loop.rollout.close()
     if world > 1:
         dist.destroy_process_group()
 

@@ -49,3 +49,25 @@ def formula_input(n=4):
     g = torch.tensor([1.0, -1.0, 0.5, -0.5] * ((n + 3) // 4), dtype=torch.float64)[:n]
     g = g.view(n, 1, 1, 1)
     return (b * (0.5 + 0.5 * g * (r - c)) * (0.7 + 0.3 * noise)).clamp(0, 1).float()
+
+
+def formula_batch(n=16):
+    """A replay batch (obs, actions, rewards, next_obs, dones) as numpy, the
+    layout DDPGTrainer.update receives (training/trainers.py:143-146)."""
+    obs = formula_input(n)
+    nxt = obs.roll(1, 0).flip(3).contiguous()
+    act = hash_u(2 * n, 4242).reshape(n, 2).float()
+    rew = (20 * hash_u(n, 4343) - 10).float()
+    done = (torch.arange(n) % 5 == 3)
+    return obs.numpy(), act.numpy(), rew.numpy(), nxt.numpy(), done.numpy()
+
+
+def param_summary(module):
+    """Per-tensor (sum, abs-sum, 32 strided elements) of a state_dict — small
+    enough for a fixture, dense enough to catch a wrong update."""
+    out = {}
+    for k, t in module.state_dict().items():
+        v = t.detach().double().reshape(-1)
+        stride = max(1, v.numel() // 32)
+        out[k] = [float(v.sum()), float(v.abs().sum())] + [float(x) for x in v[::stride][:32]]
+    return out

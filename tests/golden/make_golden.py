@@ -368,9 +368,83 @@ def gen_actor():
     with torch.no_grad():
         out['config_actor'] = c(x).numpy()
     out['config_actor_keys'] = np.array(list(c.state_dict().keys()))
+    from models.ddpg.modules import Critic
+    from formulas import hash_u
+    cr = Critic(config['model']['critic'])
+    cr.load_state_dict(formula_state_dict(cr.state_dict()))
+    cr.eval()
+    act = hash_u(8, 77).reshape(4, 2).float()
+    with torch.no_grad():
+        out['config_critic'] = cr(x, act).numpy()
+    out['config_critic_keys'] = np.array(list(cr.state_dict().keys()))
     out['actor_cnn_keys'] = np.array(list(a.state_dict().keys()))
     np.savez_compressed(os.path.join(HERE, 'actor.npz'), **out)
     print('wrote actor.npz')
+
+
+def no_dropout(net_config):
+    for part in net_config:
+        for branch in part.get('modules', []):
+            for m in branch:
+                if m['name'] == 'dropout':
+                    m['args']['p'] = 0.0
+    return net_config
+
+
+def gen_ddpg_update(double=False):
+    """training/trainers.py DDPGTrainer.update, run as the reference runs it
+    (models in train mode: BatchNorm on batch statistics), three updates on a
+    formula batch.  Dropout p is set to 0 so the run is deterministic.
+    double=True: the same in float64 (models .double(), the module-level
+    to_torch_tensor helper producing float64) — float32 runs of this update
+    drift apart after the first Adam step (near-zero bias gradients get full
+    +-lr steps), float64 pins all three updates tightly."""
+    import copy
+    import threading
+    from types import SimpleNamespace
+
+    import torch
+    from models.ddpg.model import create_model
+    from training.trainers import DDPGTrainer
+    from utils.util import TrainingDecay
+    sys.path.insert(0, HERE)
+    from formulas import formula_batch, formula_state_dict, param_summary
+    with open(os.path.join(REF, 'config.json')) as f:
+        cfg = json.load(f)
+    no_dropout(cfg['model']['actor'])
+    no_dropout(cfg['model']['critic'])
+    torch.manual_seed(0)
+    target = create_model(cfg['model'])
+    target.actor.load_state_dict(formula_state_dict(target.actor.state_dict()))
+    target.critic.load_state_dict(formula_state_dict(target.critic.state_dict()))
+    target.train()
+    if double:
+        import training.trainers as trainers_mod
+        target.actor.double()
+        target.critic.double()
+        trainers_mod.to_torch_tensor = lambda a, cpu=False: torch.from_numpy(
+            np.asarray(a, np.float64))
+    model = copy.deepcopy(target)            # managers.py:82
+    tr = DDPGTrainer(cfg, 0, target, copy.deepcopy(target), [model], None, None,
+                     threading.Lock(), None, None, SimpleNamespace(value=0),
+                     SimpleNamespace(value=0))
+    tr.target_actor, tr.target_critic = target.get_actor(), target.get_critic()
+    tr.actor, tr.critic = model.get_actor(), model.get_critic()
+    tr.actor_optim = torch.optim.Adam(tr.actor.parameters(), lr=0.)
+    tr.critic_optim = torch.optim.Adam(tr.critic.parameters(), lr=0.)
+    tr.actor_decay = TrainingDecay(cfg['training']['actor_train_decay'])
+    tr.critic_decay = TrainingDecay(cfg['training']['critic_train_decay'])
+    batch = formula_batch(16)
+    out = {'critic_loss': [], 'actor_loss': [], 'td_error': []}
+    for _ in range(3):
+        metrics, info = tr.update(batch)
+        out['critic_loss'].append(float(metrics['critic_loss']))
+        out['actor_loss'].append(float(metrics['actor_loss']))
+        out['td_error'].append([float(x) for x in info['td_error'].reshape(-1)])
+    for name, net in (('actor', tr.actor), ('critic', tr.critic), ('target_actor', tr.target_actor),
+                      ('target_critic', tr.target_critic)):
+        out[name] = param_summary(net)
+    dump('ddpg_update_f64.json' if double else 'ddpg_update.json', out)
 
 
 def gen_config_keys():
@@ -412,6 +486,8 @@ def main():
     gen_prioritized_replay()
     gen_random_process_and_decay()
     gen_actor()
+    gen_ddpg_update()
+    gen_ddpg_update(double=True)
 
 
 if __name__ == '__main__':

@@ -63,3 +63,41 @@ def test_flops_figure():
     from aido1_amd.actor import flops_per_sample
     # 50.8 M MAC = 101.6 MFLOP per env per decision
     assert abs(flops_per_sample() / 1e6 - 101.6) < 0.2
+
+
+def _per_sample_train_mode(actor, x):
+    """The reference's acting: train-mode modules, one observation per call."""
+    import copy as _copy
+    a = _copy.deepcopy(actor)
+    a.train()
+    with torch.no_grad():
+        return torch.cat([a(x[i:i + 1]) for i in range(x.shape[0])])
+
+
+def test_fused_reference_mode_equals_per_sample_train_mode():
+    from aido1_amd.actor import ConfigActor, FusedActor
+    from test_trainer import no_dropout
+    a = ConfigActor(no_dropout(golden('reference_config.json')['model']['actor']))
+    a.load_state_dict(formula_state_dict(a.state_dict()))
+    x = formula_input(4)
+    ref = _per_sample_train_mode(a, x)
+    f = FusedActor(a, dtype=torch.float32, mode='reference')
+    y = f(x)
+    np.testing.assert_allclose(y.numpy(), ref.numpy(), rtol=1e-4, atol=1e-5)
+    # ring order: the same stack stored in rotated slots
+    order = [2, 0, 1]
+    ring = torch.empty_like(x)
+    ring[:, order] = x
+    np.testing.assert_allclose(f(ring, order).numpy(), ref.numpy(), rtol=1e-4, atol=1e-5)
+
+
+def test_fused_reference_mode_dropout_live_and_refresh():
+    from aido1_amd.actor import ConfigActor, FusedActor
+    a = ConfigActor(golden('reference_config.json')['model']['actor'])
+    f = FusedActor(a, dtype=torch.float32, mode='reference')
+    assert f.p_drop == 0.5
+    x = formula_input(4)
+    assert not torch.equal(f(x), f(x))              # dropout is live in train mode
+    b = ConfigActor(golden('reference_config.json')['model']['actor'])
+    f.refresh(b)
+    assert torch.equal(f.w[2], b.layers()[0][2].weight.contiguous(memory_format=torch.channels_last))

@@ -43,3 +43,57 @@ def test_rollout_runs_and_counts(gpu):
     a = roll.actions
     assert (a.abs() <= 1.0).all()
     roll.close()
+
+
+@pytest.mark.parametrize('dtype,tol', [(torch.float32, 2e-5), (torch.bfloat16, 2e-2)])
+def test_sample_norm_kernel_matches_two_pass(gpu, dtype, tol):
+    """dt_sample_norm (include/dtactor.h) vs a float64 two-pass restatement of
+    lrelu -> BatchNorm2d(train) on each sample alone."""
+    from aido1_amd.actor import ConfigActor, FusedActor
+    f = FusedActor(ConfigActor(golden('reference_config.json')['model']['actor']),
+                   dtype=dtype, mode='reference').to(gpu)
+    torch.manual_seed(0)
+    for i, (h, w) in enumerate([(57, 77), (27, 37), (12, 17), (9, 14)]):
+        with torch.no_grad():
+            f.gamma[i].uniform_(0.5, 1.5)
+            f.beta[i].uniform_(-0.1, 0.1)
+        x = (torch.randn(5, 32, h, w, device=gpu) * 2 + 3).to(dtype) \
+            .contiguous(memory_format=torch.channels_last)
+        xd = torch.nn.functional.leaky_relu(x.double())
+        m = xd.mean((2, 3), keepdim=True)
+        v = (xd - m).square().mean((2, 3), keepdim=True)
+        ref = (xd - m) / torch.sqrt(v + 1e-5) * f.gamma[i].double().view(1, -1, 1, 1) + \
+            f.beta[i].double().view(1, -1, 1, 1)
+        y = f._lrelu_sample_norm(x.clone(memory_format=torch.channels_last), i)
+        err = (y.double() - ref).abs().max().item()
+        assert err < tol * max(1.0, ref.abs().max().item()), (i, err)
+
+
+def test_reference_mode_matches_per_sample_train_mode(gpu):
+    from aido1_amd.actor import ConfigActor, FusedActor
+    from test_trainer import no_dropout
+    a = ConfigActor(no_dropout(golden('reference_config.json')['model']['actor']))
+    a.load_state_dict(formula_state_dict(a.state_dict()))
+    x = formula_input(4)
+    a.train()
+    with torch.no_grad():
+        ref = torch.cat([a(x[i:i + 1]) for i in range(4)])
+    f32 = FusedActor(a.to(gpu), dtype=torch.float32, mode='reference')
+    np.testing.assert_allclose(f32(x.to(gpu)).cpu().numpy(), ref.numpy(), rtol=1e-4, atol=1e-4)
+    # fp16: per-sample normalisation of nearly flat channels amplifies the
+    # conv outputs' fp16 rounding; formula frames are the harsh case
+    h = FusedActor(a, dtype=torch.float16, mode='reference')
+    assert torch.max(torch.abs(h(x.to(gpu)).cpu() - ref)) < 5e-2
+    # rendered frames (what the rollout feeds it)
+    from aido1_amd.rollout import ActorRollout
+    roll = ActorRollout(golden('reference_config.json'), 32, device=0, seed=3)
+    roll.reset()
+    for _ in range(4):
+        roll.step()
+    frames = roll.stack()
+    a_cpu = ConfigActor(no_dropout(golden('reference_config.json')['model']['actor']))
+    a_cpu.load_state_dict(formula_state_dict(a_cpu.state_dict()))
+    a_cpu.train()
+    with torch.no_grad():
+        ref = torch.cat([a_cpu(frames[i:i + 1].cpu()) for i in range(32)])
+    assert torch.max(torch.abs(h(frames).cpu() - ref)) < 1.5e-2

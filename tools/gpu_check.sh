@@ -22,6 +22,10 @@ if [ -n "$RENDER" ]; then
 fi
 if [ -n "$ACTOR" ]; then
   run bench_actor 600 python bench.py --config actor --steps 100 --warmup 10 --cpu-seconds 0
+  run bench_actor_eval 600 python bench.py --config actor --actor-mode eval --steps 100 --warmup 10 --cpu-seconds 0
+fi
+if [ -n "$TRAIN" ]; then
+  run bench_train 600 python bench.py --config train --steps 50 --warmup 5 --cpu-seconds 0
 fi
 if [ -n "$PROFILE" ]; then
   export TMPDIR=/tmp
