@@ -1,20 +1,12 @@
 // Observation path: build-defined 120x160 ego-centric top-down raster of the
 // lane markings fused with the features/line_detector1.py colour/edge filter
-// and PreliminaryTransformer's grey conversion.  One 256-thread workgroup per
-// environment; the frame never leaves LDS until its outputs are written:
-//
-//   raster:  tile background per pixel (get_grid_coords of the pixel's world
-//            point) + lane markings as Bresenham polylines (utils/bresenham.py
-//            semantics: both endpoints, major-axis swap, D = 2dy - dx)
-//   pass A:  Sobel 3x3 (max-|dx|+|dy| channel), NMS direction, HSV inRange
-//            bits, rgb2gray -> gray (f32, written here: 16 B per lane)
-//   pass B:  Canny non-maximum suppression + double threshold
-//   hyst:    Canny hysteresis to a fixed point (__syncthreads_or)
-//   pass C:  ellipse dilation of the colour masks + edges -> 4 u8 masks
-//            (16 B per lane stores)
-//
-// LDS: palette image 19.2 KB + magnitudes 38.4 KB + work bits 19.2 KB ~ 78 KB
-// -> two workgroups per CU.
+// and PreliminaryTransformer's grey conversion.  render_kernel (below, "fused
+// render kernel") runs one 768-thread workgroup per environment and keeps the
+// frame in LDS (~71 KB: 4-pixel palette words + a 16-bit work image) until its
+// outputs are written: grey into the frame ring, four u8 masks.  Markings are
+// Bresenham polylines (utils/bresenham.py semantics: both endpoints,
+// major-axis swap, D = 2dy - dx).  line_detect_kernel is the standalone
+// LineDetectorHSV on caller-supplied BGR images (dt_line_detect).
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
