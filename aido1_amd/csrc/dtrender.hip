@@ -402,6 +402,69 @@ __device__ inline int mag16(const FusedLds& S, int r, int c) {
                                                                   : 0;
 }
 
+__device__ __forceinline__ uint32_t bg_color(const FusedLds& S, const RenderArgs& a, float fi,
+                                             float fj) {
+  if (fi >= 0.0f && fj >= 0.0f && fi < (float)a.width && fj < (float)a.height) {
+    const int k = S.kind[(int)fj * a.width + (int)fi];
+    return k > 0 ? PAL_ROAD : (k == 0 ? PAL_OFFROAD : PAL_FLOOR);
+  }
+  return PAL_FLOOR;
+}
+
+// phase 4 of render_kernel for a dilation radius known at compile time: the
+// ellipse offsets become constant byte shifts (one v_alignbyte each) and the
+// structuring-element test a scalar branch.
+template <int R>
+__device__ __forceinline__ void write_masks(const FusedLds& S, const LineDev& L, uint8_t* mb) {
+  const uint32_t blo = S.bits_lo, bhi = S.bits_hi;
+  const uint64_t dmask = L.dil_mask;
+  for (int q = threadIdx.x; q < NW / 4; q += blockDim.x) {
+    const int r = q / (WPR / 4), cw0 = 4 * (q - r * (WPR / 4));
+    uint32_t dil[4] = {0, 0, 0, 0};
+#pragma unroll
+    for (int dy = -R; dy <= R; ++dy) {
+      const int rr = r + dy;
+      if ((unsigned)rr >= (unsigned)H) continue;
+      const uint32_t* row = S.img + rr * WPR;
+      const uint4 cur = *reinterpret_cast<const uint4*>(row + cw0);
+      // palette index bytes -> colour-bit bytes (v_perm LUT); 0 outside the image
+      const uint32_t wv[6] = {
+          cw0 > 0 ? __builtin_amdgcn_perm(bhi, blo, row[cw0 - 1]) : 0u,
+          __builtin_amdgcn_perm(bhi, blo, cur.x), __builtin_amdgcn_perm(bhi, blo, cur.y),
+          __builtin_amdgcn_perm(bhi, blo, cur.z), __builtin_amdgcn_perm(bhi, blo, cur.w),
+          cw0 + 4 < WPR ? __builtin_amdgcn_perm(bhi, blo, row[cw0 + 4]) : 0u};
+#pragma unroll
+      for (int dx = -R; dx <= R; ++dx) {
+        if (!((dmask >> ((dy + 3) * 7 + (dx + 3))) & 1ull)) continue;  // uniform
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dil[j] |= shift_bytes(wv[j], wv[j + 1], wv[j + 2], dx);
+      }
+    }
+    // edge bytes from the 16 work entries of this chunk
+    const uint16_t* wk = S.work + r * W + 4 * cw0;
+    uint32_t edg[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const uint2 v = *reinterpret_cast<const uint2*>(wk + 4 * j);
+      edg[j] = ((v.x >> 14) & 1u) | ((v.x >> 30) & 1u) << 8 | ((v.y >> 14) & 1u) << 16 |
+               ((v.y >> 30) & 1u) << 24;
+    }
+    uint32_t o[4][4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      o[0][j] = (dil[j] & 0x01010101u) * 255u;
+      o[1][j] = ((dil[j] >> 1) & 0x01010101u) * 255u;
+      o[2][j] = ((dil[j] >> 2) & 0x01010101u) * 255u;
+      o[3][j] = edg[j] * 255u;
+    }
+    const int p0 = r * W + 4 * cw0;
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+      *reinterpret_cast<uint4*>(mb + k * NPIX + p0) = make_uint4(o[k][0], o[k][1], o[k][2],
+                                                                  o[k][3]);
+  }
+}
+
 __global__ __launch_bounds__(1024) void render_kernel(RenderArgs a) {
   __shared__ __attribute__((aligned(16))) FusedLds S;
   const int e = blockIdx.x;
@@ -449,18 +512,30 @@ __global__ __launch_bounds__(1024) void render_kernel(RenderArgs a) {
     const int r = w / WPR, c0 = 4 * (w - r * WPR);
     const float f = (119.5f - (float)r) * kRes;
     const float bx = V.cx + f * V.dirx, bz = V.cz + f * V.dirz;
-    uint32_t word = 0;
+    // tiles are convex and each coordinate is a monotone float function of the
+    // column, so when both end pixels of the word fall in one tile all four do
+    float fi4[4], fj4[4];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 4; i += 3) {
       const float l = ((float)(c0 + i) - 79.5f) * kRes;
       const float wx = bx + l * V.rx, wz = bz + l * V.rz;
-      const float fi = floorf(wx * a.inv_ts), fj = floorf(wz * a.inv_ts);
-      uint32_t col = PAL_FLOOR;
-      if (fi >= 0.0f && fj >= 0.0f && fi < (float)a.width && fj < (float)a.height) {
-        const int k = S.kind[(int)fj * a.width + (int)fi];
-        col = k > 0 ? PAL_ROAD : (k == 0 ? PAL_OFFROAD : PAL_FLOOR);
+      fi4[i] = floorf(wx * a.inv_ts);
+      fj4[i] = floorf(wz * a.inv_ts);
+    }
+    uint32_t word;
+    if (fi4[0] == fi4[3] && fj4[0] == fj4[3]) {
+      word = bg_color(S, a, fi4[0], fj4[0]) * 0x01010101u;
+    } else {
+#pragma unroll
+      for (int i = 1; i < 3; ++i) {
+        const float l = ((float)(c0 + i) - 79.5f) * kRes;
+        const float wx = bx + l * V.rx, wz = bz + l * V.rz;
+        fi4[i] = floorf(wx * a.inv_ts);
+        fj4[i] = floorf(wz * a.inv_ts);
       }
-      word |= col << (8 * i);
+      word = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) word |= bg_color(S, a, fi4[i], fj4[i]) << (8 * i);
     }
     S.img[w] = word;
   }
@@ -483,22 +558,22 @@ __global__ __launch_bounds__(1024) void render_kernel(RenderArgs a) {
     if (act) {
       const int r = w / WPR, cw = w - r * WPR;
       const int ru = r > 0 ? r - 1 : 0, rd = r < H - 1 ? r + 1 : H - 1;
+      // all nine words loaded up front, combined branch-free.  Side words at
+      // the image edge clamp to the word itself: BORDER_REPLICATE repeats the
+      // edge pixel, whose byte the mid / up / down comparisons already cover.
+      const int cl = cw > 0 ? cw - 1 : cw, cr = cw < WPR - 1 ? cw + 1 : cw;
       const uint32_t mid = S.img[w];
-      const uint32_t rep = (mid & 255u) * 0x01010101u;
-      // side bytes (BORDER_REPLICATE: an edge column repeats itself)
-      const uint32_t lm = cw > 0 ? 1u : 0u, rm = cw < WPR - 1 ? 1u : 0u;
-      bool u = mid == rep && S.img[ru * WPR + cw] == rep && S.img[rd * WPR + cw] == rep;
-      if (lm) {
-        u = u && (S.img[ru * WPR + cw - 1] >> 24) == (mid & 255u) &&
-            (S.img[r * WPR + cw - 1] >> 24) == (mid & 255u) &&
-            (S.img[rd * WPR + cw - 1] >> 24) == (mid & 255u);
-      }
-      if (rm) {
-        u = u && (S.img[ru * WPR + cw + 1] & 255u) == (mid & 255u) &&
-            (S.img[r * WPR + cw + 1] & 255u) == (mid & 255u) &&
-            (S.img[rd * WPR + cw + 1] & 255u) == (mid & 255u);
-      }
-      uni = u;
+      const uint32_t up = S.img[ru * WPR + cw], dn = S.img[rd * WPR + cw];
+      const uint32_t ul = S.img[ru * WPR + cl], ml = S.img[r * WPR + cl],
+                     dl = S.img[rd * WPR + cl];
+      const uint32_t ur = S.img[ru * WPR + cr], mr = S.img[r * WPR + cr],
+                     dr = S.img[rd * WPR + cr];
+      const uint32_t b = mid & 255u;
+      const uint32_t rep = b * 0x01010101u;
+      const uint32_t diff = (mid ^ rep) | (up ^ rep) | (dn ^ rep) |
+                            (((ul >> 24) ^ b) | ((ml >> 24) ^ b) | ((dl >> 24) ^ b)) |
+                            (((ur ^ b) | (mr ^ b) | (dr ^ b)) & 255u);
+      uni = diff == 0u;
       if (uni) *reinterpret_cast<uint2*>(S.work + 4 * w) = make_uint2(0u, 0u);
       if (gbase) {
         float4 g;
@@ -507,7 +582,8 @@ __global__ __launch_bounds__(1024) void render_kernel(RenderArgs a) {
         g.z = S.pal_gray[(mid >> 16) & 255u];
         g.w = S.pal_gray[mid >> 24];
         if (fresh) {
-          for (int sl = 0; sl < a.slots; ++sl)
+#pragma clang loop vectorize(disable) interleave(disable)
+          for (int sl = 0; sl < a.slots; ++sl)  // 16-B stores, not split by the vectoriser
             *reinterpret_cast<float4*>(gbase + sl * NPIX + 4 * w) = g;
         } else {
           *reinterpret_cast<float4*>(gbase + a.slot * NPIX + 4 * w) = g;
@@ -638,50 +714,11 @@ __global__ __launch_bounds__(1024) void render_kernel(RenderArgs a) {
   // phase 4: masks, 16 pixels (4 words) per lane
   if (a.masks && !(a.skip & 32)) {
     uint8_t* mb = a.masks + (size_t)e * 4 * NPIX;
-    const int R = L.dil_r;
-    const uint32_t blo = S.bits_lo, bhi = S.bits_hi;
-    for (int q = tid; q < NW / 4; q += blockDim.x) {
-      const int r = q / (WPR / 4), cw0 = 4 * (q - r * (WPR / 4));
-      uint32_t dil[4] = {0, 0, 0, 0};
-      for (int dy = -R; dy <= R; ++dy) {
-        const int rr = r + dy;
-        if ((unsigned)rr >= (unsigned)H) continue;
-        const uint32_t* row = S.img + rr * WPR;
-        const uint4 cur = *reinterpret_cast<const uint4*>(row + cw0);
-        // palette index bytes -> colour-bit bytes (v_perm LUT); 0 outside the image
-        const uint32_t wv[6] = {
-            cw0 > 0 ? __builtin_amdgcn_perm(bhi, blo, row[cw0 - 1]) : 0u,
-            __builtin_amdgcn_perm(bhi, blo, cur.x), __builtin_amdgcn_perm(bhi, blo, cur.y),
-            __builtin_amdgcn_perm(bhi, blo, cur.z), __builtin_amdgcn_perm(bhi, blo, cur.w),
-            cw0 + 4 < WPR ? __builtin_amdgcn_perm(bhi, blo, row[cw0 + 4]) : 0u};
-        for (int dx = -R; dx <= R; ++dx) {
-          if (!((L.dil_mask >> ((dy + 3) * 7 + (dx + 3))) & 1ull)) continue;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) dil[j] |= shift_bytes(wv[j], wv[j + 1], wv[j + 2], dx);
-        }
-      }
-      // edge bytes from the 16 work entries of this chunk
-      const uint16_t* wk = S.work + r * W + 4 * cw0;
-      uint32_t edg[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const uint2 v = *reinterpret_cast<const uint2*>(wk + 4 * j);
-        edg[j] = ((v.x >> 14) & 1u) | ((v.x >> 30) & 1u) << 8 | ((v.y >> 14) & 1u) << 16 |
-                 ((v.y >> 30) & 1u) << 24;
-      }
-      uint32_t o[4][4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        o[0][j] = (dil[j] & 0x01010101u) * 255u;
-        o[1][j] = ((dil[j] >> 1) & 0x01010101u) * 255u;
-        o[2][j] = ((dil[j] >> 2) & 0x01010101u) * 255u;
-        o[3][j] = edg[j] * 255u;
-      }
-      const int p0 = r * W + 4 * cw0;
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-        *reinterpret_cast<uint4*>(mb + k * NPIX + p0) = make_uint4(o[k][0], o[k][1], o[k][2],
-                                                                    o[k][3]);
+    switch (L.dil_r) {
+      case 0: write_masks<0>(S, L, mb); break;
+      case 1: write_masks<1>(S, L, mb); break;
+      case 2: write_masks<2>(S, L, mb); break;
+      default: write_masks<3>(S, L, mb); break;
     }
   }
 }
