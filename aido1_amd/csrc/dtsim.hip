@@ -59,7 +59,8 @@ __global__ __launch_bounds__(64) void step_kernel(dt::State st, dt::MapDev md, d
                                                   uint8_t* __restrict__ done_out,
                                                   float2* __restrict__ obs,
                                                   double* __restrict__ lanepos,
-                                                  int32_t* __restrict__ tile_out) {
+                                                  int32_t* __restrict__ tile_out,
+                                                  uint32_t* __restrict__ list_count) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const MapLds M = dt::stage_map(md, lds);
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
@@ -179,6 +180,14 @@ __global__ __launch_bounds__(64) void step_kernel(dt::State st, dt::MapDev md, d
   dt::wave_add(st.stats + 0, nsim);
   dt::wave_add(st.stats + 1, active ? 1u : 0u);
   dt::wave_add(st.stats + 3, (active && dn) ? 1u : 0u);
+  if (list_count) {  // this wave's finished envs -> its own 64-slot segment, count stored
+    const bool fin = active && dn;  // (plain stores: nothing to reset between steps)
+    const uint64_t m = __ballot(fin);
+    const int lane = threadIdx.x & 63;
+    const int wave = e >> 6;
+    if (fin) st.spawn_list[64 * wave + __popcll(m & ((1ull << lane) - 1ull))] = e;
+    if (lane == 0) list_count[wave] = (uint32_t)__popcll(m);
+  }
   if (active) {
     if (obs) obs[e] = inl ? make_float2((float)lp[0], (float)lp[3]) : make_float2(0.0f, 0.0f);
     st.x[e] = x;
@@ -189,39 +198,93 @@ __global__ __launch_bounds__(64) void step_kernel(dt::State st, dt::MapDev md, d
   }
 }
 
-// Simulator.reset + EnvironmentWrapper.reset counters (A13): one wave per env,
-// so the envs that finished in a step respawn in parallel across the chip
-// instead of one after another inside their step wave.  flags: NULL = every
-// env, else envs with flags[e] != 0 (the reset mask, or dt_step's done flags
-// for the auto-reset).  obs (nullable) receives the new (dist, angle_rad).
+// Simulator.reset + EnvironmentWrapper.reset counters (A13): one 256-thread
+// workgroup per pending env, so the envs that finished in a step respawn in
+// parallel across the chip instead of one after another inside their step
+// wave.  Mask mode (dt_reset): one block per env, flags NULL = every env, else
+// envs with flags[e] != 0.  List mode (dt_step's auto-reset): a fixed grid
+// strides over the done list step_kernel compacted.  obs (nullable) receives
+// the new (dist, angle_rad).
 constexpr int kSpawnThreads = 256;  // proposals per round: one accept in ~37, so ~1 round
+constexpr int kSpawnGrid = 1024;    // auto-reset launch: 4 workgroups per CU
+
+// The i-th finished env of the last dt_step: wave w's envs occupy global
+// indices [prefix(w), prefix(w) + count[w]) of the concatenated segments.
+__device__ int list_env(const int32_t* list, const uint32_t* count, int n_waves, uint32_t i) {
+  const int lane = threadIdx.x & 63;
+  uint32_t base = 0;
+  for (int w0 = 0; w0 < n_waves; w0 += 64) {
+    const uint32_t c = (w0 + lane < n_waves) ? count[w0 + lane] : 0u;
+    uint32_t incl = c;  // inclusive scan over the 64 lanes
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const uint32_t t = __shfl_up(incl, o);
+      if (lane >= o) incl += t;
+    }
+    const uint32_t total = __shfl(incl, 63);
+    if (i < base + total) {
+      const uint64_t past = __ballot(base + incl <= i);  // waves wholly before i
+      const int w = __popcll(past);
+      const uint32_t before = w == 0 ? 0u : __shfl(incl, w - 1);
+      return list[64 * (w0 + w) + (i - base - before)];
+    }
+    base += total;
+  }
+  return -1;
+}
+
+__device__ uint32_t list_total(const uint32_t* count, int n_waves) {
+  const int lane = threadIdx.x & 63;
+  uint32_t s = 0;
+  for (int w = lane; w < n_waves; w += 64) s += count[w];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+  return s;
+}
 
 __global__ __launch_bounds__(kSpawnThreads) void spawn_kernel(dt::State st, dt::MapDev md, dt::Geo g,
                                                    uint32_t max_attempts, uint32_t env_base,
                                                    const uint8_t* __restrict__ flags,
-                                                   float2* __restrict__ obs) {
+                                                   const uint32_t* __restrict__ list_count,
+                                                   int n_waves, float2* __restrict__ obs) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  const int e = blockIdx.x;
-  if (flags != nullptr && flags[e] == 0) return;  // block-uniform
   __shared__ double scratch[6 * (kSpawnThreads / 64)];
+  __shared__ int s_env;
+  // list mode (auto-reset): blocks stride over dt_step's finished envs;
+  // mask mode: one block per env, flags NULL = every env
+  const uint32_t cnt = list_count ? list_total(list_count, n_waves) : (uint32_t)gridDim.x;
+  if (blockIdx.x >= cnt) return;  // block-uniform
+  if (!list_count && flags != nullptr && flags[blockIdx.x] == 0) return;
   const MapLds M = dt::stage_map(md, lds);
-  double x = 0.0, z = 0.0, ang = 0.0, dist = 0.0, arad = 0.0;
-  const uint32_t episode = st.episode[e];
-  const bool ok = dt::spawn_block(M, g, max_attempts, env_base + (uint32_t)e, st.seed[e],
-                                  episode, scratch, x, z, ang, dist, arad);
-  if (threadIdx.x != 0) return;
-  if (!ok) {
-    atomicOr(st.err, dt::kErrSpawn);
-    return;
+  for (uint32_t i = blockIdx.x; i < cnt; i += list_count ? gridDim.x : cnt) {
+    if (list_count) {
+      if (threadIdx.x < 64) {
+        const int env = list_env(st.spawn_list, list_count, n_waves, i);
+        if (threadIdx.x == 0) s_env = env;
+      }
+      __syncthreads();
+    }
+    const int e = list_count ? s_env : (int)i;
+    double x = 0.0, z = 0.0, ang = 0.0, dist = 0.0, arad = 0.0;
+    const uint32_t episode = st.episode[e];
+    const bool ok = dt::spawn_block(M, g, max_attempts, env_base + (uint32_t)e, st.seed[e],
+                                    episode, scratch, x, z, ang, dist, arad);
+    if (threadIdx.x == 0) {
+      if (!ok) {
+        atomicOr(st.err, dt::kErrSpawn);
+      } else {
+        st.x[e] = x;
+        st.z[e] = z;
+        st.angle[e] = ang;
+        st.step_count[e] = 0u;
+        st.env_step[e] = 0u;
+        st.episode[e] = episode + 1u;
+        atomicAdd(st.stats + 2, 1ull);
+        if (obs) obs[e] = make_float2((float)dist, (float)arad);  // accepted => in a lane
+      }
+    }
+    __syncthreads();  // scratch / s_env are reused by the next env of this block
   }
-  st.x[e] = x;
-  st.z[e] = z;
-  st.angle[e] = ang;
-  st.step_count[e] = 0u;
-  st.env_step[e] = 0u;
-  st.episode[e] = episode + 1u;
-  atomicAdd(st.stats + 2, 1ull);
-  if (obs) obs[e] = make_float2((float)dist, (float)arad);  // accepted => in a lane
 }
 
 __global__ __launch_bounds__(64) void lane_pos_kernel(dt::State st, dt::MapDev md, dt::Geo g,
@@ -366,7 +429,7 @@ int dt_create(const dt_config* cfg, const dt_map* map, uint64_t seed, int32_t n_
 
   // state: x z angle seed (8 B) | step_count env_step episode (4 B) | err
   const size_t N = (size_t)n_envs, N8 = N * 8, N4 = (N * 4 + 255) & ~255ul;
-  const size_t total = 4 * N8 + 3 * N4 + 256 + 256;
+  const size_t total = 4 * N8 + 3 * N4 + 256 + 256 + N4 + N4;
   if (hipMalloc(&h->st_buf, total) != hipSuccess) return fail("hipMalloc(state)");
   if (hipMemset(h->st_buf, 0, total) != hipSuccess) return fail("hipMemset(state)");
   char* sb = (char*)h->st_buf;
@@ -379,6 +442,8 @@ int dt_create(const dt_config* cfg, const dt_map* map, uint64_t seed, int32_t n_
   h->st.episode = (uint32_t*)(sb + 4 * N8 + 2 * N4);
   h->st.err = (uint32_t*)(sb + 4 * N8 + 3 * N4);
   h->st.stats = (unsigned long long*)(sb + 4 * N8 + 3 * N4 + 256);
+  h->st.spawn_list = (int32_t*)(sb + 4 * N8 + 3 * N4 + 512);
+  h->st.spawn_count = (uint32_t*)(sb + 4 * N8 + 4 * N4 + 512);
   *out = h;
   rc = dt_render_init(h, map);
   if (rc == DT_OK) rc = dt_seed(h, nullptr, seed, 0);
@@ -418,7 +483,7 @@ int dt_reset(dt_handle* h, const uint8_t* mask, void* stream) {
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(spawn_kernel, dim3(h->n), dim3(kSpawnThreads), h->lds_bytes, s, h->st,
                      h->map, h->geo, h->sc.max_spawn_attempts, h->env_base, mask,
-                     (float2*)nullptr);
+                     (const uint32_t*)nullptr, 0, (float2*)nullptr);
   HIP_OR_FAIL(h, hipGetLastError());
   return DT_OK;
 }
@@ -431,14 +496,18 @@ int dt_step(dt_handle* h, const float* actions, double* reward, double* reward_m
     return DT_E_ARG;
   }
   hipStream_t s = (hipStream_t)stream;
+  uint32_t* list_count = h->sc.auto_reset ? h->st.spawn_count : nullptr;
   hipLaunchKernelGGL(step_kernel, dim3(grid_of(h->n)), dim3(dt::kWave), h->lds_bytes, s, h->st,
                      h->map, h->geo, h->sc, h->n, h->env_base, (const float2*)actions, reward, reward_mod,
-                     done, (float2*)obs, lanepos, tile);
+                     done, (float2*)obs, lanepos, tile, list_count);
   HIP_OR_FAIL(h, hipGetLastError());
   if (h->sc.auto_reset) {
-    hipLaunchKernelGGL(spawn_kernel, dim3(h->n), dim3(kSpawnThreads), h->lds_bytes, s, h->st,
-                       h->map, h->geo, h->sc.max_spawn_attempts, h->env_base,
-                       (const uint8_t*)done, (float2*)obs);
+    // a fixed grid over the compacted done list (a few hundred of 4096 envs
+    // finish per decision): no launch of thousands of idle workgroups
+    const int grid = h->n < kSpawnGrid ? h->n : kSpawnGrid;
+    hipLaunchKernelGGL(spawn_kernel, dim3(grid), dim3(kSpawnThreads), h->lds_bytes, s, h->st,
+                       h->map, h->geo, h->sc.max_spawn_attempts, h->env_base, (const uint8_t*)nullptr,
+                       (const uint32_t*)list_count, grid_of(h->n), (float2*)obs);
     HIP_OR_FAIL(h, hipGetLastError());
   }
   return DT_OK;

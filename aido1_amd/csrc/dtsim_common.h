@@ -40,6 +40,8 @@ struct State {
   uint32_t* episode;
   uint32_t* err;  // one word, OR of kErr*
   unsigned long long* stats;  // [4] sim steps, decisions, resets, episodes done
+  int32_t* spawn_list;        // [n] envs that finished in the last dt_step, 64 per step wave
+  uint32_t* spawn_count;      // [ceil(n/64)] how many of its 64 slots each step wave filled
 };
 
 // One atomic per wave: lane-sum through the 64-wide reduction, lane 0 adds.
