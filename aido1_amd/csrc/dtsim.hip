@@ -60,11 +60,13 @@ __global__ __launch_bounds__(64) void step_kernel(dt::State st, dt::MapDev md, d
                                                   float2* __restrict__ obs,
                                                   double* __restrict__ lanepos,
                                                   int32_t* __restrict__ tile_out,
-                                                  uint32_t* __restrict__ list_count) {
+                                                  uint32_t* __restrict__ list_count,
+                                                  const uint8_t* __restrict__ step_mask) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const MapLds M = dt::stage_map(md, lds);
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  const bool active = e < n;
+  // envs outside step_mask (dt_step_masked) are left exactly as they were
+  const bool active = e < n && (step_mask == nullptr || step_mask[e] != 0);
   const int ei = active ? e : 0;
 
   double x = st.x[ei], z = st.z[ei], ang = st.angle[ei];
@@ -478,6 +480,15 @@ int dt_seed(dt_handle* h, const uint64_t* seeds, uint64_t base, uint32_t env_id_
   return DT_OK;
 }
 
+int dt_seed_env(dt_handle* h, int32_t env, uint64_t seed) {
+  if (!h || env < 0 || env >= h->n) return DT_E_ARG;
+  HIP_OR_FAIL(h, hipSetDevice(h->device));
+  const uint32_t zero = 0;
+  HIP_OR_FAIL(h, hipMemcpy(h->st.seed + env, &seed, 8, hipMemcpyHostToDevice));
+  HIP_OR_FAIL(h, hipMemcpy(h->st.episode + env, &zero, 4, hipMemcpyHostToDevice));
+  return DT_OK;
+}
+
 int dt_reset(dt_handle* h, const uint8_t* mask, void* stream) {
   if (!h) return DT_E_ARG;
   hipStream_t s = (hipStream_t)stream;
@@ -488,8 +499,9 @@ int dt_reset(dt_handle* h, const uint8_t* mask, void* stream) {
   return DT_OK;
 }
 
-int dt_step(dt_handle* h, const float* actions, double* reward, double* reward_mod,
-            uint8_t* done, float* obs, double* lanepos, int32_t* tile, void* stream) {
+int dt_step_masked(dt_handle* h, const uint8_t* mask, const float* actions, double* reward,
+                   double* reward_mod, uint8_t* done, float* obs, double* lanepos, int32_t* tile,
+                   void* stream) {
   if (!h) return DT_E_ARG;
   if (!actions || !reward || !reward_mod || !done) {
     h->err = "dt_step: actions, reward, reward_mod and done are required";
@@ -499,11 +511,11 @@ int dt_step(dt_handle* h, const float* actions, double* reward, double* reward_m
   uint32_t* list_count = h->sc.auto_reset ? h->st.spawn_count : nullptr;
   hipLaunchKernelGGL(step_kernel, dim3(grid_of(h->n)), dim3(dt::kWave), h->lds_bytes, s, h->st,
                      h->map, h->geo, h->sc, h->n, h->env_base, (const float2*)actions, reward, reward_mod,
-                     done, (float2*)obs, lanepos, tile, list_count);
+                     done, (float2*)obs, lanepos, tile, list_count, mask);
   HIP_OR_FAIL(h, hipGetLastError());
   if (h->sc.auto_reset) {
-    // a fixed grid over the compacted done list (a few hundred of 4096 envs
-    // finish per decision): no launch of thousands of idle workgroups
+    // a fixed grid over the finished envs (a few hundred of 4096 per
+    // decision): no launch of thousands of idle workgroups
     const int grid = h->n < kSpawnGrid ? h->n : kSpawnGrid;
     hipLaunchKernelGGL(spawn_kernel, dim3(grid), dim3(kSpawnThreads), h->lds_bytes, s, h->st,
                        h->map, h->geo, h->sc.max_spawn_attempts, h->env_base, (const uint8_t*)nullptr,
@@ -511,6 +523,11 @@ int dt_step(dt_handle* h, const float* actions, double* reward, double* reward_m
     HIP_OR_FAIL(h, hipGetLastError());
   }
   return DT_OK;
+}
+
+int dt_step(dt_handle* h, const float* actions, double* reward, double* reward_mod,
+            uint8_t* done, float* obs, double* lanepos, int32_t* tile, void* stream) {
+  return dt_step_masked(h, nullptr, actions, reward, reward_mod, done, obs, lanepos, tile, stream);
 }
 
 int dt_lane_pos(dt_handle* h, double* lanepos, int32_t* tile, void* stream) {

@@ -117,6 +117,11 @@ class VecEnv:
         self._check(rc, 'dt_seed')
 
     # ---- hot path ----------------------------------------------------------------------
+    def seed_env(self, env, seed):
+        """Re-seed one env (its episode counter restarts); the others are untouched."""
+        self._check(self._L.dt_seed_env(self._h, int(env), int(seed) & 0xFFFFFFFFFFFFFFFF),
+                    'dt_seed_env')
+
     def reset(self, mask=None):
         """Simulator.reset for every env (or the envs where mask != 0); returns the
         (dist, angle_rad) lane observation [n,2] f32."""
@@ -127,16 +132,27 @@ class VecEnv:
         self._reset_obs.copy_(torch.stack([lp[:, 0], lp[:, 3]], 1).nan_to_num(0.0).float())
         return self._reset_obs
 
-    def step_into(self, actions, out=None):
-        """Launch one EnvironmentWrapper.step for all envs into `out` (no sync)."""
+    def step_into(self, actions, out=None, mask=None):
+        """Launch one EnvironmentWrapper.step for all envs into `out` (no sync);
+        with `mask` (device [n] u8), only the envs where it is nonzero step — the
+        others keep their state and their entries of `out`."""
         out = out or self.out
         if actions.dtype != torch.float32 or not actions.is_contiguous() or \
                 actions.device != self.device or tuple(actions.shape) != (self.n, 2):
             raise ValueError('actions must be a contiguous float32 [%d,2] tensor on %s'
                              % (self.n, self.device))
-        rc = self._L.dt_step(self._h, _ptr(actions), _ptr(out.reward), _ptr(out.reward_mod),
-                             _ptr(out.done), _ptr(out.obs), _ptr(out.lanepos), _ptr(out.tile),
-                             self._stream())
+        if mask is None:
+            rc = self._L.dt_step(self._h, _ptr(actions), _ptr(out.reward), _ptr(out.reward_mod),
+                                 _ptr(out.done), _ptr(out.obs), _ptr(out.lanepos),
+                                 _ptr(out.tile), self._stream())
+        else:
+            if mask.dtype != torch.uint8 or mask.device != self.device or \
+                    tuple(mask.shape) != (self.n,) or not mask.is_contiguous():
+                raise ValueError('mask must be a contiguous uint8 [%d] tensor on %s'
+                                 % (self.n, self.device))
+            rc = self._L.dt_step_masked(self._h, _ptr(mask), _ptr(actions), _ptr(out.reward),
+                                        _ptr(out.reward_mod), _ptr(out.done), _ptr(out.obs),
+                                        _ptr(out.lanepos), _ptr(out.tile), self._stream())
         self._check(rc, 'dt_step')
         return out
 

@@ -119,6 +119,12 @@ int32_t dt_abi_version(void);
  * Also zeroes every env's episode counter.  Synchronous. */
 int dt_seed(dt_handle* h, const uint64_t* seeds, uint64_t base, uint32_t env_id_base);
 
+/* Replaces: DuckietownEnvironmentWrapper.change_model(seed) for ONE env of the
+ * batch (utils/env_wrappers.py:126-130, one env per pyramid_worker.py port):
+ * env's seed = seed, its episode counter = 0; the others are untouched.
+ * Synchronous. */
+int dt_seed_env(dt_handle* h, int32_t env, uint64_t seed);
+
 /* ---- hot path -------------------------------------------------------- */
 
 /* Replaces: Simulator.reset() (spawn by rejection sampling, MAX_SPAWN_ATTEMPTS,
@@ -143,6 +149,13 @@ int dt_reset(dt_handle* h, const uint8_t* mask, void* stream);
  */
 int dt_step(dt_handle* h, const float* actions, double* reward, double* reward_mod,
             uint8_t* done, float* obs, double* lanepos, int32_t* tile, void* stream);
+
+/* dt_step for the envs where mask (device [n] u8) is nonzero; the others keep
+ * their state and their output entries (the env server batches whichever
+ * per-env step requests are pending: pyramid_worker.py:25-32). */
+int dt_step_masked(dt_handle* h, const uint8_t* mask, const float* actions, double* reward,
+                   double* reward_mod, uint8_t* done, float* obs, double* lanepos, int32_t* tile,
+                   void* stream);
 
 /* Replaces: Simulator.get_lane_pos2(cur_pos, cur_angle) for every env (no step).
  * lanepos device [n,4] f64 (NaN if NotInLane); tile device [n] i32 (nullable). */
