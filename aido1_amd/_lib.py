@@ -21,7 +21,7 @@ SOURCES = ['dtsim.hip', 'dtrender.hip', 'dtreplay.hip', 'dtactor.hip']
 HEADERS = ['dtsim_common.h', 'dtrender.h']
 PUBLIC_HEADERS = ['dtsim.h', 'dtreplay.h', 'dtactor.h']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 HIP_FLAGS = ['--offload-arch=gfx950', '-O3', '-fPIC', '-shared', '-std=c++17',
              '-ffp-contract=off', '-munsafe-fp-atomics']
@@ -33,8 +33,8 @@ class DtError(RuntimeError):
 
 class DtMap(ctypes.Structure):
     _fields_ = [('width', ctypes.c_int32), ('height', ctypes.c_int32),
-                ('kind', ctypes.c_void_p), ('curves', ctypes.c_void_p),
-                ('headings', ctypes.c_void_p)]
+                ('kind', ctypes.c_void_p), ('curve_start', ctypes.c_void_p),
+                ('curves', ctypes.c_void_p), ('headings', ctypes.c_void_p)]
 
 
 def _sources():

@@ -29,7 +29,8 @@ __constant__ HsvTables c_hsv = make_hsv_tables();
 // and, for curve 0 only, a dashed yellow centre line (0.20 tile to its left,
 // every other of the 8 segments).  A line of width w is kW parallel polylines
 // 0.7 px apart (closer than 1 px so curved thick lines have no holes): white 7
-// (4.2 cm), yellow 4 (2.1 cm).  oracle/render_oracle.c restates this.
+// (4.2 cm), yellow 4 (2.1 cm).  Intersection tiles get none.
+// oracle/render_oracle.c restates this.
 constexpr int kSegs = 8, kWhiteW = 7, kYellowW = 4;
 constexpr double kWhiteOff = 0.26, kYellowOff = -0.20, kHalfStep = 0.0035;
 
@@ -57,9 +58,11 @@ void build_marks(const dt_map* m, double ts, std::vector<float4>& yellow,
                  std::vector<float4>& white) {
   const int T = m->width * m->height;
   for (int t = 0; t < T; ++t) {
-    if (m->kind[t] <= 0) continue;
+    // lane markings on straight and curve tiles; intersections are plain road
+    // (build-defined: their painted stop lines are not part of this raster)
+    if (m->kind[t] <= 0 || m->kind[t] > DT_TILE_CURVE_RIGHT) continue;
     for (int c = 0; c < 2; ++c) {
-      const double* cp = m->curves + (size_t)t * 24 + c * 12;
+      const double* cp = m->curves + (size_t)(m->curve_start[t] + c) * 12;
       double px[kSegs + 1], pz[kSegs + 1], rx[kSegs + 1], rz[kSegs + 1];
       for (int k = 0; k <= kSegs; ++k) {
         double dx, dz;

@@ -335,12 +335,12 @@ int dt_create(const dt_config* cfg, const dt_map* map, uint64_t seed, int32_t n_
               int32_t device, dt_handle** out) {
   g_create_err.clear();
   if (!cfg || !map || !out || n_envs <= 0 || !map->kind || !map->curves || !map->headings ||
-      map->width <= 0 || map->height <= 0) {
+      !map->curve_start || map->width <= 0 || map->height <= 0) {
     g_create_err = "dt_create: bad argument";
     return DT_E_ARG;
   }
   const int T = map->width * map->height;
-  if (T > dt::kMaxLdsTiles) {
+  if (T > dt::kMaxLdsTiles) {  // (also the render's LDS kind table)
     g_create_err = "dt_create: map larger than the LDS staging limit (256 tiles)";
     return DT_E_ARG;
   }
@@ -348,6 +348,20 @@ int dt_create(const dt_config* cfg, const dt_map* map, uint64_t seed, int32_t n_
     g_create_err = "dt_create: bad config";
     return DT_E_ARG;
   }
+  // curve table: monotone, a drivable tile has curves, an off-road tile none
+  if (map->curve_start[0] != 0) {
+    g_create_err = "dt_create: curve_start[0] must be 0";
+    return DT_E_ARG;
+  }
+  for (int t = 0; t < T; ++t) {
+    const int32_t k = map->curve_start[t + 1] - map->curve_start[t];
+    if (k < 0 || k > 12 || (map->kind[t] > 0) != (k > 0)) {
+      g_create_err = "dt_create: tile " + std::to_string(t) + " has " + std::to_string(k) +
+                     " curves for kind " + std::to_string(map->kind[t]);
+      return DT_E_ARG;
+    }
+  }
+  const int C = map->curve_start[T];
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) {
     g_create_err = "dt_create: no HIP device " + std::to_string(device);
@@ -408,26 +422,40 @@ int dt_create(const dt_config* cfg, const dt_map* map, uint64_t seed, int32_t n_
     return DT_E_HIP;
   };
   if (hipSetDevice(device) != hipSuccess) return fail("hipSetDevice failed");
-  // map image: curves | headings | kind | drivable
-  const size_t cb = (size_t)T * 24 * 8, hb = (size_t)T * 6 * 8, kb = ((size_t)T + 15) & ~15ul,
+  // map image: curves | headings | curve_start (u16) | kind | drivable
+  if (dt::map_lds_bytes(T, (int)drv.size(), C) > dt::kMaxMapLdsBytes) {
+    g_create_err = "dt_create: map image over the LDS budget (" +
+                   std::to_string(dt::map_lds_bytes(T, (int)drv.size(), C)) + " B)";
+    delete h;
+    return DT_E_ARG;
+  }
+  std::vector<uint16_t> cs(T + 1);
+  for (int t = 0; t <= T; ++t) cs[t] = (uint16_t)map->curve_start[t];
+  const size_t cb = (size_t)C * 12 * 8, hb = (size_t)C * 3 * 8,
+               sb16 = ((size_t)(T + 1) * 2 + 15) & ~15ul, kb = ((size_t)T + 15) & ~15ul,
                db = (drv.size() * 2 + 15) & ~15ul;
-  if (hipMalloc(&h->map_buf, cb + hb + kb + db) != hipSuccess) return fail("hipMalloc(map)");
+  if (hipMalloc(&h->map_buf, cb + hb + sb16 + kb + db) != hipSuccess)
+    return fail("hipMalloc(map)");
   char* mb = (char*)h->map_buf;
-  if (hipMemcpy(mb, map->curves, cb, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(mb + cb, map->headings, hb, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(mb + cb + hb, map->kind, (size_t)T, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(mb + cb + hb + kb, drv.data(), drv.size() * 2, hipMemcpyHostToDevice) !=
+  if ((cb && hipMemcpy(mb, map->curves, cb, hipMemcpyHostToDevice) != hipSuccess) ||
+      (hb && hipMemcpy(mb + cb, map->headings, hb, hipMemcpyHostToDevice) != hipSuccess) ||
+      hipMemcpy(mb + cb + hb, cs.data(), (size_t)(T + 1) * 2, hipMemcpyHostToDevice) !=
+          hipSuccess ||
+      hipMemcpy(mb + cb + hb + sb16, map->kind, (size_t)T, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(mb + cb + hb + sb16 + kb, drv.data(), drv.size() * 2, hipMemcpyHostToDevice) !=
           hipSuccess)
     return fail("hipMemcpy(map)");
   h->map.width = map->width;
   h->map.height = map->height;
   h->map.n_tiles = T;
   h->map.n_drivable = (int)drv.size();
+  h->map.n_curves = C;
   h->map.curves = (const double*)mb;
   h->map.headings = (const double*)(mb + cb);
-  h->map.kind = (const int8_t*)(mb + cb + hb);
-  h->map.drivable = (const int16_t*)(mb + cb + hb + kb);
-  h->lds_bytes = dt::map_lds_bytes(T, (int)drv.size());
+  h->map.curve_start = (const uint16_t*)(mb + cb + hb);
+  h->map.kind = (const int8_t*)(mb + cb + hb + sb16);
+  h->map.drivable = (const int16_t*)(mb + cb + hb + sb16 + kb);
+  h->lds_bytes = dt::map_lds_bytes(T, (int)drv.size(), C);
 
   // state: x z angle seed (8 B) | step_count env_step episode (4 B) | err
   const size_t N = (size_t)n_envs, N8 = N * 8, N4 = (N * 4 + 255) & ~255ul;

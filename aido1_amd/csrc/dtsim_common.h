@@ -18,9 +18,8 @@
 namespace dt {
 
 constexpr int kWave = 64;
-constexpr int kMaxTiles = 1024;  // LDS staging: 24+6 doubles + 1 kind byte per tile (<= 246 KB
-                                 // worst case is over budget; dt_create enforces kMaxLdsTiles)
-constexpr int kMaxLdsTiles = 256;
+constexpr int kMaxLdsTiles = 256;             // tiles staged in LDS (kinds: render too)
+constexpr size_t kMaxMapLdsBytes = 48 * 1024;  // map image in LDS (dt_create enforces)
 
 constexpr uint32_t kTagTile = 0x54494C45u;    // 'TILE'
 constexpr uint32_t kTagSpawnA = 0x53504E41u;  // 'SPNA'
@@ -54,9 +53,10 @@ __device__ inline void wave_add(unsigned long long* p, unsigned v) {
 
 // Map image in device memory; staged into LDS by each block.
 struct MapDev {
-  int32_t width, height, n_tiles, n_drivable;
-  const double* curves;     // [T,2,4,3]
-  const double* headings;   // [T,2,3]
+  int32_t width, height, n_tiles, n_drivable, n_curves;
+  const double* curves;     // [C,4,3]
+  const double* headings;   // [C,3]
+  const uint16_t* curve_start;  // [T+1]
   const int8_t* kind;       // [T]
   const int16_t* drivable;  // [n_drivable] tile index of the k-th drivable tile (load order)
 };
@@ -65,13 +65,15 @@ struct MapDev {
 struct MapLds {
   const double* curves;
   const double* headings;
+  const uint16_t* curve_start;
   const int8_t* kind;
   const int16_t* drivable;
   int32_t width, height, n_drivable;
 };
 
-__host__ __device__ inline size_t map_lds_bytes(int n_tiles, int n_drivable) {
-  size_t b = (size_t)n_tiles * (24 + 6) * sizeof(double);
+__host__ __device__ inline size_t map_lds_bytes(int n_tiles, int n_drivable, int n_curves) {
+  size_t b = (size_t)n_curves * (12 + 3) * sizeof(double);
+  b += ((size_t)(n_tiles + 1) * 2 + 15) & ~(size_t)15;
   b += ((size_t)n_tiles + 15) & ~(size_t)15;
   b += ((size_t)n_drivable * 2 + 15) & ~(size_t)15;
   return b;
@@ -80,18 +82,21 @@ __host__ __device__ inline size_t map_lds_bytes(int n_tiles, int n_drivable) {
 // Cooperative copy of the map into LDS; every thread of the block calls it.
 __device__ inline MapLds stage_map(const MapDev& m, unsigned char* lds) {
   double* cv = reinterpret_cast<double*>(lds);
-  double* hd = cv + (size_t)m.n_tiles * 24;
-  int8_t* kd = reinterpret_cast<int8_t*>(hd + (size_t)m.n_tiles * 6);
+  double* hd = cv + (size_t)m.n_curves * 12;
+  uint16_t* cs = reinterpret_cast<uint16_t*>(hd + (size_t)m.n_curves * 3);
+  int8_t* kd = reinterpret_cast<int8_t*>(cs) + (((size_t)(m.n_tiles + 1) * 2 + 15) & ~(size_t)15);
   int16_t* dv = reinterpret_cast<int16_t*>(kd + (((size_t)m.n_tiles + 15) & ~(size_t)15));
   const int tid = threadIdx.x, nt = blockDim.x;
-  for (int i = tid; i < m.n_tiles * 24; i += nt) cv[i] = m.curves[i];
-  for (int i = tid; i < m.n_tiles * 6; i += nt) hd[i] = m.headings[i];
+  for (int i = tid; i < m.n_curves * 12; i += nt) cv[i] = m.curves[i];
+  for (int i = tid; i < m.n_curves * 3; i += nt) hd[i] = m.headings[i];
+  for (int i = tid; i <= m.n_tiles; i += nt) cs[i] = m.curve_start[i];
   for (int i = tid; i < m.n_tiles; i += nt) kd[i] = m.kind[i];
   for (int i = tid; i < m.n_drivable; i += nt) dv[i] = m.drivable[i];
   __syncthreads();
   MapLds r;
   r.curves = cv;
   r.headings = hd;
+  r.curve_start = cs;
   r.kind = kd;
   r.drivable = dv;
   r.width = m.width;
@@ -242,10 +247,19 @@ __device__ inline bool lane_pos(const MapLds& M, const Geo& g, double x, double 
   const int t = tile_of(M, g, x, z);
   if (t < 0 || M.kind[t] <= 0) return false;
   const double dx = c, dz = -s;
-  const double* hd = M.headings + t * 6;
-  const double d0 = (hd[0] * dx + hd[1] * 0.0) + hd[2] * dz;
-  const double d1 = (hd[3] * dx + hd[4] * 0.0) + hd[5] * dz;
-  const double* cp = M.curves + t * 24 + ((d1 > d0) ? 12 : 0);
+  // closest curve = np.argmax(curve_headings @ dir): the first of the largest
+  const int k0 = M.curve_start[t], k1 = M.curve_start[t + 1];
+  int best = k0;
+  double bd = 0.0;
+  for (int k = k0; k < k1; ++k) {
+    const double* hd = M.headings + 3 * k;
+    const double d = (hd[0] * dx + hd[1] * 0.0) + hd[2] * dz;
+    if (k == k0 || d > bd) {
+      bd = d;
+      best = k;
+    }
+  }
+  const double* cp = M.curves + 12 * best;
   // bezier_closest, 8 levels.  One endpoint distance is carried between levels:
   // the kept half's end was evaluated at the same t one level earlier, and the
   // function is deterministic, so the result is bit-identical to re-evaluating.

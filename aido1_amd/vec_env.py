@@ -71,8 +71,10 @@ class VecEnv:
         self._kind = np.ascontiguousarray(self.map.kind, np.int8)
         self._curves = np.ascontiguousarray(self.map.curves, np.float64)
         self._headings = np.ascontiguousarray(self.map.headings, np.float64)
+        self._curve_start = np.ascontiguousarray(self.map.curve_start, np.int32)
         m = _lib.DtMap(self.map.width, self.map.height,
                        self._kind.ctypes.data_as(ctypes.c_void_p),
+                       self._curve_start.ctypes.data_as(ctypes.c_void_p),
                        self._curves.ctypes.data_as(ctypes.c_void_p),
                        self._headings.ctypes.data_as(ctypes.c_void_p))
         h = ctypes.c_void_p()

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DT_ABI_VERSION 1
+#define DT_ABI_VERSION 2  /* 2: dt_map curves per tile vary (curve_start), intersections */
 
 /* error codes */
 #define DT_OK 0
@@ -52,6 +52,9 @@ extern "C" {
 #define DT_TILE_STRAIGHT 1
 #define DT_TILE_CURVE_LEFT 2
 #define DT_TILE_CURVE_RIGHT 3
+#define DT_TILE_3WAY_LEFT 4      /* upstream kind.startswith('3way'): 6 lane curves */
+#define DT_TILE_3WAY_RIGHT 5
+#define DT_TILE_4WAY 6           /* a tile name containing '4' (angle 2): 12 lane curves */
 
 /* Simulator + EnvironmentWrapper constants.  Every value mirrors an upstream
  * gym-duckietown constant or a reference config key; the host fills them from
@@ -87,13 +90,16 @@ typedef struct dt_config {
 typedef struct dt_map {
   int32_t width;
   int32_t height;
-  const int8_t* kind;      /* host [height*width] DT_TILE_* */
-  const double* curves;    /* host [height*width, 2, 4, 3] world-frame Bezier control points
-                              (upstream _get_curve: template * tile_size @ R_y + centre);
-                              ignored for non-drivable tiles */
-  const double* headings;  /* host [height*width, 2, 3] curve headings (P3 - P0) divided by the
-                              Frobenius norm of the tile's heading matrix (the
-                              closest_curve_point np.linalg.norm quirk) */
+  const int8_t* kind;           /* host [height*width] DT_TILE_* */
+  const int32_t* curve_start;   /* host [height*width + 1]: tile t owns curves
+                                   curve_start[t] .. curve_start[t+1]-1 (2 for straight /
+                                   curve tiles, 6 for 3-way, 12 for 4-way, 0 off-road) */
+  const double* curves;         /* host [C, 4, 3] world-frame Bezier control points, C =
+                                   curve_start[height*width] (upstream _get_curve: template
+                                   * tile_size @ R_y + centre) */
+  const double* headings;       /* host [C, 3] curve headings (P3 - P0) divided by the
+                                   Frobenius norm of the tile's heading matrix (the
+                                   closest_curve_point np.linalg.norm quirk) */
 } dt_map;
 
 typedef struct dt_handle dt_handle;

@@ -103,11 +103,15 @@ static int lane_pos(const ctx_t* C, double x, double z, double angle, double lp[
   if (t < 0 || C->map->kind[t] <= 0) return 0;
   double c = cos(angle), s = sin(angle);
   double dx = c, dz = -s;
-  const double* hd = C->map->headings + (size_t)t * 6;
-  double d0 = (hd[0] * dx + hd[1] * 0.0) + hd[2] * dz;
-  double d1 = (hd[3] * dx + hd[4] * 0.0) + hd[5] * dz;
-  int ci = (d1 > d0) ? 1 : 0; /* np.argmax: first max wins */
-  const double* cps = C->map->curves + (size_t)t * 24 + ci * 12;
+  /* np.argmax(curve_headings @ dir): the first of the largest */
+  int k0 = C->map->curve_start[t], k1 = C->map->curve_start[t + 1], ci = k0;
+  double best = 0.0;
+  for (int k = k0; k < k1; ++k) {
+    const double* hd = C->map->headings + (size_t)k * 3;
+    double d = (hd[0] * dx + hd[1] * 0.0) + hd[2] * dz;
+    if (k == k0 || d > best) { best = d; ci = k; }
+  }
+  const double* cps = C->map->curves + (size_t)ci * 12;
   double tb = 0.0, tt = 1.0;
   for (int n = 8; n > 0; --n) {
     double mid = (tb + tt) * 0.5;

@@ -46,12 +46,13 @@ class _LineParams(ctypes.Structure):
 
 class _Map(ctypes.Structure):
     _fields_ = [('width', ctypes.c_int32), ('height', ctypes.c_int32),
-                ('kind', ctypes.c_void_p), ('curves', ctypes.c_void_p),
-                ('headings', ctypes.c_void_p)]
+                ('kind', ctypes.c_void_p), ('curve_start', ctypes.c_void_p),
+                ('curves', ctypes.c_void_p), ('headings', ctypes.c_void_p)]
 
 
 _MODES = {'wheels': 0, 'tanh': 1, 'steering': 2}
-_KINDS = {'straight': 1, 'curve_left': 2, 'curve_right': 3}
+_KINDS = {'straight': 1, 'curve_left': 2, 'curve_right': 3, '3way_left': 4, '3way_right': 5,
+          '4way': 6}
 
 
 def make_cfg(sc: 'R.SimConfig', auto_reset=True):
@@ -89,19 +90,27 @@ class OracleMap:
         T = m.grid_width * m.grid_height
         self.width, self.height = m.grid_width, m.grid_height
         self.kind = np.full(T, -1, np.int8)
-        self.curves = np.zeros((T, 2, 4, 3))
-        self.headings = np.zeros((T, 2, 3))
+        per_tile = [None] * T
         for t, tile in enumerate(m.grid):
             if tile is None:
                 continue
             if tile['drivable']:
                 self.kind[t] = _KINDS[tile['kind']]
-                self.curves[t] = tile['curves']
-                self.headings[t] = R.tile_headings(tile['curves'])
+                per_tile[t] = tile['curves']
             else:
                 self.kind[t] = 0
-        self.c = _Map(self.width, self.height, self.kind.ctypes.data, self.curves.ctypes.data,
-                      self.headings.ctypes.data)
+        self.curve_start = np.zeros(T + 1, np.int32)
+        self.curve_start[1:] = np.cumsum([0 if c is None else len(c) for c in per_tile])
+        C = int(self.curve_start[-1])
+        self.curves = np.zeros((C, 4, 3))
+        self.headings = np.zeros((C, 3))
+        for t, cv in enumerate(per_tile):
+            if cv is not None:
+                a, b = self.curve_start[t], self.curve_start[t + 1]
+                self.curves[a:b] = cv
+                self.headings[a:b] = R.tile_headings(cv)
+        self.c = _Map(self.width, self.height, self.kind.ctypes.data, self.curve_start.ctypes.data,
+                      self.curves.ctypes.data, self.headings.ctypes.data)
 
 
 def _p(a):

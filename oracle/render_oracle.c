@@ -58,10 +58,10 @@ static int build_marks(const dt_map* m, double ts, seg_t* out, int cap, int* ny)
   /* pass 0: yellow, pass 1: white (same tile order) */
   for (int pass = 0; pass < 2; ++pass) {
     for (int t = 0; t < m->width * m->height; ++t) {
-      if (m->kind[t] <= 0) continue;
+      if (m->kind[t] <= 0 || m->kind[t] > DT_TILE_CURVE_RIGHT) continue;  /* no marks on intersections */
       for (int c = 0; c < 2; ++c) {
         if (pass == 0 && c != 0) continue;
-        const double* cp = m->curves + (size_t)t * 24 + c * 12;
+        const double* cp = m->curves + (size_t)(m->curve_start[t] + c) * 12;
         double X[9], Z[9], RX[9], RZ[9];
         for (int k = 0; k <= 8; ++k) curve_sample(cp, (double)k / 8, &X[k], &Z[k], &RX[k], &RZ[k]);
         int wdt = pass == 0 ? 4 : 7;  /* parallel polylines 0.7 px apart */

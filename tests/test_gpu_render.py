@@ -25,7 +25,7 @@ def poses(n, rng, env=None):
     return x, z, a
 
 
-@pytest.mark.parametrize('map_name', ['loop_empty', 'zigzag'])
+@pytest.mark.parametrize('map_name', ['loop_empty', 'zigzag', 'intersections'])
 def test_render_parity(gpu, map_name):
     from aido1_amd.config import EnvConfig
     from aido1_amd.render import RenderOutput

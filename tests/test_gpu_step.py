@@ -88,6 +88,7 @@ def test_reset_properties_full_size(gpu):
     ('loop_empty', 'tanh', 1000, 40),
     ('zigzag', 'steering', 4096, 40),
     ('small_loop', 'wheels', 65, 100),
+    ('intersections', 'wheels', 4096, 60),   # 3-way / 4-way tiles
 ])
 def test_step_parity(gpu, map_name, mode, n, steps):
     env, ob = make_pair(n, map_name=map_name, action_mode=mode)

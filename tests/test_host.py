@@ -65,6 +65,7 @@ def test_maps_parse_errors():
     with pytest.raises(ValueError):
         parse_rows([['straight/S', 'grass'], ['grass']])
     with pytest.raises(NotImplementedError):
-        parse_rows([['4way']])
+        parse_rows([['roundabout/N']])
+    assert parse_rows([['4way']]).kind.tolist() == [6]
     m = parse_rows([['empty', 'grass', 'straight/E']])
     assert m.kind.tolist() == [-1, 0, 1]

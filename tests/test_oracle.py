@@ -201,7 +201,8 @@ def test_golden_env_wrapper_on_c_oracle():
 
 # ---- C restatement == numpy restatement ---------------------------------------
 @pytest.mark.parametrize('map_name,mode', [('loop_empty', 'wheels'), ('zigzag', 'tanh'),
-                                           ('small_loop', 'steering')])
+                                           ('small_loop', 'steering'),
+                                           ('intersections', 'wheels')])
 def test_c_oracle_matches_numpy(map_name, mode):
     rows = map_rows(map_name)
     n = 12
