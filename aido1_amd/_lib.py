@@ -17,7 +17,7 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_PATH = os.path.join(PKG_DIR, 'libdtsim.so')
 CSRC = os.path.join(PKG_DIR, 'csrc')
-SOURCES = ['dtsim.hip', 'dtrender.hip', 'dtreplay.hip', 'dtactor.hip']
+SOURCES = ['dtsim.hip', 'dtrender.hip', 'dtreplay.hip', 'dtactor.hip', 'dtconv1.hip']
 HEADERS = ['dtsim_common.h', 'dtrender.h']
 PUBLIC_HEADERS = ['dtsim.h', 'dtreplay.h', 'dtactor.h']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
@@ -125,6 +125,10 @@ def lib():
             # dtactor.h
             'dt_sample_norm': (ctypes.c_int, [vp, vp, i32, i32, i32, vp, vp, ctypes.c_float,
                                               ctypes.c_float, i32, vp]),
+            'dt_conv1': (ctypes.c_int, [vp, i32, i32, ctypes.POINTER(i32), vp, vp, vp, vp,
+                                        ctypes.c_float, vp]),
+            'dt_conv1_norm': (ctypes.c_int, [vp, i32, vp, vp, vp, ctypes.c_float, vp]),
+            'dt_conv1_bands': (i32, []),
         }
         for name, (res, args) in sig.items():
             if not hasattr(L, name):

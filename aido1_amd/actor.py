@@ -270,6 +270,9 @@ class FusedActor(nn.Module):
         self.b1 = nn.Parameter(torch.empty_like(lin1.bias, dtype=dtype), requires_grad=False)
         self.w2 = nn.Parameter(torch.empty_like(lin2.weight, dtype=dtype), requires_grad=False)
         self.b2 = nn.Parameter(torch.empty_like(lin2.bias, dtype=dtype), requires_grad=False)
+        # conv1 as dt_conv1's MFMA A fragments (fp16 path; see include/dtactor.h)
+        self.register_buffer('w0frag', torch.zeros(16, 64, 8, dtype=torch.float16, device=dev))
+        self.register_buffer('b0f', torch.zeros(convs[0].out_channels, device=dev))
         self.refresh(actor)
 
     @torch.no_grad()
@@ -304,6 +307,8 @@ class FusedActor(nn.Module):
             self.b1.copy_(b1 + w1 @ t_flat)
         self.w2.copy_(lin2.weight)
         self.b2.copy_(lin2.bias)
+        self.w0frag.copy_(conv1_fragments(convs[0].weight.detach()))
+        self.b0f.copy_(convs[0].bias.detach())
 
     def _lrelu_sample_norm(self, x, i):
         """LeakyReLU then BatchNorm2d in train mode on a batch of one, for every
@@ -329,17 +334,48 @@ class FusedActor(nn.Module):
         b = self.beta[i].view(1, -1, 1, 1)
         return ((x - mean) / torch.sqrt(var + self.eps[i]) * g + b).to(self.dtype)
 
+    def _conv1_hip(self, ring, order):
+        """Layer 1 by dt_conv1 straight from the f32 ring (+ the reference-mode
+        per-sample norm from its band statistics); returns the channels_last
+        [N,32,57,77] fp16 activation."""
+        from aido1_amd import _lib
+        import ctypes
+        L = _lib.lib()
+        n, slots = ring.shape[0], ring.shape[1]
+        y = torch.empty(n, 57, 77, 32, dtype=torch.float16, device=ring.device)
+        ref = self.mode == 'reference'
+        part = torch.empty(n, L.dt_conv1_bands(), 32, 2, device=ring.device) if ref else None
+        o = (ctypes.c_int32 * 3)(*[int(v) for v in order])
+        stream = torch.cuda.current_stream(ring.device).cuda_stream
+        rc = L.dt_conv1(ring.data_ptr(), n, slots, o, self.w0frag.data_ptr(),
+                        self.b0f.data_ptr(), y.data_ptr(),
+                        part.data_ptr() if ref else None, 0.01, stream)
+        if rc == 0 and ref:
+            rc = L.dt_conv1_norm(y.data_ptr(), n, part.data_ptr(), self.gamma[0].data_ptr(),
+                                 self.beta[0].data_ptr(), self.eps[0], stream)
+        if rc != 0:
+            raise _lib.DtError('dt_conv1 failed (%d)' % rc)
+        return y.permute(0, 3, 1, 2)
+
     @torch.no_grad()
     def forward(self, x, order=None):
         """x: [N,3,120,160] stack (oldest first), or the frame ring with
         `order` = ring slots oldest->newest (RenderOutput.order())."""
-        w0 = self.w[0]
-        if order is not None:
-            inv = sorted(range(len(order)), key=lambda c: order[c])
-            w0 = w0[:, inv].contiguous(memory_format=torch.channels_last)
-        x = x.to(self.dtype, memory_format=torch.channels_last)
         ref = self.mode == 'reference'
-        for i in range(4):
+        first = 0
+        if (x.is_cuda and self.dtype == torch.float16 and x.dtype == torch.float32 and
+                x.is_contiguous() and tuple(x.shape[2:]) == (120, 160) and x.shape[1] >= 3 and
+                self.w[0].shape == (32, 3, 8, 8)):
+            # the fp16 product path: conv1 is the hand-written MFMA kernel
+            x = self._conv1_hip(x, order if order is not None else [0, 1, 2])
+            first = 1
+        else:
+            w0 = self.w[0]
+            if order is not None:
+                inv = sorted(range(len(order)), key=lambda c: order[c])
+                w0 = w0[:, inv].contiguous(memory_format=torch.channels_last)
+            x = x.to(self.dtype, memory_format=torch.channels_last)
+        for i in range(first, 4):
             x = F.conv2d(x, w0 if i == 0 else self.w[i], self.b[i], stride=self.strides[i])
             x = self._lrelu_sample_norm(x, i) if ref else F.leaky_relu(x)
         # flatten in NCHW order, as the reference's view(x.size(0), -1)
@@ -349,6 +385,18 @@ class FusedActor(nn.Module):
         x = F.leaky_relu(F.linear(x, self.w1, self.b1))
         x = F.linear(x, self.w2, self.b2).float()
         return apply_head(x, self.head, self.max_action)
+
+
+def conv1_fragments(w):
+    """conv1 weights [32, 3, 8, 8] -> dt_conv1's MFMA A fragments [16, 64, 8]
+    fp16: element [s][l][j] = w[l % 32][j % 4][s // 2][4 (s % 2) + 2 (l // 32)
+    + j // 4], zero for the padding channel j % 4 == 3."""
+    dev = w.device
+    s = torch.arange(16, device=dev).view(16, 1, 1)
+    ln = torch.arange(64, device=dev).view(1, 64, 1)
+    j = torch.arange(8, device=dev).view(1, 1, 8)
+    wp = torch.cat([w.float(), torch.zeros(w.shape[0], 1, 8, 8, device=dev)], 1)
+    return wp[ln % 32, j % 4, s // 2, 4 * (s % 2) + 2 * (ln // 32) + j // 4].to(torch.float16)
 
 
 def flops_per_sample():

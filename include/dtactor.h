@@ -28,6 +28,29 @@ extern "C" {
 int dt_sample_norm(const void* x, void* y, int32_t n, int32_t hw, int32_t c, const float* gamma,
                    const float* beta, float eps, float slope, int32_t dtype, void* stream);
 
+/* dt_conv1: the actor's first layer, conv_2d(3 -> 32, 8x8, stride 2) + bias +
+ * LeakyReLU (config.json actor; duckietown_rl/ddpg.py:36,56), read straight
+ * from the observation ring: channel c of the stack is ring slot order[c]
+ * (oldest first, the Transformer order).  An MFMA implicit GEMM in fp16 with
+ * f32 accumulation (aido1_amd/csrc/dtconv1.hip).
+ *   ring      device f32 [n, slots, 120, 160]
+ *   wfrag     device fp16 [16, 64, 8]: the weights as the MFMA A fragments,
+ *             element [s][l][j] = w[co = l%32][c = j%4][ky = s/2]
+ *             [kx = 4*(s%2) + 2*(l/32) + j/4], 0 for c = 3 (aido1_amd/actor.py)
+ *   bias      device f32 [32]
+ *   y         device fp16 [n, 57, 77, 32] (NHWC)
+ *   partials  device f32 [n, dt_conv1_bands(), 32, 2] or NULL: per band and
+ *             channel (mean, M2) of the LeakyReLU outputs, for dt_conv1_norm */
+int dt_conv1(const float* ring, int32_t n, int32_t slots, const int32_t* order, const void* wfrag,
+             const float* bias, void* y, float* partials, float slope, void* stream);
+
+/* dt_conv1_norm: the train-mode batch-of-one BatchNorm after conv1 (as
+ * dt_sample_norm) from dt_conv1's band statistics, merged with Chan's
+ * formula; y is normalised in place. */
+int dt_conv1_norm(void* y, int32_t n, const float* partials, const float* gamma,
+                  const float* beta, float eps, void* stream);
+int32_t dt_conv1_bands(void);
+
 #ifdef __cplusplus
 }
 #endif

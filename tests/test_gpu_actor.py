@@ -97,3 +97,51 @@ def test_reference_mode_matches_per_sample_train_mode(gpu):
     with torch.no_grad():
         ref = torch.cat([a_cpu(frames[i:i + 1].cpu()) for i in range(32)])
     assert torch.max(torch.abs(h(frames).cpu() - ref)) < 1.5e-2
+
+
+@pytest.mark.parametrize('slots,order', [(3, [0, 1, 2]), (4, [2, 3, 0])])
+def test_conv1_kernel_matches_conv2d(gpu, slots, order):
+    """dt_conv1 (MFMA implicit GEMM on the ring) vs conv2d + LeakyReLU in f32 on
+    the same fp16-rounded inputs and weights; band statistics and the merged
+    per-sample norm vs float64."""
+    import ctypes
+    import torch.nn.functional as F
+    from aido1_amd import _lib
+    from aido1_amd.actor import conv1_fragments
+    L = _lib.lib()
+    torch.manual_seed(1)
+    n = 37
+    ring = torch.rand(n, slots, 120, 160, device=gpu)
+    w = torch.randn(32, 3, 8, 8, device=gpu) * 0.08
+    b = torch.randn(32, device=gpu) * 0.2
+    x = ring[:, order].half().float()
+    ref = F.leaky_relu(F.conv2d(x, w.half().float(), b, stride=2))      # [n,32,57,77]
+    y = torch.empty(n, 57, 77, 32, dtype=torch.float16, device=gpu)
+    nb = L.dt_conv1_bands()
+    part = torch.empty(n, nb, 32, 2, device=gpu)
+    o = (ctypes.c_int32 * 3)(*order)
+    s = torch.cuda.current_stream().cuda_stream
+    assert L.dt_conv1(ring.data_ptr(), n, slots, o, conv1_fragments(w).data_ptr(), b.data_ptr(),
+                      y.data_ptr(), part.data_ptr(), 0.01, s) == 0
+    got = y.permute(0, 3, 1, 2).float()
+    err = (got - ref).abs().max().item()
+    assert err < 2e-3 * max(1.0, ref.abs().max().item()), err
+    # band statistics (mean, M2) of the f32 outputs
+    r64 = ref.double()
+    for band in range(nb):
+        rows = r64[:, :, 8 * band:8 * band + 8]
+        mean = rows.mean((2, 3))
+        m2 = ((rows - mean[:, :, None, None]) ** 2).sum((2, 3))
+        assert torch.allclose(part[:, band, :, 0].double(), mean, rtol=1e-3, atol=1e-3)
+        assert torch.allclose(part[:, band, :, 1].double(), m2, rtol=2e-3, atol=1e-2)
+    gamma = torch.rand(32, device=gpu) + 0.5
+    beta = torch.rand(32, device=gpu) - 0.5
+    y16 = y.permute(0, 3, 1, 2).double()          # what the norm pass normalises
+    assert L.dt_conv1_norm(y.data_ptr(), n, part.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
+                           1e-5, s) == 0
+    m = r64.mean((2, 3), keepdim=True)
+    v = ((r64 - m) ** 2).mean((2, 3), keepdim=True)
+    want = (y16 - m) / torch.sqrt(v + 1e-5) * gamma.double().view(1, -1, 1, 1) + \
+        beta.double().view(1, -1, 1, 1)
+    err = (y.permute(0, 3, 1, 2).double() - want).abs().max().item()
+    assert err < 5e-3 * max(1.0, want.abs().max().item()), err    # fp16 output rounding
