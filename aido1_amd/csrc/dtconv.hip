@@ -1,0 +1,762 @@
+// The actor's first convolution (config.json actor: conv_2d 3 -> 32, 8x8,
+// stride 2, then leaky_relu) as a gfx950 MFMA implicit GEMM that reads the
+// observation ring in place -- see include/dtactor.h (dt_conv1).
+//
+// Per workgroup: one sample x one band of kBand output rows.
+//   load   the band's 2*kBand+6 input rows from the three f32 ring slots (in
+//          the stack's oldest -> newest order), converted to fp16 as 4-channel
+//          pixels (channel 3 = 0) in LDS: a row is 160 px x 8 B
+//   mma    per wave, tiles of 32 output pixels x 32 channels with
+//          v_mfma_f32_32x32x16_f16: A = weights (row = out channel), B = the
+//          im2col column of a pixel (k = (ky, kx, c), 16 k per step = one
+//          kernel row half: 2 px x 4 ch per lane half = one 16-B LDS read);
+//          16 steps cover K = 8 x 8 x 4
+//   out    bias + LeakyReLU, fp16 NHWC (each lane: one pixel, 16 channels as
+//          four 8-B groups); with `partials`, the band's per-channel count /
+//          mean / M2 by two passes over the register-resident outputs
+//          (reference mode: the per-sample BatchNorm statistics, merged by
+//          dt_conv1_norm with Chan's formula)
+#include <hip/hip_fp16.h>
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/dtactor.h"
+
+// diagnostic builds only (tools/conv32_micro.py): bit 0 skips the prefetch
+// loads, 1 the MFMA section, 2 the output stores, 3 the statistics, 4 the ring
+// commit; the product build is 0
+#ifndef DTCONV_SKIP
+#define DTCONV_SKIP 0
+#endif
+
+namespace {
+
+constexpr int IH = 120, IW = 160, OH = 57, OW = 77, CO = 32;
+constexpr int kBand = 8;                     // output rows per workgroup
+constexpr int kBands = (OH + kBand - 1) / kBand;
+constexpr int kInRows = 2 * kBand + 6;       // input rows a band needs
+constexpr int kWaves = 4;
+constexpr int kThreads = 64 * kWaves;
+constexpr int kBandPix = kBand * OW;                 // 616
+constexpr int kTiles = (kBandPix + 31) / 32;         // 20
+constexpr int kTilesPerWave = (kTiles + kWaves - 1) / kWaves;  // 5
+
+using half8 = __attribute__((ext_vector_type(8))) _Float16;
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+using u32x4 = __attribute__((ext_vector_type(4))) uint32_t;
+
+__device__ __forceinline__ float lrelu(float v, float s) { return v > 0.0f ? v : v * s; }
+
+// Persistent kernels: two workgroups per CU (the VGPR budget of these kernels),
+// each striding over (sample, band) items with its weights held in registers.
+int persistent_grid() {
+  static int g = 0;
+  if (!g) {
+    int dev = 0, cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    g = 2 * cus;
+  }
+  return g;
+}
+
+__global__ void __launch_bounds__(kThreads, 2)   // 2 waves / SIMD: <= 256 VGPRs
+conv1_kernel(int n_items, const float* __restrict__ ring, int slots, int s0, int s1, int s2,
+             const half8* __restrict__ wfrag, const float* __restrict__ bias,
+             __half* __restrict__ y, float* __restrict__ partials, float slope) {
+  __shared__ __attribute__((aligned(16))) uint2 img[kInRows * IW];   // 4 x fp16 per pixel
+  __shared__ float red[kWaves][2][CO];
+  __shared__ float mean_s[CO];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // weights once per workgroup (persistent: the grid strides over items):
+  // this lane's A fragments of the 16 k-steps (row = out channel)
+  half8 wa[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) wa[s] = wfrag[s * 64 + lane];
+  for (int item = blockIdx.x; item < n_items; item += gridDim.x) {
+  const int n = item / kBands, band = item - n * kBands;
+  const int oy0 = band * kBand;
+  const int rows_out = (OH - oy0) < kBand ? (OH - oy0) : kBand;
+  const int band_pix = rows_out * OW;
+  __syncthreads();   // the previous item's readers of img / red are done
+
+  // ---- load: input rows 2*oy0 .. 2*oy0 + kInRows - 1, 4 px per item ----------------
+  // all of the band's loads are issued before any is converted
+  const float* base = ring + (size_t)n * slots * IH * IW;
+  const float* p0 = base + (size_t)s0 * IH * IW;
+  const float* p1 = base + (size_t)s1 * IH * IW;
+  const float* p2 = base + (size_t)s2 * IH * IW;
+  constexpr int kItems = kInRows * (IW / 4);
+  constexpr int kPer = (kItems + kThreads - 1) / kThreads;
+  float4 la[kPer], lb[kPer], lc[kPer];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int it = tid + k * kThreads;
+    const int r = it / (IW / 4), q = it - r * (IW / 4);
+    const int iy = 2 * oy0 + r;
+    la[k] = lb[k] = lc[k] = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (it < kItems && iy < IH) {
+      const size_t off = (size_t)iy * IW + 4 * q;
+      la[k] = *reinterpret_cast<const float4*>(p0 + off);
+      lb[k] = *reinterpret_cast<const float4*>(p1 + off);
+      lc[k] = *reinterpret_cast<const float4*>(p2 + off);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int it = tid + k * kThreads;
+    if (it >= kItems) continue;
+    const int r = it / (IW / 4), q = it - r * (IW / 4);
+    const float av[4] = {la[k].x, la[k].y, la[k].z, la[k].w};
+    const float bv[4] = {lb[k].x, lb[k].y, lb[k].z, lb[k].w};
+    const float cv[4] = {lc[k].x, lc[k].y, lc[k].z, lc[k].w};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const __half2 lo = __floats2half2_rn(av[i], bv[i]);
+      const __half2 hi = __floats2half2_rn(cv[i], 0.0f);
+      uint2 px;
+      px.x = *reinterpret_cast<const uint32_t*>(&lo);
+      px.y = *reinterpret_cast<const uint32_t*>(&hi);
+      img[r * IW + 4 * q + i] = px;
+    }
+  }
+  __syncthreads();
+
+  // ---- MFMA: tile t covers band pixels 32t .. 32t+31 ---------------------------------
+  const int col = lane & 31, h = lane >> 5;
+  float out[kTilesPerWave][16];
+  float bco[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) bco[r] = bias[(r & 3) + 8 * (r >> 2) + 4 * h];
+#pragma unroll
+  for (int ti = 0; ti < kTilesPerWave; ++ti) {
+    const int t = wave + kWaves * ti;
+    const int p = 32 * t + col;                       // this lane's pixel (B column)
+    const bool valid = t < kTiles && p < band_pix;
+    const int pc = valid ? p : 0;
+    const int oyl = pc / OW, ox = pc - oyl * OW;
+    const uint2* src = img + (2 * oyl) * IW + 2 * ox + 2 * h;
+    f32x16 acc = {};
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+      const int ky = s >> 1, kx0 = (s & 1) * 4;
+      const half8 bfrag = *reinterpret_cast<const half8*>(src + ky * IW + kx0);
+      acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wa[s], bfrag, acc, 0, 0, 0);
+    }
+#pragma unroll
+    for (int r = 0; r < 16; ++r) out[ti][r] = valid ? lrelu(acc[r] + bco[r], slope) : 0.0f;
+    if (valid) {   // channels (r&3) + 8*(r>>2) + 4h: four groups of 4 consecutive channels
+      __half* dst = y + (((size_t)n * OH + oy0 + oyl) * OW + ox) * CO;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const __half2 v0 = __floats2half2_rn(out[ti][4 * g + 0], out[ti][4 * g + 1]);
+        const __half2 v1 = __floats2half2_rn(out[ti][4 * g + 2], out[ti][4 * g + 3]);
+        uint2 v;
+        v.x = *reinterpret_cast<const uint32_t*>(&v0);
+        v.y = *reinterpret_cast<const uint32_t*>(&v1);
+        *reinterpret_cast<uint2*>(dst + 8 * g + 4 * h) = v;
+      }
+    }
+  }
+  if (partials) {
+  // ---- band statistics per channel: two passes over the register-resident outputs ----
+  // pass 1: sum -> band mean
+  float acc16[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    float v = 0.0f;
+#pragma unroll
+    for (int ti = 0; ti < kTilesPerWave; ++ti) v += out[ti][r];   // invalid pixels hold 0
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 32);   // over the 32 pixels
+    acc16[r] = v;
+  }
+  if (col == 0)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[wave][0][(r & 3) + 8 * (r >> 2) + 4 * h] = acc16[r];
+  __syncthreads();
+  if (tid < CO) {
+    float s = 0.0f;
+    for (int w = 0; w < kWaves; ++w) s += red[w][0][tid];
+    mean_s[tid] = s / (float)band_pix;
+  }
+  __syncthreads();
+  // pass 2: M2 about the band mean
+#pragma unroll
+  for (int r = 0; r < 16; ++r) {
+    const float mu = mean_s[(r & 3) + 8 * (r >> 2) + 4 * h];
+    float v = 0.0f;
+#pragma unroll
+    for (int ti = 0; ti < kTilesPerWave; ++ti) {
+      const int t = wave + kWaves * ti;
+      const bool valid = t < kTiles && 32 * t + col < band_pix;
+      const float d = out[ti][r] - mu;
+      v += valid ? d * d : 0.0f;
+    }
+#pragma unroll
+    for (int o = 16; o > 0; o >>= 1) v += __shfl_xor(v, o, 32);
+    acc16[r] = v;
+  }
+  if (col == 0)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[wave][1][(r & 3) + 8 * (r >> 2) + 4 * h] = acc16[r];
+  __syncthreads();
+  if (tid < CO) {
+    float m2 = 0.0f;
+    for (int w = 0; w < kWaves; ++w) m2 += red[w][1][tid];
+    float* pp = partials + (((size_t)n * kBands + band) * CO + tid) * 2;
+    pp[0] = mean_s[tid];
+    pp[1] = m2;
+  }
+  }  // partials
+  }  // item
+}
+
+// Reference mode: merge the bands' (mean, M2) per sample and channel (Chan et
+// al.), then y = (y - mean) / sqrt(var + eps) * gamma + beta in place (biased
+// variance: BatchNorm2d's train-mode normalisation of a batch of one).
+__global__ void __launch_bounds__(256)
+conv1_norm_kernel(__half* __restrict__ y, const float* __restrict__ partials,
+                  const float* __restrict__ gamma, const float* __restrict__ beta, float eps) {
+  __shared__ float sc[CO], sh[CO];
+  const int n = blockIdx.x, tid = threadIdx.x;
+  if (tid < CO) {
+    const float* pp = partials + (size_t)n * kBands * CO * 2;
+    float cnt = 0.0f, mean = 0.0f, m2 = 0.0f;
+    for (int b = 0; b < kBands; ++b) {
+      const float nb = (float)(((OH - b * kBand) < kBand ? (OH - b * kBand) : kBand) * OW);
+      const float mb = pp[(b * CO + tid) * 2], m2b = pp[(b * CO + tid) * 2 + 1];
+      const float tot = cnt + nb;
+      const float d = mb - mean;
+      mean += d * (nb / tot);
+      m2 += m2b + d * d * (cnt * nb / tot);
+      cnt = tot;
+    }
+    const float var = m2 / cnt;
+    const float s = gamma[tid] / sqrtf(var + eps);
+    sc[tid] = s;
+    sh[tid] = beta[tid] - mean * s;
+  }
+  __syncthreads();
+  // 8 channels (16 B) per item
+  uint4* base = reinterpret_cast<uint4*>(y + (size_t)n * OH * OW * CO);
+  const int items = OH * OW * CO / 8;
+  for (int i = tid; i < items; i += blockDim.x) {
+    uint4 v = base[i];
+    const int c0 = (i & 3) * 8;
+    __half2* hv = reinterpret_cast<__half2*>(&v);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float2 f = __half22float2(hv[k]);
+      hv[k] = __floats2half2_rn(f.x * sc[c0 + 2 * k] + sh[c0 + 2 * k],
+                                f.y * sc[c0 + 2 * k + 1] + sh[c0 + 2 * k + 1]);
+    }
+    base[i] = v;
+  }
+}
+
+
+// ---- the 32-channel 4x4 convolutions (conv2..conv4) ----------------------------------
+// One template for config.json's conv_2d(32 -> 32, 4x4, stride ST) layers.
+//
+// A persistent workgroup streams whole samples (n = blockIdx.x, + gridDim.x, ...)
+// through a ring of input rows in LDS.  A step is NW tiles of 32 consecutive
+// output pixels, one per wave; while a step's MFMAs run, the input rows the
+// NEXT step adds are already in flight into registers, and they are written to
+// the ring (after the previous layer's BatchNorm, kIn 1) once the step's
+// epilogue is done: one barrier per step, HBM loads overlapped with compute.
+//
+//   ring  input row r of the WG's k-th sample lives in slot (k*IH + r) % kRing
+//         (ConvGeom::ring() rows: a step's rows plus its successor's); a row is
+//         IW pixels x 64 B, stride-2 layers store the even then the odd
+//         columns (a lane's neighbour reads the next pixel of the same plane),
+//         and chunk c (8 channels) of the pixel at position pos sits at
+//         16 * (c ^ ((pos >> 2) & 3)): 16 lanes of a ds_read_b128 group read
+//         16 distinct 16-B slots of the 256-B bank row
+//   in    kIn 1: y = x * sc + sh with the previous layer's train-mode
+//         batch-of-one BatchNorm, (sc, sh) from its statistics (Chan's merge)
+//   mma   v_mfma_f32_32x32x16_f16, A = weights (32 steps of 16 k, held in
+//         registers for the whole launch), B = the pixel's im2col column:
+//         step s reads 8 channels of input pixel (ky, kx) = (s/8, (s/2)%4) at
+//         channel 16*(s%2) + 8*h
+//   out   bias + LeakyReLU, then kOut 0: fp16 NHWC + per-sample Welford
+//         statistics (mean, M2) -> part[n][32][2]; 1: fp16 NHWC only (eval
+//         mode, BN folded); 2: one step holds the whole sample: exact two-pass
+//         statistics over the registers, BatchNorm, written flattened in NCHW
+//         order (the reference's view(x.size(0), -1)) for the first linear;
+//         3: flattened, no norm
+template <int IH, int IW, int OH, int OW, int ST, int NW>
+struct ConvGeom {
+  static constexpr int kPix = OH * OW;
+  static constexpr int kTiles = (kPix + 31) / 32;
+  static constexpr int kSteps = (kTiles + NW - 1) / NW;
+  static constexpr int kStepPix = 32 * NW;
+  // input rows step j reads: lo(j) .. hi(j)
+  __host__ __device__ static constexpr int lo(int j) { return ST * ((kStepPix * j) / OW); }
+  __host__ __device__ static constexpr int hi(int j) {
+    const int end = kStepPix * (j + 1) < kPix ? kStepPix * (j + 1) : kPix;
+    const int r = ST * ((end - 1) / OW) + 3;
+    return r < IH - 1 ? r : IH - 1;
+  }
+  // first row the step after j loads (its earlier rows are already in the ring)
+  __host__ __device__ static constexpr int first_new(int j) {
+    return (j + 1 == kSteps) ? 0 : (hi(j) + 1 > lo(j + 1) ? hi(j) + 1 : lo(j + 1));
+  }
+  __host__ __device__ static constexpr int last_new(int j) {
+    return (j + 1 == kSteps) ? hi(0) : hi(j + 1);
+  }
+  // ring rows: step j's rows and its successor's held at once
+  static constexpr int ring() {
+    int m = 0;
+    for (int j = 0; j < kSteps; ++j) {
+      const int span = (j + 1 < kSteps) ? hi(j + 1) - lo(j) + 1 : (IH - lo(j)) + hi(0) + 1;
+      m = span > m ? span : m;
+    }
+    return m;
+  }
+  // most rows one step's prefetch brings in
+  static constexpr int max_new() {
+    int m = 0;
+    for (int j = 0; j < kSteps; ++j) {
+      const int r = last_new(j) - first_new(j) + 1;
+      m = r > m ? r : m;
+    }
+    return m;
+  }
+};
+
+// (lo, hi) fp16 pair -> (fp16(lo * s0 + h0), fp16(hi * s1 + h1)): an f32 fma of
+// the fp16 input rounded once, one v_fma_mix per element
+__device__ __forceinline__ uint32_t norm_pair(uint32_t x, float s0, float h0, float s1, float h1) {
+  uint32_t d;
+  asm("v_fma_mixlo_f16 %0, %1, %2, %3 op_sel_hi:[1,0,0]" : "=v"(d) : "v"(x), "v"(s0), "v"(h0));
+  asm("v_fma_mixhi_f16 %0, %1, %2, %3 op_sel:[1,0,0] op_sel_hi:[1,0,0]"
+      : "+v"(d) : "v"(x), "v"(s1), "v"(h1));
+  return d;
+}
+
+// byte offset of (pixel px, 16-B chunk c) inside a ring row
+template <int IW, int ST>
+__device__ __forceinline__ int ring_off(int px, int c) {
+  constexpr int kHalfW = (IW + 1) / 2;
+  const int pos = ST == 2 ? ((px & 1) ? kHalfW + (px >> 1) : (px >> 1)) : px;
+  return 64 * pos + 16 * (c ^ ((pos >> 2) & 3));
+}
+
+template <int IH, int IW, int OH, int OW, int ST, int NW, int kIn, int kOut, int kPrevRows>
+__global__ void __launch_bounds__(64 * NW, 1)   // one wave per SIMD: the full register file
+conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfrag,
+              const float* __restrict__ bias, const float* __restrict__ prev_part,
+              const float* __restrict__ in_gamma, const float* __restrict__ in_beta, float in_eps,
+              __half* __restrict__ y, float* __restrict__ part,
+              const float* __restrict__ out_gamma, const float* __restrict__ out_beta,
+              float out_eps, float slope) {
+  using G = ConvGeom<IH, IW, OH, OW, ST, NW>;
+  constexpr int kRing = G::ring();
+  constexpr int kRowU4 = IW * 4;                  // 16-B chunks per input row
+  constexpr int kRowBytes = IW * 64;
+  constexpr int kThreads = 64 * NW;
+  constexpr int kPre = (G::max_new() * kRowU4 + kThreads - 1) / kThreads;
+  static_assert(kOut < 2 || G::kSteps == 1, "the in-kernel norm needs the sample in one step");
+  __shared__ __attribute__((aligned(16))) uint4 ring[kRing * kRowU4];
+  __shared__ float s_sc[3][CO], s_sh[3][CO];   // input norm of samples k % 3
+  __shared__ float red[NW][CO][3];
+  __shared__ float s_mean[CO], s_rstd[CO], s_bias[CO];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 31, h = lane >> 5;
+  unsigned char* rb = reinterpret_cast<unsigned char*>(ring);
+
+  const int my = n > (int)blockIdx.x ? (n - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
+  const int total = my * G::kSteps;
+  if (total == 0) return;
+  auto sample = [&](int k) __attribute__((always_inline)) { return (int)blockIdx.x + k * (int)gridDim.x; };
+
+  // the previous layer's BatchNorm of the WG's k-th sample (threads < CO), in
+  // two halves: the statistics loads are issued ahead of a step's prefetch
+  // (so waiting for them never waits for the prefetch), merged after its MFMAs
+  constexpr int kPB = (IH + kPrevRows - 1) / kPrevRows;
+  float st[kIn == 1 ? kPB : 1][2];
+  float gam = 0.0f, bet = 0.0f;
+  auto stats_load = [&](int k) __attribute__((always_inline)) {
+    // every thread, every step, sample clamped: a fixed count of loads on
+    // every path keeps the compiler's vmcnt waits exact
+    if (kIn == 1) {
+      const int ns = sample(k) < n ? sample(k) : n - 1;
+      const float* pp = prev_part + (size_t)ns * kPB * CO * 2;
+      const int c = tid & (CO - 1);
+#pragma unroll
+      for (int q = 0; q < kPB; ++q) {
+        st[q][0] = pp[(q * CO + c) * 2];
+        st[q][1] = pp[(q * CO + c) * 2 + 1];
+      }
+      gam = in_gamma[c];
+      bet = in_beta[c];
+    }
+  };
+  auto stats_merge = [&](int k) __attribute__((always_inline)) {
+    if (kIn == 1 && tid < CO) {
+      float cnt = 0.0f, mean = 0.0f, m2 = 0.0f;
+#pragma unroll
+      for (int q = 0; q < kPB; ++q) {
+        const int rq = (IH - q * kPrevRows) < kPrevRows ? (IH - q * kPrevRows) : kPrevRows;
+        const float nb = (float)(rq * IW);
+        const float tot = cnt + nb, d = st[q][0] - mean;
+        mean += d * (nb / tot);
+        m2 += st[q][1] + d * d * (cnt * nb / tot);
+        cnt = tot;
+      }
+      const float sc = gam / sqrtf(m2 / cnt + in_eps);
+      s_sc[k % 3][tid] = sc;
+      s_sh[k % 3][tid] = bet - mean * sc;
+    }
+  };
+  // new rows r0..r1 of the k-th sample: chunk q = tid + i*kThreads of the
+  // contiguous range into registers, later into the ring as they are
+  auto issue = [&](u32x4 (&pre)[kPre], int k, int r0, int r1) __attribute__((always_inline)) {
+    // unconditional (clamped chunk and sample): see stats_load
+    const int cnt = (r1 - r0 + 1) * kRowU4;
+    const int ns = sample(k) < n ? sample(k) : n - 1;
+    const u32x4* src = reinterpret_cast<const u32x4*>(x + ((size_t)ns * IH + r0) * IW * CO);
+#pragma unroll
+    for (int i = 0; i < kPre; ++i) {
+      const int q = tid + i * kThreads;
+      pre[i] = src[q < cnt ? q : cnt - 1];
+    }
+  };
+  auto commit = [&](const u32x4 (&pre)[kPre], int k, int r0, int r1) __attribute__((always_inline)) {
+    const int cnt = (r1 - r0 + 1) * kRowU4;
+#pragma unroll
+    for (int i = 0; i < kPre; ++i) {
+      const int q = tid + i * kThreads;
+      if (q >= cnt) continue;
+      const int r = q / kRowU4, qq = q - r * kRowU4;
+      const int slot = (k * IH + r0 + r) % kRing;
+      *reinterpret_cast<u32x4*>(rb + slot * kRowBytes + ring_off<IW, ST>(qq >> 2, qq & 3)) = pre[i];
+    }
+  };
+
+  // weights and bias for the whole launch (row = out channel = lane & 31)
+  half8 wa[32];
+#pragma unroll
+  for (int s = 0; s < 32; ++s) wa[s] = wfrag[s * 64 + lane];
+  if (tid < CO) s_bias[tid] = bias[tid];
+  float w_cnt = 0.0f, w_mean[16], w_m2[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) w_mean[r] = w_m2[r] = 0.0f;
+
+  // One step.  At its start the ring holds step g's rows and registers `cur`
+  // the rows of step g+1 (loaded during step g-1); it loads step g+2's new
+  // rows into `nxt`, computes, and commits `cur` to the ring: HBM reads run
+  // two steps ahead of the MFMAs.
+  auto step = [&](int g, int k, int j, u32x4 (&nxt)[kPre], const u32x4 (&cur)[kPre]) __attribute__((always_inline)) {
+    const int ns = sample(k);
+    const bool last_j = j + 1 == G::kSteps;
+    const int k1 = last_j ? k + 1 : k, j1 = last_j ? 0 : j + 1;   // step g+1
+    const bool last_j1 = j1 + 1 == G::kSteps;
+    const int k2 = last_j1 ? k1 + 1 : k1;                         // step g+2
+    const bool stats2 = g + 2 < total && last_j1;   // step g+2 starts sample k2
+    stats_load(k2);
+    if (!(DTCONV_SKIP & 1)) issue(nxt, k2, G::first_new(j1), G::last_new(j1));
+
+    // the input norm of this sample for this lane's B channels 16*(s%2) + 8h + j
+    float isc[2][8], ish[2][8];
+    if (kIn == 1) {
+#pragma unroll
+      for (int e = 0; e < 2; ++e)
+#pragma unroll
+        for (int q = 0; q < 8; ++q) {
+          isc[e][q] = s_sc[k % 3][16 * e + 8 * h + q];
+          ish[e][q] = s_sh[k % 3][16 * e + 8 * h + q];
+        }
+    }
+    // this wave's tile
+    const int t = NW * j + wave;
+    const int p = 32 * t + col;
+    const bool valid = p < G::kPix;
+    const int pc = valid ? p : 0;
+    const int oy = pc / OW, ox = pc - oy * OW;
+    int row[4];
+#pragma unroll
+    for (int ky = 0; ky < 4; ++ky) row[ky] = ((k * IH + ST * oy + ky) % kRing) * kRowBytes;
+    int off[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) off[q] = ring_off<IW, ST>(ST * ox + (q >> 1), 2 * (q & 1) + h);
+    // 4 groups (ky) of 8 B fragments: group g+1's LDS reads are in flight
+    // while group g's MFMAs run
+    f32x16 acc;   // starts at the bias
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = s_bias[(r & 3) + 8 * (r >> 2) + 4 * h];
+    half8 bq[2][8];
+    auto ld = [&](half8 (&b)[8], int gy) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) b[i] = *reinterpret_cast<const half8*>(rb + row[gy] + off[i]);
+    };
+    auto mm = [&](half8 (&b)[8], int gy) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        half8 bf = b[i];
+        if (kIn == 1) {
+          u32x4 u = __builtin_bit_cast(u32x4, bf);
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+            u[q] = norm_pair(u[q], isc[i & 1][2 * q], ish[i & 1][2 * q], isc[i & 1][2 * q + 1],
+                             ish[i & 1][2 * q + 1]);
+          bf = __builtin_bit_cast(half8, u);
+        }
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wa[8 * gy + i], bf, acc, 0, 0, 0);
+      }
+    };
+    if (!(DTCONV_SKIP & 2)) ld(bq[0], 0);
+#pragma unroll
+    for (int gy = 0; gy < 4 && !(DTCONV_SKIP & 2); ++gy) {
+      if (gy < 3) ld(bq[(gy + 1) & 1], gy + 1);
+      __builtin_amdgcn_sched_barrier(0);
+      mm(bq[gy & 1], gy);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (stats2) stats_merge(k2);   // read by step g+2, after two barriers
+    float v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = lrelu(acc[r], slope);
+
+    // epilogue
+    if (kOut <= 1) {
+      if (valid && !(DTCONV_SKIP & 4)) {
+        __half* dst = y + ((size_t)ns * G::kPix + p) * CO;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const __half2 v0 = __floats2half2_rn(v[4 * q + 0], v[4 * q + 1]);
+          const __half2 v1 = __floats2half2_rn(v[4 * q + 2], v[4 * q + 3]);
+          uint2 u;
+          u.x = *reinterpret_cast<const uint32_t*>(&v0);
+          u.y = *reinterpret_cast<const uint32_t*>(&v1);
+          *reinterpret_cast<uint2*>(dst + 8 * q + 4 * h) = u;
+        }
+      }
+      if (kOut == 0 && valid && !(DTCONV_SKIP & 8)) {   // Welford over this lane's pixels
+        w_cnt += 1.0f;
+        const float inv = 1.0f / w_cnt;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float d = v[r] - w_mean[r];
+          w_mean[r] += d * inv;
+          w_m2[r] += d * (v[r] - w_mean[r]);
+        }
+      }
+      if (kOut == 0 && last_j) {
+        // merge the 32 lanes of each half (same 16 channels), then the waves
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+          const float nb = __shfl_xor(w_cnt, o, 32);
+          const float tot = w_cnt + nb;
+          const float fa = tot > 0.0f ? nb / tot : 0.0f, fb = tot > 0.0f ? w_cnt * nb / tot : 0.0f;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float mb = __shfl_xor(w_mean[r], o, 32), m2b = __shfl_xor(w_m2[r], o, 32);
+            const float d = mb - w_mean[r];
+            w_mean[r] += d * fa;
+            w_m2[r] += m2b + d * d * fb;
+          }
+          w_cnt = tot;
+        }
+        if (col == 0)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int c = (r & 3) + 8 * (r >> 2) + 4 * h;
+            red[wave][c][0] = w_cnt;
+            red[wave][c][1] = w_mean[r];
+            red[wave][c][2] = w_m2[r];
+          }
+        __syncthreads();
+        if (tid < CO) {
+          float cnt = 0.0f, mean = 0.0f, m2 = 0.0f;
+          for (int w = 0; w < NW; ++w) {
+            const float nb = red[w][tid][0];
+            if (nb <= 0.0f) continue;
+            const float tot = cnt + nb, d = red[w][tid][1] - mean;
+            mean += d * (nb / tot);
+            m2 += red[w][tid][2] + d * d * (cnt * nb / tot);
+            cnt = tot;
+          }
+          float* pp = part + ((size_t)ns * CO + tid) * 2;
+          pp[0] = mean;
+          pp[1] = m2;
+        }
+        w_cnt = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) w_mean[r] = w_m2[r] = 0.0f;
+      }
+    } else {   // the whole sample is in this step: BatchNorm of a batch of one, flatten
+      if (kOut == 2) {
+        // pass 1: mean
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          float sum = valid ? v[r] : 0.0f;
+#pragma unroll
+          for (int o = 16; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 32);
+          if (col == 0) red[wave][(r & 3) + 8 * (r >> 2) + 4 * h][0] = sum;
+        }
+        __syncthreads();
+        if (tid < CO) {
+          float sum = 0.0f;
+          for (int w = 0; w < NW; ++w) sum += red[w][tid][0];
+          s_mean[tid] = sum / (float)G::kPix;
+        }
+        __syncthreads();
+        // pass 2: M2 about the mean
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float d = v[r] - s_mean[(r & 3) + 8 * (r >> 2) + 4 * h];
+          float m2 = valid ? d * d : 0.0f;
+#pragma unroll
+          for (int o = 16; o > 0; o >>= 1) m2 += __shfl_xor(m2, o, 32);
+          if (col == 0) red[wave][(r & 3) + 8 * (r >> 2) + 4 * h][1] = m2;
+        }
+        __syncthreads();
+        if (tid < CO) {
+          float m2 = 0.0f;
+          for (int w = 0; w < NW; ++w) m2 += red[w][tid][1];
+          const float sc = out_gamma[tid] / sqrtf(m2 / (float)G::kPix + out_eps);
+          s_rstd[tid] = sc;
+          s_mean[tid] = out_beta[tid] - s_mean[tid] * sc;   // now the shift
+        }
+        __syncthreads();
+      }
+      if (valid) {
+        __half* dst = y + (size_t)ns * CO * G::kPix;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int c = (r & 3) + 8 * (r >> 2) + 4 * h;
+          const float o = kOut == 2 ? v[r] * s_rstd[c] + s_mean[c] : v[r];
+          dst[(size_t)c * G::kPix + p] = __float2half(o);
+        }
+      }
+    }
+
+    // step g+1's rows into the ring: their slots held rows no wave reads in
+    // this step; the barrier publishes them for the next
+    if (g + 1 < total && !(DTCONV_SKIP & 16)) commit(cur, k1, G::first_new(j), G::last_new(j));
+    __syncthreads();
+  };
+
+  // prologue: step 0's rows into the ring, step 1's into registers
+  u32x4 pa[kPre], pb[kPre];
+  stats_load(0);
+  stats_merge(0);
+  if (G::kSteps == 1 && total > 1) {
+    stats_load(1);
+    stats_merge(1);
+  }
+  issue(pa, 0, 0, G::hi(0));
+  commit(pa, 0, 0, G::hi(0));
+  if (total > 1)
+    issue(pb, G::kSteps == 1 ? 1 : 0, G::first_new(0), G::last_new(0));
+  __syncthreads();
+
+  int k = 0, j = 0;
+  for (int g = 0; g < total; g += 2) {
+    step(g, k, j, pa, pb);
+    if (++j == G::kSteps) { j = 0; ++k; }
+    if (g + 1 < total) {
+      step(g + 1, k, j, pb, pa);
+      if (++j == G::kSteps) { j = 0; ++k; }
+    }
+  }
+}
+
+template <int IH, int IW, int OH, int OW, int ST, int NW, int kIn, int kOut, int kPrevRows = IH>
+int launch_conv32(int n, const void* x, const void* wfrag, const float* bias,
+                  const float* prev_part, const float* ig, const float* ibt,
+                  float ieps, void* y, float* part, const float* og, const float* obt, float oeps,
+                  float slope, hipStream_t s) {
+  auto kern = conv32_kernel<IH, IW, OH, OW, ST, NW, kIn, kOut, kPrevRows>;
+  static int grid = 0;   // resident workgroups: one wave of them, persistent
+  if (!grid) {
+    int dev = 0, cus = 256, per = 1;
+    if (hipGetDevice(&dev) == hipSuccess)
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, 64 * NW, 0) != hipSuccess ||
+        per < 1)
+      per = 1;
+    grid = per * cus;
+  }
+  const int g = n < grid ? n : grid;
+  hipLaunchKernelGGL(kern, dim3(g), dim3(64 * NW), 0, s, n, (const __half*)x, (const half8*)wfrag,
+                     bias, prev_part, ig, ibt, ieps, (__half*)y, part, og, obt, oeps,
+                     slope);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
+// waves (tiles per step) per layer: conv2 / conv3 two (2-3 rings per CU), conv4
+// four (its 4 tiles in one step for the in-kernel norm)
+constexpr int kConv2Waves = 2, kConv3Waves = 2, kConv4Waves = 4;
+
+}  // namespace
+
+extern "C" int dt_conv1(const float* ring, int32_t n, int32_t slots, const int32_t* order,
+                        const void* wfrag, const float* bias, void* y, float* partials,
+                        float slope, void* stream) {
+  if (!ring || !wfrag || !bias || !y || !order || n < 0 || slots < 3) return DT_E_ARG;
+  for (int i = 0; i < 3; ++i)
+    if (order[i] < 0 || order[i] >= slots) return DT_E_ARG;
+  if (n == 0) return DT_OK;
+  const int items = n * kBands;
+  const int grid = items < persistent_grid() ? items : persistent_grid();
+  hipLaunchKernelGGL(conv1_kernel, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, items,
+                     ring, slots, order[0], order[1], order[2], (const half8*)wfrag, bias,
+                     (__half*)y, partials, slope);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
+extern "C" int dt_conv1_norm(void* y, int32_t n, const float* partials, const float* gamma,
+                             const float* beta, float eps, void* stream) {
+  if (!y || !partials || !gamma || !beta || n < 0) return DT_E_ARG;
+  if (n == 0) return DT_OK;
+  hipLaunchKernelGGL(conv1_norm_kernel, dim3(n), dim3(256), 0, (hipStream_t)stream, (__half*)y,
+                     partials, gamma, beta, eps);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
+extern "C" int32_t dt_conv1_bands(void) { return kBands; }
+
+// conv2..conv4 of the reference actor (see include/dtactor.h)
+extern "C" int dt_conv32(int32_t layer, int32_t n, const void* x, const void* wfrag,
+                         const float* bias, const float* prev_part, const float* in_gamma,
+                         const float* in_beta, float in_eps, void* y, float* part,
+                         const float* out_gamma, const float* out_beta, float out_eps,
+                         float slope, void* stream) {
+  if (!x || !wfrag || !bias || !y || n < 0) return DT_E_ARG;
+  if (n == 0) return DT_OK;
+  const bool in = prev_part != nullptr;
+  if (in && (!in_gamma || !in_beta)) return DT_E_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  switch (layer) {
+    case 2:   // 57x77 -> 27x37, stride 2; input norm from conv1's bands
+      if (in != (part != nullptr)) return DT_E_ARG;
+      return in ? launch_conv32<57, 77, 27, 37, 2, kConv2Waves, 1, 0, kBand>(
+                      n, x, wfrag, bias, prev_part, in_gamma, in_beta, in_eps, y, part,
+                      nullptr, nullptr, 0.f, slope, s)
+                : launch_conv32<57, 77, 27, 37, 2, kConv2Waves, 0, 1>(
+                      n, x, wfrag, bias, nullptr, nullptr, nullptr, 0.f, y, nullptr, nullptr,
+                      nullptr, 0.f, slope, s);
+    case 3:   // 27x37 -> 12x17, stride 2; input norm from conv2's per-sample statistics
+      if (in != (part != nullptr)) return DT_E_ARG;
+      return in ? launch_conv32<27, 37, 12, 17, 2, kConv3Waves, 1, 0>(
+                      n, x, wfrag, bias, prev_part, in_gamma, in_beta, in_eps, y, part,
+                      nullptr, nullptr, 0.f, slope, s)
+                : launch_conv32<27, 37, 12, 17, 2, kConv3Waves, 0, 1>(
+                      n, x, wfrag, bias, nullptr, nullptr, nullptr, 0.f, y, nullptr, nullptr,
+                      nullptr, 0.f, slope, s);
+    case 4:   // 12x17 -> 9x14, stride 1, whole sample per step; its own norm in-kernel; flattened
+      if (in != (out_gamma != nullptr)) return DT_E_ARG;
+      return in ? launch_conv32<12, 17, 9, 14, 1, kConv4Waves, 1, 2>(
+                      n, x, wfrag, bias, prev_part, in_gamma, in_beta, in_eps, y, nullptr,
+                      out_gamma, out_beta, out_eps, slope, s)
+                : launch_conv32<12, 17, 9, 14, 1, kConv4Waves, 0, 3>(
+                      n, x, wfrag, bias, nullptr, nullptr, nullptr, 0.f, y, nullptr, nullptr,
+                      nullptr, 0.f, slope, s);
+    default:
+      return DT_E_ARG;
+  }
+}

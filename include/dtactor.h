@@ -32,7 +32,7 @@ int dt_sample_norm(const void* x, void* y, int32_t n, int32_t hw, int32_t c, con
  * LeakyReLU (config.json actor; duckietown_rl/ddpg.py:36,56), read straight
  * from the observation ring: channel c of the stack is ring slot order[c]
  * (oldest first, the Transformer order).  An MFMA implicit GEMM in fp16 with
- * f32 accumulation (aido1_amd/csrc/dtconv1.hip).
+ * f32 accumulation (aido1_amd/csrc/dtconv.hip).
  *   ring      device f32 [n, slots, 120, 160]
  *   wfrag     device fp16 [16, 64, 8]: the weights as the MFMA A fragments,
  *             element [s][l][j] = w[co = l%32][c = j%4][ky = s/2]
@@ -50,6 +50,28 @@ int dt_conv1(const float* ring, int32_t n, int32_t slots, const int32_t* order, 
 int dt_conv1_norm(void* y, int32_t n, const float* partials, const float* gamma,
                   const float* beta, float eps, void* stream);
 int32_t dt_conv1_bands(void);
+
+/* dt_conv32: conv2 / conv3 / conv4 of the actor (layer = 2, 3, 4: conv_2d
+ * 32 -> 32, 4x4, strides 2, 2, 1) + bias + LeakyReLU, MFMA fp16 with f32
+ * accumulation, NHWC fp16 in and out (aido1_amd/csrc/dtconv.hip): persistent
+ * workgroups stream whole samples through an LDS ring of input rows.
+ *   wfrag      device fp16 [32, 64, 8] A fragments: [s][l][j] =
+ *              w[l%32][16*(s%2) + 8*(l/32) + j][(s/2)/4][(s/2)%4]
+ *   prev_part  the previous layer's band statistics (dt_conv1's partials for
+ *              layer 2, this call's `part` of layer 2 / 3 for 3 / 4) or NULL:
+ *              with it, the previous BatchNorm (in_gamma, in_beta, in_eps) is
+ *              applied per sample while the input is staged (reference mode)
+ *   part       layers 2, 3 with prev_part: out [n, 32, 2], the sample's
+ *              per-channel (mean, M2) of the LeakyReLU outputs
+ *   y          layers 2, 3: [n, OH, OW, 32]; layer 4: [n, 32*9*14] flattened in
+ *              NCHW order, normalised by (out_gamma, out_beta, out_eps) when
+ *              prev_part is given (the last BatchNorm, whole sample in-kernel)
+ * Without prev_part the layer is the eval-mode one (BatchNorms folded into
+ * the weights by the caller). */
+int dt_conv32(int32_t layer, int32_t n, const void* x, const void* wfrag, const float* bias,
+              const float* prev_part, const float* in_gamma, const float* in_beta, float in_eps,
+              void* y, float* part, const float* out_gamma, const float* out_beta,
+              float out_eps, float slope, void* stream);
 
 #ifdef __cplusplus
 }

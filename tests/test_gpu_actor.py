@@ -145,3 +145,61 @@ def test_conv1_kernel_matches_conv2d(gpu, slots, order):
         beta.double().view(1, -1, 1, 1)
     err = (y.permute(0, 3, 1, 2).double() - want).abs().max().item()
     assert err < 5e-3 * max(1.0, want.abs().max().item()), err    # fp16 output rounding
+
+
+@pytest.mark.parametrize('n', [19, 1100])
+@pytest.mark.parametrize('layer,shape,stride', [(2, (57, 77), 2), (3, (27, 37), 2), (4, (12, 17), 1)])
+def test_conv32_layers_match_conv2d(gpu, layer, shape, stride, n):
+    """dt_conv32 without statistics (the eval-mode layer) vs conv2d + LeakyReLU
+    on the same fp16 data; layer 4 writes the NCHW flatten.  n = 1100 exceeds
+    the resident grid, so workgroups stream several samples through the ring."""
+    import torch.nn.functional as F
+    from aido1_amd import _lib
+    from aido1_amd.actor import conv32_fragments
+    L = _lib.lib()
+    torch.manual_seed(layer)
+    x = (torch.rand(n, 32, *shape, device=gpu) * 2 - 0.5).half()
+    w = (torch.randn(32, 32, 4, 4, device=gpu) * 0.05).half()
+    b = (torch.randn(32, device=gpu) * 0.1).half().float()
+    ref = F.leaky_relu(F.conv2d(x.float(), w.float(), b, stride=stride))
+    xh = x.permute(0, 2, 3, 1).contiguous()                        # NHWC
+    oh, ow = ref.shape[2:]
+    y = torch.empty(n, 32 * oh * ow if layer == 4 else oh * ow * 32, dtype=torch.float16,
+                    device=gpu)
+    s = torch.cuda.current_stream().cuda_stream
+    assert L.dt_conv32(layer, n, xh.data_ptr(), conv32_fragments(w.float()).data_ptr(),
+                       b.data_ptr(), None, None, None, 0.0, y.data_ptr(), None, None, None,
+                       0.0, 0.01, s) == 0
+    got = y.view(n, 32, oh, ow) if layer == 4 else y.view(n, oh, ow, 32).permute(0, 3, 1, 2)
+    err = (got.float() - ref).abs().max().item()
+    assert err < 3e-3 * max(1.0, ref.abs().max().item()), err
+
+
+def test_fp16_eval_mode_close_to_fp32(gpu):
+    from aido1_amd.actor import ConfigActor, FusedActor
+    a = ConfigActor(golden('reference_config.json')['model']['actor'])
+    a.load_state_dict(formula_state_dict(a.state_dict()))
+    a.eval()
+    x = formula_input(4)
+    with torch.no_grad():
+        ref = a(x)
+    f = FusedActor(a.to(gpu), dtype=torch.float16, mode='eval')
+    assert torch.max(torch.abs(f(x.to(gpu)).cpu() - ref)) < 1e-2
+
+
+def test_hip_convs_reference_mode_many_samples(gpu):
+    """The fp16 HIP conv chain in reference mode (every per-sample BatchNorm
+    applied by the next kernel) vs the f32 MIOpen + dt_sample_norm path, for
+    more samples than the persistent grid holds at once."""
+    from aido1_amd.actor import ConfigActor, FusedActor
+    from test_trainer import no_dropout
+    a = ConfigActor(no_dropout(golden('reference_config.json')['model']['actor']))
+    a.load_state_dict(formula_state_dict(a.state_dict()))
+    torch.manual_seed(5)
+    x = torch.rand(1100, 3, 120, 160, device=gpu)
+    h = FusedActor(a.to(gpu), dtype=torch.float16, mode='reference')
+    f = FusedActor(a, dtype=torch.float32, mode='reference')
+    got = h(x)
+    want = f(x)
+    assert torch.isfinite(got).all()
+    assert torch.max(torch.abs(got - want)).item() < 2e-2
