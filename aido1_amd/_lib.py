@@ -21,7 +21,7 @@ SOURCES = ['dtsim.hip', 'dtrender.hip', 'dtreplay.hip', 'dtactor.hip', 'dtconv.h
 HEADERS = ['dtsim_common.h', 'dtrender.h']
 PUBLIC_HEADERS = ['dtsim.h', 'dtreplay.h', 'dtactor.h']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 HIP_FLAGS = ['--offload-arch=gfx950', '-O3', '-fPIC', '-shared', '-std=c++17',
              '-ffp-contract=off', '-munsafe-fp-atomics']
@@ -34,7 +34,9 @@ class DtError(RuntimeError):
 class DtMap(ctypes.Structure):
     _fields_ = [('width', ctypes.c_int32), ('height', ctypes.c_int32),
                 ('kind', ctypes.c_void_p), ('curve_start', ctypes.c_void_p),
-                ('curves', ctypes.c_void_p), ('headings', ctypes.c_void_p)]
+                ('curves', ctypes.c_void_p), ('headings', ctypes.c_void_p),
+                ('n_objects', ctypes.c_int32), ('objects', ctypes.c_void_p),
+                ('n_spawn_objects', ctypes.c_int32), ('spawn_objects', ctypes.c_void_p)]
 
 
 def _sources():

@@ -28,6 +28,8 @@ DEFAULT_ROBOT_SPEED = 1.20
 DEFAULT_FRAMERATE = 30
 DEFAULT_FRAME_SKIP = 1
 MAX_SPAWN_ATTEMPTS = 5000
+SAFETY_RAD_MULT = 1.8      # [upstream] objects: safety circles (AGENT_SAFETY_RAD, radii)
+MIN_SPAWN_OBJ_DIST = 0.25  # [upstream] _inconvenient_spawn margin
 REWARD_INVALID_POSE = -1000
 
 
@@ -56,6 +58,7 @@ class DtConfig(ctypes.Structure):
         ('reward_speed_measured', ctypes.c_int32),
         ('front_probe_length', ctypes.c_int32),
         ('auto_reset', ctypes.c_int32),
+        ('safety_rad_mult', ctypes.c_double),
     ]
 
 
@@ -120,6 +123,7 @@ class EnvConfig:
         c.reward_speed_measured = int(self.reward_speed_measured)
         c.front_probe_length = int(self.front_probe_length)
         c.auto_reset = int(self.auto_reset)
+        c.safety_rad_mult = SAFETY_RAD_MULT
         return c
 
     def replace(self, **kw):

@@ -138,13 +138,16 @@ __global__ __launch_bounds__(64) void step_kernel(dt::State st, dt::MapDev md, d
         sd = true;
       } else {
         const double sp = sc.speed_measured ? speed : g.robot_speed;
+        // compute_reward: proximity_penalty2 at the actual centre (0 without objects)
+        const double pen =
+            M.n_obj ? dt::proximity_penalty(M, g, x + g.off * c, z + g.off * (-s)) : 0.0;
         lp_fresh = true;
         lp_inl = dt::lane_pos<false>(M, g, x, z, c, s, lp);
         if (lp_inl) {
           const double ad = fabs(lp[0]);
-          r = ((1.0 * sp) * lp[1] + (-10.0) * ad) + 40.0 * 0.0;
+          r = ((1.0 * sp) * lp[1] + (-10.0) * ad) + 40.0 * pen;
         } else {
-          r = 40.0 * 0.0;
+          r = 40.0 * pen;
         }
       }
       // BaselineAggregationFunction (aggregation_functions.py:25-32)
@@ -362,6 +365,16 @@ int dt_create(const dt_config* cfg, const dt_map* map, uint64_t seed, int32_t n_
     }
   }
   const int C = map->curve_start[T];
+  const int NO = map->n_objects, NS = map->n_spawn_objects;
+  if (NO < 0 || NO > 256 || NS < 0 || NS > 256 || (NO > 0 && !map->objects) ||
+      (NS > 0 && !map->spawn_objects)) {
+    g_create_err = "dt_create: bad object tables (n_objects / n_spawn_objects in 0..256)";
+    return DT_E_ARG;
+  }
+  if (NO > 0 && !(cfg->safety_rad_mult > 0.0)) {
+    g_create_err = "dt_create: objects need safety_rad_mult > 0";
+    return DT_E_ARG;
+  }
   int ndev = 0;
   if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= device || device < 0) {
     g_create_err = "dt_create: no HIP device " + std::to_string(device);
@@ -401,6 +414,10 @@ int dt_create(const dt_config* cfg, const dt_map* map, uint64_t seed, int32_t n_
   g.accept_deg = cfg->accept_start_angle_deg;
   g.reset_safety = cfg->reset_safety;
   g.robot_speed = cfg->robot_speed;
+  g.robot_length = cfg->robot_length;
+  g.agent_safety_rad =
+      ((cfg->robot_length > cfg->robot_width ? cfg->robot_length : cfg->robot_width) / 2) *
+      cfg->safety_rad_mult;
   StepCfg& sc = h->sc;
   sc.repeat = cfg->repeat_actions;
   sc.frame_skip = cfg->frame_skip;
@@ -422,27 +439,32 @@ int dt_create(const dt_config* cfg, const dt_map* map, uint64_t seed, int32_t n_
     return DT_E_HIP;
   };
   if (hipSetDevice(device) != hipSuccess) return fail("hipSetDevice failed");
-  // map image: curves | headings | curve_start (u16) | kind | drivable
-  if (dt::map_lds_bytes(T, (int)drv.size(), C) > dt::kMaxMapLdsBytes) {
-    g_create_err = "dt_create: map image over the LDS budget (" +
-                   std::to_string(dt::map_lds_bytes(T, (int)drv.size(), C)) + " B)";
+  // map image: curves | headings | objects | spawn objects | curve_start (u16) | kind |
+  // drivable
+  const size_t lds = dt::map_lds_bytes(T, (int)drv.size(), C, NO, NS);
+  if (lds > dt::kMaxMapLdsBytes) {
+    g_create_err = "dt_create: map image over the LDS budget (" + std::to_string(lds) + " B)";
     delete h;
     return DT_E_ARG;
   }
   std::vector<uint16_t> cs(T + 1);
   for (int t = 0; t <= T; ++t) cs[t] = (uint16_t)map->curve_start[t];
   const size_t cb = (size_t)C * 12 * 8, hb = (size_t)C * 3 * 8,
+               ob = (size_t)NO * DT_OBJ_STRIDE * 8, spb = (size_t)NS * 4 * 8,
                sb16 = ((size_t)(T + 1) * 2 + 15) & ~15ul, kb = ((size_t)T + 15) & ~15ul,
                db = (drv.size() * 2 + 15) & ~15ul;
-  if (hipMalloc(&h->map_buf, cb + hb + sb16 + kb + db) != hipSuccess)
+  if (hipMalloc(&h->map_buf, cb + hb + ob + spb + sb16 + kb + db) != hipSuccess)
     return fail("hipMalloc(map)");
   char* mb = (char*)h->map_buf;
+  char* m_cs = mb + cb + hb + ob + spb;
   if ((cb && hipMemcpy(mb, map->curves, cb, hipMemcpyHostToDevice) != hipSuccess) ||
       (hb && hipMemcpy(mb + cb, map->headings, hb, hipMemcpyHostToDevice) != hipSuccess) ||
-      hipMemcpy(mb + cb + hb, cs.data(), (size_t)(T + 1) * 2, hipMemcpyHostToDevice) !=
-          hipSuccess ||
-      hipMemcpy(mb + cb + hb + sb16, map->kind, (size_t)T, hipMemcpyHostToDevice) != hipSuccess ||
-      hipMemcpy(mb + cb + hb + sb16 + kb, drv.data(), drv.size() * 2, hipMemcpyHostToDevice) !=
+      (ob && hipMemcpy(mb + cb + hb, map->objects, ob, hipMemcpyHostToDevice) != hipSuccess) ||
+      (spb && hipMemcpy(mb + cb + hb + ob, map->spawn_objects, spb, hipMemcpyHostToDevice) !=
+                  hipSuccess) ||
+      hipMemcpy(m_cs, cs.data(), (size_t)(T + 1) * 2, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(m_cs + sb16, map->kind, (size_t)T, hipMemcpyHostToDevice) != hipSuccess ||
+      hipMemcpy(m_cs + sb16 + kb, drv.data(), drv.size() * 2, hipMemcpyHostToDevice) !=
           hipSuccess)
     return fail("hipMemcpy(map)");
   h->map.width = map->width;
@@ -450,12 +472,16 @@ int dt_create(const dt_config* cfg, const dt_map* map, uint64_t seed, int32_t n_
   h->map.n_tiles = T;
   h->map.n_drivable = (int)drv.size();
   h->map.n_curves = C;
+  h->map.n_obj = NO;
+  h->map.n_spawn_obj = NS;
   h->map.curves = (const double*)mb;
   h->map.headings = (const double*)(mb + cb);
-  h->map.curve_start = (const uint16_t*)(mb + cb + hb);
-  h->map.kind = (const int8_t*)(mb + cb + hb + sb16);
-  h->map.drivable = (const int16_t*)(mb + cb + hb + sb16 + kb);
-  h->lds_bytes = dt::map_lds_bytes(T, (int)drv.size(), C);
+  h->map.obj = (const double*)(mb + cb + hb);
+  h->map.spawn_obj = (const double*)(mb + cb + hb + ob);
+  h->map.curve_start = (const uint16_t*)m_cs;
+  h->map.kind = (const int8_t*)(m_cs + sb16);
+  h->map.drivable = (const int16_t*)(m_cs + sb16 + kb);
+  h->lds_bytes = lds;
 
   // state: x z angle seed (8 B) | step_count env_step episode (4 B) | err
   const size_t N = (size_t)n_envs, N8 = N * 8, N4 = (N * 4 + 255) & ~255ul;

@@ -53,9 +53,11 @@ __device__ inline void wave_add(unsigned long long* p, unsigned v) {
 
 // Map image in device memory; staged into LDS by each block.
 struct MapDev {
-  int32_t width, height, n_tiles, n_drivable, n_curves;
+  int32_t width, height, n_tiles, n_drivable, n_curves, n_obj, n_spawn_obj;
   const double* curves;     // [C,4,3]
   const double* headings;   // [C,3]
+  const double* obj;        // [n_obj, DT_OBJ_STRIDE] collidable static objects
+  const double* spawn_obj;  // [n_spawn_obj, 4] x, y, z, spawn radius
   const uint16_t* curve_start;  // [T+1]
   const int8_t* kind;       // [T]
   const int16_t* drivable;  // [n_drivable] tile index of the k-th drivable tile (load order)
@@ -65,14 +67,18 @@ struct MapDev {
 struct MapLds {
   const double* curves;
   const double* headings;
+  const double* obj;
+  const double* spawn_obj;
   const uint16_t* curve_start;
   const int8_t* kind;
   const int16_t* drivable;
-  int32_t width, height, n_drivable;
+  int32_t width, height, n_drivable, n_obj, n_spawn_obj;
 };
 
-__host__ __device__ inline size_t map_lds_bytes(int n_tiles, int n_drivable, int n_curves) {
+__host__ __device__ inline size_t map_lds_bytes(int n_tiles, int n_drivable, int n_curves,
+                                                int n_obj = 0, int n_spawn_obj = 0) {
   size_t b = (size_t)n_curves * (12 + 3) * sizeof(double);
+  b += ((size_t)n_obj * DT_OBJ_STRIDE + (size_t)n_spawn_obj * 4) * sizeof(double);
   b += ((size_t)(n_tiles + 1) * 2 + 15) & ~(size_t)15;
   b += ((size_t)n_tiles + 15) & ~(size_t)15;
   b += ((size_t)n_drivable * 2 + 15) & ~(size_t)15;
@@ -83,12 +89,16 @@ __host__ __device__ inline size_t map_lds_bytes(int n_tiles, int n_drivable, int
 __device__ inline MapLds stage_map(const MapDev& m, unsigned char* lds) {
   double* cv = reinterpret_cast<double*>(lds);
   double* hd = cv + (size_t)m.n_curves * 12;
-  uint16_t* cs = reinterpret_cast<uint16_t*>(hd + (size_t)m.n_curves * 3);
+  double* ob = hd + (size_t)m.n_curves * 3;
+  double* so = ob + (size_t)m.n_obj * DT_OBJ_STRIDE;
+  uint16_t* cs = reinterpret_cast<uint16_t*>(so + (size_t)m.n_spawn_obj * 4);
   int8_t* kd = reinterpret_cast<int8_t*>(cs) + (((size_t)(m.n_tiles + 1) * 2 + 15) & ~(size_t)15);
   int16_t* dv = reinterpret_cast<int16_t*>(kd + (((size_t)m.n_tiles + 15) & ~(size_t)15));
   const int tid = threadIdx.x, nt = blockDim.x;
   for (int i = tid; i < m.n_curves * 12; i += nt) cv[i] = m.curves[i];
   for (int i = tid; i < m.n_curves * 3; i += nt) hd[i] = m.headings[i];
+  for (int i = tid; i < m.n_obj * DT_OBJ_STRIDE; i += nt) ob[i] = m.obj[i];
+  for (int i = tid; i < m.n_spawn_obj * 4; i += nt) so[i] = m.spawn_obj[i];
   for (int i = tid; i <= m.n_tiles; i += nt) cs[i] = m.curve_start[i];
   for (int i = tid; i < m.n_tiles; i += nt) kd[i] = m.kind[i];
   for (int i = tid; i < m.n_drivable; i += nt) dv[i] = m.drivable[i];
@@ -96,12 +106,16 @@ __device__ inline MapLds stage_map(const MapDev& m, unsigned char* lds) {
   MapLds r;
   r.curves = cv;
   r.headings = hd;
+  r.obj = ob;
+  r.spawn_obj = so;
   r.curve_start = cs;
   r.kind = kd;
   r.drivable = dv;
   r.width = m.width;
   r.height = m.height;
   r.n_drivable = m.n_drivable;
+  r.n_obj = m.n_obj;
+  r.n_spawn_obj = m.n_spawn_obj;
   return r;
 }
 
@@ -152,6 +166,7 @@ struct Geo {  // constants hoisted per launch
   double ts, inv_ts, wheel_dist, dt, off, robot_width, front, rad2deg, two_pi, accept_deg,
       reset_safety;
   double robot_speed;
+  double robot_length, agent_safety_rad;   // objects: agent box and safety circle
 };
 
 // floor(v / ts) exactly as numpy computes it (correctly rounded division, then
@@ -178,7 +193,105 @@ __device__ inline bool drivable(const MapLds& M, const Geo& g, double x, double 
   return t >= 0 && M.kind[t] > 0;
 }
 
-// _valid_pose with precomputed (c, s) = (cos, sin)(angle) (A6)
+// ---- static objects [upstream collision.py; §8f-3] ---------------------------------
+// _collision(get_agent_corners(centre, angle)): separating-axis test of the
+// agent's box (ROBOT_WIDTH x ROBOT_LENGTH about the actual centre (px, pz))
+// against every collidable object's box.  Axes: the agent's forward / right
+// vectors (upstream: generate_norm's eigenvectors of the box, the same axes)
+// and each object's two precomputed norms; boxes overlap on an axis when their
+// closed projection intervals meet, and collide when they overlap on all four.
+__device__ inline bool collide(const MapLds& M, const Geo& g, double px, double pz, double c,
+                               double s) {
+  if (M.n_obj == 0) return false;
+  const double fx = c, fz = -s, rx = s, rz = c;   // get_dir_vec, get_right_vec
+  const double hw = g.robot_width * 0.5, hl = g.robot_length * 0.5;
+  double ax[4], az[4];   // agent_boundbox corner order
+  ax[0] = (px - hw * rx) - hl * fx;
+  az[0] = (pz - hw * rz) - hl * fz;
+  ax[1] = (px + hw * rx) - hl * fx;
+  az[1] = (pz + hw * rz) - hl * fz;
+  ax[2] = (px + hw * rx) + hl * fx;
+  az[2] = (pz + hw * rz) + hl * fz;
+  ax[3] = (px - hw * rx) + hl * fx;
+  az[3] = (pz - hw * rz) + hl * fz;
+  double amin[2], amax[2];   // the agent on its own axes
+#pragma unroll
+  for (int a = 0; a < 2; ++a) {
+    const double nx = a == 0 ? fx : rx, nz = a == 0 ? fz : rz;
+    double lo = ax[0] * nx + az[0] * nz, hi = lo;
+#pragma unroll
+    for (int k = 1; k < 4; ++k) {
+      const double p = ax[k] * nx + az[k] * nz;
+      lo = p < lo ? p : lo;
+      hi = p > hi ? p : hi;
+    }
+    amin[a] = lo;
+    amax[a] = hi;
+  }
+  for (int o = 0; o < M.n_obj; ++o) {
+    const double* ob = M.obj + (size_t)o * DT_OBJ_STRIDE;
+    bool sep = false;
+    // the object's corners on the agent's axes
+#pragma unroll
+    for (int a = 0; a < 2 && !sep; ++a) {
+      const double nx = a == 0 ? fx : rx, nz = a == 0 ? fz : rz;
+      double lo = ob[DT_OBJ_CORNERS] * nx + ob[DT_OBJ_CORNERS + 1] * nz, hi = lo;
+#pragma unroll
+      for (int k = 1; k < 4; ++k) {
+        const double p = ob[DT_OBJ_CORNERS + 2 * k] * nx + ob[DT_OBJ_CORNERS + 2 * k + 1] * nz;
+        lo = p < lo ? p : lo;
+        hi = p > hi ? p : hi;
+      }
+      sep = amax[a] < lo || hi < amin[a];
+    }
+    // the agent's corners on the object's axes
+#pragma unroll
+    for (int a = 0; a < 2 && !sep; ++a) {
+      const double nx = ob[DT_OBJ_NORMS + 2 * a], nz = ob[DT_OBJ_NORMS + 2 * a + 1];
+      double lo = ax[0] * nx + az[0] * nz, hi = lo;
+#pragma unroll
+      for (int k = 1; k < 4; ++k) {
+        const double p = ax[k] * nx + az[k] * nz;
+        lo = p < lo ? p : lo;
+        hi = p > hi ? p : hi;
+      }
+      sep = hi < ob[DT_OBJ_PROJ + 2 * a] || ob[DT_OBJ_PROJ + 2 * a + 1] < lo;
+    }
+    if (!sep) return true;
+  }
+  return false;
+}
+
+// proximity_penalty2 at the actual centre: the sum of the negative
+// (|c_o - p| - AGENT_SAFETY_RAD - r_o) over the collidable objects
+// (safety_circle_overlap; 0 when no safety circle meets the agent's)
+__device__ inline double proximity_penalty(const MapLds& M, const Geo& g, double px, double pz) {
+  double pen = 0.0;
+  for (int o = 0; o < M.n_obj; ++o) {
+    const double* ob = M.obj + (size_t)o * DT_OBJ_STRIDE;
+    const double dx = ob[DT_OBJ_CENTER] - px, dy = ob[DT_OBJ_CENTER + 1] - 0.0,
+                 dz = ob[DT_OBJ_CENTER + 2] - pz;
+    const double d = sqrt((dx * dx + dy * dy) + dz * dz);
+    const double sc = (d - g.agent_safety_rad) - ob[DT_OBJ_SAFETY_RAD];
+    if (sc < 0.0) pen = pen + sc;
+  }
+  return pen;
+}
+
+// _inconvenient_spawn(propose_pos): within max(max_coords) * 0.5 * scale +
+// MIN_SPAWN_OBJ_DIST (precomputed radius) of any object's position
+__device__ inline bool inconvenient_spawn(const MapLds& M, double x, double z) {
+  for (int o = 0; o < M.n_spawn_obj; ++o) {
+    const double* so = M.spawn_obj + 4 * (size_t)o;
+    const double dx = so[0] - x, dy = so[1] - 0.0, dz = so[2] - z;
+    if (sqrt((dx * dx + dy * dy) + dz * dz) < so[3]) return true;
+  }
+  return false;
+}
+
+// _valid_pose with precomputed (c, s) = (cos, sin)(angle) (A6): the centre and
+// both wheels and the front drivable (scaled by safety) and no collision (the
+// unscaled agent box)
 __device__ inline bool valid_pose(const MapLds& M, const Geo& g, double x, double z, double c,
                                   double s, double safety) {
   const double px = x + g.off * c;
@@ -189,7 +302,7 @@ __device__ inline bool valid_pose(const MapLds& M, const Geo& g, double x, doubl
   ok = ok && drivable(M, g, px - kw * s, pz - kw * c);
   ok = ok && drivable(M, g, px + kw * s, pz + kw * c);
   ok = ok && drivable(M, g, px + kf * c, pz + kf * (-s));
-  return ok;
+  return ok && !collide(M, g, px, pz, c, s);
 }
 
 // bezier_point (A9): coefficients are exact dyadics for the bisection's t values
@@ -320,6 +433,7 @@ __device__ inline bool spawn_try(const MapLds& M, const Geo& g, uint32_t k0, uin
   ox = px;
   oz = pz;
   oa = pa;
+  if (inconvenient_spawn(M, px, pz)) return false;
   if (!valid_pose(M, g, px, pz, c, s, g.reset_safety)) return false;
   double lp[4];
   if (!lane_pos(M, g, px, pz, c, s, lp)) return false;

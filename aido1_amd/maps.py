@@ -14,6 +14,19 @@ expressions, so the control points are the reference's.
 
 Curves are stored compactly for the C ABI (dt_map): tile t owns curves
 curve_start[t] .. curve_start[t+1]-1 of ``curves`` [C,4,3] / ``headings`` [C,3].
+
+Static objects follow upstream Simulator._load_objects and
+collision.py: world position = tile_size * (x, y, z), scale = height /
+mesh max y, footprint corners = the mesh's x/z box scaled, offset to the
+position and rotated about it by `rotate` degrees (rotate_point), axes =
+generate_norm (eigenvectors of the corners' covariance -- for a square
+footprint that is the world x/z axes whatever the rotation, as upstream),
+safety radius = SAFETY_RAD_MULT * hypot(max |x|, max |z|) * scale.  An object
+is collidable (checked by _collision / proximity_penalty2) when it is static,
+not a traffic light, and its box meets a drivable tile (_collidable_object);
+every object counts for _inconvenient_spawn.  The meshes are not in this
+container, so the per-kind boxes below are assumptions (override them per
+object with ``mesh_min`` / ``mesh_max``).
 """
 import math
 import os
@@ -23,6 +36,24 @@ import numpy as np
 import yaml
 
 MAP_DIR = os.path.join(os.path.dirname(os.path.abspath(__file__)), 'maps')
+
+SAFETY_RAD_MULT = 1.8
+MIN_SPAWN_OBJ_DIST = 0.25
+# mesh bounding boxes (min, max) in mesh units, y up -- ASSUMED (the upstream
+# .obj meshes are absent); with `height` only their proportions matter
+MESH_EXTENTS = {
+    'duckie': ((-0.5, 0.0, -0.4), (0.5, 1.0, 0.4)),
+    'cone': ((-0.35, 0.0, -0.35), (0.35, 1.0, 0.35)),
+    'barrier': ((-1.0, 0.0, -0.2), (1.0, 1.0, 0.2)),
+    'duckiebot': ((-0.6, 0.0, -0.45), (0.6, 1.0, 0.45)),
+    'truck': ((-1.2, 0.0, -0.5), (1.2, 1.0, 0.5)),
+    'bus': ((-1.5, 0.0, -0.5), (1.5, 1.0, 0.5)),
+    'house': ((-0.6, 0.0, -0.5), (0.6, 1.0, 0.5)),
+    'building': ((-0.6, 0.0, -0.6), (0.6, 1.0, 0.6)),
+    'tree': ((-0.4, 0.0, -0.4), (0.4, 1.0, 0.4)),
+    'trafficlight': ((-0.1, 0.0, -0.1), (0.1, 1.0, 0.1)),
+    'sign': ((-0.15, 0.0, -0.02), (0.15, 1.0, 0.02)),
+}
 
 TILE_EMPTY, TILE_OFFROAD, TILE_STRAIGHT, TILE_CURVE_LEFT, TILE_CURVE_RIGHT = -1, 0, 1, 2, 3
 TILE_3WAY_LEFT, TILE_3WAY_RIGHT, TILE_4WAY = 4, 5, 6
@@ -76,6 +107,120 @@ def rotation_y(angle):
     ])
 
 
+# ---- static objects: upstream collision.py restated -----------------------------------
+def rotate_point(px, py, cx, cy, theta):
+    """Rotate (px, py) about (cx, cy) by theta (upstream graphics/collision)."""
+    dx = px - cx
+    dy = py - cy
+    new_dx = dx * math.cos(theta) + dy * math.sin(theta)
+    new_dy = dy * math.cos(theta) - dx * math.sin(theta)
+    return cx + new_dx, cy + new_dy
+
+
+def generate_corners(pos, min_coords, max_coords, theta, scale):
+    """Footprint corners [4, 2] (x, z) of an object at world `pos`."""
+    px, pz = pos[0], pos[-1]
+    return np.array([
+        rotate_point(min_coords[0] * scale + px, min_coords[-1] * scale + pz, px, pz, theta),
+        rotate_point(max_coords[0] * scale + px, min_coords[-1] * scale + pz, px, pz, theta),
+        rotate_point(max_coords[0] * scale + px, max_coords[-1] * scale + pz, px, pz, theta),
+        rotate_point(min_coords[0] * scale + px, max_coords[-1] * scale + pz, px, pz, theta),
+    ])
+
+
+def generate_norm(corners):
+    """The box's two axes (rows, unit): eigenvectors of the corners' covariance."""
+    ca = np.cov(corners, y=None, rowvar=False, bias=True)
+    _, vect = np.linalg.eig(ca)
+    return np.ascontiguousarray(vect.T.real)
+
+
+def _proj(corners, axis):
+    p = corners @ axis
+    return p.min(), p.max()
+
+
+def sat_intersects(c1, n1, c2, n2):
+    """Separating-axis test of two boxes (corners [4,2], axes [2,2]): no axis of
+    either separates their closed projection intervals."""
+    for axis in np.concatenate([n1, n2]):
+        a0, a1 = _proj(c1, axis)
+        b0, b1 = _proj(c2, axis)
+        if a1 < b0 or b1 < a0:
+            return False
+    return True
+
+
+def tile_corners(i, j, width):
+    px, pz = i * width, j * width
+    return np.array([[px, pz], [px + width, pz], [px + width, pz + width], [px, pz + width]])
+
+
+def find_candidate_tiles(corners, tile_size):
+    mn = np.floor(np.amin(corners, axis=0) / tile_size).astype(int)
+    mx = np.floor(np.amax(corners, axis=0) / tile_size).astype(int)
+    return [(x, y) for x in range(mn[0], mx[0] + 1) for y in range(mn[1], mx[1] + 1)]
+
+
+@dataclass
+class MapObject:
+    kind: str
+    pos: np.ndarray            # world (x, y, z)
+    rotate: float              # degrees
+    scale: float
+    min_coords: np.ndarray
+    max_coords: np.ndarray
+    static: bool
+    corners: np.ndarray        # [4, 2]
+    norms: np.ndarray          # [2, 2]
+    safety_radius: float
+    collidable: bool = False
+
+    @property
+    def spawn_radius(self):
+        """_inconvenient_spawn: max(max_coords) * 0.5 * scale + MIN_SPAWN_OBJ_DIST."""
+        return float(np.max(self.max_coords)) * 0.5 * self.scale + MIN_SPAWN_OBJ_DIST
+
+    def record(self):
+        """The DT_OBJ_STRIDE doubles of include/dtsim.h for this object."""
+        r = np.zeros(20, np.float64)
+        r[0:3] = self.pos
+        r[3] = self.safety_radius
+        r[4:12] = self.corners.reshape(-1)
+        r[12:16] = self.norms.reshape(-1)
+        for a in range(2):
+            r[16 + 2 * a:18 + 2 * a] = _proj(self.corners, self.norms[a])
+        return r
+
+
+def parse_object(desc, tile_size):
+    kind = desc['kind']
+    pos = desc['pos']
+    x, z = pos[0:2]
+    y = pos[2] if len(pos) == 3 else 0.0
+    world = tile_size * np.array((x, y, z), np.float64)
+    if 'mesh_min' in desc or 'mesh_max' in desc:
+        mn, mx = desc['mesh_min'], desc['mesh_max']
+    elif kind in MESH_EXTENTS or kind.startswith('sign'):
+        mn, mx = MESH_EXTENTS[kind if kind in MESH_EXTENTS else 'sign']
+    else:
+        raise ValueError('object kind %r has no known extents: give mesh_min / mesh_max' % kind)
+    mn = np.array(mn, np.float64)
+    mx = np.array(mx, np.float64)
+    if 'height' in desc and 'scale' in desc:
+        raise ValueError('cannot specify both height and scale')
+    scale = desc['height'] / mx[1] if 'height' in desc else float(desc.get('scale', 1.0))
+    static = bool(desc.get('static', True))
+    if not static:
+        raise NotImplementedError('dynamic (non-static) objects are not supported')
+    rotate = float(desc.get('rotate', 0.0))
+    corners = generate_corners(world, mn, mx, np.radians(rotate), scale)
+    ext = np.max([np.abs(mn), np.abs(mx)], axis=0)
+    safety = SAFETY_RAD_MULT * (np.hypot(ext[0], ext[2]) * scale)
+    return MapObject(kind, world, rotate, scale, mn, mx, static, corners,
+                     generate_norm(corners), float(safety))
+
+
 @dataclass
 class TileMap:
     name: str
@@ -88,9 +233,22 @@ class TileMap:
     headings: np.ndarray     # [C, 3] float64
     curve_start: np.ndarray  # [H*W + 1] int32
     rows: list
+    objects: list = None     # [MapObject]
 
     def tile_curves(self, t):
         return self.curves[self.curve_start[t]:self.curve_start[t + 1]]
+
+    @property
+    def object_table(self):
+        """[K, 20] float64 records of the collidable objects (dt_map.objects)."""
+        recs = [o.record() for o in (self.objects or []) if o.collidable]
+        return np.array(recs, np.float64).reshape(-1, 20)
+
+    @property
+    def spawn_table(self):
+        """[M, 4] float64 (x, y, z, radius) of every object (dt_map.spawn_objects)."""
+        recs = [np.r_[o.pos, o.spawn_radius] for o in (self.objects or [])]
+        return np.array(recs, np.float64).reshape(-1, 4)
 
     @property
     def drivable(self):
@@ -113,7 +271,7 @@ def tile_curves(kind, orient, i, j, tile_size):
     return pts
 
 
-def parse_rows(rows, name='custom', tile_size=0.61):
+def parse_rows(rows, name='custom', tile_size=0.61, objects=()):
     H, W = len(rows), len(rows[0])
     kind = np.full(H * W, TILE_EMPTY, np.int8)
     orient = np.zeros(H * W, np.int8)
@@ -152,8 +310,18 @@ def parse_rows(rows, name='custom', tile_size=0.61):
         curves[a:b] = pts
         h = pts[:, -1, :] - pts[:, 0, :]          # closest_curve_point: one Frobenius norm
         headings[a:b] = h / np.linalg.norm(h).reshape(1, -1)
+    objs = [parse_object(d, tile_size) for d in objects]
+    for o in objs:   # _collidable_object: static, not a traffic light, meets a drivable tile
+        if o.kind == 'trafficlight':
+            continue
+        for (ti, tj) in find_candidate_tiles(o.corners, tile_size):
+            if 0 <= ti < W and 0 <= tj < H and kind[tj * W + ti] > 0 and sat_intersects(
+                    o.corners, o.norms, tile_corners(ti, tj, tile_size),
+                    np.array([[1.0, 0.0], [0.0, 1.0]])):
+                o.collidable = True
+                break
     return TileMap(name, W, H, tile_size, kind, orient, curves, headings, curve_start,
-                   [list(r) for r in rows])
+                   [list(r) for r in rows], objs)
 
 
 def load_map(name_or_path, tile_size=0.61):
@@ -162,11 +330,11 @@ def load_map(name_or_path, tile_size=0.61):
         path = os.path.join(MAP_DIR, name_or_path + '.yaml')
     with open(path) as f:
         doc = yaml.safe_load(f)
-    if doc.get('objects'):
-        raise NotImplementedError('maps with objects (collision / proximity penalty) are '
-                                  'SURVEY §8f item 3')
+    objects = doc.get('objects') or []
+    if isinstance(objects, dict):   # newer map format: named objects
+        objects = list(objects.values())
     name = os.path.splitext(os.path.basename(path))[0]
-    return parse_rows(doc['tiles'], name, tile_size)
+    return parse_rows(doc['tiles'], name, tile_size, objects)
 
 
 def available_maps():

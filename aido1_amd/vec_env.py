@@ -72,11 +72,16 @@ class VecEnv:
         self._curves = np.ascontiguousarray(self.map.curves, np.float64)
         self._headings = np.ascontiguousarray(self.map.headings, np.float64)
         self._curve_start = np.ascontiguousarray(self.map.curve_start, np.int32)
+        self._objects = np.ascontiguousarray(self.map.object_table, np.float64)
+        self._spawn_objects = np.ascontiguousarray(self.map.spawn_table, np.float64)
         m = _lib.DtMap(self.map.width, self.map.height,
                        self._kind.ctypes.data_as(ctypes.c_void_p),
                        self._curve_start.ctypes.data_as(ctypes.c_void_p),
                        self._curves.ctypes.data_as(ctypes.c_void_p),
-                       self._headings.ctypes.data_as(ctypes.c_void_p))
+                       self._headings.ctypes.data_as(ctypes.c_void_p),
+                       len(self._objects), self._objects.ctypes.data_as(ctypes.c_void_p),
+                       len(self._spawn_objects),
+                       self._spawn_objects.ctypes.data_as(ctypes.c_void_p))
         h = ctypes.c_void_p()
         rc = self._L.dt_create(ctypes.byref(cfg), ctypes.byref(m), ctypes.c_uint64(seed),
                                self.n, device, ctypes.byref(h))

@@ -29,7 +29,8 @@
 extern "C" {
 #endif
 
-#define DT_ABI_VERSION 2  /* 2: dt_map curves per tile vary (curve_start), intersections */
+#define DT_ABI_VERSION 3  /* 2: curves per tile vary (curve_start), intersections;
+                             3: static objects in dt_map, safety_rad_mult */
 
 /* error codes */
 #define DT_OK 0
@@ -83,7 +84,24 @@ typedef struct dt_config {
   int32_t reward_speed_measured; /* 0: compute_reward(.., self.robot_speed); 1: measured |dpos|/dt */
   int32_t front_probe_length; /* 1: _valid_pose front probe uses ROBOT_LENGTH, 0: ROBOT_WIDTH */
   int32_t auto_reset;         /* 1: dt_step resets done envs in the same launch (VectorEnv) */
+  double safety_rad_mult;     /* SAFETY_RAD_MULT 1.8: AGENT_SAFETY_RAD =
+                                 max(robot_length, robot_width) / 2 * it (objects) */
 } dt_config;
+
+/* One collidable static object of dt_map.objects: DT_OBJ_STRIDE doubles
+ * (upstream Simulator._load_objects -> collidable_centers / _corners / _norms /
+ * _safety_radii, precomputed on the host by aido1_amd/maps.py):
+ *   [DT_OBJ_CENTER + 0..2]  world position (x, y, z)
+ *   [DT_OBJ_SAFETY_RAD]     safety radius (SAFETY_RAD_MULT * calculate_safety_radius)
+ *   [DT_OBJ_CORNERS + 2k]   corner k (x, z), k = 0..3 (generate_corners)
+ *   [DT_OBJ_NORMS + 2a]     axis a (x, z), a = 0, 1 (generate_norm)
+ *   [DT_OBJ_PROJ + 2a]      (min, max) of the corners projected on axis a */
+#define DT_OBJ_CENTER 0
+#define DT_OBJ_SAFETY_RAD 3
+#define DT_OBJ_CORNERS 4
+#define DT_OBJ_NORMS 12
+#define DT_OBJ_PROJ 16
+#define DT_OBJ_STRIDE 20
 
 /* A tile map.  Tile (i, j) is grid[j * width + i]; i follows +x, j follows +z
  * (upstream get_grid_coords / _get_tile). */
@@ -100,6 +118,12 @@ typedef struct dt_map {
   const double* headings;       /* host [C, 3] curve headings (P3 - P0) divided by the
                                    Frobenius norm of the tile's heading matrix (the
                                    closest_curve_point np.linalg.norm quirk) */
+  int32_t n_objects;            /* collidable static objects (0: none; <= 256) */
+  const double* objects;        /* host [n_objects, DT_OBJ_STRIDE] or NULL: _collision in
+                                   _valid_pose, proximity_penalty2 in the reward */
+  int32_t n_spawn_objects;      /* visible objects for _inconvenient_spawn (<= 256) */
+  const double* spawn_objects;  /* host [n_spawn_objects, 4] or NULL: (x, y, z, r): a
+                                   spawn proposal within r of (x, y, z) is rejected */
 } dt_map;
 
 typedef struct dt_handle dt_handle;

@@ -48,6 +48,8 @@ void oracle_philox(const uint32_t ctr[4], const uint32_t key[2], uint32_t out[4]
   memcpy(out, c, sizeof c);
 }
 
+static double norm3_(double a, double b, double c) { return sqrt((a * a + b * b) + c * c); }
+
 /* ---- map helpers (A5) ---------------------------------------------------- */
 typedef struct {
   const dt_config* cfg;
@@ -66,6 +68,76 @@ static int drivable(const ctx_t* C, double x, double z) {
   return t >= 0 && C->map->kind[t] > 0;
 }
 
+/* ---- static objects (dtsim_ref.py _collision /
+ * proximity_penalty2 / _inconvenient_spawn over the DT_OBJ_* records) ------- */
+static void proj4(const double* xs, const double* zs, int stride, double nx, double nz,
+                  double* lo, double* hi) {
+  double l = xs[0] * nx + zs[0] * nz, h = l;
+  for (int k = 1; k < 4; ++k) {
+    double p = xs[k * stride] * nx + zs[k * stride] * nz;
+    if (p < l) l = p;
+    if (p > h) h = p;
+  }
+  *lo = l;
+  *hi = h;
+}
+
+/* agent box at the actual centre (px, pz) vs every collidable object, by
+ * separating axes (agent axes: dir / right) */
+static int collide(const ctx_t* C, double px, double pz, double c, double s) {
+  const dt_map* m = C->map;
+  if (m->n_objects <= 0) return 0;
+  double fx = c, fz = -s, rx = s, rz = c;
+  double hw = C->cfg->robot_width * 0.5, hl = C->cfg->robot_length * 0.5;
+  double ax[4], az[4];
+  ax[0] = (px - hw * rx) - hl * fx; az[0] = (pz - hw * rz) - hl * fz;
+  ax[1] = (px + hw * rx) - hl * fx; az[1] = (pz + hw * rz) - hl * fz;
+  ax[2] = (px + hw * rx) + hl * fx; az[2] = (pz + hw * rz) + hl * fz;
+  ax[3] = (px - hw * rx) + hl * fx; az[3] = (pz - hw * rz) + hl * fz;
+  for (int o = 0; o < m->n_objects; ++o) {
+    const double* ob = m->objects + (size_t)o * DT_OBJ_STRIDE;
+    const double* cx = ob + DT_OBJ_CORNERS;
+    int sep = 0;
+    for (int a = 0; a < 2 && !sep; ++a) {
+      double nx = a == 0 ? fx : rx, nz = a == 0 ? fz : rz, al, ah, bl, bh;
+      proj4(ax, az, 1, nx, nz, &al, &ah);
+      proj4(cx, cx + 1, 2, nx, nz, &bl, &bh);
+      sep = ah < bl || bh < al;
+    }
+    for (int a = 0; a < 2 && !sep; ++a) {
+      double nx = ob[DT_OBJ_NORMS + 2 * a], nz = ob[DT_OBJ_NORMS + 2 * a + 1], al, ah;
+      proj4(ax, az, 1, nx, nz, &al, &ah);
+      sep = ah < ob[DT_OBJ_PROJ + 2 * a] || ob[DT_OBJ_PROJ + 2 * a + 1] < al;
+    }
+    if (!sep) return 1;
+  }
+  return 0;
+}
+
+static double proximity(const ctx_t* C, double px, double pz) {
+  const dt_map* m = C->map;
+  const dt_config* g = C->cfg;
+  double asr = ((g->robot_length > g->robot_width ? g->robot_length : g->robot_width) / 2) *
+               g->safety_rad_mult;
+  double pen = 0.0;
+  for (int o = 0; o < m->n_objects; ++o) {
+    const double* ob = m->objects + (size_t)o * DT_OBJ_STRIDE;
+    double d = norm3_(ob[0] - px, ob[1] - 0.0, ob[2] - pz);
+    double sc = (d - asr) - ob[DT_OBJ_SAFETY_RAD];
+    if (sc < 0) pen = pen + sc;
+  }
+  return pen;
+}
+
+static int inconvenient(const ctx_t* C, double x, double z) {
+  const dt_map* m = C->map;
+  for (int o = 0; o < m->n_spawn_objects; ++o) {
+    const double* so = m->spawn_objects + 4 * (size_t)o;
+    if (norm3_(so[0] - x, so[1] - 0.0, so[2] - z) < so[3]) return 1;
+  }
+  return 0;
+}
+
 /* _valid_pose (A6) */
 static int valid_pose(const ctx_t* C, double x, double z, double angle, double safety) {
   const dt_config* g = C->cfg;
@@ -79,7 +151,7 @@ static int valid_pose(const ctx_t* C, double x, double z, double angle, double s
   if (!drivable(C, px - kw * s, pz - kw * c)) return 0;
   if (!drivable(C, px + kw * s, pz + kw * c)) return 0;
   if (!drivable(C, px + kf * c, pz + kf * (-s))) return 0;
-  return 1;
+  return !collide(C, px, pz, c, s);
 }
 
 /* bezier_point (A9) with exact dyadic coefficients */
@@ -222,6 +294,7 @@ static int spawn(const ctx_t* C, uint64_t seed, uint32_t env, uint32_t episode, 
     double px = (fi + u01(a[0], a[1])) * g->road_tile_size;
     double pz = (fj + u01(a[2], a[3])) * g->road_tile_size;
     double pa = g->two_pi * u01(b[0], b[1]);
+    if (inconvenient(C, px, pz)) continue;
     if (!valid_pose(C, px, pz, pa, g->reset_safety)) continue;
     double lp[4];
     if (!lane_pos(C, px, pz, pa, lp)) continue;
@@ -286,11 +359,15 @@ int oracle_step(const dt_config* cfg, const dt_map* map, int n, uint32_t env_bas
       } else {
         double lp[4];
         double sp = cfg->reward_speed_measured ? speed : cfg->robot_speed;
+        double off = cfg->camera_forward_dist - (cfg->robot_length / 2);
+        double pen = map->n_objects > 0 ? proximity(&C, x[e] + off * cos(angle[e]),
+                                                     z[e] + off * (-sin(angle[e])))
+                                         : 0.0;
         if (lane_pos(&C, x[e], z[e], angle[e], lp)) {
           double ad = lp[0] < 0 ? -lp[0] : lp[0];
-          r = ((1.0 * sp) * lp[1] + (-10) * ad) + 40 * 0.0;
+          r = ((1.0 * sp) * lp[1] + (-10) * ad) + 40 * pen;
         } else {
-          r = 40 * 0.0;
+          r = 40 * pen;
         }
       }
       double rm = (r == -1000) ? -10 : (r > 0 ? r + 10 : r + 4);

@@ -34,7 +34,8 @@ class _Cfg(ctypes.Structure):
         [(n, ctypes.c_uint32) for n in ('max_steps', 'max_env_steps', 'max_spawn_attempts')] + \
         [(n, ctypes.c_int32) for n in ('repeat_actions', 'frame_skip', 'action_mode',
                                        'clip_action', 'reward_speed_measured',
-                                       'front_probe_length', 'auto_reset')]
+                                       'front_probe_length', 'auto_reset')] + \
+        [('safety_rad_mult', ctypes.c_double)]
 
 
 class _LineParams(ctypes.Structure):
@@ -47,7 +48,9 @@ class _LineParams(ctypes.Structure):
 class _Map(ctypes.Structure):
     _fields_ = [('width', ctypes.c_int32), ('height', ctypes.c_int32),
                 ('kind', ctypes.c_void_p), ('curve_start', ctypes.c_void_p),
-                ('curves', ctypes.c_void_p), ('headings', ctypes.c_void_p)]
+                ('curves', ctypes.c_void_p), ('headings', ctypes.c_void_p),
+                ('n_objects', ctypes.c_int32), ('objects', ctypes.c_void_p),
+                ('n_spawn_objects', ctypes.c_int32), ('spawn_objects', ctypes.c_void_p)]
 
 
 _MODES = {'wheels': 0, 'tanh': 1, 'steering': 2}
@@ -79,14 +82,15 @@ def make_cfg(sc: 'R.SimConfig', auto_reset=True):
     c.reward_speed_measured = int(sc.reward_speed_measured)
     c.front_probe_length = int(sc.front_probe_length)
     c.auto_reset = int(auto_reset)
+    c.safety_rad_mult = R.SAFETY_RAD_MULT
     return c
 
 
 class OracleMap:
     """Map arrays built by the oracle's own MapRef (restated _load_map/_get_curve)."""
 
-    def __init__(self, rows, road_tile_size=R.ROAD_TILE_SIZE):
-        m = R.MapRef(rows, road_tile_size)
+    def __init__(self, rows, road_tile_size=R.ROAD_TILE_SIZE, objects=()):
+        m = R.MapRef(rows, road_tile_size, objects)
         T = m.grid_width * m.grid_height
         self.width, self.height = m.grid_width, m.grid_height
         self.kind = np.full(T, -1, np.int8)
@@ -109,8 +113,27 @@ class OracleMap:
                 a, b = self.curve_start[t], self.curve_start[t + 1]
                 self.curves[a:b] = cv
                 self.headings[a:b] = R.tile_headings(cv)
+        # objects in the ABI layout (include/dtsim.h DT_OBJ_*), from the oracle's MapRef
+        recs = []
+        for pos, c, nv, r in zip(m.collidable_centers, m.collidable_corners,
+                                 m.collidable_norms, m.collidable_safety_radii):
+            rec = np.zeros(20)
+            rec[0:3] = pos
+            rec[3] = r
+            rec[4:12] = np.asarray(c).reshape(-1)
+            rec[12:16] = np.asarray(nv).reshape(-1)
+            for a in range(2):
+                p = np.asarray(c) @ np.asarray(nv)[a]
+                rec[16 + 2 * a], rec[17 + 2 * a] = p.min(), p.max()
+            recs.append(rec)
+        self.objects = np.ascontiguousarray(np.array(recs).reshape(-1, 20))
+        self.spawn_objects = np.ascontiguousarray(np.array(
+            [np.r_[o['pos'], max(o['max_coords']) * 0.5 * o['scale'] + R.MIN_SPAWN_OBJ_DIST]
+             for o in m.objects]).reshape(-1, 4))
         self.c = _Map(self.width, self.height, self.kind.ctypes.data, self.curve_start.ctypes.data,
-                      self.curves.ctypes.data, self.headings.ctypes.data)
+                      self.curves.ctypes.data, self.headings.ctypes.data,
+                      len(self.objects), self.objects.ctypes.data,
+                      len(self.spawn_objects), self.spawn_objects.ctypes.data)
 
 
 def _p(a):
@@ -120,7 +143,8 @@ def _p(a):
 class OracleBatch:
     """N envs stepped by the C oracle with the product's batch semantics."""
 
-    def __init__(self, rows, n, seed=123, sim_config=None, auto_reset=True, env_base=0):
+    def __init__(self, rows, n, seed=123, sim_config=None, auto_reset=True, env_base=0,
+                 objects=()):
         if not os.path.exists(SO) or os.path.getmtime(SO) < max(
                 os.path.getmtime(os.path.join(HERE, f)) for f in os.listdir(HERE)
                 if f.endswith('.c')):
@@ -128,7 +152,7 @@ class OracleBatch:
         self.L = ctypes.CDLL(SO)
         self.sc = sim_config or R.SimConfig()
         self.cfg = make_cfg(self.sc, auto_reset)
-        self.map = OracleMap(rows, self.sc.road_tile_size)
+        self.map = OracleMap(rows, self.sc.road_tile_size, objects)
         self.n = n
         self.env_base = env_base
         self.seed = np.full(n, seed, np.uint64)

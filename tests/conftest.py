@@ -30,6 +30,13 @@ def map_rows(name):
         return yaml.safe_load(f)['tiles']
 
 
+def map_objects(name):
+    """The map file's `objects` list (static objects)."""
+    import yaml
+    with open(os.path.join(REPO, 'aido1_amd', 'maps', name + '.yaml')) as f:
+        return yaml.safe_load(f).get('objects') or []
+
+
 @pytest.fixture(scope='session')
 def gpu():
     import torch

@@ -9,7 +9,7 @@ import numpy as np
 import pytest
 import torch
 
-from conftest import golden, map_rows
+from conftest import golden, map_objects, map_rows
 from oracle import dtsim_ref as R
 from oracle import oracle_c as OC
 
@@ -27,7 +27,8 @@ def make_pair(n, map_name='loop_empty', seed=1234, env_base=0, **cfg_kw):
     sc_kw = {k: v for k, v in cfg_kw.items() if k in R.SimConfig().__dict__}
     sc = R.SimConfig(**sc_kw)
     ob = OC.OracleBatch(map_rows(map_name), n, seed=seed, sim_config=sc,
-                        auto_reset=ec.auto_reset, env_base=env_base)
+                        auto_reset=ec.auto_reset, env_base=env_base,
+                        objects=map_objects(map_name))
     return env, ob
 
 
@@ -89,6 +90,7 @@ def test_reset_properties_full_size(gpu):
     ('zigzag', 'steering', 4096, 40),
     ('small_loop', 'wheels', 65, 100),
     ('intersections', 'wheels', 4096, 60),   # 3-way / 4-way tiles
+    ('loop_obstacles', 'wheels', 4096, 80),  # static objects
 ])
 def test_step_parity(gpu, map_name, mode, n, steps):
     env, ob = make_pair(n, map_name=map_name, action_mode=mode)

@@ -11,7 +11,7 @@ import math
 import numpy as np
 import pytest
 
-from conftest import golden, map_rows
+from conftest import golden, map_objects, map_rows
 from oracle import dtsim_ref as R
 from oracle import oracle_c as OC
 from oracle import philox_ref as P
@@ -202,13 +202,16 @@ def test_golden_env_wrapper_on_c_oracle():
 # ---- C restatement == numpy restatement ---------------------------------------
 @pytest.mark.parametrize('map_name,mode', [('loop_empty', 'wheels'), ('zigzag', 'tanh'),
                                            ('small_loop', 'steering'),
-                                           ('intersections', 'wheels')])
+                                           ('intersections', 'wheels'),
+                                           ('loop_obstacles', 'wheels')])
 def test_c_oracle_matches_numpy(map_name, mode):
     rows = map_rows(map_name)
+    objs = map_objects(map_name)
     n = 12
     sc = R.SimConfig(action_mode=mode, max_env_steps=60)
-    ob = OC.OracleBatch(rows, n, seed=99, sim_config=sc)
-    envs = [R.EnvironmentWrapperRef(R.SimulatorRef(rows, seed=99, env_id=i, cfg=sc))
+    ob = OC.OracleBatch(rows, n, seed=99, sim_config=sc, objects=objs)
+    envs = [R.EnvironmentWrapperRef(R.SimulatorRef(rows, seed=99, env_id=i, cfg=sc,
+                                                   objects=objs))
             for i in range(n)]
     ob.reset()
     for e in envs:
