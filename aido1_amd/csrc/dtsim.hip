@@ -50,6 +50,54 @@ __device__ inline void map_action(int mode, float a0, float a1, double& vl, doub
   }
 }
 
+// Spawn-ahead refill of env e (every thread of a 64-thread block; A13): make
+// the slots of keys want-1 and want hold their reset poses.  Race-free against
+// a dt_step lane of the same launch: that lane reads slot (key & 1) of its
+// episode counter k, then (after a fence) raises want to k + 2; this block only
+// writes slots of keys it reads as missing among {want-1, want}, which are
+// never k's while the lane may still read it.
+__device__ void refill_env(const dt::State& st, const dt::MapDev& md, const dt::Geo& g, int n,
+                           uint32_t max_attempts, uint32_t env_base, int e, unsigned char* lds) {
+  if (e >= n) return;
+  const uint32_t w = __hip_atomic_load(st.want + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  bool need[2];
+  uint32_t key[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    key[i] = w - 1u + (uint32_t)i;
+    const uint32_t have = __hip_atomic_load(st.pre_key + (size_t)(key[i] & 1u) * n + e,
+                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    need[i] = (i == 1 || w > 0u) && (have & ~dt::kKeyFailed) != key[i];
+  }
+  if (!need[0] && !need[1]) return;  // block-uniform
+  const MapLds M = dt::stage_map(md, lds);
+  const uint64_t seed = st.seed[e];
+  for (int i = 0; i < 2; ++i) {
+    if (!need[i]) continue;
+    double x = 0.0, z = 0.0, a = 0.0, lp[2] = {0.0, 0.0};
+    const bool ok = dt::spawn_one(M, g, max_attempts, env_base + (uint32_t)e, seed, key[i], x, z,
+                                  a, lp);
+    if (threadIdx.x == 0) {
+      const size_t sl = key[i] & 1u;
+      double* p = st.pre + sl * 5 * (size_t)n + e;
+      p[0] = x;
+      p[(size_t)n] = z;
+      p[2 * (size_t)n] = a;
+      p[3 * (size_t)n] = lp[0];
+      p[4 * (size_t)n] = lp[1];
+      __threadfence();   // the pose before its key
+      __hip_atomic_store(st.pre_key + sl * n + e, ok ? key[i] : (key[i] | dt::kKeyFailed),
+                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+__global__ __launch_bounds__(64) void refill_kernel(dt::State st, dt::MapDev md, dt::Geo g, int n,
+                                                    uint32_t max_attempts, uint32_t env_base) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  refill_env(st, md, g, n, max_attempts, env_base, (int)blockIdx.x, lds);
+}
+
 // EnvironmentWrapper.step (utils/env_wrappers.py:213-253) x repeat Simulator.step.
 __global__ __launch_bounds__(64) void step_kernel(dt::State st, dt::MapDev md, dt::Geo g,
                                                   StepCfg sc, int n, uint32_t env_base,
@@ -60,9 +108,18 @@ __global__ __launch_bounds__(64) void step_kernel(dt::State st, dt::MapDev md, d
                                                   float2* __restrict__ obs,
                                                   double* __restrict__ lanepos,
                                                   int32_t* __restrict__ tile_out,
-                                                  uint32_t* __restrict__ list_count,
+                                                  int n_step_blocks, int refill_envs,
+                                                  uint32_t max_attempts,
                                                   const uint8_t* __restrict__ step_mask) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  // blocks past the step's: the spawn-ahead refill, refill_envs envs each,
+  // running on the CUs the step leaves idle (block-uniform branch)
+  if ((int)blockIdx.x >= n_step_blocks) {
+    const int b = (int)blockIdx.x - n_step_blocks;
+    for (int i = 0; i < refill_envs; ++i)
+      refill_env(st, md, g, n, max_attempts, env_base, b * refill_envs + i, lds);
+    return;
+  }
   const MapLds M = dt::stage_map(md, lds);
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   // envs outside step_mask (dt_step_masked) are left exactly as they were
@@ -182,19 +239,40 @@ __global__ __launch_bounds__(64) void step_kernel(dt::State st, dt::MapDev md, d
     if (tile_out) tile_out[e] = dt::tile_of(M, g, x, z);
   }
 
+  // auto-reset (VectorEnv): the reset pose of the env's next spawn key was
+  // computed ahead (refill_env) -- take it, then ask for the key after next
+  bool reset_now = false;
+  double odist = 0.0, oarad = 0.0;
+  if (active && dn && sc.auto_reset) {
+    const uint32_t k = st.episode[e];
+    const size_t sl = k & 1u;
+    const uint32_t have =
+        __hip_atomic_load(st.pre_key + sl * n + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (have == k) {
+      const double* p = st.pre + sl * 5 * (size_t)n + e;
+      x = p[0];
+      z = p[(size_t)n];
+      ang = p[2 * (size_t)n];
+      odist = p[3 * (size_t)n];
+      oarad = p[4 * (size_t)n];
+      step_count = 0u;
+      env_step = 0u;
+      st.episode[e] = k + 1u;
+      reset_now = true;
+      __threadfence();   // the slot's reads are done before want moves past them
+      __hip_atomic_store(st.want + e, k + 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      atomicOr(st.err, dt::kErrSpawn);   // failed (or, impossibly, not ready): env stays put
+    }
+  }
   dt::wave_add(st.stats + 0, nsim);
   dt::wave_add(st.stats + 1, active ? 1u : 0u);
+  dt::wave_add(st.stats + 2, reset_now ? 1u : 0u);
   dt::wave_add(st.stats + 3, (active && dn) ? 1u : 0u);
-  if (list_count) {  // this wave's finished envs -> its own 64-slot segment, count stored
-    const bool fin = active && dn;  // (plain stores: nothing to reset between steps)
-    const uint64_t m = __ballot(fin);
-    const int lane = threadIdx.x & 63;
-    const int wave = e >> 6;
-    if (fin) st.spawn_list[64 * wave + __popcll(m & ((1ull << lane) - 1ull))] = e;
-    if (lane == 0) list_count[wave] = (uint32_t)__popcll(m);
-  }
   if (active) {
-    if (obs) obs[e] = inl ? make_float2((float)lp[0], (float)lp[3]) : make_float2(0.0f, 0.0f);
+    if (obs)
+      obs[e] = reset_now ? make_float2((float)odist, (float)oarad)
+                         : (inl ? make_float2((float)lp[0], (float)lp[3]) : make_float2(0.0f, 0.0f));
     st.x[e] = x;
     st.z[e] = z;
     st.angle[e] = ang;
@@ -203,92 +281,37 @@ __global__ __launch_bounds__(64) void step_kernel(dt::State st, dt::MapDev md, d
   }
 }
 
-// Simulator.reset + EnvironmentWrapper.reset counters (A13): one 256-thread
-// workgroup per pending env, so the envs that finished in a step respawn in
-// parallel across the chip instead of one after another inside their step
-// wave.  Mask mode (dt_reset): one block per env, flags NULL = every env, else
-// envs with flags[e] != 0.  List mode (dt_step's auto-reset): a fixed grid
-// strides over the done list step_kernel compacted.  obs (nullable) receives
-// the new (dist, angle_rad).
+// Simulator.reset + EnvironmentWrapper.reset counters (A13) for dt_reset: one
+// 256-thread workgroup per env (flags NULL = every env, else envs with
+// flags[e] != 0), so the envs respawn in parallel across the chip.  Afterwards
+// want = the new counter + 1 and refill_kernel tops up the spawn-ahead slots.
 constexpr int kSpawnThreads = 256;  // proposals per round: one accept in ~37, so ~1 round
-constexpr int kSpawnGrid = 1024;    // auto-reset launch: 4 workgroups per CU
-
-// The i-th finished env of the last dt_step: wave w's envs occupy global
-// indices [prefix(w), prefix(w) + count[w]) of the concatenated segments.
-__device__ int list_env(const int32_t* list, const uint32_t* count, int n_waves, uint32_t i) {
-  const int lane = threadIdx.x & 63;
-  uint32_t base = 0;
-  for (int w0 = 0; w0 < n_waves; w0 += 64) {
-    const uint32_t c = (w0 + lane < n_waves) ? count[w0 + lane] : 0u;
-    uint32_t incl = c;  // inclusive scan over the 64 lanes
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const uint32_t t = __shfl_up(incl, o);
-      if (lane >= o) incl += t;
-    }
-    const uint32_t total = __shfl(incl, 63);
-    if (i < base + total) {
-      const uint64_t past = __ballot(base + incl <= i);  // waves wholly before i
-      const int w = __popcll(past);
-      const uint32_t before = w == 0 ? 0u : __shfl(incl, w - 1);
-      return list[64 * (w0 + w) + (i - base - before)];
-    }
-    base += total;
-  }
-  return -1;
-}
-
-__device__ uint32_t list_total(const uint32_t* count, int n_waves) {
-  const int lane = threadIdx.x & 63;
-  uint32_t s = 0;
-  for (int w = lane; w < n_waves; w += 64) s += count[w];
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
-  return s;
-}
 
 __global__ __launch_bounds__(kSpawnThreads) void spawn_kernel(dt::State st, dt::MapDev md, dt::Geo g,
                                                    uint32_t max_attempts, uint32_t env_base,
-                                                   const uint8_t* __restrict__ flags,
-                                                   const uint32_t* __restrict__ list_count,
-                                                   int n_waves, float2* __restrict__ obs) {
+                                                   const uint8_t* __restrict__ flags) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   __shared__ double scratch[6 * (kSpawnThreads / 64)];
-  __shared__ int s_env;
-  // list mode (auto-reset): blocks stride over dt_step's finished envs;
-  // mask mode: one block per env, flags NULL = every env
-  const uint32_t cnt = list_count ? list_total(list_count, n_waves) : (uint32_t)gridDim.x;
-  if (blockIdx.x >= cnt) return;  // block-uniform
-  if (!list_count && flags != nullptr && flags[blockIdx.x] == 0) return;
+  if (flags != nullptr && flags[blockIdx.x] == 0) return;  // block-uniform
   const MapLds M = dt::stage_map(md, lds);
-  for (uint32_t i = blockIdx.x; i < cnt; i += list_count ? gridDim.x : cnt) {
-    if (list_count) {
-      if (threadIdx.x < 64) {
-        const int env = list_env(st.spawn_list, list_count, n_waves, i);
-        if (threadIdx.x == 0) s_env = env;
-      }
-      __syncthreads();
+  const int e = (int)blockIdx.x;
+  double x = 0.0, z = 0.0, ang = 0.0, dist = 0.0, arad = 0.0;
+  const uint32_t episode = st.episode[e];
+  const bool ok = dt::spawn_block(M, g, max_attempts, env_base + (uint32_t)e, st.seed[e], episode,
+                                  scratch, x, z, ang, dist, arad);
+  if (threadIdx.x == 0) {
+    if (!ok) {
+      atomicOr(st.err, dt::kErrSpawn);
+    } else {
+      st.x[e] = x;
+      st.z[e] = z;
+      st.angle[e] = ang;
+      st.step_count[e] = 0u;
+      st.env_step[e] = 0u;
+      st.episode[e] = episode + 1u;
+      st.want[e] = episode + 2u;
+      atomicAdd(st.stats + 2, 1ull);
     }
-    const int e = list_count ? s_env : (int)i;
-    double x = 0.0, z = 0.0, ang = 0.0, dist = 0.0, arad = 0.0;
-    const uint32_t episode = st.episode[e];
-    const bool ok = dt::spawn_block(M, g, max_attempts, env_base + (uint32_t)e, st.seed[e],
-                                    episode, scratch, x, z, ang, dist, arad);
-    if (threadIdx.x == 0) {
-      if (!ok) {
-        atomicOr(st.err, dt::kErrSpawn);
-      } else {
-        st.x[e] = x;
-        st.z[e] = z;
-        st.angle[e] = ang;
-        st.step_count[e] = 0u;
-        st.env_step[e] = 0u;
-        st.episode[e] = episode + 1u;
-        atomicAdd(st.stats + 2, 1ull);
-        if (obs) obs[e] = make_float2((float)dist, (float)arad);  // accepted => in a lane
-      }
-    }
-    __syncthreads();  // scratch / s_env are reused by the next env of this block
   }
 }
 
@@ -482,10 +505,15 @@ int dt_create(const dt_config* cfg, const dt_map* map, uint64_t seed, int32_t n_
   h->map.kind = (const int8_t*)(m_cs + sb16);
   h->map.drivable = (const int16_t*)(m_cs + sb16 + kb);
   h->lds_bytes = lds;
+  if (const char* v = getenv("DTSIM_REFILL_ENVS")) {   // diagnostic: envs per refill block
+    const int r = atoi(v);
+    h->refill_envs = r >= 1 && r <= 64 ? r : 1;
+  }
 
-  // state: x z angle seed (8 B) | step_count env_step episode (4 B) | err
+  // state: x z angle seed (8 B) | step_count env_step episode (4 B) | err | stats |
+  // spawn-ahead: pre (2 x 5 x 8 B) | pre_key (2 x 4 B) | want (4 B)
   const size_t N = (size_t)n_envs, N8 = N * 8, N4 = (N * 4 + 255) & ~255ul;
-  const size_t total = 4 * N8 + 3 * N4 + 256 + 256 + N4 + N4;
+  const size_t total = 4 * N8 + 3 * N4 + 256 + 256 + 10 * N8 + 3 * N4;
   if (hipMalloc(&h->st_buf, total) != hipSuccess) return fail("hipMalloc(state)");
   if (hipMemset(h->st_buf, 0, total) != hipSuccess) return fail("hipMemset(state)");
   char* sb = (char*)h->st_buf;
@@ -498,8 +526,9 @@ int dt_create(const dt_config* cfg, const dt_map* map, uint64_t seed, int32_t n_
   h->st.episode = (uint32_t*)(sb + 4 * N8 + 2 * N4);
   h->st.err = (uint32_t*)(sb + 4 * N8 + 3 * N4);
   h->st.stats = (unsigned long long*)(sb + 4 * N8 + 3 * N4 + 256);
-  h->st.spawn_list = (int32_t*)(sb + 4 * N8 + 3 * N4 + 512);
-  h->st.spawn_count = (uint32_t*)(sb + 4 * N8 + 4 * N4 + 512);
+  h->st.pre = (double*)(sb + 4 * N8 + 3 * N4 + 512);
+  h->st.pre_key = (uint32_t*)(sb + 14 * N8 + 3 * N4 + 512);
+  h->st.want = (uint32_t*)(sb + 14 * N8 + 5 * N4 + 512);
   *out = h;
   rc = dt_render_init(h, map);
   if (rc == DT_OK) rc = dt_seed(h, nullptr, seed, 0);
@@ -523,32 +552,53 @@ int dt_destroy(dt_handle* h) {
   return DT_OK;
 }
 
+// Spawn-ahead after the seeds or episode counters changed: drop every slot of
+// envs [e0, e1), want = counter + 1, then fill both slots (synchronous).
+static int refill_from_counters(dt_handle* h, int e0, int e1) {
+  const size_t n = (size_t)h->n, m = (size_t)(e1 - e0);
+  std::vector<uint32_t> ep(m), want(m);
+  HIP_OR_FAIL(h, hipMemcpy(ep.data(), h->st.episode + e0, m * 4, hipMemcpyDeviceToHost));
+  for (size_t i = 0; i < m; ++i) want[i] = ep[i] + 1u;
+  HIP_OR_FAIL(h, hipMemcpy(h->st.want + e0, want.data(), m * 4, hipMemcpyHostToDevice));
+  HIP_OR_FAIL(h, hipMemset(h->st.pre_key + e0, 0xFF, m * 4));
+  HIP_OR_FAIL(h, hipMemset(h->st.pre_key + n + e0, 0xFF, m * 4));
+  hipLaunchKernelGGL(refill_kernel, dim3(h->n), dim3(dt::kWave), h->lds_bytes, (hipStream_t)0,
+                     h->st, h->map, h->geo, h->n, h->sc.max_spawn_attempts, h->env_base);
+  HIP_OR_FAIL(h, hipGetLastError());
+  HIP_OR_FAIL(h, hipDeviceSynchronize());
+  return DT_OK;
+}
+
 int dt_seed(dt_handle* h, const uint64_t* seeds, uint64_t base, uint32_t env_id_base) {
   if (!h) return DT_E_ARG;
   h->env_base = env_id_base;
   HIP_OR_FAIL(h, hipSetDevice(h->device));
+  HIP_OR_FAIL(h, hipDeviceSynchronize());
   std::vector<uint64_t> s(h->n);
   for (int i = 0; i < h->n; ++i) s[i] = seeds ? seeds[i] : base;
   HIP_OR_FAIL(h, hipMemcpy(h->st.seed, s.data(), s.size() * 8, hipMemcpyHostToDevice));
   HIP_OR_FAIL(h, hipMemset(h->st.episode, 0, (size_t)h->n * 4));
-  return DT_OK;
+  return refill_from_counters(h, 0, h->n);
 }
 
 int dt_seed_env(dt_handle* h, int32_t env, uint64_t seed) {
   if (!h || env < 0 || env >= h->n) return DT_E_ARG;
   HIP_OR_FAIL(h, hipSetDevice(h->device));
+  HIP_OR_FAIL(h, hipDeviceSynchronize());
   const uint32_t zero = 0;
   HIP_OR_FAIL(h, hipMemcpy(h->st.seed + env, &seed, 8, hipMemcpyHostToDevice));
   HIP_OR_FAIL(h, hipMemcpy(h->st.episode + env, &zero, 4, hipMemcpyHostToDevice));
-  return DT_OK;
+  return refill_from_counters(h, env, env + 1);
 }
 
 int dt_reset(dt_handle* h, const uint8_t* mask, void* stream) {
   if (!h) return DT_E_ARG;
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(spawn_kernel, dim3(h->n), dim3(kSpawnThreads), h->lds_bytes, s, h->st,
-                     h->map, h->geo, h->sc.max_spawn_attempts, h->env_base, mask,
-                     (const uint32_t*)nullptr, 0, (float2*)nullptr);
+                     h->map, h->geo, h->sc.max_spawn_attempts, h->env_base, mask);
+  HIP_OR_FAIL(h, hipGetLastError());
+  hipLaunchKernelGGL(refill_kernel, dim3(h->n), dim3(dt::kWave), h->lds_bytes, s, h->st, h->map,
+                     h->geo, h->n, h->sc.max_spawn_attempts, h->env_base);
   HIP_OR_FAIL(h, hipGetLastError());
   return DT_OK;
 }
@@ -562,20 +612,16 @@ int dt_step_masked(dt_handle* h, const uint8_t* mask, const float* actions, doub
     return DT_E_ARG;
   }
   hipStream_t s = (hipStream_t)stream;
-  uint32_t* list_count = h->sc.auto_reset ? h->st.spawn_count : nullptr;
-  hipLaunchKernelGGL(step_kernel, dim3(grid_of(h->n)), dim3(dt::kWave), h->lds_bytes, s, h->st,
-                     h->map, h->geo, h->sc, h->n, h->env_base, (const float2*)actions, reward, reward_mod,
-                     done, (float2*)obs, lanepos, tile, list_count, mask);
+  // step blocks, then (auto-reset) refill blocks, one env each by default:
+  // this decision's resets use poses computed in earlier launches, and the
+  // refill of the ones consumed last decision overlaps this decision's step
+  const int gs = grid_of(h->n);
+  const int re = h->refill_envs;
+  const int grid = gs + (h->sc.auto_reset ? (h->n + re - 1) / re : 0);
+  hipLaunchKernelGGL(step_kernel, dim3(grid), dim3(dt::kWave), h->lds_bytes, s, h->st, h->map,
+                     h->geo, h->sc, h->n, h->env_base, (const float2*)actions, reward, reward_mod,
+                     done, (float2*)obs, lanepos, tile, gs, re, h->sc.max_spawn_attempts, mask);
   HIP_OR_FAIL(h, hipGetLastError());
-  if (h->sc.auto_reset) {
-    // a fixed grid over the finished envs (a few hundred of 4096 per
-    // decision): no launch of thousands of idle workgroups
-    const int grid = h->n < kSpawnGrid ? h->n : kSpawnGrid;
-    hipLaunchKernelGGL(spawn_kernel, dim3(grid), dim3(kSpawnThreads), h->lds_bytes, s, h->st,
-                       h->map, h->geo, h->sc.max_spawn_attempts, h->env_base, (const uint8_t*)nullptr,
-                       (const uint32_t*)list_count, grid_of(h->n), (float2*)obs);
-    HIP_OR_FAIL(h, hipGetLastError());
-  }
   return DT_OK;
 }
 
@@ -621,7 +667,10 @@ int dt_set_state(dt_handle* h, const double* x, const double* z, const double* a
   if (step_count)
     HIP_OR_FAIL(h, hipMemcpy(h->st.step_count, step_count, N * 4, hipMemcpyHostToDevice));
   if (env_step) HIP_OR_FAIL(h, hipMemcpy(h->st.env_step, env_step, N * 4, hipMemcpyHostToDevice));
-  if (episode) HIP_OR_FAIL(h, hipMemcpy(h->st.episode, episode, N * 4, hipMemcpyHostToDevice));
+  if (episode) {
+    HIP_OR_FAIL(h, hipMemcpy(h->st.episode, episode, N * 4, hipMemcpyHostToDevice));
+    return refill_from_counters(h, 0, h->n);   // spawn-ahead keys follow the counters
+  }
   return DT_OK;
 }
 

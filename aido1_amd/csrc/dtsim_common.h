@@ -39,9 +39,16 @@ struct State {
   uint32_t* episode;
   uint32_t* err;  // one word, OR of kErr*
   unsigned long long* stats;  // [4] sim steps, decisions, resets, episodes done
-  int32_t* spawn_list;        // [n] envs that finished in the last dt_step, 64 per step wave
-  uint32_t* spawn_count;      // [ceil(n/64)] how many of its 64 slots each step wave filled
+  // spawn-ahead: slot k & 1 of env e holds the reset pose of spawn key k
+  // (x, z, angle, lane dist, angle_rad) when pre_key[k & 1][e] == k (bit 31:
+  // the spawn failed); want[e] = the highest key that must be ready, one past
+  // the key the env's next reset consumes (its episode counter)
+  double* pre;                // [2][5][n]
+  uint32_t* pre_key;          // [2][n]
+  uint32_t* want;             // [n]
 };
+constexpr uint32_t kKeyFailed = 0x80000000u;
+constexpr uint32_t kKeyNone = 0xFFFFFFFFu;
 
 // One atomic per wave: lane-sum through the 64-wide reduction, lane 0 adds.
 __device__ inline void wave_add(unsigned long long* p, unsigned v) {
@@ -445,7 +452,8 @@ __device__ inline bool spawn_try(const MapLds& M, const Geo& g, uint32_t k0, uin
 }
 
 // Wave-cooperative Simulator.reset of ONE env (every argument wave-uniform;
-// all 64 lanes must call).  The 64 lanes test proposals k = 64*round + lane in
+// all 64 lanes must call); lp_out (optional) receives the winner's
+// (dist, angle_rad).  The 64 lanes test proposals k = 64*round + lane in
 // parallel; the lowest accepting lane of the first round with any acceptance
 // wins, which is exactly the first accepted k of a sequential rejection loop
 // over the same i.i.d. stream — so the spawn distribution is upstream's and the
@@ -453,7 +461,7 @@ __device__ inline bool spawn_try(const MapLds& M, const Geo& g, uint32_t k0, uin
 // max_attempts proposals were all rejected (upstream raises).
 __device__ inline bool spawn_one(const MapLds& M, const Geo& g, uint32_t max_attempts,
                                  uint32_t env, uint64_t seed, uint32_t episode, double& x,
-                                 double& z, double& ang) {
+                                 double& z, double& ang, double* lp_out = nullptr) {
   const int lane = threadIdx.x & 63;
   const uint32_t k0 = (uint32_t)seed, k1 = (uint32_t)(seed >> 32);
   const U4 tw = philox(0u, episode, env, kTagTile, k0, k1);
@@ -463,15 +471,19 @@ __device__ inline bool spawn_one(const MapLds& M, const Geo& g, uint32_t max_att
   const double fi = (double)(ti % M.width), fj = (double)(ti / M.width);
   for (uint32_t base = 0; base < max_attempts; base += kWave) {
     const uint32_t k = base + (uint32_t)lane;
-    double px, pz, pa;
+    double px, pz, pa, lpo[2] = {0.0, 0.0};
     const bool ok = (k < max_attempts) && spawn_try(M, g, k0, k1, env, episode, k, fi, fj, px,
-                                                    pz, pa);
+                                                    pz, pa, lpo);
     const uint64_t acc = __ballot(ok);
     if (acc) {
       const int w = __ffsll((unsigned long long)acc) - 1;
       x = bcast(px, w);
       z = bcast(pz, w);
       ang = bcast(pa, w);
+      if (lp_out) {
+        lp_out[0] = bcast(lpo[0], w);
+        lp_out[1] = bcast(lpo[1], w);
+      }
       return true;
     }
   }
