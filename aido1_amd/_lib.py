@@ -86,9 +86,12 @@ def lib():
             import torch  # noqa: F401
         except ImportError:
             pass
-        if _stale():
-            build()
-        L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        path = os.environ.get('DTSIM_DIAG_LIB')  # diagnostic builds (tools/), loaded as is
+        if not path:
+            path = LIB_PATH
+            if _stale():
+                build()
+        L = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
         vp, i32, u32, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64
         i64, f64 = ctypes.c_int64, ctypes.c_double
         sig = {

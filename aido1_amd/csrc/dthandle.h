@@ -24,7 +24,6 @@ struct dt_handle {
   void* st_buf = nullptr;
   size_t lds_bytes = 0;
   uint32_t env_base = 0;
-  int32_t refill_envs = 1;     // spawn-ahead envs per refill block (DTSIM_REFILL_ENVS)
   // observation path (dtrender.hip)
   dt_line_params line_params{};
   dr::LineDev line{};

@@ -22,6 +22,34 @@ namespace {
 
 using dt::MapLds;
 
+// Diagnostic build only (-DDTSIM_STAMPS, tools/step_stamps.sh): wave 0 of the
+// first 64 step blocks records the shader clock at fixed points of the step.
+#ifdef DTSIM_STAMPS
+constexpr int kStamps = 16;
+__device__ unsigned long long g_stamps[64 * kStamps];
+#define STAMP(i)                                                                    \
+  do {                                                                              \
+    const unsigned long long _t = __builtin_amdgcn_s_memtime();                     \
+    if (threadIdx.x == 0 && blockIdx.x < 64) g_stamps[blockIdx.x * kStamps + (i)] = _t; \
+  } while (0)
+__device__ unsigned long long g_rstamps[4096 * 4];  // refill blocks: entry, exit, items
+#define RFSTAMP(b, i, v)                                                            \
+  do {                                                                              \
+    if (threadIdx.x == 0 && (b) < 4096) g_rstamps[(b) * 4 + (i)] = (v);             \
+  } while (0)
+#define RSTAMP(i)                                                                   \
+  do {                                                                              \
+    const unsigned long long _t = __builtin_amdgcn_s_memrealtime();                 \
+    if (threadIdx.x == 0 && blockIdx.x < 64) g_stamps[blockIdx.x * kStamps + (i)] = _t; \
+  } while (0)
+#else
+#define STAMP(i) \
+  do {           \
+  } while (0)
+#define RSTAMP(i) STAMP(i)
+#define RFSTAMP(b, i, v) STAMP(i)
+#endif
+
 __device__ inline void map_action(int mode, float a0, float a1, double& vl, double& vr) {
   if (mode == DT_ACTION_TANH) {
     // utils/env_wrappers.py:214-216: in-place float32 `action /= 2; action += 0.5`
@@ -50,56 +78,108 @@ __device__ inline void map_action(int mode, float a0, float a1, double& vl, doub
   }
 }
 
-// Spawn-ahead refill of env e (every thread of a 64-thread block; A13): make
-// the slots of keys want-1 and want hold their reset poses.  Race-free against
-// a dt_step lane of the same launch: that lane reads slot (key & 1) of its
-// episode counter k, then (after a fence) raises want to k + 2; this block only
-// writes slots of keys it reads as missing among {want-1, want}, which are
-// never k's while the lane may still read it.
-__device__ void refill_env(const dt::State& st, const dt::MapDev& md, const dt::Geo& g, int n,
-                           uint32_t max_attempts, uint32_t env_base, int e, unsigned char* lds) {
-  if (e >= n) return;
-  const uint32_t w = __hip_atomic_load(st.want + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  bool need[2];
-  uint32_t key[2];
+// Spawn-ahead refill (A13) of envs [e0, e0 + ne), one 256-thread block: the
+// first ne lanes read want, both slot keys and the seed of one env each (one
+// round of independent loads) and list the keys missing among {want-1, want};
+// the block stages the map only when the list is not empty and then computes
+// the listed (env, key) items: one item (the usual case) with all 256 threads
+// (spawn_block: one round of 256 proposals almost always holds the first
+// accepted one), several with one wave each in parallel (spawn_one).  Groups
+// are small (kRefillEnvs), so the refill finishes inside the step it runs
+// beside.
+// Race-free against a dt_step lane of the same launch: key k = that lane's
+// episode counter was made ready by an earlier launch (every launch refills
+// every key missing at its start), the lane reads slot k & 1 at its start and
+// raises want to k + 2 only after those reads returned; this block writes only
+// slots of keys it reads as missing among {want-1, want}, never k's while the
+// lane may still read it.
+constexpr int kBlock = 256;        // step and refill blocks (4 waves)
+
+// Publish a spawn-ahead slot.  No fence: the pose is read by a later launch
+// only (the kernel boundary orders it), and this launch's scans read the key.
+__device__ inline void put_slot(const dt::State& st, int n, int e, uint32_t key, bool ok, double x,
+                                double z, double a, double dist, double arad) {
+  const size_t sl = key & 1u;
+  double* p = st.pre + sl * 5 * (size_t)n + e;
+  p[0] = x;
+  p[(size_t)n] = z;
+  p[2 * (size_t)n] = a;
+  p[3 * (size_t)n] = dist;
+  p[4 * (size_t)n] = arad;
+  __hip_atomic_store(st.pre_key + sl * n + e, ok ? key : (key | dt::kKeyFailed), __ATOMIC_RELAXED,
+                     __HIP_MEMORY_SCOPE_AGENT);
+}
+constexpr int kRefillEnvs = 4;     // envs scanned per refill block
+
+__device__ int refill_group(const dt::State& st, const dt::MapDev& md, const dt::Geo& g, int n,
+                             uint32_t max_attempts, uint32_t env_base, int e0, int ne,
+                             unsigned char* lds) {
+  __shared__ int32_t item_env[2 * kRefillEnvs];
+  __shared__ uint32_t item_key[2 * kRefillEnvs];
+  __shared__ uint64_t item_seed[2 * kRefillEnvs];
+  __shared__ int32_t n_items;
+  __shared__ double scratch[6 * (kBlock / 64)];
+  const int tid = threadIdx.x;
+  if (tid == 0) n_items = 0;
+  __syncthreads();
+  const int e = e0 + tid;
+  if (tid < ne && e < n) {
+    const uint32_t w = __hip_atomic_load(st.want + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t h0 = __hip_atomic_load(st.pre_key + e, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t h1 = __hip_atomic_load(st.pre_key + (size_t)n + e, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t seed = st.seed[e];
 #pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    key[i] = w - 1u + (uint32_t)i;
-    const uint32_t have = __hip_atomic_load(st.pre_key + (size_t)(key[i] & 1u) * n + e,
-                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    need[i] = (i == 1 || w > 0u) && (have & ~dt::kKeyFailed) != key[i];
-  }
-  if (!need[0] && !need[1]) return;  // block-uniform
-  const MapLds M = dt::stage_map(md, lds);
-  const uint64_t seed = st.seed[e];
-  for (int i = 0; i < 2; ++i) {
-    if (!need[i]) continue;
-    double x = 0.0, z = 0.0, a = 0.0, lp[2] = {0.0, 0.0};
-    const bool ok = dt::spawn_one(M, g, max_attempts, env_base + (uint32_t)e, seed, key[i], x, z,
-                                  a, lp);
-    if (threadIdx.x == 0) {
-      const size_t sl = key[i] & 1u;
-      double* p = st.pre + sl * 5 * (size_t)n + e;
-      p[0] = x;
-      p[(size_t)n] = z;
-      p[2 * (size_t)n] = a;
-      p[3 * (size_t)n] = lp[0];
-      p[4 * (size_t)n] = lp[1];
-      __threadfence();   // the pose before its key
-      __hip_atomic_store(st.pre_key + sl * n + e, ok ? key[i] : (key[i] | dt::kKeyFailed),
-                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    for (int i = 0; i < 2; ++i) {
+      const uint32_t key = w - 1u + (uint32_t)i;
+      const uint32_t have = (key & 1u) ? h1 : h0;
+      if ((i == 1 || w > 0u) && (have & ~dt::kKeyFailed) != key) {
+        const int slot = atomicAdd(&n_items, 1);
+        item_env[slot] = e;
+        item_key[slot] = key;
+        item_seed[slot] = seed;
+      }
     }
   }
+  __syncthreads();
+  const int cnt = n_items;
+  if (cnt == 0) return 0;  // block-uniform
+  const dt::MapLds M = dt::stage_map(md, lds);
+  if (cnt == 1) {  // the usual case: all four waves on the one item
+    double x = 0.0, z = 0.0, a = 0.0, dist = 0.0, arad = 0.0;
+    const bool ok = dt::spawn_block(M, g, max_attempts, env_base + (uint32_t)item_env[0],
+                                    item_seed[0], item_key[0], scratch, x, z, a, dist, arad);
+    if (tid == 0) put_slot(st, n, item_env[0], item_key[0], ok, x, z, a, dist, arad);
+  } else {  // several: one wave per item (64 proposals per round), waves in parallel
+    const int wave = tid >> 6, nw = (int)(blockDim.x >> 6);
+    for (int it = wave; it < cnt; it += nw) {  // wave-uniform
+      double x = 0.0, z = 0.0, a = 0.0, lp[2] = {0.0, 0.0};
+      const bool ok = dt::spawn_one(M, g, max_attempts, env_base + (uint32_t)item_env[it],
+                                    item_seed[it], item_key[it], x, z, a, lp);
+      if ((tid & 63) == 0) put_slot(st, n, item_env[it], item_key[it], ok, x, z, a, lp[0], lp[1]);
+    }
+  }
+  return cnt;
 }
 
-__global__ __launch_bounds__(64) void refill_kernel(dt::State st, dt::MapDev md, dt::Geo g, int n,
-                                                    uint32_t max_attempts, uint32_t env_base) {
+__global__ __launch_bounds__(kBlock) void refill_kernel(dt::State st, dt::MapDev md, dt::Geo g,
+                                                        int n, uint32_t max_attempts,
+                                                        uint32_t env_base) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  refill_env(st, md, g, n, max_attempts, env_base, (int)blockIdx.x, lds);
+  refill_group(st, md, g, n, max_attempts, env_base, (int)blockIdx.x * kRefillEnvs, kRefillEnvs,
+               lds);
+}
+
+// 0, available only once v's load has returned (the asm reads v).
+__device__ inline uint32_t after_load(double v) {
+  uint32_t z;
+  asm volatile("v_mov_b32 %0, 0 ; %1" : "=v"(z) : "v"(v));
+  return z;
 }
 
 // EnvironmentWrapper.step (utils/env_wrappers.py:213-253) x repeat Simulator.step.
-__global__ __launch_bounds__(64) void step_kernel(dt::State st, dt::MapDev md, dt::Geo g,
+__global__ __launch_bounds__(kBlock) void step_kernel(dt::State st, dt::MapDev md, dt::Geo g,
                                                   StepCfg sc, int n, uint32_t env_base,
                                                   const float2* __restrict__ act,
                                                   double* __restrict__ rew,
@@ -108,27 +188,59 @@ __global__ __launch_bounds__(64) void step_kernel(dt::State st, dt::MapDev md, d
                                                   float2* __restrict__ obs,
                                                   double* __restrict__ lanepos,
                                                   int32_t* __restrict__ tile_out,
-                                                  int n_step_blocks, int refill_envs,
-                                                  uint32_t max_attempts,
+                                                  int n_step_blocks, uint32_t max_attempts,
                                                   const uint8_t* __restrict__ step_mask) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  // blocks past the step's: the spawn-ahead refill, refill_envs envs each,
+  // blocks past the step's: the spawn-ahead refill, kRefillEnvs envs each,
   // running on the CUs the step leaves idle (block-uniform branch)
   if ((int)blockIdx.x >= n_step_blocks) {
-    const int b = (int)blockIdx.x - n_step_blocks;
-    for (int i = 0; i < refill_envs; ++i)
-      refill_env(st, md, g, n, max_attempts, env_base, b * refill_envs + i, lds);
+    const int rb = (int)blockIdx.x - n_step_blocks;
+    RFSTAMP(rb, 0, __builtin_amdgcn_s_memrealtime());
+    const int items = refill_group(st, md, g, n, max_attempts, env_base, rb * kRefillEnvs,
+                                   kRefillEnvs, lds);
+    RFSTAMP(rb, 1, __builtin_amdgcn_s_memrealtime());
+    RFSTAMP(rb, 2, (unsigned long long)items);
+    (void)items;
     return;
   }
-  const MapLds M = dt::stage_map(md, lds);
+  // the step waves win issue arbitration against refill waves sharing their SIMD
+  __builtin_amdgcn_s_setprio(3);
+  RSTAMP(9);
+  STAMP(0);
   const int e = blockIdx.x * blockDim.x + threadIdx.x;
   // envs outside step_mask (dt_step_masked) are left exactly as they were
   const bool active = e < n && (step_mask == nullptr || step_mask[e] != 0);
   const int ei = active ? e : 0;
 
+  // the env's state and (auto-reset) the spawn-ahead slot of its next key are
+  // loaded before the map is staged, so their latency hides behind it.  Key k
+  // (= the episode counter) was made ready by an earlier launch and its slot
+  // is not rewritten before this env consumes it (refill_group), so the slot
+  // can be read up front.
   double x = st.x[ei], z = st.z[ei], ang = st.angle[ei];
   uint32_t step_count = st.step_count[ei], env_step = st.env_step[ei];
   const float2 a = act[ei];
+  uint32_t key = 0u, have = dt::kKeyNone;
+  double pre[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  if (sc.auto_reset) {  // both slots (no load waits on the episode counter)
+    key = st.episode[ei];
+    const uint32_t h0 = __hip_atomic_load(st.pre_key + ei, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t h1 = __hip_atomic_load(st.pre_key + (size_t)n + ei, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT);
+    double p0[5], p1[5];
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+      p0[q] = st.pre[q * (size_t)n + ei];
+      p1[q] = st.pre[(5 + q) * (size_t)n + ei];
+    }
+    const bool odd = (key & 1u) != 0u;
+    have = odd ? h1 : h0;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) pre[q] = odd ? p1[q] : p0[q];
+  }
+  const MapLds M = dt::stage_map(md, lds);
+  STAMP(1);
 
   double vl, vr;
   map_action(sc.action_mode, a.x, a.y, vl, vr);
@@ -147,6 +259,7 @@ __global__ __launch_bounds__(64) void step_kernel(dt::State st, dt::MapDev md, d
     sincos(rot, &sr, &cr);
   }
   const double kstraight = g.dt * wl;
+  STAMP(2);
 
   double tr = 0.0, trm = 0.0;
   bool dn = !active;
@@ -179,6 +292,7 @@ __global__ __launch_bounds__(64) void step_kernel(dt::State st, dt::MapDev md, d
         }
         step_count += 1u;
         nsim += 1u;
+        if (rep == 1) STAMP(11);
         if (sc.speed_measured) {
           const double a1 = x - ox, a3 = z - oz;
           speed = sqrt((a1 * a1 + 0.0 * 0.0) + a3 * a3) / g.dt;
@@ -187,7 +301,9 @@ __global__ __launch_bounds__(64) void step_kernel(dt::State st, dt::MapDev md, d
       // _compute_done_reward (A11)
       double r;
       bool sd = false;
-      if (!dt::valid_pose(M, g, x, z, c, s, 1.0)) {
+      const bool vp = dt::valid_pose(M, g, x, z, c, s, 1.0);
+      if (rep == 1) STAMP(12);
+      if (!vp) {
         r = -1000.0;
         sd = true;
       } else if (step_count >= sc.max_steps) {
@@ -200,6 +316,7 @@ __global__ __launch_bounds__(64) void step_kernel(dt::State st, dt::MapDev md, d
             M.n_obj ? dt::proximity_penalty(M, g, x + g.off * c, z + g.off * (-s)) : 0.0;
         lp_fresh = true;
         lp_inl = dt::lane_pos<false>(M, g, x, z, c, s, lp);
+        if (rep == 1) STAMP(13);
         if (lp_inl) {
           const double ad = fabs(lp[0]);
           r = ((1.0 * sp) * lp[1] + (-10.0) * ad) + 40.0 * pen;
@@ -214,16 +331,27 @@ __global__ __launch_bounds__(64) void step_kernel(dt::State st, dt::MapDev md, d
       env_step += 1u;
       dn = sd || env_step > sc.max_env_steps;
     }
+    STAMP(3 + (rep < 3 ? rep : 2));
   }
   trm = trm * sc.reward_scale;
 
-  bool inl;
+  // auto-reset (VectorEnv): a finished env takes the reset pose of its next
+  // spawn key, computed ahead (refill_group), and asks for the key after next
+  const bool want_reset = active && dn && sc.auto_reset;
+  const bool reset_now = want_reset && have == key;
+  if (want_reset && !reset_now)
+    atomicOr(st.err, dt::kErrSpawn);   // failed (or, impossibly, not ready): env stays put
+
+  // terminal lane pose: the obs of an env that stays, and the optional lanepos
+  // output; an env being reset reports its reset pose's obs instead
+  bool inl = false;
   if (lp_fresh) {  // same pose as the last reward: only the angle is missing
     inl = lp_inl;
-    if (inl) dt::finish_angle(g, lp);
-  } else {
-    inl = active && dt::lane_pos<true>(M, g, x, z, c, s, lp);
+    if (inl && (lanepos || !reset_now)) dt::finish_angle(g, lp);
+  } else if (active && (lanepos || !reset_now)) {
+    inl = dt::lane_pos<true>(M, g, x, z, c, s, lp);
   }
+  STAMP(6);
   if (active) {
     rew[e] = tr;
     rewm[e] = trm;
@@ -238,40 +366,26 @@ __global__ __launch_bounds__(64) void step_kernel(dt::State st, dt::MapDev md, d
     }
     if (tile_out) tile_out[e] = dt::tile_of(M, g, x, z);
   }
-
-  // auto-reset (VectorEnv): the reset pose of the env's next spawn key was
-  // computed ahead (refill_env) -- take it, then ask for the key after next
-  bool reset_now = false;
-  double odist = 0.0, oarad = 0.0;
-  if (active && dn && sc.auto_reset) {
-    const uint32_t k = st.episode[e];
-    const size_t sl = k & 1u;
-    const uint32_t have =
-        __hip_atomic_load(st.pre_key + sl * n + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (have == k) {
-      const double* p = st.pre + sl * 5 * (size_t)n + e;
-      x = p[0];
-      z = p[(size_t)n];
-      ang = p[2 * (size_t)n];
-      odist = p[3 * (size_t)n];
-      oarad = p[4 * (size_t)n];
-      step_count = 0u;
-      env_step = 0u;
-      st.episode[e] = k + 1u;
-      reset_now = true;
-      __threadfence();   // the slot's reads are done before want moves past them
-      __hip_atomic_store(st.want + e, k + 2u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    } else {
-      atomicOr(st.err, dt::kErrSpawn);   // failed (or, impossibly, not ready): env stays put
-    }
+  if (reset_now) {
+    x = pre[0];
+    z = pre[1];
+    ang = pre[2];
+    step_count = 0u;
+    env_step = 0u;
+    st.episode[e] = key + 1u;
+    // want moves past key only once the slot's loads have returned: the store's
+    // value depends on the last of them (loads return in order)
+    __hip_atomic_store(st.want + e, key + 2u + after_load(pre[4]), __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
   }
-  dt::wave_add(st.stats + 0, nsim);
-  dt::wave_add(st.stats + 1, active ? 1u : 0u);
-  dt::wave_add(st.stats + 2, reset_now ? 1u : 0u);
-  dt::wave_add(st.stats + 3, (active && dn) ? 1u : 0u);
+  STAMP(7);
+  dt::wave_count(st.stats + 0, nsim, sc.repeat * sc.frame_skip);
+  dt::wave_count(st.stats + 1, active ? 1u : 0u, 1);
+  dt::wave_count(st.stats + 2, reset_now ? 1u : 0u, 1);
+  dt::wave_count(st.stats + 3, (active && dn) ? 1u : 0u, 1);
   if (active) {
     if (obs)
-      obs[e] = reset_now ? make_float2((float)odist, (float)oarad)
+      obs[e] = reset_now ? make_float2((float)pre[3], (float)pre[4])
                          : (inl ? make_float2((float)lp[0], (float)lp[3]) : make_float2(0.0f, 0.0f));
     st.x[e] = x;
     st.z[e] = z;
@@ -279,6 +393,8 @@ __global__ __launch_bounds__(64) void step_kernel(dt::State st, dt::MapDev md, d
     st.step_count[e] = step_count;
     st.env_step[e] = env_step;
   }
+  STAMP(8);
+  RSTAMP(10);
 }
 
 // Simulator.reset + EnvironmentWrapper.reset counters (A13) for dt_reset: one
@@ -344,10 +460,21 @@ __global__ __launch_bounds__(64) void lane_pos_kernel(dt::State st, dt::MapDev m
   } while (0)
 
 int grid_of(int n) { return (n + dt::kWave - 1) / dt::kWave; }
+int refill_grid(int n, int ne) { return (n + ne - 1) / ne; }
 
 }  // namespace
 
 extern "C" {
+
+#ifdef DTSIM_STAMPS
+int dt_diag_stamps(unsigned long long* out) {  // 64 x kStamps shader-clock stamps
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(g_stamps)) == hipSuccess ? 0 : -1;
+}
+int dt_diag_rstamps(unsigned long long* out) {  // refill blocks: entry, exit (real time), items
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rstamps), sizeof(g_rstamps)) == hipSuccess ? 0
+                                                                                          : -1;
+}
+#endif
 
 int32_t dt_abi_version(void) { return DT_ABI_VERSION; }
 
@@ -505,10 +632,6 @@ int dt_create(const dt_config* cfg, const dt_map* map, uint64_t seed, int32_t n_
   h->map.kind = (const int8_t*)(m_cs + sb16);
   h->map.drivable = (const int16_t*)(m_cs + sb16 + kb);
   h->lds_bytes = lds;
-  if (const char* v = getenv("DTSIM_REFILL_ENVS")) {   // diagnostic: envs per refill block
-    const int r = atoi(v);
-    h->refill_envs = r >= 1 && r <= 64 ? r : 1;
-  }
 
   // state: x z angle seed (8 B) | step_count env_step episode (4 B) | err | stats |
   // spawn-ahead: pre (2 x 5 x 8 B) | pre_key (2 x 4 B) | want (4 B)
@@ -562,7 +685,7 @@ static int refill_from_counters(dt_handle* h, int e0, int e1) {
   HIP_OR_FAIL(h, hipMemcpy(h->st.want + e0, want.data(), m * 4, hipMemcpyHostToDevice));
   HIP_OR_FAIL(h, hipMemset(h->st.pre_key + e0, 0xFF, m * 4));
   HIP_OR_FAIL(h, hipMemset(h->st.pre_key + n + e0, 0xFF, m * 4));
-  hipLaunchKernelGGL(refill_kernel, dim3(h->n), dim3(dt::kWave), h->lds_bytes, (hipStream_t)0,
+  hipLaunchKernelGGL(refill_kernel, dim3(refill_grid(h->n, kRefillEnvs)), dim3(kBlock), h->lds_bytes, (hipStream_t)0,
                      h->st, h->map, h->geo, h->n, h->sc.max_spawn_attempts, h->env_base);
   HIP_OR_FAIL(h, hipGetLastError());
   HIP_OR_FAIL(h, hipDeviceSynchronize());
@@ -597,7 +720,7 @@ int dt_reset(dt_handle* h, const uint8_t* mask, void* stream) {
   hipLaunchKernelGGL(spawn_kernel, dim3(h->n), dim3(kSpawnThreads), h->lds_bytes, s, h->st,
                      h->map, h->geo, h->sc.max_spawn_attempts, h->env_base, mask);
   HIP_OR_FAIL(h, hipGetLastError());
-  hipLaunchKernelGGL(refill_kernel, dim3(h->n), dim3(dt::kWave), h->lds_bytes, s, h->st, h->map,
+  hipLaunchKernelGGL(refill_kernel, dim3(refill_grid(h->n, kRefillEnvs)), dim3(kBlock), h->lds_bytes, s, h->st, h->map,
                      h->geo, h->n, h->sc.max_spawn_attempts, h->env_base);
   HIP_OR_FAIL(h, hipGetLastError());
   return DT_OK;
@@ -612,15 +735,14 @@ int dt_step_masked(dt_handle* h, const uint8_t* mask, const float* actions, doub
     return DT_E_ARG;
   }
   hipStream_t s = (hipStream_t)stream;
-  // step blocks, then (auto-reset) refill blocks, one env each by default:
-  // this decision's resets use poses computed in earlier launches, and the
-  // refill of the ones consumed last decision overlaps this decision's step
-  const int gs = grid_of(h->n);
-  const int re = h->refill_envs;
-  const int grid = gs + (h->sc.auto_reset ? (h->n + re - 1) / re : 0);
-  hipLaunchKernelGGL(step_kernel, dim3(grid), dim3(dt::kWave), h->lds_bytes, s, h->st, h->map,
+  // step blocks, then (auto-reset) refill blocks of kRefillEnvs envs: this
+  // decision's resets use poses computed in earlier launches, and the refill of
+  // the ones consumed last decision overlaps this decision's step
+  const int gs = (h->n + kBlock - 1) / kBlock;
+  const int grid = gs + (h->sc.auto_reset ? refill_grid(h->n, kRefillEnvs) : 0);
+  hipLaunchKernelGGL(step_kernel, dim3(grid), dim3(kBlock), h->lds_bytes, s, h->st, h->map,
                      h->geo, h->sc, h->n, h->env_base, (const float2*)actions, reward, reward_mod,
-                     done, (float2*)obs, lanepos, tile, gs, re, h->sc.max_spawn_attempts, mask);
+                     done, (float2*)obs, lanepos, tile, gs, h->sc.max_spawn_attempts, mask);
   HIP_OR_FAIL(h, hipGetLastError());
   return DT_OK;
 }

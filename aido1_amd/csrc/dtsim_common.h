@@ -50,13 +50,15 @@ struct State {
 constexpr uint32_t kKeyFailed = 0x80000000u;
 constexpr uint32_t kKeyNone = 0xFFFFFFFFu;
 
-// One atomic per wave: lane-sum through the 64-wide reduction, lane 0 adds.
-__device__ inline void wave_add(unsigned long long* p, unsigned v) {
-  unsigned long long s = v;
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) s += __shfl_xor(s, o);
+// One atomic per wave: the lane sum of v (0 <= v <= vmax, vmax wave-uniform)
+// from one ballot per bit, lane 0 adds.
+__device__ inline void wave_count(unsigned long long* p, unsigned v, unsigned vmax) {
+  unsigned long long s = 0;
+  for (int b = 0; (vmax >> b) != 0u; ++b)
+    s += (unsigned long long)__popcll(__ballot((v >> b) & 1u)) << b;
   if ((threadIdx.x & 63) == 0 && s) atomicAdd(p, s);
 }
+
 
 // Map image in device memory; staged into LDS by each block.
 struct MapDev {
@@ -305,10 +307,13 @@ __device__ inline bool valid_pose(const MapLds& M, const Geo& g, double x, doubl
   const double pz = z + g.off * (-s);
   const double kw = (safety * 0.5) * g.robot_width;
   const double kf = (safety * 0.5) * g.front;
-  bool ok = drivable(M, g, px, pz);
-  ok = ok && drivable(M, g, px - kw * s, pz - kw * c);
-  ok = ok && drivable(M, g, px + kw * s, pz + kw * c);
-  ok = ok && drivable(M, g, px + kf * c, pz + kf * (-s));
+  // all four probes evaluated (no short-circuit): they are independent, so
+  // their latencies overlap instead of adding up
+  const bool d0 = drivable(M, g, px, pz);
+  const bool d1 = drivable(M, g, px - kw * s, pz - kw * c);
+  const bool d2 = drivable(M, g, px + kw * s, pz + kw * c);
+  const bool d3 = drivable(M, g, px + kf * c, pz + kf * (-s));
+  const bool ok = d0 & d1 & d2 & d3;
   return ok && !collide(M, g, px, pz, c, s);
 }
 
@@ -383,18 +388,19 @@ __device__ inline bool lane_pos(const MapLds& M, const Geo& g, double x, double 
   // bezier_closest, 8 levels.  One endpoint distance is carried between levels:
   // the kept half's end was evaluated at the same t one level earlier, and the
   // function is deterministic, so the result is bit-identical to re-evaluating.
+  // The midpoint is evaluated once, before the comparison: it is the new end
+  // whichever half is kept (one evaluation, no divergent branches).
   double tb = 0.0, tt = 1.0;
   double db = dist2_to(cp, tb, x, z), dtp = dist2_to(cp, tt, x, z);
 #pragma unroll
   for (int n = 8; n > 0; --n) {
     const double mid = (tb + tt) * 0.5;
-    if (root_less(db, dtp)) {
-      tt = mid;
-      if (n > 1) dtp = dist2_to(cp, tt, x, z);
-    } else {
-      tb = mid;
-      if (n > 1) db = dist2_to(cp, tb, x, z);
-    }
+    const double dm = n > 1 ? dist2_to(cp, mid, x, z) : 0.0;
+    const bool left = root_less(db, dtp);
+    tt = left ? mid : tt;
+    dtp = left ? dm : dtp;
+    tb = left ? tb : mid;
+    db = left ? db : dm;
   }
   const double tm = (tb + tt) * 0.5;
   double qx, qy, qz;

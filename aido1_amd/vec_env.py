@@ -163,6 +163,10 @@ class VecEnv:
         self._check(rc, 'dt_step')
         return out
 
+    def capture(self, actions, out=None, render=None):
+        """StepGraph of len(actions) consecutive decisions (see StepGraph)."""
+        return StepGraph(self, actions, out or self.out, render)
+
     def step(self, actions):
         """Returns (obs [n,2] f32, (reward [n] f64, reward_mod [n] f64), done [n] bool,
         info) — the EnvironmentWrapper.step tuple, batched."""
@@ -226,3 +230,38 @@ class VecEnv:
                 arrs.append(None)
         p = [a.ctypes.data_as(ctypes.c_void_p) if a is not None else _NULL for a in arrs]
         self._check(self._L.dt_set_state(self._h, *p), 'dt_set_state')
+
+
+class StepGraph:
+    """k consecutive VecEnv.step launches (plus, optionally, the render of each
+    decision) captured once into a HIP graph and replayed as one launch.
+
+    The reference steps one Simulator per Python call; here a decision of all
+    envs is one kernel of ~25 us, so an eager loop is bound by the host's
+    per-call cost.  A graph issues the k kernels back to back with no host in
+    between.  Each launch reads its own slice actions[i] ([k, n, 2] f32 on the
+    env's device; the caller refills it between replays), writes `out`, and the
+    env state advances exactly as k eager step_into calls would (the auto-reset
+    spawn-ahead path is graph-safe: tests/test_gpu_step.py).  With `render`, k
+    must be a multiple of the ring's slot count so that the slots baked into the
+    graph continue the ring's order on every replay.
+    """
+
+    def __init__(self, env, actions, out, render=None):
+        if actions.dim() != 3 or tuple(actions.shape[1:]) != (env.n, 2):
+            raise ValueError('actions must be [k, %d, 2]' % env.n)
+        self.k = int(actions.shape[0])
+        if render is not None and self.k % render.slots:
+            raise ValueError('k (%d) must be a multiple of the ring slots (%d)'
+                             % (self.k, render.slots))
+        self.env, self.actions, self.out, self.render = env, actions, out, render
+        torch.cuda.synchronize(env.device)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            for i in range(self.k):
+                env.step_into(actions[i], out)
+                if render is not None:
+                    env.render_into(render, fresh=out.done)
+
+    def replay(self):
+        self.graph.replay()

@@ -36,13 +36,16 @@ sys.path.insert(0, REPO)
 METRIC = 'env-steps/sec (whole node) at 4096 envs/GPU; pose/reward max-abs-err vs CPU ref'
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
 
-# Algorithmic HBM bytes of one dt_step (step_kernel + spawn_kernel), DESIGN.md §3.1:
-# step, per env:   reads pose 24 + step_count,env_step 8 + action 8             = 40
-#                  writes pose 24 + counters 8 + reward 8 + reward_mod 8 + done 1 + obs 8 = 57
-# spawn, per env:  reads its done flag 1
-#        per reset: reads seed 8 + episode 4; writes pose 24 + counters 12 + obs 8 = 56
-STEP_BYTES_PER_ENV = 40 + 57 + 1
-SPAWN_BYTES_PER_RESET = 56
+# Algorithmic HBM bytes of one dt_step launch (step_kernel: step lanes + the
+# spawn-ahead refill blocks), DESIGN.md §3.1-3.2:
+# step, per env:    reads pose 24 + step_count,env_step 8 + action 8               = 40
+#                   writes pose 24 + counters 8 + reward 8 + reward_mod 8 + done 1 + obs 8 = 57
+# refill scan, per env: reads want 4 + both slot keys 8                          = 12
+# per reset:  step lane reads episode 4 + slot key 4 + slot pose/lane 40, writes
+#             episode 4 + want 4 (56); the refill of the consumed key reads seed 8,
+#             writes slot pose/lane 40 + key 4 (52)                               = 108
+STEP_BYTES_PER_ENV = 40 + 57 + 12
+SPAWN_BYTES_PER_RESET = 108
 
 
 def parse():
@@ -59,6 +62,9 @@ def parse():
     p.add_argument('--batch-size', type=int, default=0, help='train: 0 = config.json (64)')
     p.add_argument('--buffer-size', type=int, default=131072)
     p.add_argument('--updates-per-step', type=int, default=1)
+    p.add_argument('--graph-steps', type=int, default=30,
+                   help='lane config: decisions per HIP-graph replay (VecEnv.capture); '
+                        '0 = one eager launch per decision')
     p.add_argument('--seed', type=int, default=1234)
     p.add_argument('--cpu-seconds', type=float, default=1.5,
                    help='per-process seconds of the CPU baseline sample (0 = skip)')
@@ -173,31 +179,50 @@ def main():
     for i in range(args.warmup):
         one(i)
     torch.cuda.synchronize(dev)
+    G = args.graph_steps if render is None else 0
+    if G:
+        # the timed decisions as HIP graphs of G launches each, captured up
+        # front over their own action slices (StepGraph)
+        if args.steps % G:
+            raise SystemExit('--steps must be a multiple of --graph-steps')
+        graphs = [env.capture(actions[args.warmup + c * G:args.warmup + (c + 1) * G], out)
+                  for c in range(args.steps // G)]
+        gev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in graphs]
     env.stats(reset=True)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
+          for _ in range(args.steps)] if not G else []
     rev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)] if render is not None else None
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    for k in range(args.steps):
-        i = args.warmup + k
-        ev[k][0].record()
-        env.step_into(actions[i], out)
-        ev[k][1].record()
-        if render is not None:
-            rev[k][0].record()
-            env.render_into(render, fresh=out.done)
-            rev[k][1].record()
+    if G:
+        for c, gr in enumerate(graphs):
+            gev[c][0].record()
+            gr.replay()
+            gev[c][1].record()
+    else:
+        for k in range(args.steps):
+            i = args.warmup + k
+            ev[k][0].record()
+            env.step_into(actions[i], out)
+            ev[k][1].record()
+            if render is not None:
+                rev[k][0].record()
+                env.render_into(render, fresh=out.done)
+                rev[k][1].record()
     torch.cuda.synchronize(dev)
     if world > 1:
         dist.barrier()
     elapsed = time.perf_counter() - t0
     st = env.stats()
     env.check()
-    step_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    if G:  # per launch inside the graphs: replay time / launches (gaps included)
+        step_ms = float(np.mean([a.elapsed_time(b) for a, b in gev])) / G
+    else:
+        step_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     render_ms = float(np.mean([a.elapsed_time(b) for a, b in rev])) if rev else None
 
     sims = torch.tensor([st['sim_steps'], st['decisions'], st['resets']], dtype=torch.float64,
@@ -211,7 +236,7 @@ def main():
 
     if rank == 0:
         if render is None:
-            kname, kms = 'step_kernel+spawn_kernel', step_ms
+            kname, kms = 'step_kernel', step_ms
             bytes_per_launch = STEP_BYTES_PER_ENV * n + SPAWN_BYTES_PER_RESET * resets / max(
                 1.0, decisions / n)
         else:
@@ -240,6 +265,8 @@ def main():
                 'map': args.map, 'envs_per_gpu': n, 'repeat_actions': 3,
                 'actions': 'U[0,1)^2 wheel velocities, resident in HBM',
                 'auto_reset': True, 'global_envs': n * world,
+                'launch': ('HIP graphs of %d decisions (VecEnv.capture)' % G if G else
+                           'one eager launch per decision'),
                 'parallelism': 'env shards (%d x %d), no collective' % (world, n)},
             'counts': {'env_steps': sim_steps, 'decisions': decisions, 'resets': resets,
                        'elapsed_s': tmax},

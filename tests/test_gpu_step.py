@@ -219,3 +219,31 @@ def test_graph_capture_matches_eager(gpu):
         assert torch.equal(r1, env2.out.reward)
     for k in ('x', 'z', 'angle', 'episode'):
         assert np.array_equal(env1.get_state()[k], env2.get_state()[k])
+
+
+def test_step_graph_chunks_match_eager(gpu):
+    """VecEnv.capture: two replays of a 6-decision graph == 12 eager decisions
+    (auto-reset on; the spawn-ahead slots advance across replays)."""
+    n = 1024
+    env1, _ = make_pair(n, seed=11)
+    env2, _ = make_pair(n, seed=11)
+    env1.reset()
+    env2.reset()
+    rng = np.random.default_rng(3)
+    acts = torch.from_numpy(rng.uniform(0, 1, (12, n, 2)).astype(np.float32)).to(gpu)
+    buf = torch.empty(6, n, 2, dtype=torch.float32, device=gpu)
+    sg = env2.capture(buf)
+    rewards = []
+    for k in range(12):
+        env1.step_into(acts[k])
+        rewards.append(env1.out.reward.clone())
+    for c in range(2):
+        buf.copy_(acts[6 * c:6 * c + 6])
+        sg.replay()
+        torch.cuda.synchronize()
+        assert torch.equal(rewards[6 * c + 5], env2.out.reward)
+    for k in ('x', 'z', 'angle', 'episode', 'step_count', 'env_step'):
+        assert np.array_equal(env1.get_state()[k], env2.get_state()[k])
+    assert env1.stats() == env2.stats()
+    env1.check()
+    env2.check()

@@ -15,7 +15,7 @@ run() {  # run <name> <timeout> cmd...; stop on fault-like exit codes
   case $rc in 0|1|5) return 0;; *) echo "fatal rc=$rc, stopping"; exit $rc;; esac
 }
 run smi 60 rocm-smi --showproductname
-run pytest_gpu 900 python -m pytest $TESTS -x -q -m gpu
+run pytest_gpu 900 python -u -m pytest $TESTS -x -q -m gpu --timeout 180 --timeout-method thread
 run bench 600 python bench.py --steps $STEPS --warmup 30 ${BENCH_ARGS}
 if [ -n "$RENDER" ]; then
   run bench_render 600 python bench.py --config render --steps $STEPS --warmup 30 --cpu-seconds 0
