@@ -515,6 +515,27 @@ int dt_create(const dt_config* cfg, const dt_map* map, uint64_t seed, int32_t n_
     }
   }
   const int C = map->curve_start[T];
+  // ground-plane curve records (dt::kCurveRec); the step math drops the y terms
+  std::vector<double> rec((size_t)C * dt::kCurveRec);
+  for (int k = 0; k < C; ++k) {
+    const double* cp = map->curves + 12 * (size_t)k;
+    const double* hd = map->headings + 3 * (size_t)k;
+    if (cp[1] != 0.0 || cp[4] != 0.0 || cp[7] != 0.0 || cp[10] != 0.0 || hd[1] != 0.0) {
+      g_create_err = "dt_create: curve " + std::to_string(k) + " leaves the ground plane (y != 0)";
+      return DT_E_ARG;
+    }
+    double* r = rec.data() + (size_t)k * dt::kCurveRec;
+    for (int i = 0; i < 4; ++i) {
+      r[2 * i] = cp[3 * i];
+      r[2 * i + 1] = cp[3 * i + 2];
+    }
+    for (int i = 0; i < 3; ++i) {  // bezier_tangent's differences, as it computes them
+      r[8 + 2 * i] = cp[3 * (i + 1)] - cp[3 * i];
+      r[8 + 2 * i + 1] = cp[3 * (i + 1) + 2] - cp[3 * i + 2];
+    }
+    r[14] = hd[0];
+    r[15] = hd[2];
+  }
   const int NO = map->n_objects, NS = map->n_spawn_objects;
   if (NO < 0 || NO > 256 || NS < 0 || NS > 256 || (NO > 0 && !map->objects) ||
       (NS > 0 && !map->spawn_objects)) {
@@ -589,7 +610,7 @@ int dt_create(const dt_config* cfg, const dt_map* map, uint64_t seed, int32_t n_
     return DT_E_HIP;
   };
   if (hipSetDevice(device) != hipSuccess) return fail("hipSetDevice failed");
-  // map image: curves | headings | objects | spawn objects | curve_start (u16) | kind |
+  // map image: curve records | objects | spawn objects | curve_start (u16) | kind |
   // drivable
   const size_t lds = dt::map_lds_bytes(T, (int)drv.size(), C, NO, NS);
   if (lds > dt::kMaxMapLdsBytes) {
@@ -599,18 +620,17 @@ int dt_create(const dt_config* cfg, const dt_map* map, uint64_t seed, int32_t n_
   }
   std::vector<uint16_t> cs(T + 1);
   for (int t = 0; t <= T; ++t) cs[t] = (uint16_t)map->curve_start[t];
-  const size_t cb = (size_t)C * 12 * 8, hb = (size_t)C * 3 * 8,
+  const size_t cb = rec.size() * 8,
                ob = (size_t)NO * DT_OBJ_STRIDE * 8, spb = (size_t)NS * 4 * 8,
                sb16 = ((size_t)(T + 1) * 2 + 15) & ~15ul, kb = ((size_t)T + 15) & ~15ul,
                db = (drv.size() * 2 + 15) & ~15ul;
-  if (hipMalloc(&h->map_buf, cb + hb + ob + spb + sb16 + kb + db) != hipSuccess)
+  if (hipMalloc(&h->map_buf, cb + ob + spb + sb16 + kb + db) != hipSuccess)
     return fail("hipMalloc(map)");
   char* mb = (char*)h->map_buf;
-  char* m_cs = mb + cb + hb + ob + spb;
-  if ((cb && hipMemcpy(mb, map->curves, cb, hipMemcpyHostToDevice) != hipSuccess) ||
-      (hb && hipMemcpy(mb + cb, map->headings, hb, hipMemcpyHostToDevice) != hipSuccess) ||
-      (ob && hipMemcpy(mb + cb + hb, map->objects, ob, hipMemcpyHostToDevice) != hipSuccess) ||
-      (spb && hipMemcpy(mb + cb + hb + ob, map->spawn_objects, spb, hipMemcpyHostToDevice) !=
+  char* m_cs = mb + cb + ob + spb;
+  if ((cb && hipMemcpy(mb, rec.data(), cb, hipMemcpyHostToDevice) != hipSuccess) ||
+      (ob && hipMemcpy(mb + cb, map->objects, ob, hipMemcpyHostToDevice) != hipSuccess) ||
+      (spb && hipMemcpy(mb + cb + ob, map->spawn_objects, spb, hipMemcpyHostToDevice) !=
                   hipSuccess) ||
       hipMemcpy(m_cs, cs.data(), (size_t)(T + 1) * 2, hipMemcpyHostToDevice) != hipSuccess ||
       hipMemcpy(m_cs + sb16, map->kind, (size_t)T, hipMemcpyHostToDevice) != hipSuccess ||
@@ -625,9 +645,8 @@ int dt_create(const dt_config* cfg, const dt_map* map, uint64_t seed, int32_t n_
   h->map.n_obj = NO;
   h->map.n_spawn_obj = NS;
   h->map.curves = (const double*)mb;
-  h->map.headings = (const double*)(mb + cb);
-  h->map.obj = (const double*)(mb + cb + hb);
-  h->map.spawn_obj = (const double*)(mb + cb + hb + ob);
+  h->map.obj = (const double*)(mb + cb);
+  h->map.spawn_obj = (const double*)(mb + cb + ob);
   h->map.curve_start = (const uint16_t*)m_cs;
   h->map.kind = (const int8_t*)(m_cs + sb16);
   h->map.drivable = (const int16_t*)(m_cs + sb16 + kb);

@@ -60,11 +60,22 @@ __device__ inline void wave_count(unsigned long long* p, unsigned v, unsigned vm
 }
 
 
+// A lane curve as the step math reads it.  Every map curve lies in the ground
+// plane (y = 0 for each control point and heading; dt_create checks), so the
+// y terms of bezier_point / bezier_tangent / get_lane_pos2 are exact zeros and
+// drop out without changing a result: a term b*b = +0 added to a*a >= +0, and
+// 0 * (finite) = +-0 added to a nonzero value, leave the sums unchanged (a
+// zero's sign never reaches a comparison or a nonzero output).  Per curve:
+//   [0..7]   P0x P0z P1x P1z P2x P2z P3x P3z     control points
+//   [8..13]  (P1-P0), (P2-P1), (P3-P2) in x, z  tangent differences (host-made,
+//            the same subtractions bezier_tangent does)
+//   [14..15] heading x, z                        (P3-P0) / np.linalg.norm quirk
+constexpr int kCurveRec = 16;
+
 // Map image in device memory; staged into LDS by each block.
 struct MapDev {
   int32_t width, height, n_tiles, n_drivable, n_curves, n_obj, n_spawn_obj;
-  const double* curves;     // [C,4,3]
-  const double* headings;   // [C,3]
+  const double* curves;     // [C,kCurveRec] ground-plane curve records (CurveRec)
   const double* obj;        // [n_obj, DT_OBJ_STRIDE] collidable static objects
   const double* spawn_obj;  // [n_spawn_obj, 4] x, y, z, spawn radius
   const uint16_t* curve_start;  // [T+1]
@@ -75,7 +86,6 @@ struct MapDev {
 // LDS view of the map.
 struct MapLds {
   const double* curves;
-  const double* headings;
   const double* obj;
   const double* spawn_obj;
   const uint16_t* curve_start;
@@ -86,7 +96,7 @@ struct MapLds {
 
 __host__ __device__ inline size_t map_lds_bytes(int n_tiles, int n_drivable, int n_curves,
                                                 int n_obj = 0, int n_spawn_obj = 0) {
-  size_t b = (size_t)n_curves * (12 + 3) * sizeof(double);
+  size_t b = (size_t)n_curves * kCurveRec * sizeof(double);
   b += ((size_t)n_obj * DT_OBJ_STRIDE + (size_t)n_spawn_obj * 4) * sizeof(double);
   b += ((size_t)(n_tiles + 1) * 2 + 15) & ~(size_t)15;
   b += ((size_t)n_tiles + 15) & ~(size_t)15;
@@ -97,15 +107,13 @@ __host__ __device__ inline size_t map_lds_bytes(int n_tiles, int n_drivable, int
 // Cooperative copy of the map into LDS; every thread of the block calls it.
 __device__ inline MapLds stage_map(const MapDev& m, unsigned char* lds) {
   double* cv = reinterpret_cast<double*>(lds);
-  double* hd = cv + (size_t)m.n_curves * 12;
-  double* ob = hd + (size_t)m.n_curves * 3;
+  double* ob = cv + (size_t)m.n_curves * kCurveRec;
   double* so = ob + (size_t)m.n_obj * DT_OBJ_STRIDE;
   uint16_t* cs = reinterpret_cast<uint16_t*>(so + (size_t)m.n_spawn_obj * 4);
   int8_t* kd = reinterpret_cast<int8_t*>(cs) + (((size_t)(m.n_tiles + 1) * 2 + 15) & ~(size_t)15);
   int16_t* dv = reinterpret_cast<int16_t*>(kd + (((size_t)m.n_tiles + 15) & ~(size_t)15));
   const int tid = threadIdx.x, nt = blockDim.x;
-  for (int i = tid; i < m.n_curves * 12; i += nt) cv[i] = m.curves[i];
-  for (int i = tid; i < m.n_curves * 3; i += nt) hd[i] = m.headings[i];
+  for (int i = tid; i < m.n_curves * kCurveRec; i += nt) cv[i] = m.curves[i];
   for (int i = tid; i < m.n_obj * DT_OBJ_STRIDE; i += nt) ob[i] = m.obj[i];
   for (int i = tid; i < m.n_spawn_obj * 4; i += nt) so[i] = m.spawn_obj[i];
   for (int i = tid; i <= m.n_tiles; i += nt) cs[i] = m.curve_start[i];
@@ -114,7 +122,6 @@ __device__ inline MapLds stage_map(const MapDev& m, unsigned char* lds) {
   __syncthreads();
   MapLds r;
   r.curves = cv;
-  r.headings = hd;
   r.obj = ob;
   r.spawn_obj = so;
   r.curve_start = cs;
@@ -182,11 +189,18 @@ struct Geo {  // constants hoisted per launch
 // floor), via the reciprocal: RN(v * inv_ts) is within 2 ulp of RN(v / ts), so
 // their floors can only differ when the quotient is within a few ulp of an
 // integer — only then is the real division done.
+// The rare exact paths are out-of-line calls: as inline code the compiler
+// speculates them (the division and sqrt are single IR operations) and every
+// lane would pay for them on every call.
+static __device__ __noinline__ double floor_div_exact(double v, double ts) { return floor(v / ts); }
+
 __device__ inline double floor_div_ts(double v, const Geo& g) {
   const double q = v * g.inv_ts;
   const double f = floor(q);
-  const double tol = 1e-12 * (fabs(q) + 1.0);
-  if (q - f < tol || (f + 1.0) - q < tol) return floor(v / g.ts);
+  const double r = q - f;
+  // |q| < 2^9 on any map: a few ulp are < 1e-12; beyond, both floors are off
+  // the grid and the tile is -1 either way
+  if (r < 1e-9 || r > 1.0 - 1e-9) return floor_div_exact(v, g.ts);
   return f;
 }
 
@@ -317,41 +331,46 @@ __device__ inline bool valid_pose(const MapLds& M, const Geo& g, double x, doubl
   return ok && !collide(M, g, px, pz, c, s);
 }
 
-// bezier_point (A9): coefficients are exact dyadics for the bisection's t values
-__device__ inline void bez_xz(const double* __restrict__ cp, double t, double& ox, double& oy,
-                              double& oz) {
+// bezier_point (A9) in the ground plane: coefficients are exact dyadics for
+// the bisection's t values
+__device__ inline void bez_xz(const double* __restrict__ cv, double t, double& ox, double& oz) {
   const double u = 1.0 - t;
   const double c0 = u * u * u, c1 = 3.0 * t * (u * u), c2 = 3.0 * (t * t) * u, c3 = t * t * t;
-  double px = c0 * cp[0], py = c0 * cp[1], pz = c0 * cp[2];
-  px = px + c1 * cp[3];
-  py = py + c1 * cp[4];
-  pz = pz + c1 * cp[5];
-  px = px + c2 * cp[6];
-  py = py + c2 * cp[7];
-  pz = pz + c2 * cp[8];
-  px = px + c3 * cp[9];
-  py = py + c3 * cp[10];
-  pz = pz + c3 * cp[11];
+  double px = c0 * cv[0], pz = c0 * cv[1];
+  px = px + c1 * cv[2];
+  pz = pz + c1 * cv[3];
+  px = px + c2 * cv[4];
+  pz = pz + c2 * cv[5];
+  px = px + c3 * cv[6];
+  pz = pz + c3 * cv[7];
   ox = px;
-  oy = py;
   oz = pz;
 }
 
 // squared distance |B(t) - p|^2, summed as np.linalg.norm's dot (unfused, in order)
-__device__ inline double dist2_to(const double* __restrict__ cp, double t, double x, double z) {
-  double bx, by, bz;
-  bez_xz(cp, t, bx, by, bz);
-  const double a = bx - x, b = by - 0.0, c = bz - z;
-  return (a * a + b * b) + c * c;
+__device__ inline double dist2_to(const double* __restrict__ cv, double t, double x, double z) {
+  double bx, bz;
+  bez_xz(cv, t, bx, bz);
+  const double a = bx - x, c = bz - z;
+  return a * a + c * c;
+}
+
+// the same at an end point: B(0) = P0 and B(1) = P3 exactly (the other terms
+// are +-0), so only the distance is left to compute
+__device__ inline double dist2_pt(double px, double pz, double x, double z) {
+  const double a = px - x, c = pz - z;
+  return a * a + c * c;
 }
 
 // sqrt(a) < sqrt(b), the comparison bezier_closest makes, decided on the
 // squares: sqrt is monotone, so only when a and b are within a few ulp (where
 // rounding could make the roots equal) are the roots taken.
+static __device__ __noinline__ bool root_less_exact(double a, double b) { return sqrt(a) < sqrt(b); }
+
 __device__ inline bool root_less(double a, double b) {
   const double d = b - a;
   if (fabs(d) > 8.0 * 2.220446049250313e-16 * fmax(a, b)) return a < b;
-  return sqrt(a) < sqrt(b);
+  return root_less_exact(a, b);
 }
 
 // angle_rad = acos(dot_dir), negated right of the tangent (get_lane_pos2);
@@ -377,25 +396,25 @@ __device__ inline bool lane_pos(const MapLds& M, const Geo& g, double x, double 
   int best = k0;
   double bd = 0.0;
   for (int k = k0; k < k1; ++k) {
-    const double* hd = M.headings + 3 * k;
-    const double d = (hd[0] * dx + hd[1] * 0.0) + hd[2] * dz;
+    const double* hd = M.curves + kCurveRec * k + 14;
+    const double d = hd[0] * dx + hd[1] * dz;
     if (k == k0 || d > bd) {
       bd = d;
       best = k;
     }
   }
-  const double* cp = M.curves + 12 * best;
+  const double* cv = M.curves + kCurveRec * best;
   // bezier_closest, 8 levels.  One endpoint distance is carried between levels:
   // the kept half's end was evaluated at the same t one level earlier, and the
   // function is deterministic, so the result is bit-identical to re-evaluating.
   // The midpoint is evaluated once, before the comparison: it is the new end
   // whichever half is kept (one evaluation, no divergent branches).
   double tb = 0.0, tt = 1.0;
-  double db = dist2_to(cp, tb, x, z), dtp = dist2_to(cp, tt, x, z);
+  double db = dist2_pt(cv[0], cv[1], x, z), dtp = dist2_pt(cv[6], cv[7], x, z);
 #pragma unroll
   for (int n = 8; n > 0; --n) {
     const double mid = (tb + tt) * 0.5;
-    const double dm = n > 1 ? dist2_to(cp, mid, x, z) : 0.0;
+    const double dm = n > 1 ? dist2_to(cv, mid, x, z) : 0.0;
     const bool left = root_less(db, dtp);
     tt = left ? mid : tt;
     dtp = left ? dm : dtp;
@@ -403,27 +422,24 @@ __device__ inline bool lane_pos(const MapLds& M, const Geo& g, double x, double 
     db = left ? db : dm;
   }
   const double tm = (tb + tt) * 0.5;
-  double qx, qy, qz;
-  bez_xz(cp, tm, qx, qy, qz);
+  double qx, qz;
+  bez_xz(cv, tm, qx, qz);
   const double u = 1.0 - tm;
   const double a0 = 3.0 * (u * u), a1 = 6.0 * u * tm, a2 = 3.0 * (tm * tm);
-  double tx = a0 * (cp[3] - cp[0]), ty = a0 * (cp[4] - cp[1]), tz = a0 * (cp[5] - cp[2]);
-  tx = tx + a1 * (cp[6] - cp[3]);
-  ty = ty + a1 * (cp[7] - cp[4]);
-  tz = tz + a1 * (cp[8] - cp[5]);
-  tx = tx + a2 * (cp[9] - cp[6]);
-  ty = ty + a2 * (cp[10] - cp[7]);
-  tz = tz + a2 * (cp[11] - cp[8]);
-  const double nn = sqrt((tx * tx + ty * ty) + tz * tz);
+  double tx = a0 * cv[8], tz = a0 * cv[9];
+  tx = tx + a1 * cv[10];
+  tz = tz + a1 * cv[11];
+  tx = tx + a2 * cv[12];
+  tz = tz + a2 * cv[13];
+  const double nn = sqrt(tx * tx + tz * tz);
   tx = tx / nn;
-  ty = ty / nn;
   tz = tz / nn;
-  double dot = (dx * tx + 0.0 * ty) + dz * tz;
+  double dot = dx * tx + dz * tz;
   dot = dot > 1.0 ? 1.0 : dot;
   dot = dot < -1.0 ? -1.0 : dot;
   const double rx = 0.0 - tz, rz = tx;
   const double px = x - qx, pz = z - qz;
-  const double dist = (px * rx + (0.0 - qy) * 0.0) + pz * rz;
+  const double dist = px * rx + pz * rz;
   lp[0] = dist;
   lp[1] = dot;
   lp[2] = (dx * rx + 0.0) + dz * rz;  // side of the tangent (sign of the angle)
