@@ -54,13 +54,14 @@ struct LineDev {
   uint64_t dil_mask;           // k x k ellipse, bit (dy+3)*7 + (dx+3)
   int32_t dil_r;               // k / 2
   int32_t canny_lo, canny_hi;  // cvFloor of the thresholds (L1)
+  uint32_t pal_bits[2];        // colour bits of palette entries 0-3 / 4-7 (one byte each)
 };
 
 // bits of the per-pixel work byte
 constexpr uint8_t B_WHITE = 1, B_YELLOW = 2, B_RED = 4, B_DIR_SHIFT = 3;  // dir: 2 bits
 constexpr uint8_t B_CAND = 0x20, B_EDGE = 0x40;
 
-__device__ inline void bgr_to_hsv(const int* __restrict__ sdiv, const int* __restrict__ hdiv,
+__host__ __device__ inline void bgr_to_hsv(const int* __restrict__ sdiv, const int* __restrict__ hdiv,
                                   int b, int g, int r, int& h, int& s, int& v) {
   v = b > g ? b : g;
   v = v > r ? v : r;
@@ -76,11 +77,11 @@ __device__ inline void bgr_to_hsv(const int* __restrict__ sdiv, const int* __res
   h = hh;
 }
 
-__device__ inline bool in_range(const uint8_t lo[3], const uint8_t hi[3], int h, int s, int v) {
+__host__ __device__ inline bool in_range(const uint8_t lo[3], const uint8_t hi[3], int h, int s, int v) {
   return lo[0] <= h && h <= hi[0] && lo[1] <= s && s <= hi[1] && lo[2] <= v && v <= hi[2];
 }
 
-__device__ inline uint8_t color_bits(const LineDev& L, int h, int s, int v) {
+__host__ __device__ inline uint8_t color_bits(const LineDev& L, int h, int s, int v) {
   uint8_t bits = 0;
   if (in_range(L.lo[0], L.hi[0], h, s, v)) bits |= B_WHITE;
   if (in_range(L.lo[1], L.hi[1], h, s, v)) bits |= B_YELLOW;

@@ -124,6 +124,14 @@ LineDev to_line_dev(const dt_line_params& p) {
   }
   L.canny_lo = (int)floor(lo);
   L.canny_hi = (int)floor(hi);
+  // colour bits of each palette entry (HSV + inRange once per parameter set)
+  L.pal_bits[0] = L.pal_bits[1] = 0;
+  for (int i = 0; i < PAL_N; ++i) {
+    const uint32_t q = kPalette[i];
+    int hh, ss, vv;
+    bgr_to_hsv(kHsvHost.sdiv, kHsvHost.hdiv, q & 255, (q >> 8) & 255, (q >> 16) & 255, hh, ss, vv);
+    L.pal_bits[i >> 2] |= (uint32_t)color_bits(L, hh, ss, vv) << (8 * (i & 3));
+  }
   return L;
 }
 
@@ -347,6 +355,7 @@ struct FusedLds {
   uint32_t pal_swar[PAL_N];
   float pal_gray[PAL_N];
   uint32_t bits_lo, bits_hi;  // colour bits of palette entries 0-3 / 4-7 (one byte each)
+  View view;
   int32_t nlist, nweak;
   int8_t kind[dt::kMaxLdsTiles];
 };
@@ -482,65 +491,72 @@ __global__ __launch_bounds__(1024) void render_kernel(RenderArgs a) {
     S.pal_gray[tid] = (float)((rr * 0.2125 + gg * 0.7154) + bb * 0.0721);
   }
   if (tid == 0) {
-    uint32_t lo = 0, hi = 0;
-    const HsvTables& T = c_hsv;
-    for (int i = 0; i < PAL_N; ++i) {
-      const uint32_t p = kPalette[i];
-      int h, sat, v;
-      bgr_to_hsv(T.sdiv, T.hdiv, p & 255, (p >> 8) & 255, (p >> 16) & 255, h, sat, v);
-      const uint32_t b = color_bits(L, h, sat, v);
-      if (i < 4) lo |= b << (8 * i); else hi |= b << (8 * (i - 4));
-    }
-    S.bits_lo = lo;
-    S.bits_hi = hi;
+    S.bits_lo = L.pal_bits[0];
+    S.bits_hi = L.pal_bits[1];
     S.nlist = 0;
     S.nweak = 0;
   }
   for (int i = tid; i < a.width * a.height; i += blockDim.x) S.kind[i] = a.kind[i];
 
-  const double ang = a.angle[e];
-  double sd, cd;
-  sincos(ang, &sd, &cd);
-  View V;
-  V.cx = (float)(a.x[e] + a.cam_fwd * cd);
-  V.cz = (float)(a.z[e] + a.cam_fwd * (-sd));
-  V.dirx = (float)cd;
-  V.dirz = -(float)sd;
-  V.rx = (float)sd;
-  V.rz = (float)cd;
+  if (tid == 64) {  // the camera frame, once per workgroup (wave 1; wave 0 has the palette)
+    const double ang = a.angle[e];
+    double sd, cd;
+    sincos(ang, &sd, &cd);
+    View v;
+    v.cx = (float)(a.x[e] + a.cam_fwd * cd);
+    v.cz = (float)(a.z[e] + a.cam_fwd * (-sd));
+    v.dirx = (float)cd;
+    v.dirz = -(float)sd;
+    v.rx = (float)sd;
+    v.rz = (float)cd;
+    S.view = v;
+  }
   __syncthreads();
+  const View V = S.view;
 
-  // phase 0: background, one word (4 pixels) per lane
-  for (int w = tid; w < NW && !(a.skip & 1); w += blockDim.x) {
-    const int r = w / WPR, c0 = 4 * (w - r * WPR);
+  // phase 0: background, a 16-pixel span (4 words) per lane.  Tiles are convex
+  // and each coordinate is a monotone float function of the column, so when
+  // both end pixels of a span (or word) fall in one tile, all between do: one
+  // lookup and one 16-byte store for the common uniform span.
+  for (int q = tid; q < NW / 4 && !(a.skip & 1); q += blockDim.x) {
+    const int r = q / (WPR / 4), c0 = 16 * (q - r * (WPR / 4));
     const float f = (119.5f - (float)r) * kRes;
     const float bx = V.cx + f * V.dirx, bz = V.cz + f * V.dirz;
-    // tiles are convex and each coordinate is a monotone float function of the
-    // column, so when both end pixels of the word fall in one tile all four do
-    float fi4[4], fj4[4];
+    float fi[16], fj[16];
 #pragma unroll
-    for (int i = 0; i < 4; i += 3) {
+    for (int i = 0; i < 16; i += 15) {
       const float l = ((float)(c0 + i) - 79.5f) * kRes;
       const float wx = bx + l * V.rx, wz = bz + l * V.rz;
-      fi4[i] = floorf(wx * a.inv_ts);
-      fj4[i] = floorf(wz * a.inv_ts);
+      fi[i] = floorf(wx * a.inv_ts);
+      fj[i] = floorf(wz * a.inv_ts);
     }
-    uint32_t word;
-    if (fi4[0] == fi4[3] && fj4[0] == fj4[3]) {
-      word = bg_color(S, a, fi4[0], fj4[0]) * 0x01010101u;
+    uint4 words;
+    if (fi[0] == fi[15] && fj[0] == fj[15]) {
+      const uint32_t wd = bg_color(S, a, fi[0], fj[0]) * 0x01010101u;
+      words = make_uint4(wd, wd, wd, wd);
     } else {
 #pragma unroll
-      for (int i = 1; i < 3; ++i) {
+      for (int i = 1; i < 15; ++i) {
         const float l = ((float)(c0 + i) - 79.5f) * kRes;
         const float wx = bx + l * V.rx, wz = bz + l * V.rz;
-        fi4[i] = floorf(wx * a.inv_ts);
-        fj4[i] = floorf(wz * a.inv_ts);
+        fi[i] = floorf(wx * a.inv_ts);
+        fj[i] = floorf(wz * a.inv_ts);
       }
-      word = 0;
+      uint32_t wd[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) word |= bg_color(S, a, fi4[i], fj4[i]) << (8 * i);
+      for (int k = 0; k < 4; ++k) {
+        const int i0 = 4 * k, i3 = 4 * k + 3;
+        if (fi[i0] == fi[i3] && fj[i0] == fj[i3]) {
+          wd[k] = bg_color(S, a, fi[i0], fj[i0]) * 0x01010101u;
+        } else {
+          wd[k] = 0;
+#pragma unroll
+          for (int i = 0; i < 4; ++i) wd[k] |= bg_color(S, a, fi[i0 + i], fj[i0 + i]) << (8 * i);
+        }
+      }
+      words = make_uint4(wd[0], wd[1], wd[2], wd[3]);
     }
-    S.img[w] = word;
+    *reinterpret_cast<uint4*>(S.img + 4 * q) = words;
   }
   __syncthreads();
   uint8_t* img8 = reinterpret_cast<uint8_t*>(S.img);
@@ -551,58 +567,75 @@ __global__ __launch_bounds__(1024) void render_kernel(RenderArgs a) {
   }
   __syncthreads();
 
-  // phase 1: exact uniformity test of the 3 x 6 byte neighbourhood, grey
+  // phase 1: exact uniformity test of the 3 x 6 byte neighbourhood, grey.  A
+  // lane takes a column of 4 words (rows 4g..4g+3 of word column cw), so the
+  // 6 x 3 words around them are loaded once for all four, and a wave's
+  // grey stores of one row are contiguous.
   const bool fresh = a.fresh != nullptr && a.fresh[e] != 0;
   float* gbase = a.gray ? a.gray + (size_t)e * a.slots * NPIX : nullptr;
-  for (int w0 = 0; w0 < NW && !(a.skip & 4); w0 += blockDim.x) {
-    const int w = w0 + tid;
-    const bool act = w < NW;
-    bool uni = false;
+  constexpr int kRowsPerLane = 4, NQ = NW / kRowsPerLane;
+  for (int q0 = 0; q0 < NQ && !(a.skip & 4); q0 += blockDim.x) {
+    const int q = q0 + tid;
+    const bool act = q < NQ;
+    bool uni[kRowsPerLane] = {false, false, false, false};
+    int wq[kRowsPerLane] = {0, 0, 0, 0};
     if (act) {
-      const int r = w / WPR, cw = w - r * WPR;
-      const int ru = r > 0 ? r - 1 : 0, rd = r < H - 1 ? r + 1 : H - 1;
-      // all nine words loaded up front, combined branch-free.  Side words at
-      // the image edge clamp to the word itself: BORDER_REPLICATE repeats the
-      // edge pixel, whose byte the mid / up / down comparisons already cover.
+      const int rg = q / WPR, cw = q - rg * WPR, r0 = kRowsPerLane * rg;
+      // side words at the image edge clamp to the word itself: BORDER_REPLICATE
+      // repeats the edge pixel, whose byte the mid / up / down comparisons
+      // already cover; rows clamp the same way
       const int cl = cw > 0 ? cw - 1 : cw, cr = cw < WPR - 1 ? cw + 1 : cw;
-      const uint32_t mid = S.img[w];
-      const uint32_t up = S.img[ru * WPR + cw], dn = S.img[rd * WPR + cw];
-      const uint32_t ul = S.img[ru * WPR + cl], ml = S.img[r * WPR + cl],
-                     dl = S.img[rd * WPR + cl];
-      const uint32_t ur = S.img[ru * WPR + cr], mr = S.img[r * WPR + cr],
-                     dr = S.img[rd * WPR + cr];
-      const uint32_t b = mid & 255u;
-      const uint32_t rep = b * 0x01010101u;
-      const uint32_t diff = (mid ^ rep) | (up ^ rep) | (dn ^ rep) |
-                            (((ul >> 24) ^ b) | ((ml >> 24) ^ b) | ((dl >> 24) ^ b)) |
-                            (((ur ^ b) | (mr ^ b) | (dr ^ b)) & 255u);
-      uni = diff == 0u;
-      if (uni) *reinterpret_cast<uint2*>(S.work + 4 * w) = make_uint2(0u, 0u);
-      if (gbase) {
-        float4 g;
-        g.x = S.pal_gray[mid & 255u];
-        g.y = S.pal_gray[(mid >> 8) & 255u];
-        g.z = S.pal_gray[(mid >> 16) & 255u];
-        g.w = S.pal_gray[mid >> 24];
-        if (fresh) {
-#pragma clang loop vectorize(disable) interleave(disable)
-          for (int sl = 0; sl < a.slots; ++sl)  // 16-B stores, not split by the vectoriser
-            *reinterpret_cast<float4*>(gbase + sl * NPIX + 4 * w) = g;
-        } else {
-          *reinterpret_cast<float4*>(gbase + a.slot * NPIX + 4 * w) = g;
-        }
+      uint32_t col[kRowsPerLane + 2][3];
+#pragma unroll
+      for (int i = 0; i < kRowsPerLane + 2; ++i) {
+        int rr = r0 - 1 + i;
+        rr = rr < 0 ? 0 : (rr > H - 1 ? H - 1 : rr);
+        col[i][0] = S.img[rr * WPR + cl];
+        col[i][1] = S.img[rr * WPR + cw];
+        col[i][2] = S.img[rr * WPR + cr];
       }
-      if (a.rgb) {
-        uint8_t* o = a.rgb + ((size_t)e * NPIX + 4 * w) * 3;
-        for (int i = 0; i < 4; ++i) {
-          const uint32_t p = kPalette[(mid >> (8 * i)) & 255u];
-          o[3 * i + 0] = (p >> 16) & 255;
-          o[3 * i + 1] = (p >> 8) & 255;
-          o[3 * i + 2] = p & 255;
+#pragma unroll
+      for (int k = 0; k < kRowsPerLane; ++k) {
+        const int w = (r0 + k) * WPR + cw;
+        wq[k] = w;
+        const uint32_t mid = col[k + 1][1], up = col[k][1], dn = col[k + 2][1];
+        const uint32_t b = mid & 255u;
+        const uint32_t rep = b * 0x01010101u;
+        const uint32_t diff =
+            (mid ^ rep) | (up ^ rep) | (dn ^ rep) |
+            (((col[k][0] >> 24) ^ b) | ((col[k + 1][0] >> 24) ^ b) | ((col[k + 2][0] >> 24) ^ b)) |
+            (((col[k][2] ^ b) | (col[k + 1][2] ^ b) | (col[k + 2][2] ^ b)) & 255u);
+        uni[k] = diff == 0u;
+        // every word's work entries start at 0; phase 2a overwrites the listed ones
+        *reinterpret_cast<uint2*>(S.work + 4 * w) = make_uint2(0u, 0u);
+        if (gbase) {
+          float4 g;
+          g.x = S.pal_gray[mid & 255u];
+          g.y = S.pal_gray[(mid >> 8) & 255u];
+          g.z = S.pal_gray[(mid >> 16) & 255u];
+          g.w = S.pal_gray[mid >> 24];
+          if (fresh) {
+#pragma clang loop vectorize(disable) interleave(disable)
+            for (int sl = 0; sl < a.slots; ++sl)  // 16-B stores, not split by the vectoriser
+              *reinterpret_cast<float4*>(gbase + sl * NPIX + 4 * w) = g;
+          } else {
+            *reinterpret_cast<float4*>(gbase + a.slot * NPIX + 4 * w) = g;
+          }
+        }
+        if (a.rgb) {
+          uint8_t* o = a.rgb + ((size_t)e * NPIX + 4 * w) * 3;
+          for (int i = 0; i < 4; ++i) {
+            const uint32_t p = kPalette[(mid >> (8 * i)) & 255u];
+            o[3 * i + 0] = (p >> 16) & 255;
+            o[3 * i + 1] = (p >> 8) & 255;
+            o[3 * i + 2] = p & 255;
+          }
         }
       }
     }
-    wave_push(&S.nlist, S.list, NW, act && !uni, (uint16_t)w);
+#pragma unroll
+    for (int k = 0; k < kRowsPerLane; ++k)
+      wave_push(&S.nlist, S.list, NW, act && !uni[k], (uint16_t)wq[k]);
   }
   __syncthreads();
 
@@ -793,7 +826,7 @@ int dt_render_init(dt_handle* h, const dt_map* map) {
   h->render_skip = sk ? atoi(sk) : 0;
   const char* th = getenv("DTSIM_RENDER_THREADS");  // tuning: workgroup size
   h->render_threads = th ? atoi(th) : kRenderThreads;
-  if (h->render_threads < 64 || h->render_threads > 1024 || (h->render_threads & 63))
+  if (h->render_threads < 128 || h->render_threads > 1024 || (h->render_threads & 63))
     h->render_threads = kRenderThreads;
   return DT_OK;
 }
