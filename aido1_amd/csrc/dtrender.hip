@@ -151,7 +151,11 @@ __device__ inline void load_tables(Lds& S) {
 }
 
 // Bresenham (utils/bresenham.py:6-34) into the palette image.
-__device__ inline void draw_line(uint8_t* img, int x0, int y0, int x1, int y1, uint8_t col) {
+// LDS byte pointer: 32-bit addressing (a generic pointer makes every pixel
+// address a 64-bit multiply-add)
+using lds_u8 = __attribute__((address_space(3))) uint8_t;
+
+__device__ inline void draw_line(lds_u8* img, int x0, int y0, int x1, int y1, uint8_t col) {
   int dx = x1 - x0, dy = y1 - y0;
   const int xsign = dx > 0 ? 1 : -1, ysign = dy > 0 ? 1 : -1;
   dx = dx < 0 ? -dx : dx;
@@ -163,15 +167,18 @@ __device__ inline void draw_line(uint8_t* img, int x0, int y0, int x1, int y1, u
     const int t = dx; dx = dy; dy = t;
     xx = 0; xy = ysign; yx = xsign; yy = 0;
   }
-  int D = 2 * dy - dx, y = 0;
+  // the pixel of step x is (x0 + x*xx + y*yx, y0 + x*xy + y*yy); tracked
+  // incrementally (no per-pixel multiplies)
+  int D = 2 * dy - dx, px = x0, py = y0;
+  int ad = y0 * W + x0;  // pixel address, stepped with the pixel
+  const int amaj = xy * W + xx, amin = yy * W + yx;
   for (int x = 0; x <= dx; ++x) {
-    const int px = x0 + x * xx + y * yx, py = y0 + x * xy + y * yy;
-    if ((unsigned)px < (unsigned)W && (unsigned)py < (unsigned)H) img[py * W + px] = col;
-    if (D >= 0) {
-      y += 1;
-      D -= 2 * dx;
-    }
-    D += 2 * dy;
+    if ((unsigned)px < (unsigned)W && (unsigned)py < (unsigned)H) img[(uint32_t)ad] = col;
+    const bool st = D >= 0;
+    px += xx + (st ? yx : 0);
+    py += xy + (st ? yy : 0);
+    ad += amaj + (st ? amin : 0);
+    D += 2 * dy - (st ? 2 * dx : 0);
   }
 }
 
@@ -185,7 +192,7 @@ __device__ inline int proj(float v) {  // round-to-nearest pixel, clamped far of
   return (int)v;
 }
 
-__device__ inline void draw_one(uint8_t* img, const View& V, float4 q, uint8_t col) {
+__device__ inline void draw_one(lds_u8* img, const View& V, float4 q, uint8_t col) {
   const float ax = q.x - V.cx, az = q.y - V.cz, bx = q.z - V.cx, bz = q.w - V.cz;
   const float fa = ax * V.dirx + az * V.dirz, la = ax * V.rx + az * V.rz;
   const float fb = bx * V.dirx + bz * V.dirz, lb = bx * V.rx + bz * V.rz;
@@ -200,7 +207,7 @@ __device__ inline void draw_one(uint8_t* img, const View& V, float4 q, uint8_t c
 
 // Every thread draws segments tid, tid + T, ...; the (L2-resident) segment
 // loads of a thread are issued together, four at a time, before any is drawn.
-__device__ inline void draw_segments(uint8_t* img, const View& V, const float4* __restrict__ seg,
+__device__ inline void draw_segments(lds_u8* img, const View& V, const float4* __restrict__ seg,
                                      int nseg, uint8_t col) {
   const int T = blockDim.x;
   for (int s0 = threadIdx.x; s0 < nseg; s0 += 4 * T) {
@@ -387,6 +394,18 @@ __device__ inline int sobel_swar(uint32_t a00, uint32_t a01, uint32_t a02, uint3
   return best;
 }
 
+// b (< 256) in all four bytes: one v_perm, not a 32-bit multiply
+__device__ inline uint32_t splat_byte(uint32_t b) { return __builtin_amdgcn_perm(0u, b, 0u); }
+
+// bytes of 0 / 1 -> 0 / 255 (= m * 255 mod 2^32: no byte borrows), shift and
+// subtract instead of a quarter-rate v_mul_lo_u32 (asm: the compiler folds the
+// two back into the multiply)
+__device__ inline uint32_t bytes01_to_ff(uint32_t m) {
+  uint32_t r;
+  asm("v_lshlrev_b32 %0, 8, %1\n\tv_sub_u32 %0, %0, %1" : "=&v"(r) : "v"(m));
+  return r;
+}
+
 // byte-lane shift of a row of words: result byte i = pixel (i + d) (0 outside)
 __device__ inline uint32_t shift_bytes(uint32_t prev, uint32_t cur, uint32_t next, int d) {
   if (d == 0) return cur;
@@ -394,18 +413,30 @@ __device__ inline uint32_t shift_bytes(uint32_t prev, uint32_t cur, uint32_t nex
   return (cur << (-8 * d)) | (prev >> (32 + 8 * d));
 }
 
-__device__ inline void wave_push(int32_t* counter, uint16_t* list, int cap, bool want,
-                                 uint16_t value) {
-  const uint64_t m = __ballot(want);
-  if (!m) return;
-  const int lane = threadIdx.x & 63;
-  const int leader = __ffsll((unsigned long long)m) - 1;
+// Up to four pushes per lane in one go (every lane of the wave calls): the
+// lane counts (0..4) are summed and prefix-summed bit-plane by bit-plane with
+// three ballots, lane 0 reserves the wave's slots with one LDS atomic, and each
+// lane writes its items consecutively from its prefix.
+__device__ inline void wave_push4(int32_t* counter, uint16_t* list, int cap, const bool want[4],
+                                  const uint16_t value[4]) {
+  const uint32_t cnt = (uint32_t)want[0] + want[1] + want[2] + want[3];
+  const uint64_t b0 = __ballot(cnt & 1u), b1 = __ballot(cnt & 2u), b2 = __ballot(cnt & 4u);
+  const int total = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+  if (total == 0) return;  // wave-uniform
+  const auto mb = [](uint64_t m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  };
   int base = 0;
-  if (lane == leader) base = atomicAdd(counter, __popcll(m));
-  base = __shfl(base, leader);
-  if (want) {
-    const int slot = base + __popcll(m & ((1ull << lane) - 1ull));
-    if (slot < cap) list[slot] = value;
+  if ((threadIdx.x & 63) == 0) base = atomicAdd(counter, total);
+  base = __builtin_amdgcn_readlane(base, 0);
+  int slot = base + mb(b0) + 2 * mb(b1) + 4 * mb(b2);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (want[k]) {
+      if (slot < cap) list[slot] = value[k];
+      ++slot;
+    }
   }
 }
 
@@ -417,7 +448,7 @@ __device__ inline int mag16(const FusedLds& S, int r, int c) {
 __device__ __forceinline__ uint32_t bg_color(const FusedLds& S, const RenderArgs& a, float fi,
                                              float fj) {
   if (fi >= 0.0f && fj >= 0.0f && fi < (float)a.width && fj < (float)a.height) {
-    const int k = S.kind[(int)fj * a.width + (int)fi];
+    const int k = S.kind[__mul24((int)fj, a.width) + (int)fi];  // 24-bit: full-rate multiply
     return k > 0 ? PAL_ROAD : (k == 0 ? PAL_OFFROAD : PAL_FLOOR);
   }
   return PAL_FLOOR;
@@ -458,16 +489,16 @@ __device__ __forceinline__ void write_masks(const FusedLds& S, const LineDev& L,
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const uint2 v = *reinterpret_cast<const uint2*>(wk + 4 * j);
-      edg[j] = ((v.x >> 14) & 1u) | ((v.x >> 30) & 1u) << 8 | ((v.y >> 14) & 1u) << 16 |
-               ((v.y >> 30) & 1u) << 24;
+      // the high byte of each 16-bit entry (v_perm), EDGE = its bit 6
+      edg[j] = (__builtin_amdgcn_perm(v.y, v.x, 0x07050301u) >> 6) & 0x01010101u;
     }
     uint32_t o[4][4];
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      o[0][j] = (dil[j] & 0x01010101u) * 255u;
-      o[1][j] = ((dil[j] >> 1) & 0x01010101u) * 255u;
-      o[2][j] = ((dil[j] >> 2) & 0x01010101u) * 255u;
-      o[3][j] = edg[j] * 255u;
+      o[0][j] = bytes01_to_ff(dil[j] & 0x01010101u);
+      o[1][j] = bytes01_to_ff((dil[j] >> 1) & 0x01010101u);
+      o[2][j] = bytes01_to_ff((dil[j] >> 2) & 0x01010101u);
+      o[3][j] = bytes01_to_ff(edg[j]);
     }
     const int p0 = r * W + 4 * cw0;
 #pragma unroll
@@ -532,7 +563,7 @@ __global__ __launch_bounds__(1024) void render_kernel(RenderArgs a) {
     }
     uint4 words;
     if (fi[0] == fi[15] && fj[0] == fj[15]) {
-      const uint32_t wd = bg_color(S, a, fi[0], fj[0]) * 0x01010101u;
+      const uint32_t wd = splat_byte(bg_color(S, a, fi[0], fj[0]));
       words = make_uint4(wd, wd, wd, wd);
     } else {
 #pragma unroll
@@ -547,7 +578,7 @@ __global__ __launch_bounds__(1024) void render_kernel(RenderArgs a) {
       for (int k = 0; k < 4; ++k) {
         const int i0 = 4 * k, i3 = 4 * k + 3;
         if (fi[i0] == fi[i3] && fj[i0] == fj[i3]) {
-          wd[k] = bg_color(S, a, fi[i0], fj[i0]) * 0x01010101u;
+          wd[k] = splat_byte(bg_color(S, a, fi[i0], fj[i0]));
         } else {
           wd[k] = 0;
 #pragma unroll
@@ -561,9 +592,9 @@ __global__ __launch_bounds__(1024) void render_kernel(RenderArgs a) {
   __syncthreads();
   uint8_t* img8 = reinterpret_cast<uint8_t*>(S.img);
   if (!(a.skip & 2)) {
-    draw_segments(img8, V, a.marks, a.n_yellow, PAL_YELLOW);
+    draw_segments((lds_u8*)img8, V, a.marks, a.n_yellow, PAL_YELLOW);
     __syncthreads();
-    draw_segments(img8, V, a.marks + a.n_yellow, a.n_white, PAL_WHITE);
+    draw_segments((lds_u8*)img8, V, a.marks + a.n_yellow, a.n_white, PAL_WHITE);
   }
   __syncthreads();
 
@@ -600,7 +631,7 @@ __global__ __launch_bounds__(1024) void render_kernel(RenderArgs a) {
         wq[k] = w;
         const uint32_t mid = col[k + 1][1], up = col[k][1], dn = col[k + 2][1];
         const uint32_t b = mid & 255u;
-        const uint32_t rep = b * 0x01010101u;
+        const uint32_t rep = splat_byte(b);
         const uint32_t diff =
             (mid ^ rep) | (up ^ rep) | (dn ^ rep) |
             (((col[k][0] >> 24) ^ b) | ((col[k + 1][0] >> 24) ^ b) | ((col[k + 2][0] >> 24) ^ b)) |
@@ -633,9 +664,15 @@ __global__ __launch_bounds__(1024) void render_kernel(RenderArgs a) {
         }
       }
     }
+    static_assert(kRowsPerLane == 4, "wave_push4 takes four items per lane");
+    bool push[4];
+    uint16_t pv[4];
 #pragma unroll
-    for (int k = 0; k < kRowsPerLane; ++k)
-      wave_push(&S.nlist, S.list, NW, act && !uni[k], (uint16_t)wq[k]);
+    for (int k = 0; k < 4; ++k) {
+      push[k] = act && !uni[k];
+      pv[k] = (uint16_t)wq[k];
+    }
+    wave_push4(&S.nlist, S.list, NW, push, pv);
   }
   __syncthreads();
 
@@ -709,8 +746,7 @@ __global__ __launch_bounds__(1024) void render_kernel(RenderArgs a) {
         *reinterpret_cast<uint2*>(S.work + 4 * w) =
             make_uint2(cur.x | setb[0] | (setb[1] << 16), cur.y | setb[2] | (setb[3] << 16));
     }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) wave_push(&S.nweak, S.weak, kWeakCap, want[i], wk[i]);
+    wave_push4(&S.nweak, S.weak, kWeakCap, want, wk);
   }
   __syncthreads();
 

@@ -23,6 +23,10 @@ MASK_WHITE, MASK_YELLOW, MASK_RED, MASK_EDGES = range(4)
 # Algorithmic HBM bytes per env per render launch (DESIGN.md "render kernel"):
 # writes: grey frame f32 76,800 + 4 u8 masks 76,800; reads: pose 24.
 RENDER_BYTES_PER_ENV = 4 * NPIX + 4 * NPIX + 24
+# ... plus, per env respawned by the step before it, the first frame into the
+# ring's other two slots (Transformer.reset stacks three copies,
+# utils/reward_shaping/env_utils.py:60-63)
+RENDER_BYTES_PER_FRESH = 2 * 4 * NPIX
 
 
 class LineParams(ctypes.Structure):

@@ -240,9 +240,11 @@ def main():
             bytes_per_launch = STEP_BYTES_PER_ENV * n + SPAWN_BYTES_PER_RESET * resets / max(
                 1.0, decisions / n)
         else:
-            from aido1_amd.render import RENDER_BYTES_PER_ENV
+            from aido1_amd.render import RENDER_BYTES_PER_ENV, RENDER_BYTES_PER_FRESH
             kname, kms = 'render_kernel', render_ms
-            bytes_per_launch = RENDER_BYTES_PER_ENV * n
+            # resets per launch = the envs the render refills (fresh = done)
+            bytes_per_launch = (RENDER_BYTES_PER_ENV * n + RENDER_BYTES_PER_FRESH * resets /
+                                max(1.0, decisions / n))
         achieved = bytes_per_launch / (kms * 1e-3) / 1e9
         line = {
             'metric': METRIC,
