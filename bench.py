@@ -38,14 +38,14 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
 
 # Algorithmic HBM bytes of one dt_step launch (step_kernel: step lanes + the
 # spawn-ahead refill blocks), DESIGN.md §3.1-3.2:
-# step, per env:    reads pose 24 + step_count,env_step 8 + action 8               = 40
-#                   writes pose 24 + counters 8 + reward 8 + reward_mod 8 + done 1 + obs 8 = 57
-# refill scan, per env: reads want 4 + both slot keys 8                          = 12
-# per reset:  step lane reads episode 4 + slot key 4 + slot pose/lane 40, writes
-#             episode 4 + want 4 (56); the refill of the consumed key reads seed 8,
-#             writes slot pose/lane 40 + key 4 (52)                               = 108
-STEP_BYTES_PER_ENV = 40 + 57 + 12
-SPAWN_BYTES_PER_RESET = 108
+# step, per env:  reads pose 24 + step_count,env_step 8 + action 8 + episode 4
+#                 + both spawn-ahead slots (keys 8, records 80; read up front)  = 132
+#                 writes pose 24 + counters 8 + reward 8 + reward_mod 8 + done 1 + obs 8 = 57
+# refill scan, per env: reads want 4 + both slot keys 8 + seed 8                 = 20
+# per reset:  the step lane writes episode 4 + want 4; the refill of the
+#             consumed key writes its slot record 40 + key 4                      = 52
+STEP_BYTES_PER_ENV = 132 + 57 + 20
+SPAWN_BYTES_PER_RESET = 52
 
 
 def parse():

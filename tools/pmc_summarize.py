@@ -14,7 +14,7 @@ import sys
 
 ROUND = sys.argv[1] if len(sys.argv) > 1 else 'r01'
 OUT = 'gpurun_out'
-KERNELS = {'lane': ('step_kernel+spawn_kernel', ['step_kernel', 'spawn_kernel']),
+KERNELS = {'lane': ('step_kernel', ['step_kernel']),
            'render': ('render_kernel', ['render_kernel'])}
 
 
