@@ -382,14 +382,12 @@ __device__ inline void finish_angle(const Geo& g, double lp[4]) {
   lp[3] = ang;
 }
 
-// get_lane_pos2 (A8-A10).  Returns false when NotInLane.
-// lp = {dist, dot_dir, angle_deg, angle_rad}; without kAngle the acos is left
-// out and lp[2] holds the side value for finish_angle.
-template <bool kAngle = true>
-__device__ inline bool lane_pos(const MapLds& M, const Geo& g, double x, double z, double c,
-                                double s, double lp[4]) {
+// get_lane_pos2 (A8-A10), in three parts: the closest curve of the tile
+// (nullptr when NotInLane), bezier_closest's parameter, and the lane pose.
+__device__ inline const double* closest_curve(const MapLds& M, const Geo& g, double x, double z,
+                                              double c, double s) {
   const int t = tile_of(M, g, x, z);
-  if (t < 0 || M.kind[t] <= 0) return false;
+  if (t < 0 || M.kind[t] <= 0) return nullptr;
   const double dx = c, dz = -s;
   // closest curve = np.argmax(curve_headings @ dir): the first of the largest
   const int k0 = M.curve_start[t], k1 = M.curve_start[t + 1];
@@ -403,12 +401,15 @@ __device__ inline bool lane_pos(const MapLds& M, const Geo& g, double x, double 
       best = k;
     }
   }
-  const double* cv = M.curves + kCurveRec * best;
-  // bezier_closest, 8 levels.  One endpoint distance is carried between levels:
-  // the kept half's end was evaluated at the same t one level earlier, and the
-  // function is deterministic, so the result is bit-identical to re-evaluating.
-  // The midpoint is evaluated once, before the comparison: it is the new end
-  // whichever half is kept (one evaluation, no divergent branches).
+  return M.curves + kCurveRec * best;
+}
+
+// bezier_closest, 8 levels.  One endpoint distance is carried between levels:
+// the kept half's end was evaluated at the same t one level earlier, and the
+// function is deterministic, so the result is bit-identical to re-evaluating.
+// The midpoint is evaluated once, before the comparison: it is the new end
+// whichever half is kept (one evaluation, no divergent branches).
+__device__ inline double bezier_closest(const double* cv, double x, double z) {
   double tb = 0.0, tt = 1.0;
   double db = dist2_pt(cv[0], cv[1], x, z), dtp = dist2_pt(cv[6], cv[7], x, z);
 #pragma unroll
@@ -421,7 +422,15 @@ __device__ inline bool lane_pos(const MapLds& M, const Geo& g, double x, double 
     tb = left ? tb : mid;
     db = left ? db : dm;
   }
-  const double tm = (tb + tt) * 0.5;
+  return (tb + tt) * 0.5;
+}
+
+// lp = {dist, dot_dir, angle_deg, angle_rad} at the curve point tm; without
+// kAngle the acos is left out and lp[2] holds the side value for finish_angle.
+template <bool kAngle>
+__device__ inline void lane_pose_at(const Geo& g, const double* cv, double tm, double x, double z,
+                                    double c, double s, double lp[4]) {
+  const double dx = c, dz = -s;
   double qx, qz;
   bez_xz(cv, tm, qx, qz);
   const double u = 1.0 - tm;
@@ -444,6 +453,15 @@ __device__ inline bool lane_pos(const MapLds& M, const Geo& g, double x, double 
   lp[1] = dot;
   lp[2] = (dx * rx + 0.0) + dz * rz;  // side of the tangent (sign of the angle)
   if (kAngle) finish_angle(g, lp);
+}
+
+// get_lane_pos2 (A8-A10).  Returns false when NotInLane.
+template <bool kAngle = true>
+__device__ inline bool lane_pos(const MapLds& M, const Geo& g, double x, double z, double c,
+                                double s, double lp[4]) {
+  const double* cv = closest_curve(M, g, x, z, c, s);
+  if (!cv) return false;
+  lane_pose_at<kAngle>(g, cv, bezier_closest(cv, x, z), x, z, c, s, lp);
   return true;
 }
 
