@@ -109,7 +109,10 @@ __device__ inline void put_slot(const dt::State& st, int n, int e, uint32_t key,
   __hip_atomic_store(st.pre_key + sl * n + e, ok ? key : (key | dt::kKeyFailed), __ATOMIC_RELAXED,
                      __HIP_MEMORY_SCOPE_AGENT);
 }
-constexpr int kRefillEnvs = 4;     // envs scanned per refill block
+#ifndef DTSIM_REFILL_ENVS
+#define DTSIM_REFILL_ENVS 8
+#endif
+constexpr int kRefillEnvs = DTSIM_REFILL_ENVS;  // envs scanned per refill block
 
 __device__ int refill_group(const dt::State& st, const dt::MapDev& md, const dt::Geo& g, int n,
                              uint32_t max_attempts, uint32_t env_base, int e0, int ne,
