@@ -35,7 +35,7 @@ def main():
     deltas, real, stamps_mid = [], [], []
     L.dt_diag_rstamps.argtypes = [ctypes.c_void_p]
     rbuf = np.zeros((4096, 4), np.uint64)
-    nr = (n + 3) // 4
+    nr = (n + 7) // 8   # refill groups of kRefillEnvs = 8
     rinfo = []
     prev_exit = None
     sg = env.capture(acts[40:60], out)
