@@ -67,15 +67,25 @@ class ReplayBuffer:
     def _slots(self, n):
         return (self._next_idx + torch.arange(n, device=self.device)) % self._maxsize
 
-    def _write(self, fields, slots):
+    def _write(self, fields, slots, start):
+        """Rows `slots` (= start, start+1, ... mod size) of every field."""
         n = slots.shape[0]
         if n > self._maxsize:        # later adds overwrite earlier ones
             fields = [f[n - self._maxsize:] for f in fields]
             slots = slots[n - self._maxsize:]
+            start = (start + n - self._maxsize) % self._maxsize
+            n = self._maxsize
         if self.storage is None:
             self._alloc(fields)
         for name, f in zip(FIELDS, fields):
-            self.storage[name].index_copy_(0, slots, f.to(self.storage[name].dtype))
+            if start + n <= self._maxsize:   # one contiguous block: a plain copy
+                self.storage[name][start:start + n].copy_(f)
+            else:
+                self.storage[name].index_copy_(0, slots, f.to(self.storage[name].dtype))
+
+    def _reserve(self, n):
+        """Device slots of the next n adds (before _advance)."""
+        return self._slots(n)
 
     def _advance(self, n):
         self._next_idx = (self._next_idx + n) % self._maxsize
@@ -89,9 +99,33 @@ class ReplayBuffer:
     def add_batch(self, obs_t, action, reward, obs_tp1, done, _batched=True):
         fields = self._fields(obs_t, action, reward, obs_tp1, done, _batched)
         n = fields[0].shape[0]
-        self._write(fields, self._slots(n))
+        start = self._next_idx
+        self._write(fields, self._reserve(n), start)
         self._advance(n)
 
+    def add_batch_ring(self, obs_t, action, reward, ring, order, done):
+        """add_batch with obs_tp1 = ring[:, order] (a rollout's frame ring in its
+        stack order), copied from the ring straight into the buffer rows.
+        Returns obs_tp1 as stored: a view of the buffer rows (the next
+        decision's obs_t, valid until the buffer comes round to them), or a copy
+        where the rows would not be one block or would be overwritten by the
+        next add."""
+        n = ring.shape[0]
+        p = self._next_idx
+        if self.storage is None or p + n > self._maxsize or 2 * n > self._maxsize:
+            nxt = ring[:, list(order)]
+            self.add_batch(obs_t, action, reward, nxt, done)
+            return nxt
+        self._reserve(n)
+        st = self.storage
+        st['obs'][p:p + n].copy_(torch.as_tensor(obs_t, device=self.device))
+        st['action'][p:p + n].copy_(torch.as_tensor(action, device=self.device))
+        st['reward'][p:p + n].copy_(torch.as_tensor(reward, device=self.device))
+        for k, sl in enumerate(order):
+            st['next_obs'][p:p + n, k].copy_(ring[:, sl])
+        st['done'][p:p + n].copy_(torch.as_tensor(done, device=self.device).to(torch.bool))
+        self._advance(n)
+        return st['next_obs'][p:p + n]
     def _encode_sample(self, idxes):
         """buffers.py:38-52: (obs, actions, rewards, next_obs, dones) rows."""
         return tuple(self.storage[name].index_select(0, idxes) for name in FIELDS)
@@ -134,16 +168,17 @@ class PrioritizedReplayBuffer(ReplayBuffer):
             msg = self._L.dt_per_last_error(self._h) or b''
             raise _lib.DtError('%s failed (%d): %s' % (what, rc, msg.decode()))
 
-    def add_batch(self, obs_t, action, reward, obs_tp1, done, _batched=True):
-        """n consecutive add() calls (buffers.py:169-174)."""
-        fields = self._fields(obs_t, action, reward, obs_tp1, done, _batched)
-        n = fields[0].shape[0]
+    def _reserve(self, n):
+        """n consecutive add() calls' tree updates (buffers.py:169-174): every
+        new leaf gets max_priority**alpha; returns the slots."""
         slots = torch.empty(n, dtype=torch.int64, device=self.device)
         with torch.cuda.device(self.device):
             self._check(self._L.dt_per_add(self._h, n, ctypes.c_void_p(slots.data_ptr()),
                                            self._stream()), 'dt_per_add')
-        self._write(fields, slots)
-        self._advance(n)
+        return slots
+
+    def _advance(self, n):
+        super()._advance(n)
         assert self._next_idx == self._L.dt_per_next_idx(self._h)
 
     def sample(self, batch_size, beta=0.5, u=None):

@@ -9,8 +9,9 @@ Here one process per GPU runs, per iteration:
 
   ActorRollout.step          one decision for n envs (actor on the frame ring,
                              exploration noise, 3 sim steps, render)
-  replay.add_batch           n transitions (obs, mapped action, reward_mod,
-                             next_obs, done), HBM-resident
+  replay.add_batch_ring      n transitions (obs, mapped action, reward_mod,
+                             next_obs, done), HBM-resident; next_obs copied
+                             from the frame ring, obs = the previous rows
   replay.sample              batch_size transitions (proportional, GPU trees)
   DDPGTrainer.update         critic + actor + soft target update (grads
                              all-reduced over ranks with RCCL)
@@ -72,10 +73,11 @@ class TrainLoop:
 
     def step(self, timing=None):
         r, rm, done = self.rollout.step(timing)
-        nxt = self.rollout.stack()
         rew = rm if self.reward_modified else r        # explorers.py:205-206
-        self.replay.add_batch(self.obs, self.rollout.actions, rew, nxt, done)
-        self.obs = nxt
+        # next_obs straight from the frame ring into the buffer; the stored rows
+        # are the next decision's obs (no stacked copy of the ring)
+        self.obs = self.replay.add_batch_ring(self.obs, self.rollout.actions, rew,
+                                              self.rollout.ring, self.rollout.order(), done)
         self.decisions += 1
         if len(self.replay) >= max(self.batch_size, 2):
             for _ in range(self.updates_per_step):

@@ -52,3 +52,29 @@ def test_sample_empty_raises():
     from aido1_amd.replay import ReplayBuffer
     with pytest.raises(ValueError):
         ReplayBuffer(4, device='cpu').sample(2)
+
+
+def test_add_batch_ring_equals_add_batch():
+    """add_batch_ring (next_obs straight from a frame ring in stack order, the
+    returned rows chained as the next obs) stores what add_batch of the
+    stacked copies stores, across the wrap of the buffer."""
+    from aido1_amd.replay import ReplayBuffer
+    g = torch.Generator().manual_seed(0)
+    n, size = 3, 8
+    a, b = ReplayBuffer(size, device='cpu'), ReplayBuffer(size, device='cpu')
+    ring = torch.rand(n, 3, 2, 2, generator=g)
+    obs_a = obs_b = ring[:, [0, 1, 2]].clone()
+    for t in range(7):
+        order = [(t + 1 + k) % 3 for k in range(3)]
+        ring[:, order[-1]] = torch.rand(n, 2, 2, generator=g)   # the newest frame
+        act = torch.rand(n, 2, generator=g)
+        rew = torch.rand(n, generator=g, dtype=torch.float64)
+        done = torch.rand(n, generator=g) < 0.3
+        nxt = ring[:, order]
+        b.add_batch(obs_b, act, rew, nxt, done)
+        obs_b = nxt
+        obs_a = a.add_batch_ring(obs_a, act, rew, ring, order, done)
+        assert torch.equal(obs_a, obs_b)
+    assert a._next_idx == b._next_idx and len(a) == len(b)
+    for k in a.storage:
+        assert torch.equal(a.storage[k], b.storage[k]), k
