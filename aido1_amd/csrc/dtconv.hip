@@ -274,7 +274,7 @@ conv1_norm_kernel(__half* __restrict__ y, const float* __restrict__ partials,
 //         and chunk c (8 channels) of the pixel at position pos sits at
 //         16 * (c ^ ((pos >> 2) & 3)): 16 lanes of a ds_read_b128 group read
 //         16 distinct 16-B slots of the 256-B bank row
-//   in    kIn 1: y = x * sc + sh with the previous layer's train-mode
+//   in    kIn 1 (at ring commit, once per element): y = x * sc + sh with the previous layer's train-mode
 //         batch-of-one BatchNorm, (sc, sh) from its statistics (Chan's merge)
 //   mma   v_mfma_f32_32x32x16_f16, A = weights (32 steps of 16 k, held in
 //         registers for the whole launch), B = the pixel's im2col column:
@@ -424,15 +424,32 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
       pre[i] = src[q < cnt ? q : cnt - 1];
     }
   };
+  // kIn 1: the previous layer's BatchNorm is applied here, once per input
+  // element (a thread's chunks all hold channels 8*(tid&3)..+7: kThreads and
+  // kRowU4 are multiples of 4), not on every B-fragment read of it
   auto commit = [&](const u32x4 (&pre)[kPre], int k, int r0, int r1) __attribute__((always_inline)) {
     const int cnt = (r1 - r0 + 1) * kRowU4;
+    float csc[8], csh[8];
+    if (kIn == 1) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        csc[e] = s_sc[k % 3][8 * (tid & 3) + e];
+        csh[e] = s_sh[k % 3][8 * (tid & 3) + e];
+      }
+    }
 #pragma unroll
     for (int i = 0; i < kPre; ++i) {
       const int q = tid + i * kThreads;
       if (q >= cnt) continue;
       const int r = q / kRowU4, qq = q - r * kRowU4;
       const int slot = (k * IH + r0 + r) % kRing;
-      *reinterpret_cast<u32x4*>(rb + slot * kRowBytes + ring_off<IW, ST>(qq >> 2, qq & 3)) = pre[i];
+      u32x4 u = pre[i];
+      if (kIn == 1) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e)
+          u[e] = norm_pair(u[e], csc[2 * e], csh[2 * e], csc[2 * e + 1], csh[2 * e + 1]);
+      }
+      *reinterpret_cast<u32x4*>(rb + slot * kRowBytes + ring_off<IW, ST>(qq >> 2, qq & 3)) = u;
     }
   };
 
@@ -459,17 +476,6 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
     stats_load(k2);
     if (!(DTCONV_SKIP & 1)) issue(nxt, k2, G::first_new(j1), G::last_new(j1));
 
-    // the input norm of this sample for this lane's B channels 16*(s%2) + 8h + j
-    float isc[2][8], ish[2][8];
-    if (kIn == 1) {
-#pragma unroll
-      for (int e = 0; e < 2; ++e)
-#pragma unroll
-        for (int q = 0; q < 8; ++q) {
-          isc[e][q] = s_sc[k % 3][16 * e + 8 * h + q];
-          ish[e][q] = s_sh[k % 3][16 * e + 8 * h + q];
-        }
-    }
     // this wave's tile
     const int t = NW * j + wave;
     const int p = 32 * t + col;
@@ -494,18 +500,8 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
     };
     auto mm = [&](half8 (&b)[8], int gy) __attribute__((always_inline)) {
 #pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        half8 bf = b[i];
-        if (kIn == 1) {
-          u32x4 u = __builtin_bit_cast(u32x4, bf);
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-            u[q] = norm_pair(u[q], isc[i & 1][2 * q], ish[i & 1][2 * q], isc[i & 1][2 * q + 1],
-                             ish[i & 1][2 * q + 1]);
-          bf = __builtin_bit_cast(half8, u);
-        }
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wa[8 * gy + i], bf, acc, 0, 0, 0);
-      }
+      for (int i = 0; i < 8; ++i)   // the ring rows are already normalised (commit)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wa[8 * gy + i], b[i], acc, 0, 0, 0);
     };
     if (!(DTCONV_SKIP & 2)) ld(bq[0], 0);
 #pragma unroll
@@ -648,6 +644,7 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
     stats_load(1);
     stats_merge(1);
   }
+  __syncthreads();   // the merged statistics, read by commit
   issue(pa, 0, 0, G::hi(0));
   commit(pa, 0, 0, G::hi(0));
   if (total > 1)
