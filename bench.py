@@ -183,10 +183,9 @@ def main():
     if G:
         # the timed decisions as HIP graphs of G launches each, captured up
         # front over their own action slices (StepGraph)
-        if args.steps % G:
-            raise SystemExit('--steps must be a multiple of --graph-steps')
-        graphs = [env.capture(actions[args.warmup + c * G:args.warmup + (c + 1) * G], out)
-                  for c in range(args.steps // G)]
+        bounds = list(range(0, args.steps, G)) + [args.steps]   # the last takes the rest
+        graphs = [env.capture(actions[args.warmup + a:args.warmup + b], out)
+                  for a, b in zip(bounds[:-1], bounds[1:])]
         gev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                for _ in graphs]
     env.stats(reset=True)
@@ -220,7 +219,7 @@ def main():
     st = env.stats()
     env.check()
     if G:  # per launch inside the graphs: replay time / launches (gaps included)
-        step_ms = float(np.mean([a.elapsed_time(b) for a, b in gev])) / G
+        step_ms = float(np.sum([a.elapsed_time(b) for a, b in gev])) / args.steps
     else:
         step_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     render_ms = float(np.mean([a.elapsed_time(b) for a, b in rev])) if rev else None
