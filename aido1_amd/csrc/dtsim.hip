@@ -78,48 +78,56 @@ __device__ inline void map_action(int mode, float a0, float a1, double& vl, doub
   }
 }
 
-// Spawn-ahead refill (A13) of envs [e0, e0 + ne), one 256-thread block: the
-// first ne lanes read want, both slot keys and the seed of one env each (one
-// round of independent loads) and list the keys missing among {want-1, want};
-// the block stages the map only when the list is not empty and then computes
-// the listed (env, key) items: one item (the usual case) with all 256 threads
-// (spawn_block: one round of 256 proposals almost always holds the first
-// accepted one), several with one wave each in parallel (spawn_one).  Groups
-// are small (kRefillEnvs), so the refill finishes inside the step it runs
-// beside.
-// Race-free against a dt_step lane of the same launch: key k = that lane's
-// episode counter was made ready by an earlier launch (every launch refills
-// every key missing at its start), the lane reads slot k & 1 at its start and
-// raises want to k + 2 only after those reads returned; this block writes only
-// slots of keys it reads as missing among {want-1, want}, never k's while the
-// lane may still read it.
+// Spawn-ahead reset (A13).  Each env keeps a window of kSlots
+// precomputed reset poses: key j (the episode counter the env has when it takes
+// that reset) lives in slot j % kSlots, tagged with the env's launch tick at the
+// time it was written.  want[e] - 1 is the env's episode counter as its last
+// launch left it; the window is the keys [want - 1, want - 1 + kSlots).
+//
+// refill_group refills envs [e0, e0 + ne) with one 256-thread block: the first
+// ne lanes read want, the slot words, tick and seed of one env each and list
+// the window's missing keys; the block stages the map only when the list is
+// not empty and computes the items: one with all 256 threads (spawn_block: one
+// round of 256 proposals almost always holds the first accepted one), several
+// with one wave each in parallel (spawn_one).
+//
+// Race-free against the step lanes of the same launch:
+//  * a step lane consumes a slot only if an earlier launch wrote it (tag older
+//    than the lane's tick; a refill of the same launch tags with the tick it
+//    reads, which is >= the lane's), so it never reads a slot being written;
+//  * a refill writes only slots whose key is outside the window it read, and
+//    a lane moves its window (want store) only after its last slot loads
+//    returned.
+// A standalone refill (dt_seed, dt_reset: no step lane runs) tags tick - 1,
+// usable by the next launch.
 constexpr int kBlock = 256;        // step and refill blocks (4 waves)
 
-// Publish a spawn-ahead slot.  No fence: the pose is read by a later launch
-// only (the kernel boundary orders it), and this launch's scans read the key.
-__device__ inline void put_slot(const dt::State& st, int n, int e, uint32_t key, bool ok, double x,
-                                double z, double a, double dist, double arad) {
-  const size_t sl = key & 1u;
+__device__ inline void put_slot(const dt::State& st, int n, int e, uint32_t key, bool ok,
+                                uint32_t tag, double x, double z, double a, double dist,
+                                double arad) {
+  const size_t sl = key % (uint32_t)dt::kSlots;
   double* p = st.pre + sl * 5 * (size_t)n + e;
   p[0] = x;
   p[(size_t)n] = z;
   p[2 * (size_t)n] = a;
   p[3 * (size_t)n] = dist;
   p[4 * (size_t)n] = arad;
-  __hip_atomic_store(st.pre_key + sl * n + e, ok ? key : (key | dt::kKeyFailed), __ATOMIC_RELAXED,
-                     __HIP_MEMORY_SCOPE_AGENT);
+  const uint64_t w = ((uint64_t)tag << 32) | (ok ? key : (key | dt::kKeyFailed));
+  __hip_atomic_store(st.pre_key + sl * n + e, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 #ifndef DTSIM_REFILL_ENVS
 #define DTSIM_REFILL_ENVS 8
 #endif
 constexpr int kRefillEnvs = DTSIM_REFILL_ENVS;  // envs scanned per refill block
+constexpr int kMaxItems = dt::kSlots * kRefillEnvs;
 
 __device__ int refill_group(const dt::State& st, const dt::MapDev& md, const dt::Geo& g, int n,
                              uint32_t max_attempts, uint32_t env_base, int e0, int ne,
-                             unsigned char* lds) {
-  __shared__ int32_t item_env[2 * kRefillEnvs];
-  __shared__ uint32_t item_key[2 * kRefillEnvs];
-  __shared__ uint64_t item_seed[2 * kRefillEnvs];
+                             uint32_t tag_back, unsigned char* lds) {
+  __shared__ int32_t item_env[kMaxItems];
+  __shared__ uint32_t item_key[kMaxItems];
+  __shared__ uint32_t item_tag[kMaxItems];
+  __shared__ uint64_t item_seed[kMaxItems];
   __shared__ int32_t n_items;
   __shared__ double scratch[6 * (kBlock / 64)];
   const int tid = threadIdx.x;
@@ -128,19 +136,22 @@ __device__ int refill_group(const dt::State& st, const dt::MapDev& md, const dt:
   const int e = e0 + tid;
   if (tid < ne && e < n) {
     const uint32_t w = __hip_atomic_load(st.want + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t h0 = __hip_atomic_load(st.pre_key + e, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t h1 = __hip_atomic_load(st.pre_key + (size_t)n + e, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t tag =
+        __hip_atomic_load(st.tick + e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) - tag_back;
+    uint32_t have[dt::kSlots];
+#pragma unroll
+    for (int s = 0; s < dt::kSlots; ++s)
+      have[s] = (uint32_t)__hip_atomic_load(st.pre_key + (size_t)s * n + e, __ATOMIC_RELAXED,
+                                             __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t seed = st.seed[e];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
+    for (int i = 0; i < dt::kSlots; ++i) {
       const uint32_t key = w - 1u + (uint32_t)i;
-      const uint32_t have = (key & 1u) ? h1 : h0;
-      if ((i == 1 || w > 0u) && (have & ~dt::kKeyFailed) != key) {
+      if ((i > 0 || w > 0u) && (have[key % (uint32_t)dt::kSlots] & ~dt::kKeyFailed) != key) {
         const int slot = atomicAdd(&n_items, 1);
         item_env[slot] = e;
         item_key[slot] = key;
+        item_tag[slot] = tag;
         item_seed[slot] = seed;
       }
     }
@@ -149,18 +160,19 @@ __device__ int refill_group(const dt::State& st, const dt::MapDev& md, const dt:
   const int cnt = n_items;
   if (cnt == 0) return 0;  // block-uniform
   const dt::MapLds M = dt::stage_map(md, lds);
-  if (cnt == 1) {  // the usual case: all four waves on the one item
+  if (cnt == 1) {  // all four waves on the one item
     double x = 0.0, z = 0.0, a = 0.0, dist = 0.0, arad = 0.0;
     const bool ok = dt::spawn_block(M, g, max_attempts, env_base + (uint32_t)item_env[0],
                                     item_seed[0], item_key[0], scratch, x, z, a, dist, arad);
-    if (tid == 0) put_slot(st, n, item_env[0], item_key[0], ok, x, z, a, dist, arad);
+    if (tid == 0) put_slot(st, n, item_env[0], item_key[0], ok, item_tag[0], x, z, a, dist, arad);
   } else {  // several: one wave per item (64 proposals per round), waves in parallel
     const int wave = tid >> 6, nw = (int)(blockDim.x >> 6);
     for (int it = wave; it < cnt; it += nw) {  // wave-uniform
       double x = 0.0, z = 0.0, a = 0.0, lp[2] = {0.0, 0.0};
       const bool ok = dt::spawn_one(M, g, max_attempts, env_base + (uint32_t)item_env[it],
                                     item_seed[it], item_key[it], x, z, a, lp);
-      if ((tid & 63) == 0) put_slot(st, n, item_env[it], item_key[it], ok, x, z, a, lp[0], lp[1]);
+      if ((tid & 63) == 0)
+        put_slot(st, n, item_env[it], item_key[it], ok, item_tag[it], x, z, a, lp[0], lp[1]);
     }
   }
   return cnt;
@@ -171,7 +183,7 @@ __global__ __launch_bounds__(kBlock) void refill_kernel(dt::State st, dt::MapDev
                                                         uint32_t env_base) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   refill_group(st, md, g, n, max_attempts, env_base, (int)blockIdx.x * kRefillEnvs, kRefillEnvs,
-               lds);
+               1u, lds);
 }
 
 // 0, available only once v's load has returned (the asm reads v).
@@ -181,70 +193,25 @@ __device__ inline uint32_t after_load(double v) {
   return z;
 }
 
-// EnvironmentWrapper.step (utils/env_wrappers.py:213-253) x repeat Simulator.step.
-__global__ __launch_bounds__(kBlock) void step_kernel(dt::State st, dt::MapDev md, dt::Geo g,
-                                                  StepCfg sc, int n, uint32_t env_base,
-                                                  const float2* __restrict__ act,
-                                                  double* __restrict__ rew,
-                                                  double* __restrict__ rewm,
-                                                  uint8_t* __restrict__ done_out,
-                                                  float2* __restrict__ obs,
-                                                  double* __restrict__ lanepos,
-                                                  int32_t* __restrict__ tile_out,
-                                                  int n_step_blocks, uint32_t max_attempts,
-                                                  const uint8_t* __restrict__ step_mask) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  // blocks past the step's: the spawn-ahead refill, kRefillEnvs envs each,
-  // running on the CUs the step leaves idle (block-uniform branch)
-  if ((int)blockIdx.x >= n_step_blocks) {
-    const int rb = (int)blockIdx.x - n_step_blocks;
-    RFSTAMP(rb, 0, __builtin_amdgcn_s_memrealtime());
-    const int items = refill_group(st, md, g, n, max_attempts, env_base, rb * kRefillEnvs,
-                                   kRefillEnvs, lds);
-    RFSTAMP(rb, 1, __builtin_amdgcn_s_memrealtime());
-    RFSTAMP(rb, 2, (unsigned long long)items);
-    (void)items;
-    return;
-  }
-  // the step waves win issue arbitration against refill waves sharing their SIMD
-  __builtin_amdgcn_s_setprio(3);
-  RSTAMP(9);
-  STAMP(0);
-  const int e = blockIdx.x * blockDim.x + threadIdx.x;
-  // envs outside step_mask (dt_step_masked) are left exactly as they were
-  const bool active = e < n && (step_mask == nullptr || step_mask[e] != 0);
-  const int ei = active ? e : 0;
+// One EnvironmentWrapper.step of one lane: repeat x frame_skip Simulator steps
+// (A4 _update_pos, A11 _compute_done_reward) and the BaselineAggregation of
+// their rewards (utils/env_wrappers.py:213-253).  c, s = cos, sin of ang on
+// entry and on exit.
+struct Decision {
+  double tr, trm;  // reward sum, aggregated reward x reward_scale
+  bool dn;
+  unsigned nsim;   // Simulator steps run
+  // lane position of the last reward computation; valid while the pose has not
+  // moved since (reused for the terminal output instead of a 4th bisection)
+  bool lp_fresh, lp_inl;
+  double lp[4];
+};
 
-  // the env's state and (auto-reset) the spawn-ahead slot of its next key are
-  // loaded before the map is staged, so their latency hides behind it.  Key k
-  // (= the episode counter) was made ready by an earlier launch and its slot
-  // is not rewritten before this env consumes it (refill_group), so the slot
-  // can be read up front.
-  double x = st.x[ei], z = st.z[ei], ang = st.angle[ei];
-  uint32_t step_count = st.step_count[ei], env_step = st.env_step[ei];
-  const float2 a = act[ei];
-  uint32_t key = 0u, have = dt::kKeyNone;
-  double pre[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
-  if (sc.auto_reset) {  // both slots (no load waits on the episode counter)
-    key = st.episode[ei];
-    const uint32_t h0 = __hip_atomic_load(st.pre_key + ei, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
-    const uint32_t h1 = __hip_atomic_load(st.pre_key + (size_t)n + ei, __ATOMIC_RELAXED,
-                                          __HIP_MEMORY_SCOPE_AGENT);
-    double p0[5], p1[5];
-#pragma unroll
-    for (int q = 0; q < 5; ++q) {
-      p0[q] = st.pre[q * (size_t)n + ei];
-      p1[q] = st.pre[(5 + q) * (size_t)n + ei];
-    }
-    const bool odd = (key & 1u) != 0u;
-    have = odd ? h1 : h0;
-#pragma unroll
-    for (int q = 0; q < 5; ++q) pre[q] = odd ? p1[q] : p0[q];
-  }
-  const MapLds M = dt::stage_map(md, lds);
-  STAMP(1);
-
+__device__ __forceinline__ void sim_decision(const MapLds& M, const dt::Geo& g, const StepCfg& sc,
+                                             bool active, float2 a, double& x, double& z,
+                                             double& ang, double& c, double& s,
+                                             uint32_t& step_count, uint32_t& env_step,
+                                             Decision& D) {
   double vl, vr;
   map_action(sc.action_mode, a.x, a.y, vl, vr);
   if (sc.clip) {  // Simulator.step: np.clip(action, -1, 1)
@@ -267,12 +234,8 @@ __global__ __launch_bounds__(kBlock) void step_kernel(dt::State st, dt::MapDev m
   double tr = 0.0, trm = 0.0;
   bool dn = !active;
   unsigned nsim = 0;
-  // lane position of the last reward computation; valid while the pose has not
-  // moved since (reused for the terminal output instead of a 4th bisection)
-  double lp[4];
+  double* lp = D.lp;
   bool lp_fresh = false, lp_inl = false;
-  double c = 0.0, s = 0.0;
-  sincos(ang, &s, &c);
   for (int rep = 0; rep < sc.repeat; ++rep) {
     if (!dn) {
       lp_fresh = false;
@@ -336,65 +299,200 @@ __global__ __launch_bounds__(kBlock) void step_kernel(dt::State st, dt::MapDev m
     }
     STAMP(3 + (rep < 3 ? rep : 2));
   }
-  trm = trm * sc.reward_scale;
+  D.tr = tr;
+  D.trm = trm * sc.reward_scale;
+  D.dn = dn;
+  D.nsim = nsim;
+  D.lp_fresh = lp_fresh;
+  D.lp_inl = lp_inl;
+}
 
-  // auto-reset (VectorEnv): a finished env takes the reset pose of its next
-  // spawn key, computed ahead (refill_group), and asks for the key after next
-  const bool want_reset = active && dn && sc.auto_reset;
-  const bool reset_now = want_reset && have == key;
-  if (want_reset && !reset_now)
-    atomicOr(st.err, dt::kErrSpawn);   // failed (or, impossibly, not ready): env stays put
-
-  // terminal lane pose: the obs of an env that stays, and the optional lanepos
-  // output; an env being reset reports its reset pose's obs instead
-  bool inl = false;
-  if (lp_fresh) {  // same pose as the last reward: only the angle is missing
-    inl = lp_inl;
-    if (inl && (lanepos || !reset_now)) dt::finish_angle(g, lp);
-  } else if (active && (lanepos || !reset_now)) {
-    inl = dt::lane_pos<true>(M, g, x, z, c, s, lp);
+// EnvironmentWrapper.step (utils/env_wrappers.py:213-253) x repeat
+// Simulator.step, k decisions in one launch (dt_step: k = 1; dt_step_many).
+// The pose, counters and spawn-ahead bookkeeping stay in registers across the
+// decisions and the map is staged once.  Outputs of decision d are at
+// [d * n + env].  Blocks past n_step_blocks are the spawn-ahead refill.
+__global__ __launch_bounds__(kBlock) void step_kernel(dt::State st, dt::MapDev md, dt::Geo g,
+                                                  StepCfg sc, int n, uint32_t env_base, int k,
+                                                  const float2* __restrict__ act,
+                                                  double* __restrict__ rew,
+                                                  double* __restrict__ rewm,
+                                                  uint8_t* __restrict__ done_out,
+                                                  float2* __restrict__ obs,
+                                                  double* __restrict__ lanepos,
+                                                  int32_t* __restrict__ tile_out,
+                                                  int n_step_blocks, uint32_t max_attempts,
+                                                  const uint8_t* __restrict__ step_mask) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  // blocks past the step's: the spawn-ahead refill, kRefillEnvs envs each,
+  // running on the CUs the step leaves idle (block-uniform branch)
+  if ((int)blockIdx.x >= n_step_blocks) {
+    const int rb = (int)blockIdx.x - n_step_blocks;
+    RFSTAMP(rb, 0, __builtin_amdgcn_s_memrealtime());
+    const int items = refill_group(st, md, g, n, max_attempts, env_base, rb * kRefillEnvs,
+                                   kRefillEnvs, 0u, lds);
+    RFSTAMP(rb, 1, __builtin_amdgcn_s_memrealtime());
+    RFSTAMP(rb, 2, (unsigned long long)items);
+    (void)items;
+    return;
   }
-  STAMP(6);
-  if (active) {
-    rew[e] = tr;
-    rewm[e] = trm;
-    done_out[e] = (uint8_t)dn;
-    if (lanepos) {
-      const double nan = __longlong_as_double(0x7ff8000000000000LL);
-      double* o = lanepos + 4 * (size_t)e;
-      o[0] = inl ? lp[0] : nan;
-      o[1] = inl ? lp[1] : nan;
-      o[2] = inl ? lp[2] : nan;
-      o[3] = inl ? lp[3] : nan;
+  // the step waves win issue arbitration against refill waves sharing their SIMD
+  __builtin_amdgcn_s_setprio(3);
+  RSTAMP(9);
+  STAMP(0);
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  const int lane = threadIdx.x & 63;
+  const bool in_range = e < n;
+  // envs outside step_mask (dt_step_masked) are left exactly as they were
+  const bool active = in_range && (step_mask == nullptr || step_mask[e] != 0);
+  const int ei = in_range ? e : 0;
+
+  // state and the spawn-ahead slot words are loaded before the map is staged,
+  // so their latency hides behind it
+  double x = st.x[ei], z = st.z[ei], ang = st.angle[ei];
+  uint32_t step_count = st.step_count[ei], env_step = st.env_step[ei];
+  float2 a = act[ei];
+  const uint32_t tick = st.tick[ei];
+  uint32_t key = 0u;
+  uint64_t seed = 0u, words[dt::kSlots];
+  if (sc.auto_reset) {
+    key = st.episode[ei];
+    seed = st.seed[ei];
+#pragma unroll
+    for (int q = 0; q < dt::kSlots; ++q)
+      words[q] = __hip_atomic_load(st.pre_key + (size_t)q * n + ei, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const MapLds M = dt::stage_map(md, lds);
+  STAMP(1);
+  // bit i: key + i is ready (written by an earlier launch); of those, failed
+  const uint32_t key0 = key;
+  uint32_t ready = 0u, failed = 0u;
+  if (sc.auto_reset) {
+#pragma unroll
+    for (int q = 0; q < dt::kSlots; ++q) {
+      const uint32_t kw = (uint32_t)words[q], tag = (uint32_t)(words[q] >> 32);
+      const uint32_t rel = (kw & ~dt::kKeyFailed) - key;
+      if (rel < (uint32_t)dt::kSlots && (int32_t)(tick - tag) > 0) {
+        ready |= 1u << rel;
+        if (kw & dt::kKeyFailed) failed |= 1u << rel;
+      }
     }
-    if (tile_out) tile_out[e] = dt::tile_of(M, g, x, z);
   }
-  if (reset_now) {
-    x = pre[0];
-    z = pre[1];
-    ang = pre[2];
-    step_count = 0u;
-    env_step = 0u;
-    st.episode[e] = key + 1u;
-    // want moves past key only once the slot's loads have returned: the store's
-    // value depends on the last of them (loads return in order)
-    __hip_atomic_store(st.want + e, key + 2u + after_load(pre[4]), __ATOMIC_RELAXED,
-                       __HIP_MEMORY_SCOPE_AGENT);
+
+  double c = 0.0, s = 0.0;
+  sincos(ang, &s, &c);
+  unsigned nsim_t = 0, act_t = 0, resets_t = 0, dones_t = 0;
+  double rp[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  for (int d = 0; d < k; ++d) {
+    // the next decision's action and this decision's reset pose (if ready),
+    // loaded while the decision runs
+    const float2 an = act[(size_t)(d + 1 < k ? d + 1 : d) * n + ei];
+    const uint32_t rel = key - key0;
+    const bool slot_ready = rel < (uint32_t)dt::kSlots && ((ready >> rel) & 1u) != 0u;
+    if (slot_ready) {
+      const size_t sl = key % (uint32_t)dt::kSlots;
+#pragma unroll
+      for (int q = 0; q < 5; ++q) rp[q] = st.pre[(sl * 5 + q) * (size_t)n + ei];
+    }
+    asm volatile("" ::: "memory");  // keep the loads here, ahead of the decision
+
+    Decision D;
+    sim_decision(M, g, sc, active, a, x, z, ang, c, s, step_count, env_step, D);
+
+    // auto-reset (VectorEnv): a finished env takes the reset pose of its next
+    // spawn key; a key not ready is computed here, the whole wave on one env
+    const bool want_reset = active && D.dn && sc.auto_reset;
+    bool ok = slot_ready && ((failed >> rel) & 1u) == 0u;
+    uint64_t need = __ballot(want_reset && !slot_ready);
+    while (need) {  // wave-uniform
+      const int l = __ffsll((unsigned long long)need) - 1;
+      need &= need - 1u;
+      const uint32_t el = (uint32_t)__shfl(ei, l), kl = (uint32_t)__shfl((int)key, l);
+      const uint64_t sd = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(seed >> 32), l) << 32) |
+                          (uint64_t)(uint32_t)__shfl((int)(uint32_t)seed, l);
+      double sx = 0.0, sz = 0.0, sa = 0.0, slp[2] = {0.0, 0.0};
+      const bool sok = dt::spawn_one(M, g, max_attempts, env_base + el, sd, kl, sx, sz, sa, slp);
+      if (lane == l) {
+        rp[0] = sx;
+        rp[1] = sz;
+        rp[2] = sa;
+        rp[3] = slp[0];
+        rp[4] = slp[1];
+        ok = sok;
+      }
+    }
+    const bool reset_now = want_reset && ok;
+    if (want_reset && !ok) atomicOr(st.err, dt::kErrSpawn);  // failed: env stays put
+
+    // terminal lane pose: the obs of an env that stays, and the optional lanepos
+    // output; an env being reset reports its reset pose's obs instead
+    const bool need_lp = lanepos != nullptr || (obs != nullptr && !reset_now);
+    bool inl = false;
+    if (D.lp_fresh) {  // same pose as the last reward: only the angle is missing
+      inl = D.lp_inl;
+      if (inl && need_lp) dt::finish_angle(g, D.lp);
+    } else if (active && need_lp) {
+      inl = dt::lane_pos<true>(M, g, x, z, c, s, D.lp);
+    }
+    STAMP(6);
+    if (active) {
+      const size_t o = (size_t)d * n + e;
+      rew[o] = D.tr;
+      rewm[o] = D.trm;
+      done_out[o] = (uint8_t)D.dn;
+      if (lanepos) {
+        const double nan = __longlong_as_double(0x7ff8000000000000LL);
+        double* lo = lanepos + 4 * o;
+        lo[0] = inl ? D.lp[0] : nan;
+        lo[1] = inl ? D.lp[1] : nan;
+        lo[2] = inl ? D.lp[2] : nan;
+        lo[3] = inl ? D.lp[3] : nan;
+      }
+      if (tile_out) tile_out[o] = dt::tile_of(M, g, x, z);
+      if (obs)
+        obs[o] = reset_now ? make_float2((float)rp[3], (float)rp[4])
+                           : (inl ? make_float2((float)D.lp[0], (float)D.lp[3])
+                                  : make_float2(0.0f, 0.0f));
+    }
+    if (reset_now) {
+      x = rp[0];
+      z = rp[1];
+      ang = rp[2];
+      sincos(ang, &s, &c);
+      step_count = 0u;
+      env_step = 0u;
+      key += 1u;
+    }
+    nsim_t += D.nsim;
+    act_t += active ? 1u : 0u;
+    resets_t += reset_now ? 1u : 0u;
+    dones_t += (active && D.dn) ? 1u : 0u;
+    a = an;
   }
   STAMP(7);
-  dt::wave_count(st.stats + 0, nsim, sc.repeat * sc.frame_skip);
-  dt::wave_count(st.stats + 1, active ? 1u : 0u, 1);
-  dt::wave_count(st.stats + 2, reset_now ? 1u : 0u, 1);
-  dt::wave_count(st.stats + 3, (active && dn) ? 1u : 0u, 1);
-  if (active) {
-    if (obs)
-      obs[e] = reset_now ? make_float2((float)pre[3], (float)pre[4])
-                         : (inl ? make_float2((float)lp[0], (float)lp[3]) : make_float2(0.0f, 0.0f));
-    st.x[e] = x;
-    st.z[e] = z;
-    st.angle[e] = ang;
-    st.step_count[e] = step_count;
-    st.env_step[e] = env_step;
+  const unsigned kk = (unsigned)k;
+  dt::wave_count(st.stats + 0, nsim_t, kk * (unsigned)(sc.repeat * sc.frame_skip));
+  dt::wave_count(st.stats + 1, act_t, kk);
+  dt::wave_count(st.stats + 2, resets_t, kk);
+  dt::wave_count(st.stats + 3, dones_t, kk);
+  if (in_range) {
+    if (active) {
+      st.x[e] = x;
+      st.z[e] = z;
+      st.angle[e] = ang;
+      st.step_count[e] = step_count;
+      st.env_step[e] = env_step;
+    }
+    __hip_atomic_store(st.tick + e, tick + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (key != key0) {
+      st.episode[e] = key;
+      // the window moves past the consumed keys only once the slot loads have
+      // returned: the store's value depends on the last of them (loads return
+      // in order)
+      __hip_atomic_store(st.want + e, key + 1u + after_load(rp[4]), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   STAMP(8);
   RSTAMP(10);
@@ -656,9 +754,11 @@ int dt_create(const dt_config* cfg, const dt_map* map, uint64_t seed, int32_t n_
   h->lds_bytes = lds;
 
   // state: x z angle seed (8 B) | step_count env_step episode (4 B) | err | stats |
-  // spawn-ahead: pre (2 x 5 x 8 B) | pre_key (2 x 4 B) | want (4 B)
+  // spawn-ahead: pre (kSlots x 5 x 8 B) | pre_key (kSlots x 8 B) | want tick (4 B)
   const size_t N = (size_t)n_envs, N8 = N * 8, N4 = (N * 4 + 255) & ~255ul;
-  const size_t total = 4 * N8 + 3 * N4 + 256 + 256 + 10 * N8 + 3 * N4;
+  const size_t S = (size_t)dt::kSlots;
+  const size_t spawn_at = 4 * N8 + 3 * N4 + 512;
+  const size_t total = spawn_at + 6 * S * N8 + 2 * N4;
   if (hipMalloc(&h->st_buf, total) != hipSuccess) return fail("hipMalloc(state)");
   if (hipMemset(h->st_buf, 0, total) != hipSuccess) return fail("hipMemset(state)");
   char* sb = (char*)h->st_buf;
@@ -671,9 +771,10 @@ int dt_create(const dt_config* cfg, const dt_map* map, uint64_t seed, int32_t n_
   h->st.episode = (uint32_t*)(sb + 4 * N8 + 2 * N4);
   h->st.err = (uint32_t*)(sb + 4 * N8 + 3 * N4);
   h->st.stats = (unsigned long long*)(sb + 4 * N8 + 3 * N4 + 256);
-  h->st.pre = (double*)(sb + 4 * N8 + 3 * N4 + 512);
-  h->st.pre_key = (uint32_t*)(sb + 14 * N8 + 3 * N4 + 512);
-  h->st.want = (uint32_t*)(sb + 14 * N8 + 5 * N4 + 512);
+  h->st.pre = (double*)(sb + spawn_at);
+  h->st.pre_key = (uint64_t*)(sb + spawn_at + 5 * S * N8);
+  h->st.want = (uint32_t*)(sb + spawn_at + 6 * S * N8);
+  h->st.tick = (uint32_t*)(sb + spawn_at + 6 * S * N8 + N4);
   *out = h;
   rc = dt_render_init(h, map);
   if (rc == DT_OK) rc = dt_seed(h, nullptr, seed, 0);
@@ -698,15 +799,15 @@ int dt_destroy(dt_handle* h) {
 }
 
 // Spawn-ahead after the seeds or episode counters changed: drop every slot of
-// envs [e0, e1), want = counter + 1, then fill both slots (synchronous).
+// envs [e0, e1), want = counter + 1, then fill the window (synchronous).
 static int refill_from_counters(dt_handle* h, int e0, int e1) {
   const size_t n = (size_t)h->n, m = (size_t)(e1 - e0);
   std::vector<uint32_t> ep(m), want(m);
   HIP_OR_FAIL(h, hipMemcpy(ep.data(), h->st.episode + e0, m * 4, hipMemcpyDeviceToHost));
   for (size_t i = 0; i < m; ++i) want[i] = ep[i] + 1u;
   HIP_OR_FAIL(h, hipMemcpy(h->st.want + e0, want.data(), m * 4, hipMemcpyHostToDevice));
-  HIP_OR_FAIL(h, hipMemset(h->st.pre_key + e0, 0xFF, m * 4));
-  HIP_OR_FAIL(h, hipMemset(h->st.pre_key + n + e0, 0xFF, m * 4));
+  for (size_t q = 0; q < (size_t)dt::kSlots; ++q)
+    HIP_OR_FAIL(h, hipMemset(h->st.pre_key + q * n + e0, 0xFF, m * 8));
   hipLaunchKernelGGL(refill_kernel, dim3(refill_grid(h->n, kRefillEnvs)), dim3(kBlock), h->lds_bytes, (hipStream_t)0,
                      h->st, h->map, h->geo, h->n, h->sc.max_spawn_attempts, h->env_base);
   HIP_OR_FAIL(h, hipGetLastError());
@@ -763,8 +864,9 @@ int dt_step_masked(dt_handle* h, const uint8_t* mask, const float* actions, doub
   const int gs = (h->n + kBlock - 1) / kBlock;
   const int grid = gs + (h->sc.auto_reset ? refill_grid(h->n, kRefillEnvs) : 0);
   hipLaunchKernelGGL(step_kernel, dim3(grid), dim3(kBlock), h->lds_bytes, s, h->st, h->map,
-                     h->geo, h->sc, h->n, h->env_base, (const float2*)actions, reward, reward_mod,
-                     done, (float2*)obs, lanepos, tile, gs, h->sc.max_spawn_attempts, mask);
+                     h->geo, h->sc, h->n, h->env_base, 1, (const float2*)actions, reward,
+                     reward_mod, done, (float2*)obs, lanepos, tile, gs, h->sc.max_spawn_attempts,
+                     mask);
   HIP_OR_FAIL(h, hipGetLastError());
   return DT_OK;
 }
@@ -772,6 +874,24 @@ int dt_step_masked(dt_handle* h, const uint8_t* mask, const float* actions, doub
 int dt_step(dt_handle* h, const float* actions, double* reward, double* reward_mod,
             uint8_t* done, float* obs, double* lanepos, int32_t* tile, void* stream) {
   return dt_step_masked(h, nullptr, actions, reward, reward_mod, done, obs, lanepos, tile, stream);
+}
+
+int dt_step_many(dt_handle* h, int32_t k, const float* actions, double* reward,
+                 double* reward_mod, uint8_t* done, float* obs, void* stream) {
+  if (!h) return DT_E_ARG;
+  if (k < 1 || !actions || !reward || !reward_mod || !done) {
+    h->err = "dt_step_many: k >= 1, actions, reward, reward_mod and done are required";
+    return DT_E_ARG;
+  }
+  hipStream_t s = (hipStream_t)stream;
+  const int gs = (h->n + kBlock - 1) / kBlock;
+  const int grid = gs + (h->sc.auto_reset ? refill_grid(h->n, kRefillEnvs) : 0);
+  hipLaunchKernelGGL(step_kernel, dim3(grid), dim3(kBlock), h->lds_bytes, s, h->st, h->map,
+                     h->geo, h->sc, h->n, h->env_base, (int)k, (const float2*)actions, reward,
+                     reward_mod, done, (float2*)obs, (double*)nullptr, (int32_t*)nullptr, gs,
+                     h->sc.max_spawn_attempts, (const uint8_t*)nullptr);
+  HIP_OR_FAIL(h, hipGetLastError());
+  return DT_OK;
 }
 
 int dt_lane_pos(dt_handle* h, double* lanepos, int32_t* tile, void* stream) {

@@ -39,16 +39,20 @@ struct State {
   uint32_t* episode;
   uint32_t* err;  // one word, OR of kErr*
   unsigned long long* stats;  // [4] sim steps, decisions, resets, episodes done
-  // spawn-ahead: slot k & 1 of env e holds the reset pose of spawn key k
-  // (x, z, angle, lane dist, angle_rad) when pre_key[k & 1][e] == k (bit 31:
-  // the spawn failed); want[e] = the highest key that must be ready, one past
-  // the key the env's next reset consumes (its episode counter)
-  double* pre;                // [2][5][n]
-  uint32_t* pre_key;          // [2][n]
+  // spawn-ahead: slot k % kSlots of env e holds the reset pose
+  // of spawn key k (x, z, angle, lane dist, angle_rad) when the low word of
+  // pre_key[k % kSlots][e] is k (bit 31: the spawn failed); its high word is
+  // the launch tick the slot was written in.  want[e] - 1 = the env's episode
+  // counter as its last launch left it; the window [want - 1, want - 1 +
+  // kSlots) is kept filled.  tick[e] counts the step launches over env e.
+  double* pre;                // [kSlots][5][n]
+  uint64_t* pre_key;          // [kSlots][n]
   uint32_t* want;             // [n]
+  uint32_t* tick;             // [n]
 };
 constexpr uint32_t kKeyFailed = 0x80000000u;
 constexpr uint32_t kKeyNone = 0xFFFFFFFFu;
+constexpr int kSlots = 8;    // power of two
 
 // One atomic per wave: the lane sum of v (0 <= v <= vmax, vmax wave-uniform)
 // from one ballot per bit, lane 0 adds.

@@ -163,6 +163,24 @@ class VecEnv:
         self._check(rc, 'dt_step')
         return out
 
+    def step_many_into(self, actions, out):
+        """k decisions in one launch (dt_step_many): actions [k, n, 2] f32 on the
+        device, out a StepOutput(k * n, ...) whose entries of decision d are at
+        [d * n:(d + 1) * n] (view them as [k, n]); lanepos/tile are not
+        produced.  Same results as k step_into calls."""
+        k = int(actions.shape[0]) if actions.dim() == 3 else 0
+        if actions.dtype != torch.float32 or not actions.is_contiguous() or \
+                actions.device != self.device or k < 1 or tuple(actions.shape[1:]) != (self.n, 2):
+            raise ValueError('actions must be a contiguous float32 [k,%d,2] tensor on %s'
+                             % (self.n, self.device))
+        if out.reward.numel() != k * self.n or (out.obs is not None and
+                                                out.obs.shape[0] != k * self.n):
+            raise ValueError('out must be a StepOutput of k * n = %d entries' % (k * self.n))
+        self._check(self._L.dt_step_many(self._h, k, _ptr(actions), _ptr(out.reward),
+                                         _ptr(out.reward_mod), _ptr(out.done), _ptr(out.obs),
+                                         self._stream()), 'dt_step_many')
+        return out
+
     def capture(self, actions, out=None, render=None):
         """StepGraph of len(actions) consecutive decisions (see StepGraph)."""
         return StepGraph(self, actions, out or self.out, render)

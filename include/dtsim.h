@@ -187,6 +187,16 @@ int dt_step_masked(dt_handle* h, const uint8_t* mask, const float* actions, doub
                    double* reward_mod, uint8_t* done, float* obs, double* lanepos, int32_t* tile,
                    void* stream);
 
+/* k consecutive dt_step calls in one launch (plus a spawn-ahead refill launch):
+ * the same results as k dt_step calls over actions[d], with the outputs of
+ * decision d at [d * n + env].  The explorer's rollout loop
+ * (training/explorers.py) over k actions known ahead, e.g. random ones.
+ *   actions    device [k,n,2] f32                                          required
+ *   reward, reward_mod  device [k,n] f64; done device [k,n] u8             required
+ *   obs        device [k,n,2] f32, as dt_step's                            nullable */
+int dt_step_many(dt_handle* h, int32_t k, const float* actions, double* reward,
+                 double* reward_mod, uint8_t* done, float* obs, void* stream);
+
 /* Replaces: Simulator.get_lane_pos2(cur_pos, cur_angle) for every env (no step).
  * lanepos device [n,4] f64 (NaN if NotInLane); tile device [n] i32 (nullable). */
 int dt_lane_pos(dt_handle* h, double* lanepos, int32_t* tile, void* stream);

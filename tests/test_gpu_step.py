@@ -247,3 +247,48 @@ def test_step_graph_chunks_match_eager(gpu):
     assert env1.stats() == env2.stats()
     env1.check()
     env2.check()
+
+
+@pytest.mark.parametrize('k,map_name', [(1, 'loop_empty'), (7, 'loop_empty'), (30, 'zigzag'),
+                                        (12, 'loop_obstacles'), (64, 'small_loop')])
+def test_step_many_matches_oracle(gpu, k, map_name):
+    """dt_step_many: k decisions per launch == k oracle steps, per decision;
+    three launches back to back, then an eager dt_step continues the state.
+    Envs finishing more often than their ready slots cover spawn inline."""
+    from aido1_amd.vec_env import StepOutput
+    n = 4096
+    env, ob = make_pair(n, map_name=map_name)
+    env.reset()
+    ob.reset()
+    rng = np.random.default_rng(31)
+    out = StepOutput(k * n, gpu, lanepos=False, tile=False)
+    ndone = 0
+    multi = 0
+    for _ in range(3):
+        a = rng.uniform(0, 1, (k, n, 2)).astype(np.float32)
+        env.step_many_into(torch.from_numpy(a).to(gpu), out)
+        torch.cuda.synchronize()
+        rew = out.reward.view(k, n).cpu().numpy()
+        rewm = out.reward_mod.view(k, n).cpu().numpy()
+        done = out.done.view(k, n).cpu().numpy()
+        obs = out.obs.view(k, n, 2).cpu().numpy()
+        per_env = np.zeros(n, np.int64)
+        for d in range(k):
+            ref = ob.step(a[d])
+            assert np.array_equal(done[d], ref['done']), d
+            assert np.max(np.abs(rew[d] - ref['reward'])) <= TOL_TIGHT, d
+            assert np.max(np.abs(rewm[d] - ref['reward_mod'])) <= TOL_TIGHT, d
+            assert np.max(np.abs(obs[d] - ref['obs'])) <= 1e-6, d
+            per_env += ref['done']
+        compare_state(env, ob)
+        ndone += int(per_env.sum())
+        multi += int((per_env >= 8).sum())
+    assert ndone > 0
+    a = rng.uniform(0, 1, (n, 2)).astype(np.float32)
+    out1 = env.step_into(torch.from_numpy(a).to(gpu))
+    ref = ob.step(a)
+    torch.cuda.synchronize()
+    compare_out(out1, ref)
+    compare_state(env, ob)
+    print('k=%d %s: dones %d, envs with >= 8 in a launch %d' % (k, map_name, ndone, multi))
+    env.check()
