@@ -46,12 +46,22 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
 #             consumed key writes its slot record 40 + key 4                      = 52
 STEP_BYTES_PER_ENV = 132 + 57 + 20
 SPAWN_BYTES_PER_RESET = 52
+# One dt_step_many launch of k decisions (step_kernel over k):
+# per env, once: reads pose 24 + step_count,env_step 8 + episode,tick 8 + seed 8
+#                + the 8 slot words 64 = 112; writes pose 24 + counters 8 + tick 4 = 36
+#   refill scan: want 4 + tick 4 + slot words 64 + seed 8 = 80
+# per env and decision: action 8 + reward 8 + reward_mod 8 + done 1 + obs 8 = 33
+# per reset: the slot's pose 40 read; episode + want 8 written; the refill of the
+#            consumed key writes its slot record 40 + word 8 = 96
+MANY_BYTES_PER_ENV = 112 + 36 + 80
+MANY_BYTES_PER_ENV_DECISION = 33
+MANY_BYTES_PER_RESET = 96
 
 
 def parse():
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
-    p.add_argument('--steps', type=int, default=300)
+    p.add_argument('--steps', type=int, default=320)
     p.add_argument('--warmup', type=int, default=30)
     p.add_argument('--envs', type=int, default=4096)
     p.add_argument('--map', default='loop_empty')
@@ -62,9 +72,12 @@ def parse():
     p.add_argument('--batch-size', type=int, default=0, help='train: 0 = config.json (64)')
     p.add_argument('--buffer-size', type=int, default=131072)
     p.add_argument('--updates-per-step', type=int, default=1)
+    p.add_argument('--many', type=int, default=16,
+                   help='lane config: decisions per dt_step_many launch (0 = dt_step per '
+                        'decision, in HIP graphs of --graph-steps)')
     p.add_argument('--graph-steps', type=int, default=30,
-                   help='lane config: decisions per HIP-graph replay (VecEnv.capture); '
-                        '0 = one eager launch per decision')
+                   help='lane config with --many 0: decisions per HIP-graph replay '
+                        '(VecEnv.capture); 0 = one eager launch per decision')
     p.add_argument('--seed', type=int, default=1234)
     p.add_argument('--cpu-seconds', type=float, default=1.5,
                    help='per-process seconds of the CPU baseline sample (0 = skip)')
@@ -176,10 +189,24 @@ def main():
         if render is not None:
             env.render_into(render, fresh=out.done)
 
-    for i in range(args.warmup):
-        one(i)
+    M = max(0, args.many) if render is None else 0
+    G = max(0, args.graph_steps) if render is None and not M else 0
+    if M:
+        # k = M decisions per launch (dt_step_many), outputs of every decision kept
+        mb = list(range(0, args.steps, M)) + [args.steps]   # the last takes the rest
+        chunks = list(zip(mb[:-1], mb[1:]))
+        outs = {}
+        for a, b in chunks + [(0, M)]:
+            if b - a not in outs:
+                outs[b - a] = StepOutput((b - a) * n, dev, lanepos=False, tile=False)
+        mev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+               for _ in chunks]
+        for i in range(0, args.warmup, M):   # warmup launches of M decisions too
+            env.step_many_into(actions[:M], outs[M])
+    else:
+        for i in range(args.warmup):
+            one(i)
     torch.cuda.synchronize(dev)
-    G = args.graph_steps if render is None else 0
     if G:
         # the timed decisions as HIP graphs of G launches each, captured up
         # front over their own action slices (StepGraph)
@@ -190,14 +217,19 @@ def main():
                for _ in graphs]
     env.stats(reset=True)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)] if not G else []
+          for _ in range(args.steps)] if not (G or M) else []
     rev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
            for _ in range(args.steps)] if render is not None else None
     if world > 1:
         dist.barrier()
     torch.cuda.synchronize(dev)
     t0 = time.perf_counter()
-    if G:
+    if M:
+        for c, (a, b) in enumerate(chunks):
+            mev[c][0].record()
+            env.step_many_into(actions[args.warmup + a:args.warmup + b], outs[b - a])
+            mev[c][1].record()
+    elif G:
         for c, gr in enumerate(graphs):
             gev[c][0].record()
             gr.replay()
@@ -218,7 +250,10 @@ def main():
     elapsed = time.perf_counter() - t0
     st = env.stats()
     env.check()
-    if G:  # per launch inside the graphs: replay time / launches (gaps included)
+    if M:  # per decision: launch times / decisions (a launch runs M of them)
+        step_ms = float(np.sum([a.elapsed_time(b) for a, b in mev])) / args.steps
+        launch_ms = float(np.mean([a.elapsed_time(b) for a, b in mev]))
+    elif G:  # per launch inside the graphs: replay time / launches (gaps included)
         step_ms = float(np.sum([a.elapsed_time(b) for a, b in gev])) / args.steps
     else:
         step_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
@@ -234,7 +269,13 @@ def main():
     tmax = float(tmax.item())
 
     if rank == 0:
-        if render is None:
+        if render is None and M:
+            # one launch = len(chunks) of them over args.steps decisions
+            kname, kms = 'step_kernel', launch_ms
+            per = args.steps / len(chunks)
+            bytes_per_launch = ((MANY_BYTES_PER_ENV + MANY_BYTES_PER_ENV_DECISION * per) * n +
+                                MANY_BYTES_PER_RESET * resets / len(chunks))
+        elif render is None:
             kname, kms = 'step_kernel', step_ms
             bytes_per_launch = STEP_BYTES_PER_ENV * n + SPAWN_BYTES_PER_RESET * resets / max(
                 1.0, decisions / n)
@@ -266,7 +307,8 @@ def main():
                 'map': args.map, 'envs_per_gpu': n, 'repeat_actions': 3,
                 'actions': 'U[0,1)^2 wheel velocities, resident in HBM',
                 'auto_reset': True, 'global_envs': n * world,
-                'launch': ('HIP graphs of %d decisions (VecEnv.capture)' % G if G else
+                'launch': ('dt_step_many: %d decisions per launch' % M if M else
+                           'HIP graphs of %d decisions (VecEnv.capture)' % G if G else
                            'one eager launch per decision'),
                 'parallelism': 'env shards (%d x %d), no collective' % (world, n)},
             'counts': {'env_steps': sim_steps, 'decisions': decisions, 'resets': resets,
@@ -278,6 +320,9 @@ def main():
         }
         if render_ms is not None:
             line['step_kernel_ms'] = step_ms
+        if M:
+            line['roofline']['decisions_per_launch'] = args.steps / len(chunks)
+            line['step_ms_per_decision'] = step_ms
         if world == 1 and args.cpu_seconds > 0:
             line['cpu_baseline'] = cpu_baseline(args.cpu_seconds, args.cpu_procs, args.map)
         else:
