@@ -267,6 +267,10 @@ __device__ __forceinline__ void sim_decision(const MapLds& M, const dt::Geo& g, 
       // _compute_done_reward (A11)
       double r;
       bool sd = false;
+      // get_lane_pos2 of the new pose ahead of _valid_pose: two independent
+      // float64 chains for the scheduler; used below only if the pose is valid
+      double lq[4] = {0.0, 0.0, 0.0, 0.0};
+      const bool lq_inl = dt::lane_pos<false>(M, g, x, z, c, s, lq);
       const bool vp = dt::valid_pose(M, g, x, z, c, s, 1.0);
       if (rep == 1) STAMP(12);
       if (!vp) {
@@ -281,7 +285,11 @@ __device__ __forceinline__ void sim_decision(const MapLds& M, const dt::Geo& g, 
         const double pen =
             M.n_obj ? dt::proximity_penalty(M, g, x + g.off * c, z + g.off * (-s)) : 0.0;
         lp_fresh = true;
-        lp_inl = dt::lane_pos<false>(M, g, x, z, c, s, lp);
+        lp_inl = lq_inl;
+        lp[0] = lq[0];
+        lp[1] = lq[1];
+        lp[2] = lq[2];
+        lp[3] = lq[3];
         if (rep == 1) STAMP(13);
         if (lp_inl) {
           const double ad = fabs(lp[0]);
