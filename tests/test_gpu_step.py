@@ -254,7 +254,9 @@ def test_step_graph_chunks_match_eager(gpu):
 def test_step_many_matches_oracle(gpu, k, map_name):
     """dt_step_many: k decisions per launch == k oracle steps, per decision;
     three launches back to back, then an eager dt_step continues the state.
-    Envs finishing more often than their ready slots cover spawn inline."""
+    Envs finishing more often than their ready slots cover spawn inline.
+    (The two-wave step_pair_kernel; test_step_many_single_wave covers the
+    one-wave path.)"""
     from aido1_amd.vec_env import StepOutput
     n = 4096
     env, ob = make_pair(n, map_name=map_name)
@@ -292,3 +294,18 @@ def test_step_many_matches_oracle(gpu, k, map_name):
     compare_state(env, ob)
     print('k=%d %s: dones %d, envs with >= 8 in a launch %d' % (k, map_name, ndone, multi))
     env.check()
+
+
+def test_step_many_single_wave(gpu):
+    """DTSIM_STEP_PAIR=0 (step_kernel over k decisions) in a child process, the
+    setting being read once per process: the same check at k = 16 and 64."""
+    import os
+    import subprocess
+    import sys
+    code = ('import sys, pytest; sys.exit(pytest.main(["-x", "-q", "-m", "gpu", "-p", '
+            '"no:cacheprovider", "-k", "step_many_matches_oracle and (16 or 64 or 30)", '
+            '"%s"]))' % os.path.abspath(__file__))
+    env = dict(os.environ, DTSIM_STEP_PAIR='0')
+    r = subprocess.run([sys.executable, '-c', code], env=env, cwd=os.path.dirname(__file__),
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
