@@ -270,8 +270,11 @@ def main():
 
     if rank == 0:
         if render is None and M:
-            # one launch = len(chunks) of them over args.steps decisions
-            kname, kms = 'step_kernel', launch_ms
+            # one launch = len(chunks) of them over args.steps decisions;
+            # step_pair_kernel unless DTSIM_STEP_PAIR=0
+            kname = ('step_kernel' if os.environ.get('DTSIM_STEP_PAIR', '1').startswith('0')
+                     else 'step_pair_kernel')
+            kms = launch_ms
             per = args.steps / len(chunks)
             bytes_per_launch = ((MANY_BYTES_PER_ENV + MANY_BYTES_PER_ENV_DECISION * per) * n +
                                 MANY_BYTES_PER_RESET * resets / len(chunks))

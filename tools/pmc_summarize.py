@@ -14,8 +14,8 @@ import sys
 
 ROUND = sys.argv[1] if len(sys.argv) > 1 else 'r01'
 OUT = 'gpurun_out'
-KERNELS = {'lane': ('step_kernel', ['step_kernel']),
-           'render': ('render_kernel', ['render_kernel'])}
+KERNELS = {'lane': [('step_pair_kernel', ['step_pair_kernel']), ('step_kernel', ['step_kernel'])],
+           'render': [('render_kernel', ['render_kernel'])]}
 
 
 def per_dispatch(path, needle):
@@ -36,7 +36,10 @@ def main():
             shutil.copy(f, 'profiles/%s_%s_kernel_stats.csv' % (ROUND, cfg))
             print('copied', f)
     out = {}
-    for cfg, (label, names) in KERNELS.items():
+    if os.path.exists('profiles/pmc_traffic.json'):   # keep kernels this run did not profile
+        with open('profiles/pmc_traffic.json') as f:
+            out = json.load(f)
+    for cfg, label, names in [(c, l, n) for c, ks in KERNELS.items() for l, n in ks]:
         fetch = write = 0.0
         ok = True
         for ctr in ('FETCH_SIZE', 'WRITE_SIZE'):
