@@ -107,12 +107,16 @@ __device__ inline void put_slot(const dt::State& st, int n, int e, uint32_t key,
                                 uint32_t tag, double x, double z, double a, double dist,
                                 double arad) {
   const size_t sl = key % (uint32_t)dt::kSlots;
-  double* p = st.pre + sl * 5 * (size_t)n + e;
+  double* p = st.pre + sl * dt::kSlotRec * (size_t)n + e;
+  double sa = 0.0, ca = 1.0;
+  sincos(a, &sa, &ca);
   p[0] = x;
   p[(size_t)n] = z;
   p[2 * (size_t)n] = a;
   p[3 * (size_t)n] = dist;
   p[4 * (size_t)n] = arad;
+  p[5 * (size_t)n] = sa;
+  p[6 * (size_t)n] = ca;
   const uint64_t w = ((uint64_t)tag << 32) | (ok ? key : (key | dt::kKeyFailed));
   __hip_atomic_store(st.pre_key + sl * n + e, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -447,7 +451,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(dt::State st, dt::MapDev m
   double c = 0.0, s = 0.0;
   sincos(ang, &s, &c);
   unsigned nsim_t = 0, act_t = 0, resets_t = 0, dones_t = 0;
-  double rp[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  double rp[dt::kSlotRec] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 1.0};
   for (int d = 0; d < k; ++d) {
     // the next decision's action and this decision's reset pose (if ready),
     // loaded while the decision runs
@@ -457,7 +461,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(dt::State st, dt::MapDev m
     if (slot_ready) {
       const size_t sl = key % (uint32_t)dt::kSlots;
 #pragma unroll
-      for (int q = 0; q < 5; ++q) rp[q] = st.pre[(sl * 5 + q) * (size_t)n + ei];
+      for (int q = 0; q < dt::kSlotRec; ++q) rp[q] = st.pre[(sl * dt::kSlotRec + q) * (size_t)n + ei];
     }
     asm volatile("" ::: "memory");  // keep the loads here, ahead of the decision
 
@@ -483,6 +487,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(dt::State st, dt::MapDev m
         rp[2] = sa;
         rp[3] = slp[0];
         rp[4] = slp[1];
+        sincos(sa, &rp[5], &rp[6]);
         ok = sok;
       }
     }
@@ -523,7 +528,8 @@ __global__ __launch_bounds__(kBlock) void step_kernel(dt::State st, dt::MapDev m
       x = rp[0];
       z = rp[1];
       ang = rp[2];
-      sincos(ang, &s, &c);
+      s = rp[5];  // sincos(ang), made with the slot
+      c = rp[6];
       step_count = 0u;
       env_step = 0u;
       key += 1u;
@@ -554,7 +560,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(dt::State st, dt::MapDev m
       // the window moves past the consumed keys only once the slot loads have
       // returned: the store's value depends on the last of them (loads return
       // in order)
-      __hip_atomic_store(st.want + e, key + 1u + after_load(rp[4]), __ATOMIC_RELAXED,
+      __hip_atomic_store(st.want + e, key + 1u + after_load(rp[dt::kSlotRec - 1]), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -622,7 +628,7 @@ __global__ __launch_bounds__(kBlock) void step_pair_kernel(dt::State st, dt::Map
   sincos(ang, &s, &c);
   unsigned nsim_t = 0, act_t = 0, resets_t = 0, dones_t = 0;
   uint32_t phase = 0u;
-  double rp[5] = {0.0, 0.0, 0.0, 0.0, 0.0};
+  double rp[dt::kSlotRec] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 1.0};
   for (int d = 0; d < k; ++d) {
     const float2 an = act[(size_t)(d + 1 < k ? d + 1 : d) * n + ei];
     const uint32_t rel = key - key0;
@@ -630,7 +636,7 @@ __global__ __launch_bounds__(kBlock) void step_pair_kernel(dt::State st, dt::Map
     if (slot_ready) {
       const size_t sl = key % (uint32_t)dt::kSlots;
 #pragma unroll
-      for (int q = 0; q < 5; ++q) rp[q] = st.pre[(sl * 5 + q) * (size_t)n + ei];
+      for (int q = 0; q < dt::kSlotRec; ++q) rp[q] = st.pre[(sl * dt::kSlotRec + q) * (size_t)n + ei];
     }
     asm volatile("" ::: "memory");
 
@@ -655,6 +661,7 @@ __global__ __launch_bounds__(kBlock) void step_pair_kernel(dt::State st, dt::Map
         rp[2] = sa;
         rp[3] = slp[0];
         rp[4] = slp[1];
+        sincos(sa, &rp[5], &rp[6]);
         ok = sok;
       }
     }
@@ -686,7 +693,8 @@ __global__ __launch_bounds__(kBlock) void step_pair_kernel(dt::State st, dt::Map
       x = rp[0];
       z = rp[1];
       ang = rp[2];
-      sincos(ang, &s, &c);
+      s = rp[5];  // sincos(ang), made with the slot
+      c = rp[6];
       step_count = 0u;
       env_step = 0u;
       key += 1u;
@@ -714,7 +722,7 @@ __global__ __launch_bounds__(kBlock) void step_pair_kernel(dt::State st, dt::Map
     __hip_atomic_store(st.tick + e, tick + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (key != key0) {
       st.episode[e] = key;
-      __hip_atomic_store(st.want + e, key + 1u + after_load(rp[4]), __ATOMIC_RELAXED,
+      __hip_atomic_store(st.want + e, key + 1u + after_load(rp[dt::kSlotRec - 1]), __ATOMIC_RELAXED,
                          __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -976,11 +984,12 @@ int dt_create(const dt_config* cfg, const dt_map* map, uint64_t seed, int32_t n_
   h->lds_bytes = lds;
 
   // state: x z angle seed (8 B) | step_count env_step episode (4 B) | err | stats |
-  // spawn-ahead: pre (kSlots x 5 x 8 B) | pre_key (kSlots x 8 B) | want tick (4 B)
+  // spawn-ahead: pre (kSlots x kSlotRec x 8 B) | pre_key (kSlots x 8 B) | want tick (4 B)
   const size_t N = (size_t)n_envs, N8 = N * 8, N4 = (N * 4 + 255) & ~255ul;
   const size_t S = (size_t)dt::kSlots;
   const size_t spawn_at = 4 * N8 + 3 * N4 + 512;
-  const size_t total = spawn_at + 6 * S * N8 + 2 * N4;
+  const size_t R = (size_t)dt::kSlotRec;
+  const size_t total = spawn_at + (R + 1) * S * N8 + 2 * N4;
   if (hipMalloc(&h->st_buf, total) != hipSuccess) return fail("hipMalloc(state)");
   if (hipMemset(h->st_buf, 0, total) != hipSuccess) return fail("hipMemset(state)");
   char* sb = (char*)h->st_buf;
@@ -994,9 +1003,9 @@ int dt_create(const dt_config* cfg, const dt_map* map, uint64_t seed, int32_t n_
   h->st.err = (uint32_t*)(sb + 4 * N8 + 3 * N4);
   h->st.stats = (unsigned long long*)(sb + 4 * N8 + 3 * N4 + 256);
   h->st.pre = (double*)(sb + spawn_at);
-  h->st.pre_key = (uint64_t*)(sb + spawn_at + 5 * S * N8);
-  h->st.want = (uint32_t*)(sb + spawn_at + 6 * S * N8);
-  h->st.tick = (uint32_t*)(sb + spawn_at + 6 * S * N8 + N4);
+  h->st.pre_key = (uint64_t*)(sb + spawn_at + R * S * N8);
+  h->st.want = (uint32_t*)(sb + spawn_at + (R + 1) * S * N8);
+  h->st.tick = (uint32_t*)(sb + spawn_at + (R + 1) * S * N8 + N4);
   *out = h;
   rc = dt_render_init(h, map);
   if (rc == DT_OK) rc = dt_seed(h, nullptr, seed, 0);

@@ -40,12 +40,13 @@ struct State {
   uint32_t* err;  // one word, OR of kErr*
   unsigned long long* stats;  // [4] sim steps, decisions, resets, episodes done
   // spawn-ahead: slot k % kSlots of env e holds the reset pose
-  // of spawn key k (x, z, angle, lane dist, angle_rad) when the low word of
+  // of spawn key k (x, z, angle, lane dist, angle_rad, sin and cos of the
+  // angle) when the low word of
   // pre_key[k % kSlots][e] is k (bit 31: the spawn failed); its high word is
   // the launch tick the slot was written in.  want[e] - 1 = the env's episode
   // counter as its last launch left it; the window [want - 1, want - 1 +
   // kSlots) is kept filled.  tick[e] counts the step launches over env e.
-  double* pre;                // [kSlots][5][n]
+  double* pre;                // [kSlots][kSlotRec][n]
   uint64_t* pre_key;          // [kSlots][n]
   uint32_t* want;             // [n]
   uint32_t* tick;             // [n]
@@ -53,6 +54,7 @@ struct State {
 constexpr uint32_t kKeyFailed = 0x80000000u;
 constexpr uint32_t kKeyNone = 0xFFFFFFFFu;
 constexpr int kSlots = 8;    // power of two
+constexpr int kSlotRec = 7;  // x, z, angle, lane dist, angle_rad, sin, cos
 
 // One atomic per wave: the lane sum of v (0 <= v <= vmax, vmax wave-uniform)
 // from one ballot per bit, lane 0 adds.

@@ -36,26 +36,26 @@ sys.path.insert(0, REPO)
 METRIC = 'env-steps/sec (whole node) at 4096 envs/GPU; pose/reward max-abs-err vs CPU ref'
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
 
-# Algorithmic HBM bytes of one dt_step launch (step_kernel: step lanes + the
-# spawn-ahead refill blocks), DESIGN.md §3.1-3.2:
-# step, per env:  reads pose 24 + step_count,env_step 8 + action 8 + episode 4
-#                 + both spawn-ahead slots (keys 8, records 80; read up front)  = 132
-#                 writes pose 24 + counters 8 + reward 8 + reward_mod 8 + done 1 + obs 8 = 57
-# refill scan, per env: reads want 4 + both slot keys 8 + seed 8                 = 20
-# per reset:  the step lane writes episode 4 + want 4; the refill of the
-#             consumed key writes its slot record 40 + key 4                      = 52
-STEP_BYTES_PER_ENV = 132 + 57 + 20
-SPAWN_BYTES_PER_RESET = 52
-# One dt_step_many launch of k decisions (step_kernel over k):
+# Algorithmic HBM bytes of one dt_step launch (step_kernel, k = 1: step lanes +
+# the spawn-ahead refill blocks), DESIGN.md §3.1-3.2:
+# step, per env:  reads pose 24 + step_count,env_step 8 + action 8 + episode,tick 8
+#                 + seed 8 + the 8 slot words 64                                 = 120
+#                 writes pose 24 + counters 8 + tick 4 + reward 8 + reward_mod 8
+#                 + done 1 + obs 8                                               = 61
+# refill scan, per env: want 4 + tick 4 + slot words 64 + seed 8                 = 80
+# per reset:  the slot's record 56 read; episode + want 8 written; the refill of
+#             the consumed key writes its slot record 56 + word 8                = 128
+STEP_BYTES_PER_ENV = 120 + 61 + 80
+SPAWN_BYTES_PER_RESET = 128
+# One dt_step_many launch of k decisions (step_pair_kernel over k):
 # per env, once: reads pose 24 + step_count,env_step 8 + episode,tick 8 + seed 8
 #                + the 8 slot words 64 = 112; writes pose 24 + counters 8 + tick 4 = 36
-#   refill scan: want 4 + tick 4 + slot words 64 + seed 8 = 80
+#   refill scan: 80 (as above)
 # per env and decision: action 8 + reward 8 + reward_mod 8 + done 1 + obs 8 = 33
-# per reset: the slot's pose 40 read; episode + want 8 written; the refill of the
-#            consumed key writes its slot record 40 + word 8 = 96
+# per reset: 128 (as above)
 MANY_BYTES_PER_ENV = 112 + 36 + 80
 MANY_BYTES_PER_ENV_DECISION = 33
-MANY_BYTES_PER_RESET = 96
+MANY_BYTES_PER_RESET = 128
 
 
 def parse():
