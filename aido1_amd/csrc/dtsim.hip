@@ -102,6 +102,7 @@ __device__ inline void map_action(int mode, float a0, float a1, double& vl, doub
 // A standalone refill (dt_seed, dt_reset: no step lane runs) tags tick - 1,
 // usable by the next launch.
 constexpr int kBlock = 256;        // step and refill blocks (4 waves)
+constexpr int kPairBlock = 128;    // step_pair_kernel launches: one pair of waves
 
 __device__ inline void put_slot(const dt::State& st, int n, int e, uint32_t key, bool ok,
                                 uint32_t tag, double x, double z, double a, double dist,
@@ -591,7 +592,7 @@ __global__ __launch_bounds__(kBlock) void step_pair_kernel(dt::State st, dt::Map
   __builtin_amdgcn_s_setprio(3);
   const int wave = (int)(threadIdx.x >> 6), role = wave & 1, pair = wave >> 1;
   const int lane = threadIdx.x & 63;
-  const int e = (int)blockIdx.x * (kBlock / 2) + pair * 64 + lane;
+  const int e = (int)blockIdx.x * (int)(blockDim.x / 2) + pair * 64 + lane;
   const bool active = e < n;
   const int ei = active ? e : 0;
 
@@ -1119,8 +1120,10 @@ int dt_step_many(dt_handle* h, int32_t k, const float* actions, double* reward,
   static const bool pair = !(getenv("DTSIM_STEP_PAIR") && getenv("DTSIM_STEP_PAIR")[0] == '0');
   const int rb = h->sc.auto_reset ? refill_grid(h->n, kRefillEnvs) : 0;
   if (pair) {
-    const int gs = (h->n + kBlock / 2 - 1) / (kBlock / 2);
-    hipLaunchKernelGGL(step_pair_kernel, dim3(gs + rb), dim3(kBlock), h->lds_bytes, s, h->st,
+    // one pair (two waves, 64 envs) per workgroup: the exchange barriers stay
+    // pair-local; the refill blocks of the launch run with 128 threads too
+    const int gs = (h->n + 63) / 64;
+    hipLaunchKernelGGL(step_pair_kernel, dim3(gs + rb), dim3(kPairBlock), h->lds_bytes, s, h->st,
                        h->map, h->geo, h->sc, h->n, h->env_base, (int)k,
                        (const float2*)actions, reward, reward_mod, done, (float2*)obs, gs,
                        h->sc.max_spawn_attempts);
