@@ -34,6 +34,25 @@ struct dt_handle {
   std::string err;
 };
 
+// Launch entry points run on the handle's GPU whatever the calling thread's
+// current device is (a VecEnv on cuda:1 called from a thread whose current
+// device is 0); the caller's current device is restored on return.
+struct DevGuard {
+  int prev = -1;
+  explicit DevGuard(int device) {
+    if (hipGetDevice(&prev) == hipSuccess && prev != device) {
+      if (hipSetDevice(device) != hipSuccess) prev = -1;
+    } else {
+      prev = -1;
+    }
+  }
+  ~DevGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+  DevGuard(const DevGuard&) = delete;
+  DevGuard& operator=(const DevGuard&) = delete;
+};
+
 // dtrender.hip: lane-marking polylines of the map + default line params
 int dt_render_init(dt_handle* h, const dt_map* map);
 void dt_render_free(dt_handle* h);

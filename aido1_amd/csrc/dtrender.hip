@@ -910,6 +910,7 @@ int dt_render(dt_handle* h, const dt_render_io* io, void* stream) {
     h->err = "dt_render: gray_slot out of range";
     return DT_E_ARG;
   }
+  DevGuard dg(h->device);
   RenderArgs a{};
   a.x = h->st.x;
   a.z = h->st.z;

@@ -1071,6 +1071,7 @@ int dt_seed_env(dt_handle* h, int32_t env, uint64_t seed) {
 
 int dt_reset(dt_handle* h, const uint8_t* mask, void* stream) {
   if (!h) return DT_E_ARG;
+  DevGuard dg(h->device);
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(spawn_kernel, dim3(h->n), dim3(kSpawnThreads), h->lds_bytes, s, h->st,
                      h->map, h->geo, h->sc.max_spawn_attempts, h->env_base, mask);
@@ -1089,6 +1090,7 @@ int dt_step_masked(dt_handle* h, const uint8_t* mask, const float* actions, doub
     h->err = "dt_step: actions, reward, reward_mod and done are required";
     return DT_E_ARG;
   }
+  DevGuard dg(h->device);
   hipStream_t s = (hipStream_t)stream;
   // step blocks, then (auto-reset) refill blocks of kRefillEnvs envs: this
   // decision's resets use poses computed in earlier launches, and the refill of
@@ -1115,6 +1117,7 @@ int dt_step_many(dt_handle* h, int32_t k, const float* actions, double* reward,
     h->err = "dt_step_many: k >= 1, actions, reward, reward_mod and done are required";
     return DT_E_ARG;
   }
+  DevGuard dg(h->device);
   hipStream_t s = (hipStream_t)stream;
   // two waves per 64 envs (step_pair_kernel); DTSIM_STEP_PAIR=0: one (step_kernel)
   static const bool pair = !(getenv("DTSIM_STEP_PAIR") && getenv("DTSIM_STEP_PAIR")[0] == '0');
@@ -1141,6 +1144,7 @@ int dt_step_many(dt_handle* h, int32_t k, const float* actions, double* reward,
 
 int dt_lane_pos(dt_handle* h, double* lanepos, int32_t* tile, void* stream) {
   if (!h) return DT_E_ARG;
+  DevGuard dg(h->device);
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(lane_pos_kernel, dim3(grid_of(h->n)), dim3(dt::kWave), h->lds_bytes, s,
                      h->st, h->map, h->geo, h->n, lanepos, tile);

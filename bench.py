@@ -1,11 +1,12 @@
 #!/usr/bin/env python
-"""bench.py — BASELINE.json's metric: env-steps/s (whole node) at 4096 envs/GPU.
+"""bench.py — BASELINE.json's metric: env-steps/s (whole node) at 4096 envs/GPU,
+with pose/reward max-abs-err vs the CPU oracle in the same line.
 
 Workload (BASELINE.json configs[1]): 4096 envs per GPU
 on loop_empty, lane-pose (dist, angle) observation, i.i.d. U[0,1)^2 wheel
 actions (the train.py contract after utils/env_wrappers.py:214-216), Philox
 spawn streams keyed by seed 1234, auto-reset on done or at the 2000-step wrapper
-cap.  One bench "step" = one VecEnv.step = one EnvironmentWrapper.step for every
+cap.  One bench "step" = one decision = one EnvironmentWrapper.step for every
 env = up to repeat_actions (3) Simulator steps each; the unit counted is the
 Simulator step (env-step), read back exactly from the device counters (envs
 that finish mid-repeat run fewer).  Actions for every step are generated and
@@ -13,18 +14,40 @@ resident in HBM before the timed region.
 
   python bench.py [--gpus N --steps K --warmup W] [--config lane|render|actor|train]
 
-Other configs (not the headline line): render = configs[2] (obs pipeline),
-actor = configs[3] (actor in the loop), train = configs[4] (full DDPG: rollout +
-GPU prioritized replay + update + RCCL gradient all-reduce).
+Timed region (config 2): the K decisions are split into equal launches of
+dt_step_many (at most --many decisions each) and the launches are captured in
+ONE HIP graph before the timed region, so the wall clock is the kernels' time
+and not Python's launch cost.  After it, outside the timed region:
+  * parity: the C oracle (oracle/dtsim_oracle.c, test infrastructure) re-runs
+    every env of this rank from the saved start state through the same actions;
+    reward/reward_mod/obs/done of every decision and the end pose are compared
+    with the timed launches' outputs, and a second GPU pass (dt_step, one
+    decision per launch, tile + lane pose asked for) checks tile indices;
+  * render: K dt_render launches (configs[2]'s 120x160 raster + grey +
+    line_detector1 masks) over the same envs, timed per launch with HIP events
+    on the launch stream -> the HBM-bound kernel's roofline, plus a bit-exact
+    check of 64 envs' frames against oracle/render_oracle.c.
 
-N > 1: launched by torch.distributed.run, one rank per GPU; envs shard by
-env_id_base = rank * envs (disjoint spawn streams), no data-path collective;
-timing = barrier + synchronize on both sides, max over ranks; value = all
-ranks' env-steps / that time.  Rank 0 prints one JSON line.
+Other configs (not the headline line): render = configs[2] on its own (step +
+render per decision), actor = configs[3] (actor in the loop), train =
+configs[4] (full DDPG: rollout + GPU prioritized replay + update + RCCL
+gradient all-reduce).
+
+N > 1: `python bench.py --gpus N` starts torch.distributed.run with N ranks as
+a child process BEFORE anything touches the GPU (the driver may also launch
+torch.distributed.run itself; WORLD_SIZE must then equal --gpus).  One rank per
+GPU over RCCL; envs shard by env_id_base = rank * envs (disjoint spawn
+streams), no data-path collective; timing = barrier + synchronize on both
+sides, max over ranks; value = all ranks' env-steps / that time.  Rank 0 prints
+one JSON line with every rank's counts.  `--dry-run` runs the same launcher and
+reduction on CPU over gloo with no kernels (tests/test_bench_launcher.py).
 """
 import argparse
 import json
+import math
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -35,30 +58,25 @@ sys.path.insert(0, REPO)
 
 METRIC = 'env-steps/sec (whole node) at 4096 envs/GPU; pose/reward max-abs-err vs CPU ref'
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
+FP64_VECTOR_PEAK_TFLOPS = 78.6   # MI355X spec: fp64 vector = 1/2 of fp32 vector 157.3 TF
+BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16/fp16 MFMA (spec)
 
-# Algorithmic HBM bytes of one dt_step launch (step_kernel, k = 1: step lanes +
-# the spawn-ahead refill blocks), DESIGN.md §3.1-3.2:
-# step, per env:  reads pose 24 + step_count,env_step 8 + action 8 + episode,tick 8
-#                 + seed 8 + the 8 slot words 64                                 = 120
-#                 writes pose 24 + counters 8 + tick 4 + reward 8 + reward_mod 8
-#                 + done 1 + obs 8                                               = 61
-# refill scan, per env: want 4 + tick 4 + slot words 64 + seed 8                 = 80
-# per reset:  the slot's record 56 read; episode + want 8 written; the refill of
-#             the consumed key writes its slot record 56 + word 8                = 128
-STEP_BYTES_PER_ENV = 120 + 61 + 80
-SPAWN_BYTES_PER_RESET = 128
-# One dt_step_many launch of k decisions (step_pair_kernel over k):
+# algorithmic HBM bytes per env-step of config 2 = action 8 +
+# state read 28 + state write 28 + reward 4 + done 1 + dist/angle 8 + tile 4.
+SURVEY_BYTES_PER_ENV_STEP = 81
+# What one dt_step_many launch of k decisions really has to move (DESIGN.md
+# §3.1; state stays in registers across the k decisions):
 # per env, once: reads pose 24 + step_count,env_step 8 + episode,tick 8 + seed 8
 #                + the 8 slot words 64 = 112; writes pose 24 + counters 8 + tick 4 = 36
-#   refill scan: 80 (as above)
+#   refill scan: want 4 + tick 4 + slot words 64 + seed 8 = 80
 # per env and decision: action 8 + reward 8 + reward_mod 8 + done 1 + obs 8 = 33
-# per reset: 128 (as above)
+# per reset: the slot's 56-B record read, episode + want 8, refilled record 56 + word 8 = 128
 MANY_BYTES_PER_ENV = 112 + 36 + 80
 MANY_BYTES_PER_ENV_DECISION = 33
 MANY_BYTES_PER_RESET = 128
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=320)
@@ -72,22 +90,50 @@ def parse():
     p.add_argument('--batch-size', type=int, default=0, help='train: 0 = config.json (64)')
     p.add_argument('--buffer-size', type=int, default=131072)
     p.add_argument('--updates-per-step', type=int, default=1)
-    p.add_argument('--many', type=int, default=16,
-                   help='lane config: decisions per dt_step_many launch (0 = dt_step per '
-                        'decision, in HIP graphs of --graph-steps)')
-    p.add_argument('--graph-steps', type=int, default=30,
-                   help='lane config with --many 0: decisions per HIP-graph replay '
-                        '(VecEnv.capture); 0 = one eager launch per decision')
+    p.add_argument('--many', type=int, default=20,
+                   help='lane config: most decisions per dt_step_many launch; the K timed '
+                        'decisions are split into ceil(K / many) equal launches')
+    p.add_argument('--no-graph', action='store_true',
+                   help='lane config: launch the timed dt_step_many calls eagerly')
+    p.add_argument('--no-parity', action='store_true', help='skip the oracle parity pass')
+    p.add_argument('--no-render', action='store_true', help='skip the render sub-record')
+    p.add_argument('--render-steps', type=int, default=0,
+                   help='render sub-record launches (0 = --steps)')
     p.add_argument('--seed', type=int, default=1234)
-    p.add_argument('--cpu-seconds', type=float, default=1.5,
-                   help='per-process seconds of the CPU baseline sample (0 = skip)')
-    p.add_argument('--cpu-procs', type=int, default=0)
-    return p.parse_args()
+    p.add_argument('--cpu-steps', type=int, default=100000,
+                   help='CPU baseline: timed env-steps per process after 1000 warm-up steps '
+                        '(BASELINE.md §3); 0 = skip')
+    p.add_argument('--cpu-procs', type=int, default=0,
+                   help='CPU baseline processes (0 = the box CPU share: min(16, affinity))')
+    p.add_argument('--dry-run', action='store_true',
+                   help='launcher/reduction check on CPU over gloo, no kernels')
+    return p.parse_args(argv)
+
+
+# ---- N-rank launcher ---------------------------------------------------------------
+def _free_port():
+    s = socket.socket()
+    s.bind(('127.0.0.1', 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def launch(args, argv):
+    """Start N ranks with torch.distributed.run as a child process and return its
+    exit code.  Runs before torch is imported here, so no GPU is touched by the
+    parent (it must never exec after HIP initialisation)."""
+    cmd = [sys.executable, '-m', 'torch.distributed.run', '--nnodes=1',
+           '--nproc-per-node', str(args.gpus), '--master-addr', '127.0.0.1',
+           '--master-port', str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault('HSA_ENABLE_IPC_MODE_LEGACY', '0')
+    return subprocess.call(cmd, env=env)
 
 
 # ---- CPU baseline: the oracle's numpy restatement of step(), one env/process ----
 def _cpu_worker(args):
-    idx, seconds, map_name = args
+    idx, warm, steps_wanted, map_name = args
     import yaml
     from oracle import dtsim_ref as R
     with open(os.path.join(REPO, 'aido1_amd', 'maps', map_name + '.yaml')) as f:
@@ -95,31 +141,39 @@ def _cpu_worker(args):
     env = R.EnvironmentWrapperRef(R.SimulatorRef(rows, seed=1234, env_id=idx))
     env.reset()
     rng = np.random.default_rng(1234 + idx)
-    steps = 0
-    t0 = time.perf_counter()
-    while time.perf_counter() - t0 < seconds:
-        for _ in range(20):
+
+    def run(target):
+        steps = 0
+        while steps < target:
             a = rng.random(2, dtype=np.float32)
             before = env.sim.step_count
             _, _, d = env.step(a)
             steps += env.sim.step_count - before
             if d:
                 env.reset()
+        return steps
+    run(warm)
+    t0 = time.perf_counter()
+    steps = run(steps_wanted)
     return steps, time.perf_counter() - t0
 
 
-def cpu_baseline(seconds, procs, map_name):
+def cpu_baseline(steps, procs, map_name):
+    """one env per process, 1,000 warm-up env-steps, then `steps`
+    timed env-steps per process; aggregate = sum of steps / slowest process."""
     import multiprocessing as mp
+    try:
+        avail = len(os.sched_getaffinity(0))
+    except AttributeError:
+        avail = os.cpu_count() or 1
     if procs <= 0:
-        try:
-            avail = len(os.sched_getaffinity(0))
-        except AttributeError:
-            avail = os.cpu_count() or 1
+        # the GPU box's CPU share is 16 per GPU (harness rule; os.cpu_count() shows
+        # the whole host there), so the pool is capped at 16 processes
         procs = max(1, min(16, avail))
     ctx = mp.get_context('spawn')
     with ctx.Pool(procs) as pool:
-        res = pool.map(_cpu_worker, [(i, seconds, map_name) for i in range(procs)])
-    steps = sum(r[0] for r in res)
+        res = pool.map(_cpu_worker, [(i, 1000, steps, map_name) for i in range(procs)])
+    total = sum(r[0] for r in res)
     wall = max(r[1] for r in res)
     model = ''
     try:
@@ -130,268 +184,530 @@ def cpu_baseline(seconds, procs, map_name):
                     break
     except OSError:
         pass
-    return {'value': steps / wall, 'unit': 'env-steps/s', 'cores': procs, 'kind': 'port',
-            'sample': '%d processes x %.1f s, one env each: oracle/dtsim_ref.py numpy-float64 '
-                      'restatement of Simulator.step + EnvironmentWrapper.step (no render), '
-                      '%s, U[0,1)^2 wheel actions, auto-reset; %d env-steps; host CPU: %s'
-                      % (procs, seconds, map_name, steps, model)}
+    return {'value': total / wall, 'unit': 'env-steps/s', 'cores': procs, 'kind': 'port',
+            'procs': procs, 'host_cores': os.cpu_count(), 'affinity_cores': avail,
+            'per_process': total / wall / procs,
+            'sample': '%d processes x (1000 warm-up + %d timed env-steps), one env each: '
+                      'oracle/dtsim_ref.py numpy-float64 restatement of Simulator.step + '
+                      'EnvironmentWrapper.step (no render), %s, U[0,1)^2 wheel actions, '
+                      'auto-reset; %d timed env-steps in %.1f s; host CPU: %s (%s logical '
+                      'cores, pool capped at the box share of 16)'
+                      % (procs, steps, map_name, total, wall, model, os.cpu_count())}
 
 
-def load_traffic(kernel):
-    """Per-launch HBM bytes from a committed rocprofv3 PMC summary (or None)."""
+def load_pmc(kernel):
+    """Per-launch PMC record of a kernel from profiles/pmc_traffic.json (or None)."""
     path = os.path.join(REPO, 'profiles', 'pmc_traffic.json')
     if not os.path.exists(path):
         return None
     with open(path) as f:
         d = json.load(f)
     v = d.get(kernel)
-    return v.get('hbm_bytes_per_launch') if isinstance(v, dict) else None
+    return v if isinstance(v, dict) else None
 
 
-def main():
-    args = parse()
-    import torch
-    import torch.distributed as dist
-    world = int(os.environ.get('WORLD_SIZE', '1'))
-    rank = int(os.environ.get('RANK', '0'))
-    local = int(os.environ.get('LOCAL_RANK', '0'))
-    if world > 1:
-        torch.cuda.set_device(local)
-        dist.init_process_group('nccl', device_id=torch.device('cuda', local))
-    else:
-        torch.cuda.set_device(0)
-    dev = torch.device('cuda', local if world > 1 else 0)
+def split_even(total, most):
+    """`total` decisions as ceil(total/most) launches whose sizes differ by <= 1."""
+    if total <= 0:
+        return []
+    nl = -(-total // max(1, most))
+    return [total // nl + (1 if i < total % nl else 0) for i in range(nl)]
 
+
+class _Slice:
+    """A StepOutput-shaped view of decisions [a, b) of a k*n-entry StepOutput."""
+
+    def __init__(self, out, a, b, n):
+        for name in ('reward', 'reward_mod', 'done', 'obs', 'lanepos', 'tile'):
+            t = getattr(out, name)
+            setattr(self, name, t[a * n:b * n] if t is not None else None)
+
+
+# ---- process group ---------------------------------------------------------------------
+class Ctx:
+    def __init__(self, args):
+        import torch
+        import torch.distributed as dist
+        self.torch, self.dist = torch, dist
+        self.world = int(os.environ.get('WORLD_SIZE', '1'))
+        self.rank = int(os.environ.get('RANK', '0'))
+        self.local = int(os.environ.get('LOCAL_RANK', '0'))
+        if self.world != args.gpus:
+            raise SystemExit('bench.py: WORLD_SIZE=%d but --gpus %d' % (self.world, args.gpus))
+        self.dry = args.dry_run
+        if self.dry:
+            self.dev = torch.device('cpu')
+            self.backend = 'gloo'
+        else:
+            torch.cuda.set_device(self.local)
+            self.dev = torch.device('cuda', self.local)
+            self.backend = 'nccl'
+        self.pg = False
+        if self.world > 1:
+            if self.dry:
+                dist.init_process_group('gloo')
+            else:
+                dist.init_process_group('nccl', device_id=self.dev)
+            self.pg = True
+
+    def barrier(self):
+        if self.pg:
+            self.dist.barrier()
+
+    def sync(self):
+        if not self.dry:
+            self.torch.cuda.synchronize(self.dev)
+
+    def gather(self, values):
+        """Every rank's float64 vector -> [world, len] list (rank order)."""
+        t = self.torch.tensor(values, dtype=self.torch.float64, device=self.dev)
+        if not self.pg:
+            return [t.tolist()]
+        parts = [self.torch.zeros_like(t) for _ in range(self.world)]
+        self.dist.all_gather(parts, t)
+        return [p.tolist() for p in parts]
+
+    def close(self):
+        if self.pg:
+            self.dist.destroy_process_group()
+
+
+def rank_report(ctx, counts, elapsed):
+    """All ranks' (env_steps, decisions, resets, elapsed) -> totals + per-rank list."""
+    rows = ctx.gather(list(counts) + [elapsed])
+    tot = [sum(r[i] for r in rows) for i in range(len(counts))]
+    tmax = max(r[-1] for r in rows)
+    per = [{'rank': i, 'env_steps': r[0], 'decisions': r[1], 'resets': r[2], 'elapsed_s': r[-1]}
+           for i, r in enumerate(rows)]
+    return tot, tmax, per
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = parse(argv)
+    if 'WORLD_SIZE' not in os.environ and args.gpus > 1:
+        sys.exit(launch(args, argv))
+    ctx = Ctx(args)
+    if args.dry_run:
+        return bench_dry(args, ctx)
+    if args.config == 'actor':
+        return bench_actor(args, ctx)
+    if args.config == 'train':
+        return bench_train(args, ctx)
+    if args.config == 'render':
+        return bench_render_config(args, ctx)
+    return bench_lane(args, ctx)
+
+
+def bench_dry(args, ctx):
+    """No kernels: each rank 'steps' its shard synthetically, then the same
+    barrier/max/sum/gather as the GPU path."""
+    ctx.barrier()
+    t0 = time.perf_counter()
+    steps = args.envs * args.steps * 3
+    elapsed = time.perf_counter() - t0 + 1e-6
+    ctx.barrier()
+    tot, tmax, per = rank_report(ctx, [steps, args.envs * args.steps, 0], elapsed)
+    if ctx.rank == 0:
+        print(json.dumps({'metric': METRIC, 'value': tot[0] / tmax, 'unit': 'env-steps/s',
+                          'n_gpus': ctx.world, 'steps': args.steps, 'warmup': args.warmup,
+                          'dry_run': True, 'backend': ctx.backend,
+                          'process_group_world': ctx.world if ctx.pg else 1,
+                          'per_rank': per,
+                          'config': {'envs_per_gpu': args.envs,
+                                     'global_envs': args.envs * ctx.world}}), flush=True)
+    ctx.close()
+
+
+# ---- config 2: the headline line -------------------------------------------------------
+def bench_lane(args, ctx):
+    torch = ctx.torch
     from aido1_amd.config import EnvConfig
     from aido1_amd.vec_env import StepOutput, VecEnv
-
-    n = args.envs
-    if args.config == 'actor':
-        return bench_actor(args, dev, rank, world, dist)
-    if args.config == 'train':
-        return bench_train(args, dev, rank, world, dist)
-    env = VecEnv(n, seed=args.seed, device=dev.index,
-                 config=EnvConfig(map_name=args.map), env_id_base=rank * n)
-    out = StepOutput(n, dev, lanepos=False, tile=False)
+    dev, rank, n = ctx.dev, ctx.rank, args.envs
+    env = VecEnv(n, seed=args.seed, device=dev.index, config=EnvConfig(map_name=args.map),
+                 env_id_base=rank * n)
     g = torch.Generator(device=dev)
     g.manual_seed(args.seed + 7919 * rank)
-    total = args.warmup + args.steps
-    actions = torch.rand(total, n, 2, generator=g, device=dev, dtype=torch.float32)
-    render = None
-    if args.config == 'render':
-        from aido1_amd.render import RenderOutput
-        render = RenderOutput(n, dev)
+    W, K = args.warmup, args.steps
+    actions = torch.rand(W + K, n, 2, generator=g, device=dev, dtype=torch.float32)
     env.reset()
-    torch.cuda.synchronize(dev)
+    ctx.sync()
 
-    def one(i):
-        env.step_into(actions[i], out)
-        if render is not None:
-            env.render_into(render, fresh=out.done)
+    # warm-up: the same launch shape as the timed region
+    for a, b in _bounds(split_even(W, args.many)):
+        wout = StepOutput((b - a) * n, dev, lanepos=False, tile=False)
+        env.step_many_into(actions[a:b], wout)
+    ctx.sync()
+    start = env.get_state()
 
-    M = max(0, args.many) if render is None else 0
-    G = max(0, args.graph_steps) if render is None and not M else 0
-    if M:
-        # k = M decisions per launch (dt_step_many), outputs of every decision kept
-        mb = list(range(0, args.steps, M)) + [args.steps]   # the last takes the rest
-        chunks = list(zip(mb[:-1], mb[1:]))
-        outs = {}
-        for a, b in chunks + [(0, M)]:
-            if b - a not in outs:
-                outs[b - a] = StepOutput((b - a) * n, dev, lanepos=False, tile=False)
-        mev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in chunks]
-        for i in range(0, args.warmup, M):   # warmup launches of M decisions too
-            env.step_many_into(actions[:M], outs[M])
-    else:
-        for i in range(args.warmup):
-            one(i)
-    torch.cuda.synchronize(dev)
-    if G:
-        # the timed decisions as HIP graphs of G launches each, captured up
-        # front over their own action slices (StepGraph)
-        bounds = list(range(0, args.steps, G)) + [args.steps]   # the last takes the rest
-        graphs = [env.capture(actions[args.warmup + a:args.warmup + b], out)
-                  for a, b in zip(bounds[:-1], bounds[1:])]
-        gev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-               for _ in graphs]
+    sizes = split_even(K, args.many)
+    out = StepOutput(K * n, dev, lanepos=False, tile=False)
+    plan = [(W + a, W + b, _Slice(out, a, b, n)) for a, b in _bounds(sizes)]
+
+    def run_timed():
+        for a, b, o in plan:
+            env.step_many_into(actions[a:b], o)
+    graph = None
+    if not args.no_graph:
+        graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(graph):     # capture only: nothing runs here
+            run_timed()
+        ctx.sync()
     env.stats(reset=True)
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)] if not (G or M) else []
-    rev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)] if render is not None else None
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    ctx.barrier()
+    ctx.sync()
     t0 = time.perf_counter()
-    if M:
-        for c, (a, b) in enumerate(chunks):
-            mev[c][0].record()
-            env.step_many_into(actions[args.warmup + a:args.warmup + b], outs[b - a])
-            mev[c][1].record()
-    elif G:
-        for c, gr in enumerate(graphs):
-            gev[c][0].record()
-            gr.replay()
-            gev[c][1].record()
+    e0.record()
+    if graph is not None:
+        graph.replay()
     else:
-        for k in range(args.steps):
-            i = args.warmup + k
-            ev[k][0].record()
-            env.step_into(actions[i], out)
-            ev[k][1].record()
-            if render is not None:
-                rev[k][0].record()
-                env.render_into(render, fresh=out.done)
-                rev[k][1].record()
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+        run_timed()
+    e1.record()
+    ctx.sync()
+    ctx.barrier()
     elapsed = time.perf_counter() - t0
     st = env.stats()
     env.check()
-    if M:  # per decision: launch times / decisions (a launch runs M of them)
-        step_ms = float(np.sum([a.elapsed_time(b) for a, b in mev])) / args.steps
-        launch_ms = float(np.mean([a.elapsed_time(b) for a, b in mev]))
-    elif G:  # per launch inside the graphs: replay time / launches (gaps included)
-        step_ms = float(np.sum([a.elapsed_time(b) for a, b in gev])) / args.steps
-    else:
-        step_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    render_ms = float(np.mean([a.elapsed_time(b) for a, b in rev])) if rev else None
+    launches_ms = e0.elapsed_time(e1)
+    tot, tmax, per = rank_report(ctx, [st['sim_steps'], st['decisions'], st['resets']], elapsed)
+    sim_steps, decisions, resets = tot
 
-    sims = torch.tensor([st['sim_steps'], st['decisions'], st['resets']], dtype=torch.float64,
-                        device=dev)
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(sims, op=dist.ReduceOp.SUM)
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    sim_steps, decisions, resets = (float(v) for v in sims.tolist())
-    tmax = float(tmax.item())
+    parity = None if args.no_parity else lane_parity(env, start, actions[W:], out, rank, args)
+    render = None if args.no_render else render_record(env, args, ctx)
+    # parity: worst over ranks
+    if parity is not None and ctx.pg:
+        keys = ['pose_max_abs_err', 'reward_max_abs_err', 'reward_mod_max_abs_err',
+                'obs_max_abs_err', 'tile_mismatches', 'done_mismatches', 'counter_mismatches',
+                'check_pass_max_abs_diff']
+        rows = ctx.gather([parity[k] for k in keys])
+        for i, k in enumerate(keys):
+            vals = [r[i] for r in rows]
+            parity[k] = sum(vals) if k.endswith('mismatches') else max(vals)
+        parity['envs_checked'] *= ctx.world
 
     if rank == 0:
-        if render is None and M:
-            # one launch = len(chunks) of them over args.steps decisions;
-            # step_pair_kernel unless DTSIM_STEP_PAIR=0
-            kname = ('step_kernel' if os.environ.get('DTSIM_STEP_PAIR', '1').startswith('0')
-                     else 'step_pair_kernel')
-            kms = launch_ms
-            per = args.steps / len(chunks)
-            bytes_per_launch = ((MANY_BYTES_PER_ENV + MANY_BYTES_PER_ENV_DECISION * per) * n +
-                                MANY_BYTES_PER_RESET * resets / len(chunks))
-        elif render is None:
-            kname, kms = 'step_kernel', step_ms
-            bytes_per_launch = STEP_BYTES_PER_ENV * n + SPAWN_BYTES_PER_RESET * resets / max(
-                1.0, decisions / n)
-        else:
-            from aido1_amd.render import RENDER_BYTES_PER_ENV, RENDER_BYTES_PER_FRESH
-            kname, kms = 'render_kernel', render_ms
-            # resets per launch = the envs the render refills (fresh = done)
-            bytes_per_launch = (RENDER_BYTES_PER_ENV * n + RENDER_BYTES_PER_FRESH * resets /
-                                max(1.0, decisions / n))
-        achieved = bytes_per_launch / (kms * 1e-3) / 1e9
+        nl = len(sizes)
+        kms = launches_ms / nl
+        steps_per_launch = st['sim_steps'] / nl      # this rank's launches
+        resets_per_launch = st['resets'] / nl
+        survey_bytes = SURVEY_BYTES_PER_ENV_STEP * steps_per_launch
+        fused_bytes = (MANY_BYTES_PER_ENV + MANY_BYTES_PER_ENV_DECISION * K / nl) * n + \
+            MANY_BYTES_PER_RESET * resets_per_launch
+        achieved = survey_bytes / (kms * 1e-3) / 1e9
+        kname = ('step_kernel' if os.environ.get('DTSIM_STEP_PAIR', '1').startswith('0')
+                 else 'step_pair_kernel')
+        pmc = load_pmc(kname) or {}
         line = {
             'metric': METRIC,
             'value': sim_steps / tmax,
             'unit': 'env-steps/s',
-            'n_gpus': world,
-            'steps': args.steps,
-            'warmup': args.warmup,
-            'ms_per_step': tmax / args.steps * 1e3,
+            'n_gpus': ctx.world,
+            'steps': K,
+            'warmup': W,
+            'ms_per_step': tmax / K * 1e3,
             'higher_is_better': True,
             'scaling': 'weak',
             'vs_baseline': None,
             'dtype': 'f64',
             'data': 'synthetic',
             'config': {
-                'workload': ('config2: %d envs/GPU, lane-pose (dist, angle) obs' % n
-                             if render is None else
-                             'config3: %d envs/GPU, lane-pose + 120x160 top-down render + '
-                             'line_detector1 HSV/edge obs' % n),
+                'workload': 'config2: %d envs/GPU, lane-pose (dist, angle) obs' % n,
                 'map': args.map, 'envs_per_gpu': n, 'repeat_actions': 3,
                 'actions': 'U[0,1)^2 wheel velocities, resident in HBM',
-                'auto_reset': True, 'global_envs': n * world,
-                'launch': ('dt_step_many: %d decisions per launch' % M if M else
-                           'HIP graphs of %d decisions (VecEnv.capture)' % G if G else
-                           'one eager launch per decision'),
-                'parallelism': 'env shards (%d x %d), no collective' % (world, n)},
+                'auto_reset': True, 'global_envs': n * ctx.world,
+                'launch': 'dt_step_many: %d launches of %s decisions%s' % (
+                    nl, '/'.join(str(s) for s in sorted(set(sizes), reverse=True)),
+                    ', one HIP graph' if graph is not None else ', eager'),
+                'parallelism': 'env shards (%d x %d), no collective' % (ctx.world, n)},
             'counts': {'env_steps': sim_steps, 'decisions': decisions, 'resets': resets,
                        'elapsed_s': tmax},
+            'per_rank': per,
+            'process_group': {'backend': 'nccl (RCCL)' if ctx.pg else None,
+                              'world': ctx.dist.get_world_size() if ctx.pg else 1},
+            'parity': parity,
             'roofline': {'bound': 'hbm', 'kernel': kname, 'achieved': achieved,
                          'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
-                         'traffic': load_traffic(kname), 'avg_kernel_ms': kms,
-                         'algorithmic_bytes_per_launch': bytes_per_launch},
+                         'traffic': pmc.get('hbm_bytes_per_launch'),
+                         'traffic_per': 'launch of %d decisions' % pmc['decisions_per_launch']
+                         if 'decisions_per_launch' in pmc else None,
+                         'avg_kernel_ms': kms,
+                         'algorithmic_bytes_per_launch': survey_bytes,
+                         'algorithmic_basis': 'SURVEY §8d 81 B/env-step x %.0f env-steps '
+                                              'per launch' % steps_per_launch,
+                         'fused_bytes_per_launch': fused_bytes,
+                         'decisions_per_launch': K / nl,
+                         'note': 'not HBM-bound (BASELINE.md §4): the bound is one env\'s '
+                                 'float64 dependency chain; see step_bound'},
+            'step_ms_per_decision': launches_ms / K,
+            'step_bound': step_bound_record(kname, kms, K / nl, n, pmc),
+            'render': render,
         }
-        if render_ms is not None:
-            line['step_kernel_ms'] = step_ms
-        if M:
-            line['roofline']['decisions_per_launch'] = args.steps / len(chunks)
-            line['step_ms_per_decision'] = step_ms
-        if world == 1 and args.cpu_seconds > 0:
-            line['cpu_baseline'] = cpu_baseline(args.cpu_seconds, args.cpu_procs, args.map)
+        if ctx.world == 1 and args.cpu_steps > 0:
+            line['cpu_baseline'] = cpu_baseline(args.cpu_steps, args.cpu_procs, args.map)
         else:
             line['cpu_baseline'] = None
         print(json.dumps(line), flush=True)
     env.close()
-    if world > 1:
-        dist.destroy_process_group()
+    ctx.close()
 
 
-BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16 MFMA (spec)
+def _bounds(sizes):
+    a = 0
+    for s in sizes:
+        yield a, a + s
+        a += s
 
 
-def bench_actor(args, dev, rank, world, dist):
-    """BASELINE configs[3]: 4096 envs/GPU, mixed small_loop/zigzag, actor in the loop."""
+def step_bound_record(kname, kms, dec_per_launch, n, pmc):
+    """The config-2 kernel's real bound: per-decision time of one env's float64
+    chain, and the fp64 issue rate it reaches vs the chip's (PMC counts from
+    profiles/pmc_traffic.json when present)."""
+    rec = {'us_per_decision': kms * 1e3 / dec_per_launch,
+           'waves': 2 * n // 64 if kname == 'step_pair_kernel' else n // 64,
+           'simds_on_chip': 1024}
+    f = pmc.get('fp64_flops_per_launch')
+    if f:
+        tf = f / (kms * 1e-3) / 1e12
+        rec.update({'fp64_tflops': tf, 'fp64_peak_tflops': FP64_VECTOR_PEAK_TFLOPS,
+                    'fp64_frac': tf / FP64_VECTOR_PEAK_TFLOPS})
+    return rec
+
+
+def lane_parity(env, start, actions, out, rank, args):
+    """Every env of this rank re-run by the C oracle (test infrastructure, used
+    here as the checker only) from `start` through the timed decisions'
+    actions, compared with the timed launches' outputs; then a dt_step check
+    pass from the same start state with tile indices asked for."""
     import torch
+    import yaml
+    from aido1_amd.vec_env import StepOutput
+    from oracle import oracle_c as OC
+    n, K = env.n, out.reward.numel() // env.n
+    with open(os.path.join(REPO, 'aido1_amd', 'maps', args.map + '.yaml')) as f:
+        rows = yaml.safe_load(f)['tiles']
+    t0 = time.perf_counter()
+    end = env.get_state()
+    acts = actions[:K].cpu().numpy()
+    g = {k: getattr(out, k).view(K, n, -1).squeeze(-1).cpu().numpy()
+         for k in ('reward', 'reward_mod', 'done')}
+    g['obs'] = out.obs.view(K, n, 2).cpu().numpy()
+    ob = OC.OracleBatch(rows, n, seed=args.seed, env_base=rank * n)
+    ob.set_state(**start)
+    refs = []
+    err = {'reward': 0.0, 'reward_mod': 0.0, 'obs': 0.0}
+    done_mm = 0
+    for d in range(K):
+        r = ob.step(acts[d])
+        refs.append(r)
+        for k in err:
+            err[k] = max(err[k], float(np.max(np.abs(g[k][d] - r[k]))))
+        done_mm += int(np.count_nonzero(g['done'][d] != r['done']))
+    o = ob.state()
+    pose_err = max(float(np.max(np.abs(end[k] - o[k]))) for k in ('x', 'z', 'angle'))
+    cnt_mm = sum(int(np.count_nonzero(end[k] != o[k]))
+                 for k in ('step_count', 'env_step', 'episode'))
+    # check pass: dt_step from the same start, tile + lane pose produced
+    env.set_state(**start)
+    full = StepOutput(n, env.device)
+    tile_mm = 0
+    chk = 0.0
+    for d in range(K):
+        env.step_into(actions[d], full)
+        torch.cuda.synchronize(env.device)
+        tile_mm += int(np.count_nonzero(full.tile.cpu().numpy() != refs[d]['tile']))
+        done_mm += int(np.count_nonzero(full.done.cpu().numpy() != refs[d]['done']))
+        chk = max(chk, float(np.max(np.abs(full.reward.cpu().numpy() - g['reward'][d]))))
+    end2 = env.get_state()
+    chk = max(chk, max(float(np.max(np.abs(end2[k] - end[k]))) for k in ('x', 'z', 'angle')))
+    env.check()
+    return {'envs_checked': n, 'decisions': K, 'oracle': 'oracle/dtsim_oracle.c (C restatement)',
+            'pose_max_abs_err': pose_err, 'reward_max_abs_err': err['reward'],
+            'reward_mod_max_abs_err': err['reward_mod'], 'obs_max_abs_err': err['obs'],
+            'done_mismatches': done_mm, 'tile_mismatches': tile_mm,
+            'counter_mismatches': cnt_mm, 'check_pass_max_abs_diff': chk,
+            'tolerance': {'pose': 1e-5, 'reward': 1e-5, 'tile_done': 'exact'},
+            'ok': bool(pose_err <= 1e-5 and err['reward'] <= 1e-5 and err['reward_mod'] <= 1e-5
+                       and done_mm == 0 and tile_mm == 0 and cnt_mm == 0),
+            'seconds': time.perf_counter() - t0}
+
+
+def render_record(env, args, ctx):
+    """configs[2]'s HBM-bound kernel on the same envs: K dt_render launches, each
+    timed with HIP events on the launch stream; 64 envs' frames checked bit for
+    bit against oracle/render_oracle.c."""
+    torch = ctx.torch
+    from aido1_amd.render import RENDER_BYTES_PER_ENV, RenderOutput
+    n = env.n
+    K = args.render_steps or args.steps
+    ro = RenderOutput(n, env.device)
+    env.render_into(ro)               # first render fills the ring (not timed)
+    for _ in range(3):
+        env.render_into(ro)
+    ctx.sync()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(K)]
+    for a, b in ev:
+        a.record()
+        env.render_into(ro)
+        b.record()
+    ctx.sync()
+    ms = [a.elapsed_time(b) for a, b in ev]
+    kms = float(np.mean(ms))
+    bytes_per_launch = RENDER_BYTES_PER_ENV * n
+    achieved = bytes_per_launch / (kms * 1e-3) / 1e9
+    rec = {'kernel': 'render_kernel', 'launches': K, 'envs': n, 'bound': 'hbm',
+           'avg_kernel_ms': kms, 'min_kernel_ms': float(np.min(ms)),
+           'algorithmic_bytes_per_launch': bytes_per_launch,
+           'algorithmic_basis': 'per env: grey f32 76,800 + 4 u8 masks 76,800 written + pose '
+                                '24 read (SURVEY §8d config 3 minus the step\'s 81 B)',
+           'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
+           'frac': achieved / HBM_PEAK_GBS,
+           'env_steps_per_s_equiv': n / (kms * 1e-3)}
+    pmc = load_pmc('render_kernel') or {}
+    rec['traffic'] = pmc.get('hbm_bytes_per_launch')
+    if not args.no_parity:
+        rec['parity'] = render_parity(env, ro, args)
+    return rec
+
+
+def render_parity(env, ro, args, m=64):
+    import yaml
+    from aido1_amd.render import RenderOutput
+    from oracle import oracle_c as OC
+    with open(os.path.join(REPO, 'aido1_amd', 'maps', args.map + '.yaml')) as f:
+        rows = yaml.safe_load(f)['tiles']
+    s = env.get_state()
+    idx = np.linspace(0, env.n - 1, m).astype(np.int64)
+    gray, masks, _ = OC.OracleRender(rows).render(s['x'][idx], s['z'][idx], s['angle'][idx])
+    g = ro.ring[idx.tolist(), ro.slot].cpu().numpy()
+    mk = ro.masks[idx.tolist()].cpu().numpy()
+    return {'envs_checked': m, 'oracle': 'oracle/render_oracle.c',
+            'gray_mismatches': int(np.count_nonzero(g != gray)),
+            'mask_mismatches': int(np.count_nonzero(mk != masks))}
+
+
+# ---- config 3 on its own -----------------------------------------------------------------
+def bench_render_config(args, ctx):
+    """configs[2]: per decision one dt_step + one dt_render (the frame ring
+    refilled for respawned envs), eager launches timed per kernel."""
+    torch = ctx.torch
+    from aido1_amd.config import EnvConfig
+    from aido1_amd.render import RENDER_BYTES_PER_ENV, RENDER_BYTES_PER_FRESH, RenderOutput
+    from aido1_amd.vec_env import StepOutput, VecEnv
+    dev, rank, n = ctx.dev, ctx.rank, args.envs
+    env = VecEnv(n, seed=args.seed, device=dev.index, config=EnvConfig(map_name=args.map),
+                 env_id_base=rank * n)
+    out = StepOutput(n, dev, lanepos=False, tile=False)
+    g = torch.Generator(device=dev)
+    g.manual_seed(args.seed + 7919 * rank)
+    actions = torch.rand(args.warmup + args.steps, n, 2, generator=g, device=dev,
+                         dtype=torch.float32)
+    ro = RenderOutput(n, dev)
+    env.reset()
+    for i in range(args.warmup):
+        env.step_into(actions[i], out)
+        env.render_into(ro, fresh=out.done)
+    ctx.sync()
+    env.stats(reset=True)
+    sev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    rev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(args.steps)]
+    ctx.barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    for k in range(args.steps):
+        sev[k][0].record()
+        env.step_into(actions[args.warmup + k], out)
+        sev[k][1].record()
+        rev[k][0].record()
+        env.render_into(ro, fresh=out.done)
+        rev[k][1].record()
+    ctx.sync()
+    ctx.barrier()
+    elapsed = time.perf_counter() - t0
+    st = env.stats()
+    env.check()
+    tot, tmax, per = rank_report(ctx, [st['sim_steps'], st['decisions'], st['resets']], elapsed)
+    if rank == 0:
+        kms = float(np.mean([a.elapsed_time(b) for a, b in rev]))
+        step_ms = float(np.mean([a.elapsed_time(b) for a, b in sev]))
+        bpl = RENDER_BYTES_PER_ENV * n + RENDER_BYTES_PER_FRESH * st['resets'] / args.steps
+        achieved = bpl / (kms * 1e-3) / 1e9
+        pmc = load_pmc('render_kernel') or {}
+        print(json.dumps({
+            'metric': METRIC, 'value': tot[0] / tmax, 'unit': 'env-steps/s',
+            'n_gpus': ctx.world, 'steps': args.steps, 'warmup': args.warmup,
+            'ms_per_step': tmax / args.steps * 1e3, 'higher_is_better': True,
+            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f64 pose / f32 grey / u8 masks',
+            'data': 'synthetic',
+            'config': {'workload': 'config3: %d envs/GPU, lane-pose + 120x160 top-down render '
+                                   '+ line_detector1 HSV/edge obs' % n,
+                       'map': args.map, 'envs_per_gpu': n, 'global_envs': n * ctx.world,
+                       'launch': 'per decision: dt_step + dt_render, eager',
+                       'parallelism': 'env shards (%d x %d), no collective' % (ctx.world, n)},
+            'counts': {'env_steps': tot[0], 'decisions': tot[1], 'resets': tot[2],
+                       'elapsed_s': tmax},
+            'per_rank': per,
+            'roofline': {'bound': 'hbm', 'kernel': 'render_kernel', 'achieved': achieved,
+                         'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
+                         'traffic': pmc.get('hbm_bytes_per_launch'), 'avg_kernel_ms': kms,
+                         'algorithmic_bytes_per_launch': bpl},
+            'step_kernel_ms': step_ms, 'cpu_baseline': None}), flush=True)
+    env.close()
+    ctx.close()
+
+
+# ---- configs 4 and 5 -----------------------------------------------------------------------
+def bench_actor(args, ctx):
+    """BASELINE configs[3]: 4096 envs/GPU, mixed small_loop/zigzag, actor in the loop."""
+    torch = ctx.torch
     from aido1_amd.actor import flops_per_sample
     from aido1_amd.rollout import ActorRollout
     with open(os.path.join(REPO, 'aido1_amd', 'configs', 'reference_config.json')) as f:
         cfg = json.load(f)
-    n = args.envs
+    dev, rank, n = ctx.dev, ctx.rank, args.envs
     torch.manual_seed(args.seed)
     roll = ActorRollout(cfg, n, maps=('small_loop', 'zigzag'), device=dev.index, seed=args.seed,
                         env_id_base=rank * n, actor_mode=args.actor_mode)
     roll.reset()
     for _ in range(args.warmup):
         roll.step()
-    torch.cuda.synchronize(dev)
+    ctx.sync()
     roll.stats(reset=True)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
+    ctx.barrier()
+    ctx.sync()
     t0 = time.perf_counter()
     for k in range(args.steps):
         roll.step(timing=ev[k])
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+    ctx.sync()
+    ctx.barrier()
     elapsed = time.perf_counter() - t0
     st = roll.stats()
     actor_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    sims = torch.tensor([st['sim_steps'], st['decisions'], st['resets']], dtype=torch.float64,
-                        device=dev)
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(sims, op=dist.ReduceOp.SUM)
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    sim_steps, decisions, resets = (float(v) for v in sims.tolist())
-    tmax = float(tmax.item())
+    tot, tmax, per = rank_report(ctx, [st['sim_steps'], st['decisions'], st['resets']], elapsed)
     if rank == 0:
         tflops = n * flops_per_sample() / (actor_ms * 1e-3) / 1e12
         print(json.dumps({
-            'metric': METRIC, 'value': sim_steps / tmax, 'unit': 'env-steps/s', 'n_gpus': world,
-            'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': tmax / args.steps * 1e3,
+            'metric': METRIC, 'value': tot[0] / tmax, 'unit': 'env-steps/s',
+            'n_gpus': ctx.world, 'steps': args.steps, 'warmup': args.warmup,
+            'ms_per_step': tmax / args.steps * 1e3,
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
             'dtype': 'f64 env / %s actor' % str(roll.actor.dtype).replace('torch.', ''),
             'data': 'synthetic',
             'config': {'workload': 'config4: %d envs/GPU, actor in the loop (ConfigActor, '
                                    'config.json), mixed small_loop/zigzag' % n,
-                       'actor_mode': args.actor_mode, 'envs_per_gpu': n, 'global_envs': n * world, 'repeat_actions': 3,
+                       'actor_mode': args.actor_mode, 'envs_per_gpu': n,
+                       'global_envs': n * ctx.world, 'repeat_actions': 3,
                        'weights': 'random init (no checkpoint offline)',
-                       'parallelism': 'env shards (%d x %d), no collective' % (world, n)},
-            'counts': {'env_steps': sim_steps, 'decisions': decisions, 'resets': resets,
+                       'parallelism': 'env shards (%d x %d), no collective' % (ctx.world, n)},
+            'counts': {'env_steps': tot[0], 'decisions': tot[1], 'resets': tot[2],
                        'elapsed_s': tmax},
+            'per_rank': per,
             'roofline': {'bound': 'mfma', 'kernel': 'actor forward (fp16 MFMA convs + linears)',
                          'achieved': tflops, 'peak': BF16_DENSE_PEAK_TFLOPS, 'unit': 'TFLOP/s',
                          'frac': tflops / BF16_DENSE_PEAK_TFLOPS, 'traffic': None,
@@ -399,76 +715,68 @@ def bench_actor(args, dev, rank, world, dist):
                          'algorithmic_flops_per_launch': n * flops_per_sample()},
             'cpu_baseline': None}), flush=True)
     roll.close()
-    if world > 1:
-        dist.destroy_process_group()
+    ctx.close()
 
 
-def bench_train(args, dev, rank, world, dist):
+def bench_train(args, ctx):
     """BASELINE configs[4]: full DDPG on every GPU — actor-in-loop rollout of
     4096 envs, GPU prioritized replay, one update per decision, gradients
     all-reduced over RCCL (world > 1).  value = env-steps/s; updates/s beside."""
-    import torch
+    torch = ctx.torch
     from aido1_amd.actor import flops_per_sample
     from aido1_amd.train_loop import TrainLoop
     with open(os.path.join(REPO, 'aido1_amd', 'configs', 'reference_config.json')) as f:
         cfg = json.load(f)
-    n = args.envs
+    dev, rank, n = ctx.dev, ctx.rank, args.envs
     loop = TrainLoop(cfg, n, device=dev.index, seed=args.seed, env_id_base=rank * n,
                      buffer_size=args.buffer_size, batch_size=args.batch_size or None,
                      updates_per_step=args.updates_per_step, actor_mode=args.actor_mode)
     loop.reset()
     for _ in range(max(args.warmup, 2)):
         loop.step()
-    torch.cuda.synchronize(dev)
+    ctx.sync()
     loop.rollout.stats(reset=True)
     u0 = loop.updates
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(args.steps)]
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize(dev)
+    ctx.barrier()
+    ctx.sync()
     t0 = time.perf_counter()
     for k in range(args.steps):
         loop.step(timing=ev[k])
-    torch.cuda.synchronize(dev)
-    if world > 1:
-        dist.barrier()
+    ctx.sync()
+    ctx.barrier()
     elapsed = time.perf_counter() - t0
     st = loop.rollout.stats()
     actor_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
-    sims = torch.tensor([st['sim_steps'], st['decisions'], st['resets'], loop.updates - u0],
-                        dtype=torch.float64, device=dev)
-    tmax = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(sims, op=dist.ReduceOp.SUM)
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    sim_steps, decisions, resets, updates = (float(v) for v in sims.tolist())
-    tmax = float(tmax.item())
+    tot, tmax, per = rank_report(ctx, [st['sim_steps'], st['decisions'], st['resets'],
+                                       loop.updates - u0], elapsed)
+    sim_steps, decisions, resets, updates = tot
     if rank == 0:
         tflops = n * flops_per_sample() / (actor_ms * 1e-3) / 1e12
+        nparams = sum(p.numel() for p in loop.trainer.actor.parameters()) + \
+            sum(p.numel() for p in loop.trainer.critic.parameters())
         print(json.dumps({
-            'metric': METRIC, 'value': sim_steps / tmax, 'unit': 'env-steps/s', 'n_gpus': world,
-            'steps': args.steps, 'warmup': args.warmup, 'ms_per_step': tmax / args.steps * 1e3,
+            'metric': METRIC, 'value': sim_steps / tmax, 'unit': 'env-steps/s',
+            'n_gpus': ctx.world, 'steps': args.steps, 'warmup': args.warmup,
+            'ms_per_step': tmax / args.steps * 1e3,
             'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
             'dtype': 'f64 env / %s actor / f32 update' % str(
                 loop.rollout.actor.dtype).replace('torch.', ''), 'data': 'synthetic',
             'config': {'workload': 'config5: %d envs/GPU full DDPG (rollout + GPU prioritized '
                                    'replay + update + grad all-reduce)' % n,
                        'actor_mode': args.actor_mode, 'envs_per_gpu': n,
-                       'global_envs': n * world, 'batch_size_per_gpu': loop.batch_size,
+                       'global_envs': n * ctx.world, 'batch_size_per_gpu': loop.batch_size,
                        'buffer_size_per_gpu': args.buffer_size,
                        'updates_per_step': args.updates_per_step,
                        'weights': 'random init (config.json xavier_normal)',
                        'parallelism': 'env shards (%d x %d) + data-parallel update, RCCL '
-                                      'all-reduce of %d gradients' % (
-                                          world, n, sum(p.numel() for p in
-                                                        loop.trainer.actor.parameters()) +
-                                          sum(p.numel() for p in
-                                              loop.trainer.critic.parameters()))},
+                                      'all-reduce of %d gradients' % (ctx.world, n, nparams)},
             'counts': {'env_steps': sim_steps, 'decisions': decisions, 'resets': resets,
                        'updates_all_ranks': updates, 'elapsed_s': tmax,
                        'synchronous_updates_per_s': args.steps / tmax,
                        'samples_per_s': loop.batch_size * updates / tmax},
+            'per_rank': per,
             'roofline': {'bound': 'mfma', 'kernel': 'actor forward (fp16 MFMA convs + linears)',
                          'achieved': tflops, 'peak': BF16_DENSE_PEAK_TFLOPS, 'unit': 'TFLOP/s',
                          'frac': tflops / BF16_DENSE_PEAK_TFLOPS, 'traffic': None,
@@ -476,8 +784,7 @@ def bench_train(args, dev, rank, world, dist):
                          'algorithmic_flops_per_launch': n * flops_per_sample()},
             'cpu_baseline': None}), flush=True)
     loop.rollout.close()
-    if world > 1:
-        dist.destroy_process_group()
+    ctx.close()
 
 
 if __name__ == '__main__':

@@ -1,0 +1,102 @@
+"""A20 on the GPU: DDPG.act noise / epsilon / every-second-random on cuda
+against the reference's golden vectors (tests/golden/random_process.json:
+OrnsteinUhlenbeckProcess.sample given the normals numpy drew,
+utils/random_process.py:42-47, and the cycle decay of utils/util.py:20-74 that
+training/explorers.py:92-114 clips into epsilon).  The same code runs in
+ActorRollout for 4096 explorers at once."""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+
+def test_ou_on_gpu_matches_reference_given_its_normals(gpu):
+    """One OU process per env, 4096 envs, every env fed the reference's normals:
+    each row reproduces the reference's samples exactly (f64 +, *, sqrt)."""
+    from aido1_amd.explore import OUNoise
+    fx = golden('random_process.json')
+    n = 4096
+    ou = OUNoise(n, size=2, theta=0.15, mu=0.0, sigma=0.3, sigma_min=0.15, device=gpu)
+    normals = torch.tensor(fx['normals'], dtype=torch.float64, device=gpu)
+    got = []
+    for t in range(len(fx['ou'])):
+        got.append(ou.sample(normals[t].view(1, 2).expand(n, 2)))
+    got = torch.stack(got).cpu().numpy()                     # [T, n, 2] f32
+    ref = np.asarray(fx['ou'], np.float32)                   # [T, 2]
+    assert np.array_equal(got, np.broadcast_to(ref[:, None, :], got.shape))
+    # sigma annealing state after T samples
+    assert float(ou.n_steps[0]) == len(fx['ou'])
+
+
+def test_ou_reset_of_finished_envs_on_gpu(gpu):
+    from aido1_amd.explore import OUNoise
+    fx = golden('random_process.json')
+    ou = OUNoise(8, size=2, theta=0.15, mu=0.0, sigma=0.3, sigma_min=0.15, device=gpu)
+    normals = torch.tensor(fx['normals'], dtype=torch.float64, device=gpu)
+    for t in range(5):
+        ou.sample(normals[t].view(1, 2).expand(8, 2))
+    mask = torch.tensor([1, 0, 1, 0, 0, 0, 0, 1], dtype=torch.uint8, device=gpu)
+    ou.reset_states(mask)
+    x = ou.x.cpu().numpy()
+    assert (x[[0, 2, 7]] == 0).all()
+    assert np.array_equal(x[1], np.asarray(x[3]))           # untouched rows keep the state
+    assert (x[[1, 3, 4, 5, 6]] != 0).all()
+
+
+def test_cycle_epsilon_on_gpu_matches_decay_fn(gpu):
+    """CycleEpsilon (rollout.py) on cuda vs the reference's cycle decay with the
+    golden parameters (cycle_len 32, 24000 episodes); GPU cos may differ from
+    libm's in the last place."""
+    from aido1_amd.rollout import CycleEpsilon
+    fx = golden('random_process.json')
+    cfg = golden('reference_config.json')
+    n = 4096
+    ce = CycleEpsilon(cfg, n, gpu)
+    ce.cl.fill_(32.0)
+    ce.max_step.fill_(32.0 * (24000 // 32))
+    steps = torch.tensor(fx['decay_steps'], dtype=torch.int64, device=gpu)
+    for s, ref in zip(steps, fx['decay']['cycle']):
+        got = ce(s.expand(n)).cpu().numpy()
+        assert np.max(np.abs(got - ref)) <= 1e-15, (int(s), got[0], ref)
+
+
+def test_cycle_lengths_drawn_in_reference_range(gpu):
+    from aido1_amd.rollout import CycleEpsilon
+    cfg = golden('reference_config.json')
+    L = cfg['training']['epsilon_cycle_len']
+    ce = CycleEpsilon(cfg, 4096, gpu)
+    cl = ce.cl.cpu().numpy()
+    assert cl.min() >= L // 2 and cl.max() <= 2 * L          # explorers.py:92-99
+    assert len(np.unique(cl)) > L                             # drawn per explorer
+
+
+def test_explore_actions_on_gpu(gpu):
+    """explorers.py:178-194 for 4096 explorers on cuda: the non-random rows are
+    DDPG.act (actor + 2*eps*OU for a tanh head, clipped to [-1, 1],
+    models/ddpg/model.py:74-102) of the OU state the call advanced; the random
+    rows are only even explorer ids, at about epsilon_ratio * epsilon."""
+    from aido1_amd.explore import OUNoise, act, explore_actions
+    cfg = golden('reference_config.json')
+    n = 4096
+    g = torch.Generator(device=gpu)
+    g.manual_seed(0)
+    ou = OUNoise.from_config(cfg, n, device=gpu, generator=g)
+    eps = torch.full((n,), 0.5, dtype=torch.float64, device=gpu)
+    ids = torch.arange(n, device=gpu)
+    out = torch.rand(n, 2, device=gpu, generator=g) * 2.4 - 1.2
+    a = explore_actions(out, ou, eps, ids, cfg, generator=g, head='tanh')
+    det = act(out, (eps.unsqueeze(1) * ou.x).float(), 'tanh')
+    same = (a == det).all(1)
+    odd = ids % 2 == 1
+    assert same[odd].all()                                    # odd: never random
+    rnd = ~same
+    assert not rnd[odd].any()
+    frac = rnd[~odd].float().mean().item()
+    ratio = cfg['training']['epsilon_ratio'] * 0.5
+    assert abs(frac - ratio) < 0.05, frac
+    r = a[rnd]
+    assert ((r >= 0) & (r < 1)).all()                        # U[0,1)^2 random action
+    assert (a.abs() <= 1.0).all()

@@ -1,0 +1,114 @@
+"""Configs 4 and 5 at their BASELINE size on one GPU, and the observation path
+at 4096 envs and on the objects map.
+
+* config 4 (BASELINE configs[3]): ActorRollout, 4096 envs on mixed
+  small_loop / zigzag, the fp16 HIP conv chain in reference mode; property
+  checks on every env and the per-sample fp32 reference-mode actor (the
+  reference's explorers: train-mode batch-of-one BatchNorm,
+  training/explorers.py:46 + models/ddpg/model.py:74-88) on 64 sampled envs.
+* config 5 (BASELINE configs[4]): TrainLoop, 4096 envs, prioritized replay at
+  capacity 2^17 wrapping around, segment-tree invariants (replay.check()).
+* render parity vs oracle/render_oracle.c at 4096 envs and on loop_obstacles.
+"""
+import numpy as np
+import pytest
+import torch
+
+from conftest import golden, map_rows
+
+pytestmark = pytest.mark.gpu
+
+
+def _no_dropout_cfg():
+    from test_trainer import no_dropout
+    cfg = golden('reference_config.json')
+    cfg = dict(cfg)
+    cfg['model'] = dict(cfg['model'])
+    cfg['model']['actor'] = no_dropout(cfg['model']['actor'])
+    return cfg
+
+
+def test_config4_actor_rollout_at_size(gpu):
+    from aido1_amd.actor import ConfigActor
+    from aido1_amd.rollout import ActorRollout
+    cfg = _no_dropout_cfg()
+    torch.manual_seed(11)
+    actor = ConfigActor(cfg['model']['actor'])
+    ref_actor = ConfigActor(cfg['model']['actor'])
+    ref_actor.load_state_dict(actor.state_dict())
+    n = 4096
+    roll = ActorRollout(cfg, n, maps=('small_loop', 'zigzag'), device=0, seed=1234, actor=actor,
+                        actor_mode='reference')
+    assert [e.n for e in roll.envs] == [2048, 2048]
+    roll.reset()
+    done_total = 0
+    for _ in range(6):
+        r, rm, d = roll.step()
+        done_total += int(d.sum())
+    torch.cuda.synchronize()
+    st = roll.stats()
+    assert st['decisions'] == n * 6
+    assert n * 6 <= st['sim_steps'] <= n * 18
+    assert torch.isfinite(roll.ring).all()
+    assert float(roll.ring.min()) >= 0.0 and float(roll.ring.max()) <= 1.0
+    assert torch.isfinite(r).all() and torch.isfinite(rm).all()
+    a = roll.actions
+    assert ((a >= 0.0) & (a <= 1.0)).all()          # tanh head mapped a/2 + 0.5 in place
+    for env in roll.envs:
+        env.check()
+    # the fp16 HIP conv chain on the live ring vs the fp32 per-sample reference
+    idx = torch.linspace(0, n - 1, 64).long()
+    out = roll.actor(roll.ring, roll.order())[idx].float().cpu()
+    frames = roll.stack()[idx].cpu()
+    ref_actor.train()
+    with torch.no_grad():
+        ref = torch.cat([ref_actor(frames[i:i + 1]) for i in range(64)])
+    err = torch.max(torch.abs(out - ref)).item()
+    assert err < 1.5e-2, err
+    roll.close()
+
+
+def test_config5_train_loop_at_size(gpu):
+    from aido1_amd.train_loop import TrainLoop
+    cfg = golden('reference_config.json')
+    n = 4096
+    cap = 1 << 17
+    loop = TrainLoop(cfg, n_envs=n, device=0, seed=1234, buffer_size=cap, prioritized=True,
+                     graph=True)
+    loop.reset()
+    steps = cap // n + 2                          # fills and wraps the buffer
+    for _ in range(steps):
+        loop.step()
+    torch.cuda.synchronize()
+    assert len(loop.replay) == cap
+    assert loop.decisions == steps and loop.updates == steps
+    assert torch.isfinite(loop.metrics['critic_loss']) and torch.isfinite(loop.metrics['actor_loss'])
+    loop.replay.check()
+    s, mn, mp = loop.replay.trees()
+    assert float(mp) >= 1.0 and float(s) > 0.0 and float(mn) > 0.0
+    assert loop.rollout.stats()['decisions'] == n * steps
+    loop.rollout.close()
+
+
+@pytest.mark.parametrize('map_name,n', [('loop_empty', 4096), ('loop_obstacles', 512)])
+def test_render_parity_at_size(gpu, map_name, n):
+    from aido1_amd.config import EnvConfig
+    from aido1_amd.render import RenderOutput
+    from aido1_amd.vec_env import VecEnv
+    from oracle import oracle_c as OC
+    env = VecEnv(n, seed=7, config=EnvConfig(map_name=map_name))
+    env.reset()
+    rng = np.random.default_rng(5)
+    a = torch.from_numpy(rng.random((n, 2), dtype=np.float32)).to(gpu)
+    for _ in range(3):                              # move off the spawn poses
+        env.step_into(a)
+    torch.cuda.synchronize()
+    s = env.get_state()
+    out = RenderOutput(n, gpu, slots=1)
+    env.render_into(out)
+    torch.cuda.synchronize()
+    g, m, _ = OC.OracleRender(map_rows(map_name)).render(s['x'], s['z'], s['angle'])
+    assert np.array_equal(out.masks.cpu().numpy(), m)
+    assert np.array_equal(out.ring[:, 0].cpu().numpy(), g)
+    assert (m[:, 0] > 0).any() and (m[:, 3] > 0).any()
+    env.check()

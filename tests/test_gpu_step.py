@@ -249,8 +249,11 @@ def test_step_graph_chunks_match_eager(gpu):
     env2.check()
 
 
-@pytest.mark.parametrize('k,map_name', [(1, 'loop_empty'), (7, 'loop_empty'), (30, 'zigzag'),
-                                        (12, 'loop_obstacles'), (64, 'small_loop')])
+@pytest.mark.parametrize('k,map_name', [(1, 'loop_empty'), (7, 'loop_empty'), (16, 'loop_empty'),
+                                        (20, 'loop_empty'), (30, 'zigzag'),
+                                        (12, 'loop_obstacles'), (64, 'small_loop')],
+                         ids=['1-loop_empty', '7-loop_empty', '16-loop_empty', '20-loop_empty',
+                              '30-zigzag', '12-loop_obstacles', '64-small_loop'])
 def test_step_many_matches_oracle(gpu, k, map_name):
     """dt_step_many: k decisions per launch == k oracle steps, per decision;
     three launches back to back, then an eager dt_step continues the state.
@@ -298,12 +301,15 @@ def test_step_many_matches_oracle(gpu, k, map_name):
 
 def test_step_many_single_wave(gpu):
     """DTSIM_STEP_PAIR=0 (step_kernel over k decisions) in a child process, the
-    setting being read once per process: the same check at k = 16 and 64."""
+    setting being read once per process: the same check at k = 16 (loop_empty),
+    12 (loop_obstacles, where the pair kernel splits proximity_penalty across
+    its two waves), 30 (zigzag) and 64 (small_loop)."""
     import os
     import subprocess
     import sys
     code = ('import sys, pytest; sys.exit(pytest.main(["-x", "-q", "-m", "gpu", "-p", '
-            '"no:cacheprovider", "-k", "step_many_matches_oracle and (16 or 64 or 30)", '
+            '"no:cacheprovider", "-k", "step_many_matches_oracle and (16-loop_empty or 12-loop_obstacles or '
+            '30-zigzag or 64-small_loop)", '
             '"%s"]))' % os.path.abspath(__file__))
     env = dict(os.environ, DTSIM_STEP_PAIR='0')
     r = subprocess.run([sys.executable, '-c', code], env=env, cwd=os.path.dirname(__file__),

@@ -1,11 +1,13 @@
 #!/bin/bash
 # Round profiles: rocprofv3 --kernel-trace --stats of every bench config, then
-# PMC HBM traffic of the configs 2-3 kernels (FETCH_SIZE and WRITE_SIZE in
-# separate passes: they do not fit one TCC pass).  Each GPU step has its own
-# time limit; a fault/timeout stops the script.  Outputs under gpurun_out/.
+# PMC passes of the headline line's kernels (FETCH_SIZE, WRITE_SIZE and the
+# fp64 instruction counters in separate passes: they do not fit one pass).
+# Each GPU step has its own time limit; a fault/timeout stops the script.
+# Outputs under gpurun_out/; tools/pmc_summarize.py <round> turns them into
+# profiles/.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd); mkdir -p gpurun_out; export TMPDIR=/tmp
-STEPS=${STEPS:-100}
+STEPS=${STEPS:-20}; WARM=${WARM:-5}
 step() {  # step <name> <timeout> cmd...
   local name=$1 t=$2; shift 2
   echo "=== $name"
@@ -15,18 +17,21 @@ step() {  # step <name> <timeout> cmd...
   [ $rc -eq 0 ] || { echo "stopping"; exit $rc; }
 }
 declare -A ARGS=(
-  [lane]="--steps $STEPS --warmup 20 --cpu-seconds 0"
-  [render]="--config render --steps $STEPS --warmup 20 --cpu-seconds 0"
-  [actor]="--config actor --steps 30 --warmup 5 --cpu-seconds 0"
-  [train]="--config train --steps 30 --warmup 5 --cpu-seconds 0")
+  [lane]="--steps $STEPS --warmup $WARM --cpu-steps 0"
+  [render]="--config render --steps 100 --warmup 20 --cpu-steps 0"
+  [actor]="--config actor --steps 30 --warmup 5 --cpu-steps 0"
+  [train]="--config train --steps 30 --warmup 10 --cpu-steps 0")
 for cfg in ${CONFIGS:-lane render actor train}; do
   step "trace_$cfg" 600 rocprofv3 --kernel-trace --stats --output-format csv \
       -d "$ROOT/gpurun_out/trace_$cfg" -o run -- python3 "$ROOT/bench.py" ${ARGS[$cfg]}
 done
-for cfg in ${PMC_CONFIGS:-lane render}; do
-  for ctr in FETCH_SIZE WRITE_SIZE; do
-    step "pmc_${cfg}_$ctr" 600 rocprofv3 --pmc $ctr --output-format csv \
-        -d "$ROOT/gpurun_out/pmc_${cfg}_$ctr" -o run -- python3 "$ROOT/bench.py" ${ARGS[$cfg]}
+declare -A PMC=(
+  [FETCH_SIZE]="FETCH_SIZE" [WRITE_SIZE]="WRITE_SIZE"
+  [FP64]="SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64")
+for cfg in ${PMC_CONFIGS:-lane}; do
+  for tag in ${PMC_SETS:-FETCH_SIZE WRITE_SIZE FP64}; do
+    step "pmc_${cfg}_$tag" 300 rocprofv3 --pmc ${PMC[$tag]} --output-format csv \
+        -d "$ROOT/gpurun_out/pmc_${cfg}_$tag" -o run -- python3 "$ROOT/bench.py" ${ARGS[$cfg]} --no-parity
   done
 done
 echo done
