@@ -43,7 +43,41 @@ __device__ unsigned long long g_rstamps[4096 * 4];  // refill blocks: entry, exi
     const unsigned long long _t = __builtin_amdgcn_s_memrealtime();                 \
     if (threadIdx.x == 0 && blockIdx.x < 64) g_stamps[blockIdx.x * kStamps + (i)] = _t; \
   } while (0)
+// step_pair_kernel: lane 0 of both waves of the first 64 blocks, decisions
+// 0..7: [block][role][decision][point] shader clock; point 15 of decision 0
+// = real time at entry, of decision 1 = real time at exit
+constexpr int kPDec = 8;
+__device__ unsigned long long g_pstamps[64 * 4 * kPDec * 16];
+#define PSTAMP(d, i, v)                                                             \
+  do {                                                                              \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 64 && (d) >= 0 && (d) < kPDec)      \
+      g_pstamps[((blockIdx.x * 4 + (threadIdx.x >> 6)) * kPDec + (d)) * 16 + (i)] = (v); \
+  } while (0)
+#define PSTAMPT(d, i) PSTAMP(d, i, __builtin_amdgcn_s_memtime())
+// every block of step_fan_kernel: entry / exit real time, HW_ID, XCC_ID
+__device__ unsigned long long g_bstamps[4096 * 4];
+__device__ inline unsigned hw_id() {
+  unsigned v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(v));
+  return v;
+}
+__device__ inline unsigned xcc_id() {
+  unsigned v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+  return v;
+}
+#define BSTAMP(i, v)                                                                 \
+  do {                                                                              \
+    if (threadIdx.x == 0 && blockIdx.x < 4096) g_bstamps[blockIdx.x * 4 + (i)] = (v); \
+  } while (0)
 #else
+#define BSTAMP(i, v) \
+  do {               \
+  } while (0)
+#define PSTAMP(d, i, v) \
+  do {                  \
+  } while (0)
+#define PSTAMPT(d, i) PSTAMP(d, i, 0)
 #define STAMP(i) \
   do {           \
   } while (0)
@@ -228,7 +262,8 @@ __device__ __forceinline__ void sim_decision(const MapLds& M, const dt::Geo& g, 
                                              double& ang, double& c, double& s,
                                              uint32_t& step_count, uint32_t& env_step,
                                              Decision& D, PairX* X = nullptr, int role = 0,
-                                             int pair = 0, uint32_t* phase = nullptr) {
+                                             int pair = 0, uint32_t* phase = nullptr,
+                                             int dstamp = -1) {
   double vl, vr;
   map_action(sc.action_mode, a.x, a.y, vl, vr);
   if (sc.clip) {  // Simulator.step: np.clip(action, -1, 1)
@@ -257,6 +292,7 @@ __device__ __forceinline__ void sim_decision(const MapLds& M, const dt::Geo& g, 
     const bool live = !dn;
     // pair mode: every wave runs every sim step (the exchange barrier); a
     // finished lane's pose is restored afterwards
+    if (rep == 1) PSTAMPT(dstamp, 12);
     if (kPair || live) {
       const double x0 = x, z0 = z, a0 = ang, c0 = c, s0 = s;
       const uint32_t sc0 = step_count;
@@ -275,8 +311,10 @@ __device__ __forceinline__ void sim_decision(const MapLds& M, const dt::Geo& g, 
           const double ndz = ddz * cr - ddx * sr;
           x = cx + ndx;
           z = cz + ndz;
+          if (rep == 1) PSTAMPT(dstamp, 13);
           ang = ang + rot;
           sincos(ang, &s, &c);
+          if (rep == 1) PSTAMP(dstamp, 14, __builtin_amdgcn_s_memtime() + (s > 2.0 ? 1 : 0));
         }
         step_count += 1u;
         nsim += 1u;
@@ -286,6 +324,7 @@ __device__ __forceinline__ void sim_decision(const MapLds& M, const dt::Geo& g, 
           speed = sqrt((a1 * a1 + 0.0 * 0.0) + a3 * a3) / g.dt;
         }
       }
+      PSTAMPT(dstamp, 1 + 3 * rep);
       if (kPair && !live) {
         x = x0;
         z = z0;
@@ -318,7 +357,9 @@ __device__ __forceinline__ void sim_decision(const MapLds& M, const dt::Geo& g, 
           X->d1[pair][ph][ln] = lq[1];
           X->pen[pair][ph][ln] = pen;
         }
+        PSTAMPT(dstamp, 2 + 3 * rep);
         __syncthreads();
+        PSTAMPT(dstamp, 3 + 3 * rep);
         if (role == 0) {
           lq_inl = X->inl[pair][ph][ln] != 0;
           lq[0] = X->d0[pair][ph][ln];
@@ -590,6 +631,8 @@ __global__ __launch_bounds__(kBlock) void step_pair_kernel(dt::State st, dt::Map
   }
   __shared__ PairX X;
   __builtin_amdgcn_s_setprio(3);
+  PSTAMP(0, 15, __builtin_amdgcn_s_memrealtime());
+  PSTAMP(3, 15, __builtin_amdgcn_s_memtime());
   const int wave = (int)(threadIdx.x >> 6), role = wave & 1, pair = wave >> 1;
   const int lane = threadIdx.x & 63;
   const int e = (int)blockIdx.x * (int)(blockDim.x / 2) + pair * 64 + lane;
@@ -642,8 +685,10 @@ __global__ __launch_bounds__(kBlock) void step_pair_kernel(dt::State st, dt::Map
     asm volatile("" ::: "memory");
 
     Decision D;
+    PSTAMPT(d, 0);
     sim_decision<true>(M, g, sc, active, a, x, z, ang, c, s, step_count, env_step, D, &X, role,
-                       pair, &phase);
+                       pair, &phase, d);
+    PSTAMPT(d, 10);
 
     const bool want_reset = active && D.dn && sc.auto_reset;
     bool ok = slot_ready && ((failed >> rel) & 1u) == 0u;
@@ -705,7 +750,10 @@ __global__ __launch_bounds__(kBlock) void step_pair_kernel(dt::State st, dt::Map
     resets_t += reset_now ? 1u : 0u;
     dones_t += (active && D.dn) ? 1u : 0u;
     a = an;
+    PSTAMPT(d, 11);
   }
+  PSTAMP(1, 15, __builtin_amdgcn_s_memrealtime());
+  PSTAMP(2, 15, __builtin_amdgcn_s_memtime());
   // role 1 is past its last slot read before role 0 moves the window
   __syncthreads();
   if (role != 0) return;
@@ -715,6 +763,362 @@ __global__ __launch_bounds__(kBlock) void step_pair_kernel(dt::State st, dt::Map
   dt::wave_count(st.stats + 2, resets_t, kk);
   dt::wave_count(st.stats + 3, dones_t, kk);
   if (active) {
+    st.x[e] = x;
+    st.z[e] = z;
+    st.angle[e] = ang;
+    st.step_count[e] = step_count;
+    st.env_step[e] = env_step;
+    __hip_atomic_store(st.tick + e, tick + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (key != key0) {
+      st.episode[e] = key;
+      __hip_atomic_store(st.want + e, key + 1u + after_load(rp[dt::kSlotRec - 1]), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+// dt_step_many in fan mode (the default): 16 envs per 256-thread workgroup,
+// each env on one lane quad of each of the block's four waves.  Within a
+// decision the poses of the repeat (<= 3) Simulator steps do not depend on any
+// validity or lane-pose result (those only decide whether a step is kept), so
+// every wave computes the pose chain -- the quad computes the decision's
+// sincos(rot) and the three sincos(angle) on its four lanes at once -- and the
+// step math fans out: wave 0 runs _valid_pose of the three poses (a drivable
+// probe per lane), wave r (1..3) get_lane_pos2 of pose r (three bisection
+// levels per round on the quad) and its acos.  One barrier per decision swaps
+// the results through LDS; then every wave runs the same reward / done /
+// aggregation chain over the steps actually taken, the same reset, and writes
+// its share of the outputs.  4096 envs are 1024 waves, one per SIMD.
+// Bit-identical to step_kernel (the same operations on the same operands;
+// tests/test_gpu_step.py runs all three kernels).
+constexpr int kFanEnvs = 16;                // envs per workgroup
+constexpr int kFanBlock = 4 * 64;           // four waves
+constexpr int kFanSteps = 3;                // repeat * frame_skip handled
+
+struct FanX {  // [parity][env][step], rows padded to 4 for wide LDS reads
+  double dist[2][kFanEnvs][4], dot[2][kFanEnvs][4], arad[2][kFanEnvs][4], pen[2][kFanEnvs][4];
+  uint8_t inl[2][kFanEnvs][4], vp[2][kFanEnvs][4];
+};
+
+__global__ __launch_bounds__(kFanBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) void step_fan_kernel(dt::State st, dt::MapDev md,
+                                                             dt::Geo g, StepCfg sc, int n,
+                                                             uint32_t env_base, int k,
+                                                             const float2* __restrict__ act,
+                                                             double* __restrict__ rew,
+                                                             double* __restrict__ rewm,
+                                                             uint8_t* __restrict__ done_out,
+                                                             float2* __restrict__ obs,
+                                                             int n_step_blocks,
+                                                             uint32_t max_attempts) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+#ifdef DTSIM_STAMPS
+  BSTAMP(0, __builtin_amdgcn_s_memrealtime());
+  BSTAMP(2, hw_id());
+  BSTAMP(3, xcc_id());
+#endif
+  if ((int)blockIdx.x >= n_step_blocks) {  // spawn-ahead refill blocks
+    refill_group(st, md, g, n, max_attempts, env_base,
+                 ((int)blockIdx.x - n_step_blocks) * kRefillEnvs, kRefillEnvs, 0u, lds);
+    BSTAMP(1, __builtin_amdgcn_s_memrealtime());
+    return;
+  }
+  __shared__ FanX X;
+  __builtin_amdgcn_s_setprio(3);
+  PSTAMP(0, 15, __builtin_amdgcn_s_memrealtime());
+  PSTAMP(3, 15, __builtin_amdgcn_s_memtime());
+  const int wave = (int)(threadIdx.x >> 6), lane = (int)(threadIdx.x & 63);
+  const int q = lane & 3, le = lane >> 2;
+  const int e = (int)blockIdx.x * kFanEnvs + le;
+  const bool active = e < n;
+  const int ei = active ? e : 0;
+  const bool lead = q == 0;   // the lane of the quad that stores
+
+  double x = st.x[ei], z = st.z[ei], ang = st.angle[ei];
+  uint32_t step_count = st.step_count[ei], env_step = st.env_step[ei];
+  float2 a = act[ei];
+  const uint32_t tick = st.tick[ei];
+  uint32_t key = 0u;
+  uint64_t seed = 0u, words[dt::kSlots];
+  if (sc.auto_reset) {
+    key = st.episode[ei];
+    seed = st.seed[ei];
+#pragma unroll
+    for (int j = 0; j < dt::kSlots; ++j)
+      words[j] = __hip_atomic_load(st.pre_key + (size_t)j * n + ei, __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
+  }
+  const MapLds M = dt::stage_map(md, lds);
+  const uint32_t key0 = key;
+  uint32_t ready = 0u, failed = 0u;
+  if (sc.auto_reset) {
+#pragma unroll
+    for (int j = 0; j < dt::kSlots; ++j) {
+      const uint32_t kw = (uint32_t)words[j], tag = (uint32_t)(words[j] >> 32);
+      const uint32_t rel = (kw & ~dt::kKeyFailed) - key;
+      if (rel < (uint32_t)dt::kSlots && (int32_t)(tick - tag) > 0) {
+        ready |= 1u << rel;
+        if (kw & dt::kKeyFailed) failed |= 1u << rel;
+      }
+    }
+  }
+
+  double c = 0.0, s = 0.0;
+  sincos(ang, &s, &c);
+  unsigned nsim_t = 0, act_t = 0, resets_t = 0, dones_t = 0;
+  double rp[dt::kSlotRec] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 1.0};
+  const int R = sc.repeat;
+  for (int d = 0; d < k; ++d) {
+    const int par = d & 1;
+    const float2 an = act[(size_t)(d + 1 < k ? d + 1 : d) * n + ei];
+    const uint32_t rel = key - key0;
+    const bool slot_ready = rel < (uint32_t)dt::kSlots && ((ready >> rel) & 1u) != 0u;
+    if (slot_ready) {
+      const size_t sl = key % (uint32_t)dt::kSlots;
+#pragma unroll
+      for (int j = 0; j < dt::kSlotRec; ++j)
+        rp[j] = st.pre[(sl * dt::kSlotRec + j) * (size_t)n + ei];
+    }
+    asm volatile("" ::: "memory");
+    PSTAMPT(d, 0);
+
+    // ---- the pose chain (every wave) ----
+    double vl, vr;
+    map_action(sc.action_mode, a.x, a.y, vl, vr);
+    if (sc.clip) {
+      vl = vl < -1.0 ? -1.0 : (vl > 1.0 ? 1.0 : vl);
+      vr = vr < -1.0 ? -1.0 : (vr > 1.0 ? 1.0 : vr);
+    }
+    const double wl = vl * g.robot_speed * 1.0, wr = vr * g.robot_speed * 1.0;
+    const bool straight = (wl == wr);
+    double r_icc = 0.0, rot = 0.0;
+    if (!straight) {
+      const double l = g.wheel_dist;
+      const double w_rot = (wr - wl) / l;
+      r_icc = (l * (wl + wr)) / (2.0 * (wl - wr));
+      rot = w_rot * g.dt;
+    }
+    const double kstraight = g.dt * wl;
+    // the angles of the three steps and the sincos of rot / angle 1..3, one per lane
+    const double a1 = ang + rot, a2 = a1 + rot, a3 = a2 + rot;
+    double sq = 0.0, cq = 1.0;
+    if (!straight) sincos(q == 0 ? rot : (q == 1 ? a1 : (q == 2 ? a2 : a3)), &sq, &cq);
+    const double sr = dt::qget<0>(sq), cr = dt::qget<0>(cq);
+    double px[kFanSteps + 1], pz[kFanSteps + 1], pa[kFanSteps + 1], pc[kFanSteps + 1],
+        ps[kFanSteps + 1], spd[kFanSteps + 1];
+    px[0] = x;
+    pz[0] = z;
+    pa[0] = ang;
+    pc[0] = c;
+    ps[0] = s;
+    spd[0] = 0.0;
+    if (straight) {
+#pragma unroll
+      for (int r = 1; r <= kFanSteps; ++r) {
+        px[r] = px[r - 1] + kstraight * c;
+        pz[r] = pz[r - 1] + kstraight * (-s);
+        pa[r] = ang;
+        pc[r] = c;
+        ps[r] = s;
+      }
+    } else {
+      pa[1] = a1;
+      pa[2] = a2;
+      pa[3] = a3;
+      ps[1] = dt::qget<1>(sq);
+      pc[1] = dt::qget<1>(cq);
+      ps[2] = dt::qget<2>(sq);
+      pc[2] = dt::qget<2>(cq);
+      ps[3] = dt::qget<3>(sq);
+      pc[3] = dt::qget<3>(cq);
+#pragma unroll
+      for (int r = 1; r <= kFanSteps; ++r) {
+        const double xo = px[r - 1], zo = pz[r - 1];
+        const double cx = xo + r_icc * ps[r - 1];
+        const double cz = zo + r_icc * pc[r - 1];
+        const double ddx = xo - cx, ddz = zo - cz;
+        const double ndx = ddx * cr + ddz * sr;
+        const double ndz = ddz * cr - ddx * sr;
+        px[r] = cx + ndx;
+        pz[r] = cz + ndz;
+      }
+    }
+    if (sc.speed_measured) {
+#pragma unroll
+      for (int r = 1; r <= kFanSteps; ++r) {
+        const double a1d = px[r] - px[r - 1], a3d = pz[r] - pz[r - 1];
+        spd[r] = sqrt((a1d * a1d + 0.0 * 0.0) + a3d * a3d) / g.dt;
+      }
+    }
+
+    PSTAMPT(d, 1);
+    // ---- the step math, fanned out over the waves ----
+    if (wave == 0) {
+#pragma unroll
+      for (int r = 1; r <= kFanSteps; ++r) {
+        const bool vp = dt::valid_pose_q(M, g, q, px[r], pz[r], pc[r], ps[r], 1.0);
+        const double pen = M.n_obj ? dt::proximity_penalty(M, g, px[r] + g.off * pc[r],
+                                                           pz[r] + g.off * (-ps[r]))
+                                   : 0.0;
+        if (lead) {
+          X.vp[par][le][r - 1] = vp ? 1 : 0;
+          X.pen[par][le][r - 1] = pen;
+        }
+      }
+    } else {
+      const int r = wave;
+      double lp[4] = {0.0, 0.0, 0.0, 0.0};
+      const bool inl = dt::lane_pos_q(M, g, q, px[r], pz[r], pc[r], ps[r], lp);
+      if (lead) {
+        X.inl[par][le][r - 1] = inl ? 1 : 0;
+        X.dist[par][le][r - 1] = lp[0];
+        X.dot[par][le][r - 1] = lp[1];
+        X.arad[par][le][r - 1] = lp[3];
+      }
+    }
+    PSTAMPT(d, 2);
+    __syncthreads();
+    PSTAMPT(d, 3);
+
+    // ---- reward / done / aggregation over the steps taken (every wave) ----
+    // every exchanged value is read at once (one wait), then the chain runs
+    // on registers
+    double xd[kFanSteps], xo[kFanSteps], xa[kFanSteps], xp[kFanSteps];
+    bool xi[kFanSteps], xv[kFanSteps];
+    {
+      const uint32_t vpw = *reinterpret_cast<const uint32_t*>(X.vp[par][le]);
+      const uint32_t inw = *reinterpret_cast<const uint32_t*>(X.inl[par][le]);
+#pragma unroll
+      for (int r = 0; r < kFanSteps; ++r) {
+        xd[r] = X.dist[par][le][r];
+        xo[r] = X.dot[par][le][r];
+        xa[r] = X.arad[par][le][r];
+        xp[r] = X.pen[par][le][r];
+        xv[r] = ((vpw >> (8 * r)) & 0xFFu) != 0u;
+        xi[r] = ((inw >> (8 * r)) & 0xFFu) != 0u;
+      }
+    }
+    // branch-free: every step's reward is formed and kept only if the step
+    // was taken (the same operations on the same operands as sim_decision)
+    double tr = 0.0, trm = 0.0;
+    bool dn = !active;
+    unsigned nsim = 0;
+    int last = 0;   // the pose the env ends the decision on (0: none taken)
+    const double kR = g.robot_speed;
+#pragma unroll
+    for (int r = 1; r <= kFanSteps; ++r) {
+      const bool live = !dn && r <= R;
+      const uint32_t sc1 = step_count + 1u;
+      const bool vp = xv[r - 1];
+      const bool cap = sc1 >= sc.max_steps;
+      const double sp = sc.speed_measured ? spd[r] : kR;
+      const double pen = xp[r - 1];
+      const double ad = fabs(xd[r - 1]);
+      const double rin = ((1.0 * sp) * xo[r - 1] + (-10.0) * ad) + 40.0 * pen;
+      const double rout = 40.0 * pen;
+      double rr = xi[r - 1] ? rin : rout;
+      rr = cap ? 0.0 : rr;
+      rr = vp ? rr : -1000.0;
+      const bool sd = !vp || cap;
+      const double rm = (rr == -1000.0) ? -10.0 : (rr > 0.0 ? rr + 10.0 : rr + 4.0);
+      const double tr1 = tr + rr, trm1 = trm + rm;
+      const uint32_t es1 = env_step + 1u;
+      tr = live ? tr1 : tr;
+      trm = live ? trm1 : trm;
+      step_count = live ? sc1 : step_count;
+      env_step = live ? es1 : env_step;
+      nsim += live ? 1u : 0u;
+      last = live ? r : last;
+      dn = live ? (sd || es1 > sc.max_env_steps) : dn;
+    }
+    trm = trm * sc.reward_scale;
+    double fx = x, fz = z, fa = ang, fc = c, fs = s;
+    bool inl_last = false;
+    double dist_last = 0.0, arad_last = 0.0;
+#pragma unroll
+    for (int r = 1; r <= kFanSteps; ++r)
+      if (last == r) {
+        fx = px[r];
+        fz = pz[r];
+        fa = pa[r];
+        fc = pc[r];
+        fs = ps[r];
+        inl_last = xi[r - 1];
+        dist_last = xd[r - 1];
+        arad_last = xa[r - 1];
+      }
+    x = fx;
+    z = fz;
+    ang = fa;
+    c = fc;
+    s = fs;
+
+    PSTAMPT(d, 4);
+    // ---- auto-reset ----
+    const bool want_reset = active && dn && sc.auto_reset;
+    bool ok = slot_ready && ((failed >> rel) & 1u) == 0u;
+    uint64_t need = __ballot(want_reset && !slot_ready && lead);
+    while (need) {  // wave-uniform; every wave computes the same spawns
+      const int l = __ffsll((unsigned long long)need) - 1;
+      need &= need - 1u;
+      const uint32_t el = (uint32_t)__shfl(ei, l), kl = (uint32_t)__shfl((int)key, l);
+      const uint64_t sd = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(seed >> 32), l) << 32) |
+                          (uint64_t)(uint32_t)__shfl((int)(uint32_t)seed, l);
+      double sx = 0.0, sz = 0.0, sa = 0.0, slp[2] = {0.0, 0.0};
+      const bool sok = dt::spawn_one(M, g, max_attempts, env_base + el, sd, kl, sx, sz, sa, slp);
+      if (le == (l >> 2)) {
+        rp[0] = sx;
+        rp[1] = sz;
+        rp[2] = sa;
+        rp[3] = slp[0];
+        rp[4] = slp[1];
+        sincos(sa, &rp[5], &rp[6]);
+        ok = sok;
+      }
+    }
+    const bool reset_now = want_reset && ok;
+    if (wave == 0 && lead && want_reset && !ok) atomicOr(st.err, dt::kErrSpawn);
+
+    if (active && lead) {
+      const size_t o = (size_t)d * n + e;
+      if (wave == 0) {
+        rew[o] = tr;
+        rewm[o] = trm;
+      } else if (wave == 1) {
+        done_out[o] = (uint8_t)dn;
+      } else if (wave == 2 && obs) {
+        obs[o] = reset_now ? make_float2((float)rp[3], (float)rp[4])
+                           : (inl_last ? make_float2((float)dist_last, (float)arad_last)
+                                       : make_float2(0.0f, 0.0f));
+      }
+    }
+    x = reset_now ? rp[0] : x;
+    z = reset_now ? rp[1] : z;
+    ang = reset_now ? rp[2] : ang;
+    s = reset_now ? rp[5] : s;
+    c = reset_now ? rp[6] : c;
+    step_count = reset_now ? 0u : step_count;
+    env_step = reset_now ? 0u : env_step;
+    key += reset_now ? 1u : 0u;
+    nsim_t += nsim;
+    act_t += active ? 1u : 0u;
+    resets_t += reset_now ? 1u : 0u;
+    dones_t += (active && dn) ? 1u : 0u;
+    a = an;
+    PSTAMPT(d, 5);
+  }
+  PSTAMP(1, 15, __builtin_amdgcn_s_memrealtime());
+  PSTAMP(2, 15, __builtin_amdgcn_s_memtime());
+  BSTAMP(1, __builtin_amdgcn_s_memrealtime());
+  // every wave is past its last slot read before wave 0 moves the window
+  __syncthreads();
+  if (wave != 0) return;
+  const unsigned kk = (unsigned)k;
+  const unsigned m = lead ? 1u : 0u;
+  dt::wave_count(st.stats + 0, nsim_t * m, kk * (unsigned)(sc.repeat * sc.frame_skip));
+  dt::wave_count(st.stats + 1, act_t * m, kk);
+  dt::wave_count(st.stats + 2, resets_t * m, kk);
+  dt::wave_count(st.stats + 3, dones_t * m, kk);
+  if (active && lead) {
     st.x[e] = x;
     st.z[e] = z;
     st.angle[e] = ang;
@@ -801,6 +1205,12 @@ extern "C" {
 #ifdef DTSIM_STAMPS
 int dt_diag_stamps(unsigned long long* out) {  // 64 x kStamps shader-clock stamps
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(g_stamps)) == hipSuccess ? 0 : -1;
+}
+int dt_diag_pstamps(unsigned long long* out) {  // step_pair_kernel stamps (g_pstamps)
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pstamps), sizeof(g_pstamps)) == hipSuccess ? 0 : -1;
+}
+int dt_diag_bstamps(unsigned long long* out) {  // step_fan_kernel per-block stamps
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_bstamps), sizeof(g_bstamps)) == hipSuccess ? 0 : -1;
 }
 int dt_diag_rstamps(unsigned long long* out) {  // refill blocks: entry, exit (real time), items
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_rstamps), sizeof(g_rstamps)) == hipSuccess ? 0
@@ -1119,10 +1529,25 @@ int dt_step_many(dt_handle* h, int32_t k, const float* actions, double* reward,
   }
   DevGuard dg(h->device);
   hipStream_t s = (hipStream_t)stream;
-  // two waves per 64 envs (step_pair_kernel); DTSIM_STEP_PAIR=0: one (step_kernel)
-  static const bool pair = !(getenv("DTSIM_STEP_PAIR") && getenv("DTSIM_STEP_PAIR")[0] == '0');
+  // DTSIM_STEP_KERNEL: fan (default: 16 envs x 4 waves per workgroup), pair
+  // (two waves per 64 envs) or one (one wave per 64 envs, step_kernel);
+  // DTSIM_STEP_PAIR=0 (older spelling) selects one
+  static const int mode = [] {
+    const char* k = getenv("DTSIM_STEP_KERNEL");
+    const char* p = getenv("DTSIM_STEP_PAIR");
+    if (k && !strcmp(k, "one")) return 0;
+    if (k && !strcmp(k, "pair")) return 1;
+    if (p && p[0] == '0') return 0;
+    return 2;
+  }();
   const int rb = h->sc.auto_reset ? refill_grid(h->n, kRefillEnvs) : 0;
-  if (pair) {
+  if (mode == 2 && h->sc.repeat * h->sc.frame_skip <= kFanSteps && h->sc.frame_skip == 1) {
+    const int gs = (h->n + kFanEnvs - 1) / kFanEnvs;
+    hipLaunchKernelGGL(step_fan_kernel, dim3(gs + rb), dim3(kFanBlock), h->lds_bytes, s, h->st,
+                       h->map, h->geo, h->sc, h->n, h->env_base, (int)k,
+                       (const float2*)actions, reward, reward_mod, done, (float2*)obs, gs,
+                       h->sc.max_spawn_attempts);
+  } else if (mode >= 1) {
     // one pair (two waves, 64 envs) per workgroup: the exchange barriers stay
     // pair-local; the refill blocks of the launch run with 128 threads too
     const int gs = (h->n + 63) / 64;
@@ -1212,3 +1637,79 @@ int dt_check(dt_handle* h, uint32_t* flags) {
 }
 
 }  // extern "C"
+
+#ifdef DTSIM_STAMPS
+// Diagnostic build only: cycles of one wave (64 envs, their current poses)
+// per call of a step-math piece, in a loop on the LDS-staged map.
+namespace {
+__device__ unsigned long long g_micro[64];
+__global__ __launch_bounds__(64) void micro_kernel(dt::State st, dt::MapDev md, dt::Geo g,
+                                                   int iters, int which) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const MapLds M = dt::stage_map(md, lds);
+  const int lane = threadIdx.x;
+  double x = st.x[lane], z = st.z[lane], a = st.angle[lane];
+  double s, c;
+  sincos(a, &s, &c);
+  double acc = 0.0;
+  const double* cv = dt::closest_curve(M, g, x, z, c, s);
+  if (!cv) cv = M.curves;
+  __builtin_amdgcn_s_waitcnt(0);
+  const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+  for (int i = 0; i < iters; ++i) {
+    if (which == 0) {
+      double lp[4];
+      const bool in = dt::lane_pos<false>(M, g, x, z, c, s, lp);
+      acc = acc + (in ? lp[0] : 1.0);
+    } else if (which == 1) {
+      acc = acc + (dt::valid_pose(M, g, x, z, c, s, 1.0) ? 1.0 : 2.0);
+    } else if (which == 2) {
+      double s2, c2;
+      sincos(x, &s2, &c2);
+      acc = acc + s2 + c2;
+    } else if (which == 3) {
+      acc = acc + dt::bezier_closest(cv, x, z);
+    } else if (which == 4) {
+      const double* cc = dt::closest_curve(M, g, x, z, c, s);
+      acc = acc + (cc ? cc[0] : 1.0);
+    } else if (which == 5) {
+      acc = acc + (double)dt::tile_of(M, g, x, z);
+    } else if (which == 6) {
+      double lp[4];
+      dt::lane_pose_at<false>(g, cv, 0.3, x, z, c, s, lp);
+      acc = acc + lp[0];
+    } else if (which == 7) {
+      acc = acc + (dt::drivable(M, g, x, z) ? 1.0 : 2.0);
+    } else if (which == 8) {
+      double lp[4];
+      const bool in = dt::lane_pos_lean<false>(M, g, x, z, c, s, lp);
+      acc = acc + (in ? lp[0] : 1.0);
+    } else if (which == 9) {
+      acc = acc + (dt::valid_pose_lean(M, g, x, z, c, s, 1.0) ? 1.0 : 2.0);
+    } else if (which == 10) {
+      bool nr = false;
+      acc = acc + dt::bezier_closest_fast(cv, x, z, nr) + (nr ? 1.0 : 0.0);
+    } else if (which == 11) {
+      bool nr = false;
+      acc = acc + (double)dt::tile_of_fast(M, g, x, z, nr) + (nr ? 1.0 : 0.0);
+    } else if (which == 12) {
+      bool nr = false;
+      const double* cc = dt::closest_curve_fast(M, g, x, z, c, s, nr);
+      acc = acc + (cc ? cc[0] : 1.0) + (nr ? 1.0 : 0.0);
+    }
+    x = x + acc * 1e-300;
+  }
+  const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+  st.x[lane] = x;  // keep the loop live (the pose moves by < 1 ulp)
+  if (lane == 0) g_micro[0] = t1 - t0;
+}
+}  // namespace
+
+extern "C" int dt_diag_micro(dt_handle* h, int iters, int which, unsigned long long* out) {
+  HIP_OR_FAIL(h, hipSetDevice(h->device));
+  hipLaunchKernelGGL(micro_kernel, dim3(1), dim3(64), h->lds_bytes, 0, h->st, h->map, h->geo,
+                     iters, which);
+  HIP_OR_FAIL(h, hipDeviceSynchronize());
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_micro), 8) == hipSuccess ? 0 : -1;
+}
+#endif

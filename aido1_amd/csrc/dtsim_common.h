@@ -97,6 +97,9 @@ struct MapLds {
   const uint16_t* curve_start;
   const int8_t* kind;
   const int16_t* drivable;
+  // per tile, packed for one LDS read: first curve (bits 0-15), curve count
+  // (16-23), kind > 0 (bit 24)
+  const uint32_t* tinfo;
   int32_t width, height, n_drivable, n_obj, n_spawn_obj;
 };
 
@@ -107,6 +110,7 @@ __host__ __device__ inline size_t map_lds_bytes(int n_tiles, int n_drivable, int
   b += ((size_t)(n_tiles + 1) * 2 + 15) & ~(size_t)15;
   b += ((size_t)n_tiles + 15) & ~(size_t)15;
   b += ((size_t)n_drivable * 2 + 15) & ~(size_t)15;
+  b += (size_t)n_tiles * 4;
   return b;
 }
 
@@ -125,6 +129,12 @@ __device__ inline MapLds stage_map(const MapDev& m, unsigned char* lds) {
   for (int i = tid; i <= m.n_tiles; i += nt) cs[i] = m.curve_start[i];
   for (int i = tid; i < m.n_tiles; i += nt) kd[i] = m.kind[i];
   for (int i = tid; i < m.n_drivable; i += nt) dv[i] = m.drivable[i];
+  uint32_t* ti = reinterpret_cast<uint32_t*>(
+      reinterpret_cast<unsigned char*>(dv) + (((size_t)m.n_drivable * 2 + 15) & ~(size_t)15));
+  for (int i = tid; i < m.n_tiles; i += nt) {
+    const uint32_t k0 = m.curve_start[i], k1 = m.curve_start[i + 1];
+    ti[i] = k0 | ((k1 - k0) << 16) | (m.kind[i] > 0 ? (1u << 24) : 0u);
+  }
   __syncthreads();
   MapLds r;
   r.curves = cv;
@@ -133,6 +143,7 @@ __device__ inline MapLds stage_map(const MapDev& m, unsigned char* lds) {
   r.curve_start = cs;
   r.kind = kd;
   r.drivable = dv;
+  r.tinfo = ti;
   r.width = m.width;
   r.height = m.height;
   r.n_drivable = m.n_drivable;
@@ -220,6 +231,33 @@ __device__ inline int tile_of(const MapLds& M, const Geo& g, double x, double z)
 __device__ inline bool drivable(const MapLds& M, const Geo& g, double x, double z) {
   const int t = tile_of(M, g, x, z);
   return t >= 0 && M.kind[t] > 0;
+}
+
+// ---- branch-free fast forms -----------------------------------------------------
+// The exact forms above decide their rare cases (a quotient within ulps of a
+// tile edge, two distances within ulps) with a divergent branch on every call,
+// and the exec-mask juggling of those branches costs more than the float64 math
+// around them.  The *_fast forms take the common-case answer unconditionally
+// and OR a `near` flag when the exact form could answer differently; a caller
+// re-runs the exact form only for lanes with `near` set (one branch per call,
+// essentially never taken), so results are identical to the exact forms.
+__device__ inline double floor_div_fast(double v, const Geo& g, bool& near) {
+  const double q = v * g.inv_ts;
+  const double f = floor(q);
+  const double r = q - f;
+  near |= (r < 1e-9) | (r > 1.0 - 1e-9);
+  return f;
+}
+
+__device__ inline int tile_of_fast(const MapLds& M, const Geo& g, double x, double z, bool& near) {
+  const double fi = floor_div_fast(x, g, near), fj = floor_div_fast(z, g, near);
+  const bool in = (fi >= 0.0) & (fj >= 0.0) & (fi < (double)M.width) & (fj < (double)M.height);
+  return in ? (int)fj * M.width + (int)fi : -1;
+}
+
+__device__ inline bool drivable_fast(const MapLds& M, const Geo& g, double x, double z, bool& near) {
+  const int t = tile_of_fast(M, g, x, z, near);
+  return ((M.tinfo[t < 0 ? 0 : t] >> 24) & 1u) != 0u && t >= 0;
 }
 
 // ---- static objects [upstream collision.py; §8f-3] ---------------------------------
@@ -337,6 +375,31 @@ __device__ inline bool valid_pose(const MapLds& M, const Geo& g, double x, doubl
   return ok && !collide(M, g, px, pz, c, s);
 }
 
+// valid_pose without the collision test: the four drivable probes (fast form)
+__device__ inline bool probes_fast(const MapLds& M, const Geo& g, double x, double z, double c,
+                                   double s, double safety, bool& near) {
+  const double px = x + g.off * c;
+  const double pz = z + g.off * (-s);
+  const double kw = (safety * 0.5) * g.robot_width;
+  const double kf = (safety * 0.5) * g.front;
+  const bool d0 = drivable_fast(M, g, px, pz, near);
+  const bool d1 = drivable_fast(M, g, px - kw * s, pz - kw * c, near);
+  const bool d2 = drivable_fast(M, g, px + kw * s, pz + kw * c, near);
+  const bool d3 = drivable_fast(M, g, px + kf * c, pz + kf * (-s), near);
+  return d0 & d1 & d2 & d3;
+}
+
+// valid_pose, identical results: the fast probes, the exact form only for a
+// lane whose probes came near a tile edge
+__device__ inline bool valid_pose_lean(const MapLds& M, const Geo& g, double x, double z, double c,
+                                       double s, double safety) {
+  bool near = false;
+  bool ok = probes_fast(M, g, x, z, c, s, safety, near);
+  if (__builtin_expect(near, 0)) return valid_pose(M, g, x, z, c, s, safety);
+  if (M.n_obj && ok) ok = !collide(M, g, x + g.off * c, z + g.off * (-s), c, s);
+  return ok;
+}
+
 // bezier_point (A9) in the ground plane: coefficients are exact dyadics for
 // the bisection's t values
 __device__ inline void bez_xz(const double* __restrict__ cv, double t, double& ox, double& oz) {
@@ -431,6 +494,28 @@ __device__ inline double bezier_closest(const double* cv, double x, double z) {
   return (tb + tt) * 0.5;
 }
 
+// bezier_closest with plain comparisons of the squared distances; `near` is
+// set when any level compared two values close enough for the roots to round
+// equal (where root_less takes the roots), and the caller then re-runs
+// bezier_closest.  Same evaluation order as bezier_closest otherwise.
+__device__ inline double bezier_closest_fast(const double* cv, double x, double z, bool& near) {
+  double tb = 0.0, tt = 1.0;
+  double db = dist2_pt(cv[0], cv[1], x, z), dtp = dist2_pt(cv[6], cv[7], x, z);
+#pragma unroll
+  for (int n = 8; n > 0; --n) {
+    const double mid = (tb + tt) * 0.5;
+    const double dm = n > 1 ? dist2_to(cv, mid, x, z) : 0.0;
+    const double d = dtp - db;
+    near |= !(fabs(d) > 8.0 * 2.220446049250313e-16 * fmax(db, dtp));
+    const bool left = db < dtp;
+    tt = left ? mid : tt;
+    dtp = left ? dm : dtp;
+    tb = left ? tb : mid;
+    db = left ? db : dm;
+  }
+  return (tb + tt) * 0.5;
+}
+
 // lp = {dist, dot_dir, angle_deg, angle_rad} at the curve point tm; without
 // kAngle the acos is left out and lp[2] holds the side value for finish_angle.
 template <bool kAngle>
@@ -471,6 +556,178 @@ __device__ inline bool lane_pos(const MapLds& M, const Geo& g, double x, double 
   return true;
 }
 
+// closest_curve with the fast tile lookup and the packed tile word: the
+// headings of a tile's first two curves are read together (one LDS round
+// trip), the rest (intersection tiles) in the loop
+__device__ inline const double* closest_curve_fast(const MapLds& M, const Geo& g, double x,
+                                                   double z, double c, double s, bool& near) {
+  const int t = tile_of_fast(M, g, x, z, near);
+  const uint32_t info = M.tinfo[t < 0 ? 0 : t];
+  if (t < 0 || ((info >> 24) & 1u) == 0u) return nullptr;
+  const double dx = c, dz = -s;
+  const int k0 = (int)(info & 0xFFFFu), nc = (int)((info >> 16) & 0xFFu);
+  const double* h0 = M.curves + kCurveRec * k0 + 14;
+  const double* h1 = h0 + (nc > 1 ? kCurveRec : 0);
+  const double hx0 = h0[0], hz0 = h0[1], hx1 = h1[0], hz1 = h1[1];
+  double bd = hx0 * dx + hz0 * dz;
+  int best = k0;
+  const double d1 = hx1 * dx + hz1 * dz;
+  if (nc > 1 && d1 > bd) {
+    bd = d1;
+    best = k0 + 1;
+  }
+  for (int k = k0 + 2; k < k0 + nc; ++k) {
+    const double* hd = M.curves + kCurveRec * k + 14;
+    const double d = hd[0] * dx + hd[1] * dz;
+    if (d > bd) {
+      bd = d;
+      best = k;
+    }
+  }
+  return M.curves + kCurveRec * best;
+}
+
+// get_lane_pos2, identical results to lane_pos: the fast forms, and lane_pos
+// itself only for a lane that came near a tile edge or a distance tie
+template <bool kAngle = true>
+__device__ inline bool lane_pos_lean(const MapLds& M, const Geo& g, double x, double z, double c,
+                                     double s, double lp[4]) {
+  bool near = false;
+  const double* cv = closest_curve_fast(M, g, x, z, c, s, near);
+  double tm = 0.0;
+  if (cv) tm = bezier_closest_fast(cv, x, z, near);
+  if (__builtin_expect(near, 0)) return lane_pos<kAngle>(M, g, x, z, c, s, lp);
+  if (!cv) return false;
+  lane_pose_at<kAngle>(g, cv, tm, x, z, c, s, lp);
+  return true;
+}
+
+// ---- quad forms: one env on the 4 lanes of a DPP quad -----------------------------
+// step_fan_kernel runs every env on the four lanes of a quad (lane & 3 = q);
+// the lanes hold the same state and make the same decisions, and split the
+// data-parallel parts of the step math: the four drivable probes of
+// _valid_pose, the sincos of the decision's rotation and angles, and three
+// bisection levels per round of bezier_closest.  Values cross lanes with DPP
+// quad_perm moves (no LDS, no waits).
+template <int J>
+__device__ __forceinline__ int qget(int v) {
+  return __builtin_amdgcn_mov_dpp(v, J * 0x55, 0xF, 0xF, true);
+}
+template <int J>
+__device__ __forceinline__ double qget(double v) {
+  const long long u = __double_as_longlong(v);
+  const int lo = qget<J>((int)(uint32_t)u), hi = qget<J>((int)(uint32_t)(u >> 32));
+  return __longlong_as_double((long long)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo));
+}
+// AND / OR of a flag over the quad
+__device__ __forceinline__ bool qall(bool b) {
+  int v = b ? 1 : 0;
+  v &= __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true);   // [1,0,3,2]
+  v &= __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true);   // [2,3,0,1]
+  return v != 0;
+}
+__device__ __forceinline__ bool qany(bool b) {
+  int v = b ? 1 : 0;
+  v |= __builtin_amdgcn_mov_dpp(v, 0xB1, 0xF, 0xF, true);
+  v |= __builtin_amdgcn_mov_dpp(v, 0x4E, 0xF, 0xF, true);
+  return v != 0;
+}
+
+// The drivable probes of _valid_pose at one pose, probe q on lane q: the same
+// operands as valid_pose (px - kw*s == px + -(kw*s) exactly).  Returns this
+// lane's probe; `near` as floor_div_fast.
+__device__ inline bool probe_q(const MapLds& M, const Geo& g, int q, double x, double z, double c,
+                               double s, double safety, bool& near) {
+  const double px = x + g.off * c;
+  const double pz = z + g.off * (-s);
+  const double kw = (safety * 0.5) * g.robot_width;
+  const double kf = (safety * 0.5) * g.front;
+  const double ws = kw * s, wc = kw * c, fc = kf * c, fs = kf * (-s);
+  const double ox = q == 1 ? -ws : (q == 2 ? ws : fc);
+  const double oz = q == 1 ? -wc : (q == 2 ? wc : fs);
+  const double tx = q == 0 ? px : px + ox;
+  const double tz = q == 0 ? pz : pz + oz;
+  return drivable_fast(M, g, tx, tz, near);
+}
+
+// _valid_pose at one pose over a quad, identical to valid_pose
+__device__ inline bool valid_pose_q(const MapLds& M, const Geo& g, int q, double x, double z,
+                                    double c, double s, double safety) {
+  bool near = false;
+  bool ok = qall(probe_q(M, g, q, x, z, c, s, safety, near));
+  if (__builtin_expect(qany(near), 0)) return valid_pose(M, g, x, z, c, s, safety);
+  if (M.n_obj && ok) ok = !collide(M, g, x + g.off * c, z + g.off * (-s), c, s);
+  return ok;
+}
+
+// bezier_closest over a quad: per round, the first level's comparison is known
+// (both end distances are), so the four lanes evaluate the four points the
+// next three levels can need -- the midpoint m1, the midpoint m2 of the half
+// kept, and both candidate midpoints of m2's halves -- and every lane then
+// walks the three levels.  The t values and distances are the ones the
+// sequential bisection computes (the same dyadic midpoints, the same
+// dist2_to), so the result is identical; `near` as bezier_closest_fast.
+__device__ inline double bezier_closest_q(const double* cv, int q, double x, double z,
+                                          bool& near) {
+  constexpr double kTol = 8.0 * 2.220446049250313e-16;
+  double tb = 0.0, tt = 1.0;
+  double db = dist2_pt(cv[0], cv[1], x, z), dtp = dist2_pt(cv[6], cv[7], x, z);
+#pragma unroll
+  for (int n = 8; n > 0; n -= 3) {
+    // level n (comparison known)
+    near |= !(fabs(dtp - db) > kTol * fmax(db, dtp));
+    const bool l1 = db < dtp;
+    const double m1 = (tb + tt) * 0.5;
+    const double lo1 = l1 ? tb : m1, hi1 = l1 ? m1 : tt;
+    const double m2 = (lo1 + hi1) * 0.5;
+    const double m3a = (lo1 + m2) * 0.5, m3b = (m2 + hi1) * 0.5;
+    const double tq = q == 0 ? m1 : (q == 1 ? m2 : (q == 2 ? m3a : m3b));
+    const double dq = dist2_to(cv, tq, x, z);
+    const double dm1 = qget<0>(dq);
+    // level n - 1
+    const double e_lo = l1 ? db : dm1, e_hi = l1 ? dm1 : dtp;
+    if (n - 1 == 0) {
+      tb = lo1;
+      tt = hi1;
+      break;
+    }
+    const double dm2 = qget<1>(dq);
+    near |= !(fabs(e_hi - e_lo) > kTol * fmax(e_lo, e_hi));
+    const bool l2 = e_lo < e_hi;
+    const double lo2 = l2 ? lo1 : m2, hi2 = l2 ? m2 : hi1;
+    const double d_lo2 = l2 ? e_lo : dm2, d_hi2 = l2 ? dm2 : e_hi;
+    if (n - 2 == 0) {
+      tb = lo2;
+      tt = hi2;
+      break;
+    }
+    // level n - 2
+    const double dm3a = qget<2>(dq), dm3b = qget<3>(dq);
+    near |= !(fabs(d_hi2 - d_lo2) > kTol * fmax(d_lo2, d_hi2));
+    const bool l3 = d_lo2 < d_hi2;
+    const double m3 = l2 ? m3a : m3b, dm3 = l2 ? dm3a : dm3b;
+    tb = l3 ? lo2 : m3;
+    tt = l3 ? m3 : hi2;
+    db = l3 ? d_lo2 : dm3;
+    dtp = l3 ? dm3 : d_hi2;
+  }
+  return (tb + tt) * 0.5;
+}
+
+// get_lane_pos2 over a quad (every lane returns the full result), identical
+// to lane_pos<true>
+__device__ inline bool lane_pos_q(const MapLds& M, const Geo& g, int q, double x, double z,
+                                  double c, double s, double lp[4]) {
+  bool near = false;
+  const double* cv = closest_curve_fast(M, g, x, z, c, s, near);
+  double tm = 0.0;
+  if (cv) tm = bezier_closest_q(cv, q, x, z, near);
+  if (__builtin_expect(near, 0)) return lane_pos<true>(M, g, x, z, c, s, lp);
+  if (!cv) return false;
+  lane_pose_at<true>(g, cv, tm, x, z, c, s, lp);
+  return true;
+}
+
 // One spawn proposal (A13): returns true if accepted.
 __device__ inline bool spawn_try(const MapLds& M, const Geo& g, uint32_t k0, uint32_t k1,
                                  uint32_t env, uint32_t episode, uint32_t k, double fi,
@@ -487,9 +744,9 @@ __device__ inline bool spawn_try(const MapLds& M, const Geo& g, uint32_t k0, uin
   oz = pz;
   oa = pa;
   if (inconvenient_spawn(M, px, pz)) return false;
-  if (!valid_pose(M, g, px, pz, c, s, g.reset_safety)) return false;
+  if (!valid_pose_lean(M, g, px, pz, c, s, g.reset_safety)) return false;
   double lp[4];
-  if (!lane_pos(M, g, px, pz, c, s, lp)) return false;
+  if (!lane_pos_lean<true>(M, g, px, pz, c, s, lp)) return false;
   if (lp_out) {
     lp_out[0] = lp[0];
     lp_out[1] = lp[3];

@@ -396,8 +396,7 @@ def bench_lane(args, ctx):
         fused_bytes = (MANY_BYTES_PER_ENV + MANY_BYTES_PER_ENV_DECISION * K / nl) * n + \
             MANY_BYTES_PER_RESET * resets_per_launch
         achieved = survey_bytes / (kms * 1e-3) / 1e9
-        kname = ('step_kernel' if os.environ.get('DTSIM_STEP_PAIR', '1').startswith('0')
-                 else 'step_pair_kernel')
+        kname = step_kernel_name()
         pmc = load_pmc(kname) or {}
         line = {
             'metric': METRIC,
@@ -460,12 +459,23 @@ def _bounds(sizes):
         a += s
 
 
+def step_kernel_name():
+    """The kernel dt_step_many launches (DTSIM_STEP_KERNEL, see dtsim.hip)."""
+    k = os.environ.get('DTSIM_STEP_KERNEL', '')
+    if k == 'one' or os.environ.get('DTSIM_STEP_PAIR', '1').startswith('0'):
+        return 'step_kernel'
+    return 'step_pair_kernel' if k == 'pair' else 'step_fan_kernel'
+
+
+STEP_WAVES_PER_64_ENVS = {'step_kernel': 1, 'step_pair_kernel': 2, 'step_fan_kernel': 16}
+
+
 def step_bound_record(kname, kms, dec_per_launch, n, pmc):
     """The config-2 kernel's real bound: per-decision time of one env's float64
     chain, and the fp64 issue rate it reaches vs the chip's (PMC counts from
     profiles/pmc_traffic.json when present)."""
     rec = {'us_per_decision': kms * 1e3 / dec_per_launch,
-           'waves': 2 * n // 64 if kname == 'step_pair_kernel' else n // 64,
+           'waves': STEP_WAVES_PER_64_ENVS[kname] * n // 64,
            'simds_on_chip': 1024}
     f = pmc.get('fp64_flops_per_launch')
     if f:

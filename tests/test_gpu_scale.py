@@ -85,7 +85,12 @@ def test_config5_train_loop_at_size(gpu):
     assert torch.isfinite(loop.metrics['critic_loss']) and torch.isfinite(loop.metrics['actor_loss'])
     loop.replay.check()
     s, mn, mp = loop.replay.trees()
-    assert float(mp) >= 1.0 and float(s) > 0.0 and float(mn) > 0.0
+    # roots at index 1 (segment_tree.py layout): total priority mass, smallest
+    # priority; the leaves [cap, 2cap) all hold written transitions
+    assert mp.item() >= 1.0 and s[1].item() > 0.0 and mn[1].item() > 0.0
+    leaves = s[cap:].cpu().numpy()
+    assert (leaves > 0.0).all()
+    assert abs(leaves.sum() - s[1].item()) <= 1e-9 * s[1].item()
     assert loop.rollout.stats()['decisions'] == n * steps
     loop.rollout.close()
 

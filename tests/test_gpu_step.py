@@ -258,8 +258,8 @@ def test_step_many_matches_oracle(gpu, k, map_name):
     """dt_step_many: k decisions per launch == k oracle steps, per decision;
     three launches back to back, then an eager dt_step continues the state.
     Envs finishing more often than their ready slots cover spawn inline.
-    (The two-wave step_pair_kernel; test_step_many_single_wave covers the
-    one-wave path.)"""
+    (The default fan kernel, step_fan_kernel; test_step_many_other_kernels
+    covers step_pair_kernel and the one-wave step_kernel.)"""
     from aido1_amd.vec_env import StepOutput
     n = 4096
     env, ob = make_pair(n, map_name=map_name)
@@ -299,11 +299,13 @@ def test_step_many_matches_oracle(gpu, k, map_name):
     env.check()
 
 
-def test_step_many_single_wave(gpu):
-    """DTSIM_STEP_PAIR=0 (step_kernel over k decisions) in a child process, the
-    setting being read once per process: the same check at k = 16 (loop_empty),
-    12 (loop_obstacles, where the pair kernel splits proximity_penalty across
-    its two waves), 30 (zigzag) and 64 (small_loop)."""
+@pytest.mark.parametrize('kernel', ['pair', 'one'])
+def test_step_many_other_kernels(gpu, kernel):
+    """DTSIM_STEP_KERNEL=pair (step_pair_kernel: two waves per 64 envs) and
+    =one (step_kernel over k decisions), each in a child process (the setting
+    is read once per process): the same check at k = 16 (loop_empty), 12
+    (loop_obstacles, where the pair kernel splits proximity_penalty across its
+    two waves), 30 (zigzag) and 64 (small_loop)."""
     import os
     import subprocess
     import sys
@@ -311,7 +313,8 @@ def test_step_many_single_wave(gpu):
             '"no:cacheprovider", "-k", "step_many_matches_oracle and (16-loop_empty or 12-loop_obstacles or '
             '30-zigzag or 64-small_loop)", '
             '"%s"]))' % os.path.abspath(__file__))
-    env = dict(os.environ, DTSIM_STEP_PAIR='0')
+    env = dict(os.environ, DTSIM_STEP_KERNEL=kernel)
     r = subprocess.run([sys.executable, '-c', code], env=env, cwd=os.path.dirname(__file__),
                        capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert '4 passed' in r.stdout, r.stdout[-2000:]
