@@ -794,6 +794,7 @@ __global__ __launch_bounds__(kBlock) void step_pair_kernel(dt::State st, dt::Map
 constexpr int kFanEnvs = 16;                // envs per workgroup
 constexpr int kFanBlock = 4 * 64;           // four waves
 constexpr int kFanSteps = 3;                // repeat * frame_skip handled
+constexpr int kFanMaxK = 64;                // decisions per launch (actions staged in LDS)
 
 struct FanX {  // [parity][env][step], rows padded to 4 for wide LDS reads
   double dist[2][kFanEnvs][4], dot[2][kFanEnvs][4], arad[2][kFanEnvs][4], pen[2][kFanEnvs][4];
@@ -809,7 +810,8 @@ __global__ __launch_bounds__(kFanBlock) __attribute__((amdgpu_waves_per_eu(2, 2)
                                                              uint8_t* __restrict__ done_out,
                                                              float2* __restrict__ obs,
                                                              int n_step_blocks,
-                                                             uint32_t max_attempts) {
+                                                             uint32_t max_attempts,
+                                                             uint32_t map_lds_offset) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
 #ifdef DTSIM_STAMPS
   BSTAMP(0, __builtin_amdgcn_s_memrealtime());
@@ -835,7 +837,6 @@ __global__ __launch_bounds__(kFanBlock) __attribute__((amdgpu_waves_per_eu(2, 2)
 
   double x = st.x[ei], z = st.z[ei], ang = st.angle[ei];
   uint32_t step_count = st.step_count[ei], env_step = st.env_step[ei];
-  float2 a = act[ei];
   const uint32_t tick = st.tick[ei];
   uint32_t key = 0u;
   uint64_t seed = 0u, words[dt::kSlots];
@@ -847,7 +848,26 @@ __global__ __launch_bounds__(kFanBlock) __attribute__((amdgpu_waves_per_eu(2, 2)
       words[j] = __hip_atomic_load(st.pre_key + (size_t)j * n + ei, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
   }
-  const MapLds M = dt::stage_map(md, lds);
+  // staged in LDS behind the map image: the block's spawn-ahead slot records
+  // (the whole window; a lane reads only slots an earlier launch wrote, which
+  // no block of this launch rewrites) and its actions of all k decisions
+  // (k <= kFanMaxK; the host splits longer runs) -- no global load and no
+  // prefetch register in the decision loop
+  double* sslot = reinterpret_cast<double*>(lds + map_lds_offset);   // [kSlots*kSlotRec][16]
+  float2* sact = reinterpret_cast<float2*>(sslot + dt::kSlots * dt::kSlotRec * kFanEnvs);
+  {
+    const int e0 = (int)blockIdx.x * kFanEnvs;
+    for (int i = (int)threadIdx.x; i < k * kFanEnvs; i += kFanBlock) {
+      const int dd = i / kFanEnvs, j = i % kFanEnvs;
+      if (e0 + j < n) sact[i] = act[(size_t)dd * n + e0 + j];
+    }
+    if (sc.auto_reset)
+      for (int i = (int)threadIdx.x; i < dt::kSlots * dt::kSlotRec * kFanEnvs; i += kFanBlock) {
+        const int row = i / kFanEnvs, j = i % kFanEnvs;
+        if (e0 + j < n) sslot[i] = st.pre[(size_t)row * n + e0 + j];
+      }
+  }
+  const MapLds M = dt::stage_map(md, lds);   // its barrier also covers sact
   const uint32_t key0 = key;
   uint32_t ready = 0u, failed = 0u;
   if (sc.auto_reset) {
@@ -869,16 +889,9 @@ __global__ __launch_bounds__(kFanBlock) __attribute__((amdgpu_waves_per_eu(2, 2)
   const int R = sc.repeat;
   for (int d = 0; d < k; ++d) {
     const int par = d & 1;
-    const float2 an = act[(size_t)(d + 1 < k ? d + 1 : d) * n + ei];
+    const float2 a = sact[d * kFanEnvs + le];
     const uint32_t rel = key - key0;
     const bool slot_ready = rel < (uint32_t)dt::kSlots && ((ready >> rel) & 1u) != 0u;
-    if (slot_ready) {
-      const size_t sl = key % (uint32_t)dt::kSlots;
-#pragma unroll
-      for (int j = 0; j < dt::kSlotRec; ++j)
-        rp[j] = st.pre[(sl * dt::kSlotRec + j) * (size_t)n + ei];
-    }
-    asm volatile("" ::: "memory");
     PSTAMPT(d, 0);
 
     // ---- the pose chain (every wave) ----
@@ -1056,6 +1069,11 @@ __global__ __launch_bounds__(kFanBlock) __attribute__((amdgpu_waves_per_eu(2, 2)
     // ---- auto-reset ----
     const bool want_reset = active && dn && sc.auto_reset;
     bool ok = slot_ready && ((failed >> rel) & 1u) == 0u;
+    if (want_reset && slot_ready) {
+      const int sl = (int)(key % (uint32_t)dt::kSlots);
+#pragma unroll
+      for (int j = 0; j < dt::kSlotRec; ++j) rp[j] = sslot[(sl * dt::kSlotRec + j) * kFanEnvs + le];
+    }
     uint64_t need = __ballot(want_reset && !slot_ready && lead);
     while (need) {  // wave-uniform; every wave computes the same spawns
       const int l = __ffsll((unsigned long long)need) - 1;
@@ -1103,7 +1121,6 @@ __global__ __launch_bounds__(kFanBlock) __attribute__((amdgpu_waves_per_eu(2, 2)
     act_t += active ? 1u : 0u;
     resets_t += reset_now ? 1u : 0u;
     dones_t += (active && dn) ? 1u : 0u;
-    a = an;
     PSTAMPT(d, 5);
   }
   PSTAMP(1, 15, __builtin_amdgcn_s_memrealtime());
@@ -1126,9 +1143,10 @@ __global__ __launch_bounds__(kFanBlock) __attribute__((amdgpu_waves_per_eu(2, 2)
     st.env_step[e] = env_step;
     __hip_atomic_store(st.tick + e, tick + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (key != key0) {
+      // the slot records were read into LDS before the staging barrier, so
+      // the window can move
       st.episode[e] = key;
-      __hip_atomic_store(st.want + e, key + 1u + after_load(rp[dt::kSlotRec - 1]), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(st.want + e, key + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
@@ -1543,10 +1561,20 @@ int dt_step_many(dt_handle* h, int32_t k, const float* actions, double* reward,
   const int rb = h->sc.auto_reset ? refill_grid(h->n, kRefillEnvs) : 0;
   if (mode == 2 && h->sc.repeat * h->sc.frame_skip <= kFanSteps && h->sc.frame_skip == 1) {
     const int gs = (h->n + kFanEnvs - 1) / kFanEnvs;
-    hipLaunchKernelGGL(step_fan_kernel, dim3(gs + rb), dim3(kFanBlock), h->lds_bytes, s, h->st,
-                       h->map, h->geo, h->sc, h->n, h->env_base, (int)k,
-                       (const float2*)actions, reward, reward_mod, done, (float2*)obs, gs,
-                       h->sc.max_spawn_attempts);
+    const size_t off = (h->lds_bytes + 15) & ~(size_t)15;
+    const size_t slots = (size_t)dt::kSlots * dt::kSlotRec * kFanEnvs * sizeof(double);
+    // runs of more than kFanMaxK decisions: consecutive launches (the state,
+    // counters and spawn window carry over exactly as between calls)
+    for (int d0 = 0; d0 < k; d0 += kFanMaxK) {
+      const int kk = k - d0 < kFanMaxK ? k - d0 : kFanMaxK;
+      const size_t o = (size_t)d0 * h->n;
+      hipLaunchKernelGGL(step_fan_kernel, dim3(gs + rb), dim3(kFanBlock),
+                         off + slots + (size_t)kk * kFanEnvs * sizeof(float2), s, h->st, h->map,
+                         h->geo,
+                         h->sc, h->n, h->env_base, kk, (const float2*)actions + o, reward + o,
+                         reward_mod + o, done + o, obs ? (float2*)obs + o : (float2*)nullptr, gs,
+                         h->sc.max_spawn_attempts, (uint32_t)off);
+    }
   } else if (mode >= 1) {
     // one pair (two waves, 64 envs) per workgroup: the exchange barriers stay
     // pair-local; the refill blocks of the launch run with 128 threads too
@@ -1696,6 +1724,49 @@ __global__ __launch_bounds__(64) void micro_kernel(dt::State st, dt::MapDev md, 
       bool nr = false;
       const double* cc = dt::closest_curve_fast(M, g, x, z, c, s, nr);
       acc = acc + (cc ? cc[0] : 1.0) + (nr ? 1.0 : 0.0);
+    } else if (which == 13) {
+      double lp[4];
+      const bool in = dt::lane_pos_q(M, g, lane & 3, x, z, c, s, lp);
+      acc = acc + (in ? lp[0] + lp[3] : 1.0);
+    } else if (which == 14) {
+      bool nr = false;
+      acc = acc + dt::bezier_closest_q(cv, lane & 3, x, z, nr) + (nr ? 1.0 : 0.0);
+    } else if (which == 15) {
+      double lp[4];
+      dt::lane_pose_at<true>(g, cv, 0.3 + acc * 1e-300, x, z, c, s, lp);
+      acc = acc + lp[0] + lp[3];
+    } else if (which == 16) {
+      acc = acc + (dt::valid_pose_q(M, g, lane & 3, x, z, c, s, 1.0) ? 1.0 : 2.0);
+    } else if (which == 18) {
+      acc = acc + sqrt(x * x + 1.0);
+    } else if (which == 19) {
+      acc = acc + 1.0 / (x + 2.0);
+    } else if (which == 20) {
+      double v = x;
+#pragma unroll
+      for (int j = 0; j < 7; ++j) v = v * 1.0000001 + 1e-3;
+      acc = acc + v;
+    } else if (which == 21) {
+      const double tm = 0.3 + acc * 1e-300;
+      const double u = 1.0 - tm;
+      const double a0 = 3.0 * (u * u), a1 = 6.0 * u * tm, a2 = 3.0 * (tm * tm);
+      double tx = a0 * cv[8], tz = a0 * cv[9];
+      tx = tx + a1 * cv[10];
+      tz = tz + a1 * cv[11];
+      tx = tx + a2 * cv[12];
+      tz = tz + a2 * cv[13];
+      const double nn = sqrt(tx * tx + tz * tz);
+      acc = acc + tx / nn + tz / nn;
+    } else if (which == 22) {
+      double bx, bz;
+      dt::bez_xz(cv, 0.3 + acc * 1e-300, bx, bz);
+      acc = acc + bx + bz;
+    } else if (which == 23) {
+      acc = acc + acos(x * 1e-3);
+    } else if (which == 17) {
+      double lp[4];
+      dt::lane_pose_at<false>(g, cv, 0.3 + acc * 1e-300, x, z, c, s, lp);
+      acc = acc + lp[0] + lp[2];
     }
     x = x + acc * 1e-300;
   }

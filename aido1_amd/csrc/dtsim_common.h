@@ -556,6 +556,7 @@ __device__ inline bool lane_pos(const MapLds& M, const Geo& g, double x, double 
   return true;
 }
 
+
 // closest_curve with the fast tile lookup and the packed tile word: the
 // headings of a tile's first two curves are read together (one LDS round
 // trip), the rest (intersection tiles) in the loop

@@ -181,6 +181,29 @@ class VecEnv:
                                          self._stream()), 'dt_step_many')
         return out
 
+    def bind_step_many(self, actions, out):
+        """A zero-argument callable that launches step_many_into(actions, out)
+        on the current stream with its ctypes arguments built once (checked
+        here): the launch then costs one foreign call, for timed loops.  The
+        callable returns dt_step_many's status (0 = DT_OK)."""
+        k = int(actions.shape[0]) if actions.dim() == 3 else 0
+        if actions.dtype != torch.float32 or not actions.is_contiguous() or \
+                actions.device != self.device or k < 1 or tuple(actions.shape[1:]) != (self.n, 2):
+            raise ValueError('actions must be a contiguous float32 [k,%d,2] tensor on %s'
+                             % (self.n, self.device))
+        if out.reward.numel() != k * self.n or (out.obs is not None and
+                                                out.obs.shape[0] != k * self.n):
+            raise ValueError('out must be a StepOutput of k * n = %d entries' % (k * self.n))
+        fn = self._L.dt_step_many
+        args = (self._h, k, _ptr(actions), _ptr(out.reward), _ptr(out.reward_mod),
+                _ptr(out.done), _ptr(out.obs), self._stream())
+        keep = (actions, out)
+
+        def launch():
+            keep  # noqa: B018 (the tensors stay alive with the callable)
+            return fn(*args)
+        return launch
+
     def capture(self, actions, out=None, render=None):
         """StepGraph of len(actions) consecutive decisions (see StepGraph)."""
         return StepGraph(self, actions, out or self.out, render)

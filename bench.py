@@ -15,9 +15,11 @@ resident in HBM before the timed region.
   python bench.py [--gpus N --steps K --warmup W] [--config lane|render|actor|train]
 
 Timed region (config 2): the K decisions are split into equal launches of
-dt_step_many (at most --many decisions each) and the launches are captured in
-ONE HIP graph before the timed region, so the wall clock is the kernels' time
-and not Python's launch cost.  After it, outside the timed region:
+dt_step_many (at most --many decisions each); each launch is one prebound
+foreign call (VecEnv.bind_step_many: arguments built and checked before the
+timed region), so the wall clock is the kernels' time plus one launch and one
+synchronize, not Python's per-call cost (--graph: one captured HIP graph
+instead, which costs more per replay on ROCm: tools/launch_probe.py).  After it, outside the timed region:
   * parity: the C oracle (oracle/dtsim_oracle.c, test infrastructure) re-runs
     every env of this rank from the saved start state through the same actions;
     reward/reward_mod/obs/done of every decision and the end pose are compared
@@ -93,8 +95,9 @@ def parse(argv=None):
     p.add_argument('--many', type=int, default=20,
                    help='lane config: most decisions per dt_step_many launch; the K timed '
                         'decisions are split into ceil(K / many) equal launches')
-    p.add_argument('--no-graph', action='store_true',
-                   help='lane config: launch the timed dt_step_many calls eagerly')
+    p.add_argument('--graph', action='store_true',
+                   help='lane config: replay the timed launches as one captured HIP graph '
+                        '(default: prebound eager dt_step_many calls)')
     p.add_argument('--no-parity', action='store_true', help='skip the oracle parity pass')
     p.add_argument('--no-render', action='store_true', help='skip the render sub-record')
     p.add_argument('--render-steps', type=int, default=0,
@@ -345,29 +348,32 @@ def bench_lane(args, ctx):
     out = StepOutput(K * n, dev, lanepos=False, tile=False)
     plan = [(W + a, W + b, _Slice(out, a, b, n)) for a, b in _bounds(sizes)]
 
-    def run_timed():
-        for a, b, o in plan:
-            env.step_many_into(actions[a:b], o)
     graph = None
-    if not args.no_graph:
+    if args.graph:
+        # the launches as one captured HIP graph (capture only: nothing runs here)
         graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(graph):     # capture only: nothing runs here
-            run_timed()
+        with torch.cuda.graph(graph):
+            for a, b, o in plan:
+                env.step_many_into(actions[a:b], o)
         ctx.sync()
+        calls = [graph.replay]
+    else:
+        # prebound dt_step_many calls: one foreign call per launch, arguments
+        # built and checked before the timed region
+        calls = [env.bind_step_many(actions[a:b], o) for a, b, o in plan]
     env.stats(reset=True)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     ctx.barrier()
     ctx.sync()
+    e0.record()          # enqueued ahead of the launches; brackets them on the stream
     t0 = time.perf_counter()
-    e0.record()
-    if graph is not None:
-        graph.replay()
-    else:
-        run_timed()
+    rcs = [f() for f in calls]
     e1.record()
     ctx.sync()
     ctx.barrier()
     elapsed = time.perf_counter() - t0
+    if any(rcs):
+        raise RuntimeError('dt_step_many failed in the timed region: %s' % rcs)
     st = env.stats()
     env.check()
     launches_ms = e0.elapsed_time(e1)
@@ -418,7 +424,7 @@ def bench_lane(args, ctx):
                 'auto_reset': True, 'global_envs': n * ctx.world,
                 'launch': 'dt_step_many: %d launches of %s decisions%s' % (
                     nl, '/'.join(str(s) for s in sorted(set(sizes), reverse=True)),
-                    ', one HIP graph' if graph is not None else ', eager'),
+                    ', one HIP graph' if graph is not None else ', prebound eager calls'),
                 'parallelism': 'env shards (%d x %d), no collective' % (ctx.world, n)},
             'counts': {'env_steps': sim_steps, 'decisions': decisions, 'resets': resets,
                        'elapsed_s': tmax},

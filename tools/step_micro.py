@@ -13,7 +13,9 @@ from aido1_amd.vec_env import VecEnv  # noqa: E402
 
 NAMES = ['lane_pos', 'valid_pose', 'sincos', 'bezier_closest', 'closest_curve', 'tile_of',
          'lane_pose_at', 'drivable', 'lane_pos_lean', 'valid_pose_lean', 'bezier_closest_fast',
-         'tile_of_fast', 'closest_curve_fast']
+         'tile_of_fast', 'closest_curve_fast', 'lane_pos_q', 'bezier_closest_q',
+         'lane_pose_at<true>', 'valid_pose_q', 'lane_pose_at<false> (t varies)', 'sqrt chain',
+         'div chain', '14 dep fp64 ops', 'tangent+sqrt+2div', 'bez_xz', 'acos']
 
 
 def main():
