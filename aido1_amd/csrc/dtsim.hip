@@ -801,6 +801,10 @@ struct FanX {  // [parity][env][step], rows padded to 4 for wide LDS reads
   uint8_t inl[2][kFanEnvs][4], vp[2][kFanEnvs][4];
 };
 
+// kLean: the common configuration as compile-time facts (wheel-velocity
+// actions clipped to [-1, 1], the nominal speed in the reward, auto-reset, no
+// collidable objects); the generic instantiation reads them from StepCfg / the map
+template <bool kLean>
 __global__ __launch_bounds__(kFanBlock) __attribute__((amdgpu_waves_per_eu(2, 2))) void step_fan_kernel(dt::State st, dt::MapDev md,
                                                              dt::Geo g, StepCfg sc, int n,
                                                              uint32_t env_base, int k,
@@ -887,6 +891,11 @@ __global__ __launch_bounds__(kFanBlock) __attribute__((amdgpu_waves_per_eu(2, 2)
   unsigned nsim_t = 0, act_t = 0, resets_t = 0, dones_t = 0;
   double rp[dt::kSlotRec] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 1.0};
   const int R = sc.repeat;
+  const int act_mode = kLean ? DT_ACTION_WHEELS : sc.action_mode;
+  const bool clip = kLean ? true : sc.clip != 0;
+  const bool speed_measured = kLean ? false : sc.speed_measured != 0;
+  const bool auto_reset = kLean ? true : sc.auto_reset != 0;
+  const bool objs = kLean ? false : M.n_obj != 0;
   for (int d = 0; d < k; ++d) {
     const int par = d & 1;
     const float2 a = sact[d * kFanEnvs + le];
@@ -896,8 +905,8 @@ __global__ __launch_bounds__(kFanBlock) __attribute__((amdgpu_waves_per_eu(2, 2)
 
     // ---- the pose chain (every wave) ----
     double vl, vr;
-    map_action(sc.action_mode, a.x, a.y, vl, vr);
-    if (sc.clip) {
+    map_action(act_mode, a.x, a.y, vl, vr);
+    if (clip) {
       vl = vl < -1.0 ? -1.0 : (vl > 1.0 ? 1.0 : vl);
       vr = vr < -1.0 ? -1.0 : (vr > 1.0 ? 1.0 : vr);
     }
@@ -955,7 +964,7 @@ __global__ __launch_bounds__(kFanBlock) __attribute__((amdgpu_waves_per_eu(2, 2)
         pz[r] = cz + ndz;
       }
     }
-    if (sc.speed_measured) {
+    if (speed_measured) {
 #pragma unroll
       for (int r = 1; r <= kFanSteps; ++r) {
         const double a1d = px[r] - px[r - 1], a3d = pz[r] - pz[r - 1];
@@ -968,10 +977,10 @@ __global__ __launch_bounds__(kFanBlock) __attribute__((amdgpu_waves_per_eu(2, 2)
     if (wave == 0) {
 #pragma unroll
       for (int r = 1; r <= kFanSteps; ++r) {
-        const bool vp = dt::valid_pose_q(M, g, q, px[r], pz[r], pc[r], ps[r], 1.0);
-        const double pen = M.n_obj ? dt::proximity_penalty(M, g, px[r] + g.off * pc[r],
-                                                           pz[r] + g.off * (-ps[r]))
-                                   : 0.0;
+        const bool vp = dt::valid_pose_q<!kLean>(M, g, q, px[r], pz[r], pc[r], ps[r], 1.0);
+        const double pen = objs ? dt::proximity_penalty(M, g, px[r] + g.off * pc[r],
+                                                        pz[r] + g.off * (-ps[r]))
+                                : 0.0;
         if (lead) {
           X.vp[par][le][r - 1] = vp ? 1 : 0;
           X.pen[par][le][r - 1] = pen;
@@ -1023,7 +1032,7 @@ __global__ __launch_bounds__(kFanBlock) __attribute__((amdgpu_waves_per_eu(2, 2)
       const uint32_t sc1 = step_count + 1u;
       const bool vp = xv[r - 1];
       const bool cap = sc1 >= sc.max_steps;
-      const double sp = sc.speed_measured ? spd[r] : kR;
+      const double sp = speed_measured ? spd[r] : kR;
       const double pen = xp[r - 1];
       const double ad = fabs(xd[r - 1]);
       const double rin = ((1.0 * sp) * xo[r - 1] + (-10.0) * ad) + 40.0 * pen;
@@ -1067,7 +1076,7 @@ __global__ __launch_bounds__(kFanBlock) __attribute__((amdgpu_waves_per_eu(2, 2)
 
     PSTAMPT(d, 4);
     // ---- auto-reset ----
-    const bool want_reset = active && dn && sc.auto_reset;
+    const bool want_reset = active && dn && auto_reset;
     bool ok = slot_ready && ((failed >> rel) & 1u) == 0u;
     if (want_reset && slot_ready) {
       const int sl = (int)(key % (uint32_t)dt::kSlots);
@@ -1565,10 +1574,13 @@ int dt_step_many(dt_handle* h, int32_t k, const float* actions, double* reward,
     const size_t slots = (size_t)dt::kSlots * dt::kSlotRec * kFanEnvs * sizeof(double);
     // runs of more than kFanMaxK decisions: consecutive launches (the state,
     // counters and spawn window carry over exactly as between calls)
+    const bool lean = h->sc.action_mode == DT_ACTION_WHEELS && h->sc.clip && !h->sc.speed_measured &&
+                      h->sc.auto_reset && h->map.n_obj == 0;
     for (int d0 = 0; d0 < k; d0 += kFanMaxK) {
       const int kk = k - d0 < kFanMaxK ? k - d0 : kFanMaxK;
       const size_t o = (size_t)d0 * h->n;
-      hipLaunchKernelGGL(step_fan_kernel, dim3(gs + rb), dim3(kFanBlock),
+      hipLaunchKernelGGL(lean ? step_fan_kernel<true> : step_fan_kernel<false>, dim3(gs + rb),
+                         dim3(kFanBlock),
                          off + slots + (size_t)kk * kFanEnvs * sizeof(float2), s, h->st, h->map,
                          h->geo,
                          h->sc, h->n, h->env_base, kk, (const float2*)actions + o, reward + o,

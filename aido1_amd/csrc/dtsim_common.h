@@ -651,13 +651,15 @@ __device__ inline bool probe_q(const MapLds& M, const Geo& g, int q, double x, d
   return drivable_fast(M, g, tx, tz, near);
 }
 
-// _valid_pose at one pose over a quad, identical to valid_pose
+// _valid_pose at one pose over a quad, identical to valid_pose (kObj false:
+// the caller guarantees a map without collidable objects)
+template <bool kObj = true>
 __device__ inline bool valid_pose_q(const MapLds& M, const Geo& g, int q, double x, double z,
                                     double c, double s, double safety) {
   bool near = false;
   bool ok = qall(probe_q(M, g, q, x, z, c, s, safety, near));
   if (__builtin_expect(qany(near), 0)) return valid_pose(M, g, x, z, c, s, safety);
-  if (M.n_obj && ok) ok = !collide(M, g, x + g.off * c, z + g.off * (-s), c, s);
+  if (kObj && M.n_obj && ok) ok = !collide(M, g, x + g.off * c, z + g.off * (-s), c, s);
   return ok;
 }
 
@@ -673,6 +675,9 @@ __device__ inline double bezier_closest_q(const double* cv, int q, double x, dou
   constexpr double kTol = 8.0 * 2.220446049250313e-16;
   double tb = 0.0, tt = 1.0;
   double db = dist2_pt(cv[0], cv[1], x, z), dtp = dist2_pt(cv[6], cv[7], x, z);
+  // lane constants (lane 0 takes m1, whose side is known per round)
+  const bool q0 = q == 0;
+  const double fl = (double)(((0x3010200u >> (8 * q)) & 0xFFu)) * 0.25;   // 1/2, 1/4, 3/4
 #pragma unroll
   for (int n = 8; n > 0; n -= 3) {
     // level n (comparison known)
@@ -682,7 +687,12 @@ __device__ inline double bezier_closest_q(const double* cv, int q, double x, dou
     const double lo1 = l1 ? tb : m1, hi1 = l1 ? m1 : tt;
     const double m2 = (lo1 + hi1) * 0.5;
     const double m3a = (lo1 + m2) * 0.5, m3b = (m2 + hi1) * 0.5;
-    const double tq = q == 0 ? m1 : (q == 1 ? m2 : (q == 2 ? m3a : m3b));
+    // this lane's point, lo1 + f * (hi1 - lo1) with f = {m1's side, 1/2, 1/4,
+    // 3/4}: every t here is a dyadic rational with at most 10 significant
+    // bits, so the product and sum are exact and equal the midpoints above
+    // bit for bit (no per-lane branch)
+    const double fq = q0 ? (l1 ? 1.0 : 0.0) : fl;
+    const double tq = lo1 + fq * (hi1 - lo1);
     const double dq = dist2_to(cv, tq, x, z);
     const double dm1 = qget<0>(dq);
     // level n - 1
