@@ -1,0 +1,290 @@
+"""The single-process DDPG of duckietown_rl on the GPU:
+``CriticCNN``, ``DDPG`` (predict / train / save / load) and the
+random-eviction ``ReplayBuffer``, the API of
+
+  * duckietown_rl/ddpg.py:16-62   ActorCNN (aido1_amd.actor.ActorCNN, same names)
+  * duckietown_rl/ddpg.py:65-99   CriticCNN
+  * duckietown_rl/ddpg.py:102-195 DDPG
+  * duckietown_rl/utils.py:18-57  ReplayBuffer
+
+so duckietown_rl's training script drops in unchanged.  What changes is where
+the data lives: the replay storage is preallocated device memory (frames never
+leave HBM), ``sample`` gathers a batch on the device, and ``train`` runs the
+whole iteration there -- optionally as one captured HIP graph per iteration
+(``graph=True``), since a batch-64 iteration is a few hundred small kernels
+and launch-bound otherwise.
+
+Semantics kept exactly (tests/test_ddpg.py pins them against the reference's
+own DDPG.train run in float32 and float64, tests/golden/ddpg_single*.json):
+  * eviction: a full buffer removes a uniformly drawn list position with
+    Python's ``random.randrange`` and appends the new transition; sampling
+    draws list positions with ``np.random.randint`` -- the same global RNG
+    streams the reference consumes, in the same order;
+  * ``done = 1 - done``, target ``reward + (done * discount * Q'(s', pi'(s')))``,
+    MSE critic loss, actor loss ``-Q(s, pi(s)).mean()``, Adam (actor lr 1e-4,
+    critic torch's default 1e-3), soft updates ``tau * p + (1 - tau) * t``,
+    critic first;
+  * every network in train mode (BatchNorm on batch statistics, dropout live),
+    as the reference never calls .eval().
+"""
+import os
+import random
+
+import numpy as np
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from aido1_amd.actor import FLAT, ActorCNN
+
+
+class CriticCNN(nn.Module):
+    """duckietown_rl/ddpg.py:65-99 (same attribute names, so the reference's
+    ``{name}_critic.pth`` state dicts load)."""
+
+    def __init__(self, action_dim=2):
+        super().__init__()
+        self.lr = nn.LeakyReLU()
+        self.conv1 = nn.Conv2d(3, 32, 8, stride=2)
+        self.conv2 = nn.Conv2d(32, 32, 4, stride=2)
+        self.conv3 = nn.Conv2d(32, 32, 4, stride=2)
+        self.conv4 = nn.Conv2d(32, 32, 4, stride=1)
+        self.bn1 = nn.BatchNorm2d(32)
+        self.bn2 = nn.BatchNorm2d(32)
+        self.bn3 = nn.BatchNorm2d(32)
+        self.bn4 = nn.BatchNorm2d(32)
+        self.dropout = nn.Dropout(.5)   # constructed (and unused) as in the reference
+        self.lin1 = nn.Linear(FLAT, 256)
+        self.lin2 = nn.Linear(256 + action_dim, 128)
+        self.lin3 = nn.Linear(128, 1)
+
+    def forward(self, states, actions):
+        x = self.bn1(self.lr(self.conv1(states)))
+        x = self.bn2(self.lr(self.conv2(x)))
+        x = self.bn3(self.lr(self.conv3(x)))
+        x = self.bn4(self.lr(self.conv4(x)))
+        x = x.flatten(1)
+        x = self.lr(self.lin1(x))
+        x = self.lr(self.lin2(torch.cat([x, actions], 1)))
+        return self.lin3(x)
+
+
+def _as_tensor(x, device, dtype):
+    if torch.is_tensor(x):
+        return x.to(device=device, dtype=dtype)
+    return torch.as_tensor(np.asarray(x), device=device).to(dtype)
+
+
+class ReplayBuffer:
+    """duckietown_rl/utils.py:18-57 with device storage.
+
+    The reference keeps a Python list of tuples; a full buffer pops a random
+    list position and appends.  Here the list holds storage slot numbers
+    (``_order``): the popped position's slot is reused for the appended
+    transition, so ``_order[i]`` is the slot of the reference's
+    ``storage[i]`` at every point, and ``sample`` reads the same transitions
+    for the same ``np.random.randint`` draws."""
+
+    def __init__(self, max_size, device=None, dtype=torch.float32):
+        self.max_size = int(max_size)
+        self.device = torch.device(device) if device is not None else (
+            torch.device('cuda', torch.cuda.current_device()) if torch.cuda.is_available()
+            else torch.device('cpu'))
+        self.dtype = dtype
+        self._order = []
+        self._s = None
+
+    def __len__(self):
+        return len(self._order)
+
+    @property
+    def storage(self):
+        """The reference's ``storage`` view: a list of (state, next_state,
+        action, reward, done) device tensors, list order."""
+        return [tuple(t[j] for t in self._s) for j in self._order]
+
+    def _alloc(self, state, action):
+        shape = tuple(state.shape)
+        n = self.max_size
+        kw = dict(device=self.device, dtype=self.dtype)
+        self._s = (torch.zeros((n,) + shape, **kw), torch.zeros((n,) + shape, **kw),
+                   torch.zeros((n,) + tuple(action.shape), **kw), torch.zeros(n, **kw),
+                   torch.zeros(n, **kw))
+
+    def _slot(self):
+        if len(self._order) < self.max_size:
+            slot = len(self._order)
+        else:
+            # "Remove random element in the memory before adding a new one"
+            slot = self._order.pop(random.randrange(len(self._order)))
+        self._order.append(slot)
+        return slot
+
+    def add(self, state, next_state, action, reward, done):
+        state = _as_tensor(state, self.device, self.dtype)
+        action = _as_tensor(action, self.device, self.dtype)
+        if self._s is None:
+            self._alloc(state, action)
+        slot = self._slot()
+        s, ns, a, r, d = self._s
+        s[slot] = state
+        ns[slot] = _as_tensor(next_state, self.device, self.dtype)
+        a[slot] = action
+        r[slot] = float(reward)
+        d[slot] = float(done)
+
+    def add_batch(self, states, next_states, actions, rewards, dones):
+        """len(states) consecutive ``add`` calls (the same eviction draws, in
+        order) with one device scatter per field; a slot written twice keeps
+        the later transition, as sequential adds would."""
+        states = _as_tensor(states, self.device, self.dtype)
+        actions = _as_tensor(actions, self.device, self.dtype)
+        if self._s is None:
+            self._alloc(states[0], actions[0])
+        slots = [self._slot() for _ in range(states.shape[0])]
+        keep = {}
+        for i, sl in enumerate(slots):
+            keep[sl] = i
+        src = torch.as_tensor(list(keep.values()), device=self.device)
+        dst = torch.as_tensor(list(keep.keys()), device=self.device)
+        s, ns, a, r, d = self._s
+        s.index_copy_(0, dst, states.index_select(0, src))
+        ns.index_copy_(0, dst, _as_tensor(next_states, self.device, self.dtype).index_select(0, src))
+        a.index_copy_(0, dst, actions.index_select(0, src))
+        r.index_copy_(0, dst, _as_tensor(rewards, self.device, self.dtype).reshape(-1)[src])
+        d.index_copy_(0, dst, _as_tensor(dones, self.device, self.dtype).reshape(-1)[src])
+
+    def sample_slots(self, batch_size=100):
+        """The storage slots of ``np.random.randint(0, len, size=batch_size)``."""
+        ind = np.random.randint(0, len(self._order), size=batch_size)
+        order = self._order
+        return [order[i] for i in ind]
+
+    def gather(self, slots, flat=True):
+        idx = slots if torch.is_tensor(slots) else torch.as_tensor(slots, device=self.device)
+        s, ns, a, r, d = self._s
+        st, nx = s.index_select(0, idx), ns.index_select(0, idx)
+        if flat:
+            st, nx = st.flatten(1), nx.flatten(1)
+        return {'state': st, 'next_state': nx, 'action': a.index_select(0, idx),
+                'reward': r.index_select(0, idx).reshape(-1, 1),
+                'done': d.index_select(0, idx).reshape(-1, 1)}
+
+    def sample(self, batch_size=100, flat=True):
+        return self.gather(self.sample_slots(batch_size), flat)
+
+
+def soft_update_(target, source, tau):
+    """``target = tau * param + (1 - tau) * target`` for every parameter
+    (duckietown_rl/ddpg.py:178-182), two products rounded separately."""
+    tp = [p.data for p in target.parameters()]
+    sp = [p.data for p in source.parameters()]
+    a = torch._foreach_mul(sp, tau)
+    b = torch._foreach_mul(tp, 1 - tau)
+    torch._foreach_add_(a, b)
+    torch._foreach_copy_(tp, a)
+
+
+class DDPG:
+    """duckietown_rl/ddpg.py:102-195 on one device.  ``net_type`` 'cnn' only
+    (the dense variant's modules are not in the reference tree).
+
+    graph=True (GPU): from the third ``train`` iteration on, one iteration is
+    a captured HIP graph replay (static batch buffers filled by a device
+    gather from the sampled slots; Adam in its capturable form)."""
+
+    def __init__(self, state_dim=None, action_dim=2, max_action=1.0, net_type='cnn', device=None,
+                 dtype=torch.float32, graph=False, log=print):
+        if net_type != 'cnn':
+            raise NotImplementedError("net_type 'dense' (ActorDense / CriticDense are not in "
+                                      'the reference tree)')
+        self.state_dim = state_dim
+        self.flat = False
+        self.device = torch.device(device) if device is not None else (
+            torch.device('cuda', torch.cuda.current_device()) if torch.cuda.is_available()
+            else torch.device('cpu'))
+        self.dtype = dtype
+        self.actor = ActorCNN(action_dim, max_action).to(self.device, dtype)
+        self.actor_target = ActorCNN(action_dim, max_action).to(self.device, dtype)
+        self.actor_target.load_state_dict(self.actor.state_dict())
+        self.critic = CriticCNN(action_dim).to(self.device, dtype)
+        self.critic_target = CriticCNN(action_dim).to(self.device, dtype)
+        self.critic_target.load_state_dict(self.critic.state_dict())
+        self.graph = bool(graph) and self.device.type == 'cuda'
+        cap = dict(capturable=True, foreach=True) if self.graph else {}
+        self.actor_optimizer = torch.optim.Adam(self.actor.parameters(), lr=1e-4, **cap)
+        self.critic_optimizer = torch.optim.Adam(self.critic.parameters(), **cap)
+        self.log = log
+        self._iters = 0
+        self._g = None
+        self._slots = None
+        self._key = None
+
+    def predict(self, state):
+        assert state.shape[0] == 3
+        x = _as_tensor(state, self.device, self.dtype).unsqueeze(0)
+        return self.actor(x).detach().cpu().numpy().flatten()
+
+    # ---- one iteration (duckietown_rl/ddpg.py:144-182) ----------------------------
+    def _iteration(self, b, discount, tau):
+        state, action, next_state = b['state'], b['action'], b['next_state']
+        done = 1 - b['done']
+        reward = b['reward']
+        target_Q = self.critic_target(next_state, self.actor_target(next_state))
+        target_Q = reward + (done * discount * target_Q).detach()
+        current_Q = self.critic(state, action)
+        critic_loss = F.mse_loss(current_Q, target_Q)
+        self.critic_optimizer.zero_grad(set_to_none=not self.graph)
+        critic_loss.backward()
+        self.critic_optimizer.step()
+        actor_loss = -self.critic(state, self.actor(state)).mean()
+        self.actor_optimizer.zero_grad(set_to_none=not self.graph)
+        actor_loss.backward()
+        self.actor_optimizer.step()
+        with torch.no_grad():
+            soft_update_(self.critic_target, self.critic, tau)
+            soft_update_(self.actor_target, self.actor, tau)
+        self.critic_loss, self.actor_loss = critic_loss.detach(), actor_loss.detach()
+
+    def _capture(self, replay_buffer, batch_size, discount, tau):
+        """Record one iteration as a HIP graph.  Capture only records (no kernel
+        runs, so no parameter moves); the two eager iterations before it did
+        the lazy work (MIOpen find, Adam state, grads allocated in place)."""
+        slots = torch.zeros(batch_size, dtype=torch.int64, device=self.device)
+        torch.cuda.synchronize(self.device)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            self._iteration(replay_buffer.gather(slots, self.flat), discount, tau)
+        self._g, self._slots = g, slots
+        self._key = (batch_size, discount, tau, id(replay_buffer), replay_buffer._s[0].data_ptr())
+
+    def train(self, replay_buffer, iterations, batch_size=64, discount=0.99, tau=0.001):
+        """duckietown_rl/ddpg.py:141-183.  Each iteration draws its batch with
+        np.random.randint (sample_slots) exactly as the reference does."""
+        for it in range(iterations):
+            if it % 10 == 0 and self.log is not None:
+                self.log('Train iteration:', it)
+            slots = replay_buffer.sample_slots(batch_size)
+            if self.graph and self._iters >= 2:
+                key = (batch_size, discount, tau, id(replay_buffer),
+                       replay_buffer._s[0].data_ptr())
+                if self._g is None or self._key != key:
+                    self._capture(replay_buffer, batch_size, discount, tau)
+                self._slots.copy_(torch.as_tensor(slots, dtype=torch.int64))
+                self._g.replay()
+            else:
+                self._iteration(replay_buffer.gather(slots, self.flat), discount, tau)
+            self._iters += 1
+
+    def save(self, filename, directory):
+        torch.save(self.actor.state_dict(), os.path.join(directory, '%s_actor.pth' % filename))
+        torch.save(self.critic.state_dict(), os.path.join(directory, '%s_critic.pth' % filename))
+
+    def load(self, filename, directory):
+        self.actor.load_state_dict(torch.load(os.path.join(directory, '%s_actor.pth' % filename),
+                                              map_location=self.device, weights_only=True))
+        self.critic.load_state_dict(torch.load(os.path.join(directory, '%s_critic.pth' % filename),
+                                               map_location=self.device, weights_only=True))
+
+    def close(self):
+        pass

@@ -447,6 +447,62 @@ def gen_ddpg_update(double=False):
     dump('ddpg_update_f64.json' if double else 'ddpg_update.json', out)
 
 
+def gen_ddpg_single(double=False):
+    """duckietown_rl/ddpg.py DDPG.train over duckietown_rl/utils.py ReplayBuffer:
+    20 formula transitions added to a max_size-12 buffer (8 random-eviction
+    pops), then three train iterations of batch 8, one call each so the
+    parameters are summarised after every iteration.  Seeds: random 7, numpy 11.
+    Dropout p=0 (deterministic).  double=True: the module's FloatTensor makes
+    float64 and the nets are .double() (float32 drifts after the first Adam step,
+    as for gen_ddpg_update)."""
+    import torch
+    import duckietown_rl.ddpg as dd
+    from duckietown_rl.utils import ReplayBuffer
+    sys.path.insert(0, HERE)
+    from formulas import formula_batch, formula_state_dict, param_summary
+    if double:
+        shim = types.SimpleNamespace(**{k: getattr(torch, k) for k in dir(torch)
+                                        if not k.startswith('__')})
+        shim.FloatTensor = lambda a: torch.from_numpy(np.asarray(a, np.float64))
+        dd.torch = shim
+    try:
+        torch.manual_seed(0)
+        agent = dd.DDPG(None, 2, 1.0, 'cnn')
+        for net, tgt in ((agent.actor, agent.actor_target), (agent.critic, agent.critic_target)):
+            sd = formula_state_dict(net.state_dict())
+            net.load_state_dict(sd)
+            tgt.load_state_dict(sd)
+        for net in (agent.actor, agent.actor_target):
+            net.dropout.p = 0.0
+        if double:
+            for net in (agent.actor, agent.actor_target, agent.critic, agent.critic_target):
+                net.double()
+            agent.actor_optimizer = torch.optim.Adam(agent.actor.parameters(), lr=1e-4)
+            agent.critic_optimizer = torch.optim.Adam(agent.critic.parameters())
+        obs, act, rew, nxt, done = formula_batch(20)
+        dt = np.float64 if double else np.float32
+        random.seed(7)
+        np.random.seed(11)
+        rb = ReplayBuffer(12)
+        for i in range(20):
+            # 0-d arrays: the reference's np.array(x, copy=False) refuses Python
+            # floats under numpy 2 (same values as the training script's floats)
+            rb.add(obs[i].astype(dt), nxt[i].astype(dt), act[i].astype(dt),
+                   np.asarray(float(rew[i]), dt), np.asarray(float(done[i]), dt))
+        order = [int(np.argmin(np.abs(rew - s[3]))) for s in rb.storage]
+        out = {'storage_order': order, 'iterations': []}
+        for _ in range(3):
+            agent.train(rb, 1, batch_size=8)
+            out['iterations'].append({name: param_summary(net) for name, net in (
+                ('actor', agent.actor), ('critic', agent.critic),
+                ('actor_target', agent.actor_target), ('critic_target', agent.critic_target))})
+        out['numpy_after'] = int(np.random.randint(0, 1 << 30))
+        out['random_after'] = random.randrange(1 << 30)
+    finally:
+        dd.torch = torch
+    dump('ddpg_single_f64.json' if double else 'ddpg_single.json', out)
+
+
 def gen_config_keys():
     """The config.json keys the env path reads (wrapper section, actor head, the
     explorer's noise/epsilon keys) — a data extract, not the file."""
@@ -488,6 +544,8 @@ def main():
     gen_actor()
     gen_ddpg_update()
     gen_ddpg_update(double=True)
+    gen_ddpg_single()
+    gen_ddpg_single(double=True)
 
 
 if __name__ == '__main__':

@@ -1,0 +1,168 @@
+"""Single-process DDPG (aido1_amd/ddpg.py) against the reference's own
+duckietown_rl DDPG.train over its random-eviction ReplayBuffer
+(duckietown_rl/ddpg.py:141-183, duckietown_rl/utils.py:18-57).
+
+tests/golden/ddpg_single{,_f64}.json (make_golden.gen_ddpg_single): 20 formula
+transitions into a max_size-12 buffer (random.seed 7, so 8 random-eviction
+pops), then three one-iteration train calls of batch 8 (np.random.seed 11),
+parameters of all four nets summarised after each, plus the next draw of both
+global RNGs (so the number of draws consumed is pinned too).  Dropout p=0.
+
+Tolerances (same reasoning as tests/test_trainer.py): float64 pins every
+iteration tightly (1e-8 relative; conv biases and the running means that carry
+them 1e-5 absolute, CPU reduction order); float32 pins iteration 1 to 1e-4 and
+bounds iterations 2-3 by Adam's +-lr per step on near-zero-gradient biases."""
+import random
+import sys
+
+import numpy as np
+import pytest
+import torch
+
+from conftest import GOLDEN, golden
+
+sys.path.insert(0, GOLDEN)
+from formulas import formula_batch, formula_state_dict, param_summary  # noqa: E402
+
+NETS = ('actor', 'critic', 'actor_target', 'critic_target')
+
+
+def run_single(device, dtype, graph=False, iterations=3):
+    from aido1_amd.ddpg import DDPG, ReplayBuffer
+    torch.manual_seed(0)
+    agent = DDPG(None, 2, 1.0, 'cnn', device=device, dtype=dtype, graph=graph, log=None)
+    for net, tgt in ((agent.actor, agent.actor_target), (agent.critic, agent.critic_target)):
+        sd = formula_state_dict(net.state_dict())
+        net.load_state_dict(sd)
+        tgt.load_state_dict(sd)
+    agent.actor.dropout.p = agent.actor_target.dropout.p = 0.0
+    obs, act, rew, nxt, done = formula_batch(20)
+    random.seed(7)
+    np.random.seed(11)
+    rb = ReplayBuffer(12, device=device, dtype=dtype)
+    for i in range(20):
+        rb.add(obs[i], nxt[i], act[i], float(rew[i]), float(done[i]))
+    order = [int(np.argmin(np.abs(rew - float(s[3])))) for s in rb.storage]
+    summaries = []
+    for _ in range(iterations):
+        agent.train(rb, 1, batch_size=8)
+        summaries.append({n: param_summary(getattr(agent, n)) for n in NETS})
+    rng_after = (int(np.random.randint(0, 1 << 30)), random.randrange(1 << 30))
+    return order, summaries, rng_after
+
+
+def check(fixture, order, summaries, rng_after, rtol, atol, later_rtol):
+    ref = golden(fixture)
+    assert order == ref['storage_order']
+    assert rng_after == (ref['numpy_after'], ref['random_after'])
+    for k, (got_it, ref_it) in enumerate(zip(summaries, ref['iterations'])):
+        tight = k == 0 or later_rtol == rtol
+        for name in NETS:
+            got, exp = got_it[name], ref_it[name]
+            assert list(got) == list(exp), name          # reference state_dict keys
+            for key, vals in exp.items():
+                g, r = np.asarray(got[key]), np.asarray(vals)
+                if tight:
+                    a_ = 1e-5 if (key.endswith(('.bias', 'running_mean')) and 'conv' in key
+                                  or 'running_mean' in key) else atol
+                    np.testing.assert_allclose(g, r, rtol=rtol, atol=a_,
+                                               err_msg='it%d %s.%s' % (k, name, key))
+                else:
+                    # float32 after the first Adam step: at most 2*lr per step
+                    # and iteration on any element (lr <= 1e-3), sums skipped
+                    bound = 2 * 1e-3 * (k + 1) + atol + later_rtol * np.abs(r[1:]).max()
+                    assert np.abs(g[1:] - r[1:]).max() <= bound, ('it%d' % k, name, key)
+
+
+def test_ddpg_single_f64_cpu():
+    check('ddpg_single_f64.json', *run_single('cpu', torch.float64), rtol=1e-8, atol=1e-9,
+          later_rtol=1e-8)
+
+
+def test_ddpg_single_f32_cpu():
+    check('ddpg_single.json', *run_single('cpu', torch.float32), rtol=1e-4, atol=1e-4,
+          later_rtol=0.05)
+
+
+def test_replay_buffer_eviction_and_sample():
+    """The slot list mirrors the reference list under pops; sample returns the
+    transitions at the reference's np.random.randint positions."""
+    from aido1_amd.ddpg import ReplayBuffer
+    random.seed(3)
+    np.random.seed(4)
+    rb = ReplayBuffer(5, device='cpu', dtype=torch.float64)
+    ref_list = []
+    rstate = random.getstate()
+    for i in range(17):
+        rb.add(np.full((3, 2, 2), i, np.float64), np.full((3, 2, 2), -i, np.float64),
+               np.array([i, i + .5]), float(i), float(i % 2))
+    random.setstate(rstate)
+    for i in range(17):
+        if len(ref_list) >= 5:
+            ref_list.pop(random.randrange(len(ref_list)))
+        ref_list.append(i)
+    assert [int(s[3]) for s in rb.storage] == ref_list
+    nstate = np.random.get_state()
+    b = rb.sample(6, flat=False)
+    np.random.set_state(nstate)
+    ind = np.random.randint(0, 5, size=6)
+    want = [ref_list[i] for i in ind]
+    assert b['reward'].reshape(-1).tolist() == want
+    assert b['state'].shape == (6, 3, 2, 2) and b['reward'].shape == (6, 1)
+    assert b['done'].reshape(-1).tolist() == [w % 2 for w in want]
+    assert torch.equal(b['next_state'][:, 0, 0, 0], -b['reward'].reshape(-1))
+    assert rb.sample(2, flat=True)['state'].shape == (2, 12)
+
+
+def test_add_batch_equals_sequential_adds():
+    from aido1_amd.ddpg import ReplayBuffer
+    x = np.arange(30, dtype=np.float64).reshape(10, 3)
+    a, b = (ReplayBuffer(4, device='cpu', dtype=torch.float64) for _ in range(2))
+    random.seed(5)
+    for i in range(10):
+        a.add(x[i], -x[i], x[i, :2], x[i, 0], 0.0)
+    random.seed(5)
+    b.add_batch(x, -x, x[:, :2], x[:, 0], np.zeros(10))
+    assert a._order == b._order
+    for ta, tb in zip(a._s, b._s):
+        assert torch.equal(ta, tb)
+
+
+def test_save_load_roundtrip(tmp_path):
+    from aido1_amd.ddpg import DDPG
+    a = DDPG(None, 2, 1.0, 'cnn', device='cpu', log=None)
+    a.save('m', str(tmp_path))
+    b = DDPG(None, 2, 1.0, 'cnn', device='cpu', log=None)
+    b.load('m', str(tmp_path))
+    for pa, pb in zip(a.critic.state_dict().values(), b.critic.state_dict().values()):
+        assert torch.equal(pa, pb)
+    s = np.random.default_rng(0).random((3, 120, 160)).astype(np.float32)
+    a.actor.eval(), b.actor.eval()
+    np.testing.assert_array_equal(a.predict(s), b.predict(s))
+
+
+@pytest.mark.gpu
+def test_gpu_ddpg_single_f64(gpu):
+    check('ddpg_single_f64.json', *run_single(gpu, torch.float64), rtol=1e-8, atol=1e-9,
+          later_rtol=1e-8)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize('graph', [False, True])
+def test_gpu_ddpg_single_f32(gpu, graph):
+    """graph=True: iteration 3 is a HIP-graph replay (iterations 1-2 eager)."""
+    check('ddpg_single.json', *run_single(gpu, torch.float32, graph=graph), rtol=1e-4,
+          atol=1e-4, later_rtol=0.05)
+
+
+@pytest.mark.gpu
+def test_gpu_ddpg_graph_matches_eager_f64(gpu):
+    """Graph replays of the float64 iteration land where eager iterations do."""
+    o1, s1, r1 = run_single(gpu, torch.float64, graph=False, iterations=5)
+    o2, s2, r2 = run_single(gpu, torch.float64, graph=True, iterations=5)
+    assert o1 == o2 and r1 == r2
+    for a, b in zip(s1, s2):
+        for name in NETS:
+            for key in a[name]:
+                np.testing.assert_allclose(b[name][key], a[name][key], rtol=1e-9, atol=1e-9,
+                                           err_msg=name + key)
