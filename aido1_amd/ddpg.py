@@ -36,6 +36,7 @@ import torch.nn as nn
 import torch.nn.functional as F
 
 from aido1_amd.actor import FLAT, ActorCNN
+from aido1_amd.optim import float64_steps
 
 
 class CriticCNN(nn.Module):
@@ -210,10 +211,20 @@ class DDPG:
         self.critic = CriticCNN(action_dim).to(self.device, dtype)
         self.critic_target = CriticCNN(action_dim).to(self.device, dtype)
         self.critic_target.load_state_dict(self.critic.state_dict())
+        # channels_last on the GPU, as trainer.py: MIOpen's NCHW train-mode
+        # BatchNorm loses float32 precision on large planes;
+        # its NHWC path is accurate
+        self._cl = self.device.type == 'cuda'
+        if self._cl:
+            for m in (self.actor, self.actor_target, self.critic, self.critic_target):
+                m.to(memory_format=torch.channels_last)
         self.graph = bool(graph) and self.device.type == 'cuda'
         cap = dict(capturable=True, foreach=True) if self.graph else {}
         self.actor_optimizer = torch.optim.Adam(self.actor.parameters(), lr=1e-4, **cap)
         self.critic_optimizer = torch.optim.Adam(self.critic.parameters(), **cap)
+        if self.graph:
+            float64_steps(self.actor_optimizer)
+            float64_steps(self.critic_optimizer)
         self.log = log
         self._iters = 0
         self._g = None
@@ -223,11 +234,16 @@ class DDPG:
     def predict(self, state):
         assert state.shape[0] == 3
         x = _as_tensor(state, self.device, self.dtype).unsqueeze(0)
+        if self._cl:
+            x = x.contiguous(memory_format=torch.channels_last)
         return self.actor(x).detach().cpu().numpy().flatten()
 
     # ---- one iteration (duckietown_rl/ddpg.py:144-182) ----------------------------
     def _iteration(self, b, discount, tau):
         state, action, next_state = b['state'], b['action'], b['next_state']
+        if self._cl and state.dim() == 4:
+            state = state.contiguous(memory_format=torch.channels_last)
+            next_state = next_state.contiguous(memory_format=torch.channels_last)
         done = 1 - b['done']
         reward = b['reward']
         target_Q = self.critic_target(next_state, self.actor_target(next_state))

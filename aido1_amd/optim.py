@@ -39,13 +39,33 @@ class AdamW(Optimizer):
         return loss
 
 
+def float64_steps(opt):
+    """Pre-create a capturable torch Adam's state with float64 `step` tensors.
+
+    torch keeps a capturable Adam's step count as a float32 device tensor, so
+    its bias corrections 1 - b^t are rounded to float32 (1 - 0.999 is off by
+    1.3e-5 relative, which moves every update by ~6e-6 relative), while plain
+    Adam computes them in float64 from a Python number.  With float64 steps
+    the graph path's update is plain Adam's to the last bits."""
+    for group in opt.param_groups:
+        for p in group['params']:
+            st = opt.state[p]
+            if not st:
+                st['step'] = torch.zeros((), dtype=torch.float64, device=p.device)
+                st['exp_avg'] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st['exp_avg_sq'] = torch.zeros_like(p, memory_format=torch.preserve_format)
+    return opt
+
+
 def make_optimizer(kind, params, capturable=False, device=None):
     """capturable: Adam with a device-tensor lr and step counters, so the step
-    can live inside a HIP graph (the lr is then set with fill_)."""
+    can live inside a HIP graph (the lr is then set with fill_; float64, so a
+    float64 update sees the lr the eager path would)."""
     if kind == 'adam':
         if capturable:
-            return torch.optim.Adam(params, lr=torch.tensor(0.0, device=device), capturable=True,
-                                    foreach=True)
+            return float64_steps(torch.optim.Adam(
+                params, lr=torch.tensor(0.0, dtype=torch.float64, device=device),
+                capturable=True, foreach=True))
         return torch.optim.Adam(params, lr=0.)
     if kind == 'adamw':
         return AdamW(params, lr=0., weight_decay=0.0001)
