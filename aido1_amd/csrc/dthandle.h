@@ -30,7 +30,7 @@ struct dt_handle {
   void* mark_buf = nullptr;   // float4 segments (x0, z0, x1, z1): yellow then white
   int32_t n_yellow = 0, n_white = 0;
   int32_t render_skip = 0;
-  int32_t render_threads = 768;  // DTSIM_RENDER_SKIP (diagnostic phase ablation)
+  int32_t render_threads = 768;  // DTSIM_RENDER_THREADS (tuning)
   std::string err;
 };
 

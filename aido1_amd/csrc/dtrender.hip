@@ -19,6 +19,32 @@ namespace {
 
 using namespace dr;
 
+#ifdef DTSIM_STAMPS
+// render_kernel per workgroup (diagnostics, tools/render_stamps.py): [0] real
+// time at entry, [1] at exit, [2] HW_ID, [3] XCC_ID, [4..15] shader clock at
+// the phase points RSTAMP(4..15) (thread 0, after the barrier that ends a phase)
+__device__ unsigned long long g_renstamps[4096 * 24];
+__device__ inline unsigned ren_hw_id() {
+  unsigned v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_HW_ID)" : "=s"(v));
+  return v;
+}
+__device__ inline unsigned ren_xcc_id() {
+  unsigned v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+  return v;
+}
+#define RENSTAMP(i, v)                                                              \
+  do {                                                                              \
+    if (threadIdx.x == 0 && e < 4096) g_renstamps[e * 24 + (i)] = (v); \
+  } while (0)
+#else
+#define RENSTAMP(i, v) \
+  do {                 \
+  } while (0)
+#endif
+#define RENT(i) RENSTAMP(i, __builtin_amdgcn_s_memtime())
+
 constexpr HsvTables kHsvHost = make_hsv_tables();
 __constant__ HsvTables c_hsv = make_hsv_tables();
 
@@ -182,6 +208,43 @@ __device__ inline void draw_line(lds_u8* img, int x0, int y0, int x1, int y1, ui
   }
 }
 
+// Pixels [xa, xb) of the line draw_line(x0, y0, x1, y1) would draw, the
+// same pixels in the same order: draw_line's minor coordinate after x major
+// steps is y(x) = floor((2 dy x + dx) / (2 dx)) (dx > 0; 0 for a single
+// point) and its decision variable D(x) = 2 dy (x + 1) - dx - 2 dx y(x), so a
+// part starts where the sequential walk would be (the quotient is exact: it is
+// at least 1 / (2 dx) from the next integer, far above float rounding).
+__device__ inline void draw_line_part(lds_u8* img, int x0, int y0, int x1, int y1, uint8_t col,
+                                      int part, int parts) {
+  int dx = x1 - x0, dy = y1 - y0;
+  const int xsign = dx > 0 ? 1 : -1, ysign = dy > 0 ? 1 : -1;
+  dx = dx < 0 ? -dx : dx;
+  dy = dy < 0 ? -dy : dy;
+  int xx, xy, yx, yy;
+  if (dx > dy) {
+    xx = xsign; xy = 0; yx = 0; yy = ysign;
+  } else {
+    const int t = dx; dx = dy; dy = t;
+    xx = 0; xy = ysign; yx = xsign; yy = 0;
+  }
+  const int n = dx + 1;
+  const int xa = (n * part) / parts, xb = (n * (part + 1)) / parts;
+  if (xa >= xb) return;
+  const int ya = dx > 0 ? (int)floorf((float)(2 * dy * xa + dx) / (float)(2 * dx)) : 0;
+  int D = 2 * dy * (xa + 1) - dx - 2 * dx * ya;
+  int px = x0 + xa * xx + ya * yx, py = y0 + xa * xy + ya * yy;
+  int ad = py * W + px;
+  const int amaj = xy * W + xx, amin = yy * W + yx;
+  for (int x = xa; x < xb; ++x) {
+    if ((unsigned)px < (unsigned)W && (unsigned)py < (unsigned)H) img[(uint32_t)ad] = col;
+    const bool st = D >= 0;
+    px += xx + (st ? yx : 0);
+    py += xy + (st ? yy : 0);
+    ad += amaj + (st ? amin : 0);
+    D += 2 * dy - (st ? 2 * dx : 0);
+  }
+}
+
 struct View {  // f32 camera frame of one env
   float cx, cz, dirx, dirz, rx, rz;
 };
@@ -192,35 +255,20 @@ __device__ inline int proj(float v) {  // round-to-nearest pixel, clamped far of
   return (int)v;
 }
 
-__device__ inline void draw_one(lds_u8* img, const View& V, float4 q, uint8_t col) {
+// a segment's pixel endpoints, or false when it is culled (wholly off one
+// side of the frame, or degenerate: a segment is <= ~10 px at 1 cm/px)
+__device__ inline bool project_seg(const View& V, float4 q, int& c0, int& r0, int& c1, int& r1) {
   const float ax = q.x - V.cx, az = q.y - V.cz, bx = q.z - V.cx, bz = q.w - V.cz;
   const float fa = ax * V.dirx + az * V.dirz, la = ax * V.rx + az * V.rz;
   const float fb = bx * V.dirx + bz * V.dirz, lb = bx * V.rx + bz * V.rz;
-  const int c0 = proj(la * kInvRes + 79.5f), r0 = proj(119.5f - fa * kInvRes);
-  const int c1 = proj(lb * kInvRes + 79.5f), r1 = proj(119.5f - fb * kInvRes);
+  c0 = proj(la * kInvRes + 79.5f);
+  r0 = proj(119.5f - fa * kInvRes);
+  c1 = proj(lb * kInvRes + 79.5f);
+  r1 = proj(119.5f - fb * kInvRes);
   if ((c0 < 0 && c1 < 0) || (c0 >= W && c1 >= W) || (r0 < 0 && r1 < 0) || (r0 >= H && r1 >= H))
-    return;
+    return false;
   const int len = (c1 > c0 ? c1 - c0 : c0 - c1) + (r1 > r0 ? r1 - r0 : r0 - r1);
-  if (len > 400) return;  // degenerate (a segment is <= ~10 px at 1 cm/px)
-  draw_line(img, c0, r0, c1, r1, col);
-}
-
-// Every thread draws segments tid, tid + T, ...; the (L2-resident) segment
-// loads of a thread are issued together, four at a time, before any is drawn.
-__device__ inline void draw_segments(lds_u8* img, const View& V, const float4* __restrict__ seg,
-                                     int nseg, uint8_t col) {
-  const int T = blockDim.x;
-  for (int s0 = threadIdx.x; s0 < nseg; s0 += 4 * T) {
-    float4 q[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int s = s0 + k * T;
-      q[k] = s < nseg ? seg[s] : make_float4(-1e9f, -1e9f, -1e9f, -1e9f);
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      if (s0 + k * T < nseg) draw_one(img, V, q[k], col);
-  }
+  return len <= 400;
 }
 
 // pass A for one pixel: Sobel/NMS dir + colour bits into work, magnitude into mag
@@ -348,10 +396,14 @@ struct RenderArgs {
 //   4  masks: colour bits from img through a v_perm LUT, SWAR ellipse
 //      dilation, edge bits from work; 16 px per lane, four uint4 stores
 // LDS ~71 KB -> two workgroups per CU.
+#ifndef DTSIM_MARK_PARTS
+#define DTSIM_MARK_PARTS 4  // lanes per marking segment (draw_line_part)
+#endif
 constexpr int kRenderThreads = 768;  // 12 waves (measured best of 256-1024); LDS per workgroup is fixed (~71 KB)
 constexpr int WPR = W / 4;          // words per row
 constexpr int NW = NPIX / 4;        // words per image
 constexpr int kWeakCap = 2048;
+enum { kNList = 0, kNWeak = 1, kNSeg = 2, kNSegW = 3 };
 constexpr uint16_t WK_MAG = 0x7FF, WK_DIR_SHIFT = 11, WK_CAND = 1 << 13, WK_EDGE = 1 << 14;
 
 struct FusedLds {
@@ -363,7 +415,7 @@ struct FusedLds {
   float pal_gray[PAL_N];
   uint32_t bits_lo, bits_hi;  // colour bits of palette entries 0-3 / 4-7 (one byte each)
   View view;
-  int32_t nlist, nweak;
+  int32_t cnt[4];  // list counters: kNList, kNWeak, kNSeg, kNSegW
   int8_t kind[dt::kMaxLdsTiles];
 };
 
@@ -440,6 +492,57 @@ __device__ inline void wave_push4(int32_t* counter, uint16_t* list, int cap, con
   }
 }
 
+// A slot for each of up to four items per lane (every lane of the wave calls):
+// the wave_push4 bit-plane prefix, returning the slots instead of storing.
+__device__ inline void wave_slots4(int32_t* counter, const bool want[4], int slot[4]) {
+  const uint32_t cnt = (uint32_t)want[0] + want[1] + want[2] + want[3];
+  const uint64_t b0 = __ballot(cnt & 1u), b1 = __ballot(cnt & 2u), b2 = __ballot(cnt & 4u);
+  const int total = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+  if (total == 0) return;  // wave-uniform
+  const auto mb = [](uint64_t m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  };
+  int base = 0;
+  if ((threadIdx.x & 63) == 0) base = atomicAdd(counter, total);
+  base = __builtin_amdgcn_readlane(base, 0);
+  int next = base + mb(b0) + 2 * mb(b1) + 4 * mb(b2);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    slot[k] = next;
+    next += want[k] ? 1 : 0;
+  }
+}
+
+// wave_slots4 for two lists at once: one LDS atomic on a packed counter
+// (list A in the low 16 bits, list B in the high 16 bits; each < 65536).
+__device__ inline void wave_slots4x2(int32_t* counter, const bool wa[4], const bool wb[4],
+                                     int sa[4], int sb[4]) {
+  const uint32_t ca = (uint32_t)wa[0] + wa[1] + wa[2] + wa[3];
+  const uint32_t cb = (uint32_t)wb[0] + wb[1] + wb[2] + wb[3];
+  const uint64_t a0 = __ballot(ca & 1u), a1 = __ballot(ca & 2u), a2 = __ballot(ca & 4u);
+  const uint64_t b0 = __ballot(cb & 1u), b1 = __ballot(cb & 2u), b2 = __ballot(cb & 4u);
+  const uint32_t ta = __popcll(a0) + 2 * __popcll(a1) + 4 * __popcll(a2);
+  const uint32_t tb = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+  if ((ta | tb) == 0u) return;  // wave-uniform
+  const auto mb = [](uint64_t m) {
+    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+  };
+  int base = 0;
+  if ((threadIdx.x & 63) == 0) base = atomicAdd(counter, (int)(ta | (tb << 16)));
+  base = __builtin_amdgcn_readlane(base, 0);
+  int na = (base & 0xFFFF) + mb(a0) + 2 * mb(a1) + 4 * mb(a2);
+  int nb = (int)((uint32_t)base >> 16) + mb(b0) + 2 * mb(b1) + 4 * mb(b2);
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    sa[k] = na;
+    na += wa[k] ? 1 : 0;
+    sb[k] = nb;
+    nb += wb[k] ? 1 : 0;
+  }
+}
+
 __device__ inline int mag16(const FusedLds& S, int r, int c) {
   return ((unsigned)r < (unsigned)H && (unsigned)c < (unsigned)W) ? (S.work[r * W + c] & WK_MAG)
                                                                   : 0;
@@ -508,95 +611,200 @@ __device__ __forceinline__ void write_masks(const FusedLds& S, const LineDev& L,
   }
 }
 
-__global__ __launch_bounds__(1024) void render_kernel(RenderArgs a) {
-  __shared__ __attribute__((aligned(16))) FusedLds S;
-  const int e = blockIdx.x;
+__device__ inline View view_of(double x, double z, double ang, double cam_fwd) {
+  double sd, cd;
+  sincos(ang, &sd, &cd);
+  View v;
+  v.cx = (float)(x + cam_fwd * cd);
+  v.cz = (float)(z + cam_fwd * (-sd));
+  v.dirx = (float)cd;
+  v.dirz = -(float)sd;
+  v.rx = (float)sd;
+  v.rz = (float)cd;
+  return v;
+}
+
+// One env of render_kernel.
+__device__ __forceinline__ void render_env(const RenderArgs& a, FusedLds& S, int e) {
   const int tid = threadIdx.x;
   const LineDev& L = a.line;
-  if (tid < PAL_N) {
-    const uint32_t p = kPalette[tid];
-    S.pal_swar[tid] = swar_of(p);
-    const double inv = 1.0 / 255.0;
-    const double rr = (double)((p >> 16) & 255) * inv, gg = (double)((p >> 8) & 255) * inv,
-                 bb = (double)(p & 255) * inv;
-    S.pal_gray[tid] = (float)((rr * 0.2125 + gg * 0.7154) + bb * 0.0721);
-  }
-  if (tid == 0) {
-    S.bits_lo = L.pal_bits[0];
-    S.bits_hi = L.pal_bits[1];
-    S.nlist = 0;
-    S.nweak = 0;
-  }
-  for (int i = tid; i < a.width * a.height; i += blockDim.x) S.kind[i] = a.kind[i];
-
-  if (tid == 64) {  // the camera frame, once per workgroup (wave 1; wave 0 has the palette)
-    const double ang = a.angle[e];
-    double sd, cd;
-    sincos(ang, &sd, &cd);
-    View v;
-    v.cx = (float)(a.x[e] + a.cam_fwd * cd);
-    v.cz = (float)(a.z[e] + a.cam_fwd * (-sd));
-    v.dirx = (float)cd;
-    v.dirz = -(float)sd;
-    v.rx = (float)sd;
-    v.rz = (float)cd;
-    S.view = v;
-  }
-  __syncthreads();
+  const int T = blockDim.x, nmark = a.n_yellow + a.n_white;
+  const bool mfast = nmark <= 4 * T;
+#ifdef DTSIM_STAMPS
+  RENSTAMP(0, __builtin_amdgcn_s_memrealtime());
+  RENSTAMP(2, ren_hw_id());
+  RENSTAMP(3, ren_xcc_id());
+#endif
+  RENT(4);
+  RENT(5);
+  int32_t* const C = S.cnt;
   const View V = S.view;
+  // the marking segments' loads (L2-resident), first used after the background
+  float4 mq[4];
+  if (mfast && !(a.skip & 2)) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int sidx = tid + k * T;
+      mq[k] = sidx < nmark ? a.marks[sidx] : make_float4(-1e9f, -1e9f, -1e9f, -1e9f);
+    }
+  }
 
-  // phase 0: background, a 16-pixel span (4 words) per lane.  Tiles are convex
-  // and each coordinate is a monotone float function of the column, so when
-  // both end pixels of a span (or word) fall in one tile, all between do: one
-  // lookup and one 16-byte store for the common uniform span.
-  for (int q = tid; q < NW / 4 && !(a.skip & 1); q += blockDim.x) {
-    const int r = q / (WPR / 4), c0 = 16 * (q - r * (WPR / 4));
+  // phase 0: background.  Tiles are convex and each coordinate is a monotone
+  // float function of the column, so along a row the tile index steps
+  // monotonically.  0a: a 16-pixel span (4 words) per lane; its end pixels'
+  // tiles decide it when they are one tile, or two edge-adjacent tiles of one
+  // colour (then every pixel between is in one of the two); such spans are one
+  // 16-byte store.  The rest (a tile edge of two colours, or a corner, inside)
+  // are listed (wave-aggregated) and 0b resolves them a word per lane, so the
+  // per-pixel path runs only where it is needed instead of on every lane of a
+  // wave that holds one such span.
+  const auto tile_f = [&](int r, int c, float& fi, float& fj) {
     const float f = (119.5f - (float)r) * kRes;
     const float bx = V.cx + f * V.dirx, bz = V.cz + f * V.dirz;
-    float fi[16], fj[16];
-#pragma unroll
-    for (int i = 0; i < 16; i += 15) {
-      const float l = ((float)(c0 + i) - 79.5f) * kRes;
-      const float wx = bx + l * V.rx, wz = bz + l * V.rz;
-      fi[i] = floorf(wx * a.inv_ts);
-      fj[i] = floorf(wz * a.inv_ts);
-    }
-    uint4 words;
-    if (fi[0] == fi[15] && fj[0] == fj[15]) {
-      const uint32_t wd = splat_byte(bg_color(S, a, fi[0], fj[0]));
-      words = make_uint4(wd, wd, wd, wd);
-    } else {
-#pragma unroll
-      for (int i = 1; i < 15; ++i) {
-        const float l = ((float)(c0 + i) - 79.5f) * kRes;
-        const float wx = bx + l * V.rx, wz = bz + l * V.rz;
-        fi[i] = floorf(wx * a.inv_ts);
-        fj[i] = floorf(wz * a.inv_ts);
+    const float l = ((float)c - 79.5f) * kRes;
+    const float wx = bx + l * V.rx, wz = bz + l * V.rz;
+    fi = floorf(wx * a.inv_ts);
+    fj = floorf(wz * a.inv_ts);
+  };
+  constexpr int NSPAN = NW / 4;
+  for (int q0 = 0; q0 < NSPAN && !(a.skip & 1); q0 += blockDim.x) {
+    const int q = q0 + tid;
+    bool want[4] = {false, false, false, false};
+    uint16_t val[4] = {(uint16_t)q, 0, 0, 0};
+    if (q < NSPAN) {
+      const int r = q / (WPR / 4), c0 = 16 * (q - r * (WPR / 4));
+      float fi0, fj0, fi1, fj1;
+      tile_f(r, c0, fi0, fj0);
+      tile_f(r, c0 + 15, fi1, fj1);
+      const uint32_t col0 = bg_color(S, a, fi0, fj0);
+      bool uni = fi0 == fi1 && fj0 == fj1;
+      if (!uni && fabsf(fi1 - fi0) + fabsf(fj1 - fj0) == 1.0f)
+        uni = bg_color(S, a, fi1, fj1) == col0;
+      if (uni) {
+        const uint32_t wd = splat_byte(col0);
+        *reinterpret_cast<uint4*>(S.img + 4 * q) = make_uint4(wd, wd, wd, wd);
       }
-      uint32_t wd[4];
+      want[0] = !uni;
+    }
+    wave_push4(&C[kNList], S.list, NW, want, val);
+  }
+  __syncthreads();
+  {
+    const int nspan = C[kNList];
+    for (int i = tid; i < 4 * nspan; i += blockDim.x) {
+      const int q = S.list[i >> 2];
+      const int r = q / (WPR / 4), c = 16 * (q - r * (WPR / 4)) + 4 * (i & 3);
+      float fi[4], fj[4];
+      tile_f(r, c, fi[0], fj[0]);
+      tile_f(r, c + 3, fi[3], fj[3]);
+      const uint32_t col0 = bg_color(S, a, fi[0], fj[0]);
+      uint32_t wd;
+      if (fi[0] == fi[3] && fj[0] == fj[3]) {
+        wd = splat_byte(col0);
+      } else {
+        tile_f(r, c + 1, fi[1], fj[1]);
+        tile_f(r, c + 2, fi[2], fj[2]);
+        wd = col0;
+#pragma unroll
+        for (int k = 1; k < 4; ++k) wd |= bg_color(S, a, fi[k], fj[k]) << (8 * k);
+      }
+      S.img[4 * q + (i & 3)] = wd;
+    }
+  }
+  __syncthreads();
+  if (tid == 0) C[kNList] = 0;   // the span list is consumed; phase 1 reuses it
+  RENT(6);
+  uint8_t* img8 = reinterpret_cast<uint8_t*>(S.img);
+  // markings: yellow, then white over it.  Every lane projects up to four
+  // segments and lists the visible ones (pixel endpoints as int16 x 4) in the
+  // work image, which is scratch until phase 1; after a barrier the lanes draw
+  // the listed segments, so no lane idles on a culled one while another walks
+  // a line.  Up to 4 x blockDim segments (mfast) their loads were issued at
+  // kernel entry and the two colours are listed in one pass (yellow from the
+  // bottom of the scratch, white from the top); more take batches.
+  if (!(a.skip & 2)) {
+    uint2* segl = reinterpret_cast<uint2*>(S.work);
+    constexpr int kSegCap = NPIX / 4;  // uint2 records in the work image
+    const auto pack = [](int c0, int r0, int c1, int r1) {
+      return make_uint2((uint32_t)(uint16_t)c0 | ((uint32_t)(uint16_t)r0 << 16),
+                        (uint32_t)(uint16_t)c1 | ((uint32_t)(uint16_t)r1 << 16));
+    };
+    const auto draw = [&](uint2 v, uint8_t col) {
+      draw_line((lds_u8*)img8, (int)(int16_t)(v.x & 0xFFFFu), (int)(int16_t)(v.x >> 16),
+                (int)(int16_t)(v.y & 0xFFFFu), (int)(int16_t)(v.y >> 16), col);
+    };
+    constexpr int kParts = DTSIM_MARK_PARTS;
+    const auto draw_part = [&](uint2 v, uint8_t col, int part) {
+      draw_line_part((lds_u8*)img8, (int)(int16_t)(v.x & 0xFFFFu), (int)(int16_t)(v.x >> 16),
+                     (int)(int16_t)(v.y & 0xFFFFu), (int)(int16_t)(v.y >> 16), col, part, kParts);
+    };
+    if (mfast) {
+      bool vy[4], vw[4];
+      int cc0[4], rr0[4], cc1[4], rr1[4], sy[4], sw[4];
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const int i0 = 4 * k, i3 = 4 * k + 3;
-        if (fi[i0] == fi[i3] && fj[i0] == fj[i3]) {
-          wd[k] = splat_byte(bg_color(S, a, fi[i0], fj[i0]));
-        } else {
-          wd[k] = 0;
+        const int sidx = tid + k * T;
+        const bool v = sidx < nmark && project_seg(V, mq[k], cc0[k], rr0[k], cc1[k], rr1[k]);
+        vy[k] = v && sidx < a.n_yellow;
+        vw[k] = v && sidx >= a.n_yellow;
+      }
+      RENT(16);
+      wave_slots4x2(&C[kNSeg], vy, vw, sy, sw);  // yellow count | white count << 16
+      RENT(17);
 #pragma unroll
-          for (int i = 0; i < 4; ++i) wd[k] |= bg_color(S, a, fi[i0 + i], fj[i0 + i]) << (8 * i);
+      for (int k = 0; k < 4; ++k) {
+        if (vy[k]) segl[sy[k]] = pack(cc0[k], rr0[k], cc1[k], rr1[k]);
+        if (vw[k]) segl[kSegCap - 1 - sw[k]] = pack(cc0[k], rr0[k], cc1[k], rr1[k]);
+      }
+      __syncthreads();
+      RENT(14);
+      // kParts lanes per segment, each drawing its share of the pixels
+      const int ny = C[kNSeg] & 0xFFFF, nw = (int)((uint32_t)C[kNSeg] >> 16);
+      for (int i = tid; i < kParts * ny; i += T) draw_part(segl[i / kParts], PAL_YELLOW, i % kParts);
+      __syncthreads();
+      RENT(18);
+      for (int i = tid; i < kParts * nw; i += T)
+        draw_part(segl[kSegCap - 1 - i / kParts], PAL_WHITE, i % kParts);
+#ifdef DTSIM_STAMPS
+      if (tid == 0) C[kNSeg] = ny + nw;
+#endif
+    } else {
+      const int batch = 4 * T;  // <= kSegCap (T <= 1024 -> 4096)
+      int listed = 0;           // S.nseg at the start of the batch
+#pragma unroll 1
+      for (int colr = 0; colr < 2; ++colr) {
+        const float4* seg = colr == 0 ? a.marks : a.marks + a.n_yellow;
+        const int nseg = colr == 0 ? a.n_yellow : a.n_white;
+        const uint8_t col = colr == 0 ? PAL_YELLOW : PAL_WHITE;
+#pragma unroll 1
+        for (int b0 = 0; b0 < nseg; b0 += batch) {
+          const int bn = nseg - b0 < batch ? nseg - b0 : batch;
+          float4 q[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int sidx = tid + k * T;
+            q[k] = sidx < bn ? seg[b0 + sidx] : make_float4(-1e9f, -1e9f, -1e9f, -1e9f);
+          }
+          bool vis[4];
+          int cc0[4], rr0[4], cc1[4], rr1[4], slot[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            vis[k] = tid + k * T < bn && project_seg(V, q[k], cc0[k], rr0[k], cc1[k], rr1[k]);
+          wave_slots4(&C[kNSeg], vis, slot);
+#pragma unroll
+          for (int k = 0; k < 4; ++k)
+            if (vis[k]) segl[slot[k] % kSegCap] = pack(cc0[k], rr0[k], cc1[k], rr1[k]);
+          __syncthreads();
+          const int end = C[kNSeg];
+          for (int i = listed + tid; i < end; i += T) draw(segl[i % kSegCap], col);
+          listed = end;
+          __syncthreads();
         }
       }
-      words = make_uint4(wd[0], wd[1], wd[2], wd[3]);
     }
-    *reinterpret_cast<uint4*>(S.img + 4 * q) = words;
   }
   __syncthreads();
-  uint8_t* img8 = reinterpret_cast<uint8_t*>(S.img);
-  if (!(a.skip & 2)) {
-    draw_segments((lds_u8*)img8, V, a.marks, a.n_yellow, PAL_YELLOW);
-    __syncthreads();
-    draw_segments((lds_u8*)img8, V, a.marks + a.n_yellow, a.n_white, PAL_WHITE);
-  }
-  __syncthreads();
+  RENT(7);
 
   // phase 1: exact uniformity test of the 3 x 6 byte neighbourhood, grey.  A
   // lane takes a column of 4 words (rows 4g..4g+3 of word column cw), so the
@@ -672,12 +880,13 @@ __global__ __launch_bounds__(1024) void render_kernel(RenderArgs a) {
       push[k] = act && !uni[k];
       pv[k] = (uint16_t)wq[k];
     }
-    wave_push4(&S.nlist, S.list, NW, push, pv);
+    wave_push4(&C[kNList], S.list, NW, push, pv);
   }
   __syncthreads();
+  RENT(8);
 
   // phase 2a: gradients of the listed words
-  const int nlist = (a.skip & 8) ? 0 : S.nlist;
+  const int nlist = (a.skip & 8) ? 0 : C[kNList];
   for (int li = tid; li < nlist; li += blockDim.x) {
     const int w = S.list[li];
     const int r = w / WPR, c0 = 4 * (w - r * WPR);
@@ -705,6 +914,7 @@ __global__ __launch_bounds__(1024) void render_kernel(RenderArgs a) {
     *reinterpret_cast<uint2*>(S.work + 4 * w) = make_uint2(out[0], out[1]);
   }
   __syncthreads();
+  RENT(9);
 
   // phase 2b: NMS + double threshold on the listed words
   for (int i0 = 0; i0 < nlist; i0 += blockDim.x) {
@@ -746,12 +956,13 @@ __global__ __launch_bounds__(1024) void render_kernel(RenderArgs a) {
         *reinterpret_cast<uint2*>(S.work + 4 * w) =
             make_uint2(cur.x | setb[0] | (setb[1] << 16), cur.y | setb[2] | (setb[3] << 16));
     }
-    wave_push4(&S.nweak, S.weak, kWeakCap, want, wk);
+    wave_push4(&C[kNWeak], S.weak, kWeakCap, want, wk);
   }
   __syncthreads();
+  RENT(10);
 
   // phase 3: hysteresis (weak candidates 8-connected to an edge become edges)
-  const int nweak = (a.skip & 16) ? 0 : S.nweak;
+  const int nweak = (a.skip & 16) ? 0 : C[kNWeak];
   if (nweak > 0) {
     const bool overflow = nweak > kWeakCap;
     const int cnt = overflow ? NPIX : nweak;
@@ -782,6 +993,11 @@ __global__ __launch_bounds__(1024) void render_kernel(RenderArgs a) {
       if (!__syncthreads_or(changed)) break;
     }
   }
+  RENT(11);
+#ifdef DTSIM_STAMPS
+  RENSTAMP(12, (unsigned long long)nlist | ((unsigned long long)nweak << 32));
+  RENSTAMP(15, (unsigned long long)C[kNSeg]);
+#endif
 
   // phase 4: masks, 16 pixels (4 words) per lane
   if (a.masks && !(a.skip & 32)) {
@@ -793,6 +1009,42 @@ __global__ __launch_bounds__(1024) void render_kernel(RenderArgs a) {
       default: write_masks<3>(S, L, mb); break;
     }
   }
+  RENT(13);
+#ifdef DTSIM_STAMPS
+  RENSTAMP(1, __builtin_amdgcn_s_memrealtime());
+#endif
+}
+
+// One workgroup per env (a persistent variant, two workgroups per CU looping
+// over envs with the palette and tile kinds staged once, was measured slower:
+// the loop keeps loop-invariant values live across envs, and the kernel then
+// spills at the 80 VGPRs that two workgroups per CU allow).
+// waves_per_eu(6): two 768-thread workgroups per CU need <= 85 VGPRs
+__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void render_kernel(
+    RenderArgs a) {
+  __shared__ __attribute__((aligned(16))) FusedLds S;
+  const int tid = threadIdx.x;
+  const LineDev& L = a.line;
+  if (tid < PAL_N) {
+    const uint32_t p = kPalette[tid];
+    S.pal_swar[tid] = swar_of(p);
+    const double inv = 1.0 / 255.0;
+    const double rr = (double)((p >> 16) & 255) * inv, gg = (double)((p >> 8) & 255) * inv,
+                 bb = (double)(p & 255) * inv;
+    S.pal_gray[tid] = (float)((rr * 0.2125 + gg * 0.7154) + bb * 0.0721);
+  }
+  if (tid == 0) {
+    S.bits_lo = L.pal_bits[0];
+    S.bits_hi = L.pal_bits[1];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) S.cnt[i] = 0;
+  }
+  for (int i = tid; i < a.width * a.height; i += blockDim.x) S.kind[i] = a.kind[i];
+  // the camera frame, once per workgroup (wave 1; wave 0 has the palette)
+  const int e = blockIdx.x;
+  if (tid == 64) S.view = view_of(a.x[e], a.z[e], a.angle[e], a.cam_fwd);
+  __syncthreads();
+  render_env(a, S, e);
 }
 
 // LineDetectorHSV on caller BGR images (one workgroup per image, <= 19200 px).
@@ -864,6 +1116,7 @@ int dt_render_init(dt_handle* h, const dt_map* map) {
   h->render_threads = th ? atoi(th) : kRenderThreads;
   if (h->render_threads < 128 || h->render_threads > 1024 || (h->render_threads & 63))
     h->render_threads = kRenderThreads;
+
   return DT_OK;
 }
 
@@ -873,6 +1126,12 @@ void dt_render_free(dt_handle* h) {
 }
 
 extern "C" {
+
+#ifdef DTSIM_STAMPS
+int dt_diag_renstamps(unsigned long long* out) {  // render_kernel per-workgroup stamps
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_renstamps), sizeof(g_renstamps)) == hipSuccess ? 0 : -1;
+}
+#endif
 
 int dt_default_line_params(dt_line_params* p) {
   if (!p) return DT_E_ARG;

@@ -10,7 +10,7 @@ i=0
 for ctr in $SETS; do
   i=$((i+1))
   timeout -k 10 240 rocprofv3 --pmc ${ctr//,/ } --output-format csv -d "$ROOT/gpurun_out/kpmc_$i" -o run -- \
-    python3 "$ROOT/bench.py" --config $CONFIG --steps 10 --warmup 3 --cpu-seconds 0 $ARGS > "gpurun_out/kpmc_$i.log" 2>&1 || { echo "fail $i"; exit 1; }
+    python3 "$ROOT/bench.py" --config $CONFIG --steps 10 --warmup 3 --cpu-steps 0 $ARGS > "gpurun_out/kpmc_$i.log" 2>&1 || { echo "fail $i"; exit 1; }
   python3 - "$ROOT/gpurun_out/kpmc_$i/run_counter_collection.csv" "$KERNEL" <<'PY'
 import csv, sys, collections
 tot = collections.defaultdict(lambda: collections.defaultdict(float)); n = collections.defaultdict(collections.Counter)

@@ -34,7 +34,7 @@ def per_dispatch(path, needle, counter=None):
     vals = {}
     for row in csv.DictReader(open(path)):
         name = row.get('Kernel_Name', '')
-        if needle + '(' not in name and not name.endswith(needle):
+        if needle + '(' not in name and needle + '<' not in name and not name.endswith(needle):
             continue
         if counter and row.get('Counter_Name') != counter:
             continue

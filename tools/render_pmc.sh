@@ -9,7 +9,7 @@ for skip in ${SKIPS:-0}; do
   for ctr in $SETS; do
     i=$((i+1))
     DTSIM_RENDER_SKIP=$skip timeout -k 10 180 rocprofv3 --pmc ${ctr//,/ } --output-format csv -d "$ROOT/gpurun_out/rpmc_$i" -o run -- \
-      python3 "$ROOT/bench.py" --config render --steps 20 --warmup 3 --cpu-seconds 0 > "gpurun_out/rpmc_$i.log" 2>&1 || { echo "fail $i"; exit 1; }
+      python3 "$ROOT/bench.py" --config render --steps 20 --warmup 3 --cpu-steps 0 > "gpurun_out/rpmc_$i.log" 2>&1 || { echo "fail $i"; exit 1; }
     python3 - "$ROOT/gpurun_out/rpmc_$i/run_counter_collection.csv" "$skip" <<'PY'
 import csv, sys, collections
 tot = collections.defaultdict(float); n = collections.Counter()
