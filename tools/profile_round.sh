@@ -17,10 +17,17 @@ step() {  # step <name> <timeout> cmd...
   [ $rc -eq 0 ] || { echo "stopping"; exit $rc; }
 }
 declare -A ARGS=(
-  [lane]="--steps $STEPS --warmup $WARM --cpu-steps 0"
+  [lane]="--steps $STEPS --warmup 20 --cpu-steps 0"
   [render]="--config render --steps 100 --warmup 20 --cpu-steps 0"
   [actor]="--config actor --steps 30 --warmup 5 --cpu-steps 0"
   [train]="--config train --steps 30 --warmup 10 --cpu-steps 0")
+# plain runs first (no profiler): the bench lines DESIGN quotes
+if [ -z "$NO_PLAIN" ]; then
+  step bench_lane_driver 300 python3 "$ROOT/bench.py" --steps 20 --warmup 5
+  step bench_lane_320 300 python3 "$ROOT/bench.py" --steps 320 --warmup 20 --cpu-steps 0
+  for cfg in render actor train; do step "bench_$cfg" 600 python3 "$ROOT/bench.py" ${ARGS[$cfg]}; done
+  step bench_actor_eval 600 python3 "$ROOT/bench.py" ${ARGS[actor]} --actor-mode eval
+fi
 for cfg in ${CONFIGS:-lane render actor train}; do
   step "trace_$cfg" 600 rocprofv3 --kernel-trace --stats --output-format csv \
       -d "$ROOT/gpurun_out/trace_$cfg" -o run -- python3 "$ROOT/bench.py" ${ARGS[$cfg]}
