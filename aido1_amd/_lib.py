@@ -23,8 +23,11 @@ PUBLIC_HEADERS = ['dtsim.h', 'dtreplay.h', 'dtactor.h']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ABI_VERSION = 3
 
+# -pragma-unroll-threshold: dt_conv12's step loops must unroll fully (its conv1
+# outputs are register arrays indexed by step) past clang's default limit
 HIP_FLAGS = ['--offload-arch=gfx950', '-O3', '-fPIC', '-shared', '-std=c++17',
-             '-ffp-contract=off', '-munsafe-fp-atomics']
+             '-ffp-contract=off', '-munsafe-fp-atomics', '-mllvm',
+             '-pragma-unroll-threshold=1000000']
 
 
 class DtError(RuntimeError):
@@ -137,6 +140,8 @@ def lib():
             'dt_conv1_bands': (i32, []),
             'dt_conv32': (ctypes.c_int, [i32, i32, vp, vp, vp, vp, vp, vp, ctypes.c_float, vp,
                                          vp, vp, vp, ctypes.c_float, ctypes.c_float, vp]),
+            'dt_conv12': (ctypes.c_int, [vp, i32, i32, ctypes.POINTER(i32), vp, vp, vp, vp,
+                                         ctypes.c_float, vp, vp, vp, vp, ctypes.c_float, vp]),
         }
         for name, (res, args) in sig.items():
             if not hasattr(L, name):

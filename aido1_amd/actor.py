@@ -18,6 +18,7 @@ zero-copy: the first conv's input channels are permuted to the ring's slot
 order instead of gathering the Transformer stack.
 """
 import copy
+import os
 
 import torch
 import torch.nn as nn
@@ -275,6 +276,13 @@ class FusedActor(nn.Module):
         self.register_buffer('w0frag', torch.zeros(16, 64, 8, dtype=torch.float16, device=dev))
         self.register_buffer('wfrag', torch.zeros(3, 32, 64, 8, dtype=torch.float16, device=dev))
         self.register_buffer('bf', torch.zeros(4, 32, device=dev))
+        # DTCONV_FUSED12=1: conv1 + bn1 + conv2 as one kernel (dt_conv12, the
+        # conv1 activation kept on chip); measured slower than dt_conv1 +
+        # dt_conv32, so off by default.  DTCONV_CHUNK: samples
+        # per pass through the chain (0: the whole batch; smaller passes, meant
+        # to keep the conv1 activation in the MALL, measured slower too)
+        self.fused12 = os.environ.get('DTCONV_FUSED12', '0') == '1'
+        self.chunk = int(os.environ.get('DTCONV_CHUNK', '0'))
         self.refresh(actor)
 
     @torch.no_grad()
@@ -346,27 +354,62 @@ class FusedActor(nn.Module):
         stages its input (the last one in conv4's epilogue).  Returns the
         flattened [N, 4032] fp16 activation in NCHW order."""
         from aido1_amd import _lib
-        import ctypes
         L = _lib.lib()
         n, slots = ring.shape[0], ring.shape[1]
         dev = ring.device
+        flat = torch.empty(n, FLAT, dtype=torch.float16, device=dev)
+        chunk = n if self.chunk <= 0 else max(1, min(n, self.chunk))
+        bufs = self._chunk_buffers(chunk, dev)
+        rc = 0
+        for c0 in range(0, n, chunk):
+            c = min(chunk, n - c0)
+            rc = self._convs_chunk(L, ring[c0:c0 + c], slots, order, flat[c0:c0 + c], bufs)
+            if rc != 0:
+                break
+        if rc != 0:
+            raise _lib.DtError('dt_conv1 / dt_conv12 / dt_conv32 failed (%d)' % rc)
+        return flat
+
+    def _chunk_buffers(self, chunk, dev):
+        key = (chunk, dev, self.mode, self.fused12)
+        if getattr(self, '_bufs_key', None) != key:
+            f16 = torch.float16
+            ref = self.mode == 'reference'
+            self._bufs = {
+                'y1': None if self.fused12 else torch.empty(chunk, 57, 77, 32, dtype=f16, device=dev),
+                'p1': torch.empty(chunk, _lib_bands(), 32, 2, device=dev)
+                if (ref and not self.fused12) else None,
+                'y2': torch.empty(chunk, 27, 37, 32, dtype=f16, device=dev),
+                'y3': torch.empty(chunk, 12, 17, 32, dtype=f16, device=dev),
+                'p2': torch.empty(chunk, 1, 32, 2, device=dev) if ref else None,
+                'p3': torch.empty(chunk, 1, 32, 2, device=dev) if ref else None}
+            self._bufs_key = key
+        return self._bufs
+
+    def _convs_chunk(self, L, ring, slots, order, flat, B):
+        import ctypes
+        n = ring.shape[0]
         ref = self.mode == 'reference'
-        f16 = torch.float16
-        stream = torch.cuda.current_stream(dev).cuda_stream
-        y1 = torch.empty(n, 57, 77, 32, dtype=f16, device=dev)
-        y2 = torch.empty(n, 27, 37, 32, dtype=f16, device=dev)
-        y3 = torch.empty(n, 12, 17, 32, dtype=f16, device=dev)
-        flat = torch.empty(n, FLAT, dtype=f16, device=dev)
-        p1 = torch.empty(n, L.dt_conv1_bands(), 32, 2, device=dev) if ref else None
-        p2 = torch.empty(n, 1, 32, 2, device=dev) if ref else None
-        p3 = torch.empty(n, 1, 32, 2, device=dev) if ref else None
+        stream = torch.cuda.current_stream(ring.device).cuda_stream
         ptr = (lambda t: t.data_ptr() if t is not None else None)
         o = (ctypes.c_int32 * 3)(*[int(v) for v in order])
-        rc = L.dt_conv1(ring.data_ptr(), n, slots, o, self.w0frag.data_ptr(),
-                        self.bf[0].data_ptr(), y1.data_ptr(), ptr(p1), 0.01, stream)
-        ins = [(y1, p1, 0), (y2, p2, 1), (y3, p3, 2)]
+        y2, y3, p2, p3 = B['y2'], B['y3'], B['p2'], B['p3']
+        if self.fused12:
+            # conv1 -> bn1 -> conv2 in one kernel (the conv1 activation stays on chip)
+            rc = L.dt_conv12(ring.data_ptr(), n, slots, o, self.w0frag.data_ptr(),
+                             self.bf[0].data_ptr(), self.gamma[0].data_ptr() if ref else None,
+                             self.beta[0].data_ptr() if ref else None,
+                             self.eps[0] if ref else 0.0, self.wfrag[0].data_ptr(),
+                             self.bf[1].data_ptr(), y2.data_ptr(), ptr(p2), 0.01, stream)
+            first = 1
+        else:
+            y1, p1 = B['y1'], B['p1']
+            rc = L.dt_conv1(ring.data_ptr(), n, slots, o, self.w0frag.data_ptr(),
+                            self.bf[0].data_ptr(), y1.data_ptr(), ptr(p1), 0.01, stream)
+            first = 0
+        ins = [(B['y1'], B['p1'], 0), (y2, p2, 1), (y3, p3, 2)]
         outs = [(y2, p2), (y3, p3), (flat, None)]
-        for layer in range(3):
+        for layer in range(first, 3):
             if rc != 0:
                 break
             x, pp, g = ins[layer]
@@ -381,9 +424,7 @@ class FusedActor(nn.Module):
                 self.gamma[3].data_ptr() if (ref and last) else None,
                 self.beta[3].data_ptr() if (ref and last) else None,
                 self.eps[3] if ref else 0.0, 0.01, stream)
-        if rc != 0:
-            raise _lib.DtError('dt_conv1 / dt_conv32 failed (%d)' % rc)
-        return flat
+        return rc
 
     @torch.no_grad()
     def forward(self, x, order=None):
@@ -418,6 +459,11 @@ class FusedActor(nn.Module):
         x = F.leaky_relu(F.linear(x, self.w1, self.b1))
         x = F.linear(x, self.w2, self.b2).float()
         return apply_head(x, self.head, self.max_action)
+
+
+def _lib_bands():
+    from aido1_amd import _lib
+    return _lib.lib().dt_conv1_bands()
 
 
 def conv1_fragments(w):

@@ -73,6 +73,26 @@ int dt_conv32(int32_t layer, int32_t n, const void* x, const void* wfrag, const 
               void* y, float* part, const float* out_gamma, const float* out_beta,
               float out_eps, float slope, void* stream);
 
+/* dt_conv12: dt_conv1 + its BatchNorm + dt_conv32 layer 2 in one kernel: one
+ * workgroup per sample keeps the sample's conv1 activation (57 x 77 x 32,
+ * fp16) in registers, reduces its per-sample BatchNorm statistics there and
+ * feeds conv2 from them through LDS, so the activation never goes to HBM.
+ *   ring, slots, order, w1frag, b1  as dt_conv1
+ *   gamma1, beta1, eps1  conv1's BatchNorm (reference mode: the sample's own
+ *            statistics), or gamma1 = NULL for the eval-mode network (BN
+ *            folded into conv2 by the caller)
+ *   w2frag, b2  conv2 as dt_conv32's layer 2
+ *   y2       device fp16 [n, 27, 37, 32] (NHWC)
+ *   part2    device f32 [n, 32, 2]: the sample's per-channel (mean, M2) of
+ *            conv2's LeakyReLU outputs (reference mode; NULL in eval mode),
+ *            the prev_part of dt_conv32 layer 3
+ * Replaces the reference's conv1 -> leaky_relu -> bn1 -> conv2 -> leaky_relu
+ * (duckietown_rl/ddpg.py:56, config.json actor conv layers 1-2). */
+int dt_conv12(const float* ring, int32_t n, int32_t slots, const int32_t* order,
+              const void* w1frag, const float* b1, const float* gamma1, const float* beta1,
+              float eps1, const void* w2frag, const float* b2, void* y2, float* part2,
+              float slope, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
