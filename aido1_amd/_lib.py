@@ -115,6 +115,8 @@ def lib():
             'dt_default_line_params': (ctypes.c_int, [vp]),
             'dt_set_line_params': (ctypes.c_int, [vp, vp]),
             'dt_line_detect': (ctypes.c_int, [vp, vp, i32, i32, i32, vp, vp, vp]),
+            'dt_hough_lines': (ctypes.c_int, [vp, i32, i32, i32, i32, i32, i32, i32, vp, vp,
+                                              vp]),
             'dt_get_state': (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp]),
             'dt_set_state': (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp]),
             'dt_check': (ctypes.c_int, [vp, ctypes.POINTER(u32)]),

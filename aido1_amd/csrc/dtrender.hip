@@ -1088,6 +1088,185 @@ __global__ __launch_bounds__(kThreads) void line_detect_kernel(LineDev L, const 
   }
 }
 
+
+// ---- LineDetectorHSV._HoughLine: cv2.HoughLinesP(edge, 1, pi/180, ...) ------------
+// (features/line_detector1.py:63-70).  The progressive probabilistic Hough
+// transform is sequential over its random point order (each visited point
+// changes the accumulator and the mask the next ones see), so one wave runs
+// one image: the 180 angles' votes and their max are lane-parallel (angles
+// lane, lane + 64, lane + 128), the walks along a found line wave-uniform.
+// The accumulator lives in LDS as int16 counts over the rho range an h x w
+// image reaches (counts go negative: a kept line takes back the votes of
+// every pixel it clears, visited or not, as OpenCV does), the mask as bits,
+// the point list in the rest of the LDS (an image with more edge pixels than
+// fit, ~8k at 120 x 160, is flagged: counts[e] = -1).  The random
+// order is OpenCV's RNG(~0) multiply-with-carry; oracle/hough_oracle.c
+// restates the same algorithm on the CPU.
+constexpr int kHoughAngles = 180;
+struct HoughTab {
+  float cs[2 * kHoughAngles];   // (float)(cos(n*theta)/rho), (float)(sin(n*theta)/rho), host-built
+};
+
+__global__ __launch_bounds__(64) void hough_kernel(const uint8_t* __restrict__ img, int h, int w,
+                                                   HoughTab tab, int numangle, int numrho, int rlo,
+                                                   int nr, int threshold, int min_len, int gap,
+                                                   int max_lines, int max_pts,
+                                                   int32_t* __restrict__ lines,
+                                                   int32_t* __restrict__ counts,
+                                                   int32_t* __restrict__ trace) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char hl[];
+  const int e = blockIdx.x, lane = threadIdx.x, np = h * w;
+  int16_t* acc = reinterpret_cast<int16_t*>(hl);                      // [numangle][nr]
+  uint32_t* mask = reinterpret_cast<uint32_t*>(hl + ((2 * numangle * nr + 15) & ~15));  // bits
+  uint16_t* pts = reinterpret_cast<uint16_t*>(reinterpret_cast<unsigned char*>(mask) +
+                                              (((np + 31) / 32 * 4 + 15) & ~15));       // [max_pts]
+  const uint8_t* im = img + (size_t)e * np;
+  for (int i = lane; i < (numangle * nr + 1) / 2; i += 64) reinterpret_cast<uint32_t*>(acc)[i] = 0u;
+  // the edge pixels in row-major order (ballot compaction keeps the order);
+  // the mask as bits, one 32-bit word per half-ballot
+  int count = 0;
+  for (int p0 = 0; p0 < np; p0 += 64) {
+    const int p = p0 + lane;
+    const bool on = p < np && im[p] != 0;
+    const uint64_t b = __ballot(on);
+    if (lane == 0 && p0 < np) mask[p0 >> 5] = (uint32_t)b;
+    if (lane == 0 && p0 + 32 < np) mask[(p0 >> 5) + 1] = (uint32_t)(b >> 32);
+    const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
+                                                   __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
+    if (on && count + pre < max_pts) pts[count + pre] = (uint16_t)p;
+    count += __popcll(b);
+  }
+  const auto on_mask = [&](int q) { return (mask[q >> 5] >> (q & 31)) & 1u; };
+  float c3[3], s3[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const int n = lane + 64 * t;
+    c3[t] = n < numangle ? tab.cs[2 * n] : 0.0f;
+    s3[t] = n < numangle ? tab.cs[2 * n + 1] : 0.0f;
+  }
+  // rho r lives in row r - rlo of acc (OpenCV's r + (numrho - 1) / 2 is the
+  // same cell shifted: only the reachable range is kept)
+  const int roff = -rlo;
+  (void)numrho;
+  const int shift = 16;
+  uint64_t state = ~0ull;
+  int nlines = 0;
+  bool overflow = count > max_pts;
+  int32_t* out = lines + (size_t)e * max_lines * 4;
+  int it = 0;
+  __syncthreads();
+  for (; count > 0 && !overflow; count--, ++it) {
+    state = (uint64_t)(uint32_t)state * 4164903690ull + (uint32_t)(state >> 32);
+    const int idx = (int)((uint32_t)state % (uint32_t)count);
+    const int p = pts[idx];
+    const int last = pts[count - 1];
+    __builtin_amdgcn_wave_barrier();
+    if (lane == 0) pts[idx] = (uint16_t)last;
+    const int i = p / w, j = p - i * w;
+    if (!on_mask(p)) continue;
+    // vote: the first angle reaching the largest count
+    int bv = threshold - 1, bn = 0;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      const int n = lane + 64 * t;
+      if (n < numangle) {
+        const int r = __float2int_rn((float)j * c3[t] + (float)i * s3[t]) + roff;
+        int16_t* a = acc + n * nr + r;
+        const int v = (int)*a + 1;
+        overflow |= v > 32767;
+        *a = (int16_t)v;
+        if (bv < v) {   // n increases with t: strict keeps the first
+          bv = v;
+          bn = n;
+        }
+      }
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+      const int ov = __shfl_xor(bv, o), on = __shfl_xor(bn, o);
+      const bool take = ov > bv || (ov == bv && on < bn);
+      bv = take ? ov : bv;
+      bn = take ? on : bn;
+    }
+    if (trace && e == 0 && lane == 0 && it < 4096) {
+      trace[4 * it] = idx;
+      trace[4 * it + 1] = p;
+      trace[4 * it + 2] = bv;
+      trace[4 * it + 3] = bn;
+    }
+    if (bv < threshold) continue;   // wave-uniform (the reduced values)
+    const float a = -tab.cs[2 * bn + 1], b = tab.cs[2 * bn];
+    int x0 = j, y0 = i, dx0, dy0;
+    const bool xflag = fabsf(a) > fabsf(b);
+    if (xflag) {
+      dx0 = a > 0.0f ? 1 : -1;
+      dy0 = __float2int_rn(b * (float)(1 << shift) / fabsf(a));
+      y0 = (y0 << shift) + (1 << (shift - 1));
+    } else {
+      dy0 = b > 0.0f ? 1 : -1;
+      dx0 = __float2int_rn(a * (float)(1 << shift) / fabsf(b));
+      x0 = (x0 << shift) + (1 << (shift - 1));
+    }
+    int ex[2] = {0, 0}, ey[2] = {0, 0};
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      int g = 0, x = x0, y = y0;
+      const int dx = k ? -dx0 : dx0, dy = k ? -dy0 : dy0;
+      for (;; x += dx, y += dy) {
+        const int j1 = xflag ? x : x >> shift, i1 = xflag ? y >> shift : y;
+        if (j1 < 0 || j1 >= w || i1 < 0 || i1 >= h) break;
+        if (on_mask(i1 * w + j1)) {
+          g = 0;
+          ey[k] = i1;
+          ex[k] = j1;
+        } else if (++g > gap) {
+          break;
+        }
+      }
+    }
+    const bool good = abs(ex[1] - ex[0]) >= min_len || abs(ey[1] - ey[0]) >= min_len;
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      int x = x0, y = y0;
+      const int dx = k ? -dx0 : dx0, dy = k ? -dy0 : dy0;
+      for (;; x += dx, y += dy) {
+        const int j1 = xflag ? x : x >> shift, i1 = xflag ? y >> shift : y;
+        const int q = i1 * w + j1;
+        if (on_mask(q)) {
+          if (good) {
+#pragma unroll
+            for (int t = 0; t < 3; ++t) {
+              const int n = lane + 64 * t;
+              if (n < numangle) {
+                const int r = __float2int_rn((float)j1 * c3[t] + (float)i1 * s3[t]) + roff;
+                const int v = (int)acc[n * nr + r] - 1;
+                overflow |= v < -32768;
+                acc[n * nr + r] = (int16_t)v;
+              }
+            }
+          }
+          __builtin_amdgcn_wave_barrier();
+          if (lane == 0) mask[q >> 5] &= ~(1u << (q & 31));
+          __builtin_amdgcn_wave_barrier();
+        }
+        if (i1 == ey[k] && j1 == ex[k]) break;
+      }
+    }
+    if (good) {
+      if (lane == 0) {
+        out[4 * nlines] = ex[0];
+        out[4 * nlines + 1] = ey[0];
+        out[4 * nlines + 2] = ex[1];
+        out[4 * nlines + 3] = ey[1];
+      }
+      if (++nlines >= max_lines) break;
+    }
+    overflow = __ballot(overflow) != 0;
+  }
+  const bool any_over = __ballot(overflow) != 0;
+  if (lane == 0) counts[e] = any_over ? -1 : nlines;
+}
+
 }  // namespace
 
 int dt_render_init(dt_handle* h, const dt_map* map) {
@@ -1199,6 +1378,64 @@ int dt_render(dt_handle* h, const dt_render_io* io, void* stream) {
     return DT_E_HIP;
   }
   return DT_OK;
+}
+
+// diagnostics (tools/hough_debug.py): image 0's visit order into this buffer
+static int32_t* hough_trace = nullptr;
+extern "C" int dt_diag_hough_trace(int32_t* device_buf) {
+  hough_trace = device_buf;
+  return 0;
+}
+
+int dt_hough_lines(const uint8_t* edge, int32_t n, int32_t height, int32_t width,
+                   int32_t threshold, int32_t min_line_length, int32_t max_line_gap,
+                   int32_t max_lines, int32_t* lines, int32_t* counts, void* stream) {
+  if (!edge || !lines || !counts || n < 0 || height <= 0 || width <= 0 || max_lines <= 0 ||
+      height * width > 65536 || threshold < 1)
+    return DT_E_ARG;
+  if (n == 0) return DT_OK;
+  // cv2.HoughLinesP(edge, 1, np.pi / 180, ...): rho and theta as OpenCV's float
+  // parameters, the table as OpenCV builds it (double trig, rounded to float)
+  const float rho = 1.0f, theta = (float)(3.141592653589793 / 180.0);
+  const int numangle = (int)lrint(3.141592653589793 / theta);
+  if (numangle > kHoughAngles) return DT_E_ARG;
+  HoughTab tab{};
+  for (int k = 0; k < numangle; ++k) {
+    tab.cs[2 * k] = (float)(cos((double)k * theta) * (1.0f / rho));
+    tab.cs[2 * k + 1] = (float)(sin((double)k * theta) * (1.0f / rho));
+  }
+  const int numrho = (int)lrintf((float)((width + height) * 2 + 1) / rho);
+  // the rho an h x w image reaches: r(x, y) is linear, so its extremes per
+  // angle are at the corners (the kernel's float math and rounding)
+  int rlo = 1 << 30, rhi = -(1 << 30);
+  for (int k = 0; k < numangle; ++k)
+    for (int cy = 0; cy < 2; ++cy)
+      for (int cx = 0; cx < 2; ++cx) {
+        const float xx = (float)(cx * (width - 1)), yy = (float)(cy * (height - 1));
+        const int r = (int)lrintf(xx * tab.cs[2 * k] + yy * tab.cs[2 * k + 1]);
+        rlo = r < rlo ? r : rlo;
+        rhi = r > rhi ? r : rhi;
+      }
+  const int nr = rhi - rlo + 1;
+  const size_t fixed = (size_t)((2 * numangle * nr + 15) & ~15) +
+                       (((height * width + 31) / 32 * 4 + 15) & ~15);
+  if (fixed + 2 * 1024 > 160 * 1024) return DT_E_ARG;
+  // the point list takes the rest of the LDS (an image with more edge
+  // pixels than that is flagged with counts = -1)
+  int max_pts = (int)((160 * 1024 - fixed) / 2);
+  max_pts = max_pts > height * width ? height * width : max_pts;
+  const size_t lds = fixed + 2 * (size_t)max_pts;
+  static bool attr = false;   // dynamic LDS past 64 KB must be allowed per kernel
+  if (!attr) {
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&hough_kernel),
+                            hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
+      return DT_E_HIP;
+    attr = true;
+  }
+  hipLaunchKernelGGL(hough_kernel, dim3(n), dim3(64), lds, (hipStream_t)stream, edge, height,
+                     width, tab, numangle, numrho, rlo, nr, threshold, min_line_length,
+                     max_line_gap, max_lines, max_pts, lines, counts, hough_trace);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 
 int dt_line_detect(const dt_line_params* p, const uint8_t* bgr, int32_t n, int32_t height,

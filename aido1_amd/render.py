@@ -9,6 +9,8 @@
 - ``line_detect``: LineDetectorHSV (setImage + _colorFilter for white, yellow,
   red + the Canny edge map) on caller-supplied BGR images.
 - ``stack_view``: the Transformer's oldest-first [N,3,120,160] view of the ring.
+- ``hough_lines`` / ``find_normals`` / ``detect_lines``: LineDetectorHSV's
+  _HoughLine, _findNormal and detectLines on those masks.
 """
 import ctypes
 
@@ -139,3 +141,86 @@ def line_detect(bgr, params=None, hsv=False, stream=None):
     if rc != 0:
         raise _lib.DtError('dt_line_detect failed (%d)' % rc)
     return (masks, hsv_t) if hsv else masks
+
+
+# ---- LineDetectorHSV.detectLines (features/line_detector1.py:63-132) ------------------
+# Hough parameters are not in the reference (dtu.Configurable, :18-34); these
+# are the Duckietown line-detector defaults (recalled).
+HOUGH_DEFAULTS = {'hough_threshold': 2, 'hough_min_line_length': 3, 'hough_max_line_gap': 1}
+COLOR_PLANE = {'white': MASK_WHITE, 'yellow': MASK_YELLOW, 'red': MASK_RED}
+
+
+def hough_lines(edge, threshold=2, min_line_length=3, max_line_gap=1, max_lines=512,
+                stream=None):
+    """_HoughLine (:63-70): cv2.HoughLinesP(edge, 1, pi/180, threshold,
+    min_line_length, max_line_gap) on a [n, h, w] uint8 CUDA tensor (non-zero =
+    edge), one wave per image (include/dtsim.h dt_hough_lines).  Returns
+    (lines [n, max_lines, 4] int32 (x1, y1, x2, y2) in OpenCV's order, counts
+    [n] int32, -1 for an image with more edge pixels than the kernel holds)."""
+    L = _lib.lib()
+    if edge.dtype != torch.uint8 or edge.dim() != 3 or not edge.is_cuda:
+        raise ValueError('edge must be a [n,h,w] uint8 CUDA tensor')
+    edge = edge.contiguous()
+    n, h, w = edge.shape
+    lines = torch.zeros(n, max_lines, 4, dtype=torch.int32, device=edge.device)
+    counts = torch.zeros(n, dtype=torch.int32, device=edge.device)
+    s = stream if stream is not None else torch.cuda.current_stream(edge.device).cuda_stream
+    rc = L.dt_hough_lines(ctypes.c_void_p(edge.data_ptr()), n, h, w, int(threshold),
+                          int(min_line_length), int(max_line_gap), int(max_lines),
+                          ctypes.c_void_p(lines.data_ptr()), ctypes.c_void_p(counts.data_ptr()),
+                          ctypes.c_void_p(s))
+    if rc != 0:
+        raise _lib.DtError('dt_hough_lines failed (%d)' % rc)
+    return lines, counts
+
+
+def find_normals(bw, lines, counts):
+    """_findNormal + _correctPixelOrdering (:72-123), batched on the device:
+    bw [n, h, w] (the dilated colour mask), lines [n, L, 4] int32 with counts
+    [n] valid rows.  Returns (lines reordered in place of a copy, centers
+    [n, L, 2] f64, normals [n, L, 2] f64); rows past counts[i] are zero.  The
+    arithmetic is the reference's float64 numpy, operation for operation."""
+    n, nl, _ = lines.shape
+    h, w = bw.shape[1], bw.shape[2]
+    valid = torch.arange(nl, device=lines.device).view(1, nl) < counts.view(n, 1)
+    x1, y1, x2, y2 = (lines[..., k].to(torch.int64) for k in range(4))
+    length = ((x1 - x2) ** 2 + (y1 - y2) ** 2).to(torch.float64).sqrt()
+    length = torch.where(valid, length, torch.ones_like(length))
+    dx = (y2 - y1).to(torch.float64) / length
+    dy = (x1 - x2).to(torch.float64) / length
+    cx = (x1 + x2).to(torch.float64) / 2
+    cy = (y1 + y2).to(torch.float64) / 2
+
+    def bound(v, b):
+        v = v.to(torch.int64)            # .astype('int'): truncation toward zero
+        return v.clamp(0, b - 1)
+    x3, y3 = bound(cx - 3. * dx, w), bound(cy - 3. * dy, h)
+    x4, y4 = bound(cx + 3. * dx, w), bound(cy + 3. * dy, h)
+    img = torch.arange(n, device=lines.device).view(n, 1)
+    sign = ((bw[img, y3, x3] > 0) & (bw[img, y4, x4] == 0)).to(torch.float64) * 2 - 1
+    nx, ny = dx * sign, dy * sign
+    flip = ((x2 - x1).to(torch.float64) * ny - (y2 - y1).to(torch.float64) * nx) > 0
+    out = torch.where(flip.unsqueeze(-1), lines[..., [2, 3, 0, 1]], lines)
+    zero = torch.zeros_like(cx)
+    centers = torch.stack([torch.where(valid, cx, zero), torch.where(valid, cy, zero)], -1)
+    normals = torch.stack([torch.where(valid, nx, zero), torch.where(valid, ny, zero)], -1)
+    out = torch.where(valid.unsqueeze(-1), out, torch.zeros_like(out))
+    return out, centers, normals
+
+
+def detect_lines(masks, color, params=None, max_lines=512):
+    """detectLines(color) (:125-132) for every image of a dt_render /
+    line_detect mask batch [n, 4, h, w]: bw = the dilated colour plane,
+    edge_color = bw AND the edge plane (_colorFilter :55), Hough, normals.
+    Returns a dict with the reference Detections fields (lines, normals, area,
+    centers) plus counts (valid rows per image)."""
+    p = dict(HOUGH_DEFAULTS, **(params or {}))
+    bw = masks[:, COLOR_PLANE[color]]
+    edge_color = bw & masks[:, MASK_EDGES]
+    lines, counts = hough_lines(edge_color, p['hough_threshold'], p['hough_min_line_length'],
+                                p['hough_max_line_gap'], max_lines)
+    if bool((counts < 0).any()):
+        raise _lib.DtError('dt_hough_lines: an image had more edge pixels than fit in LDS')
+    lines, centers, normals = find_normals(bw, lines, counts)
+    return {'lines': lines, 'normals': normals, 'area': bw, 'centers': centers,
+            'counts': counts}

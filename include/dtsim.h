@@ -256,6 +256,20 @@ int dt_set_line_params(dt_handle* h, const dt_line_params* p);
 int dt_line_detect(const dt_line_params* p, const uint8_t* bgr, int32_t n, int32_t height,
                    int32_t width, uint8_t* masks, uint8_t* hsv, void* stream);
 
+/* LineDetectorHSV._HoughLine (features/line_detector1.py:63-70):
+ * cv2.HoughLinesP(edge, rho 1, theta pi/180, threshold, min_line_length,
+ * max_line_gap) on n u8 images (non-zero = edge), e.g. a dt_render mask
+ * plane (edge_color = the colour mask AND the edge mask, :55).  edge device
+ * [n, height, width] u8 (height*width <= 65536 and the accumulator + image
+ * within 160 KB of LDS: 120x160 fits); lines device [n, max_lines, 4] i32
+ * (x1, y1, x2, y2) in OpenCV's order; counts device [n] i32 = lines found,
+ * or -1 when the image had more edge pixels than the kernel's LDS point list
+ * holds (~8k at 120x160; the image's lines are then not valid).  One wave per image; runs on the
+ * current device. */
+int dt_hough_lines(const uint8_t* edge, int32_t n, int32_t height, int32_t width,
+                   int32_t threshold, int32_t min_line_length, int32_t max_line_gap,
+                   int32_t max_lines, int32_t* lines, int32_t* counts, void* stream);
+
 /* ---- state access (parity injection; synchronous) ---------------------- */
 /* x, z, angle: host [n] f64; step_count (Simulator), env_step (wrapper),
  * episode (resets so far, keys the Philox spawn stream): host [n] u32.
