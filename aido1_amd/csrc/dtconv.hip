@@ -20,6 +20,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <cstdlib>
 
 #include "../../include/dtactor.h"
 
@@ -213,19 +214,286 @@ conv1_kernel(int n_items, const float* __restrict__ ring, int slots, int s0, int
   }  // item
 }
 
+// ---- conv1, streaming form (the default; DTCONV1_BANDED=1 selects conv1_kernel) ----
+// A persistent workgroup of kSW waves streams whole samples (n = blockIdx.x,
+// + gridDim.x, ...).  The input rows go through a ring of kSRing rows in LDS
+// (fp16 4-channel pixels as in conv1_kernel), each row read from HBM once per
+// sample (the banded form re-reads 1.375x for its halos).  A step is kSW tiles
+// of 32 consecutive output pixels, one per wave; while a step's MFMAs run, the
+// rows of the step after next are in flight into registers, and the next
+// step's rows (loaded a step earlier) are converted into the ring after the
+// epilogue: one barrier per step (conv32_kernel's schedule).  Two workgroups
+// per CU, so one's barrier leaves the other's MFMAs running.  Reference mode:
+// per-lane Welford statistics over the sample, merged (Chan) into ONE
+// (mean, M2) per sample and channel: dt_conv1_bands() is 1.
+constexpr int kSW = 4;
+constexpr int kSThreads = 64 * kSW;
+constexpr int kSPix = OH * OW;                          // 4389
+constexpr int kSTiles = (kSPix + 31) / 32;              // 138
+constexpr int kSSteps = (kSTiles + kSW - 1) / kSW;      // 35
+constexpr int kSStepPix = 32 * kSW;
+constexpr int kSRing = 32;                              // rows (a power of two)
+constexpr int kSRowB = IW * 8;                          // 1280 B
+constexpr int kSQuads = IW / 4;                         // 4-pixel load items per row
+__host__ __device__ constexpr int s_lo(int j) { return 2 * ((kSStepPix * j) / OW); }
+__host__ __device__ constexpr int s_hi(int j) {
+  const int end = kSStepPix * (j + 1) < kSPix ? kSStepPix * (j + 1) : kSPix;
+  const int r = 2 * ((end - 1) / OW) + 7;
+  return r < IH - 1 ? r : IH - 1;
+}
+__host__ __device__ constexpr int s_first_new(int j) {
+  return (j + 1 == kSSteps) ? 0 : (s_hi(j) + 1 > s_lo(j + 1) ? s_hi(j) + 1 : s_lo(j + 1));
+}
+__host__ __device__ constexpr int s_last_new(int j) {
+  return (j + 1 == kSSteps) ? s_hi(0) : s_hi(j + 1);
+}
+constexpr int s_span() {   // rows one step reads plus the rows its successor adds
+  int m = 0;
+  for (int j = 0; j < kSSteps; ++j) {
+    const int span = (j + 1 < kSSteps) ? s_hi(j + 1) - s_lo(j) + 1 : (IH - s_lo(j)) + s_hi(0) + 1;
+    m = span > m ? span : m;
+  }
+  return m;
+}
+constexpr int s_max_new() {
+  int m = s_hi(0) + 1;
+  for (int j = 0; j < kSSteps; ++j) {
+    const int r = s_last_new(j) - s_first_new(j) + 1;
+    m = r > m ? r : m;
+  }
+  return m;
+}
+static_assert(s_span() <= kSRing, "conv1 stream ring");
+constexpr int kSPre = (s_max_new() * kSQuads + kSThreads - 1) / kSThreads;
+
+template <bool kStats>
+__global__ void __launch_bounds__(kSThreads, 2)   // 2 waves / SIMD: <= 256 registers
+conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, int s2,
+              const half8* __restrict__ wfrag, const float* __restrict__ bias,
+              __half* __restrict__ y, float* __restrict__ partials, float slope) {
+  __shared__ __attribute__((aligned(16))) unsigned char rb[kSRing * kSRowB];
+  __shared__ float red[kSW][CO][3];
+  __shared__ float s_bias[CO];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 31, h = lane >> 5;
+  const int my = n > (int)blockIdx.x ? (n - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
+  const int total = my * kSSteps;
+  if (total == 0) return;
+  auto sample = [&](int k) __attribute__((always_inline)) { return (int)blockIdx.x + k * (int)gridDim.x; };
+  const size_t plane = (size_t)IH * IW;
+
+  // rows r0..r1 of the k-th sample into registers: item q = (row, 4-pixel quad),
+  // one float4 per stacked frame; every load issued on every path (clamped item
+  // and sample), so the compiler's vmcnt waits stay exact
+  auto issue = [&](float4 (&pre)[kSPre][3], int k, int r0, int r1) __attribute__((always_inline)) {
+    const int cnt = (r1 - r0 + 1) * kSQuads;
+    const int ns = sample(k) < n ? sample(k) : n - 1;
+    const float* base = ring + (size_t)ns * slots * plane + (size_t)r0 * IW;
+    const float* p0 = base + (size_t)s0 * plane;
+    const float* p1 = base + (size_t)s1 * plane;
+    const float* p2 = base + (size_t)s2 * plane;
+#pragma unroll
+    for (int i = 0; i < kSPre; ++i) {
+      const int q = tid + i * kSThreads;
+      const int qc = q < cnt ? q : cnt - 1;
+      const int r = qc / kSQuads, qq = qc - r * kSQuads;
+      const int off = r * IW + 4 * qq;
+      pre[i][0] = *reinterpret_cast<const float4*>(p0 + off);
+      pre[i][1] = *reinterpret_cast<const float4*>(p1 + off);
+      pre[i][2] = *reinterpret_cast<const float4*>(p2 + off);
+    }
+  };
+  // fp16 4-channel pixels (channel 3 = 0) into the ring: row R of the stream
+  // (k * IH + r) sits in slot R % kSRing
+  auto commit = [&](const float4 (&pre)[kSPre][3], int k, int r0, int r1) __attribute__((always_inline)) {
+    const int cnt = (r1 - r0 + 1) * kSQuads;
+#pragma unroll
+    for (int i = 0; i < kSPre; ++i) {
+      const int q = tid + i * kSThreads;
+      if (q >= cnt) continue;
+      const int r = q / kSQuads, qq = q - r * kSQuads;
+      const int slot = (k * IH + r0 + r) & (kSRing - 1);
+      const float av[4] = {pre[i][0].x, pre[i][0].y, pre[i][0].z, pre[i][0].w};
+      const float bv[4] = {pre[i][1].x, pre[i][1].y, pre[i][1].z, pre[i][1].w};
+      const float cv[4] = {pre[i][2].x, pre[i][2].y, pre[i][2].z, pre[i][2].w};
+      uint32_t u[8];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const __half2 lo = __floats2half2_rn(av[e], bv[e]);
+        const __half2 hi = __floats2half2_rn(cv[e], 0.0f);
+        u[2 * e] = *reinterpret_cast<const uint32_t*>(&lo);
+        u[2 * e + 1] = *reinterpret_cast<const uint32_t*>(&hi);
+      }
+      u32x4* dst = reinterpret_cast<u32x4*>(rb + slot * kSRowB + 32 * qq);
+      dst[0] = u32x4{u[0], u[1], u[2], u[3]};
+      dst[1] = u32x4{u[4], u[5], u[6], u[7]};
+    }
+  };
+
+  half8 wa[16];
+#pragma unroll
+  for (int s = 0; s < 16; ++s) wa[s] = wfrag[s * 64 + lane];
+  if (tid < CO) s_bias[tid] = bias[tid];
+  float w_cnt = 0.0f, w_mean[16], w_m2[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) w_mean[r] = w_m2[r] = 0.0f;
+
+  auto step = [&](int g, int k, int j, float4 (&nxt)[kSPre][3], const float4 (&cur)[kSPre][3]) __attribute__((always_inline)) {
+    const int ns = sample(k);
+    const bool last_j = j + 1 == kSSteps;
+    const int k1 = last_j ? k + 1 : k, j1 = last_j ? 0 : j + 1;   // step g+1
+    const int k2 = (j1 + 1 == kSSteps) ? k1 + 1 : k1;             // step g+2
+    issue(nxt, k2, s_first_new(j1), s_last_new(j1));
+
+    const int t = kSW * j + wave;
+    const int p = 32 * t + col;
+    const bool valid = p < kSPix;
+    const int pc = valid ? p : 0;
+    const int oy = pc / OW, ox = pc - oy * OW;
+    const int rbase = k * IH + 2 * oy;
+    const int cx = (2 * ox + 2 * h) * 8;
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = s_bias[(r & 3) + 8 * (r >> 2) + 4 * h];
+    // kernel rows in pairs: the next pair's 4 B fragments are in flight while
+    // this pair's MFMAs run
+    half8 bq[2][4];
+    auto ld = [&](half8 (&b)[4], int gy) __attribute__((always_inline)) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int ky = 2 * gy + (i >> 1), kx0 = (i & 1) * 4;
+        const int off = ((rbase + ky) & (kSRing - 1)) * kSRowB + cx + kx0 * 8;
+        b[i] = *reinterpret_cast<const half8*>(rb + off);
+      }
+    };
+    ld(bq[0], 0);
+#pragma unroll
+    for (int gy = 0; gy < 4; ++gy) {
+      if (gy < 3) ld(bq[(gy + 1) & 1], gy + 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wa[4 * gy + i], bq[gy & 1][i], acc, 0, 0, 0);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    float v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = lrelu(acc[r], slope);
+    if (valid) {   // channels (r&3) + 8*(r>>2) + 4h: four groups of 4 consecutive channels
+      __half* dst = y + ((size_t)ns * kSPix + p) * CO;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const __half2 v0 = __floats2half2_rn(v[4 * q + 0], v[4 * q + 1]);
+        const __half2 v1 = __floats2half2_rn(v[4 * q + 2], v[4 * q + 3]);
+        uint2 u;
+        u.x = *reinterpret_cast<const uint32_t*>(&v0);
+        u.y = *reinterpret_cast<const uint32_t*>(&v1);
+        *reinterpret_cast<uint2*>(dst + 8 * q + 4 * h) = u;
+      }
+    }
+    if (kStats) {
+      if (valid) {   // Welford over this lane's pixels
+        w_cnt += 1.0f;
+        const float inv = 1.0f / w_cnt;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float d = v[r] - w_mean[r];
+          w_mean[r] += d * inv;
+          w_m2[r] += d * (v[r] - w_mean[r]);
+        }
+      }
+      if (last_j) {   // the 32 lanes of each half (same 16 channels), then the waves
+#pragma unroll
+        for (int o = 1; o < 32; o <<= 1) {
+          const float nb = __shfl_xor(w_cnt, o, 32);
+          const float tot = w_cnt + nb;
+          const float fa = tot > 0.0f ? nb / tot : 0.0f, fb = tot > 0.0f ? w_cnt * nb / tot : 0.0f;
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const float mb = __shfl_xor(w_mean[r], o, 32), m2b = __shfl_xor(w_m2[r], o, 32);
+            const float d = mb - w_mean[r];
+            w_mean[r] += d * fa;
+            w_m2[r] += m2b + d * d * fb;
+          }
+          w_cnt = tot;
+        }
+        if (col == 0)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
+            const int c = (r & 3) + 8 * (r >> 2) + 4 * h;
+            red[wave][c][0] = w_cnt;
+            red[wave][c][1] = w_mean[r];
+            red[wave][c][2] = w_m2[r];
+          }
+        __syncthreads();
+        if (tid < CO) {
+          float cnt = 0.0f, mean = 0.0f, m2 = 0.0f;
+          for (int w = 0; w < kSW; ++w) {
+            const float nb = red[w][tid][0];
+            if (nb <= 0.0f) continue;
+            const float tot = cnt + nb, d = red[w][tid][1] - mean;
+            mean += d * (nb / tot);
+            m2 += red[w][tid][2] + d * d * (cnt * nb / tot);
+            cnt = tot;
+          }
+          float* pp = partials + ((size_t)ns * CO + tid) * 2;
+          pp[0] = mean;
+          pp[1] = m2;
+        }
+        w_cnt = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) w_mean[r] = w_m2[r] = 0.0f;
+      }
+    }
+    // step g+1's rows into the ring: their slots hold rows no wave reads in
+    // this step; the barrier publishes them for the next
+    if (g + 1 < total) commit(cur, k1, s_first_new(j), s_last_new(j));
+    __syncthreads();
+  };
+
+  // prologue: step 0's rows into the ring, step 1's into registers
+  float4 pa[kSPre][3], pb[kSPre][3];
+  issue(pa, 0, 0, s_hi(0));
+  commit(pa, 0, 0, s_hi(0));
+  if (total > 1) issue(pb, kSSteps == 1 ? 1 : 0, s_first_new(0), s_last_new(0));
+  __syncthreads();
+  int k = 0, j = 0;
+  for (int g = 0; g < total; g += 2) {
+    step(g, k, j, pa, pb);
+    if (++j == kSSteps) { j = 0; ++k; }
+    if (g + 1 < total) {
+      step(g + 1, k, j, pb, pa);
+      if (++j == kSSteps) { j = 0; ++k; }
+    }
+  }
+}
+
+bool conv1_banded() {
+  static int b = -1;
+  if (b < 0) {
+    const char* e = getenv("DTCONV1_BANDED");
+    b = (e && e[0] == '1') ? 1 : 0;
+  }
+  return b == 1;
+}
+int conv1_bands() { return conv1_banded() ? kBands : 1; }
+int conv1_band_rows() { return conv1_banded() ? kBand : OH; }
+
 // Reference mode: merge the bands' (mean, M2) per sample and channel (Chan et
 // al.), then y = (y - mean) / sqrt(var + eps) * gamma + beta in place (biased
 // variance: BatchNorm2d's train-mode normalisation of a batch of one).
 __global__ void __launch_bounds__(256)
 conv1_norm_kernel(__half* __restrict__ y, const float* __restrict__ partials,
-                  const float* __restrict__ gamma, const float* __restrict__ beta, float eps) {
+                  const float* __restrict__ gamma, const float* __restrict__ beta, float eps,
+                  int bands, int band_rows) {
   __shared__ float sc[CO], sh[CO];
   const int n = blockIdx.x, tid = threadIdx.x;
   if (tid < CO) {
-    const float* pp = partials + (size_t)n * kBands * CO * 2;
+    const float* pp = partials + (size_t)n * bands * CO * 2;
     float cnt = 0.0f, mean = 0.0f, m2 = 0.0f;
-    for (int b = 0; b < kBands; ++b) {
-      const float nb = (float)(((OH - b * kBand) < kBand ? (OH - b * kBand) : kBand) * OW);
+    for (int b = 0; b < bands; ++b) {
+      const int rows = (OH - b * band_rows) < band_rows ? (OH - b * band_rows) : band_rows;
+      const float nb = (float)(rows * OW);
       const float mb = pp[(b * CO + tid) * 2], m2b = pp[(b * CO + tid) * 2 + 1];
       const float tot = cnt + nb;
       const float d = mb - mean;
@@ -1161,6 +1429,28 @@ extern "C" int dt_conv1(const float* ring, int32_t n, int32_t slots, const int32
   for (int i = 0; i < 3; ++i)
     if (order[i] < 0 || order[i] >= slots) return DT_E_ARG;
   if (n == 0) return DT_OK;
+  if (!conv1_banded()) {
+    static int grid = 0;   // resident workgroups, persistent
+    if (!grid) {
+      int dev = 0, cus = 256, per = 2;
+      if (hipGetDevice(&dev) == hipSuccess)
+        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, conv1s_kernel<true>, kSThreads, 0) !=
+              hipSuccess || per < 1)
+        per = 1;
+      grid = per * cus;
+    }
+    const int g = n < grid ? n : grid;
+    if (partials)
+      hipLaunchKernelGGL(conv1s_kernel<true>, dim3(g), dim3(kSThreads), 0, (hipStream_t)stream, n,
+                         ring, slots, order[0], order[1], order[2], (const half8*)wfrag, bias,
+                         (__half*)y, partials, slope);
+    else
+      hipLaunchKernelGGL(conv1s_kernel<false>, dim3(g), dim3(kSThreads), 0, (hipStream_t)stream,
+                         n, ring, slots, order[0], order[1], order[2], (const half8*)wfrag, bias,
+                         (__half*)y, nullptr, slope);
+    return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+  }
   const int items = n * kBands;
   const int grid = items < persistent_grid() ? items : persistent_grid();
   hipLaunchKernelGGL(conv1_kernel, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, items,
@@ -1174,11 +1464,11 @@ extern "C" int dt_conv1_norm(void* y, int32_t n, const float* partials, const fl
   if (!y || !partials || !gamma || !beta || n < 0) return DT_E_ARG;
   if (n == 0) return DT_OK;
   hipLaunchKernelGGL(conv1_norm_kernel, dim3(n), dim3(256), 0, (hipStream_t)stream, (__half*)y,
-                     partials, gamma, beta, eps);
+                     partials, gamma, beta, eps, conv1_bands(), conv1_band_rows());
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 
-extern "C" int32_t dt_conv1_bands(void) { return kBands; }
+extern "C" int32_t dt_conv1_bands(void) { return conv1_bands(); }
 
 #ifdef DTSIM_STAMPS
 extern "C" int dt_diag_c12stamps(unsigned long long* out) {
@@ -1224,7 +1514,11 @@ extern "C" int dt_conv32(int32_t layer, int32_t n, const void* x, const void* wf
   switch (layer) {
     case 2:   // 57x77 -> 27x37, stride 2; input norm from conv1's bands
       if (in != (part != nullptr)) return DT_E_ARG;
-      return in ? launch_conv32<57, 77, 27, 37, 2, kConv2Waves, 1, 0, kBand>(
+      if (in && conv1_banded())
+        return launch_conv32<57, 77, 27, 37, 2, kConv2Waves, 1, 0, kBand>(
+            n, x, wfrag, bias, prev_part, in_gamma, in_beta, in_eps, y, part, nullptr, nullptr,
+            0.f, slope, s);
+      return in ? launch_conv32<57, 77, 27, 37, 2, kConv2Waves, 1, 0, 57>(
                       n, x, wfrag, bias, prev_part, in_gamma, in_beta, in_eps, y, part,
                       nullptr, nullptr, 0.f, slope, s)
                 : launch_conv32<57, 77, 27, 37, 2, kConv2Waves, 0, 1>(
