@@ -48,6 +48,39 @@ using f32x16 = __attribute__((ext_vector_type(16))) float;
 using u32x4 = __attribute__((ext_vector_type(4))) uint32_t;
 
 __device__ __forceinline__ float lrelu(float v, float s) { return v > 0.0f ? v : v * s; }
+// the same for 0 <= s <= 1 as two instructions (a multiply and a max)
+__device__ __forceinline__ float lrelu2(float v, float s) { return fmaxf(v, v * s); }
+
+// One pixel's 32 channels as fp16 NHWC from a 32x32x16 MFMA tile (lane = pixel
+// column, register r = channel (r&3) + 8*(r>>2) + 4h): v_permlane32_swap pairs
+// the two half-waves' 4-channel groups, so each lane stores two 16-B chunks
+// (channels 16m + 8h .. +7 at byte 32m + 16h) instead of four 8-B ones.  Every
+// lane runs the swaps (they exchange across the half-waves); `valid` lanes store.
+__device__ __forceinline__ void store_px32(__half* px, const float (&v)[16], int h, bool valid) {
+  uint32_t u[4][2];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const __half2 v0 = __floats2half2_rn(v[4 * q + 0], v[4 * q + 1]);
+    const __half2 v1 = __floats2half2_rn(v[4 * q + 2], v[4 * q + 3]);
+    u[q][0] = *reinterpret_cast<const uint32_t*>(&v0);
+    u[q][1] = *reinterpret_cast<const uint32_t*>(&v1);
+  }
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const auto r = __builtin_amdgcn_permlane32_swap(u[2 * m][e], u[2 * m + 1][e], false, false);
+      u[2 * m][e] = r[0];
+      u[2 * m + 1][e] = r[1];
+    }
+  if (valid) {
+    unsigned char* dst = reinterpret_cast<unsigned char*>(px);
+#pragma unroll
+    for (int m = 0; m < 2; ++m)
+      *reinterpret_cast<uint4*>(dst + 32 * m + 16 * h) =
+          make_uint4(u[2 * m][0], u[2 * m][1], u[2 * m + 1][0], u[2 * m + 1][1]);
+  }
+}
 
 // Persistent kernels: two workgroups per CU (the VGPR budget of these kernels),
 // each striding over (sample, band) items with its weights held in registers.
@@ -282,22 +315,31 @@ conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, 
   auto sample = [&](int k) __attribute__((always_inline)) { return (int)blockIdx.x + k * (int)gridDim.x; };
   const size_t plane = (size_t)IH * IW;
 
-  // rows r0..r1 of the k-th sample into registers: item q = (row, 4-pixel quad),
-  // one float4 per stacked frame; every load issued on every path (clamped item
-  // and sample), so the compiler's vmcnt waits stay exact
+  // a thread's load items are fixed (row r_i, quad qq_i of the step's range);
+  // only the range start and length change per step
+  int it_r[kSPre], it_off[kSPre], it_lds[kSPre];
+#pragma unroll
+  for (int i = 0; i < kSPre; ++i) {
+    const int q = tid + i * kSThreads;
+    it_r[i] = q / kSQuads;
+    it_off[i] = it_r[i] * IW + 4 * (q - it_r[i] * kSQuads);
+    it_lds[i] = 32 * (q - it_r[i] * kSQuads);
+  }
+  // rows r0..r1 of the k-th sample into registers, one float4 per stacked
+  // frame; every load issued on every path (items past the range re-load the
+  // range's first quad, the sample is clamped), so the compiler's vmcnt waits
+  // stay exact.  A step may add no rows (r0 = r1 + 1, up to IH at the end of a
+  // sample): its loads then read the sample's row 0, never past the plane.
   auto issue = [&](float4 (&pre)[kSPre][3], int k, int r0, int r1) __attribute__((always_inline)) {
-    const int cnt = (r1 - r0 + 1) * kSQuads;
+    const int rows = r1 - r0 + 1;
     const int ns = sample(k) < n ? sample(k) : n - 1;
-    const float* base = ring + (size_t)ns * slots * plane + (size_t)r0 * IW;
+    const float* base = ring + (size_t)ns * slots * plane + (size_t)(rows > 0 ? r0 : 0) * IW;
     const float* p0 = base + (size_t)s0 * plane;
     const float* p1 = base + (size_t)s1 * plane;
     const float* p2 = base + (size_t)s2 * plane;
 #pragma unroll
     for (int i = 0; i < kSPre; ++i) {
-      const int q = tid + i * kSThreads;
-      const int qc = q < cnt ? q : cnt - 1;
-      const int r = qc / kSQuads, qq = qc - r * kSQuads;
-      const int off = r * IW + 4 * qq;
+      const int off = it_r[i] < rows ? it_off[i] : 0;
       pre[i][0] = *reinterpret_cast<const float4*>(p0 + off);
       pre[i][1] = *reinterpret_cast<const float4*>(p1 + off);
       pre[i][2] = *reinterpret_cast<const float4*>(p2 + off);
@@ -306,13 +348,11 @@ conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, 
   // fp16 4-channel pixels (channel 3 = 0) into the ring: row R of the stream
   // (k * IH + r) sits in slot R % kSRing
   auto commit = [&](const float4 (&pre)[kSPre][3], int k, int r0, int r1) __attribute__((always_inline)) {
-    const int cnt = (r1 - r0 + 1) * kSQuads;
+    const int rows = r1 - r0 + 1;
 #pragma unroll
     for (int i = 0; i < kSPre; ++i) {
-      const int q = tid + i * kSThreads;
-      if (q >= cnt) continue;
-      const int r = q / kSQuads, qq = q - r * kSQuads;
-      const int slot = (k * IH + r0 + r) & (kSRing - 1);
+      if (it_r[i] >= rows) continue;
+      const int slot = (k * IH + r0 + it_r[i]) & (kSRing - 1);
       const float av[4] = {pre[i][0].x, pre[i][0].y, pre[i][0].z, pre[i][0].w};
       const float bv[4] = {pre[i][1].x, pre[i][1].y, pre[i][1].z, pre[i][1].w};
       const float cv[4] = {pre[i][2].x, pre[i][2].y, pre[i][2].z, pre[i][2].w};
@@ -324,7 +364,7 @@ conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, 
         u[2 * e] = *reinterpret_cast<const uint32_t*>(&lo);
         u[2 * e + 1] = *reinterpret_cast<const uint32_t*>(&hi);
       }
-      u32x4* dst = reinterpret_cast<u32x4*>(rb + slot * kSRowB + 32 * qq);
+      u32x4* dst = reinterpret_cast<u32x4*>(rb + slot * kSRowB + it_lds[i]);
       dst[0] = u32x4{u[0], u[1], u[2], u[3]};
       dst[1] = u32x4{u[4], u[5], u[6], u[7]};
     }
@@ -343,7 +383,7 @@ conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, 
     const bool last_j = j + 1 == kSSteps;
     const int k1 = last_j ? k + 1 : k, j1 = last_j ? 0 : j + 1;   // step g+1
     const int k2 = (j1 + 1 == kSSteps) ? k1 + 1 : k1;             // step g+2
-    issue(nxt, k2, s_first_new(j1), s_last_new(j1));
+    if (!(DTCONV_SKIP & 1)) issue(nxt, k2, s_first_new(j1), s_last_new(j1));
 
     const int t = kSW * j + wave;
     const int p = 32 * t + col;
@@ -366,9 +406,9 @@ conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, 
         b[i] = *reinterpret_cast<const half8*>(rb + off);
       }
     };
-    ld(bq[0], 0);
+    if (!(DTCONV_SKIP & 2)) ld(bq[0], 0);
 #pragma unroll
-    for (int gy = 0; gy < 4; ++gy) {
+    for (int gy = 0; gy < 4 && !(DTCONV_SKIP & 2); ++gy) {
       if (gy < 3) ld(bq[(gy + 1) & 1], gy + 1);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -378,23 +418,12 @@ conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, 
     }
     float v[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = lrelu(acc[r], slope);
-    if (valid) {   // channels (r&3) + 8*(r>>2) + 4h: four groups of 4 consecutive channels
-      __half* dst = y + ((size_t)ns * kSPix + p) * CO;
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const __half2 v0 = __floats2half2_rn(v[4 * q + 0], v[4 * q + 1]);
-        const __half2 v1 = __floats2half2_rn(v[4 * q + 2], v[4 * q + 3]);
-        uint2 u;
-        u.x = *reinterpret_cast<const uint32_t*>(&v0);
-        u.y = *reinterpret_cast<const uint32_t*>(&v1);
-        *reinterpret_cast<uint2*>(dst + 8 * q + 4 * h) = u;
-      }
-    }
-    if (kStats) {
+    for (int r = 0; r < 16; ++r) v[r] = lrelu2(acc[r], slope);
+    if (!(DTCONV_SKIP & 4)) store_px32(y + ((size_t)ns * kSPix + pc) * CO, v, h, valid);
+    if (kStats && !(DTCONV_SKIP & 8)) {
       if (valid) {   // Welford over this lane's pixels
         w_cnt += 1.0f;
-        const float inv = 1.0f / w_cnt;
+        const float inv = __builtin_amdgcn_rcpf(w_cnt);   // 1 ulp: an O(1e-7) relative weight error
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const float d = v[r] - w_mean[r];
@@ -447,7 +476,7 @@ conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, 
     }
     // step g+1's rows into the ring: their slots hold rows no wave reads in
     // this step; the barrier publishes them for the next
-    if (g + 1 < total) commit(cur, k1, s_first_new(j), s_last_new(j));
+    if (g + 1 < total && !(DTCONV_SKIP & 16)) commit(cur, k1, s_first_new(j), s_last_new(j));
     __syncthreads();
   };
 
@@ -457,6 +486,11 @@ conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, 
   commit(pa, 0, 0, s_hi(0));
   if (total > 1) issue(pb, kSSteps == 1 ? 1 : 0, s_first_new(0), s_last_new(0));
   __syncthreads();
+  // drain the prologue's loads: they land in other registers than the loop's
+  // prefetch sets, and without this the compiler's wait analysis merges that
+  // state into the loop header and waits for the previous step's prefetch
+  // before every step's MFMAs (instead of at the commit that reads it)
+  __builtin_amdgcn_s_waitcnt(0);
   int k = 0, j = 0;
   for (int g = 0; g < total; g += 2) {
     step(g, k, j, pa, pb);
@@ -782,22 +816,11 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
     if (stats2) stats_merge(k2);   // read by step g+2, after two barriers
     float v[16];
 #pragma unroll
-    for (int r = 0; r < 16; ++r) v[r] = lrelu(acc[r], slope);
+    for (int r = 0; r < 16; ++r) v[r] = lrelu2(acc[r], slope);
 
     // epilogue
     if (kOut <= 1) {
-      if (valid && !(DTCONV_SKIP & 4)) {
-        __half* dst = y + ((size_t)ns * G::kPix + p) * CO;
-#pragma unroll
-        for (int q = 0; q < 4; ++q) {
-          const __half2 v0 = __floats2half2_rn(v[4 * q + 0], v[4 * q + 1]);
-          const __half2 v1 = __floats2half2_rn(v[4 * q + 2], v[4 * q + 3]);
-          uint2 u;
-          u.x = *reinterpret_cast<const uint32_t*>(&v0);
-          u.y = *reinterpret_cast<const uint32_t*>(&v1);
-          *reinterpret_cast<uint2*>(dst + 8 * q + 4 * h) = u;
-        }
-      }
+      if (!(DTCONV_SKIP & 4)) store_px32(y + ((size_t)ns * G::kPix + pc) * CO, v, h, valid);
       if (kOut == 0 && valid && !(DTCONV_SKIP & 8)) {   // Welford over this lane's pixels
         w_cnt += 1.0f;
         const float inv = 1.0f / w_cnt;
