@@ -30,6 +30,10 @@
 #ifndef DTCONV_SKIP
 #define DTCONV_SKIP 0
 #endif
+// conv1s_kernel: B-fragment groups (4 ds_read_b128 each) in flight, 2..4
+#ifndef DTCONV1_BDEPTH
+#define DTCONV1_BDEPTH 2
+#endif
 
 namespace {
 
@@ -395,9 +399,10 @@ conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, 
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = s_bias[(r & 3) + 8 * (r >> 2) + 4 * h];
-    // kernel rows in pairs: the next pair's 4 B fragments are in flight while
-    // this pair's MFMAs run
-    half8 bq[2][4];
+    // kernel rows in pairs (4 B fragments a group): DTCONV1_BDEPTH groups in
+    // flight while a group's MFMAs run
+    constexpr int kBD = DTCONV1_BDEPTH;
+    half8 bq[kBD][4];
     auto ld = [&](half8 (&b)[4], int gy) __attribute__((always_inline)) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
@@ -406,14 +411,22 @@ conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, 
         b[i] = *reinterpret_cast<const half8*>(rb + off);
       }
     };
-    if (!(DTCONV_SKIP & 2)) ld(bq[0], 0);
+    if (DTCONV_SKIP & 32) {   // diagnostic: MFMAs on fragments not read from LDS
+#pragma unroll
+      for (int q = 0; q < kBD; ++q)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) bq[q][i] = wa[i];
+    }
+    if (!(DTCONV_SKIP & 34))
+#pragma unroll
+      for (int gy = 0; gy < kBD - 1; ++gy) ld(bq[gy], gy);
 #pragma unroll
     for (int gy = 0; gy < 4 && !(DTCONV_SKIP & 2); ++gy) {
-      if (gy < 3) ld(bq[(gy + 1) & 1], gy + 1);
+      if (gy + kBD - 1 < 4 && !(DTCONV_SKIP & 32)) ld(bq[(gy + kBD - 1) % kBD], gy + kBD - 1);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wa[4 * gy + i], bq[gy & 1][i], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wa[4 * gy + i], bq[gy % kBD][i], acc, 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
     float v[16];

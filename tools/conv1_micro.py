@@ -10,9 +10,11 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-OUT = os.path.join(ROOT, 'build', 'conv1_variants')
+OUT = os.path.join(ROOT, 'build', 'conv1_variants' + os.environ.get('CONV1_TAG', ''))
 SKIPS = {'full': 0, 'no_prefetch': 1, 'no_mma': 2, 'no_store': 4, 'no_stats': 8,
-         'no_commit': 16, 'only_mma': 1 | 4 | 8 | 16, 'only_io': 2 | 8 | 16, 'none': 31}
+         'no_commit': 16, 'only_mma': 1 | 4 | 8 | 16, 'only_io': 2 | 8 | 16, 'none': 31,
+         'no_ldsread': 32}
+ONLY = [v for v in os.environ.get('CONV1_ONLY', '').split(',') if v]   # subset of SKIPS
 
 
 def build(defines):
@@ -21,6 +23,8 @@ def build(defines):
     os.makedirs(OUT, exist_ok=True)
     src = os.path.join(ROOT, 'aido1_amd', 'csrc', 'dtconv.hip')
     for name, bits in SKIPS.items():
+        if ONLY and name not in ONLY:
+            continue
         so = os.path.join(OUT, 'libconv1_%s.so' % name)
         subprocess.check_call([_lib.HIPCC] + _lib.HIP_FLAGS + ['-DDTCONV_SKIP=%d' % bits] +
                               ['-D' + d for d in defines] + ['-o', so, src])
@@ -38,9 +42,16 @@ def run(n, reps):
     part = torch.empty(n, 8, 32, 2, device=dev)
     o = (ctypes.c_int32 * 3)(0, 1, 2)
     s = torch.cuda.current_stream().cuda_stream
+    if os.environ.get('CONV1_DATA') == 'zero':     # same work, quiet operands
+        ring.zero_()
+        wf.zero_()
+    elif os.environ.get('CONV1_DATA') == 'frames':  # piecewise-constant, like rendered frames
+        ring.copy_((ring * 4).floor() / 4)
     byts = n * (3 * 120 * 160 * 4 + 57 * 77 * 32 * 2)
     print('%-12s %9s %9s' % ('variant', 'conv1 us', 'TB/s'))
     for name in SKIPS:
+        if ONLY and name not in ONLY:
+            continue
         L = ctypes.CDLL(os.path.join(OUT, 'libconv1_%s.so' % name))
         L.dt_conv1.argtypes = [ctypes.c_void_p, ctypes.c_int32, ctypes.c_int32,
                                ctypes.POINTER(ctypes.c_int32)] + [ctypes.c_void_p] * 4 + \
