@@ -40,7 +40,11 @@ int dt_sample_norm(const void* x, void* y, int32_t n, int32_t hw, int32_t c, con
  *   bias      device f32 [32]
  *   y         device fp16 [n, 57, 77, 32] (NHWC)
  *   partials  device f32 [n, dt_conv1_bands(), 32, 2] or NULL: per band and
- *             channel (mean, M2) of the LeakyReLU outputs, for dt_conv1_norm */
+ *             channel (mean, M2) of the LeakyReLU outputs, for dt_conv1_norm
+ *             and dt_conv32 layer 2.  dt_conv1_bands() is 1 for the default
+ *             streaming kernel (one band = the whole 57-row sample) and 8 for
+ *             the banded kernel (8-row bands; DTCONV1_BANDED=1 in the
+ *             environment, read once per process). */
 int dt_conv1(const float* ring, int32_t n, int32_t slots, const int32_t* order, const void* wfrag,
              const float* bias, void* y, float* partials, float slope, void* stream);
 
