@@ -99,18 +99,20 @@ def test_reference_mode_matches_per_sample_train_mode(gpu):
     assert torch.max(torch.abs(h(frames).cpu() - ref)) < 1.5e-2
 
 
-@pytest.mark.parametrize('slots,order', [(3, [0, 1, 2]), (4, [2, 3, 0])])
-def test_conv1_kernel_matches_conv2d(gpu, slots, order):
+@pytest.mark.parametrize('slots,order,n', [(3, [0, 1, 2], 37), (4, [2, 3, 0], 37),
+                                           (4, [1, 2, 3], 1100)])
+def test_conv1_kernel_matches_conv2d(gpu, slots, order, n):
     """dt_conv1 (MFMA implicit GEMM on the ring) vs conv2d + LeakyReLU in f32 on
     the same fp16-rounded inputs and weights; band statistics and the merged
-    per-sample norm vs float64."""
+    per-sample norm vs float64.  n = 1100 is more samples than the streaming
+    kernel's resident workgroups, so each workgroup streams several samples
+    through its row ring."""
     import ctypes
     import torch.nn.functional as F
     from aido1_amd import _lib
     from aido1_amd.actor import conv1_fragments
     L = _lib.lib()
     torch.manual_seed(1)
-    n = 37
     ring = torch.rand(n, slots, 120, 160, device=gpu)
     w = torch.randn(32, 3, 8, 8, device=gpu) * 0.08
     b = torch.randn(32, device=gpu) * 0.2
