@@ -58,9 +58,17 @@ __device__ __forceinline__ float lrelu2(float v, float s) { return fmaxf(v, v * 
 // One pixel's 32 channels as fp16 NHWC from a 32x32x16 MFMA tile (lane = pixel
 // column, register r = channel (r&3) + 8*(r>>2) + 4h): v_permlane32_swap pairs
 // the two half-waves' 4-channel groups, so each lane stores two 16-B chunks
-// (channels 16m + 8h .. +7 at byte 32m + 16h) instead of four 8-B ones.  Every
-// lane runs the swaps (they exchange across the half-waves); `valid` lanes store.
-__device__ __forceinline__ void store_px32(__half* px, const float (&v)[16], int h, bool valid) {
+// (channels 16m + 8h .. +7 at byte 32m + 16h) instead of four 8-B ones.
+// `sample` is the sample's first element (wave-uniform), `px` the lane's pixel.
+// Branch-free: the stores are buffer stores over the sample's bytes and an
+// invalid lane's offset lies past them (the hardware drops it), so every path
+// issues the same memory instructions and the compiler's vmcnt waits for the
+// next prefetch stay exact (an `if (valid)` around the stores made them wait
+// for the stores too).
+template <int kPix>
+__device__ __forceinline__ void store_px32(__half* sample, int px, const float (&v)[16], int h,
+                                           bool valid) {
+  constexpr int kBytes = kPix * 32 * 2;
   uint32_t u[4][2];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
@@ -77,12 +85,13 @@ __device__ __forceinline__ void store_px32(__half* px, const float (&v)[16], int
       u[2 * m][e] = r[0];
       u[2 * m + 1][e] = r[1];
     }
-  if (valid) {
-    unsigned char* dst = reinterpret_cast<unsigned char*>(px);
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(sample), 0, kBytes,
+                                                      0x00020000);
+  const int off = valid ? px * 64 + 16 * h : kBytes;
 #pragma unroll
-    for (int m = 0; m < 2; ++m)
-      *reinterpret_cast<uint4*>(dst + 32 * m + 16 * h) =
-          make_uint4(u[2 * m][0], u[2 * m][1], u[2 * m + 1][0], u[2 * m + 1][1]);
+  for (int m = 0; m < 2; ++m) {
+    const u32x4 d = {u[2 * m][0], u[2 * m][1], u[2 * m + 1][0], u[2 * m + 1][1]};
+    __builtin_amdgcn_raw_buffer_store_b128(d, rsrc, off + 32 * m, 0, 0);
   }
 }
 
@@ -432,7 +441,7 @@ conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, 
     float v[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = lrelu2(acc[r], slope);
-    if (!(DTCONV_SKIP & 4)) store_px32(y + ((size_t)ns * kSPix + pc) * CO, v, h, valid);
+    if (!(DTCONV_SKIP & 4)) store_px32<kSPix>(y + (size_t)ns * kSPix * CO, pc, v, h, valid);
     if (kStats && !(DTCONV_SKIP & 8)) {
       if (valid) {   // Welford over this lane's pixels
         w_cnt += 1.0f;
@@ -833,7 +842,7 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
 
     // epilogue
     if (kOut <= 1) {
-      if (!(DTCONV_SKIP & 4)) store_px32(y + ((size_t)ns * G::kPix + pc) * CO, v, h, valid);
+      if (!(DTCONV_SKIP & 4)) store_px32<G::kPix>(y + (size_t)ns * G::kPix * CO, pc, v, h, valid);
       if (kOut == 0 && valid && !(DTCONV_SKIP & 8)) {   // Welford over this lane's pixels
         w_cnt += 1.0f;
         const float inv = 1.0f / w_cnt;
@@ -923,13 +932,17 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
         }
         __syncthreads();
       }
-      if (valid) {
-        __half* dst = y + (size_t)ns * CO * G::kPix;
+      {   // branch-free (see store_px32): invalid lanes store past the sample
+        constexpr int kBytes = G::kPix * CO * 2;
+        const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+            reinterpret_cast<void*>(y + (size_t)ns * CO * G::kPix), 0, kBytes, 0x00020000);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int c = (r & 3) + 8 * (r >> 2) + 4 * h;
           const float o = kOut == 2 ? v[r] * s_rstd[c] + s_mean[c] : v[r];
-          dst[(size_t)c * G::kPix + p] = __float2half(o);
+          const __half ho = __float2half(o);
+          __builtin_amdgcn_raw_buffer_store_b16(*reinterpret_cast<const unsigned short*>(&ho), rsrc,
+                                                valid ? (c * G::kPix + p) * 2 : kBytes, 0, 0);
         }
       }
     }
