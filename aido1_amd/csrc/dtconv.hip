@@ -898,37 +898,44 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
       }
     } else {   // the whole sample is in this step: BatchNorm of a batch of one, flatten
       if (kOut == 2) {
-        // pass 1: mean
+        // per wave, two passes over its own 32 pixels (shuffles only: exact
+        // mean, then M2 about it); the waves' (n, mean, M2) merged with
+        // Chan's formula by threads < CO: two barriers a sample, not four
+        float nw = valid ? 1.0f : 0.0f;
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1) nw += __shfl_xor(nw, o, 32);
+        const float inw = nw > 0.0f ? 1.0f / nw : 0.0f;
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           float sum = valid ? v[r] : 0.0f;
 #pragma unroll
           for (int o = 16; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 32);
-          if (col == 0) red[wave][(r & 3) + 8 * (r >> 2) + 4 * h][0] = sum;
-        }
-        __syncthreads();
-        if (tid < CO) {
-          float sum = 0.0f;
-          for (int w = 0; w < NW; ++w) sum += red[w][tid][0];
-          s_mean[tid] = sum / (float)G::kPix;
-        }
-        __syncthreads();
-        // pass 2: M2 about the mean
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-          const float d = v[r] - s_mean[(r & 3) + 8 * (r >> 2) + 4 * h];
-          float m2 = valid ? d * d : 0.0f;
+          const float mw = sum * inw;
+          const float d = valid ? v[r] - mw : 0.0f;
+          float m2 = d * d;
 #pragma unroll
           for (int o = 16; o > 0; o >>= 1) m2 += __shfl_xor(m2, o, 32);
-          if (col == 0) red[wave][(r & 3) + 8 * (r >> 2) + 4 * h][1] = m2;
+          if (col == 0) {
+            const int c = (r & 3) + 8 * (r >> 2) + 4 * h;
+            red[wave][c][0] = nw;
+            red[wave][c][1] = mw;
+            red[wave][c][2] = m2;
+          }
         }
         __syncthreads();
         if (tid < CO) {
-          float m2 = 0.0f;
-          for (int w = 0; w < NW; ++w) m2 += red[w][tid][1];
+          float cnt = 0.0f, mean = 0.0f, m2 = 0.0f;
+          for (int w = 0; w < NW; ++w) {
+            const float nb = red[w][tid][0];
+            if (nb <= 0.0f) continue;
+            const float tot = cnt + nb, d = red[w][tid][1] - mean;
+            mean += d * (nb / tot);
+            m2 += red[w][tid][2] + d * d * (cnt * nb / tot);
+            cnt = tot;
+          }
           const float sc = out_gamma[tid] / sqrtf(m2 / (float)G::kPix + out_eps);
           s_rstd[tid] = sc;
-          s_mean[tid] = out_beta[tid] - s_mean[tid] * sc;   // now the shift
+          s_mean[tid] = out_beta[tid] - mean * sc;   // the shift
         }
         __syncthreads();
       }
