@@ -30,9 +30,14 @@
 #ifndef DTCONV_SKIP
 #define DTCONV_SKIP 0
 #endif
-// conv1s_kernel: B-fragment groups (4 ds_read_b128 each) in flight, 2..4
+// conv1s_kernel: B-fragment groups in flight, 2..4
 #ifndef DTCONV1_BDEPTH
 #define DTCONV1_BDEPTH 2
+#endif
+// conv1s_kernel's reduction layout: 1 = K 192 (3-channel pixels, 12 MFMAs a
+// tile), 0 = K 256 (4-channel pixels with a zero channel, 16 MFMAs a tile)
+#ifndef DTCONV1_K192
+#define DTCONV1_K192 1
 #endif
 
 namespace {
@@ -279,7 +284,11 @@ constexpr int kSTiles = (kSPix + 31) / 32;              // 138
 constexpr int kSSteps = (kSTiles + kSW - 1) / kSW;      // 35
 constexpr int kSStepPix = 32 * kSW;
 constexpr int kSRing = 32;                              // rows (a power of two)
-constexpr int kSRowB = IW * 8;                          // 1280 B
+constexpr bool kK192 = DTCONV1_K192 != 0;
+constexpr int kSPxB = kK192 ? 6 : 8;                    // bytes a ring pixel: fp16 x 3 (x 4)
+constexpr int kSRowB = IW * kSPxB;                      // 960 (1280) B
+constexpr int kSMfma = kK192 ? 12 : 16;                 // MFMAs a tile
+constexpr int kSGrp = kK192 ? 3 : 4;                    // MFMAs a B-fragment group
 constexpr int kSQuads = IW / 4;                         // 4-pixel load items per row
 __host__ __device__ constexpr int s_lo(int j) { return 2 * ((kSStepPix * j) / OW); }
 __host__ __device__ constexpr int s_hi(int j) {
@@ -336,7 +345,7 @@ conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, 
     const int q = tid + i * kSThreads;
     it_r[i] = q / kSQuads;
     it_off[i] = it_r[i] * IW + 4 * (q - it_r[i] * kSQuads);
-    it_lds[i] = 32 * (q - it_r[i] * kSQuads);
+    it_lds[i] = 4 * kSPxB * (q - it_r[i] * kSQuads);
   }
   // rows r0..r1 of the k-th sample into registers, one float4 per stacked
   // frame; every load issued on every path (items past the range re-load the
@@ -369,23 +378,56 @@ conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, 
       const float av[4] = {pre[i][0].x, pre[i][0].y, pre[i][0].z, pre[i][0].w};
       const float bv[4] = {pre[i][1].x, pre[i][1].y, pre[i][1].z, pre[i][1].w};
       const float cv[4] = {pre[i][2].x, pre[i][2].y, pre[i][2].z, pre[i][2].w};
-      uint32_t u[8];
+      if constexpr (kK192) {
+        // 4 pixels x 3 channels, pixel-major: (a0 b0)(c0 a1)(b1 c1)(a2 b2)(c2 a3)(b3 c3)
+        const float f[12] = {av[0], bv[0], cv[0], av[1], bv[1], cv[1],
+                             av[2], bv[2], cv[2], av[3], bv[3], cv[3]};
+        uint32_t u[6];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const __half2 lo = __floats2half2_rn(av[e], bv[e]);
-        const __half2 hi = __floats2half2_rn(cv[e], 0.0f);
-        u[2 * e] = *reinterpret_cast<const uint32_t*>(&lo);
-        u[2 * e + 1] = *reinterpret_cast<const uint32_t*>(&hi);
+        for (int e = 0; e < 6; ++e) {
+          const __half2 hv = __floats2half2_rn(f[2 * e], f[2 * e + 1]);
+          u[e] = *reinterpret_cast<const uint32_t*>(&hv);
+        }
+        uint2* dst = reinterpret_cast<uint2*>(rb + slot * kSRowB + it_lds[i]);   // 8-B aligned
+        dst[0] = make_uint2(u[0], u[1]);
+        dst[1] = make_uint2(u[2], u[3]);
+        dst[2] = make_uint2(u[4], u[5]);
+      } else {
+        uint32_t u[8];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const __half2 lo = __floats2half2_rn(av[e], bv[e]);
+          const __half2 hi = __floats2half2_rn(cv[e], 0.0f);
+          u[2 * e] = *reinterpret_cast<const uint32_t*>(&lo);
+          u[2 * e + 1] = *reinterpret_cast<const uint32_t*>(&hi);
+        }
+        u32x4* dst = reinterpret_cast<u32x4*>(rb + slot * kSRowB + it_lds[i]);
+        dst[0] = u32x4{u[0], u[1], u[2], u[3]};
+        dst[1] = u32x4{u[4], u[5], u[6], u[7]};
       }
-      u32x4* dst = reinterpret_cast<u32x4*>(rb + slot * kSRowB + it_lds[i]);
-      dst[0] = u32x4{u[0], u[1], u[2], u[3]};
-      dst[1] = u32x4{u[4], u[5], u[6], u[7]};
     }
   };
 
-  half8 wa[16];
+  // A fragments.  K 192: MFMA s covers kernel rows ky = 2(s/3) + h (h = the
+  // lane half) and 8 of the 24 (kx, c) values of a row, t = 8(s%3) + j ->
+  // kx = t/3, c = t%3: a lane's 8 k are 16 contiguous bytes of a ring row.
+  // Gathered once from the dt_conv1 fragment layout (include/dtactor.h).
+  half8 wa[kSMfma];
+  if constexpr (kK192) {
+    const _Float16* wh = reinterpret_cast<const _Float16*>(wfrag);
+    const int co = lane & 31, hh = lane >> 5;
 #pragma unroll
-  for (int s = 0; s < 16; ++s) wa[s] = wfrag[s * 64 + lane];
+    for (int s = 0; s < kSMfma; ++s)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int ky = 2 * (s / 3) + hh, t = 8 * (s % 3) + e, kx = t / 3, c = t % 3;
+        const int s1 = 2 * ky + kx / 4, l1 = co + 32 * ((kx & 3) >> 1), j1 = 4 * (kx & 1) + c;
+        wa[s][e] = wh[(s1 * 64 + l1) * 8 + j1];
+      }
+  } else {
+#pragma unroll
+    for (int s = 0; s < kSMfma; ++s) wa[s] = wfrag[s * 64 + lane];
+  }
   if (tid < CO) s_bias[tid] = bias[tid];
   float w_cnt = 0.0f, w_mean[16], w_m2[16];
 #pragma unroll
@@ -404,27 +446,34 @@ conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, 
     const int pc = valid ? p : 0;
     const int oy = pc / OW, ox = pc - oy * OW;
     const int rbase = k * IH + 2 * oy;
-    const int cx = (2 * ox + 2 * h) * 8;
+    const int cx = kK192 ? 12 * ox : (2 * ox + 2 * h) * 8;
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = s_bias[(r & 3) + 8 * (r >> 2) + 4 * h];
-    // kernel rows in pairs (4 B fragments a group): DTCONV1_BDEPTH groups in
-    // flight while a group's MFMAs run
+    // kernel rows in pairs (one group: kSGrp B fragments = kSGrp MFMAs);
+    // DTCONV1_BDEPTH groups in flight while a group's MFMAs run
     constexpr int kBD = DTCONV1_BDEPTH;
-    half8 bq[kBD][4];
-    auto ld = [&](half8 (&b)[4], int gy) __attribute__((always_inline)) {
+    half8 bq[kBD][kSGrp];
+    auto ld = [&](half8 (&b)[kSGrp], int gy) __attribute__((always_inline)) {
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int ky = 2 * gy + (i >> 1), kx0 = (i & 1) * 4;
-        const int off = ((rbase + ky) & (kSRing - 1)) * kSRowB + cx + kx0 * 8;
-        b[i] = *reinterpret_cast<const half8*>(rb + off);
+      for (int i = 0; i < kSGrp; ++i) {
+        if constexpr (kK192) {   // row 2gy + h, bytes 12 ox + 16 i: 4-B aligned
+          using u32x4a = __attribute__((ext_vector_type(4), aligned(4))) uint32_t;
+          const int off = ((rbase + 2 * gy + h) & (kSRing - 1)) * kSRowB + cx + 16 * i;
+          const u32x4a w = *reinterpret_cast<const u32x4a*>(rb + off);
+          b[i] = __builtin_bit_cast(half8, w);
+        } else {
+          const int ky = 2 * gy + (i >> 1), kx0 = (i & 1) * 4;
+          const int off = ((rbase + ky) & (kSRing - 1)) * kSRowB + cx + kx0 * 8;
+          b[i] = *reinterpret_cast<const half8*>(rb + off);
+        }
       }
     };
     if (DTCONV_SKIP & 32) {   // diagnostic: MFMAs on fragments not read from LDS
 #pragma unroll
       for (int q = 0; q < kBD; ++q)
 #pragma unroll
-        for (int i = 0; i < 4; ++i) bq[q][i] = wa[i];
+        for (int i = 0; i < kSGrp; ++i) bq[q][i] = wa[i];
     }
     if (!(DTCONV_SKIP & 34))
 #pragma unroll
@@ -434,8 +483,8 @@ conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, 
       if (gy + kBD - 1 < 4 && !(DTCONV_SKIP & 32)) ld(bq[(gy + kBD - 1) % kBD], gy + kBD - 1);
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wa[4 * gy + i], bq[gy % kBD][i], acc, 0, 0, 0);
+      for (int i = 0; i < kSGrp; ++i)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wa[kSGrp * gy + i], bq[gy % kBD][i], acc, 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
     float v[16];
