@@ -42,6 +42,14 @@ class DtMap(ctypes.Structure):
                 ('n_spawn_objects', ctypes.c_int32), ('spawn_objects', ctypes.c_void_p)]
 
 
+class DtExploreParams(ctypes.Structure):
+    """include/dtactor.h DtExploreParams."""
+    _fields_ = [(k, ctypes.c_double) for k in
+                ('pi', 'eps_span', 'eps_final', 'eps_initial', 'ou_m', 'ou_c', 'ou_sigma_min',
+                 'ou_sqrt_dt', 'ou_theta', 'ou_mu', 'ou_dt')] + \
+        [('eps_ratio_f', ctypes.c_float), ('head', ctypes.c_int32)]
+
+
 def _sources():
     return [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
 
@@ -142,6 +150,9 @@ def lib():
             'dt_conv1_bands': (i32, []),
             'dt_conv32': (ctypes.c_int, [i32, i32, vp, vp, vp, vp, vp, vp, ctypes.c_float, vp,
                                          vp, vp, vp, ctypes.c_float, ctypes.c_float, vp]),
+            'dt_explore': (ctypes.c_int, [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
+                                          ctypes.POINTER(DtExploreParams), vp, vp]),
+            'dt_explore_done': (ctypes.c_int, [i32, vp, vp, vp, vp, i32, vp]),
             'dt_conv12': (ctypes.c_int, [vp, i32, i32, ctypes.POINTER(i32), vp, vp, vp, vp,
                                          ctypes.c_float, vp, vp, vp, vp, ctypes.c_float, vp]),
         }

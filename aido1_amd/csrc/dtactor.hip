@@ -190,3 +190,105 @@ extern "C" int dt_sample_norm(const void* x, void* y, int32_t n, int32_t hw, int
                                                       beta, eps, slope);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
+
+// ---- dt_explore / dt_explore_done: the rollout's per-decision action choice --------------
+// One lane per explorer; every operation is the one (and in the order) the
+// torch restatement in aido1_amd/explore.py + rollout.CycleEpsilon performs,
+// so the two agree bit for bit given the same normals and uniforms
+// (-ffp-contract=off: no fused multiply-adds).
+namespace {
+
+__global__ void __launch_bounds__(256)
+explore_kernel(int n, const float* __restrict__ actor_out, const double* __restrict__ normals,
+               const float* __restrict__ coin, const float* __restrict__ uni,
+               double* __restrict__ ou_x, double* __restrict__ ou_steps,
+               const int64_t* __restrict__ episode, const double* __restrict__ cycle,
+               const double* __restrict__ max_step, const int64_t* __restrict__ explorer_id,
+               DtExploreParams p, float* __restrict__ actions) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  // epsilon: CycleEpsilon (explorers.py:92-111 over utils/util.py:36-40)
+  const double ep = (double)episode[i], cl = cycle[i];
+  const double rel = 1.0 - ep / max_step[i];
+  const double cosv = 0.5 * (cos(p.pi * fmod(ep, cl) / cl) + 1.0);
+  double eps = cosv * p.eps_span * rel + p.eps_final;
+  eps = eps < p.eps_final ? p.eps_final : eps;
+  eps = eps > p.eps_initial ? p.eps_initial : eps;
+  // OU sample (utils/random_process.py:42-47): sigma annealed, then the step
+  double sigma = p.ou_m * ou_steps[i] + p.ou_c;
+  sigma = sigma < p.ou_sigma_min ? p.ou_sigma_min : sigma;
+  const double sd = sigma * p.ou_sqrt_dt;
+  const double2 x = reinterpret_cast<const double2*>(ou_x)[i];
+  const double2 z = reinterpret_cast<const double2*>(normals)[i];
+  const double x0 = x.x + p.ou_theta * (p.ou_mu - x.x) * p.ou_dt + sd * z.x;
+  const double x1 = x.y + p.ou_theta * (p.ou_mu - x.y) * p.ou_dt + sd * z.y;
+  reinterpret_cast<double2*>(ou_x)[i] = make_double2(x0, x1);
+  ou_steps[i] = ou_steps[i] + 1.0;
+  // DDPG.act (models/ddpg/model.py:74-102): noise = eps * OU (float32 sample)
+  const float n0 = (float)(eps * (double)(float)x0), n1 = (float)(eps * (double)(float)x1);
+  const float2 o = reinterpret_cast<const float2*>(actor_out)[i];
+  float a0, a1;
+  if (p.head == 0) {          // tanh: noise doubled, clipped to [-1, 1]
+    a0 = fminf(fmaxf(o.x + 2.0f * n0, -1.0f), 1.0f);
+    a1 = fminf(fmaxf(o.y + 2.0f * n1, -1.0f), 1.0f);
+  } else if (p.head == 1) {   // sigmoid: clipped to [0, 1]
+    a0 = fminf(fmaxf(o.x + n0, 0.0f), 1.0f);
+    a1 = fminf(fmaxf(o.y + n1, 0.0f), 1.0f);
+  } else {
+    a0 = o.x + n0;
+    a1 = o.y + n1;
+  }
+  // every_second_random (explorers.py:178-194): even ids act uniformly at
+  // random with probability epsilon_ratio * epsilon
+  if (coin && (explorer_id[i] & 1) == 0 && coin[i] < p.eps_ratio_f * (float)eps) {
+    const float2 u = reinterpret_cast<const float2*>(uni)[i];
+    a0 = u.x;
+    a1 = u.y;
+  }
+  reinterpret_cast<float2*>(actions)[i] = make_float2(a0, a1);
+}
+
+__global__ void __launch_bounds__(256)
+explore_done_kernel(int n, const uint8_t* __restrict__ done, double* __restrict__ ou_x,
+                    int64_t* __restrict__ episode, float* __restrict__ actions, int tanh_map) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  if (tanh_map) {   // the wrapper's in-place a / 2 + 0.5 (env_wrappers.py:214-216)
+    float2 a = reinterpret_cast<float2*>(actions)[i];
+    a.x = a.x / 2.0f + 0.5f;
+    a.y = a.y / 2.0f + 0.5f;
+    reinterpret_cast<float2*>(actions)[i] = a;
+  }
+  if (done[i]) {    // explorers.py:170 reset_states + the episode count
+    reinterpret_cast<double2*>(ou_x)[i] = make_double2(0.0, 0.0);
+    episode[i] = episode[i] + 1;
+  }
+}
+
+}  // namespace
+
+extern "C" int dt_explore(int32_t n, const float* actor_out, const double* normals,
+                          const float* coin, const float* uni, double* ou_x, double* ou_steps,
+                          const int64_t* episode, const double* cycle, const double* max_step,
+                          const int64_t* explorer_id, const DtExploreParams* params,
+                          float* actions, void* stream) {
+  if (n < 0 || !params || (params->head < 0 || params->head > 2)) return DT_E_ARG;
+  if (n == 0) return DT_OK;
+  if (!actor_out || !normals || !ou_x || !ou_steps || !episode || !cycle || !max_step ||
+      !actions || (coin && (!uni || !explorer_id)))
+    return DT_E_ARG;
+  explore_kernel<<<(n + 255) / 256, 256, 0, (hipStream_t)stream>>>(
+      n, actor_out, normals, coin, uni, ou_x, ou_steps, episode, cycle, max_step, explorer_id,
+      *params, actions);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
+extern "C" int dt_explore_done(int32_t n, const uint8_t* done, double* ou_x, int64_t* episode,
+                               float* actions, int32_t tanh_map, void* stream) {
+  if (n < 0 || (n > 0 && (!done || !ou_x || !episode || (tanh_map && !actions))))
+    return DT_E_ARG;
+  if (n == 0) return DT_OK;
+  explore_done_kernel<<<(n + 255) / 256, 256, 0, (hipStream_t)stream>>>(n, done, ou_x, episode,
+                                                                        actions, tanh_map);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}

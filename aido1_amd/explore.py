@@ -152,3 +152,70 @@ def explore_actions(actor_out, ou, epsilon, explorer_id, config, generator=None,
         u = torch.rand(n, actor_out.shape[1], device=dev, generator=generator)
         a = torch.where(rnd.unsqueeze(1), u, a)
     return a
+
+
+_HEADS = {'tanh': 0, 'sigmoid': 1}
+
+
+class FusedExplore:
+    """explore_actions + rollout.CycleEpsilon (+ the post-step OU reset and
+    episode count) as the dt_explore / dt_explore_done HIP kernels
+    (include/dtactor.h): one launch each instead of ~25 element-wise torch
+    kernels per decision.  The random numbers are the torch restatement's own
+    draws in its order (randn [n, 2] f64 for the OU normals, then rand [n] and
+    rand [n, 2] for every_second_random), so for one generator state both
+    paths produce the same actions and states bit for bit
+    (tests/test_gpu_explore.py)."""
+
+    def __init__(self, config, ou, cycle_eps, explorer_id, head='tanh'):
+        from aido1_amd import _lib
+        t = config['training']
+        self.L = _lib.lib()
+        self.ou, self.ce, self.ids = ou, cycle_eps, explorer_id.long().contiguous()
+        self.every_second_random = bool(t.get('every_second_random'))
+        p = _lib.DtExploreParams()
+        p.pi, p.eps_span = math.pi, cycle_eps.i - cycle_eps.f
+        p.eps_final, p.eps_initial = cycle_eps.f, cycle_eps.i
+        p.ou_m, p.ou_c, p.ou_sigma_min = ou.m, ou.c, ou.sigma_min
+        p.ou_sqrt_dt, p.ou_theta, p.ou_mu, p.ou_dt = math.sqrt(ou.dt), ou.theta, ou.mu, ou.dt
+        p.eps_ratio_f = float(np.float32(t['epsilon_ratio'])) if self.every_second_random else 0.0
+        p.head = _HEADS.get(head, 2)
+        self.params = p
+        self.tanh = head == 'tanh'
+        assert ou.size == 2 and ou.x.is_contiguous() and ou.n_steps.is_contiguous()
+
+    def __call__(self, actor_out, episode, actions, generator=None):
+        """actions[:] = explore_actions(actor_out, ou, cycle_eps(episode), ...)."""
+        from aido1_amd import _lib
+        n, dev = self.ou.n, self.ou.x.device
+        ao = actor_out.float().contiguous()
+        assert ao.shape == (n, 2) and actions.shape == (n, 2) and actions.is_contiguous()
+        assert episode.dtype == torch.int64 and episode.is_contiguous()
+        normals = torch.randn(n, 2, dtype=torch.float64, device=dev, generator=generator)
+        coin = uni = None
+        if self.every_second_random:
+            coin = torch.rand(n, device=dev, generator=generator)
+            uni = torch.rand(n, 2, device=dev, generator=generator)
+        rc = self.L.dt_explore(n, ao.data_ptr(), normals.data_ptr(),
+                               coin.data_ptr() if coin is not None else None,
+                               uni.data_ptr() if uni is not None else None,
+                               self.ou.x.data_ptr(), self.ou.n_steps.data_ptr(), episode.data_ptr(),
+                               self.ce.cl.data_ptr(), self.ce.max_step.data_ptr(),
+                               self.ids.data_ptr(), self.params, actions.data_ptr(),
+                               torch.cuda.current_stream(dev).cuda_stream)
+        if rc != 0:
+            raise _lib.DtError('dt_explore failed (%d)' % rc)
+        return actions
+
+    def done(self, done, episode, actions=None):
+        """After the step: the wrapper's tanh map of `actions` (when given and
+        the head is tanh), then OU reset + episode += 1 where done."""
+        from aido1_amd import _lib
+        n, dev = self.ou.n, self.ou.x.device
+        assert done.dtype == torch.uint8 and done.numel() == n and done.is_contiguous()
+        tm = int(actions is not None and self.tanh)
+        rc = self.L.dt_explore_done(n, done.data_ptr(), self.ou.x.data_ptr(), episode.data_ptr(),
+                                    actions.data_ptr() if tm else None, tm,
+                                    torch.cuda.current_stream(dev).cuda_stream)
+        if rc != 0:
+            raise _lib.DtError('dt_explore_done failed (%d)' % rc)

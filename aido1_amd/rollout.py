@@ -21,7 +21,7 @@ import torch
 from aido1_amd.actor import ConfigActor, FusedActor
 from aido1_amd.config import EnvConfig
 from aido1_amd.env_wrappers import map_tanh_in_place
-from aido1_amd.explore import OUNoise, explore_actions
+from aido1_amd.explore import FusedExplore, OUNoise, explore_actions
 from aido1_amd.render import H, W, RenderOutput
 from aido1_amd.vec_env import StepOutput, VecEnv
 
@@ -48,7 +48,7 @@ class CycleEpsilon:
 class ActorRollout:
     def __init__(self, config, n_envs=4096, maps=('small_loop', 'zigzag'), device=0, seed=1234,
                  env_id_base=0, actor=None, dtype=torch.float16, masks=True,
-                 actor_mode='reference'):
+                 actor_mode='reference', fused_explore=True):
         self.config = config
         self.device = torch.device('cuda', device)
         self.n = n_envs
@@ -92,6 +92,10 @@ class ActorRollout:
         self.episode = torch.zeros(n_envs, dtype=torch.int64, device=self.device)
         self.explorer_id = torch.arange(env_id_base, env_id_base + n_envs, device=self.device)
         self.actor_events = None
+        # dt_explore (include/dtactor.h); fused_explore=False keeps the torch
+        # restatement (explore.py), which draws the same numbers
+        self.fx = FusedExplore(config, self.ou, self.eps, self.explorer_id, head=head) \
+            if fused_explore else None
 
     def reset(self):
         for env, ro in zip(self.envs, self.renders):
@@ -119,12 +123,18 @@ class ActorRollout:
         out = self.actor(self.ring, self.order())
         if timing is not None:
             timing[1].record()
-        eps = self.eps(self.episode)
-        self.actions.copy_(explore_actions(out, self.ou, eps, self.explorer_id, self.config,
-                                           generator=self.gen, head=self.head))
+        if self.fx is not None:
+            self.fx(out, self.episode, self.actions, generator=self.gen)
+        else:
+            eps = self.eps(self.episode)
+            self.actions.copy_(explore_actions(out, self.ou, eps, self.explorer_id, self.config,
+                                               generator=self.gen, head=self.head))
         for env, o, ro, sl in zip(self.envs, self.outs, self.renders, self.slices):
             env.step_into(self.actions[sl], o)
             env.render_into(ro, fresh=o.done)
+        if self.fx is not None:   # tanh map, OU reset and episode count in one kernel
+            self.fx.done(self.done, self.episode, self.actions)
+            return self.reward, self.reward_mod, self.done
         if self.head == 'tanh':   # the wrapper's in-place a/2 + 0.5 (env_wrappers.py:214-216)
             map_tanh_in_place(self.actions)
         d = self.done.bool()

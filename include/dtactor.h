@@ -97,6 +97,39 @@ int dt_conv12(const float* ring, int32_t n, int32_t slots, const int32_t* order,
               float eps1, const void* w2frag, const float* b2, void* y2, float* part2,
               float slope, void* stream);
 
+/* dt_explore: SingleThreadExplorer's action choice for n explorers at once,
+ * one fused pass replacing the torch restatement's ~25 element-wise kernels
+ * (aido1_amd/explore.py explore_actions + rollout.CycleEpsilon; the same
+ * operations in the same order, so the two agree bit for bit):
+ *   epsilon  = clip(cycle decay of episode[i], final, initial)
+ *              (training/explorers.py:92-111, utils/util.py:36-40)
+ *   OU step  x += theta (mu - x) dt + max(m steps + c, sigma_min) sqrt(dt) z,
+ *              steps += 1 (utils/random_process.py:42-47)
+ *   action   = clip(actor_out + (2 if tanh) * float(eps * float(x)))
+ *              (models/ddpg/model.py:74-102)
+ *   every_second_random (coin != NULL): even explorer ids take uni[i] when
+ *              coin[i] < float(ratio) * float(eps) (explorers.py:178-194)
+ *   actor_out f32 [n, 2]; normals f64 [n, 2]; coin f32 [n], uni f32 [n, 2]
+ *   ou_x f64 [n, 2] and ou_steps f64 [n] updated in place; episode i64 [n];
+ *   cycle, max_step f64 [n]; explorer_id i64 [n]; actions f32 [n, 2] out. */
+typedef struct DtExploreParams {
+  double pi, eps_span, eps_final, eps_initial;          /* eps_span = initial - final */
+  double ou_m, ou_c, ou_sigma_min, ou_sqrt_dt, ou_theta, ou_mu, ou_dt;
+  float eps_ratio_f;                                    /* (float)epsilon_ratio */
+  int32_t head;                                         /* 0 tanh, 1 sigmoid, 2 none */
+} DtExploreParams;
+
+int dt_explore(int32_t n, const float* actor_out, const double* normals, const float* coin,
+               const float* uni, double* ou_x, double* ou_steps, const int64_t* episode,
+               const double* cycle, const double* max_step, const int64_t* explorer_id,
+               const DtExploreParams* params, float* actions, void* stream);
+
+/* dt_explore_done: after the step, (tanh_map) actions = actions / 2 + 0.5 in
+ * place (utils/env_wrappers.py:214-216), and every explorer with done[i]
+ * gets its OU state zeroed and episode[i] += 1 (explorers.py:170). */
+int dt_explore_done(int32_t n, const uint8_t* done, double* ou_x, int64_t* episode,
+                    float* actions, int32_t tanh_map, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -100,3 +100,50 @@ def test_explore_actions_on_gpu(gpu):
     r = a[rnd]
     assert ((r >= 0) & (r < 1)).all()                        # U[0,1)^2 random action
     assert (a.abs() <= 1.0).all()
+
+
+@pytest.mark.parametrize('esr', [True, False])
+def test_fused_explore_matches_torch_path(gpu, esr):
+    """dt_explore / dt_explore_done (include/dtactor.h, the rollout's product
+    path) vs the torch restatement above (explore_actions + CycleEpsilon +
+    map_tanh_in_place + reset_states), 4096 explorers over 6 decisions with
+    done envs in between: same generator state -> identical actions, OU
+    states, annealing counters and episode counts (bit for bit)."""
+    import copy
+    from aido1_amd.env_wrappers import map_tanh_in_place
+    from aido1_amd.explore import FusedExplore, OUNoise, explore_actions
+    from aido1_amd.rollout import CycleEpsilon
+    cfg = copy.deepcopy(golden('reference_config.json'))
+    cfg['training']['every_second_random'] = esr
+    n = 4096
+
+    def build():
+        g = torch.Generator(device=gpu)
+        g.manual_seed(5)
+        return g, OUNoise.from_config(cfg, n, device=gpu, generator=g), \
+            CycleEpsilon(cfg, n, gpu, generator=g)
+    ga, oua, cea = build()
+    gb, oub, ceb = build()
+    assert torch.equal(cea.cl, ceb.cl)
+    g3 = torch.Generator(device=gpu)
+    g3.manual_seed(11)
+    ids = torch.arange(n, device=gpu)
+    epa = torch.randint(0, 5000, (n,), device=gpu, generator=g3)
+    epb = epa.clone()
+    fx = FusedExplore(cfg, oub, ceb, ids, head='tanh')
+    actb = torch.empty(n, 2, device=gpu)
+    n_rand = 0
+    for t in range(6):
+        out = torch.rand(n, 2, device=gpu, generator=g3) * 2.4 - 1.2
+        a = explore_actions(out, oua, cea(epa), ids, cfg, generator=ga, head='tanh')
+        fx(out, epb, actb, generator=gb)
+        assert torch.equal(a, actb), t
+        assert torch.equal(oua.x, oub.x) and torch.equal(oua.n_steps, oub.n_steps), t
+        n_rand += int(((a >= 0) & (a < 1)).all(1).sum())
+        done = (torch.rand(n, device=gpu, generator=g3) < 0.2).to(torch.uint8)
+        map_tanh_in_place(a)
+        oua.reset_states(done.bool())
+        epa += done.long()
+        fx.done(done, epb, actb)
+        assert torch.equal(a, actb) and torch.equal(epa, epb) and torch.equal(oua.x, oub.x), t
+    assert n_rand > 0
