@@ -19,6 +19,15 @@ Here one process per GPU runs, per iteration:
   rollout actor refresh      the acting copy follows the target actor, which
                              is what the reference's explorers act with
 
+With overlap=True the update of decision t runs on a side stream while the
+main stream runs decision t+1's rollout (actor, exploration, steps, render);
+the main stream waits for it before decision t+1's add_batch_ring (the add
+and update_priorities both write the sum tree) and only then refreshes the
+acting copy, so the explorers act with weights one update older -- the
+reference's explorers act with whatever the asynchronous trainer last
+published (training/managers.py:113-124), so a lag of one update is within
+its semantics.  overlap=False keeps the strictly sequential order.
+
 Nothing in the loop synchronises with the host.  Transition semantics: the
 stored next_obs of a finished env is its respawn stack (auto-reset), harmless
 because notdone = 0 removes Q(s') from its target.
@@ -37,7 +46,7 @@ class TrainLoop:
     def __init__(self, config, n_envs=4096, maps=('small_loop', 'zigzag'), device=0, seed=1234,
                  env_id_base=0, buffer_size=None, prioritized=True, batch_size=None,
                  updates_per_step=1, refresh_every=1, obs_dtype=None, actor_dtype=torch.float16,
-                 actor_mode='reference', masks=False, graph=True):
+                 actor_mode='reference', masks=False, graph=True, overlap=False):
         t = config['training']
         self.config = config
         self.device = torch.device('cuda', device)
@@ -66,6 +75,9 @@ class TrainLoop:
         self.updates = 0
         self.decisions = 0
         self.metrics = None
+        self.side = torch.cuda.Stream(self.device) if overlap else None
+        self.pending = False        # an update is in flight on self.side
+        self.refresh_due = False
 
     def reset(self):
         self.rollout.reset()
@@ -74,15 +86,37 @@ class TrainLoop:
     def step(self, timing=None):
         r, rm, done = self.rollout.step(timing)
         rew = rm if self.reward_modified else r        # explorers.py:205-206
+        if self.pending:   # the previous update (side stream) precedes this add
+            torch.cuda.current_stream(self.device).wait_stream(self.side)
+            self.pending = False
+            if self.refresh_due:
+                self.rollout.load_actor(self.trainer.target_actor)
+                self.refresh_due = False
         # next_obs straight from the frame ring into the buffer; the stored rows
         # are the next decision's obs (no stacked copy of the ring)
         self.obs = self.replay.add_batch_ring(self.obs, self.rollout.actions, rew,
                                               self.rollout.ring, self.rollout.order(), done)
         self.decisions += 1
         if len(self.replay) >= max(self.batch_size, 2):
-            for _ in range(self.updates_per_step):
-                self._update()
+            if self.side is not None:
+                self.side.wait_stream(torch.cuda.current_stream(self.device))
+                with torch.cuda.stream(self.side):
+                    for _ in range(self.updates_per_step):
+                        self._update()
+                self.pending = True
+            else:
+                for _ in range(self.updates_per_step):
+                    self._update()
         return r, rm, done
+
+    def flush(self):
+        """Join an in-flight update (overlap=True) and apply its refresh."""
+        if self.pending:
+            torch.cuda.current_stream(self.device).wait_stream(self.side)
+            self.pending = False
+            if self.refresh_due:
+                self.rollout.load_actor(self.trainer.target_actor)
+                self.refresh_due = False
 
     def _update(self):
         if self.prioritized:
@@ -95,4 +129,7 @@ class TrainLoop:
             self.replay.update_priorities(idx, pr)
         self.updates += 1
         if self.updates % self.refresh_every == 0:
-            self.rollout.load_actor(self.trainer.target_actor)
+            if self.side is not None:
+                self.refresh_due = True     # applied on the main stream (step / flush)
+            else:
+                self.rollout.load_actor(self.trainer.target_actor)

@@ -92,6 +92,9 @@ def parse(argv=None):
     p.add_argument('--batch-size', type=int, default=0, help='train: 0 = config.json (64)')
     p.add_argument('--buffer-size', type=int, default=131072)
     p.add_argument('--updates-per-step', type=int, default=1)
+    p.add_argument('--overlap', action='store_true',
+                   help='train: run each update beside the next rollout (side stream); '
+                        'measured slower, DESIGN 3.8')
     p.add_argument('--many', type=int, default=20,
                    help='lane config: most decisions per dt_step_many launch; the K timed '
                         'decisions are split into ceil(K / many) equal launches')
@@ -746,7 +749,8 @@ def bench_train(args, ctx):
     dev, rank, n = ctx.dev, ctx.rank, args.envs
     loop = TrainLoop(cfg, n, device=dev.index, seed=args.seed, env_id_base=rank * n,
                      buffer_size=args.buffer_size, batch_size=args.batch_size or None,
-                     updates_per_step=args.updates_per_step, actor_mode=args.actor_mode)
+                     updates_per_step=args.updates_per_step, actor_mode=args.actor_mode,
+                     overlap=args.overlap)
     loop.reset()
     for _ in range(max(args.warmup, 2)):
         loop.step()
@@ -760,6 +764,7 @@ def bench_train(args, ctx):
     t0 = time.perf_counter()
     for k in range(args.steps):
         loop.step(timing=ev[k])
+    loop.flush()
     ctx.sync()
     ctx.barrier()
     elapsed = time.perf_counter() - t0
@@ -785,6 +790,9 @@ def bench_train(args, ctx):
                        'global_envs': n * ctx.world, 'batch_size_per_gpu': loop.batch_size,
                        'buffer_size_per_gpu': args.buffer_size,
                        'updates_per_step': args.updates_per_step,
+                       'update_overlap': None if not args.overlap else
+                       'update t on a side stream beside rollout t+1; acting weights one '
+                       'update behind (the reference explorers act asynchronously)',
                        'weights': 'random init (config.json xavier_normal)',
                        'parallelism': 'env shards (%d x %d) + data-parallel update, RCCL '
                                       'all-reduce of %d gradients' % (ctx.world, n, nparams)},

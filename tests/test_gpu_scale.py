@@ -68,17 +68,21 @@ def test_config4_actor_rollout_at_size(gpu):
     roll.close()
 
 
-def test_config5_train_loop_at_size(gpu):
+@pytest.mark.parametrize('overlap', [False, True])
+def test_config5_train_loop_at_size(gpu, overlap):
+    """overlap=True: each update on a side stream beside the next rollout
+    (bench --overlap); the trees must stay consistent under it."""
     from aido1_amd.train_loop import TrainLoop
     cfg = golden('reference_config.json')
     n = 4096
     cap = 1 << 17
     loop = TrainLoop(cfg, n_envs=n, device=0, seed=1234, buffer_size=cap, prioritized=True,
-                     graph=True)
+                     graph=True, overlap=overlap)
     loop.reset()
     steps = cap // n + 2                          # fills and wraps the buffer
     for _ in range(steps):
         loop.step()
+    loop.flush()
     torch.cuda.synchronize()
     assert len(loop.replay) == cap
     assert loop.decisions == steps and loop.updates == steps
