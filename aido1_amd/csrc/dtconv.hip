@@ -717,8 +717,12 @@ __device__ __forceinline__ int ring_off(int px, int c) {
   return 64 * pos + 16 * (c ^ ((pos >> 2) & 3));
 }
 
+// conv4 (NW 4) waves per SIMD: 1 holds its 317 registers; 2 spills ~60 (diagnostic)
+#ifndef DTCONV4_OCC
+#define DTCONV4_OCC 1
+#endif
 template <int IH, int IW, int OH, int OW, int ST, int NW, int kIn, int kOut, int kPrevRows>
-__global__ void __launch_bounds__(64 * NW, 1)   // one wave per SIMD: the full register file
+__global__ void __launch_bounds__(64 * NW, NW == 4 ? DTCONV4_OCC : 1)   // 1: one wave per SIMD, the full register file
 conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfrag,
               const float* __restrict__ bias, const float* __restrict__ prev_part,
               const float* __restrict__ in_gamma, const float* __restrict__ in_beta, float in_eps,
