@@ -21,7 +21,7 @@ SOURCES = ['dtsim.hip', 'dtrender.hip', 'dtreplay.hip', 'dtactor.hip', 'dtconv.h
 HEADERS = ['dtsim_common.h', 'dtrender.h']
 PUBLIC_HEADERS = ['dtsim.h', 'dtreplay.h', 'dtactor.h']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
-ABI_VERSION = 3
+ABI_VERSION = 4
 
 # -pragma-unroll-threshold: dt_conv12's step loops must unroll fully (its conv1
 # outputs are register arrays indexed by step) past clang's default limit
@@ -120,6 +120,7 @@ def lib():
             'dt_seed_env': (ctypes.c_int, [vp, i32, u64]),
             'dt_lane_pos': (ctypes.c_int, [vp, vp, vp, vp]),
             'dt_render': (ctypes.c_int, [vp, vp, vp]),
+            'dt_copy_pose': (ctypes.c_int, [vp, vp, vp]),
             'dt_default_line_params': (ctypes.c_int, [vp]),
             'dt_set_line_params': (ctypes.c_int, [vp, vp]),
             'dt_line_detect': (ctypes.c_int, [vp, vp, i32, i32, i32, vp, vp, vp]),

@@ -29,8 +29,7 @@ struct dt_handle {
   dr::LineDev line{};
   void* mark_buf = nullptr;   // float4 segments (x0, z0, x1, z1): yellow then white
   int32_t n_yellow = 0, n_white = 0;
-  int32_t render_skip = 0;
-  int32_t render_threads = 768;  // DTSIM_RENDER_THREADS (tuning)
+  void* render_spill = nullptr;  // per env: listed words past the LDS list (dtrender.hip)
   std::string err;
 };
 
@@ -52,6 +51,16 @@ struct DevGuard {
   DevGuard(const DevGuard&) = delete;
   DevGuard& operator=(const DevGuard&) = delete;
 };
+
+// record a failed HIP call in the handle and return DT_E_HIP
+#define HIP_OR_FAIL(h, expr)                                                   \
+  do {                                                                         \
+    hipError_t _e = (expr);                                                    \
+    if (_e != hipSuccess) {                                                    \
+      (h)->err = std::string(#expr) + ": " + hipGetErrorString(_e);             \
+      return DT_E_HIP;                                                         \
+    }                                                                          \
+  } while (0)
 
 // dtrender.hip: lane-marking polylines of the map + default line params
 int dt_render_init(dt_handle* h, const dt_map* map);

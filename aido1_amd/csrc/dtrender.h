@@ -17,20 +17,27 @@ constexpr int kThreads = 256;
 constexpr float kRes = 0.01f;        // metres per pixel
 constexpr float kInvRes = 100.0f;
 
-// palette of the raster (index -> packed B | G << 8 | R << 16)
-enum : uint8_t { PAL_FLOOR = 0, PAL_OFFROAD = 1, PAL_ROAD = 2, PAL_YELLOW = 3, PAL_WHITE = 4,
-                 PAL_RED = 5, PAL_N = 8 };
+// Raster bytes.  The background is a plain byte (floor / grass / road); the
+// markings are OR-ed into it, so yellow and white can be drawn in any order
+// and concurrently with the background fix-up: yellow sets bit 2 (4..6 =
+// yellow over any background), white sets bits 0-2 (7 = white, also over
+// yellow) — exactly "yellow drawn first, white over it" of the oracle.
+// kPalette maps every byte value to its colour (packed B | G << 8 | R << 16).
+enum : uint8_t { PAL_FLOOR = 0, PAL_OFFROAD = 1, PAL_ROAD = 2, PAL_RED = 3, PAL_YELLOW = 4,
+                 PAL_WHITE = 7, PAL_N = 8 };
 __host__ __device__ constexpr uint32_t rgb_pack(uint32_t r, uint32_t g, uint32_t b) {
   return b | (g << 8) | (r << 16);
 }
+constexpr uint32_t kYellowRgb = rgb_pack(255, 230, 0);
 constexpr uint32_t kPalette[PAL_N] = {
     rgb_pack(0, 0, 0),        // floor / outside the map
     rgb_pack(72, 132, 52),    // grass (any non-drivable tile)
     rgb_pack(56, 56, 60),     // road surface
-    rgb_pack(255, 230, 0),    // yellow centre line
-    rgb_pack(250, 250, 250),  // white edge line
-    rgb_pack(220, 30, 30),    // red stop line (intersections; unused on loop maps)
-    0, 0};
+    rgb_pack(220, 30, 30),    // red stop line (never drawn: intersections carry no markings)
+    kYellowRgb,               // yellow centre line over floor / grass / road
+    kYellowRgb,
+    kYellowRgb,
+    rgb_pack(250, 250, 250)};  // white edge line
 
 // OpenCV RGB2HSV_b fixed-point tables (hsv_shift = 12):
 //   sdiv[i] = round((255 << 12) / i), hdiv180[i] = round((180 << 12) / (6 i)).

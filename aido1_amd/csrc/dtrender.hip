@@ -176,101 +176,6 @@ __device__ inline void load_tables(Lds& S) {
   }
 }
 
-// Bresenham (utils/bresenham.py:6-34) into the palette image.
-// LDS byte pointer: 32-bit addressing (a generic pointer makes every pixel
-// address a 64-bit multiply-add)
-using lds_u8 = __attribute__((address_space(3))) uint8_t;
-
-__device__ inline void draw_line(lds_u8* img, int x0, int y0, int x1, int y1, uint8_t col) {
-  int dx = x1 - x0, dy = y1 - y0;
-  const int xsign = dx > 0 ? 1 : -1, ysign = dy > 0 ? 1 : -1;
-  dx = dx < 0 ? -dx : dx;
-  dy = dy < 0 ? -dy : dy;
-  int xx, xy, yx, yy;
-  if (dx > dy) {
-    xx = xsign; xy = 0; yx = 0; yy = ysign;
-  } else {
-    const int t = dx; dx = dy; dy = t;
-    xx = 0; xy = ysign; yx = xsign; yy = 0;
-  }
-  // the pixel of step x is (x0 + x*xx + y*yx, y0 + x*xy + y*yy); tracked
-  // incrementally (no per-pixel multiplies)
-  int D = 2 * dy - dx, px = x0, py = y0;
-  int ad = y0 * W + x0;  // pixel address, stepped with the pixel
-  const int amaj = xy * W + xx, amin = yy * W + yx;
-  for (int x = 0; x <= dx; ++x) {
-    if ((unsigned)px < (unsigned)W && (unsigned)py < (unsigned)H) img[(uint32_t)ad] = col;
-    const bool st = D >= 0;
-    px += xx + (st ? yx : 0);
-    py += xy + (st ? yy : 0);
-    ad += amaj + (st ? amin : 0);
-    D += 2 * dy - (st ? 2 * dx : 0);
-  }
-}
-
-// Pixels [xa, xb) of the line draw_line(x0, y0, x1, y1) would draw, the
-// same pixels in the same order: draw_line's minor coordinate after x major
-// steps is y(x) = floor((2 dy x + dx) / (2 dx)) (dx > 0; 0 for a single
-// point) and its decision variable D(x) = 2 dy (x + 1) - dx - 2 dx y(x), so a
-// part starts where the sequential walk would be (the quotient is exact: it is
-// at least 1 / (2 dx) from the next integer, far above float rounding).
-__device__ inline void draw_line_part(lds_u8* img, int x0, int y0, int x1, int y1, uint8_t col,
-                                      int part, int parts) {
-  int dx = x1 - x0, dy = y1 - y0;
-  const int xsign = dx > 0 ? 1 : -1, ysign = dy > 0 ? 1 : -1;
-  dx = dx < 0 ? -dx : dx;
-  dy = dy < 0 ? -dy : dy;
-  int xx, xy, yx, yy;
-  if (dx > dy) {
-    xx = xsign; xy = 0; yx = 0; yy = ysign;
-  } else {
-    const int t = dx; dx = dy; dy = t;
-    xx = 0; xy = ysign; yx = xsign; yy = 0;
-  }
-  const int n = dx + 1;
-  const int xa = (n * part) / parts, xb = (n * (part + 1)) / parts;
-  if (xa >= xb) return;
-  const int ya = dx > 0 ? (int)floorf((float)(2 * dy * xa + dx) / (float)(2 * dx)) : 0;
-  int D = 2 * dy * (xa + 1) - dx - 2 * dx * ya;
-  int px = x0 + xa * xx + ya * yx, py = y0 + xa * xy + ya * yy;
-  int ad = py * W + px;
-  const int amaj = xy * W + xx, amin = yy * W + yx;
-  for (int x = xa; x < xb; ++x) {
-    if ((unsigned)px < (unsigned)W && (unsigned)py < (unsigned)H) img[(uint32_t)ad] = col;
-    const bool st = D >= 0;
-    px += xx + (st ? yx : 0);
-    py += xy + (st ? yy : 0);
-    ad += amaj + (st ? amin : 0);
-    D += 2 * dy - (st ? 2 * dx : 0);
-  }
-}
-
-struct View {  // f32 camera frame of one env
-  float cx, cz, dirx, dirz, rx, rz;
-};
-
-__device__ inline int proj(float v) {  // round-to-nearest pixel, clamped far off-screen
-  v = floorf(v + 0.5f);
-  v = v < -100000.0f ? -100000.0f : (v > 100000.0f ? 100000.0f : v);
-  return (int)v;
-}
-
-// a segment's pixel endpoints, or false when it is culled (wholly off one
-// side of the frame, or degenerate: a segment is <= ~10 px at 1 cm/px)
-__device__ inline bool project_seg(const View& V, float4 q, int& c0, int& r0, int& c1, int& r1) {
-  const float ax = q.x - V.cx, az = q.y - V.cz, bx = q.z - V.cx, bz = q.w - V.cz;
-  const float fa = ax * V.dirx + az * V.dirz, la = ax * V.rx + az * V.rz;
-  const float fb = bx * V.dirx + bz * V.dirz, lb = bx * V.rx + bz * V.rz;
-  c0 = proj(la * kInvRes + 79.5f);
-  r0 = proj(119.5f - fa * kInvRes);
-  c1 = proj(lb * kInvRes + 79.5f);
-  r1 = proj(119.5f - fb * kInvRes);
-  if ((c0 < 0 && c1 < 0) || (c0 >= W && c1 >= W) || (r0 < 0 && r1 < 0) || (r0 >= H && r1 >= H))
-    return false;
-  const int len = (c1 > c0 ? c1 - c0 : c0 - c1) + (r1 > r0 ? r1 - r0 : r0 - r1);
-  return len <= 400;
-}
-
 // pass A for one pixel: Sobel/NMS dir + colour bits into work, magnitude into mag
 template <class Fetch>
 __device__ inline void pass_a_pixel(const Fetch& fetch, Lds& S, const LineDev& L, int hgt,
@@ -360,6 +265,10 @@ __device__ inline uint8_t pass_c_pixel(const Lds& S, const LineDev& L, int hgt, 
   return bits;
 }
 
+struct View {  // f32 camera frame of one env
+  float cx, cz, dirx, dirz, rx, rz;
+};
+
 struct RenderArgs {
   const double* x;
   const double* z;
@@ -375,49 +284,76 @@ struct RenderArgs {
   const uint8_t* fresh;
   uint8_t* masks;
   uint8_t* rgb;
+  uint16_t* spill;   // per env kSpillHalves: entries and list of slots >= list_cap
+  int32_t list_cap;  // listed words kept in LDS (<= kListCap)
   LineDev line;
   int32_t n;
-  int32_t skip;  // diagnostics only (DTSIM_RENDER_SKIP): bit k skips phase k; outputs invalid
 };
 
 // ---- fused render kernel ----------------------------------------------------------
-// Works on 4-pixel words (u32 of palette indices, row-major, 40 words per row)
-// and a 16-bit work image  [mag 11 b | NMS dir 2 b | CAND | EDGE].  Phases,
-// each a barrier apart:
-//   0  background words + Bresenham markings into img
-//   1  every word: 3x3-pixel neighbourhood of all 4 pixels one colour?  yes ->
-//      Sobel = 0 (work 0); no -> word index appended to `list`
-//      (wave-aggregated LDS atomic).  Grey from the palette LUT, stored here
-//      (float4 per lane).
-//   2a listed words: SWAR 3-channel Sobel -> mag + dir into work
-//   2b listed words: Canny NMS (branch-free neighbour select) + thresholds;
-//      weak pixels appended to `weak`
-//   3  hysteresis over the weak list to a fixed point
-//   4  masks: colour bits from img through a v_perm LUT, SWAR ellipse
-//      dilation, edge bits from work; 16 px per lane, four uint4 stores
-// LDS ~71 KB -> two workgroups per CU.
+// One 512-thread workgroup per env, three per CU (LDS <= 53 KB).  The frame is
+// 4-pixel words of raster bytes (img); Canny's work entries exist only for the
+// LISTED words (a word whose 3x3-pixel neighbourhood is not one colour: every
+// other word has Sobel 0 and its masks are its own colour bits).  Phases, a
+// barrier apart:
+//   0a  background of every 16-pixel span decided by its end pixels (uniform:
+//       one 16-B store; otherwise zeroed and listed) + projection of the
+//       marking segments, the visible ones listed
+//   0b  listed spans resolved a word at a time, OR-ed in, beside the markings
+//       drawn with Bresenham, OR-ed in (raster byte encoding, dtrender.h):
+//       order-free, so one pass
+//   1   every 16-pixel quad: neighbourhood uniformity of its 4 words, grey
+//       (float4 stores into the frame ring), masks of all-uniform quads;
+//       non-uniform words get a slot (list + wmap), their quads are listed
+//   2a  listed words: SWAR 3-channel Sobel -> entry (mag | dir)
+//   2b  listed words: Canny NMS + double threshold; weak pixels listed
+//   3   hysteresis over the weak list to a fixed point
+//   4   listed quads: colour bits via a v_perm LUT, SWAR ellipse dilation,
+//       edge bits, 16 px per lane, four 16-B stores
+// Slots past list_cap (a frame with more than kListCap non-uniform words:
+// never on the shipped maps) keep their entries in a per-env global spill
+// area; the workgroup then runs the phases' spill instantiation.
 #ifndef DTSIM_MARK_PARTS
-#define DTSIM_MARK_PARTS 4  // lanes per marking segment (draw_line_part)
+#define DTSIM_MARK_PARTS 2  // lanes per marking segment (draw_line_part)
 #endif
-constexpr int kRenderThreads = 768;  // 12 waves (measured best of 256-1024); LDS per workgroup is fixed (~71 KB)
+#ifndef DTSIM_RENDER_THREADS
+#define DTSIM_RENDER_THREADS 512
+#endif
+constexpr int kRenderThreads = DTSIM_RENDER_THREADS;
 constexpr int WPR = W / 4;          // words per row
 constexpr int NW = NPIX / 4;        // words per image
-constexpr int kWeakCap = 2048;
-enum { kNList = 0, kNWeak = 1, kNSeg = 2, kNSegW = 3 };
+constexpr int QPR = WPR / 4;        // 16-pixel quads per row
+constexpr int NQ = NW / 4;          // quads per image (also the background spans)
+constexpr int kListCap = 2048;      // listed words kept in LDS
+constexpr int kWeakCap = 512;
+constexpr int kSegRecs = kListCap * 10 / 8;  // uint2 segment records over the entry area
+constexpr int kSpillHalves = 5 * NW;         // global spill per env: 4 entries + 1 list word
+enum { kNSpan = 0, kNSeg = 1, kNList = 2, kNQuad = 3, kNWeak = 4, kNCnt = 8 };
 constexpr uint16_t WK_MAG = 0x7FF, WK_DIR_SHIFT = 11, WK_CAND = 1 << 13, WK_EDGE = 1 << 14;
 
-struct FusedLds {
+struct RenderLds {
   uint32_t img[NW];
-  uint16_t work[NPIX];
-  uint16_t list[NW];
+  uint16_t wmap[NW];  // word -> its slot + 1; 0: a uniform neighbourhood (not listed)
+  union {
+    struct {
+      uint16_t ent[4 * kListCap];  // slot s: the work entries of its 4 pixels
+      uint16_t list[kListCap];     // slot s -> word
+    } w;
+    uint2 seg[kSegRecs];           // phase 0: visible segments (yellow up, white down)
+  } u;
+  uint16_t qlist[NQ];  // phase 0: the non-uniform background spans
   uint16_t weak[kWeakCap];
   uint32_t pal_swar[PAL_N];
   float pal_gray[PAL_N];
-  uint32_t bits_lo, bits_hi;  // colour bits of palette entries 0-3 / 4-7 (one byte each)
+  uint32_t bits_lo, bits_hi;  // colour bits of raster bytes 0-3 / 4-7 (one byte each)
   View view;
-  int32_t cnt[4];  // list counters: kNList, kNWeak, kNSeg, kNSegW
+  int32_t cnt[kNCnt];
   int8_t kind[dt::kMaxLdsTiles];
 };
+static_assert(sizeof(RenderLds) <= 163840 / 3, "three render workgroups per CU");
+// segments projected in one round (loads issued at entry): 4 per lane, and
+// their records must fit the record area
+constexpr int kMarkFast = 4 * kRenderThreads < kSegRecs ? 4 * kRenderThreads : kSegRecs;
 
 __device__ inline uint32_t swar_of(uint32_t bgr) {  // B | G << 10 | R << 20
   return (bgr & 255u) | (((bgr >> 8) & 255u) << 10) | (((bgr >> 16) & 255u) << 20);
@@ -465,53 +401,49 @@ __device__ inline uint32_t shift_bytes(uint32_t prev, uint32_t cur, uint32_t nex
   return (cur << (-8 * d)) | (prev >> (32 + 8 * d));
 }
 
-// Up to four pushes per lane in one go (every lane of the wave calls): the
-// lane counts (0..4) are summed and prefix-summed bit-plane by bit-plane with
-// three ballots, lane 0 reserves the wave's slots with one LDS atomic, and each
-// lane writes its items consecutively from its prefix.
-__device__ inline void wave_push4(int32_t* counter, uint16_t* list, int cap, const bool want[4],
-                                  const uint16_t value[4]) {
-  const uint32_t cnt = (uint32_t)want[0] + want[1] + want[2] + want[3];
-  const uint64_t b0 = __ballot(cnt & 1u), b1 = __ballot(cnt & 2u), b2 = __ballot(cnt & 4u);
-  const int total = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
-  if (total == 0) return;  // wave-uniform
-  const auto mb = [](uint64_t m) {
-    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-  };
-  int base = 0;
-  if ((threadIdx.x & 63) == 0) base = atomicAdd(counter, total);
-  base = __builtin_amdgcn_readlane(base, 0);
-  int slot = base + mb(b0) + 2 * mb(b1) + 4 * mb(b2);
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    if (want[k]) {
-      if (slot < cap) list[slot] = value[k];
-      ++slot;
-    }
-  }
+__device__ inline int lane_prefix(uint64_t m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
+                                        __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
 // A slot for each of up to four items per lane (every lane of the wave calls):
-// the wave_push4 bit-plane prefix, returning the slots instead of storing.
+// the lane counts (0..4) are summed and prefix-summed bit-plane by bit-plane
+// with three ballots, and lane 0 reserves the wave's slots with one LDS atomic.
 __device__ inline void wave_slots4(int32_t* counter, const bool want[4], int slot[4]) {
   const uint32_t cnt = (uint32_t)want[0] + want[1] + want[2] + want[3];
   const uint64_t b0 = __ballot(cnt & 1u), b1 = __ballot(cnt & 2u), b2 = __ballot(cnt & 4u);
   const int total = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
   if (total == 0) return;  // wave-uniform
-  const auto mb = [](uint64_t m) {
-    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-  };
   int base = 0;
   if ((threadIdx.x & 63) == 0) base = atomicAdd(counter, total);
   base = __builtin_amdgcn_readlane(base, 0);
-  int next = base + mb(b0) + 2 * mb(b1) + 4 * mb(b2);
+  int next = base + lane_prefix(b0) + 2 * lane_prefix(b1) + 4 * lane_prefix(b2);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     slot[k] = next;
     next += want[k] ? 1 : 0;
   }
+}
+
+// One item per lane: its slot (ballot prefix, one LDS atomic per wave).
+__device__ inline int wave_slot1(int32_t* counter, bool want) {
+  const uint64_t b = __ballot(want);
+  if (b == 0) return 0;  // wave-uniform
+  int base = 0;
+  if ((threadIdx.x & 63) == 0) base = atomicAdd(counter, __popcll(b));
+  base = __builtin_amdgcn_readlane(base, 0);
+  return base + lane_prefix(b);
+}
+
+// wave_slots4 + the stores: item k of a lane goes to list[slot] (dropped past cap;
+// the count still grows, so the caller sees the overflow).
+__device__ inline void wave_push4(int32_t* counter, uint16_t* list, int cap, const bool want[4],
+                                  const uint16_t value[4]) {
+  int slot[4];
+  wave_slots4(counter, want, slot);
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (want[k] && slot[k] < cap) list[slot[k]] = value[k];
 }
 
 // wave_slots4 for two lists at once: one LDS atomic on a packed counter
@@ -525,15 +457,12 @@ __device__ inline void wave_slots4x2(int32_t* counter, const bool wa[4], const b
   const uint32_t ta = __popcll(a0) + 2 * __popcll(a1) + 4 * __popcll(a2);
   const uint32_t tb = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
   if ((ta | tb) == 0u) return;  // wave-uniform
-  const auto mb = [](uint64_t m) {
-    return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32),
-                                          __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-  };
   int base = 0;
   if ((threadIdx.x & 63) == 0) base = atomicAdd(counter, (int)(ta | (tb << 16)));
   base = __builtin_amdgcn_readlane(base, 0);
-  int na = (base & 0xFFFF) + mb(a0) + 2 * mb(a1) + 4 * mb(a2);
-  int nb = (int)((uint32_t)base >> 16) + mb(b0) + 2 * mb(b1) + 4 * mb(b2);
+  int na = (base & 0xFFFF) + lane_prefix(a0) + 2 * lane_prefix(a1) + 4 * lane_prefix(a2);
+  int nb = (int)((uint32_t)base >> 16) + lane_prefix(b0) + 2 * lane_prefix(b1) +
+           4 * lane_prefix(b2);
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
     sa[k] = na;
@@ -543,72 +472,92 @@ __device__ inline void wave_slots4x2(int32_t* counter, const bool wa[4], const b
   }
 }
 
-__device__ inline int mag16(const FusedLds& S, int r, int c) {
-  return ((unsigned)r < (unsigned)H && (unsigned)c < (unsigned)W) ? (S.work[r * W + c] & WK_MAG)
-                                                                  : 0;
+using lds_u32 = __attribute__((address_space(3))) uint32_t;
+
+// OR a raster byte into the image (ds_or_b32: order-free against the other
+// markings and the background fix-up of phase 0b)
+__device__ __forceinline__ void or_pixel(lds_u32* img, uint32_t ad, uint32_t col) {
+  __hip_atomic_fetch_or(img + (ad >> 2), col << (8 * (ad & 3u)), __ATOMIC_RELAXED,
+                        __HIP_MEMORY_SCOPE_WORKGROUP);
 }
 
-__device__ __forceinline__ uint32_t bg_color(const FusedLds& S, const RenderArgs& a, float fi,
+// Pixels [xa, xb) of the Bresenham line (utils/bresenham.py:6-34) from (x0, y0)
+// to (x1, y1), the same pixels in the same order as the sequential walk: its
+// minor coordinate after x major steps is y(x) = floor((2 dy x + dx) / (2 dx))
+// (dx > 0; 0 for a single point) and its decision variable D(x) = 2 dy (x + 1)
+// - dx - 2 dx y(x), so a part starts where the walk would be (the quotient is
+// exact: it is at least 1 / (2 dx) from the next integer, far above float
+// rounding; checked exhaustively for dx <= 420).
+__device__ inline void draw_line_part(lds_u32* img, int x0, int y0, int x1, int y1, uint32_t col,
+                                      int part, int parts) {
+  int dx = x1 - x0, dy = y1 - y0;
+  const int xsign = dx > 0 ? 1 : -1, ysign = dy > 0 ? 1 : -1;
+  dx = dx < 0 ? -dx : dx;
+  dy = dy < 0 ? -dy : dy;
+  int xx, xy, yx, yy;
+  if (dx > dy) {
+    xx = xsign; xy = 0; yx = 0; yy = ysign;
+  } else {
+    const int t = dx; dx = dy; dy = t;
+    xx = 0; xy = ysign; yx = xsign; yy = 0;
+  }
+  const int n = dx + 1;
+  const int xa = (n * part) / parts, xb = (n * (part + 1)) / parts;
+  if (xa >= xb) return;
+  const int ya = dx > 0 ? (int)floorf((float)(2 * dy * xa + dx) / (float)(2 * dx)) : 0;
+  int D = 2 * dy * (xa + 1) - dx - 2 * dx * ya;
+  int px = x0 + xa * xx + ya * yx, py = y0 + xa * xy + ya * yy;
+  int ad = py * W + px;  // pixel (byte) address, stepped with the pixel
+  const int amaj = xy * W + xx, amin = yy * W + yx;
+  for (int x = xa; x < xb; ++x) {
+    if ((unsigned)px < (unsigned)W && (unsigned)py < (unsigned)H) or_pixel(img, (uint32_t)ad, col);
+    const bool st = D >= 0;
+    px += xx + (st ? yx : 0);
+    py += xy + (st ? yy : 0);
+    ad += amaj + (st ? amin : 0);
+    D += 2 * dy - (st ? 2 * dx : 0);
+  }
+}
+
+__device__ inline int proj(float v) {  // round-to-nearest pixel, clamped far off-screen
+  v = floorf(v + 0.5f);
+  v = v < -100000.0f ? -100000.0f : (v > 100000.0f ? 100000.0f : v);
+  return (int)v;
+}
+
+// a segment's pixel endpoints, or false when it is culled (wholly off one
+// side of the frame, or degenerate: a segment is <= ~10 px at 1 cm/px)
+__device__ inline bool project_seg(const View& V, float4 q, int& c0, int& r0, int& c1, int& r1) {
+  const float ax = q.x - V.cx, az = q.y - V.cz, bx = q.z - V.cx, bz = q.w - V.cz;
+  const float fa = ax * V.dirx + az * V.dirz, la = ax * V.rx + az * V.rz;
+  const float fb = bx * V.dirx + bz * V.dirz, lb = bx * V.rx + bz * V.rz;
+  c0 = proj(la * kInvRes + 79.5f);
+  r0 = proj(119.5f - fa * kInvRes);
+  c1 = proj(lb * kInvRes + 79.5f);
+  r1 = proj(119.5f - fb * kInvRes);
+  if ((c0 < 0 && c1 < 0) || (c0 >= W && c1 >= W) || (r0 < 0 && r1 < 0) || (r0 >= H && r1 >= H))
+    return false;
+  const int len = (c1 > c0 ? c1 - c0 : c0 - c1) + (r1 > r0 ? r1 - r0 : r0 - r1);
+  return len <= 400;
+}
+
+__device__ inline uint2 seg_pack(int c0, int r0, int c1, int r1) {
+  return make_uint2((uint32_t)(uint16_t)c0 | ((uint32_t)(uint16_t)r0 << 16),
+                    (uint32_t)(uint16_t)c1 | ((uint32_t)(uint16_t)r1 << 16));
+}
+
+__device__ inline void seg_draw(lds_u32* img, uint2 v, uint32_t col, int part, int parts) {
+  draw_line_part(img, (int)(int16_t)(v.x & 0xFFFFu), (int)(int16_t)(v.x >> 16),
+                 (int)(int16_t)(v.y & 0xFFFFu), (int)(int16_t)(v.y >> 16), col, part, parts);
+}
+
+__device__ __forceinline__ uint32_t bg_color(const RenderLds& S, const RenderArgs& a, float fi,
                                              float fj) {
   if (fi >= 0.0f && fj >= 0.0f && fi < (float)a.width && fj < (float)a.height) {
     const int k = S.kind[__mul24((int)fj, a.width) + (int)fi];  // 24-bit: full-rate multiply
     return k > 0 ? PAL_ROAD : (k == 0 ? PAL_OFFROAD : PAL_FLOOR);
   }
   return PAL_FLOOR;
-}
-
-// phase 4 of render_kernel for a dilation radius known at compile time: the
-// ellipse offsets become constant byte shifts (one v_alignbyte each) and the
-// structuring-element test a scalar branch.
-template <int R>
-__device__ __forceinline__ void write_masks(const FusedLds& S, const LineDev& L, uint8_t* mb) {
-  const uint32_t blo = S.bits_lo, bhi = S.bits_hi;
-  const uint64_t dmask = L.dil_mask;
-  for (int q = threadIdx.x; q < NW / 4; q += blockDim.x) {
-    const int r = q / (WPR / 4), cw0 = 4 * (q - r * (WPR / 4));
-    uint32_t dil[4] = {0, 0, 0, 0};
-#pragma unroll
-    for (int dy = -R; dy <= R; ++dy) {
-      const int rr = r + dy;
-      if ((unsigned)rr >= (unsigned)H) continue;
-      const uint32_t* row = S.img + rr * WPR;
-      const uint4 cur = *reinterpret_cast<const uint4*>(row + cw0);
-      // palette index bytes -> colour-bit bytes (v_perm LUT); 0 outside the image
-      const uint32_t wv[6] = {
-          cw0 > 0 ? __builtin_amdgcn_perm(bhi, blo, row[cw0 - 1]) : 0u,
-          __builtin_amdgcn_perm(bhi, blo, cur.x), __builtin_amdgcn_perm(bhi, blo, cur.y),
-          __builtin_amdgcn_perm(bhi, blo, cur.z), __builtin_amdgcn_perm(bhi, blo, cur.w),
-          cw0 + 4 < WPR ? __builtin_amdgcn_perm(bhi, blo, row[cw0 + 4]) : 0u};
-#pragma unroll
-      for (int dx = -R; dx <= R; ++dx) {
-        if (!((dmask >> ((dy + 3) * 7 + (dx + 3))) & 1ull)) continue;  // uniform
-#pragma unroll
-        for (int j = 0; j < 4; ++j) dil[j] |= shift_bytes(wv[j], wv[j + 1], wv[j + 2], dx);
-      }
-    }
-    // edge bytes from the 16 work entries of this chunk
-    const uint16_t* wk = S.work + r * W + 4 * cw0;
-    uint32_t edg[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const uint2 v = *reinterpret_cast<const uint2*>(wk + 4 * j);
-      // the high byte of each 16-bit entry (v_perm), EDGE = its bit 6
-      edg[j] = (__builtin_amdgcn_perm(v.y, v.x, 0x07050301u) >> 6) & 0x01010101u;
-    }
-    uint32_t o[4][4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      o[0][j] = bytes01_to_ff(dil[j] & 0x01010101u);
-      o[1][j] = bytes01_to_ff((dil[j] >> 1) & 0x01010101u);
-      o[2][j] = bytes01_to_ff((dil[j] >> 2) & 0x01010101u);
-      o[3][j] = bytes01_to_ff(edg[j]);
-    }
-    const int p0 = r * W + 4 * cw0;
-#pragma unroll
-    for (int k = 0; k < 4; ++k)
-      *reinterpret_cast<uint4*>(mb + k * NPIX + p0) = make_uint4(o[k][0], o[k][1], o[k][2],
-                                                                  o[k][3]);
-  }
 }
 
 __device__ inline View view_of(double x, double z, double ang, double cam_fwd) {
@@ -624,283 +573,129 @@ __device__ inline View view_of(double x, double z, double ang, double cam_fwd) {
   return v;
 }
 
-// One env of render_kernel.
-__device__ __forceinline__ void render_env(const RenderArgs& a, FusedLds& S, int e) {
+// Where the work entries and the list of a slot live: LDS below cap; with
+// kSpill, the per-env global spill area at and above it.
+template <bool kSpill>
+struct Slots {
+  RenderLds& S;
+  uint16_t* gent;   // spill: entries of slot s at [4 s]
+  uint16_t* glist;  // spill: word of slot s at [s]
+  int cap;
+  __device__ uint2 ent4(int s) const {
+    if (!kSpill || s < cap) return *reinterpret_cast<const uint2*>(S.u.w.ent + 4 * s);
+    return *reinterpret_cast<const uint2*>(gent + 4 * s);
+  }
+  __device__ void set_ent4(int s, uint2 v) const {
+    if (!kSpill || s < cap)
+      *reinterpret_cast<uint2*>(S.u.w.ent + 4 * s) = v;
+    else
+      *reinterpret_cast<uint2*>(gent + 4 * s) = v;
+  }
+  __device__ uint16_t ent(int s, int i) const {
+    if (!kSpill || s < cap) return S.u.w.ent[4 * s + i];
+    return gent[4 * s + i];
+  }
+  __device__ void set_ent(int s, int i, uint16_t v) const {
+    if (!kSpill || s < cap)
+      S.u.w.ent[4 * s + i] = v;
+    else
+      gent[4 * s + i] = v;
+  }
+  __device__ int word(int s) const {
+    if (!kSpill || s < cap) return S.u.w.list[s];
+    return glist[s];
+  }
+  // work entry of pixel (r, c): 0 outside the image and in unlisted words
+  __device__ uint32_t at(int r, int c) const {
+    if ((unsigned)r >= (unsigned)H || (unsigned)c >= (unsigned)W) return 0u;
+    const int s = S.wmap[r * WPR + (c >> 2)];
+    return s ? (uint32_t)ent(s - 1, c & 3) : 0u;
+  }
+};
+
+// phase 4 for one listed quad and a dilation radius known at compile time:
+// the ellipse offsets become constant byte shifts (one v_alignbyte each) and
+// the structuring-element test a scalar branch.
+template <int R, bool kSpill>
+__device__ __forceinline__ void quad_masks(const RenderLds& S, const Slots<kSpill>& sl,
+                                           const LineDev& L, uint8_t* mb, int q) {
+  const uint32_t blo = S.bits_lo, bhi = S.bits_hi;
+  const uint64_t dmask = L.dil_mask;
+  const int r = q / QPR, cw0 = 4 * (q - r * QPR);
+  uint32_t dil[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int dy = -R; dy <= R; ++dy) {
+    const int rr = r + dy;
+    if ((unsigned)rr >= (unsigned)H) continue;
+    const uint32_t* row = S.img + rr * WPR;
+    const uint4 cur = *reinterpret_cast<const uint4*>(row + cw0);
+    // raster bytes -> colour-bit bytes (v_perm LUT); 0 outside the image
+    const uint32_t wv[6] = {
+        cw0 > 0 ? __builtin_amdgcn_perm(bhi, blo, row[cw0 - 1]) : 0u,
+        __builtin_amdgcn_perm(bhi, blo, cur.x), __builtin_amdgcn_perm(bhi, blo, cur.y),
+        __builtin_amdgcn_perm(bhi, blo, cur.z), __builtin_amdgcn_perm(bhi, blo, cur.w),
+        cw0 + 4 < WPR ? __builtin_amdgcn_perm(bhi, blo, row[cw0 + 4]) : 0u};
+#pragma unroll
+    for (int dx = -R; dx <= R; ++dx) {
+      if (!((dmask >> ((dy + 3) * 7 + (dx + 3))) & 1ull)) continue;  // uniform
+#pragma unroll
+      for (int j = 0; j < 4; ++j) dil[j] |= shift_bytes(wv[j], wv[j + 1], wv[j + 2], dx);
+    }
+  }
+  // edge bytes from the work entries of the quad's listed words
+  const uint64_t wm = *reinterpret_cast<const uint64_t*>(S.wmap + r * WPR + cw0);
+  uint32_t edg[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int s = (int)((wm >> (16 * j)) & 0xFFFFu);
+    const uint2 v = s ? sl.ent4(s - 1) : make_uint2(0u, 0u);
+    // the high byte of each 16-bit entry (v_perm), EDGE = its bit 6
+    edg[j] = (__builtin_amdgcn_perm(v.y, v.x, 0x07050301u) >> 6) & 0x01010101u;
+  }
+  uint32_t o[4][4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    o[0][j] = bytes01_to_ff(dil[j] & 0x01010101u);
+    o[1][j] = bytes01_to_ff((dil[j] >> 1) & 0x01010101u);
+    o[2][j] = bytes01_to_ff((dil[j] >> 2) & 0x01010101u);
+    o[3][j] = bytes01_to_ff(edg[j]);
+  }
+  const int p0 = r * W + 4 * cw0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    *reinterpret_cast<uint4*>(mb + k * NPIX + p0) = make_uint4(o[k][0], o[k][1], o[k][2], o[k][3]);
+}
+
+// Phases 2a-3 (Sobel, NMS, hysteresis) on the listed words.
+template <bool kSpill>
+__device__ __forceinline__ void canny(const RenderArgs& a, RenderLds& S, int e,
+                                                int nlist) {
   const int tid = threadIdx.x;
+  constexpr int T = kRenderThreads;
   const LineDev& L = a.line;
-  const int T = blockDim.x, nmark = a.n_yellow + a.n_white;
-  const bool mfast = nmark <= 4 * T;
-#ifdef DTSIM_STAMPS
-  RENSTAMP(0, __builtin_amdgcn_s_memrealtime());
-  RENSTAMP(2, ren_hw_id());
-  RENSTAMP(3, ren_xcc_id());
-#endif
-  RENT(4);
-  RENT(5);
-  int32_t* const C = S.cnt;
-  const View V = S.view;
-  // the marking segments' loads (L2-resident), first used after the background
-  float4 mq[4];
-  if (mfast && !(a.skip & 2)) {
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int sidx = tid + k * T;
-      mq[k] = sidx < nmark ? a.marks[sidx] : make_float4(-1e9f, -1e9f, -1e9f, -1e9f);
-    }
-  }
-
-  // phase 0: background.  Tiles are convex and each coordinate is a monotone
-  // float function of the column, so along a row the tile index steps
-  // monotonically.  0a: a 16-pixel span (4 words) per lane; its end pixels'
-  // tiles decide it when they are one tile, or two edge-adjacent tiles of one
-  // colour (then every pixel between is in one of the two); such spans are one
-  // 16-byte store.  The rest (a tile edge of two colours, or a corner, inside)
-  // are listed (wave-aggregated) and 0b resolves them a word per lane, so the
-  // per-pixel path runs only where it is needed instead of on every lane of a
-  // wave that holds one such span.
-  const auto tile_f = [&](int r, int c, float& fi, float& fj) {
-    const float f = (119.5f - (float)r) * kRes;
-    const float bx = V.cx + f * V.dirx, bz = V.cz + f * V.dirz;
-    const float l = ((float)c - 79.5f) * kRes;
-    const float wx = bx + l * V.rx, wz = bz + l * V.rz;
-    fi = floorf(wx * a.inv_ts);
-    fj = floorf(wz * a.inv_ts);
-  };
-  constexpr int NSPAN = NW / 4;
-  for (int q0 = 0; q0 < NSPAN && !(a.skip & 1); q0 += blockDim.x) {
-    const int q = q0 + tid;
-    bool want[4] = {false, false, false, false};
-    uint16_t val[4] = {(uint16_t)q, 0, 0, 0};
-    if (q < NSPAN) {
-      const int r = q / (WPR / 4), c0 = 16 * (q - r * (WPR / 4));
-      float fi0, fj0, fi1, fj1;
-      tile_f(r, c0, fi0, fj0);
-      tile_f(r, c0 + 15, fi1, fj1);
-      const uint32_t col0 = bg_color(S, a, fi0, fj0);
-      bool uni = fi0 == fi1 && fj0 == fj1;
-      if (!uni && fabsf(fi1 - fi0) + fabsf(fj1 - fj0) == 1.0f)
-        uni = bg_color(S, a, fi1, fj1) == col0;
-      if (uni) {
-        const uint32_t wd = splat_byte(col0);
-        *reinterpret_cast<uint4*>(S.img + 4 * q) = make_uint4(wd, wd, wd, wd);
-      }
-      want[0] = !uni;
-    }
-    wave_push4(&C[kNList], S.list, NW, want, val);
-  }
-  __syncthreads();
-  {
-    const int nspan = C[kNList];
-    for (int i = tid; i < 4 * nspan; i += blockDim.x) {
-      const int q = S.list[i >> 2];
-      const int r = q / (WPR / 4), c = 16 * (q - r * (WPR / 4)) + 4 * (i & 3);
-      float fi[4], fj[4];
-      tile_f(r, c, fi[0], fj[0]);
-      tile_f(r, c + 3, fi[3], fj[3]);
-      const uint32_t col0 = bg_color(S, a, fi[0], fj[0]);
-      uint32_t wd;
-      if (fi[0] == fi[3] && fj[0] == fj[3]) {
-        wd = splat_byte(col0);
-      } else {
-        tile_f(r, c + 1, fi[1], fj[1]);
-        tile_f(r, c + 2, fi[2], fj[2]);
-        wd = col0;
-#pragma unroll
-        for (int k = 1; k < 4; ++k) wd |= bg_color(S, a, fi[k], fj[k]) << (8 * k);
-      }
-      S.img[4 * q + (i & 3)] = wd;
-    }
-  }
-  __syncthreads();
-  if (tid == 0) C[kNList] = 0;   // the span list is consumed; phase 1 reuses it
-  RENT(6);
-  uint8_t* img8 = reinterpret_cast<uint8_t*>(S.img);
-  // markings: yellow, then white over it.  Every lane projects up to four
-  // segments and lists the visible ones (pixel endpoints as int16 x 4) in the
-  // work image, which is scratch until phase 1; after a barrier the lanes draw
-  // the listed segments, so no lane idles on a culled one while another walks
-  // a line.  Up to 4 x blockDim segments (mfast) their loads were issued at
-  // kernel entry and the two colours are listed in one pass (yellow from the
-  // bottom of the scratch, white from the top); more take batches.
-  if (!(a.skip & 2)) {
-    uint2* segl = reinterpret_cast<uint2*>(S.work);
-    constexpr int kSegCap = NPIX / 4;  // uint2 records in the work image
-    const auto pack = [](int c0, int r0, int c1, int r1) {
-      return make_uint2((uint32_t)(uint16_t)c0 | ((uint32_t)(uint16_t)r0 << 16),
-                        (uint32_t)(uint16_t)c1 | ((uint32_t)(uint16_t)r1 << 16));
-    };
-    const auto draw = [&](uint2 v, uint8_t col) {
-      draw_line((lds_u8*)img8, (int)(int16_t)(v.x & 0xFFFFu), (int)(int16_t)(v.x >> 16),
-                (int)(int16_t)(v.y & 0xFFFFu), (int)(int16_t)(v.y >> 16), col);
-    };
-    constexpr int kParts = DTSIM_MARK_PARTS;
-    const auto draw_part = [&](uint2 v, uint8_t col, int part) {
-      draw_line_part((lds_u8*)img8, (int)(int16_t)(v.x & 0xFFFFu), (int)(int16_t)(v.x >> 16),
-                     (int)(int16_t)(v.y & 0xFFFFu), (int)(int16_t)(v.y >> 16), col, part, kParts);
-    };
-    if (mfast) {
-      bool vy[4], vw[4];
-      int cc0[4], rr0[4], cc1[4], rr1[4], sy[4], sw[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int sidx = tid + k * T;
-        const bool v = sidx < nmark && project_seg(V, mq[k], cc0[k], rr0[k], cc1[k], rr1[k]);
-        vy[k] = v && sidx < a.n_yellow;
-        vw[k] = v && sidx >= a.n_yellow;
-      }
-      RENT(16);
-      wave_slots4x2(&C[kNSeg], vy, vw, sy, sw);  // yellow count | white count << 16
-      RENT(17);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        if (vy[k]) segl[sy[k]] = pack(cc0[k], rr0[k], cc1[k], rr1[k]);
-        if (vw[k]) segl[kSegCap - 1 - sw[k]] = pack(cc0[k], rr0[k], cc1[k], rr1[k]);
-      }
-      __syncthreads();
-      RENT(14);
-      // kParts lanes per segment, each drawing its share of the pixels
-      const int ny = C[kNSeg] & 0xFFFF, nw = (int)((uint32_t)C[kNSeg] >> 16);
-      for (int i = tid; i < kParts * ny; i += T) draw_part(segl[i / kParts], PAL_YELLOW, i % kParts);
-      __syncthreads();
-      RENT(18);
-      for (int i = tid; i < kParts * nw; i += T)
-        draw_part(segl[kSegCap - 1 - i / kParts], PAL_WHITE, i % kParts);
-#ifdef DTSIM_STAMPS
-      if (tid == 0) C[kNSeg] = ny + nw;
-#endif
-    } else {
-      const int batch = 4 * T;  // <= kSegCap (T <= 1024 -> 4096)
-      int listed = 0;           // S.nseg at the start of the batch
-#pragma unroll 1
-      for (int colr = 0; colr < 2; ++colr) {
-        const float4* seg = colr == 0 ? a.marks : a.marks + a.n_yellow;
-        const int nseg = colr == 0 ? a.n_yellow : a.n_white;
-        const uint8_t col = colr == 0 ? PAL_YELLOW : PAL_WHITE;
-#pragma unroll 1
-        for (int b0 = 0; b0 < nseg; b0 += batch) {
-          const int bn = nseg - b0 < batch ? nseg - b0 : batch;
-          float4 q[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int sidx = tid + k * T;
-            q[k] = sidx < bn ? seg[b0 + sidx] : make_float4(-1e9f, -1e9f, -1e9f, -1e9f);
-          }
-          bool vis[4];
-          int cc0[4], rr0[4], cc1[4], rr1[4], slot[4];
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            vis[k] = tid + k * T < bn && project_seg(V, q[k], cc0[k], rr0[k], cc1[k], rr1[k]);
-          wave_slots4(&C[kNSeg], vis, slot);
-#pragma unroll
-          for (int k = 0; k < 4; ++k)
-            if (vis[k]) segl[slot[k] % kSegCap] = pack(cc0[k], rr0[k], cc1[k], rr1[k]);
-          __syncthreads();
-          const int end = C[kNSeg];
-          for (int i = listed + tid; i < end; i += T) draw(segl[i % kSegCap], col);
-          listed = end;
-          __syncthreads();
-        }
-      }
-    }
-  }
-  __syncthreads();
-  RENT(7);
-
-  // phase 1: exact uniformity test of the 3 x 6 byte neighbourhood, grey.  A
-  // lane takes a column of 4 words (rows 4g..4g+3 of word column cw), so the
-  // 6 x 3 words around them are loaded once for all four, and a wave's
-  // grey stores of one row are contiguous.
-  const bool fresh = a.fresh != nullptr && a.fresh[e] != 0;
-  float* gbase = a.gray ? a.gray + (size_t)e * a.slots * NPIX : nullptr;
-  constexpr int kRowsPerLane = 4, NQ = NW / kRowsPerLane;
-  for (int q0 = 0; q0 < NQ && !(a.skip & 4); q0 += blockDim.x) {
-    const int q = q0 + tid;
-    const bool act = q < NQ;
-    bool uni[kRowsPerLane] = {false, false, false, false};
-    int wq[kRowsPerLane] = {0, 0, 0, 0};
-    if (act) {
-      const int rg = q / WPR, cw = q - rg * WPR, r0 = kRowsPerLane * rg;
-      // side words at the image edge clamp to the word itself: BORDER_REPLICATE
-      // repeats the edge pixel, whose byte the mid / up / down comparisons
-      // already cover; rows clamp the same way
-      const int cl = cw > 0 ? cw - 1 : cw, cr = cw < WPR - 1 ? cw + 1 : cw;
-      uint32_t col[kRowsPerLane + 2][3];
-#pragma unroll
-      for (int i = 0; i < kRowsPerLane + 2; ++i) {
-        int rr = r0 - 1 + i;
-        rr = rr < 0 ? 0 : (rr > H - 1 ? H - 1 : rr);
-        col[i][0] = S.img[rr * WPR + cl];
-        col[i][1] = S.img[rr * WPR + cw];
-        col[i][2] = S.img[rr * WPR + cr];
-      }
-#pragma unroll
-      for (int k = 0; k < kRowsPerLane; ++k) {
-        const int w = (r0 + k) * WPR + cw;
-        wq[k] = w;
-        const uint32_t mid = col[k + 1][1], up = col[k][1], dn = col[k + 2][1];
-        const uint32_t b = mid & 255u;
-        const uint32_t rep = splat_byte(b);
-        const uint32_t diff =
-            (mid ^ rep) | (up ^ rep) | (dn ^ rep) |
-            (((col[k][0] >> 24) ^ b) | ((col[k + 1][0] >> 24) ^ b) | ((col[k + 2][0] >> 24) ^ b)) |
-            (((col[k][2] ^ b) | (col[k + 1][2] ^ b) | (col[k + 2][2] ^ b)) & 255u);
-        uni[k] = diff == 0u;
-        // every word's work entries start at 0; phase 2a overwrites the listed ones
-        *reinterpret_cast<uint2*>(S.work + 4 * w) = make_uint2(0u, 0u);
-        if (gbase) {
-          float4 g;
-          g.x = S.pal_gray[mid & 255u];
-          g.y = S.pal_gray[(mid >> 8) & 255u];
-          g.z = S.pal_gray[(mid >> 16) & 255u];
-          g.w = S.pal_gray[mid >> 24];
-          if (fresh) {
-#pragma clang loop vectorize(disable) interleave(disable)
-            for (int sl = 0; sl < a.slots; ++sl)  // 16-B stores, not split by the vectoriser
-              *reinterpret_cast<float4*>(gbase + sl * NPIX + 4 * w) = g;
-          } else {
-            *reinterpret_cast<float4*>(gbase + a.slot * NPIX + 4 * w) = g;
-          }
-        }
-        if (a.rgb) {
-          uint8_t* o = a.rgb + ((size_t)e * NPIX + 4 * w) * 3;
-          for (int i = 0; i < 4; ++i) {
-            const uint32_t p = kPalette[(mid >> (8 * i)) & 255u];
-            o[3 * i + 0] = (p >> 16) & 255;
-            o[3 * i + 1] = (p >> 8) & 255;
-            o[3 * i + 2] = p & 255;
-          }
-        }
-      }
-    }
-    static_assert(kRowsPerLane == 4, "wave_push4 takes four items per lane");
-    bool push[4];
-    uint16_t pv[4];
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      push[k] = act && !uni[k];
-      pv[k] = (uint16_t)wq[k];
-    }
-    wave_push4(&C[kNList], S.list, NW, push, pv);
-  }
-  __syncthreads();
-  RENT(8);
+  Slots<kSpill> sl{S, a.spill + (size_t)e * kSpillHalves, a.spill + (size_t)e * kSpillHalves + 4 * NW,
+                   a.list_cap};
+  const uint8_t* img8 = reinterpret_cast<const uint8_t*>(S.img);
 
   // phase 2a: gradients of the listed words
-  const int nlist = (a.skip & 8) ? 0 : C[kNList];
-  for (int li = tid; li < nlist; li += blockDim.x) {
-    const int w = S.list[li];
-    const int r = w / WPR, c0 = 4 * (w - r * WPR);
+  for (int s = tid; s < nlist; s += T) {
+    const int w = sl.word(s);
+    const int r = w / WPR, cw = w - r * WPR;
     const int rows[3] = {r > 0 ? r - 1 : 0, r, r < H - 1 ? r + 1 : H - 1};
     uint32_t nb[3][6];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
-      const uint8_t* rowp = img8 + rows[k] * W;
-#pragma unroll
-      for (int j = 0; j < 6; ++j) {
-        int cc = c0 - 1 + j;
-        cc = cc < 0 ? 0 : (cc > W - 1 ? W - 1 : cc);
-        nb[k][j] = S.pal_swar[rowp[cc]];
-      }
+      const uint32_t* rowp = S.img + rows[k] * WPR;
+      const uint32_t m = rowp[cw];
+      // BORDER_REPLICATE: the pixel left of column 0 is column 0, right of 159 is 159
+      const uint32_t lb = cw > 0 ? rowp[cw - 1] >> 24 : (m & 255u);
+      const uint32_t rb = cw < WPR - 1 ? rowp[cw + 1] & 255u : (m >> 24);
+      nb[k][0] = S.pal_swar[lb];
+      nb[k][1] = S.pal_swar[m & 255u];
+      nb[k][2] = S.pal_swar[(m >> 8) & 255u];
+      nb[k][3] = S.pal_swar[(m >> 16) & 255u];
+      nb[k][4] = S.pal_swar[m >> 24];
+      nb[k][5] = S.pal_swar[rb];
     }
     uint32_t out[2] = {0u, 0u};
 #pragma unroll
@@ -911,20 +706,20 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, FusedLds& S, int
       const uint32_t v = (uint32_t)m | ((uint32_t)nms_dir(dx, dy) << WK_DIR_SHIFT);
       out[i >> 1] |= v << (16 * (i & 1));
     }
-    *reinterpret_cast<uint2*>(S.work + 4 * w) = make_uint2(out[0], out[1]);
+    sl.set_ent4(s, make_uint2(out[0], out[1]));
   }
   __syncthreads();
   RENT(9);
 
   // phase 2b: NMS + double threshold on the listed words
-  for (int i0 = 0; i0 < nlist; i0 += blockDim.x) {
-    const int li = i0 + tid;
-    uint16_t wk[4] = {0, 0, 0, 0};
+  for (int s0 = 0; s0 < nlist; s0 += T) {
+    const int s = s0 + tid;
     bool want[4] = {false, false, false, false};
-    if (li < nlist) {
-      const int w = S.list[li];
+    uint16_t wk[4] = {0, 0, 0, 0};
+    if (s < nlist) {
+      const int w = sl.word(s);
       const int r = w / WPR, c0 = 4 * (w - r * WPR);
-      const uint2 cur = *reinterpret_cast<const uint2*>(S.work + 4 * w);
+      const uint2 cur = sl.ent4(s);
       const uint32_t vv[4] = {cur.x & 0xFFFFu, cur.x >> 16, cur.y & 0xFFFFu, cur.y >> 16};
       uint32_t setb[4] = {0, 0, 0, 0};
 #pragma unroll
@@ -936,8 +731,8 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, FusedLds& S, int
           // dir 0: (0,-1)/(0,+1); 1: (-1,0)/(+1,0); 2: (-1,-1)/(+1,+1); 3: (-1,+1)/(+1,-1)
           const int dy1 = dir == 0 ? 0 : -1;
           const int dx1 = dir == 0 ? -1 : (dir == 1 ? 0 : (dir == 2 ? -1 : 1));
-          const int n1 = mag16(S, r + dy1, c + dx1);
-          const int n2 = mag16(S, r - dy1, c - dx1);
+          const int n1 = (int)(sl.at(r + dy1, c + dx1) & WK_MAG);
+          const int n2 = (int)(sl.at(r - dy1, c - dx1) & WK_MAG);
           const bool keep = m > n1 && (dir >= 2 ? m > n2 : m >= n2);
           if (keep) {
             if (m > L.canny_hi) {
@@ -953,40 +748,42 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, FusedLds& S, int
       // only this lane writes these four entries; neighbours read only the
       // magnitude bits, which do not change
       if (setb[0] | setb[1] | setb[2] | setb[3])
-        *reinterpret_cast<uint2*>(S.work + 4 * w) =
-            make_uint2(cur.x | setb[0] | (setb[1] << 16), cur.y | setb[2] | (setb[3] << 16));
+        sl.set_ent4(s, make_uint2(cur.x | setb[0] | (setb[1] << 16),
+                                  cur.y | setb[2] | (setb[3] << 16)));
     }
-    wave_push4(&C[kNWeak], S.weak, kWeakCap, want, wk);
+    wave_push4(&S.cnt[kNWeak], S.weak, kWeakCap, want, wk);
   }
   __syncthreads();
   RENT(10);
 
   // phase 3: hysteresis (weak candidates 8-connected to an edge become edges)
-  const int nweak = (a.skip & 16) ? 0 : C[kNWeak];
+  const int nweak = S.cnt[kNWeak];
   if (nweak > 0) {
     const bool overflow = nweak > kWeakCap;
-    const int cnt = overflow ? NPIX : nweak;
+    const int cnt = overflow ? 4 * nlist : nweak;
     for (;;) {
       int changed = 0;
-      for (int i = tid; i < cnt; i += blockDim.x) {
-        const int idx = overflow ? i : S.weak[i];
-        const uint16_t b = S.work[idx];
-        if ((b & (WK_CAND | WK_EDGE)) != WK_CAND) continue;
+      for (int i = tid; i < cnt; i += T) {
+        int idx;
+        if (overflow) {
+          const int w = sl.word(i >> 2);
+          const int r = w / WPR;
+          idx = r * W + 4 * (w - r * WPR) + (i & 3);
+        } else {
+          idx = S.weak[i];
+        }
         const int r = idx / W, c = idx - r * W;
+        const uint32_t b = sl.at(r, c);
+        if ((b & (WK_CAND | WK_EDGE)) != WK_CAND) continue;
         bool hit = false;
-        for (int dy = -1; dy <= 1 && !hit; ++dy) {
-          const int rr = r + dy;
-          if ((unsigned)rr >= (unsigned)H) continue;
-          for (int dx = -1; dx <= 1; ++dx) {
-            const int cc = c + dx;
-            if ((unsigned)cc < (unsigned)W && (S.work[rr * W + cc] & WK_EDGE)) {
+        for (int dy = -1; dy <= 1 && !hit; ++dy)
+          for (int dx = -1; dx <= 1; ++dx)
+            if (sl.at(r + dy, c + dx) & WK_EDGE) {
               hit = true;
               break;
             }
-          }
-        }
         if (hit) {
-          S.work[idx] = b | WK_EDGE;
+          sl.set_ent(S.wmap[r * WPR + (c >> 2)] - 1, c & 3, (uint16_t)(b | WK_EDGE));
           changed = 1;
         }
       }
@@ -994,35 +791,343 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, FusedLds& S, int
     }
   }
   RENT(11);
-#ifdef DTSIM_STAMPS
-  RENSTAMP(12, (unsigned long long)nlist | ((unsigned long long)nweak << 32));
-  RENSTAMP(15, (unsigned long long)C[kNSeg]);
-#endif
 
-  // phase 4: masks, 16 pixels (4 words) per lane
-  if (a.masks && !(a.skip & 32)) {
-    uint8_t* mb = a.masks + (size_t)e * 4 * NPIX;
-    switch (L.dil_r) {
-      case 0: write_masks<0>(S, L, mb); break;
-      case 1: write_masks<1>(S, L, mb); break;
-      case 2: write_masks<2>(S, L, mb); break;
-      default: write_masks<3>(S, L, mb); break;
+}
+
+// Output phase: grey of every pixel and the four masks of every quad, no
+// barrier after.  Grey: a wave's 64 quads are 256 consecutive words, stored as
+// four 1-KB wave instructions (lane l of store j writes word 64 j + l of the
+// wave's run).  Masks: a lane per quad, consecutive lanes consecutive 16-B
+// pieces of each plane, so every line of a plane is written whole by one
+// instruction: a quad without a listed word (and radius <= 1) takes its own
+// colour bits, the others the dilation + edge path.
+template <bool kSpill>
+__device__ __forceinline__ void write_outputs(const RenderArgs& a, RenderLds& S, int e,
+                                              uint8_t* mbase) {
+  const int tid = threadIdx.x;
+  constexpr int T = kRenderThreads;
+  const LineDev& L = a.line;
+  const Slots<kSpill> sl{S, a.spill + (size_t)e * kSpillHalves,
+                         a.spill + (size_t)e * kSpillHalves + 4 * NW, a.list_cap};
+  const bool fresh = a.fresh != nullptr && a.fresh[e] != 0;
+  float* gbase = a.gray ? a.gray + (size_t)e * a.slots * NPIX : nullptr;
+  const uint32_t blo = S.bits_lo, bhi = S.bits_hi;
+  const bool quick_masks = L.dil_r <= 1;
+  const int lane = tid & 63;
+  for (int q0 = 0; q0 < NQ; q0 += T) {
+    const int wbase = 4 * (q0 + (tid - lane));
+    if (gbase) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int w = wbase + 64 * j + lane;
+        if (w < NW) {
+          const uint32_t v = S.img[w];
+          float4 g;
+          g.x = S.pal_gray[v & 255u];
+          g.y = S.pal_gray[(v >> 8) & 255u];
+          g.z = S.pal_gray[(v >> 16) & 255u];
+          g.w = S.pal_gray[v >> 24];
+          if (fresh) {
+#pragma clang loop vectorize(disable) interleave(disable)
+            for (int k = 0; k < a.slots; ++k)
+              *reinterpret_cast<float4*>(gbase + k * NPIX + 4 * w) = g;
+          } else {
+            *reinterpret_cast<float4*>(gbase + a.slot * NPIX + 4 * w) = g;
+          }
+        }
+      }
+    }
+    const int q = q0 + tid;
+    if (q < NQ) {
+      if (mbase) {
+        if (quick_masks && *reinterpret_cast<const uint64_t*>(S.wmap + 4 * q) == 0ull) {
+          const uint4 m = *reinterpret_cast<const uint4*>(S.img + 4 * q);
+          const uint32_t mw[4] = {m.x, m.y, m.z, m.w};
+          uint32_t o[3][4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const uint32_t cb = __builtin_amdgcn_perm(bhi, blo, mw[j]);
+            o[0][j] = bytes01_to_ff(cb & 0x01010101u);
+            o[1][j] = bytes01_to_ff((cb >> 1) & 0x01010101u);
+            o[2][j] = bytes01_to_ff((cb >> 2) & 0x01010101u);
+          }
+#pragma unroll
+          for (int k = 0; k < 3; ++k)
+            *reinterpret_cast<uint4*>(mbase + k * NPIX + 16 * q) =
+                make_uint4(o[k][0], o[k][1], o[k][2], o[k][3]);
+          *reinterpret_cast<uint4*>(mbase + 3 * NPIX + 16 * q) = make_uint4(0u, 0u, 0u, 0u);
+        } else {
+          switch (L.dil_r) {
+            case 0: quad_masks<0>(S, sl, L, mbase, q); break;
+            case 1: quad_masks<1>(S, sl, L, mbase, q); break;
+            case 2: quad_masks<2>(S, sl, L, mbase, q); break;
+            default: quad_masks<3>(S, sl, L, mbase, q); break;
+          }
+        }
+      }
+      if (a.rgb) {
+        const uint4 m = *reinterpret_cast<const uint4*>(S.img + 4 * q);
+        uint8_t* o = a.rgb + ((size_t)e * NPIX + 16 * q) * 3;
+        const uint32_t mw[4] = {m.x, m.y, m.z, m.w};
+        for (int i = 0; i < 16; ++i) {
+          const uint32_t p = kPalette[(mw[i >> 2] >> (8 * (i & 3))) & 255u];
+          o[3 * i + 0] = (p >> 16) & 255;
+          o[3 * i + 1] = (p >> 8) & 255;
+          o[3 * i + 2] = p & 255;
+        }
+      }
     }
   }
-  RENT(13);
+}
+
+// One env of render_kernel.
+__device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, int e) {
+  const int tid = threadIdx.x;
+  constexpr int T = kRenderThreads;
+  const LineDev& L = a.line;
+  const int nmark = a.n_yellow + a.n_white;
+  const bool mfast = nmark <= kMarkFast;
 #ifdef DTSIM_STAMPS
+  RENSTAMP(0, __builtin_amdgcn_s_memrealtime());
+  RENSTAMP(2, ren_hw_id());
+  RENSTAMP(3, ren_xcc_id());
+#endif
+  RENT(4);
+  int32_t* const C = S.cnt;
+  const View V = S.view;
+  lds_u32* const img = (lds_u32*)S.img;
+  // the marking segments' loads (L2-resident), first used after the background
+  float4 mq[4];
+  if (mfast) {
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int sidx = tid + k * T;
+      mq[k] = sidx < nmark ? a.marks[sidx] : make_float4(-1e9f, -1e9f, -1e9f, -1e9f);
+    }  // (mfast: nmark <= kMarkFast <= 4 T)
+  }
+
+  // phase 0a: background.  Tiles are convex and each coordinate is a monotone
+  // float function of the column, so along a row the tile index steps
+  // monotonically: a 16-pixel span whose end pixels lie in one tile, or in two
+  // edge-adjacent tiles of one colour, is that colour (every pixel between is
+  // in one of the two): one 16-byte store.  The others are zeroed and listed;
+  // 0b resolves them a word per lane.
+  const auto tile_f = [&](int r, int c, float& fi, float& fj) {
+    const float f = (119.5f - (float)r) * kRes;
+    const float bx = V.cx + f * V.dirx, bz = V.cz + f * V.dirz;
+    const float l = ((float)c - 79.5f) * kRes;
+    const float wx = bx + l * V.rx, wz = bz + l * V.rz;
+    fi = floorf(wx * a.inv_ts);
+    fj = floorf(wz * a.inv_ts);
+  };
+  for (int q0 = 0; q0 < NQ; q0 += T) {
+    const int q = q0 + tid;
+    bool want = false;
+    if (q < NQ) {
+      const int r = q / QPR, c0 = 16 * (q - r * QPR);
+      float fi0, fj0, fi1, fj1;
+      tile_f(r, c0, fi0, fj0);
+      tile_f(r, c0 + 15, fi1, fj1);
+      const uint32_t col0 = bg_color(S, a, fi0, fj0);
+      bool uni = fi0 == fi1 && fj0 == fj1;
+      if (!uni && fabsf(fi1 - fi0) + fabsf(fj1 - fj0) == 1.0f)
+        uni = bg_color(S, a, fi1, fj1) == col0;
+      const uint32_t wd = uni ? splat_byte(col0) : 0u;
+      *reinterpret_cast<uint4*>(S.img + 4 * q) = make_uint4(wd, wd, wd, wd);
+      want = !uni;
+    }
+    const int slot = wave_slot1(&C[kNSpan], want);
+    if (want) S.qlist[slot] = (uint16_t)q;
+  }
+  // ... and the markings' projection: every lane projects up to four segments
+  // and lists the visible ones (pixel endpoints as int16 x 4; yellow from the
+  // bottom of the record area, white from the top)
+  if (mfast) {
+    bool vy[4], vw[4];
+    int cc0[4], rr0[4], cc1[4], rr1[4], sy[4], sw[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int sidx = tid + k * T;
+      const bool v = sidx < nmark && project_seg(V, mq[k], cc0[k], rr0[k], cc1[k], rr1[k]);
+      vy[k] = v && sidx < a.n_yellow;
+      vw[k] = v && sidx >= a.n_yellow;
+    }
+    wave_slots4x2(&C[kNSeg], vy, vw, sy, sw);  // yellow count | white count << 16
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      if (vy[k]) S.u.seg[sy[k]] = seg_pack(cc0[k], rr0[k], cc1[k], rr1[k]);
+      if (vw[k]) S.u.seg[kSegRecs - 1 - sw[k]] = seg_pack(cc0[k], rr0[k], cc1[k], rr1[k]);
+    }
+  }
+  __syncthreads();
+  RENT(5);
+
+  // phase 0b: the listed spans' words and the marking segments (DTSIM_MARK_PARTS
+  // lanes per segment), all OR-ed into the image in one pass
+  constexpr int kParts = DTSIM_MARK_PARTS;
+  {
+    const int nspan = C[kNSpan];
+    const int ny = mfast ? (C[kNSeg] & 0xFFFF) : 0, nw = mfast ? (int)((uint32_t)C[kNSeg] >> 16) : 0;
+    const int nbg = 4 * nspan, items = nbg + kParts * (ny + nw);
+    for (int i = tid; i < items; i += T) {
+      if (i < nbg) {
+        const int q = S.qlist[i >> 2];
+        const int r = q / QPR, c = 16 * (q - r * QPR) + 4 * (i & 3);
+        float fi[4], fj[4];
+        tile_f(r, c, fi[0], fj[0]);
+        tile_f(r, c + 3, fi[3], fj[3]);
+        const uint32_t col0 = bg_color(S, a, fi[0], fj[0]);
+        uint32_t wd;
+        if (fi[0] == fi[3] && fj[0] == fj[3]) {
+          wd = splat_byte(col0);
+        } else {
+          tile_f(r, c + 1, fi[1], fj[1]);
+          tile_f(r, c + 2, fi[2], fj[2]);
+          wd = col0;
+#pragma unroll
+          for (int k = 1; k < 4; ++k) wd |= bg_color(S, a, fi[k], fj[k]) << (8 * k);
+        }
+        __hip_atomic_fetch_or(img + 4 * q + (i & 3), wd, __ATOMIC_RELAXED,
+                              __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else {
+        const int j = i - nbg, sidx = j / kParts;
+        const bool yel = sidx < ny;
+        seg_draw(img, S.u.seg[yel ? sidx : kSegRecs - 1 - (sidx - ny)], yel ? PAL_YELLOW : PAL_WHITE,
+                 j - sidx * kParts, kParts);
+      }
+    }
+  }
+  if (!mfast) {
+    // more segments than one projection round: batches of 4 T per colour, each
+    // listed, then drawn (order-free, so batches need no order)
+    int listed = 0;
+#pragma unroll 1
+    for (int colr = 0; colr < 2; ++colr) {
+      const float4* seg = colr == 0 ? a.marks : a.marks + a.n_yellow;
+      const int nseg = colr == 0 ? a.n_yellow : a.n_white;
+      const uint32_t col = colr == 0 ? PAL_YELLOW : PAL_WHITE;
+#pragma unroll 1
+      for (int b0 = 0; b0 < nseg; b0 += kMarkFast) {
+        bool vis[4];
+        int cc0[4], rr0[4], cc1[4], rr1[4], slot[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int sidx = b0 + tid + k * T;
+          const bool in = tid + k * T < kMarkFast && sidx < nseg;
+          const float4 q = in ? seg[sidx] : make_float4(-1e9f, -1e9f, -1e9f, -1e9f);
+          vis[k] = in && project_seg(V, q, cc0[k], rr0[k], cc1[k], rr1[k]);
+        }
+        wave_slots4(&C[kNSeg], vis, slot);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          if (vis[k]) S.u.seg[slot[k] % kSegRecs] = seg_pack(cc0[k], rr0[k], cc1[k], rr1[k]);
+        __syncthreads();
+        const int end = C[kNSeg];
+        for (int i = listed * kParts + tid; i < end * kParts; i += T)
+          seg_draw(img, S.u.seg[(i / kParts) % kSegRecs], col, i % kParts, kParts);
+        listed = end;
+        __syncthreads();
+      }
+    }
+  }
+  __syncthreads();
+  RENT(6);
+
+  // phase 1: per 16-pixel quad (4 words of a row): the 3 x 6-word neighbourhood
+  // decides each word's uniformity exactly (all 18 pixels around it one
+  // byte).  Non-uniform words get a slot (list + wmap); a quad with one takes
+  // the dilation path of the output phase (every quad does when the dilation
+  // radius is >= 2: uniformity only covers +-1 pixel).
+  uint8_t* mbase = a.masks ? a.masks + (size_t)e * 4 * NPIX : nullptr;
+  for (int q0 = 0; q0 < NQ && mbase; q0 += T) {
+    const int q = q0 + tid;
+    const bool act = q < NQ;
+    bool non[4] = {false, false, false, false};
+    int r = 0, cw0 = 0;
+    if (act) {
+      r = q / QPR;
+      cw0 = 4 * (q - r * QPR);
+      uint32_t m[3][4], lw[3], rw[3];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        int rr = r - 1 + k;
+        rr = rr < 0 ? 0 : (rr > H - 1 ? H - 1 : rr);
+        const uint32_t* row = S.img + rr * WPR;
+        const uint4 v = *reinterpret_cast<const uint4*>(row + cw0);
+        m[k][0] = v.x;
+        m[k][1] = v.y;
+        m[k][2] = v.z;
+        m[k][3] = v.w;
+        // side words at the image edge clamp to the quad's own edge word:
+        // BORDER_REPLICATE repeats the edge pixel, already compared
+        lw[k] = cw0 > 0 ? row[cw0 - 1] : v.x;
+        rw[k] = cw0 + 4 < WPR ? row[cw0 + 4] : v.w;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const uint32_t mid = m[1][j];
+        const uint32_t b = mid & 255u;
+        const uint32_t rep = splat_byte(b);
+        const uint32_t l0 = j > 0 ? m[0][j - 1] : lw[0], l1 = j > 0 ? m[1][j - 1] : lw[1],
+                       l2 = j > 0 ? m[2][j - 1] : lw[2];
+        const uint32_t r0 = j < 3 ? m[0][j + 1] : rw[0], r1 = j < 3 ? m[1][j + 1] : rw[1],
+                       r2 = j < 3 ? m[2][j + 1] : rw[2];
+        const uint32_t diff = (mid ^ rep) | (m[0][j] ^ rep) | (m[2][j] ^ rep) |
+                              (((l0 >> 24) ^ b) | ((l1 >> 24) ^ b) | ((l2 >> 24) ^ b)) |
+                              (((r0 ^ b) | (r1 ^ b) | (r2 ^ b)) & 255u);
+        non[j] = diff != 0u;
+      }
+    }
+    int slot[4] = {0, 0, 0, 0};
+    wave_slots4(&C[kNList], non, slot);
+    if (act) {
+      uint16_t* gl = a.spill + (size_t)e * kSpillHalves + 4 * NW;
+      uint32_t wm[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int w = r * WPR + cw0 + j;
+        wm[j] = non[j] ? (uint32_t)slot[j] + 1u : 0u;
+        if (non[j]) {
+          if (slot[j] < a.list_cap)
+            S.u.w.list[slot[j]] = (uint16_t)w;
+          else
+            gl[slot[j]] = (uint16_t)w;
+        }
+      }
+      *reinterpret_cast<uint2*>(S.wmap + r * WPR + cw0) =
+          make_uint2(wm[0] | (wm[1] << 16), wm[2] | (wm[3] << 16));
+    }
+  }
+  __syncthreads();
+  RENT(8);
+
+  // phases 2-3, then the outputs
+  const int nlist = C[kNList];
+  if (nlist <= a.list_cap) {
+    if (mbase) canny<false>(a, S, e, nlist);
+    RENT(13);
+    write_outputs<false>(a, S, e, mbase);
+  } else {
+    if (mbase) canny<true>(a, S, e, nlist);
+    RENT(13);
+    write_outputs<true>(a, S, e, mbase);
+  }
+#ifdef DTSIM_STAMPS
+  RENSTAMP(12, (unsigned long long)C[kNList] | ((unsigned long long)C[kNWeak] << 32));
+  RENSTAMP(15, (unsigned long long)C[kNSeg]);
+  RENSTAMP(14, __builtin_amdgcn_s_memtime());
   RENSTAMP(1, __builtin_amdgcn_s_memrealtime());
 #endif
 }
 
-// One workgroup per env (a persistent variant, two workgroups per CU looping
-// over envs with the palette and tile kinds staged once, was measured slower:
-// the loop keeps loop-invariant values live across envs, and the kernel then
-// spills at the 80 VGPRs that two workgroups per CU allow).
-// waves_per_eu(6): two 768-thread workgroups per CU need <= 85 VGPRs
-__global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void render_kernel(
-    RenderArgs a) {
-  __shared__ __attribute__((aligned(16))) FusedLds S;
+// One workgroup per env, three per CU.
+// waves_per_eu(6): three 512-thread workgroups per CU need <= 85 VGPRs
+#ifndef DTSIM_RENDER_WPE
+#define DTSIM_RENDER_WPE 6
+#endif
+__global__ __launch_bounds__(kRenderThreads) __attribute__((amdgpu_waves_per_eu(DTSIM_RENDER_WPE))) void
+render_kernel(RenderArgs a) {
+  __shared__ __attribute__((aligned(16))) RenderLds S;
   const int tid = threadIdx.x;
   const LineDev& L = a.line;
   if (tid < PAL_N) {
@@ -1037,9 +1142,9 @@ __global__ __launch_bounds__(1024) __attribute__((amdgpu_waves_per_eu(6))) void 
     S.bits_lo = L.pal_bits[0];
     S.bits_hi = L.pal_bits[1];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) S.cnt[i] = 0;
+    for (int i = 0; i < kNCnt; ++i) S.cnt[i] = 0;
   }
-  for (int i = tid; i < a.width * a.height; i += blockDim.x) S.kind[i] = a.kind[i];
+  for (int i = tid; i < a.width * a.height; i += kRenderThreads) S.kind[i] = a.kind[i];
   // the camera frame, once per workgroup (wave 1; wave 0 has the palette)
   const int e = blockIdx.x;
   if (tid == 64) S.view = view_of(a.x[e], a.z[e], a.angle[e], a.cam_fwd);
@@ -1289,19 +1394,20 @@ int dt_render_init(dt_handle* h, const dt_map* map) {
   }
   dt_default_line_params(&h->line_params);
   h->line = to_line_dev(h->line_params);
-  const char* sk = getenv("DTSIM_RENDER_SKIP");  // diagnostics: phase ablation
-  h->render_skip = sk ? atoi(sk) : 0;
-  const char* th = getenv("DTSIM_RENDER_THREADS");  // tuning: workgroup size
-  h->render_threads = th ? atoi(th) : kRenderThreads;
-  if (h->render_threads < 128 || h->render_threads > 1024 || (h->render_threads & 63))
-    h->render_threads = kRenderThreads;
-
+  // overflow store of the render's listed words (RenderLds: slots past the
+  // LDS list; never touched on the shipped maps, sized for a whole frame)
+  if (hipMalloc(&h->render_spill, (size_t)h->n * kSpillHalves * sizeof(uint16_t)) != hipSuccess) {
+    h->err = "hipMalloc(render spill) failed";
+    return DT_E_HIP;
+  }
   return DT_OK;
 }
 
 void dt_render_free(dt_handle* h) {
   if (h->mark_buf) (void)hipFree(h->mark_buf);
   h->mark_buf = nullptr;
+  if (h->render_spill) (void)hipFree(h->render_spill);
+  h->render_spill = nullptr;
 }
 
 extern "C" {
@@ -1348,11 +1454,16 @@ int dt_render(dt_handle* h, const dt_render_io* io, void* stream) {
     h->err = "dt_render: gray_slot out of range";
     return DT_E_ARG;
   }
+  if (io->list_cap < 0) {
+    h->err = "dt_render: list_cap must be >= 0";
+    return DT_E_ARG;
+  }
   DevGuard dg(h->device);
   RenderArgs a{};
-  a.x = h->st.x;
-  a.z = h->st.z;
-  a.angle = h->st.angle;
+  const size_t n = (size_t)h->n;
+  a.x = io->pose ? io->pose : h->st.x;
+  a.z = io->pose ? io->pose + n : h->st.z;
+  a.angle = io->pose ? io->pose + 2 * n : h->st.angle;
   a.kind = h->map.kind;
   a.width = h->map.width;
   a.height = h->map.height;
@@ -1369,14 +1480,23 @@ int dt_render(dt_handle* h, const dt_render_io* io, void* stream) {
   a.rgb = io->rgb;
   a.line = h->line;
   a.n = h->n;
-  a.skip = h->render_skip;
-  hipLaunchKernelGGL(render_kernel, dim3(h->n), dim3(h->render_threads), 0, (hipStream_t)stream,
-                     a);
+  a.spill = (uint16_t*)h->render_spill;
+  a.list_cap = io->list_cap > 0 && io->list_cap < kListCap ? io->list_cap : kListCap;
+  hipLaunchKernelGGL(render_kernel, dim3(h->n), dim3(kRenderThreads), 0, (hipStream_t)stream, a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     h->err = std::string("dt_render launch: ") + hipGetErrorString(e);
     return DT_E_HIP;
   }
+  return DT_OK;
+}
+
+int dt_copy_pose(dt_handle* h, double* pose, void* stream) {
+  if (!h || !pose) return DT_E_ARG;
+  DevGuard dg(h->device);
+  // x, z and angle are consecutive n-double planes of the state buffer (dt_create)
+  HIP_OR_FAIL(h, hipMemcpyAsync(pose, h->st.x, 3 * (size_t)h->n * sizeof(double),
+                                hipMemcpyDeviceToDevice, (hipStream_t)stream));
   return DT_OK;
 }
 

@@ -1213,15 +1213,6 @@ __global__ __launch_bounds__(64) void lane_pos_kernel(dt::State st, dt::MapDev m
   if (tile_out) tile_out[e] = dt::tile_of(M, g, x, z);
 }
 
-#define HIP_OR_FAIL(h, expr)                                                   \
-  do {                                                                         \
-    hipError_t _e = (expr);                                                    \
-    if (_e != hipSuccess) {                                                    \
-      (h)->err = std::string(#expr) + ": " + hipGetErrorString(_e);             \
-      return DT_E_HIP;                                                         \
-    }                                                                          \
-  } while (0)
-
 int grid_of(int n) { return (n + dt::kWave - 1) / dt::kWave; }
 int refill_grid(int n, int ne) { return (n + ne - 1) / ne; }
 

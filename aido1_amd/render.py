@@ -64,7 +64,8 @@ class LineParams(ctypes.Structure):
 class RenderIO(ctypes.Structure):
     _fields_ = [('gray', ctypes.c_void_p), ('gray_slots', ctypes.c_int32),
                 ('gray_slot', ctypes.c_int32), ('fresh', ctypes.c_void_p),
-                ('masks', ctypes.c_void_p), ('rgb', ctypes.c_void_p)]
+                ('masks', ctypes.c_void_p), ('rgb', ctypes.c_void_p),
+                ('pose', ctypes.c_void_p), ('list_cap', ctypes.c_int32)]
 
 
 class RenderOutput:
@@ -103,22 +104,50 @@ class RenderOutput:
         return self.ring[:, self.order()]
 
 
-def render_into(env, out, fresh=None):
-    """Render every env's current pose into `out` (advancing the frame ring).
-    fresh: optional [n] u8 device tensor; nonzero -> the frame fills every slot
-    (Transformer.reset semantics): pass the done flags of an auto-resetting
-    step.  The first render after RenderOutput creation / restart() fills every
-    slot of every env."""
+def _render_io(env, out, fresh, pose, list_cap):
     if out.slot < 0:
         fresh = out._all
     slot = out.advance()
-    io = RenderIO(ctypes.c_void_p(out.ring.data_ptr()), out.slots, slot,
-                  ctypes.c_void_p(fresh.data_ptr()) if fresh is not None else None,
-                  ctypes.c_void_p(out.masks.data_ptr()) if out.masks is not None else None,
-                  ctypes.c_void_p(out.rgb.data_ptr()) if out.rgb is not None else None)
+    if pose is not None and (pose.dtype != torch.float64 or not pose.is_contiguous() or
+                             tuple(pose.shape) != (3, env.n) or pose.device != env.device):
+        raise ValueError('pose must be a contiguous float64 [3, %d] tensor on %s'
+                         % (env.n, env.device))
+    return RenderIO(ctypes.c_void_p(out.ring.data_ptr()), out.slots, slot,
+                    ctypes.c_void_p(fresh.data_ptr()) if fresh is not None else None,
+                    ctypes.c_void_p(out.masks.data_ptr()) if out.masks is not None else None,
+                    ctypes.c_void_p(out.rgb.data_ptr()) if out.rgb is not None else None,
+                    ctypes.c_void_p(pose.data_ptr()) if pose is not None else None,
+                    int(list_cap))
+
+
+def render_into(env, out, fresh=None, pose=None, list_cap=0):
+    """Render every env's current pose (or `pose`, a [3, n] f64 x/z/angle
+    snapshot from VecEnv.copy_pose) into `out`, advancing the frame ring.
+    fresh: optional [n] u8 device tensor; nonzero -> the frame fills every slot
+    (Transformer.reset semantics): pass the done flags of an auto-resetting
+    step.  The first render after RenderOutput creation / restart() fills every
+    slot of every env.  list_cap > 0 (tests only) forces the kernel's
+    global-memory overflow path."""
+    io = _render_io(env, out, fresh, pose, list_cap)
     rc = env._L.dt_render(env._h, ctypes.byref(io), env._stream())
     env._check(rc, 'dt_render')
     return out
+
+
+def bind_render(env, out, stream, fresh=None, pose=None):
+    """A zero-argument callable that launches render_into(out, fresh, pose) on
+    `stream` (a torch.cuda.Stream) with its ctypes arguments built once, for
+    timed loops.  The ring slot is taken (advanced) at bind time, so bind the
+    calls of consecutive decisions in their order.  Returns dt_render's status."""
+    io = _render_io(env, out, fresh, pose, 0)
+    fn, h, st = env._L.dt_render, env._h, ctypes.c_void_p(stream.cuda_stream)
+    ref = ctypes.byref(io)
+    keep = (out, fresh, pose, io, stream)
+
+    def launch():
+        keep  # noqa: B018 (the buffers stay alive with the callable)
+        return fn(h, ref, st)
+    return launch
 
 
 def line_detect(bgr, params=None, hsv=False, stream=None):

@@ -204,6 +204,41 @@ class VecEnv:
             return fn(*args)
         return launch
 
+    def bind_step(self, actions, out, stream):
+        """A zero-argument callable that launches step_into(actions, out) on
+        `stream` (a torch.cuda.Stream) with its ctypes arguments built and
+        checked once, for timed loops (one foreign call per launch).  Returns
+        dt_step's status."""
+        if actions.dtype != torch.float32 or not actions.is_contiguous() or \
+                actions.device != self.device or tuple(actions.shape) != (self.n, 2):
+            raise ValueError('actions must be a contiguous float32 [%d,2] tensor on %s'
+                             % (self.n, self.device))
+        fn = self._L.dt_step
+        args = (self._h, _ptr(actions), _ptr(out.reward), _ptr(out.reward_mod), _ptr(out.done),
+                _ptr(out.obs), _ptr(out.lanepos), _ptr(out.tile),
+                ctypes.c_void_p(stream.cuda_stream))
+        keep = (actions, out, stream)
+
+        def launch():
+            keep  # noqa: B018 (the tensors stay alive with the callable)
+            return fn(*args)
+        return launch
+
+    def bind_copy_pose(self, pose, stream):
+        """A zero-argument callable for copy_pose(pose) on `stream`."""
+        if pose.dtype != torch.float64 or not pose.is_contiguous() or \
+                tuple(pose.shape) != (3, self.n) or pose.device != self.device:
+            raise ValueError('pose must be a contiguous float64 [3, %d] tensor on %s'
+                             % (self.n, self.device))
+        fn = self._L.dt_copy_pose
+        args = (self._h, _ptr(pose), ctypes.c_void_p(stream.cuda_stream))
+        keep = (pose, stream)
+
+        def launch():
+            keep  # noqa: B018
+            return fn(*args)
+        return launch
+
     def capture(self, actions, out=None, render=None):
         """StepGraph of len(actions) consecutive decisions (see StepGraph)."""
         return StepGraph(self, actions, out or self.out, render)
@@ -226,11 +261,22 @@ class VecEnv:
         return lp, tile
 
     # ---- observation path (config 3) ----------------------------------------------------
-    def render_into(self, out, fresh=None):
-        """Top-down raster + grey + line masks of every env's current pose into a
-        RenderOutput (see aido1_amd/render.py)."""
+    def render_into(self, out, fresh=None, pose=None, list_cap=0):
+        """Top-down raster + grey + line masks of every env's current pose (or of a
+        copy_pose snapshot) into a RenderOutput (see aido1_amd/render.py)."""
         from aido1_amd.render import render_into
-        return render_into(self, out, fresh)
+        return render_into(self, out, fresh, pose, list_cap)
+
+    def copy_pose(self, pose):
+        """Enqueue a copy of every env's (x, z, angle) into pose, a contiguous
+        float64 [3, n] device tensor (dt_copy_pose): the render of this decision
+        reads the snapshot while the next step runs on another stream."""
+        if pose.dtype != torch.float64 or not pose.is_contiguous() or \
+                tuple(pose.shape) != (3, self.n) or pose.device != self.device:
+            raise ValueError('pose must be a contiguous float64 [3, %d] tensor on %s'
+                             % (self.n, self.device))
+        self._check(self._L.dt_copy_pose(self._h, _ptr(pose), self._stream()), 'dt_copy_pose')
+        return pose
 
     def set_line_params(self, params):
         self._check(self._L.dt_set_line_params(self._h, ctypes.byref(params)),

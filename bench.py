@@ -2,38 +2,41 @@
 """bench.py — BASELINE.json's metric: env-steps/s (whole node) at 4096 envs/GPU,
 with pose/reward max-abs-err vs the CPU oracle in the same line.
 
-Workload (BASELINE.json configs[1]): 4096 envs per GPU
-on loop_empty, lane-pose (dist, angle) observation, i.i.d. U[0,1)^2 wheel
-actions (the train.py contract after utils/env_wrappers.py:214-216), Philox
-spawn streams keyed by seed 1234, auto-reset on done or at the 2000-step wrapper
-cap.  One bench "step" = one decision = one EnvironmentWrapper.step for every
-env = up to repeat_actions (3) Simulator steps each; the unit counted is the
-Simulator step (env-step), read back exactly from the device counters (envs
-that finish mid-repeat run fewer).  Actions for every step are generated and
-resident in HBM before the timed region.
+Headline workload (default, --config render): BASELINE.json configs[2], the
+largest single-GPU configuration: 4096 envs per GPU on loop_empty, i.i.d.
+U[0,1)^2 wheel actions (the train.py contract after utils/env_wrappers.py:214-216)
+resident in HBM, Philox spawn streams keyed by seed 1234, auto-reset on done or
+at the 2000-step wrapper cap, and per decision the full observation path: the
+120x160 top-down raster + grey frame into the 3-slot Transformer ring (the
+ring refilled for respawned envs) + the features/line_detector1 masks.  One
+bench "step" = one decision = one EnvironmentWrapper.step for every env = up to
+repeat_actions (3) Simulator steps each, plus the render of the pose it ends
+in; the unit counted is the Simulator step (env-step), read back exactly from
+the device counters.
 
-  python bench.py [--gpus N --steps K --warmup W] [--config lane|render|actor|train]
-
-Timed region (config 2): the K decisions are split into equal launches of
-dt_step_many (at most --many decisions each); each launch is one prebound
-foreign call (VecEnv.bind_step_many: arguments built and checked before the
-timed region), so the wall clock is the kernels' time plus one launch and one
-synchronize, not Python's per-call cost (--graph: one captured HIP graph
-instead, which costs more per replay on ROCm: tools/launch_probe.py).  After it, outside the timed region:
+Timed region: per decision, dt_step on the step stream, a dt_copy_pose
+snapshot of the poses, and dt_render of that snapshot on a second stream, so
+the step of decision d + 1 runs beside the render of decision d (the render of
+d reads only d's snapshot and d's done flags; the snapshot buffer of d is
+reused by d + 2 only after render d finished).  After it, outside the timed
+region:
   * parity: the C oracle (oracle/dtsim_oracle.c, test infrastructure) re-runs
     every env of this rank from the saved start state through the same actions;
-    reward/reward_mod/obs/done of every decision and the end pose are compared
-    with the timed launches' outputs, and a second GPU pass (dt_step, one
-    decision per launch, tile + lane pose asked for) checks tile indices;
-  * render: K dt_render launches (configs[2]'s 120x160 raster + grey +
-    line_detector1 masks) over the same envs, timed per launch with HIP events
-    on the launch stream -> the HBM-bound kernel's roofline, plus a bit-exact
-    check of 64 envs' frames against oracle/render_oracle.c.
+    reward/reward_mod/obs/done of every decision and the end pose/counters are
+    compared with the timed launches' outputs, and a second GPU pass (dt_step,
+    tile index asked for) checks tile indices; 64 envs' whole frame stacks
+    (the last three decisions' frames, as the ring holds them) and masks are
+    compared bit for bit with oracle/render_oracle.c renders of the oracle's
+    poses;
+  * roofline: render_kernel's algorithmic bytes (grey + masks + pose, plus the
+    ring refill of respawned envs) / its mean duration from HIP events on the
+    render stream;
+  * config2: BASELINE configs[1] (lane-pose obs only, dt_step_many launches) as
+    a sub-record with its own parity and roofline.
 
-Other configs (not the headline line): render = configs[2] on its own (step +
-render per decision), actor = configs[3] (actor in the loop), train =
-configs[4] (full DDPG: rollout + GPU prioritized replay + update + RCCL
-gradient all-reduce).
+Other configs: --config lane (configs[1] as the headline), actor = configs[3]
+(actor in the loop), train = configs[4] (full DDPG: rollout + GPU prioritized
+replay + update + RCCL gradient all-reduce).
 
 N > 1: `python bench.py --gpus N` starts torch.distributed.run with N ranks as
 a child process BEFORE anything touches the GPU (the driver may also launch
@@ -81,11 +84,11 @@ MANY_BYTES_PER_RESET = 128
 def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
-    p.add_argument('--steps', type=int, default=320)
-    p.add_argument('--warmup', type=int, default=30)
+    p.add_argument('--steps', type=int, default=100)
+    p.add_argument('--warmup', type=int, default=10)
     p.add_argument('--envs', type=int, default=4096)
     p.add_argument('--map', default='loop_empty')
-    p.add_argument('--config', default='lane', choices=['lane', 'render', 'actor', 'train'])
+    p.add_argument('--config', default='render', choices=['render', 'lane', 'actor', 'train'])
     p.add_argument('--actor-mode', default='reference', choices=['reference', 'eval'],
                    help="actor/train: 'reference' = train-mode batch-of-one BatchNorm + live "
                         "dropout as the reference's explorers act; 'eval' = BN folded")
@@ -102,13 +105,18 @@ def parse(argv=None):
                    help='lane config: replay the timed launches as one captured HIP graph '
                         '(default: prebound eager dt_step_many calls)')
     p.add_argument('--no-parity', action='store_true', help='skip the oracle parity pass')
-    p.add_argument('--no-render', action='store_true', help='skip the render sub-record')
-    p.add_argument('--render-steps', type=int, default=0,
-                   help='render sub-record launches (0 = --steps)')
+    p.add_argument('--obs-mode', default='pipe', choices=['pipe', 'pipe-lo', 'serial'],
+                   help='render: step/render stream arrangement (ObsLoop)')
+    p.add_argument('--no-lane', action='store_true', help='render: skip the config-2 sub-record')
+    p.add_argument('--lane-steps', type=int, default=320,
+                   help='render: decisions timed by the config-2 sub-record')
+    p.add_argument('--lane-warmup', type=int, default=20)
     p.add_argument('--seed', type=int, default=1234)
-    p.add_argument('--cpu-steps', type=int, default=100000,
-                   help='CPU baseline: timed env-steps per process after 1000 warm-up steps '
-                        '(BASELINE.md §3); 0 = skip')
+    p.add_argument('--cpu-steps', type=int, default=30000,
+                   help='config-2 CPU baseline: timed env-steps per process after 1000 warm-up '
+                        'steps (BASELINE.md §3); 0 = skip every CPU baseline')
+    p.add_argument('--cpu-decisions', type=int, default=1000,
+                   help='config-3 CPU baseline: timed decisions (step + render) per process')
     p.add_argument('--cpu-procs', type=int, default=0,
                    help='CPU baseline processes (0 = the box CPU share: min(16, affinity))')
     p.add_argument('--dry-run', action='store_true',
@@ -137,14 +145,18 @@ def launch(args, argv):
     return subprocess.call(cmd, env=env)
 
 
-# ---- CPU baseline: the oracle's numpy restatement of step(), one env/process ----
-def _cpu_worker(args):
-    idx, warm, steps_wanted, map_name = args
+# ---- CPU baselines, one env per process ------------------------
+def _map_rows(map_name):
     import yaml
-    from oracle import dtsim_ref as R
     with open(os.path.join(REPO, 'aido1_amd', 'maps', map_name + '.yaml')) as f:
-        rows = yaml.safe_load(f)['tiles']
-    env = R.EnvironmentWrapperRef(R.SimulatorRef(rows, seed=1234, env_id=idx))
+        return yaml.safe_load(f)['tiles']
+
+
+def _cpu_worker(args):
+    """configs[1]: the numpy restatement of Simulator.step + EnvironmentWrapper.step."""
+    idx, warm, steps_wanted, map_name = args
+    from oracle import dtsim_ref as R
+    env = R.EnvironmentWrapperRef(R.SimulatorRef(_map_rows(map_name), seed=1234, env_id=idx))
     env.reset()
     rng = np.random.default_rng(1234 + idx)
 
@@ -164,10 +176,56 @@ def _cpu_worker(args):
     return steps, time.perf_counter() - t0
 
 
-def cpu_baseline(steps, procs, map_name):
-    """one env per process, 1,000 warm-up env-steps, then `steps`
-    timed env-steps per process; aggregate = sum of steps / slowest process."""
+def _cpu_obs_worker(args):
+    """configs[2]: per decision the numpy step restatement, then the C restatement
+    of the raster + grey + LineDetectorHSV filter (oracle/render_oracle.c) of
+    the pose it ends in, pushed into a 3-frame stack (Transformer; a respawn
+    refills the stack, utils/reward_shaping/env_utils.py:54-70)."""
+    idx, warm, decisions, map_name = args
+    from oracle import dtsim_ref as R
+    from oracle import oracle_c as OC
+    rows = _map_rows(map_name)
+    env = R.EnvironmentWrapperRef(R.SimulatorRef(rows, seed=1234, env_id=idx))
+    rend = OC.OracleRender(rows)
+    env.reset()
+    rng = np.random.default_rng(1234 + idx)
+    stack = np.zeros((3, 120, 160), np.float32)
+
+    def run(k):
+        steps = 0
+        for _ in range(k):
+            a = rng.random(2, dtype=np.float32)
+            before = env.sim.step_count
+            _, _, d = env.step(a)
+            steps += env.sim.step_count - before
+            if d:
+                env.reset()
+            p = env.sim.cur_pos
+            g, m, _ = rend.render((p[0],), (p[2],), (env.sim.cur_angle,))
+            if d:
+                stack[:] = g[0]
+            else:
+                stack[:2] = stack[1:]
+                stack[2] = g[0]
+        return steps
+    run(warm)
+    t0 = time.perf_counter()
+    steps = run(decisions)
+    return steps, time.perf_counter() - t0
+
+
+def _cpu_pool(worker, items, procs):
     import multiprocessing as mp
+    pool = mp.get_context('spawn').Pool(procs)
+    try:
+        res = pool.map(worker, items)
+    finally:
+        pool.close()   # workers exit on their own (no terminate(): no SIGTERM under a profiler)
+        pool.join()
+    return res
+
+
+def _cpu_info(procs):
     try:
         avail = len(os.sched_getaffinity(0))
     except AttributeError:
@@ -176,11 +234,6 @@ def cpu_baseline(steps, procs, map_name):
         # the GPU box's CPU share is 16 per GPU (harness rule; os.cpu_count() shows
         # the whole host there), so the pool is capped at 16 processes
         procs = max(1, min(16, avail))
-    ctx = mp.get_context('spawn')
-    with ctx.Pool(procs) as pool:
-        res = pool.map(_cpu_worker, [(i, 1000, steps, map_name) for i in range(procs)])
-    total = sum(r[0] for r in res)
-    wall = max(r[1] for r in res)
     model = ''
     try:
         with open('/proc/cpuinfo') as f:
@@ -190,15 +243,47 @@ def cpu_baseline(steps, procs, map_name):
                     break
     except OSError:
         pass
+    return procs, avail, model
+
+
+DEVIATION = ('BASELINE.md §3 asks for P = nproc processes; the pool is capped at the GPU box\'s '
+             'CPU share of 16 per GPU (harness rule), so cores = processes = %d of %s logical '
+             'cores on the host')
+
+
+def cpu_baseline(steps, procs, map_name):
+    """configs[1]: one env per process, 1,000 warm-up env-steps,
+    then `steps` timed env-steps per process; aggregate = sum / slowest process."""
+    procs, avail, model = _cpu_info(procs)
+    res = _cpu_pool(_cpu_worker, [(i, 1000, steps, map_name) for i in range(procs)], procs)
+    total = sum(r[0] for r in res)
+    wall = max(r[1] for r in res)
     return {'value': total / wall, 'unit': 'env-steps/s', 'cores': procs, 'kind': 'port',
             'procs': procs, 'host_cores': os.cpu_count(), 'affinity_cores': avail,
-            'per_process': total / wall / procs,
+            'per_process': total / wall / procs, 'deviation': DEVIATION % (procs, os.cpu_count()),
             'sample': '%d processes x (1000 warm-up + %d timed env-steps), one env each: '
                       'oracle/dtsim_ref.py numpy-float64 restatement of Simulator.step + '
                       'EnvironmentWrapper.step (no render), %s, U[0,1)^2 wheel actions, '
-                      'auto-reset; %d timed env-steps in %.1f s; host CPU: %s (%s logical '
-                      'cores, pool capped at the box share of 16)'
-                      % (procs, steps, map_name, total, wall, model, os.cpu_count())}
+                      'auto-reset; %d timed env-steps in %.1f s; host CPU: %s'
+                      % (procs, steps, map_name, total, wall, model)}
+
+
+def cpu_obs_baseline(decisions, procs, map_name):
+    """configs[2] (BASELINE.md §3 obs path): one env per process, 20 warm-up
+    decisions, then `decisions` timed decisions of step + render + line filter."""
+    procs, avail, model = _cpu_info(procs)
+    res = _cpu_pool(_cpu_obs_worker, [(i, 20, decisions, map_name) for i in range(procs)], procs)
+    total = sum(r[0] for r in res)
+    wall = max(r[1] for r in res)
+    return {'value': total / wall, 'unit': 'env-steps/s', 'cores': procs, 'kind': 'port',
+            'procs': procs, 'host_cores': os.cpu_count(), 'affinity_cores': avail,
+            'per_process': total / wall / procs, 'deviation': DEVIATION % (procs, os.cpu_count()),
+            'sample': '%d processes x (20 warm-up + %d timed decisions), one env each: per '
+                      'decision oracle/dtsim_ref.py (numpy float64 Simulator.step x repeat 3 + '
+                      'EnvironmentWrapper) then oracle/render_oracle.c (C, -O2, scalar: '
+                      '120x160 raster + grey + HSV/inRange/dilate/Canny masks) and the 3-frame '
+                      'stack, %s, U[0,1)^2 wheel actions, auto-reset; %d timed env-steps in '
+                      '%.1f s; host CPU: %s' % (procs, decisions, map_name, total, wall, model)}
 
 
 def load_pmc(kernel):
@@ -300,9 +385,13 @@ def main(argv=None):
         return bench_actor(args, ctx)
     if args.config == 'train':
         return bench_train(args, ctx)
-    if args.config == 'render':
-        return bench_render_config(args, ctx)
-    return bench_lane(args, ctx)
+    if args.config == 'lane':
+        line = lane_record(args, ctx, args.steps, args.warmup, cpu=True)
+        if ctx.rank == 0:
+            print(json.dumps(line), flush=True)
+        ctx.close()
+        return
+    return bench_obs(args, ctx)
 
 
 def bench_dry(args, ctx):
@@ -325,8 +414,198 @@ def bench_dry(args, ctx):
     ctx.close()
 
 
-# ---- config 2: the headline line -------------------------------------------------------
-def bench_lane(args, ctx):
+def _bounds(sizes):
+    a = 0
+    for s in sizes:
+        yield a, a + s
+        a += s
+
+
+def worst_over_ranks(ctx, parity, keys):
+    """Parity fields: mismatch counts summed, errors maxed over ranks."""
+    if parity is None or not ctx.pg:
+        return parity
+    rows = ctx.gather([parity[k] for k in keys])
+    for i, k in enumerate(keys):
+        vals = [r[i] for r in rows]
+        parity[k] = sum(vals) if k.endswith('mismatches') else max(vals)
+    parity['envs_checked'] *= ctx.world
+    parity['ok'] = all(r[0] > 0 for r in ctx.gather([1.0 if parity['ok'] else 0.0]))
+    return parity
+
+
+STEP_PARITY_KEYS = ['pose_max_abs_err', 'reward_max_abs_err', 'reward_mod_max_abs_err',
+                    'obs_max_abs_err', 'tile_mismatches', 'done_mismatches', 'counter_mismatches',
+                    'check_pass_max_abs_diff']
+
+
+# ---- config 3: the headline line --------------------------------------------------------
+class ObsLoop:
+    """Per decision: dt_step -> dt_copy_pose snapshot (step stream), dt_render of
+    the snapshot (render stream, fresh = the step's done flags).  Step d + 1
+    waits only for render d - 1 (the snapshot buffer it overwrites).
+    mode 'serial': step and render of each decision on one stream, no snapshot;
+    'pipe': the step stream has the higher priority; 'pipe-lo': the render's."""
+
+    def __init__(self, env, ro, torch, mode='pipe'):
+        self.env, self.ro, self.torch, self.mode = env, ro, torch, mode
+        lo, hi = torch.cuda.Stream.priority_range()
+        self.s_step = torch.cuda.Stream(env.device, priority=hi if mode == 'pipe' else lo)
+        self.s_rend = self.s_step if mode == 'serial' else \
+            torch.cuda.Stream(env.device, priority=hi if mode == 'pipe-lo' else lo)
+        self.pose = [torch.empty(3, env.n, dtype=torch.float64, device=env.device)
+                     for _ in range(2)]
+
+    def events(self, k):
+        E = self.torch.cuda.Event
+        return ([E() for _ in range(k)],
+                [(E(enable_timing=True), E(enable_timing=True)) for _ in range(k)],
+                [(E(enable_timing=True), E(enable_timing=True)) for _ in range(k)])
+
+    def bind(self, actions, outs):
+        """The per-decision foreign calls, built and checked before the timed
+        region (the ring slots are taken here, in decision order)."""
+        from aido1_amd.render import bind_render
+        env, serial = self.env, self.mode == 'serial'
+        calls = []
+        for d in range(len(outs)):
+            pose = None if serial else self.pose[d % 2]
+            calls.append((env.bind_step(actions[d], outs[d], self.s_step),
+                          None if serial else env.bind_copy_pose(pose, self.s_step),
+                          bind_render(env, self.ro, self.s_rend, fresh=outs[d].done, pose=pose)))
+        return calls
+
+    def run(self, calls, ev):
+        """Launch the bound decisions; returns the calls' status codes."""
+        torch, env = self.torch, self.env
+        ev_step, t_rend, t_step = ev
+        ss, sr = self.s_step, self.s_rend
+        ss.wait_stream(torch.cuda.current_stream(env.device))
+        serial = self.mode == 'serial'
+        rcs = 0
+        for d, (step, copy, rend) in enumerate(calls):
+            if d >= 2 and not serial:
+                ss.wait_event(t_rend[d - 2][1])
+            t_step[d][0].record(ss)
+            rcs |= step()
+            t_step[d][1].record(ss)
+            if not serial:
+                rcs |= copy()
+                ev_step[d].record(ss)
+                sr.wait_event(ev_step[d])
+            t_rend[d][0].record(sr)
+            rcs |= rend()
+            t_rend[d][1].record(sr)
+        torch.cuda.current_stream(env.device).wait_stream(sr)
+        return rcs
+
+
+def bench_obs(args, ctx):
+    torch = ctx.torch
+    from aido1_amd.config import EnvConfig
+    from aido1_amd.render import RENDER_BYTES_PER_ENV, RENDER_BYTES_PER_FRESH, RenderOutput
+    from aido1_amd.vec_env import StepOutput, VecEnv
+    dev, rank, n = ctx.dev, ctx.rank, args.envs
+    W, K = args.warmup, args.steps
+    env = VecEnv(n, seed=args.seed, device=dev.index, config=EnvConfig(map_name=args.map),
+                 env_id_base=rank * n)
+    g = torch.Generator(device=dev)
+    g.manual_seed(args.seed + 7919 * rank)
+    actions = torch.rand(W + K, n, 2, generator=g, device=dev, dtype=torch.float32)
+    ro = RenderOutput(n, dev)          # 3-slot grey ring (Transformer stack) + 4 masks
+    loop = ObsLoop(env, ro, torch, args.obs_mode)
+    env.reset()
+    wouts = [StepOutput(n, dev, lanepos=False, tile=False) for _ in range(2)]
+    if loop.run(loop.bind(actions[:W], [wouts[d % 2] for d in range(W)]), loop.events(W)):
+        raise RuntimeError('a warm-up decision failed')
+    ctx.sync()
+    start = env.get_state()
+    env.stats(reset=True)
+    out = StepOutput(K * n, dev, lanepos=False, tile=False)
+    outs = [_Slice(out, d, d + 1, n) for d in range(K)]
+    ev = loop.events(K)
+    calls = loop.bind(actions[W:], outs)
+    ctx.barrier()
+    ctx.sync()
+    t0 = time.perf_counter()
+    rcs = loop.run(calls, ev)
+    t_host = time.perf_counter() - t0
+    ctx.sync()
+    ctx.barrier()
+    elapsed = time.perf_counter() - t0
+    if rcs:
+        raise RuntimeError('a dt_step / dt_copy_pose / dt_render call failed in the timed region')
+    st = env.stats()
+    env.check()
+    tot, tmax, per = rank_report(ctx, [st['sim_steps'], st['decisions'], st['resets']], elapsed)
+    rend_ms = [a.elapsed_time(b) for a, b in ev[1]]
+    step_ms = [a.elapsed_time(b) for a, b in ev[2]]
+
+    parity = None
+    if not args.no_parity:
+        parity = step_parity(env, start, actions[W:], out, rank, args, frames=ro)
+    parity = worst_over_ranks(ctx, parity, STEP_PARITY_KEYS + ['gray_mismatches',
+                                                               'mask_mismatches'])
+    env.close()
+    lane = None if args.no_lane else lane_record(args, ctx, args.lane_steps, args.lane_warmup,
+                                                 cpu=True)
+    if rank == 0:
+        kms = float(np.mean(rend_ms))
+        fresh_per_launch = st['resets'] / K
+        bpl = RENDER_BYTES_PER_ENV * n + RENDER_BYTES_PER_FRESH * fresh_per_launch
+        achieved = bpl / (kms * 1e-3) / 1e9
+        pmc = load_pmc('render_kernel') or {}
+        line = {
+            'metric': METRIC, 'value': tot[0] / tmax, 'unit': 'env-steps/s',
+            'n_gpus': ctx.world, 'steps': K, 'warmup': W,
+            'ms_per_step': tmax / K * 1e3, 'higher_is_better': True,
+            'scaling': 'weak', 'vs_baseline': None,
+            'dtype': 'f64 step / f32 raster + grey / u8 masks',
+            'data': 'synthetic',
+            'config': {'workload': 'config3: %d envs/GPU, lane pose + 120x160 top-down render + '
+                                   'grey frame ring + line_detector1 HSV/edge masks' % n,
+                       'map': args.map, 'envs_per_gpu': n, 'global_envs': n * ctx.world,
+                       'repeat_actions': 3, 'auto_reset': True,
+                       'actions': 'U[0,1)^2 wheel velocities, resident in HBM',
+                       'launch': ('per decision: dt_step + dt_copy_pose (step stream), dt_render '
+                                  'of the snapshot (render stream); step d+1 beside render d (%s)'
+                                  % args.obs_mode) if args.obs_mode != 'serial' else
+                       'per decision: dt_step then dt_render on one stream',
+                       'parallelism': 'env shards (%d x %d), no collective' % (ctx.world, n)},
+            'counts': {'env_steps': tot[0], 'decisions': tot[1], 'resets': tot[2],
+                       'elapsed_s': tmax},
+            'per_rank': per,
+            'process_group': {'backend': 'nccl (RCCL)' if ctx.pg else None,
+                              'world': ctx.dist.get_world_size() if ctx.pg else 1},
+            'parity': parity,
+            'roofline': {'bound': 'hbm', 'kernel': 'render_kernel', 'achieved': achieved,
+                         'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
+                         'traffic': pmc.get('hbm_bytes_per_launch'),
+                         'traffic_round': pmc.get('round'),
+                         'avg_kernel_ms': kms, 'min_kernel_ms': float(np.min(rend_ms)),
+                         'max_kernel_ms': float(np.max(rend_ms)),
+                         'algorithmic_bytes_per_launch': bpl,
+                         'algorithmic_basis': 'per env: grey f32 76,800 + 4 u8 masks 76,800 '
+                                              'written + pose 24 read (SURVEY §8d config 3 '
+                                              'without the step\'s 81 B); plus 153,600 B of '
+                                              'ring refill per respawned env (%.1f per launch)'
+                                              % fresh_per_launch,
+                         'timing': 'HIP events on the render stream around each dt_render'},
+            'step_kernel_ms': float(np.mean(step_ms)),
+            'host_enqueue_ms_per_step': t_host / K * 1e3,
+            'config2': lane,
+        }
+        line['cpu_baseline'] = (cpu_obs_baseline(args.cpu_decisions, args.cpu_procs, args.map)
+                                if ctx.world == 1 and args.cpu_steps > 0 else None)
+        print(json.dumps(line), flush=True)
+    ctx.close()
+
+
+# ---- config 2 ------------------------------------------------------------------------------
+def lane_record(args, ctx, K, W, cpu):
+    """BASELINE configs[1]: lane-pose obs only; the K timed decisions split into
+    equal dt_step_many launches of at most --many decisions, each one prebound
+    foreign call (--graph: one captured HIP graph)."""
     torch = ctx.torch
     from aido1_amd.config import EnvConfig
     from aido1_amd.vec_env import StepOutput, VecEnv
@@ -335,7 +614,6 @@ def bench_lane(args, ctx):
                  env_id_base=rank * n)
     g = torch.Generator(device=dev)
     g.manual_seed(args.seed + 7919 * rank)
-    W, K = args.warmup, args.steps
     actions = torch.rand(W + K, n, 2, generator=g, device=dev, dtype=torch.float32)
     env.reset()
     ctx.sync()
@@ -382,109 +660,76 @@ def bench_lane(args, ctx):
     launches_ms = e0.elapsed_time(e1)
     tot, tmax, per = rank_report(ctx, [st['sim_steps'], st['decisions'], st['resets']], elapsed)
     sim_steps, decisions, resets = tot
-
-    parity = None if args.no_parity else lane_parity(env, start, actions[W:], out, rank, args)
-    render = None if args.no_render else render_record(env, args, ctx)
-    # parity: worst over ranks
-    if parity is not None and ctx.pg:
-        keys = ['pose_max_abs_err', 'reward_max_abs_err', 'reward_mod_max_abs_err',
-                'obs_max_abs_err', 'tile_mismatches', 'done_mismatches', 'counter_mismatches',
-                'check_pass_max_abs_diff']
-        rows = ctx.gather([parity[k] for k in keys])
-        for i, k in enumerate(keys):
-            vals = [r[i] for r in rows]
-            parity[k] = sum(vals) if k.endswith('mismatches') else max(vals)
-        parity['envs_checked'] *= ctx.world
-
-    if rank == 0:
-        nl = len(sizes)
-        kms = launches_ms / nl
-        steps_per_launch = st['sim_steps'] / nl      # this rank's launches
-        resets_per_launch = st['resets'] / nl
-        survey_bytes = SURVEY_BYTES_PER_ENV_STEP * steps_per_launch
-        fused_bytes = (MANY_BYTES_PER_ENV + MANY_BYTES_PER_ENV_DECISION * K / nl) * n + \
-            MANY_BYTES_PER_RESET * resets_per_launch
-        achieved = survey_bytes / (kms * 1e-3) / 1e9
-        kname = step_kernel_name()
-        pmc = load_pmc(kname) or {}
-        line = {
-            'metric': METRIC,
-            'value': sim_steps / tmax,
-            'unit': 'env-steps/s',
-            'n_gpus': ctx.world,
-            'steps': K,
-            'warmup': W,
-            'ms_per_step': tmax / K * 1e3,
-            'higher_is_better': True,
-            'scaling': 'weak',
-            'vs_baseline': None,
-            'dtype': 'f64',
-            'data': 'synthetic',
-            'config': {
-                'workload': 'config2: %d envs/GPU, lane-pose (dist, angle) obs' % n,
-                'map': args.map, 'envs_per_gpu': n, 'repeat_actions': 3,
-                'actions': 'U[0,1)^2 wheel velocities, resident in HBM',
-                'auto_reset': True, 'global_envs': n * ctx.world,
-                'launch': 'dt_step_many: %d launches of %s decisions%s' % (
-                    nl, '/'.join(str(s) for s in sorted(set(sizes), reverse=True)),
-                    ', one HIP graph' if graph is not None else ', prebound eager calls'),
-                'parallelism': 'env shards (%d x %d), no collective' % (ctx.world, n)},
-            'counts': {'env_steps': sim_steps, 'decisions': decisions, 'resets': resets,
-                       'elapsed_s': tmax},
-            'per_rank': per,
-            'process_group': {'backend': 'nccl (RCCL)' if ctx.pg else None,
-                              'world': ctx.dist.get_world_size() if ctx.pg else 1},
-            'parity': parity,
-            'roofline': {'bound': 'hbm', 'kernel': kname, 'achieved': achieved,
-                         'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
-                         'traffic': pmc.get('hbm_bytes_per_launch'),
-                         'traffic_per': 'launch of %d decisions' % pmc['decisions_per_launch']
-                         if 'decisions_per_launch' in pmc else None,
-                         'avg_kernel_ms': kms,
-                         'algorithmic_bytes_per_launch': survey_bytes,
-                         'algorithmic_basis': 'SURVEY §8d 81 B/env-step x %.0f env-steps '
-                                              'per launch' % steps_per_launch,
-                         'fused_bytes_per_launch': fused_bytes,
-                         'decisions_per_launch': K / nl,
-                         'note': 'not HBM-bound (BASELINE.md §4): the bound is one env\'s '
-                                 'float64 dependency chain; see step_bound'},
-            'step_ms_per_decision': launches_ms / K,
-            'step_bound': step_bound_record(kname, kms, K / nl, n, pmc),
-            'render': render,
-        }
-        if ctx.world == 1 and args.cpu_steps > 0:
-            line['cpu_baseline'] = cpu_baseline(args.cpu_steps, args.cpu_procs, args.map)
-        else:
-            line['cpu_baseline'] = None
-        print(json.dumps(line), flush=True)
+    parity = None if args.no_parity else step_parity(env, start, actions[W:], out, rank, args)
+    parity = worst_over_ranks(ctx, parity, STEP_PARITY_KEYS)
     env.close()
-    ctx.close()
+    if rank != 0:
+        return None
+    nl = len(sizes)
+    kms = launches_ms / nl
+    steps_per_launch = st['sim_steps'] / nl      # this rank's launches
+    resets_per_launch = st['resets'] / nl
+    survey_bytes = SURVEY_BYTES_PER_ENV_STEP * steps_per_launch
+    fused_bytes = (MANY_BYTES_PER_ENV + MANY_BYTES_PER_ENV_DECISION * K / nl) * n + \
+        MANY_BYTES_PER_RESET * resets_per_launch
+    achieved = survey_bytes / (kms * 1e-3) / 1e9
+    kname = 'step_fan_kernel'
+    pmc = load_pmc(kname) or {}
+    line = {
+        'metric': METRIC,
+        'value': sim_steps / tmax,
+        'unit': 'env-steps/s',
+        'n_gpus': ctx.world,
+        'steps': K,
+        'warmup': W,
+        'ms_per_step': tmax / K * 1e3,
+        'higher_is_better': True,
+        'scaling': 'weak',
+        'vs_baseline': None,
+        'dtype': 'f64',
+        'data': 'synthetic',
+        'config': {
+            'workload': 'config2: %d envs/GPU, lane-pose (dist, angle) obs' % n,
+            'map': args.map, 'envs_per_gpu': n, 'repeat_actions': 3,
+            'actions': 'U[0,1)^2 wheel velocities, resident in HBM',
+            'auto_reset': True, 'global_envs': n * ctx.world,
+            'launch': 'dt_step_many: %d launches of %s decisions%s' % (
+                nl, '/'.join(str(s) for s in sorted(set(sizes), reverse=True)),
+                ', one HIP graph' if graph is not None else ', prebound eager calls'),
+            'parallelism': 'env shards (%d x %d), no collective' % (ctx.world, n)},
+        'counts': {'env_steps': sim_steps, 'decisions': decisions, 'resets': resets,
+                   'elapsed_s': tmax},
+        'per_rank': per,
+        'process_group': {'backend': 'nccl (RCCL)' if ctx.pg else None,
+                          'world': ctx.dist.get_world_size() if ctx.pg else 1},
+        'parity': parity,
+        'roofline': {'bound': 'hbm', 'kernel': kname, 'achieved': achieved,
+                     'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
+                     'traffic': pmc.get('hbm_bytes_per_launch'),
+                     'traffic_per': 'launch of %d decisions' % pmc['decisions_per_launch']
+                     if 'decisions_per_launch' in pmc else None,
+                     'avg_kernel_ms': kms,
+                     'algorithmic_bytes_per_launch': survey_bytes,
+                     'algorithmic_basis': 'SURVEY §8d 81 B/env-step x %.0f env-steps '
+                                          'per launch' % steps_per_launch,
+                     'fused_bytes_per_launch': fused_bytes,
+                     'decisions_per_launch': K / nl,
+                     'note': 'not HBM-bound (BASELINE.md §4): the bound is one env\'s '
+                             'float64 dependency chain; see step_bound'},
+        'step_ms_per_decision': launches_ms / K,
+        'step_bound': step_bound_record(kms, K / nl, n, pmc),
+    }
+    line['cpu_baseline'] = (cpu_baseline(args.cpu_steps, args.cpu_procs, args.map)
+                            if cpu and ctx.world == 1 and args.cpu_steps > 0 else None)
+    return line
 
 
-def _bounds(sizes):
-    a = 0
-    for s in sizes:
-        yield a, a + s
-        a += s
-
-
-def step_kernel_name():
-    """The kernel dt_step_many launches (DTSIM_STEP_KERNEL, see dtsim.hip)."""
-    k = os.environ.get('DTSIM_STEP_KERNEL', '')
-    if k == 'one' or os.environ.get('DTSIM_STEP_PAIR', '1').startswith('0'):
-        return 'step_kernel'
-    return 'step_pair_kernel' if k == 'pair' else 'step_fan_kernel'
-
-
-STEP_WAVES_PER_64_ENVS = {'step_kernel': 1, 'step_pair_kernel': 2, 'step_fan_kernel': 16}
-
-
-def step_bound_record(kname, kms, dec_per_launch, n, pmc):
+def step_bound_record(kms, dec_per_launch, n, pmc):
     """The config-2 kernel's real bound: per-decision time of one env's float64
     chain, and the fp64 issue rate it reaches vs the chip's (PMC counts from
     profiles/pmc_traffic.json when present)."""
     rec = {'us_per_decision': kms * 1e3 / dec_per_launch,
-           'waves': STEP_WAVES_PER_64_ENVS[kname] * n // 64,
+           'waves': 16 * n // 64,   # step_fan_kernel: each env on a quad of 4 waves
            'simds_on_chip': 1024}
     f = pmc.get('fp64_flops_per_launch')
     if f:
@@ -494,27 +739,29 @@ def step_bound_record(kname, kms, dec_per_launch, n, pmc):
     return rec
 
 
-def lane_parity(env, start, actions, out, rank, args):
+def step_parity(env, start, actions, out, rank, args, frames=None, m=64):
     """Every env of this rank re-run by the C oracle (test infrastructure, used
     here as the checker only) from `start` through the timed decisions'
     actions, compared with the timed launches' outputs; then a dt_step check
-    pass from the same start state with tile indices asked for."""
+    pass from the same start state with tile indices asked for.  With `frames`
+    (the RenderOutput of the timed decisions), m envs' frame stacks (oldest
+    first, as the Transformer concatenates them) and masks are compared with
+    oracle/render_oracle.c renders of the oracle's poses."""
     import torch
-    import yaml
     from aido1_amd.vec_env import StepOutput
     from oracle import oracle_c as OC
     n, K = env.n, out.reward.numel() // env.n
-    with open(os.path.join(REPO, 'aido1_amd', 'maps', args.map + '.yaml')) as f:
-        rows = yaml.safe_load(f)['tiles']
+    rows = _map_rows(args.map)
     t0 = time.perf_counter()
     end = env.get_state()
     acts = actions[:K].cpu().numpy()
     g = {k: getattr(out, k).view(K, n, -1).squeeze(-1).cpu().numpy()
          for k in ('reward', 'reward_mod', 'done')}
     g['obs'] = out.obs.view(K, n, 2).cpu().numpy()
+    idx = np.linspace(0, n - 1, m).astype(np.int64)
     ob = OC.OracleBatch(rows, n, seed=args.seed, env_base=rank * n)
     ob.set_state(**start)
-    refs = []
+    refs, track = [], []
     err = {'reward': 0.0, 'reward_mod': 0.0, 'obs': 0.0}
     done_mm = 0
     for d in range(K):
@@ -523,10 +770,35 @@ def lane_parity(env, start, actions, out, rank, args):
         for k in err:
             err[k] = max(err[k], float(np.max(np.abs(g[k][d] - r[k]))))
         done_mm += int(np.count_nonzero(g['done'][d] != r['done']))
+        if frames is not None and d >= K - frames.slots:
+            o = ob.state()
+            track.append((o['x'][idx].copy(), o['z'][idx].copy(), o['angle'][idx].copy(),
+                          r['done'][idx].copy()))
     o = ob.state()
     pose_err = max(float(np.max(np.abs(end[k] - o[k]))) for k in ('x', 'z', 'angle'))
     cnt_mm = sum(int(np.count_nonzero(end[k] != o[k]))
                  for k in ('step_count', 'env_step', 'episode'))
+    rec = {'envs_checked': n, 'decisions': K, 'oracle': 'oracle/dtsim_oracle.c (C restatement)'}
+    if frames is not None:
+        # the ring as the Transformer holds it after the last decisions: a
+        # respawn refills every slot with its frame, otherwise append + drop
+        R = OC.OracleRender(rows)
+        stack = None
+        masks = None
+        for x, z, a, dn in track:
+            gr, masks, _ = R.render(x, z, a)
+            if stack is None:
+                stack = np.repeat(gr[:, None], frames.slots, 1)
+            else:
+                stack = np.where(dn[:, None, None, None] != 0, gr[:, None],
+                                 np.concatenate([stack[:, 1:], gr[:, None]], 1))
+        got = frames.stack_view()[idx.tolist()].cpu().numpy()
+        keep = frames.slots - len(track) if len(track) < frames.slots else 0
+        rec.update({'frame_envs_checked': m, 'frame_oracle': 'oracle/render_oracle.c',
+                    'frames_per_env': frames.slots - keep,
+                    'gray_mismatches': int(np.count_nonzero(got[:, keep:] != stack[:, keep:])),
+                    'mask_mismatches': int(np.count_nonzero(
+                        frames.masks[idx.tolist()].cpu().numpy() != masks))})
     # check pass: dt_step from the same start, tile + lane pose produced
     env.set_state(**start)
     full = StepOutput(n, env.device)
@@ -541,142 +813,18 @@ def lane_parity(env, start, actions, out, rank, args):
     end2 = env.get_state()
     chk = max(chk, max(float(np.max(np.abs(end2[k] - end[k]))) for k in ('x', 'z', 'angle')))
     env.check()
-    return {'envs_checked': n, 'decisions': K, 'oracle': 'oracle/dtsim_oracle.c (C restatement)',
-            'pose_max_abs_err': pose_err, 'reward_max_abs_err': err['reward'],
-            'reward_mod_max_abs_err': err['reward_mod'], 'obs_max_abs_err': err['obs'],
-            'done_mismatches': done_mm, 'tile_mismatches': tile_mm,
-            'counter_mismatches': cnt_mm, 'check_pass_max_abs_diff': chk,
-            'tolerance': {'pose': 1e-5, 'reward': 1e-5, 'tile_done': 'exact'},
-            'ok': bool(pose_err <= 1e-5 and err['reward'] <= 1e-5 and err['reward_mod'] <= 1e-5
-                       and done_mm == 0 and tile_mm == 0 and cnt_mm == 0),
-            'seconds': time.perf_counter() - t0}
-
-
-def render_record(env, args, ctx):
-    """configs[2]'s HBM-bound kernel on the same envs: K dt_render launches, each
-    timed with HIP events on the launch stream; 64 envs' frames checked bit for
-    bit against oracle/render_oracle.c."""
-    torch = ctx.torch
-    from aido1_amd.render import RENDER_BYTES_PER_ENV, RenderOutput
-    n = env.n
-    K = args.render_steps or args.steps
-    ro = RenderOutput(n, env.device)
-    env.render_into(ro)               # first render fills the ring (not timed)
-    for _ in range(3):
-        env.render_into(ro)
-    ctx.sync()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(K)]
-    for a, b in ev:
-        a.record()
-        env.render_into(ro)
-        b.record()
-    ctx.sync()
-    ms = [a.elapsed_time(b) for a, b in ev]
-    kms = float(np.mean(ms))
-    bytes_per_launch = RENDER_BYTES_PER_ENV * n
-    achieved = bytes_per_launch / (kms * 1e-3) / 1e9
-    rec = {'kernel': 'render_kernel', 'launches': K, 'envs': n, 'bound': 'hbm',
-           'avg_kernel_ms': kms, 'min_kernel_ms': float(np.min(ms)),
-           'algorithmic_bytes_per_launch': bytes_per_launch,
-           'algorithmic_basis': 'per env: grey f32 76,800 + 4 u8 masks 76,800 written + pose '
-                                '24 read (SURVEY §8d config 3 minus the step\'s 81 B)',
-           'achieved': achieved, 'peak': HBM_PEAK_GBS, 'unit': 'GB/s',
-           'frac': achieved / HBM_PEAK_GBS,
-           'env_steps_per_s_equiv': n / (kms * 1e-3)}
-    pmc = load_pmc('render_kernel') or {}
-    rec['traffic'] = pmc.get('hbm_bytes_per_launch')
-    if not args.no_parity:
-        rec['parity'] = render_parity(env, ro, args)
+    frames_ok = frames is None or (rec['gray_mismatches'] == 0 and rec['mask_mismatches'] == 0)
+    rec.update({'pose_max_abs_err': pose_err, 'reward_max_abs_err': err['reward'],
+                'reward_mod_max_abs_err': err['reward_mod'], 'obs_max_abs_err': err['obs'],
+                'done_mismatches': done_mm, 'tile_mismatches': tile_mm,
+                'counter_mismatches': cnt_mm, 'check_pass_max_abs_diff': chk,
+                'tolerance': {'pose': 1e-5, 'reward': 1e-5, 'tile_done': 'exact',
+                              'frames_masks': 'exact'},
+                'ok': bool(pose_err <= 1e-5 and err['reward'] <= 1e-5 and
+                           err['reward_mod'] <= 1e-5 and done_mm == 0 and tile_mm == 0 and
+                           cnt_mm == 0 and frames_ok),
+                'seconds': time.perf_counter() - t0})
     return rec
-
-
-def render_parity(env, ro, args, m=64):
-    import yaml
-    from aido1_amd.render import RenderOutput
-    from oracle import oracle_c as OC
-    with open(os.path.join(REPO, 'aido1_amd', 'maps', args.map + '.yaml')) as f:
-        rows = yaml.safe_load(f)['tiles']
-    s = env.get_state()
-    idx = np.linspace(0, env.n - 1, m).astype(np.int64)
-    gray, masks, _ = OC.OracleRender(rows).render(s['x'][idx], s['z'][idx], s['angle'][idx])
-    g = ro.ring[idx.tolist(), ro.slot].cpu().numpy()
-    mk = ro.masks[idx.tolist()].cpu().numpy()
-    return {'envs_checked': m, 'oracle': 'oracle/render_oracle.c',
-            'gray_mismatches': int(np.count_nonzero(g != gray)),
-            'mask_mismatches': int(np.count_nonzero(mk != masks))}
-
-
-# ---- config 3 on its own -----------------------------------------------------------------
-def bench_render_config(args, ctx):
-    """configs[2]: per decision one dt_step + one dt_render (the frame ring
-    refilled for respawned envs), eager launches timed per kernel."""
-    torch = ctx.torch
-    from aido1_amd.config import EnvConfig
-    from aido1_amd.render import RENDER_BYTES_PER_ENV, RENDER_BYTES_PER_FRESH, RenderOutput
-    from aido1_amd.vec_env import StepOutput, VecEnv
-    dev, rank, n = ctx.dev, ctx.rank, args.envs
-    env = VecEnv(n, seed=args.seed, device=dev.index, config=EnvConfig(map_name=args.map),
-                 env_id_base=rank * n)
-    out = StepOutput(n, dev, lanepos=False, tile=False)
-    g = torch.Generator(device=dev)
-    g.manual_seed(args.seed + 7919 * rank)
-    actions = torch.rand(args.warmup + args.steps, n, 2, generator=g, device=dev,
-                         dtype=torch.float32)
-    ro = RenderOutput(n, dev)
-    env.reset()
-    for i in range(args.warmup):
-        env.step_into(actions[i], out)
-        env.render_into(ro, fresh=out.done)
-    ctx.sync()
-    env.stats(reset=True)
-    sev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
-    rev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-           for _ in range(args.steps)]
-    ctx.barrier()
-    ctx.sync()
-    t0 = time.perf_counter()
-    for k in range(args.steps):
-        sev[k][0].record()
-        env.step_into(actions[args.warmup + k], out)
-        sev[k][1].record()
-        rev[k][0].record()
-        env.render_into(ro, fresh=out.done)
-        rev[k][1].record()
-    ctx.sync()
-    ctx.barrier()
-    elapsed = time.perf_counter() - t0
-    st = env.stats()
-    env.check()
-    tot, tmax, per = rank_report(ctx, [st['sim_steps'], st['decisions'], st['resets']], elapsed)
-    if rank == 0:
-        kms = float(np.mean([a.elapsed_time(b) for a, b in rev]))
-        step_ms = float(np.mean([a.elapsed_time(b) for a, b in sev]))
-        bpl = RENDER_BYTES_PER_ENV * n + RENDER_BYTES_PER_FRESH * st['resets'] / args.steps
-        achieved = bpl / (kms * 1e-3) / 1e9
-        pmc = load_pmc('render_kernel') or {}
-        print(json.dumps({
-            'metric': METRIC, 'value': tot[0] / tmax, 'unit': 'env-steps/s',
-            'n_gpus': ctx.world, 'steps': args.steps, 'warmup': args.warmup,
-            'ms_per_step': tmax / args.steps * 1e3, 'higher_is_better': True,
-            'scaling': 'weak', 'vs_baseline': None, 'dtype': 'f64 pose / f32 grey / u8 masks',
-            'data': 'synthetic',
-            'config': {'workload': 'config3: %d envs/GPU, lane-pose + 120x160 top-down render '
-                                   '+ line_detector1 HSV/edge obs' % n,
-                       'map': args.map, 'envs_per_gpu': n, 'global_envs': n * ctx.world,
-                       'launch': 'per decision: dt_step + dt_render, eager',
-                       'parallelism': 'env shards (%d x %d), no collective' % (ctx.world, n)},
-            'counts': {'env_steps': tot[0], 'decisions': tot[1], 'resets': tot[2],
-                       'elapsed_s': tmax},
-            'per_rank': per,
-            'roofline': {'bound': 'hbm', 'kernel': 'render_kernel', 'achieved': achieved,
-                         'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
-                         'traffic': pmc.get('hbm_bytes_per_launch'), 'avg_kernel_ms': kms,
-                         'algorithmic_bytes_per_launch': bpl},
-            'step_kernel_ms': step_ms, 'cpu_baseline': None}), flush=True)
-    env.close()
-    ctx.close()
 
 
 # ---- configs 4 and 5 -----------------------------------------------------------------------

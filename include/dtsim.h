@@ -29,8 +29,9 @@
 extern "C" {
 #endif
 
-#define DT_ABI_VERSION 3  /* 2: curves per tile vary (curve_start), intersections;
-                             3: static objects in dt_map, safety_rad_mult */
+#define DT_ABI_VERSION 4  /* 2: curves per tile vary (curve_start), intersections;
+                             3: static objects in dt_map, safety_rad_mult;
+                             4: dt_render_io.pose / list_cap, dt_copy_pose */
 
 /* error codes */
 #define DT_OK 0
@@ -187,7 +188,8 @@ int dt_step_masked(dt_handle* h, const uint8_t* mask, const float* actions, doub
                    double* reward_mod, uint8_t* done, float* obs, double* lanepos, int32_t* tile,
                    void* stream);
 
-/* k consecutive dt_step calls in one launch (plus a spawn-ahead refill launch):
+/* k consecutive dt_step calls in one launch (the spawn-ahead refill blocks run in
+ * the same grid):
  * the same results as k dt_step calls over actions[d], with the outputs of
  * decision d at [d * n + env].  The explorer's rollout loop
  * (training/explorers.py) over k actions known ahead, e.g. random ones.
@@ -236,6 +238,12 @@ typedef struct dt_render_io {
                            utils/reward_shaping/env_utils.py:60-63) */
   uint8_t* masks;       /* device [n, 4, 120, 160] u8 255/0 {white, yellow, red, edges}, or NULL */
   uint8_t* rgb;         /* device [n, 120, 160, 3] u8 RGB raster, or NULL */
+  const double* pose;   /* device [3, n] f64 planes (x, z, angle) to render, or NULL = the
+                           handle's current state (a dt_copy_pose snapshot lets the next
+                           dt_step run on another stream while this render reads it) */
+  int32_t list_cap;     /* 0 in production.  > 0 lowers the number of non-uniform words
+                           the kernel keeps in LDS, so tests exercise the global-memory
+                           overflow path (results are identical either way) */
 } dt_render_io;
 
 /* Replaces, per env and fused in one launch (one workgroup per env, the frame
@@ -245,8 +253,13 @@ typedef struct dt_render_io {
  * (utils/reward_shaping/env_utils.py:48-51) and LineDetectorHSV.setImage +
  * _colorFilter (features/line_detector1.py:134-141, :36-57): HSV inRange,
  * ellipse dilation, Canny(bgr, lo, hi, 3).  Renders the CURRENT pose (call it
- * after dt_step). */
+ * after dt_step), or io->pose. */
 int dt_render(dt_handle* h, const dt_render_io* io, void* stream);
+
+/* Enqueue a copy of every env's current pose into pose (device [3, n] f64:
+ * x, z, angle planes) on `stream`: the render of decision d can then read the
+ * snapshot while dt_step of decision d + 1 runs on another stream. */
+int dt_copy_pose(dt_handle* h, double* pose, void* stream);
 int dt_set_line_params(dt_handle* h, const dt_line_params* p);
 
 /* LineDetectorHSV on caller images (no environment): bgr device [n, height,

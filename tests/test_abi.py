@@ -68,3 +68,21 @@ def test_no_gpu_fails_loudly():
     from aido1_amd.vec_env import VecEnv
     with pytest.raises(_lib.DtError):
         VecEnv(8)
+
+
+def test_render_io_layout_matches_header(tmp_path):
+    from aido1_amd.render import LineParams, RenderIO
+    src = tmp_path / 'rio.c'
+    fields = [f[0] for f in RenderIO._fields_]
+    body = '\n'.join('printf("%%zu ", offsetof(dt_render_io, %s));' % f for f in fields)
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "dtsim.h"\nint main(){'
+                   + body + 'printf("%zu %zu\\n", sizeof(dt_render_io), sizeof(dt_line_params));'
+                   ' return 0;}')
+    exe = tmp_path / 'rio'
+    subprocess.run(['gcc', '-I', os.path.join(REPO, 'include'), '-o', str(exe), str(src)],
+                   check=True)
+    vals = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True,
+                                           check=True).stdout.split()]
+    assert vals[:len(fields)] == [getattr(RenderIO, f).offset for f in fields]
+    assert vals[len(fields)] == ctypes.sizeof(RenderIO)
+    assert vals[len(fields) + 1] == ctypes.sizeof(LineParams)

@@ -99,3 +99,67 @@ def test_line_detect_parity(gpu, shape):
         rm, rh = OC.OracleRender(map_rows('loop_empty'), params=p).line_detect(img, hsv=True)
         assert np.array_equal(hsv.cpu().numpy(), rh)
         assert np.array_equal(masks.cpu().numpy(), rm)
+
+
+def _render_setup(gpu, map_name, n=256, seed=11):
+    from aido1_amd.config import EnvConfig
+    from aido1_amd.vec_env import VecEnv
+    env = VecEnv(n, seed=seed, config=EnvConfig(map_name=map_name))
+    env.reset()
+    rng = np.random.default_rng(seed)
+    x, z, a = poses(n, rng)
+    s = env.get_state()
+    x[n // 2:], z[n // 2:], a[n // 2:] = s['x'][n // 2:], s['z'][n // 2:], s['angle'][n // 2:]
+    env.set_state(x=x, z=z, angle=a)
+    return env, x, z, a
+
+
+@pytest.mark.parametrize('list_cap', [1, 64, 700])
+def test_render_spill_path_matches_oracle(gpu, list_cap):
+    """Frames with more non-uniform words than the LDS list holds keep the rest
+    in the global spill area: forcing a small cap must not change a bit."""
+    from aido1_amd.render import RenderOutput
+    env, x, z, a = _render_setup(gpu, 'loop_empty')
+    out = RenderOutput(env.n, gpu, slots=1)
+    env.render_into(out, list_cap=list_cap)
+    torch.cuda.synchronize()
+    g, m, _ = OC.OracleRender(map_rows('loop_empty')).render(x, z, a)
+    assert np.array_equal(out.masks.cpu().numpy(), m)
+    assert np.array_equal(out.ring[:, 0].cpu().numpy(), g)
+
+
+@pytest.mark.parametrize('dil,lo,hi', [(1, 80.0, 200.0), (5, 40.0, 120.0), (7, 80.0, 200.0),
+                                       (3, 200.0, 80.0)])
+def test_render_line_params_match_oracle(gpu, dil, lo, hi):
+    """Other dilation sizes (radius >= 2: every quad takes the dilation path)
+    and Canny thresholds (swapped ones are reordered, as cv2.Canny does)."""
+    from aido1_amd.render import LineParams, RenderOutput
+    env, x, z, a = _render_setup(gpu, 'zigzag', seed=13)
+    lp = LineParams.default()
+    lp.dilation_kernel_size, lp.canny_lo, lp.canny_hi = dil, lo, hi
+    env.set_line_params(lp)
+    p = OC.line_params_default()
+    p.dilation_kernel_size, p.canny_lo, p.canny_hi = dil, lo, hi
+    out = RenderOutput(env.n, gpu, slots=1)
+    env.render_into(out)
+    torch.cuda.synchronize()
+    g, m, _ = OC.OracleRender(map_rows('zigzag'), params=p).render(x, z, a)
+    assert np.array_equal(out.masks.cpu().numpy(), m)
+    assert np.array_equal(out.ring[:, 0].cpu().numpy(), g)
+
+
+def test_render_pose_snapshot(gpu):
+    """dt_copy_pose + dt_render_io.pose: the render reads the snapshot, not the
+    state a later step has moved on."""
+    from aido1_amd.render import RenderOutput
+    env, x, z, a = _render_setup(gpu, 'loop_empty', n=128, seed=17)
+    snap = torch.empty(3, env.n, dtype=torch.float64, device=gpu)
+    env.copy_pose(snap)
+    env.step_into(torch.full((env.n, 2), 0.7, device=gpu))   # moves every env
+    out = RenderOutput(env.n, gpu, slots=1)
+    env.render_into(out, pose=snap)
+    torch.cuda.synchronize()
+    assert np.array_equal(snap.cpu().numpy(), np.stack([x, z, a]))
+    g, m, _ = OC.OracleRender(map_rows('loop_empty')).render(x, z, a)
+    assert np.array_equal(out.masks.cpu().numpy(), m)
+    assert np.array_equal(out.ring[:, 0].cpu().numpy(), g)

@@ -1,10 +1,13 @@
 """Diagnostic: where a render_kernel workgroup spends its time (shader-clock
 stamps of the -DDTSIM_STAMPS build, tools/step_stamps.sh; run with
 DTSIM_DIAG_LIB=aido1_amd/libdtsim_stamps.so).  Thread 0 of every workgroup
-stamps after each phase's barrier: 4 entry, 5 prologue (palette, tiles, view),
-6 background, 7 markings, 8 uniformity + grey stores, 9 Sobel, 10 NMS,
-11 hysteresis, 13 masks; [0]/[1] real time at entry/exit, [2] HW_ID,
-[3] XCC_ID, [12] nlist | nweak << 32."""
+stamps after each phase's barrier: 4 entry, 5 background spans + segment
+projection, 6 span fix-up + markings, 8 uniformity + grey + uniform masks,
+9 Sobel, 10 NMS, 11/13 hysteresis, 14 outputs (grey + masks); [0]/[1] real time at
+entry/exit, [2] HW_ID, [3] XCC_ID, [12] nlist | nweak << 32, [15] visible
+segments (yellow | white << 16).
+With TIME_ONLY=1 (production library): mean dt_render time of 4096 envs
+alone, back to back, from HIP events."""
 import ctypes
 import os
 import sys
@@ -19,8 +22,34 @@ from aido1_amd.render import RenderOutput  # noqa: E402
 from aido1_amd.vec_env import StepOutput, VecEnv  # noqa: E402
 
 
+def time_only(n):
+    dev = torch.device('cuda', 0)
+    env = VecEnv(n, seed=1234, device=0, config=EnvConfig(map_name=os.environ.get('MAP', 'loop_empty')))
+    out = StepOutput(n, dev, lanepos=False, tile=False)
+    ro = RenderOutput(n, dev)
+    env.reset()
+    acts = torch.rand(30, n, 2, device=dev)
+    for it in range(10):
+        env.step_into(acts[it], out)
+        env.render_into(ro, fresh=out.done)
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(20)]
+    for a, b in ev:
+        a.record()
+        env.render_into(ro)
+        b.record()
+    torch.cuda.synchronize()
+    ms = [a.elapsed_time(b) for a, b in ev]
+    print('render alone, %d envs: mean %.4f ms, min %.4f ms -> %.1f %% of 8 TB/s'
+          % (n, np.mean(ms), np.min(ms), 100 * 153624 * n / (np.mean(ms) * 1e-3) / 8e12))
+    env.close()
+
+
 def main():
     n = int(os.environ.get('ENVS', '4096'))
+    if os.environ.get('TIME_ONLY'):
+        return time_only(n)
     dev = torch.device('cuda', 0)
     env = VecEnv(n, seed=1234, device=0, config=EnvConfig(map_name=os.environ.get('MAP', 'loop_empty')))
     out = StepOutput(n, dev, lanepos=False, tile=False)
@@ -41,11 +70,11 @@ def main():
         recs.append(buf[:min(n, 4096)].astype(np.int64).copy())
     b = np.stack(recs)                     # [launch, wg, 16]
     real = (b[..., 1] - b[..., 0]) / 100.0  # us (100 MHz real-time clock)
-    cyc = b[..., 13] - b[..., 4]
+    cyc = b[..., 14] - b[..., 4]
     clk = np.median(cyc / (real * 1e3))
-    names = ['prologue', 'background', 'markings', 'uniform+grey', 'sobel', 'nms', 'hysteresis',
-             'masks']
-    pts = [4, 5, 6, 7, 8, 9, 10, 11, 13]
+    names = ['spans+proj', 'fixup+marks', 'uniformity', 'sobel', 'nms', 'hysteresis',
+             'output']
+    pts = [4, 5, 6, 8, 9, 10, 13, 14]
     seg = np.stack([b[..., pts[i + 1]] - b[..., pts[i]] for i in range(len(names))], -1)
     print('launches %d, workgroups %d; workgroup life median %.2f us (p10 %.2f, p90 %.2f); '
           'shader clock %.2f GHz' % (b.shape[0], b.shape[1], np.median(real),
@@ -55,15 +84,9 @@ def main():
         print('  %-13s median %7.0f cyc  mean %7.0f  p90 %7.0f  (%4.1f %% of the median life)'
               % (nm, np.median(seg[..., i]), seg[..., i].mean(), np.percentile(seg[..., i], 90),
                  100 * np.median(seg[..., i]) / tot))
-    wpush = b[..., 14] - b[..., 6]
-    print('  markings split: to the lists ready %.0f cyc, drawing %.0f cyc; visible '
-          'segments median %d (p90 %d)' % (np.median(wpush), np.median(b[..., 7] - b[..., 14]),
-                                          np.median(b[..., 15]), np.percentile(b[..., 15], 90)))
-    print('  wave 0 in the markings: projection %.0f, list slots %.0f, records + barrier %.0f, '
-          'yellow draw %.0f, white draw %.0f cyc' % (
-              np.median(b[..., 16] - b[..., 6]), np.median(b[..., 17] - b[..., 16]),
-              np.median(b[..., 14] - b[..., 17]), np.median(b[..., 18] - b[..., 14]),
-              np.median(b[..., 7] - b[..., 18])))
+    segs = b[..., 15] & 0xFFFFFFFF
+    vis = (segs & 0xFFFF) + (segs >> 16)
+    print('  visible segments median %d (p90 %d)' % (np.median(vis), np.percentile(vis, 90)))
     nl = b[..., 12] & 0xFFFFFFFF
     nw = b[..., 12] >> 32
     print('  nlist median %d (p90 %d, max %d) of 4800 words; nweak median %d max %d'
