@@ -47,7 +47,7 @@ class DtExploreParams(ctypes.Structure):
     _fields_ = [(k, ctypes.c_double) for k in
                 ('pi', 'eps_span', 'eps_final', 'eps_initial', 'ou_m', 'ou_c', 'ou_sigma_min',
                  'ou_sqrt_dt', 'ou_theta', 'ou_mu', 'ou_dt')] + \
-        [('eps_ratio_f', ctypes.c_float), ('head', ctypes.c_int32)]
+        [('eps_ratio', ctypes.c_double), ('head', ctypes.c_int32)]
 
 
 def _sources():
@@ -63,19 +63,25 @@ def _stale():
     return any(os.path.exists(d) and os.path.getmtime(d) > t for d in deps)
 
 
-def build(force=False, verbose=False):
-    """Compile libdtsim.so for gfx950 in-tree."""
-    if not force and not _stale():
+# diagnostic build with conv1s_kernel's ring loads bounds-checked (DTCONV_CHECK,
+# tests/test_gpu_actor.py); loaded only by that test, in a subprocess
+CHECK_LIB_PATH = os.path.join(PKG_DIR, 'libdtsim_check.so')
+
+
+def build(force=False, verbose=False, path=LIB_PATH, defines=()):
+    """Compile libdtsim.so (or a diagnostic variant at `path` with -D defines)
+    for gfx950 in-tree."""
+    if not force and path == LIB_PATH and not _stale():
         return LIB_PATH
-    tmp = LIB_PATH + '.tmp%d' % os.getpid()
-    cmd = [HIPCC] + HIP_FLAGS + ['-o', tmp] + _sources()
+    tmp = path + '.tmp%d' % os.getpid()
+    cmd = [HIPCC] + HIP_FLAGS + ['-D' + d for d in defines] + ['-o', tmp] + _sources()
     if verbose:
         print(' '.join(cmd))
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
-        raise DtError('hipcc failed building libdtsim.so:\n' + r.stderr[-4000:])
-    os.replace(tmp, LIB_PATH)
-    return LIB_PATH
+        raise DtError('hipcc failed building %s:\n' % os.path.basename(path) + r.stderr[-4000:])
+    os.replace(tmp, path)
+    return path
 
 
 _OPTIONAL = set()

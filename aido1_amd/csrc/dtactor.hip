@@ -200,7 +200,7 @@ namespace {
 
 __global__ void __launch_bounds__(256)
 explore_kernel(int n, const float* __restrict__ actor_out, const double* __restrict__ normals,
-               const float* __restrict__ coin, const float* __restrict__ uni,
+               const double* __restrict__ coin, const float* __restrict__ uni,
                double* __restrict__ ou_x, double* __restrict__ ou_steps,
                const int64_t* __restrict__ episode, const double* __restrict__ cycle,
                const double* __restrict__ max_step, const int64_t* __restrict__ explorer_id,
@@ -224,23 +224,26 @@ explore_kernel(int n, const float* __restrict__ actor_out, const double* __restr
   const double x1 = x.y + p.ou_theta * (p.ou_mu - x.y) * p.ou_dt + sd * z.y;
   reinterpret_cast<double2*>(ou_x)[i] = make_double2(x0, x1);
   ou_steps[i] = ou_steps[i] + 1.0;
-  // DDPG.act (models/ddpg/model.py:74-102): noise = eps * OU (float32 sample)
-  const float n0 = (float)(eps * (double)(float)x0), n1 = (float)(eps * (double)(float)x1);
+  // DDPG.act (models/ddpg/model.py:74-102): the sample is float32; epsilon is
+  // an np.float64, so noise = epsilon * sample is float64 (numpy 2, NEP 50),
+  // doubled for a tanh head, and `action += noise` adds in float64 and rounds
+  // once to the float32 action (tests/golden/explorer.json pins this)
+  const double nz0 = eps * (double)(float)x0, nz1 = eps * (double)(float)x1;
   const float2 o = reinterpret_cast<const float2*>(actor_out)[i];
   float a0, a1;
   if (p.head == 0) {          // tanh: noise doubled, clipped to [-1, 1]
-    a0 = fminf(fmaxf(o.x + 2.0f * n0, -1.0f), 1.0f);
-    a1 = fminf(fmaxf(o.y + 2.0f * n1, -1.0f), 1.0f);
+    a0 = fminf(fmaxf((float)((double)o.x + 2.0 * nz0), -1.0f), 1.0f);
+    a1 = fminf(fmaxf((float)((double)o.y + 2.0 * nz1), -1.0f), 1.0f);
   } else if (p.head == 1) {   // sigmoid: clipped to [0, 1]
-    a0 = fminf(fmaxf(o.x + n0, 0.0f), 1.0f);
-    a1 = fminf(fmaxf(o.y + n1, 0.0f), 1.0f);
+    a0 = fminf(fmaxf((float)((double)o.x + nz0), 0.0f), 1.0f);
+    a1 = fminf(fmaxf((float)((double)o.y + nz1), 0.0f), 1.0f);
   } else {
-    a0 = o.x + n0;
-    a1 = o.y + n1;
+    a0 = (float)((double)o.x + nz0);
+    a1 = (float)((double)o.y + nz1);
   }
   // every_second_random (explorers.py:178-194): even ids act uniformly at
-  // random with probability epsilon_ratio * epsilon
-  if (coin && (explorer_id[i] & 1) == 0 && coin[i] < p.eps_ratio_f * (float)eps) {
+  // random when random.uniform(0, 1) < epsilon_ratio * epsilon (float64)
+  if (coin && (explorer_id[i] & 1) == 0 && coin[i] < p.eps_ratio * eps) {
     const float2 u = reinterpret_cast<const float2*>(uni)[i];
     a0 = u.x;
     a1 = u.y;
@@ -268,7 +271,7 @@ explore_done_kernel(int n, const uint8_t* __restrict__ done, double* __restrict_
 }  // namespace
 
 extern "C" int dt_explore(int32_t n, const float* actor_out, const double* normals,
-                          const float* coin, const float* uni, double* ou_x, double* ou_steps,
+                          const double* coin, const float* uni, double* ou_x, double* ou_steps,
                           const int64_t* episode, const double* cycle, const double* max_step,
                           const int64_t* explorer_id, const DtExploreParams* params,
                           float* actions, void* stream) {

@@ -321,6 +321,23 @@ constexpr int s_max_new() {
 static_assert(s_span() <= kSRing, "conv1 stream ring");
 constexpr int kSPre = (s_max_new() * kSQuads + kSThreads - 1) / kSThreads;
 
+#ifdef DTCONV_CHECK
+// Bounds-checked diagnostic build (tests/test_gpu_actor.py): every frame-ring
+// load of conv1s_kernel checks its float4 against the n x slots x 120 x 160
+// ring and sets this word when it would read past it (round 2 fixed such a
+// read on the last sample's row-free step).
+__device__ unsigned int g_conv1_oob;
+#define CONV1_CHECK(p)                                                          \
+  do {                                                                          \
+    const size_t e_ = (size_t)((p) - ring);                                     \
+    if (e_ + 4 > (size_t)n * (size_t)slots * plane) atomicOr(&g_conv1_oob, 1u); \
+  } while (0)
+#else
+#define CONV1_CHECK(p) \
+  do {                 \
+  } while (0)
+#endif
+
 template <bool kStats>
 __global__ void __launch_bounds__(kSThreads, 2)   // 2 waves / SIMD: <= 256 registers
 conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, int s2,
@@ -362,6 +379,9 @@ conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, 
 #pragma unroll
     for (int i = 0; i < kSPre; ++i) {
       const int off = it_r[i] < rows ? it_off[i] : 0;
+      CONV1_CHECK(p0 + off);
+      CONV1_CHECK(p1 + off);
+      CONV1_CHECK(p2 + off);
       pre[i][0] = *reinterpret_cast<const float4*>(p0 + off);
       pre[i][1] = *reinterpret_cast<const float4*>(p1 + off);
       pre[i][2] = *reinterpret_cast<const float4*>(p2 + off);
@@ -1567,6 +1587,19 @@ extern "C" int dt_conv1(const float* ring, int32_t n, int32_t slots, const int32
                      (__half*)y, partials, slope);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
+
+#ifdef DTCONV_CHECK
+// diagnostic build only: the out-of-bounds word of conv1s_kernel (synchronous;
+// clears it)
+extern "C" int dt_diag_conv1_oob(unsigned int* out) {
+  if (hipDeviceSynchronize() != hipSuccess) return DT_E_HIP;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_conv1_oob), sizeof(unsigned int)) != hipSuccess)
+    return DT_E_HIP;
+  const unsigned int zero = 0;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_conv1_oob), &zero, sizeof(zero)) == hipSuccess ? DT_OK
+                                                                                      : DT_E_HIP;
+}
+#endif
 
 extern "C" int dt_conv1_norm(void* y, int32_t n, const float* partials, const float* gamma,
                              const float* beta, float eps, void* stream) {

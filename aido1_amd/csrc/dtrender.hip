@@ -406,23 +406,39 @@ __device__ inline int lane_prefix(uint64_t m) {
                                         __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// A slot for each of up to four items per lane (every lane of the wave calls):
-// the lane counts (0..4) are summed and prefix-summed bit-plane by bit-plane
-// with three ballots, and lane 0 reserves the wave's slots with one LDS atomic.
-__device__ inline void wave_slots4(int32_t* counter, const bool want[4], int slot[4]) {
-  const uint32_t cnt = (uint32_t)want[0] + want[1] + want[2] + want[3];
-  const uint64_t b0 = __ballot(cnt & 1u), b1 = __ballot(cnt & 2u), b2 = __ballot(cnt & 4u);
-  const int total = __popcll(b0) + 2 * __popcll(b1) + 4 * __popcll(b2);
+// A slot for each of up to N items per lane (every lane of the wave calls):
+// the lane counts (0..N) are summed and prefix-summed bit-plane by bit-plane
+// with one ballot per bit, and lane 0 reserves the wave's slots with one LDS
+// atomic.
+template <int N>
+__device__ inline void wave_slotsN(int32_t* counter, const bool* want, int* slot) {
+  constexpr int NB = N < 2 ? 1 : (N < 4 ? 2 : (N < 8 ? 3 : (N < 16 ? 4 : 5)));
+  uint32_t cnt = 0;
+#pragma unroll
+  for (int k = 0; k < N; ++k) cnt += want[k] ? 1u : 0u;
+  uint64_t b[NB];
+  int total = 0;
+#pragma unroll
+  for (int i = 0; i < NB; ++i) {
+    b[i] = __ballot((cnt >> i) & 1u);
+    total += __popcll(b[i]) << i;
+  }
   if (total == 0) return;  // wave-uniform
   int base = 0;
   if ((threadIdx.x & 63) == 0) base = atomicAdd(counter, total);
   base = __builtin_amdgcn_readlane(base, 0);
-  int next = base + lane_prefix(b0) + 2 * lane_prefix(b1) + 4 * lane_prefix(b2);
+  int next = base;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int i = 0; i < NB; ++i) next += lane_prefix(b[i]) << i;
+#pragma unroll
+  for (int k = 0; k < N; ++k) {
     slot[k] = next;
     next += want[k] ? 1 : 0;
   }
+}
+
+__device__ inline void wave_slots4(int32_t* counter, const bool want[4], int slot[4]) {
+  wave_slotsN<4>(counter, want, slot);
 }
 
 // One item per lane: its slot (ballot prefix, one LDS atomic per wave).
@@ -675,7 +691,6 @@ __device__ __forceinline__ void canny(const RenderArgs& a, RenderLds& S, int e,
   const LineDev& L = a.line;
   Slots<kSpill> sl{S, a.spill + (size_t)e * kSpillHalves, a.spill + (size_t)e * kSpillHalves + 4 * NW,
                    a.list_cap};
-  const uint8_t* img8 = reinterpret_cast<const uint8_t*>(S.img);
 
   // phase 2a: gradients of the listed words
   for (int s = tid; s < nlist; s += T) {
@@ -711,47 +726,88 @@ __device__ __forceinline__ void canny(const RenderArgs& a, RenderLds& S, int e,
   __syncthreads();
   RENT(9);
 
-  // phase 2b: NMS + double threshold on the listed words
-  for (int s0 = 0; s0 < nlist; s0 += T) {
-    const int s = s0 + tid;
-    bool want[4] = {false, false, false, false};
-    uint16_t wk[4] = {0, 0, 0, 0};
-    if (s < nlist) {
-      const int w = sl.word(s);
-      const int r = w / WPR, c0 = 4 * (w - r * WPR);
-      const uint2 cur = sl.ent4(s);
+  // phase 2b: NMS + double threshold on the listed words, branch-free: the
+  // entries of the 3 x 3 word neighbourhood are read once (0 outside the
+  // image and for unlisted words: their Sobel is 0), each pixel's two
+  // neighbours selected by its direction class
+  constexpr int U = 1;
+  for (int s0 = 0; s0 < nlist; s0 += U * T) {
+    if (s0 + (tid & ~63) >= nlist) break;   // wave-uniform: nothing left for this wave
+    bool want[4 * U];
+    uint16_t wk[4 * U];
+    uint2 nv[U];
+    bool upd[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int s = s0 + tid + u * T;
+      const bool act = s < nlist;
+      const int sc = act ? s : nlist - 1;
+      const int w = sl.word(sc);
+      const int r = w / WPR, cw = w - r * WPR, c0 = 4 * cw;
+      const uint2 cur = sl.ent4(sc);
+      uint2 nb[3][3];
+#pragma unroll
+      for (int dy = -1; dy <= 1; ++dy) {
+#pragma unroll
+        for (int dx = -1; dx <= 1; ++dx) {
+          if (dy == 0 && dx == 0) {
+            nb[1][1] = cur;
+            continue;
+          }
+          const int rr = r + dy, cc = cw + dx;
+          const bool in = (unsigned)rr < (unsigned)H && (unsigned)cc < (unsigned)WPR;
+          const int slot = S.wmap[in ? rr * WPR + cc : w];
+          const uint2 v = sl.ent4(slot > 0 ? slot - 1 : 0);
+          nb[dy + 1][dx + 1] = (in && slot > 0) ? v : make_uint2(0u, 0u);
+        }
+      }
+      // magnitudes of the 3 x 6 pixel block around the word
+      uint32_t M[3][6];
+#pragma unroll
+      for (int k = 0; k < 3; ++k) {
+        M[k][0] = (nb[k][0].y >> 16) & WK_MAG;
+        M[k][1] = nb[k][1].x & WK_MAG;
+        M[k][2] = (nb[k][1].x >> 16) & WK_MAG;
+        M[k][3] = nb[k][1].y & WK_MAG;
+        M[k][4] = (nb[k][1].y >> 16) & WK_MAG;
+        M[k][5] = nb[k][2].x & WK_MAG;
+      }
       const uint32_t vv[4] = {cur.x & 0xFFFFu, cur.x >> 16, cur.y & 0xFFFFu, cur.y >> 16};
-      uint32_t setb[4] = {0, 0, 0, 0};
+      uint32_t setb[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         const int m = (int)(vv[i] & WK_MAG);
-        if (m > L.canny_lo) {
-          const int dir = (int)(vv[i] >> WK_DIR_SHIFT) & 3;
-          const int c = c0 + i;
-          // dir 0: (0,-1)/(0,+1); 1: (-1,0)/(+1,0); 2: (-1,-1)/(+1,+1); 3: (-1,+1)/(+1,-1)
-          const int dy1 = dir == 0 ? 0 : -1;
-          const int dx1 = dir == 0 ? -1 : (dir == 1 ? 0 : (dir == 2 ? -1 : 1));
-          const int n1 = (int)(sl.at(r + dy1, c + dx1) & WK_MAG);
-          const int n2 = (int)(sl.at(r - dy1, c - dx1) & WK_MAG);
-          const bool keep = m > n1 && (dir >= 2 ? m > n2 : m >= n2);
-          if (keep) {
-            if (m > L.canny_hi) {
-              setb[i] = WK_CAND | WK_EDGE;
-            } else {
-              setb[i] = WK_CAND;
-              want[i] = true;
-              wk[i] = (uint16_t)(r * W + c);
-            }
-          }
-        }
+        const int dir = (int)(vv[i] >> WK_DIR_SHIFT) & 3;
+        // dir 0: (0,-1)/(0,+1); 1: (-1,0)/(+1,0); 2: (-1,-1)/(+1,+1); 3: (-1,+1)/(+1,-1).
+        // Selected with all-ones masks, not a select chain: the chain becomes an
+        // indexed read of M, which the compiler then keeps in scratch memory.
+        const uint32_t d0 = 0u - (uint32_t)(dir == 0), d1 = 0u - (uint32_t)(dir == 1),
+                       d2 = 0u - (uint32_t)(dir == 2), d3 = 0u - (uint32_t)(dir == 3);
+        const int n1 = (int)((d0 & M[1][i]) | (d1 & M[0][i + 1]) | (d2 & M[0][i]) |
+                             (d3 & M[0][i + 2]));
+        const int n2 = (int)((d0 & M[1][i + 2]) | (d1 & M[2][i + 1]) | (d2 & M[2][i + 2]) |
+                             (d3 & M[2][i]));
+        const bool keep = act && m > L.canny_lo && m > n1 && (dir >= 2 ? m > n2 : m >= n2);
+        const bool strong = m > L.canny_hi;
+        setb[i] = keep ? (strong ? (uint32_t)(WK_CAND | WK_EDGE) : (uint32_t)WK_CAND) : 0u;
+        want[4 * u + i] = keep && !strong;
+        wk[4 * u + i] = (uint16_t)(r * W + c0 + i);
       }
       // only this lane writes these four entries; neighbours read only the
       // magnitude bits, which do not change
-      if (setb[0] | setb[1] | setb[2] | setb[3])
-        sl.set_ent4(s, make_uint2(cur.x | setb[0] | (setb[1] << 16),
-                                  cur.y | setb[2] | (setb[3] << 16)));
+      upd[u] = (setb[0] | setb[1] | setb[2] | setb[3]) != 0u;
+      nv[u] = make_uint2(cur.x | setb[0] | (setb[1] << 16), cur.y | setb[2] | (setb[3] << 16));
     }
-    wave_push4(&S.cnt[kNWeak], S.weak, kWeakCap, want, wk);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (upd[u]) sl.set_ent4(s0 + tid + u * T, nv[u]);
+    int slot[4 * U];
+#pragma unroll
+    for (int k = 0; k < 4 * U; ++k) slot[k] = 0;
+    wave_slotsN<4 * U>(&S.cnt[kNWeak], want, slot);
+#pragma unroll
+    for (int k = 0; k < 4 * U; ++k)
+      if (want[k] && slot[k] < kWeakCap) S.weak[slot[k]] = wk[k];
   }
   __syncthreads();
   RENT(10);
@@ -1039,29 +1095,32 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, in
   // the dilation path of the output phase (every quad does when the dilation
   // radius is >= 2: uniformity only covers +-1 pixel).
   uint8_t* mbase = a.masks ? a.masks + (size_t)e * 4 * NPIX : nullptr;
-  for (int q0 = 0; q0 < NQ && mbase; q0 += T) {
-    const int q = q0 + tid;
-    const bool act = q < NQ;
-    bool non[4] = {false, false, false, false};
-    int r = 0, cw0 = 0;
-    if (act) {
-      r = q / QPR;
-      cw0 = 4 * (q - r * QPR);
+  constexpr int kQuadPer = (NQ + T - 1) / T;  // quads per lane (3 at 512 threads)
+  if (mbase) {
+    bool non[4 * kQuadPer];
+#pragma unroll
+    for (int k = 0; k < kQuadPer; ++k) {
+      // straight-line over the lane's quads (clamped, flagged): their LDS
+      // reads and tests interleave
+      const int qq = tid + k * T;
+      const bool act = qq < NQ;
+      const int q = act ? qq : NQ - 1;
+      const int r = q / QPR, cw0 = 4 * (q - r * QPR);
       uint32_t m[3][4], lw[3], rw[3];
 #pragma unroll
-      for (int k = 0; k < 3; ++k) {
-        int rr = r - 1 + k;
+      for (int i = 0; i < 3; ++i) {
+        int rr = r - 1 + i;
         rr = rr < 0 ? 0 : (rr > H - 1 ? H - 1 : rr);
         const uint32_t* row = S.img + rr * WPR;
         const uint4 v = *reinterpret_cast<const uint4*>(row + cw0);
-        m[k][0] = v.x;
-        m[k][1] = v.y;
-        m[k][2] = v.z;
-        m[k][3] = v.w;
+        m[i][0] = v.x;
+        m[i][1] = v.y;
+        m[i][2] = v.z;
+        m[i][3] = v.w;
         // side words at the image edge clamp to the quad's own edge word:
         // BORDER_REPLICATE repeats the edge pixel, already compared
-        lw[k] = cw0 > 0 ? row[cw0 - 1] : v.x;
-        rw[k] = cw0 + 4 < WPR ? row[cw0 + 4] : v.w;
+        lw[i] = row[cw0 > 0 ? cw0 - 1 : cw0];
+        rw[i] = row[cw0 + 4 < WPR ? cw0 + 4 : cw0 + 3];
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -1075,27 +1134,34 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, in
         const uint32_t diff = (mid ^ rep) | (m[0][j] ^ rep) | (m[2][j] ^ rep) |
                               (((l0 >> 24) ^ b) | ((l1 >> 24) ^ b) | ((l2 >> 24) ^ b)) |
                               (((r0 ^ b) | (r1 ^ b) | (r2 ^ b)) & 255u);
-        non[j] = diff != 0u;
+        non[4 * k + j] = act && diff != 0u;
       }
     }
-    int slot[4] = {0, 0, 0, 0};
-    wave_slots4(&C[kNList], non, slot);
-    if (act) {
-      uint16_t* gl = a.spill + (size_t)e * kSpillHalves + 4 * NW;
-      uint32_t wm[4];
+    int slot[4 * kQuadPer];
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int w = r * WPR + cw0 + j;
-        wm[j] = non[j] ? (uint32_t)slot[j] + 1u : 0u;
-        if (non[j]) {
-          if (slot[j] < a.list_cap)
-            S.u.w.list[slot[j]] = (uint16_t)w;
-          else
-            gl[slot[j]] = (uint16_t)w;
+    for (int k = 0; k < 4 * kQuadPer; ++k) slot[k] = 0;
+    wave_slotsN<4 * kQuadPer>(&C[kNList], non, slot);
+    uint16_t* gl = a.spill + (size_t)e * kSpillHalves + 4 * NW;
+#pragma unroll
+    for (int k = 0; k < kQuadPer; ++k) {
+      const int q = tid + k * T;
+      if (q < NQ) {
+        uint32_t wm[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int w = 4 * q + j;
+          const int sj = slot[4 * k + j];
+          wm[j] = non[4 * k + j] ? (uint32_t)sj + 1u : 0u;
+          if (non[4 * k + j]) {
+            if (sj < a.list_cap)
+              S.u.w.list[sj] = (uint16_t)w;
+            else
+              gl[sj] = (uint16_t)w;
+          }
         }
+        *reinterpret_cast<uint2*>(S.wmap + 4 * q) =
+            make_uint2(wm[0] | (wm[1] << 16), wm[2] | (wm[3] << 16));
       }
-      *reinterpret_cast<uint2*>(S.wmap + r * WPR + cw0) =
-          make_uint2(wm[0] | (wm[1] << 16), wm[2] | (wm[3] << 16));
     }
   }
   __syncthreads();
@@ -1129,6 +1195,13 @@ __global__ __launch_bounds__(kRenderThreads) __attribute__((amdgpu_waves_per_eu(
 render_kernel(RenderArgs a) {
   __shared__ __attribute__((aligned(16))) RenderLds S;
   const int tid = threadIdx.x;
+#ifdef DTSIM_STAMPS
+  {
+    const int e = blockIdx.x;
+    RENSTAMP(16, __builtin_amdgcn_s_memtime());
+    RENSTAMP(17, __builtin_amdgcn_s_memrealtime());
+  }
+#endif
   const LineDev& L = a.line;
   if (tid < PAL_N) {
     const uint32_t p = kPalette[tid];

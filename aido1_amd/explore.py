@@ -12,7 +12,9 @@ Restates, with a leading env dimension on the GPU:
     = epsilon * OU sample; with every_second_random, explorers with an even id
     take a U[0,1)^2 action with probability epsilon_ratio * epsilon.
 The normals come from torch's Philox generator instead of numpy's global
-RandomState (tests pin the arithmetic by feeding the reference's normals).
+RandomState, the coin (float64) and uniforms likewise; tests pin the
+arithmetic and the loop's order of draws by feeding the reference's own
+(tests/golden/explorer.json).
 """
 import math
 
@@ -107,10 +109,13 @@ class OUNoise:
 
 
 def act(actor_out, noise=None, head='tanh'):
-    """DDPG.act on a batch of actor outputs (models/ddpg/model.py:74-102)."""
+    """DDPG.act on a batch of actor outputs (models/ddpg/model.py:74-102).  noise
+    is float64 (epsilon is an np.float64 there, so epsilon * sample is float64
+    under numpy 2), and `action += noise` adds in float64 and rounds once to
+    the float32 action."""
     a = actor_out
     if noise is not None:
-        a = a + (2 * noise if head == 'tanh' else noise)
+        a = (a.double() + (2 * noise if head == 'tanh' else noise)).float()
     if head == 'tanh':
         return a.clamp(-1.0, 1.0)
     if head == 'sigmoid':
@@ -138,18 +143,24 @@ class EpsilonSchedule:
         return np.asarray(eps, np.float64)
 
 
-def explore_actions(actor_out, ou, epsilon, explorer_id, config, generator=None, head='tanh'):
-    """training/explorers.py:178-194 for a batch: epsilon [n] tensor, explorer_id
-    [n] int tensor (the p_id each env plays)."""
+def explore_actions(actor_out, ou, epsilon, explorer_id, config, generator=None, head='tanh',
+                    draws=None):
+    """training/explorers.py:178-194 for a batch: epsilon [n] float64 tensor,
+    explorer_id [n] int tensor (the p_id each env plays).  draws: optional
+    (normals [n, 2] f64, coin [n] f64, uniforms [n, 2] f32) to use instead of
+    the generator's (tests inject the reference's own draws)."""
     t = config['training']
-    noise = (epsilon.unsqueeze(1) * ou.sample()).float()
+    normals, coin, u = draws if draws is not None else (None, None, None)
+    noise = epsilon.double().unsqueeze(1) * ou.sample(normals).double()
     a = act(actor_out, noise, head)
     if t.get('every_second_random'):
         n = actor_out.shape[0]
         dev = actor_out.device
-        coin = torch.rand(n, device=dev, generator=generator)
-        rnd = (explorer_id % 2 == 0) & (coin < t['epsilon_ratio'] * epsilon.float())
-        u = torch.rand(n, actor_out.shape[1], device=dev, generator=generator)
+        if coin is None:
+            coin = torch.rand(n, dtype=torch.float64, device=dev, generator=generator)
+        rnd = (explorer_id % 2 == 0) & (coin < t['epsilon_ratio'] * epsilon.double())
+        if u is None:
+            u = torch.rand(n, actor_out.shape[1], device=dev, generator=generator)
         a = torch.where(rnd.unsqueeze(1), u, a)
     return a
 
@@ -162,8 +173,8 @@ class FusedExplore:
     episode count) as the dt_explore / dt_explore_done HIP kernels
     (include/dtactor.h): one launch each instead of ~25 element-wise torch
     kernels per decision.  The random numbers are the torch restatement's own
-    draws in its order (randn [n, 2] f64 for the OU normals, then rand [n] and
-    rand [n, 2] for every_second_random), so for one generator state both
+    draws in its order (randn [n, 2] f64 for the OU normals, then rand [n] f64 and
+    rand [n, 2] f32 for every_second_random), so for one generator state both
     paths produce the same actions and states bit for bit
     (tests/test_gpu_explore.py)."""
 
@@ -178,7 +189,7 @@ class FusedExplore:
         p.eps_final, p.eps_initial = cycle_eps.f, cycle_eps.i
         p.ou_m, p.ou_c, p.ou_sigma_min = ou.m, ou.c, ou.sigma_min
         p.ou_sqrt_dt, p.ou_theta, p.ou_mu, p.ou_dt = math.sqrt(ou.dt), ou.theta, ou.mu, ou.dt
-        p.eps_ratio_f = float(np.float32(t['epsilon_ratio'])) if self.every_second_random else 0.0
+        p.eps_ratio = float(t['epsilon_ratio']) if self.every_second_random else 0.0
         p.head = _HEADS.get(head, 2)
         self.params = p
         self.tanh = head == 'tanh'
@@ -194,7 +205,7 @@ class FusedExplore:
         normals = torch.randn(n, 2, dtype=torch.float64, device=dev, generator=generator)
         coin = uni = None
         if self.every_second_random:
-            coin = torch.rand(n, device=dev, generator=generator)
+            coin = torch.rand(n, dtype=torch.float64, device=dev, generator=generator)
             uni = torch.rand(n, 2, device=dev, generator=generator)
         rc = self.L.dt_explore(n, ao.data_ptr(), normals.data_ptr(),
                                coin.data_ptr() if coin is not None else None,

@@ -1,8 +1,8 @@
 """Actor-in-loop batched rollout (BASELINE configs[3]).
 
 One GPU runs `n_envs` environments split over maps (mixed small_loop /
-zigzag), all rendering into ONE shared frame ring so a single actor forward
-covers every env.  Per decision:
+zigzag), all rendering into ONE shared frame ring so one actor forward covers
+every exploring env.  Per decision:
 
   actor (fp16 MFMA, ring read zero-copy; actor_mode 'reference' = the reference's
   train-mode batch-of-one BatchNorm + live dropout, 'eval' = BN folded)  -> DDPG.act noise / every-
@@ -12,6 +12,14 @@ covers every env.  Per decision:
 
 which is SingleThreadExplorer._explore_episode's loop body
 (training/explorers.py:177-211) for thousands of explorers at once.
+
+Exploring and exploiting explorers (config.json:183-186: 7 exploring_virtual +
+1 exploiting_virtual): the last n_exploit envs (n / 8 by default) are
+exploiters.  They act with their own copy of the weights (load_exploit_actor;
+TrainLoop gives it the target actor, which the reference's exploiters
+hard-copy, explorers.py:104-105) with epsilon 0: no noise, no random actions,
+the action the clipped actor output (explorers.py:116, 182-184).  The OU
+process still advances for them, as the reference samples it every step.
 """
 import math
 
@@ -21,7 +29,7 @@ import torch
 from aido1_amd.actor import ConfigActor, FusedActor
 from aido1_amd.config import EnvConfig
 from aido1_amd.env_wrappers import map_tanh_in_place
-from aido1_amd.explore import FusedExplore, OUNoise, explore_actions
+from aido1_amd.explore import FusedExplore, OUNoise, act, explore_actions
 from aido1_amd.render import H, W, RenderOutput
 from aido1_amd.vec_env import StepOutput, VecEnv
 
@@ -48,7 +56,7 @@ class CycleEpsilon:
 class ActorRollout:
     def __init__(self, config, n_envs=4096, maps=('small_loop', 'zigzag'), device=0, seed=1234,
                  env_id_base=0, actor=None, dtype=torch.float16, masks=True,
-                 actor_mode='reference', fused_explore=True):
+                 actor_mode='reference', fused_explore=True, n_exploit=None):
         self.config = config
         self.device = torch.device('cuda', device)
         self.n = n_envs
@@ -85,12 +93,26 @@ class ActorRollout:
             actor = ConfigActor(config['model']['actor'])
         self.actor_mode = actor_mode
         self.actor = FusedActor(actor.to(self.device), dtype=dtype, mode=actor_mode)
+        if n_exploit is None:
+            t = config['training']
+            n_xpl = t.get('num_threads_exploiting', 0) + t.get('num_threads_exploiting_virtual', 0)
+            n_exp = t.get('num_threads_exploring', 0) + t.get('num_threads_exploring_virtual', 0)
+            n_exploit = (n_envs * n_xpl) // (n_xpl + n_exp) if n_xpl + n_exp else 0
+        self.n_exploit = int(n_exploit)
+        self.n_explore = n_envs - self.n_exploit
+        self.exploit_actor = FusedActor(actor, dtype=dtype, mode=actor_mode) \
+            if self.n_exploit else None
+        self.actor_out = torch.zeros(n_envs, 2, dtype=torch.float32, device=self.device)
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(seed + 17 * env_id_base)
         self.ou = OUNoise.from_config(config, n_envs, device=self.device, generator=self.gen)
         self.eps = CycleEpsilon(config, n_envs, self.device, generator=self.gen)
         self.episode = torch.zeros(n_envs, dtype=torch.int64, device=self.device)
-        self.explorer_id = torch.arange(env_id_base, env_id_base + n_envs, device=self.device)
+        # the p_id parity decides every_second_random; exploiters get odd ids
+        # (their actions are replaced by the clipped actor output anyway)
+        ids = torch.arange(env_id_base, env_id_base + n_envs, device=self.device)
+        ids[self.n_explore:] = ids[self.n_explore:] | 1
+        self.explorer_id = ids
         self.actor_events = None
         # dt_explore (include/dtactor.h); fused_explore=False keeps the torch
         # restatement (explore.py), which draws the same numbers
@@ -113,14 +135,29 @@ class ActorRollout:
         return self.ring[:, self.order()]
 
     def load_actor(self, actor):
-        """Act with `actor`'s current weights from the next decision on."""
+        """The exploring envs act with `actor`'s current weights from the next
+        decision on (the reference's model workers act with the trained
+        model, training/managers.py:182-208)."""
         self.actor.refresh(actor)
+
+    def load_exploit_actor(self, actor):
+        """The exploiting envs act with `actor`'s weights (explorers.py:104-105
+        hard-copies the target model at every episode start; here the whole
+        exploiter block is refreshed at once)."""
+        if self.exploit_actor is not None:
+            self.exploit_actor.refresh(actor)
 
     def step(self, timing=None):
         """One decision for every env; returns (reward, reward_mod, done) views."""
         if timing is not None:
             timing[0].record()
-        out = self.actor(self.ring, self.order())
+        ne = self.n_explore
+        if self.exploit_actor is None:
+            out = self.actor(self.ring, self.order())
+        else:
+            out = self.actor_out
+            out[:ne] = self.actor(self.ring[:ne], self.order())
+            out[ne:] = self.exploit_actor(self.ring[ne:], self.order())
         if timing is not None:
             timing[1].record()
         if self.fx is not None:
@@ -129,6 +166,8 @@ class ActorRollout:
             eps = self.eps(self.episode)
             self.actions.copy_(explore_actions(out, self.ou, eps, self.explorer_id, self.config,
                                                generator=self.gen, head=self.head))
+        if self.exploit_actor is not None:   # epsilon 0: DDPG.act without noise
+            self.actions[ne:] = act(out[ne:], None, self.head)
         for env, o, ro, sl in zip(self.envs, self.outs, self.renders, self.slices):
             env.step_into(self.actions[sl], o)
             env.render_into(ro, fresh=o.done)

@@ -16,8 +16,12 @@ Here one process per GPU runs, per iteration:
   DDPGTrainer.update         critic + actor + soft target update (grads
                              all-reduced over ranks with RCCL)
   replay.update_priorities   |td_error| + eps
-  rollout actor refresh      the acting copy follows the target actor, which
-                             is what the reference's explorers act with
+  rollout actor refresh      the exploring envs act with the trained (online)
+                             actor, as the reference's model workers do
+                             (training/managers.py:182-208 pass
+                             models[p_id], the models DDPGTrainer.update
+                             steps); the exploiting envs with the target
+                             actor (explorers.py:104-105, managers.py:239-262)
 
 With overlap=True the update of decision t runs on a side stream while the
 main stream runs decision t+1's rollout (actor, exploration, steps, render);
@@ -46,7 +50,7 @@ class TrainLoop:
     def __init__(self, config, n_envs=4096, maps=('small_loop', 'zigzag'), device=0, seed=1234,
                  env_id_base=0, buffer_size=None, prioritized=True, batch_size=None,
                  updates_per_step=1, refresh_every=1, obs_dtype=None, actor_dtype=torch.float16,
-                 actor_mode='reference', masks=False, graph=True, overlap=False):
+                 actor_mode='reference', masks=False, graph=True, overlap=False, n_exploit=None):
         t = config['training']
         self.config = config
         self.device = torch.device('cuda', device)
@@ -60,8 +64,10 @@ class TrainLoop:
         critic = ConfigCritic(config['model']['critic'])
         self.trainer = DDPGTrainer(config, actor, critic, device=self.device, graph=graph)
         self.rollout = ActorRollout(config, n_envs, maps=maps, device=device, seed=seed,
-                                    env_id_base=env_id_base, actor=self.trainer.target_actor,
-                                    dtype=actor_dtype, masks=masks, actor_mode=actor_mode)
+                                    env_id_base=env_id_base, actor=self.trainer.actor,
+                                    dtype=actor_dtype, masks=masks, actor_mode=actor_mode,
+                                    n_exploit=n_exploit)
+        self.rollout.load_exploit_actor(self.trainer.target_actor)
         size = int(buffer_size or t['buffer_size'])
         gen = torch.Generator(device=self.device)
         gen.manual_seed(seed * 7919 + env_id_base)
@@ -90,7 +96,7 @@ class TrainLoop:
             torch.cuda.current_stream(self.device).wait_stream(self.side)
             self.pending = False
             if self.refresh_due:
-                self.rollout.load_actor(self.trainer.target_actor)
+                self._refresh()
                 self.refresh_due = False
         # next_obs straight from the frame ring into the buffer; the stored rows
         # are the next decision's obs (no stacked copy of the ring)
@@ -115,8 +121,12 @@ class TrainLoop:
             torch.cuda.current_stream(self.device).wait_stream(self.side)
             self.pending = False
             if self.refresh_due:
-                self.rollout.load_actor(self.trainer.target_actor)
+                self._refresh()
                 self.refresh_due = False
+
+    def _refresh(self):
+        self.rollout.load_actor(self.trainer.actor)
+        self.rollout.load_exploit_actor(self.trainer.target_actor)
 
     def _update(self):
         if self.prioritized:
@@ -132,4 +142,4 @@ class TrainLoop:
             if self.side is not None:
                 self.refresh_due = True     # applied on the main stream (step / flush)
             else:
-                self.rollout.load_actor(self.trainer.target_actor)
+                self._refresh()

@@ -105,21 +105,22 @@ int dt_conv12(const float* ring, int32_t n, int32_t slots, const int32_t* order,
  *              (training/explorers.py:92-111, utils/util.py:36-40)
  *   OU step  x += theta (mu - x) dt + max(m steps + c, sigma_min) sqrt(dt) z,
  *              steps += 1 (utils/random_process.py:42-47)
- *   action   = clip(actor_out + (2 if tanh) * float(eps * float(x)))
- *              (models/ddpg/model.py:74-102)
+ *   action   = clip(float(actor_out + (2 if tanh) * (eps * float(x))))
+ *              (models/ddpg/model.py:74-102: the noise is float64, the sum
+ *              rounded once to float32, as numpy 2 evaluates it)
  *   every_second_random (coin != NULL): even explorer ids take uni[i] when
- *              coin[i] < float(ratio) * float(eps) (explorers.py:178-194)
- *   actor_out f32 [n, 2]; normals f64 [n, 2]; coin f32 [n], uni f32 [n, 2]
+ *              coin[i] < ratio * eps in float64 (explorers.py:178-194)
+ *   actor_out f32 [n, 2]; normals f64 [n, 2]; coin f64 [n], uni f32 [n, 2]
  *   ou_x f64 [n, 2] and ou_steps f64 [n] updated in place; episode i64 [n];
  *   cycle, max_step f64 [n]; explorer_id i64 [n]; actions f32 [n, 2] out. */
 typedef struct DtExploreParams {
   double pi, eps_span, eps_final, eps_initial;          /* eps_span = initial - final */
   double ou_m, ou_c, ou_sigma_min, ou_sqrt_dt, ou_theta, ou_mu, ou_dt;
-  float eps_ratio_f;                                    /* (float)epsilon_ratio */
+  double eps_ratio;                                     /* epsilon_ratio */
   int32_t head;                                         /* 0 tanh, 1 sigmoid, 2 none */
 } DtExploreParams;
 
-int dt_explore(int32_t n, const float* actor_out, const double* normals, const float* coin,
+int dt_explore(int32_t n, const float* actor_out, const double* normals, const double* coin,
                const float* uni, double* ou_x, double* ou_steps, const int64_t* episode,
                const double* cycle, const double* max_step, const int64_t* explorer_id,
                const DtExploreParams* params, float* actions, void* stream);

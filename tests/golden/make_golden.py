@@ -503,6 +503,166 @@ def gen_ddpg_single(double=False):
     dump('ddpg_single_f64.json' if double else 'ddpg_single.json', out)
 
 
+def gen_explorer():
+    """SingleThreadExplorer._explore_episode (training/explorers.py:164-213), the
+    reference's own loop, over the oracle SimulatorRef (the reference's own
+    EnvironmentWrapper around it, as gen_env_wrapper): records every random
+    draw in the loop's order -- the OU normals (utils/random_process.py:42-47),
+    the every-second-random coin (random.uniform) and random action
+    (np.random.random) -- the actor output DDPG.act saw (a stub actor: the
+    network itself is pinned by gen_actor), the action handed to env.step and
+    the replay tuple's action after the wrapper's in-place map, reward (the
+    reward_modified choice) and done.  Explorers: exploring p_id 0 (even: every
+    second random) and 1, and the exploiting_virtual explorer (epsilon 0, no
+    noise; explorers.py:104-116, 182-184)."""
+    import torch
+
+    import training.explorers as tx
+    import utils.env_wrappers as ew
+    import utils.random_process as rp
+    from utils.util import create_decay_fn
+    sys.path.insert(0, REPO)
+    from oracle import dtsim_ref as R
+    with open(os.path.join(REF, 'config.json')) as f:
+        config = json.load(f)
+    rows = [['curve_left/W', 'straight/W', 'curve_left/N'],
+            ['straight/S', 'grass', 'straight/N'],
+            ['curve_left/S', 'straight/E', 'curve_left/E']]
+    log = {}
+
+    class RandProxy:       # numpy.random / random with the loop's draws recorded
+        def __init__(self, real):
+            self.real = real
+
+        def normal(self, *a, **k):
+            v = self.real.normal(*a, **k)
+            log['normals'].append([float(x) for x in np.atleast_1d(v)])
+            return v
+
+        def random(self, *a, **k):
+            v = self.real.random(*a, **k)
+            log['randoms'].append([float(x) for x in np.atleast_1d(v)])
+            return v
+
+        def uniform(self, *a, **k):
+            v = self.real.uniform(*a, **k)
+            log['coins'].append(float(v))
+            return v
+
+        def __getattr__(self, k):
+            return getattr(self.real, k)
+
+    class NpProxy:
+        random = RandProxy(np.random)
+
+        def __getattr__(self, k):
+            return getattr(np, k)
+    rp.np = NpProxy()
+    tx.np = NpProxy()
+    tx.random = RandProxy(random)
+
+    class StubActor(torch.nn.Module):
+        """A deterministic function of the observation (the stacked frame
+        markers below), so consecutive decisions see different outputs."""
+        def forward(self, x):
+            m = x.double().mean()
+            out = torch.stack([torch.tanh(3.0 * torch.sin(7.0 * m) - 0.2),
+                               torch.tanh(2.0 * torch.cos(5.0 * m) + 0.1)]).float().view(1, 2)
+            log['actor_out'].append([float(v) for v in out.view(-1)])
+            return out
+
+    class OracleDT(ew.BaseEnvironment):
+        def __init__(self, seed):
+            self.sim = R.SimulatorRef(rows, seed=seed, env_id=0, cfg=R.SimConfig(max_env_steps=60))
+
+        def _obs(self):
+            # a 1 x 2 x 2 marker of the pose (from_numpy'd, as the reference's env returns)
+            x, z = float(self.sim.cur_pos[0]), float(self.sim.cur_pos[2])
+            return [[[x, z], [float(self.sim.cur_angle), 0.25]]]
+
+        def step(self, action):
+            _, r, d, info = self.sim.step(np.array(action, np.float64))
+            return [self._obs(), r, d, None]
+
+        def reset(self):
+            self.sim.reset()
+            return self._obs()
+
+        def get_observation(self):
+            return self._obs()
+
+        def change_model(self, seed):
+            return 'ok'
+
+        def collect_garbage(self):
+            pass
+
+    out = []
+    t = config['training']
+    cycle_len = 20
+    decay = create_decay_fn('cycle', initial_value=t['initial_epsilon'],
+                            final_value=t['final_epsilon'], cycle_len=cycle_len,
+                            num_cycles=t['max_episodes'] // cycle_len)
+    for kind, p_id in (('exploration_virtual', 0), ('exploration_virtual', 1),
+                       ('exploiting_virtual', 7)):
+        cfg = json.loads(json.dumps(config))
+        cfg['environment']['wrapper']['max_env_steps'] = 60
+        seed_box = {}
+        ew.DuckietownEnvironmentWrapper = lambda **kw: OracleDT(seed_box['seed'])
+        seed_box['seed'] = 31 + p_id
+        model = tx.create_model(cfg['model'])
+        model.actor = StubActor()
+        explorer = tx.SingleThreadExplorer(kind, cfg, p_id, model,
+                                           {'env_type': 'normal', 'env_init_args': {},
+                                            'env_config': {}}, [], None, None, None)
+        if kind.startswith('exploiting'):
+            explorer.model.actor = StubActor()
+        orig_step = explorer.environment.step
+
+        def step(action, orig_step=orig_step):
+            log['action'].append([float(v) for v in action])   # before the in-place map
+            return orig_step(action)
+        explorer.environment.step = step
+        ou = rp.create_action_random_process(cfg)
+        episodes = []
+        for e in range(3):
+            # episode counters that are multiples of the cycle: cos(0) = 1 exactly
+            ep = e * cycle_len
+            eps = min(t['initial_epsilon'], max(t['final_epsilon'], decay(ep)))
+            if kind.startswith('exploiting'):
+                eps = 0.0
+            for k in ('normals', 'randoms', 'coins', 'actor_out', 'action'):
+                log[k] = []
+            metrics = {'reward': 0.0, 'reward_modified': 0.0, 'step': 0, 'epsilon': eps}
+            ou.reset_states()
+            replay, _ = explorer._explore_episode(ou, eps, metrics, t)
+            # per decision: which draws happened (the coin only for even
+            # exploring ids, the random action only when the coin came up)
+            steps, ci, ri, ai = [], 0, 0, 0
+            for d, (obs, act, rew, nxt, done) in enumerate(replay):
+                rec = {'normals': log['normals'][d], 'action': log['action'][d],
+                       'replay_action': [float(v) for v in act], 'reward': float(rew),
+                       'done': bool(done)}
+                if kind.startswith('exploration') and t['every_second_random'] and p_id % 2 == 0:
+                    rec['coin'] = log['coins'][ci]
+                    ci += 1
+                    if rec['coin'] < t['epsilon_ratio'] * eps:
+                        rec['random'] = log['randoms'][ri]
+                        ri += 1
+                        steps.append(rec)
+                        continue
+                rec['actor_out'] = log['actor_out'][ai]
+                ai += 1
+                steps.append(rec)
+            assert ci == len(log['coins']) and ri == len(log['randoms'])
+            assert ai == len(log['actor_out'])
+            episodes.append({'episode_counter': ep, 'epsilon': eps, 'ou_steps_before':
+                             float(ou.n_steps) - len(steps), 'steps': steps})
+        out.append({'exploration_type': kind, 'p_id': p_id, 'cycle_len': cycle_len,
+                    'episodes': episodes})
+    dump('explorer.json', {'numpy': np.__version__, 'explorers': out})
+
+
 def gen_config_keys():
     """The config.json keys the env path reads (wrapper section, actor head, the
     explorer's noise/epsilon keys) — a data extract, not the file."""
@@ -513,7 +673,9 @@ def gen_config_keys():
             'initial_epsilon', 'final_epsilon', 'epsilon_ratio', 'max_episodes',
             'every_second_random', 'alpha', 'beta', 'batch_size', 'buffer_size', 'gamma', 'tau',
             'optimizer', 'critic_loss', 'actor_train_decay', 'critic_train_decay',
-            'num_threads_training', 'update_steps_between_update')
+            'num_threads_training', 'update_steps_between_update', 'num_threads_exploring',
+            'num_threads_exploring_virtual', 'num_threads_exploiting',
+            'num_threads_exploiting_virtual')
     mini = {'environment': {'wrapper': cfg['environment']['wrapper']},
             'model': {'num_action': cfg['model']['num_action'], 'actor': cfg['model']['actor'],
                       'critic': cfg['model']['critic']},
@@ -531,6 +693,11 @@ def gen_config_keys():
 
 def main():
     sys.path.insert(0, REF)
+    only = os.environ.get('ONLY')   # e.g. ONLY=gen_explorer: regenerate one fixture
+    if only:
+        install_stubs()
+        globals()[only]()
+        return
     gen_config_keys()
     install_stubs()
     gen_bresenham()
@@ -546,6 +713,7 @@ def main():
     gen_ddpg_update(double=True)
     gen_ddpg_single()
     gen_ddpg_single(double=True)
+    gen_explorer()
 
 
 if __name__ == '__main__':

@@ -55,3 +55,44 @@ def test_every_second_random():
     assert not odd_rand.any()           # odd explorers never take the random branch
     frac = ((a[0::2] >= 0).all(1) & (a[0::2] < 1).all(1)).float().mean().item()
     assert 0.2 < frac < 0.45            # ~epsilon_ratio * eps = 0.25 (+ noise hits)
+
+
+def _explorer_fixture():
+    return golden('explorer.json')['explorers']
+
+
+def test_explorer_loop_matches_reference_fixture():
+    """The reference's own SingleThreadExplorer._explore_episode (training/
+    explorers.py:164-213), recorded in tests/golden/explorer.json with every
+    draw of its loop: the batched restatement (explore.py: OU sample ->
+    DDPG.act noise / every-second-random -> the wrapper's in-place tanh map),
+    fed those draws and the recorded actor outputs, reproduces each decision's
+    action and stored replay action bit for bit, for exploring (even and odd
+    p_id) and exploiting explorers, across episodes (OU reset per episode,
+    sigma annealing carried over)."""
+    from aido1_amd.env_wrappers import map_tanh_in_place
+    from aido1_amd.explore import OUNoise, act, explore_actions
+    cfg = golden('reference_config.json')
+    for ex in _explorer_fixture():
+        exploit = ex['exploration_type'].startswith('exploiting')
+        ou = OUNoise.from_config(cfg, 1)
+        ids = torch.tensor([ex['p_id']])
+        for epi in ex['episodes']:
+            ou.reset_states()
+            assert float(ou.n_steps[0]) == epi['ou_steps_before']
+            eps = torch.tensor([epi['epsilon']], dtype=torch.float64)
+            for st in epi['steps']:
+                normals = torch.tensor([st['normals']], dtype=torch.float64)
+                out = torch.tensor([st.get('actor_out', [0.0, 0.0])], dtype=torch.float32)
+                if exploit:
+                    ou.sample(normals)          # drawn every step, unused (explorers.py:178)
+                    a = act(out, None, 'tanh')
+                else:
+                    coin = torch.tensor([st['coin']], dtype=torch.float64) if 'coin' in st \
+                        else torch.tensor([1.0], dtype=torch.float64)
+                    uni = torch.tensor([st.get('random', [0.0, 0.0])], dtype=torch.float32)
+                    a = explore_actions(out, ou, eps, ids, cfg, head='tanh',
+                                        draws=(normals, coin, uni))
+                assert a.view(-1).tolist() == [float(np.float32(v)) for v in st['action']], st
+                map_tanh_in_place(a)
+                assert a.view(-1).tolist() == [float(np.float32(v)) for v in st['replay_action']]

@@ -88,7 +88,7 @@ def test_explore_actions_on_gpu(gpu):
     ids = torch.arange(n, device=gpu)
     out = torch.rand(n, 2, device=gpu, generator=g) * 2.4 - 1.2
     a = explore_actions(out, ou, eps, ids, cfg, generator=g, head='tanh')
-    det = act(out, (eps.unsqueeze(1) * ou.x).float(), 'tanh')
+    det = act(out, eps.unsqueeze(1) * ou.x.float().double(), 'tanh')
     same = (a == det).all(1)
     odd = ids % 2 == 1
     assert same[odd].all()                                    # odd: never random
@@ -147,3 +147,57 @@ def test_fused_explore_matches_torch_path(gpu, esr):
         fx.done(done, epb, actb)
         assert torch.equal(a, actb) and torch.equal(epa, epb) and torch.equal(oua.x, oub.x), t
     assert n_rand > 0
+
+
+def test_dt_explore_matches_reference_explorer_loop(gpu):
+    """dt_explore / dt_explore_done (the kernels ActorRollout runs) against the
+    reference's own _explore_episode (tests/golden/explorer.json): the recorded
+    OU normals, coin, random action and actor outputs injected, 64 copies of
+    each explorer; actions, stored (mapped) actions, OU reset at episode ends
+    and the epsilon of the episode counter (cycle schedule) reproduced bit for
+    bit.  The exploiting explorer (explorers.py:182-184) acts with the clipped
+    actor output, as ActorRollout's exploiter block does."""
+    from aido1_amd.explore import FusedExplore, OUNoise
+    from aido1_amd.rollout import CycleEpsilon
+    cfg = golden('reference_config.json')
+    m = 64
+    for ex in golden('explorer.json')['explorers']:
+        exploit = ex['exploration_type'].startswith('exploiting')
+        ou = OUNoise.from_config(cfg, m, device=gpu)
+        ce = CycleEpsilon(cfg, m, gpu)
+        L = ex['cycle_len']
+        ce.cl.fill_(float(L))
+        ce.max_step.fill_(float(L * (cfg['training']['max_episodes'] // L)))
+        ids = torch.full((m,), ex['p_id'], dtype=torch.int64, device=gpu)
+        fx = FusedExplore(cfg, ou, ce, ids, head='tanh')
+        episode = torch.zeros(m, dtype=torch.int64, device=gpu)
+        actions = torch.zeros(m, 2, dtype=torch.float32, device=gpu)
+        for epi in ex['episodes']:
+            episode.fill_(epi['episode_counter'])
+            ou.reset_states()
+            for st in epi['steps']:
+                out = torch.tensor(st.get('actor_out', [0.0, 0.0]), dtype=torch.float32,
+                                   device=gpu).expand(m, 2).contiguous()
+                normals = torch.tensor(st['normals'], dtype=torch.float64,
+                                       device=gpu).expand(m, 2).contiguous()
+                coin = torch.full((m,), st.get('coin', 1.0), dtype=torch.float64, device=gpu)
+                uni = torch.tensor(st.get('random', [0.0, 0.0]), dtype=torch.float32,
+                                   device=gpu).expand(m, 2).contiguous()
+                rc = fx.L.dt_explore(m, out.data_ptr(), normals.data_ptr(),
+                                     coin.data_ptr() if fx.every_second_random else None,
+                                     uni.data_ptr(), ou.x.data_ptr(), ou.n_steps.data_ptr(),
+                                     episode.data_ptr(), ce.cl.data_ptr(), ce.max_step.data_ptr(),
+                                     ids.data_ptr(), fx.params, actions.data_ptr(),
+                                     torch.cuda.current_stream(gpu).cuda_stream)
+                assert rc == 0
+                if exploit:
+                    actions.copy_(out.clamp(-1.0, 1.0))
+                want = torch.tensor(st['action'], dtype=torch.float32, device=gpu)
+                assert torch.equal(actions, want.expand(m, 2)), (ex['p_id'], st)
+                done = torch.full((m,), int(st['done']), dtype=torch.uint8, device=gpu)
+                ep0 = episode.clone()
+                fx.done(done, episode, actions)
+                want = torch.tensor(st['replay_action'], dtype=torch.float32, device=gpu)
+                assert torch.equal(actions, want.expand(m, 2))
+                if st['done']:
+                    assert torch.equal(episode, ep0 + 1) and not ou.x.any()

@@ -1,7 +1,8 @@
 """Diagnostic: where a render_kernel workgroup spends its time (shader-clock
 stamps of the -DDTSIM_STAMPS build, tools/step_stamps.sh; run with
 DTSIM_DIAG_LIB=aido1_amd/libdtsim_stamps.so).  Thread 0 of every workgroup
-stamps after each phase's barrier: 4 entry, 5 background spans + segment
+stamps after each phase's barrier: 16 kernel entry (17 its real time), 4 after the
+prologue (palette, tiles, view), 5 background spans + segment
 projection, 6 span fix-up + markings, 8 uniformity + grey + uniform masks,
 9 Sobel, 10 NMS, 11/13 hysteresis, 14 outputs (grey + masks); [0]/[1] real time at
 entry/exit, [2] HW_ID, [3] XCC_ID, [12] nlist | nweak << 32, [15] visible
@@ -69,12 +70,12 @@ def main():
         L.dt_diag_renstamps(buf.ctypes.data_as(ctypes.c_void_p))
         recs.append(buf[:min(n, 4096)].astype(np.int64).copy())
     b = np.stack(recs)                     # [launch, wg, 16]
-    real = (b[..., 1] - b[..., 0]) / 100.0  # us (100 MHz real-time clock)
-    cyc = b[..., 14] - b[..., 4]
+    real = (b[..., 1] - b[..., 17]) / 100.0  # us (100 MHz real-time clock), from kernel entry
+    cyc = b[..., 14] - b[..., 16]
     clk = np.median(cyc / (real * 1e3))
-    names = ['spans+proj', 'fixup+marks', 'uniformity', 'sobel', 'nms', 'hysteresis',
-             'output']
-    pts = [4, 5, 6, 8, 9, 10, 13, 14]
+    names = ['prologue', 'spans+proj', 'fixup+marks', 'uniformity', 'sobel', 'nms',
+             'hysteresis', 'output']
+    pts = [16, 4, 5, 6, 8, 9, 10, 13, 14]
     seg = np.stack([b[..., pts[i + 1]] - b[..., pts[i]] for i in range(len(names))], -1)
     print('launches %d, workgroups %d; workgroup life median %.2f us (p10 %.2f, p90 %.2f); '
           'shader clock %.2f GHz' % (b.shape[0], b.shape[1], np.median(real),
@@ -93,7 +94,7 @@ def main():
           % (np.median(nl), np.percentile(nl, 90), nl.max(), np.median(nw), nw.max()))
     # launch span and concurrency
     last = b[-1]
-    t0 = last[:, 0].min()
+    t0 = last[:, 17].min()
     span = (last[:, 1].max() - t0) / 100.0
     hw = last[:, 2]
     cu = (hw >> 8) & 0xF
@@ -101,7 +102,7 @@ def main():
     se = (hw >> 13) & 7
     xcc = last[:, 3] & 0xF
     key = ((xcc * 8 + se) * 2 + sh) * 16 + cu
-    ev = np.concatenate([np.stack([last[:, 0], np.ones(len(last))], 1),
+    ev = np.concatenate([np.stack([last[:, 17], np.ones(len(last))], 1),
                          np.stack([last[:, 1], -np.ones(len(last))], 1)])
     ev = ev[np.lexsort((ev[:, 1], ev[:, 0]))]
     conc = np.cumsum(ev[:, 1])

@@ -38,7 +38,7 @@ def main():
         pr = info['td_error'].detach().abs().reshape(-1).double() + 1e-6
         loop.replay.update_priorities(idx, pr)
         ev[5].record()
-        loop.rollout.load_actor(loop.trainer.target_actor)
+        loop._refresh()
         ev[6].record()
         torch.cuda.synchronize()
         for i, k in enumerate(names):
