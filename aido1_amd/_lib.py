@@ -122,7 +122,7 @@ def lib():
             'dt_reset': (ctypes.c_int, [vp, vp, vp]),
             'dt_step': (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp]),
             'dt_step_masked': (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
-            'dt_step_many': (ctypes.c_int, [vp, i32, vp, vp, vp, vp, vp, vp]),
+            'dt_step_many': (ctypes.c_int, [vp, i32, vp, vp, vp, vp, vp, vp, vp]),
             'dt_seed_env': (ctypes.c_int, [vp, i32, u64]),
             'dt_lane_pos': (ctypes.c_int, [vp, vp, vp, vp]),
             'dt_render': (ctypes.c_int, [vp, vp, vp]),

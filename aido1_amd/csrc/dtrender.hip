@@ -937,7 +937,11 @@ __device__ __forceinline__ void write_outputs(const RenderArgs& a, RenderLds& S,
 }
 
 // One env of render_kernel.
-__device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, int e) {
+__device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, int e
+#ifdef DTSIM_EARLY_MARKS
+                                           , const float4 (&mq)[4]
+#endif
+) {
   const int tid = threadIdx.x;
   constexpr int T = kRenderThreads;
   const LineDev& L = a.line;
@@ -952,6 +956,7 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, in
   int32_t* const C = S.cnt;
   const View V = S.view;
   lds_u32* const img = (lds_u32*)S.img;
+#ifndef DTSIM_EARLY_MARKS
   // the marking segments' loads (L2-resident), first used after the background
   float4 mq[4];
   if (mfast) {
@@ -961,6 +966,7 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, in
       mq[k] = sidx < nmark ? a.marks[sidx] : make_float4(-1e9f, -1e9f, -1e9f, -1e9f);
     }  // (mfast: nmark <= kMarkFast <= 4 T)
   }
+#endif
 
   // phase 0a: background.  Tiles are convex and each coordinate is a monotone
   // float function of the column, so along a row the tile index steps
@@ -995,6 +1001,7 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, in
     const int slot = wave_slot1(&C[kNSpan], want);
     if (want) S.qlist[slot] = (uint16_t)q;
   }
+  RENT(18);
   // ... and the markings' projection: every lane projects up to four segments
   // and lists the visible ones (pixel endpoints as int16 x 4; yellow from the
   // bottom of the record area, white from the top)
@@ -1220,9 +1227,25 @@ render_kernel(RenderArgs a) {
   for (int i = tid; i < a.width * a.height; i += kRenderThreads) S.kind[i] = a.kind[i];
   // the camera frame, once per workgroup (wave 1; wave 0 has the palette)
   const int e = blockIdx.x;
+#ifdef DTSIM_EARLY_MARKS
+  float4 mq[4];
+  {
+    const int nmark = a.n_yellow + a.n_white;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int sidx = tid + k * kRenderThreads;
+      mq[k] = nmark <= kMarkFast && sidx < nmark ? a.marks[sidx]
+                                                 : make_float4(-1e9f, -1e9f, -1e9f, -1e9f);
+    }
+  }
+#endif
   if (tid == 64) S.view = view_of(a.x[e], a.z[e], a.angle[e], a.cam_fwd);
   __syncthreads();
-  render_env(a, S, e);
+  render_env(a, S, e
+#ifdef DTSIM_EARLY_MARKS
+             , mq
+#endif
+  );
 }
 
 // LineDetectorHSV on caller BGR images (one workgroup per image, <= 19200 px).

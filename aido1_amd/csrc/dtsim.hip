@@ -43,9 +43,9 @@ __device__ unsigned long long g_rstamps[4096 * 4];  // refill blocks: entry, exi
     const unsigned long long _t = __builtin_amdgcn_s_memrealtime();                 \
     if (threadIdx.x == 0 && blockIdx.x < 64) g_stamps[blockIdx.x * kStamps + (i)] = _t; \
   } while (0)
-// step_pair_kernel: lane 0 of both waves of the first 64 blocks, decisions
-// 0..7: [block][role][decision][point] shader clock; point 15 of decision 0
-// = real time at entry, of decision 1 = real time at exit
+// step_fan_kernel: lane 0 of each wave of the first 64 blocks, decisions 0..7:
+// [block][wave][decision][point] shader clock; point 15 of decision 0 = real
+// time at entry, of decision 1 = real time at exit
 constexpr int kPDec = 8;
 __device__ unsigned long long g_pstamps[64 * 4 * kPDec * 16];
 #define PSTAMP(d, i, v)                                                             \
@@ -136,7 +136,6 @@ __device__ inline void map_action(int mode, float a0, float a1, double& vl, doub
 // A standalone refill (dt_seed, dt_reset: no step lane runs) tags tick - 1,
 // usable by the next launch.
 constexpr int kBlock = 256;        // step and refill blocks (4 waves)
-constexpr int kPairBlock = 128;    // step_pair_kernel launches: one pair of waves
 
 __device__ inline void put_slot(const dt::State& st, int n, int e, uint32_t key, bool ok,
                                 uint32_t tag, double x, double z, double a, double dist,
@@ -247,23 +246,11 @@ struct Decision {
   double lp[4];
 };
 
-// Pair mode (step_pair_kernel): two waves step the same 64 envs; role 0 runs
-// _valid_pose, role 1 get_lane_pos2 and the proximity penalty, and they swap
-// the results through LDS at one barrier per sim step (double-buffered by
-// phase parity).  Both roles then make the same decisions from the same data.
-struct PairX {
-  double d0[2][2][64], d1[2][2][64], pen[2][2][64];  // [pair][parity][lane]
-  uint8_t inl[2][2][64], vp[2][2][64];
-};
-
-template <bool kPair>
 __device__ __forceinline__ void sim_decision(const MapLds& M, const dt::Geo& g, const StepCfg& sc,
                                              bool active, float2 a, double& x, double& z,
                                              double& ang, double& c, double& s,
                                              uint32_t& step_count, uint32_t& env_step,
-                                             Decision& D, PairX* X = nullptr, int role = 0,
-                                             int pair = 0, uint32_t* phase = nullptr,
-                                             int dstamp = -1) {
+                                             Decision& D) {
   double vl, vr;
   map_action(sc.action_mode, a.x, a.y, vl, vr);
   if (sc.clip) {  // Simulator.step: np.clip(action, -1, 1)
@@ -290,13 +277,7 @@ __device__ __forceinline__ void sim_decision(const MapLds& M, const dt::Geo& g, 
   bool lp_fresh = false, lp_inl = false;
   for (int rep = 0; rep < sc.repeat; ++rep) {
     const bool live = !dn;
-    // pair mode: every wave runs every sim step (the exchange barrier); a
-    // finished lane's pose is restored afterwards
-    if (rep == 1) PSTAMPT(dstamp, 12);
-    if (kPair || live) {
-      const double x0 = x, z0 = z, a0 = ang, c0 = c, s0 = s;
-      const uint32_t sc0 = step_count;
-      const unsigned ns0 = nsim;
+    if (live) {
       double speed = 0.0;
       for (int f = 0; f < sc.frame_skip; ++f) {
         const double ox = x, oz = z;
@@ -311,10 +292,8 @@ __device__ __forceinline__ void sim_decision(const MapLds& M, const dt::Geo& g, 
           const double ndz = ddz * cr - ddx * sr;
           x = cx + ndx;
           z = cz + ndz;
-          if (rep == 1) PSTAMPT(dstamp, 13);
           ang = ang + rot;
           sincos(ang, &s, &c);
-          if (rep == 1) PSTAMP(dstamp, 14, __builtin_amdgcn_s_memtime() + (s > 2.0 ? 1 : 0));
         }
         step_count += 1u;
         nsim += 1u;
@@ -324,88 +303,47 @@ __device__ __forceinline__ void sim_decision(const MapLds& M, const dt::Geo& g, 
           speed = sqrt((a1 * a1 + 0.0 * 0.0) + a3 * a3) / g.dt;
         }
       }
-      PSTAMPT(dstamp, 1 + 3 * rep);
-      if (kPair && !live) {
-        x = x0;
-        z = z0;
-        ang = a0;
-        c = c0;
-        s = s0;
-        step_count = sc0;
-        nsim = ns0;
-      }
       // _compute_done_reward (A11).  get_lane_pos2 of the new pose is computed
       // beside _valid_pose (independent float64 chains) and used only if the
       // pose is valid.
       double lq[4] = {0.0, 0.0, 0.0, 0.0};
-      bool lq_inl = false, vp = false;
-      double pen = 0.0;
-      if (!kPair) {
-        lq_inl = dt::lane_pos<false>(M, g, x, z, c, s, lq);
-        vp = dt::valid_pose(M, g, x, z, c, s, 1.0);
-      } else {
-        const int ph = (int)(*phase & 1u), ln = (int)(threadIdx.x & 63u);
-        *phase += 1u;
-        if (role == 0) {
-          vp = dt::valid_pose(M, g, x, z, c, s, 1.0);
-          X->vp[pair][ph][ln] = vp ? 1 : 0;
-        } else {
-          lq_inl = dt::lane_pos<false>(M, g, x, z, c, s, lq);
-          pen = M.n_obj ? dt::proximity_penalty(M, g, x + g.off * c, z + g.off * (-s)) : 0.0;
-          X->inl[pair][ph][ln] = lq_inl ? 1 : 0;
-          X->d0[pair][ph][ln] = lq[0];
-          X->d1[pair][ph][ln] = lq[1];
-          X->pen[pair][ph][ln] = pen;
-        }
-        PSTAMPT(dstamp, 2 + 3 * rep);
-        __syncthreads();
-        PSTAMPT(dstamp, 3 + 3 * rep);
-        if (role == 0) {
-          lq_inl = X->inl[pair][ph][ln] != 0;
-          lq[0] = X->d0[pair][ph][ln];
-          lq[1] = X->d1[pair][ph][ln];
-          pen = X->pen[pair][ph][ln];
-        } else {
-          vp = X->vp[pair][ph][ln] != 0;
-        }
-      }
+      const bool lq_inl = dt::lane_pos<false>(M, g, x, z, c, s, lq);
+      const bool vp = dt::valid_pose(M, g, x, z, c, s, 1.0);
       if (rep == 1) STAMP(12);
-      if (live) {
-        lp_fresh = false;
-        double r;
-        bool sd = false;
-        if (!vp) {
-          r = -1000.0;
-          sd = true;
-        } else if (step_count >= sc.max_steps) {
-          r = 0.0;
-          sd = true;
+      lp_fresh = false;
+      double r;
+      bool sd = false;
+      if (!vp) {
+        r = -1000.0;
+        sd = true;
+      } else if (step_count >= sc.max_steps) {
+        r = 0.0;
+        sd = true;
+      } else {
+        const double sp = sc.speed_measured ? speed : g.robot_speed;
+        // compute_reward: proximity_penalty2 at the actual centre (0 without objects)
+        const double pen =
+            M.n_obj ? dt::proximity_penalty(M, g, x + g.off * c, z + g.off * (-s)) : 0.0;
+        lp_fresh = true;
+        lp_inl = lq_inl;
+        lp[0] = lq[0];
+        lp[1] = lq[1];
+        lp[2] = lq[2];
+        lp[3] = lq[3];
+        if (rep == 1) STAMP(13);
+        if (lp_inl) {
+          const double ad = fabs(lp[0]);
+          r = ((1.0 * sp) * lp[1] + (-10.0) * ad) + 40.0 * pen;
         } else {
-          const double sp = sc.speed_measured ? speed : g.robot_speed;
-          // compute_reward: proximity_penalty2 at the actual centre (0 without objects)
-          if (!kPair)
-            pen = M.n_obj ? dt::proximity_penalty(M, g, x + g.off * c, z + g.off * (-s)) : 0.0;
-          lp_fresh = true;
-          lp_inl = lq_inl;
-          lp[0] = lq[0];
-          lp[1] = lq[1];
-          lp[2] = lq[2];
-          lp[3] = lq[3];
-          if (rep == 1) STAMP(13);
-          if (lp_inl) {
-            const double ad = fabs(lp[0]);
-            r = ((1.0 * sp) * lp[1] + (-10.0) * ad) + 40.0 * pen;
-          } else {
-            r = 40.0 * pen;
-          }
+          r = 40.0 * pen;
         }
-        // BaselineAggregationFunction (aggregation_functions.py:25-32)
-        const double rm = (r == -1000.0) ? -10.0 : (r > 0.0 ? r + 10.0 : r + 4.0);
-        tr = tr + r;
-        trm = trm + rm;
-        env_step += 1u;
-        dn = sd || env_step > sc.max_env_steps;
       }
+      // BaselineAggregationFunction (aggregation_functions.py:25-32)
+      const double rm = (r == -1000.0) ? -10.0 : (r > 0.0 ? r + 10.0 : r + 4.0);
+      tr = tr + r;
+      trm = trm + rm;
+      env_step += 1u;
+      dn = sd || env_step > sc.max_env_steps;
     }
     STAMP(3 + (rep < 3 ? rep : 2));
   }
@@ -508,7 +446,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(dt::State st, dt::MapDev m
     asm volatile("" ::: "memory");  // keep the loads here, ahead of the decision
 
     Decision D;
-    sim_decision<false>(M, g, sc, active, a, x, z, ang, c, s, step_count, env_step, D);
+    sim_decision(M, g, sc, active, a, x, z, ang, c, s, step_count, env_step, D);
 
     // auto-reset (VectorEnv): a finished env takes the reset pose of its next
     // spawn key; a key not ready is computed here, the whole wave on one env
@@ -610,173 +548,6 @@ __global__ __launch_bounds__(kBlock) void step_kernel(dt::State st, dt::MapDev m
   RSTAMP(10);
 }
 
-// dt_step_many in pair mode: the step of §3.1 with two waves per 64 envs
-// (sim_decision<true>): both roles load and update the same state, role 0
-// writes reward/done, counters and state, role 1 the obs.  Every wave runs
-// every decision and sim step, so the block's barriers line up.
-__global__ __launch_bounds__(kBlock) void step_pair_kernel(dt::State st, dt::MapDev md,
-                                                       dt::Geo g, StepCfg sc, int n,
-                                                       uint32_t env_base, int k,
-                                                       const float2* __restrict__ act,
-                                                       double* __restrict__ rew,
-                                                       double* __restrict__ rewm,
-                                                       uint8_t* __restrict__ done_out,
-                                                       float2* __restrict__ obs,
-                                                       int n_step_blocks, uint32_t max_attempts) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  if ((int)blockIdx.x >= n_step_blocks) {  // spawn-ahead refill blocks
-    refill_group(st, md, g, n, max_attempts, env_base,
-                 ((int)blockIdx.x - n_step_blocks) * kRefillEnvs, kRefillEnvs, 0u, lds);
-    return;
-  }
-  __shared__ PairX X;
-  __builtin_amdgcn_s_setprio(3);
-  PSTAMP(0, 15, __builtin_amdgcn_s_memrealtime());
-  PSTAMP(3, 15, __builtin_amdgcn_s_memtime());
-  const int wave = (int)(threadIdx.x >> 6), role = wave & 1, pair = wave >> 1;
-  const int lane = threadIdx.x & 63;
-  const int e = (int)blockIdx.x * (int)(blockDim.x / 2) + pair * 64 + lane;
-  const bool active = e < n;
-  const int ei = active ? e : 0;
-
-  double x = st.x[ei], z = st.z[ei], ang = st.angle[ei];
-  uint32_t step_count = st.step_count[ei], env_step = st.env_step[ei];
-  float2 a = act[ei];
-  const uint32_t tick = st.tick[ei];
-  uint32_t key = 0u;
-  uint64_t seed = 0u, words[dt::kSlots];
-  if (sc.auto_reset) {
-    key = st.episode[ei];
-    seed = st.seed[ei];
-#pragma unroll
-    for (int q = 0; q < dt::kSlots; ++q)
-      words[q] = __hip_atomic_load(st.pre_key + (size_t)q * n + ei, __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
-  }
-  const MapLds M = dt::stage_map(md, lds);
-  const uint32_t key0 = key;
-  uint32_t ready = 0u, failed = 0u;
-  if (sc.auto_reset) {
-#pragma unroll
-    for (int q = 0; q < dt::kSlots; ++q) {
-      const uint32_t kw = (uint32_t)words[q], tag = (uint32_t)(words[q] >> 32);
-      const uint32_t rel = (kw & ~dt::kKeyFailed) - key;
-      if (rel < (uint32_t)dt::kSlots && (int32_t)(tick - tag) > 0) {
-        ready |= 1u << rel;
-        if (kw & dt::kKeyFailed) failed |= 1u << rel;
-      }
-    }
-  }
-
-  double c = 0.0, s = 0.0;
-  sincos(ang, &s, &c);
-  unsigned nsim_t = 0, act_t = 0, resets_t = 0, dones_t = 0;
-  uint32_t phase = 0u;
-  double rp[dt::kSlotRec] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0, 1.0};
-  for (int d = 0; d < k; ++d) {
-    const float2 an = act[(size_t)(d + 1 < k ? d + 1 : d) * n + ei];
-    const uint32_t rel = key - key0;
-    const bool slot_ready = rel < (uint32_t)dt::kSlots && ((ready >> rel) & 1u) != 0u;
-    if (slot_ready) {
-      const size_t sl = key % (uint32_t)dt::kSlots;
-#pragma unroll
-      for (int q = 0; q < dt::kSlotRec; ++q) rp[q] = st.pre[(sl * dt::kSlotRec + q) * (size_t)n + ei];
-    }
-    asm volatile("" ::: "memory");
-
-    Decision D;
-    PSTAMPT(d, 0);
-    sim_decision<true>(M, g, sc, active, a, x, z, ang, c, s, step_count, env_step, D, &X, role,
-                       pair, &phase, d);
-    PSTAMPT(d, 10);
-
-    const bool want_reset = active && D.dn && sc.auto_reset;
-    bool ok = slot_ready && ((failed >> rel) & 1u) == 0u;
-    uint64_t need = __ballot(want_reset && !slot_ready);
-    while (need) {  // wave-uniform; both roles compute the same spawns
-      const int l = __ffsll((unsigned long long)need) - 1;
-      need &= need - 1u;
-      const uint32_t el = (uint32_t)__shfl(ei, l), kl = (uint32_t)__shfl((int)key, l);
-      const uint64_t sd = ((uint64_t)(uint32_t)__shfl((int)(uint32_t)(seed >> 32), l) << 32) |
-                          (uint64_t)(uint32_t)__shfl((int)(uint32_t)seed, l);
-      double sx = 0.0, sz = 0.0, sa = 0.0, slp[2] = {0.0, 0.0};
-      const bool sok = dt::spawn_one(M, g, max_attempts, env_base + el, sd, kl, sx, sz, sa, slp);
-      if (lane == l) {
-        rp[0] = sx;
-        rp[1] = sz;
-        rp[2] = sa;
-        rp[3] = slp[0];
-        rp[4] = slp[1];
-        sincos(sa, &rp[5], &rp[6]);
-        ok = sok;
-      }
-    }
-    const bool reset_now = want_reset && ok;
-    if (role == 0 && want_reset && !ok) atomicOr(st.err, dt::kErrSpawn);
-
-    if (active) {
-      const size_t o = (size_t)d * n + e;
-      if (role == 0) {
-        rew[o] = D.tr;
-        rewm[o] = D.trm;
-        done_out[o] = (uint8_t)D.dn;
-      } else if (obs) {
-        bool inl = false;
-        if (!reset_now) {
-          if (D.lp_fresh) {
-            inl = D.lp_inl;
-            if (inl) dt::finish_angle(g, D.lp);
-          } else {
-            inl = dt::lane_pos<true>(M, g, x, z, c, s, D.lp);
-          }
-        }
-        obs[o] = reset_now ? make_float2((float)rp[3], (float)rp[4])
-                           : (inl ? make_float2((float)D.lp[0], (float)D.lp[3])
-                                  : make_float2(0.0f, 0.0f));
-      }
-    }
-    if (reset_now) {
-      x = rp[0];
-      z = rp[1];
-      ang = rp[2];
-      s = rp[5];  // sincos(ang), made with the slot
-      c = rp[6];
-      step_count = 0u;
-      env_step = 0u;
-      key += 1u;
-    }
-    nsim_t += D.nsim;
-    act_t += active ? 1u : 0u;
-    resets_t += reset_now ? 1u : 0u;
-    dones_t += (active && D.dn) ? 1u : 0u;
-    a = an;
-    PSTAMPT(d, 11);
-  }
-  PSTAMP(1, 15, __builtin_amdgcn_s_memrealtime());
-  PSTAMP(2, 15, __builtin_amdgcn_s_memtime());
-  // role 1 is past its last slot read before role 0 moves the window
-  __syncthreads();
-  if (role != 0) return;
-  const unsigned kk = (unsigned)k;
-  dt::wave_count(st.stats + 0, nsim_t, kk * (unsigned)(sc.repeat * sc.frame_skip));
-  dt::wave_count(st.stats + 1, act_t, kk);
-  dt::wave_count(st.stats + 2, resets_t, kk);
-  dt::wave_count(st.stats + 3, dones_t, kk);
-  if (active) {
-    st.x[e] = x;
-    st.z[e] = z;
-    st.angle[e] = ang;
-    st.step_count[e] = step_count;
-    st.env_step[e] = env_step;
-    __hip_atomic_store(st.tick + e, tick + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (key != key0) {
-      st.episode[e] = key;
-      __hip_atomic_store(st.want + e, key + 1u + after_load(rp[dt::kSlotRec - 1]), __ATOMIC_RELAXED,
-                         __HIP_MEMORY_SCOPE_AGENT);
-    }
-  }
-}
-
 // dt_step_many in fan mode (the default): 16 envs per 256-thread workgroup,
 // each env on one lane quad of each of the block's four waves.  Within a
 // decision the poses of the repeat (<= 3) Simulator steps do not depend on any
@@ -813,6 +584,7 @@ __global__ __launch_bounds__(kFanBlock) __attribute__((amdgpu_waves_per_eu(2, 2)
                                                              double* __restrict__ rewm,
                                                              uint8_t* __restrict__ done_out,
                                                              float2* __restrict__ obs,
+                                                             double* __restrict__ pose_out,
                                                              int n_step_blocks,
                                                              uint32_t max_attempts,
                                                              uint32_t map_lds_offset) {
@@ -1116,6 +888,13 @@ __global__ __launch_bounds__(kFanBlock) __attribute__((amdgpu_waves_per_eu(2, 2)
         obs[o] = reset_now ? make_float2((float)rp[3], (float)rp[4])
                            : (inl_last ? make_float2((float)dist_last, (float)arad_last)
                                        : make_float2(0.0f, 0.0f));
+      } else if (wave == 3 && pose_out) {
+        // the pose the decision ends in (the reset pose after a respawn): what a
+        // render of this decision draws, [d][x | z | angle][env]
+        double* po = pose_out + (size_t)d * 3 * n + e;
+        po[0] = reset_now ? rp[0] : x;
+        po[n] = reset_now ? rp[1] : z;
+        po[2 * (size_t)n] = reset_now ? rp[2] : ang;
       }
     }
     x = reset_now ? rp[0] : x;
@@ -1224,7 +1003,7 @@ extern "C" {
 int dt_diag_stamps(unsigned long long* out) {  // 64 x kStamps shader-clock stamps
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), sizeof(g_stamps)) == hipSuccess ? 0 : -1;
 }
-int dt_diag_pstamps(unsigned long long* out) {  // step_pair_kernel stamps (g_pstamps)
+int dt_diag_pstamps(unsigned long long* out) {  // step_fan_kernel per-wave stamps (g_pstamps)
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_pstamps), sizeof(g_pstamps)) == hipSuccess ? 0 : -1;
 }
 int dt_diag_bstamps(unsigned long long* out) {  // step_fan_kernel per-block stamps
@@ -1539,7 +1318,7 @@ int dt_step(dt_handle* h, const float* actions, double* reward, double* reward_m
 }
 
 int dt_step_many(dt_handle* h, int32_t k, const float* actions, double* reward,
-                 double* reward_mod, uint8_t* done, float* obs, void* stream) {
+                 double* reward_mod, uint8_t* done, float* obs, double* pose, void* stream) {
   if (!h) return DT_E_ARG;
   if (k < 1 || !actions || !reward || !reward_mod || !done) {
     h->err = "dt_step_many: k >= 1, actions, reward, reward_mod and done are required";
@@ -1547,19 +1326,9 @@ int dt_step_many(dt_handle* h, int32_t k, const float* actions, double* reward,
   }
   DevGuard dg(h->device);
   hipStream_t s = (hipStream_t)stream;
-  // DTSIM_STEP_KERNEL: fan (default: 16 envs x 4 waves per workgroup), pair
-  // (two waves per 64 envs) or one (one wave per 64 envs, step_kernel);
-  // DTSIM_STEP_PAIR=0 (older spelling) selects one
-  static const int mode = [] {
-    const char* k = getenv("DTSIM_STEP_KERNEL");
-    const char* p = getenv("DTSIM_STEP_PAIR");
-    if (k && !strcmp(k, "one")) return 0;
-    if (k && !strcmp(k, "pair")) return 1;
-    if (p && p[0] == '0') return 0;
-    return 2;
-  }();
   const int rb = h->sc.auto_reset ? refill_grid(h->n, kRefillEnvs) : 0;
-  if (mode == 2 && h->sc.repeat * h->sc.frame_skip <= kFanSteps && h->sc.frame_skip == 1) {
+  if (h->sc.repeat * h->sc.frame_skip <= kFanSteps && h->sc.frame_skip == 1) {
+    // step_fan_kernel: 16 envs x 4 waves per workgroup
     const int gs = (h->n + kFanEnvs - 1) / kFanEnvs;
     const size_t off = (h->lds_bytes + 15) & ~(size_t)15;
     const size_t slots = (size_t)dt::kSlots * dt::kSlotRec * kFanEnvs * sizeof(double);
@@ -1575,26 +1344,30 @@ int dt_step_many(dt_handle* h, int32_t k, const float* actions, double* reward,
                          off + slots + (size_t)kk * kFanEnvs * sizeof(float2), s, h->st, h->map,
                          h->geo,
                          h->sc, h->n, h->env_base, kk, (const float2*)actions + o, reward + o,
-                         reward_mod + o, done + o, obs ? (float2*)obs + o : (float2*)nullptr, gs,
-                         h->sc.max_spawn_attempts, (uint32_t)off);
+                         reward_mod + o, done + o, obs ? (float2*)obs + o : (float2*)nullptr,
+                         pose ? pose + 3 * o : (double*)nullptr, gs, h->sc.max_spawn_attempts,
+                         (uint32_t)off);
+      HIP_OR_FAIL(h, hipGetLastError());
     }
-  } else if (mode >= 1) {
-    // one pair (two waves, 64 envs) per workgroup: the exchange barriers stay
-    // pair-local; the refill blocks of the launch run with 128 threads too
-    const int gs = (h->n + 63) / 64;
-    hipLaunchKernelGGL(step_pair_kernel, dim3(gs + rb), dim3(kPairBlock), h->lds_bytes, s, h->st,
-                       h->map, h->geo, h->sc, h->n, h->env_base, (int)k,
-                       (const float2*)actions, reward, reward_mod, done, (float2*)obs, gs,
-                       h->sc.max_spawn_attempts);
-  } else {
-    const int gs = (h->n + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL(step_kernel, dim3(gs + rb), dim3(kBlock), h->lds_bytes, s, h->st,
-                       h->map, h->geo, h->sc, h->n, h->env_base, (int)k,
-                       (const float2*)actions, reward, reward_mod, done, (float2*)obs,
-                       (double*)nullptr, (int32_t*)nullptr, gs, h->sc.max_spawn_attempts,
-                       (const uint8_t*)nullptr);
+    return DT_OK;
   }
-  HIP_OR_FAIL(h, hipGetLastError());
+  // the generic path (more than three Simulator steps per decision, or
+  // frame_skip > 1): step_kernel over the k decisions, or one launch per
+  // decision when the poses are asked for
+  const int gs = (h->n + kBlock - 1) / kBlock;
+  for (int d0 = 0; d0 < k; d0 += pose ? 1 : k) {
+    const int kk = pose ? 1 : k;
+    const size_t o = (size_t)d0 * h->n;
+    hipLaunchKernelGGL(step_kernel, dim3(gs + rb), dim3(kBlock), h->lds_bytes, s, h->st,
+                       h->map, h->geo, h->sc, h->n, h->env_base, kk,
+                       (const float2*)actions + o, reward + o, reward_mod + o, done + o,
+                       obs ? (float2*)obs + o : (float2*)nullptr, (double*)nullptr,
+                       (int32_t*)nullptr, gs, h->sc.max_spawn_attempts, (const uint8_t*)nullptr);
+    HIP_OR_FAIL(h, hipGetLastError());
+    if (pose)
+      HIP_OR_FAIL(h, hipMemcpyAsync(pose + 3 * o, h->st.x, 3 * (size_t)h->n * sizeof(double),
+                                    hipMemcpyDeviceToDevice, s));
+  }
   return DT_OK;
 }
 

@@ -163,41 +163,47 @@ class VecEnv:
         self._check(rc, 'dt_step')
         return out
 
-    def step_many_into(self, actions, out):
+    def _check_many(self, actions, out, pose):
+        k = int(actions.shape[0]) if actions.dim() == 3 else 0
+        if actions.dtype != torch.float32 or not actions.is_contiguous() or \
+                actions.device != self.device or k < 1 or tuple(actions.shape[1:]) != (self.n, 2):
+            raise ValueError('actions must be a contiguous float32 [k,%d,2] tensor on %s'
+                             % (self.n, self.device))
+        if out.reward.numel() != k * self.n or (out.obs is not None and
+                                                out.obs.shape[0] != k * self.n):
+            raise ValueError('out must be a StepOutput of k * n = %d entries' % (k * self.n))
+        if pose is not None and (pose.dtype != torch.float64 or not pose.is_contiguous() or
+                                 tuple(pose.shape) != (k, 3, self.n) or
+                                 pose.device != self.device):
+            raise ValueError('pose must be a contiguous float64 [k, 3, %d] tensor on %s'
+                             % (self.n, self.device))
+        return k
+
+    def step_many_into(self, actions, out, pose=None):
         """k decisions in one launch (dt_step_many): actions [k, n, 2] f32 on the
         device, out a StepOutput(k * n, ...) whose entries of decision d are at
         [d * n:(d + 1) * n] (view them as [k, n]); lanepos/tile are not
-        produced.  Same results as k step_into calls."""
-        k = int(actions.shape[0]) if actions.dim() == 3 else 0
-        if actions.dtype != torch.float32 or not actions.is_contiguous() or \
-                actions.device != self.device or k < 1 or tuple(actions.shape[1:]) != (self.n, 2):
-            raise ValueError('actions must be a contiguous float32 [k,%d,2] tensor on %s'
-                             % (self.n, self.device))
-        if out.reward.numel() != k * self.n or (out.obs is not None and
-                                                out.obs.shape[0] != k * self.n):
-            raise ValueError('out must be a StepOutput of k * n = %d entries' % (k * self.n))
+        produced.  pose: optional [k, 3, n] f64, each decision's end pose (what
+        a render of that decision draws: render_into(..., pose=pose[d])).
+        Same results as k step_into calls."""
+        k = self._check_many(actions, out, pose)
         self._check(self._L.dt_step_many(self._h, k, _ptr(actions), _ptr(out.reward),
                                          _ptr(out.reward_mod), _ptr(out.done), _ptr(out.obs),
-                                         self._stream()), 'dt_step_many')
+                                         _ptr(pose), self._stream()), 'dt_step_many')
         return out
 
-    def bind_step_many(self, actions, out):
-        """A zero-argument callable that launches step_many_into(actions, out)
-        on the current stream with its ctypes arguments built once (checked
-        here): the launch then costs one foreign call, for timed loops.  The
-        callable returns dt_step_many's status (0 = DT_OK)."""
-        k = int(actions.shape[0]) if actions.dim() == 3 else 0
-        if actions.dtype != torch.float32 or not actions.is_contiguous() or \
-                actions.device != self.device or k < 1 or tuple(actions.shape[1:]) != (self.n, 2):
-            raise ValueError('actions must be a contiguous float32 [k,%d,2] tensor on %s'
-                             % (self.n, self.device))
-        if out.reward.numel() != k * self.n or (out.obs is not None and
-                                                out.obs.shape[0] != k * self.n):
-            raise ValueError('out must be a StepOutput of k * n = %d entries' % (k * self.n))
+    def bind_step_many(self, actions, out, pose=None, stream=None):
+        """A zero-argument callable that launches step_many_into(actions, out,
+        pose) on `stream` (default: the current stream) with its ctypes
+        arguments built once (checked here): the launch then costs one foreign
+        call, for timed loops.  The callable returns dt_step_many's status
+        (0 = DT_OK)."""
+        k = self._check_many(actions, out, pose)
         fn = self._L.dt_step_many
+        st = ctypes.c_void_p(stream.cuda_stream) if stream is not None else self._stream()
         args = (self._h, k, _ptr(actions), _ptr(out.reward), _ptr(out.reward_mod),
-                _ptr(out.done), _ptr(out.obs), self._stream())
-        keep = (actions, out)
+                _ptr(out.done), _ptr(out.obs), _ptr(pose), st)
+        keep = (actions, out, pose, stream)
 
         def launch():
             keep  # noqa: B018 (the tensors stay alive with the callable)

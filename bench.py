@@ -99,14 +99,15 @@ def parse(argv=None):
                    help='train: run each update beside the next rollout (side stream); '
                         'measured slower, DESIGN 3.8')
     p.add_argument('--many', type=int, default=20,
-                   help='lane config: most decisions per dt_step_many launch; the K timed '
-                        'decisions are split into ceil(K / many) equal launches')
+                   help='most decisions per dt_step_many launch (lane config, and the render '
+                        'config\'s many mode); K decisions are split into ceil(K / many) '
+                        'equal launches')
     p.add_argument('--graph', action='store_true',
                    help='lane config: replay the timed launches as one captured HIP graph '
                         '(default: prebound eager dt_step_many calls)')
     p.add_argument('--no-parity', action='store_true', help='skip the oracle parity pass')
-    p.add_argument('--obs-mode', default='pipe', choices=['pipe', 'pipe-lo', 'serial'],
-                   help='render: step/render stream arrangement (ObsLoop)')
+    p.add_argument('--obs-mode', default='many', choices=['many', 'serial', 'pipe'],
+                   help='render: how the steps are launched (ObsLoop)')
     p.add_argument('--no-lane', action='store_true', help='render: skip the config-2 sub-record')
     p.add_argument('--lane-steps', type=int, default=320,
                    help='render: decisions timed by the config-2 sub-record')
@@ -441,20 +442,25 @@ STEP_PARITY_KEYS = ['pose_max_abs_err', 'reward_max_abs_err', 'reward_mod_max_ab
 
 # ---- config 3: the headline line --------------------------------------------------------
 class ObsLoop:
-    """Per decision: dt_step -> dt_copy_pose snapshot (step stream), dt_render of
-    the snapshot (render stream, fresh = the step's done flags).  Step d + 1
-    waits only for render d - 1 (the snapshot buffer it overwrites).
-    mode 'serial': step and render of each decision on one stream, no snapshot;
-    'pipe': the step stream has the higher priority; 'pipe-lo': the render's."""
+    """The decisions of BASELINE configs[2], each a step of every env and the
+    render of the pose it ends in (fresh = the step's done flags).  Modes:
+      'many'   (default) the actions are known ahead (random), so dt_step_many
+               steps a chunk of decisions in one launch (the fan kernel, 4.5 us
+               a decision) and writes each decision's end pose; then the
+               chunk's renders, each of its decision's pose and done flags.
+      'serial' dt_step then dt_render of each decision on one stream.
+      'pipe'   dt_step + dt_copy_pose on a high-priority stream, dt_render of
+               the snapshot on another: step d + 1 beside render d.
+    Every mode computes the same frames, masks and step outputs."""
 
-    def __init__(self, env, ro, torch, mode='pipe'):
+    def __init__(self, env, ro, torch, mode='many', chunk=20):
         self.env, self.ro, self.torch, self.mode = env, ro, torch, mode
         lo, hi = torch.cuda.Stream.priority_range()
         self.s_step = torch.cuda.Stream(env.device, priority=hi if mode == 'pipe' else lo)
-        self.s_rend = self.s_step if mode == 'serial' else \
-            torch.cuda.Stream(env.device, priority=hi if mode == 'pipe-lo' else lo)
-        self.pose = [torch.empty(3, env.n, dtype=torch.float64, device=env.device)
-                     for _ in range(2)]
+        self.s_rend = torch.cuda.Stream(env.device) if mode == 'pipe' else self.s_step
+        self.chunk = max(1, min(int(chunk), 64))
+        np_ = self.chunk if mode == 'many' else 2
+        self.pose = torch.empty(np_, 3, env.n, dtype=torch.float64, device=env.device)
 
     def events(self, k):
         E = self.torch.cuda.Event
@@ -462,40 +468,53 @@ class ObsLoop:
                 [(E(enable_timing=True), E(enable_timing=True)) for _ in range(k)],
                 [(E(enable_timing=True), E(enable_timing=True)) for _ in range(k)])
 
-    def bind(self, actions, outs):
-        """The per-decision foreign calls, built and checked before the timed
-        region (the ring slots are taken here, in decision order)."""
+    def bind(self, actions, out):
+        """The foreign calls of len(actions) decisions writing `out` (a
+        StepOutput of k * n entries), built and checked before the timed region
+        (the ring slots are taken here, in decision order)."""
         from aido1_amd.render import bind_render
-        env, serial = self.env, self.mode == 'serial'
-        calls = []
-        for d in range(len(outs)):
+        env, n, k = self.env, self.env.n, int(actions.shape[0])
+        groups = []
+        if self.mode == 'many':
+            for a, b in _bounds(split_even(k, self.chunk)):
+                pose = self.pose[:b - a]
+                step = env.bind_step_many(actions[a:b], _Slice(out, a, b, n), pose=pose,
+                                          stream=self.s_step)
+                rend = [bind_render(env, self.ro, self.s_rend, fresh=out.done[d * n:(d + 1) * n],
+                                    pose=pose[d - a]) for d in range(a, b)]
+                groups.append((a, step, None, rend))
+            return groups
+        serial = self.mode == 'serial'
+        for d in range(k):
+            o = _Slice(out, d, d + 1, n)
             pose = None if serial else self.pose[d % 2]
-            calls.append((env.bind_step(actions[d], outs[d], self.s_step),
-                          None if serial else env.bind_copy_pose(pose, self.s_step),
-                          bind_render(env, self.ro, self.s_rend, fresh=outs[d].done, pose=pose)))
-        return calls
+            groups.append((d, env.bind_step(actions[d], o, self.s_step),
+                           None if serial else env.bind_copy_pose(pose, self.s_step),
+                           [bind_render(env, self.ro, self.s_rend, fresh=o.done, pose=pose)]))
+        return groups
 
-    def run(self, calls, ev):
-        """Launch the bound decisions; returns the calls' status codes."""
+    def run(self, groups, ev):
+        """Launch the bound decisions; returns the OR of the calls' status codes."""
         torch, env = self.torch, self.env
         ev_step, t_rend, t_step = ev
         ss, sr = self.s_step, self.s_rend
         ss.wait_stream(torch.cuda.current_stream(env.device))
-        serial = self.mode == 'serial'
         rcs = 0
-        for d, (step, copy, rend) in enumerate(calls):
-            if d >= 2 and not serial:
-                ss.wait_event(t_rend[d - 2][1])
-            t_step[d][0].record(ss)
+        for d0, step, copy, rends in groups:
+            if self.mode == 'pipe' and d0 >= 2:
+                ss.wait_event(t_rend[d0 - 2][1])
+            t_step[d0][0].record(ss)
             rcs |= step()
-            t_step[d][1].record(ss)
-            if not serial:
+            t_step[d0][1].record(ss)
+            if copy is not None:
                 rcs |= copy()
-                ev_step[d].record(ss)
-                sr.wait_event(ev_step[d])
-            t_rend[d][0].record(sr)
-            rcs |= rend()
-            t_rend[d][1].record(sr)
+            if sr is not ss:
+                ev_step[d0].record(ss)
+                sr.wait_event(ev_step[d0])
+            for i, rend in enumerate(rends):
+                t_rend[d0 + i][0].record(sr)
+                rcs |= rend()
+                t_rend[d0 + i][1].record(sr)
         torch.cuda.current_stream(env.device).wait_stream(sr)
         return rcs
 
@@ -513,18 +532,17 @@ def bench_obs(args, ctx):
     g.manual_seed(args.seed + 7919 * rank)
     actions = torch.rand(W + K, n, 2, generator=g, device=dev, dtype=torch.float32)
     ro = RenderOutput(n, dev)          # 3-slot grey ring (Transformer stack) + 4 masks
-    loop = ObsLoop(env, ro, torch, args.obs_mode)
+    loop = ObsLoop(env, ro, torch, args.obs_mode, args.many)
     env.reset()
-    wouts = [StepOutput(n, dev, lanepos=False, tile=False) for _ in range(2)]
-    if loop.run(loop.bind(actions[:W], [wouts[d % 2] for d in range(W)]), loop.events(W)):
+    wout = StepOutput(max(W, 1) * n, dev, lanepos=False, tile=False)
+    if W and loop.run(loop.bind(actions[:W], wout), loop.events(W)):
         raise RuntimeError('a warm-up decision failed')
     ctx.sync()
     start = env.get_state()
     env.stats(reset=True)
     out = StepOutput(K * n, dev, lanepos=False, tile=False)
-    outs = [_Slice(out, d, d + 1, n) for d in range(K)]
     ev = loop.events(K)
-    calls = loop.bind(actions[W:], outs)
+    calls = loop.bind(actions[W:], out)
     ctx.barrier()
     ctx.sync()
     t0 = time.perf_counter()
@@ -539,7 +557,8 @@ def bench_obs(args, ctx):
     env.check()
     tot, tmax, per = rank_report(ctx, [st['sim_steps'], st['decisions'], st['resets']], elapsed)
     rend_ms = [a.elapsed_time(b) for a, b in ev[1]]
-    step_ms = [a.elapsed_time(b) for a, b in ev[2]]
+    starts = [g[0] for g in calls]
+    step_ms = [ev[2][d][0].elapsed_time(ev[2][d][1]) for d in starts]
 
     parity = None
     if not args.no_parity:
@@ -567,10 +586,15 @@ def bench_obs(args, ctx):
                        'map': args.map, 'envs_per_gpu': n, 'global_envs': n * ctx.world,
                        'repeat_actions': 3, 'auto_reset': True,
                        'actions': 'U[0,1)^2 wheel velocities, resident in HBM',
-                       'launch': ('per decision: dt_step + dt_copy_pose (step stream), dt_render '
-                                  'of the snapshot (render stream); step d+1 beside render d (%s)'
-                                  % args.obs_mode) if args.obs_mode != 'serial' else
-                       'per decision: dt_step then dt_render on one stream',
+                       'launch': {
+                           'many': 'dt_step_many over chunks of <= %d decisions (each '
+                                   'decision\'s end pose written), then each decision\'s '
+                                   'dt_render of that pose with its done flags as fresh; one '
+                                   'stream, prebound calls' % args.many,
+                           'serial': 'per decision: dt_step then dt_render, one stream, prebound',
+                           'pipe': 'per decision: dt_step + dt_copy_pose (high-priority stream), '
+                                   'dt_render of the snapshot (render stream), prebound'
+                       }[args.obs_mode],
                        'parallelism': 'env shards (%d x %d), no collective' % (ctx.world, n)},
             'counts': {'env_steps': tot[0], 'decisions': tot[1], 'resets': tot[2],
                        'elapsed_s': tmax},
@@ -591,7 +615,8 @@ def bench_obs(args, ctx):
                                               'ring refill per respawned env (%.1f per launch)'
                                               % fresh_per_launch,
                          'timing': 'HIP events on the render stream around each dt_render'},
-            'step_kernel_ms': float(np.mean(step_ms)),
+            'step_launch_ms': float(np.mean(step_ms)),
+            'step_launches': len(starts),
             'host_enqueue_ms_per_step': t_host / K * 1e3,
             'config2': lane,
         }

@@ -31,7 +31,8 @@ extern "C" {
 
 #define DT_ABI_VERSION 4  /* 2: curves per tile vary (curve_start), intersections;
                              3: static objects in dt_map, safety_rad_mult;
-                             4: dt_render_io.pose / list_cap, dt_copy_pose */
+                             4: dt_render_io.pose / list_cap, dt_copy_pose,
+                                dt_step_many pose output */
 
 /* error codes */
 #define DT_OK 0
@@ -189,15 +190,17 @@ int dt_step_masked(dt_handle* h, const uint8_t* mask, const float* actions, doub
                    void* stream);
 
 /* k consecutive dt_step calls in one launch (the spawn-ahead refill blocks run in
- * the same grid):
- * the same results as k dt_step calls over actions[d], with the outputs of
- * decision d at [d * n + env].  The explorer's rollout loop
+ * the same grid): the same results as k dt_step calls over actions[d], with the
+ * outputs of decision d at [d * n + env].  The explorer's rollout loop
  * (training/explorers.py) over k actions known ahead, e.g. random ones.
  *   actions    device [k,n,2] f32                                          required
  *   reward, reward_mod  device [k,n] f64; done device [k,n] u8             required
- *   obs        device [k,n,2] f32, as dt_step's                            nullable */
+ *   obs        device [k,n,2] f32, as dt_step's                            nullable
+ *   pose       device [k,3,n] f64: the pose each decision ends in (x, z, angle
+ *              planes; the reset pose after a respawn), i.e. what dt_render of
+ *              that decision draws (dt_render_io.pose = pose + 3 n d)  nullable */
 int dt_step_many(dt_handle* h, int32_t k, const float* actions, double* reward,
-                 double* reward_mod, uint8_t* done, float* obs, void* stream);
+                 double* reward_mod, uint8_t* done, float* obs, double* pose, void* stream);
 
 /* Replaces: Simulator.get_lane_pos2(cur_pos, cur_angle) for every env (no step).
  * lanepos device [n,4] f64 (NaN if NotInLane); tile device [n] i32 (nullable). */

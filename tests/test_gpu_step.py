@@ -258,8 +258,8 @@ def test_step_many_matches_oracle(gpu, k, map_name):
     """dt_step_many: k decisions per launch == k oracle steps, per decision;
     three launches back to back, then an eager dt_step continues the state.
     Envs finishing more often than their ready slots cover spawn inline.
-    (The default fan kernel, step_fan_kernel; test_step_many_other_kernels
-    covers step_pair_kernel and the one-wave step_kernel.)"""
+    (The fan kernel, step_fan_kernel; test_step_many_generic_path covers
+    step_kernel over k decisions.)"""
     from aido1_amd.vec_env import StepOutput
     n = 4096
     env, ob = make_pair(n, map_name=map_name)
@@ -299,22 +299,62 @@ def test_step_many_matches_oracle(gpu, k, map_name):
     env.check()
 
 
-@pytest.mark.parametrize('kernel', ['pair', 'one'])
-def test_step_many_other_kernels(gpu, kernel):
-    """DTSIM_STEP_KERNEL=pair (step_pair_kernel: two waves per 64 envs) and
-    =one (step_kernel over k decisions), each in a child process (the setting
-    is read once per process): the same check at k = 16 (loop_empty), 12
-    (loop_obstacles, where the pair kernel splits proximity_penalty across its
-    two waves), 30 (zigzag) and 64 (small_loop)."""
-    import os
-    import subprocess
-    import sys
-    code = ('import sys, pytest; sys.exit(pytest.main(["-x", "-q", "-m", "gpu", "-p", '
-            '"no:cacheprovider", "-k", "step_many_matches_oracle and (16-loop_empty or 12-loop_obstacles or '
-            '30-zigzag or 64-small_loop)", '
-            '"%s"]))' % os.path.abspath(__file__))
-    env = dict(os.environ, DTSIM_STEP_KERNEL=kernel)
-    r = subprocess.run([sys.executable, '-c', code], env=env, cwd=os.path.dirname(__file__),
-                       capture_output=True, text=True, timeout=300)
-    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
-    assert '4 passed' in r.stdout, r.stdout[-2000:]
+@pytest.mark.parametrize('k,repeat,map_name', [(16, 4, 'loop_empty'), (9, 5, 'loop_obstacles')])
+def test_step_many_generic_path(gpu, k, repeat, map_name):
+    """More Simulator steps per decision than the fan kernel holds (repeat 4-5):
+    dt_step_many runs step_kernel over the k decisions; same check against the
+    oracle, with and without the per-decision poses (which then take one
+    launch per decision)."""
+    from aido1_amd.vec_env import StepOutput
+    n = 2048
+    for with_pose in (False, True):
+        env, ob = make_pair(n, map_name=map_name, repeat_actions=repeat)
+        env.reset()
+        ob.reset()
+        rng = np.random.default_rng(37)
+        out = StepOutput(k * n, gpu, lanepos=False, tile=False)
+        pose = torch.empty(k, 3, n, dtype=torch.float64, device=gpu) if with_pose else None
+        for _ in range(2):
+            a = rng.uniform(0, 1, (k, n, 2)).astype(np.float32)
+            env.step_many_into(torch.from_numpy(a).to(gpu), out, pose=pose)
+            torch.cuda.synchronize()
+            rew = out.reward.view(k, n).cpu().numpy()
+            done = out.done.view(k, n).cpu().numpy()
+            for d in range(k):
+                ref = ob.step(a[d])
+                assert np.array_equal(done[d], ref['done']), d
+                assert np.max(np.abs(rew[d] - ref['reward'])) <= TOL_TIGHT, d
+                if with_pose:
+                    o = ob.state()
+                    p = pose[d].cpu().numpy()
+                    assert np.max(np.abs(p[0] - o['x'])) <= TOL_TIGHT
+                    assert np.max(np.abs(p[2] - o['angle'])) <= TOL_TIGHT
+            compare_state(env, ob)
+        env.check()
+
+
+@pytest.mark.parametrize('k', [1, 20, 64])
+def test_step_many_pose_output(gpu, k):
+    """dt_step_many's per-decision poses (fan kernel) == the oracle's pose after
+    each decision (the reset pose after a respawn), i.e. what a render of that
+    decision draws."""
+    from aido1_amd.vec_env import StepOutput
+    n = 4096
+    env, ob = make_pair(n)
+    env.reset()
+    ob.reset()
+    rng = np.random.default_rng(41)
+    out = StepOutput(k * n, gpu, lanepos=False, tile=False)
+    pose = torch.empty(k, 3, n, dtype=torch.float64, device=gpu)
+    for _ in range(2):
+        a = rng.uniform(0, 1, (k, n, 2)).astype(np.float32)
+        env.step_many_into(torch.from_numpy(a).to(gpu), out, pose=pose)
+        torch.cuda.synchronize()
+        p = pose.cpu().numpy()
+        for d in range(k):
+            ob.step(a[d])
+            o = ob.state()
+            for j, key in enumerate(('x', 'z', 'angle')):
+                assert np.max(np.abs(p[d, j] - o[key])) <= TOL_TIGHT, (d, key)
+        compare_state(env, ob)
+    env.check()

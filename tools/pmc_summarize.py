@@ -22,7 +22,6 @@ ROUND = sys.argv[1] if len(sys.argv) > 1 else 'r02'
 OUT = 'gpurun_out'
 # label -> (bench config whose PMC passes hold it, kernel-name needles)
 KERNELS = {'step_fan_kernel': ('lane', ['step_fan_kernel']),
-           'step_pair_kernel': ('lane', ['step_pair_kernel']),
            'step_kernel': ('lane', ['step_kernel']),
            'render_kernel': ('lane', ['render_kernel'])}
 WIDE_READS = set()      # kernels whose reads are 16-B-per-lane streams

@@ -58,10 +58,11 @@ def main():
               % (name, m.mean(), m.min(), m.max(), 100 * byt / (m.mean() * 1e-3) / 8e12))
     # host enqueue rate of bench.py's loop
     import bench
-    for mode in ('serial', 'pipe'):
+    big = StepOutput(K * n, dev, lanepos=False, tile=False)
+    for mode in ('many', 'serial', 'pipe'):
         loop = bench.ObsLoop(env, ro, torch, mode)
         ev = loop.events(K)
-        calls = loop.bind(acts[10:10 + K], outs[10:10 + K])
+        calls = loop.bind(acts[10:10 + K], big)
         torch.cuda.synchronize()
         t0 = time.perf_counter()
         loop.run(calls, ev)

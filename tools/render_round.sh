@@ -7,11 +7,11 @@ timeout -k 10 300 python -u -m pytest tests/test_gpu_render.py -x -q --timeout 1
 tail -1 gpurun_out/rr_pytest.log
 timeout -k 10 120 python tools/render_bench.py || exit 1
 DTSIM_DIAG_LIB=$PWD/aido1_amd/libdtsim_stamps.so timeout -k 10 120 python tools/render_stamps.py || exit 1
-for m in pipe serial; do
+for m in many serial pipe; do
   timeout -k 10 300 python bench.py --steps 100 --warmup 10 --cpu-steps 0 --no-lane --obs-mode $m > gpurun_out/rr_$m.json 2> gpurun_out/rr_$m.err || { tail -30 gpurun_out/rr_$m.err; exit 1; }
   python -c "
 import json; d=json.load(open('gpurun_out/rr_$m.json'))
-print('$m', 'value %.4g' % d['value'], 'ms/step %.4f' % d['ms_per_step'], 'render ms %.4f' % d['roofline']['avg_kernel_ms'], 'frac %.3f' % d['roofline']['frac'], 'step ms %.4f' % d['step_kernel_ms'], 'host %.4f' % d['host_enqueue_ms_per_step'], 'parity', d['parity']['ok'])"
+print('$m', 'value %.4g' % d['value'], 'ms/step %.4f' % d['ms_per_step'], 'render ms %.4f' % d['roofline']['avg_kernel_ms'], 'frac %.3f' % d['roofline']['frac'], 'step ms/launch %.4f' % d['step_launch_ms'], 'host %.4f' % d['host_enqueue_ms_per_step'], 'parity', d['parity']['ok'])"
 done
 TIME_ONLY=1 timeout -k 10 -s KILL 120 rocprofv3 --pmc WRITE_SIZE --output-format csv -d gpurun_out/rr_w -o run -- python3 tools/render_stamps.py > /dev/null 2>&1 || exit 1
 python3 -c "

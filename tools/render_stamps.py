@@ -85,6 +85,8 @@ def main():
         print('  %-13s median %7.0f cyc  mean %7.0f  p90 %7.0f  (%4.1f %% of the median life)'
               % (nm, np.median(seg[..., i]), seg[..., i].mean(), np.percentile(seg[..., i], 90),
                  100 * np.median(seg[..., i]) / tot))
+    print('  spans+proj split: spans %.0f, projection + lists %.0f cyc (medians)'
+          % (np.median(b[..., 18] - b[..., 4]), np.median(b[..., 5] - b[..., 18])))
     segs = b[..., 15] & 0xFFFFFFFF
     vis = (segs & 0xFFFF) + (segs >> 16)
     print('  visible segments median %d (p90 %d)' % (np.median(vis), np.percentile(vis, 90)))
