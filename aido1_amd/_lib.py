@@ -21,13 +21,10 @@ SOURCES = ['dtsim.hip', 'dtrender.hip', 'dtreplay.hip', 'dtactor.hip', 'dtconv.h
 HEADERS = ['dtsim_common.h', 'dtrender.h']
 PUBLIC_HEADERS = ['dtsim.h', 'dtreplay.h', 'dtactor.h']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
-ABI_VERSION = 4
+ABI_VERSION = 5
 
-# -pragma-unroll-threshold: dt_conv12's step loops must unroll fully (its conv1
-# outputs are register arrays indexed by step) past clang's default limit
 HIP_FLAGS = ['--offload-arch=gfx950', '-O3', '-fPIC', '-shared', '-std=c++17',
-             '-ffp-contract=off', '-munsafe-fp-atomics', '-mllvm',
-             '-pragma-unroll-threshold=1000000']
+             '-ffp-contract=off', '-munsafe-fp-atomics']
 
 
 class DtError(RuntimeError):
@@ -148,20 +145,18 @@ def lib():
             'dt_per_update': (ctypes.c_int, [vp, i32, vp, vp, vp]),
             'dt_per_read': (ctypes.c_int, [vp, vp, vp, vp, vp]),
             'dt_per_check': (ctypes.c_int, [vp]),
+            'dt_frame_add': (ctypes.c_int, [i32, i64, vp, i64, vp, i32, vp, vp, i32, vp, vp, vp]),
             # dtactor.h
             'dt_sample_norm': (ctypes.c_int, [vp, vp, i32, i32, i32, vp, vp, ctypes.c_float,
                                               ctypes.c_float, i32, vp]),
             'dt_conv1': (ctypes.c_int, [vp, i32, i32, ctypes.POINTER(i32), vp, vp, vp, vp,
                                         ctypes.c_float, vp]),
             'dt_conv1_norm': (ctypes.c_int, [vp, i32, vp, vp, vp, ctypes.c_float, vp]),
-            'dt_conv1_bands': (i32, []),
             'dt_conv32': (ctypes.c_int, [i32, i32, vp, vp, vp, vp, vp, vp, ctypes.c_float, vp,
                                          vp, vp, vp, ctypes.c_float, ctypes.c_float, vp]),
             'dt_explore': (ctypes.c_int, [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                           ctypes.POINTER(DtExploreParams), vp, vp]),
             'dt_explore_done': (ctypes.c_int, [i32, vp, vp, vp, vp, i32, vp]),
-            'dt_conv12': (ctypes.c_int, [vp, i32, i32, ctypes.POINTER(i32), vp, vp, vp, vp,
-                                         ctypes.c_float, vp, vp, vp, vp, ctypes.c_float, vp]),
         }
         for name, (res, args) in sig.items():
             if not hasattr(L, name):

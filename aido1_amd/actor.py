@@ -18,7 +18,6 @@ zero-copy: the first conv's input channels are permuted to the ring's slot
 order instead of gathering the Transformer stack.
 """
 import copy
-import os
 
 import torch
 import torch.nn as nn
@@ -276,28 +275,22 @@ class FusedActor(nn.Module):
         self.register_buffer('w0frag', torch.zeros(16, 64, 8, dtype=torch.float16, device=dev))
         self.register_buffer('wfrag', torch.zeros(3, 32, 64, 8, dtype=torch.float16, device=dev))
         self.register_buffer('bf', torch.zeros(4, 32, device=dev))
-        # DTCONV_FUSED12=1: conv1 + bn1 + conv2 as one kernel (dt_conv12, the
-        # conv1 activation kept on chip); measured slower than dt_conv1 +
-        # dt_conv32, so off by default.  DTCONV_CHUNK: samples
-        # per pass through the chain (0: the whole batch; smaller passes, meant
-        # to keep the conv1 activation in the MALL, measured slower too)
-        self.fused12 = os.environ.get('DTCONV_FUSED12', '0') == '1'
-        self.chunk = int(os.environ.get('DTCONV_CHUNK', '0'))
         self.refresh(actor)
 
     @torch.no_grad()
     def refresh(self, actor):
         convs, bns, lin1, lin2 = actor.layers()
         if self.mode == 'reference':
-            for i, (conv, bn) in enumerate(zip(convs, bns)):
-                self.w[i].copy_(conv.weight)
-                self.b[i].copy_(conv.bias)
-                self.gamma[i].copy_(bn.weight)
-                self.beta[i].copy_(bn.bias)
-            self.w1.copy_(lin1.weight)
-            self.b1.copy_(lin1.bias)
+            ws = [c.weight for c in convs]
+            bs = [c.bias for c in convs]
+            torch._foreach_copy_(
+                list(self.w) + list(self.b) + list(self.gamma) + list(self.beta) +
+                [self.w1, self.b1, self.w2, self.b2],
+                ws + bs + [bn.weight for bn in bns] + [bn.bias for bn in bns] +
+                [lin1.weight, lin1.bias, lin2.weight, lin2.bias])
         else:
             scale = shift = None
+            ws, bs = [], []
             for i, (conv, bn) in enumerate(zip(convs, bns)):
                 w = conv.weight.detach().double()
                 b = conv.bias.detach().double()
@@ -306,6 +299,8 @@ class FusedActor(nn.Module):
                     w = w * scale.view(1, -1, 1, 1)
                 self.w[i].copy_(w)
                 self.b[i].copy_(b)
+                ws.append(w)
+                bs.append(b)
                 scale = bn.weight.detach().double() / torch.sqrt(
                     bn.running_var.detach().double() + bn.eps)
                 shift = bn.bias.detach().double() - bn.running_mean.detach().double() * scale
@@ -315,13 +310,24 @@ class FusedActor(nn.Module):
             t_flat = shift.repeat_interleave(FLAT // shift.numel())
             self.w1.copy_(w1 * s_flat.view(1, -1))
             self.b1.copy_(b1 + w1 @ t_flat)
-        self.w2.copy_(lin2.weight)
-        self.b2.copy_(lin2.bias)
-        self.w0frag.copy_(conv1_fragments(self.w[0].float()))
+            self.w2.copy_(lin2.weight)
+            self.b2.copy_(lin2.bias)
+        self._fragments(ws, bs)
+
+    def _fragments(self, ws, bs):
+        """The MFMA A fragments (fp16) and f32 biases of the four convs for
+        dt_conv1 / dt_conv32, from weights of any float dtype and memory
+        format: one gather a layer through index maps built once (the layouts
+        of conv1_fragments / conv32_fragments)."""
+        dev = self.w0frag.device
+        if getattr(self, '_fidx', None) is None or self._fidx[0].device != dev:
+            self._fidx = (conv1_fragment_index(dev), conv32_fragment_index(dev))
+            self._w0pad = torch.zeros(32 * 3 * 64 + 1, device=dev)   # + the zero channel's slot
+        self._w0pad[:-1].view(32, 3, 8, 8).copy_(ws[0])
+        self.w0frag.view(-1).copy_(torch.take(self._w0pad, self._fidx[0]))
         for i in range(1, 4):
-            self.wfrag[i - 1].copy_(conv32_fragments(self.w[i].float()))
-        for i in range(4):
-            self.bf[i].copy_(self.b[i].float())
+            self.wfrag[i - 1].view(-1).copy_(torch.take(ws[i], self._fidx[1]))
+        torch._foreach_copy_(list(self.bf.unbind(0)), list(bs))
 
     def _lrelu_sample_norm(self, x, i):
         """LeakyReLU then BatchNorm2d in train mode on a batch of one, for every
@@ -358,68 +364,50 @@ class FusedActor(nn.Module):
         n, slots = ring.shape[0], ring.shape[1]
         dev = ring.device
         flat = torch.empty(n, FLAT, dtype=torch.float16, device=dev)
-        chunk = n if self.chunk <= 0 else max(1, min(n, self.chunk))
-        bufs = self._chunk_buffers(chunk, dev)
-        rc = 0
-        for c0 in range(0, n, chunk):
-            c = min(chunk, n - c0)
-            rc = self._convs_chunk(L, ring[c0:c0 + c], slots, order, flat[c0:c0 + c], bufs)
-            if rc != 0:
-                break
+        rc = self._convs(L, ring, slots, order, flat, self._conv_buffers(n, dev))
         if rc != 0:
-            raise _lib.DtError('dt_conv1 / dt_conv12 / dt_conv32 failed (%d)' % rc)
+            raise _lib.DtError('dt_conv1 / dt_conv32 failed (%d)' % rc)
         return flat
 
-    def _chunk_buffers(self, chunk, dev):
-        key = (chunk, dev, self.mode, self.fused12)
+    def _conv_buffers(self, n, dev):
+        """The intermediate activations (fp16 NHWC) and, in reference mode, the
+        per-sample BatchNorm statistics [n, 32, 2] of conv1..conv3."""
+        key = (n, dev, self.mode)
         if getattr(self, '_bufs_key', None) != key:
             f16 = torch.float16
             ref = self.mode == 'reference'
             self._bufs = {
-                'y1': None if self.fused12 else torch.empty(chunk, 57, 77, 32, dtype=f16, device=dev),
-                'p1': torch.empty(chunk, _lib_bands(), 32, 2, device=dev)
-                if (ref and not self.fused12) else None,
-                'y2': torch.empty(chunk, 27, 37, 32, dtype=f16, device=dev),
-                'y3': torch.empty(chunk, 12, 17, 32, dtype=f16, device=dev),
-                'p2': torch.empty(chunk, 1, 32, 2, device=dev) if ref else None,
-                'p3': torch.empty(chunk, 1, 32, 2, device=dev) if ref else None}
+                'y1': torch.empty(n, 57, 77, 32, dtype=f16, device=dev),
+                'y2': torch.empty(n, 27, 37, 32, dtype=f16, device=dev),
+                'y3': torch.empty(n, 12, 17, 32, dtype=f16, device=dev),
+                'p1': torch.empty(n, 32, 2, device=dev) if ref else None,
+                'p2': torch.empty(n, 32, 2, device=dev) if ref else None,
+                'p3': torch.empty(n, 32, 2, device=dev) if ref else None}
             self._bufs_key = key
         return self._bufs
 
-    def _convs_chunk(self, L, ring, slots, order, flat, B):
+    def _convs(self, L, ring, slots, order, flat, B):
         import ctypes
         n = ring.shape[0]
         ref = self.mode == 'reference'
         stream = torch.cuda.current_stream(ring.device).cuda_stream
         ptr = (lambda t: t.data_ptr() if t is not None else None)
         o = (ctypes.c_int32 * 3)(*[int(v) for v in order])
-        y2, y3, p2, p3 = B['y2'], B['y3'], B['p2'], B['p3']
-        if self.fused12:
-            # conv1 -> bn1 -> conv2 in one kernel (the conv1 activation stays on chip)
-            rc = L.dt_conv12(ring.data_ptr(), n, slots, o, self.w0frag.data_ptr(),
-                             self.bf[0].data_ptr(), self.gamma[0].data_ptr() if ref else None,
-                             self.beta[0].data_ptr() if ref else None,
-                             self.eps[0] if ref else 0.0, self.wfrag[0].data_ptr(),
-                             self.bf[1].data_ptr(), y2.data_ptr(), ptr(p2), 0.01, stream)
-            first = 1
-        else:
-            y1, p1 = B['y1'], B['p1']
-            rc = L.dt_conv1(ring.data_ptr(), n, slots, o, self.w0frag.data_ptr(),
-                            self.bf[0].data_ptr(), y1.data_ptr(), ptr(p1), 0.01, stream)
-            first = 0
-        ins = [(B['y1'], B['p1'], 0), (y2, p2, 1), (y3, p3, 2)]
-        outs = [(y2, p2), (y3, p3), (flat, None)]
-        for layer in range(first, 3):
+        rc = L.dt_conv1(ring.data_ptr(), n, slots, o, self.w0frag.data_ptr(),
+                        self.bf[0].data_ptr(), B['y1'].data_ptr(), ptr(B['p1']), 0.01, stream)
+        ins = [(B['y1'], B['p1']), (B['y2'], B['p2']), (B['y3'], B['p3'])]
+        outs = [(B['y2'], B['p2']), (B['y3'], B['p3']), (flat, None)]
+        for layer in range(3):
             if rc != 0:
                 break
-            x, pp, g = ins[layer]
+            x, pp = ins[layer]
             y, po = outs[layer]
             last = layer == 2
             rc = L.dt_conv32(
                 layer + 2, n, x.data_ptr(), self.wfrag[layer].data_ptr(),
                 self.bf[layer + 1].data_ptr(), ptr(pp),
-                self.gamma[g].data_ptr() if ref else None,
-                self.beta[g].data_ptr() if ref else None, self.eps[g] if ref else 0.0,
+                self.gamma[layer].data_ptr() if ref else None,
+                self.beta[layer].data_ptr() if ref else None, self.eps[layer] if ref else 0.0,
                 y.data_ptr(), ptr(po),
                 self.gamma[3].data_ptr() if (ref and last) else None,
                 self.beta[3].data_ptr() if (ref and last) else None,
@@ -461,11 +449,6 @@ class FusedActor(nn.Module):
         return apply_head(x, self.head, self.max_action)
 
 
-def _lib_bands():
-    from aido1_amd import _lib
-    return _lib.lib().dt_conv1_bands()
-
-
 def conv1_fragments(w):
     """conv1 weights [32, 3, 8, 8] -> dt_conv1's MFMA A fragments [16, 64, 8]
     fp16: element [s][l][j] = w[l % 32][j % 4][s // 2][4 (s % 2) + 2 (l // 32)
@@ -488,6 +471,26 @@ def conv32_fragments(w):
     j = torch.arange(8, device=dev).view(1, 1, 8)
     return w.float()[ln % 32, 16 * (s % 2) + 8 * (ln // 32) + j, (s // 2) // 4,
                      (s // 2) % 4].to(torch.float16)
+
+
+def conv1_fragment_index(dev):
+    """conv1_fragments' layout as flat indices into the weights [32, 3, 8, 8]
+    viewed 1-D, the padding channel pointing past them (at a zero)."""
+    s = torch.arange(16, device=dev).view(16, 1, 1)
+    ln = torch.arange(64, device=dev).view(1, 64, 1)
+    j = torch.arange(8, device=dev).view(1, 1, 8)
+    c = j % 4
+    flat = ((ln % 32) * 3 + c) * 64 + (s // 2) * 8 + 4 * (s % 2) + 2 * (ln // 32) + j // 4
+    return torch.where(c < 3, flat, torch.full_like(flat, 32 * 3 * 64)).reshape(-1)
+
+
+def conv32_fragment_index(dev):
+    """conv32_fragments' layout as flat indices into the weights [32, 32, 4, 4]."""
+    s = torch.arange(32, device=dev).view(32, 1, 1)
+    ln = torch.arange(64, device=dev).view(1, 64, 1)
+    j = torch.arange(8, device=dev).view(1, 1, 8)
+    ci = 16 * (s % 2) + 8 * (ln // 32) + j
+    return ((((ln % 32) * 32 + ci) * 4 + (s // 2) // 4) * 4 + (s // 2) % 4).reshape(-1)
 
 
 def flops_per_sample():

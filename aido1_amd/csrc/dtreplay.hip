@@ -203,6 +203,42 @@ sample_kernel(const double* sum, const double* mn, int64_t cap, int64_t len, int
   w_out[i] = pow(p_sample * (double)len, -beta) / s_maxw;          // :231-232
 }
 
+// Frame store (aido1_amd/replay.py, ReplayBuffer frame_envs): one workgroup
+// per env copies the env's newest frame (`frame4` float4s at src + e *
+// src_stride4, the rollout ring's newest slot) into frame row base_row + e,
+// and its lane 0 advances the env's stack of frame rows: the transition's obs
+// is the stack before, its next_obs the stack after -- the older rows shifted
+// left and the new row appended, or every entry the new row where `done`
+// marks a respawned env (the renderer refilled every slot of its stack).
+constexpr int kFrameThreads = 256;
+
+__global__ void __launch_bounds__(kFrameThreads)
+frame_add_kernel(int64_t frame4, const float4* __restrict__ src, int64_t src_stride4,
+                 float4* __restrict__ dst, int k, int32_t* __restrict__ stack,
+                 const uint8_t* __restrict__ done, int32_t base_row, int32_t* __restrict__ obs_ptr,
+                 int32_t* __restrict__ next_ptr) {
+  const int e = blockIdx.x;
+  const float4* s = src + (size_t)e * src_stride4;
+  float4* d = dst + (size_t)e * frame4;
+#pragma unroll 4
+  for (int64_t i = threadIdx.x; i < frame4; i += kFrameThreads) d[i] = s[i];
+  if (threadIdx.x == 0) {
+    const int32_t row = base_row + e;
+    const bool fresh = done != nullptr && done[e] != 0;
+    int32_t* st = stack + (size_t)e * k;
+    int32_t* op = obs_ptr + (size_t)e * k;
+    int32_t* np = next_ptr + (size_t)e * k;
+    for (int j = 0; j < k; ++j) op[j] = st[j];
+    for (int j = 0; j + 1 < k; ++j) {
+      const int32_t v = fresh ? row : st[j + 1];
+      np[j] = v;
+      st[j] = v;
+    }
+    np[k - 1] = row;
+    st[k - 1] = row;
+  }
+}
+
 #define PER_HIP(h, expr)                                                       \
   do {                                                                         \
     hipError_t _e = (expr);                                                    \
@@ -330,6 +366,19 @@ int dt_per_read(dt_per* h, double* sum_dev, double* min_dev, double* max_priorit
   if (max_priority_dev)
     PER_HIP(h, hipMemcpyAsync(max_priority_dev, h->maxp, 8, hipMemcpyDeviceToDevice, s));
   return DT_OK;
+}
+
+int dt_frame_add(int32_t n, int64_t frame_elems, const float* src, int64_t src_env_stride,
+                 float* dst, int32_t k, int32_t* stack, const uint8_t* done, int32_t base_row,
+                 int32_t* obs_ptr, int32_t* next_ptr, void* stream) {
+  if (n < 0 || k < 1 || frame_elems < 4 || frame_elems % 4 || src_env_stride % 4) return DT_E_ARG;
+  if (n == 0) return DT_OK;
+  if (!src || !dst || !stack || !obs_ptr || !next_ptr || base_row < 0) return DT_E_ARG;
+  if (((uintptr_t)src | (uintptr_t)dst) & 15) return DT_E_ARG;
+  frame_add_kernel<<<n, kFrameThreads, 0, (hipStream_t)stream>>>(
+      frame_elems / 4, reinterpret_cast<const float4*>(src), src_env_stride / 4,
+      reinterpret_cast<float4*>(dst), k, stack, done, base_row, obs_ptr, next_ptr);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 
 int dt_per_check(dt_per* h) {

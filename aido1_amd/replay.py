@@ -14,6 +14,18 @@ their footprint).  ``add`` takes one transition as the reference does;
 rollout — and equals that many ``add`` calls in order.  ``sample`` returns
 device tensors in the reference's order; ``random.random`` / ``random.randint``
 are replaced by float64 uniforms (``u``, or drawn from ``generator``).
+
+Frame store (``frame_envs=n``, what TrainLoop uses): a batched rollout of n
+envs adds n transitions a decision whose observations are Transformer stacks
+of k frames, and consecutive stacks of an env share k - 1 frames
+(obs_t = next_obs of the env's previous transition).  Storing both stacks
+per transition moves 2k frames an env a decision; the frame store keeps each
+decision's ONE new frame per env in a ring of frame blocks (n rows a block,
+``size / n + 2k`` blocks) and gives every transition two int32 [k] rows of
+frame indices, written by dt_frame_add (include/dtreplay.h) in one kernel
+with the frame copy.  ``sample`` gathers the stacks through them, so it
+returns what the stacked storage returns.  Needs ``size % n == 0`` and
+float32 observations; only ``add_batch_ring`` adds to it.
 """
 import ctypes
 
@@ -25,9 +37,14 @@ FIELDS = ('obs', 'action', 'reward', 'next_obs', 'done')
 
 
 class ReplayBuffer:
-    def __init__(self, size, device=None, obs_dtype=None, generator=None):
+    def __init__(self, size, device=None, obs_dtype=None, generator=None, frame_envs=None):
         if size < 1:
             raise ValueError('size must be >= 1')
+        if frame_envs is not None:
+            if frame_envs < 1 or size % frame_envs:
+                raise ValueError('frame_envs must divide size')
+            if obs_dtype not in (None, torch.float32):
+                raise ValueError('the frame store holds float32 observations')
         self._maxsize = int(size)
         self._next_idx = 0
         self._len = 0
@@ -38,6 +55,11 @@ class ReplayBuffer:
         self.obs_dtype = obs_dtype
         self.gen = generator
         self.storage = None
+        self.frame_envs = int(frame_envs) if frame_envs else None
+        self.frames = None          # frame store: [blocks * n, H, W] float32
+        self._fblock = 0            # frame blocks written so far
+        self._begin_at = None       # decisions counter at the last stack begin
+        self._decisions = 0
 
     def __len__(self):
         return self._len
@@ -97,6 +119,8 @@ class ReplayBuffer:
         self.add_batch(obs_t, action, reward, obs_tp1, done, _batched=False)
 
     def add_batch(self, obs_t, action, reward, obs_tp1, done, _batched=True):
+        if self.frame_envs is not None:
+            raise ValueError('the frame store adds through add_batch_ring only')
         fields = self._fields(obs_t, action, reward, obs_tp1, done, _batched)
         n = fields[0].shape[0]
         start = self._next_idx
@@ -110,6 +134,8 @@ class ReplayBuffer:
         decision's obs_t, valid until the buffer comes round to them), or a copy
         where the rows would not be one block or would be overwritten by the
         next add."""
+        if self.frame_envs is not None:
+            return self._frame_add(obs_t, action, reward, ring, order, done)
         n = ring.shape[0]
         p = self._next_idx
         if self.storage is None or p + n > self._maxsize or 2 * n > self._maxsize:
@@ -126,9 +152,98 @@ class ReplayBuffer:
         st['done'][p:p + n].copy_(torch.as_tensor(done, device=self.device).to(torch.bool))
         self._advance(n)
         return st['next_obs'][p:p + n]
+
+    # ---- frame store ---------------------------------------------------------------
+    def _frame_block(self, frames):
+        """Write frames [n, H, W] (any strides) as the next frame block; returns
+        the block's first row."""
+        n = self.frame_envs
+        b = self._fblock % (self.frames.shape[0] // n)
+        self.frames[b * n:(b + 1) * n].copy_(frames)
+        self._fblock += 1
+        return b * n
+
+    def _frame_add(self, obs_t, action, reward, ring, order, done):
+        n, k = self.frame_envs, len(order)
+        if ring.shape[0] != n:
+            raise ValueError('add_batch_ring: the frame store holds %d envs, got %d'
+                             % (n, ring.shape[0]))
+        if self.frames is None:
+            blocks = self._maxsize // n + 2 * k
+            self.frames = torch.zeros((blocks * n,) + tuple(ring.shape[2:]), dtype=torch.float32,
+                                      device=self.device)
+            self._stack = torch.zeros(n, k, dtype=torch.int32, device=self.device)
+            self.storage = {
+                'obs_ptr': torch.zeros(self._maxsize, k, dtype=torch.int32, device=self.device),
+                'next_ptr': torch.zeros(self._maxsize, k, dtype=torch.int32, device=self.device)}
+        if obs_t is not None:
+            # a new chain (the first add, or a rollout reset): obs_t's k frames
+            # become k frame blocks.  Live transitions reference at most
+            # size / n + k blocks, so one begin per size / n decisions is safe.
+            if (self._begin_at is not None and self._len == self._maxsize
+                    and self._decisions - self._begin_at < self._maxsize // n):
+                raise ValueError('frame store: a new observation chain within size / n '
+                                 'decisions of the previous one')
+            obs_t = torch.as_tensor(obs_t, device=self.device)
+            ar = torch.arange(n, dtype=torch.int32, device=self.device)
+            for j in range(k):
+                self._stack[:, j] = ar + self._frame_block(obs_t[:, j])
+            self._begin_at = self._decisions
+        elif self._begin_at is None:
+            raise ValueError('frame store: the first add_batch_ring needs obs_t')
+        p = self._next_idx
+        self._reserve(n)
+        st = self.storage
+        fields = self._fields(torch.zeros(n, 1), action, reward, torch.zeros(n, 1), done, True)
+        if 'action' not in st:
+            for name, f in zip(FIELDS, fields):
+                if name not in ('obs', 'next_obs'):
+                    st[name] = torch.zeros((self._maxsize,) + tuple(f.shape[1:]), dtype=f.dtype,
+                                           device=self.device)
+        st['action'][p:p + n].copy_(fields[1])
+        st['reward'][p:p + n].copy_(fields[2])
+        st['done'][p:p + n].copy_(fields[4])
+        newest = ring[:, order[-1]]
+        b = self._fblock % (self.frames.shape[0] // n)
+        dn = fields[4]
+        if self.device.type == 'cuda':
+            L = _lib.lib()
+            if not newest[0].is_contiguous() or ring.dtype != torch.float32:
+                raise ValueError('frame store: the ring must be float32 with contiguous frames')
+            fe = newest[0].numel()
+            with torch.cuda.device(self.device):
+                rc = L.dt_frame_add(n, fe, newest.data_ptr(), newest.stride(0),
+                                    self.frames[b * n].data_ptr(), k, self._stack.data_ptr(),
+                                    dn.view(torch.uint8).data_ptr(), b * n,
+                                    st['obs_ptr'][p].data_ptr(), st['next_ptr'][p].data_ptr(),
+                                    ctypes.c_void_p(torch.cuda.current_stream(self.device)
+                                                    .cuda_stream))
+            if rc != 0:
+                raise _lib.DtError('dt_frame_add failed (%d)' % rc)
+            self._fblock += 1
+        else:   # CPU tensors (tests): the same bookkeeping in torch
+            row0 = self._frame_block(newest)
+            rows = torch.arange(n, dtype=torch.int32) + row0
+            st['obs_ptr'][p:p + n].copy_(self._stack)
+            nxt = torch.cat([self._stack[:, 1:], rows[:, None]], 1)
+            nxt[dn] = rows[dn, None]
+            st['next_ptr'][p:p + n].copy_(nxt)
+            self._stack.copy_(nxt)
+        self._decisions += 1
+        self._advance(n)
+        return None
+
     def _encode_sample(self, idxes):
         """buffers.py:38-52: (obs, actions, rewards, next_obs, dones) rows."""
-        return tuple(self.storage[name].index_select(0, idxes) for name in FIELDS)
+        st = self.storage
+        if self.frames is not None:
+            shp = (idxes.shape[0], st['obs_ptr'].shape[1]) + tuple(self.frames.shape[1:])
+            obs = self.frames.index_select(0, st['obs_ptr'].index_select(0, idxes).reshape(-1))
+            nxt = self.frames.index_select(0, st['next_ptr'].index_select(0, idxes).reshape(-1))
+            return (obs.view(shp), st['action'].index_select(0, idxes),
+                    st['reward'].index_select(0, idxes), nxt.view(shp),
+                    st['done'].index_select(0, idxes))
+        return tuple(st[name].index_select(0, idxes) for name in FIELDS)
 
     def uniforms(self, batch_size):
         return torch.rand(batch_size, dtype=torch.float64, device=self.device, generator=self.gen)
@@ -146,8 +261,9 @@ class ReplayBuffer:
 class PrioritizedReplayBuffer(ReplayBuffer):
     """buffers.py:140-259 on the GPU (segment trees in csrc/dtreplay.hip)."""
 
-    def __init__(self, size, alpha=0.5, device=None, obs_dtype=None, generator=None):
-        super().__init__(size, device, obs_dtype, generator)
+    def __init__(self, size, alpha=0.5, device=None, obs_dtype=None, generator=None,
+                 frame_envs=None):
+        super().__init__(size, device, obs_dtype, generator, frame_envs)
         if not alpha > 0:
             raise ValueError('alpha must be > 0')   # buffers.py:158
         self._alpha = alpha

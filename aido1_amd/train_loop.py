@@ -10,8 +10,9 @@ Here one process per GPU runs, per iteration:
   ActorRollout.step          one decision for n envs (actor on the frame ring,
                              exploration noise, 3 sim steps, render)
   replay.add_batch_ring      n transitions (obs, mapped action, reward_mod,
-                             next_obs, done), HBM-resident; next_obs copied
-                             from the frame ring, obs = the previous rows
+                             next_obs, done), HBM-resident; the frame store
+                             copies each env's newest frame from the ring
+                             and keeps frame indices for obs / next_obs
   replay.sample              batch_size transitions (proportional, GPU trees)
   DDPGTrainer.update         critic + actor + soft target update (grads
                              all-reduced over ranks with RCCL)
@@ -71,11 +72,16 @@ class TrainLoop:
         size = int(buffer_size or t['buffer_size'])
         gen = torch.Generator(device=self.device)
         gen.manual_seed(seed * 7919 + env_id_base)
+        # the frame store (replay.py): one frame per env a decision instead of
+        # two stacked observations per transition
+        fe = n_envs if (size % n_envs == 0 and obs_dtype in (None, torch.float32)) else None
         if prioritized:
             self.replay = PrioritizedReplayBuffer(size, t['alpha'], device=self.device,
-                                                  obs_dtype=obs_dtype, generator=gen)
+                                                  obs_dtype=obs_dtype, generator=gen,
+                                                  frame_envs=fe)
         else:
-            self.replay = ReplayBuffer(size, device=self.device, obs_dtype=obs_dtype, generator=gen)
+            self.replay = ReplayBuffer(size, device=self.device, obs_dtype=obs_dtype, generator=gen,
+                                       frame_envs=fe)
         self.prioritized = prioritized
         self.obs = None
         self.updates = 0
@@ -98,8 +104,9 @@ class TrainLoop:
             if self.refresh_due:
                 self._refresh()
                 self.refresh_due = False
-        # next_obs straight from the frame ring into the buffer; the stored rows
-        # are the next decision's obs (no stacked copy of the ring)
+        # next_obs straight from the frame ring into the buffer (frame store:
+        # the newest frame only; otherwise the stored rows are the next
+        # decision's obs); self.obs is None after the first add
         self.obs = self.replay.add_batch_ring(self.obs, self.rollout.actions, rew,
                                               self.rollout.ring, self.rollout.order(), done)
         self.decisions += 1

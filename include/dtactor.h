@@ -39,21 +39,17 @@ int dt_sample_norm(const void* x, void* y, int32_t n, int32_t hw, int32_t c, con
  *             [kx = 4*(s%2) + 2*(l/32) + j/4], 0 for c = 3 (aido1_amd/actor.py)
  *   bias      device f32 [32]
  *   y         device fp16 [n, 57, 77, 32] (NHWC)
- *   partials  device f32 [n, dt_conv1_bands(), 32, 2] or NULL: per band and
- *             channel (mean, M2) of the LeakyReLU outputs, for dt_conv1_norm
- *             and dt_conv32 layer 2.  dt_conv1_bands() is 1 for the default
- *             streaming kernel (one band = the whole 57-row sample) and 8 for
- *             the banded kernel (8-row bands; DTCONV1_BANDED=1 in the
- *             environment, read once per process). */
+ *   partials  device f32 [n, 32, 2] or NULL: the sample's per-channel
+ *             (mean, M2) of the LeakyReLU outputs (reference mode), for
+ *             dt_conv1_norm and dt_conv32 layer 2 */
 int dt_conv1(const float* ring, int32_t n, int32_t slots, const int32_t* order, const void* wfrag,
              const float* bias, void* y, float* partials, float slope, void* stream);
 
 /* dt_conv1_norm: the train-mode batch-of-one BatchNorm after conv1 (as
- * dt_sample_norm) from dt_conv1's band statistics, merged with Chan's
- * formula; y is normalised in place. */
+ * dt_sample_norm) from dt_conv1's per-sample statistics; y is normalised in
+ * place. */
 int dt_conv1_norm(void* y, int32_t n, const float* partials, const float* gamma,
                   const float* beta, float eps, void* stream);
-int32_t dt_conv1_bands(void);
 
 /* dt_conv32: conv2 / conv3 / conv4 of the actor (layer = 2, 3, 4: conv_2d
  * 32 -> 32, 4x4, strides 2, 2, 1) + bias + LeakyReLU, MFMA fp16 with f32
@@ -61,7 +57,7 @@ int32_t dt_conv1_bands(void);
  * workgroups stream whole samples through an LDS ring of input rows.
  *   wfrag      device fp16 [32, 64, 8] A fragments: [s][l][j] =
  *              w[l%32][16*(s%2) + 8*(l/32) + j][(s/2)/4][(s/2)%4]
- *   prev_part  the previous layer's band statistics (dt_conv1's partials for
+ *   prev_part  the previous layer's statistics [n, 32, 2] (dt_conv1's partials for
  *              layer 2, this call's `part` of layer 2 / 3 for 3 / 4) or NULL:
  *              with it, the previous BatchNorm (in_gamma, in_beta, in_eps) is
  *              applied per sample while the input is staged (reference mode)
@@ -76,26 +72,6 @@ int dt_conv32(int32_t layer, int32_t n, const void* x, const void* wfrag, const 
               const float* prev_part, const float* in_gamma, const float* in_beta, float in_eps,
               void* y, float* part, const float* out_gamma, const float* out_beta,
               float out_eps, float slope, void* stream);
-
-/* dt_conv12: dt_conv1 + its BatchNorm + dt_conv32 layer 2 in one kernel: one
- * workgroup per sample keeps the sample's conv1 activation (57 x 77 x 32,
- * fp16) in registers, reduces its per-sample BatchNorm statistics there and
- * feeds conv2 from them through LDS, so the activation never goes to HBM.
- *   ring, slots, order, w1frag, b1  as dt_conv1
- *   gamma1, beta1, eps1  conv1's BatchNorm (reference mode: the sample's own
- *            statistics), or gamma1 = NULL for the eval-mode network (BN
- *            folded into conv2 by the caller)
- *   w2frag, b2  conv2 as dt_conv32's layer 2
- *   y2       device fp16 [n, 27, 37, 32] (NHWC)
- *   part2    device f32 [n, 32, 2]: the sample's per-channel (mean, M2) of
- *            conv2's LeakyReLU outputs (reference mode; NULL in eval mode),
- *            the prev_part of dt_conv32 layer 3
- * Replaces the reference's conv1 -> leaky_relu -> bn1 -> conv2 -> leaky_relu
- * (duckietown_rl/ddpg.py:56, config.json actor conv layers 1-2). */
-int dt_conv12(const float* ring, int32_t n, int32_t slots, const int32_t* order,
-              const void* w1frag, const float* b1, const float* gamma1, const float* beta1,
-              float eps1, const void* w2frag, const float* b2, void* y2, float* part2,
-              float slope, void* stream);
 
 /* dt_explore: SingleThreadExplorer's action choice for n explorers at once,
  * one fused pass replacing the torch restatement's ~25 element-wise kernels

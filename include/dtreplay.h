@@ -70,6 +70,25 @@ int dt_per_read(dt_per* h, double* sum_dev, double* min_dev, double* max_priorit
  * reference's asserts reject (message in dt_per_last_error). */
 int dt_per_check(dt_per* h);
 
+/* dt_frame_add: one decision of the frame store behind
+ * ReplayBuffer.add_batch_ring (aido1_amd/replay.py, frame_envs).  Replaces the
+ * two stacked observation copies buffers.py:29-36 stores per transition
+ * (obs_t, obs_tp1; the Transformer stack of 3 frames each): a decision adds
+ * ONE frame per env, and a transition keeps frame-row indices instead.
+ *   src        device f32, env e's newest frame at src + e * src_env_stride
+ *              (the rollout ring's newest slot); frame_elems floats a frame,
+ *              a multiple of 4, src and dst 16-B aligned
+ *   dst        device f32 [n, frame_elems]: frame rows base_row .. base_row + n - 1
+ *   stack      device int32 [n, k]: each env's current stack as frame rows
+ *              (oldest first), advanced in place
+ *   done       device uint8 [n] or NULL: respawned envs, whose whole stack
+ *              becomes the new row (the renderer refilled every slot)
+ *   obs_ptr    device int32 [n, k] out: the stack before (the transition's obs)
+ *   next_ptr   device int32 [n, k] out: the stack after (its next_obs) */
+int dt_frame_add(int32_t n, int64_t frame_elems, const float* src, int64_t src_env_stride,
+                 float* dst, int32_t k, int32_t* stack, const uint8_t* done, int32_t base_row,
+                 int32_t* obs_ptr, int32_t* next_ptr, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -29,10 +29,12 @@
 extern "C" {
 #endif
 
-#define DT_ABI_VERSION 4  /* 2: curves per tile vary (curve_start), intersections;
+#define DT_ABI_VERSION 5  /* 2: curves per tile vary (curve_start), intersections;
                              3: static objects in dt_map, safety_rad_mult;
                              4: dt_render_io.pose / list_cap, dt_copy_pose,
-                                dt_step_many pose output */
+                                dt_step_many pose output;
+                             5: dtactor.h: dt_conv12 and dt_conv1_bands
+                                removed, partials [n, 32, 2] */
 
 /* error codes */
 #define DT_OK 0

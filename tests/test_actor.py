@@ -101,3 +101,28 @@ def test_fused_reference_mode_dropout_live_and_refresh():
     b = ConfigActor(golden('reference_config.json')['model']['actor'])
     f.refresh(b)
     assert torch.equal(f.w[2], b.layers()[0][2].weight.contiguous(memory_format=torch.channels_last))
+
+
+@pytest.mark.parametrize('mode', ['reference', 'eval'])
+def test_refresh_fragments_match_fragment_builders(mode):
+    """refresh() gathers the MFMA fragments through index maps; they equal
+    conv1_fragments / conv32_fragments of the weights it derives, and the f32
+    biases are the layers' (folded) biases."""
+    from aido1_amd.actor import (ConfigActor, FusedActor, conv1_fragments,
+                                 conv32_fragments)
+    torch.manual_seed(3)
+    a = ConfigActor(golden('reference_config.json')['model']['actor'])
+    for m in a.modules():
+        if isinstance(m, torch.nn.BatchNorm2d):
+            m.running_mean.uniform_(-0.5, 0.5)
+            m.running_var.uniform_(0.5, 2.0)
+    f = FusedActor(a, dtype=torch.float16, mode=mode)
+    assert torch.equal(f.w0frag, conv1_fragments(f.w[0].float()))
+    for i in range(1, 4):
+        assert torch.equal(f.wfrag[i - 1], conv32_fragments(f.w[i].float()))
+    convs = a.layers()[0]
+    if mode == 'reference':
+        for i in range(4):
+            assert torch.equal(f.bf[i], convs[i].bias.detach())
+    else:
+        assert torch.allclose(f.bf, torch.stack([b.float() for b in f.b]), rtol=1e-3, atol=1e-3)

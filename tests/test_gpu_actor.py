@@ -119,8 +119,7 @@ def test_conv1_kernel_matches_conv2d(gpu, slots, order, n):
     x = ring[:, order].half().float()
     ref = F.leaky_relu(F.conv2d(x, w.half().float(), b, stride=2))      # [n,32,57,77]
     y = torch.empty(n, 57, 77, 32, dtype=torch.float16, device=gpu)
-    nb = L.dt_conv1_bands()
-    part = torch.empty(n, nb, 32, 2, device=gpu)
+    part = torch.empty(n, 32, 2, device=gpu)
     o = (ctypes.c_int32 * 3)(*order)
     s = torch.cuda.current_stream().cuda_stream
     wf = conv1_fragments(w)     # held: a temporary's memory could be reused before the launch
@@ -129,15 +128,12 @@ def test_conv1_kernel_matches_conv2d(gpu, slots, order, n):
     got = y.permute(0, 3, 1, 2).float()
     err = (got - ref).abs().max().item()
     assert err < 2e-3 * max(1.0, ref.abs().max().item()), err
-    # band statistics (mean, M2) of the f32 outputs
+    # per-sample statistics (mean, M2) of the f32 outputs
     r64 = ref.double()
-    br = -(-57 // nb)     # output rows per band: 57 (streaming conv1) or 8 (DTCONV1_BANDED=1)
-    for band in range(nb):
-        rows = r64[:, :, br * band:br * band + br]
-        mean = rows.mean((2, 3))
-        m2 = ((rows - mean[:, :, None, None]) ** 2).sum((2, 3))
-        assert torch.allclose(part[:, band, :, 0].double(), mean, rtol=1e-3, atol=1e-3)
-        assert torch.allclose(part[:, band, :, 1].double(), m2, rtol=2e-3, atol=1e-2)
+    mean = r64.mean((2, 3))
+    m2 = ((r64 - mean[:, :, None, None]) ** 2).sum((2, 3))
+    assert torch.allclose(part[..., 0].double(), mean, rtol=1e-3, atol=1e-3)
+    assert torch.allclose(part[..., 1].double(), m2, rtol=2e-3, atol=1e-2)
     gamma = torch.rand(32, device=gpu) + 0.5
     beta = torch.rand(32, device=gpu) - 0.5
     y16 = y.permute(0, 3, 1, 2).double()          # what the norm pass normalises
@@ -210,83 +206,6 @@ def test_hip_convs_reference_mode_many_samples(gpu):
     assert torch.max(torch.abs(got - want)).item() < 2e-2
 
 
-@pytest.mark.parametrize('ref_mode', [True, False])
-@pytest.mark.parametrize('n,slots,order', [(37, 3, [0, 1, 2]), (300, 4, [2, 3, 0])])
-def test_conv12_kernel_matches_conv2d(gpu, ref_mode, n, slots, order):
-    """dt_conv12 (conv1 -> per-sample BatchNorm -> conv2 in one kernel, the conv1
-    activation held in registers) vs an f32 restatement on the same fp16-rounded
-    inputs and weights: conv2d + LeakyReLU, the sample's own BatchNorm over the
-    fp16-rounded conv1 outputs (what the kernel normalises; statistics in
-    float64), conv2d + LeakyReLU; and the conv2 statistics (mean, M2)."""
-    import ctypes
-    import torch.nn.functional as F
-    from aido1_amd import _lib
-    from aido1_amd.actor import conv1_fragments, conv32_fragments
-    L = _lib.lib()
-    torch.manual_seed(11 + n)
-    ring = torch.rand(n, slots, 120, 160, device=gpu)
-    w1 = torch.randn(32, 3, 8, 8, device=gpu) * 0.08
-    b1 = torch.randn(32, device=gpu) * 0.2
-    w2 = (torch.randn(32, 32, 4, 4, device=gpu) * 0.05).half().float()
-    b2 = torch.randn(32, device=gpu) * 0.1
-    g1 = torch.rand(32, device=gpu) + 0.5
-    be1 = torch.rand(32, device=gpu) - 0.5
-    x = ring[:, order].half().float()
-    h1 = F.leaky_relu(F.conv2d(x, w1.half().float(), b1, stride=2)).double()   # [n,32,57,77]
-    h16 = h1.half().double()
-    if ref_mode:
-        m = h1.mean((2, 3), keepdim=True)
-        v = ((h16 - m) ** 2).mean((2, 3), keepdim=True)
-        h16 = ((h16 - m) / torch.sqrt(v + 1e-5) * g1.double().view(1, -1, 1, 1) +
-               be1.double().view(1, -1, 1, 1)).half().double()
-    want = F.leaky_relu(F.conv2d(h16, w2.double(), b2.double(), stride=2))    # [n,32,27,37]
-    y2 = torch.empty(n, 27, 37, 32, dtype=torch.float16, device=gpu)
-    p2 = torch.empty(n, 32, 2, device=gpu) if ref_mode else None
-    o = (ctypes.c_int32 * 3)(*order)
-    s = torch.cuda.current_stream().cuda_stream
-    # the fragment tensors must outlive the launch (a temporary's memory is
-    # reused by the next allocation on the stream before the kernel runs)
-    w1f, w2f = conv1_fragments(w1), conv32_fragments(w2)
-    rc = L.dt_conv12(ring.data_ptr(), n, slots, o, w1f.data_ptr(), b1.data_ptr(),
-                     g1.data_ptr() if ref_mode else None, be1.data_ptr() if ref_mode else None,
-                     1e-5, w2f.data_ptr(), b2.data_ptr(), y2.data_ptr(),
-                     p2.data_ptr() if ref_mode else None, 0.01, s)
-    assert rc == 0
-    got = y2.permute(0, 3, 1, 2).double()
-    err = (got - want).abs().max().item()
-    assert err < 1e-2 * max(1.0, want.abs().max().item()), err
-    if ref_mode:
-        mean = want.mean((2, 3))
-        m2 = ((want - mean[:, :, None, None]) ** 2).sum((2, 3))
-        assert torch.allclose(p2[..., 0].double(), mean, rtol=1e-2, atol=1e-2)
-        assert torch.allclose(p2[..., 1].double(), m2, rtol=2e-2, atol=1e-1)
-
-
-def test_conv12_matches_unfused_chain(gpu, monkeypatch):
-    """The FusedActor reference-mode forward with dt_conv12 (DTCONV_FUSED12=1)
-    equals the default chain (dt_conv1 + dt_conv32 layer 2) up to the order of
-    the BatchNorm statistics' sums; and chunked passes (DTCONV_CHUNK) equal
-    one pass."""
-    from aido1_amd.actor import ConfigActor, FusedActor
-    from test_trainer import no_dropout
-    a = ConfigActor(no_dropout(golden('reference_config.json')['model']['actor']))
-    a.load_state_dict(formula_state_dict(a.state_dict()))
-    torch.manual_seed(6)
-    x = torch.rand(260, 3, 120, 160, device=gpu)
-    a = a.to(gpu)
-    monkeypatch.setenv('DTCONV_FUSED12', '0')
-    old = FusedActor(a, dtype=torch.float16, mode='reference')
-    monkeypatch.setenv('DTCONV_FUSED12', '1')
-    new = FusedActor(a, dtype=torch.float16, mode='reference')
-    assert new.fused12 and not old.fused12
-    want = old(x)
-    assert torch.max(torch.abs(new(x) - want)).item() < 5e-3
-    monkeypatch.setenv('DTCONV_FUSED12', '0')
-    monkeypatch.setenv('DTCONV_CHUNK', '96')
-    chunked = FusedActor(a, dtype=torch.float16, mode='reference')
-    assert torch.equal(chunked(x), want)
-
-
 def test_rollout_exploiter_block(gpu):
     """config.json:183-186's 7 exploring + 1 exploiting explorers: the last n/8
     envs act with load_exploit_actor's weights, epsilon 0 (explorers.py:116,
@@ -343,7 +262,7 @@ for slots, order, n in ((4, [1, 2, 3], 1100), (3, [2, 0, 1], 37), (3, [0, 1, 2],
     w = torch.randn(32, 3, 8, 8, device=dev) * 0.08
     b = torch.randn(32, device=dev) * 0.2
     y = torch.empty(n, 57, 77, 32, dtype=torch.float16, device=dev)
-    part = torch.empty(n, L.dt_conv1_bands(), 32, 2, device=dev)
+    part = torch.empty(n, 32, 2, device=dev)
     wf = conv1_fragments(w)
     o = (ctypes.c_int32 * 3)(*order)
     assert L.dt_conv1(ring.data_ptr(), n, slots, o, wf.data_ptr(), b.data_ptr(), y.data_ptr(),

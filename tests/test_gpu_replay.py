@@ -111,3 +111,28 @@ def test_per_rejects_like_reference_asserts(gpu):
     one.add_batch(*_payload([0], gpu))
     with pytest.raises(DtError, match='at least 2'):
         one.sample(4, beta=0.4)
+
+
+def test_frame_store_gpu_equals_stacked_per(gpu):
+    """dt_frame_add (include/dtreplay.h) behind PrioritizedReplayBuffer's frame
+    store: the same sampled indices, weights and stacks as the stacked
+    storage, across wraps and respawns."""
+    import sys
+    sys.path.insert(0, __import__('os').path.dirname(__file__))
+    from test_replay import _frame_steps
+    from aido1_amd.replay import PrioritizedReplayBuffer
+    g = torch.Generator().manual_seed(3)
+    n, size = 256, 1024
+    a = PrioritizedReplayBuffer(size, 0.6, device=gpu, frame_envs=n)
+    b = PrioritizedReplayBuffer(size, 0.6, device=gpu)
+    for t in _frame_steps(a, b, n, 9, g):
+        u = torch.rand(64, generator=g, dtype=torch.float64)
+        ra, rb = a.sample(64, 0.4, u=u), b.sample(64, 0.4, u=u)
+        for x, y in zip(ra, rb):
+            assert torch.equal(x, y)
+        pr = torch.rand(64, generator=g, dtype=torch.float64) + 0.1
+        a.update_priorities(ra[-1], pr)
+        b.update_priorities(rb[-1], pr)
+    idx = torch.arange(size, device=gpu)
+    for x, y in zip(a._encode_sample(idx), b._encode_sample(idx)):
+        assert torch.equal(x, y)

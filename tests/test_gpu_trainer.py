@@ -25,25 +25,36 @@ def test_update_matches_reference_gpu(gpu, graph):
         assert tr._graphs is not None and len(tr._graphs) == 1
 
 
-@pytest.mark.parametrize('prioritized,graph', [(True, True), (False, False)])
-def test_train_loop_runs(gpu, prioritized, graph):
+@pytest.mark.parametrize('prioritized,graph,size', [(True, True, 1000), (False, False, 1000),
+                                                     (True, True, 1024)])
+def test_train_loop_runs(gpu, prioritized, graph, size):
+    """size 1024 = 8 decisions of 128 envs: the frame store (replay.py)."""
     from aido1_amd.train_loop import TrainLoop
     cfg = golden('reference_config.json')
-    loop = TrainLoop(cfg, n_envs=128, device=0, seed=5, buffer_size=1000, batch_size=32,
+    loop = TrainLoop(cfg, n_envs=128, device=0, seed=5, buffer_size=size, batch_size=32,
                      prioritized=prioritized, graph=graph)
+    assert (loop.replay.frame_envs is not None) == (size == 1024)
     w0 = loop.trainer.actor.net.input_nets[0].internal_modules[0].kernel.weight.detach().clone()
     t0 = loop.rollout.actor.w[1].detach().clone()
     loop.reset()
     for _ in range(12):
         loop.step()
     torch.cuda.synchronize()
-    assert len(loop.replay) == 1000 and loop.updates == 12 and loop.decisions == 12
+    assert len(loop.replay) == size and loop.updates == 12 and loop.decisions == 12
     assert torch.isfinite(loop.metrics['critic_loss']) and torch.isfinite(loop.metrics['actor_loss'])
     w1 = loop.trainer.actor.net.input_nets[0].internal_modules[0].kernel.weight
     assert not torch.equal(w0, w1)
     assert not torch.equal(t0, loop.rollout.actor.w[1])      # acting copy follows the target
     st = loop.replay.storage
-    assert st['obs'].shape == (1000, 3, 120, 160) and st['action'].shape == (1000, 2)
+    if size == 1024:
+        obs, act, rew, nxt, done = loop.replay._encode_sample(torch.arange(size, device=gpu))
+        # the last decision's next_obs is the rollout's current stack
+        assert torch.equal(nxt[-128:], loop.rollout.stack())
+        # obs of a decision = next_obs of the env's previous decision
+        assert torch.equal(obs[-128:], nxt[-256:-128])
+        assert obs.shape == (size, 3, 120, 160) and st['action'].shape == (size, 2)
+    else:
+        assert st['obs'].shape == (1000, 3, 120, 160) and st['action'].shape == (1000, 2)
     assert float(st['action'].min()) >= 0.0                  # mapped a/2 + 0.5 stored
     if prioritized:
         loop.replay.check()

@@ -78,3 +78,63 @@ def test_add_batch_ring_equals_add_batch():
     assert a._next_idx == b._next_idx and len(a) == len(b)
     for k in a.storage:
         assert torch.equal(a.storage[k], b.storage[k]), k
+
+
+def _frame_steps(a, b, n, steps, g, per=False):
+    """Feed a (frame store) and b (stacked storage) the same decisions of a
+    frame ring with the rollout's semantics: one new frame a decision in the
+    slot order advances, and a respawned env's whole stack is its new frame
+    (the renderer's fresh refill).  Yields after every decision."""
+    dev = a.device
+    ring = torch.rand(n, 3, 2, 4, generator=g).to(dev)
+    obs_a = obs_b = ring[:, [0, 1, 2]].clone()
+    for t in range(steps):
+        order = [(t + 1 + k) % 3 for k in range(3)]
+        done = (torch.rand(n, generator=g) < 0.3).to(dev)
+        new = torch.rand(n, 2, 4, generator=g).to(dev)
+        ring[:, order[-1]] = new
+        ring[done] = new[done, None]
+        act = torch.rand(n, 2, generator=g).to(dev)
+        rew = torch.rand(n, generator=g, dtype=torch.float64).to(dev)
+        nxt = ring[:, order].clone()
+        b.add_batch(obs_b, act, rew, nxt, done)
+        obs_b = nxt
+        obs_a = a.add_batch_ring(obs_a, act, rew, ring, order, done)
+        assert obs_a is None
+        yield t
+
+
+def test_frame_store_samples_equal_stacked_storage():
+    """The frame store (frame_envs: one frame per env a decision plus frame
+    indices) returns the stacks the stacked storage (buffers.py:29-52) returns
+    for the same indices, across many wraps of the buffer and respawns."""
+    from aido1_amd.replay import ReplayBuffer
+    g = torch.Generator().manual_seed(1)
+    n, size = 3, 9
+    a = ReplayBuffer(size, device='cpu', frame_envs=n)
+    b = ReplayBuffer(size, device='cpu')
+    for _ in _frame_steps(a, b, n, 13, g):
+        assert len(a) == len(b) and a._next_idx == b._next_idx
+        u = torch.rand(32, generator=g, dtype=torch.float64)
+        for x, y in zip(a.sample(32, u=u), b.sample(32, u=u)):
+            assert torch.equal(x, y)
+    # every row, not only sampled ones
+    idx = torch.arange(size)
+    for x, y in zip(a._encode_sample(idx), b._encode_sample(idx)):
+        assert torch.equal(x, y)
+    assert a.frames.shape[0] == (size // n + 6) * n   # 2k blocks beyond the transitions'
+
+
+def test_frame_store_rejects():
+    from aido1_amd.replay import ReplayBuffer
+    with pytest.raises(ValueError):
+        ReplayBuffer(10, device='cpu', frame_envs=3)          # must divide size
+    with pytest.raises(ValueError):
+        ReplayBuffer(9, device='cpu', frame_envs=3, obs_dtype=torch.bfloat16)
+    rb = ReplayBuffer(9, device='cpu', frame_envs=3)
+    with pytest.raises(ValueError):
+        rb.add_batch(*_batch(0, 3))
+    ring = torch.zeros(3, 3, 2, 2)
+    with pytest.raises(ValueError):                            # the first add needs obs_t
+        rb.add_batch_ring(None, torch.zeros(3, 2), torch.zeros(3), ring, [0, 1, 2],
+                          torch.zeros(3, dtype=torch.bool))

@@ -31,7 +31,6 @@ def run(n, reps):
     dev = torch.device('cuda', 0)
     torch.manual_seed(0)
     shapes = {2: (57, 77, 27, 37), 3: (27, 37, 12, 17), 4: (12, 17, 9, 14)}
-    bands = {2: 8, 3: 1, 4: 1}
     res = {}
     for name in SKIPS:
         L = ctypes.CDLL(os.path.join(OUT, 'libconv_%s.so' % name))
@@ -42,7 +41,7 @@ def run(n, reps):
             x = (torch.rand(n, ih, iw, 32, device=dev) * 2).half()
             w = (torch.randn(32 * 64 * 8, device=dev) * 0.05).half()
             b = torch.zeros(32, device=dev)
-            pp = torch.rand(n, bands[layer], 32, 2, device=dev) + 0.5
+            pp = torch.rand(n, 32, 2, device=dev) + 0.5
             g = torch.ones(32, device=dev)
             bt = torch.zeros(32, device=dev)
             y = torch.empty(n, oh * ow * 32, dtype=torch.float16, device=dev)
