@@ -38,6 +38,7 @@ between them otherwise.  Inputs are copied into static buffers; Adam is the
 capturable variant with a device-tensor learning rate set by fill_ before
 each replay.  Dropout draws stay fresh per replay (graph-safe Philox offsets).
 """
+import contextlib
 import copy
 
 import torch
@@ -83,6 +84,10 @@ def hard_update(target, source):
     """models/torch_utils.py:12-14."""
     torch._foreach_copy_([p.data for p in target.parameters()],
                          [p.data for p in source.parameters()])
+
+
+def _nullctx():
+    return contextlib.nullcontext()
 
 
 class DDPGTrainer:
@@ -145,22 +150,58 @@ class DDPGTrainer:
                     raise ValueError('graph mode needs a fixed batch shape')
                 self._in[k].copy_(v)
 
+    def _grads(self, loss, module):
+        """zero_grad + loss.backward() for `module`'s parameters
+        (trainers.py:178-179, 197-198) as torch.autograd.grad: the same
+        gradients, written into .grad, and none computed for the other
+        networks on the path.  The reference's actor_loss.backward() also
+        runs the critic's whole backward and fills the critic's .grad, which
+        its next critic_optim.zero_grad() discards unread; here the critic's
+        conv trunk (independent of the actor) is not differentiated at all."""
+        params = [p for p in module.parameters() if p.requires_grad]
+        grads = torch.autograd.grad(loss, params, allow_unused=True, materialize_grads=True)
+        if all(p.grad is not None for p in params):
+            torch._foreach_copy_([p.grad for p in params], list(grads))
+        else:
+            for p, g in zip(params, grads):
+                p.grad = g
+
     # ---- the three stages (trainers.py:156-229) ------------------------------------
+    def _fork(self):
+        """A side stream joined to the current one (GPU), or None (CPU)."""
+        if self.device.type != 'cuda':
+            return None
+        if getattr(self, '_side', None) is None:
+            self._side = torch.cuda.Stream(self.device)
+        self._side.wait_stream(torch.cuda.current_stream(self.device))
+        return self._side
+
+    def _join(self, side, *tensors):
+        if side is not None:
+            cur = torch.cuda.current_stream(self.device)
+            cur.wait_stream(side)
+            for t in tensors:
+                t.record_stream(cur)
+
     def _stage_critic(self):
         x = self._in
-        with torch.no_grad():
-            next_actions = self.target_actor(x['nxt'])
-            next_v = self.target_critic(x['nxt'], next_actions)
-            self._y = x['rew'] + x['notdone'] * self.gamma * next_v
+        # the targets' forward (target actor -> target critic on next_obs) and
+        # the critic's forward on obs are independent: two streams, so their
+        # batch-64 kernels (a few CUs each) run side by side -- in a HIP graph
+        # two branches of the captured DAG
+        side = self._fork()
+        with torch.cuda.stream(side) if side is not None else _nullctx():
+            with torch.no_grad():
+                next_actions = self.target_actor(x['nxt'])
+                next_v = self.target_critic(x['nxt'], next_actions)
+                self._y = x['rew'] + x['notdone'] * self.gamma * next_v
         y_predicted = self.critic(x['obs'], x['act'])
+        self._join(side, self._y)
         if self.critic_loss_kind == 'mse_loss':
             critic_loss = F.mse_loss(y_predicted, self._y)
         else:
             critic_loss = F.smooth_l1_loss(y_predicted, self._y)
-        self.critic_optim.zero_grad(set_to_none=not self.graph)
-        critic_loss.backward()
-        # keep no autograd graph alive past backward (a live graph pins the
-        # AccumulateGrad nodes to the eager stream and breaks graph capture)
+        self._grads(critic_loss, self.critic)
         self._critic_loss = critic_loss.detach()
 
     def _stage_actor(self):
@@ -168,17 +209,22 @@ class DDPGTrainer:
         self.critic_optim.step()
         pred_actions = self.actor(x['obs'])
         actor_loss = -1.0 * torch.mean(self.critic(x['obs'], pred_actions))
-        self.actor_optim.zero_grad(set_to_none=not self.graph)
-        actor_loss.backward()
+        self._grads(actor_loss, self.actor)
         self._actor_loss = actor_loss.detach()
 
     def _stage_targets(self):
         x = self._in
+        # the TD-error forward reads only the (already stepped) critic: it runs
+        # beside the actor step and the soft updates
+        side = self._fork()
+        with torch.cuda.stream(side) if side is not None else _nullctx():
+            with torch.no_grad():                                    # trainers.py:223-229
+                self._td = self._y - self.critic(x['obs'], x['act'])
         self.actor_optim.step()
         soft_update(self.target_actor, self.actor, self.tau)       # trainers.py:215-216
         soft_update(self.target_critic, self.critic, self.tau)
-        with torch.no_grad():                                        # trainers.py:223-229
-            self._td = self._y - self.critic(x['obs'], x['act'])
+        self._join(side, self._td)
+        with torch.no_grad():
             self._metrics = (torch.sqrt(self._critic_loss), self._actor_loss)
 
     def _capture(self):

@@ -72,6 +72,20 @@ def check(fixture, order, summaries, rng_after, rtol, atol, later_rtol):
                 if tight:
                     a_ = 1e-5 if (key.endswith(('.bias', 'running_mean')) and 'conv' in key
                                   or 'running_mean' in key) else atol
+                    if rtol > 1e-6 and (key.endswith('.bias') and 'conv' in key
+                                        or 'running_mean' in key):
+                        # float32: a conv bias feeding a BatchNorm has a ~0
+                        # gradient whose sign depends on the host's summation
+                        # order, and Adam's first step turns it into +-lr
+                        # (lr <= 1e-3): elements within 2 lr, the two sums
+                        # within 2 lr per element; the BatchNorm's running
+                        # mean (momentum 0.1) follows that bias
+                        np.testing.assert_allclose(g[2:], r[2:], rtol=rtol, atol=2.5e-3,
+                                                   err_msg='it%d %s.%s' % (k, name, key))
+                        np.testing.assert_allclose(g[:2], r[:2], rtol=rtol,
+                                                   atol=2e-3 * (g.size - 2) * 2,
+                                                   err_msg='it%d %s.%s' % (k, name, key))
+                        continue
                     np.testing.assert_allclose(g, r, rtol=rtol, atol=a_,
                                                err_msg='it%d %s.%s' % (k, name, key))
                 else:

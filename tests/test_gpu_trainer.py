@@ -48,10 +48,12 @@ def test_train_loop_runs(gpu, prioritized, graph, size):
     st = loop.replay.storage
     if size == 1024:
         obs, act, rew, nxt, done = loop.replay._encode_sample(torch.arange(size, device=gpu))
+        p = loop.replay._next_idx          # 12 decisions of 128 rows: 512
+        assert p == 512
         # the last decision's next_obs is the rollout's current stack
-        assert torch.equal(nxt[-128:], loop.rollout.stack())
+        assert torch.equal(nxt[p - 128:p], loop.rollout.stack())
         # obs of a decision = next_obs of the env's previous decision
-        assert torch.equal(obs[-128:], nxt[-256:-128])
+        assert torch.equal(obs[p - 128:p], nxt[p - 256:p - 128])
         assert obs.shape == (size, 3, 120, 160) and st['action'].shape == (size, 2)
     else:
         assert st['obs'].shape == (1000, 3, 120, 160) and st['action'].shape == (1000, 2)
