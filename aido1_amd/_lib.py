@@ -17,9 +17,10 @@ PKG_DIR = os.path.dirname(os.path.abspath(__file__))
 REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_PATH = os.path.join(PKG_DIR, 'libdtsim.so')
 CSRC = os.path.join(PKG_DIR, 'csrc')
-SOURCES = ['dtsim.hip', 'dtrender.hip', 'dtreplay.hip', 'dtactor.hip', 'dtconv.hip']
+SOURCES = ['dtsim.hip', 'dtrender.hip', 'dtreplay.hip', 'dtactor.hip', 'dtconv.hip',
+           'dttrain.hip']
 HEADERS = ['dtsim_common.h', 'dtrender.h']
-PUBLIC_HEADERS = ['dtsim.h', 'dtreplay.h', 'dtactor.h']
+PUBLIC_HEADERS = ['dtsim.h', 'dtreplay.h', 'dtactor.h', 'dttrain.h']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ABI_VERSION = 5
 
@@ -146,6 +147,12 @@ def lib():
             'dt_per_read': (ctypes.c_int, [vp, vp, vp, vp, vp]),
             'dt_per_check': (ctypes.c_int, [vp]),
             'dt_frame_add': (ctypes.c_int, [i32, i64, vp, i64, vp, i32, vp, vp, i32, vp, vp, vp]),
+            # dttrain.h
+            'dt_train_work_floats': (i64, [i64]),
+            'dt_bn_leaky_fwd': (ctypes.c_int, [i64, vp, vp, ctypes.c_float, vp, vp, ctypes.c_float,
+                                               ctypes.c_float, vp, vp, vp, vp, vp, vp, vp, vp]),
+            'dt_bn_leaky_bwd': (ctypes.c_int, [i64, vp, vp, vp, vp, ctypes.c_float, vp, vp, vp, vp,
+                                               vp, vp]),
             # dtactor.h
             'dt_sample_norm': (ctypes.c_int, [vp, vp, i32, i32, i32, vp, vp, ctypes.c_float,
                                               ctypes.c_float, i32, vp]),

@@ -99,13 +99,28 @@ def _init_weight(w, mode, conv):
 
 
 class _Seq(nn.Module):       # MetaNet: ".internal_modules.<i>"
+    # conv -> LeakyReLU -> BatchNorm blocks in train mode on the GPU (f32) run
+    # their tail as dt_bn_leaky_fwd / _bwd (train_ops.py, include/dttrain.h)
+    fused_tail = True
+
     def __init__(self, mods):
         super().__init__()
         self.internal_modules = nn.ModuleList(mods)
 
     def forward(self, x):
-        for m in self.internal_modules:
+        mods = self.internal_modules
+        i, k = 0, len(mods)
+        while i < k:
+            m = mods[i]
+            if (self.fused_tail and i + 2 < k and isinstance(m, _Conv)
+                    and isinstance(mods[i + 2], nn.BatchNorm2d)):
+                from aido1_amd import train_ops
+                if train_ops.applicable(x, m.kernel, mods[i + 1], mods[i + 2]):
+                    x = train_ops.conv_leaky_bn(x, m.kernel, mods[i + 1], mods[i + 2])
+                    i += 3
+                    continue
             x = m(x)
+            i += 1
         return x
 
 

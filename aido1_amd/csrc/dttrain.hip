@@ -1,0 +1,367 @@
+// The fused training-mode tail of a conv block (bias + LeakyReLU + BatchNorm
+// with batch statistics) for the DDPG update: see include/dttrain.h.
+//
+// Each kernel is one grid-stride pass over the NHWC f32 activation, one
+// float4 (4 channels of one pixel) per thread and step: 1024 threads (16
+// waves, one workgroup a CU) cover 128 pixels a step and a thread always holds
+// the same 4 channels (tid & 7).  At most 256 workgroups, so the last one
+// merges at most 256 partials a channel: 32 threads a channel, 8 each.
+// The per-channel reductions are per-thread partials -> the workgroup's (via
+// LDS) -> global partials; the workgroup that finishes last (a counter in the
+// scratch, reset by that workgroup) merges them and writes the channel
+// results, so no second launch and no host round trip is needed.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/dttrain.h"
+
+namespace {
+
+constexpr int C = 32;          // channels (every conv of config.json's actor / critic)
+constexpr int kT = 1024;       // threads a workgroup
+constexpr int kSlots = kT / 8; // pixels a workgroup step covers
+constexpr int kMaxGrid = 256;
+constexpr int kFin = kT / C;   // threads a channel in the final merge
+constexpr int kCounters = 16;  // floats at the end of the scratch holding the counters
+
+int grid_of(int64_t m) {
+  const int64_t q = m * 8;                           // float4 items
+  int64_t g = (q + 2 * kT - 1) / (2 * kT);           // >= 2 items a thread
+  if (g < 1) g = 1;
+  if (g > kMaxGrid) g = kMaxGrid;
+  return (int)g;
+}
+
+// Chan et al.: merge (nb, mb, m2b) into (n, mean, m2)
+__device__ __forceinline__ void chan(float& n, float& mean, float& m2, float nb, float mb,
+                                     float m2b) {
+  if (nb <= 0.0f) return;
+  const float tot = n + nb;
+  const float d = mb - mean;
+  const float f = nb / tot;
+  mean += d * f;
+  m2 += m2b + d * d * n * f;
+  n = tot;
+}
+
+// Partials cross workgroups (and XCDs, whose L2s are not coherent): they are
+// written through to memory (agent-scope relaxed atomic stores: `sc1`, the
+// line leaves the XCD's L2) and read back the same way by the last arriver,
+// so no release fence has to write back the L2 full of this launch's
+// activations (MI355X_MICROARCH.md, inter-workgroup visibility).
+__device__ __forceinline__ void st_wt(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ float ld_wt(const float* p) {
+  return __hip_atomic_load(const_cast<float*>(p), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// true for the workgroup that arrives last at `counter` (which it resets);
+// every workgroup's write-through partials have landed before it arrives
+__device__ bool last_arrival(unsigned int* counter) {
+  __shared__ bool last;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned int old =
+        __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    last = old == gridDim.x - 1;
+    if (last) __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  return last;
+}
+
+__device__ __forceinline__ float4 ld4(const float* p, int64_t q) {
+  return reinterpret_cast<const float4*>(p)[q];
+}
+__device__ __forceinline__ void st4(float* p, int64_t q, float4 v) {
+  reinterpret_cast<float4*>(p)[q] = v;
+}
+
+// ---- forward 1: a = leaky(z + bias) and the batch statistics of a --------------------
+__global__ void __launch_bounds__(kT)
+bn_stats_kernel(int64_t m, const float* __restrict__ z, const float* __restrict__ bias, float slope,
+                float eps, float momentum, float* __restrict__ running_mean,
+                float* __restrict__ running_var, int64_t* __restrict__ nbt,
+                float* __restrict__ a, float* __restrict__ mean_invstd,
+                float* __restrict__ work) {
+  __shared__ float red[kSlots][C][3];
+  const int tid = threadIdx.x, cg = tid & 7, slot = tid >> 3;
+  const float4 b = ld4(bias, cg);
+  float n = 0.0f, mean[4] = {0, 0, 0, 0}, m2[4] = {0, 0, 0, 0};
+  const int64_t items = m * 8, stride = (int64_t)gridDim.x * kT;
+  for (int64_t q = (int64_t)blockIdx.x * kT + tid; q < items; q += stride) {
+    const float4 v = ld4(z, q);
+    float x[4] = {v.x + b.x, v.y + b.y, v.z + b.z, v.w + b.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) x[k] = x[k] > 0.0f ? x[k] : x[k] * slope;
+    st4(a, q, make_float4(x[0], x[1], x[2], x[3]));
+    n += 1.0f;
+    const float inv = 1.0f / n;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float d = x[k] - mean[k];
+      mean[k] += d * inv;
+      m2[k] += d * (x[k] - mean[k]);
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    red[slot][4 * cg + k][0] = n;
+    red[slot][4 * cg + k][1] = mean[k];
+    red[slot][4 * cg + k][2] = m2[k];
+  }
+  __syncthreads();
+  float* part = work;   // [grid][C][3]
+  // 128 slots a channel: kFin threads a channel merge 4 each, then one thread
+  __shared__ float red2[kFin][C][3];
+  {
+    const int ch = tid & (C - 1), j = tid / C;
+    float cn = 0.0f, cm = 0.0f, cm2 = 0.0f;
+    for (int s = j; s < kSlots; s += kFin) chan(cn, cm, cm2, red[s][ch][0], red[s][ch][1], red[s][ch][2]);
+    red2[j][ch][0] = cn;
+    red2[j][ch][1] = cm;
+    red2[j][ch][2] = cm2;
+  }
+  __syncthreads();
+  if (tid < C) {
+    float cn = 0.0f, cm = 0.0f, cm2 = 0.0f;
+    for (int s = 0; s < kFin; ++s) chan(cn, cm, cm2, red2[s][tid][0], red2[s][tid][1], red2[s][tid][2]);
+    float* p = part + ((size_t)blockIdx.x * C + tid) * 3;
+    st_wt(p, cn);
+    st_wt(p + 1, cm);
+    st_wt(p + 2, cm2);
+  }
+  unsigned int* counters = reinterpret_cast<unsigned int*>(work + (size_t)kMaxGrid * C * 3);
+  if (!last_arrival(&counters[0])) return;
+  // the last workgroup: kFin threads a channel over the partials, then one
+  {
+    const int ch = tid & (C - 1), j = tid / C;
+    float cn = 0.0f, cm = 0.0f, cm2 = 0.0f;
+    constexpr int kPer = kMaxGrid / kFin;   // 8: all loads issued before the merges
+    float pn[kPer], pm[kPer], pq[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int g = j + k * kFin;
+      const float* p = part + ((size_t)(g < (int)gridDim.x ? g : 0) * C + ch) * 3;
+      pn[k] = g < (int)gridDim.x ? ld_wt(p) : 0.0f;
+      pm[k] = ld_wt(p + 1);
+      pq[k] = ld_wt(p + 2);
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) chan(cn, cm, cm2, pn[k], pm[k], pq[k]);
+    red2[j][ch][0] = cn;
+    red2[j][ch][1] = cm;
+    red2[j][ch][2] = cm2;
+  }
+  __syncthreads();
+  if (tid < C) {
+    float cn = 0.0f, cm = 0.0f, cm2 = 0.0f;
+    for (int s = 0; s < kFin; ++s) chan(cn, cm, cm2, red2[s][tid][0], red2[s][tid][1], red2[s][tid][2]);
+    const float var = cm2 / cn;                       // biased: the normalisation
+    mean_invstd[tid] = cm;
+    mean_invstd[C + tid] = 1.0f / sqrtf(var + eps);
+    const float unbiased = cn > 1.0f ? cm2 / (cn - 1.0f) : var;
+    running_mean[tid] = (1.0f - momentum) * running_mean[tid] + momentum * cm;
+    running_var[tid] = (1.0f - momentum) * running_var[tid] + momentum * unbiased;
+    if (tid == 0 && nbt) nbt[0] += 1;
+  }
+}
+
+// ---- forward 2: y = (a - mean) * invstd * gamma + beta -------------------------------
+__global__ void __launch_bounds__(kT)
+bn_apply_kernel(int64_t m, const float* __restrict__ a, const float* __restrict__ mean_invstd,
+                const float* __restrict__ gamma, const float* __restrict__ beta,
+                float* __restrict__ y) {
+  const int cg = threadIdx.x & 7;
+  const float4 mu = ld4(mean_invstd, cg), is = ld4(mean_invstd + C, cg);
+  const float4 g = ld4(gamma, cg), bt = ld4(beta, cg);
+  const float4 sc = make_float4(is.x * g.x, is.y * g.y, is.z * g.z, is.w * g.w);
+  const int64_t items = m * 8, stride = (int64_t)gridDim.x * kT;
+  for (int64_t q = (int64_t)blockIdx.x * kT + threadIdx.x; q < items; q += stride) {
+    const float4 v = ld4(a, q);
+    st4(y, q, make_float4((v.x - mu.x) * sc.x + bt.x, (v.y - mu.y) * sc.y + bt.y,
+                          (v.z - mu.z) * sc.z + bt.z, (v.w - mu.w) * sc.w + bt.w));
+  }
+}
+
+// sums of kN per-channel values over the workgroup's threads -> part[block][C][kN]
+template <int kN>
+__device__ void block_sums(float (&acc)[kN][4], float* __restrict__ part) {
+  __shared__ float red[kSlots][C][kN];
+  __shared__ float red2[kFin][C][kN];
+  const int tid = threadIdx.x, cg = tid & 7, slot = tid >> 3;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+#pragma unroll
+    for (int j = 0; j < kN; ++j) red[slot][4 * cg + k][j] = acc[j][k];
+  __syncthreads();
+  {
+    const int ch = tid & (C - 1), q = tid / C;
+#pragma unroll
+    for (int j = 0; j < kN; ++j) {
+      float t = 0.0f;
+      for (int sl = q; sl < kSlots; sl += kFin) t += red[sl][ch][j];
+      red2[q][ch][j] = t;
+    }
+  }
+  __syncthreads();
+  if (tid < C) {
+#pragma unroll
+    for (int j = 0; j < kN; ++j) {
+      float t = 0.0f;
+      for (int q = 0; q < kFin; ++q) t += red2[q][tid][j];
+      st_wt(part + ((size_t)blockIdx.x * C + tid) * kN + j, t);
+    }
+  }
+}
+
+// the last workgroup: per-channel totals of the kN partial columns -> out[j][C]
+template <int kN>
+__device__ void final_sums(const float* __restrict__ part, float* const (&out)[kN]) {
+  __shared__ float red[kFin][C][kN];
+  const int tid = threadIdx.x, ch = tid & (C - 1), q = tid / C;
+  float s[kN];
+#pragma unroll
+  for (int j = 0; j < kN; ++j) s[j] = 0.0f;
+  constexpr int kPer = kMaxGrid / kFin;   // 8: all loads issued before the sums
+  float v[kPer][kN];
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int g = q + k * kFin;
+#pragma unroll
+    for (int j = 0; j < kN; ++j)
+      v[k][j] = g < (int)gridDim.x ? ld_wt(part + ((size_t)g * C + ch) * kN + j) : 0.0f;
+  }
+#pragma unroll
+  for (int k = 0; k < kPer; ++k)
+#pragma unroll
+    for (int j = 0; j < kN; ++j) s[j] += v[k][j];
+#pragma unroll
+  for (int j = 0; j < kN; ++j) red[q][ch][j] = s[j];
+  __syncthreads();
+  if (tid < C) {
+#pragma unroll
+    for (int j = 0; j < kN; ++j) {
+      float t = 0.0f;
+      for (int k = 0; k < kFin; ++k) t += red[k][tid][j];
+      out[j][tid] = t;
+    }
+  }
+}
+
+// ---- backward 1: dbeta = sum(dy), dgamma = sum(dy * xhat) ---------------------------
+__global__ void __launch_bounds__(kT)
+bn_bwd_reduce_kernel(int64_t m, const float* __restrict__ dy, const float* __restrict__ a,
+                     const float* __restrict__ mean_invstd, float* __restrict__ dgamma,
+                     float* __restrict__ dbeta, float* __restrict__ work) {
+  const int cg = threadIdx.x & 7;
+  const float4 mu = ld4(mean_invstd, cg), is = ld4(mean_invstd + C, cg);
+  const float mus[4] = {mu.x, mu.y, mu.z, mu.w}, iss[4] = {is.x, is.y, is.z, is.w};
+  float acc[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
+  const int64_t items = m * 8, stride = (int64_t)gridDim.x * kT;
+  for (int64_t q = (int64_t)blockIdx.x * kT + threadIdx.x; q < items; q += stride) {
+    const float4 g4 = ld4(dy, q), a4 = ld4(a, q);
+    const float g[4] = {g4.x, g4.y, g4.z, g4.w}, x[4] = {a4.x, a4.y, a4.z, a4.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      acc[0][k] += g[k];
+      acc[1][k] += g[k] * ((x[k] - mus[k]) * iss[k]);
+    }
+  }
+  block_sums<2>(acc, work);
+  unsigned int* counters = reinterpret_cast<unsigned int*>(work + (size_t)kMaxGrid * C * 3);
+  if (!last_arrival(&counters[1])) return;
+  float* const out[2] = {dbeta, dgamma};
+  final_sums<2>(work, out);
+}
+
+// ---- backward 2: dz, and dbias = sum(dz) ----------------------------------------------
+__global__ void __launch_bounds__(kT)
+bn_bwd_apply_kernel(int64_t m, const float* __restrict__ dy, const float* __restrict__ a,
+                    const float* __restrict__ mean_invstd, const float* __restrict__ gamma,
+                    const float* __restrict__ dgamma, const float* __restrict__ dbeta, float slope,
+                    float* __restrict__ dz, float* __restrict__ dbias, float* __restrict__ work) {
+  const int cg = threadIdx.x & 7;
+  const float inv_m = 1.0f / (float)m;
+  float mu[4], is[4], k1[4], k2[4], k3[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int c = 4 * cg + k;
+    mu[k] = mean_invstd[c];
+    is[k] = mean_invstd[C + c];
+    k1[k] = gamma[c] * is[k];          // da = k1 * (dy - k2 - xhat * k3)
+    k2[k] = dbeta[c] * inv_m;
+    k3[k] = dgamma[c] * inv_m;
+  }
+  float acc[1][4] = {{0, 0, 0, 0}};
+  const int64_t items = m * 8, stride = (int64_t)gridDim.x * kT;
+  for (int64_t q = (int64_t)blockIdx.x * kT + threadIdx.x; q < items; q += stride) {
+    const float4 g4 = ld4(dy, q), a4 = ld4(a, q);
+    const float g[4] = {g4.x, g4.y, g4.z, g4.w}, x[4] = {a4.x, a4.y, a4.z, a4.w};
+    float o[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const float xh = (x[k] - mu[k]) * is[k];
+      const float da = k1[k] * (g[k] - k2[k] - xh * k3[k]);
+      o[k] = x[k] > 0.0f ? da : da * slope;
+      acc[0][k] += o[k];
+    }
+    st4(dz, q, make_float4(o[0], o[1], o[2], o[3]));
+  }
+  float* part = work + (size_t)kMaxGrid * C * 2;   // beside backward 1's partials
+  block_sums<1>(acc, part);
+  unsigned int* counters = reinterpret_cast<unsigned int*>(work + (size_t)kMaxGrid * C * 3);
+  if (!last_arrival(&counters[2])) return;
+  float* const out[1] = {dbias};
+  final_sums<1>(part, out);
+}
+
+bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
+
+}  // namespace
+
+extern "C" {
+
+int64_t dt_train_work_floats(int64_t m) {
+  (void)m;
+  return (int64_t)kMaxGrid * C * 3 + kCounters;
+}
+
+int dt_bn_leaky_fwd(int64_t m, const float* z, const float* bias, float slope, const float* gamma,
+                    const float* beta, float eps, float momentum, float* running_mean,
+                    float* running_var, int64_t* num_batches_tracked, float* a, float* y,
+                    float* mean_invstd, float* work, void* stream) {
+  if (m < 1 || !z || !bias || !gamma || !beta || !running_mean || !running_var || !a || !y ||
+      !mean_invstd || !work)
+    return DT_E_ARG;
+  if (!aligned16(z) || !aligned16(a) || !aligned16(y) || !aligned16(bias) ||
+      !aligned16(mean_invstd) || !aligned16(gamma) || !aligned16(beta))
+    return DT_E_ARG;
+  const int g = grid_of(m);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(bn_stats_kernel, dim3(g), dim3(kT), 0, s, m, z, bias, slope, eps, momentum,
+                     running_mean, running_var, num_batches_tracked, a, mean_invstd, work);
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(g), dim3(kT), 0, s, m, a, mean_invstd, gamma, beta, y);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
+int dt_bn_leaky_bwd(int64_t m, const float* dy, const float* a, const float* mean_invstd,
+                    const float* gamma, float slope, float* dz, float* dbias, float* dgamma,
+                    float* dbeta, float* work, void* stream) {
+  if (m < 1 || !dy || !a || !mean_invstd || !gamma || !dz || !dbias || !dgamma || !dbeta || !work)
+    return DT_E_ARG;
+  if (!aligned16(dy) || !aligned16(a) || !aligned16(dz) || !aligned16(mean_invstd))
+    return DT_E_ARG;
+  const int g = grid_of(m);
+  hipStream_t s = (hipStream_t)stream;
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(g), dim3(kT), 0, s, m, dy, a, mean_invstd, dgamma,
+                     dbeta, work);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(g), dim3(kT), 0, s, m, dy, a, mean_invstd, gamma,
+                     dgamma, dbeta, slope, dz, dbias, work);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
+}  // extern "C"

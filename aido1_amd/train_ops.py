@@ -1,0 +1,91 @@
+"""The fused conv-block tail of the DDPG update (include/dttrain.h).
+
+Every conv block of config.json's actor and critic is conv_2d -> leaky_relu
+-> batch_norm_2d (models/ddpg/modules.py MetaNet), and the trainer runs all
+four networks in train mode (training/trainers.py:143-237).  On the GPU in
+float32 with channels_last activations, ``conv_leaky_bn`` runs the
+convolution without its bias (MIOpen) and then dt_bn_leaky_fwd: bias,
+LeakyReLU, the batch statistics, the running-statistics update and
+num_batches_tracked in one kernel, the normalisation in a second; its
+backward is dt_bn_leaky_bwd (two kernels for BatchNorm's, LeakyReLU's and the
+bias's gradients).  torch runs eight kernels for the forward tail and five for
+the backward.  The modules, parameters and state_dict are the unchanged
+torch ones; ``applicable`` says when the fused tail replaces them.
+"""
+import ctypes
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from aido1_amd import _lib
+
+C = 32
+
+
+def applicable(x, conv, act, bn):
+    return (x.is_cuda and x.dtype == torch.float32 and bn.training and bn.track_running_stats
+            and bn.affine and bn.momentum is not None and bn.running_mean is not None
+            and conv.bias is not None and conv.out_channels == C and conv.groups == 1
+            and tuple(conv.padding) == (0, 0) and tuple(conv.dilation) == (1, 1)
+            and isinstance(act, nn.LeakyReLU) and bn.num_features == C
+            and conv.weight.dtype == torch.float32)
+
+
+def _work(bn, key, dev):
+    """A scratch buffer per BatchNorm and direction, zeroed once (the kernels
+    leave their counters at zero): plain attributes, not state."""
+    name = '_dt_work_' + key
+    w = getattr(bn, name, None)
+    if w is None or w.device != dev:
+        w = torch.zeros(int(_lib.lib().dt_train_work_floats(0)), device=dev)
+        setattr(bn, name, w)
+    return w
+
+
+def _stream(dev):
+    return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+class _BnLeaky(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z, bias, gamma, beta, bn, slope):
+        L = _lib.lib()
+        m = z.numel() // C
+        a = torch.empty_like(z)
+        y = torch.empty_like(z)
+        mi = torch.empty(2 * C, device=z.device)
+        nbt = bn.num_batches_tracked
+        rc = L.dt_bn_leaky_fwd(m, z.data_ptr(), bias.data_ptr(), slope, gamma.data_ptr(),
+                               beta.data_ptr(), bn.eps, bn.momentum, bn.running_mean.data_ptr(),
+                               bn.running_var.data_ptr(),
+                               nbt.data_ptr() if nbt is not None else None, a.data_ptr(),
+                               y.data_ptr(), mi.data_ptr(), _work(bn, 'fwd', z.device).data_ptr(),
+                               _stream(z.device))
+        if rc != 0:
+            raise _lib.DtError('dt_bn_leaky_fwd failed (%d)' % rc)
+        ctx.save_for_backward(a, mi, gamma)
+        ctx.bn, ctx.slope = bn, slope
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        a, mi, gamma = ctx.saved_tensors
+        dy = dy.contiguous(memory_format=torch.channels_last)
+        L = _lib.lib()
+        dz = torch.empty_like(a)
+        g = torch.empty(3, C, device=a.device)      # dbias, dgamma, dbeta
+        rc = L.dt_bn_leaky_bwd(a.numel() // C, dy.data_ptr(), a.data_ptr(), mi.data_ptr(),
+                               gamma.data_ptr(), ctx.slope, dz.data_ptr(), g[0].data_ptr(),
+                               g[1].data_ptr(), g[2].data_ptr(),
+                               _work(ctx.bn, 'bwd', a.device).data_ptr(), _stream(a.device))
+        if rc != 0:
+            raise _lib.DtError('dt_bn_leaky_bwd failed (%d)' % rc)
+        return dz, g[0], g[1], g[2], None, None
+
+
+def conv_leaky_bn(x, conv, act, bn):
+    """bn(act(conv(x))) for a train-mode block (see the module docstring)."""
+    z = F.conv2d(x, conv.weight, None, conv.stride)
+    z = z.contiguous(memory_format=torch.channels_last)
+    return _BnLeaky.apply(z, conv.bias, bn.weight, bn.bias, bn, float(act.negative_slope))

@@ -1,0 +1,73 @@
+/* dttrain.h — C-ABI of the fused training-mode layer tail of the DDPG update
+ * (BASELINE configs[4]).
+ *
+ * Every conv block of the reference's actor and critic is conv_2d ->
+ * leaky_relu -> batch_norm_2d (config.json:19-170, models/ddpg/modules.py
+ * MetaNet), and every network is in train mode during the update
+ * (training/trainers.py:143-237, managers.py:264-268): BatchNorm normalises
+ * with the batch statistics and updates its running statistics.  These two
+ * calls replace, per block, torch's bias add, LeakyReLU, BatchNorm (MIOpen's
+ * three kernels) and num_batches_tracked increment in the forward, and
+ * BatchNorm's backward, LeakyReLU's backward and the bias-gradient reduction
+ * in the backward: two kernels each way (aido1_amd/csrc/dttrain.hip).  The
+ * convolution itself stays MIOpen's (called without bias).
+ *
+ * Layout: NHWC float32 (torch channels_last), m = N*H*W pixels of exactly 32
+ * channels.  Per-channel reductions run per workgroup (Welford for the
+ * statistics, plain f32 sums in the backward) and the last workgroup to
+ * finish merges the partials (Chan's formula) and writes the per-channel
+ * results, so one launch does the whole reduction.
+ *
+ *   work   device scratch, dt_train_work_floats(m) floats, zeroed ONCE before
+ *          its first use (the kernels leave their counters at zero again); one
+ *          buffer per call site in flight (a forward and a backward of the
+ *          same layer may not share one).
+ *
+ * Conventions as dtsim.h: 0 or a negative DT_E_* code; device pointers; work
+ * goes on `stream` (a hipStream_t).
+ */
+#ifndef AIDO1_AMD_DTTRAIN_H
+#define AIDO1_AMD_DTTRAIN_H
+
+#include <stdint.h>
+
+#include "dtsim.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+int64_t dt_train_work_floats(int64_t m);
+
+/* Forward: a = leaky_relu(z + bias, slope); y = (a - mean) * invstd * gamma +
+ * beta with the batch mean and biased variance of a over the m pixels
+ * (invstd = 1 / sqrt(var + eps)); running_mean / running_var move by
+ * `momentum` towards mean and the unbiased variance, num_batches_tracked += 1
+ * (torch.nn.BatchNorm2d.forward in train mode).
+ *   z, a, y            device f32 [m, 32]
+ *   bias, gamma, beta  device f32 [32]
+ *   running_mean, running_var  device f32 [32], updated in place
+ *   num_batches_tracked        device int64 [1] or NULL
+ *   mean_invstd        device f32 [64] out: mean[32] then invstd[32] (saved
+ *                      for the backward) */
+int dt_bn_leaky_fwd(int64_t m, const float* z, const float* bias, float slope, const float* gamma,
+                    const float* beta, float eps, float momentum, float* running_mean,
+                    float* running_var, int64_t* num_batches_tracked, float* a, float* y,
+                    float* mean_invstd, float* work, void* stream);
+
+/* Backward of dt_bn_leaky_fwd given dy (device f32 [m, 32]):
+ *   dgamma = sum(dy * xhat), dbeta = sum(dy), xhat = (a - mean) * invstd;
+ *   da = gamma * invstd * (dy - dbeta / m - xhat * dgamma / m);
+ *   dz = a > 0 ? da : slope * da  (LeakyReLU's backward: a > 0 iff z + bias > 0);
+ *   dbias = sum(dz).
+ *   dz            device f32 [m, 32] out
+ *   dbias, dgamma, dbeta  device f32 [32] out (overwritten) */
+int dt_bn_leaky_bwd(int64_t m, const float* dy, const float* a, const float* mean_invstd,
+                    const float* gamma, float slope, float* dz, float* dbias, float* dgamma,
+                    float* dbeta, float* work, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* AIDO1_AMD_DTTRAIN_H */

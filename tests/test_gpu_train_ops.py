@@ -1,0 +1,94 @@
+"""The fused conv-block tail of the DDPG update (include/dttrain.h,
+aido1_amd/train_ops.py) against float64 torch: bias + LeakyReLU + train-mode
+BatchNorm forward (outputs, running statistics, num_batches_tracked) and its
+backward (input, bias, gamma and beta gradients); then whole networks with
+and without it.  float32 kernels against float64 math: rtol 1e-4 / atol 1e-5
+on outputs, 1e-4 relative to the largest element on gradients (reductions of
+up to 281k terms in a different order)."""
+import copy
+
+import pytest
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from conftest import golden
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_tail(z, bias, bn, slope):
+    a = F.leaky_relu(z + bias.view(1, -1, 1, 1), slope)
+    return F.batch_norm(a, bn.running_mean, bn.running_var, bn.weight, bn.bias, True,
+                        bn.momentum, bn.eps)
+
+
+@pytest.mark.parametrize('shape', [(64, 32, 57, 77), (64, 32, 9, 14), (3, 32, 5, 7)])
+def test_bn_leaky_tail_matches_float64(gpu, shape):
+    from aido1_amd.train_ops import _BnLeaky
+    torch.manual_seed(sum(shape))
+    cl = torch.channels_last
+    z = (torch.randn(shape, device=gpu) * 2 + 0.3).contiguous(memory_format=cl)
+    bias = torch.randn(32, device=gpu) * 0.5
+    bn = nn.BatchNorm2d(32).to(gpu)
+    with torch.no_grad():
+        bn.weight.uniform_(0.5, 1.5)
+        bn.bias.uniform_(-0.5, 0.5)
+        bn.running_mean.uniform_(-1, 1)
+        bn.running_var.uniform_(0.5, 2)
+    ref_bn = copy.deepcopy(bn).double()
+    dy = torch.randn(shape, device=gpu).contiguous(memory_format=cl)
+
+    zl = z.clone().requires_grad_(True)
+    bl = bias.clone().requires_grad_(True)
+    y = _BnLeaky.apply(zl, bl, bn.weight, bn.bias, bn, 0.01)
+    y.backward(dy)
+
+    zr = z.double().requires_grad_(True)
+    br = bias.double().requires_grad_(True)
+    yr = _ref_tail(zr, br, ref_bn, 0.01)
+    yr.backward(dy.double())
+
+    torch.testing.assert_close(y.double(), yr.detach(), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(bn.running_mean.double(), ref_bn.running_mean, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(bn.running_var.double(), ref_bn.running_var, rtol=1e-5, atol=1e-6)
+    assert int(bn.num_batches_tracked) == 1
+    for got, want in ((zl.grad, zr.grad), (bl.grad, br.grad), (bn.weight.grad, ref_bn.weight.grad),
+                      (bn.bias.grad, ref_bn.bias.grad)):
+        scale = want.abs().max().item()
+        assert (got.double() - want).abs().max().item() <= 1e-4 * scale + 1e-6
+
+
+@pytest.mark.parametrize('kind', ['actor', 'critic'])
+def test_networks_with_and_without_fused_tail(gpu, kind):
+    """A config.json actor / critic in train mode, f32 channels_last, batch 64:
+    forward, every parameter gradient and the BatchNorm running statistics
+    with the fused tail match torch's modules."""
+    from aido1_amd.actor import ConfigActor, ConfigCritic, _Seq
+    cfg = golden('reference_config.json')['model']
+    torch.manual_seed(4)
+    net = (ConfigActor(cfg['actor']) if kind == 'actor' else ConfigCritic(cfg['critic']))
+    for m in net.modules():
+        if isinstance(m, nn.Dropout):
+            m.p = 0.0
+    net = net.to(gpu).to(memory_format=torch.channels_last).train()
+    ref = copy.deepcopy(net)
+    x = torch.rand(64, 3, 120, 160, device=gpu).contiguous(memory_format=torch.channels_last)
+    args = (x,) if kind == 'actor' else (x, torch.rand(64, 2, device=gpu))
+    try:
+        _Seq.fused_tail = False
+        out_ref = ref(*args)
+        out_ref.square().mean().backward()
+    finally:
+        _Seq.fused_tail = True
+    out = net(*args)
+    out.square().mean().backward()
+    torch.testing.assert_close(out, out_ref, rtol=1e-4, atol=1e-5)
+    for (name, p), (_, q) in zip(net.named_parameters(), ref.named_parameters()):
+        scale = q.grad.abs().max().item()
+        assert (p.grad - q.grad).abs().max().item() <= 2e-4 * scale + 1e-7, name
+    for (name, b), (_, c) in zip(net.named_buffers(), ref.named_buffers()):
+        if b.dtype.is_floating_point:
+            torch.testing.assert_close(b, c, rtol=1e-5, atol=1e-6, msg=name)
+        else:
+            assert torch.equal(b, c), name
