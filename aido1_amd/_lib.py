@@ -153,6 +153,8 @@ def lib():
                                                ctypes.c_float, vp, vp, vp, vp, vp, vp, vp, vp]),
             'dt_bn_leaky_bwd': (ctypes.c_int, [i64, vp, vp, vp, vp, ctypes.c_float, vp, vp, vp, vp,
                                                vp, vp]),
+            'dt_adam': (ctypes.c_int, [i32, vp, vp, vp, vp, f64, f64, f64, vp, vp]),
+            'dt_soft_update': (ctypes.c_int, [i32, vp, vp, f64, vp]),
             # dtactor.h
             'dt_sample_norm': (ctypes.c_int, [vp, vp, i32, i32, i32, vp, vp, ctypes.c_float,
                                               ctypes.c_float, i32, vp]),

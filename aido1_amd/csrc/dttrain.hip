@@ -319,6 +319,59 @@ bn_bwd_apply_kernel(int64_t m, const float* __restrict__ dy, const float* __rest
   final_sums<1>(part, out);
 }
 
+// ---- multi-tensor Adam and soft update -------------------------------------------------
+constexpr int kMtThreads = 256;
+
+__global__ void __launch_bounds__(kMtThreads)
+adam_kernel(const dt_mt_tensor* __restrict__ tensors, const int32_t* __restrict__ chunks,
+            double* __restrict__ step, const double* __restrict__ lr, double beta1, double beta2,
+            double eps, unsigned int* __restrict__ counter) {
+  const dt_mt_tensor t = tensors[chunks[2 * blockIdx.x]];
+  const int64_t start = (int64_t)chunks[2 * blockIdx.x + 1] * DT_MT_CHUNK;
+  const int64_t end = start + DT_MT_CHUNK < t.n ? start + DT_MT_CHUNK : t.n;
+  const double st = *step + 1.0;
+  // torch: step_size = -(lr / (1 - b1^t)), bc2_sqrt = (1 - b2^t)^0.5, Python
+  // doubles passed to float32 element ops
+  const float step_size = (float)(-(*lr / (1.0 - pow(beta1, st))));
+  const float bc2_sqrt = (float)sqrt(1.0 - pow(beta2, st));
+  const float w = (float)(1.0 - beta1), b2 = (float)beta2, ob2 = (float)(1.0 - beta2);
+  const float fe = (float)eps;
+  for (int64_t i = start + threadIdx.x; i < end; i += kMtThreads) {
+    const float g = t.b[i];
+    float m = t.c[i];
+    m = w < 0.5f ? m + w * (g - m) : g - (g - m) * (1.0f - w);          // lerp
+    float v = t.d[i] * b2;                                              // mul_
+    v = v + ob2 * g * g;                                                // addcmul_
+    const float den = sqrtf(v) / bc2_sqrt + fe;                         // sqrt, div_, add_
+    t.a[i] = t.a[i] + step_size * (m / den);                            // addcdiv_
+    t.c[i] = m;
+    t.d[i] = v;
+  }
+  // the step count moves once every workgroup has read it
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned int old =
+        __hip_atomic_fetch_add(counter, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (old == gridDim.x - 1) {
+      __hip_atomic_store(counter, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(step, st, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kMtThreads)
+soft_update_kernel(const dt_mt_tensor* __restrict__ tensors, const int32_t* __restrict__ chunks,
+                   float keep, float tau) {
+  const dt_mt_tensor t = tensors[chunks[2 * blockIdx.x]];
+  const int64_t start = (int64_t)chunks[2 * blockIdx.x + 1] * DT_MT_CHUNK;
+  const int64_t end = start + DT_MT_CHUNK < t.n ? start + DT_MT_CHUNK : t.n;
+  for (int64_t i = start + threadIdx.x; i < end; i += kMtThreads) {
+    const float x = t.a[i] * keep;
+    const float y = t.b[i] * tau;
+    t.a[i] = x + y;
+  }
+}
+
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace
@@ -361,6 +414,27 @@ int dt_bn_leaky_bwd(int64_t m, const float* dy, const float* a, const float* mea
                      dbeta, work);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(g), dim3(kT), 0, s, m, dy, a, mean_invstd, gamma,
                      dgamma, dbeta, slope, dz, dbias, work);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
+int dt_adam(int32_t n_chunks, const dt_mt_tensor* tensors, const int32_t* chunks, double* step,
+            const double* lr, double beta1, double beta2, double eps, uint32_t* counter,
+            void* stream) {
+  if (n_chunks < 0 || (n_chunks > 0 && (!tensors || !chunks || !step || !lr || !counter)))
+    return DT_E_ARG;
+  if (n_chunks == 0) return DT_OK;
+  hipLaunchKernelGGL(adam_kernel, dim3(n_chunks), dim3(kMtThreads), 0, (hipStream_t)stream,
+                     tensors, chunks, step, lr, beta1, beta2, eps, counter);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
+int dt_soft_update(int32_t n_chunks, const dt_mt_tensor* tensors, const int32_t* chunks,
+                   double tau, void* stream) {
+  if (n_chunks < 0 || (n_chunks > 0 && (!tensors || !chunks))) return DT_E_ARG;
+  if (n_chunks == 0) return DT_OK;
+  // torch: target * (1.0 - tau) + param * tau with the Python doubles as float32 scalars
+  hipLaunchKernelGGL(soft_update_kernel, dim3(n_chunks), dim3(kMtThreads), 0, (hipStream_t)stream,
+                     tensors, chunks, (float)(1.0 - tau), (float)tau);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 

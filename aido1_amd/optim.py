@@ -2,10 +2,14 @@
 (training/trainers.py:258-268): "adam" (torch Adam, lr set per step by the
 decay), "adamw" (models/adamw.py: Adam followed by p -= p * lr * wd), "sgd"
 (momentum 0.9, weight decay 1e-4).  All start at lr 0 as the reference's."""
+import ctypes
 import math
 
+import numpy as np
 import torch
 from torch.optim.optimizer import Optimizer
+
+MT_CHUNK = 4096       # DT_MT_CHUNK (include/dttrain.h)
 
 
 class AdamW(Optimizer):
@@ -57,12 +61,144 @@ def float64_steps(opt):
     return opt
 
 
+class MultiTensorTable:
+    """Device tables for include/dttrain.h's multi-tensor kernels: one
+    dt_mt_tensor row (up to four float32 tensors of n elements, same strides)
+    per entry and the (tensor, chunk) pairs, one workgroup per DT_MT_CHUNK
+    elements.  Built eagerly (an H2D copy), so before any graph capture."""
+
+    ROW = np.dtype([('a', '<u8'), ('b', '<u8'), ('c', '<u8'), ('d', '<u8'), ('n', '<i8')])
+
+    def __init__(self, rows, device):
+        tab = np.zeros(len(rows), self.ROW)
+        chunks = []
+        for i, r in enumerate(rows):
+            ptrs = [t.data_ptr() for t in r] + [0] * (4 - len(r))
+            n = r[0].numel()
+            tab[i] = tuple(ptrs) + (n,)
+            chunks += [(i, c) for c in range((n + MT_CHUNK - 1) // MT_CHUNK)]
+        self.key = self.key_of(rows)
+        self.tensors = torch.from_numpy(tab.view(np.uint8).copy()).to(device)
+        self.chunks = torch.tensor(chunks, dtype=torch.int32, device=device).reshape(-1)
+        self.n_chunks = len(chunks)
+
+    @staticmethod
+    def key_of(rows):
+        return tuple(t.data_ptr() for r in rows for t in r)
+
+    @staticmethod
+    def fits(rows):
+        """float32 CUDA tensors, dense, each row's tensors with the same strides."""
+        for r in rows:
+            t0 = r[0]
+            for t in r:
+                if (not t.is_cuda or t.dtype != torch.float32 or t.stride() != t0.stride()
+                        or t.shape != t0.shape or not (
+                            t.is_contiguous() or (t.dim() == 4 and t.is_contiguous(
+                                memory_format=torch.channels_last)))):
+                    return False
+        return True
+
+
+class DeviceAdam(torch.optim.Adam):
+    """Capturable torch Adam whose step is ONE dt_adam launch over all
+    parameters (include/dttrain.h) instead of torch's ~10 foreach kernels
+    plus a per-parameter division for the float64 bias corrections.  The
+    state is torch's (exp_avg, exp_avg_sq per parameter; one shared float64
+    step tensor), so state_dict / load_state_dict are Adam's.  The lr is a
+    float64 device tensor, set with fill_ (TrainingDecay).  Falls back to
+    torch's step for anything dt_adam does not cover (CPU, non-float32,
+    weight decay, amsgrad, maximize)."""
+
+    def __init__(self, params, device):
+        super().__init__(params, lr=torch.tensor(0.0, dtype=torch.float64, device=device),
+                         capturable=True, foreach=True)
+        self._step_t = torch.zeros((), dtype=torch.float64, device=device)
+        self._counter = torch.zeros(1, dtype=torch.int32, device=device)
+        for group in self.param_groups:
+            for p in group['params']:
+                st = self.state[p]
+                st['step'] = self._step_t
+                st['exp_avg'] = torch.zeros_like(p, memory_format=torch.preserve_format)
+                st['exp_avg_sq'] = torch.zeros_like(p, memory_format=torch.preserve_format)
+        self._table = None
+
+    def _rows(self):
+        rows = []
+        for group in self.param_groups:
+            for p in group['params']:
+                if p.grad is not None:
+                    st = self.state[p]
+                    rows.append((p, p.grad, st['exp_avg'], st['exp_avg_sq']))
+        return rows
+
+    @torch.no_grad()
+    def step(self, closure=None):
+        g = self.param_groups[0]
+        rows = self._rows()
+        if (len(self.param_groups) != 1 or g['weight_decay'] or g['amsgrad'] or g['maximize']
+                or not torch.is_tensor(g['lr']) or not rows or not MultiTensorTable.fits(rows)
+                or any(self.state[r[0]]['step'] is not self._step_t for r in rows)):
+            # torch's step increments every state's step: give each its own
+            for group in self.param_groups:
+                for p in group['params']:
+                    st = self.state[p]
+                    if st.get('step') is self._step_t:
+                        st['step'] = self._step_t.clone()
+            return super().step(closure)
+        if self._table is None or self._table.key != MultiTensorTable.key_of(rows):
+            self._table = MultiTensorTable(rows, self._step_t.device)
+        from aido1_amd import _lib
+        t = self._table
+        b1, b2 = g['betas']
+        rc = _lib.lib().dt_adam(t.n_chunks, t.tensors.data_ptr(), t.chunks.data_ptr(),
+                                self._step_t.data_ptr(), g['lr'].data_ptr(), float(b1), float(b2),
+                                float(g['eps']), self._counter.data_ptr(),
+                                ctypes.c_void_p(torch.cuda.current_stream(self._step_t.device)
+                                                .cuda_stream))
+        if rc != 0:
+            raise _lib.DtError('dt_adam failed (%d)' % rc)
+        return None
+
+
+class SoftUpdate:
+    """models/torch_utils.py:5-9 for a (target, source) module pair: one
+    dt_soft_update launch on the GPU, torch foreach ops otherwise."""
+
+    def __init__(self):
+        self._tables = {}
+
+    @torch.no_grad()
+    def __call__(self, target, source, tau):
+        rows = [(t.data, s.data) for t, s in zip(target.parameters(), source.parameters())]
+        if not rows or not MultiTensorTable.fits(rows):
+            tp = [r[0] for r in rows]
+            a = torch._foreach_mul(tp, 1.0 - tau)
+            b = torch._foreach_mul([r[1] for r in rows], tau)
+            torch._foreach_add_(a, b)
+            torch._foreach_copy_(tp, a)
+            return
+        key = (id(target), id(source))
+        t = self._tables.get(key)
+        if t is None or t.key != MultiTensorTable.key_of(rows):
+            t = self._tables[key] = MultiTensorTable(rows, rows[0][0].device)
+        from aido1_amd import _lib
+        rc = _lib.lib().dt_soft_update(t.n_chunks, t.tensors.data_ptr(), t.chunks.data_ptr(),
+                                       float(tau), ctypes.c_void_p(torch.cuda.current_stream(
+                                           rows[0][0].device).cuda_stream))
+        if rc != 0:
+            raise _lib.DtError('dt_soft_update failed (%d)' % rc)
+
+
 def make_optimizer(kind, params, capturable=False, device=None):
     """capturable: Adam with a device-tensor lr and step counters, so the step
     can live inside a HIP graph (the lr is then set with fill_; float64, so a
     float64 update sees the lr the eager path would)."""
     if kind == 'adam':
         if capturable:
+            dev = torch.device(device) if device is not None else None
+            if dev is not None and dev.type == 'cuda':
+                return DeviceAdam(params, dev)
             return float64_steps(torch.optim.Adam(
                 params, lr=torch.tensor(0.0, dtype=torch.float64, device=device),
                 capturable=True, foreach=True))

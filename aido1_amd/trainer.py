@@ -46,7 +46,7 @@ import torch.nn.functional as F
 
 from aido1_amd.distributed import GradAllReduce, world
 from aido1_amd.explore import create_decay_fn
-from aido1_amd.optim import make_optimizer
+from aido1_amd.optim import SoftUpdate, make_optimizer
 
 
 class TrainingDecay:
@@ -69,15 +69,14 @@ class TrainingDecay:
             self.realization[name] = fn(step)
 
 
+_SOFT = SoftUpdate()
+
+
 def soft_update(target, source, tau):
     """models/torch_utils.py:5-9: t <- t * (1 - tau) + p * tau (two products
-    rounded separately, as the reference's expression)."""
-    tp = [p.data for p in target.parameters()]
-    sp = [p.data for p in source.parameters()]
-    a = torch._foreach_mul(tp, 1.0 - tau)
-    b = torch._foreach_mul(sp, tau)
-    torch._foreach_add_(a, b)
-    torch._foreach_copy_(tp, a)
+    rounded separately, as the reference's expression); one dt_soft_update
+    launch on the GPU (optim.SoftUpdate)."""
+    _SOFT(target, source, tau)
 
 
 def hard_update(target, source):
@@ -162,9 +161,9 @@ class DDPGTrainer:
         grads = torch.autograd.grad(loss, params, allow_unused=True, materialize_grads=True)
         if all(p.grad is not None for p in params):
             torch._foreach_copy_([p.grad for p in params], list(grads))
-        else:
+        else:   # .grad in the parameter's own memory format (DeviceAdam's layout)
             for p, g in zip(params, grads):
-                p.grad = g
+                p.grad = torch.empty_like(p).copy_(g)
 
     # ---- the three stages (trainers.py:156-229) ------------------------------------
     def _fork(self):

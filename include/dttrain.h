@@ -66,6 +66,37 @@ int dt_bn_leaky_bwd(int64_t m, const float* dy, const float* a, const float* mea
                     const float* gamma, float slope, float* dz, float* dbias, float* dgamma,
                     float* dbeta, float* work, void* stream);
 
+/* Multi-tensor steps over a network's parameters in one launch.  `tensors`
+ * is a device table, one entry per parameter (the roles of a, b, c, d per
+ * call below, n elements each, float32); `chunks` a device table of
+ * (tensor index, chunk index) int32 pairs, one workgroup per chunk of
+ * DT_MT_CHUNK elements. */
+#define DT_MT_CHUNK 4096
+typedef struct dt_mt_tensor {
+  float* a;
+  float* b;
+  float* c;
+  float* d;
+  int64_t n;
+} dt_mt_tensor;
+
+/* torch.optim.Adam's step (no weight decay, amsgrad or maximize;
+ * trainers.py:258-268 "adam"), a = param, b = grad, c = exp_avg, d = exp_avg_sq:
+ *   t = *step + 1 (*step is written back by the last workgroup);
+ *   c = lerp(c, b, 1 - beta1); d = d * beta2 + (1 - beta2) * b * b;
+ *   a = a - lr / (1 - beta1^t) * c / (sqrt(d) / sqrt(1 - beta2^t) + eps)
+ * with the bias corrections in float64 from *step and *lr (device float64),
+ * each element op rounded to float32 in torch's order.
+ *   counter  device uint32, zero before the first call (left at zero) */
+int dt_adam(int32_t n_chunks, const dt_mt_tensor* tensors, const int32_t* chunks, double* step,
+            const double* lr, double beta1, double beta2, double eps, uint32_t* counter,
+            void* stream);
+
+/* Soft target update (models/torch_utils.py:5-9), a = target, b = source:
+ * a = a * (1 - tau) + b * tau, the two products rounded separately. */
+int dt_soft_update(int32_t n_chunks, const dt_mt_tensor* tensors, const int32_t* chunks,
+                   double tau, void* stream);
+
 #ifdef __cplusplus
 }
 #endif
