@@ -23,7 +23,7 @@ OUT = 'gpurun_out'
 # label -> (bench config whose PMC passes hold it, kernel-name needles)
 KERNELS = {'step_fan_kernel': ('lane', ['step_fan_kernel']),
            'step_kernel': ('lane', ['step_kernel']),
-           'render_kernel': ('lane', ['render_kernel'])}
+           'render_kernel': ('render', ['render_kernel'])}
 WIDE_READS = set()      # kernels whose reads are 16-B-per-lane streams
 FP64 = ('SQ_INSTS_VALU_ADD_F64', 'SQ_INSTS_VALU_MUL_F64', 'SQ_INSTS_VALU_FMA_F64',
         'SQ_INSTS_VALU_TRANS_F64')

@@ -17,14 +17,14 @@ step() {  # step <name> <timeout> cmd...
   [ $rc -eq 0 ] || { echo "stopping"; exit $rc; }
 }
 declare -A ARGS=(
-  [lane]="--steps $STEPS --warmup 20 --cpu-steps 0"
-  [render]="--config render --steps 100 --warmup 20 --cpu-steps 0"
+  [lane]="--config lane --steps $STEPS --warmup 20 --cpu-steps 0"
+  [render]="--config render --steps 100 --warmup 20 --cpu-steps 0 --no-lane"
   [actor]="--config actor --steps 30 --warmup 5 --cpu-steps 0"
   [train]="--config train --steps 30 --warmup 10 --cpu-steps 0")
 # plain runs first (no profiler): the bench lines DESIGN quotes
 if [ -z "$NO_PLAIN" ]; then
-  step bench_lane_driver 300 python3 "$ROOT/bench.py" --steps 20 --warmup 5
-  step bench_lane_320 300 python3 "$ROOT/bench.py" --steps 320 --warmup 20 --cpu-steps 0
+  step bench_driver 400 python3 "$ROOT/bench.py"
+  step bench_lane_320 300 python3 "$ROOT/bench.py" --config lane --steps 320 --warmup 20 --cpu-steps 0
   for cfg in render actor train; do step "bench_$cfg" 600 python3 "$ROOT/bench.py" ${ARGS[$cfg]}; done
   step bench_actor_eval 600 python3 "$ROOT/bench.py" ${ARGS[actor]} --actor-mode eval
 fi
@@ -35,7 +35,7 @@ done
 declare -A PMC=(
   [FETCH_SIZE]="FETCH_SIZE" [WRITE_SIZE]="WRITE_SIZE"
   [FP64]="SQ_INSTS_VALU_ADD_F64 SQ_INSTS_VALU_MUL_F64 SQ_INSTS_VALU_FMA_F64 SQ_INSTS_VALU_TRANS_F64")
-for cfg in ${PMC_CONFIGS:-lane}; do
+for cfg in ${PMC_CONFIGS:-lane render}; do
   for tag in ${PMC_SETS:-FETCH_SIZE WRITE_SIZE FP64}; do
     step "pmc_${cfg}_$tag" 300 rocprofv3 --pmc ${PMC[$tag]} --output-format csv \
         -d "$ROOT/gpurun_out/pmc_${cfg}_$tag" -o run -- python3 "$ROOT/bench.py" ${ARGS[$cfg]} --no-parity
