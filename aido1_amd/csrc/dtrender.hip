@@ -1300,7 +1300,7 @@ __global__ __launch_bounds__(kThreads) void line_detect_kernel(LineDev L, const 
 // image reaches (counts go negative: a kept line takes back the votes of
 // every pixel it clears, visited or not, as OpenCV does), the mask as bits,
 // the point list in the rest of the LDS (an image with more edge pixels than
-// fit, ~8k at 120 x 160, is flagged: counts[e] = -1).  The random
+// fit, ~16k at 120 x 160, is flagged: counts[e] = -1).  The random
 // order is OpenCV's RNG(~0) multiply-with-carry; oracle/hough_oracle.c
 // restates the same algorithm on the CPU.
 constexpr int kHoughAngles = 180;

@@ -282,7 +282,7 @@ int dt_line_detect(const dt_line_params* p, const uint8_t* bgr, int32_t n, int32
  * within 160 KB of LDS: 120x160 fits); lines device [n, max_lines, 4] i32
  * (x1, y1, x2, y2) in OpenCV's order; counts device [n] i32 = lines found,
  * or -1 when the image had more edge pixels than the kernel's LDS point list
- * holds (~8k at 120x160; the image's lines are then not valid).  One wave per image; runs on the
+ * holds (~16k points at 120x160, of its 19,200 pixels; the image's lines are then not valid).  One wave per image; runs on the
  * current device. */
 int dt_hough_lines(const uint8_t* edge, int32_t n, int32_t height, int32_t width,
                    int32_t threshold, int32_t min_line_length, int32_t max_line_gap,
