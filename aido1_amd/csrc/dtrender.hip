@@ -291,25 +291,29 @@ struct RenderArgs {
 };
 
 // ---- fused render kernel ----------------------------------------------------------
-// One 512-thread workgroup per env, three per CU (LDS <= 53 KB).  The frame is
-// 4-pixel words of raster bytes (img); Canny's work entries exist only for the
-// LISTED words (a word whose 3x3-pixel neighbourhood is not one colour: every
-// other word has Sobel 0 and its masks are its own colour bits).  Phases, a
-// barrier apart:
+// One 512-thread workgroup per env, four per CU (LDS <= 40 KB, <= 64 VGPRs):
+// 16 envs a CU at 4096 envs are exactly four rounds.  The frame is 4-pixel
+// words of raster bytes (img; a palette index in bits 0-2 of each byte);
+// Canny's work entries exist only for the LISTED words (a word whose
+// 3x3-pixel neighbourhood is not one colour: every other word has Sobel 0 and
+// its masks are its own colour bits).  A listed word's slot + 1 lives in the
+// spare bits 3-7 of its own bytes (slot1_of), so no word -> slot map takes
+// LDS.  Phases, a barrier apart:
 //   0a  background of every 16-pixel span decided by its end pixels (uniform:
 //       one 16-B store; otherwise zeroed and listed) + projection of the
 //       marking segments, the visible ones listed
 //   0b  listed spans resolved a word at a time, OR-ed in, beside the markings
 //       drawn with Bresenham, OR-ed in (raster byte encoding, dtrender.h):
 //       order-free, so one pass
-//   1   every 16-pixel quad: neighbourhood uniformity of its 4 words, grey
-//       (float4 stores into the frame ring), masks of all-uniform quads;
-//       non-uniform words get a slot (list + wmap), their quads are listed
-//   2a  listed words: SWAR 3-channel Sobel -> entry (mag | dir)
+//   1   every 16-pixel quad: neighbourhood uniformity of its 4 words;
+//       non-uniform words get a slot (the list)
+//   2a  listed words: SWAR 3-channel Sobel -> entry (mag | dir); the slot + 1
+//       into the word's spare bits
 //   2b  listed words: Canny NMS + double threshold; weak pixels listed
 //   3   hysteresis over the weak list to a fixed point
-//   4   listed quads: colour bits via a v_perm LUT, SWAR ellipse dilation,
-//       edge bits, 16 px per lane, four 16-B stores
+//   4   outputs: grey (float4 stores into the frame ring); masks: colour bits
+//       via a v_perm LUT, for quads with a listed word SWAR ellipse dilation
+//       and edge bits, 16 px per lane, four 16-B stores
 // Slots past list_cap (a frame with more than kListCap non-uniform words:
 // never on the shipped maps) keep their entries in a per-env global spill
 // area; the workgroup then runs the phases' spill instantiation.
@@ -324,24 +328,25 @@ constexpr int WPR = W / 4;          // words per row
 constexpr int NW = NPIX / 4;        // words per image
 constexpr int QPR = WPR / 4;        // 16-pixel quads per row
 constexpr int NQ = NW / 4;          // quads per image (also the background spans)
-constexpr int kListCap = 2048;      // listed words kept in LDS
+constexpr int kListCap = 1984;      // listed words kept in LDS (loop_empty: median 631, max 1412)
 constexpr int kWeakCap = 512;
-constexpr int kSegRecs = kListCap * 10 / 8;  // uint2 segment records over the entry area
+constexpr int kSegRecs = 2176;     // uint2 segment records (phase 0, over the entry area)
 constexpr int kSpillHalves = 5 * NW;         // global spill per env: 4 entries + 1 list word
 enum { kNSpan = 0, kNSeg = 1, kNList = 2, kNQuad = 3, kNWeak = 4, kNCnt = 8 };
 constexpr uint16_t WK_MAG = 0x7FF, WK_DIR_SHIFT = 11, WK_CAND = 1 << 13, WK_EDGE = 1 << 14;
 
 struct RenderLds {
-  uint32_t img[NW];
-  uint16_t wmap[NW];  // word -> its slot + 1; 0: a uniform neighbourhood (not listed)
+  uint32_t img[NW];   // raster bytes; from phase 2a a listed word's slot + 1 in bits 3-7
   union {
     struct {
       uint16_t ent[4 * kListCap];  // slot s: the work entries of its 4 pixels
       uint16_t list[kListCap];     // slot s -> word
     } w;
-    uint2 seg[kSegRecs];           // phase 0: visible segments (yellow up, white down)
+    struct {
+      uint2 seg[kSegRecs];         // phase 0: visible segments (yellow up, white down)
+      uint16_t qlist[NQ];          // phase 0: the non-uniform background spans
+    } p;
   } u;
-  uint16_t qlist[NQ];  // phase 0: the non-uniform background spans
   uint16_t weak[kWeakCap];
   uint32_t pal_swar[PAL_N];
   float pal_gray[PAL_N];
@@ -350,7 +355,8 @@ struct RenderLds {
   int32_t cnt[kNCnt];
   int8_t kind[dt::kMaxLdsTiles];
 };
-static_assert(sizeof(RenderLds) <= 163840 / 3, "three render workgroups per CU");
+static_assert(sizeof(RenderLds) <= 163840 / 4, "four render workgroups per CU");
+static_assert(sizeof(((RenderLds*)0)->u.p) <= sizeof(((RenderLds*)0)->u.w), "phase-0 lists");
 // segments projected in one round (loads issued at entry): 4 per lane, and
 // their records must fit the record area
 constexpr int kMarkFast = 4 * kRenderThreads < kSegRecs ? 4 * kRenderThreads : kSegRecs;
@@ -392,6 +398,17 @@ __device__ inline uint32_t bytes01_to_ff(uint32_t m) {
   uint32_t r;
   asm("v_lshlrev_b32 %0, 8, %1\n\tv_sub_u32 %0, %0, %1" : "=&v"(r) : "v"(m));
   return r;
+}
+
+// A listed word's slot + 1 (0: not listed) in the spare bits 3-7 of its raster
+// bytes 0..2 (13 bits: a slot < NW).  Readers of raster bytes mask kPalMask.
+constexpr uint32_t kPalMask = 0x07070707u;
+__device__ __forceinline__ uint32_t slot1_enc(uint32_t s1) {
+  return ((s1 & 31u) << 3) | (((s1 >> 5) & 31u) << 11) | ((s1 >> 10) << 19);
+}
+__device__ __forceinline__ int slot1_of(uint32_t w) {
+  return (int)(__builtin_amdgcn_ubfe(w, 3, 5) | (__builtin_amdgcn_ubfe(w, 11, 5) << 5) |
+               (__builtin_amdgcn_ubfe(w, 19, 3) << 10));
 }
 
 // byte-lane shift of a row of words: result byte i = pixel (i + d) (0 outside)
@@ -624,7 +641,7 @@ struct Slots {
   // work entry of pixel (r, c): 0 outside the image and in unlisted words
   __device__ uint32_t at(int r, int c) const {
     if ((unsigned)r >= (unsigned)H || (unsigned)c >= (unsigned)W) return 0u;
-    const int s = S.wmap[r * WPR + (c >> 2)];
+    const int s = slot1_of(S.img[r * WPR + (c >> 2)]);
     return s ? (uint32_t)ent(s - 1, c & 3) : 0u;
   }
 };
@@ -645,12 +662,15 @@ __device__ __forceinline__ void quad_masks(const RenderLds& S, const Slots<kSpil
     if ((unsigned)rr >= (unsigned)H) continue;
     const uint32_t* row = S.img + rr * WPR;
     const uint4 cur = *reinterpret_cast<const uint4*>(row + cw0);
-    // raster bytes -> colour-bit bytes (v_perm LUT); 0 outside the image
+    // raster bytes (slot bits masked) -> colour-bit bytes (v_perm LUT); 0
+    // outside the image
     const uint32_t wv[6] = {
-        cw0 > 0 ? __builtin_amdgcn_perm(bhi, blo, row[cw0 - 1]) : 0u,
-        __builtin_amdgcn_perm(bhi, blo, cur.x), __builtin_amdgcn_perm(bhi, blo, cur.y),
-        __builtin_amdgcn_perm(bhi, blo, cur.z), __builtin_amdgcn_perm(bhi, blo, cur.w),
-        cw0 + 4 < WPR ? __builtin_amdgcn_perm(bhi, blo, row[cw0 + 4]) : 0u};
+        cw0 > 0 ? __builtin_amdgcn_perm(bhi, blo, row[cw0 - 1] & kPalMask) : 0u,
+        __builtin_amdgcn_perm(bhi, blo, cur.x & kPalMask),
+        __builtin_amdgcn_perm(bhi, blo, cur.y & kPalMask),
+        __builtin_amdgcn_perm(bhi, blo, cur.z & kPalMask),
+        __builtin_amdgcn_perm(bhi, blo, cur.w & kPalMask),
+        cw0 + 4 < WPR ? __builtin_amdgcn_perm(bhi, blo, row[cw0 + 4] & kPalMask) : 0u};
 #pragma unroll
     for (int dx = -R; dx <= R; ++dx) {
       if (!((dmask >> ((dy + 3) * 7 + (dx + 3))) & 1ull)) continue;  // uniform
@@ -659,11 +679,12 @@ __device__ __forceinline__ void quad_masks(const RenderLds& S, const Slots<kSpil
     }
   }
   // edge bytes from the work entries of the quad's listed words
-  const uint64_t wm = *reinterpret_cast<const uint64_t*>(S.wmap + r * WPR + cw0);
+  const uint4 own = *reinterpret_cast<const uint4*>(S.img + r * WPR + cw0);
+  const uint32_t ow[4] = {own.x, own.y, own.z, own.w};
   uint32_t edg[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
-    const int s = (int)((wm >> (16 * j)) & 0xFFFFu);
+    const int s = slot1_of(ow[j]);
     const uint2 v = s ? sl.ent4(s - 1) : make_uint2(0u, 0u);
     // the high byte of each 16-bit entry (v_perm), EDGE = its bit 6
     edg[j] = (__builtin_amdgcn_perm(v.y, v.x, 0x07050301u) >> 6) & 0x01010101u;
@@ -701,10 +722,10 @@ __device__ __forceinline__ void canny(const RenderArgs& a, RenderLds& S, int e,
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
       const uint32_t* rowp = S.img + rows[k] * WPR;
-      const uint32_t m = rowp[cw];
+      const uint32_t m = rowp[cw] & kPalMask;   // (other lanes set slot bits meanwhile)
       // BORDER_REPLICATE: the pixel left of column 0 is column 0, right of 159 is 159
-      const uint32_t lb = cw > 0 ? rowp[cw - 1] >> 24 : (m & 255u);
-      const uint32_t rb = cw < WPR - 1 ? rowp[cw + 1] & 255u : (m >> 24);
+      const uint32_t lb = cw > 0 ? (rowp[cw - 1] >> 24) & 7u : (m & 255u);
+      const uint32_t rb = cw < WPR - 1 ? rowp[cw + 1] & 7u : (m >> 24);
       nb[k][0] = S.pal_swar[lb];
       nb[k][1] = S.pal_swar[m & 255u];
       nb[k][2] = S.pal_swar[(m >> 8) & 255u];
@@ -722,6 +743,10 @@ __device__ __forceinline__ void canny(const RenderArgs& a, RenderLds& S, int e,
       out[i >> 1] |= v << (16 * (i & 1));
     }
     sl.set_ent4(s, make_uint2(out[0], out[1]));
+    // the word's slot + 1 into its spare bits (this lane is the word's only
+    // writer; concurrent readers mask them off)
+    __hip_atomic_fetch_or((lds_u32*)S.img + w, slot1_enc((uint32_t)s + 1u), __ATOMIC_RELAXED,
+                          __HIP_MEMORY_SCOPE_WORKGROUP);
   }
   __syncthreads();
   RENT(9);
@@ -756,7 +781,7 @@ __device__ __forceinline__ void canny(const RenderArgs& a, RenderLds& S, int e,
           }
           const int rr = r + dy, cc = cw + dx;
           const bool in = (unsigned)rr < (unsigned)H && (unsigned)cc < (unsigned)WPR;
-          const int slot = S.wmap[in ? rr * WPR + cc : w];
+          const int slot = slot1_of(S.img[in ? rr * WPR + cc : w]);
           const uint2 v = sl.ent4(slot > 0 ? slot - 1 : 0);
           nb[dy + 1][dx + 1] = (in && slot > 0) ? v : make_uint2(0u, 0u);
         }
@@ -839,7 +864,7 @@ __device__ __forceinline__ void canny(const RenderArgs& a, RenderLds& S, int e,
               break;
             }
         if (hit) {
-          sl.set_ent(S.wmap[r * WPR + (c >> 2)] - 1, c & 3, (uint16_t)(b | WK_EDGE));
+          sl.set_ent(slot1_of(S.img[r * WPR + (c >> 2)]) - 1, c & 3, (uint16_t)(b | WK_EDGE));
           changed = 1;
         }
       }
@@ -877,7 +902,7 @@ __device__ __forceinline__ void write_outputs(const RenderArgs& a, RenderLds& S,
       for (int j = 0; j < 4; ++j) {
         const int w = wbase + 64 * j + lane;
         if (w < NW) {
-          const uint32_t v = S.img[w];
+          const uint32_t v = S.img[w] & kPalMask;
           float4 g;
           g.x = S.pal_gray[v & 255u];
           g.y = S.pal_gray[(v >> 8) & 255u];
@@ -896,8 +921,8 @@ __device__ __forceinline__ void write_outputs(const RenderArgs& a, RenderLds& S,
     const int q = q0 + tid;
     if (q < NQ) {
       if (mbase) {
-        if (quick_masks && *reinterpret_cast<const uint64_t*>(S.wmap + 4 * q) == 0ull) {
-          const uint4 m = *reinterpret_cast<const uint4*>(S.img + 4 * q);
+        const uint4 m = *reinterpret_cast<const uint4*>(S.img + 4 * q);
+        if (quick_masks && ((m.x | m.y | m.z | m.w) & ~kPalMask) == 0u) {   // no listed word
           const uint32_t mw[4] = {m.x, m.y, m.z, m.w};
           uint32_t o[3][4];
 #pragma unroll
@@ -926,7 +951,7 @@ __device__ __forceinline__ void write_outputs(const RenderArgs& a, RenderLds& S,
         uint8_t* o = a.rgb + ((size_t)e * NPIX + 16 * q) * 3;
         const uint32_t mw[4] = {m.x, m.y, m.z, m.w};
         for (int i = 0; i < 16; ++i) {
-          const uint32_t p = kPalette[(mw[i >> 2] >> (8 * (i & 3))) & 255u];
+          const uint32_t p = kPalette[(mw[i >> 2] >> (8 * (i & 3))) & 7u];
           o[3 * i + 0] = (p >> 16) & 255;
           o[3 * i + 1] = (p >> 8) & 255;
           o[3 * i + 2] = p & 255;
@@ -999,7 +1024,7 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, in
       want = !uni;
     }
     const int slot = wave_slot1(&C[kNSpan], want);
-    if (want) S.qlist[slot] = (uint16_t)q;
+    if (want) S.u.p.qlist[slot] = (uint16_t)q;
   }
   RENT(18);
   // ... and the markings' projection: every lane projects up to four segments
@@ -1018,8 +1043,8 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, in
     wave_slots4x2(&C[kNSeg], vy, vw, sy, sw);  // yellow count | white count << 16
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
-      if (vy[k]) S.u.seg[sy[k]] = seg_pack(cc0[k], rr0[k], cc1[k], rr1[k]);
-      if (vw[k]) S.u.seg[kSegRecs - 1 - sw[k]] = seg_pack(cc0[k], rr0[k], cc1[k], rr1[k]);
+      if (vy[k]) S.u.p.seg[sy[k]] = seg_pack(cc0[k], rr0[k], cc1[k], rr1[k]);
+      if (vw[k]) S.u.p.seg[kSegRecs - 1 - sw[k]] = seg_pack(cc0[k], rr0[k], cc1[k], rr1[k]);
     }
   }
   __syncthreads();
@@ -1034,7 +1059,7 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, in
     const int nbg = 4 * nspan, items = nbg + kParts * (ny + nw);
     for (int i = tid; i < items; i += T) {
       if (i < nbg) {
-        const int q = S.qlist[i >> 2];
+        const int q = S.u.p.qlist[i >> 2];
         const int r = q / QPR, c = 16 * (q - r * QPR) + 4 * (i & 3);
         float fi[4], fj[4];
         tile_f(r, c, fi[0], fj[0]);
@@ -1055,7 +1080,7 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, in
       } else {
         const int j = i - nbg, sidx = j / kParts;
         const bool yel = sidx < ny;
-        seg_draw(img, S.u.seg[yel ? sidx : kSegRecs - 1 - (sidx - ny)], yel ? PAL_YELLOW : PAL_WHITE,
+        seg_draw(img, S.u.p.seg[yel ? sidx : kSegRecs - 1 - (sidx - ny)], yel ? PAL_YELLOW : PAL_WHITE,
                  j - sidx * kParts, kParts);
       }
     }
@@ -1083,11 +1108,11 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, in
         wave_slots4(&C[kNSeg], vis, slot);
 #pragma unroll
         for (int k = 0; k < 4; ++k)
-          if (vis[k]) S.u.seg[slot[k] % kSegRecs] = seg_pack(cc0[k], rr0[k], cc1[k], rr1[k]);
+          if (vis[k]) S.u.p.seg[slot[k] % kSegRecs] = seg_pack(cc0[k], rr0[k], cc1[k], rr1[k]);
         __syncthreads();
         const int end = C[kNSeg];
         for (int i = listed * kParts + tid; i < end * kParts; i += T)
-          seg_draw(img, S.u.seg[(i / kParts) % kSegRecs], col, i % kParts, kParts);
+          seg_draw(img, S.u.p.seg[(i / kParts) % kSegRecs], col, i % kParts, kParts);
         listed = end;
         __syncthreads();
       }
@@ -1098,7 +1123,7 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, in
 
   // phase 1: per 16-pixel quad (4 words of a row): the 3 x 6-word neighbourhood
   // decides each word's uniformity exactly (all 18 pixels around it one
-  // byte).  Non-uniform words get a slot (list + wmap); a quad with one takes
+  // byte).  Non-uniform words get a slot (the list); a quad with one takes
   // the dilation path of the output phase (every quad does when the dilation
   // radius is >= 2: uniformity only covers +-1 pixel).
   uint8_t* mbase = a.masks ? a.masks + (size_t)e * 4 * NPIX : nullptr;
@@ -1153,12 +1178,10 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, in
     for (int k = 0; k < kQuadPer; ++k) {
       const int q = tid + k * T;
       if (q < NQ) {
-        uint32_t wm[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
           const int w = 4 * q + j;
           const int sj = slot[4 * k + j];
-          wm[j] = non[4 * k + j] ? (uint32_t)sj + 1u : 0u;
           if (non[4 * k + j]) {
             if (sj < a.list_cap)
               S.u.w.list[sj] = (uint16_t)w;
@@ -1166,8 +1189,6 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, in
               gl[sj] = (uint16_t)w;
           }
         }
-        *reinterpret_cast<uint2*>(S.wmap + 4 * q) =
-            make_uint2(wm[0] | (wm[1] << 16), wm[2] | (wm[3] << 16));
       }
     }
   }
@@ -1193,10 +1214,10 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, in
 #endif
 }
 
-// One workgroup per env, three per CU.
-// waves_per_eu(6): three 512-thread workgroups per CU need <= 85 VGPRs
+// One workgroup per env, four per CU.
+// waves_per_eu(8): four 512-thread workgroups per CU need <= 64 VGPRs
 #ifndef DTSIM_RENDER_WPE
-#define DTSIM_RENDER_WPE 6
+#define DTSIM_RENDER_WPE 8
 #endif
 __global__ __launch_bounds__(kRenderThreads) __attribute__((amdgpu_waves_per_eu(DTSIM_RENDER_WPE))) void
 render_kernel(RenderArgs a) {

@@ -111,6 +111,34 @@ def main():
     print('last launch: span %.1f us, distinct CUs %d, workgroups per CU %.1f, max concurrent '
           'workgroups %d (%.2f per CU)' % (span, len(np.unique(key)), len(last) / len(np.unique(key)),
                                            conc.max(), conc.max() / len(np.unique(key))))
+    # per-CU timelines of the last launch: when each CU's first workgroup
+    # starts and its last ends, how many of its slots are busy on average over
+    # that span, and the gap from a workgroup's end to the next start on the CU
+    t_start = (last[:, 17] - t0) / 100.0
+    t_end = (last[:, 1] - t0) / 100.0
+    firsts, lasts, occ, gaps = [], [], [], []
+    for k in np.unique(key):
+        sel = key == k
+        st, en = np.sort(t_start[sel]), np.sort(t_end[sel])
+        firsts.append(st[0])
+        lasts.append(en[-1])
+        occ.append((en - st).sum() if False else (t_end[sel] - t_start[sel]).sum() / (en[-1] - st[0]))
+        # each start after the first 4 follows some end: the latest end before it
+        for s0 in st[4:]:
+            prev = en[en <= s0 + 1e-9]
+            if len(prev):
+                gaps.append(s0 - prev[-1])
+    firsts, lasts, occ = np.array(firsts), np.array(lasts), np.array(occ)
+    print('per CU: first start median %.1f us (max %.1f), last end median %.1f us (min %.1f, '
+          'max %.1f), busy slots over its span mean %.2f' % (np.median(firsts), firsts.max(),
+                                                              np.median(lasts), lasts.min(),
+                                                              lasts.max(), occ.mean()))
+    if gaps:
+        g = np.array(gaps)
+        print('end -> next start on a CU: median %.2f us, p90 %.2f us, max %.2f us'
+              % (np.median(g), np.percentile(g, 90), g.max()))
+    hist = np.histogram(t_start, bins=10, range=(0, span))[0]
+    print('workgroup starts per tenth of the span:', hist.tolist())
     env.close()
 
 
