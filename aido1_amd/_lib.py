@@ -22,7 +22,7 @@ SOURCES = ['dtsim.hip', 'dtrender.hip', 'dtreplay.hip', 'dtactor.hip', 'dtconv.h
 HEADERS = ['dtsim_common.h', 'dtrender.h']
 PUBLIC_HEADERS = ['dtsim.h', 'dtreplay.h', 'dtactor.h', 'dttrain.h']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
-ABI_VERSION = 5
+ABI_VERSION = 6
 
 HIP_FLAGS = ['--offload-arch=gfx950', '-O3', '-fPIC', '-shared', '-std=c++17',
              '-ffp-contract=off', '-munsafe-fp-atomics']
@@ -38,6 +38,13 @@ class DtMap(ctypes.Structure):
                 ('curves', ctypes.c_void_p), ('headings', ctypes.c_void_p),
                 ('n_objects', ctypes.c_int32), ('objects', ctypes.c_void_p),
                 ('n_spawn_objects', ctypes.c_int32), ('spawn_objects', ctypes.c_void_p)]
+
+
+class DtConvSet(ctypes.Structure):
+    """include/dtactor.h dt_conv_set: the second weight set of a split launch."""
+    _fields_ = [('n0', ctypes.c_int32), ('wfrag', ctypes.c_void_p), ('bias', ctypes.c_void_p),
+                ('in_gamma', ctypes.c_void_p), ('in_beta', ctypes.c_void_p),
+                ('out_gamma', ctypes.c_void_p), ('out_beta', ctypes.c_void_p)]
 
 
 class DtExploreParams(ctypes.Structure):
@@ -160,9 +167,15 @@ def lib():
                                               ctypes.c_float, i32, vp]),
             'dt_conv1': (ctypes.c_int, [vp, i32, i32, ctypes.POINTER(i32), vp, vp, vp, vp,
                                         ctypes.c_float, vp]),
+            'dt_conv1_split': (ctypes.c_int, [vp, i32, i32, ctypes.POINTER(i32), vp, vp,
+                                              ctypes.POINTER(DtConvSet), vp, vp, ctypes.c_float,
+                                              vp]),
             'dt_conv1_norm': (ctypes.c_int, [vp, i32, vp, vp, vp, ctypes.c_float, vp]),
             'dt_conv32': (ctypes.c_int, [i32, i32, vp, vp, vp, vp, vp, vp, ctypes.c_float, vp,
                                          vp, vp, vp, ctypes.c_float, ctypes.c_float, vp]),
+            'dt_conv32_split': (ctypes.c_int, [i32, i32, vp, vp, vp, vp, vp, vp, ctypes.c_float,
+                                               vp, vp, vp, vp, ctypes.c_float, ctypes.c_float,
+                                               ctypes.POINTER(DtConvSet), vp]),
             'dt_explore': (ctypes.c_int, [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                           ctypes.POINTER(DtExploreParams), vp, vp]),
             'dt_explore_done': (ctypes.c_int, [i32, vp, vp, vp, vp, i32, vp]),

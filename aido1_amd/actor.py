@@ -429,6 +429,85 @@ class FusedActor(nn.Module):
                 self.eps[3] if ref else 0.0, 0.01, stream)
         return rc
 
+    def _pairable(self, other, x):
+        return (other is not None and other.mode == self.mode and x.is_cuda and
+                self.dtype == torch.float16 and other.dtype == torch.float16 and
+                x.dtype == torch.float32 and x.is_contiguous() and
+                tuple(x.shape[2:]) == (120, 160) and x.shape[1] >= 3 and
+                self.w[0].shape == (32, 3, 8, 8) and other.w[0].shape == (32, 3, 8, 8))
+
+    @torch.no_grad()
+    def forward_pair(self, other, x, order, n0, out=None):
+        """The samples [0, n0) through this actor and [n0, n) through `other`
+        (the exploiting explorers' copy, rollout.ActorRollout) with ONE launch
+        per convolution: dt_conv1_split / dt_conv32_split split the persistent
+        workgroups between the two weight sets (include/dtactor.h).  Returns
+        [n, 2] (into `out` if given); each row equals the forward of its own
+        actor."""
+        n = x.shape[0]
+        if out is None:
+            out = torch.empty(n, 2, dtype=torch.float32, device=x.device)
+        if not self._pairable(other, x) or not 0 < n0 < n:
+            out[:n0] = self(x[:n0], order)
+            out[n0:] = other(x[n0:], order)
+            return out
+        flat = self._convs_pair(other, x, order, n0)
+        for a, sl in ((self, slice(0, n0)), (other, slice(n0, n))):
+            out[sl] = a._head(flat[sl])
+        return out
+
+    def _convs_pair(self, other, x, order, n0):
+        """_convs_hip over both weight sets: the flattened [n, 4032] fp16
+        activations, rows [0, n0) from this actor's weights, the rest from
+        `other`'s."""
+        import ctypes
+        from aido1_amd import _lib
+        L = _lib.lib()
+        n = x.shape[0]
+        ref = self.mode == 'reference'
+        flat = torch.empty(n, FLAT, dtype=torch.float16, device=x.device)
+        B = self._conv_buffers(n, x.device)
+        stream = torch.cuda.current_stream(x.device).cuda_stream
+        ptr = (lambda t: t.data_ptr() if t is not None else None)
+        o = (ctypes.c_int32 * 3)(*[int(v) for v in order])
+        s1 = _lib.DtConvSet(n0, other.w0frag.data_ptr(), other.bf[0].data_ptr())
+        rc = L.dt_conv1_split(x.data_ptr(), n, x.shape[1], o, self.w0frag.data_ptr(),
+                              self.bf[0].data_ptr(), ctypes.byref(s1), B['y1'].data_ptr(),
+                              ptr(B['p1']), 0.01, stream)
+        ins = [(B['y1'], B['p1']), (B['y2'], B['p2']), (B['y3'], B['p3'])]
+        outs = [(B['y2'], B['p2']), (B['y3'], B['p3']), (flat, None)]
+        for layer in range(3):
+            if rc != 0:
+                break
+            xi, pp = ins[layer]
+            y, po = outs[layer]
+            last = layer == 2
+            s2 = _lib.DtConvSet(n0, other.wfrag[layer].data_ptr(), other.bf[layer + 1].data_ptr(),
+                                ptr(other.gamma[layer]) if ref else None,
+                                ptr(other.beta[layer]) if ref else None,
+                                ptr(other.gamma[3]) if (ref and last) else None,
+                                ptr(other.beta[3]) if (ref and last) else None)
+            rc = L.dt_conv32_split(
+                layer + 2, n, xi.data_ptr(), self.wfrag[layer].data_ptr(),
+                self.bf[layer + 1].data_ptr(), ptr(pp),
+                self.gamma[layer].data_ptr() if ref else None,
+                self.beta[layer].data_ptr() if ref else None, self.eps[layer] if ref else 0.0,
+                y.data_ptr(), ptr(po),
+                self.gamma[3].data_ptr() if (ref and last) else None,
+                self.beta[3].data_ptr() if (ref and last) else None,
+                self.eps[3] if ref else 0.0, 0.01, ctypes.byref(s2), stream)
+        if rc != 0:
+            raise _lib.DtError('dt_conv1_split / dt_conv32_split failed (%d)' % rc)
+        return flat
+
+    def _head(self, x):
+        """dropout (reference mode) -> lin1 -> LeakyReLU -> lin2 -> head."""
+        if self.mode == 'reference' and self.p_drop > 0:
+            x = F.dropout(x, self.p_drop, training=True)
+        x = F.leaky_relu(F.linear(x, self.w1, self.b1))
+        x = F.linear(x, self.w2, self.b2).float()
+        return apply_head(x, self.head, self.max_action)
+
     @torch.no_grad()
     def forward(self, x, order=None):
         """x: [N,3,120,160] stack (oldest first), or the frame ring with
@@ -457,11 +536,7 @@ class FusedActor(nn.Module):
                 x = self._lrelu_sample_norm(x, i) if ref else F.leaky_relu(x)
             # flatten in NCHW order, as the reference's view(x.size(0), -1)
             x = x.contiguous().flatten(1)
-        if ref and self.p_drop > 0:
-            x = F.dropout(x, self.p_drop, training=True)
-        x = F.leaky_relu(F.linear(x, self.w1, self.b1))
-        x = F.linear(x, self.w2, self.b2).float()
-        return apply_head(x, self.head, self.max_action)
+        return self._head(x)
 
 
 def conv1_fragments(w):

@@ -83,6 +83,48 @@ __device__ __forceinline__ void store_px32(__half* sample, int px, const float (
   }
 }
 
+// ---- two weight sets in one launch -----------------------------------------------
+// Samples [0, n0) use the launch's weights, [n0, n) a second set (the exploiting
+// explorers' actor): the persistent workgroups split in proportion, g0 for the
+// first set, the rest for the second, and each loads only its own set.  One set:
+// n0 = n, g0 = gridDim.x.
+struct WeightSplit {
+  int n0, g0;
+  const void* wfrag;
+  const float *bias, *in_gamma, *in_beta, *out_gamma, *out_beta;
+};
+struct SplitPart {
+  bool set2;
+  int bid, gdim, sbeg, send, my;   // this WG's index / count in its part, its samples
+};
+__device__ __forceinline__ SplitPart split_part(const WeightSplit& ws, int n) {
+  SplitPart p;
+  p.set2 = (int)blockIdx.x >= ws.g0;
+  p.bid = p.set2 ? (int)blockIdx.x - ws.g0 : (int)blockIdx.x;
+  p.gdim = p.set2 ? (int)gridDim.x - ws.g0 : ws.g0;
+  p.sbeg = p.set2 ? ws.n0 : 0;
+  p.send = p.set2 ? n : ws.n0;
+  const int nloc = p.send - p.sbeg;
+  p.my = nloc > p.bid ? (nloc - p.bid + p.gdim - 1) / p.gdim : 0;
+  return p;
+}
+// host: the grid of a launch over n samples (n0 of them with the first set) on
+// `grid` resident workgroups; fills ws.n0 / ws.g0
+inline int split_grid(WeightSplit& ws, int n, int n0, int grid) {
+  if (n0 <= 0 || n0 >= n) {   // one set
+    ws.n0 = n;
+    ws.g0 = n < grid ? n : grid;
+    return ws.g0;
+  }
+  int g0 = (int)(((long long)grid * n0 + n / 2) / n);
+  g0 = g0 < 1 ? 1 : (g0 > grid - 1 ? grid - 1 : g0);
+  const int g1raw = grid - g0;
+  ws.n0 = n0;
+  ws.g0 = n0 < g0 ? n0 : g0;
+  const int g1 = (n - n0) < g1raw ? (n - n0) : g1raw;
+  return ws.g0 + g1;
+}
+
 // ---- conv1 ----------------------------------------------------------------------
 // A persistent workgroup of kSW waves streams whole samples (n = blockIdx.x,
 // + gridDim.x, ...).  The input rows go through a ring of kSRing rows in LDS
@@ -159,16 +201,21 @@ template <bool kStats>
 __global__ void __launch_bounds__(kSThreads, 2)   // 2 waves / SIMD: <= 256 registers
 conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, int s2,
               const half8* __restrict__ wfrag, const float* __restrict__ bias,
-              __half* __restrict__ y, float* __restrict__ partials, float slope) {
+              __half* __restrict__ y, float* __restrict__ partials, float slope, WeightSplit ws) {
   __shared__ __attribute__((aligned(16))) unsigned char rb[kSRing * kSRowB];
   __shared__ float red[kSW][CO][3];
   __shared__ float s_bias[CO];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 31, h = lane >> 5;
-  const int my = n > (int)blockIdx.x ? (n - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
-  const int total = my * kSSteps;
+  const SplitPart sp = split_part(ws, n);
+  if (sp.set2) {
+    wfrag = static_cast<const half8*>(ws.wfrag);
+    bias = ws.bias;
+  }
+  const int send = sp.send;
+  const int total = sp.my * kSSteps;
   if (total == 0) return;
-  auto sample = [&](int k) __attribute__((always_inline)) { return (int)blockIdx.x + k * (int)gridDim.x; };
+  auto sample = [&](int k) __attribute__((always_inline)) { return sp.sbeg + sp.bid + k * sp.gdim; };
   const size_t plane = (size_t)IH * IW;
 
   // a thread's load items are fixed (row r_i, quad qq_i of the step's range);
@@ -188,7 +235,7 @@ conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, 
   // sample): its loads then read the sample's row 0, never past the plane.
   auto issue = [&](float4 (&pre)[kSPre][3], int k, int r0, int r1) __attribute__((always_inline)) {
     const int rows = r1 - r0 + 1;
-    const int ns = sample(k) < n ? sample(k) : n - 1;
+    const int ns = sample(k) < send ? sample(k) : send - 1;
     const float* base = ring + (size_t)ns * slots * plane + (size_t)(rows > 0 ? r0 : 0) * IW;
     const float* p0 = base + (size_t)s0 * plane;
     const float* p1 = base + (size_t)s1 * plane;
@@ -542,7 +589,7 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
               const float* __restrict__ in_gamma, const float* __restrict__ in_beta, float in_eps,
               __half* __restrict__ y, float* __restrict__ part,
               const float* __restrict__ out_gamma, const float* __restrict__ out_beta,
-              float out_eps, float slope) {
+              float out_eps, float slope, WeightSplit ws) {
   using G = ConvGeom<IH, IW, OH, OW, ST, NW>;
   constexpr int kRing = G::ring();
   constexpr int kRowU4 = IW * 4;                  // 16-B chunks per input row
@@ -558,10 +605,19 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
   const int col = lane & 31, h = lane >> 5;
   unsigned char* rb = reinterpret_cast<unsigned char*>(ring);
 
-  const int my = n > (int)blockIdx.x ? (n - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x : 0;
-  const int total = my * G::kSteps;
+  const SplitPart sp = split_part(ws, n);
+  if (sp.set2) {
+    wfrag = static_cast<const half8*>(ws.wfrag);
+    bias = ws.bias;
+    in_gamma = ws.in_gamma;
+    in_beta = ws.in_beta;
+    out_gamma = ws.out_gamma;
+    out_beta = ws.out_beta;
+  }
+  const int send = sp.send;
+  const int total = sp.my * G::kSteps;
   if (total == 0) return;
-  auto sample = [&](int k) __attribute__((always_inline)) { return (int)blockIdx.x + k * (int)gridDim.x; };
+  auto sample = [&](int k) __attribute__((always_inline)) { return sp.sbeg + sp.bid + k * sp.gdim; };
 
   // the previous layer's BatchNorm of the WG's k-th sample (threads < CO), in
   // two halves: the statistics loads are issued ahead of a step's prefetch
@@ -572,7 +628,7 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
     // every thread, every step, sample clamped: a fixed count of loads on
     // every path keeps the compiler's vmcnt waits exact
     if (kIn == 1) {
-      const int ns = sample(k) < n ? sample(k) : n - 1;
+      const int ns = sample(k) < send ? sample(k) : send - 1;
       const int c = tid & (CO - 1);
       const float* pp = prev_part + ((size_t)ns * CO + c) * 2;
       st[0] = pp[0];
@@ -594,7 +650,7 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
   auto issue = [&](u32x4 (&pre)[kPre], int k, int r0, int r1) __attribute__((always_inline)) {
     // unconditional (clamped chunk and sample): see stats_load
     const int cnt = (r1 - r0 + 1) * kRowU4;
-    const int ns = sample(k) < n ? sample(k) : n - 1;
+    const int ns = sample(k) < send ? sample(k) : send - 1;
     const u32x4* src = reinterpret_cast<const u32x4*>(x + ((size_t)ns * IH + r0) * IW * CO);
 #pragma unroll
     for (int i = 0; i < kPre; ++i) {
@@ -844,7 +900,7 @@ template <int IH, int IW, int OH, int OW, int ST, int NW, int kIn, int kOut>
 int launch_conv32(int n, const void* x, const void* wfrag, const float* bias,
                   const float* prev_part, const float* ig, const float* ibt,
                   float ieps, void* y, float* part, const float* og, const float* obt, float oeps,
-                  float slope, hipStream_t s) {
+                  float slope, hipStream_t s, WeightSplit ws, int n0) {
   auto kern = conv32_kernel<IH, IW, OH, OW, ST, NW, kIn, kOut>;
   static int grid = 0;   // resident workgroups: one wave of them, persistent
   if (!grid) {
@@ -856,10 +912,10 @@ int launch_conv32(int n, const void* x, const void* wfrag, const float* bias,
       per = 1;
     grid = per * cus;
   }
-  const int g = n < grid ? n : grid;
+  const int g = split_grid(ws, n, n0, grid);
   hipLaunchKernelGGL(kern, dim3(g), dim3(64 * NW), 0, s, n, (const __half*)x, (const half8*)wfrag,
                      bias, prev_part, ig, ibt, ieps, (__half*)y, part, og, obt, oeps,
-                     slope);
+                     slope, ws);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 
@@ -869,33 +925,45 @@ constexpr int kConv2Waves = 2, kConv3Waves = 2, kConv4Waves = 4;
 
 }  // namespace
 
-extern "C" int dt_conv1(const float* ring, int32_t n, int32_t slots, const int32_t* order,
-                        const void* wfrag, const float* bias, void* y, float* partials,
-                        float slope, void* stream) {
+extern "C" int dt_conv1_split(const float* ring, int32_t n, int32_t slots, const int32_t* order,
+                              const void* wfrag, const float* bias, const dt_conv_set* set2,
+                              void* y, float* partials, float slope, void* stream) {
   if (!ring || !wfrag || !bias || !y || !order || n < 0 || slots < 3) return DT_E_ARG;
   for (int i = 0; i < 3; ++i)
     if (order[i] < 0 || order[i] >= slots) return DT_E_ARG;
+  if (set2 && (set2->n0 < 0 || set2->n0 > n || !set2->wfrag || !set2->bias)) return DT_E_ARG;
   if (n == 0) return DT_OK;
-    static int grid = 0;   // resident workgroups, persistent
-    if (!grid) {
-      int dev = 0, cus = 256, per = 2;
-      if (hipGetDevice(&dev) == hipSuccess)
-        (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, conv1s_kernel<true>, kSThreads, 0) !=
-              hipSuccess || per < 1)
-        per = 1;
-      grid = per * cus;
-    }
-    const int g = n < grid ? n : grid;
-    if (partials)
-      hipLaunchKernelGGL(conv1s_kernel<true>, dim3(g), dim3(kSThreads), 0, (hipStream_t)stream, n,
-                         ring, slots, order[0], order[1], order[2], (const half8*)wfrag, bias,
-                         (__half*)y, partials, slope);
-    else
-      hipLaunchKernelGGL(conv1s_kernel<false>, dim3(g), dim3(kSThreads), 0, (hipStream_t)stream,
-                         n, ring, slots, order[0], order[1], order[2], (const half8*)wfrag, bias,
-                         (__half*)y, nullptr, slope);
-    return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+  static int grid = 0;   // resident workgroups, persistent
+  if (!grid) {
+    int dev = 0, cus = 256, per = 2;
+    if (hipGetDevice(&dev) == hipSuccess)
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, conv1s_kernel<true>, kSThreads, 0) !=
+            hipSuccess || per < 1)
+      per = 1;
+    grid = per * cus;
+  }
+  WeightSplit ws{};
+  if (set2) {
+    ws.wfrag = set2->wfrag;
+    ws.bias = set2->bias;
+  }
+  const int g = split_grid(ws, n, set2 ? set2->n0 : n, grid);
+  if (partials)
+    hipLaunchKernelGGL(conv1s_kernel<true>, dim3(g), dim3(kSThreads), 0, (hipStream_t)stream, n,
+                       ring, slots, order[0], order[1], order[2], (const half8*)wfrag, bias,
+                       (__half*)y, partials, slope, ws);
+  else
+    hipLaunchKernelGGL(conv1s_kernel<false>, dim3(g), dim3(kSThreads), 0, (hipStream_t)stream, n,
+                       ring, slots, order[0], order[1], order[2], (const half8*)wfrag, bias,
+                       (__half*)y, nullptr, slope, ws);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
+extern "C" int dt_conv1(const float* ring, int32_t n, int32_t slots, const int32_t* order,
+                        const void* wfrag, const float* bias, void* y, float* partials,
+                        float slope, void* stream) {
+  return dt_conv1_split(ring, n, slots, order, wfrag, bias, nullptr, y, partials, slope, stream);
 }
 
 #ifdef DTCONV_CHECK
@@ -921,42 +989,66 @@ extern "C" int dt_conv1_norm(void* y, int32_t n, const float* partials, const fl
 }
 
 // conv2..conv4 of the reference actor (see include/dtactor.h)
-extern "C" int dt_conv32(int32_t layer, int32_t n, const void* x, const void* wfrag,
-                         const float* bias, const float* prev_part, const float* in_gamma,
-                         const float* in_beta, float in_eps, void* y, float* part,
-                         const float* out_gamma, const float* out_beta, float out_eps,
-                         float slope, void* stream) {
+extern "C" int dt_conv32_split(int32_t layer, int32_t n, const void* x, const void* wfrag,
+                               const float* bias, const float* prev_part, const float* in_gamma,
+                               const float* in_beta, float in_eps, void* y, float* part,
+                               const float* out_gamma, const float* out_beta, float out_eps,
+                               float slope, const dt_conv_set* set2, void* stream) {
   if (!x || !wfrag || !bias || !y || n < 0) return DT_E_ARG;
-  if (n == 0) return DT_OK;
   const bool in = prev_part != nullptr;
   if (in && (!in_gamma || !in_beta)) return DT_E_ARG;
+  if (set2 && (set2->n0 < 0 || set2->n0 > n || !set2->wfrag || !set2->bias ||
+               (in && (!set2->in_gamma || !set2->in_beta)) ||
+               ((out_gamma != nullptr) != (set2->out_gamma != nullptr)) ||
+               ((out_beta != nullptr) != (set2->out_beta != nullptr))))
+    return DT_E_ARG;
+  if (n == 0) return DT_OK;
+  WeightSplit ws{};
+  if (set2) {
+    ws.wfrag = set2->wfrag;
+    ws.bias = set2->bias;
+    ws.in_gamma = set2->in_gamma;
+    ws.in_beta = set2->in_beta;
+    ws.out_gamma = set2->out_gamma;
+    ws.out_beta = set2->out_beta;
+  }
+  const int n0 = set2 ? set2->n0 : n;
   hipStream_t s = (hipStream_t)stream;
   switch (layer) {
     case 2:   // 57x77 -> 27x37, stride 2; input norm from conv1's per-sample statistics
       if (in != (part != nullptr)) return DT_E_ARG;
       return in ? launch_conv32<57, 77, 27, 37, 2, kConv2Waves, 1, 0>(
                       n, x, wfrag, bias, prev_part, in_gamma, in_beta, in_eps, y, part,
-                      nullptr, nullptr, 0.f, slope, s)
+                      nullptr, nullptr, 0.f, slope, s, ws, n0)
                 : launch_conv32<57, 77, 27, 37, 2, kConv2Waves, 0, 1>(
                       n, x, wfrag, bias, nullptr, nullptr, nullptr, 0.f, y, nullptr, nullptr,
-                      nullptr, 0.f, slope, s);
+                      nullptr, 0.f, slope, s, ws, n0);
     case 3:   // 27x37 -> 12x17, stride 2; input norm from conv2's per-sample statistics
       if (in != (part != nullptr)) return DT_E_ARG;
       return in ? launch_conv32<27, 37, 12, 17, 2, kConv3Waves, 1, 0>(
                       n, x, wfrag, bias, prev_part, in_gamma, in_beta, in_eps, y, part,
-                      nullptr, nullptr, 0.f, slope, s)
+                      nullptr, nullptr, 0.f, slope, s, ws, n0)
                 : launch_conv32<27, 37, 12, 17, 2, kConv3Waves, 0, 1>(
                       n, x, wfrag, bias, nullptr, nullptr, nullptr, 0.f, y, nullptr, nullptr,
-                      nullptr, 0.f, slope, s);
+                      nullptr, 0.f, slope, s, ws, n0);
     case 4:   // 12x17 -> 9x14, stride 1, whole sample per step; its own norm in-kernel; flattened
       if (in != (out_gamma != nullptr)) return DT_E_ARG;
       return in ? launch_conv32<12, 17, 9, 14, 1, kConv4Waves, 1, 2>(
                       n, x, wfrag, bias, prev_part, in_gamma, in_beta, in_eps, y, nullptr,
-                      out_gamma, out_beta, out_eps, slope, s)
+                      out_gamma, out_beta, out_eps, slope, s, ws, n0)
                 : launch_conv32<12, 17, 9, 14, 1, kConv4Waves, 0, 3>(
                       n, x, wfrag, bias, nullptr, nullptr, nullptr, 0.f, y, nullptr, nullptr,
-                      nullptr, 0.f, slope, s);
+                      nullptr, 0.f, slope, s, ws, n0);
     default:
       return DT_E_ARG;
   }
+}
+
+extern "C" int dt_conv32(int32_t layer, int32_t n, const void* x, const void* wfrag,
+                         const float* bias, const float* prev_part, const float* in_gamma,
+                         const float* in_beta, float in_eps, void* y, float* part,
+                         const float* out_gamma, const float* out_beta, float out_eps,
+                         float slope, void* stream) {
+  return dt_conv32_split(layer, n, x, wfrag, bias, prev_part, in_gamma, in_beta, in_eps, y, part,
+                         out_gamma, out_beta, out_eps, slope, nullptr, stream);
 }

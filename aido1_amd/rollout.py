@@ -155,9 +155,9 @@ class ActorRollout:
         if self.exploit_actor is None:
             out = self.actor(self.ring, self.order())
         else:
-            out = self.actor_out
-            out[:ne] = self.actor(self.ring[:ne], self.order())
-            out[ne:] = self.exploit_actor(self.ring[ne:], self.order())
+            # one launch per convolution over both weight sets (dt_conv*_split)
+            out = self.actor.forward_pair(self.exploit_actor, self.ring, self.order(), ne,
+                                          out=self.actor_out)
         if timing is not None:
             timing[1].record()
         if self.fx is not None:

@@ -73,6 +73,37 @@ int dt_conv32(int32_t layer, int32_t n, const void* x, const void* wfrag, const 
               void* y, float* part, const float* out_gamma, const float* out_beta,
               float out_eps, float slope, void* stream);
 
+/* A second weight set for the samples [n0, n) of one dt_conv1_split /
+ * dt_conv32_split launch.  config.json:183-186 runs 7 exploring and 1
+ * exploiting explorer, and the exploiters act with their own copy of the
+ * weights (the target model, training/explorers.py:104-105), so one decision
+ * runs the actor with two weight sets.  The persistent workgroups are split
+ * in proportion to the two sample counts and each loads one set; every
+ * sample's result is the one a separate launch with its set gives.  The
+ * layouts are those of the launch's own arguments; in_* / out_* are
+ * dt_conv32's (NULL exactly where the launch's are). */
+typedef struct dt_conv_set {
+  int32_t n0;               /* samples [0, n0) use the launch's weights */
+  const void* wfrag;        /* [n0, n): these */
+  const float* bias;
+  const float* in_gamma;
+  const float* in_beta;
+  const float* out_gamma;
+  const float* out_beta;
+} dt_conv_set;
+
+/* dt_conv1 with an optional second weight set (set2 NULL = dt_conv1). */
+int dt_conv1_split(const float* ring, int32_t n, int32_t slots, const int32_t* order,
+                   const void* wfrag, const float* bias, const dt_conv_set* set2, void* y,
+                   float* partials, float slope, void* stream);
+
+/* dt_conv32 with an optional second weight set (set2 NULL = dt_conv32). */
+int dt_conv32_split(int32_t layer, int32_t n, const void* x, const void* wfrag,
+                    const float* bias, const float* prev_part, const float* in_gamma,
+                    const float* in_beta, float in_eps, void* y, float* part,
+                    const float* out_gamma, const float* out_beta, float out_eps, float slope,
+                    const dt_conv_set* set2, void* stream);
+
 /* dt_explore: SingleThreadExplorer's action choice for n explorers at once,
  * one fused pass replacing the torch restatement's ~25 element-wise kernels
  * (aido1_amd/explore.py explore_actions + rollout.CycleEpsilon; the same

@@ -29,12 +29,14 @@
 extern "C" {
 #endif
 
-#define DT_ABI_VERSION 5  /* 2: curves per tile vary (curve_start), intersections;
+#define DT_ABI_VERSION 6  /* 2: curves per tile vary (curve_start), intersections;
                              3: static objects in dt_map, safety_rad_mult;
                              4: dt_render_io.pose / list_cap, dt_copy_pose,
                                 dt_step_many pose output;
                              5: dtactor.h: dt_conv12 and dt_conv1_bands
-                                removed, partials [n, 32, 2] */
+                                removed, partials [n, 32, 2];
+                             6: dtactor.h: dt_conv1_split / dt_conv32_split
+                                (two weight sets in one launch) */
 
 /* error codes */
 #define DT_OK 0

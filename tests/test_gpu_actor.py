@@ -276,3 +276,40 @@ for slots, order, n in ((4, [1, 2, 3], 1100), (3, [2, 0, 1], 37), (3, [0, 1, 2],
     r = subprocess.run([sys.executable, '-c', code], env=env, capture_output=True, text=True,
                        timeout=300)
     assert r.returncode == 0, r.stdout + r.stderr[-3000:]
+
+
+@pytest.mark.parametrize('mode', ['reference', 'eval'])
+@pytest.mark.parametrize('n,n0', [(600, 525), (97, 1), (97, 96), (4096, 3584)])
+def test_split_launch_matches_separate_actors(gpu, mode, n, n0):
+    """dt_conv1_split / dt_conv32_split (include/dtactor.h): one launch per
+    convolution over two weight sets gives every sample exactly (bit for bit)
+    what a launch with its own set gives -- the exploring / exploiting split of
+    rollout.ActorRollout (explorers.py:104-105, config.json:183-186)."""
+    from aido1_amd.actor import ConfigActor, FusedActor
+    cfg = golden('reference_config.json')['model']['actor']
+    torch.manual_seed(7)
+    a, b = ConfigActor(cfg), ConfigActor(cfg)
+    if mode == 'eval':
+        for m in (a, b):
+            for bn in [x for x in m.modules() if isinstance(x, torch.nn.BatchNorm2d)]:
+                bn.running_mean.uniform_(-0.2, 0.2)
+                bn.running_var.uniform_(0.5, 2.0)
+    fa = FusedActor(a.to(gpu), dtype=torch.float16, mode=mode)
+    fb = FusedActor(b.to(gpu), dtype=torch.float16, mode=mode)
+    if mode == 'reference':
+        with torch.no_grad():
+            for f in (fa, fb):
+                for p in list(f.gamma) + list(f.beta):
+                    p.uniform_(0.5, 1.5)
+    g = torch.Generator(device=gpu).manual_seed(n)
+    ring = torch.rand(n, 3, 120, 160, device=gpu, generator=g)
+    order = [2, 0, 1]
+    flat = fa._convs_pair(fb, ring, order, n0).clone()
+    fa_flat = fa._convs_hip(ring[:n0].contiguous(), order)
+    fb_flat = fb._convs_hip(ring[n0:].contiguous(), order)
+    assert torch.equal(flat[:n0], fa_flat)
+    assert torch.equal(flat[n0:], fb_flat)
+    fa.p_drop = fb.p_drop = 0.0
+    out = fa.forward_pair(fb, ring, order, n0)
+    ref = torch.cat([fa(ring[:n0].contiguous(), order), fb(ring[n0:].contiguous(), order)])
+    assert torch.allclose(out, ref, atol=1e-3), (out - ref).abs().max()
