@@ -10,7 +10,7 @@ import subprocess
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-OUT = os.path.join(ROOT, 'build', 'conv1_variants' + os.environ.get('CONV1_TAG', ''))
+OUT = os.path.join(ROOT, 'diag_so', 'conv1_variants' + os.environ.get('CONV1_TAG', ''))  # travels with gpurun (build/ does not)
 SKIPS = {'full': 0, 'no_prefetch': 1, 'no_mma': 2, 'no_store': 4, 'no_stats': 8,
          'no_commit': 16, 'only_mma': 1 | 4 | 8 | 16, 'only_io': 2 | 8 | 16, 'none': 31,
          'no_ldsread': 32}
