@@ -22,10 +22,6 @@
 #ifndef DTCONV_SKIP
 #define DTCONV_SKIP 0
 #endif
-// dt_conv1's kernel: 1 = conv1r_kernel (row strips, 16x16x32), 0 = conv1s_kernel
-#ifndef DTCONV1_FORM
-#define DTCONV1_FORM 1
-#endif
 // conv1s_kernel: B-fragment groups in flight, 2..4
 #ifndef DTCONV1_BDEPTH
 #define DTCONV1_BDEPTH 2
@@ -459,278 +455,6 @@ conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, 
       if (++j == kSSteps) { j = 0; ++k; }
     }
   }
-}
-
-// ---- conv1, row-strip form: conv1r_kernel ------------------------------------------
-// The same persistent row stream as conv1s_kernel, but a wave's unit of work
-// is a STRIP: 16 output columns x kRR (3) output rows, on
-// v_mfma_f32_16x16x32_f16 (A = weights: row = out channel in a half of 16,
-// K = one kernel row: kx 0..7 x 4 fp16 channels, the 4th zero; B = one input
-// row's 16 pixels' 8-pixel windows).  Output row oy reads input rows 2oy..2oy+7,
-// so a strip's 3 rows read 12 input rows, and each B fragment (one
-// ds_read_b128, 16-B aligned) feeds up to 3 rows x 2 halves = 6 MFMAs: 12 LDS
-// reads for 48 MFMAs, against 12 for 12 in conv1s_kernel's 32-pixel tiles.
-// Per sample: 19 row blocks x 5 column tiles (cols 64..79: 13 valid) = 95
-// units plus one idle slot = 24 steps of 4 units (one per wave, one barrier a
-// step): every sample deals the same units to the same waves, so its result
-// does not depend on where it falls in the workgroup's sequence (or on the
-// weight-set split).  Reference mode: per-lane Welford over the lane's
-// (pixel, 8 channels), flushed per sample into LDS (double-buffered by sample
-// parity) and merged (Chan) by wave 0 in the step after the sample's last.
-constexpr int kRW = 4;
-constexpr int kRThreads = 64 * kRW;
-constexpr int kRR = 3;                        // output rows a unit
-constexpr int kRCT = 5;                       // 16-pixel column tiles
-constexpr int kRBlk = OH / kRR;               // 19 row blocks
-static_assert(kRBlk * kRR == OH, "conv1r row blocks");
-constexpr int kRU = kRBlk * kRCT;             // 95 units a sample
-constexpr int kRSteps = (kRU + kRW - 1) / kRW;  // 24 steps a sample
-constexpr int kRUP = kRSteps * kRW;           // 96 unit slots a sample (the last idle)
-constexpr int kRIn = 2 * kRR + 6;             // 12 input rows a unit
-constexpr int kRRing = 32;                    // ring rows (a power of two)
-constexpr int kRRowB = IW * 8;                // 1280 B: fp16 x 4 channels a pixel
-constexpr int kRQuads = IW / 4;               // 4-pixel load items per row
-constexpr int kRMaxNew = kRIn;                // new rows a step (12 at a sample start)
-constexpr int kRPre = (kRMaxNew * kRQuads + kRThreads - 1) / kRThreads;
-using f32x4 = __attribute__((ext_vector_type(4))) float;
-
-__host__ __device__ constexpr int r_srow(int u) {   // stream row of unit slot u's first input row
-  return (u / kRUP) * IH + 2 * kRR * ((u % kRUP) / kRCT < kRBlk - 1 ? (u % kRUP) / kRCT : kRBlk - 1);
-}
-
-template <bool kStats>
-__global__ void __launch_bounds__(kRThreads, 2)
-conv1r_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, int s2,
-              const half8* __restrict__ wfrag, const float* __restrict__ bias,
-              __half* __restrict__ y, float* __restrict__ partials, float slope, WeightSplit ws) {
-  // + 64 B: the last column tile's invalid lanes read up to 48 B past a row
-  __shared__ __attribute__((aligned(16))) unsigned char rb[kRRing * kRRowB + 64];
-  __shared__ float red[2][kRW][CO][3];
-  __shared__ float s_bias[CO];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int n16 = lane & 15, g4 = lane >> 4;
-  const SplitPart sp = split_part(ws, n);
-  if (sp.set2) {
-    wfrag = static_cast<const half8*>(ws.wfrag);
-    bias = ws.bias;
-  }
-  const int send = sp.send;
-  const int U = sp.my * kRUP;
-  if (U == 0) return;
-  const int steps = sp.my * kRSteps;
-  auto sample = [&](int k) __attribute__((always_inline)) { return sp.sbeg + sp.bid + k * sp.gdim; };
-  const size_t plane = (size_t)IH * IW;
-  auto hi_of = [&](int st) __attribute__((always_inline)) {
-    return r_srow(kRW * st + kRW - 1) + kRIn - 1;
-  };
-
-  int it_r[kRPre], it_off[kRPre], it_lds[kRPre];
-#pragma unroll
-  for (int i = 0; i < kRPre; ++i) {
-    const int q = tid + i * kRThreads;
-    it_r[i] = q / kRQuads;
-    it_off[i] = it_r[i] * IW + 4 * (q - it_r[i] * kRQuads);
-    it_lds[i] = 32 * (q - it_r[i] * kRQuads);
-  }
-  // stream rows r0..r1 (one sample's; none when r1 < r0) into registers: every
-  // load issued on every path (clamped), so the compiler's vmcnt waits stay exact
-  auto issue = [&](float4 (&pre)[kRPre][3], int r0, int r1) __attribute__((always_inline)) {
-    const int rows = r1 - r0 + 1;
-    const int k = r0 / IH;
-    const int ns = sample(k) < send ? sample(k) : send - 1;
-    const float* base = ring + (size_t)ns * slots * plane + (size_t)(rows > 0 ? r0 - k * IH : 0) * IW;
-    const float* p0 = base + (size_t)s0 * plane;
-    const float* p1 = base + (size_t)s1 * plane;
-    const float* p2 = base + (size_t)s2 * plane;
-#pragma unroll
-    for (int i = 0; i < kRPre; ++i) {
-      const int off = it_r[i] < rows ? it_off[i] : 0;
-      CONV1_CHECK(p0 + off);
-      CONV1_CHECK(p1 + off);
-      CONV1_CHECK(p2 + off);
-      pre[i][0] = *reinterpret_cast<const float4*>(p0 + off);
-      pre[i][1] = *reinterpret_cast<const float4*>(p1 + off);
-      pre[i][2] = *reinterpret_cast<const float4*>(p2 + off);
-    }
-  };
-  // 4 pixels x (3 channels + a zero) fp16 = 32 B into ring slot (r0 + row) % kRRing
-  auto commit = [&](const float4 (&pre)[kRPre][3], int r0, int r1) __attribute__((always_inline)) {
-    const int rows = r1 - r0 + 1;
-#pragma unroll
-    for (int i = 0; i < kRPre; ++i) {
-      if (it_r[i] >= rows) continue;
-      const int slot = (r0 + it_r[i]) & (kRRing - 1);
-      const float av[4] = {pre[i][0].x, pre[i][0].y, pre[i][0].z, pre[i][0].w};
-      const float bv[4] = {pre[i][1].x, pre[i][1].y, pre[i][1].z, pre[i][1].w};
-      const float cv[4] = {pre[i][2].x, pre[i][2].y, pre[i][2].z, pre[i][2].w};
-      uint32_t u[8];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const __half2 lo = __floats2half2_rn(av[e], bv[e]);
-        const __half2 hi = __floats2half2_rn(cv[e], 0.0f);
-        u[2 * e] = *reinterpret_cast<const uint32_t*>(&lo);
-        u[2 * e + 1] = *reinterpret_cast<const uint32_t*>(&hi);
-      }
-      u32x4* dst = reinterpret_cast<u32x4*>(rb + slot * kRRowB + it_lds[i]);
-      dst[0] = u32x4{u[0], u[1], u[2], u[3]};
-      dst[1] = u32x4{u[4], u[5], u[6], u[7]};
-    }
-  };
-
-  // A fragments: wa[ky][h] = rows 16h..16h+15 (out channels), k = (kx, c) of
-  // kernel row ky, lane (m = n16, group g4): kx = 2 g4 + e / 4, c = e % 4 --
-  // one 16-B load each from the dt_conv1 fragment layout (include/dtactor.h)
-  half8 wa[8][2];
-#pragma unroll
-  for (int ky = 0; ky < 8; ++ky)
-#pragma unroll
-    for (int h = 0; h < 2; ++h)
-      wa[ky][h] = wfrag[(2 * ky + (g4 >> 1)) * 64 + 32 * (g4 & 1) + 16 * h + n16];
-  if (tid < CO) s_bias[tid] = bias[tid];
-  float w_cnt = 0.0f, w_mean[8], w_m2[8];
-#pragma unroll
-  for (int r = 0; r < 8; ++r) w_mean[r] = w_m2[r] = 0.0f;
-
-  // wave 0: the (mean, M2) of sample k from the 4 waves' flushes
-  auto merge = [&](int k) __attribute__((always_inline)) {
-    if (kStats && tid < CO) {
-      float cnt = 0.0f, mean = 0.0f, m2 = 0.0f;
-      for (int w = 0; w < kRW; ++w) {
-        const float nb = red[k & 1][w][tid][0];
-        if (nb <= 0.0f) continue;
-        const float tot = cnt + nb, d = red[k & 1][w][tid][1] - mean;
-        mean += d * (nb / tot);
-        m2 += red[k & 1][w][tid][2] + d * d * (cnt * nb / tot);
-        cnt = tot;
-      }
-      float* pp = partials + ((size_t)sample(k) * CO + tid) * 2;
-      pp[0] = mean;
-      pp[1] = m2;
-    }
-  };
-
-  auto unit = [&](int u) __attribute__((always_inline)) {
-    const int k = u / kRUP, ul = u - k * kRUP;
-    const int b = ul / kRCT, j = ul - b * kRCT;
-    const int ns = sample(k);
-    const int ox = 16 * j + n16;
-    const bool valid = ox < OW;
-    const int sr = k * IH + 2 * kRR * b;
-    f32x4 acc[kRR][2];
-#pragma unroll
-    for (int i = 0; i < kRR; ++i)
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) acc[i][h][r] = s_bias[16 * h + 4 * g4 + r];
-    half8 bq[kRIn];
-    const int cb = 16 * (16 * j + n16 + g4);   // pixels 2 ox + 2 g4, +1: 16-B aligned
-#pragma unroll
-    for (int r = 0; r < kRIn; ++r)
-      bq[r] = (DTCONV_SKIP & 32) ? wa[r & 7][0]
-                                 : *reinterpret_cast<const half8*>(
-                                       rb + ((sr + r) & (kRRing - 1)) * kRRowB + cb);
-#pragma unroll
-    for (int r = 0; r < kRIn && !(DTCONV_SKIP & 2); ++r)
-#pragma unroll
-      for (int i = 0; i < kRR; ++i) {
-        const int ky = r - 2 * i;
-        if (ky < 0 || ky > 7) continue;
-#pragma unroll
-        for (int h = 0; h < 2; ++h)
-          acc[i][h] = __builtin_amdgcn_mfma_f32_16x16x32_f16(wa[ky][h], bq[r], acc[i][h], 0, 0, 0);
-      }
-    // epilogue: bias (in acc) + LeakyReLU, fp16 NHWC (8 B: 4 channels a lane
-    // and half), Welford over the valid pixels
-    constexpr int kBytes = kSPix * CO * 2;
-    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
-        reinterpret_cast<void*>(y + (size_t)ns * kSPix * CO), 0, kBytes, 0x00020000);
-#pragma unroll
-    for (int i = 0; i < kRR; ++i) {
-      const int oy = kRR * b + i;
-      float v[8];
-#pragma unroll
-      for (int h = 0; h < 2; ++h)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) v[4 * h + r] = lrelu2(acc[i][h][r], slope);
-#pragma unroll
-      for (int h = 0; h < 2; ++h) {
-        const __half2 a0 = __floats2half2_rn(v[4 * h + 0], v[4 * h + 1]);
-        const __half2 a1 = __floats2half2_rn(v[4 * h + 2], v[4 * h + 3]);
-        using u32x2 = __attribute__((ext_vector_type(2))) uint32_t;
-        const u32x2 d = {*reinterpret_cast<const uint32_t*>(&a0),
-                         *reinterpret_cast<const uint32_t*>(&a1)};
-        const int off = valid ? ((oy * OW + ox) * CO + 16 * h + 4 * g4) * 2 : kBytes;
-        if (!(DTCONV_SKIP & 4)) __builtin_amdgcn_raw_buffer_store_b64(d, rsrc, off, 0, 0);
-      }
-      if (kStats && valid && !(DTCONV_SKIP & 8)) {
-        w_cnt += 1.0f;
-        const float inv = __builtin_amdgcn_rcpf(w_cnt);
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const float d = v[r] - w_mean[r];
-          w_mean[r] += d * inv;
-          w_m2[r] += d * (v[r] - w_mean[r]);
-        }
-      }
-    }
-    // the wave's last unit of sample k: its statistics into red[k & 1]
-    if (kStats && ul + kRW >= kRU) {
-#pragma unroll
-      for (int o = 1; o < 16; o <<= 1) {   // the 16 pixels of a channel group
-        const float nb = __shfl_xor(w_cnt, o, 16);
-        const float tot = w_cnt + nb;
-        const float fa = tot > 0.0f ? nb / tot : 0.0f, fb = tot > 0.0f ? w_cnt * nb / tot : 0.0f;
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const float mb = __shfl_xor(w_mean[r], o, 16), m2b = __shfl_xor(w_m2[r], o, 16);
-          const float d = mb - w_mean[r];
-          w_mean[r] += d * fa;
-          w_m2[r] += m2b + d * d * fb;
-        }
-        w_cnt = tot;
-      }
-      if (n16 == 0)
-#pragma unroll
-        for (int r = 0; r < 8; ++r) {
-          const int c = 16 * (r >> 2) + 4 * g4 + (r & 3);
-          red[k & 1][wave][c][0] = w_cnt;
-          red[k & 1][wave][c][1] = w_mean[r];
-          red[k & 1][wave][c][2] = w_m2[r];
-        }
-      w_cnt = 0.0f;
-#pragma unroll
-      for (int r = 0; r < 8; ++r) w_mean[r] = w_m2[r] = 0.0f;
-    }
-  };
-
-  auto step = [&](int st, float4 (&nxt)[kRPre][3], const float4 (&cur)[kRPre][3]) __attribute__((always_inline)) {
-    // step st + 2's new rows into registers (none past the last step)
-    if (!(DTCONV_SKIP & 1)) {
-      if (st + 2 < steps) issue(nxt, hi_of(st + 1) + 1, hi_of(st + 2));
-      else issue(nxt, 1, 0);
-    }
-    // a sample whose last step was st - 1: its flushes are behind the barrier
-    if (st > 0 && st % kRSteps == 0) merge(st / kRSteps - 1);
-    const int u = kRW * st + wave;
-    if (u % kRUP < kRU) unit(u);
-    if (st + 1 < steps && !(DTCONV_SKIP & 16)) commit(cur, hi_of(st) + 1, hi_of(st + 1));
-    __syncthreads();
-  };
-
-  float4 pa[kRPre][3], pb[kRPre][3];
-  issue(pa, 0, hi_of(0));
-  commit(pa, 0, hi_of(0));
-  if (steps > 1) issue(pb, hi_of(0) + 1, hi_of(1));
-  else issue(pb, 1, 0);
-  __syncthreads();
-  __builtin_amdgcn_s_waitcnt(0);
-  for (int st = 0; st < steps; st += 2) {
-    step(st, pa, pb);
-    if (st + 1 < steps) step(st + 1, pb, pa);
-  }
-  // the last sample's statistics (its last unit was in the final step)
-  merge(sp.my - 1);
 }
 
 // Reference mode: y = (y - mean) / sqrt(var + eps) * gamma + beta in place from
@@ -1224,28 +948,6 @@ extern "C" int dt_conv1_split(const float* ring, int32_t n, int32_t slots, const
     ws.wfrag = set2->wfrag;
     ws.bias = set2->bias;
   }
-#if DTCONV1_FORM == 1
-  static int rgrid = 0;
-  if (!rgrid) {
-    int dev = 0, cus = 256, per = 2;
-    if (hipGetDevice(&dev) == hipSuccess)
-      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, conv1r_kernel<true>, kRThreads, 0) !=
-            hipSuccess || per < 1)
-      per = 1;
-    rgrid = per * cus;
-  }
-  const int gr = split_grid(ws, n, set2 ? set2->n0 : n, rgrid);
-  if (partials)
-    hipLaunchKernelGGL(conv1r_kernel<true>, dim3(gr), dim3(kRThreads), 0, (hipStream_t)stream, n,
-                       ring, slots, order[0], order[1], order[2], (const half8*)wfrag, bias,
-                       (__half*)y, partials, slope, ws);
-  else
-    hipLaunchKernelGGL(conv1r_kernel<false>, dim3(gr), dim3(kRThreads), 0, (hipStream_t)stream, n,
-                       ring, slots, order[0], order[1], order[2], (const half8*)wfrag, bias,
-                       (__half*)y, nullptr, slope, ws);
-  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
-#endif
   const int g = split_grid(ws, n, set2 ? set2->n0 : n, grid);
   if (partials)
     hipLaunchKernelGGL(conv1s_kernel<true>, dim3(g), dim3(kSThreads), 0, (hipStream_t)stream, n,

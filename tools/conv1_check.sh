@@ -1,13 +1,13 @@
 #!/bin/bash
-# conv1 form check: actor GPU tests, then dt_conv1 alone (tools/conv1_micro.py)
-# for the row-strip (new) and streaming-tile (old) forms on random and
-# frame-like operands, then the config-4 bench line
+# conv1 check: actor GPU tests, then dt_conv1 alone (tools/conv1_micro.py
+# variants built beforehand into diag_so/conv1_variants$TAG, TAGS selects) on
+# random and frame-like operands, then the config-4 bench line
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out; export TMPDIR=/tmp
 timeout -k 10 400 python -u -m pytest tests/test_gpu_actor.py -x -q --timeout 200 --timeout-method thread > gpurun_out/c1_pytest.log 2>&1 || { tail -40 gpurun_out/c1_pytest.log; exit 1; }
 tail -1 gpurun_out/c1_pytest.log
-for tag in _new _old; do
+for tag in ${TAGS:-""}; do
   for data in random frames; do
     echo "== $tag $data"
     CONV1_ONLY=full CONV1_TAG=$tag CONV1_DATA=$data timeout -k 10 120 python tools/conv1_micro.py 2>&1 | grep -v amdgpu.ids || exit 1

@@ -4,7 +4,7 @@
 # piecewise-constant operands (tools/conv1_micro.py variants in diag_so/, TAGS / DATAS select).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd); mkdir -p gpurun_out; export TMPDIR=/tmp
-for tag in ${TAGS:-_new _old}; do for data in ${DATAS:-random zero frames}; do
+for tag in ${TAGS:-""}; do for data in ${DATAS:-random zero frames}; do
   CONV1_DATA=$data CONV1_TAG=$tag CONV1_ONLY=full timeout -k 10 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_WAVE_CYCLES \
       --kernel-trace --output-format csv -d "$ROOT/gpurun_out/clk_$tag$data" -o run -- python3 "$ROOT/tools/conv1_micro.py" > gpurun_out/clk_$tag$data.log 2>&1 || { echo "fail $data"; exit 1; }
   python3 - "$ROOT/gpurun_out/clk_$tag$data" "$tag $data" <<'PY'
