@@ -140,20 +140,19 @@ constexpr int kBlock = 256;        // step and refill blocks (4 waves)
 __device__ inline void put_slot(const dt::State& st, int n, int e, uint32_t key, bool ok,
                                 uint32_t tag, double x, double z, double a, double dist,
                                 double arad) {
-  (void)n;
-  const uint32_t sl = key % (uint32_t)dt::kSlots;
-  double* p = dt::slot_rec(st, (size_t)e, sl);
+  const size_t sl = key % (uint32_t)dt::kSlots;
+  double* p = st.pre + sl * dt::kSlotRec * (size_t)n + e;
   double sa = 0.0, ca = 1.0;
   sincos(a, &sa, &ca);
   p[0] = x;
-  p[1] = z;
-  p[2] = a;
-  p[3] = dist;
-  p[4] = arad;
-  p[5] = sa;
-  p[6] = ca;
+  p[(size_t)n] = z;
+  p[2 * (size_t)n] = a;
+  p[3 * (size_t)n] = dist;
+  p[4 * (size_t)n] = arad;
+  p[5 * (size_t)n] = sa;
+  p[6 * (size_t)n] = ca;
   const uint64_t w = ((uint64_t)tag << 32) | (ok ? key : (key | dt::kKeyFailed));
-  __hip_atomic_store(dt::slot_word(st, (size_t)e, sl), w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __hip_atomic_store(st.pre_key + sl * n + e, w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 #ifndef DTSIM_REFILL_ENVS
 #define DTSIM_REFILL_ENVS 8
@@ -181,7 +180,7 @@ __device__ int refill_group(const dt::State& st, const dt::MapDev& md, const dt:
     uint32_t have[dt::kSlots];
 #pragma unroll
     for (int s = 0; s < dt::kSlots; ++s)
-      have[s] = (uint32_t)__hip_atomic_load(dt::slot_word(st, (size_t)e, (uint32_t)s), __ATOMIC_RELAXED,
+      have[s] = (uint32_t)__hip_atomic_load(st.pre_key + (size_t)s * n + e, __ATOMIC_RELAXED,
                                              __HIP_MEMORY_SCOPE_AGENT);
     const uint64_t seed = st.seed[e];
 #pragma unroll
@@ -409,7 +408,7 @@ __global__ __launch_bounds__(kBlock) void step_kernel(dt::State st, dt::MapDev m
     seed = st.seed[ei];
 #pragma unroll
     for (int q = 0; q < dt::kSlots; ++q)
-      words[q] = __hip_atomic_load(dt::slot_word(st, (size_t)ei, (uint32_t)q), __ATOMIC_RELAXED,
+      words[q] = __hip_atomic_load(st.pre_key + (size_t)q * n + ei, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
   }
   const MapLds M = dt::stage_map(md, lds);
@@ -440,9 +439,9 @@ __global__ __launch_bounds__(kBlock) void step_kernel(dt::State st, dt::MapDev m
     const uint32_t rel = key - key0;
     const bool slot_ready = rel < (uint32_t)dt::kSlots && ((ready >> rel) & 1u) != 0u;
     if (slot_ready) {
-      const double* pr = dt::slot_rec(st, (size_t)ei, key % (uint32_t)dt::kSlots);
+      const size_t sl = key % (uint32_t)dt::kSlots;
 #pragma unroll
-      for (int q = 0; q < dt::kSlotRec; ++q) rp[q] = pr[q];
+      for (int q = 0; q < dt::kSlotRec; ++q) rp[q] = st.pre[(sl * dt::kSlotRec + q) * (size_t)n + ei];
     }
     asm volatile("" ::: "memory");  // keep the loads here, ahead of the decision
 
@@ -622,7 +621,7 @@ __global__ __launch_bounds__(kFanBlock) __attribute__((amdgpu_waves_per_eu(2, 2)
     seed = st.seed[ei];
 #pragma unroll
     for (int j = 0; j < dt::kSlots; ++j)
-      words[j] = __hip_atomic_load(dt::slot_word(st, (size_t)ei, (uint32_t)j), __ATOMIC_RELAXED,
+      words[j] = __hip_atomic_load(st.pre_key + (size_t)j * n + ei, __ATOMIC_RELAXED,
                                    __HIP_MEMORY_SCOPE_AGENT);
   }
   // staged in LDS behind the map image: the block's spawn-ahead slot records
@@ -630,23 +629,19 @@ __global__ __launch_bounds__(kFanBlock) __attribute__((amdgpu_waves_per_eu(2, 2)
   // no block of this launch rewrites) and its actions of all k decisions
   // (k <= kFanMaxK; the host splits longer runs) -- no global load and no
   // prefetch register in the decision loop
-  // the block's records, [16 envs][kSlots][kSlotStride] as in HBM: one
-  // contiguous 8 KB block, 16 B a lane per load
-  double* sslot = reinterpret_cast<double*>(lds + map_lds_offset);
-  float2* sact = reinterpret_cast<float2*>(sslot + kFanEnvs * dt::kSlots * dt::kSlotStride);
+  double* sslot = reinterpret_cast<double*>(lds + map_lds_offset);   // [kSlots*kSlotRec][16]
+  float2* sact = reinterpret_cast<float2*>(sslot + dt::kSlots * dt::kSlotRec * kFanEnvs);
   {
     const int e0 = (int)blockIdx.x * kFanEnvs;
     for (int i = (int)threadIdx.x; i < k * kFanEnvs; i += kFanBlock) {
       const int dd = i / kFanEnvs, j = i % kFanEnvs;
       if (e0 + j < n) sact[i] = act[(size_t)dd * n + e0 + j];
     }
-    if (sc.auto_reset) {
-      constexpr int kPerEnv = dt::kSlots * dt::kSlotStride / 2;   // double2 a record block
-      const double2* src = reinterpret_cast<const double2*>(dt::slot_rec(st, (size_t)e0, 0u));
-      double2* dst = reinterpret_cast<double2*>(sslot);
-      for (int i = (int)threadIdx.x; i < kFanEnvs * kPerEnv; i += kFanBlock)
-        if (e0 + i / kPerEnv < n) dst[i] = src[i];
-    }
+    if (sc.auto_reset)
+      for (int i = (int)threadIdx.x; i < dt::kSlots * dt::kSlotRec * kFanEnvs; i += kFanBlock) {
+        const int row = i / kFanEnvs, j = i % kFanEnvs;
+        if (e0 + j < n) sslot[i] = st.pre[(size_t)row * n + e0 + j];
+      }
   }
   const MapLds M = dt::stage_map(md, lds);   // its barrier also covers sact
   const uint32_t key0 = key;
@@ -858,7 +853,7 @@ __global__ __launch_bounds__(kFanBlock) __attribute__((amdgpu_waves_per_eu(2, 2)
     if (want_reset && slot_ready) {
       const int sl = (int)(key % (uint32_t)dt::kSlots);
 #pragma unroll
-      for (int j = 0; j < dt::kSlotRec; ++j) rp[j] = sslot[(le * dt::kSlots + sl) * dt::kSlotStride + j];
+      for (int j = 0; j < dt::kSlotRec; ++j) rp[j] = sslot[(sl * dt::kSlotRec + j) * kFanEnvs + le];
     }
     uint64_t need = __ballot(want_reset && !slot_ready && lead);
     while (need) {  // wave-uniform; every wave computes the same spawns
@@ -1197,12 +1192,12 @@ int dt_create(const dt_config* cfg, const dt_map* map, uint64_t seed, int32_t n_
   h->lds_bytes = lds;
 
   // state: x z angle seed (8 B) | step_count env_step episode (4 B) | err | stats |
-  // spawn-ahead: pre (kSlots x kSlotStride x 8 B, 256-B aligned) | want tick (4 B)
+  // spawn-ahead: pre (kSlots x kSlotRec x 8 B) | pre_key (kSlots x 8 B) | want tick (4 B)
   const size_t N = (size_t)n_envs, N8 = N * 8, N4 = (N * 4 + 255) & ~255ul;
   const size_t S = (size_t)dt::kSlots;
-  const size_t spawn_at = (4 * N8 + 3 * N4 + 512 + 255) & ~255ul;
-  const size_t R = (size_t)dt::kSlotStride;
-  const size_t total = spawn_at + R * S * N8 + 2 * N4;
+  const size_t spawn_at = 4 * N8 + 3 * N4 + 512;
+  const size_t R = (size_t)dt::kSlotRec;
+  const size_t total = spawn_at + (R + 1) * S * N8 + 2 * N4;
   if (hipMalloc(&h->st_buf, total) != hipSuccess) return fail("hipMalloc(state)");
   if (hipMemset(h->st_buf, 0, total) != hipSuccess) return fail("hipMemset(state)");
   char* sb = (char*)h->st_buf;
@@ -1216,8 +1211,9 @@ int dt_create(const dt_config* cfg, const dt_map* map, uint64_t seed, int32_t n_
   h->st.err = (uint32_t*)(sb + 4 * N8 + 3 * N4);
   h->st.stats = (unsigned long long*)(sb + 4 * N8 + 3 * N4 + 256);
   h->st.pre = (double*)(sb + spawn_at);
-  h->st.want = (uint32_t*)(sb + spawn_at + R * S * N8);
-  h->st.tick = (uint32_t*)(sb + spawn_at + R * S * N8 + N4);
+  h->st.pre_key = (uint64_t*)(sb + spawn_at + R * S * N8);
+  h->st.want = (uint32_t*)(sb + spawn_at + (R + 1) * S * N8);
+  h->st.tick = (uint32_t*)(sb + spawn_at + (R + 1) * S * N8 + N4);
   *out = h;
   rc = dt_render_init(h, map);
   if (rc == DT_OK) rc = dt_seed(h, nullptr, seed, 0);
@@ -1249,10 +1245,8 @@ static int refill_from_counters(dt_handle* h, int e0, int e1) {
   HIP_OR_FAIL(h, hipMemcpy(ep.data(), h->st.episode + e0, m * 4, hipMemcpyDeviceToHost));
   for (size_t i = 0; i < m; ++i) want[i] = ep[i] + 1u;
   HIP_OR_FAIL(h, hipMemcpy(h->st.want + e0, want.data(), m * 4, hipMemcpyHostToDevice));
-  (void)n;
-  // every record of the envs, slot words included, to all ones (kKeyNone)
-  HIP_OR_FAIL(h, hipMemset(dt::slot_rec(h->st, (size_t)e0, 0u), 0xFF,
-                           m * dt::kSlots * dt::kSlotStride * sizeof(double)));
+  for (size_t q = 0; q < (size_t)dt::kSlots; ++q)
+    HIP_OR_FAIL(h, hipMemset(h->st.pre_key + q * n + e0, 0xFF, m * 8));
   hipLaunchKernelGGL(refill_kernel, dim3(refill_grid(h->n, kRefillEnvs)), dim3(kBlock), h->lds_bytes, (hipStream_t)0,
                      h->st, h->map, h->geo, h->n, h->sc.max_spawn_attempts, h->env_base);
   HIP_OR_FAIL(h, hipGetLastError());
@@ -1337,7 +1331,7 @@ int dt_step_many(dt_handle* h, int32_t k, const float* actions, double* reward,
     // step_fan_kernel: 16 envs x 4 waves per workgroup
     const int gs = (h->n + kFanEnvs - 1) / kFanEnvs;
     const size_t off = (h->lds_bytes + 15) & ~(size_t)15;
-    const size_t slots = (size_t)dt::kSlots * dt::kSlotStride * kFanEnvs * sizeof(double);
+    const size_t slots = (size_t)dt::kSlots * dt::kSlotRec * kFanEnvs * sizeof(double);
     // runs of more than kFanMaxK decisions: consecutive launches (the state,
     // counters and spawn window carry over exactly as between calls)
     const bool lean = h->sc.action_mode == DT_ACTION_WHEELS && h->sc.clip && !h->sc.speed_measured &&

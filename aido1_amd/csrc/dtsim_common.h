@@ -39,17 +39,15 @@ struct State {
   uint32_t* episode;
   uint32_t* err;  // one word, OR of kErr*
   unsigned long long* stats;  // [4] sim steps, decisions, resets, episodes done
-  // spawn-ahead: slot k % kSlots of env e is one 64-B record
-  // pre[e][k % kSlots][0..7]: the reset pose of spawn key k (x, z, angle, lane
-  // dist, angle_rad, sin and cos of the angle) and, as element 7, the slot word
-  // (slot_word): its low half is k (bit 31: the spawn failed), its high half
-  // the launch tick the slot was written in.  One refill writes one whole
-  // 64-B record (one HBM write sector, not eight scattered ones), and a
-  // workgroup's envs' records are one contiguous block.  want[e] - 1 = the
-  // env's episode counter as its last launch left it; the window [want - 1,
-  // want - 1 + kSlots) is kept filled.  tick[e] counts the step launches over
-  // env e.
-  double* pre;                // [n][kSlots][kSlotStride]
+  // spawn-ahead: slot k % kSlots of env e holds the reset pose
+  // of spawn key k (x, z, angle, lane dist, angle_rad, sin and cos of the
+  // angle) when the low word of
+  // pre_key[k % kSlots][e] is k (bit 31: the spawn failed); its high word is
+  // the launch tick the slot was written in.  want[e] - 1 = the env's episode
+  // counter as its last launch left it; the window [want - 1, want - 1 +
+  // kSlots) is kept filled.  tick[e] counts the step launches over env e.
+  double* pre;                // [kSlots][kSlotRec][n]
+  uint64_t* pre_key;          // [kSlots][n]
   uint32_t* want;             // [n]
   uint32_t* tick;             // [n]
 };
@@ -57,13 +55,6 @@ constexpr uint32_t kKeyFailed = 0x80000000u;
 constexpr uint32_t kKeyNone = 0xFFFFFFFFu;
 constexpr int kSlots = 8;    // power of two
 constexpr int kSlotRec = 7;  // x, z, angle, lane dist, angle_rad, sin, cos
-constexpr int kSlotStride = 8;  // doubles a record: kSlotRec + the slot word
-__device__ __host__ inline double* slot_rec(const State& st, size_t e, uint32_t slot) {
-  return st.pre + (e * kSlots + slot) * kSlotStride;
-}
-__device__ __host__ inline uint64_t* slot_word(const State& st, size_t e, uint32_t slot) {
-  return reinterpret_cast<uint64_t*>(slot_rec(st, e, slot) + kSlotRec);
-}
 
 // One atomic per wave: the lane sum of v (0 <= v <= vmax, vmax wave-uniform)
 // from one ballot per bit, lane 0 adds.
