@@ -22,7 +22,7 @@ SOURCES = ['dtsim.hip', 'dtrender.hip', 'dtreplay.hip', 'dtactor.hip', 'dtconv.h
 HEADERS = ['dtsim_common.h', 'dtrender.h']
 PUBLIC_HEADERS = ['dtsim.h', 'dtreplay.h', 'dtactor.h', 'dttrain.h']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
-ABI_VERSION = 6
+ABI_VERSION = 7
 
 HIP_FLAGS = ['--offload-arch=gfx950', '-O3', '-fPIC', '-shared', '-std=c++17',
              '-ffp-contract=off', '-munsafe-fp-atomics']
@@ -137,6 +137,12 @@ def lib():
             'dt_line_detect': (ctypes.c_int, [vp, vp, i32, i32, i32, vp, vp, vp]),
             'dt_hough_lines': (ctypes.c_int, [vp, i32, i32, i32, i32, i32, i32, i32, vp, vp,
                                               vp]),
+            'dt_line_detect_workspace': (ctypes.c_size_t, [i32, i32, i32]),
+            'dt_line_detect_ws': (ctypes.c_int, [vp, vp, i32, i32, i32, vp, vp, vp,
+                                                 ctypes.c_size_t, vp]),
+            'dt_hough_workspace': (ctypes.c_size_t, [i32, i32, i32]),
+            'dt_hough_lines_ws': (ctypes.c_int, [vp, i32, i32, i32, i32, i32, i32, i32, vp, vp,
+                                                 vp, ctypes.c_size_t, vp]),
             'dt_get_state': (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp]),
             'dt_set_state': (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp]),
             'dt_check': (ctypes.c_int, [vp, ctypes.POINTER(u32)]),
@@ -157,7 +163,8 @@ def lib():
             # dttrain.h
             'dt_train_work_floats': (i64, [i64]),
             'dt_bn_leaky_fwd': (ctypes.c_int, [i64, vp, vp, ctypes.c_float, vp, vp, ctypes.c_float,
-                                               ctypes.c_float, vp, vp, vp, vp, vp, vp, vp, vp]),
+                                               ctypes.c_float, vp, vp, vp, i32, vp, vp, vp, vp,
+                                               vp]),
             'dt_bn_leaky_bwd': (ctypes.c_int, [i64, vp, vp, vp, vp, ctypes.c_float, vp, vp, vp, vp,
                                                vp, vp]),
             'dt_adam': (ctypes.c_int, [i32, vp, vp, vp, vp, f64, f64, f64, vp, vp]),
@@ -202,7 +209,7 @@ def exported_symbols():
     for h in PUBLIC_HEADERS:
         with open(os.path.join(REPO_DIR, 'include', h)) as f:
             src = f.read()
-        names |= set(re.findall(r'^\s*(?:int|int32_t|int64_t|void|const char\*)\s+(dt_\w+)\s*\(',
+        names |= set(re.findall(r'^\s*(?:int|int32_t|int64_t|size_t|void|const char\*)\s+(dt_\w+)\s*\(',
                                 src, re.M))
     return sorted(names)
 

@@ -162,23 +162,32 @@ LineDev to_line_dev(const dt_line_params& p) {
 }
 
 // ---- device passes -----------------------------------------------------------------
+// LineDetectorHSV on caller images.  The per-pixel planes live in LDS (images
+// of <= NPIX pixels, line_detect_kernel) or in a caller workspace in HBM (any
+// size, line_detect_big_kernel); the passes only see the PixBuf pointers.
 struct Lds {
   int16_t mag[NPIX];
   uint8_t work[NPIX];
   int sdiv[256];
   int hdiv[256];
 };
+struct PixBuf {
+  int16_t* mag;     // [h*w] Sobel L1 magnitude (max over the channels)
+  uint8_t* work;    // [h*w] colour bits | NMS direction | candidate / edge bits
+  const int* sdiv;  // cvtColor's division tables (LDS)
+  const int* hdiv;
+};
 
-__device__ inline void load_tables(Lds& S) {
+__device__ inline void load_tables(int* sdiv, int* hdiv) {
   for (int i = threadIdx.x; i < 256; i += blockDim.x) {
-    S.sdiv[i] = c_hsv.sdiv[i];
-    S.hdiv[i] = c_hsv.hdiv[i];
+    sdiv[i] = c_hsv.sdiv[i];
+    hdiv[i] = c_hsv.hdiv[i];
   }
 }
 
 // pass A for one pixel: Sobel/NMS dir + colour bits into work, magnitude into mag
 template <class Fetch>
-__device__ inline void pass_a_pixel(const Fetch& fetch, Lds& S, const LineDev& L, int hgt,
+__device__ inline void pass_a_pixel(const Fetch& fetch, const PixBuf& S, const LineDev& L, int hgt,
                                     int wid, int r, int c) {
   int dx, dy, m;
   sobel_max(fetch, r, c, hgt, wid, dx, dy, m);
@@ -190,12 +199,12 @@ __device__ inline void pass_a_pixel(const Fetch& fetch, Lds& S, const LineDev& L
   S.work[idx] = color_bits(L, h, s, v) | (uint8_t)(nms_dir(dx, dy) << B_DIR_SHIFT);
 }
 
-__device__ inline int mag_at(const Lds& S, int hgt, int wid, int r, int c) {
+__device__ inline int mag_at(const PixBuf& S, int hgt, int wid, int r, int c) {
   return ((unsigned)r < (unsigned)hgt && (unsigned)c < (unsigned)wid) ? S.mag[r * wid + c] : 0;
 }
 
 // pass B: Canny NMS + thresholds
-__device__ inline void pass_b(Lds& S, const LineDev& L, int hgt, int wid) {
+__device__ inline void pass_b(const PixBuf& S, const LineDev& L, int hgt, int wid) {
   const int np = hgt * wid;
   for (int idx = threadIdx.x; idx < np; idx += blockDim.x) {
     const int m = S.mag[idx];
@@ -215,39 +224,43 @@ __device__ inline void pass_b(Lds& S, const LineDev& L, int hgt, int wid) {
   }
 }
 
-// Canny hysteresis: candidates 8-connected to a strong pixel become edges.
-__device__ inline void hysteresis(Lds& S, int hgt, int wid) {
+// one hysteresis visit of a weak candidate: an edge if 8-connected to an edge
+__device__ inline bool hyst_visit(const PixBuf& S, int hgt, int wid, int idx) {
+  const uint8_t b = S.work[idx];
+  if ((b & (B_CAND | B_EDGE)) != B_CAND) return false;
+  const int r = idx / wid, c = idx - r * wid;
+  bool hit = false;
+  for (int dy = -1; dy <= 1 && !hit; ++dy) {
+    const int rr = r + dy;
+    if ((unsigned)rr >= (unsigned)hgt) continue;
+    for (int dx = -1; dx <= 1; ++dx) {
+      const int cc = c + dx;
+      if ((unsigned)cc >= (unsigned)wid) continue;
+      if (S.work[rr * wid + cc] & B_EDGE) {
+        hit = true;
+        break;
+      }
+    }
+  }
+  if (hit) S.work[idx] = b | B_EDGE;
+  return hit;
+}
+
+// Canny hysteresis: candidates 8-connected to a strong pixel become edges
+// (sweeps over every pixel to a fixed point; the result is the reachability
+// closure, whatever order the sweeps visit in).
+__device__ inline void hysteresis(const PixBuf& S, int hgt, int wid) {
   const int np = hgt * wid;
   for (;;) {
     int changed = 0;
-    for (int idx = threadIdx.x; idx < np; idx += blockDim.x) {
-      const uint8_t b = S.work[idx];
-      if ((b & (B_CAND | B_EDGE)) != B_CAND) continue;
-      const int r = idx / wid, c = idx - r * wid;
-      bool hit = false;
-      for (int dy = -1; dy <= 1 && !hit; ++dy) {
-        const int rr = r + dy;
-        if ((unsigned)rr >= (unsigned)hgt) continue;
-        for (int dx = -1; dx <= 1; ++dx) {
-          const int cc = c + dx;
-          if ((unsigned)cc >= (unsigned)wid) continue;
-          if (S.work[rr * wid + cc] & B_EDGE) {
-            hit = true;
-            break;
-          }
-        }
-      }
-      if (hit) {
-        S.work[idx] = b | B_EDGE;
-        changed = 1;
-      }
-    }
+    for (int idx = threadIdx.x; idx < np; idx += blockDim.x)
+      if (hyst_visit(S, hgt, wid, idx)) changed = 1;
     if (!__syncthreads_or(changed)) break;
   }
 }
 
 // pass C for one pixel: dilated colour bits | edge bit (bit 3)
-__device__ inline uint8_t pass_c_pixel(const Lds& S, const LineDev& L, int hgt, int wid, int r,
+__device__ inline uint8_t pass_c_pixel(const PixBuf& S, const LineDev& L, int hgt, int wid, int r,
                                        int c) {
   uint8_t bits = 0;
   const int R = L.dil_r;
@@ -1276,15 +1289,16 @@ __global__ __launch_bounds__(kThreads) void line_detect_kernel(LineDev L, const 
   __shared__ __attribute__((aligned(16))) uint32_t src[NPIX];
   __shared__ __attribute__((aligned(16))) Lds S;
   const int e = blockIdx.x, np = hgt * wid;
+  const PixBuf B{S.mag, S.work, S.sdiv, S.hdiv};
   const uint8_t* in = bgr + (size_t)e * np * 3;
   for (int p = threadIdx.x; p < np; p += blockDim.x)
     src[p] = (uint32_t)in[3 * p] | ((uint32_t)in[3 * p + 1] << 8) | ((uint32_t)in[3 * p + 2] << 16);
-  load_tables(S);
+  load_tables(S.sdiv, S.hdiv);
   __syncthreads();
   const auto fetch = [&](int r, int c) -> uint32_t { return src[r * wid + c]; };
   for (int p = threadIdx.x; p < np; p += blockDim.x) {
     const int r = p / wid, c = p - r * wid;
-    pass_a_pixel(fetch, S, L, hgt, wid, r, c);
+    pass_a_pixel(fetch, B, L, hgt, wid, r, c);
     if (hsv) {
       int h, s, v;
       const uint32_t q = src[p];
@@ -1296,13 +1310,80 @@ __global__ __launch_bounds__(kThreads) void line_detect_kernel(LineDev L, const 
     }
   }
   __syncthreads();
-  pass_b(S, L, hgt, wid);
+  pass_b(B, L, hgt, wid);
   __syncthreads();
-  hysteresis(S, hgt, wid);
+  hysteresis(B, hgt, wid);
   uint8_t* mb = masks + (size_t)e * 4 * np;
   for (int p = threadIdx.x; p < np; p += blockDim.x) {
     const int r = p / wid, c = p - r * wid;
-    const uint8_t b = pass_c_pixel(S, L, hgt, wid, r, c);
+    const uint8_t b = pass_c_pixel(B, L, hgt, wid, r, c);
+    mb[p] = b & 1 ? 255 : 0;
+    mb[np + p] = b & 2 ? 255 : 0;
+    mb[2 * np + p] = b & 4 ? 255 : 0;
+    mb[3 * np + p] = b & 8 ? 255 : 0;
+  }
+}
+
+// The same on images of any size (e.g. the 640x480 camera frame of
+// duckietown_rl/env.py:12-16): one 1024-thread workgroup per image, the
+// magnitude / work planes and the weak-candidate list in the caller's
+// workspace (line_ws_stride bytes an image, L2-resident while the workgroup
+// runs).  Hysteresis sweeps only the listed weak candidates (strong pixels
+// are edges already, the rest never become edges) to the same fixed point.
+constexpr int kBigThreads = 1024;
+__host__ __device__ inline size_t line_ws_stride(int np) {
+  return ((size_t)np * 2 + 255) / 256 * 256 + ((size_t)np + 255) / 256 * 256 + (size_t)np * 4;
+}
+__global__ __launch_bounds__(kBigThreads) void line_detect_big_kernel(LineDev L, const uint8_t* bgr,
+                                                                      int hgt, int wid,
+                                                                      uint8_t* masks, uint8_t* hsv,
+                                                                      unsigned char* ws) {
+  __shared__ int sdiv[256], hdiv[256];
+  __shared__ int nweak;
+  const int e = blockIdx.x, np = hgt * wid;
+  unsigned char* base = ws + (size_t)e * line_ws_stride(np);
+  int16_t* mag = reinterpret_cast<int16_t*>(base);
+  uint8_t* work = base + ((size_t)np * 2 + 255) / 256 * 256;
+  int32_t* weak = reinterpret_cast<int32_t*>(work + ((size_t)np + 255) / 256 * 256);
+  const PixBuf B{mag, work, sdiv, hdiv};
+  const uint8_t* in = bgr + (size_t)e * np * 3;
+  load_tables(sdiv, hdiv);
+  if (threadIdx.x == 0) nweak = 0;
+  __syncthreads();
+  const auto fetch = [&](int r, int c) -> uint32_t {
+    const uint8_t* q = in + 3 * ((size_t)r * wid + c);
+    return (uint32_t)q[0] | ((uint32_t)q[1] << 8) | ((uint32_t)q[2] << 16);
+  };
+  for (int p = threadIdx.x; p < np; p += blockDim.x) {
+    const int r = p / wid, c = p - r * wid;
+    pass_a_pixel(fetch, B, L, hgt, wid, r, c);
+    if (hsv) {
+      int h, s, v;
+      const uint32_t q = fetch(r, c);
+      bgr_to_hsv(sdiv, hdiv, q & 255, (q >> 8) & 255, (q >> 16) & 255, h, s, v);
+      uint8_t* o = hsv + ((size_t)e * np + p) * 3;
+      o[0] = (uint8_t)h;
+      o[1] = (uint8_t)s;
+      o[2] = (uint8_t)v;
+    }
+  }
+  __syncthreads();
+  pass_b(B, L, hgt, wid);
+  __syncthreads();
+  for (int p = threadIdx.x; p < np; p += blockDim.x)
+    if ((work[p] & (B_CAND | B_EDGE)) == B_CAND) weak[atomicAdd(&nweak, 1)] = p;
+  __syncthreads();
+  const int nw = nweak;
+  for (;;) {
+    int changed = 0;
+    for (int i = threadIdx.x; i < nw; i += blockDim.x)
+      if (hyst_visit(B, hgt, wid, weak[i])) changed = 1;
+    if (!__syncthreads_or(changed)) break;
+  }
+  uint8_t* mb = masks + (size_t)e * 4 * np;
+  for (int p = threadIdx.x; p < np; p += blockDim.x) {
+    const int r = p / wid, c = p - r * wid;
+    const uint8_t b = pass_c_pixel(B, L, hgt, wid, r, c);
     mb[p] = b & 1 ? 255 : 0;
     mb[np + p] = b & 2 ? 255 : 0;
     mb[2 * np + p] = b & 4 ? 255 : 0;
@@ -1329,19 +1410,41 @@ struct HoughTab {
   float cs[2 * kHoughAngles];   // (float)(cos(n*theta)/rho), (float)(sin(n*theta)/rho), host-built
 };
 
+// the accumulator, mask-bit and point-list layout (LDS or workspace), bytes
+__host__ __device__ inline size_t hough_acc_bytes(int numangle, int nr) {
+  return ((size_t)2 * numangle * nr + 15) & ~(size_t)15;
+}
+__host__ __device__ inline size_t hough_mask_bytes(int np) {
+  return (((size_t)np + 31) / 32 * 4 + 15) & ~(size_t)15;
+}
+__host__ __device__ inline size_t hough_ws_stride(int numangle, int nr, int np) {
+  return (hough_acc_bytes(numangle, nr) + hough_mask_bytes(np) + (size_t)np * 4 + 255) & ~(size_t)255;
+}
+
+// kBig: the three arrays in the caller's workspace (hough_ws_stride bytes an
+// image, 32-bit point indices) instead of LDS, for images past the LDS; lane 0's
+// writes to the point list and the mask are then made visible to the wave's
+// other lanes with a workgroup fence (vector stores/loads, no LDS ordering).
+template <typename PtT, bool kBig>
 __global__ __launch_bounds__(64) void hough_kernel(const uint8_t* __restrict__ img, int h, int w,
                                                    HoughTab tab, int numangle, int numrho, int rlo,
                                                    int nr, int threshold, int min_len, int gap,
                                                    int max_lines, int max_pts,
                                                    int32_t* __restrict__ lines,
                                                    int32_t* __restrict__ counts,
-                                                   int32_t* __restrict__ trace) {
+                                                   int32_t* __restrict__ trace,
+                                                   unsigned char* __restrict__ ws) {
   extern __shared__ __attribute__((aligned(16))) unsigned char hl[];
   const int e = blockIdx.x, lane = threadIdx.x, np = h * w;
-  int16_t* acc = reinterpret_cast<int16_t*>(hl);                      // [numangle][nr]
-  uint32_t* mask = reinterpret_cast<uint32_t*>(hl + ((2 * numangle * nr + 15) & ~15));  // bits
-  uint16_t* pts = reinterpret_cast<uint16_t*>(reinterpret_cast<unsigned char*>(mask) +
-                                              (((np + 31) / 32 * 4 + 15) & ~15));       // [max_pts]
+  unsigned char* hb = kBig ? ws + (size_t)e * hough_ws_stride(numangle, nr, np) : hl;
+  int16_t* acc = reinterpret_cast<int16_t*>(hb);                      // [numangle][nr]
+  uint32_t* mask = reinterpret_cast<uint32_t*>(hb + hough_acc_bytes(numangle, nr));  // bits
+  PtT* pts = reinterpret_cast<PtT*>(reinterpret_cast<unsigned char*>(mask) +
+                                    hough_mask_bytes(np));                           // [max_pts]
+  const auto sync_wave = [&]() {
+    if (kBig) __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_wave_barrier();
+  };
   const uint8_t* im = img + (size_t)e * np;
   for (int i = lane; i < (numangle * nr + 1) / 2; i += 64) reinterpret_cast<uint32_t*>(acc)[i] = 0u;
   // the edge pixels in row-major order (ballot compaction keeps the order);
@@ -1355,7 +1458,7 @@ __global__ __launch_bounds__(64) void hough_kernel(const uint8_t* __restrict__ i
     if (lane == 0 && p0 + 32 < np) mask[(p0 >> 5) + 1] = (uint32_t)(b >> 32);
     const int pre = (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(b >> 32),
                                                    __builtin_amdgcn_mbcnt_lo((uint32_t)b, 0u));
-    if (on && count + pre < max_pts) pts[count + pre] = (uint16_t)p;
+    if (on && count + pre < max_pts) pts[count + pre] = (PtT)p;
     count += __popcll(b);
   }
   const auto on_mask = [&](int q) { return (mask[q >> 5] >> (q & 31)) & 1u; };
@@ -1376,6 +1479,8 @@ __global__ __launch_bounds__(64) void hough_kernel(const uint8_t* __restrict__ i
   bool overflow = count > max_pts;
   int32_t* out = lines + (size_t)e * max_lines * 4;
   int it = 0;
+  bool truncated = false;
+  sync_wave();
   __syncthreads();
   for (; count > 0 && !overflow; count--, ++it) {
     state = (uint64_t)(uint32_t)state * 4164903690ull + (uint32_t)(state >> 32);
@@ -1383,7 +1488,8 @@ __global__ __launch_bounds__(64) void hough_kernel(const uint8_t* __restrict__ i
     const int p = pts[idx];
     const int last = pts[count - 1];
     __builtin_amdgcn_wave_barrier();
-    if (lane == 0) pts[idx] = (uint16_t)last;
+    if (lane == 0) pts[idx] = (PtT)last;
+    sync_wave();
     const int i = p / w, j = p - i * w;
     if (!on_mask(p)) continue;
     // vote: the first angle reaching the largest count
@@ -1467,9 +1573,9 @@ __global__ __launch_bounds__(64) void hough_kernel(const uint8_t* __restrict__ i
               }
             }
           }
-          __builtin_amdgcn_wave_barrier();
+          sync_wave();
           if (lane == 0) mask[q >> 5] &= ~(1u << (q & 31));
-          __builtin_amdgcn_wave_barrier();
+          sync_wave();
         }
         if (i1 == ey[k] && j1 == ex[k]) break;
       }
@@ -1481,12 +1587,16 @@ __global__ __launch_bounds__(64) void hough_kernel(const uint8_t* __restrict__ i
         out[4 * nlines + 2] = ex[1];
         out[4 * nlines + 3] = ey[1];
       }
-      if (++nlines >= max_lines) break;
+      if (++nlines >= max_lines) {
+        // OpenCV has no cap: points still unvisited may hold more lines
+        truncated = count > 1;
+        break;
+      }
     }
     overflow = __ballot(overflow) != 0;
   }
   const bool any_over = __ballot(overflow) != 0;
-  if (lane == 0) counts[e] = any_over ? -1 : nlines;
+  if (lane == 0) counts[e] = any_over ? -1 : (truncated ? -2 : nlines);
 }
 
 }  // namespace
@@ -1624,66 +1734,129 @@ extern "C" int dt_diag_hough_trace(int32_t* device_buf) {
   return 0;
 }
 
-int dt_hough_lines(const uint8_t* edge, int32_t n, int32_t height, int32_t width,
-                   int32_t threshold, int32_t min_line_length, int32_t max_line_gap,
-                   int32_t max_lines, int32_t* lines, int32_t* counts, void* stream) {
-  if (!edge || !lines || !counts || n < 0 || height <= 0 || width <= 0 || max_lines <= 0 ||
-      height * width > 65536 || threshold < 1)
-    return DT_E_ARG;
-  if (n == 0) return DT_OK;
-  // cv2.HoughLinesP(edge, 1, np.pi / 180, ...): rho and theta as OpenCV's float
-  // parameters, the table as OpenCV builds it (double trig, rounded to float)
+namespace {
+struct HoughGeom {
+  HoughTab tab;
+  int numangle, numrho, rlo, nr;
+};
+// cv2.HoughLinesP(edge, 1, np.pi / 180, ...): rho and theta as OpenCV's float
+// parameters, the table as OpenCV builds it (double trig, rounded to float)
+HoughGeom hough_geom(int height, int width) {
+  HoughGeom G{};
   const float rho = 1.0f, theta = (float)(3.141592653589793 / 180.0);
-  const int numangle = (int)lrint(3.141592653589793 / theta);
-  if (numangle > kHoughAngles) return DT_E_ARG;
-  HoughTab tab{};
-  for (int k = 0; k < numangle; ++k) {
-    tab.cs[2 * k] = (float)(cos((double)k * theta) * (1.0f / rho));
-    tab.cs[2 * k + 1] = (float)(sin((double)k * theta) * (1.0f / rho));
+  G.numangle = (int)lrint(3.141592653589793 / theta);
+  for (int k = 0; k < G.numangle && k < kHoughAngles; ++k) {
+    G.tab.cs[2 * k] = (float)(cos((double)k * theta) * (1.0f / rho));
+    G.tab.cs[2 * k + 1] = (float)(sin((double)k * theta) * (1.0f / rho));
   }
-  const int numrho = (int)lrintf((float)((width + height) * 2 + 1) / rho);
+  G.numrho = (int)lrintf((float)((width + height) * 2 + 1) / rho);
   // the rho an h x w image reaches: r(x, y) is linear, so its extremes per
   // angle are at the corners (the kernel's float math and rounding)
   int rlo = 1 << 30, rhi = -(1 << 30);
-  for (int k = 0; k < numangle; ++k)
+  for (int k = 0; k < G.numangle && k < kHoughAngles; ++k)
     for (int cy = 0; cy < 2; ++cy)
       for (int cx = 0; cx < 2; ++cx) {
         const float xx = (float)(cx * (width - 1)), yy = (float)(cy * (height - 1));
-        const int r = (int)lrintf(xx * tab.cs[2 * k] + yy * tab.cs[2 * k + 1]);
+        const int r = (int)lrintf(xx * G.tab.cs[2 * k] + yy * G.tab.cs[2 * k + 1]);
         rlo = r < rlo ? r : rlo;
         rhi = r > rhi ? r : rhi;
       }
-  const int nr = rhi - rlo + 1;
-  const size_t fixed = (size_t)((2 * numangle * nr + 15) & ~15) +
-                       (((height * width + 31) / 32 * 4 + 15) & ~15);
+  G.rlo = rlo;
+  G.nr = rhi - rlo + 1;
+  return G;
+}
+bool hough_args_ok(const uint8_t* edge, int32_t n, int32_t height, int32_t width,
+                   int32_t threshold, int32_t max_lines, const int32_t* lines,
+                   const int32_t* counts) {
+  return edge && lines && counts && n >= 0 && height > 0 && width > 0 && max_lines > 0 &&
+         threshold >= 1 && (int64_t)height * width <= (int64_t)1 << 30;
+}
+}  // namespace
+
+size_t dt_hough_workspace(int32_t n, int32_t height, int32_t width) {
+  if (n <= 0 || height <= 0 || width <= 0) return 0;
+  const HoughGeom G = hough_geom(height, width);
+  return (size_t)n * hough_ws_stride(G.numangle, G.nr, height * width);
+}
+
+int dt_hough_lines_ws(const uint8_t* edge, int32_t n, int32_t height, int32_t width,
+                      int32_t threshold, int32_t min_line_length, int32_t max_line_gap,
+                      int32_t max_lines, int32_t* lines, int32_t* counts, void* workspace,
+                      size_t workspace_bytes, void* stream) {
+  if (!hough_args_ok(edge, n, height, width, threshold, max_lines, lines, counts)) return DT_E_ARG;
+  if (n == 0) return DT_OK;
+  const HoughGeom G = hough_geom(height, width);
+  if (G.numangle > kHoughAngles) return DT_E_ARG;
+  const int np = height * width;
+  if (workspace) {  // any size: the arrays in the workspace
+    if (workspace_bytes < (size_t)n * hough_ws_stride(G.numangle, G.nr, np)) return DT_E_ARG;
+    hipLaunchKernelGGL((hough_kernel<uint32_t, true>), dim3(n), dim3(64), 0, (hipStream_t)stream,
+                       edge, height, width, G.tab, G.numangle, G.numrho, G.rlo, G.nr, threshold,
+                       min_line_length, max_line_gap, max_lines, np, lines, counts, hough_trace,
+                       (unsigned char*)workspace);
+    return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+  }
+  if (np > 65536) return DT_E_ARG;   // 16-bit point indices in LDS
+  const size_t fixed = hough_acc_bytes(G.numangle, G.nr) + hough_mask_bytes(np);
   if (fixed + 2 * 1024 > 160 * 1024) return DT_E_ARG;
   // the point list takes the rest of the LDS (an image with more edge
   // pixels than that is flagged with counts = -1)
   int max_pts = (int)((160 * 1024 - fixed) / 2);
-  max_pts = max_pts > height * width ? height * width : max_pts;
+  max_pts = max_pts > np ? np : max_pts;
   const size_t lds = fixed + 2 * (size_t)max_pts;
   static bool attr = false;   // dynamic LDS past 64 KB must be allowed per kernel
   if (!attr) {
-    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&hough_kernel),
+    if (hipFuncSetAttribute(reinterpret_cast<const void*>(&hough_kernel<uint16_t, false>),
                             hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024) != hipSuccess)
       return DT_E_HIP;
     attr = true;
   }
-  hipLaunchKernelGGL(hough_kernel, dim3(n), dim3(64), lds, (hipStream_t)stream, edge, height,
-                     width, tab, numangle, numrho, rlo, nr, threshold, min_line_length,
-                     max_line_gap, max_lines, max_pts, lines, counts, hough_trace);
+  hipLaunchKernelGGL((hough_kernel<uint16_t, false>), dim3(n), dim3(64), lds, (hipStream_t)stream,
+                     edge, height, width, G.tab, G.numangle, G.numrho, G.rlo, G.nr, threshold,
+                     min_line_length, max_line_gap, max_lines, max_pts, lines, counts, hough_trace,
+                     (unsigned char*)nullptr);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
+int dt_hough_lines(const uint8_t* edge, int32_t n, int32_t height, int32_t width,
+                   int32_t threshold, int32_t min_line_length, int32_t max_line_gap,
+                   int32_t max_lines, int32_t* lines, int32_t* counts, void* stream) {
+  return dt_hough_lines_ws(edge, n, height, width, threshold, min_line_length, max_line_gap,
+                           max_lines, lines, counts, nullptr, 0, stream);
+}
+
+static bool line_args_ok(const dt_line_params* p, const uint8_t* bgr, int32_t n, int32_t height,
+                         int32_t width, const uint8_t* masks) {
+  return p && bgr && masks && n > 0 && height > 0 && width > 0 &&
+         (int64_t)height * width <= (int64_t)1 << 30 && p->dilation_kernel_size >= 1 &&
+         p->dilation_kernel_size <= 7 && (p->dilation_kernel_size & 1) == 1;
+}
+
+size_t dt_line_detect_workspace(int32_t n, int32_t height, int32_t width) {
+  if (n <= 0 || height <= 0 || width <= 0 || height * width <= NPIX) return 0;
+  return (size_t)n * line_ws_stride(height * width);
+}
+
+int dt_line_detect_ws(const dt_line_params* p, const uint8_t* bgr, int32_t n, int32_t height,
+                      int32_t width, uint8_t* masks, uint8_t* hsv, void* workspace,
+                      size_t workspace_bytes, void* stream) {
+  if (!line_args_ok(p, bgr, n, height, width, masks)) return DT_E_ARG;
+  if (height * width <= NPIX) {
+    hipLaunchKernelGGL(line_detect_kernel, dim3(n), dim3(kThreads), 0, (hipStream_t)stream,
+                       to_line_dev(*p), bgr, height, width, masks, hsv);
+  } else {
+    if (!workspace || workspace_bytes < (size_t)n * line_ws_stride(height * width))
+      return DT_E_ARG;
+    hipLaunchKernelGGL(line_detect_big_kernel, dim3(n), dim3(kBigThreads), 0, (hipStream_t)stream,
+                       to_line_dev(*p), bgr, height, width, masks, hsv,
+                       (unsigned char*)workspace);
+  }
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 
 int dt_line_detect(const dt_line_params* p, const uint8_t* bgr, int32_t n, int32_t height,
                    int32_t width, uint8_t* masks, uint8_t* hsv, void* stream) {
-  if (!p || !bgr || !masks || n <= 0 || height <= 0 || width <= 0 || height * width > NPIX ||
-      p->dilation_kernel_size < 1 || p->dilation_kernel_size > 7 ||
-      (p->dilation_kernel_size & 1) == 0)
-    return DT_E_ARG;
-  hipLaunchKernelGGL(line_detect_kernel, dim3(n), dim3(kThreads), 0, (hipStream_t)stream,
-                     to_line_dev(*p), bgr, height, width, masks, hsv);
-  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+  return dt_line_detect_ws(p, bgr, n, height, width, masks, hsv, nullptr, 0, stream);
 }
 
 }  // extern "C"

@@ -151,9 +151,12 @@ def bind_render(env, out, stream, fresh=None, pose=None):
 
 
 def line_detect(bgr, params=None, hsv=False, stream=None):
-    """LineDetectorHSV on a [n, h, w, 3] uint8 BGR CUDA tensor (h*w <= 19200).
-    Returns masks [n, 4, h, w] u8 ({white, yellow, red, edges}) and, if hsv,
-    the cvtColor(BGR2HSV) image [n, h, w, 3]."""
+    """LineDetectorHSV.setImage + _colorFilter (features/line_detector1.py
+    :134-141, :36-57) on a [n, h, w, 3] uint8 BGR CUDA tensor of any size.
+    Images of <= 19200 pixels run in LDS; larger ones (the 640x480 camera frame
+    of duckietown_rl/env.py:12-16) through a device workspace
+    (dt_line_detect_ws).  Returns masks [n, 4, h, w] u8 ({white, yellow, red,
+    edges}) and, if hsv, the cvtColor(BGR2HSV) image [n, h, w, 3]."""
     L = _lib.lib()
     if bgr.dtype != torch.uint8 or bgr.dim() != 4 or bgr.shape[3] != 3 or not bgr.is_cuda:
         raise ValueError('bgr must be a [n,h,w,3] uint8 CUDA tensor')
@@ -162,11 +165,16 @@ def line_detect(bgr, params=None, hsv=False, stream=None):
     p = params or LineParams.default()
     masks = torch.empty(n, 4, h, w, dtype=torch.uint8, device=bgr.device)
     hsv_t = torch.empty(n, h, w, 3, dtype=torch.uint8, device=bgr.device) if hsv else None
+    if n == 0:
+        return (masks, hsv_t) if hsv else masks
+    nbytes = L.dt_line_detect_workspace(n, h, w)
+    ws = torch.empty(nbytes, dtype=torch.uint8, device=bgr.device) if nbytes else None
     s = stream if stream is not None else torch.cuda.current_stream(bgr.device).cuda_stream
-    rc = L.dt_line_detect(ctypes.byref(p), ctypes.c_void_p(bgr.data_ptr()), n, h, w,
-                          ctypes.c_void_p(masks.data_ptr()),
-                          ctypes.c_void_p(hsv_t.data_ptr()) if hsv else None,
-                          ctypes.c_void_p(s))
+    rc = L.dt_line_detect_ws(ctypes.byref(p), ctypes.c_void_p(bgr.data_ptr()), n, h, w,
+                             ctypes.c_void_p(masks.data_ptr()),
+                             ctypes.c_void_p(hsv_t.data_ptr()) if hsv else None,
+                             ctypes.c_void_p(ws.data_ptr()) if ws is not None else None,
+                             nbytes, ctypes.c_void_p(s))
     if rc != 0:
         raise _lib.DtError('dt_line_detect failed (%d)' % rc)
     return (masks, hsv_t) if hsv else masks
@@ -179,13 +187,21 @@ HOUGH_DEFAULTS = {'hough_threshold': 2, 'hough_min_line_length': 3, 'hough_max_l
 COLOR_PLANE = {'white': MASK_WHITE, 'yellow': MASK_YELLOW, 'red': MASK_RED}
 
 
+HOUGH_TRUNCATED = -2   # dt_hough_lines: max_lines reached with points left
+HOUGH_OVERFLOW = -1    # dt_hough_lines: more edge pixels than the LDS list holds
+
+
 def hough_lines(edge, threshold=2, min_line_length=3, max_line_gap=1, max_lines=512,
-                stream=None):
+                stream=None, workspace=None):
     """_HoughLine (:63-70): cv2.HoughLinesP(edge, 1, pi/180, threshold,
     min_line_length, max_line_gap) on a [n, h, w] uint8 CUDA tensor (non-zero =
     edge), one wave per image (include/dtsim.h dt_hough_lines).  Returns
     (lines [n, max_lines, 4] int32 (x1, y1, x2, y2) in OpenCV's order, counts
-    [n] int32, -1 for an image with more edge pixels than the kernel holds)."""
+    [n] int32).  A count of -2 (HOUGH_TRUNCATED) marks an image that reached
+    max_lines with edge points still unvisited; -1 (HOUGH_OVERFLOW) one with
+    more edge pixels than the LDS point list holds.  workspace: None = the LDS
+    kernel where the image fits (else the workspace kernel), True = always the
+    workspace kernel (any size, never -1)."""
     L = _lib.lib()
     if edge.dtype != torch.uint8 or edge.dim() != 3 or not edge.is_cuda:
         raise ValueError('edge must be a [n,h,w] uint8 CUDA tensor')
@@ -193,11 +209,26 @@ def hough_lines(edge, threshold=2, min_line_length=3, max_line_gap=1, max_lines=
     n, h, w = edge.shape
     lines = torch.zeros(n, max_lines, 4, dtype=torch.int32, device=edge.device)
     counts = torch.zeros(n, dtype=torch.int32, device=edge.device)
+    if n == 0:
+        return lines, counts
+    if threshold < 1 or max_lines < 1:
+        raise ValueError('threshold and max_lines must be >= 1')
     s = stream if stream is not None else torch.cuda.current_stream(edge.device).cuda_stream
-    rc = L.dt_hough_lines(ctypes.c_void_p(edge.data_ptr()), n, h, w, int(threshold),
-                          int(min_line_length), int(max_line_gap), int(max_lines),
-                          ctypes.c_void_p(lines.data_ptr()), ctypes.c_void_p(counts.data_ptr()),
-                          ctypes.c_void_p(s))
+    ptr = lambda t: ctypes.c_void_p(t.data_ptr())  # noqa: E731
+
+    def run(ws, nbytes):
+        return L.dt_hough_lines_ws(ptr(edge), n, h, w, int(threshold), int(min_line_length),
+                                   int(max_line_gap), int(max_lines), ptr(lines), ptr(counts),
+                                   ptr(ws) if ws is not None else None, nbytes,
+                                   ctypes.c_void_p(s))
+    # the LDS kernel refuses (DT_E_ARG) an image whose accumulator does not fit
+    rc = run(None, 0) if not workspace else -1
+    if rc != 0:
+        nbytes = L.dt_hough_workspace(n, h, w)
+        ws = torch.empty(nbytes, dtype=torch.uint8, device=edge.device)
+        rc = run(ws, nbytes)
+        if rc == 0 and stream is not None:   # the workspace lives until that stream is past it
+            ws.record_stream(torch.cuda.ExternalStream(s, device=edge.device))
     if rc != 0:
         raise _lib.DtError('dt_hough_lines failed (%d)' % rc)
     return lines, counts
@@ -246,10 +277,15 @@ def detect_lines(masks, color, params=None, max_lines=512):
     p = dict(HOUGH_DEFAULTS, **(params or {}))
     bw = masks[:, COLOR_PLANE[color]]
     edge_color = bw & masks[:, MASK_EDGES]
-    lines, counts = hough_lines(edge_color, p['hough_threshold'], p['hough_min_line_length'],
-                                p['hough_max_line_gap'], max_lines)
-    if bool((counts < 0).any()):
-        raise _lib.DtError('dt_hough_lines: an image had more edge pixels than fit in LDS')
+    args = (p['hough_threshold'], p['hough_min_line_length'], p['hough_max_line_gap'])
+    ws = None
+    lines, counts = hough_lines(edge_color, *args, max_lines)
+    if bool((counts == HOUGH_OVERFLOW).any()):   # past the LDS point list: workspace kernel
+        ws = True
+        lines, counts = hough_lines(edge_color, *args, max_lines, workspace=ws)
+    while bool((counts == HOUGH_TRUNCATED).any()):   # OpenCV has no cap: grow the list
+        max_lines *= 2
+        lines, counts = hough_lines(edge_color, *args, max_lines, workspace=ws)
     lines, centers, normals = find_normals(bw, lines, counts)
     return {'lines': lines, 'normals': normals, 'area': bw, 'centers': centers,
             'counts': counts}

@@ -29,14 +29,17 @@
 extern "C" {
 #endif
 
-#define DT_ABI_VERSION 6  /* 2: curves per tile vary (curve_start), intersections;
+#define DT_ABI_VERSION 7  /* 2: curves per tile vary (curve_start), intersections;
                              3: static objects in dt_map, safety_rad_mult;
                              4: dt_render_io.pose / list_cap, dt_copy_pose,
                                 dt_step_many pose output;
                              5: dtactor.h: dt_conv12 and dt_conv1_bands
                                 removed, partials [n, 32, 2];
                              6: dtactor.h: dt_conv1_split / dt_conv32_split
-                                (two weight sets in one launch) */
+                                (two weight sets in one launch);
+                             7: dt_line_detect_ws / dt_hough_lines_ws and
+                                their workspace queries (any image size),
+                                dt_hough_lines count -2 (max_lines reached) */
 
 /* error codes */
 #define DT_OK 0
@@ -269,10 +272,19 @@ int dt_render(dt_handle* h, const dt_render_io* io, void* stream);
 int dt_copy_pose(dt_handle* h, double* pose, void* stream);
 int dt_set_line_params(dt_handle* h, const dt_line_params* p);
 
-/* LineDetectorHSV on caller images (no environment): bgr device [n, height,
- * width, 3] u8 (height*width <= 19200, e.g. 120x160); masks device [n, 4,
- * height, width] u8 as above; hsv device [n, height, width, 3] u8 or NULL
- * (cvtColor BGR2HSV).  Runs on the current device. */
+/* LineDetectorHSV on caller images (no environment; features/line_detector1.py
+ * :134-141 setImage + _colorFilter :36-57): bgr device [n, height, width, 3]
+ * u8; masks device [n, 4, height, width] u8 as above; hsv device [n, height,
+ * width, 3] u8 or NULL (cvtColor BGR2HSV).  Images of <= 19200 pixels (e.g.
+ * 120x160) run in LDS, one workgroup each; larger ones (e.g. the 640x480
+ * camera frame of duckietown_rl/env.py:12-16) need a device workspace of
+ * dt_line_detect_workspace(n, height, width) bytes (0 when none is needed) and
+ * dt_line_detect_ws.  dt_line_detect is dt_line_detect_ws without one (so it
+ * refuses larger images with DT_E_ARG).  Runs on the current device. */
+size_t dt_line_detect_workspace(int32_t n, int32_t height, int32_t width);
+int dt_line_detect_ws(const dt_line_params* p, const uint8_t* bgr, int32_t n, int32_t height,
+                      int32_t width, uint8_t* masks, uint8_t* hsv, void* workspace,
+                      size_t workspace_bytes, void* stream);
 int dt_line_detect(const dt_line_params* p, const uint8_t* bgr, int32_t n, int32_t height,
                    int32_t width, uint8_t* masks, uint8_t* hsv, void* stream);
 
@@ -280,15 +292,26 @@ int dt_line_detect(const dt_line_params* p, const uint8_t* bgr, int32_t n, int32
  * cv2.HoughLinesP(edge, rho 1, theta pi/180, threshold, min_line_length,
  * max_line_gap) on n u8 images (non-zero = edge), e.g. a dt_render mask
  * plane (edge_color = the colour mask AND the edge mask, :55).  edge device
- * [n, height, width] u8 (height*width <= 65536 and the accumulator + image
- * within 160 KB of LDS: 120x160 fits); lines device [n, max_lines, 4] i32
- * (x1, y1, x2, y2) in OpenCV's order; counts device [n] i32 = lines found,
- * or -1 when the image had more edge pixels than the kernel's LDS point list
- * holds (~16k points at 120x160, of its 19,200 pixels; the image's lines are then not valid).  One wave per image; runs on the
- * current device. */
+ * [n, height, width] u8; lines device [n, max_lines, 4] i32 (x1, y1, x2, y2)
+ * in OpenCV's order; counts device [n] i32 = lines found, or
+ *   -1: the image had more edge pixels than the LDS point list holds (~16k
+ *       points at 120x160, of its 19,200 pixels), its lines are not valid;
+ *   -2: max_lines lines were found with edge points still unvisited, so
+ *       OpenCV (which has no cap) may find more: the max_lines rows are the
+ *       first ones, the list is cut short.
+ * dt_hough_lines runs in LDS (height*width <= 65536 and the accumulator +
+ * image within 160 KB: 120x160 fits).  dt_hough_lines_ws with a workspace of
+ * dt_hough_workspace(n, height, width) bytes keeps the accumulator, mask and
+ * point list there instead: any image size, never -1.  One wave per image;
+ * runs on the current device. */
 int dt_hough_lines(const uint8_t* edge, int32_t n, int32_t height, int32_t width,
                    int32_t threshold, int32_t min_line_length, int32_t max_line_gap,
                    int32_t max_lines, int32_t* lines, int32_t* counts, void* stream);
+size_t dt_hough_workspace(int32_t n, int32_t height, int32_t width);
+int dt_hough_lines_ws(const uint8_t* edge, int32_t n, int32_t height, int32_t width,
+                      int32_t threshold, int32_t min_line_length, int32_t max_line_gap,
+                      int32_t max_lines, int32_t* lines, int32_t* counts, void* workspace,
+                      size_t workspace_bytes, void* stream);
 
 /* ---- state access (parity injection; synchronous) ---------------------- */
 /* x, z, angle: host [n] f64; step_count (Simulator), env_step (wrapper),

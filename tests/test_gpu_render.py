@@ -73,12 +73,15 @@ def test_ring_and_fresh(gpu):
         assert torch.equal(r[:, 0], r[:, 1]) and torch.equal(r[:, 2], r[:, 1])
 
 
-@pytest.mark.parametrize('shape', [(120, 160), (37, 53), (1, 1), (96, 200)])
+# (150, 200) and (480, 640) are past the LDS image (19,200 px): the workspace
+# kernel (dt_line_detect_ws); 480 x 640 is duckietown_rl/env.py:12-16's frame
+@pytest.mark.parametrize('shape', [(120, 160), (37, 53), (1, 1), (96, 200), (150, 200),
+                                   (480, 640)])
 def test_line_detect_parity(gpu, shape):
     from aido1_amd.render import LineParams, line_detect
     h, w = shape
     rng = np.random.default_rng(h * w)
-    n = 12
+    n = 12 if h * w <= 30000 else 4
     img = rng.integers(0, 256, (n, h, w, 3), dtype=np.uint8)
     # blocky content with real edges and colours in the HSV ranges
     for i in range(n // 2):
