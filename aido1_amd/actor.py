@@ -108,8 +108,11 @@ class _Seq(nn.Module):       # MetaNet: ".internal_modules.<i>"
         self.internal_modules = nn.ModuleList(mods)
 
     def forward(self, x):
+        return self.run(x, 0, len(self.internal_modules))
+
+    def run(self, x, i, k):
+        """Modules [i, k) on x."""
         mods = self.internal_modules
-        i, k = 0, len(mods)
         while i < k:
             m = mods[i]
             if (self.fused_tail and i + 2 < k and isinstance(m, _Conv)
@@ -119,6 +122,9 @@ class _Seq(nn.Module):       # MetaNet: ".internal_modules.<i>"
                     x = train_ops.conv_leaky_bn(x, m.kernel, mods[i + 1], mods[i + 2])
                     i += 3
                     continue
+            if isinstance(m, nn.BatchNorm2d) and getattr(m, '_dt_updates', 1) != 1:
+                raise NotImplementedError('repeated running-statistics updates need the fused '
+                                          'train-mode tail (train_ops)')
             x = m(x)
             i += 1
         return x
@@ -221,7 +227,29 @@ class ConfigActor(ConfigNet):
 class ConfigCritic(ConfigNet):
     """models/ddpg/modules.py Critic from config.json's "critic" list: conv
     trunk -> linear 256 on the observation, the action passed through, both
-    concatenated (258) -> linear 128 -> linear 1 (config.json:93-170)."""
+    concatenated (258) -> linear 128 -> linear 1 (config.json:93-170).
+
+    trunk(obs) + head(t, action) == forward(obs, action): the trunk is the
+    observation branch up to its first dropout or linear (the conv stack and
+    flatten, a function of obs and the conv weights only), the head the rest
+    (dropout draws included).  The trainer shares one trunk between two
+    forwards that see the same weights and batch."""
+
+    def _cut(self):
+        mods = self.net.input_nets[0].internal_modules
+        for j, m in enumerate(mods):
+            if isinstance(m, (nn.Dropout, _Lin)):
+                return j
+        return len(mods)
+
+    def trunk(self, obs):
+        return self.net.input_nets[0].run(obs, 0, self._cut())
+
+    def head(self, t, *rest):
+        seq = self.net.input_nets[0]
+        x0 = seq.run(t, self._cut(), len(seq.internal_modules))
+        x = torch.cat([x0] + [net(v) for net, v in zip(self.net.input_nets[1:], rest)], dim=1)
+        return self.net.output_nets[0](x)
 
 
 def apply_head(x, head, max_action=1.0):

@@ -84,7 +84,7 @@ __device__ __forceinline__ void st4(float* p, int64_t q, float4 v) {
 __global__ void __launch_bounds__(kT)
 bn_stats_kernel(int64_t m, const float* __restrict__ z, const float* __restrict__ bias, float slope,
                 float eps, float momentum, float* __restrict__ running_mean,
-                float* __restrict__ running_var, int64_t* __restrict__ nbt,
+                float* __restrict__ running_var, int64_t* __restrict__ nbt, int updates,
                 float* __restrict__ a, float* __restrict__ mean_invstd,
                 float* __restrict__ work) {
   __shared__ float red[kSlots][C][3];
@@ -164,9 +164,16 @@ bn_stats_kernel(int64_t m, const float* __restrict__ z, const float* __restrict_
     mean_invstd[tid] = cm;
     mean_invstd[C + tid] = 1.0f / sqrtf(var + eps);
     const float unbiased = cn > 1.0f ? cm2 / (cn - 1.0f) : var;
-    running_mean[tid] = (1.0f - momentum) * running_mean[tid] + momentum * cm;
-    running_var[tid] = (1.0f - momentum) * running_var[tid] + momentum * unbiased;
-    if (tid == 0 && nbt) nbt[0] += 1;
+    // one running-statistics update per reference forward over this batch
+    // (the same batch statistics each time: a shared trunk, trainer.py)
+    float rm = running_mean[tid], rv = running_var[tid];
+    for (int u = 0; u < updates; ++u) {
+      rm = (1.0f - momentum) * rm + momentum * cm;
+      rv = (1.0f - momentum) * rv + momentum * unbiased;
+    }
+    running_mean[tid] = rm;
+    running_var[tid] = rv;
+    if (tid == 0 && nbt) nbt[0] += updates;
   }
 }
 
@@ -385,8 +392,9 @@ int64_t dt_train_work_floats(int64_t m) {
 
 int dt_bn_leaky_fwd(int64_t m, const float* z, const float* bias, float slope, const float* gamma,
                     const float* beta, float eps, float momentum, float* running_mean,
-                    float* running_var, int64_t* num_batches_tracked, float* a, float* y,
-                    float* mean_invstd, float* work, void* stream) {
+                    float* running_var, int64_t* num_batches_tracked, int32_t updates, float* a,
+                    float* y, float* mean_invstd, float* work, void* stream) {
+  if (updates < 1) return DT_E_ARG;
   if (m < 1 || !z || !bias || !gamma || !beta || !running_mean || !running_var || !a || !y ||
       !mean_invstd || !work)
     return DT_E_ARG;
@@ -396,7 +404,7 @@ int dt_bn_leaky_fwd(int64_t m, const float* z, const float* bias, float slope, c
   const int g = grid_of(m);
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(bn_stats_kernel, dim3(g), dim3(kT), 0, s, m, z, bias, slope, eps, momentum,
-                     running_mean, running_var, num_batches_tracked, a, mean_invstd, work);
+                     running_mean, running_var, num_batches_tracked, (int)updates, a, mean_invstd, work);
   hipLaunchKernelGGL(bn_apply_kernel, dim3(g), dim3(kT), 0, s, m, a, mean_invstd, gamma, beta, y);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }

@@ -12,6 +12,7 @@ bias's gradients).  torch runs eight kernels for the forward tail and five for
 the backward.  The modules, parameters and state_dict are the unchanged
 torch ones; ``applicable`` says when the fused tail replaces them.
 """
+import contextlib
 import ctypes
 
 import torch
@@ -59,7 +60,8 @@ class _BnLeaky(torch.autograd.Function):
         rc = L.dt_bn_leaky_fwd(m, z.data_ptr(), bias.data_ptr(), slope, gamma.data_ptr(),
                                beta.data_ptr(), bn.eps, bn.momentum, bn.running_mean.data_ptr(),
                                bn.running_var.data_ptr(),
-                               nbt.data_ptr() if nbt is not None else None, a.data_ptr(),
+                               nbt.data_ptr() if nbt is not None else None,
+                               int(getattr(bn, '_dt_updates', 1)), a.data_ptr(),
                                y.data_ptr(), mi.data_ptr(), _work(bn, 'fwd', z.device).data_ptr(),
                                _stream(z.device))
         if rc != 0:
@@ -82,6 +84,21 @@ class _BnLeaky(torch.autograd.Function):
         if rc != 0:
             raise _lib.DtError('dt_bn_leaky_bwd failed (%d)' % rc)
         return dz, g[0], g[1], g[2], None, None
+
+
+@contextlib.contextmanager
+def running_updates(module, k):
+    """Inside: each fused train-mode BatchNorm of `module` moves its running
+    statistics k times (num_batches_tracked += k), as k train-mode forwards
+    over the same batch do; its output is the one forward's."""
+    bns = [m for m in module.modules() if isinstance(m, nn.BatchNorm2d)]
+    for m in bns:
+        m._dt_updates = int(k)
+    try:
+        yield
+    finally:
+        for m in bns:
+            m._dt_updates = 1
 
 
 def conv_leaky_bn(x, conv, act, bn):

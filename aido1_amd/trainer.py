@@ -203,11 +203,31 @@ class DDPGTrainer:
         self._grads(critic_loss, self.critic)
         self._critic_loss = critic_loss.detach()
 
+    def _shared_trunk(self):
+        """Share the critic's conv trunk between the actor-loss forward and the
+        TD-error forward (trainers.py:190-192, 223-226): both run the critic
+        after its step and before anything else changes it, on the same
+        observations, so the trunk output is the same tensor; only the head
+        (dropout, linears, with the action) runs twice.  The BatchNorms move
+        their running statistics twice, as the two reference forwards do
+        (dt_bn_leaky_fwd updates = 2).  The actor loss needs no gradient
+        through the trunk (it does not depend on the actor).  GPU float32 with
+        the fused train-mode tail only; elsewhere the two full forwards run."""
+        return (self.device.type == 'cuda' and self.dtype == torch.float32
+                and hasattr(self.critic, 'trunk'))
+
     def _stage_actor(self):
         x = self._in
         self.critic_optim.step()
         pred_actions = self.actor(x['obs'])
-        actor_loss = -1.0 * torch.mean(self.critic(x['obs'], pred_actions))
+        if self._shared_trunk():
+            from aido1_amd import train_ops
+            with torch.no_grad(), train_ops.running_updates(self.critic, 2):
+                self._trunk = self.critic.trunk(x['obs'])
+            q = self.critic.head(self._trunk, pred_actions)
+        else:
+            q = self.critic(x['obs'], pred_actions)
+        actor_loss = -1.0 * torch.mean(q)
         self._grads(actor_loss, self.actor)
         self._actor_loss = actor_loss.detach()
 
@@ -218,7 +238,11 @@ class DDPGTrainer:
         side = self._fork()
         with torch.cuda.stream(side) if side is not None else _nullctx():
             with torch.no_grad():                                    # trainers.py:223-229
-                self._td = self._y - self.critic(x['obs'], x['act'])
+                if self._shared_trunk():
+                    q = self.critic.head(self._trunk, x['act'])
+                else:
+                    q = self.critic(x['obs'], x['act'])
+                self._td = self._y - q
         self.actor_optim.step()
         soft_update(self.target_actor, self.actor, self.tau)       # trainers.py:215-216
         soft_update(self.target_critic, self.critic, self.tau)

@@ -43,7 +43,10 @@ int64_t dt_train_work_floats(int64_t m);
  * beta with the batch mean and biased variance of a over the m pixels
  * (invstd = 1 / sqrt(var + eps)); running_mean / running_var move by
  * `momentum` towards mean and the unbiased variance, num_batches_tracked += 1
- * (torch.nn.BatchNorm2d.forward in train mode).
+ * (torch.nn.BatchNorm2d.forward in train mode); `updates` >= 1 times, as
+ * that many train-mode forwards over the same batch would (the trainer's
+ * shared critic trunk: the actor-loss and TD-error forwards of
+ * training/trainers.py:190-192,223-226 see the same weights and batch).
  *   z, a, y            device f32 [m, 32]
  *   bias, gamma, beta  device f32 [32]
  *   running_mean, running_var  device f32 [32], updated in place
@@ -52,8 +55,8 @@ int64_t dt_train_work_floats(int64_t m);
  *                      for the backward) */
 int dt_bn_leaky_fwd(int64_t m, const float* z, const float* bias, float slope, const float* gamma,
                     const float* beta, float eps, float momentum, float* running_mean,
-                    float* running_var, int64_t* num_batches_tracked, float* a, float* y,
-                    float* mean_invstd, float* work, void* stream);
+                    float* running_var, int64_t* num_batches_tracked, int32_t updates, float* a,
+                    float* y, float* mean_invstd, float* work, void* stream);
 
 /* Backward of dt_bn_leaky_fwd given dy (device f32 [m, 32]):
  *   dgamma = sum(dy * xhat), dbeta = sum(dy), xhat = (a - mean) * invstd;

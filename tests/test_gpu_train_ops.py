@@ -141,3 +141,34 @@ def test_soft_update_gpu_bit_exact(gpu):
     soft_update(a, b, tau)
     for t, e in zip(a.parameters(), expect):
         assert torch.equal(t.data, e)
+
+
+def test_shared_critic_trunk_equals_two_forwards(gpu):
+    """trainer._shared_trunk: trunk(obs) once under running_updates(2) then
+    head() twice == two full train-mode forwards of the critic, bit for bit:
+    the outputs and every state_dict entry (running statistics moved twice,
+    num_batches_tracked += 2).  Dropout p = 0 so the heads are deterministic."""
+    from aido1_amd.actor import ConfigCritic
+    from aido1_amd.train_ops import running_updates
+    from test_trainer import no_dropout
+    cfg = golden('reference_config.json')
+    torch.manual_seed(3)
+    cl = torch.channels_last
+    a = ConfigCritic(no_dropout(cfg['model']['critic'])).to(gpu).to(memory_format=cl).train()
+    b = copy.deepcopy(a)
+    obs = torch.rand(16, 3, 120, 160, device=gpu).contiguous(memory_format=cl)
+    act1, act2 = torch.rand(16, 2, device=gpu), torch.rand(16, 2, device=gpu)
+    with torch.no_grad():
+        q1, q2 = a(obs, act1), a(obs, act2)
+        with running_updates(b, 2):
+            t = b.trunk(obs)
+        s1, s2 = b.head(t, act1), b.head(t, act2)
+    assert torch.equal(q1, s1) and torch.equal(q2, s2)
+    sa, sb = a.state_dict(), b.state_dict()
+    assert list(sa) == list(sb)
+    for k in sa:
+        assert torch.equal(sa[k], sb[k]), k
+    assert int(sb['net.input_nets.0.internal_modules.2.num_batches_tracked']) == 2
+    with pytest.raises(NotImplementedError):   # the torch BatchNorm path cannot repeat
+        with running_updates(b.cpu().double(), 2):
+            b.trunk(obs.cpu().double())
