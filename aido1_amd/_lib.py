@@ -165,8 +165,8 @@ def lib():
             'dt_bn_leaky_fwd': (ctypes.c_int, [i64, vp, vp, ctypes.c_float, vp, vp, ctypes.c_float,
                                                ctypes.c_float, vp, vp, vp, i32, vp, vp, vp, vp,
                                                vp]),
-            'dt_bn_leaky_bwd': (ctypes.c_int, [i64, vp, vp, vp, vp, ctypes.c_float, vp, vp, vp, vp,
-                                               vp, vp]),
+            'dt_bn_leaky_bwd': (ctypes.c_int, [i64, vp, vp, vp, vp, vp, ctypes.c_float, vp, vp, vp,
+                                               vp, vp, vp]),
             'dt_adam': (ctypes.c_int, [i32, vp, vp, vp, vp, f64, f64, f64, vp, vp]),
             'dt_soft_update': (ctypes.c_int, [i32, vp, vp, f64, vp]),
             # dtactor.h
@@ -186,6 +186,8 @@ def lib():
             'dt_explore': (ctypes.c_int, [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                           ctypes.POINTER(DtExploreParams), vp, vp]),
             'dt_explore_done': (ctypes.c_int, [i32, vp, vp, vp, vp, i32, vp]),
+            'dt_actor_head': (ctypes.c_int, [i32, i32, i32, vp, i32, vp, vp, vp, vp, i32,
+                                             ctypes.c_float, vp, vp]),
         }
         for name, (res, args) in sig.items():
             if not hasattr(L, name):

@@ -480,6 +480,8 @@ class FusedActor(nn.Module):
             out[n0:] = other(x[n0:], order)
             return out
         flat = self._convs_pair(other, x, order, n0)
+        if self._head_fusable(other):
+            return self._heads(other, flat, n0, out)
         for a, sl in ((self, slice(0, n0)), (other, slice(n0, n))):
             out[sl] = a._head(flat[sl])
         return out
@@ -528,6 +530,38 @@ class FusedActor(nn.Module):
             raise _lib.DtError('dt_conv1_split / dt_conv32_split failed (%d)' % rc)
         return flat
 
+    _HEAD_CODES = {'none': 0, 'tanh': 1, 'sigmoid': 2}
+
+    def _head_fusable(self, other=None):
+        nets = [self] if other is None else [self, other]
+        return all(a.dtype == torch.float16 and a.w2.is_cuda and a.w2.shape[0] == 2 and
+                   a.head == self.head and a.head in self._HEAD_CODES and
+                   a.w1.shape == self.w1.shape and a.w1.shape[0] % 8 == 0 for a in nets)
+
+    def _heads(self, other, flat, n0, out):
+        """_head over rows [0, n0) with this actor and [n0, n) with `other`:
+        dropout + lin1 per weight set (hipBLASLt into one [n, 512] buffer),
+        then LeakyReLU -> lin2 -> head for every row in ONE dt_actor_head
+        launch (include/dtactor.h), written into out [n, 2] f32."""
+        import ctypes
+        from aido1_amd import _lib
+        n, k = flat.shape[0], self.w1.shape[0]
+        h = torch.empty(n, k, dtype=torch.float16, device=flat.device)
+        o = other if other is not None else self
+        for a, sl in ((self, slice(0, n0)), (o, slice(n0, n))):
+            if sl.stop > sl.start:
+                x = flat[sl]
+                if a.mode == 'reference' and a.p_drop > 0:
+                    x = F.dropout(x, a.p_drop, training=True)
+                torch.addmm(a.b1, x, a.w1.t(), out=h[sl])
+        rc = _lib.lib().dt_actor_head(
+            n, n0, k, h.data_ptr(), k, self.w2.data_ptr(), self.b2.data_ptr(), o.w2.data_ptr(),
+            o.b2.data_ptr(), self._HEAD_CODES[self.head], 0.01, out.data_ptr(),
+            ctypes.c_void_p(torch.cuda.current_stream(flat.device).cuda_stream))
+        if rc != 0:
+            raise _lib.DtError('dt_actor_head failed (%d)' % rc)
+        return out
+
     def _head(self, x):
         """dropout (reference mode) -> lin1 -> LeakyReLU -> lin2 -> head."""
         if self.mode == 'reference' and self.p_drop > 0:
@@ -553,6 +587,9 @@ class FusedActor(nn.Module):
                 self.w[0].shape == (32, 3, 8, 8)):
             # the fp16 product path: all four convs are the hand-written MFMA kernels
             x = self._convs_hip(x, order if order is not None else [0, 1, 2])
+            if self._head_fusable() and x.shape[0] > 0:
+                out = torch.empty(x.shape[0], 2, dtype=torch.float32, device=x.device)
+                return self._heads(None, x, x.shape[0], out)
         else:
             w0 = self.w[0]
             if order is not None:

@@ -295,3 +295,72 @@ extern "C" int dt_explore_done(int32_t n, const uint8_t* done, double* ou_x, int
                                                                         actions, tanh_map);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
+
+// ---- the actor head after the first linear: LeakyReLU -> lin2 -> output ---------------
+// (config.json actor output branch: linear 512 -> 2, tanh; ddpg.py:58-62).  One
+// wave a sample: each lane takes 8 of the K inputs (16-B loads), LeakyReLU in
+// f32 rounded to fp16 (F.leaky_relu on the fp16 tensor), the two dot products
+// in f32, a wave reduction, then + bias rounded to fp16 (the fp16 GEMM's
+// output), the head in f32.  Rows [0, n0) use set a, [n0, n) set b.
+namespace {
+constexpr int kHeadWaves = 4;
+
+__global__ void __launch_bounds__(64 * kHeadWaves)
+actor_head_kernel(int n, int n0, int k, const __half* __restrict__ h, int ld,
+                  const __half* __restrict__ w2a, const __half* __restrict__ b2a,
+                  const __half* __restrict__ w2b, const __half* __restrict__ b2b, int head,
+                  float slope, float* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * kHeadWaves + (threadIdx.x >> 6);
+  if (row >= n) return;   // wave-uniform
+  const bool first = row < n0;
+  const __half* w2 = first ? w2a : w2b;
+  const __half* b2 = first ? b2a : b2b;
+  float acc0 = 0.0f, acc1 = 0.0f;
+  for (int c = 8 * lane; c < k; c += 8 * 64) {
+    float x[8], u[8], v[8];
+    Io<__half>::load(h + (size_t)row * ld + c, x);
+    Io<__half>::load(w2 + c, u);
+    Io<__half>::load(w2 + k + c, v);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const float a = __half2float(__float2half(x[j] > 0.0f ? x[j] : x[j] * slope));
+      acc0 += a * u[j];
+      acc1 += a * v[j];
+    }
+  }
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    acc0 += __shfl_xor(acc0, o);
+    acc1 += __shfl_xor(acc1, o);
+  }
+  if (lane == 0) {
+    float y[2] = {__half2float(__float2half(acc0 + __half2float(b2[0]))),
+                  __half2float(__float2half(acc1 + __half2float(b2[1])))};
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      if (head == 1) y[j] = tanhf(y[j]);
+      else if (head == 2) y[j] = 1.0f / (1.0f + expf(-y[j]));
+    }
+    *reinterpret_cast<float2*>(out + 2 * (size_t)row) = make_float2(y[0], y[1]);
+  }
+}
+}  // namespace
+
+extern "C" int dt_actor_head(int32_t n, int32_t n0, int32_t k, const void* h, int32_t ld,
+                             const void* w2a, const void* b2a, const void* w2b, const void* b2b,
+                             int32_t head, float slope, float* out, void* stream) {
+  if (n < 0 || n0 < 0 || n0 > n || k < 8 || (k & 7) != 0 || ld < k || (ld & 7) != 0 || !h ||
+      !w2a || !b2a || !out || head < 0 || head > 2 || (n0 < n && (!w2b || !b2b)))
+    return DT_E_ARG;
+  if (((reinterpret_cast<uintptr_t>(h) | reinterpret_cast<uintptr_t>(w2a) |
+        (w2b ? reinterpret_cast<uintptr_t>(w2b) : 0)) & 15) ||
+      (reinterpret_cast<uintptr_t>(out) & 7))
+    return DT_E_ARG;
+  if (n == 0) return DT_OK;
+  hipLaunchKernelGGL(actor_head_kernel, dim3((n + kHeadWaves - 1) / kHeadWaves),
+                     dim3(64 * kHeadWaves), 0, (hipStream_t)stream, n, n0, k,
+                     (const __half*)h, ld, (const __half*)w2a, (const __half*)b2a,
+                     (const __half*)w2b, (const __half*)b2b, head, slope, out);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}

@@ -80,6 +80,18 @@ __device__ __forceinline__ void st4(float* p, int64_t q, float4 v) {
   reinterpret_cast<float4*>(p)[q] = v;
 }
 
+// a = leaky_relu(z + bias): the block's activation, recomputed from the
+// convolution output wherever it is read (never stored), the same two
+// roundings each time
+__device__ __forceinline__ void leaky4(float4 v, float4 b, float slope, float (&x)[4]) {
+  x[0] = v.x + b.x;
+  x[1] = v.y + b.y;
+  x[2] = v.z + b.z;
+  x[3] = v.w + b.w;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) x[k] = x[k] > 0.0f ? x[k] : x[k] * slope;
+}
+
 // ---- forward 1: a = leaky(z + bias) and the batch statistics of a --------------------
 __global__ void __launch_bounds__(kT)
 bn_stats_kernel(int64_t m, const float* __restrict__ z, const float* __restrict__ bias, float slope,
@@ -93,11 +105,9 @@ bn_stats_kernel(int64_t m, const float* __restrict__ z, const float* __restrict_
   float n = 0.0f, mean[4] = {0, 0, 0, 0}, m2[4] = {0, 0, 0, 0};
   const int64_t items = m * 8, stride = (int64_t)gridDim.x * kT;
   for (int64_t q = (int64_t)blockIdx.x * kT + tid; q < items; q += stride) {
-    const float4 v = ld4(z, q);
-    float x[4] = {v.x + b.x, v.y + b.y, v.z + b.z, v.w + b.w};
-#pragma unroll
-    for (int k = 0; k < 4; ++k) x[k] = x[k] > 0.0f ? x[k] : x[k] * slope;
-    st4(a, q, make_float4(x[0], x[1], x[2], x[3]));
+    float x[4];
+    leaky4(ld4(z, q), b, slope, x);
+    if (a) st4(a, q, make_float4(x[0], x[1], x[2], x[3]));
     n += 1.0f;
     const float inv = 1.0f / n;
 #pragma unroll
@@ -179,18 +189,20 @@ bn_stats_kernel(int64_t m, const float* __restrict__ z, const float* __restrict_
 
 // ---- forward 2: y = (a - mean) * invstd * gamma + beta -------------------------------
 __global__ void __launch_bounds__(kT)
-bn_apply_kernel(int64_t m, const float* __restrict__ a, const float* __restrict__ mean_invstd,
-                const float* __restrict__ gamma, const float* __restrict__ beta,
-                float* __restrict__ y) {
+bn_apply_kernel(int64_t m, const float* __restrict__ z, const float* __restrict__ bias, float slope,
+                const float* __restrict__ mean_invstd, const float* __restrict__ gamma,
+                const float* __restrict__ beta, float* __restrict__ y) {
   const int cg = threadIdx.x & 7;
+  const float4 b = ld4(bias, cg);
   const float4 mu = ld4(mean_invstd, cg), is = ld4(mean_invstd + C, cg);
   const float4 g = ld4(gamma, cg), bt = ld4(beta, cg);
   const float4 sc = make_float4(is.x * g.x, is.y * g.y, is.z * g.z, is.w * g.w);
   const int64_t items = m * 8, stride = (int64_t)gridDim.x * kT;
   for (int64_t q = (int64_t)blockIdx.x * kT + threadIdx.x; q < items; q += stride) {
-    const float4 v = ld4(a, q);
-    st4(y, q, make_float4((v.x - mu.x) * sc.x + bt.x, (v.y - mu.y) * sc.y + bt.y,
-                          (v.z - mu.z) * sc.z + bt.z, (v.w - mu.w) * sc.w + bt.w));
+    float v[4];
+    leaky4(ld4(z, q), b, slope, v);
+    st4(y, q, make_float4((v[0] - mu.x) * sc.x + bt.x, (v[1] - mu.y) * sc.y + bt.y,
+                          (v[2] - mu.z) * sc.z + bt.z, (v[3] - mu.w) * sc.w + bt.w));
   }
 }
 
@@ -261,17 +273,21 @@ __device__ void final_sums(const float* __restrict__ part, float* const (&out)[k
 
 // ---- backward 1: dbeta = sum(dy), dgamma = sum(dy * xhat) ---------------------------
 __global__ void __launch_bounds__(kT)
-bn_bwd_reduce_kernel(int64_t m, const float* __restrict__ dy, const float* __restrict__ a,
+bn_bwd_reduce_kernel(int64_t m, const float* __restrict__ dy, const float* __restrict__ z,
+                     const float* __restrict__ bias, float slope,
                      const float* __restrict__ mean_invstd, float* __restrict__ dgamma,
                      float* __restrict__ dbeta, float* __restrict__ work) {
   const int cg = threadIdx.x & 7;
+  const float4 b = ld4(bias, cg);
   const float4 mu = ld4(mean_invstd, cg), is = ld4(mean_invstd + C, cg);
   const float mus[4] = {mu.x, mu.y, mu.z, mu.w}, iss[4] = {is.x, is.y, is.z, is.w};
   float acc[2][4] = {{0, 0, 0, 0}, {0, 0, 0, 0}};
   const int64_t items = m * 8, stride = (int64_t)gridDim.x * kT;
   for (int64_t q = (int64_t)blockIdx.x * kT + threadIdx.x; q < items; q += stride) {
-    const float4 g4 = ld4(dy, q), a4 = ld4(a, q);
-    const float g[4] = {g4.x, g4.y, g4.z, g4.w}, x[4] = {a4.x, a4.y, a4.z, a4.w};
+    const float4 g4 = ld4(dy, q);
+    const float g[4] = {g4.x, g4.y, g4.z, g4.w};
+    float x[4];
+    leaky4(ld4(z, q), b, slope, x);
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
       acc[0][k] += g[k];
@@ -287,7 +303,8 @@ bn_bwd_reduce_kernel(int64_t m, const float* __restrict__ dy, const float* __res
 
 // ---- backward 2: dz, and dbias = sum(dz) ----------------------------------------------
 __global__ void __launch_bounds__(kT)
-bn_bwd_apply_kernel(int64_t m, const float* __restrict__ dy, const float* __restrict__ a,
+bn_bwd_apply_kernel(int64_t m, const float* __restrict__ dy, const float* __restrict__ z,
+                    const float* __restrict__ bias,
                     const float* __restrict__ mean_invstd, const float* __restrict__ gamma,
                     const float* __restrict__ dgamma, const float* __restrict__ dbeta, float slope,
                     float* __restrict__ dz, float* __restrict__ dbias, float* __restrict__ work) {
@@ -303,11 +320,14 @@ bn_bwd_apply_kernel(int64_t m, const float* __restrict__ dy, const float* __rest
     k2[k] = dbeta[c] * inv_m;
     k3[k] = dgamma[c] * inv_m;
   }
+  const float4 b = ld4(bias, cg);
   float acc[1][4] = {{0, 0, 0, 0}};
   const int64_t items = m * 8, stride = (int64_t)gridDim.x * kT;
   for (int64_t q = (int64_t)blockIdx.x * kT + threadIdx.x; q < items; q += stride) {
-    const float4 g4 = ld4(dy, q), a4 = ld4(a, q);
-    const float g[4] = {g4.x, g4.y, g4.z, g4.w}, x[4] = {a4.x, a4.y, a4.z, a4.w};
+    const float4 g4 = ld4(dy, q);
+    const float g[4] = {g4.x, g4.y, g4.z, g4.w};
+    float x[4];
+    leaky4(ld4(z, q), b, slope, x);
     float o[4];
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -395,33 +415,36 @@ int dt_bn_leaky_fwd(int64_t m, const float* z, const float* bias, float slope, c
                     float* running_var, int64_t* num_batches_tracked, int32_t updates, float* a,
                     float* y, float* mean_invstd, float* work, void* stream) {
   if (updates < 1) return DT_E_ARG;
-  if (m < 1 || !z || !bias || !gamma || !beta || !running_mean || !running_var || !a || !y ||
+  if (m < 1 || !z || !bias || !gamma || !beta || !running_mean || !running_var || !y ||
       !mean_invstd || !work)
     return DT_E_ARG;
-  if (!aligned16(z) || !aligned16(a) || !aligned16(y) || !aligned16(bias) ||
+  if (!aligned16(z) || (a && !aligned16(a)) || !aligned16(y) || !aligned16(bias) ||
       !aligned16(mean_invstd) || !aligned16(gamma) || !aligned16(beta))
     return DT_E_ARG;
   const int g = grid_of(m);
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(bn_stats_kernel, dim3(g), dim3(kT), 0, s, m, z, bias, slope, eps, momentum,
                      running_mean, running_var, num_batches_tracked, (int)updates, a, mean_invstd, work);
-  hipLaunchKernelGGL(bn_apply_kernel, dim3(g), dim3(kT), 0, s, m, a, mean_invstd, gamma, beta, y);
+  hipLaunchKernelGGL(bn_apply_kernel, dim3(g), dim3(kT), 0, s, m, z, bias, slope, mean_invstd,
+                     gamma, beta, y);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 
-int dt_bn_leaky_bwd(int64_t m, const float* dy, const float* a, const float* mean_invstd,
-                    const float* gamma, float slope, float* dz, float* dbias, float* dgamma,
-                    float* dbeta, float* work, void* stream) {
-  if (m < 1 || !dy || !a || !mean_invstd || !gamma || !dz || !dbias || !dgamma || !dbeta || !work)
+int dt_bn_leaky_bwd(int64_t m, const float* dy, const float* z, const float* bias,
+                    const float* mean_invstd, const float* gamma, float slope, float* dz,
+                    float* dbias, float* dgamma, float* dbeta, float* work, void* stream) {
+  if (m < 1 || !dy || !z || !bias || !mean_invstd || !gamma || !dz || !dbias || !dgamma ||
+      !dbeta || !work)
     return DT_E_ARG;
-  if (!aligned16(dy) || !aligned16(a) || !aligned16(dz) || !aligned16(mean_invstd))
+  if (!aligned16(dy) || !aligned16(z) || !aligned16(bias) || !aligned16(dz) ||
+      !aligned16(mean_invstd))
     return DT_E_ARG;
   const int g = grid_of(m);
   hipStream_t s = (hipStream_t)stream;
-  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(g), dim3(kT), 0, s, m, dy, a, mean_invstd, dgamma,
-                     dbeta, work);
-  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(g), dim3(kT), 0, s, m, dy, a, mean_invstd, gamma,
-                     dgamma, dbeta, slope, dz, dbias, work);
+  hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(g), dim3(kT), 0, s, m, dy, z, bias, slope,
+                     mean_invstd, dgamma, dbeta, work);
+  hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(g), dim3(kT), 0, s, m, dy, z, bias, mean_invstd,
+                     gamma, dgamma, dbeta, slope, dz, dbias, work);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 

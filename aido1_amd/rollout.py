@@ -147,6 +147,30 @@ class ActorRollout:
         if self.exploit_actor is not None:
             self.exploit_actor.refresh(actor)
 
+    def _step_envs(self):
+        """dt_step + dt_render of every map's envs.  Several maps (config 4's
+        small_loop / zigzag mix) run on their own streams, side by side: each
+        launch covers only its share of the envs (a latency-bound step, a
+        render filling part of the chip)."""
+        groups = list(zip(self.envs, self.outs, self.renders, self.slices))
+        if len(groups) == 1 or self.device.type != 'cuda':
+            for env, o, ro, sl in groups:
+                env.step_into(self.actions[sl], o)
+                env.render_into(ro, fresh=o.done)
+            return
+        cur = torch.cuda.current_stream(self.device)
+        if getattr(self, '_env_streams', None) is None:
+            self._env_streams = [torch.cuda.Stream(self.device) for _ in groups[1:]]
+        streams = [cur] + self._env_streams
+        for s in self._env_streams:
+            s.wait_stream(cur)
+        for s, (env, o, ro, sl) in zip(streams, groups):
+            with torch.cuda.stream(s):
+                env.step_into(self.actions[sl], o)
+                env.render_into(ro, fresh=o.done)
+        for s in self._env_streams:
+            cur.wait_stream(s)
+
     def step(self, timing=None):
         """One decision for every env; returns (reward, reward_mod, done) views."""
         if timing is not None:
@@ -168,9 +192,7 @@ class ActorRollout:
                                                generator=self.gen, head=self.head))
         if self.exploit_actor is not None:   # epsilon 0: DDPG.act without noise
             self.actions[ne:] = act(out[ne:], None, self.head)
-        for env, o, ro, sl in zip(self.envs, self.outs, self.renders, self.slices):
-            env.step_into(self.actions[sl], o)
-            env.render_into(ro, fresh=o.done)
+        self._step_envs()
         if self.fx is not None:   # tanh map, OU reset and episode count in one kernel
             self.fx.done(self.done, self.episode, self.actions)
             return self.reward, self.reward_mod, self.done

@@ -8,7 +8,9 @@ convolution without its bias (MIOpen) and then dt_bn_leaky_fwd: bias,
 LeakyReLU, the batch statistics, the running-statistics update and
 num_batches_tracked in one kernel, the normalisation in a second; its
 backward is dt_bn_leaky_bwd (two kernels for BatchNorm's, LeakyReLU's and the
-bias's gradients).  torch runs eight kernels for the forward tail and five for
+bias's gradients).  The activation leaky(z + bias) is never stored: every
+kernel recomputes it from the convolution output z (one f32 add and one
+select), which saves writing a second full-size tensor per block.  torch runs eight kernels for the forward tail and five for
 the backward.  The modules, parameters and state_dict are the unchanged
 torch ones; ``applicable`` says when the fused tail replaces them.
 """
@@ -53,7 +55,6 @@ class _BnLeaky(torch.autograd.Function):
     def forward(ctx, z, bias, gamma, beta, bn, slope):
         L = _lib.lib()
         m = z.numel() // C
-        a = torch.empty_like(z)
         y = torch.empty_like(z)
         mi = torch.empty(2 * C, device=z.device)
         nbt = bn.num_batches_tracked
@@ -61,26 +62,27 @@ class _BnLeaky(torch.autograd.Function):
                                beta.data_ptr(), bn.eps, bn.momentum, bn.running_mean.data_ptr(),
                                bn.running_var.data_ptr(),
                                nbt.data_ptr() if nbt is not None else None,
-                               int(getattr(bn, '_dt_updates', 1)), a.data_ptr(),
+                               int(getattr(bn, '_dt_updates', 1)), None,
                                y.data_ptr(), mi.data_ptr(), _work(bn, 'fwd', z.device).data_ptr(),
                                _stream(z.device))
         if rc != 0:
             raise _lib.DtError('dt_bn_leaky_fwd failed (%d)' % rc)
-        ctx.save_for_backward(a, mi, gamma)
+        # the activation is recomputed from z and bias in the backward (never stored)
+        ctx.save_for_backward(z, bias, mi, gamma)
         ctx.bn, ctx.slope = bn, slope
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        a, mi, gamma = ctx.saved_tensors
+        z, bias, mi, gamma = ctx.saved_tensors
         dy = dy.contiguous(memory_format=torch.channels_last)
         L = _lib.lib()
-        dz = torch.empty_like(a)
-        g = torch.empty(3, C, device=a.device)      # dbias, dgamma, dbeta
-        rc = L.dt_bn_leaky_bwd(a.numel() // C, dy.data_ptr(), a.data_ptr(), mi.data_ptr(),
-                               gamma.data_ptr(), ctx.slope, dz.data_ptr(), g[0].data_ptr(),
-                               g[1].data_ptr(), g[2].data_ptr(),
-                               _work(ctx.bn, 'bwd', a.device).data_ptr(), _stream(a.device))
+        dz = torch.empty_like(z)
+        g = torch.empty(3, C, device=z.device)      # dbias, dgamma, dbeta
+        rc = L.dt_bn_leaky_bwd(z.numel() // C, dy.data_ptr(), z.data_ptr(), bias.data_ptr(),
+                               mi.data_ptr(), gamma.data_ptr(), ctx.slope, dz.data_ptr(),
+                               g[0].data_ptr(), g[1].data_ptr(), g[2].data_ptr(),
+                               _work(ctx.bn, 'bwd', z.device).data_ptr(), _stream(z.device))
         if rc != 0:
             raise _lib.DtError('dt_bn_leaky_bwd failed (%d)' % rc)
         return dz, g[0], g[1], g[2], None, None

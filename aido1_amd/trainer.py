@@ -91,7 +91,8 @@ def _nullctx():
 
 class DDPGTrainer:
     def __init__(self, config, actor, critic, target_actor=None, target_critic=None,
-                 device=None, sync_grads=None, bucket_mb=16, graph=False, warmup=3):
+                 device=None, sync_grads=None, bucket_mb=16, graph=False, warmup=3,
+                 conv_search=True):
         t = config['training']
         self.config = config
         self.gamma, self.tau = float(t['gamma']), float(t['tau'])
@@ -117,6 +118,7 @@ class DDPGTrainer:
         self.critic_optim = make_optimizer(t['optimizer'], self.critic.parameters(), self.graph,
                                            self.device)
         self.warmup = warmup
+        self.conv_search = bool(conv_search)
         self._graphs = None
         self._in = None
         self.actor_decay = TrainingDecay(t['actor_train_decay'])
@@ -273,6 +275,27 @@ class DDPGTrainer:
             self.critic_decay(group)
         for group in self.actor_optim.param_groups:
             self.actor_decay(group)
+        with self._conv_flags():
+            self._run_stages()
+        self.global_update_step += 1
+        metrics = {'critic_loss': self._metrics[0], 'actor_loss': self._metrics[1]}
+        return metrics, {'td_error': self._td}
+
+    def _conv_flags(self):
+        """MIOpen Find mode for the update's convolutions (cudnn.benchmark): the
+        first update of each shape searches the solvers and later ones (and the
+        captured graphs) reuse the fastest.  With the default heuristic every
+        convolution call also ran a MIOpen tensor op (SubTensorOpWithScalar1d,
+        ~5.8 us, one per call in profiles/r03_train_kernel_stats.csv);
+        measured update 2.56 -> 2.25 ms per decision (tools/train_phases.py
+        with and without TP_CUDNN_BENCH)."""
+        if self.device.type != 'cuda' or not self.conv_search:
+            return _nullctx()
+        cd = torch.backends.cudnn
+        return cd.flags(enabled=cd.enabled, benchmark=True, deterministic=cd.deterministic,
+                        allow_tf32=cd.allow_tf32)
+
+    def _run_stages(self):
         syncs = [self.sync_critic, self.sync_actor, None]
         if self.graph and self.global_update_step >= self.warmup:
             if self._graphs is None:
@@ -290,6 +313,3 @@ class DDPGTrainer:
                 st()
                 if sync is not None:
                     sync()
-        self.global_update_step += 1
-        metrics = {'critic_loss': self._metrics[0], 'actor_loss': self._metrics[1]}
-        return metrics, {'td_error': self._td}

@@ -965,7 +965,9 @@ def bench_train(args, ctx):
                        'updates_per_step': args.updates_per_step,
                        'update_overlap': None if not args.overlap else
                        'update t on a side stream beside rollout t+1; acting weights one '
-                       'update behind (the reference explorers act asynchronously)',
+                       'update behind (the reference explorers act asynchronously): a '
+                       'different schedule from the sequential loop, not the same run done '
+                       'faster',
                        'weights': 'random init (config.json xavier_normal)',
                        'parallelism': 'env shards (%d x %d) + data-parallel update, RCCL '
                                       'all-reduce of %d gradients' % (ctx.world, n, nparams)},

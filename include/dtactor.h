@@ -138,6 +138,22 @@ int dt_explore(int32_t n, const float* actor_out, const double* normals, const d
 int dt_explore_done(int32_t n, const uint8_t* done, double* ou_x, int64_t* episode,
                     float* actions, int32_t tanh_map, void* stream);
 
+/* dt_actor_head: the actor's output branch after its first linear
+ * (config.json actor: leaky_relu -> linear(512 -> 2) -> tanh;
+ * duckietown_rl/ddpg.py:58-62) for n samples in one launch, one wave each:
+ *   out[i] = head(leaky(h[i]) . w2^T + b2), rows [0, n0) with (w2a, b2a), rows
+ *   [n0, n) with (w2b, b2b) (the second weight set of dt_conv1_split).
+ *   h      device fp16 [n, ld] (the first linear's output, bias included), k
+ *          inputs used (k, ld multiples of 8)
+ *   w2*    device fp16 [2, k]; b2* device fp16 [2]
+ *   head   0 none, 1 tanh, 2 sigmoid; slope the LeakyReLU's negative slope
+ *   out    device f32 [n, 2]
+ * LeakyReLU is rounded to fp16 and the pre-head value to fp16, as the fp16
+ * tensors of the torch path are; the dot products accumulate in f32. */
+int dt_actor_head(int32_t n, int32_t n0, int32_t k, const void* h, int32_t ld, const void* w2a,
+                  const void* b2a, const void* w2b, const void* b2b, int32_t head, float slope,
+                  float* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -47,7 +47,10 @@ int64_t dt_train_work_floats(int64_t m);
  * that many train-mode forwards over the same batch would (the trainer's
  * shared critic trunk: the actor-loss and TD-error forwards of
  * training/trainers.py:190-192,223-226 see the same weights and batch).
- *   z, a, y            device f32 [m, 32]
+ *   z, y               device f32 [m, 32]
+ *   a                  device f32 [m, 32] out, or NULL: the activation is not
+ *                      stored (the normalisation and dt_bn_leaky_bwd recompute
+ *                      it from z and bias, bit for bit)
  *   bias, gamma, beta  device f32 [32]
  *   running_mean, running_var  device f32 [32], updated in place
  *   num_batches_tracked        device int64 [1] or NULL
@@ -58,16 +61,17 @@ int dt_bn_leaky_fwd(int64_t m, const float* z, const float* bias, float slope, c
                     float* running_var, int64_t* num_batches_tracked, int32_t updates, float* a,
                     float* y, float* mean_invstd, float* work, void* stream);
 
-/* Backward of dt_bn_leaky_fwd given dy (device f32 [m, 32]):
+/* Backward of dt_bn_leaky_fwd given dy (device f32 [m, 32]) and the forward's
+ * z and bias (a = leaky_relu(z + bias, slope) recomputed):
  *   dgamma = sum(dy * xhat), dbeta = sum(dy), xhat = (a - mean) * invstd;
  *   da = gamma * invstd * (dy - dbeta / m - xhat * dgamma / m);
  *   dz = a > 0 ? da : slope * da  (LeakyReLU's backward: a > 0 iff z + bias > 0);
  *   dbias = sum(dz).
  *   dz            device f32 [m, 32] out
  *   dbias, dgamma, dbeta  device f32 [32] out (overwritten) */
-int dt_bn_leaky_bwd(int64_t m, const float* dy, const float* a, const float* mean_invstd,
-                    const float* gamma, float slope, float* dz, float* dbias, float* dgamma,
-                    float* dbeta, float* work, void* stream);
+int dt_bn_leaky_bwd(int64_t m, const float* dy, const float* z, const float* bias,
+                    const float* mean_invstd, const float* gamma, float slope, float* dz,
+                    float* dbias, float* dgamma, float* dbeta, float* work, void* stream);
 
 /* Multi-tensor steps over a network's parameters in one launch.  `tensors`
  * is a device table, one entry per parameter (the roles of a, b, c, d per

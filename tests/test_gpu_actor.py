@@ -313,3 +313,23 @@ def test_split_launch_matches_separate_actors(gpu, mode, n, n0):
     out = fa.forward_pair(fb, ring, order, n0)
     ref = torch.cat([fa(ring[:n0].contiguous(), order), fb(ring[n0:].contiguous(), order)])
     assert torch.allclose(out, ref, atol=1e-3), (out - ref).abs().max()
+
+
+@pytest.mark.parametrize('n,n0', [(300, 300), (300, 257), (64, 1)])
+def test_fused_head_matches_torch_head(gpu, n, n0):
+    """dt_actor_head (LeakyReLU -> lin2 -> tanh in one launch over both weight
+    sets) against FusedActor._head (torch ops, hipBLASLt lin2) on the same
+    lin1 inputs: within the fp16 rounding of the pre-tanh value (1e-3)."""
+    from aido1_amd.actor import FLAT, ConfigActor, FusedActor
+    from test_trainer import no_dropout
+    cfg = golden('reference_config.json')['model']['actor']
+    torch.manual_seed(n + n0)
+    fa = FusedActor(ConfigActor(no_dropout(cfg)).to(gpu), dtype=torch.float16)
+    fb = FusedActor(ConfigActor(no_dropout(cfg)).to(gpu), dtype=torch.float16)
+    assert fa._head_fusable(fb)
+    flat = (torch.randn(n, FLAT, device=gpu) * 0.5).half()
+    out = torch.full((n, 2), float('nan'), device=gpu)
+    fa._heads(fb, flat, n0, out)
+    ref = torch.cat([fa._head(flat[:n0]), fb._head(flat[n0:])])
+    assert torch.isfinite(out).all()
+    assert torch.allclose(out, ref, rtol=0, atol=1e-3), (out - ref).abs().max()

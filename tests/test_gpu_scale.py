@@ -64,7 +64,28 @@ def test_config4_actor_rollout_at_size(gpu):
     with torch.no_grad():
         ref = torch.cat([ref_actor(frames[i:i + 1]) for i in range(64)])
     err = torch.max(torch.abs(out - ref)).item()
-    assert err < 1.5e-2, err
+    print('config4 fp16 actor vs fp32 per-sample CPU reference, 64 envs: max %.3g' % err)
+    assert err < 1e-2, err
+    # every env: against the float32 GPU path (MIOpen convolutions + the
+    # batched per-sample norm, 1e-5 from a float64 restatement,
+    # tests/test_gpu_actor.py), the same weights and live ring
+    from aido1_amd.actor import FusedActor
+    f32 = FusedActor(ref_actor.to(gpu), dtype=torch.float32, mode='reference')
+    f32.p_drop = 0.0
+    full = roll.actor(roll.ring, roll.order()).float()
+    full_ref = f32(roll.stack()).float()
+    diff = torch.abs(full - full_ref)
+    err_all = diff.max().item()
+    q = torch.quantile(diff.flatten(), torch.tensor([0.5, 0.99, 0.999], device=gpu)).tolist()
+    frac = (diff > 1e-2).float().mean().item()
+    print('config4 fp16 actor vs f32 GPU path, all %d envs: max %.3g, median %.3g, p99 %.3g, '
+          'p99.9 %.3g, outputs > 1e-2: %.4f' % (n, err_all, q[0], q[1], q[2], frac))
+    # fp16 under per-sample (batch-of-one) BatchNorm: a channel that is
+    # nearly flat over a frame is divided by a tiny standard deviation, which
+    # amplifies fp16 rounding (measured max 6.8e-2 over 4096 live envs, 4e-3
+    # on the 64 above); the bulk stays within 1e-2
+    assert err_all < 0.1, err_all
+    assert frac < 0.01, frac
     roll.close()
 
 

@@ -13,6 +13,8 @@ from aido1_amd.train_loop import TrainLoop  # noqa: E402
 
 
 def main():
+    if os.environ.get('TP_CUDNN_BENCH'):   # MIOpen Find-mode algorithm search (experiment)
+        torch.backends.cudnn.benchmark = True
     with open(os.path.join(os.path.dirname(__file__), '..', 'aido1_amd', 'configs',
                            'reference_config.json')) as f:
         cfg = json.load(f)
