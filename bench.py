@@ -106,9 +106,14 @@ def parse(argv=None):
                    help='lane config: replay the timed launches as one captured HIP graph '
                         '(default: prebound eager dt_step_many calls)')
     p.add_argument('--no-parity', action='store_true', help='skip the oracle parity pass')
-    p.add_argument('--obs-mode', default='many', choices=['many', 'serial', 'pipe'],
+    p.add_argument('--obs-mode', default='many', choices=['many', 'many2', 'serial', 'pipe'],
                    help='render: how the steps are launched (ObsLoop)')
     p.add_argument('--no-lane', action='store_true', help='render: skip the config-2 sub-record')
+    p.add_argument('--event-stride', type=int, default=4,
+                   help='render: HIP events around every S-th dt_render of the timed region '
+                        '(the roofline\'s average kernel duration is over those launches); '
+                        'an event pair around every launch adds ~6 us a decision of stream '
+                        'packets to the wall time (measured: 0.1805 vs 0.1745 ms per step)')
     p.add_argument('--lane-steps', type=int, default=320,
                    help='render: decisions timed by the config-2 sub-record')
     p.add_argument('--lane-warmup', type=int, default=20)
@@ -453,20 +458,24 @@ class ObsLoop:
                the snapshot on another: step d + 1 beside render d.
     Every mode computes the same frames, masks and step outputs."""
 
-    def __init__(self, env, ro, torch, mode='many', chunk=20):
+    def __init__(self, env, ro, torch, mode='many', chunk=20, event_stride=1):
         self.env, self.ro, self.torch, self.mode = env, ro, torch, mode
+        # pipe mode orders the step stream on the render end events: all recorded
+        self.event_stride = 1 if mode == 'pipe' else max(1, int(event_stride))
         lo, hi = torch.cuda.Stream.priority_range()
         self.s_step = torch.cuda.Stream(env.device, priority=hi if mode == 'pipe' else lo)
-        self.s_rend = torch.cuda.Stream(env.device) if mode == 'pipe' else self.s_step
+        two = mode in ('pipe', 'many2')
+        self.s_rend = torch.cuda.Stream(env.device) if two else self.s_step
         self.chunk = max(1, min(int(chunk), 64))
-        np_ = self.chunk if mode == 'many' else 2
+        np_ = {'many': self.chunk, 'many2': 2 * self.chunk}.get(mode, 2)
         self.pose = torch.empty(np_, 3, env.n, dtype=torch.float64, device=env.device)
 
     def events(self, k):
         E = self.torch.cuda.Event
         return ([E() for _ in range(k)],
                 [(E(enable_timing=True), E(enable_timing=True)) for _ in range(k)],
-                [(E(enable_timing=True), E(enable_timing=True)) for _ in range(k)])
+                [(E(enable_timing=True), E(enable_timing=True)) for _ in range(k)],
+                [E() for _ in range(k)])
 
     def bind(self, actions, out):
         """The foreign calls of len(actions) decisions writing `out` (a
@@ -475,9 +484,11 @@ class ObsLoop:
         from aido1_amd.render import bind_render
         env, n, k = self.env, self.env.n, int(actions.shape[0])
         groups = []
-        if self.mode == 'many':
-            for a, b in _bounds(split_even(k, self.chunk)):
-                pose = self.pose[:b - a]
+        if self.mode in ('many', 'many2'):
+            for c, (a, b) in enumerate(_bounds(split_even(k, self.chunk))):
+                # many2: chunk c's poses in half c % 2 (its renders overlap step c + 1)
+                h = self.chunk * (c % 2) if self.mode == 'many2' else 0
+                pose = self.pose[h:h + b - a]
                 step = env.bind_step_many(actions[a:b], _Slice(out, a, b, n), pose=pose,
                                           stream=self.s_step)
                 rend = [bind_render(env, self.ro, self.s_rend, fresh=out.done[d * n:(d + 1) * n],
@@ -496,13 +507,15 @@ class ObsLoop:
     def run(self, groups, ev):
         """Launch the bound decisions; returns the OR of the calls' status codes."""
         torch, env = self.torch, self.env
-        ev_step, t_rend, t_step = ev
+        ev_step, t_rend, t_step, ev_done = ev
         ss, sr = self.s_step, self.s_rend
         ss.wait_stream(torch.cuda.current_stream(env.device))
         rcs = 0
-        for d0, step, copy, rends in groups:
+        for c, (d0, step, copy, rends) in enumerate(groups):
             if self.mode == 'pipe' and d0 >= 2:
                 ss.wait_event(t_rend[d0 - 2][1])
+            if self.mode == 'many2' and c >= 2:     # its pose half is free again
+                ss.wait_event(ev_done[groups[c - 2][0]])
             t_step[d0][0].record(ss)
             rcs |= step()
             t_step[d0][1].record(ss)
@@ -512,9 +525,14 @@ class ObsLoop:
                 ev_step[d0].record(ss)
                 sr.wait_event(ev_step[d0])
             for i, rend in enumerate(rends):
-                t_rend[d0 + i][0].record(sr)
+                timed = (d0 + i) % self.event_stride == 0
+                if timed:
+                    t_rend[d0 + i][0].record(sr)
                 rcs |= rend()
-                t_rend[d0 + i][1].record(sr)
+                if timed:
+                    t_rend[d0 + i][1].record(sr)
+            if self.mode == 'many2':
+                ev_done[d0].record(sr)
         torch.cuda.current_stream(env.device).wait_stream(sr)
         return rcs
 
@@ -532,7 +550,7 @@ def bench_obs(args, ctx):
     g.manual_seed(args.seed + 7919 * rank)
     actions = torch.rand(W + K, n, 2, generator=g, device=dev, dtype=torch.float32)
     ro = RenderOutput(n, dev)          # 3-slot grey ring (Transformer stack) + 4 masks
-    loop = ObsLoop(env, ro, torch, args.obs_mode, args.many)
+    loop = ObsLoop(env, ro, torch, args.obs_mode, args.many, args.event_stride)
     env.reset()
     wout = StepOutput(max(W, 1) * n, dev, lanepos=False, tile=False)
     if W and loop.run(loop.bind(actions[:W], wout), loop.events(W)):
@@ -556,7 +574,7 @@ def bench_obs(args, ctx):
     st = env.stats()
     env.check()
     tot, tmax, per = rank_report(ctx, [st['sim_steps'], st['decisions'], st['resets']], elapsed)
-    rend_ms = [a.elapsed_time(b) for a, b in ev[1]]
+    rend_ms = [a.elapsed_time(b) for d, (a, b) in enumerate(ev[1]) if d % loop.event_stride == 0]
     starts = [g[0] for g in calls]
     step_ms = [ev[2][d][0].elapsed_time(ev[2][d][1]) for d in starts]
 
@@ -591,6 +609,11 @@ def bench_obs(args, ctx):
                                    'decision\'s end pose written), then each decision\'s '
                                    'dt_render of that pose with its done flags as fresh; one '
                                    'stream, prebound calls' % args.many,
+                           'many2': 'dt_step_many over chunks of <= %d decisions on a step '
+                                    'stream (each decision\'s end pose written, two pose '
+                                    'buffers), each decision\'s dt_render of that pose on a '
+                                    'render stream: chunk c + 1\'s steps beside chunk c\'s '
+                                    'renders; prebound calls' % args.many,
                            'serial': 'per decision: dt_step then dt_render, one stream, prebound',
                            'pipe': 'per decision: dt_step + dt_copy_pose (high-priority stream), '
                                    'dt_render of the snapshot (render stream), prebound'
@@ -614,7 +637,9 @@ def bench_obs(args, ctx):
                                               'without the step\'s 81 B); plus 153,600 B of '
                                               'ring refill per respawned env (%.1f per launch)'
                                               % fresh_per_launch,
-                         'timing': 'HIP events on the render stream around each dt_render'},
+                         'timing': 'HIP events on the render stream around every %d-th '
+                                   'dt_render of the timed region (%d launches averaged)'
+                                   % (loop.event_stride, len(rend_ms))},
             'step_launch_ms': float(np.mean(step_ms)),
             'step_launches': len(starts),
             'host_enqueue_ms_per_step': t_host / K * 1e3,
