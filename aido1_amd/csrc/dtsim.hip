@@ -140,6 +140,9 @@ constexpr int kBlock = 256;        // step and refill blocks (4 waves)
 __device__ inline void put_slot(const dt::State& st, int n, int e, uint32_t key, bool ok,
                                 uint32_t tag, double x, double z, double a, double dist,
                                 double arad) {
+#if defined(DTSIM_DIAG_SKIP_STORES) && (DTSIM_DIAG_SKIP_STORES & 16)
+  return;   // diagnostic build: no refill stores
+#endif
   const size_t sl = key % (uint32_t)dt::kSlots;
   double* p = st.pre + sl * dt::kSlotRec * (size_t)n + e;
   double sa = 0.0, ca = 1.0;
@@ -877,14 +880,17 @@ __global__ __launch_bounds__(kFanBlock) __attribute__((amdgpu_waves_per_eu(2, 2)
     const bool reset_now = want_reset && ok;
     if (wave == 0 && lead && want_reset && !ok) atomicOr(st.err, dt::kErrSpawn);
 
+#ifndef DTSIM_DIAG_SKIP_STORES
+#define DTSIM_DIAG_SKIP_STORES 0   // diagnostic builds only (tools/step_write_diag.sh)
+#endif
     if (active && lead) {
       const size_t o = (size_t)d * n + e;
       if (wave == 0) {
-        rew[o] = tr;
-        rewm[o] = trm;
+        if (!(DTSIM_DIAG_SKIP_STORES & 1)) rew[o] = tr;
+        if (!(DTSIM_DIAG_SKIP_STORES & 2)) rewm[o] = trm;
       } else if (wave == 1) {
-        done_out[o] = (uint8_t)dn;
-      } else if (wave == 2 && obs) {
+        if (!(DTSIM_DIAG_SKIP_STORES & 4)) done_out[o] = (uint8_t)dn;
+      } else if (wave == 2 && obs && !(DTSIM_DIAG_SKIP_STORES & 8)) {
         obs[o] = reset_now ? make_float2((float)rp[3], (float)rp[4])
                            : (inl_last ? make_float2((float)dist_last, (float)arad_last)
                                        : make_float2(0.0f, 0.0f));

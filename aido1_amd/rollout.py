@@ -191,7 +191,10 @@ class ActorRollout:
             self.actions.copy_(explore_actions(out, self.ou, eps, self.explorer_id, self.config,
                                                generator=self.gen, head=self.head))
         if self.exploit_actor is not None:   # epsilon 0: DDPG.act without noise
-            self.actions[ne:] = act(out[ne:], None, self.head)
+            if self.head == 'tanh':              # its clip, written in place (one kernel)
+                torch.clamp(out[ne:], -1.0, 1.0, out=self.actions[ne:])
+            else:
+                self.actions[ne:] = act(out[ne:], None, self.head)
         self._step_envs()
         if self.fx is not None:   # tanh map, OU reset and episode count in one kernel
             self.fx.done(self.done, self.episode, self.actions)
