@@ -337,6 +337,16 @@ struct RenderArgs {
 #define DTSIM_RENDER_THREADS 512
 #endif
 constexpr int kRenderThreads = DTSIM_RENDER_THREADS;
+// diagnostic builds only (tools/render_phase_valu.sh): the workgroup returns
+// after phase group k (1: background spans + projection, 2: + fix-up and
+// markings, 3: + uniformity, 4: + Canny), so SQ_INSTS_VALU per build splits the
+// kernel's instruction count by phase; the product build never stops
+#ifdef DTSIM_RENDER_STOP_AT
+#define RENDER_STOP(k) \
+  if ((k) == DTSIM_RENDER_STOP_AT) return
+#else
+#define RENDER_STOP(k)
+#endif
 constexpr int WPR = W / 4;          // words per row
 constexpr int NW = NPIX / 4;        // words per image
 constexpr int QPR = WPR / 4;        // 16-pixel quads per row
@@ -1062,6 +1072,7 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, in
   }
   __syncthreads();
   RENT(5);
+  RENDER_STOP(1);
 
   // phase 0b: the listed spans' words and the marking segments (DTSIM_MARK_PARTS
   // lanes per segment), all OR-ed into the image in one pass
@@ -1133,6 +1144,7 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, in
   }
   __syncthreads();
   RENT(6);
+  RENDER_STOP(2);
 
   // phase 1: per 16-pixel quad (4 words of a row): the 3 x 6-word neighbourhood
   // decides each word's uniformity exactly (all 18 pixels around it one
@@ -1207,16 +1219,19 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, in
   }
   __syncthreads();
   RENT(8);
+  RENDER_STOP(3);
 
   // phases 2-3, then the outputs
   const int nlist = C[kNList];
   if (nlist <= a.list_cap) {
     if (mbase) canny<false>(a, S, e, nlist);
     RENT(13);
+    RENDER_STOP(4);
     write_outputs<false>(a, S, e, mbase);
   } else {
     if (mbase) canny<true>(a, S, e, nlist);
     RENT(13);
+    RENDER_STOP(4);
     write_outputs<true>(a, S, e, mbase);
   }
 #ifdef DTSIM_STAMPS
