@@ -945,7 +945,13 @@ __device__ __forceinline__ void write_outputs(const RenderArgs& a, RenderLds& S,
     if (q < NQ) {
       if (mbase) {
         const uint4 m = *reinterpret_cast<const uint4*>(S.img + 4 * q);
-        if (quick_masks && ((m.x | m.y | m.z | m.w) & ~kPalMask) == 0u) {   // no listed word
+        // a quad without a listed word (and radius <= 1) is its own colour bits,
+        // and the dilation path gives it the same bytes: so a wave takes the
+        // quick path only when all its quads may, else every lane the dilation
+        // path (a wave of 64 quads spans six rows and usually holds a listed
+        // word: running both paths under divergence cost both)
+        const bool uni = quick_masks && ((m.x | m.y | m.z | m.w) & ~kPalMask) == 0u;
+        if (__ballot(!uni) == 0) {   // wave-uniform
           const uint32_t mw[4] = {m.x, m.y, m.z, m.w};
           uint32_t o[3][4];
 #pragma unroll
