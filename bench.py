@@ -96,8 +96,8 @@ def parse(argv=None):
     p.add_argument('--buffer-size', type=int, default=131072)
     p.add_argument('--updates-per-step', type=int, default=1)
     p.add_argument('--overlap', action='store_true',
-                   help='train: run each update beside the next rollout (side stream); '
-                        'measured slower, DESIGN 3.8')
+                   help='train: run each update beside the next rollout (side stream); a '
+                        'different schedule (acting one update behind), DESIGN 3.8')
     p.add_argument('--many', type=int, default=20,
                    help='most decisions per dt_step_many launch (lane config, and the render '
                         'config\'s many mode); K decisions are split into ceil(K / many) '
