@@ -685,15 +685,22 @@ __device__ __forceinline__ void quad_masks(const RenderLds& S, const Slots<kSpil
     if ((unsigned)rr >= (unsigned)H) continue;
     const uint32_t* row = S.img + rr * WPR;
     const uint4 cur = *reinterpret_cast<const uint4*>(row + cw0);
+    // does this row's part of the element reach past the quad's words?  (a
+    // scalar test: the 3 x 3 ellipse, the default, is a cross, whose outer
+    // rows need no side words)
+    bool side = false;
+#pragma unroll
+    for (int dx = -R; dx <= R; ++dx)
+      side |= dx != 0 && ((dmask >> ((dy + 3) * 7 + (dx + 3))) & 1ull) != 0ull;
     // raster bytes (slot bits masked) -> colour-bit bytes (v_perm LUT); 0
     // outside the image
     const uint32_t wv[6] = {
-        cw0 > 0 ? __builtin_amdgcn_perm(bhi, blo, row[cw0 - 1] & kPalMask) : 0u,
+        side && cw0 > 0 ? __builtin_amdgcn_perm(bhi, blo, row[cw0 - 1] & kPalMask) : 0u,
         __builtin_amdgcn_perm(bhi, blo, cur.x & kPalMask),
         __builtin_amdgcn_perm(bhi, blo, cur.y & kPalMask),
         __builtin_amdgcn_perm(bhi, blo, cur.z & kPalMask),
         __builtin_amdgcn_perm(bhi, blo, cur.w & kPalMask),
-        cw0 + 4 < WPR ? __builtin_amdgcn_perm(bhi, blo, row[cw0 + 4] & kPalMask) : 0u};
+        side && cw0 + 4 < WPR ? __builtin_amdgcn_perm(bhi, blo, row[cw0 + 4] & kPalMask) : 0u};
 #pragma unroll
     for (int dx = -R; dx <= R; ++dx) {
       if (!((dmask >> ((dy + 3) * 7 + (dx + 3))) & 1ull)) continue;  // uniform
