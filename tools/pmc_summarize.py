@@ -18,7 +18,9 @@ import os
 import shutil
 import sys
 
-ROUND = sys.argv[1] if len(sys.argv) > 1 else 'r02'
+if len(sys.argv) < 2:   # it writes profiles/<round>_*: no default round to overwrite
+    sys.exit('usage: python tools/pmc_summarize.py <round, e.g. r03>')
+ROUND = sys.argv[1]
 OUT = 'gpurun_out'
 # label -> (bench config whose PMC passes hold it, kernel-name needles)
 KERNELS = {'step_fan_kernel': ('lane', ['step_fan_kernel']),
