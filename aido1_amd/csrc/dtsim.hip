@@ -573,6 +573,7 @@ constexpr int kFanMaxK = 64;                // decisions per launch (actions sta
 struct FanX {  // [parity][env][step], rows padded to 4 for wide LDS reads
   double dist[2][kFanEnvs][4], dot[2][kFanEnvs][4], arad[2][kFanEnvs][4], pen[2][kFanEnvs][4];
   uint8_t inl[2][kFanEnvs][4], vp[2][kFanEnvs][4];
+  double park[kFanBlock][9];   // a lane's values across an in-loop spawn
 };
 
 // kLean: the common configuration as compile-time facts (wheel-velocity
@@ -859,6 +860,17 @@ __global__ __launch_bounds__(kFanBlock) __attribute__((amdgpu_waves_per_eu(2, 2)
       for (int j = 0; j < dt::kSlotRec; ++j) rp[j] = sslot[(sl * dt::kSlotRec + j) * kFanEnvs + le];
     }
     uint64_t need = __ballot(want_reset && !slot_ready && lead);
+    const bool parked = need != 0u;
+    if (parked) {
+      // the rare in-loop spawn needs ~60 more registers than the rest of the
+      // loop: the decision's values that live across it wait in LDS (the
+      // memory clobbers keep the compiler from forwarding them), else the
+      // kernel spills to scratch on every launch
+      double* pk = X.park[threadIdx.x];
+      pk[0] = x; pk[1] = z; pk[2] = ang; pk[3] = c; pk[4] = s;
+      pk[5] = tr; pk[6] = trm; pk[7] = dist_last; pk[8] = arad_last;
+      asm volatile("" ::: "memory");
+    }
     while (need) {  // wave-uniform; every wave computes the same spawns
       const int l = __ffsll((unsigned long long)need) - 1;
       need &= need - 1u;
@@ -877,6 +889,12 @@ __global__ __launch_bounds__(kFanBlock) __attribute__((amdgpu_waves_per_eu(2, 2)
         ok = sok;
       }
     }
+    if (parked) {
+      asm volatile("" ::: "memory");
+      const double* pk = X.park[threadIdx.x];
+      x = pk[0]; z = pk[1]; ang = pk[2]; c = pk[3]; s = pk[4];
+      tr = pk[5]; trm = pk[6]; dist_last = pk[7]; arad_last = pk[8];
+    }
     const bool reset_now = want_reset && ok;
     if (wave == 0 && lead && want_reset && !ok) atomicOr(st.err, dt::kErrSpawn);
 
@@ -884,7 +902,9 @@ __global__ __launch_bounds__(kFanBlock) __attribute__((amdgpu_waves_per_eu(2, 2)
 #define DTSIM_DIAG_SKIP_STORES 0   // diagnostic builds only (tools/step_write_diag.sh)
 #endif
     if (active && lead) {
-      const size_t o = (size_t)d * n + e;
+      // 32-bit element indices (zero-extended into global_store's vector
+      // offset): a size_t e kept its 64-bit form live through the loop
+      const uint32_t o = (uint32_t)(d * n + e);
       if (wave == 0) {
         if (!(DTSIM_DIAG_SKIP_STORES & 1)) rew[o] = tr;
         if (!(DTSIM_DIAG_SKIP_STORES & 2)) rewm[o] = trm;
@@ -897,10 +917,11 @@ __global__ __launch_bounds__(kFanBlock) __attribute__((amdgpu_waves_per_eu(2, 2)
       } else if (wave == 3 && pose_out) {
         // the pose the decision ends in (the reset pose after a respawn): what a
         // render of this decision draws, [d][x | z | angle][env]
-        double* po = pose_out + (size_t)d * 3 * n + e;
-        po[0] = reset_now ? rp[0] : x;
-        po[n] = reset_now ? rp[1] : z;
-        po[2 * (size_t)n] = reset_now ? rp[2] : ang;
+        // 32-bit indices: a hoisted pose_out + e was another spill
+        const uint32_t pi = (uint32_t)(d * 3 * n + e);
+        pose_out[pi] = reset_now ? rp[0] : x;
+        pose_out[pi + (uint32_t)n] = reset_now ? rp[1] : z;
+        pose_out[pi + 2u * (uint32_t)n] = reset_now ? rp[2] : ang;
       }
     }
     x = reset_now ? rp[0] : x;
@@ -930,17 +951,21 @@ __global__ __launch_bounds__(kFanBlock) __attribute__((amdgpu_waves_per_eu(2, 2)
   dt::wave_count(st.stats + 2, resets_t * m, kk);
   dt::wave_count(st.stats + 3, dones_t * m, kk);
   if (active && lead) {
-    st.x[e] = x;
-    st.z[e] = z;
-    st.angle[e] = ang;
-    st.step_count[e] = step_count;
-    st.env_step[e] = env_step;
-    __hip_atomic_store(st.tick + e, tick + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t eu = (uint32_t)e;
+    st.x[eu] = x;
+    st.z[eu] = z;
+    st.angle[eu] = ang;
+    st.step_count[eu] = step_count;
+    st.env_step[eu] = env_step;
+    // tick re-read (only this lane writes it): kept live through the loop it
+    // was a scratch spill
+    const uint32_t tick_end = __hip_atomic_load(st.tick + eu, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(st.tick + eu, tick_end + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (key != key0) {
       // the slot records were read into LDS before the staging barrier, so
       // the window can move
-      st.episode[e] = key;
-      __hip_atomic_store(st.want + e, key + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      st.episode[eu] = key;
+      __hip_atomic_store(st.want + eu, key + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
 }
