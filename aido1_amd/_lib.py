@@ -22,7 +22,7 @@ SOURCES = ['dtsim.hip', 'dtrender.hip', 'dtreplay.hip', 'dtactor.hip', 'dtconv.h
 HEADERS = ['dtsim_common.h', 'dtrender.h']
 PUBLIC_HEADERS = ['dtsim.h', 'dtreplay.h', 'dtactor.h', 'dttrain.h']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
-ABI_VERSION = 7
+ABI_VERSION = 8
 
 HIP_FLAGS = ['--offload-arch=gfx950', '-O3', '-fPIC', '-shared', '-std=c++17',
              '-ffp-contract=off', '-munsafe-fp-atomics']
@@ -164,10 +164,11 @@ def lib():
             'dt_train_work_floats': (i64, [i64]),
             'dt_bn_leaky_fwd': (ctypes.c_int, [i64, vp, vp, ctypes.c_float, vp, vp, ctypes.c_float,
                                                ctypes.c_float, vp, vp, vp, i32, vp, vp, vp, vp,
-                                               vp]),
+                                               vp, vp]),
             'dt_bn_leaky_bwd': (ctypes.c_int, [i64, vp, vp, vp, vp, vp, ctypes.c_float, vp, vp, vp,
-                                               vp, vp, vp]),
-            'dt_adam': (ctypes.c_int, [i32, vp, vp, vp, vp, f64, f64, f64, vp, vp]),
+                                               vp, vp, vp, vp]),
+            'dt_adam': (ctypes.c_int, [i32, vp, vp, vp, vp, f64, f64, f64, vp, vp, i32, i32, vp]),
+            'dt_guard_scan': (ctypes.c_int, [i32, vp, vp, vp]),
             'dt_soft_update': (ctypes.c_int, [i32, vp, vp, f64, vp]),
             # dtactor.h
             'dt_sample_norm': (ctypes.c_int, [vp, vp, i32, i32, i32, vp, vp, ctypes.c_float,

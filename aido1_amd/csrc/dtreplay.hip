@@ -26,7 +26,7 @@ struct dt_per {
   double* mn = nullptr;    // [2*cap]
   double* maxp = nullptr;  // [1]
   int32_t* winner = nullptr;  // [cap], -1 when idle
-  int32_t* err = nullptr;     // [1] bit 0: bad priority, bit 1: bad index
+  int32_t* err = nullptr;     // [2] bits (0: bad priority, 1: bad index), rejected entries
   void* buf = nullptr;
   std::string msg;
 };
@@ -115,6 +115,7 @@ update_kernel(double* sum, double* mn, double* maxp, int32_t* winner, int32_t* e
     const bool ok_i = j >= 0 && j < len;
     if (!ok_p) atomicOr(err, 1);
     if (!ok_i) atomicOr(err, 2);
+    if (!ok_p || !ok_i) atomicAdd(err + 1, 1);   // counted, reported by dt_per_check
     if (ok_p && ok_i) {
       atomicMax(&winner[j], i);  // the sequential loop's last write wins
       pmax = fmax(pmax, p);
@@ -289,7 +290,7 @@ int dt_per_create(int64_t size, double alpha, int32_t device, dt_per** out) {
   h->err = (int32_t*)(b + 2 * tb + wb + 64);
   const int grid = (int)std::min<int64_t>((2 * h->cap + 255) / 256, 4096);
   fill_kernel<<<grid, 256>>>(h->sum, h->mn, h->maxp, h->winner, h->cap);
-  if (hipMemset(h->err, 0, 4) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
+  if (hipMemset(h->err, 0, 8) != hipSuccess || hipDeviceSynchronize() != hipSuccess) {
     g_per_create_err = "dt_per_create: init failed";
     (void)hipFree(h->buf);
     delete h;
@@ -385,14 +386,14 @@ int dt_per_check(dt_per* h) {
   if (!h) return DT_E_ARG;
   PER_HIP(h, hipSetDevice(h->device));
   PER_HIP(h, hipDeviceSynchronize());
-  int32_t e = 0;
-  PER_HIP(h, hipMemcpy(&e, h->err, 4, hipMemcpyDeviceToHost));
-  if (!e) return DT_OK;
-  PER_HIP(h, hipMemset(h->err, 0, 4));
+  int32_t e[2] = {0, 0};
+  PER_HIP(h, hipMemcpy(e, h->err, 8, hipMemcpyDeviceToHost));
+  if (!e[0]) return DT_OK;
+  PER_HIP(h, hipMemset(h->err, 0, 8));
   h->msg = "update_priorities: ";
-  if (e & 1) h->msg += "priority must be > 0; ";
-  if (e & 2) h->msg += "index outside [0, len); ";
-  h->msg += "offending entries were skipped";
+  if (e[0] & 1) h->msg += "priority must be > 0 (NaN included); ";
+  if (e[0] & 2) h->msg += "index outside [0, len); ";
+  h->msg += std::to_string(e[1]) + " offending entries were skipped";
   return DT_E_ARG;
 }
 

@@ -47,9 +47,12 @@ __device__ __forceinline__ void chan(float& n, float& mean, float& m2, float nb,
 
 // Partials cross workgroups (and XCDs, whose L2s are not coherent): they are
 // written through to memory (agent-scope relaxed atomic stores: `sc1`, the
-// line leaves the XCD's L2) and read back the same way by the last arriver,
-// so no release fence has to write back the L2 full of this launch's
-// activations (MI355X_MICROARCH.md, inter-workgroup visibility).
+// line leaves the XCD's L2), so no release fence has to write back the L2
+// full of this launch's activations, and read back by the last arriver
+// behind an agent-scope acquire (`acquire_partials`): MI355X_MICROARCH.md's
+// consumer form for any placement of the workgroups (the `sc1`-loads-only
+// form is measured for one workgroup a CU, and two of these 1024-thread
+// workgroups fit a CU beside other streams' kernels).
 __device__ __forceinline__ void st_wt(float* p, float v) {
   __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -71,6 +74,32 @@ __device__ bool last_arrival(unsigned int* counter) {
   }
   __syncthreads();
   return last;
+}
+
+// the last arriver, before its first load of another workgroup's partials:
+// one wave invalidates the CU's L1 (agent acquire) and waits for it, the
+// barrier holds every wave until then
+__device__ __forceinline__ void acquire_partials() {
+  if (threadIdx.x < 64) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __syncthreads();
+}
+
+__device__ __forceinline__ bool finitef(float x) { return fabsf(x) <= 3.402823466e38f; }
+
+// one lane of each wave that saw a non-finite value (`bad`) reports it:
+// guard[0] |= 1 << bit, guard[1] += 1, guard[3 + bit] = min(., tick)
+__device__ __forceinline__ void guard_raise(int32_t* guard, int bit, bool bad) {
+  if (!guard || bit < 0) return;
+  const unsigned long long b = __ballot(bad);
+  if (b == 0) return;
+  if ((int)(threadIdx.x & 63) == __ffsll((long long)b) - 1) {
+    atomicOr(&guard[0], 1 << bit);
+    atomicAdd(&guard[1], 1);
+    atomicMin(&guard[3 + bit], guard[2]);
+  }
 }
 
 __device__ __forceinline__ float4 ld4(const float* p, int64_t q) {
@@ -98,7 +127,7 @@ bn_stats_kernel(int64_t m, const float* __restrict__ z, const float* __restrict_
                 float eps, float momentum, float* __restrict__ running_mean,
                 float* __restrict__ running_var, int64_t* __restrict__ nbt, int updates,
                 float* __restrict__ a, float* __restrict__ mean_invstd,
-                float* __restrict__ work) {
+                float* __restrict__ work, int32_t* __restrict__ guard) {
   __shared__ float red[kSlots][C][3];
   const int tid = threadIdx.x, cg = tid & 7, slot = tid >> 3;
   const float4 b = ld4(bias, cg);
@@ -146,6 +175,7 @@ bn_stats_kernel(int64_t m, const float* __restrict__ z, const float* __restrict_
   }
   unsigned int* counters = reinterpret_cast<unsigned int*>(work + (size_t)kMaxGrid * C * 3);
   if (!last_arrival(&counters[0])) return;
+  acquire_partials();
   // the last workgroup: kFin threads a channel over the partials, then one
   {
     const int ch = tid & (C - 1), j = tid / C;
@@ -160,6 +190,13 @@ bn_stats_kernel(int64_t m, const float* __restrict__ z, const float* __restrict_
       pm[k] = ld_wt(p + 1);
       pq[k] = ld_wt(p + 2);
     }
+    // counts back to zero: a partial the next launch fails to deliver (or
+    // that is read stale) then shows as a missing count below
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int g = j + k * kFin;
+      if (g < (int)gridDim.x) st_wt(part + ((size_t)g * C + ch) * 3, 0.0f);
+    }
 #pragma unroll
     for (int k = 0; k < kPer; ++k) chan(cn, cm, cm2, pn[k], pm[k], pq[k]);
     red2[j][ch][0] = cn;
@@ -171,8 +208,14 @@ bn_stats_kernel(int64_t m, const float* __restrict__ z, const float* __restrict_
     float cn = 0.0f, cm = 0.0f, cm2 = 0.0f;
     for (int s = 0; s < kFin; ++s) chan(cn, cm, cm2, red2[s][tid][0], red2[s][tid][1], red2[s][tid][2]);
     const float var = cm2 / cn;                       // biased: the normalisation
+    const float invstd = 1.0f / sqrtf(var + eps);
     mean_invstd[tid] = cm;
-    mean_invstd[C + tid] = 1.0f / sqrtf(var + eps);
+    mean_invstd[C + tid] = invstd;
+    // the merged count is every pixel exactly (float integers up to 2^24)
+    const bool lost = m < (int64_t(1) << 24) ? cn != (float)m
+                                              : fabsf(cn - (float)m) > 1e-6f * (float)m;
+    guard_raise(guard, DT_GUARD_BN_COUNT, lost);
+    guard_raise(guard, DT_GUARD_BN_FWD, !finitef(cm) || !finitef(invstd));
     const float unbiased = cn > 1.0f ? cm2 / (cn - 1.0f) : var;
     // one running-statistics update per reference forward over this batch
     // (the same batch statistics each time: a shared trunk, trainer.py)
@@ -239,7 +282,8 @@ __device__ void block_sums(float (&acc)[kN][4], float* __restrict__ part) {
 
 // the last workgroup: per-channel totals of the kN partial columns -> out[j][C]
 template <int kN>
-__device__ void final_sums(const float* __restrict__ part, float* const (&out)[kN]) {
+__device__ void final_sums(const float* __restrict__ part, float* const (&out)[kN],
+                           int32_t* __restrict__ guard) {
   __shared__ float red[kFin][C][kN];
   const int tid = threadIdx.x, ch = tid & (C - 1), q = tid / C;
   float s[kN];
@@ -262,12 +306,15 @@ __device__ void final_sums(const float* __restrict__ part, float* const (&out)[k
   for (int j = 0; j < kN; ++j) red[q][ch][j] = s[j];
   __syncthreads();
   if (tid < C) {
+    bool bad = false;
 #pragma unroll
     for (int j = 0; j < kN; ++j) {
       float t = 0.0f;
       for (int k = 0; k < kFin; ++k) t += red[k][tid][j];
       out[j][tid] = t;
+      bad = bad || !finitef(t);
     }
+    guard_raise(guard, DT_GUARD_BN_BWD, bad);
   }
 }
 
@@ -276,7 +323,8 @@ __global__ void __launch_bounds__(kT)
 bn_bwd_reduce_kernel(int64_t m, const float* __restrict__ dy, const float* __restrict__ z,
                      const float* __restrict__ bias, float slope,
                      const float* __restrict__ mean_invstd, float* __restrict__ dgamma,
-                     float* __restrict__ dbeta, float* __restrict__ work) {
+                     float* __restrict__ dbeta, float* __restrict__ work,
+                     int32_t* __restrict__ guard) {
   const int cg = threadIdx.x & 7;
   const float4 b = ld4(bias, cg);
   const float4 mu = ld4(mean_invstd, cg), is = ld4(mean_invstd + C, cg);
@@ -297,8 +345,9 @@ bn_bwd_reduce_kernel(int64_t m, const float* __restrict__ dy, const float* __res
   block_sums<2>(acc, work);
   unsigned int* counters = reinterpret_cast<unsigned int*>(work + (size_t)kMaxGrid * C * 3);
   if (!last_arrival(&counters[1])) return;
+  acquire_partials();
   float* const out[2] = {dbeta, dgamma};
-  final_sums<2>(work, out);
+  final_sums<2>(work, out, guard);
 }
 
 // ---- backward 2: dz, and dbias = sum(dz) ----------------------------------------------
@@ -307,7 +356,8 @@ bn_bwd_apply_kernel(int64_t m, const float* __restrict__ dy, const float* __rest
                     const float* __restrict__ bias,
                     const float* __restrict__ mean_invstd, const float* __restrict__ gamma,
                     const float* __restrict__ dgamma, const float* __restrict__ dbeta, float slope,
-                    float* __restrict__ dz, float* __restrict__ dbias, float* __restrict__ work) {
+                    float* __restrict__ dz, float* __restrict__ dbias, float* __restrict__ work,
+                    int32_t* __restrict__ guard) {
   const int cg = threadIdx.x & 7;
   const float inv_m = 1.0f / (float)m;
   float mu[4], is[4], k1[4], k2[4], k3[4];
@@ -342,8 +392,9 @@ bn_bwd_apply_kernel(int64_t m, const float* __restrict__ dy, const float* __rest
   block_sums<1>(acc, part);
   unsigned int* counters = reinterpret_cast<unsigned int*>(work + (size_t)kMaxGrid * C * 3);
   if (!last_arrival(&counters[2])) return;
+  acquire_partials();
   float* const out[1] = {dbias};
-  final_sums<1>(part, out);
+  final_sums<1>(part, out, guard);
 }
 
 // ---- multi-tensor Adam and soft update -------------------------------------------------
@@ -352,7 +403,8 @@ constexpr int kMtThreads = 256;
 __global__ void __launch_bounds__(kMtThreads)
 adam_kernel(const dt_mt_tensor* __restrict__ tensors, const int32_t* __restrict__ chunks,
             double* __restrict__ step, const double* __restrict__ lr, double beta1, double beta2,
-            double eps, unsigned int* __restrict__ counter) {
+            double eps, unsigned int* __restrict__ counter, int32_t* __restrict__ guard,
+            int grad_bit, int param_bit) {
   const dt_mt_tensor t = tensors[chunks[2 * blockIdx.x]];
   const int64_t start = (int64_t)chunks[2 * blockIdx.x + 1] * DT_MT_CHUNK;
   const int64_t end = start + DT_MT_CHUNK < t.n ? start + DT_MT_CHUNK : t.n;
@@ -363,17 +415,23 @@ adam_kernel(const dt_mt_tensor* __restrict__ tensors, const int32_t* __restrict_
   const float bc2_sqrt = (float)sqrt(1.0 - pow(beta2, st));
   const float w = (float)(1.0 - beta1), b2 = (float)beta2, ob2 = (float)(1.0 - beta2);
   const float fe = (float)eps;
+  bool bad_g = false, bad_p = false;
   for (int64_t i = start + threadIdx.x; i < end; i += kMtThreads) {
     const float g = t.b[i];
+    bad_g = bad_g || !finitef(g);
     float m = t.c[i];
     m = w < 0.5f ? m + w * (g - m) : g - (g - m) * (1.0f - w);          // lerp
     float v = t.d[i] * b2;                                              // mul_
     v = v + ob2 * g * g;                                                // addcmul_
     const float den = sqrtf(v) / bc2_sqrt + fe;                         // sqrt, div_, add_
-    t.a[i] = t.a[i] + step_size * (m / den);                            // addcdiv_
+    const float p = t.a[i] + step_size * (m / den);                    // addcdiv_
+    bad_p = bad_p || !finitef(p);
+    t.a[i] = p;
     t.c[i] = m;
     t.d[i] = v;
   }
+  guard_raise(guard, grad_bit, bad_g);
+  guard_raise(guard, param_bit, bad_p);
   // the step count moves once every workgroup has read it
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -399,6 +457,36 @@ soft_update_kernel(const dt_mt_tensor* __restrict__ tensors, const int32_t* __re
   }
 }
 
+// ---- non-finite guard scan ------------------------------------------------------------
+struct GuardSet {
+  int n;
+  dt_guard_tensor t[DT_GUARD_MAX];
+};
+constexpr int kGuardThreads = 256;
+
+__global__ void __launch_bounds__(kGuardThreads)
+guard_scan_kernel(GuardSet set, int32_t* __restrict__ guard) {
+  const int64_t tid = (int64_t)blockIdx.x * kGuardThreads + threadIdx.x;
+  const int64_t stride = (int64_t)gridDim.x * kGuardThreads;
+  for (int k = 0; k < set.n; ++k) {
+    const dt_guard_tensor t = set.t[k];
+    bool bad = false;
+    if (t.dtype == 0) {
+      const float* p = static_cast<const float*>(t.p);
+      const int64_t n4 = ((uintptr_t)p & 15) == 0 ? t.count / 4 : 0;
+      for (int64_t i = tid; i < n4; i += stride) {
+        const float4 v = reinterpret_cast<const float4*>(p)[i];
+        bad = bad || !finitef(v.x) || !finitef(v.y) || !finitef(v.z) || !finitef(v.w);
+      }
+      for (int64_t i = 4 * n4 + tid; i < t.count; i += stride) bad = bad || !finitef(p[i]);
+    } else {
+      const double* p = static_cast<const double*>(t.p);
+      for (int64_t i = tid; i < t.count; i += stride) bad = bad || !(fabs(p[i]) <= 1.79769313486231570e308);
+    }
+    guard_raise(guard, t.bit, bad);
+  }
+}
+
 bool aligned16(const void* p) { return ((uintptr_t)p & 15) == 0; }
 
 }  // namespace
@@ -413,7 +501,7 @@ int64_t dt_train_work_floats(int64_t m) {
 int dt_bn_leaky_fwd(int64_t m, const float* z, const float* bias, float slope, const float* gamma,
                     const float* beta, float eps, float momentum, float* running_mean,
                     float* running_var, int64_t* num_batches_tracked, int32_t updates, float* a,
-                    float* y, float* mean_invstd, float* work, void* stream) {
+                    float* y, float* mean_invstd, float* work, int32_t* guard, void* stream) {
   if (updates < 1) return DT_E_ARG;
   if (m < 1 || !z || !bias || !gamma || !beta || !running_mean || !running_var || !y ||
       !mean_invstd || !work)
@@ -424,7 +512,8 @@ int dt_bn_leaky_fwd(int64_t m, const float* z, const float* bias, float slope, c
   const int g = grid_of(m);
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(bn_stats_kernel, dim3(g), dim3(kT), 0, s, m, z, bias, slope, eps, momentum,
-                     running_mean, running_var, num_batches_tracked, (int)updates, a, mean_invstd, work);
+                     running_mean, running_var, num_batches_tracked, (int)updates, a, mean_invstd, work,
+                     guard);
   hipLaunchKernelGGL(bn_apply_kernel, dim3(g), dim3(kT), 0, s, m, z, bias, slope, mean_invstd,
                      gamma, beta, y);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
@@ -432,7 +521,8 @@ int dt_bn_leaky_fwd(int64_t m, const float* z, const float* bias, float slope, c
 
 int dt_bn_leaky_bwd(int64_t m, const float* dy, const float* z, const float* bias,
                     const float* mean_invstd, const float* gamma, float slope, float* dz,
-                    float* dbias, float* dgamma, float* dbeta, float* work, void* stream) {
+                    float* dbias, float* dgamma, float* dbeta, float* work, int32_t* guard,
+                    void* stream) {
   if (m < 1 || !dy || !z || !bias || !mean_invstd || !gamma || !dz || !dbias || !dgamma ||
       !dbeta || !work)
     return DT_E_ARG;
@@ -442,20 +532,21 @@ int dt_bn_leaky_bwd(int64_t m, const float* dy, const float* z, const float* bia
   const int g = grid_of(m);
   hipStream_t s = (hipStream_t)stream;
   hipLaunchKernelGGL(bn_bwd_reduce_kernel, dim3(g), dim3(kT), 0, s, m, dy, z, bias, slope,
-                     mean_invstd, dgamma, dbeta, work);
+                     mean_invstd, dgamma, dbeta, work, guard);
   hipLaunchKernelGGL(bn_bwd_apply_kernel, dim3(g), dim3(kT), 0, s, m, dy, z, bias, mean_invstd,
-                     gamma, dgamma, dbeta, slope, dz, dbias, work);
+                     gamma, dgamma, dbeta, slope, dz, dbias, work, guard);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 
 int dt_adam(int32_t n_chunks, const dt_mt_tensor* tensors, const int32_t* chunks, double* step,
             const double* lr, double beta1, double beta2, double eps, uint32_t* counter,
-            void* stream) {
+            int32_t* guard, int32_t grad_bit, int32_t param_bit, void* stream) {
   if (n_chunks < 0 || (n_chunks > 0 && (!tensors || !chunks || !step || !lr || !counter)))
     return DT_E_ARG;
   if (n_chunks == 0) return DT_OK;
   hipLaunchKernelGGL(adam_kernel, dim3(n_chunks), dim3(kMtThreads), 0, (hipStream_t)stream,
-                     tensors, chunks, step, lr, beta1, beta2, eps, counter);
+                     tensors, chunks, step, lr, beta1, beta2, eps, counter, guard, (int)grad_bit,
+                     (int)param_bit);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 
@@ -466,6 +557,27 @@ int dt_soft_update(int32_t n_chunks, const dt_mt_tensor* tensors, const int32_t*
   // torch: target * (1.0 - tau) + param * tau with the Python doubles as float32 scalars
   hipLaunchKernelGGL(soft_update_kernel, dim3(n_chunks), dim3(kMtThreads), 0, (hipStream_t)stream,
                      tensors, chunks, (float)(1.0 - tau), (float)tau);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
+int dt_guard_scan(int32_t n, const dt_guard_tensor* tensors, int32_t* guard, void* stream) {
+  if (n < 0 || n > DT_GUARD_MAX || !guard || (n > 0 && !tensors)) return DT_E_ARG;
+  GuardSet set{};
+  set.n = n;
+  int64_t most = 0;
+  for (int k = 0; k < n; ++k) {
+    const dt_guard_tensor& t = tensors[k];
+    if (t.count < 0 || (t.count > 0 && !t.p) || t.bit < 0 || t.bit > 31 || t.dtype < 0 ||
+        t.dtype > 1)
+      return DT_E_ARG;
+    set.t[k] = t;
+    most = t.count > most ? t.count : most;
+  }
+  if (most == 0) return DT_OK;
+  int64_t g = (most / 4 + kGuardThreads * 4 - 1) / (kGuardThreads * 4);
+  g = g < 1 ? 1 : (g > 1024 ? 1024 : g);
+  hipLaunchKernelGGL(guard_scan_kernel, dim3((unsigned)g), dim3(kGuardThreads), 0,
+                     (hipStream_t)stream, set, guard);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 

@@ -122,6 +122,36 @@ class DeviceAdam(torch.optim.Adam):
                 st['exp_avg'] = torch.zeros_like(p, memory_format=torch.preserve_format)
                 st['exp_avg_sq'] = torch.zeros_like(p, memory_format=torch.preserve_format)
         self._table = None
+        self.guard, self.grad_bit, self.param_bit = None, -1, -1
+
+    def set_guard(self, guard, grad_stage, param_stage):
+        """Report non-finite gradients / updated parameters into `guard`
+        (aido1_amd/guard.py): inside dt_adam, or by scans around torch's step
+        when it falls back."""
+        from aido1_amd.guard import BIT
+        self.guard, self.grad_bit, self.param_bit = guard, BIT[grad_stage], BIT[param_stage]
+
+    def load_state_dict(self, state_dict):
+        """Adam's, then the one shared float64 step tensor again (torch restores
+        a float32 step per parameter, which would send every later step down
+        the torch fallback) and the moments in their parameter's memory format
+        (the dt_adam table needs equal strides)."""
+        super().load_state_dict(state_dict)
+        step = None
+        for group in self.param_groups:
+            for p in group['params']:
+                st = self.state[p]
+                if 'step' in st and step is None:
+                    step = st['step']
+                for k in ('exp_avg', 'exp_avg_sq'):
+                    if k in st and st[k].stride() != p.stride():
+                        st[k] = torch.empty_like(p).copy_(st[k])
+        if step is not None:
+            self._step_t.copy_(torch.as_tensor(step, dtype=torch.float64))
+        for group in self.param_groups:
+            for p in group['params']:
+                self.state[p]['step'] = self._step_t
+        self._table = None
 
     def _rows(self):
         rows = []
@@ -145,7 +175,12 @@ class DeviceAdam(torch.optim.Adam):
                     st = self.state[p]
                     if st.get('step') is self._step_t:
                         st['step'] = self._step_t.clone()
-            return super().step(closure)
+            if self.guard is not None:
+                self.guard.scan(self.grad_bit, *[r[1] for r in rows])
+            out = super().step(closure)
+            if self.guard is not None:
+                self.guard.scan(self.param_bit, *[r[0] for r in rows])
+            return out
         if self._table is None or self._table.key != MultiTensorTable.key_of(rows):
             self._table = MultiTensorTable(rows, self._step_t.device)
         from aido1_amd import _lib
@@ -154,6 +189,8 @@ class DeviceAdam(torch.optim.Adam):
         rc = _lib.lib().dt_adam(t.n_chunks, t.tensors.data_ptr(), t.chunks.data_ptr(),
                                 self._step_t.data_ptr(), g['lr'].data_ptr(), float(b1), float(b2),
                                 float(g['eps']), self._counter.data_ptr(),
+                                self.guard.ptr() if self.guard is not None else None,
+                                self.grad_bit, self.param_bit,
                                 ctypes.c_void_p(torch.cuda.current_stream(self._step_t.device)
                                                 .cuda_stream))
         if rc != 0:

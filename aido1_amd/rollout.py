@@ -56,8 +56,9 @@ class CycleEpsilon:
 class ActorRollout:
     def __init__(self, config, n_envs=4096, maps=('small_loop', 'zigzag'), device=0, seed=1234,
                  env_id_base=0, actor=None, dtype=torch.float16, masks=True,
-                 actor_mode='reference', fused_explore=True, n_exploit=None):
+                 actor_mode='reference', fused_explore=True, n_exploit=None, guard=None):
         self.config = config
+        self.guard = guard      # non-finite guard (guard.py): actor outputs, rewards
         self.device = torch.device('cuda', device)
         self.n = n_envs
         k = len(maps)
@@ -184,6 +185,8 @@ class ActorRollout:
                                           out=self.actor_out)
         if timing is not None:
             timing[1].record()
+        if self.guard is not None:   # before DDPG.act's clip, which would hide a NaN
+            self.guard.scan('actor_out', out)
         if self.fx is not None:
             self.fx(out, self.episode, self.actions, generator=self.gen)
         else:
@@ -196,6 +199,8 @@ class ActorRollout:
             else:
                 self.actions[ne:] = act(out[ne:], None, self.head)
         self._step_envs()
+        if self.guard is not None:
+            self.guard.scan('env', self.reward, self.reward_mod)
         if self.fx is not None:   # tanh map, OU reset and episode count in one kernel
             self.fx.done(self.done, self.episode, self.actions)
             return self.reward, self.reward_mod, self.done

@@ -40,6 +40,7 @@ because notdone = 0 removes Q(s') from its target.
 import torch
 
 from aido1_amd.actor import ConfigActor, ConfigCritic
+from aido1_amd.guard import Guard
 from aido1_amd.replay import PrioritizedReplayBuffer, ReplayBuffer
 from aido1_amd.rollout import ActorRollout
 from aido1_amd.trainer import DDPGTrainer
@@ -63,11 +64,14 @@ class TrainLoop:
         torch.manual_seed(seed)                         # identical init on every rank
         actor = ConfigActor(config['model']['actor'])
         critic = ConfigCritic(config['model']['critic'])
-        self.trainer = DDPGTrainer(config, actor, critic, device=self.device, graph=graph)
+        # one non-finite guard for every stage of the loop (guard.py, check())
+        self.guard = Guard(self.device)
+        self.trainer = DDPGTrainer(config, actor, critic, device=self.device, graph=graph,
+                                   guard=self.guard)
         self.rollout = ActorRollout(config, n_envs, maps=maps, device=device, seed=seed,
                                     env_id_base=env_id_base, actor=self.trainer.actor,
                                     dtype=actor_dtype, masks=masks, actor_mode=actor_mode,
-                                    n_exploit=n_exploit)
+                                    n_exploit=n_exploit, guard=self.guard)
         self.rollout.load_exploit_actor(self.trainer.target_actor)
         size = int(buffer_size or t['buffer_size'])
         gen = torch.Generator(device=self.device)
@@ -130,6 +134,19 @@ class TrainLoop:
             if self.refresh_due:
                 self._refresh()
                 self.refresh_due = False
+
+    def check(self):
+        """Synchronise and raise if anything went wrong since the last check:
+        guard.NonFiniteError naming the first stages that produced NaN / Inf
+        (rollout actor outputs, rewards, the sampled batch, each stage of the
+        update, the TD errors), or the replay's rejected priorities
+        (update_priorities' asserts, counted on the device).  Returns the
+        guard's record."""
+        self.flush()
+        r = self.guard.check('training loop')
+        if self.prioritized:
+            self.replay.check()
+        return r
 
     def _refresh(self):
         self.rollout.load_actor(self.trainer.actor)

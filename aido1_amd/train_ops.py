@@ -37,7 +37,8 @@ def applicable(x, conv, act, bn):
 
 def _work(bn, key, dev):
     """A scratch buffer per BatchNorm and direction, zeroed once (the kernels
-    leave their counters at zero): plain attributes, not state."""
+    leave their counters and partial counts at zero): plain attributes, not
+    state."""
     name = '_dt_work_' + key
     w = getattr(bn, name, None)
     if w is None or w.device != dev:
@@ -48,6 +49,19 @@ def _work(bn, key, dev):
 
 def _stream(dev):
     return ctypes.c_void_p(torch.cuda.current_stream(dev).cuda_stream)
+
+
+def _guard(bn):
+    """The guard block the trainer attached (aido1_amd/guard.py), or NULL."""
+    g = getattr(bn, '_dt_guard', None)
+    return g.ptr() if g is not None else None
+
+
+def attach_guard(module, guard):
+    """Report every fused BatchNorm of `module` into `guard` (DT_GUARD_BN_*)."""
+    for m in module.modules():
+        if isinstance(m, nn.BatchNorm2d):
+            m._dt_guard = guard
 
 
 class _BnLeaky(torch.autograd.Function):
@@ -64,7 +78,7 @@ class _BnLeaky(torch.autograd.Function):
                                nbt.data_ptr() if nbt is not None else None,
                                int(getattr(bn, '_dt_updates', 1)), None,
                                y.data_ptr(), mi.data_ptr(), _work(bn, 'fwd', z.device).data_ptr(),
-                               _stream(z.device))
+                               _guard(bn), _stream(z.device))
         if rc != 0:
             raise _lib.DtError('dt_bn_leaky_fwd failed (%d)' % rc)
         # the activation is recomputed from z and bias in the backward (never stored)
@@ -82,7 +96,8 @@ class _BnLeaky(torch.autograd.Function):
         rc = L.dt_bn_leaky_bwd(z.numel() // C, dy.data_ptr(), z.data_ptr(), bias.data_ptr(),
                                mi.data_ptr(), gamma.data_ptr(), ctx.slope, dz.data_ptr(),
                                g[0].data_ptr(), g[1].data_ptr(), g[2].data_ptr(),
-                               _work(ctx.bn, 'bwd', z.device).data_ptr(), _stream(z.device))
+                               _work(ctx.bn, 'bwd', z.device).data_ptr(), _guard(ctx.bn),
+                               _stream(z.device))
         if rc != 0:
             raise _lib.DtError('dt_bn_leaky_bwd failed (%d)' % rc)
         return dz, g[0], g[1], g[2], None, None

@@ -46,7 +46,8 @@ import torch.nn.functional as F
 
 from aido1_amd.distributed import GradAllReduce, world
 from aido1_amd.explore import create_decay_fn
-from aido1_amd.optim import SoftUpdate, make_optimizer
+from aido1_amd.guard import Guard
+from aido1_amd.optim import DeviceAdam, SoftUpdate, make_optimizer
 
 
 class TrainingDecay:
@@ -92,7 +93,7 @@ def _nullctx():
 class DDPGTrainer:
     def __init__(self, config, actor, critic, target_actor=None, target_critic=None,
                  device=None, sync_grads=None, bucket_mb=16, graph=False, warmup=3,
-                 conv_search=True):
+                 conv_search=True, guard=None):
         t = config['training']
         self.config = config
         self.gamma, self.tau = float(t['gamma']), float(t['tau'])
@@ -117,6 +118,17 @@ class DDPGTrainer:
                                           self.device)
         self.critic_optim = make_optimizer(t['optimizer'], self.critic.parameters(), self.graph,
                                            self.device)
+        # non-finite guards (guard.py): every stage reports into one device
+        # block, read only by check()
+        self.guard = guard if guard is not None else Guard(self.device)
+        if self.device.type == 'cuda':
+            from aido1_amd import train_ops
+            for m in (self.actor, self.critic, self.target_actor, self.target_critic):
+                train_ops.attach_guard(m, self.guard)
+        for opt, stages in ((self.actor_optim, ('actor_grad', 'actor_param')),
+                            (self.critic_optim, ('critic_grad', 'critic_param'))):
+            if isinstance(opt, DeviceAdam):
+                opt.set_guard(self.guard, *stages)
         self.warmup = warmup
         self.conv_search = bool(conv_search)
         self._graphs = None
@@ -184,8 +196,26 @@ class DDPGTrainer:
             for t in tensors:
                 t.record_stream(cur)
 
+    def _opt_step(self, opt, module, grad_stage, param_stage):
+        """opt.step() with its gradients and results guarded: DeviceAdam reports
+        from inside dt_adam, any other optimiser is scanned around."""
+        if isinstance(opt, DeviceAdam):
+            opt.step()
+            return
+        params = [p for p in module.parameters() if p.grad is not None]
+        self.guard.scan(grad_stage, *[p.grad for p in params])
+        opt.step()
+        self.guard.scan(param_stage, *[p.data for p in params])
+
+    def check(self):
+        """Raise guard.NonFiniteError naming the stages of the updates since the
+        last check that produced NaN / Inf (synchronises)."""
+        return self.guard.check('DDPG update')
+
     def _stage_critic(self):
         x = self._in
+        self.guard.tick()
+        self.guard.scan('batch', x['obs'], x['act'], x['rew'], x['nxt'])
         # the targets' forward (target actor -> target critic on next_obs) and
         # the critic's forward on obs are independent: two streams, so their
         # batch-64 kernels (a few CUs each) run side by side -- in a HIP graph
@@ -196,6 +226,7 @@ class DDPGTrainer:
                 next_actions = self.target_actor(x['nxt'])
                 next_v = self.target_critic(x['nxt'], next_actions)
                 self._y = x['rew'] + x['notdone'] * self.gamma * next_v
+                self.guard.scan('target', self._y)
         y_predicted = self.critic(x['obs'], x['act'])
         self._join(side, self._y)
         if self.critic_loss_kind == 'mse_loss':
@@ -204,6 +235,7 @@ class DDPGTrainer:
             critic_loss = F.smooth_l1_loss(y_predicted, self._y)
         self._grads(critic_loss, self.critic)
         self._critic_loss = critic_loss.detach()
+        self.guard.scan('critic_loss', self._critic_loss)
 
     def _shared_trunk(self):
         """Share the critic's conv trunk between the actor-loss forward and the
@@ -220,7 +252,7 @@ class DDPGTrainer:
 
     def _stage_actor(self):
         x = self._in
-        self.critic_optim.step()
+        self._opt_step(self.critic_optim, self.critic, 'critic_grad', 'critic_param')
         pred_actions = self.actor(x['obs'])
         if self._shared_trunk():
             from aido1_amd import train_ops
@@ -232,6 +264,7 @@ class DDPGTrainer:
         actor_loss = -1.0 * torch.mean(q)
         self._grads(actor_loss, self.actor)
         self._actor_loss = actor_loss.detach()
+        self.guard.scan('actor_loss', self._actor_loss)
 
     def _stage_targets(self):
         x = self._in
@@ -245,7 +278,8 @@ class DDPGTrainer:
                 else:
                     q = self.critic(x['obs'], x['act'])
                 self._td = self._y - q
-        self.actor_optim.step()
+                self.guard.scan('td', self._td)
+        self._opt_step(self.actor_optim, self.actor, 'actor_grad', 'actor_param')
         soft_update(self.target_actor, self.actor, self.tau)       # trainers.py:215-216
         soft_update(self.target_critic, self.critic, self.tau)
         self._join(side, self._td)

@@ -56,8 +56,8 @@ int dt_per_sample(dt_per* h, int32_t batch, const double* u_dev, double beta, in
 /* update_priorities(idx, priorities) — buffers.py:237-259: leaf = p**alpha
  * (the last occurrence of a duplicated index wins, as the sequential loop),
  * max_priority = max(max_priority, p).  Entries the reference would reject
- * (p <= 0 or NaN, idx outside [0, len)) are skipped and flagged for
- * dt_per_check. */
+ * (p <= 0 or NaN, idx outside [0, len)) are skipped, flagged and counted
+ * for dt_per_check. */
 int dt_per_update(dt_per* h, int32_t n, const int64_t* idx_dev, const double* priorities_dev,
                   void* stream);
 
@@ -67,7 +67,8 @@ int dt_per_read(dt_per* h, double* sum_dev, double* min_dev, double* max_priorit
                 void* stream);
 
 /* Synchronises; DT_E_ARG if an update since the last check held an entry the
- * reference's asserts reject (message in dt_per_last_error). */
+ * reference's asserts reject (message in dt_per_last_error: the kinds and how
+ * many entries were skipped). */
 int dt_per_check(dt_per* h);
 
 /* dt_frame_add: one decision of the frame store behind

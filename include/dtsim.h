@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DT_ABI_VERSION 7  /* 2: curves per tile vary (curve_start), intersections;
+#define DT_ABI_VERSION 8  /* 2: curves per tile vary (curve_start), intersections;
                              3: static objects in dt_map, safety_rad_mult;
                              4: dt_render_io.pose / list_cap, dt_copy_pose,
                                 dt_step_many pose output;
@@ -39,7 +39,9 @@ extern "C" {
                                 (two weight sets in one launch);
                              7: dt_line_detect_ws / dt_hough_lines_ws and
                                 their workspace queries (any image size),
-                                dt_hough_lines count -2 (max_lines reached) */
+                                dt_hough_lines count -2 (max_lines reached);
+                             8: dttrain.h non-finite guards: dt_guard_scan, a
+                                guard word for dt_bn_leaky_fwd / _bwd / dt_adam */
 
 /* error codes */
 #define DT_OK 0

@@ -53,7 +53,12 @@ def _worker(rank, ws, port, q):
             tr.update(_batch(rank))
         torch.cuda.synchronize()
         assert tr._graphs is not None and len(tr._graphs) == 3
-        q.put((rank, _flat(tr).numpy()))
+        try:
+            tr.check()          # names the first stage that produced NaN / Inf
+            q.put((rank, _flat(tr).numpy()))
+        except Exception as e:  # noqa: BLE001 -- reported by the parent
+            q.put((rank, 'rank %d: %s' % (rank, e)))
+            raise
     finally:
         dist.destroy_process_group()
 
@@ -67,6 +72,8 @@ def test_two_rank_update_replicas_identical(gpu):
     for p in procs:
         p.start()
     res = dict(q.get(timeout=240) for _ in range(ws))
+    errs = [v for v in res.values() if isinstance(v, str)]
+    assert not errs, errs
     for p in procs:
         p.join(timeout=60)
         assert p.exitcode == 0

@@ -105,8 +105,13 @@ def test_per_rejects_like_reference_asserts(gpu):
     rb.update_priorities([7], [0.5])                   # idx >= len: buffers.py:255
     with pytest.raises(DtError, match='index'):
         rb.check()
+    rb.update_priorities([0, 3, 2], [float('nan'), 0.25, 0.0])   # NaN: counted, not dropped
+    with pytest.raises(DtError, match='2 offending entries'):
+        rb.check()
+    rb.check()                                         # cleared
     st, _, _ = rb.trees()
-    assert st[16 + 1].item() == pytest.approx(0.5 ** 0.6, rel=1e-15)   # valid entry applied
+    assert st[16 + 1].item() == pytest.approx(0.5 ** 0.6, rel=1e-15)   # valid entries applied
+    assert st[16 + 3].item() == pytest.approx(0.25 ** 0.6, rel=1e-15)
     one = PrioritizedReplayBuffer(16, 0.6, device=gpu)
     one.add_batch(*_payload([0], gpu))
     with pytest.raises(DtError, match='at least 2'):

@@ -39,12 +39,21 @@ def test_train_loop_runs(gpu, prioritized, graph, size):
     loop.reset()
     for _ in range(12):
         loop.step()
-    torch.cuda.synchronize()
+    # the guards name the first stage that produced NaN / Inf (and the
+    # replay's rejected priorities), before any assertion on the results
+    rec = loop.check()
+    assert rec['tick'] == 12
     assert len(loop.replay) == size and loop.updates == 12 and loop.decisions == 12
     assert torch.isfinite(loop.metrics['critic_loss']) and torch.isfinite(loop.metrics['actor_loss'])
     w1 = loop.trainer.actor.net.input_nets[0].internal_modules[0].kernel.weight
     assert not torch.equal(w0, w1)
-    assert not torch.equal(t0, loop.rollout.actor.w[1])      # acting copy follows the target
+    # the exploring envs act with the online actor, the exploiters with the
+    # target actor (train_loop._refresh)
+    assert not torch.equal(t0, loop.rollout.actor.w[1])
+    for mine, src in ((loop.rollout.actor, loop.trainer.actor),
+                      (loop.rollout.exploit_actor, loop.trainer.target_actor)):
+        k = src.net.input_nets[0].internal_modules[0].kernel.weight
+        assert torch.equal(mine.w[0].float(), k.detach().to(mine.w[0].dtype).float())
     st = loop.replay.storage
     if size == 1024:
         obs, act, rew, nxt, done = loop.replay._encode_sample(torch.arange(size, device=gpu))
