@@ -1355,6 +1355,12 @@ int dt_step_many(dt_handle* h, int32_t k, const float* actions, double* reward,
     h->err = "dt_step_many: k >= 1, actions, reward, reward_mod and done are required";
     return DT_E_ARG;
   }
+  // step_fan_kernel indexes one launch's outputs with 32-bit offsets (pose:
+  // 3 doubles an env a decision, kFanMaxK decisions a launch)
+  if ((int64_t)3 * kFanMaxK * h->n >= (int64_t(1) << 31)) {
+    h->err = "dt_step_many: n too large for one handle (3 * 64 * n must stay below 2^31)";
+    return DT_E_ARG;
+  }
   DevGuard dg(h->device);
   hipStream_t s = (hipStream_t)stream;
   const int rb = h->sc.auto_reset ? refill_grid(h->n, kRefillEnvs) : 0;

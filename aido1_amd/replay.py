@@ -27,6 +27,7 @@ with the frame copy.  ``sample`` gathers the stacks through them, so it
 returns what the stacked storage returns.  Needs ``size % n == 0`` and
 float32 observations; only ``add_batch_ring`` adds to it.
 """
+import collections
 import ctypes
 
 import torch
@@ -58,7 +59,9 @@ class ReplayBuffer:
         self.frame_envs = int(frame_envs) if frame_envs else None
         self.frames = None          # frame store: [blocks * n, H, W] float32
         self._fblock = 0            # frame blocks written so far
-        self._begin_at = None       # decisions counter at the last stack begin
+        self._begun = False         # a chain of stacks has begun (first add_batch_ring)
+        self._stack_lo = 0          # oldest frame block (absolute) the current stacks reference
+        self._group_lo = collections.deque()   # the same for every live decision's rows
         self._decisions = 0
 
     def __len__(self):
@@ -176,21 +179,30 @@ class ReplayBuffer:
             self.storage = {
                 'obs_ptr': torch.zeros(self._maxsize, k, dtype=torch.int32, device=self.device),
                 'next_ptr': torch.zeros(self._maxsize, k, dtype=torch.int32, device=self.device)}
+        if obs_t is None and not self._begun:
+            raise ValueError('frame store: the first add_batch_ring needs obs_t')
+        # The blocks this add writes (k for a new chain, then the newest frame)
+        # overwrite the blocks `blocks` earlier; no live transition may still
+        # reference one of those.  Live: every stored decision's rows except
+        # the oldest one's when the buffer is full (this add overwrites them).
+        blocks = self.frames.shape[0] // n
+        live = list(self._group_lo)
+        if len(live) == self._maxsize // n:
+            live = live[1:]
+        last = self._fblock + (k if obs_t is not None else 0)      # absolute, inclusive
+        if live and last - blocks >= min(live):
+            raise ValueError('frame store: a new observation chain would overwrite frames that '
+                             'stored transitions still reference (chains begun too often: '
+                             'allow about size / n decisions between resets)')
         if obs_t is not None:
             # a new chain (the first add, or a rollout reset): obs_t's k frames
-            # become k frame blocks.  Live transitions reference at most
-            # size / n + k blocks, so one begin per size / n decisions is safe.
-            if (self._begin_at is not None and self._len == self._maxsize
-                    and self._decisions - self._begin_at < self._maxsize // n):
-                raise ValueError('frame store: a new observation chain within size / n '
-                                 'decisions of the previous one')
+            # become k frame blocks
             obs_t = torch.as_tensor(obs_t, device=self.device)
             ar = torch.arange(n, dtype=torch.int32, device=self.device)
+            self._stack_lo = self._fblock
             for j in range(k):
                 self._stack[:, j] = ar + self._frame_block(obs_t[:, j])
-            self._begin_at = self._decisions
-        elif self._begin_at is None:
-            raise ValueError('frame store: the first add_batch_ring needs obs_t')
+            self._begun = True
         p = self._next_idx
         self._reserve(n)
         st = self.storage
@@ -229,6 +241,13 @@ class ReplayBuffer:
             nxt[dn] = rows[dn, None]
             st['next_ptr'][p:p + n].copy_(nxt)
             self._stack.copy_(nxt)
+        # this decision's rows reference the stacks before the add (and the
+        # newest block); afterwards the stacks drop their oldest block (an env
+        # that respawned references only the newest: a later block)
+        self._group_lo.append(self._stack_lo)
+        if len(self._group_lo) > self._maxsize // n:
+            self._group_lo.popleft()
+        self._stack_lo = min(self._stack_lo + 1, self._fblock - 1) if k > 1 else self._fblock - 1
         self._decisions += 1
         self._advance(n)
         return None

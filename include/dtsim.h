@@ -207,7 +207,9 @@ int dt_step_masked(dt_handle* h, const uint8_t* mask, const float* actions, doub
  *   obs        device [k,n,2] f32, as dt_step's                            nullable
  *   pose       device [k,3,n] f64: the pose each decision ends in (x, z, angle
  *              planes; the reset pose after a respawn), i.e. what dt_render of
- *              that decision draws (dt_render_io.pose = pose + 3 n d)  nullable */
+ *              that decision draws (dt_render_io.pose = pose + 3 n d)  nullable
+ * DT_E_ARG for a handle with 3 * 64 * n >= 2^31 (one launch's 32-bit output
+ * offsets); step such a handle with dt_step. */
 int dt_step_many(dt_handle* h, int32_t k, const float* actions, double* reward,
                  double* reward_mod, uint8_t* done, float* obs, double* pose, void* stream);
 

@@ -138,3 +138,50 @@ def test_frame_store_rejects():
     with pytest.raises(ValueError):                            # the first add needs obs_t
         rb.add_batch_ring(None, torch.zeros(3, 2), torch.zeros(3), ring, [0, 1, 2],
                           torch.zeros(3, dtype=torch.bool))
+
+
+def _begin_steps(a, b, n, begins, g):
+    """As _frame_steps, but a new observation chain (a rollout reset: obs_t
+    given again, a fresh stack) at every decision in `begins`."""
+    ring = torch.rand(n, 3, 2, 4, generator=g)
+    obs_b = ring[:, [0, 1, 2]].clone()
+    for t in range(max(begins) + 4):
+        if t in begins:
+            ring = torch.rand(n, 3, 2, 4, generator=g)
+            obs_b = ring[:, [(t + k) % 3 for k in range(3)]].clone()
+        order = [(t + 1 + k) % 3 for k in range(3)]
+        new = torch.rand(n, 2, 4, generator=g)
+        ring[:, order[-1]] = new
+        done = torch.zeros(n, dtype=torch.bool)
+        act, rew = torch.rand(n, 2, generator=g), torch.rand(n, generator=g, dtype=torch.float64)
+        nxt = ring[:, order].clone()
+        b.add_batch(obs_b, act, rew, nxt, done)
+        a.add_batch_ring(obs_b if (t in begins or t == 0) else None, act, rew, ring, order, done)
+        obs_b = nxt
+        idx = torch.arange(len(b))
+        for x, y in zip(a._encode_sample(idx), b._encode_sample(idx)):
+            assert torch.equal(x, y), t
+
+
+@pytest.mark.parametrize('begins,raises_at', [
+    ((0, 1, 2), 2),          # 3 chains in 3 decisions, buffer not full: would wrap
+    ((0, 1), None),          # within the 2k spare blocks
+    ((0, 4, 8, 12), None),   # one chain per size / n decisions: always safe
+    ((0, 4, 5), 5),          # full buffer: the reset before still referenced
+    ((0, 2, 3), 3),
+])
+def test_frame_store_chain_begins_checked_against_live_frames(begins, raises_at):
+    """A new chain writes k frame blocks; the store refuses one that would
+    overwrite blocks that stored transitions still reference, whether or not
+    the buffer is full (size 12, n 3: 4 decisions, 4 + 2k = 10 blocks), and
+    every accepted pattern samples what the stacked storage holds."""
+    from aido1_amd.replay import ReplayBuffer
+    g = torch.Generator().manual_seed(3)
+    a = ReplayBuffer(12, device='cpu', frame_envs=3)
+    b = ReplayBuffer(12, device='cpu')
+    if raises_at is None:
+        _begin_steps(a, b, 3, begins, g)
+        return
+    with pytest.raises(ValueError, match='still reference'):
+        _begin_steps(a, b, 3, begins, g)
+    assert a._decisions == raises_at
