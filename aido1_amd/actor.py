@@ -11,11 +11,16 @@ Two layouts, parameter names identical to the reference so checkpoints
   is tanh on both outputs).
 
 Both compute conv -> LeakyReLU -> BatchNorm x4 -> flatten(4032) -> dropout ->
-linear(512) -> LeakyReLU -> linear(2) -> head.  On MI355X the batched forward
-runs in bf16 (MFMA through MIOpen/hipBLASLt) with the eval-mode BatchNorms
-folded into the following conv / linear, and reads the observation ring
-zero-copy: the first conv's input channels are permuted to the ring's slot
-order instead of gathering the Transformer stack.
+linear(512) -> LeakyReLU -> linear(2) -> head.  On MI355X the batched
+forward in the rollout is ``FusedActor``: the four convolutions are
+hand-written fp16 MFMA kernels (csrc/dtconv.hip, include/dtactor.h) that read
+the observation ring zero-copy (the first conv's input channels follow the
+ring's slot order instead of gathering the Transformer stack), with f32
+accumulation.  The default mode is 'reference': the reference explorers'
+train-mode batch-of-one BatchNorm (per-sample statistics, fused into the
+convolution kernels) and live dropout; 'eval' folds the eval-mode
+BatchNorms into the following conv / linear.  The linears run as torch fp16
+GEMMs (hipBLASLt) and the head in dt_actor_head.
 """
 import copy
 
@@ -414,7 +419,8 @@ class FusedActor(nn.Module):
 
     def _conv_buffers(self, n, dev):
         """The intermediate activations (fp16 NHWC) and, in reference mode, the
-        per-sample BatchNorm statistics [n, 32, 2] of conv1..conv3."""
+        per-sample BatchNorm statistics [n, 32, 3] of conv1..conv3 (mean of the
+        stored centred values, M2, centre: include/dtactor.h)."""
         key = (n, dev, self.mode)
         if getattr(self, '_bufs_key', None) != key:
             f16 = torch.float16
@@ -423,9 +429,9 @@ class FusedActor(nn.Module):
                 'y1': torch.empty(n, 57, 77, 32, dtype=f16, device=dev),
                 'y2': torch.empty(n, 27, 37, 32, dtype=f16, device=dev),
                 'y3': torch.empty(n, 12, 17, 32, dtype=f16, device=dev),
-                'p1': torch.empty(n, 32, 2, device=dev) if ref else None,
-                'p2': torch.empty(n, 32, 2, device=dev) if ref else None,
-                'p3': torch.empty(n, 32, 2, device=dev) if ref else None}
+                'p1': torch.empty(n, 32, 3, device=dev) if ref else None,
+                'p2': torch.empty(n, 32, 3, device=dev) if ref else None,
+                'p3': torch.empty(n, 32, 3, device=dev) if ref else None}
             self._bufs_key = key
         return self._bufs
 

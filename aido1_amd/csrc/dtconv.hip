@@ -83,6 +83,26 @@ __device__ __forceinline__ void store_px32(__half* sample, int px, const float (
   }
 }
 
+// Reference mode keeps each sample's activations CENTRED in fp16: the stored
+// value is v - c with c the sample's pixel-0 output of the channel, and the
+// statistics are those of the stored values (M2 does not change, the mean
+// moves by c), so the next layer's norm (x - mean) * invstd is unchanged.  A
+// channel that is nearly flat over a frame is divided by a tiny standard
+// deviation; stored uncentred its fp16 rounding (~2^-11 |v|) is amplified by
+// that 1 / std, centred the rounding is of |v - c| ~ the channel's own spread.
+// The sample's first step publishes c (wave 0, pixel 0 = lanes 0 and 32) and
+// a barrier makes it visible; later steps read it (rewritten only after the
+// step barrier that ends the sample).  `first` is workgroup-uniform.
+__device__ __forceinline__ void centre_px32(float (&v)[16], float* s_c, bool publish, bool first,
+                                            int h) {
+  if (publish)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) s_c[(r & 3) + 8 * (r >> 2) + 4 * h] = v[r];
+  if (first) __syncthreads();
+#pragma unroll
+  for (int r = 0; r < 16; ++r) v[r] -= s_c[(r & 3) + 8 * (r >> 2) + 4 * h];
+}
+
 // ---- two weight sets in one launch -----------------------------------------------
 // Samples [0, n0) use the launch's weights, [n0, n) a second set (the exploiting
 // explorers' actor): the persistent workgroups split in proportion, g0 for the
@@ -205,6 +225,7 @@ conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, 
   __shared__ __attribute__((aligned(16))) unsigned char rb[kSRing * kSRowB];
   __shared__ float red[kSW][CO][3];
   __shared__ float s_bias[CO];
+  __shared__ float s_c[CO];   // the sample's centre (kStats): its pixel-0 outputs
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 31, h = lane >> 5;
   const SplitPart sp = split_part(ws, n);
@@ -374,6 +395,7 @@ conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, 
     float v[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = lrelu2(acc[r], slope);
+    if (kStats) centre_px32(v, s_c, j == 0 && wave == 0 && col == 0, j == 0, h);
     if (!(DTCONV_SKIP & 4)) store_px32<kSPix>(y + (size_t)ns * kSPix * CO, pc, v, h, valid);
     if (kStats && !(DTCONV_SKIP & 8)) {
       if (valid) {   // Welford over this lane's pixels
@@ -420,9 +442,10 @@ conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, 
             m2 += red[w][tid][2] + d * d * (cnt * nb / tot);
             cnt = tot;
           }
-          float* pp = partials + ((size_t)ns * CO + tid) * 2;
+          float* pp = partials + ((size_t)ns * CO + tid) * 3;
           pp[0] = mean;
           pp[1] = m2;
+          pp[2] = s_c[tid];
         }
         w_cnt = 0.0f;
 #pragma unroll
@@ -466,7 +489,7 @@ conv1_norm_kernel(__half* __restrict__ y, const float* __restrict__ partials,
   __shared__ float sc[CO], sh[CO];
   const int n = blockIdx.x, tid = threadIdx.x;
   if (tid < CO) {
-    const float* pp = partials + ((size_t)n * CO + tid) * 2;
+    const float* pp = partials + ((size_t)n * CO + tid) * 3;
     const float var = pp[1] / (float)(OH * OW);
     const float s = gamma[tid] / sqrtf(var + eps);
     sc[tid] = s;
@@ -601,6 +624,7 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
   __shared__ float s_sc[3][CO], s_sh[3][CO];   // input norm of samples k % 3
   __shared__ float red[NW][CO][3];
   __shared__ float s_mean[CO], s_rstd[CO], s_bias[CO];
+  __shared__ float s_c[CO];   // the sample's centre (kOut 0): its pixel-0 outputs
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 31, h = lane >> 5;
   unsigned char* rb = reinterpret_cast<unsigned char*>(ring);
@@ -630,7 +654,7 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
     if (kIn == 1) {
       const int ns = sample(k) < send ? sample(k) : send - 1;
       const int c = tid & (CO - 1);
-      const float* pp = prev_part + ((size_t)ns * CO + c) * 2;
+      const float* pp = prev_part + ((size_t)ns * CO + c) * 3;
       st[0] = pp[0];
       st[1] = pp[1];
       gam = in_gamma[c];
@@ -752,6 +776,7 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
 
     // epilogue
     if (kOut <= 1) {
+      if (kOut == 0) centre_px32(v, s_c, j == 0 && wave == 0 && col == 0, j == 0, h);
       if (!(DTCONV_SKIP & 4)) store_px32<G::kPix>(y + (size_t)ns * G::kPix * CO, pc, v, h, valid);
       if (kOut == 0 && valid && !(DTCONV_SKIP & 8)) {   // Welford over this lane's pixels
         w_cnt += 1.0f;
@@ -798,9 +823,10 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
             m2 += red[w][tid][2] + d * d * (cnt * nb / tot);
             cnt = tot;
           }
-          float* pp = part + ((size_t)ns * CO + tid) * 2;
+          float* pp = part + ((size_t)ns * CO + tid) * 3;
           pp[0] = mean;
           pp[1] = m2;
+          pp[2] = s_c[tid];
         }
         w_cnt = 0.0f;
 #pragma unroll

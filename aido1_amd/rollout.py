@@ -93,7 +93,8 @@ class ActorRollout:
         if actor is None:
             actor = ConfigActor(config['model']['actor'])
         self.actor_mode = actor_mode
-        self.actor = FusedActor(actor.to(self.device), dtype=dtype, mode=actor_mode)
+        self.actor_src = actor.to(self.device)     # the module the acting copies derive from
+        self.actor = FusedActor(self.actor_src, dtype=dtype, mode=actor_mode)
         if n_exploit is None:
             t = config['training']
             n_xpl = t.get('num_threads_exploiting', 0) + t.get('num_threads_exploiting_virtual', 0)

@@ -109,6 +109,11 @@ def parse(argv=None):
     p.add_argument('--obs-mode', default='many', choices=['many', 'many2', 'serial', 'pipe'],
                    help='render: how the steps are launched (ObsLoop)')
     p.add_argument('--no-lane', action='store_true', help='render: skip the config-2 sub-record')
+    p.add_argument('--no-sub', action='store_true',
+                   help='render: skip the config-4 / config-5 sub-records')
+    p.add_argument('--sub-steps', type=int, default=20,
+                   help='timed decisions of the config-4 / config-5 sub-records')
+    p.add_argument('--sub-warmup', type=int, default=5)
     p.add_argument('--event-stride', type=int, default=4,
                    help='render: HIP events around every S-th dt_render of the timed region '
                         '(the roofline\'s average kernel duration is over those launches); '
@@ -586,6 +591,11 @@ def bench_obs(args, ctx):
     env.close()
     lane = None if args.no_lane else lane_record(args, ctx, args.lane_steps, args.lane_warmup,
                                                  cpu=True)
+    # configs 4 and 5 as sub-records of the same line (not the headline)
+    c4 = c5 = None
+    if not args.no_sub:
+        c4 = actor_record(args, ctx, args.sub_steps, args.sub_warmup, parity=not args.no_parity)
+        c5 = train_record(args, ctx, args.sub_steps, args.sub_warmup, parity=not args.no_parity)
     if rank == 0:
         kms = float(np.mean(rend_ms))
         fresh_per_launch = st['resets'] / K
@@ -644,6 +654,8 @@ def bench_obs(args, ctx):
             'step_launches': len(starts),
             'host_enqueue_ms_per_step': t_host / K * 1e3,
             'config2': lane,
+            'config4': c4,
+            'config5': c5,
         }
         line['cpu_baseline'] = (cpu_obs_baseline(args.cpu_decisions, args.cpu_procs, args.map)
                                 if ctx.world == 1 and args.cpu_steps > 0 else None)
@@ -878,10 +890,13 @@ def step_parity(env, start, actions, out, rank, args, frames=None, m=64):
 
 
 # ---- configs 4 and 5 -----------------------------------------------------------------------
-def bench_actor(args, ctx):
-    """BASELINE configs[3]: 4096 envs/GPU, mixed small_loop/zigzag, actor in the loop."""
+def actor_record(args, ctx, K, W, parity=True):
+    """BASELINE configs[3]: 4096 envs/GPU, mixed small_loop/zigzag, actor in the
+    loop (the explorers' loop body, training/explorers.py:164-213).  Returns
+    the line (rank 0) or None.  parity: the fp16 HIP chain against the f32 GPU
+    path on the live frame ring, every env, dropout off in both."""
     torch = ctx.torch
-    from aido1_amd.actor import flops_per_sample
+    from aido1_amd.actor import FusedActor, flops_per_sample
     from aido1_amd.rollout import ActorRollout
     with open(os.path.join(REPO, 'aido1_amd', 'configs', 'reference_config.json')) as f:
         cfg = json.load(f)
@@ -890,16 +905,16 @@ def bench_actor(args, ctx):
     roll = ActorRollout(cfg, n, maps=('small_loop', 'zigzag'), device=dev.index, seed=args.seed,
                         env_id_base=rank * n, actor_mode=args.actor_mode)
     roll.reset()
-    for _ in range(args.warmup):
+    for _ in range(W):
         roll.step()
     ctx.sync()
     roll.stats(reset=True)
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
+          for _ in range(K)]
     ctx.barrier()
     ctx.sync()
     t0 = time.perf_counter()
-    for k in range(args.steps):
+    for k in range(K):
         roll.step(timing=ev[k])
     ctx.sync()
     ctx.barrier()
@@ -907,38 +922,69 @@ def bench_actor(args, ctx):
     st = roll.stats()
     actor_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     tot, tmax, per = rank_report(ctx, [st['sim_steps'], st['decisions'], st['resets']], elapsed)
-    if rank == 0:
-        tflops = n * flops_per_sample() / (actor_ms * 1e-3) / 1e12
-        print(json.dumps({
-            'metric': METRIC, 'value': tot[0] / tmax, 'unit': 'env-steps/s',
-            'n_gpus': ctx.world, 'steps': args.steps, 'warmup': args.warmup,
-            'ms_per_step': tmax / args.steps * 1e3,
-            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
-            'dtype': 'f64 env / %s actor' % str(roll.actor.dtype).replace('torch.', ''),
-            'data': 'synthetic',
-            'config': {'workload': 'config4: %d envs/GPU, actor in the loop (ConfigActor, '
-                                   'config.json), mixed small_loop/zigzag' % n,
-                       'actor_mode': args.actor_mode, 'envs_per_gpu': n,
-                       'global_envs': n * ctx.world, 'repeat_actions': 3,
-                       'weights': 'random init (no checkpoint offline)',
-                       'parallelism': 'env shards (%d x %d), no collective' % (ctx.world, n)},
-            'counts': {'env_steps': tot[0], 'decisions': tot[1], 'resets': tot[2],
-                       'elapsed_s': tmax},
-            'per_rank': per,
-            'roofline': {'bound': 'mfma', 'kernel': 'actor forward (fp16 MFMA convs + linears)',
-                         'achieved': tflops, 'peak': BF16_DENSE_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                         'frac': tflops / BF16_DENSE_PEAK_TFLOPS, 'traffic': None,
-                         'avg_kernel_ms': actor_ms,
-                         'algorithmic_flops_per_launch': n * flops_per_sample()},
-            'cpu_baseline': None}), flush=True)
+    par = None
+    if parity:
+        # the timed actor's weights, dropout off, fp16 chain vs f32 path (MIOpen
+        # convolutions + the per-sample norm, tests/test_gpu_actor.py)
+        drop = roll.actor.p_drop
+        roll.actor.p_drop = 0.0
+        with torch.no_grad():
+            ref = FusedActor(roll.actor_src, dtype=torch.float32, mode=roll.actor.mode)
+            ref.p_drop = 0.0
+            got = roll.actor(roll.ring, roll.order()).float()
+            want = ref(roll.stack()).float()
+        roll.actor.p_drop = drop
+        d = torch.abs(got - want)
+        par = {'vs': 'f32 GPU path (same weights, live ring, dropout off)', 'envs_checked': n,
+               'max_abs_err': d.max().item(),
+               'p99_abs_err': torch.quantile(d.flatten(), 0.99).item(),
+               'frac_above_1e-2': (d > 1e-2).float().mean().item()}
+        par['ok'] = bool(torch.isfinite(got).all()) and par['max_abs_err'] <= 1e-2
+        par = worst_over_ranks(ctx, par, ['max_abs_err', 'p99_abs_err', 'frac_above_1e-2'])
     roll.close()
+    if rank != 0:
+        return None
+    tflops = n * flops_per_sample() / (actor_ms * 1e-3) / 1e12
+    return {
+        'metric': METRIC, 'value': tot[0] / tmax, 'unit': 'env-steps/s',
+        'n_gpus': ctx.world, 'steps': K, 'warmup': W,
+        'ms_per_step': tmax / K * 1e3,
+        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+        'dtype': 'f64 env / %s actor' % str(roll.actor.dtype).replace('torch.', ''),
+        'data': 'synthetic',
+        'config': {'workload': 'config4: %d envs/GPU, actor in the loop (ConfigActor, '
+                               'config.json), mixed small_loop/zigzag' % n,
+                   'actor_mode': args.actor_mode, 'envs_per_gpu': n,
+                   'global_envs': n * ctx.world, 'repeat_actions': 3,
+                   'weights': 'random init (no checkpoint offline)',
+                   'parallelism': 'env shards (%d x %d), no collective' % (ctx.world, n)},
+        'counts': {'env_steps': tot[0], 'decisions': tot[1], 'resets': tot[2],
+                   'elapsed_s': tmax},
+        'per_rank': per,
+        'parity': par,
+        'roofline': {'bound': 'mfma', 'kernel': 'actor forward (fp16 MFMA convs + linears)',
+                     'achieved': tflops, 'peak': BF16_DENSE_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                     'frac': tflops / BF16_DENSE_PEAK_TFLOPS, 'traffic': None,
+                     'avg_kernel_ms': actor_ms,
+                     'timing': 'HIP events around the actor forward of every timed decision',
+                     'algorithmic_flops_per_launch': n * flops_per_sample()},
+        'cpu_baseline': None}
+
+
+def bench_actor(args, ctx):
+    line = actor_record(args, ctx, args.steps, args.warmup, parity=not args.no_parity)
+    if line is not None:
+        print(json.dumps(line), flush=True)
     ctx.close()
 
 
-def bench_train(args, ctx):
-    """BASELINE configs[4]: full DDPG on every GPU — actor-in-loop rollout of
-    4096 envs, GPU prioritized replay, one update per decision, gradients
-    all-reduced over RCCL (world > 1).  value = env-steps/s; updates/s beside."""
+def train_record(args, ctx, K, W, parity=True):
+    """BASELINE configs[4]: full DDPG on every GPU -- actor-in-loop rollout of
+    4096 envs, GPU prioritized replay, one update per decision
+    (training/trainers.py:143-237), gradients all-reduced over RCCL (world >
+    1).  value = env-steps/s; updates/s beside.  parity: the non-finite guards
+    of every stage (TrainLoop.check), the replay's rejected priorities and the
+    sum tree's invariants after the timed run."""
     torch = ctx.torch
     from aido1_amd.actor import flops_per_sample
     from aido1_amd.train_loop import TrainLoop
@@ -950,17 +996,17 @@ def bench_train(args, ctx):
                      updates_per_step=args.updates_per_step, actor_mode=args.actor_mode,
                      overlap=args.overlap)
     loop.reset()
-    for _ in range(max(args.warmup, 2)):
+    for _ in range(max(W, 2)):
         loop.step()
     ctx.sync()
     loop.rollout.stats(reset=True)
     u0 = loop.updates
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for _ in range(args.steps)]
+          for _ in range(K)]
     ctx.barrier()
     ctx.sync()
     t0 = time.perf_counter()
-    for k in range(args.steps):
+    for k in range(K):
         loop.step(timing=ev[k])
     loop.flush()
     ctx.sync()
@@ -971,43 +1017,72 @@ def bench_train(args, ctx):
     tot, tmax, per = rank_report(ctx, [st['sim_steps'], st['decisions'], st['resets'],
                                        loop.updates - u0], elapsed)
     sim_steps, decisions, resets, updates = tot
-    if rank == 0:
-        tflops = n * flops_per_sample() / (actor_ms * 1e-3) / 1e12
-        nparams = sum(p.numel() for p in loop.trainer.actor.parameters()) + \
-            sum(p.numel() for p in loop.trainer.critic.parameters())
-        print(json.dumps({
-            'metric': METRIC, 'value': sim_steps / tmax, 'unit': 'env-steps/s',
-            'n_gpus': ctx.world, 'steps': args.steps, 'warmup': args.warmup,
-            'ms_per_step': tmax / args.steps * 1e3,
-            'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
-            'dtype': 'f64 env / %s actor / f32 update' % str(
-                loop.rollout.actor.dtype).replace('torch.', ''), 'data': 'synthetic',
-            'config': {'workload': 'config5: %d envs/GPU full DDPG (rollout + GPU prioritized '
-                                   'replay + update + grad all-reduce)' % n,
-                       'actor_mode': args.actor_mode, 'envs_per_gpu': n,
-                       'global_envs': n * ctx.world, 'batch_size_per_gpu': loop.batch_size,
-                       'buffer_size_per_gpu': args.buffer_size,
-                       'updates_per_step': args.updates_per_step,
-                       'update_overlap': None if not args.overlap else
-                       'update t on a side stream beside rollout t+1; acting weights one '
-                       'update behind (the reference explorers act asynchronously): a '
-                       'different schedule from the sequential loop, not the same run done '
-                       'faster',
-                       'weights': 'random init (config.json xavier_normal)',
-                       'parallelism': 'env shards (%d x %d) + data-parallel update, RCCL '
-                                      'all-reduce of %d gradients' % (ctx.world, n, nparams)},
-            'counts': {'env_steps': sim_steps, 'decisions': decisions, 'resets': resets,
-                       'updates_all_ranks': updates, 'elapsed_s': tmax,
-                       'synchronous_updates_per_s': args.steps / tmax,
-                       'samples_per_s': loop.batch_size * updates / tmax},
-            'per_rank': per,
-            'roofline': {'bound': 'mfma', 'kernel': 'actor forward (fp16 MFMA convs + linears)',
-                         'achieved': tflops, 'peak': BF16_DENSE_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                         'frac': tflops / BF16_DENSE_PEAK_TFLOPS, 'traffic': None,
-                         'avg_kernel_ms': actor_ms,
-                         'algorithmic_flops_per_launch': n * flops_per_sample()},
-            'cpu_baseline': None}), flush=True)
+    par = None
+    if parity:
+        par = {'losses_finite': bool(torch.isfinite(loop.metrics['critic_loss']).item()
+                                     and torch.isfinite(loop.metrics['actor_loss']).item())}
+        try:
+            rec = loop.check()
+            par['guard'] = 'clean: no stage reported NaN / Inf over %d updates' % rec['tick']
+        except Exception as e:  # noqa: BLE001 -- reported in the line
+            par['guard'] = str(e)
+        if loop.prioritized:
+            s_, mn, mp = loop.replay.trees()
+            cap = loop.replay.capacity
+            leaves = s_[cap:].double()
+            par['tree_root_vs_leaf_sum_rel'] = abs(leaves.sum().item() - s_[1].item()) / max(
+                s_[1].item(), 1e-300)
+            par['max_priority'] = mp.item()
+            par['stored'] = len(loop.replay)
+        par['critic_loss'] = loop.metrics['critic_loss'].item()
+        par['actor_loss'] = loop.metrics['actor_loss'].item()
+    nparams = sum(p.numel() for p in loop.trainer.actor.parameters()) + \
+        sum(p.numel() for p in loop.trainer.critic.parameters())
+    dtype = str(loop.rollout.actor.dtype).replace('torch.', '')
+    batch = loop.batch_size
     loop.rollout.close()
+    if rank != 0:
+        return None
+    tflops = n * flops_per_sample() / (actor_ms * 1e-3) / 1e12
+    return {
+        'metric': METRIC, 'value': sim_steps / tmax, 'unit': 'env-steps/s',
+        'n_gpus': ctx.world, 'steps': K, 'warmup': W,
+        'ms_per_step': tmax / K * 1e3,
+        'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
+        'dtype': 'f64 env / %s actor / f32 update' % dtype, 'data': 'synthetic',
+        'config': {'workload': 'config5: %d envs/GPU full DDPG (rollout + GPU prioritized '
+                               'replay + update + grad all-reduce)' % n,
+                   'actor_mode': args.actor_mode, 'envs_per_gpu': n,
+                   'global_envs': n * ctx.world, 'batch_size_per_gpu': batch,
+                   'buffer_size_per_gpu': args.buffer_size,
+                   'updates_per_step': args.updates_per_step,
+                   'update_overlap': None if not args.overlap else
+                   'update t on a side stream beside rollout t+1; acting weights one '
+                   'update behind (the reference explorers act asynchronously): a '
+                   'different schedule from the sequential loop, not the same run done '
+                   'faster',
+                   'weights': 'random init (config.json xavier_normal)',
+                   'parallelism': 'env shards (%d x %d) + data-parallel update, RCCL '
+                                  'all-reduce of %d gradients' % (ctx.world, n, nparams)},
+        'counts': {'env_steps': sim_steps, 'decisions': decisions, 'resets': resets,
+                   'updates_all_ranks': updates, 'elapsed_s': tmax,
+                   'synchronous_updates_per_s': K / tmax,
+                   'samples_per_s': batch * updates / tmax},
+        'per_rank': per,
+        'parity': par,
+        'roofline': {'bound': 'mfma', 'kernel': 'actor forward (fp16 MFMA convs + linears)',
+                     'achieved': tflops, 'peak': BF16_DENSE_PEAK_TFLOPS, 'unit': 'TFLOP/s',
+                     'frac': tflops / BF16_DENSE_PEAK_TFLOPS, 'traffic': None,
+                     'avg_kernel_ms': actor_ms,
+                     'timing': 'HIP events around the actor forward of every timed decision',
+                     'algorithmic_flops_per_launch': n * flops_per_sample()},
+        'cpu_baseline': None}
+
+
+def bench_train(args, ctx):
+    line = train_record(args, ctx, args.steps, args.warmup, parity=not args.no_parity)
+    if line is not None:
+        print(json.dumps(line), flush=True)
     ctx.close()
 
 

@@ -39,9 +39,14 @@ int dt_sample_norm(const void* x, void* y, int32_t n, int32_t hw, int32_t c, con
  *             [kx = 4*(s%2) + 2*(l/32) + j/4], 0 for c = 3 (aido1_amd/actor.py)
  *   bias      device f32 [32]
  *   y         device fp16 [n, 57, 77, 32] (NHWC)
- *   partials  device f32 [n, 32, 2] or NULL: the sample's per-channel
- *             (mean, M2) of the LeakyReLU outputs (reference mode), for
- *             dt_conv1_norm and dt_conv32 layer 2 */
+ *   partials  device f32 [n, 32, 3] or NULL (reference mode): the sample's
+ *             per-channel (mean, M2, c) for dt_conv1_norm and dt_conv32 layer
+ *             2.  With partials, y holds the LeakyReLU outputs CENTRED: v - c,
+ *             c = the sample's pixel-0 output of the channel, and mean is the
+ *             mean of the stored (centred) values; M2 is shift-free.  So the
+ *             next BatchNorm's (y - mean) * invstd is the uncentred one, and a
+ *             nearly flat channel (tiny std) does not amplify the fp16
+ *             rounding of |v| but only of |v - c|. */
 int dt_conv1(const float* ring, int32_t n, int32_t slots, const int32_t* order, const void* wfrag,
              const float* bias, void* y, float* partials, float slope, void* stream);
 
@@ -57,12 +62,12 @@ int dt_conv1_norm(void* y, int32_t n, const float* partials, const float* gamma,
  * workgroups stream whole samples through an LDS ring of input rows.
  *   wfrag      device fp16 [32, 64, 8] A fragments: [s][l][j] =
  *              w[l%32][16*(s%2) + 8*(l/32) + j][(s/2)/4][(s/2)%4]
- *   prev_part  the previous layer's statistics [n, 32, 2] (dt_conv1's partials for
+ *   prev_part  the previous layer's statistics [n, 32, 3] (dt_conv1's partials for
  *              layer 2, this call's `part` of layer 2 / 3 for 3 / 4) or NULL:
  *              with it, the previous BatchNorm (in_gamma, in_beta, in_eps) is
  *              applied per sample while the input is staged (reference mode)
- *   part       layers 2, 3 with prev_part: out [n, 32, 2], the sample's
- *              per-channel (mean, M2) of the LeakyReLU outputs
+ *   part       layers 2, 3 with prev_part: out [n, 32, 3], the sample's
+ *              per-channel (mean, M2, c), y centred as dt_conv1's
  *   y          layers 2, 3: [n, OH, OW, 32]; layer 4: [n, 32*9*14] flattened in
  *              NCHW order, normalised by (out_gamma, out_beta, out_eps) when
  *              prev_part is given (the last BatchNorm, whole sample in-kernel)

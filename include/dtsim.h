@@ -41,7 +41,9 @@ extern "C" {
                                 their workspace queries (any image size),
                                 dt_hough_lines count -2 (max_lines reached);
                              8: dttrain.h non-finite guards: dt_guard_scan, a
-                                guard word for dt_bn_leaky_fwd / _bwd / dt_adam */
+                                guard word for dt_bn_leaky_fwd / _bwd / dt_adam;
+                                dtactor.h reference-mode partials [n, 32, 3]
+                                (mean, M2, centre) with centred activations */
 
 /* error codes */
 #define DT_OK 0

@@ -119,24 +119,28 @@ def test_conv1_kernel_matches_conv2d(gpu, slots, order, n):
     x = ring[:, order].half().float()
     ref = F.leaky_relu(F.conv2d(x, w.half().float(), b, stride=2))      # [n,32,57,77]
     y = torch.empty(n, 57, 77, 32, dtype=torch.float16, device=gpu)
-    part = torch.empty(n, 32, 2, device=gpu)
+    part = torch.empty(n, 32, 3, device=gpu)
     o = (ctypes.c_int32 * 3)(*order)
     s = torch.cuda.current_stream().cuda_stream
     wf = conv1_fragments(w)     # held: a temporary's memory could be reused before the launch
     assert L.dt_conv1(ring.data_ptr(), n, slots, o, wf.data_ptr(), b.data_ptr(),
                       y.data_ptr(), part.data_ptr(), 0.01, s) == 0
-    got = y.permute(0, 3, 1, 2).float()
+    # reference mode stores the outputs centred on the sample's pixel 0
+    c = part[..., 2]
+    tol = 2e-3 * max(1.0, ref.abs().max().item())
+    assert (c - ref[:, :, 0, 0]).abs().max().item() < tol
+    got = y.permute(0, 3, 1, 2).float() + c[:, :, None, None]
     err = (got - ref).abs().max().item()
-    assert err < 2e-3 * max(1.0, ref.abs().max().item()), err
+    assert err < tol, err
     # per-sample statistics (mean, M2) of the f32 outputs
     r64 = ref.double()
     mean = r64.mean((2, 3))
     m2 = ((r64 - mean[:, :, None, None]) ** 2).sum((2, 3))
-    assert torch.allclose(part[..., 0].double(), mean, rtol=1e-3, atol=1e-3)
+    assert torch.allclose(part[..., 0].double() + c.double(), mean, rtol=1e-3, atol=1e-3)
     assert torch.allclose(part[..., 1].double(), m2, rtol=2e-3, atol=1e-2)
     gamma = torch.rand(32, device=gpu) + 0.5
     beta = torch.rand(32, device=gpu) - 0.5
-    y16 = y.permute(0, 3, 1, 2).double()          # what the norm pass normalises
+    y16 = y.permute(0, 3, 1, 2).double() + c.double()[:, :, None, None]   # what it normalises
     assert L.dt_conv1_norm(y.data_ptr(), n, part.data_ptr(), gamma.data_ptr(), beta.data_ptr(),
                            1e-5, s) == 0
     m = r64.mean((2, 3), keepdim=True)
@@ -262,7 +266,7 @@ for slots, order, n in ((4, [1, 2, 3], 1100), (3, [2, 0, 1], 37), (3, [0, 1, 2],
     w = torch.randn(32, 3, 8, 8, device=dev) * 0.08
     b = torch.randn(32, device=dev) * 0.2
     y = torch.empty(n, 57, 77, 32, dtype=torch.float16, device=dev)
-    part = torch.empty(n, 32, 2, device=dev)
+    part = torch.empty(n, 32, 3, device=dev)
     wf = conv1_fragments(w)
     o = (ctypes.c_int32 * 3)(*order)
     assert L.dt_conv1(ring.data_ptr(), n, slots, o, wf.data_ptr(), b.data_ptr(), y.data_ptr(),

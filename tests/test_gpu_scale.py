@@ -81,11 +81,13 @@ def test_config4_actor_rollout_at_size(gpu):
     print('config4 fp16 actor vs f32 GPU path, all %d envs: max %.3g, median %.3g, p99 %.3g, '
           'p99.9 %.3g, outputs > 1e-2: %.4f' % (n, err_all, q[0], q[1], q[2], frac))
     # fp16 under per-sample (batch-of-one) BatchNorm: a channel that is
-    # nearly flat over a frame is divided by a tiny standard deviation, which
-    # amplifies fp16 rounding (measured max 6.8e-2 over 4096 live envs, 4e-3
-    # on the 64 above); the bulk stays within 1e-2
-    assert err_all < 0.1, err_all
-    assert frac < 0.01, frac
+    # nearly flat over a frame is divided by a tiny standard deviation.  Stored
+    # uncentred, its fp16 rounding (~2^-11 |v|) was amplified by that 1 / std
+    # (max 6.8e-2 over these 4096 live envs in round 3); the kernels now store
+    # each sample's activations centred on its pixel 0 (include/dtactor.h), so
+    # the rounding is of |v - c|, the channel's own spread
+    assert err_all <= 1e-2, err_all
+    assert frac == 0.0, frac
     roll.close()
 
 

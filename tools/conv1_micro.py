@@ -39,7 +39,7 @@ def run(n, reps):
     wf = (torch.randn(16 * 64 * 8, device=dev) * 0.05).half()
     b = torch.zeros(32, device=dev)
     y = torch.empty(n, 57, 77, 32, dtype=torch.float16, device=dev)
-    part = torch.empty(n, 8, 32, 2, device=dev)
+    part = torch.empty(n, 8, 32, 3, device=dev)
     o = (ctypes.c_int32 * 3)(0, 1, 2)
     s = torch.cuda.current_stream().cuda_stream
     if os.environ.get('CONV1_DATA') == 'zero':     # same work, quiet operands

@@ -41,11 +41,11 @@ def run(n, reps):
             x = (torch.rand(n, ih, iw, 32, device=dev) * 2).half()
             w = (torch.randn(32 * 64 * 8, device=dev) * 0.05).half()
             b = torch.zeros(32, device=dev)
-            pp = torch.rand(n, 32, 2, device=dev) + 0.5
+            pp = torch.rand(n, 32, 3, device=dev) + 0.5
             g = torch.ones(32, device=dev)
             bt = torch.zeros(32, device=dev)
             y = torch.empty(n, oh * ow * 32, dtype=torch.float16, device=dev)
-            part = torch.empty(n, 32, 2, device=dev)
+            part = torch.empty(n, 32, 3, device=dev)
             s = torch.cuda.current_stream().cuda_stream
             last = layer == 4
 
