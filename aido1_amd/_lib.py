@@ -18,9 +18,9 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_PATH = os.path.join(PKG_DIR, 'libdtsim.so')
 CSRC = os.path.join(PKG_DIR, 'csrc')
 SOURCES = ['dtsim.hip', 'dtrender.hip', 'dtreplay.hip', 'dtactor.hip', 'dtconv.hip',
-           'dttrain.hip']
+           'dttrain.hip', 'dtupd.hip']
 HEADERS = ['dtsim_common.h', 'dtrender.h']
-PUBLIC_HEADERS = ['dtsim.h', 'dtreplay.h', 'dtactor.h', 'dttrain.h']
+PUBLIC_HEADERS = ['dtsim.h', 'dtreplay.h', 'dtactor.h', 'dttrain.h', 'dtupd.h']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ABI_VERSION = 8
 
@@ -169,6 +169,12 @@ def lib():
                                                vp, vp, vp, vp]),
             'dt_adam': (ctypes.c_int, [i32, vp, vp, vp, vp, f64, f64, f64, vp, vp, i32, i32, vp]),
             'dt_guard_scan': (ctypes.c_int, [i32, vp, vp, vp]),
+            # dtupd.h
+            'dt_upd_conv_fwd': (ctypes.c_int, [i32, i32, i32, i32, i32, i32, vp, vp, vp, vp]),
+            'dt_upd_wgrad_work_floats': (i64, [i32, i32, i32, i32, i32, i32]),
+            'dt_upd_conv_wgrad': (ctypes.c_int, [i32, i32, i32, i32, i32, i32, vp, vp, vp, vp,
+                                                 vp]),
+            'dt_upd_conv_dgrad': (ctypes.c_int, [i32, i32, i32, i32, i32, i32, vp, vp, vp, vp]),
             'dt_soft_update': (ctypes.c_int, [i32, vp, vp, f64, vp]),
             # dtactor.h
             'dt_sample_norm': (ctypes.c_int, [vp, vp, i32, i32, i32, vp, vp, ctypes.c_float,

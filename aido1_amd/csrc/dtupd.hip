@@ -1,0 +1,420 @@
+// The DDPG update's convolutions (include/dtupd.h): config.json's conv_2d
+// layers of the actor and critic in f32 on v_mfma_f32_32x32x2_f32, forward,
+// weight gradient and input gradient, replacing MIOpen in the train-mode
+// networks of training/trainers.py:143-237.
+//
+// Every layer is C_out = 32 and NHWC, so each pass is a GEMM whose N or M is
+// the 32 channels:
+//   forward  D[pixel][co]   = sum_k  X[pixel][k]   W[co][k]     (A = im2col row, B = W)
+//   wgrad    D[co][k]       = sum_p  dZ[p][co]     X[p][k]      (A = dZ, B = im2col)
+//   dgrad    D[pixel][ci]   = sum_t  dZ[o(t)][co]  W[co][ci]    (A = dZ, B = W^T)
+// A 32x32x2 MFMA takes ONE f32 per lane for each operand (A[i = l & 31][k =
+// l >> 5], B[k = l >> 5][j = l & 31]).  A lane loads a float4 of four
+// consecutive k instead and feeds four MFMAs, element e to the e-th: the
+// k-slot kk of MFMA e is the reduction index 8s + 4kk + e, the same for A
+// and B, so the sum is the convolution's, in a different order.  Loads are
+// then 16-B pieces of one pixel's channels (32 consecutive floats a pixel per
+// half-wave: whole 128-B lines), and the weights sit in LDS.
+//
+// Geometry is compile-time (the four config.json layers at 120 x 160
+// observations); the host entry points dispatch on (C_in, KS, ST, IH, IW).
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "../../include/dtupd.h"
+
+namespace {
+
+using f32x16 = __attribute__((ext_vector_type(16))) float;
+
+template <int CIN_, int KS_, int ST_, int IH_, int IW_>
+struct Geom {
+  static constexpr int CIN = CIN_, KS = KS_, ST = ST_, IH = IH_, IW = IW_;
+  static constexpr int OH = (IH - KS) / ST + 1, OW = (IW - KS) / ST + 1;
+  static constexpr int OPIX = OH * OW;
+  static constexpr int K = KS * KS * CIN;          // reduction length (im2col row)
+  static constexpr int KROW = KS * CIN;            // contiguous floats of one kernel row
+  static constexpr int KSTEPS = K / 8;             // 8 k a float4 step (4 MFMAs)
+  static constexpr int TPS = (OPIX + 31) / 32;     // 32-pixel tiles a sample
+  static_assert(K % 8 == 0 && KROW % 4 == 0, "float4 steps stay inside a kernel row");
+  // offset (floats) of reduction index k inside a pixel's patch
+  __host__ __device__ static constexpr int koff(int k) { return (k / KROW) * IW * CIN + k % KROW; }
+  // first float of output pixel p's patch in sample s
+  __device__ static int xbase(int s, int p) {
+    const int oy = p / OW, ox = p - oy * OW;
+    return ((s * IH + oy * ST) * IW + ox * ST) * CIN;
+  }
+};
+
+using L1 = Geom<3, 8, 2, 120, 160>;
+using L2 = Geom<32, 4, 2, 57, 77>;
+using L3 = Geom<32, 4, 2, 27, 37>;
+using L4 = Geom<32, 4, 1, 12, 17>;
+
+// four consecutive floats of a patch row (16-B aligned for C_in 32, 8-B for
+// C_in 3: the row starts at 6 * ox floats)
+template <int CIN>
+__device__ __forceinline__ float4 ld4(const float* p) {
+  if constexpr (CIN % 4 == 0) {
+    return *reinterpret_cast<const float4*>(p);
+  } else {
+    const float2 a = *reinterpret_cast<const float2*>(p);
+    const float2 b = *reinterpret_cast<const float2*>(p + 2);
+    return make_float4(a.x, a.y, b.x, b.y);
+  }
+}
+
+__device__ __forceinline__ f32x16 mfma4(float4 a, float4 b, f32x16 c) {
+  c = __builtin_amdgcn_mfma_f32_32x32x2f32(a.x, b.x, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x2f32(a.y, b.y, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x2f32(a.z, b.z, c, 0, 0, 0);
+  c = __builtin_amdgcn_mfma_f32_32x32x2f32(a.w, b.w, c, 0, 0, 0);
+  return c;
+}
+
+// row of the 32x32 accumulator register r holds for lane half h
+__device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
+
+constexpr int kThreads = 256;   // 4 waves
+
+// ---- forward ---------------------------------------------------------------------------
+// A workgroup holds W in LDS ([32][K + 4]: row stride 4 floats past K, so the
+// 32 output-channel lanes of a B read fall on distinct banks) and walks
+// 32-pixel tiles of one sample each; KSPLIT waves share a tile, each a slice
+// of K, summed through LDS (the small layers: more waves than tiles).
+template <class G, int KSPLIT>
+__global__ void __launch_bounds__(kThreads)
+fwd_kernel(int n, const float* __restrict__ x, const float* __restrict__ w, float* __restrict__ z) {
+  constexpr int WST = G::K + 4;
+  constexpr int GP = 4 / KSPLIT;                 // tiles a workgroup round
+  constexpr int SPW = G::KSTEPS / KSPLIT;        // k-steps a wave
+  static_assert(G::KSTEPS % KSPLIT == 0, "even K slices");
+  __shared__ __attribute__((aligned(16))) float ws[32 * WST];
+  __shared__ float red[KSPLIT > 1 ? 4 * 16 * 64 : 1];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 31, kk = lane >> 5;
+  for (int q = tid; q < 32 * G::K / 4; q += kThreads) {
+    const int co = q / (G::K / 4), k4 = q - co * (G::K / 4);
+    *reinterpret_cast<float4*>(ws + co * WST + 4 * k4) = reinterpret_cast<const float4*>(w)[q];
+  }
+  __syncthreads();
+  const int g = wave / KSPLIT, ks = wave - g * KSPLIT;
+  const int tiles = n * G::TPS;
+  const float* wrow = ws + col * WST + 4 * kk;
+  for (int base = blockIdx.x * GP; base < tiles; base += gridDim.x * GP) {
+    const int tile = base + g;
+    const bool tvalid = tile < tiles;
+    const int tc = tvalid ? tile : 0;
+    const int s = tc / G::TPS, tb = tc - s * G::TPS;
+    const int p = tb * 32 + col;
+    const int pc = p < G::OPIX ? p : 0;          // an invalid row reads pixel 0, unused
+    const float* xl = x + G::xbase(s, pc) + 4 * kk;
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+    const int s0 = ks * SPW;
+#pragma unroll 4
+    for (int st = 0; st < SPW; ++st) {
+      const int kc = 8 * (s0 + st);
+      const float4 a = ld4<G::CIN>(xl + G::koff(kc));
+      const float4 b = *reinterpret_cast<const float4*>(wrow + kc);
+      acc = mfma4(a, b, acc);
+    }
+    if constexpr (KSPLIT > 1) {
+      if (ks > 0)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) red[(wave * 16 + r) * 64 + lane] = acc[r];
+      __syncthreads();
+      if (ks == 0)
+#pragma unroll
+        for (int r = 0; r < 16; ++r)
+#pragma unroll
+          for (int o = 1; o < KSPLIT; ++o) acc[r] += red[((wave + o) * 16 + r) * 64 + lane];
+      __syncthreads();
+    }
+    if (ks == 0 && tvalid) {
+      float* zs = z + (size_t)s * G::OPIX * 32;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const int pr = tb * 32 + acc_row(r, kk);
+        if (pr < G::OPIX) zs[pr * 32 + col] = acc[r];
+      }
+    }
+  }
+}
+
+// ---- weight gradient -------------------------------------------------------------------
+// Workgroup c sums the output pixels [c * pc, (c + 1) * pc) of all samples
+// (flattened n * OPIX); its WAVES waves take NBW 32-wide blocks of k each, so
+// a dZ value is loaded once per wave for NBW blocks.  8 pixels a step (the
+// float4 trick along the pixel index: lane (co, kk) holds dZ of pixels
+// q0 + 4kk + e).  The partial dW of the chunk goes to part[c] and
+// wgrad_reduce_kernel sums the chunks in index order.
+template <class G, int NBW, int WAVES>
+__global__ void __launch_bounds__(64 * WAVES)
+wgrad_kernel(int n, int pc, const float* __restrict__ x, const float* __restrict__ dz,
+             float* __restrict__ part) {
+  static_assert(WAVES * NBW * 32 == G::K, "the waves cover K");
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 31, kk = lane >> 5;
+  const int P = n * G::OPIX;
+  const int q_beg = blockIdx.x * pc;
+  const int q_end = q_beg + pc < P ? q_beg + pc : P;
+  int ko[NBW];
+#pragma unroll
+  for (int b = 0; b < NBW; ++b) ko[b] = G::koff((wave * NBW + b) * 32 + col);
+  f32x16 acc[NBW];
+#pragma unroll
+  for (int b = 0; b < NBW; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[b][r] = 0.0f;
+  for (int q0 = q_beg; q0 < q_end; q0 += 8) {
+    float av[4];
+    int xb[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int q = q0 + 4 * kk + e;
+      const bool ok = q < q_end;
+      const int qc = ok ? q : q_beg;
+      const int s = qc / G::OPIX, p = qc - s * G::OPIX;
+      av[e] = ok ? dz[(size_t)qc * 32 + col] : 0.0f;
+      xb[e] = G::xbase(s, p);
+    }
+#pragma unroll
+    for (int b = 0; b < NBW; ++b)
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[e], x[xb[e] + ko[b]], acc[b], 0, 0, 0);
+  }
+  // D[co][k]: lane (k = block * 32 + col), rows co
+  float* pp = part + (size_t)blockIdx.x * 32 * G::K;
+#pragma unroll
+  for (int b = 0; b < NBW; ++b)
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      pp[acc_row(r, kk) * G::K + (wave * NBW + b) * 32 + col] = acc[b][r];
+}
+
+__global__ void __launch_bounds__(256)
+wgrad_reduce_kernel(int chunks, int len, const float* __restrict__ part, float* __restrict__ dw) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= len) return;
+  float s = 0.0f;
+  for (int c = 0; c < chunks; ++c) s += part[(size_t)c * len + i];
+  dw[i] = s;
+}
+
+// ---- input gradient (C_in = 32) ----------------------------------------------------------
+// Input pixels split into ST x ST parity classes (ph, pw): in one class the
+// kernel taps that reach a pixel are the same, kh = ph + ST th, kw = pw + ST tw
+// (th, tw < KS / ST), from output pixel (a - th, b - tw) where (ih, iw) =
+// (ST a + ph, ST b + pw).  A tile is 32 consecutive (a, b) of one class, so
+// B = W^T of a tap is uniform across the tile; taps falling outside the
+// output contribute zero.  W^T sits in LDS as [tap][ci][co + 4].
+template <class G>
+struct DGeom {
+  static constexpr int ST = G::ST, T1 = G::KS / G::ST, TAPS = T1 * T1;
+  static constexpr int NCLS = ST * ST;
+  __host__ __device__ static constexpr int ac(int c) { return (G::IH - c / ST + ST - 1) / ST; }
+  __host__ __device__ static constexpr int bc(int c) { return (G::IW - c % ST + ST - 1) / ST; }
+  __host__ __device__ static constexpr int tiles(int c) { return (ac(c) * bc(c) + 31) / 32; }
+  __host__ __device__ static constexpr int first(int c) {   // first tile of class c in a sample
+    int t = 0;
+    for (int i = 0; i < c; ++i) t += tiles(i);
+    return t;
+  }
+  static constexpr int TPS = first(NCLS);
+};
+
+template <class G>
+__global__ void __launch_bounds__(kThreads)
+dgrad_kernel(int n, const float* __restrict__ dz, const float* __restrict__ w,
+             float* __restrict__ dx) {
+  using D = DGeom<G>;
+  static_assert(G::CIN == 32, "dgrad for 32-channel inputs");
+  constexpr int CST = 36;                         // co stride of a W^T row
+  __shared__ __attribute__((aligned(16))) float wt[G::KS * G::KS * 32 * CST];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 31, kk = lane >> 5;
+  // W [co][kh][kw][ci] -> wt[kh * KS + kw][ci][co]
+  for (int i = tid; i < 32 * G::K; i += kThreads) {
+    const int co = i / G::K, r = i - co * G::K;
+    const int tap = r / 32, ci = r - tap * 32;
+    wt[(tap * 32 + ci) * CST + co] = w[i];
+  }
+  __syncthreads();
+  const int tiles = n * D::TPS;
+  for (int tile = blockIdx.x * 4 + wave; tile < tiles; tile += gridDim.x * 4) {
+    const int s = tile / D::TPS;
+    int t = tile - s * D::TPS, cls = 0;
+#pragma unroll
+    for (int c = 1; c < D::NCLS; ++c)
+      if (t >= D::first(c)) cls = c;
+    t -= D::first(cls);
+    const int ph = cls / D::ST, pw = cls - ph * D::ST;
+    const int bcn = D::bc(cls), np = D::ac(cls) * bcn;
+    const int idx = t * 32 + col;
+    const int ic = idx < np ? idx : 0;
+    const int a = ic / bcn, b = ic - a * bcn;
+    const float* dzs = dz + (size_t)s * G::OPIX * 32 + 4 * kk;
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#pragma unroll
+    for (int tap = 0; tap < D::TAPS; ++tap) {
+      const int th = tap / D::T1, tw = tap - th * D::T1;
+      const int oy = a - th, ox = b - tw;
+      const bool ok = idx < np && oy >= 0 && oy < G::OH && ox >= 0 && ox < G::OW;
+      const float* src = dzs + (ok ? (oy * G::OW + ox) * 32 : 0);
+      const int kh = ph + D::ST * th, kw = pw + D::ST * tw;
+      const float* wrow = wt + ((kh * G::KS + kw) * 32 + col) * CST + 4 * kk;
+#pragma unroll
+      for (int c8 = 0; c8 < 4; ++c8) {
+        float4 av = *reinterpret_cast<const float4*>(src + 8 * c8);
+        if (!ok) av = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        const float4 bv = *reinterpret_cast<const float4*>(wrow + 8 * c8);
+        acc = mfma4(av, bv, acc);
+      }
+    }
+    float* dxs = dx + (size_t)s * G::IH * G::IW * 32;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int ir = t * 32 + acc_row(r, kk);
+      if (ir < np) {
+        const int ar = ir / bcn, br = ir - ar * bcn;
+        dxs[((D::ST * ar + ph) * G::IW + D::ST * br + pw) * 32 + col] = acc[r];
+      }
+    }
+  }
+}
+
+// ---- host ------------------------------------------------------------------------------
+int resident(const void* kern, int threads, int cap) {
+  static int cus = 0;
+  if (!cus) {
+    int dev = 0;
+    cus = 256;
+    if (hipGetDevice(&dev) == hipSuccess)
+      (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
+  }
+  int per = 1;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, kern, threads, 0) != hipSuccess || per < 1)
+    per = 1;
+  const int g = per * cus;
+  return g < cap ? g : cap;
+}
+
+template <class G, int KSPLIT>
+int launch_fwd(int n, const float* x, const float* w, float* z, hipStream_t s) {
+  constexpr int GP = 4 / KSPLIT;
+  const int tiles = n * G::TPS;
+  int grid = (tiles + GP - 1) / GP;
+  static const int res =
+      resident(reinterpret_cast<const void*>(fwd_kernel<G, KSPLIT>), kThreads, 1 << 20);
+  grid = grid < res ? grid : res;
+  hipLaunchKernelGGL((fwd_kernel<G, KSPLIT>), dim3(grid), dim3(kThreads), 0, s, n, x, w, z);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
+// chunks of the wgrad pixel range: about 1024 waves, partials capped at 2 M floats
+template <class G, int WAVES>
+int wgrad_chunks(int n, int* pc) {
+  const int P = n * G::OPIX;
+  int chunks = 1024 / WAVES;
+  const int cap = (2 << 20) / (32 * G::K);
+  chunks = chunks < cap ? chunks : cap;
+  int c = (P + chunks - 1) / chunks;
+  c = (c + 7) / 8 * 8;
+  *pc = c;
+  return (P + c - 1) / c;
+}
+
+template <class G, int NBW, int WAVES>
+int launch_wgrad(int n, const float* x, const float* dz, float* dw, float* work, hipStream_t s) {
+  int pc = 0;
+  const int chunks = wgrad_chunks<G, WAVES>(n, &pc);
+  hipLaunchKernelGGL((wgrad_kernel<G, NBW, WAVES>), dim3(chunks), dim3(64 * WAVES), 0, s, n, pc,
+                     x, dz, work);
+  const int len = 32 * G::K;
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((len + 255) / 256), dim3(256), 0, s, chunks, len,
+                     work, dw);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
+template <class G>
+int launch_dgrad(int n, const float* dz, const float* w, float* dx, hipStream_t s) {
+  const int tiles = n * DGeom<G>::TPS;
+  int grid = (tiles + 3) / 4;
+  static const int res = resident(reinterpret_cast<const void*>(dgrad_kernel<G>), kThreads, 1 << 20);
+  grid = grid < res ? grid : res;
+  hipLaunchKernelGGL(dgrad_kernel<G>, dim3(grid), dim3(kThreads), 0, s, n, dz, w, dx);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
+// which of the four layers (0: none)
+int layer_of(int cin, int ks, int st, int ih, int iw) {
+  if (cin == 3 && ks == 8 && st == 2 && ih == 120 && iw == 160) return 1;
+  if (cin == 32 && ks == 4 && st == 2 && ih == 57 && iw == 77) return 2;
+  if (cin == 32 && ks == 4 && st == 2 && ih == 27 && iw == 37) return 3;
+  if (cin == 32 && ks == 4 && st == 1 && ih == 12 && iw == 17) return 4;
+  return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int dt_upd_conv_fwd(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih, int32_t iw,
+                    const float* x, const float* w, float* z, void* stream) {
+  const int l = layer_of(cin, ks, st, ih, iw);
+  if (!l || n < 0 || (n > 0 && (!x || !w || !z))) return DT_E_ARG;
+  if (n == 0) return DT_OK;
+  hipStream_t s = (hipStream_t)stream;
+  switch (l) {
+    case 1: return launch_fwd<L1, 1>(n, x, w, z, s);
+    case 2: return launch_fwd<L2, 1>(n, x, w, z, s);
+    case 3: return launch_fwd<L3, 2>(n, x, w, z, s);
+    default: return launch_fwd<L4, 4>(n, x, w, z, s);
+  }
+}
+
+int64_t dt_upd_wgrad_work_floats(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih,
+                                 int32_t iw) {
+  int pc = 0;
+  switch (layer_of(cin, ks, st, ih, iw)) {
+    case 1: return (int64_t)wgrad_chunks<L1, 2>(n, &pc) * 32 * L1::K;
+    case 2: return (int64_t)wgrad_chunks<L2, 4>(n, &pc) * 32 * L2::K;
+    case 3: return (int64_t)wgrad_chunks<L3, 4>(n, &pc) * 32 * L3::K;
+    case 4: return (int64_t)wgrad_chunks<L4, 4>(n, &pc) * 32 * L4::K;
+    default: return -1;
+  }
+}
+
+int dt_upd_conv_wgrad(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih, int32_t iw,
+                      const float* x, const float* dz, float* dw, float* work, void* stream) {
+  const int l = layer_of(cin, ks, st, ih, iw);
+  if (!l || n < 1 || !x || !dz || !dw || !work) return DT_E_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  switch (l) {
+    case 1: return launch_wgrad<L1, 3, 2>(n, x, dz, dw, work, s);
+    case 2: return launch_wgrad<L2, 4, 4>(n, x, dz, dw, work, s);
+    case 3: return launch_wgrad<L3, 4, 4>(n, x, dz, dw, work, s);
+    default: return launch_wgrad<L4, 4, 4>(n, x, dz, dw, work, s);
+  }
+}
+
+int dt_upd_conv_dgrad(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih, int32_t iw,
+                      const float* dz, const float* w, float* dx, void* stream) {
+  const int l = layer_of(cin, ks, st, ih, iw);
+  if (l < 2 || n < 0 || (n > 0 && (!dz || !w || !dx))) return DT_E_ARG;
+  if (n == 0) return DT_OK;
+  hipStream_t s = (hipStream_t)stream;
+  switch (l) {
+    case 2: return launch_dgrad<L2>(n, dz, w, dx, s);
+    case 3: return launch_dgrad<L3>(n, dz, w, dx, s);
+    default: return launch_dgrad<L4>(n, dz, w, dx, s);
+  }
+}
+
+}  // extern "C"

@@ -4,7 +4,8 @@ Every conv block of config.json's actor and critic is conv_2d -> leaky_relu
 -> batch_norm_2d (models/ddpg/modules.py MetaNet), and the trainer runs all
 four networks in train mode (training/trainers.py:143-237).  On the GPU in
 float32 with channels_last activations, ``conv_leaky_bn`` runs the
-convolution without its bias (MIOpen) and then dt_bn_leaky_fwd: bias,
+convolution without its bias (include/dtupd.h's f32 MFMA kernels for
+config.json's layers; MIOpen for any other shape) and then dt_bn_leaky_fwd: bias,
 LeakyReLU, the batch statistics, the running-statistics update and
 num_batches_tracked in one kernel, the normalisation in a second; its
 backward is dt_bn_leaky_bwd (two kernels for BatchNorm's, LeakyReLU's and the
@@ -118,8 +119,85 @@ def running_updates(module, k):
             m._dt_updates = 1
 
 
+# (C_in, KS, ST, IH, IW) of include/dtupd.h's kernels: config.json's four
+# conv_2d layers at 120 x 160 observations
+UPD_CONV_LAYERS = {(3, 8, 2, 120, 160), (32, 4, 2, 57, 77), (32, 4, 2, 27, 37),
+                   (32, 4, 1, 12, 17)}
+
+
+def upd_conv_applicable(x, conv):
+    """The update's convolution runs on dt_upd_conv_* (f32 MFMA) for these."""
+    w = conv.weight
+    return (x.is_cuda and x.dtype == torch.float32 and w.dtype == torch.float32 and x.dim() == 4
+            and conv.out_channels == C and conv.groups == 1
+            and tuple(conv.padding) == (0, 0) and tuple(conv.dilation) == (1, 1)
+            and conv.stride[0] == conv.stride[1] and w.shape[2] == w.shape[3]
+            and (x.shape[1], w.shape[2], conv.stride[0], x.shape[2], x.shape[3])
+            in UPD_CONV_LAYERS)
+
+
+class _UpdConv(torch.autograd.Function):
+    """conv2d(x, w, stride) without bias on include/dtupd.h: NHWC f32, the
+    weight in its channels_last memory ([co][kh][kw][ci]); backward = the
+    kernels' weight gradient (deterministic chunked sum) and input gradient."""
+
+    @staticmethod
+    def forward(ctx, x, w, st):
+        cl = torch.channels_last
+        x = x.contiguous(memory_format=cl)
+        w = w.contiguous(memory_format=cl)
+        n, cin, ih, iw = x.shape
+        ks = w.shape[2]
+        oh, ow = (ih - ks) // st + 1, (iw - ks) // st + 1
+        z = torch.empty((n, C, oh, ow), device=x.device, dtype=x.dtype, memory_format=cl)
+        rc = _lib.lib().dt_upd_conv_fwd(cin, ks, st, n, ih, iw, x.data_ptr(), w.data_ptr(),
+                                        z.data_ptr(), _stream(x.device))
+        if rc != 0:
+            raise _lib.DtError('dt_upd_conv_fwd failed (%d)' % rc)
+        ctx.save_for_backward(x, w)
+        ctx.st = st
+        return z
+
+    @staticmethod
+    def backward(ctx, dz):
+        x, w = ctx.saved_tensors
+        st = ctx.st
+        cl = torch.channels_last
+        dz = dz.contiguous(memory_format=cl)
+        n, cin, ih, iw = x.shape
+        ks = w.shape[2]
+        L = _lib.lib()
+        dx = dw = None
+        if ctx.needs_input_grad[1]:
+            work = torch.empty(int(L.dt_upd_wgrad_work_floats(cin, ks, st, n, ih, iw)),
+                               device=x.device)
+            dw = torch.empty_like(w)
+            rc = L.dt_upd_conv_wgrad(cin, ks, st, n, ih, iw, x.data_ptr(), dz.data_ptr(),
+                                     dw.data_ptr(), work.data_ptr(), _stream(x.device))
+            if rc != 0:
+                raise _lib.DtError('dt_upd_conv_wgrad failed (%d)' % rc)
+        if ctx.needs_input_grad[0]:
+            if cin != C:    # the observation layer: its input never needs one here
+                dx = torch.nn.grad.conv2d_input(x.shape, w, dz, stride=st)
+            else:
+                dx = torch.empty_like(x)
+                rc = L.dt_upd_conv_dgrad(cin, ks, st, n, ih, iw, dz.data_ptr(), w.data_ptr(),
+                                         dx.data_ptr(), _stream(x.device))
+                if rc != 0:
+                    raise _lib.DtError('dt_upd_conv_dgrad failed (%d)' % rc)
+        return dx, dw, None
+
+
+def upd_conv(x, conv):
+    """conv(x) without its bias on the dtupd.h kernels (upd_conv_applicable)."""
+    return _UpdConv.apply(x, conv.weight, int(conv.stride[0]))
+
+
 def conv_leaky_bn(x, conv, act, bn):
     """bn(act(conv(x))) for a train-mode block (see the module docstring)."""
-    z = F.conv2d(x, conv.weight, None, conv.stride)
+    if upd_conv_applicable(x, conv):
+        z = upd_conv(x, conv)
+    else:
+        z = F.conv2d(x, conv.weight, None, conv.stride)
     z = z.contiguous(memory_format=torch.channels_last)
     return _BnLeaky.apply(z, conv.bias, bn.weight, bn.bias, bn, float(act.negative_slope))

@@ -1,0 +1,61 @@
+/* dtupd.h — C-ABI of the DDPG update's convolutions (SURVEY.md §8f 1,
+ * BASELINE configs[4]): hand-written f32 MFMA kernels for the conv_2d layers
+ * of config.json's actor and critic (3 -> 32 8x8 stride 2; 32 -> 32 4x4
+ * strides 2 and 1; padding 0, no dilation or groups), forward and both
+ * gradients, in place of MIOpen (training/trainers.py:143-237 runs every
+ * network in train mode through torch's conv2d and its autograd).
+ *
+ * Layout: NHWC float32 (torch channels_last), batch n, C_out = 32.  The
+ * weight is w[co][kh][kw][ci] (a channels_last [32, C_in, KS, KS] tensor),
+ * i.e. [32][K] with K = KS * KS * C_in, the im2col order of an input patch.
+ * OH = (IH - KS) / ST + 1, OW likewise.  Supported (C_in, KS, ST): (3, 8, 2),
+ * (32, 4, 2), (32, 4, 1); DT_E_ARG otherwise.
+ *
+ * Numerics: v_mfma_f32_32x32x2_f32, an exact f32 fma chain per output over
+ * its K products (the order differs from a CPU or MIOpen convolution, as
+ * theirs differ from each other); no TF32-like rounding exists on gfx950.
+ *
+ * Conventions as dtsim.h: 0 or a negative DT_E_* code; device pointers; work
+ * goes on `stream` (a hipStream_t).
+ */
+#ifndef AIDO1_AMD_DTUPD_H
+#define AIDO1_AMD_DTUPD_H
+
+#include <stdint.h>
+
+#include "dtsim.h"
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* z[n][oy][ox][co] = sum_k x[n][ST*oy + kh][ST*ox + kw][ci] * w[co][k]  (no bias)
+ *   x  device f32 [n, IH, IW, C_in];  w  device f32 [32, K];  z  device f32 [n, OH, OW, 32] */
+int dt_upd_conv_fwd(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih, int32_t iw,
+                    const float* x, const float* w, float* z, void* stream);
+
+/* Floats of scratch dt_upd_conv_wgrad needs for these dimensions (per-chunk
+ * partial weight gradients, reduced in a fixed order: deterministic). */
+int64_t dt_upd_wgrad_work_floats(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih,
+                                 int32_t iw);
+
+/* dw[co][k] = sum over the n * OH * OW output pixels of dz[pixel][co] * the
+ * pixel's input patch x[...][k] (torch.nn.grad.conv2d_weight).
+ *   dz device f32 [n, OH, OW, 32];  dw device f32 [32, K] out;
+ *   work device f32 [dt_upd_wgrad_work_floats(...)] */
+int dt_upd_conv_wgrad(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih, int32_t iw,
+                      const float* x, const float* dz, float* dw, float* work, void* stream);
+
+/* dx[n][ih][iw][ci] = sum over the (co, kh, kw) with ih = ST*oy + kh,
+ * iw = ST*ox + kw inside the output of dz[n][oy][ox][co] * w[co][kh][kw][ci]
+ * (torch.nn.grad.conv2d_input); C_in = 32 only (the first layer's input is
+ * the observation, which needs no gradient).  Every dx element is written.
+ *   dz device f32 [n, OH, OW, 32];  w [32, K];  dx device f32 [n, IH, IW, 32] out */
+int dt_upd_conv_dgrad(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih, int32_t iw,
+                      const float* dz, const float* w, float* dx, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* AIDO1_AMD_DTUPD_H */

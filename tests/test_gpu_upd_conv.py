@@ -1,0 +1,143 @@
+"""The DDPG update's convolutions (include/dtupd.h, csrc/dtupd.hip): forward,
+weight gradient and input gradient of config.json's four conv_2d layers
+against a float64 CPU restatement (torch's conv2d and torch.nn.grad), for
+batch sizes from 1 to past the persistent grid, and the train-mode conv
+blocks through autograd against the MIOpen path.  Tolerance: the kernels are
+an exact f32 fma chain per output (v_mfma_f32_32x32x2_f32) summed in another
+order, so |err| <= 2e-5 * (sum of |products|) is the bound written below
+(relative to the f64 result's scale)."""
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+LAYERS = [(3, 8, 2, 120, 160), (32, 4, 2, 57, 77), (32, 4, 2, 27, 37), (32, 4, 1, 12, 17)]
+CL = torch.channels_last
+
+
+def _data(cin, ks, n, ih, iw, seed):
+    g = torch.Generator().manual_seed(seed)
+    x = torch.rand(n, cin, ih, iw, generator=g, dtype=torch.float64) * 2 - 0.5
+    w = torch.randn(32, cin, ks, ks, generator=g, dtype=torch.float64) * (2.0 / (cin * ks * ks)) ** 0.5
+    return x, w
+
+
+def _lib_call(name, *args):
+    from aido1_amd import _lib
+    rc = getattr(_lib.lib(), name)(*args)
+    assert rc == 0, (name, rc)
+
+
+def _bound(ref_abs):
+    return 2e-5 * max(1.0, ref_abs)
+
+
+@pytest.mark.parametrize('layer', LAYERS)
+@pytest.mark.parametrize('n', [1, 5, 64])
+def test_forward_matches_f64(gpu, layer, n):
+    cin, ks, st, ih, iw = layer
+    if cin == 3 and n == 64:
+        n = 12                                   # CPU f64 reference time
+    x, w = _data(cin, ks, n, ih, iw, seed=n + ks)
+    ref = F.conv2d(x, w, stride=st)
+    xg = x.float().to(gpu).contiguous(memory_format=CL)
+    wg = w.float().to(gpu).contiguous(memory_format=CL)
+    z = torch.full(ref.shape, float('nan'), device=gpu).contiguous(memory_format=CL)
+    s = torch.cuda.current_stream().cuda_stream
+    _lib_call('dt_upd_conv_fwd', cin, ks, st, n, ih, iw, xg.data_ptr(), wg.data_ptr(), z.data_ptr(), s)
+    torch.cuda.synchronize()
+    scale = F.conv2d(x.abs(), w.abs(), stride=st).max().item()
+    err = (z.double().cpu() - ref).abs().max().item()
+    assert err <= _bound(scale), (err, scale)
+
+
+@pytest.mark.parametrize('layer', LAYERS)
+@pytest.mark.parametrize('n', [1, 7, 64])
+def test_weight_grad_matches_f64(gpu, layer, n):
+    cin, ks, st, ih, iw = layer
+    if cin == 3 and n == 64:
+        n = 12
+    x, w = _data(cin, ks, n, ih, iw, seed=3 * n + ks)
+    oh, ow = (ih - ks) // st + 1, (iw - ks) // st + 1
+    dz = torch.randn(n, 32, oh, ow, dtype=torch.float64, generator=torch.Generator().manual_seed(n))
+    ref = torch.nn.grad.conv2d_weight(x, w.shape, dz, stride=st)
+    from aido1_amd import _lib
+    L = _lib.lib()
+    xg = x.float().to(gpu).contiguous(memory_format=CL)
+    dzg = dz.float().to(gpu).contiguous(memory_format=CL)
+    dw = torch.full(w.shape, float('nan'), device=gpu).contiguous(memory_format=CL)
+    work = torch.empty(int(L.dt_upd_wgrad_work_floats(cin, ks, st, n, ih, iw)), device=gpu)
+    s = torch.cuda.current_stream().cuda_stream
+    _lib_call('dt_upd_conv_wgrad', cin, ks, st, n, ih, iw, xg.data_ptr(), dzg.data_ptr(),
+              dw.data_ptr(), work.data_ptr(), s)
+    torch.cuda.synchronize()
+    scale = torch.nn.grad.conv2d_weight(x.abs(), w.shape, dz.abs(), stride=st).max().item()
+    err = (dw.double().cpu() - ref).abs().max().item()
+    assert err <= _bound(scale), (err, scale)
+
+
+@pytest.mark.parametrize('layer', LAYERS[1:])
+@pytest.mark.parametrize('n', [1, 6, 64])
+def test_input_grad_matches_f64(gpu, layer, n):
+    cin, ks, st, ih, iw = layer
+    x, w = _data(cin, ks, n, ih, iw, seed=5 * n + ks)
+    oh, ow = (ih - ks) // st + 1, (iw - ks) // st + 1
+    dz = torch.randn(n, 32, oh, ow, dtype=torch.float64, generator=torch.Generator().manual_seed(n))
+    ref = torch.nn.grad.conv2d_input(x.shape, w, dz, stride=st)
+    wg = w.float().to(gpu).contiguous(memory_format=CL)
+    dzg = dz.float().to(gpu).contiguous(memory_format=CL)
+    dx = torch.full(x.shape, float('nan'), device=gpu).contiguous(memory_format=CL)
+    s = torch.cuda.current_stream().cuda_stream
+    _lib_call('dt_upd_conv_dgrad', cin, ks, st, n, ih, iw, dzg.data_ptr(), wg.data_ptr(),
+              dx.data_ptr(), s)
+    torch.cuda.synchronize()
+    scale = torch.nn.grad.conv2d_input(x.shape, w.abs(), dz.abs(), stride=st).max().item()
+    got = dx.double().cpu()
+    assert torch.isfinite(got).all()          # every element written (untouched rows: 0)
+    err = (got - ref).abs().max().item()
+    assert err <= _bound(scale), (err, scale)
+
+
+def test_rejects_other_geometry(gpu):
+    from aido1_amd import _lib
+    L = _lib.lib()
+    assert L.dt_upd_conv_fwd(32, 3, 1, 1, 12, 17, 0, 0, 0, None) != 0
+    assert L.dt_upd_wgrad_work_floats(16, 4, 2, 1, 57, 77) == -1
+    assert L.dt_upd_conv_dgrad(3, 8, 2, 1, 120, 160, 0, 0, 0, None) != 0
+
+
+def test_conv_block_autograd_matches_miopen(gpu):
+    """A train-mode config.json critic on the dtupd.h convolutions vs the same
+    network on MIOpen (train_ops.UPD_CONV_LAYERS emptied): outputs and every
+    parameter gradient."""
+    from conftest import golden
+    from test_trainer import no_dropout
+
+    from aido1_amd import train_ops
+    from aido1_amd.actor import ConfigCritic
+    cfg = golden('reference_config.json')
+    torch.manual_seed(4)
+    crit = ConfigCritic(no_dropout(cfg['model']['critic'])).to(gpu).to(memory_format=CL).train()
+    obs = torch.rand(16, 3, 120, 160, device=gpu).contiguous(memory_format=CL)
+    act = torch.rand(16, 2, device=gpu)
+
+    def run():
+        for p in crit.parameters():
+            p.grad = None
+        q = crit(obs, act)
+        q.sum().backward()
+        return q.detach().clone(), [p.grad.detach().clone() for p in crit.parameters()]
+
+    state = {k: v.clone() for k, v in crit.state_dict().items()}
+    q1, g1 = run()
+    crit.load_state_dict(state)
+    saved = set(train_ops.UPD_CONV_LAYERS)
+    train_ops.UPD_CONV_LAYERS.clear()
+    try:
+        q0, g0 = run()
+    finally:
+        train_ops.UPD_CONV_LAYERS.update(saved)
+    assert torch.allclose(q1, q0, rtol=1e-4, atol=1e-5)
+    for a, b in zip(g1, g0):
+        assert torch.allclose(a, b, rtol=1e-3, atol=1e-5 * max(1.0, b.abs().max().item()))
