@@ -19,7 +19,7 @@ LIB_PATH = os.path.join(PKG_DIR, 'libdtsim.so')
 CSRC = os.path.join(PKG_DIR, 'csrc')
 SOURCES = ['dtsim.hip', 'dtrender.hip', 'dtreplay.hip', 'dtactor.hip', 'dtconv.hip',
            'dttrain.hip', 'dtupd.hip']
-HEADERS = ['dtsim_common.h', 'dtrender.h']
+HEADERS = ['dtsim_common.h', 'dtrender.h', 'dtsync.h']
 PUBLIC_HEADERS = ['dtsim.h', 'dtreplay.h', 'dtactor.h', 'dttrain.h', 'dtupd.h']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ABI_VERSION = 8
@@ -171,6 +171,11 @@ def lib():
             'dt_guard_scan': (ctypes.c_int, [i32, vp, vp, vp]),
             # dtupd.h
             'dt_upd_conv_fwd': (ctypes.c_int, [i32, i32, i32, i32, i32, i32, vp, vp, vp, vp]),
+            'dt_upd_conv_fwd_bn': (ctypes.c_int, [i32, i32, i32, i32, i32, i32, vp, vp, vp,
+                                                  ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                                  vp, vp, vp, i32, vp, vp, vp, vp, vp]),
+            'dt_bn_leaky_apply': (ctypes.c_int, [i64, vp, vp, ctypes.c_float, vp, vp, vp, vp,
+                                                 vp]),
             'dt_upd_wgrad_work_floats': (i64, [i32, i32, i32, i32, i32, i32]),
             'dt_upd_conv_wgrad': (ctypes.c_int, [i32, i32, i32, i32, i32, i32, vp, vp, vp, vp,
                                                  vp]),

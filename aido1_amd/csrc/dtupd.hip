@@ -22,7 +22,9 @@
 
 #include <cstdint>
 
+#include "../../include/dttrain.h"
 #include "../../include/dtupd.h"
+#include "dtsync.h"
 
 namespace {
 
@@ -78,14 +80,99 @@ __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >
 
 constexpr int kThreads = 256;   // 4 waves
 
+// The train-mode BatchNorm after a block's conv -> LeakyReLU, fused into the
+// forward's epilogue (STATS): the batch statistics of a = leaky(z + bias).
+// A lane's accumulator column is one output channel for every tile, so each
+// lane keeps a Welford (count, mean, M2) of its channel across its tiles
+// (each tile two-pass over its <= 16 rows, Chan-merged in); at the end the
+// lane pairs and the waves merge, each workgroup writes its partial through
+// to memory, and the last to arrive merges them all (dtsync.h), writes
+// mean / invstd and moves the running statistics `updates` times, as
+// dt_bn_leaky_fwd does.
+struct FwdBn {
+  const float* bias;
+  float slope, eps, momentum;
+  float* running_mean;
+  float* running_var;
+  int64_t* nbt;
+  int updates;
+  float* mean_invstd;
+  float* work;     // [kMaxGrid][32][3] partials, then the counters (dt_train_work_floats)
+  int32_t* guard;
+};
+constexpr int kMaxGrid = 256;   // dttrain.hip's partial area
+
+template <int NT>
+__device__ void merge_partials_last(const FwdBn& fb, float cnt, float mean, float m2, int64_t m) {
+  __shared__ float red[NT / 64][32][3];
+  __shared__ float red2[NT / 32][32][3];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // lane pairs (l, l ^ 32) hold the same channel
+  chan(cnt, mean, m2, __shfl_xor(cnt, 32), __shfl_xor(mean, 32), __shfl_xor(m2, 32));
+  if (lane < 32) {
+    red[wave][lane][0] = cnt;
+    red[wave][lane][1] = mean;
+    red[wave][lane][2] = m2;
+  }
+  __syncthreads();
+  float* part = fb.work;
+  if (tid < 32) {
+    float cn = 0.0f, cm = 0.0f, cq = 0.0f;
+    for (int w = 0; w < NT / 64; ++w) chan(cn, cm, cq, red[w][tid][0], red[w][tid][1], red[w][tid][2]);
+    float* p = part + ((size_t)blockIdx.x * 32 + tid) * 3;
+    st_wt(p, cn);
+    st_wt(p + 1, cm);
+    st_wt(p + 2, cq);
+  }
+  unsigned int* counters = reinterpret_cast<unsigned int*>(part + (size_t)kMaxGrid * 32 * 3);
+  if (!last_arrival(&counters[0])) return;
+  acquire_partials();
+  {
+    constexpr int kFin = NT / 32;                   // threads a channel
+    const int ch = tid & 31, j = tid >> 5;
+    float cn = 0.0f, cm = 0.0f, cq = 0.0f;
+    for (int g = j; g < (int)gridDim.x; g += kFin) {
+      const float* p = part + ((size_t)g * 32 + ch) * 3;
+      const float pn = ld_wt(p), pm = ld_wt(p + 1), pq = ld_wt(p + 2);
+      st_wt(part + ((size_t)g * 32 + ch) * 3, 0.0f);   // counts back to zero (dtsync.h)
+      chan(cn, cm, cq, pn, pm, pq);
+    }
+    red2[j][ch][0] = cn;
+    red2[j][ch][1] = cm;
+    red2[j][ch][2] = cq;
+  }
+  __syncthreads();
+  if (tid < 32) {
+    float cn = 0.0f, cm = 0.0f, cq = 0.0f;
+    for (int s = 0; s < NT / 32; ++s) chan(cn, cm, cq, red2[s][tid][0], red2[s][tid][1], red2[s][tid][2]);
+    const float var = cq / cn;
+    const float invstd = 1.0f / sqrtf(var + fb.eps);
+    fb.mean_invstd[tid] = cm;
+    fb.mean_invstd[32 + tid] = invstd;
+    const bool lost = m < (int64_t(1) << 24) ? cn != (float)m : fabsf(cn - (float)m) > 1e-6f * (float)m;
+    guard_raise(fb.guard, DT_GUARD_BN_COUNT, lost);
+    guard_raise(fb.guard, DT_GUARD_BN_FWD, !finitef(cm) || !finitef(invstd));
+    const float unbiased = cn > 1.0f ? cq / (cn - 1.0f) : var;
+    float rm = fb.running_mean[tid], rv = fb.running_var[tid];
+    for (int u = 0; u < fb.updates; ++u) {
+      rm = (1.0f - fb.momentum) * rm + fb.momentum * cm;
+      rv = (1.0f - fb.momentum) * rv + fb.momentum * unbiased;
+    }
+    fb.running_mean[tid] = rm;
+    fb.running_var[tid] = rv;
+    if (tid == 0 && fb.nbt) fb.nbt[0] += fb.updates;
+  }
+}
+
 // ---- forward ---------------------------------------------------------------------------
 // A workgroup holds W in LDS ([32][K + 4]: row stride 4 floats past K, so the
 // 32 output-channel lanes of a B read fall on distinct banks) and walks
 // 32-pixel tiles of one sample each; KSPLIT waves share a tile, each a slice
 // of K, summed through LDS (the small layers: more waves than tiles).
-template <class G, int KSPLIT>
+template <class G, int KSPLIT, bool STATS>
 __global__ void __launch_bounds__(kThreads)
-fwd_kernel(int n, const float* __restrict__ x, const float* __restrict__ w, float* __restrict__ z) {
+fwd_kernel(int n, const float* __restrict__ x, const float* __restrict__ w, float* __restrict__ z,
+           FwdBn fb) {
   constexpr int WST = G::K + 4;
   constexpr int GP = 4 / KSPLIT;                 // tiles a workgroup round
   constexpr int SPW = G::KSTEPS / KSPLIT;        // k-steps a wave
@@ -102,6 +189,8 @@ fwd_kernel(int n, const float* __restrict__ x, const float* __restrict__ w, floa
   const int g = wave / KSPLIT, ks = wave - g * KSPLIT;
   const int tiles = n * G::TPS;
   const float* wrow = ws + col * WST + 4 * kk;
+  float w_n = 0.0f, w_mean = 0.0f, w_m2 = 0.0f;    // STATS: this lane's channel
+  const float bc = STATS ? fb.bias[col] : 0.0f;
   for (int base = blockIdx.x * GP; base < tiles; base += gridDim.x * GP) {
     const int tile = base + g;
     const bool tvalid = tile < tiles;
@@ -140,8 +229,28 @@ fwd_kernel(int n, const float* __restrict__ x, const float* __restrict__ w, floa
         const int pr = tb * 32 + acc_row(r, kk);
         if (pr < G::OPIX) zs[pr * 32 + col] = acc[r];
       }
+      if constexpr (STATS) {   // a = leaky(z + bias), as dt_bn_leaky_fwd computes it
+        float a[16], tn = 0.0f, ts = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const bool ok = tb * 32 + acc_row(r, kk) < G::OPIX;
+          const float v = acc[r] + bc;
+          a[r] = v > 0.0f ? v : v * fb.slope;
+          tn += ok ? 1.0f : 0.0f;
+          ts += ok ? a[r] : 0.0f;
+        }
+        const float tm = ts / tn;
+        float tq = 0.0f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const float d = a[r] - tm;
+          tq += tb * 32 + acc_row(r, kk) < G::OPIX ? d * d : 0.0f;
+        }
+        chan(w_n, w_mean, w_m2, tn, tm, tq);
+      }
     }
   }
+  if constexpr (STATS) merge_partials_last<kThreads>(fb, w_n, w_mean, w_m2, (int64_t)n * G::OPIX);
 }
 
 // ---- weight gradient -------------------------------------------------------------------
@@ -305,16 +414,29 @@ int resident(const void* kern, int threads, int cap) {
   return g < cap ? g : cap;
 }
 
-template <class G, int KSPLIT>
-int launch_fwd(int n, const float* x, const float* w, float* z, hipStream_t s) {
+template <class G, int KSPLIT, bool STATS>
+int launch_fwd(int n, const float* x, const float* w, float* z, const FwdBn& fb, hipStream_t s) {
   constexpr int GP = 4 / KSPLIT;
   const int tiles = n * G::TPS;
   int grid = (tiles + GP - 1) / GP;
-  static const int res =
-      resident(reinterpret_cast<const void*>(fwd_kernel<G, KSPLIT>), kThreads, 1 << 20);
+  // STATS: at most kMaxGrid partials (the last arriver merges them)
+  static const int res = resident(reinterpret_cast<const void*>(fwd_kernel<G, KSPLIT, STATS>),
+                                  kThreads, STATS ? kMaxGrid : 1 << 20);
   grid = grid < res ? grid : res;
-  hipLaunchKernelGGL((fwd_kernel<G, KSPLIT>), dim3(grid), dim3(kThreads), 0, s, n, x, w, z);
+  hipLaunchKernelGGL((fwd_kernel<G, KSPLIT, STATS>), dim3(grid), dim3(kThreads), 0, s, n, x, w, z,
+                     fb);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
+template <bool STATS>
+int dispatch_fwd(int l, int n, const float* x, const float* w, float* z, const FwdBn& fb,
+                 hipStream_t s) {
+  switch (l) {
+    case 1: return launch_fwd<L1, 1, STATS>(n, x, w, z, fb, s);
+    case 2: return launch_fwd<L2, 1, STATS>(n, x, w, z, fb, s);
+    case 3: return launch_fwd<L3, 2, STATS>(n, x, w, z, fb, s);
+    default: return launch_fwd<L4, 4, STATS>(n, x, w, z, fb, s);
+  }
 }
 
 // chunks of the wgrad pixel range: about 1024 waves, partials capped at 2 M floats
@@ -370,13 +492,21 @@ int dt_upd_conv_fwd(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih, 
   const int l = layer_of(cin, ks, st, ih, iw);
   if (!l || n < 0 || (n > 0 && (!x || !w || !z))) return DT_E_ARG;
   if (n == 0) return DT_OK;
-  hipStream_t s = (hipStream_t)stream;
-  switch (l) {
-    case 1: return launch_fwd<L1, 1>(n, x, w, z, s);
-    case 2: return launch_fwd<L2, 1>(n, x, w, z, s);
-    case 3: return launch_fwd<L3, 2>(n, x, w, z, s);
-    default: return launch_fwd<L4, 4>(n, x, w, z, s);
-  }
+  return dispatch_fwd<false>(l, n, x, w, z, FwdBn{}, (hipStream_t)stream);
+}
+
+int dt_upd_conv_fwd_bn(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih, int32_t iw,
+                       const float* x, const float* w, const float* bias, float slope, float eps,
+                       float momentum, float* running_mean, float* running_var,
+                       int64_t* num_batches_tracked, int32_t updates, float* z,
+                       float* mean_invstd, float* work, int32_t* guard, void* stream) {
+  const int l = layer_of(cin, ks, st, ih, iw);
+  if (!l || n < 1 || updates < 1 || !x || !w || !z || !bias || !running_mean || !running_var ||
+      !mean_invstd || !work)
+    return DT_E_ARG;
+  const FwdBn fb{bias, slope, eps, momentum, running_mean, running_var, num_batches_tracked,
+                 (int)updates, mean_invstd, work, guard};
+  return dispatch_fwd<true>(l, n, x, w, z, fb, (hipStream_t)stream);
 }
 
 int64_t dt_upd_wgrad_work_floats(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih,

@@ -193,11 +193,87 @@ def upd_conv(x, conv):
     return _UpdConv.apply(x, conv.weight, int(conv.stride[0]))
 
 
+class _ConvBnLeaky(torch.autograd.Function):
+    """The whole train-mode block bn(leaky(conv(x) + bias)) on the GPU kernels:
+    forward dt_upd_conv_fwd_bn (convolution + the batch statistics in its
+    epilogue) and dt_bn_leaky_apply; backward dt_bn_leaky_bwd (BatchNorm,
+    LeakyReLU and bias gradients), then the convolution's weight and input
+    gradients (dt_upd_conv_wgrad / _dgrad).  Four to five kernels each way
+    where MIOpen plus the tail ran eight or more."""
+
+    @staticmethod
+    def forward(ctx, x, w, bias, gamma, beta, bn, slope, st):
+        cl = torch.channels_last
+        x = x.contiguous(memory_format=cl)
+        w = w.contiguous(memory_format=cl)
+        n, cin, ih, iw = x.shape
+        ks = w.shape[2]
+        oh, ow = (ih - ks) // st + 1, (iw - ks) // st + 1
+        L = _lib.lib()
+        z = torch.empty((n, C, oh, ow), device=x.device, dtype=x.dtype, memory_format=cl)
+        mi = torch.empty(2 * C, device=x.device)
+        nbt = bn.num_batches_tracked
+        s = _stream(x.device)
+        rc = L.dt_upd_conv_fwd_bn(cin, ks, st, n, ih, iw, x.data_ptr(), w.data_ptr(),
+                                  bias.data_ptr(), slope, bn.eps, bn.momentum,
+                                  bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
+                                  nbt.data_ptr() if nbt is not None else None,
+                                  int(getattr(bn, '_dt_updates', 1)), z.data_ptr(), mi.data_ptr(),
+                                  _work(bn, 'fwd', x.device).data_ptr(), _guard(bn), s)
+        if rc != 0:
+            raise _lib.DtError('dt_upd_conv_fwd_bn failed (%d)' % rc)
+        y = torch.empty_like(z)
+        rc = L.dt_bn_leaky_apply(z.numel() // C, z.data_ptr(), bias.data_ptr(), slope,
+                                 mi.data_ptr(), gamma.data_ptr(), beta.data_ptr(), y.data_ptr(), s)
+        if rc != 0:
+            raise _lib.DtError('dt_bn_leaky_apply failed (%d)' % rc)
+        ctx.save_for_backward(x, w, z, bias, mi, gamma)
+        ctx.bn, ctx.slope, ctx.st = bn, slope, st
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w, z, bias, mi, gamma = ctx.saved_tensors
+        cl = torch.channels_last
+        dy = dy.contiguous(memory_format=cl)
+        L = _lib.lib()
+        s = _stream(z.device)
+        dz = torch.empty_like(z)
+        g = torch.empty(3, C, device=z.device)      # dbias, dgamma, dbeta
+        rc = L.dt_bn_leaky_bwd(z.numel() // C, dy.data_ptr(), z.data_ptr(), bias.data_ptr(),
+                               mi.data_ptr(), gamma.data_ptr(), ctx.slope, dz.data_ptr(),
+                               g[0].data_ptr(), g[1].data_ptr(), g[2].data_ptr(),
+                               _work(ctx.bn, 'bwd', z.device).data_ptr(), _guard(ctx.bn), s)
+        if rc != 0:
+            raise _lib.DtError('dt_bn_leaky_bwd failed (%d)' % rc)
+        n, cin, ih, iw = x.shape
+        ks, st = w.shape[2], ctx.st
+        dx = dw = None
+        if ctx.needs_input_grad[1]:
+            work = torch.empty(int(L.dt_upd_wgrad_work_floats(cin, ks, st, n, ih, iw)),
+                               device=x.device)
+            dw = torch.empty_like(w)
+            rc = L.dt_upd_conv_wgrad(cin, ks, st, n, ih, iw, x.data_ptr(), dz.data_ptr(),
+                                     dw.data_ptr(), work.data_ptr(), s)
+            if rc != 0:
+                raise _lib.DtError('dt_upd_conv_wgrad failed (%d)' % rc)
+        if ctx.needs_input_grad[0]:
+            if cin != C:
+                dx = torch.nn.grad.conv2d_input(x.shape, w, dz, stride=st)
+            else:
+                dx = torch.empty_like(x)
+                rc = L.dt_upd_conv_dgrad(cin, ks, st, n, ih, iw, dz.data_ptr(), w.data_ptr(),
+                                         dx.data_ptr(), s)
+                if rc != 0:
+                    raise _lib.DtError('dt_upd_conv_dgrad failed (%d)' % rc)
+        return dx, dw, g[0], g[1], g[2], None, None, None
+
+
 def conv_leaky_bn(x, conv, act, bn):
     """bn(act(conv(x))) for a train-mode block (see the module docstring)."""
     if upd_conv_applicable(x, conv):
-        z = upd_conv(x, conv)
-    else:
-        z = F.conv2d(x, conv.weight, None, conv.stride)
+        return _ConvBnLeaky.apply(x, conv.weight, conv.bias, bn.weight, bn.bias, bn,
+                                  float(act.negative_slope), int(conv.stride[0]))
+    z = F.conv2d(x, conv.weight, None, conv.stride)
     z = z.contiguous(memory_format=torch.channels_last)
     return _BnLeaky.apply(z, conv.bias, bn.weight, bn.bias, bn, float(act.negative_slope))

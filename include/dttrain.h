@@ -72,6 +72,13 @@ int dt_bn_leaky_fwd(int64_t m, const float* z, const float* bias, float slope, c
                     float* running_var, int64_t* num_batches_tracked, int32_t updates, float* a,
                     float* y, float* mean_invstd, float* work, int32_t* guard, void* stream);
 
+/* The normalisation half of dt_bn_leaky_fwd alone, from statistics already
+ * in mean_invstd (dt_upd_conv_fwd_bn, include/dtupd.h):
+ * y = (leaky_relu(z + bias) - mean) * invstd * gamma + beta. */
+int dt_bn_leaky_apply(int64_t m, const float* z, const float* bias, float slope,
+                      const float* mean_invstd, const float* gamma, const float* beta, float* y,
+                      void* stream);
+
 /* Backward of dt_bn_leaky_fwd given dy (device f32 [m, 32]) and the forward's
  * z and bias (a = leaky_relu(z + bias, slope) recomputed):
  *   dgamma = sum(dy * xhat), dbeta = sum(dy), xhat = (a - mean) * invstd;

@@ -34,6 +34,20 @@ extern "C" {
 int dt_upd_conv_fwd(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih, int32_t iw,
                     const float* x, const float* w, float* z, void* stream);
 
+/* dt_upd_conv_fwd plus the block's train-mode BatchNorm statistics, fused
+ * into its epilogue (config.json's conv_2d -> leaky_relu -> batch_norm_2d):
+ * exactly dt_bn_leaky_fwd's statistics part (include/dttrain.h) -- batch
+ * mean / biased variance of a = leaky_relu(z + bias, slope) over the
+ * n * OH * OW pixels into mean_invstd [64], running_mean / running_var moved
+ * `updates` times, num_batches_tracked += updates, DT_GUARD_BN_* reports --
+ * without a second pass over z.  dt_bn_leaky_apply then normalises.
+ *   work  dt_train_work_floats(0) floats, zeroed once (left reusable) */
+int dt_upd_conv_fwd_bn(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih, int32_t iw,
+                       const float* x, const float* w, const float* bias, float slope, float eps,
+                       float momentum, float* running_mean, float* running_var,
+                       int64_t* num_batches_tracked, int32_t updates, float* z,
+                       float* mean_invstd, float* work, int32_t* guard, void* stream);
+
 /* Floats of scratch dt_upd_conv_wgrad needs for these dimensions (per-chunk
  * partial weight gradients, reduced in a fixed order: deterministic). */
 int64_t dt_upd_wgrad_work_floats(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih,
