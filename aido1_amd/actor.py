@@ -331,7 +331,7 @@ class FusedActor(nn.Module):
         if self.mode == 'reference':
             ws = [c.weight for c in convs]
             bs = [c.bias for c in convs]
-            torch._foreach_copy_(
+            copy_grouped(
                 list(self.w) + list(self.b) + list(self.gamma) + list(self.beta) +
                 [self.w1, self.b1, self.w2, self.b2],
                 ws + bs + [bn.weight for bn in bns] + [bn.bias for bn in bns] +
@@ -608,6 +608,23 @@ class FusedActor(nn.Module):
             # flatten in NCHW order, as the reference's view(x.size(0), -1)
             x = x.contiguous().flatten(1)
         return self._head(x)
+
+
+def copy_grouped(dsts, srcs):
+    """dst.copy_(src) for every pair, one torch._foreach_copy_ per (dst dtype,
+    src dtype) group.  A single _foreach_copy_ over destinations of mixed
+    dtypes is NOT safe on this ROCm build: its multi-tensor kernel wrote the
+    fp16 conversion of the sources into the float32 destinations too (the
+    reference-mode actor's BatchNorm gamma / beta held fp16 bit pairs in their
+    first half and stale memory in the rest -- NaN after a test that left NaN
+    in freed memory; tools/nan_repro.py)."""
+    groups = {}
+    for d, s in zip(dsts, srcs):
+        groups.setdefault((d.dtype, s.dtype, d.device), ([], []))
+        groups[(d.dtype, s.dtype, d.device)][0].append(d)
+        groups[(d.dtype, s.dtype, d.device)][1].append(s)
+    for ds, ss in groups.values():
+        torch._foreach_copy_(ds, ss)
 
 
 def conv1_fragments(w):

@@ -337,3 +337,33 @@ def test_fused_head_matches_torch_head(gpu, n, n0):
     ref = torch.cat([fa._head(flat[:n0]), fb._head(flat[n0:])])
     assert torch.isfinite(out).all()
     assert torch.allclose(out, ref, rtol=0, atol=1e-3), (out - ref).abs().max()
+
+
+@pytest.mark.parametrize('channels_last', [False, True])
+def test_refresh_copies_every_parameter_exactly(gpu, channels_last):
+    """FusedActor.refresh (reference mode, fp16) copies every weight, bias,
+    gamma and beta of the source actor, whatever memory the caching allocator
+    hands it: free blocks are filled with NaN first.  A single mixed-dtype
+    torch._foreach_copy_ wrote the fp16 conversion into the float32 gamma /
+    beta on this ROCm build (round 4; actor.copy_grouped)."""
+    from aido1_amd.actor import ConfigActor, FusedActor
+    held = [torch.full((4096,), float('nan'), device=gpu) for _ in range(64)]
+    del held
+    torch.manual_seed(9)
+    a = ConfigActor(golden('reference_config.json')['model']['actor']).to(gpu)
+    with torch.no_grad():
+        for p in a.parameters():
+            p.add_(torch.randn_like(p) * 0.1)
+    if channels_last:
+        a = a.to(memory_format=torch.channels_last)
+    f = FusedActor(a, dtype=torch.float16, mode='reference')
+    torch.cuda.synchronize()
+    convs, bns, lin1, lin2 = a.layers()
+    for i in range(4):
+        assert torch.equal(f.w[i].float(), convs[i].weight.detach().half().float()), i
+        assert torch.equal(f.b[i].float(), convs[i].bias.detach().half().float()), i
+        assert torch.equal(f.gamma[i], bns[i].weight.detach()), i
+        assert torch.equal(f.beta[i], bns[i].bias.detach()), i
+    for mine, src in ((f.w1, lin1.weight), (f.b1, lin1.bias), (f.w2, lin2.weight),
+                      (f.b2, lin2.bias)):
+        assert torch.equal(mine.float(), src.detach().half().float())

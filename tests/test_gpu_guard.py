@@ -135,7 +135,12 @@ def test_train_loop_names_the_actor_output(gpu):
     loop.reset()
     for _ in range(3):
         loop.step()
-    assert loop.check()['tick'] == 3
+    try:
+        rec = loop.check()
+    except NonFiniteError:
+        _report_rollout_state(loop)
+        raise
+    assert rec['tick'] == 3
     bad = loop.trainer.actor.net.input_nets[0].internal_modules[0].kernel.weight.detach().clone()
     bad[0, 0, 0, 0] = NAN
     loop.rollout.actor.refresh(_with_conv1(loop.trainer.actor, bad))
@@ -144,6 +149,26 @@ def test_train_loop_names_the_actor_output(gpu):
         loop.check()
     assert str(e.value).split('non-finite values at ')[1].startswith('actor_out')
     assert BIT['actor_out'] == 0
+
+
+def _report_rollout_state(loop):
+    """Which of the rollout's tensors hold NaN / Inf (printed on failure)."""
+    r = loop.rollout
+    named = [('ring', r.ring), ('actor_out', r.actor_out), ('actions', r.actions)]
+    for tag, a in (('actor', r.actor), ('exploit', r.exploit_actor)):
+        if a is None:
+            continue
+        named += [(tag + '.' + k, v) for k, v in a.named_parameters()]
+        named += [(tag + '.' + k, v) for k, v in a.named_buffers()]
+        named += [(tag + '._bufs.' + k, v) for k, v in (getattr(a, '_bufs', None) or {}).items()
+                  if v is not None]
+    named += [('trainer.actor.' + k, v) for k, v in loop.trainer.actor.named_parameters()]
+    for k, v in named:
+        bad = (~torch.isfinite(v.float())).sum().item()
+        if bad:
+            rows = (~torch.isfinite(v.float().reshape(v.shape[0], -1))).any(1).nonzero()
+            print('NONFINITE %s shape %s: %d elements, rows %s' % (k, tuple(v.shape), bad,
+                                                                 rows.flatten()[:16].tolist()))
 
 
 def _with_conv1(actor, w):

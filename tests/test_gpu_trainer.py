@@ -41,7 +41,12 @@ def test_train_loop_runs(gpu, prioritized, graph, size):
         loop.step()
     # the guards name the first stage that produced NaN / Inf (and the
     # replay's rejected priorities), before any assertion on the results
-    rec = loop.check()
+    try:
+        rec = loop.check()
+    except Exception:
+        from test_gpu_guard import _report_rollout_state
+        _report_rollout_state(loop)
+        raise
     assert rec['tick'] == 12
     assert len(loop.replay) == size and loop.updates == 12 and loop.decisions == 12
     assert torch.isfinite(loop.metrics['critic_loss']) and torch.isfinite(loop.metrics['actor_loss'])

@@ -50,6 +50,19 @@ def main():
                            'reference_config.json')) as f:
         cfg = json.load(f)
     n = int(os.environ.get('ENVS', '128'))
+    if os.environ.get('POISON'):
+        # the caching allocator's free blocks full of NaN: any buffer read
+        # before it is written then shows up as non-finite
+        held = []
+        for mb in (1, 2, 4, 8, 16, 32, 64, 128, 256, 512):
+            for _ in range(3):
+                held.append(torch.full((mb << 18,), float('nan'), device='cuda'))
+        for kb in (1, 4, 16, 64, 256):
+            for _ in range(16):
+                held.append(torch.full((kb << 8,), float('nan'), device='cuda'))
+        torch.cuda.synchronize()
+        del held
+        print('poisoned the caching allocator')
     torch.manual_seed(5)
     roll = ActorRollout(cfg, n, device=0, seed=5)
     roll.reset()
