@@ -254,47 +254,60 @@ fwd_kernel(int n, const float* __restrict__ x, const float* __restrict__ w, floa
 }
 
 // ---- weight gradient -------------------------------------------------------------------
-// Workgroup c sums the output pixels [c * pc, (c + 1) * pc) of all samples
-// (flattened n * OPIX); its WAVES waves take NBW 32-wide blocks of k each, so
-// a dZ value is loaded once per wave for NBW blocks.  8 pixels a step (the
-// float4 trick along the pixel index: lane (co, kk) holds dZ of pixels
-// q0 + 4kk + e).  The partial dW of the chunk goes to part[c] and
-// wgrad_reduce_kernel sums the chunks in index order.
+// A workgroup takes whole output rows (sample s, row oy): it stages the KS
+// input rows that row reads (KS * IW * C_in contiguous floats of NHWC) and
+// the row's dZ (OW * 32) in LDS with float4 loads, then every wave runs its
+// NBW 32-wide blocks of k over the row's pixels two at a time (the MFMA's two
+// k-slots): A = dZ[pixel][co] (lane co), B = the pixel's patch value k (lane
+// k), both LDS reads.  An input pixel is read from HBM once per output row
+// that needs it, not once per (pixel, tap).  The workgroup's partial dW goes
+// to part[blockIdx.x]; wgrad_reduce_kernel sums them in index order.
+constexpr int kWgradMaxGrid = 256;
+
 template <class G, int NBW, int WAVES>
 __global__ void __launch_bounds__(64 * WAVES)
-wgrad_kernel(int n, int pc, const float* __restrict__ x, const float* __restrict__ dz,
+wgrad_kernel(int n, const float* __restrict__ x, const float* __restrict__ dz,
              float* __restrict__ part) {
   static_assert(WAVES * NBW * 32 == G::K, "the waves cover K");
+  constexpr int XROW = G::IW * G::CIN;       // floats of one input row
+  constexpr int XT = G::KS * XROW;           // the rows one output row reads
+  constexpr int DT = G::OW * 32;
+  static_assert(XROW % 4 == 0 && DT % 4 == 0, "float4 staging");
+  constexpr int NT = 64 * WAVES;
+  __shared__ __attribute__((aligned(16))) float xs[XT];
+  __shared__ __attribute__((aligned(16))) float ds[DT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 31, kk = lane >> 5;
-  const int P = n * G::OPIX;
-  const int q_beg = blockIdx.x * pc;
-  const int q_end = q_beg + pc < P ? q_beg + pc : P;
-  int ko[NBW];
+  int kr[NBW];   // k's offset inside the staged rows
 #pragma unroll
-  for (int b = 0; b < NBW; ++b) ko[b] = G::koff((wave * NBW + b) * 32 + col);
+  for (int b = 0; b < NBW; ++b) {
+    const int k = (wave * NBW + b) * 32 + col;
+    kr[b] = (k / G::KROW) * XROW + k % G::KROW;
+  }
   f32x16 acc[NBW];
 #pragma unroll
   for (int b = 0; b < NBW; ++b)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[b][r] = 0.0f;
-  for (int q0 = q_beg; q0 < q_end; q0 += 8) {
-    float av[4];
-    int xb[4];
+  const int rows = n * G::OH;
+  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+    const int sm = row / G::OH, oy = row - sm * G::OH;
+    __syncthreads();                                    // the previous row's reads
+    const float4* xsrc = reinterpret_cast<const float4*>(x + (size_t)(sm * G::IH + G::ST * oy) * XROW);
+    for (int i = tid; i < XT / 4; i += NT) reinterpret_cast<float4*>(xs)[i] = xsrc[i];
+    const float4* dsrc = reinterpret_cast<const float4*>(dz + (size_t)row * DT);
+    for (int i = tid; i < DT / 4; i += NT) reinterpret_cast<float4*>(ds)[i] = dsrc[i];
+    __syncthreads();
+#pragma unroll 2
+    for (int ox0 = 0; ox0 < G::OW; ox0 += 2) {
+      const int ox = ox0 + kk;
+      const bool ok = ox < G::OW;
+      const float a = ok ? ds[ox * 32 + col] : 0.0f;
+      const int xo = (ok ? ox : 0) * G::ST * G::CIN;
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int q = q0 + 4 * kk + e;
-      const bool ok = q < q_end;
-      const int qc = ok ? q : q_beg;
-      const int s = qc / G::OPIX, p = qc - s * G::OPIX;
-      av[e] = ok ? dz[(size_t)qc * 32 + col] : 0.0f;
-      xb[e] = G::xbase(s, p);
+      for (int b = 0; b < NBW; ++b)
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, xs[xo + kr[b]], acc[b], 0, 0, 0);
     }
-#pragma unroll
-    for (int b = 0; b < NBW; ++b)
-#pragma unroll
-      for (int e = 0; e < 4; ++e)
-        acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(av[e], x[xb[e] + ko[b]], acc[b], 0, 0, 0);
   }
   // D[co][k]: lane (k = block * 32 + col), rows co
   float* pp = part + (size_t)blockIdx.x * 32 * G::K;
@@ -305,13 +318,22 @@ wgrad_kernel(int n, int pc, const float* __restrict__ x, const float* __restrict
       pp[acc_row(r, kk) * G::K + (wave * NBW + b) * 32 + col] = acc[b][r];
 }
 
+// dw[i] = sum of the chunks' partials, chunk order fixed (four interleaved
+// running sums, then summed: deterministic)
 __global__ void __launch_bounds__(256)
 wgrad_reduce_kernel(int chunks, int len, const float* __restrict__ part, float* __restrict__ dw) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= len) return;
-  float s = 0.0f;
-  for (int c = 0; c < chunks; ++c) s += part[(size_t)c * len + i];
-  dw[i] = s;
+  float s0 = 0.0f, s1 = 0.0f, s2 = 0.0f, s3 = 0.0f;
+  int c = 0;
+  for (; c + 4 <= chunks; c += 4) {
+    s0 += part[(size_t)c * len + i];
+    s1 += part[(size_t)(c + 1) * len + i];
+    s2 += part[(size_t)(c + 2) * len + i];
+    s3 += part[(size_t)(c + 3) * len + i];
+  }
+  for (; c < chunks; ++c) s0 += part[(size_t)c * len + i];
+  dw[i] = (s0 + s1) + (s2 + s3);
 }
 
 // ---- input gradient (C_in = 32) ----------------------------------------------------------
@@ -439,25 +461,18 @@ int dispatch_fwd(int l, int n, const float* x, const float* w, float* z, const F
   }
 }
 
-// chunks of the wgrad pixel range: about 1024 waves, partials capped at 2 M floats
-template <class G, int WAVES>
-int wgrad_chunks(int n, int* pc) {
-  const int P = n * G::OPIX;
-  int chunks = 1024 / WAVES;
-  const int cap = (2 << 20) / (32 * G::K);
-  chunks = chunks < cap ? chunks : cap;
-  int c = (P + chunks - 1) / chunks;
-  c = (c + 7) / 8 * 8;
-  *pc = c;
-  return (P + c - 1) / c;
+// workgroups (= partials) of a weight-gradient launch
+template <class G>
+int wgrad_chunks(int n) {
+  const int rows = n * G::OH;
+  return rows < kWgradMaxGrid ? rows : kWgradMaxGrid;
 }
 
 template <class G, int NBW, int WAVES>
 int launch_wgrad(int n, const float* x, const float* dz, float* dw, float* work, hipStream_t s) {
-  int pc = 0;
-  const int chunks = wgrad_chunks<G, WAVES>(n, &pc);
-  hipLaunchKernelGGL((wgrad_kernel<G, NBW, WAVES>), dim3(chunks), dim3(64 * WAVES), 0, s, n, pc,
-                     x, dz, work);
+  const int chunks = wgrad_chunks<G>(n);
+  hipLaunchKernelGGL((wgrad_kernel<G, NBW, WAVES>), dim3(chunks), dim3(64 * WAVES), 0, s, n, x,
+                     dz, work);
   const int len = 32 * G::K;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((len + 255) / 256), dim3(256), 0, s, chunks, len,
                      work, dw);
@@ -511,12 +526,12 @@ int dt_upd_conv_fwd_bn(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t i
 
 int64_t dt_upd_wgrad_work_floats(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih,
                                  int32_t iw) {
-  int pc = 0;
+  if (n < 1) return -1;
   switch (layer_of(cin, ks, st, ih, iw)) {
-    case 1: return (int64_t)wgrad_chunks<L1, 2>(n, &pc) * 32 * L1::K;
-    case 2: return (int64_t)wgrad_chunks<L2, 4>(n, &pc) * 32 * L2::K;
-    case 3: return (int64_t)wgrad_chunks<L3, 4>(n, &pc) * 32 * L3::K;
-    case 4: return (int64_t)wgrad_chunks<L4, 4>(n, &pc) * 32 * L4::K;
+    case 1: return (int64_t)wgrad_chunks<L1>(n) * 32 * L1::K;
+    case 2: return (int64_t)wgrad_chunks<L2>(n) * 32 * L2::K;
+    case 3: return (int64_t)wgrad_chunks<L3>(n) * 32 * L3::K;
+    case 4: return (int64_t)wgrad_chunks<L4>(n) * 32 * L4::K;
     default: return -1;
   }
 }
