@@ -177,6 +177,7 @@ def lib():
             'dt_bn_leaky_apply': (ctypes.c_int, [i64, vp, vp, ctypes.c_float, vp, vp, vp, vp,
                                                  vp]),
             'dt_upd_wgrad_work_floats': (i64, [i32, i32, i32, i32, i32, i32]),
+            'dt_upd_bn_work_floats': (i64, []),
             'dt_upd_conv_wgrad': (ctypes.c_int, [i32, i32, i32, i32, i32, i32, vp, vp, vp, vp,
                                                  vp]),
             'dt_upd_conv_dgrad': (ctypes.c_int, [i32, i32, i32, i32, i32, i32, vp, vp, vp, vp]),

@@ -43,7 +43,9 @@ def _work(bn, key, dev):
     name = '_dt_work_' + key
     w = getattr(bn, name, None)
     if w is None or w.device != dev:
-        w = torch.zeros(int(_lib.lib().dt_train_work_floats(0)), device=dev)
+        L = _lib.lib()
+        size = L.dt_upd_bn_work_floats() if key == 'upd' else L.dt_train_work_floats(0)
+        w = torch.zeros(int(size), device=dev)
         setattr(bn, name, w)
     return w
 
@@ -219,7 +221,7 @@ class _ConvBnLeaky(torch.autograd.Function):
                                   bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
                                   nbt.data_ptr() if nbt is not None else None,
                                   int(getattr(bn, '_dt_updates', 1)), z.data_ptr(), mi.data_ptr(),
-                                  _work(bn, 'fwd', x.device).data_ptr(), _guard(bn), s)
+                                  _work(bn, 'upd', x.device).data_ptr(), _guard(bn), s)
         if rc != 0:
             raise _lib.DtError('dt_upd_conv_fwd_bn failed (%d)' % rc)
         y = torch.empty_like(z)

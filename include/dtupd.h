@@ -41,12 +41,15 @@ int dt_upd_conv_fwd(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih, 
  * n * OH * OW pixels into mean_invstd [64], running_mean / running_var moved
  * `updates` times, num_batches_tracked += updates, DT_GUARD_BN_* reports --
  * without a second pass over z.  dt_bn_leaky_apply then normalises.
- *   work  dt_train_work_floats(0) floats, zeroed once (left reusable) */
+ *   work  dt_upd_bn_work_floats() floats, zeroed once (left reusable); not
+ *         shared with dt_bn_leaky_fwd's (another partial layout) */
 int dt_upd_conv_fwd_bn(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih, int32_t iw,
                        const float* x, const float* w, const float* bias, float slope, float eps,
                        float momentum, float* running_mean, float* running_var,
                        int64_t* num_batches_tracked, int32_t updates, float* z,
                        float* mean_invstd, float* work, int32_t* guard, void* stream);
+
+int64_t dt_upd_bn_work_floats(void);
 
 /* Floats of scratch dt_upd_conv_wgrad needs for these dimensions (per-chunk
  * partial weight gradients, reduced in a fixed order: deterministic). */
