@@ -202,27 +202,13 @@ fwd_kernel(int n, const float* __restrict__ x, const float* __restrict__ w, floa
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-    // the A loads run kPre steps ahead through a register ring (a global
-    // load's latency is many steps of four MFMAs)
     const int s0 = ks * SPW;
-    constexpr int kPre = 8;
-    static_assert(SPW % kPre == 0, "whole prefetch rounds");
-    float4 pa[kPre];
-#pragma unroll
-    for (int i = 0; i < kPre; ++i) pa[i] = ld4<G::CIN>(xl + G::koff(8 * (s0 + i)));
-#pragma unroll 1
-    for (int st0 = 0; st0 < SPW; st0 += kPre) {
-#pragma unroll
-      for (int i = 0; i < kPre; ++i) {
-        const int st = st0 + i;
-        const int kc = 8 * (s0 + st);
-        const float4 a = pa[i];
-        // the last round re-loads its own step (in bounds, unused)
-        const int nx = st + kPre < SPW ? st + kPre : st;
-        pa[i] = ld4<G::CIN>(xl + G::koff(8 * (s0 + nx)));
-        const float4 b = *reinterpret_cast<const float4*>(wrow + kc);
-        acc = mfma4(a, b, acc);
-      }
+#pragma unroll 4
+    for (int st = 0; st < SPW; ++st) {
+      const int kc = 8 * (s0 + st);
+      const float4 a = ld4<G::CIN>(xl + G::koff(kc));
+      const float4 b = *reinterpret_cast<const float4*>(wrow + kc);
+      acc = mfma4(a, b, acc);
     }
     if constexpr (KSPLIT > 1) {
       if (ks > 0)
@@ -267,6 +253,80 @@ fwd_kernel(int n, const float* __restrict__ x, const float* __restrict__ w, floa
   if constexpr (STATS) merge_partials_last<kThreads>(fb, w_n, w_mean, w_m2, (int64_t)n * G::OPIX);
 }
 
+// ---- forward, whole output rows (the 3-channel observation layer) ----------------------
+// The 8 input rows one output row reads (8 x 160 x 3 floats, contiguous in
+// NHWC) are staged in LDS once, so the im2col reads (3.85 per staged float)
+// are LDS reads; three waves take the row's three 32-pixel tiles (77 pixels).
+template <class G, bool STATS>
+__global__ void __launch_bounds__(192)
+fwd_row_kernel(int n, const float* __restrict__ x, const float* __restrict__ w,
+               float* __restrict__ z, FwdBn fb) {
+  constexpr int NT = 192;
+  constexpr int WST = G::K + 4;
+  constexpr int XROW = G::IW * G::CIN;
+  constexpr int XT = G::KS * XROW;
+  static_assert(G::OW <= 96 && XT % 4 == 0 && XROW % 4 == 0, "three tiles a row");
+  __shared__ __attribute__((aligned(16))) float ws[32 * WST];
+  __shared__ __attribute__((aligned(16))) float xs[XT];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 31, kk = lane >> 5;
+  for (int q = tid; q < 32 * G::K / 4; q += NT) {
+    const int co = q / (G::K / 4), k4 = q - co * (G::K / 4);
+    *reinterpret_cast<float4*>(ws + co * WST + 4 * k4) = reinterpret_cast<const float4*>(w)[q];
+  }
+  const float* wrow = ws + col * WST + 4 * kk;
+  const int px = wave * 32 + col;                       // this lane's A row: pixel of the row
+  const float* xl = xs + (px < G::OW ? px : 0) * G::ST * G::CIN + 4 * kk;
+  float w_n = 0.0f, w_mean = 0.0f, w_m2 = 0.0f;
+  const float bc = STATS ? fb.bias[col] : 0.0f;
+  const int rows = n * G::OH;
+  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+    const int sm = row / G::OH, oy = row - sm * G::OH;
+    __syncthreads();                                    // the previous row's reads (and W)
+    const float4* src = reinterpret_cast<const float4*>(x + (size_t)(sm * G::IH + G::ST * oy) * XROW);
+    for (int i = tid; i < XT / 4; i += NT) reinterpret_cast<float4*>(xs)[i] = src[i];
+    __syncthreads();
+    f32x16 acc;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#pragma unroll 6
+    for (int st = 0; st < G::KSTEPS; ++st) {
+      const int kc = 8 * st;
+      const float* a = xl + (kc / G::KROW) * XROW + kc % G::KROW;
+      const float2 a0 = *reinterpret_cast<const float2*>(a);
+      const float2 a1 = *reinterpret_cast<const float2*>(a + 2);
+      acc = mfma4(make_float4(a0.x, a0.y, a1.x, a1.y),
+                  *reinterpret_cast<const float4*>(wrow + kc), acc);
+    }
+    float* zr = z + (size_t)row * G::OW * 32;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int pr = wave * 32 + acc_row(r, kk);
+      if (pr < G::OW) zr[pr * 32 + col] = acc[r];
+    }
+    if constexpr (STATS) {
+      float a[16], tn = 0.0f, ts = 0.0f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const bool ok = wave * 32 + acc_row(r, kk) < G::OW;
+        const float v = acc[r] + bc;
+        a[r] = v > 0.0f ? v : v * fb.slope;
+        tn += ok ? 1.0f : 0.0f;
+        ts += ok ? a[r] : 0.0f;
+      }
+      const float tm = tn > 0.0f ? ts / tn : 0.0f;
+      float tq = 0.0f;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float d = a[r] - tm;
+        tq += wave * 32 + acc_row(r, kk) < G::OW ? d * d : 0.0f;
+      }
+      chan(w_n, w_mean, w_m2, tn, tm, tq);
+    }
+  }
+  if constexpr (STATS) merge_partials_last<NT>(fb, w_n, w_mean, w_m2, (int64_t)n * G::OPIX);
+}
+
 // ---- weight gradient -------------------------------------------------------------------
 // A workgroup takes whole output rows (sample s, row oy): it stages the KS
 // input rows that row reads (KS * IW * C_in contiguous floats of NHWC) and
@@ -278,31 +338,8 @@ fwd_kernel(int n, const float* __restrict__ x, const float* __restrict__ w, floa
 // to part[blockIdx.x]; wgrad_reduce_kernel sums them in index order.
 constexpr int kWgradMaxGrid = 256;
 
-// the float4s of output row `row`'s staging (its KS input rows, its dZ row)
-// that thread threadIdx.x stores, into registers (row clamped to the last)
-template <class G, int kXI, int kDI, int NT>
-__device__ __forceinline__ void wgrad_load_row(const float* __restrict__ x,
-                                               const float* __restrict__ dz, int row, int rows,
-                                               float4 (&rx)[kXI], float4 (&rd)[kDI]) {
-  constexpr int XROW = G::IW * G::CIN, XT = G::KS * XROW, DT = G::OW * 32;
-  const int rc = row < rows ? row : rows - 1;
-  const int sm = rc / G::OH, oy = rc - sm * G::OH;
-  const float4* xsrc = reinterpret_cast<const float4*>(x + (size_t)(sm * G::IH + G::ST * oy) * XROW);
-  const float4* dsrc = reinterpret_cast<const float4*>(dz + (size_t)rc * DT);
-#pragma unroll
-  for (int j = 0; j < kXI; ++j) {
-    const int i = threadIdx.x + j * NT;
-    rx[j] = xsrc[i < XT / 4 ? i : 0];
-  }
-#pragma unroll
-  for (int j = 0; j < kDI; ++j) {
-    const int i = threadIdx.x + j * NT;
-    rd[j] = dsrc[i < DT / 4 ? i : 0];
-  }
-}
-
 template <class G, int NBW, int WAVES>
-__global__ void __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(1, 1)))
+__global__ void __launch_bounds__(64 * WAVES)
 wgrad_kernel(int n, const float* __restrict__ x, const float* __restrict__ dz,
              float* __restrict__ part) {
   static_assert(WAVES * NBW * 32 == G::K, "the waves cover K");
@@ -311,11 +348,8 @@ wgrad_kernel(int n, const float* __restrict__ x, const float* __restrict__ dz,
   constexpr int DT = G::OW * 32;
   static_assert(XROW % 4 == 0 && DT % 4 == 0, "float4 staging");
   constexpr int NT = 64 * WAVES;
-  // one float4 of padding each: the staging stores are branch-free (a
-  // thread past the end writes the pad), which keeps the register copies of
-  // the next row out of scratch
-  __shared__ __attribute__((aligned(16))) float xs[XT + 4];
-  __shared__ __attribute__((aligned(16))) float ds[DT + 4];
+  __shared__ __attribute__((aligned(16))) float xs[XT];
+  __shared__ __attribute__((aligned(16))) float ds[DT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 31, kk = lane >> 5;
   int kr[NBW];   // k's offset inside the staged rows
@@ -329,26 +363,15 @@ wgrad_kernel(int n, const float* __restrict__ x, const float* __restrict__ dz,
   for (int b = 0; b < NBW; ++b)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[b][r] = 0.0f;
-  // a row's staging: the next row's float4s are loaded into registers while
-  // this row's MFMAs run, and stored to LDS after the barrier that ends it
-  constexpr int kXI = (XT / 4 + NT - 1) / NT, kDI = (DT / 4 + NT - 1) / NT;
-  float4 rx[kXI], rd[kDI];
   const int rows = n * G::OH;
-  wgrad_load_row<G, kXI, kDI, NT>(x, dz, blockIdx.x, rows, rx, rd);
   for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+    const int sm = row / G::OH, oy = row - sm * G::OH;
     __syncthreads();                                    // the previous row's reads
-#pragma unroll
-    for (int j = 0; j < kXI; ++j) {
-      const int i = tid + j * NT;
-      reinterpret_cast<float4*>(xs)[i < XT / 4 ? i : XT / 4] = rx[j];
-    }
-#pragma unroll
-    for (int j = 0; j < kDI; ++j) {
-      const int i = tid + j * NT;
-      reinterpret_cast<float4*>(ds)[i < DT / 4 ? i : DT / 4] = rd[j];
-    }
+    const float4* xsrc = reinterpret_cast<const float4*>(x + (size_t)(sm * G::IH + G::ST * oy) * XROW);
+    for (int i = tid; i < XT / 4; i += NT) reinterpret_cast<float4*>(xs)[i] = xsrc[i];
+    const float4* dsrc = reinterpret_cast<const float4*>(dz + (size_t)row * DT);
+    for (int i = tid; i < DT / 4; i += NT) reinterpret_cast<float4*>(ds)[i] = dsrc[i];
     __syncthreads();
-    wgrad_load_row<G, kXI, kDI, NT>(x, dz, row + (int)gridDim.x, rows, rx, rd);
 #pragma unroll 2
     for (int ox0 = 0; ox0 < G::OW; ox0 += 2) {
       const int ox = ox0 + kk;
@@ -511,11 +534,22 @@ int launch_fwd(int n, const float* x, const float* w, float* z, const FwdBn& fb,
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 
+template <class G, bool STATS>
+int launch_fwd_row(int n, const float* x, const float* w, float* z, const FwdBn& fb,
+                   hipStream_t s) {
+  const int rows = n * G::OH;
+  static const int res = resident(reinterpret_cast<const void*>(fwd_row_kernel<G, STATS>), 192,
+                                  STATS ? kMaxGrid : 1 << 20);
+  const int grid = rows < res ? rows : res;
+  hipLaunchKernelGGL((fwd_row_kernel<G, STATS>), dim3(grid), dim3(192), 0, s, n, x, w, z, fb);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
 template <bool STATS>
 int dispatch_fwd(int l, int n, const float* x, const float* w, float* z, const FwdBn& fb,
                  hipStream_t s) {
   switch (l) {
-    case 1: return launch_fwd<L1, 1, STATS>(n, x, w, z, fb, s);
+    case 1: return launch_fwd_row<L1, STATS>(n, x, w, z, fb, s);
     case 2: return launch_fwd<L2, 1, STATS>(n, x, w, z, fb, s);
     case 3: return launch_fwd<L3, 2, STATS>(n, x, w, z, fb, s);
     default: return launch_fwd<L4, 4, STATS>(n, x, w, z, fb, s);
