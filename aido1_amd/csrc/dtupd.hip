@@ -100,7 +100,7 @@ struct FwdBn {
   float* work;     // [kMaxGrid][32][3] partials, then the counters (dt_upd_bn_work_floats)
   int32_t* guard;
 };
-constexpr int kMaxGrid = 512;   // workgroups (= partials) of a STATS launch
+constexpr int kMaxGrid = 256;   // workgroups (= partials) of a STATS launch
 
 template <int NT>
 __device__ void merge_partials_last(const FwdBn& fb, float cnt, float mean, float m2, int64_t m) {
@@ -251,80 +251,6 @@ fwd_kernel(int n, const float* __restrict__ x, const float* __restrict__ w, floa
     }
   }
   if constexpr (STATS) merge_partials_last<kThreads>(fb, w_n, w_mean, w_m2, (int64_t)n * G::OPIX);
-}
-
-// ---- forward, whole output rows (the 3-channel observation layer) ----------------------
-// The 8 input rows one output row reads (8 x 160 x 3 floats, contiguous in
-// NHWC) are staged in LDS once, so the im2col reads (3.85 per staged float)
-// are LDS reads; three waves take the row's three 32-pixel tiles (77 pixels).
-template <class G, bool STATS>
-__global__ void __launch_bounds__(192)
-fwd_row_kernel(int n, const float* __restrict__ x, const float* __restrict__ w,
-               float* __restrict__ z, FwdBn fb) {
-  constexpr int NT = 192;
-  constexpr int WST = G::K + 4;
-  constexpr int XROW = G::IW * G::CIN;
-  constexpr int XT = G::KS * XROW;
-  static_assert(G::OW <= 96 && XT % 4 == 0 && XROW % 4 == 0, "three tiles a row");
-  __shared__ __attribute__((aligned(16))) float ws[32 * WST];
-  __shared__ __attribute__((aligned(16))) float xs[XT];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int col = lane & 31, kk = lane >> 5;
-  for (int q = tid; q < 32 * G::K / 4; q += NT) {
-    const int co = q / (G::K / 4), k4 = q - co * (G::K / 4);
-    *reinterpret_cast<float4*>(ws + co * WST + 4 * k4) = reinterpret_cast<const float4*>(w)[q];
-  }
-  const float* wrow = ws + col * WST + 4 * kk;
-  const int px = wave * 32 + col;                       // this lane's A row: pixel of the row
-  const float* xl = xs + (px < G::OW ? px : 0) * G::ST * G::CIN + 4 * kk;
-  float w_n = 0.0f, w_mean = 0.0f, w_m2 = 0.0f;
-  const float bc = STATS ? fb.bias[col] : 0.0f;
-  const int rows = n * G::OH;
-  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
-    const int sm = row / G::OH, oy = row - sm * G::OH;
-    __syncthreads();                                    // the previous row's reads (and W)
-    const float4* src = reinterpret_cast<const float4*>(x + (size_t)(sm * G::IH + G::ST * oy) * XROW);
-    for (int i = tid; i < XT / 4; i += NT) reinterpret_cast<float4*>(xs)[i] = src[i];
-    __syncthreads();
-    f32x16 acc;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-#pragma unroll 6
-    for (int st = 0; st < G::KSTEPS; ++st) {
-      const int kc = 8 * st;
-      const float* a = xl + (kc / G::KROW) * XROW + kc % G::KROW;
-      const float2 a0 = *reinterpret_cast<const float2*>(a);
-      const float2 a1 = *reinterpret_cast<const float2*>(a + 2);
-      acc = mfma4(make_float4(a0.x, a0.y, a1.x, a1.y),
-                  *reinterpret_cast<const float4*>(wrow + kc), acc);
-    }
-    float* zr = z + (size_t)row * G::OW * 32;
-#pragma unroll
-    for (int r = 0; r < 16; ++r) {
-      const int pr = wave * 32 + acc_row(r, kk);
-      if (pr < G::OW) zr[pr * 32 + col] = acc[r];
-    }
-    if constexpr (STATS) {
-      float a[16], tn = 0.0f, ts = 0.0f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const bool ok = wave * 32 + acc_row(r, kk) < G::OW;
-        const float v = acc[r] + bc;
-        a[r] = v > 0.0f ? v : v * fb.slope;
-        tn += ok ? 1.0f : 0.0f;
-        ts += ok ? a[r] : 0.0f;
-      }
-      const float tm = tn > 0.0f ? ts / tn : 0.0f;
-      float tq = 0.0f;
-#pragma unroll
-      for (int r = 0; r < 16; ++r) {
-        const float d = a[r] - tm;
-        tq += wave * 32 + acc_row(r, kk) < G::OW ? d * d : 0.0f;
-      }
-      chan(w_n, w_mean, w_m2, tn, tm, tq);
-    }
-  }
-  if constexpr (STATS) merge_partials_last<NT>(fb, w_n, w_mean, w_m2, (int64_t)n * G::OPIX);
 }
 
 // ---- weight gradient -------------------------------------------------------------------
@@ -534,22 +460,11 @@ int launch_fwd(int n, const float* x, const float* w, float* z, const FwdBn& fb,
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 
-template <class G, bool STATS>
-int launch_fwd_row(int n, const float* x, const float* w, float* z, const FwdBn& fb,
-                   hipStream_t s) {
-  const int rows = n * G::OH;
-  static const int res = resident(reinterpret_cast<const void*>(fwd_row_kernel<G, STATS>), 192,
-                                  STATS ? kMaxGrid : 1 << 20);
-  const int grid = rows < res ? rows : res;
-  hipLaunchKernelGGL((fwd_row_kernel<G, STATS>), dim3(grid), dim3(192), 0, s, n, x, w, z, fb);
-  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
-}
-
 template <bool STATS>
 int dispatch_fwd(int l, int n, const float* x, const float* w, float* z, const FwdBn& fb,
                  hipStream_t s) {
   switch (l) {
-    case 1: return launch_fwd_row<L1, STATS>(n, x, w, z, fb, s);
+    case 1: return launch_fwd<L1, 1, STATS>(n, x, w, z, fb, s);
     case 2: return launch_fwd<L2, 1, STATS>(n, x, w, z, fb, s);
     case 3: return launch_fwd<L3, 2, STATS>(n, x, w, z, fb, s);
     default: return launch_fwd<L4, 4, STATS>(n, x, w, z, fb, s);
