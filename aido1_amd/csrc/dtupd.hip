@@ -78,7 +78,6 @@ __device__ __forceinline__ f32x16 mfma4(float4 a, float4 b, f32x16 c) {
 // row of the 32x32 accumulator register r holds for lane half h
 __device__ __forceinline__ int acc_row(int r, int h) { return (r & 3) + 8 * (r >> 2) + 4 * h; }
 
-constexpr int kThreads = 256;   // 4 waves
 
 // The train-mode BatchNorm after a block's conv -> LeakyReLU, fused into the
 // forward's epilogue (STATS): the batch statistics of a = leaky(z + bias).
@@ -129,14 +128,25 @@ __device__ void merge_partials_last(const FwdBn& fb, float cnt, float mean, floa
   acquire_partials();
   {
     constexpr int kFin = NT / 32;                   // threads a channel
+    constexpr int kPer = (kMaxGrid + kFin - 1) / kFin;   // all loads issued before the merges
     const int ch = tid & 31, j = tid >> 5;
     float cn = 0.0f, cm = 0.0f, cq = 0.0f;
-    for (int g = j; g < (int)gridDim.x; g += kFin) {
-      const float* p = part + ((size_t)g * 32 + ch) * 3;
-      const float pn = ld_wt(p), pm = ld_wt(p + 1), pq = ld_wt(p + 2);
-      st_wt(part + ((size_t)g * 32 + ch) * 3, 0.0f);   // counts back to zero (dtsync.h)
-      chan(cn, cm, cq, pn, pm, pq);
+    float pn[kPer], pm[kPer], pq[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {
+      const int g = j + k * kFin;
+      const float* p = part + ((size_t)(g < (int)gridDim.x ? g : 0) * 32 + ch) * 3;
+      pn[k] = g < (int)gridDim.x ? ld_wt(p) : 0.0f;
+      pm[k] = ld_wt(p + 1);
+      pq[k] = ld_wt(p + 2);
     }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) {   // counts back to zero (dtsync.h)
+      const int g = j + k * kFin;
+      if (g < (int)gridDim.x) st_wt(part + ((size_t)g * 32 + ch) * 3, 0.0f);
+    }
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) chan(cn, cm, cq, pn[k], pm[k], pq[k]);
     red2[j][ch][0] = cn;
     red2[j][ch][1] = cm;
     red2[j][ch][2] = cq;
@@ -165,23 +175,29 @@ __device__ void merge_partials_last(const FwdBn& fb, float cnt, float mean, floa
 }
 
 // ---- forward ---------------------------------------------------------------------------
-// A workgroup holds W in LDS ([32][K + 4]: row stride 4 floats past K, so the
-// 32 output-channel lanes of a B read fall on distinct banks) and walks
-// 32-pixel tiles of one sample each; KSPLIT waves share a tile, each a slice
-// of K, summed through LDS (the small layers: more waves than tiles).
+// A workgroup of kFwdThreads (16 waves: W is staged once for all of them, and
+// a STATS launch, capped at kMaxGrid workgroups, still has four waves a SIMD
+// to hide its loads' latency) holds W in LDS ([32][K + 4]: row stride 4
+// floats past K, so the 32 output-channel lanes of a B read fall on distinct
+// banks) and walks 32-pixel tiles of one sample each; KSPLIT waves share a
+// tile, each a slice of K, summed through LDS (the small layers: more waves
+// than tiles).
+constexpr int kFwdThreads = 1024;
+
 template <class G, int KSPLIT, bool STATS>
-__global__ void __launch_bounds__(kThreads)
+__global__ void __launch_bounds__(kFwdThreads)
 fwd_kernel(int n, const float* __restrict__ x, const float* __restrict__ w, float* __restrict__ z,
            FwdBn fb) {
   constexpr int WST = G::K + 4;
-  constexpr int GP = 4 / KSPLIT;                 // tiles a workgroup round
+  constexpr int NW = kFwdThreads / 64;
+  constexpr int GP = NW / KSPLIT;                // tiles a workgroup round
   constexpr int SPW = G::KSTEPS / KSPLIT;        // k-steps a wave
-  static_assert(G::KSTEPS % KSPLIT == 0, "even K slices");
+  static_assert(G::KSTEPS % KSPLIT == 0 && NW % KSPLIT == 0, "even K slices");
   __shared__ __attribute__((aligned(16))) float ws[32 * WST];
-  __shared__ float red[KSPLIT > 1 ? 4 * 16 * 64 : 1];
+  __shared__ float red[KSPLIT > 1 ? GP * (KSPLIT - 1) * 16 * 64 : 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 31, kk = lane >> 5;
-  for (int q = tid; q < 32 * G::K / 4; q += kThreads) {
+  for (int q = tid; q < 32 * G::K / 4; q += kFwdThreads) {
     const int co = q / (G::K / 4), k4 = q - co * (G::K / 4);
     *reinterpret_cast<float4*>(ws + co * WST + 4 * k4) = reinterpret_cast<const float4*>(w)[q];
   }
@@ -210,16 +226,17 @@ fwd_kernel(int n, const float* __restrict__ x, const float* __restrict__ w, floa
       const float4 b = *reinterpret_cast<const float4*>(wrow + kc);
       acc = mfma4(a, b, acc);
     }
-    if constexpr (KSPLIT > 1) {
+    if constexpr (KSPLIT > 1) {   // slice ks > 0 of tile g at slot g * (KSPLIT - 1) + ks - 1
+      float* rs = red + (size_t)g * (KSPLIT - 1) * 16 * 64 + lane;
       if (ks > 0)
 #pragma unroll
-        for (int r = 0; r < 16; ++r) red[(wave * 16 + r) * 64 + lane] = acc[r];
+        for (int r = 0; r < 16; ++r) rs[((ks - 1) * 16 + r) * 64] = acc[r];
       __syncthreads();
       if (ks == 0)
+#pragma unroll 1
+        for (int o = 0; o < KSPLIT - 1; ++o)
 #pragma unroll
-        for (int r = 0; r < 16; ++r)
-#pragma unroll
-          for (int o = 1; o < KSPLIT; ++o) acc[r] += red[((wave + o) * 16 + r) * 64 + lane];
+          for (int r = 0; r < 16; ++r) acc[r] += rs[(o * 16 + r) * 64];
       __syncthreads();
     }
     if (ks == 0 && tvalid) {
@@ -250,7 +267,7 @@ fwd_kernel(int n, const float* __restrict__ x, const float* __restrict__ w, floa
       }
     }
   }
-  if constexpr (STATS) merge_partials_last<kThreads>(fb, w_n, w_mean, w_m2, (int64_t)n * G::OPIX);
+  if constexpr (STATS) merge_partials_last<kFwdThreads>(fb, w_n, w_mean, w_m2, (int64_t)n * G::OPIX);
 }
 
 // ---- weight gradient -------------------------------------------------------------------
@@ -262,7 +279,10 @@ fwd_kernel(int n, const float* __restrict__ x, const float* __restrict__ w, floa
 // k), both LDS reads.  An input pixel is read from HBM once per output row
 // that needs it, not once per (pixel, tap).  The workgroup's partial dW goes
 // to part[blockIdx.x]; wgrad_reduce_kernel sums them in index order.
-constexpr int kWgradMaxGrid = 256;
+// workgroups (= partials) of a launch at most: enough to fill the chip, few
+// enough that the partials stay small next to the layer's own traffic
+template <class G>
+constexpr int wgrad_max_grid() { return G::CIN == 3 ? 512 : (G::OH > 20 ? 256 : 128); }
 
 template <class G, int NBW, int WAVES>
 __global__ void __launch_bounds__(64 * WAVES)
@@ -368,8 +388,10 @@ struct DGeom {
   static constexpr int TPS = first(NCLS);
 };
 
-template <class G>
-__global__ void __launch_bounds__(kThreads)
+// NW waves a workgroup: many for the layer with the most tiles a sample,
+// few where a sample has only a handful (more workgroups, each staging W^T)
+template <class G, int NW>
+__global__ void __launch_bounds__(64 * NW)
 dgrad_kernel(int n, const float* __restrict__ dz, const float* __restrict__ w,
              float* __restrict__ dx) {
   using D = DGeom<G>;
@@ -379,14 +401,14 @@ dgrad_kernel(int n, const float* __restrict__ dz, const float* __restrict__ w,
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 31, kk = lane >> 5;
   // W [co][kh][kw][ci] -> wt[kh * KS + kw][ci][co]
-  for (int i = tid; i < 32 * G::K; i += kThreads) {
+  for (int i = tid; i < 32 * G::K; i += 64 * NW) {
     const int co = i / G::K, r = i - co * G::K;
     const int tap = r / 32, ci = r - tap * 32;
     wt[(tap * 32 + ci) * CST + co] = w[i];
   }
   __syncthreads();
   const int tiles = n * D::TPS;
-  for (int tile = blockIdx.x * 4 + wave; tile < tiles; tile += gridDim.x * 4) {
+  for (int tile = blockIdx.x * NW + wave; tile < tiles; tile += gridDim.x * NW) {
     const int s = tile / D::TPS;
     int t = tile - s * D::TPS, cls = 0;
 #pragma unroll
@@ -402,7 +424,7 @@ dgrad_kernel(int n, const float* __restrict__ dz, const float* __restrict__ w,
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-#pragma unroll
+#pragma unroll 4
     for (int tap = 0; tap < D::TAPS; ++tap) {
       const int th = tap / D::T1, tw = tap - th * D::T1;
       const int oy = a - th, ox = b - tw;
@@ -448,14 +470,14 @@ int resident(const void* kern, int threads, int cap) {
 
 template <class G, int KSPLIT, bool STATS>
 int launch_fwd(int n, const float* x, const float* w, float* z, const FwdBn& fb, hipStream_t s) {
-  constexpr int GP = 4 / KSPLIT;
+  constexpr int GP = kFwdThreads / 64 / KSPLIT;
   const int tiles = n * G::TPS;
   int grid = (tiles + GP - 1) / GP;
   // STATS: at most kMaxGrid partials (the last arriver merges them)
   static const int res = resident(reinterpret_cast<const void*>(fwd_kernel<G, KSPLIT, STATS>),
-                                  kThreads, STATS ? kMaxGrid : 1 << 20);
+                                  kFwdThreads, STATS ? kMaxGrid : 1 << 20);
   grid = grid < res ? grid : res;
-  hipLaunchKernelGGL((fwd_kernel<G, KSPLIT, STATS>), dim3(grid), dim3(kThreads), 0, s, n, x, w, z,
+  hipLaunchKernelGGL((fwd_kernel<G, KSPLIT, STATS>), dim3(grid), dim3(kFwdThreads), 0, s, n, x, w, z,
                      fb);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
@@ -464,10 +486,10 @@ template <bool STATS>
 int dispatch_fwd(int l, int n, const float* x, const float* w, float* z, const FwdBn& fb,
                  hipStream_t s) {
   switch (l) {
-    case 1: return launch_fwd<L1, 1, STATS>(n, x, w, z, fb, s);
-    case 2: return launch_fwd<L2, 1, STATS>(n, x, w, z, fb, s);
-    case 3: return launch_fwd<L3, 2, STATS>(n, x, w, z, fb, s);
-    default: return launch_fwd<L4, 4, STATS>(n, x, w, z, fb, s);
+    case 1: return launch_fwd<L1, 2, STATS>(n, x, w, z, fb, s);
+    case 2: return launch_fwd<L2, 2, STATS>(n, x, w, z, fb, s);
+    case 3: return launch_fwd<L3, 8, STATS>(n, x, w, z, fb, s);
+    default: return launch_fwd<L4, 16, STATS>(n, x, w, z, fb, s);
   }
 }
 
@@ -475,7 +497,7 @@ int dispatch_fwd(int l, int n, const float* x, const float* w, float* z, const F
 template <class G>
 int wgrad_chunks(int n) {
   const int rows = n * G::OH;
-  return rows < kWgradMaxGrid ? rows : kWgradMaxGrid;
+  return rows < wgrad_max_grid<G>() ? rows : wgrad_max_grid<G>();
 }
 
 template <class G, int NBW, int WAVES>
@@ -489,13 +511,14 @@ int launch_wgrad(int n, const float* x, const float* dz, float* dw, float* work,
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 
-template <class G>
+template <class G, int NW>
 int launch_dgrad(int n, const float* dz, const float* w, float* dx, hipStream_t s) {
   const int tiles = n * DGeom<G>::TPS;
-  int grid = (tiles + 3) / 4;
-  static const int res = resident(reinterpret_cast<const void*>(dgrad_kernel<G>), kThreads, 1 << 20);
+  int grid = (tiles + NW - 1) / NW;
+  static const int res =
+      resident(reinterpret_cast<const void*>(dgrad_kernel<G, NW>), 64 * NW, 1 << 20);
   grid = grid < res ? grid : res;
-  hipLaunchKernelGGL(dgrad_kernel<G>, dim3(grid), dim3(kThreads), 0, s, n, dz, w, dx);
+  hipLaunchKernelGGL((dgrad_kernel<G, NW>), dim3(grid), dim3(64 * NW), 0, s, n, dz, w, dx);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 
@@ -554,10 +577,10 @@ int dt_upd_conv_wgrad(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih
   if (!l || n < 1 || !x || !dz || !dw || !work) return DT_E_ARG;
   hipStream_t s = (hipStream_t)stream;
   switch (l) {
-    case 1: return launch_wgrad<L1, 3, 2>(n, x, dz, dw, work, s);
-    case 2: return launch_wgrad<L2, 4, 4>(n, x, dz, dw, work, s);
-    case 3: return launch_wgrad<L3, 4, 4>(n, x, dz, dw, work, s);
-    default: return launch_wgrad<L4, 4, 4>(n, x, dz, dw, work, s);
+    case 1: return launch_wgrad<L1, 1, 6>(n, x, dz, dw, work, s);
+    case 2: return launch_wgrad<L2, 2, 8>(n, x, dz, dw, work, s);
+    case 3: return launch_wgrad<L3, 2, 8>(n, x, dz, dw, work, s);
+    default: return launch_wgrad<L4, 2, 8>(n, x, dz, dw, work, s);
   }
 }
 
@@ -568,9 +591,9 @@ int dt_upd_conv_dgrad(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih
   if (n == 0) return DT_OK;
   hipStream_t s = (hipStream_t)stream;
   switch (l) {
-    case 2: return launch_dgrad<L2>(n, dz, w, dx, s);
-    case 3: return launch_dgrad<L3>(n, dz, w, dx, s);
-    default: return launch_dgrad<L4>(n, dz, w, dx, s);
+    case 2: return launch_dgrad<L2, 4>(n, dz, w, dx, s);
+    case 3: return launch_dgrad<L3, 16>(n, dz, w, dx, s);
+    default: return launch_dgrad<L4, 4>(n, dz, w, dx, s);
   }
 }
 
