@@ -47,6 +47,16 @@ class DtConvSet(ctypes.Structure):
                 ('out_gamma', ctypes.c_void_p), ('out_beta', ctypes.c_void_p)]
 
 
+class DtUpdBn(ctypes.Structure):
+    """include/dtupd.h DtUpdBn: a conv trunk block's BatchNorm hand-off."""
+    _fields_ = [('part', ctypes.c_void_p), ('parts', ctypes.c_int32), ('m', ctypes.c_int64),
+                ('bias', ctypes.c_void_p), ('gamma', ctypes.c_void_p), ('beta', ctypes.c_void_p),
+                ('slope', ctypes.c_float), ('eps', ctypes.c_float), ('momentum', ctypes.c_float),
+                ('running_mean', ctypes.c_void_p), ('running_var', ctypes.c_void_p),
+                ('num_batches_tracked', ctypes.c_void_p), ('updates', ctypes.c_int32),
+                ('mean_invstd', ctypes.c_void_p), ('guard', ctypes.c_void_p)]
+
+
 class DtExploreParams(ctypes.Structure):
     """include/dtactor.h DtExploreParams."""
     _fields_ = [(k, ctypes.c_double) for k in
@@ -181,6 +191,14 @@ def lib():
             'dt_upd_conv_wgrad': (ctypes.c_int, [i32, i32, i32, i32, i32, i32, vp, vp, vp, vp,
                                                  vp]),
             'dt_upd_conv_dgrad': (ctypes.c_int, [i32, i32, i32, i32, i32, i32, vp, vp, vp, vp]),
+            'dt_upd_part_floats': (i64, []),
+            'dt_upd_conv_fwd_part': (ctypes.c_int, [i32, i32, i32, i32, i32, i32, vp,
+                                                    ctypes.POINTER(DtUpdBn), vp, vp,
+                                                    ctypes.c_float, vp, vp,
+                                                    ctypes.POINTER(i32), vp]),
+            'dt_upd_bn_finish': (ctypes.c_int, [i64, vp, ctypes.POINTER(DtUpdBn), vp, vp]),
+            'dt_upd_conv_wgrad_bn': (ctypes.c_int, [i32, i32, i32, i32, i32, i32, vp,
+                                                    ctypes.POINTER(DtUpdBn), vp, vp, vp, vp]),
             'dt_soft_update': (ctypes.c_int, [i32, vp, vp, f64, vp]),
             # dtactor.h
             'dt_sample_norm': (ctypes.c_int, [vp, vp, i32, i32, i32, vp, vp, ctypes.c_float,

@@ -105,7 +105,8 @@ def _init_weight(w, mode, conv):
 
 class _Seq(nn.Module):       # MetaNet: ".internal_modules.<i>"
     # conv -> LeakyReLU -> BatchNorm blocks in train mode on the GPU (f32) run
-    # their tail as dt_bn_leaky_fwd / _bwd (train_ops.py, include/dttrain.h)
+    # as one chain (train_ops.conv_trunk, include/dtupd.h) or block by block
+    # (train_ops.conv_leaky_bn, include/dttrain.h)
     fused_tail = True
 
     def __init__(self, mods):
@@ -123,6 +124,11 @@ class _Seq(nn.Module):       # MetaNet: ".internal_modules.<i>"
             if (self.fused_tail and i + 2 < k and isinstance(m, _Conv)
                     and isinstance(mods[i + 2], nn.BatchNorm2d)):
                 from aido1_amd import train_ops
+                blocks = train_ops.trunk_len(x, mods, i, k)
+                if blocks:
+                    x = train_ops.conv_trunk(x, mods, i, blocks)
+                    i += 3 * blocks
+                    continue
                 if train_ops.applicable(x, m.kernel, mods[i + 1], mods[i + 2]):
                     x = train_ops.conv_leaky_bn(x, m.kernel, mods[i + 1], mods[i + 2])
                     i += 3

@@ -11,13 +11,23 @@
 
 namespace {
 
-// Chan et al.: merge (nb, mb, m2b) into (n, mean, m2)
+// Chan et al.: merge (nb, mb, m2b) into (n, mean, m2).  Merges run in long
+// dependent chains (a workgroup's waves, the partials of a launch), so the
+// weight nb / tot takes the hardware reciprocal (1 ulp) instead of an IEEE
+// division (a dozen dependent instructions); merging into an empty side
+// copies exactly.
 __device__ __forceinline__ void chan(float& n, float& mean, float& m2, float nb, float mb,
                                      float m2b) {
   if (nb <= 0.0f) return;
+  if (n <= 0.0f) {
+    n = nb;
+    mean = mb;
+    m2 = m2b;
+    return;
+  }
   const float tot = n + nb;
   const float d = mb - mean;
-  const float f = nb / tot;
+  const float f = nb * __builtin_amdgcn_rcpf(tot);
   mean += d * f;
   m2 += m2b + d * d * n * f;
   n = tot;

@@ -26,6 +26,14 @@
 #include "../../include/dtupd.h"
 #include "dtsync.h"
 
+// tools/upd_micro.py builds variants that skip parts of the forward to time
+// them (1: the A loads, 2: W's staging, 4: the statistics' merge, 8: the
+// K-split sum, 16: the chain's partial loads, 32: the chain's merge); 0 in
+// the library
+#ifndef DTUPD_SKIP
+#define DTUPD_SKIP 0
+#endif
+
 namespace {
 
 using f32x16 = __attribute__((ext_vector_type(16))) float;
@@ -101,10 +109,12 @@ struct FwdBn {
 };
 constexpr int kMaxGrid = 256;   // workgroups (= partials) of a STATS launch
 
-template <int NT>
-__device__ void merge_partials_last(const FwdBn& fb, float cnt, float mean, float m2, int64_t m) {
+// the workgroup's Welford partial of its lanes' channels -> part[blockIdx.x]:
+// written through (WT) for a last-arrival merge inside this launch, plainly
+// for the next kernel (the chain of include/dtupd.h) to merge
+template <int NT, bool WT>
+__device__ void wg_partial(float* part, float cnt, float mean, float m2) {
   __shared__ float red[NT / 64][32][3];
-  __shared__ float red2[NT / 32][32][3];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   // lane pairs (l, l ^ 32) hold the same channel
   chan(cnt, mean, m2, __shfl_xor(cnt, 32), __shfl_xor(mean, 32), __shfl_xor(m2, 32));
@@ -114,15 +124,28 @@ __device__ void merge_partials_last(const FwdBn& fb, float cnt, float mean, floa
     red[wave][lane][2] = m2;
   }
   __syncthreads();
-  float* part = fb.work;
   if (tid < 32) {
     float cn = 0.0f, cm = 0.0f, cq = 0.0f;
     for (int w = 0; w < NT / 64; ++w) chan(cn, cm, cq, red[w][tid][0], red[w][tid][1], red[w][tid][2]);
     float* p = part + ((size_t)blockIdx.x * 32 + tid) * 3;
-    st_wt(p, cn);
-    st_wt(p + 1, cm);
-    st_wt(p + 2, cq);
+    if constexpr (WT) {
+      st_wt(p, cn);
+      st_wt(p + 1, cm);
+      st_wt(p + 2, cq);
+    } else {
+      p[0] = cn;
+      p[1] = cm;
+      p[2] = cq;
+    }
   }
+}
+
+template <int NT>
+__device__ void merge_partials_last(const FwdBn& fb, float cnt, float mean, float m2, int64_t m) {
+  __shared__ float red2[NT / 32][32][3];
+  const int tid = threadIdx.x;
+  float* part = fb.work;
+  wg_partial<NT, true>(part, cnt, mean, m2);
   unsigned int* counters = reinterpret_cast<unsigned int*>(part + (size_t)kMaxGrid * 32 * 3);
   if (!last_arrival(&counters[0])) return;
   acquire_partials();
@@ -174,6 +197,153 @@ __device__ void merge_partials_last(const FwdBn& fb, float cnt, float mean, floa
   }
 }
 
+// ---- the chain's hand-off (include/dtupd.h DtUpdBn) -------------------------------------
+// y = bn(leaky(z + bias)) exactly as dt_bn_leaky_apply computes it
+__device__ __forceinline__ float norm1(float z, float b, float mu, float sc, float bt, float slope) {
+  float v = z + b;
+  v = v > 0.0f ? v : v * slope;
+  return (v - mu) * sc + bt;
+}
+__device__ __forceinline__ float4 norm4(float4 z, float4 b, float4 mu, float4 sc, float4 bt,
+                                        float slope) {
+  return make_float4(norm1(z.x, b.x, mu.x, sc.x, bt.x, slope), norm1(z.y, b.y, mu.y, sc.y, bt.y, slope),
+                     norm1(z.z, b.z, mu.z, sc.z, bt.z, slope), norm1(z.w, b.w, mu.w, sc.w, bt.w, slope));
+}
+
+// Every workgroup of a chain kernel merges the producer's partials itself
+// (the same order as merge_partials_last: thread j of a channel takes partials
+// j, j + NT/32, ..., then one thread merges the NT/32 results), so all agree
+// bit for bit, and builds tab = {bias, mean, invstd * gamma, beta} per
+// channel in LDS.  The first workgroup (`finalize`) also writes mean_invstd,
+// moves the running statistics and reports to the guard, as the merging
+// workgroup of dt_upd_conv_fwd_bn does.  Two halves: norm_loads issues every
+// load (partials, parameters, running statistics) so the caller can start its
+// own loads behind them; norm_build merges and fills tab.
+constexpr int kNormPer = 8;     // partials a thread (kMaxGrid / 32 ways)
+
+struct NormRegs {
+  float pn[kNormPer], pm[kNormPer], pq[kNormPer];
+  float bias, gamma, beta, rm, rv;
+};
+
+template <int NT>
+__device__ __forceinline__ NormRegs norm_loads(const DtUpdBn& b, bool finalize) {
+  constexpr int kFin = NT / 32;
+  static_assert(kMaxGrid <= kNormPer * kFin, "one batch of loads covers every partial");
+  NormRegs r;
+  const int tid = threadIdx.x, ch = tid & 31, j = tid >> 5;
+#pragma unroll
+  for (int k = 0; k < ((DTUPD_SKIP & 16) ? 0 : kNormPer); ++k) {
+    const int g = j + k * kFin;
+    const float* p = b.part + ((size_t)(g < b.parts ? g : 0) * 32 + ch) * 3;
+    r.pn[k] = g < b.parts ? p[0] : 0.0f;
+    r.pm[k] = p[1];
+    r.pq[k] = p[2];
+  }
+  r.bias = r.gamma = r.beta = r.rm = r.rv = 0.0f;
+  if (tid < 32) {
+    r.bias = b.bias[tid];
+    r.gamma = b.gamma[tid];
+    r.beta = b.beta[tid];
+    if (finalize) {
+      r.rm = b.running_mean[tid];
+      r.rv = b.running_var[tid];
+    }
+  }
+  return r;
+}
+
+template <int NT>
+__device__ void norm_build(const DtUpdBn& b, const NormRegs& r, float (*tab)[32], bool finalize) {
+  constexpr int kFin = NT / 32;
+  __shared__ float red2[kFin][32][3];
+  const int tid = threadIdx.x;
+  if (DTUPD_SKIP & 32) {
+    if (tid < 32) {
+      tab[0][tid] = r.bias;
+      tab[1][tid] = 0.5f;
+      tab[2][tid] = r.gamma;
+      tab[3][tid] = r.beta;
+    }
+    __syncthreads();
+    return;
+  }
+  {
+    const int ch = tid & 31, j = tid >> 5;
+    float cn = 0.0f, cm = 0.0f, cq = 0.0f;
+#pragma unroll
+    for (int k = 0; k < kNormPer; ++k) chan(cn, cm, cq, r.pn[k], r.pm[k], r.pq[k]);
+    red2[j][ch][0] = cn;
+    red2[j][ch][1] = cm;
+    red2[j][ch][2] = cq;
+  }
+  __syncthreads();
+  if (tid < 32) {
+    float cn = 0.0f, cm = 0.0f, cq = 0.0f;
+    for (int q = 0; q < kFin; ++q) chan(cn, cm, cq, red2[q][tid][0], red2[q][tid][1], red2[q][tid][2]);
+    const float var = cq / cn;
+    const float invstd = 1.0f / sqrtf(var + b.eps);
+    tab[0][tid] = r.bias;
+    tab[1][tid] = cm;
+    tab[2][tid] = invstd * r.gamma;
+    tab[3][tid] = r.beta;
+    if (finalize) {
+      b.mean_invstd[tid] = cm;
+      b.mean_invstd[32 + tid] = invstd;
+      const int64_t m = b.m;
+      const bool lost = m < (int64_t(1) << 24) ? cn != (float)m : fabsf(cn - (float)m) > 1e-6f * (float)m;
+      guard_raise(b.guard, DT_GUARD_BN_COUNT, lost);
+      guard_raise(b.guard, DT_GUARD_BN_FWD, !finitef(cm) || !finitef(invstd));
+      const float unbiased = cn > 1.0f ? cq / (cn - 1.0f) : var;
+      float rm = r.rm, rv = r.rv;
+      for (int u = 0; u < b.updates; ++u) {
+        rm = (1.0f - b.momentum) * rm + b.momentum * cm;
+        rv = (1.0f - b.momentum) * rv + b.momentum * unbiased;
+      }
+      b.running_mean[tid] = rm;
+      b.running_var[tid] = rv;
+      if (tid == 0 && b.num_batches_tracked) b.num_batches_tracked[0] += b.updates;
+    }
+  }
+  __syncthreads();
+}
+
+// y = bn(leaky(z + bias)) of the chain's last block: every workgroup merges the
+// partials (norm_loads / norm_build) and normalises its share of z
+constexpr int kFinishPer = 4;       // float4s a thread
+constexpr int kFinishMaxGrid = 1024;
+
+__global__ void __launch_bounds__(1024)
+bn_finish_kernel(int64_t m, const float* __restrict__ z, DtUpdBn b, float* __restrict__ y) {
+  __shared__ __attribute__((aligned(16))) float tab[4][32];
+  const bool fin = blockIdx.x == 0;
+  const NormRegs r = norm_loads<1024>(b, fin);
+  // this thread's z (at most kFinishPer float4s: the grid covers m) loaded
+  // while the partials merge
+  const int64_t items = m * 8, stride = (int64_t)gridDim.x * 1024;
+  const int64_t q0 = (int64_t)blockIdx.x * 1024 + threadIdx.x;
+  float4 v[kFinishPer];
+#pragma unroll
+  for (int k = 0; k < kFinishPer; ++k) {
+    const int64_t q = q0 + k * stride;
+    v[k] = q < items ? reinterpret_cast<const float4*>(z)[q] : make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  }
+  norm_build<1024>(b, r, tab, fin);
+  const int cg = threadIdx.x & 7;               // the grid stride is a multiple of 8
+  const float4 tb = reinterpret_cast<const float4*>(tab[0])[cg];
+  const float4 tm = reinterpret_cast<const float4*>(tab[1])[cg];
+  const float4 ts = reinterpret_cast<const float4*>(tab[2])[cg];
+  const float4 tt = reinterpret_cast<const float4*>(tab[3])[cg];
+#pragma unroll
+  for (int k = 0; k < kFinishPer; ++k) {
+    const int64_t q = q0 + k * stride;
+    if (q < items) reinterpret_cast<float4*>(y)[q] = norm4(v[k], tb, tm, ts, tt, b.slope);
+  }
+  for (int64_t q = q0 + kFinishPer * stride; q < items; q += stride)   // past the grid's cover
+    reinterpret_cast<float4*>(y)[q] =
+        norm4(reinterpret_cast<const float4*>(z)[q], tb, tm, ts, tt, b.slope);
+}
+
 // ---- forward ---------------------------------------------------------------------------
 // A workgroup of kFwdThreads (16 waves: W is staged once for all of them, and
 // a STATS launch, capped at kMaxGrid workgroups, still has four waves a SIMD
@@ -184,10 +354,14 @@ __device__ void merge_partials_last(const FwdBn& fb, float cnt, float mean, floa
 // than tiles).
 constexpr int kFwdThreads = 1024;
 
-template <class G, int KSPLIT, bool STATS>
+
+// STATS: 0 none, 1 merged by the last workgroup (dt_upd_conv_fwd_bn), 2
+// partials for the next kernel (dt_upd_conv_fwd_part).  NORM: x is the
+// previous block's z, normalised on load (norm_loads / norm_build from `in`).
+template <class G, int KSPLIT, int STATS, bool NORM>
 __global__ void __launch_bounds__(kFwdThreads)
 fwd_kernel(int n, const float* __restrict__ x, const float* __restrict__ w, float* __restrict__ z,
-           FwdBn fb) {
+           FwdBn fb, DtUpdBn in) {
   constexpr int WST = G::K + 4;
   constexpr int NW = kFwdThreads / 64;
   constexpr int GP = NW / KSPLIT;                // tiles a workgroup round
@@ -195,13 +369,20 @@ fwd_kernel(int n, const float* __restrict__ x, const float* __restrict__ w, floa
   static_assert(G::KSTEPS % KSPLIT == 0 && NW % KSPLIT == 0, "even K slices");
   __shared__ __attribute__((aligned(16))) float ws[32 * WST];
   __shared__ float red[KSPLIT > 1 ? GP * (KSPLIT - 1) * 16 * 64 : 1];
+  __shared__ __attribute__((aligned(16))) float tab[NORM ? 4 : 1][32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 31, kk = lane >> 5;
-  for (int q = tid; q < 32 * G::K / 4; q += kFwdThreads) {
+  NormRegs nr;
+  if constexpr (NORM) {   // the partials' loads first, W's behind them
+    static_assert(G::CIN == 32, "the chain's inputs are 32-channel activations");
+    nr = norm_loads<kFwdThreads>(in, blockIdx.x == 0);
+  }
+  for (int q = tid; q < ((DTUPD_SKIP & 2) ? 0 : 32 * G::K / 4); q += kFwdThreads) {
     const int co = q / (G::K / 4), k4 = q - co * (G::K / 4);
     *reinterpret_cast<float4*>(ws + co * WST + 4 * k4) = reinterpret_cast<const float4*>(w)[q];
   }
-  __syncthreads();
+  if constexpr (NORM) norm_build<kFwdThreads>(in, nr, tab, blockIdx.x == 0);   // ends in a barrier
+  else __syncthreads();
   const int g = wave / KSPLIT, ks = wave - g * KSPLIT;
   const int tiles = n * G::TPS;
   const float* wrow = ws + col * WST + 4 * kk;
@@ -219,14 +400,23 @@ fwd_kernel(int n, const float* __restrict__ x, const float* __restrict__ w, floa
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
     const int s0 = ks * SPW;
-#pragma unroll 4
+    constexpr int kUnroll = NORM ? 2 : 4;   // NORM: its table reads need the registers
+#pragma unroll kUnroll
     for (int st = 0; st < SPW; ++st) {
       const int kc = 8 * (s0 + st);
-      const float4 a = ld4<G::CIN>(xl + G::koff(kc));
+      float4 a = (DTUPD_SKIP & 1) ? make_float4(xl[0], kc, st, 1.0f)
+                                  : ld4<G::CIN>(xl + G::koff(kc));
+      if constexpr (NORM) {   // channels c0 .. c0 + 3 of the previous block
+        const int c0 = (kc + 4 * kk) & 31;
+        a = norm4(a, *reinterpret_cast<const float4*>(&tab[0][c0]),
+                  *reinterpret_cast<const float4*>(&tab[1][c0]),
+                  *reinterpret_cast<const float4*>(&tab[2][c0]),
+                  *reinterpret_cast<const float4*>(&tab[3][c0]), in.slope);
+      }
       const float4 b = *reinterpret_cast<const float4*>(wrow + kc);
       acc = mfma4(a, b, acc);
     }
-    if constexpr (KSPLIT > 1) {   // slice ks > 0 of tile g at slot g * (KSPLIT - 1) + ks - 1
+    if constexpr (KSPLIT > 1 && !(DTUPD_SKIP & 8)) {   // slice ks > 0 of tile g at slot g * (KSPLIT - 1) + ks - 1
       float* rs = red + (size_t)g * (KSPLIT - 1) * 16 * 64 + lane;
       if (ks > 0)
 #pragma unroll
@@ -267,7 +457,9 @@ fwd_kernel(int n, const float* __restrict__ x, const float* __restrict__ w, floa
       }
     }
   }
-  if constexpr (STATS) merge_partials_last<kFwdThreads>(fb, w_n, w_mean, w_m2, (int64_t)n * G::OPIX);
+  if constexpr (STATS == 1 && !(DTUPD_SKIP & 4))
+    merge_partials_last<kFwdThreads>(fb, w_n, w_mean, w_m2, (int64_t)n * G::OPIX);
+  if constexpr (STATS == 2) wg_partial<kFwdThreads, false>(fb.work, w_n, w_mean, w_m2);
 }
 
 // ---- weight gradient -------------------------------------------------------------------
@@ -284,10 +476,12 @@ fwd_kernel(int n, const float* __restrict__ x, const float* __restrict__ w, floa
 template <class G>
 constexpr int wgrad_max_grid() { return G::CIN == 3 ? 512 : (G::OH > 20 ? 256 : 128); }
 
-template <class G, int NBW, int WAVES>
+// NORM: x is the previous block's z, staged as bn(leaky(z + bias)) with
+// in.mean_invstd (the chain's forward wrote it)
+template <class G, int NBW, int WAVES, bool NORM>
 __global__ void __launch_bounds__(64 * WAVES)
 wgrad_kernel(int n, const float* __restrict__ x, const float* __restrict__ dz,
-             float* __restrict__ part) {
+             float* __restrict__ part, DtUpdBn in) {
   static_assert(WAVES * NBW * 32 == G::K, "the waves cover K");
   constexpr int XROW = G::IW * G::CIN;       // floats of one input row
   constexpr int XT = G::KS * XROW;           // the rows one output row reads
@@ -298,6 +492,19 @@ wgrad_kernel(int n, const float* __restrict__ x, const float* __restrict__ dz,
   __shared__ __attribute__((aligned(16))) float ds[DT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 31, kk = lane >> 5;
+  // NORM: a thread's float4s are always channels 4 (tid & 7) .. + 3 (NT and a
+  // row's floats are multiples of 32)
+  float4 nb, nm, ns, nt;
+  if constexpr (NORM) {
+    static_assert(G::CIN == 32 && NT % 8 == 0, "32-channel rows");
+    const int c0 = 4 * (tid & 7);
+    nb = *reinterpret_cast<const float4*>(in.bias + c0);
+    nm = *reinterpret_cast<const float4*>(in.mean_invstd + c0);
+    const float4 is = *reinterpret_cast<const float4*>(in.mean_invstd + 32 + c0);
+    const float4 g = *reinterpret_cast<const float4*>(in.gamma + c0);
+    ns = make_float4(is.x * g.x, is.y * g.y, is.z * g.z, is.w * g.w);
+    nt = *reinterpret_cast<const float4*>(in.beta + c0);
+  }
   int kr[NBW];   // k's offset inside the staged rows
 #pragma unroll
   for (int b = 0; b < NBW; ++b) {
@@ -314,7 +521,11 @@ wgrad_kernel(int n, const float* __restrict__ x, const float* __restrict__ dz,
     const int sm = row / G::OH, oy = row - sm * G::OH;
     __syncthreads();                                    // the previous row's reads
     const float4* xsrc = reinterpret_cast<const float4*>(x + (size_t)(sm * G::IH + G::ST * oy) * XROW);
-    for (int i = tid; i < XT / 4; i += NT) reinterpret_cast<float4*>(xs)[i] = xsrc[i];
+    for (int i = tid; i < XT / 4; i += NT) {
+      float4 v = xsrc[i];
+      if constexpr (NORM) v = norm4(v, nb, nm, ns, nt, in.slope);
+      reinterpret_cast<float4*>(xs)[i] = v;
+    }
     const float4* dsrc = reinterpret_cast<const float4*>(dz + (size_t)row * DT);
     for (int i = tid; i < DT / 4; i += NT) reinterpret_cast<float4*>(ds)[i] = dsrc[i];
     __syncthreads();
@@ -468,28 +679,33 @@ int resident(const void* kern, int threads, int cap) {
   return g < cap ? g : cap;
 }
 
-template <class G, int KSPLIT, bool STATS>
-int launch_fwd(int n, const float* x, const float* w, float* z, const FwdBn& fb, hipStream_t s) {
+template <class G, int KSPLIT, int STATS, bool NORM>
+int launch_fwd(int n, const float* x, const float* w, float* z, const FwdBn& fb, const DtUpdBn& in,
+               hipStream_t s, int32_t* grid_out) {
   constexpr int GP = kFwdThreads / 64 / KSPLIT;
   const int tiles = n * G::TPS;
   int grid = (tiles + GP - 1) / GP;
-  // STATS: at most kMaxGrid partials (the last arriver merges them)
-  static const int res = resident(reinterpret_cast<const void*>(fwd_kernel<G, KSPLIT, STATS>),
-                                  kFwdThreads, STATS ? kMaxGrid : 1 << 20);
+  // STATS: at most kMaxGrid partials
+  static const int res =
+      resident(reinterpret_cast<const void*>(fwd_kernel<G, KSPLIT, STATS, NORM>), kFwdThreads,
+               STATS ? kMaxGrid : 1 << 20);
   grid = grid < res ? grid : res;
-  hipLaunchKernelGGL((fwd_kernel<G, KSPLIT, STATS>), dim3(grid), dim3(kFwdThreads), 0, s, n, x, w, z,
-                     fb);
+  hipLaunchKernelGGL((fwd_kernel<G, KSPLIT, STATS, NORM>), dim3(grid), dim3(kFwdThreads), 0, s, n,
+                     x, w, z, fb, in);
+  if (grid_out) *grid_out = grid;
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 
-template <bool STATS>
+template <int STATS, bool NORM>
 int dispatch_fwd(int l, int n, const float* x, const float* w, float* z, const FwdBn& fb,
-                 hipStream_t s) {
+                 const DtUpdBn& in, hipStream_t s, int32_t* grid_out = nullptr) {
   switch (l) {
-    case 1: return launch_fwd<L1, 2, STATS>(n, x, w, z, fb, s);
-    case 2: return launch_fwd<L2, 2, STATS>(n, x, w, z, fb, s);
-    case 3: return launch_fwd<L3, 8, STATS>(n, x, w, z, fb, s);
-    default: return launch_fwd<L4, 16, STATS>(n, x, w, z, fb, s);
+    case 1:
+      if constexpr (NORM) return DT_E_ARG;
+      else return launch_fwd<L1, 2, STATS, false>(n, x, w, z, fb, in, s, grid_out);
+    case 2: return launch_fwd<L2, 2, STATS, NORM>(n, x, w, z, fb, in, s, grid_out);
+    case 3: return launch_fwd<L3, 8, STATS, NORM>(n, x, w, z, fb, in, s, grid_out);
+    default: return launch_fwd<L4, 16, STATS, NORM>(n, x, w, z, fb, in, s, grid_out);
   }
 }
 
@@ -500,11 +716,12 @@ int wgrad_chunks(int n) {
   return rows < wgrad_max_grid<G>() ? rows : wgrad_max_grid<G>();
 }
 
-template <class G, int NBW, int WAVES>
-int launch_wgrad(int n, const float* x, const float* dz, float* dw, float* work, hipStream_t s) {
+template <class G, int NBW, int WAVES, bool NORM>
+int launch_wgrad(int n, const float* x, const DtUpdBn& in, const float* dz, float* dw, float* work,
+                 hipStream_t s) {
   const int chunks = wgrad_chunks<G>(n);
-  hipLaunchKernelGGL((wgrad_kernel<G, NBW, WAVES>), dim3(chunks), dim3(64 * WAVES), 0, s, n, x,
-                     dz, work);
+  hipLaunchKernelGGL((wgrad_kernel<G, NBW, WAVES, NORM>), dim3(chunks), dim3(64 * WAVES), 0, s, n,
+                     x, dz, work, in);
   const int len = 32 * G::K;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((len + kRedOut - 1) / kRedOut),
                      dim3(kRedOut * kRedWays), 0, s, chunks, len, work, dw);
@@ -520,6 +737,14 @@ int launch_dgrad(int n, const float* dz, const float* w, float* dx, hipStream_t 
   grid = grid < res ? grid : res;
   hipLaunchKernelGGL((dgrad_kernel<G, NW>), dim3(grid), dim3(64 * NW), 0, s, n, dz, w, dx);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+// a chain hand-off's required pointers
+bool valid_in(const DtUpdBn& b) {
+  return b.part && b.parts >= 1 && b.parts <= kMaxGrid && b.m >= 1 && b.bias && b.gamma &&
+         b.beta && b.running_mean && b.running_var && b.mean_invstd && b.updates >= 1;
 }
 
 // which of the four layers (0: none)
@@ -540,7 +765,7 @@ int dt_upd_conv_fwd(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih, 
   const int l = layer_of(cin, ks, st, ih, iw);
   if (!l || n < 0 || (n > 0 && (!x || !w || !z))) return DT_E_ARG;
   if (n == 0) return DT_OK;
-  return dispatch_fwd<false>(l, n, x, w, z, FwdBn{}, (hipStream_t)stream);
+  return dispatch_fwd<0, false>(l, n, x, w, z, FwdBn{}, DtUpdBn{}, (hipStream_t)stream);
 }
 
 int dt_upd_conv_fwd_bn(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih, int32_t iw,
@@ -554,7 +779,7 @@ int dt_upd_conv_fwd_bn(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t i
     return DT_E_ARG;
   const FwdBn fb{bias, slope, eps, momentum, running_mean, running_var, num_batches_tracked,
                  (int)updates, mean_invstd, work, guard};
-  return dispatch_fwd<true>(l, n, x, w, z, fb, (hipStream_t)stream);
+  return dispatch_fwd<1, false>(l, n, x, w, z, fb, DtUpdBn{}, (hipStream_t)stream);
 }
 
 int64_t dt_upd_bn_work_floats(void) { return (int64_t)kMaxGrid * 32 * 3 + 16; }
@@ -571,17 +796,63 @@ int64_t dt_upd_wgrad_work_floats(int32_t cin, int32_t ks, int32_t st, int32_t n,
   }
 }
 
-int dt_upd_conv_wgrad(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih, int32_t iw,
-                      const float* x, const float* dz, float* dw, float* work, void* stream) {
+int dt_upd_conv_wgrad_bn(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih, int32_t iw,
+                         const float* x, const DtUpdBn* in, const float* dz, float* dw,
+                         float* work, void* stream) {
   const int l = layer_of(cin, ks, st, ih, iw);
   if (!l || n < 1 || !x || !dz || !dw || !work) return DT_E_ARG;
+  if (in && (l == 1 || !in->mean_invstd || !in->bias || !in->gamma || !in->beta ||
+             !aligned16(in->mean_invstd) || !aligned16(in->bias) || !aligned16(in->gamma) ||
+             !aligned16(in->beta)))
+    return DT_E_ARG;
   hipStream_t s = (hipStream_t)stream;
+  const DtUpdBn b = in ? *in : DtUpdBn{};
   switch (l) {
-    case 1: return launch_wgrad<L1, 1, 6>(n, x, dz, dw, work, s);
-    case 2: return launch_wgrad<L2, 2, 8>(n, x, dz, dw, work, s);
-    case 3: return launch_wgrad<L3, 2, 8>(n, x, dz, dw, work, s);
-    default: return launch_wgrad<L4, 2, 8>(n, x, dz, dw, work, s);
+    case 1: return launch_wgrad<L1, 1, 6, false>(n, x, b, dz, dw, work, s);
+    case 2:
+      return in ? launch_wgrad<L2, 2, 8, true>(n, x, b, dz, dw, work, s)
+                : launch_wgrad<L2, 2, 8, false>(n, x, b, dz, dw, work, s);
+    case 3:
+      return in ? launch_wgrad<L3, 2, 8, true>(n, x, b, dz, dw, work, s)
+                : launch_wgrad<L3, 2, 8, false>(n, x, b, dz, dw, work, s);
+    default:
+      return in ? launch_wgrad<L4, 2, 8, true>(n, x, b, dz, dw, work, s)
+                : launch_wgrad<L4, 2, 8, false>(n, x, b, dz, dw, work, s);
   }
+}
+
+int dt_upd_conv_wgrad(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih, int32_t iw,
+                      const float* x, const float* dz, float* dw, float* work, void* stream) {
+  return dt_upd_conv_wgrad_bn(cin, ks, st, n, ih, iw, x, nullptr, dz, dw, work, stream);
+}
+
+int64_t dt_upd_part_floats(void) { return (int64_t)kMaxGrid * 32 * 3; }
+
+int dt_upd_conv_fwd_part(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih, int32_t iw,
+                         const float* x, const DtUpdBn* in, const float* w, const float* bias,
+                         float slope, float* z, float* part, int32_t* parts, void* stream) {
+  const int l = layer_of(cin, ks, st, ih, iw);
+  if (!l || n < 1 || !x || !w || !bias || !z || !part || !parts) return DT_E_ARG;
+  if (in && (l == 1 || !valid_in(*in))) return DT_E_ARG;
+  FwdBn fb{};
+  fb.bias = bias;
+  fb.slope = slope;
+  fb.work = part;
+  hipStream_t s = (hipStream_t)stream;
+  return in ? dispatch_fwd<2, true>(l, n, x, w, z, fb, *in, s, parts)
+            : dispatch_fwd<2, false>(l, n, x, w, z, fb, DtUpdBn{}, s, parts);
+}
+
+int dt_upd_bn_finish(int64_t m, const float* z, const DtUpdBn* bn, float* y, void* stream) {
+  if (m < 1 || !z || !y || !bn || !valid_in(*bn) || !aligned16(z) || !aligned16(y))
+    return DT_E_ARG;
+  const int64_t items = m * 8;
+  const int64_t per = 1024 * kFinishPer;
+  int64_t grid = (items + per - 1) / per;
+  grid = grid < kFinishMaxGrid ? grid : kFinishMaxGrid;
+  hipLaunchKernelGGL(bn_finish_kernel, dim3((unsigned)grid), dim3(1024), 0, (hipStream_t)stream, m,
+                     z, *bn, y);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 
 int dt_upd_conv_dgrad(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih, int32_t iw,

@@ -271,6 +271,179 @@ class _ConvBnLeaky(torch.autograd.Function):
         return dx, dw, g[0], g[1], g[2], None, None, None
 
 
+def _bn_handoff(bn, slope, part, parts, m, bias, gamma, beta, mi):
+    """include/dtupd.h DtUpdBn for block `bn` (pointers into live tensors)."""
+    nbt = bn.num_batches_tracked
+    g = getattr(bn, '_dt_guard', None)
+    return _lib.DtUpdBn(part.data_ptr(), int(parts), int(m), bias.data_ptr(), gamma.data_ptr(),
+                        beta.data_ptr(), float(slope), float(bn.eps), float(bn.momentum),
+                        bn.running_mean.data_ptr(), bn.running_var.data_ptr(),
+                        nbt.data_ptr() if nbt is not None else None,
+                        int(getattr(bn, '_dt_updates', 1)), mi.data_ptr(),
+                        g.ptr() if g is not None else None)
+
+
+def _part(bn, dev):
+    """Block `bn`'s partials buffer for the chain (a plain attribute)."""
+    w = getattr(bn, '_dt_part', None)
+    if w is None or w.device != dev:
+        w = torch.empty(int(_lib.lib().dt_upd_part_floats()), device=dev)
+        bn._dt_part = w
+    return w
+
+
+class _ConvTrunk(torch.autograd.Function):
+    """A chain of train-mode blocks bn_j(leaky(conv_j(.) + bias_j)) on the
+    include/dtupd.h chain kernels: conv j + 1 merges block j's statistics
+    itself and normalises z_j while loading it, so neither a last-arrival
+    merge nor y_j (a normalisation pass, a full-size tensor) exists except for
+    the last block (dt_upd_bn_finish).  Backward: dt_bn_leaky_bwd per block,
+    the weight gradient normalising z_j again while staging
+    (dt_upd_conv_wgrad_bn), the input gradient (dt_upd_conv_dgrad).  Outputs,
+    running statistics and gradients are the block-by-block path's bit for
+    bit (tests/test_gpu_upd_conv.py)."""
+
+    @staticmethod
+    def forward(ctx, x, meta, *params):
+        bns, slopes, strides = meta
+        cl = torch.channels_last
+        L = _lib.lib()
+        dev = x.device
+        s = _stream(dev)
+        x = x.contiguous(memory_format=cl)
+        ws = [params[4 * j].contiguous(memory_format=cl) for j in range(len(bns))]
+        zs, mis = [], []
+        prev = None          # the previous block's DtUpdBn
+        cur = x
+        for j, bn in enumerate(bns):
+            bias, gamma, beta = params[4 * j + 1: 4 * j + 4]
+            n, cin, ih, iw = cur.shape
+            ks, st = ws[j].shape[2], strides[j]
+            oh, ow = (ih - ks) // st + 1, (iw - ks) // st + 1
+            z = torch.empty((n, C, oh, ow), device=dev, dtype=x.dtype, memory_format=cl)
+            part = _part(bn, dev)
+            parts = ctypes.c_int32(0)
+            rc = L.dt_upd_conv_fwd_part(cin, ks, st, n, ih, iw, cur.data_ptr(),
+                                        ctypes.byref(prev) if prev is not None else None,
+                                        ws[j].data_ptr(), bias.data_ptr(), slopes[j], z.data_ptr(),
+                                        part.data_ptr(), ctypes.byref(parts), s)
+            if rc != 0:
+                raise _lib.DtError('dt_upd_conv_fwd_part failed (%d)' % rc)
+            mi = torch.empty(2 * C, device=dev)
+            prev = _bn_handoff(bn, slopes[j], part, parts.value, n * oh * ow, bias, gamma, beta,
+                               mi)
+            zs.append(z)
+            mis.append(mi)
+            cur = z
+        y = torch.empty_like(cur)
+        rc = L.dt_upd_bn_finish(cur.numel() // C, cur.data_ptr(), ctypes.byref(prev), y.data_ptr(),
+                                s)
+        if rc != 0:
+            raise _lib.DtError('dt_upd_bn_finish failed (%d)' % rc)
+        ctx.save_for_backward(x, *ws, *zs, *mis, *params)
+        ctx.meta, ctx.k = meta, len(bns)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        bns, slopes, strides = ctx.meta
+        k = ctx.k
+        saved = ctx.saved_tensors
+        x, ws, zs, mis, params = (saved[0], saved[1:1 + k], saved[1 + k:1 + 2 * k],
+                                  saved[1 + 2 * k:1 + 3 * k], saved[1 + 3 * k:])
+        cl = torch.channels_last
+        L = _lib.lib()
+        dev = x.device
+        s = _stream(dev)
+        grads = [None] * (4 * k)
+        dx = None
+        dyj = dy.contiguous(memory_format=cl)
+        for j in range(k - 1, -1, -1):
+            bias, gamma, beta = params[4 * j + 1: 4 * j + 4]
+            z = zs[j]
+            dz = torch.empty_like(z)
+            g = torch.empty(3, C, device=dev)      # dbias, dgamma, dbeta
+            rc = L.dt_bn_leaky_bwd(z.numel() // C, dyj.data_ptr(), z.data_ptr(), bias.data_ptr(),
+                                   mis[j].data_ptr(), gamma.data_ptr(), slopes[j], dz.data_ptr(),
+                                   g[0].data_ptr(), g[1].data_ptr(), g[2].data_ptr(),
+                                   _work(bns[j], 'bwd', dev).data_ptr(), _guard(bns[j]), s)
+            if rc != 0:
+                raise _lib.DtError('dt_bn_leaky_bwd failed (%d)' % rc)
+            grads[4 * j + 1], grads[4 * j + 2], grads[4 * j + 3] = g[0], g[1], g[2]
+            xin = x if j == 0 else zs[j - 1]
+            n, cin, ih, iw = xin.shape
+            w, st = ws[j], strides[j]
+            ks = w.shape[2]
+            hand = None
+            if j > 0:
+                pb, pg, pbt = params[4 * j - 3: 4 * j]
+                hand = _bn_handoff(bns[j - 1], slopes[j - 1], _part(bns[j - 1], dev), 1, 1, pb,
+                                   pg, pbt, mis[j - 1])
+            if ctx.needs_input_grad[2 + 4 * j]:
+                work = torch.empty(int(L.dt_upd_wgrad_work_floats(cin, ks, st, n, ih, iw)),
+                                   device=dev)
+                dw = torch.empty_like(w)
+                rc = L.dt_upd_conv_wgrad_bn(cin, ks, st, n, ih, iw, xin.data_ptr(),
+                                            ctypes.byref(hand) if hand is not None else None,
+                                            dz.data_ptr(), dw.data_ptr(), work.data_ptr(), s)
+                if rc != 0:
+                    raise _lib.DtError('dt_upd_conv_wgrad_bn failed (%d)' % rc)
+                grads[4 * j] = dw
+            if j > 0:
+                dyj = torch.empty_like(xin)
+                rc = L.dt_upd_conv_dgrad(cin, ks, st, n, ih, iw, dz.data_ptr(), w.data_ptr(),
+                                         dyj.data_ptr(), s)
+                if rc != 0:
+                    raise _lib.DtError('dt_upd_conv_dgrad failed (%d)' % rc)
+            elif ctx.needs_input_grad[0]:
+                dx = torch.nn.grad.conv2d_input(x.shape, w, dz, stride=st)
+        return (dx, None) + tuple(grads)
+
+
+# the chain kernels for runs of >= 2 blocks (False: block by block, for A/B runs)
+CHAIN = True
+
+
+def trunk_len(x, mods, i, k):
+    """How many consecutive train-mode blocks (conv, LeakyReLU, BatchNorm) of
+    mods[i:k], starting at mods[i] with input shape x.shape, the chain kernels
+    take (0 or >= 2): every conv one of include/dtupd.h's layers, every block
+    fused-tail applicable."""
+    if not (CHAIN and x.is_cuda and x.dtype == torch.float32 and x.dim() == 4):
+        return 0
+    shape = tuple(x.shape)
+    j = i
+    while j + 2 < k:
+        conv, act, bn = mods[j], mods[j + 1], mods[j + 2]
+        c = getattr(conv, 'kernel', None)
+        if c is None or not isinstance(bn, nn.BatchNorm2d) or not isinstance(act, nn.LeakyReLU):
+            break
+        if not applicable(x, c, act, bn):
+            break
+        w = c.weight
+        st = c.stride[0]
+        if (c.stride[0] != c.stride[1] or w.shape[2] != w.shape[3] or w.shape[1] != shape[1]
+                or (shape[1], w.shape[2], st, shape[2], shape[3]) not in UPD_CONV_LAYERS):
+            break
+        ks = w.shape[2]
+        shape = (shape[0], C, (shape[2] - ks) // st + 1, (shape[3] - ks) // st + 1)
+        j += 3
+    blocks = (j - i) // 3
+    return blocks if blocks >= 2 else 0
+
+
+def conv_trunk(x, mods, i, blocks):
+    """The chain of `blocks` blocks starting at mods[i] (trunk_len) on x."""
+    convs = [mods[i + 3 * b].kernel for b in range(blocks)]
+    acts = [mods[i + 3 * b + 1] for b in range(blocks)]
+    bns = [mods[i + 3 * b + 2] for b in range(blocks)]
+    meta = (bns, [float(a.negative_slope) for a in acts], [int(c.stride[0]) for c in convs])
+    params = []
+    for c, bn in zip(convs, bns):
+        params += [c.weight, c.bias, bn.weight, bn.bias]
+    return _ConvTrunk.apply(x, meta, *params)
+
+
 def conv_leaky_bn(x, conv, act, bn):
     """bn(act(conv(x))) for a train-mode block (see the module docstring)."""
     if upd_conv_applicable(x, conv):

@@ -43,7 +43,9 @@ extern "C" {
                              8: dttrain.h non-finite guards: dt_guard_scan, a
                                 guard word for dt_bn_leaky_fwd / _bwd / dt_adam;
                                 dtactor.h reference-mode partials [n, 32, 3]
-                                (mean, M2, centre) with centred activations */
+                                (mean, M2, centre) with centred activations;
+                                dtupd.h (the update's convolutions and the
+                                conv trunk's BatchNorm hand-off) */
 
 /* error codes */
 #define DT_OK 0

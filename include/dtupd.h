@@ -51,6 +51,55 @@ int dt_upd_conv_fwd_bn(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t i
 
 int64_t dt_upd_bn_work_floats(void);
 
+/* ---- a chain of blocks (the conv trunk) ---------------------------------------------
+ * Block j's BatchNorm statistics leave its forward as per-workgroup partials
+ * and are merged by the NEXT kernel, which normalises while it loads:
+ *   dt_upd_conv_fwd_part(block j + 1's conv, x = z_j, in = block j's BN) reads
+ *   z_j, applies y_j = bn_j(leaky(z_j + bias_j)) to every value it loads, and
+ *   writes z_{j+1} and block j + 1's partials; its first workgroup writes
+ *   block j's mean_invstd, running statistics, num_batches_tracked and guard
+ *   reports;
+ *   dt_upd_bn_finish(last block) merges the last partials and writes y.
+ * y_j itself is never stored: dt_upd_conv_wgrad_bn normalises z_j the same
+ * way when it stages block j + 1's input rows.  Values equal the
+ * block-by-block path's (dt_upd_conv_fwd_bn + dt_bn_leaky_apply) bit for bit:
+ * same partials, same merge order, same formula. */
+typedef struct DtUpdBn {
+  const float* part;             /* the producer's partials [parts][32][3] */
+  int32_t parts;                 /* as dt_upd_conv_fwd_part returned them */
+  int64_t m;                     /* pixels the partials cover (n * OH * OW) */
+  const float* bias;             /* conv bias [32] (added before leaky_relu) */
+  const float* gamma;            /* BatchNorm weight [32] */
+  const float* beta;             /* BatchNorm bias [32] */
+  float slope, eps, momentum;
+  float* running_mean;           /* [32], moved `updates` times */
+  float* running_var;
+  int64_t* num_batches_tracked;  /* may be NULL */
+  int32_t updates;
+  float* mean_invstd;            /* [64] out: batch mean, 1 / sqrt(biased var + eps) */
+  int32_t* guard;                /* DT_GUARD_BN_COUNT / _FWD reports; may be NULL */
+} DtUpdBn;
+
+/* floats of one partials buffer (any layer) */
+int64_t dt_upd_part_floats(void);
+
+/* z = conv(x') with x' = x (in == NULL: the observation) or bn_in(leaky(x +
+ * bias_in)) (in: the previous block); this block's statistics of
+ * leaky(z + bias) go to part ([dt_upd_part_floats()]), *parts = how many. */
+int dt_upd_conv_fwd_part(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih, int32_t iw,
+                         const float* x, const DtUpdBn* in, const float* w, const float* bias,
+                         float slope, float* z, float* part, int32_t* parts, void* stream);
+
+/* y = bn(leaky(z + bias)) for the chain's last block (z [m, 32]): merges
+ * bn->part and writes mean_invstd / running statistics as above */
+int dt_upd_bn_finish(int64_t m, const float* z, const DtUpdBn* bn, float* y, void* stream);
+
+/* dt_upd_conv_wgrad with the input x' = bn_in(leaky(x + bias_in)) made while
+ * staging (in->mean_invstd as the forward wrote it; in == NULL: x as is) */
+int dt_upd_conv_wgrad_bn(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih, int32_t iw,
+                         const float* x, const DtUpdBn* in, const float* dz, float* dw,
+                         float* work, void* stream);
+
 /* Floats of scratch dt_upd_conv_wgrad needs for these dimensions (per-chunk
  * partial weight gradients, reduced in a fixed order: deterministic). */
 int64_t dt_upd_wgrad_work_floats(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih,

@@ -141,3 +141,61 @@ def test_conv_block_autograd_matches_miopen(gpu):
     assert torch.allclose(q1, q0, rtol=1e-4, atol=1e-5)
     for a, b in zip(g1, g0):
         assert torch.allclose(a, b, rtol=1e-3, atol=1e-5 * max(1.0, b.abs().max().item()))
+
+
+@pytest.mark.parametrize('n,updates', [(5, 1), (64, 2)])
+def test_trunk_chain_equals_block_path(gpu, n, updates):
+    """The conv trunk as one chain (train_ops.conv_trunk: each conv merges the
+    previous block's statistics and normalises on load) against the same
+    network block by block (dt_upd_conv_fwd_bn + dt_bn_leaky_apply): output,
+    running statistics, num_batches_tracked and every gradient bit for bit
+    (same partials, merge order and formulas, include/dtupd.h)."""
+    from conftest import golden
+    from test_trainer import no_dropout
+
+    from aido1_amd import train_ops
+    from aido1_amd.actor import ConfigCritic
+    cfg = golden('reference_config.json')
+    torch.manual_seed(7)
+    crit = ConfigCritic(no_dropout(cfg['model']['critic'])).to(gpu).to(memory_format=CL).train()
+    obs = torch.rand(n, 3, 120, 160, device=gpu).contiguous(memory_format=CL)
+    act = torch.rand(n, 2, device=gpu)
+    mods = crit.net.input_nets[0].internal_modules
+    assert train_ops.trunk_len(obs, mods, 0, len(mods)) == 4
+
+    def run():
+        for p in crit.parameters():
+            p.grad = None
+        with train_ops.running_updates(crit, updates):
+            q = crit(obs, act)
+        q.square().sum().backward()
+        return (q.detach().clone(), [p.grad.detach().clone() for p in crit.parameters()],
+                [b.detach().clone() for b in crit.buffers()])
+
+    state = {k: v.clone() for k, v in crit.state_dict().items()}
+    q1, g1, b1 = run()
+    crit.load_state_dict(state)
+    train_ops.CHAIN = False
+    try:
+        q0, g0, b0 = run()
+    finally:
+        train_ops.CHAIN = True
+    assert torch.equal(q1, q0)
+    for a, b in zip(g1, g0):
+        assert torch.equal(a, b)
+    for a, b in zip(b1, b0):
+        assert torch.equal(a, b)
+    assert int(b1[-1]) == updates                     # num_batches_tracked of the last BN
+
+
+def test_chain_rejects_bad_handoff(gpu):
+    from aido1_amd import _lib
+    L = _lib.lib()
+    b = _lib.DtUpdBn()                                # all NULL
+    import ctypes
+    parts = ctypes.c_int32(0)
+    x = torch.zeros(1, 57, 77, 32, device=gpu)
+    assert L.dt_upd_conv_fwd_part(32, 4, 2, 1, 57, 77, x.data_ptr(), ctypes.byref(b), x.data_ptr(),
+                                  x.data_ptr(), 0.01, x.data_ptr(), x.data_ptr(),
+                                  ctypes.byref(parts), None) != 0
+    assert L.dt_upd_bn_finish(1, x.data_ptr(), ctypes.byref(b), x.data_ptr(), None) != 0

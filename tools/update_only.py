@@ -1,0 +1,49 @@
+"""Diagnostic (GPU): the DDPG update alone (config.json networks with their
+dropout, batch 64, graph mode) on one synthetic batch, for a per-update kernel
+profile: rocprofv3 --kernel-trace --stats -- python3 tools/update_only.py
+Prints the median update time over the timed updates."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from aido1_amd.actor import ConfigActor, ConfigCritic  # noqa: E402
+from aido1_amd.trainer import DDPGTrainer  # noqa: E402
+
+
+def main():
+    n_up = int(os.environ.get('UPDATES', '50'))
+    with open(os.path.join(os.path.dirname(__file__), '..', 'aido1_amd', 'configs',
+                           'reference_config.json')) as f:
+        cfg = json.load(f)
+    torch.manual_seed(0)
+    dev = torch.device('cuda', 0)
+    tr = DDPGTrainer(cfg, ConfigActor(cfg['model']['actor']), ConfigCritic(cfg['model']['critic']),
+                     device=dev, graph=True)
+    b = 64
+    g = torch.Generator(device=dev).manual_seed(1)
+    batch = (torch.rand(b, 3, 120, 160, device=dev, generator=g),
+             torch.rand(b, 2, device=dev, generator=g) * 2 - 1,
+             torch.rand(b, device=dev, generator=g),
+             torch.rand(b, 3, 120, 160, device=dev, generator=g),
+             torch.zeros(b, dtype=torch.bool, device=dev))
+    for _ in range(5):
+        tr.update(batch)
+    torch.cuda.synchronize()
+    times = []
+    for _ in range(n_up):
+        a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        tr.update(batch)
+        e.record()
+        torch.cuda.synchronize()
+        times.append(a.elapsed_time(e))
+    tr.check()
+    print('update %.3f ms (median of %d)' % (float(np.median(times)), n_up))
+
+
+if __name__ == '__main__':
+    main()
