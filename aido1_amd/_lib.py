@@ -196,7 +196,7 @@ def lib():
                                                     ctypes.POINTER(DtUpdBn), vp, vp,
                                                     ctypes.c_float, vp, vp,
                                                     ctypes.POINTER(i32), vp]),
-            'dt_upd_bn_finish': (ctypes.c_int, [i64, vp, ctypes.POINTER(DtUpdBn), vp, vp]),
+            'dt_upd_bn_finish': (ctypes.c_int, [i64, i32, vp, ctypes.POINTER(DtUpdBn), vp, vp]),
             'dt_upd_conv_wgrad_bn': (ctypes.c_int, [i32, i32, i32, i32, i32, i32, vp,
                                                     ctypes.POINTER(DtUpdBn), vp, vp, vp, vp]),
             'dt_soft_update': (ctypes.c_int, [i32, vp, vp, f64, vp]),

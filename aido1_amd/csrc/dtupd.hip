@@ -314,7 +314,7 @@ constexpr int kFinishPer = 4;       // float4s a thread
 constexpr int kFinishMaxGrid = 1024;
 
 __global__ void __launch_bounds__(1024)
-bn_finish_kernel(int64_t m, const float* __restrict__ z, DtUpdBn b, float* __restrict__ y) {
+bn_finish_kernel(int64_t m, int hw, const float* __restrict__ z, DtUpdBn b, float* __restrict__ y) {
   __shared__ __attribute__((aligned(16))) float tab[4][32];
   const bool fin = blockIdx.x == 0;
   const NormRegs r = norm_loads<1024>(b, fin);
@@ -334,14 +334,27 @@ bn_finish_kernel(int64_t m, const float* __restrict__ z, DtUpdBn b, float* __res
   const float4 tm = reinterpret_cast<const float4*>(tab[1])[cg];
   const float4 ts = reinterpret_cast<const float4*>(tab[2])[cg];
   const float4 tt = reinterpret_cast<const float4*>(tab[3])[cg];
+  // y as z (hw == 0) or NCHW with hw pixels a sample (the flatten that
+  // follows the trunk is then a view)
+  auto put = [&](int64_t q, float4 o) __attribute__((always_inline)) {
+    if (hw == 0) {
+      reinterpret_cast<float4*>(y)[q] = o;
+    } else {
+      const int64_t pix = q >> 3, smp = pix / hw;
+      float* d = y + (smp * 32 + 4 * cg) * hw + (pix - smp * hw);
+      d[0] = o.x;
+      d[hw] = o.y;
+      d[2 * hw] = o.z;
+      d[3 * hw] = o.w;
+    }
+  };
 #pragma unroll
   for (int k = 0; k < kFinishPer; ++k) {
     const int64_t q = q0 + k * stride;
-    if (q < items) reinterpret_cast<float4*>(y)[q] = norm4(v[k], tb, tm, ts, tt, b.slope);
+    if (q < items) put(q, norm4(v[k], tb, tm, ts, tt, b.slope));
   }
   for (int64_t q = q0 + kFinishPer * stride; q < items; q += stride)   // past the grid's cover
-    reinterpret_cast<float4*>(y)[q] =
-        norm4(reinterpret_cast<const float4*>(z)[q], tb, tm, ts, tt, b.slope);
+    put(q, norm4(reinterpret_cast<const float4*>(z)[q], tb, tm, ts, tt, b.slope));
 }
 
 // ---- forward ---------------------------------------------------------------------------
@@ -353,6 +366,7 @@ bn_finish_kernel(int64_t m, const float* __restrict__ z, DtUpdBn b, float* __res
 // tile, each a slice of K, summed through LDS (the small layers: more waves
 // than tiles).
 constexpr int kFwdThreads = 1024;
+constexpr int kFwdAllLoads = 16;    // slices of up to this many k-steps load all A first
 
 
 // STATS: 0 none, 1 merged by the last workgroup (dt_upd_conv_fwd_bn), 2
@@ -400,13 +414,14 @@ fwd_kernel(int n, const float* __restrict__ x, const float* __restrict__ w, floa
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
     const int s0 = ks * SPW;
-    constexpr int kUnroll = NORM ? 2 : 4;   // NORM: its table reads need the registers
-#pragma unroll kUnroll
-    for (int st = 0; st < SPW; ++st) {
+    // one step: A (normalised for NORM: channels c0 .. c0 + 3 of the previous
+    // block) times W's float4 from LDS, four MFMAs
+    auto step = [&](int st, float4 a) {
       const int kc = 8 * (s0 + st);
-      float4 a = (DTUPD_SKIP & 1) ? make_float4(xl[0], kc, st, 1.0f)
-                                  : ld4<G::CIN>(xl + G::koff(kc));
-      if constexpr (NORM) {   // channels c0 .. c0 + 3 of the previous block
+      if constexpr (NORM) {
+        // its table reads stay here (hoisted over the slice they need a
+        // slice's worth of registers)
+        asm volatile("" ::: "memory");
         const int c0 = (kc + 4 * kk) & 31;
         a = norm4(a, *reinterpret_cast<const float4*>(&tab[0][c0]),
                   *reinterpret_cast<const float4*>(&tab[1][c0]),
@@ -415,6 +430,24 @@ fwd_kernel(int n, const float* __restrict__ x, const float* __restrict__ w, floa
       }
       const float4 b = *reinterpret_cast<const float4*>(wrow + kc);
       acc = mfma4(a, b, acc);
+    };
+    auto load = [&](int st) -> float4 {
+      const int kc = 8 * (s0 + st);
+      return (DTUPD_SKIP & 1) ? make_float4(xl[0], kc, st, 1.0f) : ld4<G::CIN>(xl + G::koff(kc));
+    };
+    if constexpr (SPW <= kFwdAllLoads) {
+      // every A load of the slice in flight before the first MFMA: one
+      // latency a tile, the SIMD's other waves' MFMAs covering it
+      float4 av[SPW];
+#pragma unroll
+      for (int st = 0; st < SPW; ++st) av[st] = load(st);
+      asm volatile("" ::: "memory");   // keeps the scheduler from sinking loads into the MFMAs
+#pragma unroll
+      for (int st = 0; st < SPW; ++st) step(st, av[st]);
+    } else {
+      constexpr int kUnroll = NORM ? 2 : 4;   // NORM: its table reads need the registers
+#pragma unroll kUnroll
+      for (int st = 0; st < SPW; ++st) step(st, load(st));
     }
     if constexpr (KSPLIT > 1 && !(DTUPD_SKIP & 8)) {   // slice ks > 0 of tile g at slot g * (KSPLIT - 1) + ks - 1
       float* rs = red + (size_t)g * (KSPLIT - 1) * 16 * 64 + lane;
@@ -478,8 +511,8 @@ constexpr int wgrad_max_grid() { return G::CIN == 3 ? 512 : (G::OH > 20 ? 256 : 
 
 // NORM: x is the previous block's z, staged as bn(leaky(z + bias)) with
 // in.mean_invstd (the chain's forward wrote it)
-template <class G, int NBW, int WAVES, bool NORM>
-__global__ void __launch_bounds__(64 * WAVES)
+template <class G, int NBW, int WAVES, bool NORM, bool DB>
+__global__ void __launch_bounds__(64 * WAVES) __attribute__((amdgpu_waves_per_eu(1, 4)))
 wgrad_kernel(int n, const float* __restrict__ x, const float* __restrict__ dz,
              float* __restrict__ part, DtUpdBn in) {
   static_assert(WAVES * NBW * 32 == G::K, "the waves cover K");
@@ -488,8 +521,9 @@ wgrad_kernel(int n, const float* __restrict__ x, const float* __restrict__ dz,
   constexpr int DT = G::OW * 32;
   static_assert(XROW % 4 == 0 && DT % 4 == 0, "float4 staging");
   constexpr int NT = 64 * WAVES;
-  __shared__ __attribute__((aligned(16))) float xs[XT];
-  __shared__ __attribute__((aligned(16))) float ds[DT];
+  constexpr int NB = DB ? 2 : 1;             // staging buffers
+  __shared__ __attribute__((aligned(16))) float xs[NB][XT];
+  __shared__ __attribute__((aligned(16))) float ds[NB][DT];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 31, kk = lane >> 5;
   // NORM: a thread's float4s are always channels 4 (tid & 7) .. + 3 (NT and a
@@ -517,29 +551,79 @@ wgrad_kernel(int n, const float* __restrict__ x, const float* __restrict__ dz,
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[b][r] = 0.0f;
   const int rows = n * G::OH;
-  for (int row = blockIdx.x; row < rows; row += gridDim.x) {
-    const int sm = row / G::OH, oy = row - sm * G::OH;
-    __syncthreads();                                    // the previous row's reads
-    const float4* xsrc = reinterpret_cast<const float4*>(x + (size_t)(sm * G::IH + G::ST * oy) * XROW);
-    for (int i = tid; i < XT / 4; i += NT) {
-      float4 v = xsrc[i];
-      if constexpr (NORM) v = norm4(v, nb, nm, ns, nt, in.slope);
-      reinterpret_cast<float4*>(xs)[i] = v;
-    }
-    const float4* dsrc = reinterpret_cast<const float4*>(dz + (size_t)row * DT);
-    for (int i = tid; i < DT / 4; i += NT) reinterpret_cast<float4*>(ds)[i] = dsrc[i];
-    __syncthreads();
+  // a row's staging as loads into registers (fetch) and LDS stores (commit):
+  // DB fetches row i + 1 before row i's MFMAs and commits it after them
+  constexpr int PX = (XT / 4 + NT - 1) / NT, PD = (DT / 4 + NT - 1) / NT;
+  float4 rx0, rx1, rx2, rx3, rx4, rx5, rd0, rd1;   // PX <= 6, PD <= 2 (asserted)
+  static_assert(PX <= 6 && PD <= 2, "staging registers");
+#define DTUPD_FETCH(ROW)                                                                          \
+  do {                                                                                           \
+    const int sm_ = (ROW) / G::OH, oy_ = (ROW) - sm_ * G::OH;                                    \
+    const float4* xsrc_ =                                                                        \
+        reinterpret_cast<const float4*>(x + (size_t)(sm_ * G::IH + G::ST * oy_) * XROW) + tid;   \
+    const float4* dsrc_ = reinterpret_cast<const float4*>(dz + (size_t)(ROW) * DT) + tid;        \
+    if (0 < PX && tid + 0 * NT < XT / 4) rx0 = xsrc_[0 * NT];                                     \
+    if (1 < PX && tid + 1 * NT < XT / 4) rx1 = xsrc_[1 * NT];                                     \
+    if (2 < PX && tid + 2 * NT < XT / 4) rx2 = xsrc_[2 * NT];                                     \
+    if (3 < PX && tid + 3 * NT < XT / 4) rx3 = xsrc_[3 * NT];                                     \
+    if (4 < PX && tid + 4 * NT < XT / 4) rx4 = xsrc_[4 * NT];                                     \
+    if (5 < PX && tid + 5 * NT < XT / 4) rx5 = xsrc_[5 * NT];                                     \
+    if (0 < PD && tid + 0 * NT < DT / 4) rd0 = dsrc_[0 * NT];                                     \
+    if (1 < PD && tid + 1 * NT < DT / 4) rd1 = dsrc_[1 * NT];                                     \
+  } while (0)
+  auto put = [&](int buf, int i, float4 v) __attribute__((always_inline)) {
+    if constexpr (NORM) v = norm4(v, nb, nm, ns, nt, in.slope);
+    reinterpret_cast<float4*>(xs[buf])[tid + i * NT] = v;
+  };
+  auto commit = [&](int buf) __attribute__((always_inline)) {
+    if (0 < PX && tid + 0 * NT < XT / 4) put(buf, 0, rx0);
+    if (1 < PX && tid + 1 * NT < XT / 4) put(buf, 1, rx1);
+    if (2 < PX && tid + 2 * NT < XT / 4) put(buf, 2, rx2);
+    if (3 < PX && tid + 3 * NT < XT / 4) put(buf, 3, rx3);
+    if (4 < PX && tid + 4 * NT < XT / 4) put(buf, 4, rx4);
+    if (5 < PX && tid + 5 * NT < XT / 4) put(buf, 5, rx5);
+    if (0 < PD && tid + 0 * NT < DT / 4) reinterpret_cast<float4*>(ds[buf])[tid] = rd0;
+    if (1 < PD && tid + 1 * NT < DT / 4) reinterpret_cast<float4*>(ds[buf])[tid + NT] = rd1;
+  };
+  auto compute = [&](int buf) __attribute__((always_inline)) {
+    const float* xb = xs[buf];
+    const float* db = ds[buf];
 #pragma unroll 2
     for (int ox0 = 0; ox0 < G::OW; ox0 += 2) {
       const int ox = ox0 + kk;
       const bool ok = ox < G::OW;
-      const float a = ok ? ds[ox * 32 + col] : 0.0f;
+      const float a = ok ? db[ox * 32 + col] : 0.0f;
       const int xo = (ok ? ox : 0) * G::ST * G::CIN;
 #pragma unroll
       for (int b = 0; b < NBW; ++b)
-        acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, xs[xo + kr[b]], acc[b], 0, 0, 0);
+        acc[b] = __builtin_amdgcn_mfma_f32_32x32x2f32(a, xb[xo + kr[b]], acc[b], 0, 0, 0);
+    }
+  };
+  if constexpr (DB) {
+    int buf = 0;
+    if ((int)blockIdx.x < rows) {
+      DTUPD_FETCH((int)blockIdx.x);
+      commit(0);
+    }
+    __syncthreads();
+    for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+      const int next = row + gridDim.x;
+      if (next < rows) DTUPD_FETCH(next);     // in flight during this row's MFMAs
+      compute(buf);
+      if (next < rows) commit(buf ^ 1);       // the other buffer: its readers passed the barrier
+      __syncthreads();
+      buf ^= 1;
+    }
+  } else {
+    for (int row = blockIdx.x; row < rows; row += gridDim.x) {
+      __syncthreads();                        // the previous row's reads
+      DTUPD_FETCH(row);
+      commit(0);
+      __syncthreads();
+      compute(0);
     }
   }
+#undef DTUPD_FETCH
   // D[co][k]: lane (k = block * 32 + col), rows co
   float* pp = part + (size_t)blockIdx.x * 32 * G::K;
 #pragma unroll
@@ -702,8 +786,8 @@ int dispatch_fwd(int l, int n, const float* x, const float* w, float* z, const F
   switch (l) {
     case 1:
       if constexpr (NORM) return DT_E_ARG;
-      else return launch_fwd<L1, 2, STATS, false>(n, x, w, z, fb, in, s, grid_out);
-    case 2: return launch_fwd<L2, 2, STATS, NORM>(n, x, w, z, fb, in, s, grid_out);
+      else return launch_fwd<L1, 4, STATS, false>(n, x, w, z, fb, in, s, grid_out);
+    case 2: return launch_fwd<L2, 8, STATS, NORM>(n, x, w, z, fb, in, s, grid_out);
     case 3: return launch_fwd<L3, 8, STATS, NORM>(n, x, w, z, fb, in, s, grid_out);
     default: return launch_fwd<L4, 16, STATS, NORM>(n, x, w, z, fb, in, s, grid_out);
   }
@@ -716,12 +800,12 @@ int wgrad_chunks(int n) {
   return rows < wgrad_max_grid<G>() ? rows : wgrad_max_grid<G>();
 }
 
-template <class G, int NBW, int WAVES, bool NORM>
+template <class G, int NBW, int WAVES, bool NORM, bool DB = false>
 int launch_wgrad(int n, const float* x, const DtUpdBn& in, const float* dz, float* dw, float* work,
                  hipStream_t s) {
   const int chunks = wgrad_chunks<G>(n);
-  hipLaunchKernelGGL((wgrad_kernel<G, NBW, WAVES, NORM>), dim3(chunks), dim3(64 * WAVES), 0, s, n,
-                     x, dz, work, in);
+  hipLaunchKernelGGL((wgrad_kernel<G, NBW, WAVES, NORM, DB>), dim3(chunks), dim3(64 * WAVES), 0, s,
+                     n, x, dz, work, in);
   const int len = 32 * G::K;
   hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((len + kRedOut - 1) / kRedOut),
                      dim3(kRedOut * kRedWays), 0, s, chunks, len, work, dw);
@@ -808,7 +892,7 @@ int dt_upd_conv_wgrad_bn(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t
   hipStream_t s = (hipStream_t)stream;
   const DtUpdBn b = in ? *in : DtUpdBn{};
   switch (l) {
-    case 1: return launch_wgrad<L1, 1, 6, false>(n, x, b, dz, dw, work, s);
+    case 1: return launch_wgrad<L1, 1, 6, false, true>(n, x, b, dz, dw, work, s);
     case 2:
       return in ? launch_wgrad<L2, 2, 8, true>(n, x, b, dz, dw, work, s)
                 : launch_wgrad<L2, 2, 8, false>(n, x, b, dz, dw, work, s);
@@ -843,15 +927,17 @@ int dt_upd_conv_fwd_part(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t
             : dispatch_fwd<2, false>(l, n, x, w, z, fb, DtUpdBn{}, s, parts);
 }
 
-int dt_upd_bn_finish(int64_t m, const float* z, const DtUpdBn* bn, float* y, void* stream) {
-  if (m < 1 || !z || !y || !bn || !valid_in(*bn) || !aligned16(z) || !aligned16(y))
+int dt_upd_bn_finish(int64_t m, int32_t hw, const float* z, const DtUpdBn* bn, float* y,
+                     void* stream) {
+  if (m < 1 || hw < 0 || (hw > 0 && m % hw != 0) || !z || !y || !bn || !valid_in(*bn) ||
+      !aligned16(z) || !aligned16(y))
     return DT_E_ARG;
   const int64_t items = m * 8;
   const int64_t per = 1024 * kFinishPer;
   int64_t grid = (items + per - 1) / per;
   grid = grid < kFinishMaxGrid ? grid : kFinishMaxGrid;
   hipLaunchKernelGGL(bn_finish_kernel, dim3((unsigned)grid), dim3(1024), 0, (hipStream_t)stream, m,
-                     z, *bn, y);
+                     (int)hw, z, *bn, y);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 

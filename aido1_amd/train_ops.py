@@ -335,9 +335,10 @@ class _ConvTrunk(torch.autograd.Function):
             zs.append(z)
             mis.append(mi)
             cur = z
-        y = torch.empty_like(cur)
-        rc = L.dt_upd_bn_finish(cur.numel() // C, cur.data_ptr(), ctypes.byref(prev), y.data_ptr(),
-                                s)
+        # y in plain NCHW: the flatten after the trunk is a view, not a copy
+        y = torch.empty(cur.shape, device=dev, dtype=cur.dtype)
+        rc = L.dt_upd_bn_finish(cur.numel() // C, cur.shape[2] * cur.shape[3], cur.data_ptr(),
+                                ctypes.byref(prev), y.data_ptr(), s)
         if rc != 0:
             raise _lib.DtError('dt_upd_bn_finish failed (%d)' % rc)
         ctx.save_for_backward(x, *ws, *zs, *mis, *params)

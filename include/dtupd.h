@@ -91,8 +91,11 @@ int dt_upd_conv_fwd_part(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t
                          float slope, float* z, float* part, int32_t* parts, void* stream);
 
 /* y = bn(leaky(z + bias)) for the chain's last block (z [m, 32]): merges
- * bn->part and writes mean_invstd / running statistics as above */
-int dt_upd_bn_finish(int64_t m, const float* z, const DtUpdBn* bn, float* y, void* stream);
+ * bn->part and writes mean_invstd / running statistics as above.  y is laid
+ * out as z (hw = 0) or NCHW, [m / hw][32][hw] (hw = pixels a sample: the
+ * flatten after the trunk is then a view) */
+int dt_upd_bn_finish(int64_t m, int32_t hw, const float* z, const DtUpdBn* bn, float* y,
+                     void* stream);
 
 /* dt_upd_conv_wgrad with the input x' = bn_in(leaky(x + bias_in)) made while
  * staging (in->mean_invstd as the forward wrote it; in == NULL: x as is) */

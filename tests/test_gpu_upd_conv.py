@@ -198,4 +198,4 @@ def test_chain_rejects_bad_handoff(gpu):
     assert L.dt_upd_conv_fwd_part(32, 4, 2, 1, 57, 77, x.data_ptr(), ctypes.byref(b), x.data_ptr(),
                                   x.data_ptr(), 0.01, x.data_ptr(), x.data_ptr(),
                                   ctypes.byref(parts), None) != 0
-    assert L.dt_upd_bn_finish(1, x.data_ptr(), ctypes.byref(b), x.data_ptr(), None) != 0
+    assert L.dt_upd_bn_finish(1, 0, x.data_ptr(), ctypes.byref(b), x.data_ptr(), None) != 0

@@ -51,7 +51,7 @@ def load(name):
     L.dt_upd_part_floats.restype = ctypes.c_int64
     L.dt_upd_conv_fwd_part.argtypes = [i32] * 6 + [vp, ctypes.POINTER(Bn), vp, vp, f, vp, vp,
                                                    ctypes.POINTER(i32), vp]
-    L.dt_upd_bn_finish.argtypes = [ctypes.c_int64, vp, ctypes.POINTER(Bn), vp, vp]
+    L.dt_upd_bn_finish.argtypes = [ctypes.c_int64, i32, vp, ctypes.POINTER(Bn), vp, vp]
     return L
 
 
@@ -122,7 +122,7 @@ def run(n, reps):
                     y = torch.empty_like(z)
 
                     def finish():
-                        assert L.dt_upd_bn_finish(z.numel() // 32, z.data_ptr(),
+                        assert L.dt_upd_bn_finish(z.numel() // 32, 0, z.data_ptr(),
                                                   ctypes.byref(hand), y.data_ptr(), s) == 0
                     t['finish'] = timeit(torch, finish, reps)
             if name == 'full':
