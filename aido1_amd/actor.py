@@ -81,6 +81,10 @@ class _Lin(nn.Module):       # LinearWrapper: parameter path ".linear"
         _init_weight(self.linear.weight, weight_init, conv=False)
 
     def forward(self, x):
+        if x.is_cuda and _Seq.fused_tail:
+            from aido1_amd import train_ops
+            if train_ops.linear_applicable(x, self.linear):
+                return train_ops.linear(x, self.linear)
         return self.linear(x)
 
 

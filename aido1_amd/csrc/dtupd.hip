@@ -109,91 +109,165 @@ struct FwdBn {
 };
 constexpr int kMaxGrid = 256;   // workgroups (= partials) of a STATS launch
 
-// the workgroup's Welford partial of its lanes' channels -> part[blockIdx.x]:
+// ---- cross-workgroup statistics ----------------------------------------------------------
+// A launch's BatchNorm statistics travel as per-workgroup partials laid out
+// [workgroup][3][32] (count, mean, M2 of the 32 channels), merged with Chan's
+// rule (dtsync.h) in trees of cross-lane shuffles rather than long serial
+// chains, always in the same order: every merger of the same partials (the
+// last workgroup of dt_upd_conv_fwd_bn, or each workgroup of the chain's
+// next kernel) gets the same bits.  All for 1024-thread workgroups.
+struct Welford {
+  float n, mean, m2;
+};
+__device__ __forceinline__ void chan(Welford& a, const Welford& b) { chan(a.n, a.mean, a.m2, b.n, b.mean, b.m2); }
+__device__ __forceinline__ Welford shfl_xor_w(const Welford& a, int m) {
+  return Welford{__shfl_xor(a.n, m), __shfl_xor(a.mean, m), __shfl_xor(a.m2, m)};
+}
+
+// red[16][32]: 16 ways a channel -> the channel's merge in the threads t < 512
+// with (t & 15) == 0 (channel t >> 4); no barrier after
+__device__ __forceinline__ Welford merge16(const Welford (*red)[32]) {
+  const int t = threadIdx.x;
+  Welford w{0.0f, 0.0f, 0.0f};
+  if (t < 512) {   // waves 0-7 whole
+    w = red[t & 15][t >> 4];
+#pragma unroll
+    for (int m = 1; m < 16; m <<= 1) chan(w, shfl_xor_w(w, m));
+  }
+  return w;
+}
+__device__ __forceinline__ bool merge16_owner() { return threadIdx.x < 512 && (threadIdx.x & 15) == 0; }
+
+// the workgroup's partial of its lanes' channels (lane & 31) -> part[blockIdx.x]:
 // written through (WT) for a last-arrival merge inside this launch, plainly
 // for the next kernel (the chain of include/dtupd.h) to merge
 template <int NT, bool WT>
 __device__ void wg_partial(float* part, float cnt, float mean, float m2) {
-  __shared__ float red[NT / 64][32][3];
+  static_assert(NT == 1024, "16 waves");
+  __shared__ Welford red[16][32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  // lane pairs (l, l ^ 32) hold the same channel
-  chan(cnt, mean, m2, __shfl_xor(cnt, 32), __shfl_xor(mean, 32), __shfl_xor(m2, 32));
-  if (lane < 32) {
-    red[wave][lane][0] = cnt;
-    red[wave][lane][1] = mean;
-    red[wave][lane][2] = m2;
-  }
+  Welford own{cnt, mean, m2};
+  chan(own, shfl_xor_w(own, 32));            // lane pairs (l, l ^ 32) hold the same channel
+  if (lane < 32) red[wave][lane] = own;
   __syncthreads();
-  if (tid < 32) {
-    float cn = 0.0f, cm = 0.0f, cq = 0.0f;
-    for (int w = 0; w < NT / 64; ++w) chan(cn, cm, cq, red[w][tid][0], red[w][tid][1], red[w][tid][2]);
-    float* p = part + ((size_t)blockIdx.x * 32 + tid) * 3;
+  const Welford w = merge16(red);
+  if (merge16_owner()) {
+    const int ch = tid >> 4;
+    float* p = part + (size_t)blockIdx.x * 96 + ch;
     if constexpr (WT) {
-      st_wt(p, cn);
-      st_wt(p + 1, cm);
-      st_wt(p + 2, cq);
+      st_wt(p, w.n);
+      st_wt(p + 32, w.mean);
+      st_wt(p + 64, w.m2);
     } else {
-      p[0] = cn;
-      p[1] = cm;
-      p[2] = cq;
+      p[0] = w.n;
+      p[32] = w.mean;
+      p[64] = w.m2;
     }
   }
 }
 
+// Merging `parts` partials: thread t takes channels 4 (t & 7) .. + 3 of
+// partials (t >> 3) and (t >> 3) + 128 (loaded as float4s: PartLoads),
+// then the lanes of a wave merge by shuffles, the waves through LDS (merge16).
+constexpr int kPartHalf = 128;
+static_assert(kMaxGrid <= 2 * kPartHalf, "two partials a thread");
+struct PartLoads {
+  float4 n[2], mean[2], m2[2];
+};
+
+template <bool WT>
+__device__ __forceinline__ PartLoads part_loads(const float* part, int parts) {
+  PartLoads r;
+  const int t = threadIdx.x, qd = t & 7, gi = t >> 3;
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const int g = gi + kPartHalf * h;
+    const float* p = part + (size_t)(g < parts ? g : 0) * 96 + 4 * qd;
+    if constexpr (WT) {
+      r.n[h] = make_float4(ld_wt(p), ld_wt(p + 1), ld_wt(p + 2), ld_wt(p + 3));
+      r.mean[h] = make_float4(ld_wt(p + 32), ld_wt(p + 33), ld_wt(p + 34), ld_wt(p + 35));
+      r.m2[h] = make_float4(ld_wt(p + 64), ld_wt(p + 65), ld_wt(p + 66), ld_wt(p + 67));
+    } else {
+      r.n[h] = *reinterpret_cast<const float4*>(p);
+      r.mean[h] = *reinterpret_cast<const float4*>(p + 32);
+      r.m2[h] = *reinterpret_cast<const float4*>(p + 64);
+    }
+    if (g >= parts) r.n[h] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);   // merges as nothing
+  }
+  return r;
+}
+
+// -> the merge of every partial, valid in merge16_owner() threads (channel t >> 4)
+__device__ __forceinline__ Welford merge_parts(const PartLoads& r) {
+  __shared__ Welford red[16][32];
+  const int t = threadIdx.x, lane = t & 63, wave = t >> 6, qd = t & 7;
+  Welford s[4];
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    const float n4[4] = {r.n[h].x, r.n[h].y, r.n[h].z, r.n[h].w};
+    const float m4[4] = {r.mean[h].x, r.mean[h].y, r.mean[h].z, r.mean[h].w};
+    const float q4[4] = {r.m2[h].x, r.m2[h].y, r.m2[h].z, r.m2[h].w};
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      if (h == 0) s[c] = Welford{n4[c], m4[c], q4[c]};
+      else chan(s[c], Welford{n4[c], m4[c], q4[c]});
+    }
+  }
+#pragma unroll
+  for (int m = 8; m < 64; m <<= 1)          // the wave's eight partial pairs a quad
+#pragma unroll
+    for (int c = 0; c < 4; ++c) chan(s[c], shfl_xor_w(s[c], m));
+  if (lane < 8)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) red[wave][4 * qd + c] = s[c];
+  __syncthreads();
+  return merge16(red);
+}
+
 template <int NT>
 __device__ void merge_partials_last(const FwdBn& fb, float cnt, float mean, float m2, int64_t m) {
-  __shared__ float red2[NT / 32][32][3];
+  static_assert(NT == 1024, "16 waves");
   const int tid = threadIdx.x;
   float* part = fb.work;
   wg_partial<NT, true>(part, cnt, mean, m2);
-  unsigned int* counters = reinterpret_cast<unsigned int*>(part + (size_t)kMaxGrid * 32 * 3);
+  unsigned int* counters = reinterpret_cast<unsigned int*>(part + (size_t)kMaxGrid * 96);
   if (!last_arrival(&counters[0])) return;
   acquire_partials();
-  {
-    constexpr int kFin = NT / 32;                   // threads a channel
-    constexpr int kPer = (kMaxGrid + kFin - 1) / kFin;   // all loads issued before the merges
-    const int ch = tid & 31, j = tid >> 5;
-    float cn = 0.0f, cm = 0.0f, cq = 0.0f;
-    float pn[kPer], pm[kPer], pq[kPer];
+  const PartLoads r = part_loads<true>(part, gridDim.x);
+  {   // counts back to zero (dtsync.h): a partial read stale shows as a lost count
+    const int qd = tid & 7, gi = tid >> 3;
 #pragma unroll
-    for (int k = 0; k < kPer; ++k) {
-      const int g = j + k * kFin;
-      const float* p = part + ((size_t)(g < (int)gridDim.x ? g : 0) * 32 + ch) * 3;
-      pn[k] = g < (int)gridDim.x ? ld_wt(p) : 0.0f;
-      pm[k] = ld_wt(p + 1);
-      pq[k] = ld_wt(p + 2);
+    for (int h = 0; h < 2; ++h) {
+      const int g = gi + kPartHalf * h;
+      if (g < (int)gridDim.x)
+#pragma unroll
+        for (int c = 0; c < 4; ++c) st_wt(part + (size_t)g * 96 + 4 * qd + c, 0.0f);
     }
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) {   // counts back to zero (dtsync.h)
-      const int g = j + k * kFin;
-      if (g < (int)gridDim.x) st_wt(part + ((size_t)g * 32 + ch) * 3, 0.0f);
-    }
-#pragma unroll
-    for (int k = 0; k < kPer; ++k) chan(cn, cm, cq, pn[k], pm[k], pq[k]);
-    red2[j][ch][0] = cn;
-    red2[j][ch][1] = cm;
-    red2[j][ch][2] = cq;
   }
-  __syncthreads();
-  if (tid < 32) {
-    float cn = 0.0f, cm = 0.0f, cq = 0.0f;
-    for (int s = 0; s < NT / 32; ++s) chan(cn, cm, cq, red2[s][tid][0], red2[s][tid][1], red2[s][tid][2]);
-    const float var = cq / cn;
+  float rm = 0.0f, rv = 0.0f;
+  if (merge16_owner()) {
+    rm = fb.running_mean[tid >> 4];
+    rv = fb.running_var[tid >> 4];
+  }
+  const Welford w = merge_parts(r);
+  if (merge16_owner()) {
+    const int ch = tid >> 4;
+    const float var = w.m2 / w.n;
     const float invstd = 1.0f / sqrtf(var + fb.eps);
-    fb.mean_invstd[tid] = cm;
-    fb.mean_invstd[32 + tid] = invstd;
+    fb.mean_invstd[ch] = w.mean;
+    fb.mean_invstd[32 + ch] = invstd;
+    const float cn = w.n;
     const bool lost = m < (int64_t(1) << 24) ? cn != (float)m : fabsf(cn - (float)m) > 1e-6f * (float)m;
     guard_raise(fb.guard, DT_GUARD_BN_COUNT, lost);
-    guard_raise(fb.guard, DT_GUARD_BN_FWD, !finitef(cm) || !finitef(invstd));
-    const float unbiased = cn > 1.0f ? cq / (cn - 1.0f) : var;
-    float rm = fb.running_mean[tid], rv = fb.running_var[tid];
+    guard_raise(fb.guard, DT_GUARD_BN_FWD, !finitef(w.mean) || !finitef(invstd));
+    const float unbiased = cn > 1.0f ? w.m2 / (cn - 1.0f) : var;
     for (int u = 0; u < fb.updates; ++u) {
-      rm = (1.0f - fb.momentum) * rm + fb.momentum * cm;
+      rm = (1.0f - fb.momentum) * rm + fb.momentum * w.mean;
       rv = (1.0f - fb.momentum) * rv + fb.momentum * unbiased;
     }
-    fb.running_mean[tid] = rm;
-    fb.running_var[tid] = rv;
-    if (tid == 0 && fb.nbt) fb.nbt[0] += fb.updates;
+    fb.running_mean[ch] = rm;
+    fb.running_var[ch] = rv;
+    if (ch == 0 && fb.nbt) fb.nbt[0] += fb.updates;
   }
 }
 
@@ -211,43 +285,37 @@ __device__ __forceinline__ float4 norm4(float4 z, float4 b, float4 mu, float4 sc
 }
 
 // Every workgroup of a chain kernel merges the producer's partials itself
-// (the same order as merge_partials_last: thread j of a channel takes partials
-// j, j + NT/32, ..., then one thread merges the NT/32 results), so all agree
-// bit for bit, and builds tab = {bias, mean, invstd * gamma, beta} per
-// channel in LDS.  The first workgroup (`finalize`) also writes mean_invstd,
-// moves the running statistics and reports to the guard, as the merging
-// workgroup of dt_upd_conv_fwd_bn does.  Two halves: norm_loads issues every
-// load (partials, parameters, running statistics) so the caller can start its
-// own loads behind them; norm_build merges and fills tab.
-constexpr int kNormPer = 8;     // partials a thread (kMaxGrid / 32 ways)
-
+// (merge_parts: the same order as dt_upd_conv_fwd_bn's last workgroup), so
+// all agree bit for bit, and builds tab = {bias, mean, invstd * gamma, beta}
+// per channel in LDS.  The first workgroup (`finalize`) also writes
+// mean_invstd, moves the running statistics and reports to the guard, as the
+// merging workgroup of dt_upd_conv_fwd_bn does.  Two halves: norm_loads
+// issues every load (partials, parameters, running statistics) so the caller
+// can start its own loads behind them; norm_build merges and fills tab.
 struct NormRegs {
-  float pn[kNormPer], pm[kNormPer], pq[kNormPer];
+  PartLoads p;
   float bias, gamma, beta, rm, rv;
 };
 
 template <int NT>
 __device__ __forceinline__ NormRegs norm_loads(const DtUpdBn& b, bool finalize) {
-  constexpr int kFin = NT / 32;
-  static_assert(kMaxGrid <= kNormPer * kFin, "one batch of loads covers every partial");
+  static_assert(NT == 1024, "16 waves");
   NormRegs r;
-  const int tid = threadIdx.x, ch = tid & 31, j = tid >> 5;
-#pragma unroll
-  for (int k = 0; k < ((DTUPD_SKIP & 16) ? 0 : kNormPer); ++k) {
-    const int g = j + k * kFin;
-    const float* p = b.part + ((size_t)(g < b.parts ? g : 0) * 32 + ch) * 3;
-    r.pn[k] = g < b.parts ? p[0] : 0.0f;
-    r.pm[k] = p[1];
-    r.pq[k] = p[2];
+  if (DTUPD_SKIP & 16) {
+    r.p.n[0] = r.p.n[1] = r.p.mean[0] = r.p.mean[1] = r.p.m2[0] = r.p.m2[1] =
+        make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+  } else {
+    r.p = part_loads<false>(b.part, b.parts);
   }
   r.bias = r.gamma = r.beta = r.rm = r.rv = 0.0f;
-  if (tid < 32) {
-    r.bias = b.bias[tid];
-    r.gamma = b.gamma[tid];
-    r.beta = b.beta[tid];
+  if (merge16_owner()) {
+    const int ch = threadIdx.x >> 4;
+    r.bias = b.bias[ch];
+    r.gamma = b.gamma[ch];
+    r.beta = b.beta[ch];
     if (finalize) {
-      r.rm = b.running_mean[tid];
-      r.rv = b.running_var[tid];
+      r.rm = b.running_mean[ch];
+      r.rv = b.running_var[ch];
     }
   }
   return r;
@@ -255,41 +323,30 @@ __device__ __forceinline__ NormRegs norm_loads(const DtUpdBn& b, bool finalize) 
 
 template <int NT>
 __device__ void norm_build(const DtUpdBn& b, const NormRegs& r, float (*tab)[32], bool finalize) {
-  constexpr int kFin = NT / 32;
-  __shared__ float red2[kFin][32][3];
   const int tid = threadIdx.x;
   if (DTUPD_SKIP & 32) {
     if (tid < 32) {
-      tab[0][tid] = r.bias;
+      tab[0][tid] = 0.1f;
       tab[1][tid] = 0.5f;
-      tab[2][tid] = r.gamma;
-      tab[3][tid] = r.beta;
+      tab[2][tid] = 1.5f;
+      tab[3][tid] = 0.2f;
     }
     __syncthreads();
     return;
   }
-  {
-    const int ch = tid & 31, j = tid >> 5;
-    float cn = 0.0f, cm = 0.0f, cq = 0.0f;
-#pragma unroll
-    for (int k = 0; k < kNormPer; ++k) chan(cn, cm, cq, r.pn[k], r.pm[k], r.pq[k]);
-    red2[j][ch][0] = cn;
-    red2[j][ch][1] = cm;
-    red2[j][ch][2] = cq;
-  }
-  __syncthreads();
-  if (tid < 32) {
-    float cn = 0.0f, cm = 0.0f, cq = 0.0f;
-    for (int q = 0; q < kFin; ++q) chan(cn, cm, cq, red2[q][tid][0], red2[q][tid][1], red2[q][tid][2]);
+  const Welford w = merge_parts(r.p);
+  if (merge16_owner()) {
+    const int ch = tid >> 4;
+    const float cn = w.n, cm = w.mean, cq = w.m2;
     const float var = cq / cn;
     const float invstd = 1.0f / sqrtf(var + b.eps);
-    tab[0][tid] = r.bias;
-    tab[1][tid] = cm;
-    tab[2][tid] = invstd * r.gamma;
-    tab[3][tid] = r.beta;
+    tab[0][ch] = r.bias;
+    tab[1][ch] = cm;
+    tab[2][ch] = invstd * r.gamma;
+    tab[3][ch] = r.beta;
     if (finalize) {
-      b.mean_invstd[tid] = cm;
-      b.mean_invstd[32 + tid] = invstd;
+      b.mean_invstd[ch] = cm;
+      b.mean_invstd[32 + ch] = invstd;
       const int64_t m = b.m;
       const bool lost = m < (int64_t(1) << 24) ? cn != (float)m : fabsf(cn - (float)m) > 1e-6f * (float)m;
       guard_raise(b.guard, DT_GUARD_BN_COUNT, lost);
@@ -300,9 +357,9 @@ __device__ void norm_build(const DtUpdBn& b, const NormRegs& r, float (*tab)[32]
         rm = (1.0f - b.momentum) * rm + b.momentum * cm;
         rv = (1.0f - b.momentum) * rv + b.momentum * unbiased;
       }
-      b.running_mean[tid] = rm;
-      b.running_var[tid] = rv;
-      if (tid == 0 && b.num_batches_tracked) b.num_batches_tracked[0] += b.updates;
+      b.running_mean[ch] = rm;
+      b.running_var[ch] = rv;
+      if (ch == 0 && b.num_batches_tracked) b.num_batches_tracked[0] += b.updates;
     }
   }
   __syncthreads();
@@ -366,7 +423,7 @@ bn_finish_kernel(int64_t m, int hw, const float* __restrict__ z, DtUpdBn b, floa
 // tile, each a slice of K, summed through LDS (the small layers: more waves
 // than tiles).
 constexpr int kFwdThreads = 1024;
-constexpr int kFwdAllLoads = 16;    // slices of up to this many k-steps load all A first
+constexpr int kFwdAllLoads = 8;     // slices of up to this many k-steps load all A first
 
 
 // STATS: 0 none, 1 merged by the last workgroup (dt_upd_conv_fwd_bn), 2
@@ -747,6 +804,172 @@ dgrad_kernel(int n, const float* __restrict__ dz, const float* __restrict__ w,
   }
 }
 
+// ---- the linear layer after the trunk (flatten -> dropout -> linear 4032 -> 256) ----------
+// y[m][n] = b[n] + sum_k x[m][k] W[n][k] with M (the batch) small and K long:
+// library GEMMs pick one tile a workgroup over all of K (latency-bound, 20 us
+// at batch 64).  Here K is split: each wave takes a slice of k-steps of a
+// 32 x 32 output tile (float4 loads of x and W rows, the K-permutation trick),
+// the four waves of a workgroup sum through LDS into one partial, and
+// lin_reduce_kernel adds the partials in index order plus the bias.
+constexpr int kLinWaves = 4;
+
+__global__ void __launch_bounds__(64 * kLinWaves)
+lin_fwd_kernel(int m, int n, int k, int chunk, const float* __restrict__ x,
+               const float* __restrict__ w, float* __restrict__ part) {
+  __shared__ float red[kLinWaves - 1][16][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 31, kk = lane >> 5;
+  const int ntile = n / 32, tile = blockIdx.x % (ntile * ((m + 31) / 32));
+  const int split = blockIdx.x / (ntile * ((m + 31) / 32));
+  const int m0 = (tile / ntile) * 32, n0 = (tile % ntile) * 32;
+  const int steps = k / 8;
+  const int s0 = (split * kLinWaves + wave) * chunk;
+  const int s1 = s0 + chunk < steps ? s0 + chunk : steps;
+  const bool mok = m0 + col < m;
+  const float* xr = x + (size_t)(mok ? m0 + col : 0) * k + 4 * kk;
+  const float* wr = w + (size_t)(n0 + col) * k + 4 * kk;
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#pragma unroll 4
+  for (int st = s0; st < s1; ++st) {
+    float4 a = *reinterpret_cast<const float4*>(xr + 8 * st);
+    if (!mok) a = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const float4 b = *reinterpret_cast<const float4*>(wr + 8 * st);
+    acc = mfma4(a, b, acc);
+  }
+  if (wave > 0)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[wave - 1][r][lane] = acc[r];
+  __syncthreads();
+  if (wave == 0) {
+#pragma unroll
+    for (int o = 0; o < kLinWaves - 1; ++o)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] += red[o][r][lane];
+    float* pp = part + (size_t)split * m * n;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int mm = m0 + acc_row(r, kk);
+      if (mm < m) pp[(size_t)mm * n + n0 + col] = acc[r];
+    }
+  }
+}
+
+__global__ void __launch_bounds__(256)
+lin_reduce_kernel(int mn, int n, int splits, const float* __restrict__ part,
+                  const float* __restrict__ bias, float* __restrict__ y) {
+  const int i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= mn) return;
+  float s = 0.0f;
+  int p = 0;
+  for (; p + 8 <= splits; p += 8) {   // eight loads in flight, summed in index order
+    float v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) v[j] = part[(size_t)(p + j) * mn + i];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) s += v[j];
+  }
+  for (; p < splits; ++p) s += part[(size_t)p * mn + i];
+  y[i] = bias ? s + bias[i % n] : s;
+}
+
+// dx[m][k] = sum_n dy[m][n] W[n][k]: a workgroup a 32 x 32 tile of dx, its
+// four waves a quarter of n each, summed through LDS
+__global__ void __launch_bounds__(64 * kLinWaves)
+lin_dgrad_kernel(int m, int n, int k, const float* __restrict__ dy, const float* __restrict__ w,
+                 float* __restrict__ dx) {
+  __shared__ float red[kLinWaves - 1][16][64];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 31, kk = lane >> 5;
+  const int ktile = k / 32;
+  const int m0 = (blockIdx.x / ktile) * 32, k0 = (blockIdx.x % ktile) * 32;
+  const int steps = n / 8, chunk = (steps + kLinWaves - 1) / kLinWaves;
+  const int s0 = wave * chunk, s1 = s0 + chunk < steps ? s0 + chunk : steps;
+  const bool mok = m0 + col < m;
+  const float* dyr = dy + (size_t)(mok ? m0 + col : 0) * n + 4 * kk;
+  const float* wc = w + (size_t)(4 * kk) * k + k0 + col;   // W[n][k0 + col], n = 8 st + 4 kk + e
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+#pragma unroll 2
+  for (int st = s0; st < s1; ++st) {
+    float4 a = *reinterpret_cast<const float4*>(dyr + 8 * st);
+    if (!mok) a = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    const float* wp = wc + (size_t)(8 * st) * k;
+    const float4 b = make_float4(wp[0], wp[k], wp[2 * (size_t)k], wp[3 * (size_t)k]);
+    acc = mfma4(a, b, acc);
+  }
+  if (wave > 0)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) red[wave - 1][r][lane] = acc[r];
+  __syncthreads();
+  if (wave == 0) {
+#pragma unroll
+    for (int o = 0; o < kLinWaves - 1; ++o)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] += red[o][r][lane];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int mm = m0 + acc_row(r, kk);
+      if (mm < m) dx[(size_t)mm * k + k0 + col] = acc[r];
+    }
+  }
+}
+
+// dW[n][k] = sum_m dy[m][n] x[m][k] (a wave a 32 x 32 tile, all m) and
+// db[n] = sum_m dy[m][n] (the k0 = 0 tiles, m in order)
+__global__ void __launch_bounds__(64 * kLinWaves)
+lin_wgrad_kernel(int m, int n, int k, const float* __restrict__ dy, const float* __restrict__ x,
+                 float* __restrict__ dw, float* __restrict__ db) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 31, kk = lane >> 5;
+  const int ktile = k / 32, tiles = (n / 32) * ktile;
+  const int tile = blockIdx.x * kLinWaves + wave;
+  if (tile >= tiles) return;
+  const int n0 = (tile / ktile) * 32, k0 = (tile % ktile) * 32;
+  f32x16 acc;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+  const int steps = (m + 7) / 8;
+  for (int st = 0; st < steps; ++st) {
+    float av[4], bv[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int mm = 8 * st + 4 * kk + e;
+      const bool ok = mm < m;
+      av[e] = ok ? dy[(size_t)mm * n + n0 + col] : 0.0f;
+      bv[e] = ok ? x[(size_t)mm * k + k0 + col] : 0.0f;
+    }
+    acc = mfma4(make_float4(av[0], av[1], av[2], av[3]), make_float4(bv[0], bv[1], bv[2], bv[3]),
+                acc);
+  }
+#pragma unroll
+  for (int r = 0; r < 16; ++r) dw[(size_t)(n0 + acc_row(r, kk)) * k + k0 + col] = acc[r];
+  if (db && k0 == 0 && kk == 0) {      // eight loads in flight, summed in m order
+    float sb = 0.0f;
+    int mm = 0;
+    for (; mm + 8 <= m; mm += 8) {
+      float v[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = dy[(size_t)(mm + j) * n + n0 + col];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) sb += v[j];
+    }
+    for (; mm < m; ++mm) sb += dy[(size_t)mm * n + n0 + col];
+    db[n0 + col] = sb;
+  }
+}
+
+// splits of K a forward launch uses (about a wave a SIMD over the tiles)
+int lin_splits(int m, int n, int k) {
+  const int tiles = (n / 32) * ((m + 31) / 32), steps = k / 8;
+  int sw = 256 / (tiles > 0 ? tiles : 1);                 // workgroups a tile
+  sw = sw < 1 ? 1 : sw;
+  const int maxw = (steps + kLinWaves - 1) / kLinWaves;   // at least one step a wave
+  return sw < maxw ? sw : maxw;
+}
+
 // ---- host ------------------------------------------------------------------------------
 int resident(const void* kern, int threads, int cap) {
   static int cus = 0;
@@ -786,8 +1009,8 @@ int dispatch_fwd(int l, int n, const float* x, const float* w, float* z, const F
   switch (l) {
     case 1:
       if constexpr (NORM) return DT_E_ARG;
-      else return launch_fwd<L1, 4, STATS, false>(n, x, w, z, fb, in, s, grid_out);
-    case 2: return launch_fwd<L2, 8, STATS, NORM>(n, x, w, z, fb, in, s, grid_out);
+      else return launch_fwd<L1, 2, STATS, false>(n, x, w, z, fb, in, s, grid_out);
+    case 2: return launch_fwd<L2, 2, STATS, NORM>(n, x, w, z, fb, in, s, grid_out);
     case 3: return launch_fwd<L3, 8, STATS, NORM>(n, x, w, z, fb, in, s, grid_out);
     default: return launch_fwd<L4, 16, STATS, NORM>(n, x, w, z, fb, in, s, grid_out);
   }
@@ -892,7 +1115,7 @@ int dt_upd_conv_wgrad_bn(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t
   hipStream_t s = (hipStream_t)stream;
   const DtUpdBn b = in ? *in : DtUpdBn{};
   switch (l) {
-    case 1: return launch_wgrad<L1, 1, 6, false, true>(n, x, b, dz, dw, work, s);
+    case 1: return launch_wgrad<L1, 1, 6, false, false>(n, x, b, dz, dw, work, s);
     case 2:
       return in ? launch_wgrad<L2, 2, 8, true>(n, x, b, dz, dw, work, s)
                 : launch_wgrad<L2, 2, 8, false>(n, x, b, dz, dw, work, s);
@@ -911,6 +1134,49 @@ int dt_upd_conv_wgrad(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih
 }
 
 int64_t dt_upd_part_floats(void) { return (int64_t)kMaxGrid * 32 * 3; }
+
+static bool lin_shape_ok(int32_t m, int32_t n, int32_t k) {
+  return m >= 1 && n >= 32 && n % 32 == 0 && k >= 8 && k % 32 == 0;
+}
+
+int64_t dt_upd_linear_work_floats(int32_t m, int32_t n, int32_t k) {
+  if (!lin_shape_ok(m, n, k)) return -1;
+  return (int64_t)lin_splits(m, n, k) * m * n;
+}
+
+int dt_upd_linear_fwd(int32_t m, int32_t n, int32_t k, const float* x, const float* w,
+                      const float* b, float* y, float* work, void* stream) {
+  if (!lin_shape_ok(m, n, k) || !x || !w || !y || !work || !aligned16(x) || !aligned16(w))
+    return DT_E_ARG;
+  hipStream_t s = (hipStream_t)stream;
+  const int splits = lin_splits(m, n, k);
+  const int tiles = (n / 32) * ((m + 31) / 32);
+  const int steps = k / 8, chunk = (steps + splits * kLinWaves - 1) / (splits * kLinWaves);
+  hipLaunchKernelGGL(lin_fwd_kernel, dim3(tiles * splits), dim3(64 * kLinWaves), 0, s, m, n, k,
+                     chunk, x, w, work);
+  const int mn = m * n;
+  hipLaunchKernelGGL(lin_reduce_kernel, dim3((mn + 255) / 256), dim3(256), 0, s, mn, n, splits,
+                     work, b, y);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
+int dt_upd_linear_dgrad(int32_t m, int32_t n, int32_t k, const float* dy, const float* w,
+                        float* dx, void* stream) {
+  if (!lin_shape_ok(m, n, k) || !dy || !w || !dx || !aligned16(dy)) return DT_E_ARG;
+  const int grid = ((m + 31) / 32) * (k / 32);
+  hipLaunchKernelGGL(lin_dgrad_kernel, dim3(grid), dim3(64 * kLinWaves), 0, (hipStream_t)stream,
+                     m, n, k, dy, w, dx);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
+int dt_upd_linear_wgrad(int32_t m, int32_t n, int32_t k, const float* dy, const float* x,
+                        float* dw, float* db, void* stream) {
+  if (!lin_shape_ok(m, n, k) || !dy || !x || !dw) return DT_E_ARG;
+  const int tiles = (n / 32) * (k / 32);
+  hipLaunchKernelGGL(lin_wgrad_kernel, dim3((tiles + kLinWaves - 1) / kLinWaves),
+                     dim3(64 * kLinWaves), 0, (hipStream_t)stream, m, n, k, dy, x, dw, db);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
 
 int dt_upd_conv_fwd_part(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih, int32_t iw,
                          const float* x, const DtUpdBn* in, const float* w, const float* bias,

@@ -453,3 +453,66 @@ def conv_leaky_bn(x, conv, act, bn):
     z = F.conv2d(x, conv.weight, None, conv.stride)
     z = z.contiguous(memory_format=torch.channels_last)
     return _BnLeaky.apply(z, conv.bias, bn.weight, bn.bias, bn, float(act.negative_slope))
+
+
+# nn.Linear layers on include/dtupd.h's split-K kernels: long K (the 4032-wide
+# flatten of the conv trunk), N a multiple of 32, float32 on the GPU
+LINEAR_MIN_K = 1024
+
+
+def linear_applicable(x, lin):
+    w = lin.weight
+    return (x.is_cuda and x.dtype == torch.float32 and w.dtype == torch.float32 and x.dim() == 2
+            and x.shape[1] == w.shape[1] and w.shape[1] >= LINEAR_MIN_K and w.shape[1] % 32 == 0
+            and w.shape[0] % 32 == 0 and lin.bias is not None)
+
+
+class _UpdLinear(torch.autograd.Function):
+    """y = x w^T + b (torch.nn.Linear) with K split over waves and summed in a
+    fixed order; backward dx and dw / db on their own MFMA kernels
+    (include/dtupd.h).  Where the library GEMM took one tile a workgroup
+    over all of K at batch 64."""
+
+    @staticmethod
+    def forward(ctx, x, w, b):
+        x = x.contiguous()
+        w = w.contiguous()
+        m, k = x.shape
+        n = w.shape[0]
+        L = _lib.lib()
+        y = torch.empty(m, n, device=x.device, dtype=x.dtype)
+        work = torch.empty(int(L.dt_upd_linear_work_floats(m, n, k)), device=x.device)
+        rc = L.dt_upd_linear_fwd(m, n, k, x.data_ptr(), w.data_ptr(), b.data_ptr(), y.data_ptr(),
+                                 work.data_ptr(), _stream(x.device))
+        if rc != 0:
+            raise _lib.DtError('dt_upd_linear_fwd failed (%d)' % rc)
+        ctx.save_for_backward(x, w)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        dy = dy.contiguous()
+        m, k = x.shape
+        n = w.shape[0]
+        L = _lib.lib()
+        s = _stream(x.device)
+        dx = dw = db = None
+        if ctx.needs_input_grad[0]:
+            dx = torch.empty_like(x)
+            rc = L.dt_upd_linear_dgrad(m, n, k, dy.data_ptr(), w.data_ptr(), dx.data_ptr(), s)
+            if rc != 0:
+                raise _lib.DtError('dt_upd_linear_dgrad failed (%d)' % rc)
+        if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
+            dw = torch.empty_like(w)
+            db = torch.empty(n, device=x.device, dtype=x.dtype)
+            rc = L.dt_upd_linear_wgrad(m, n, k, dy.data_ptr(), x.data_ptr(), dw.data_ptr(),
+                                       db.data_ptr(), s)
+            if rc != 0:
+                raise _lib.DtError('dt_upd_linear_wgrad failed (%d)' % rc)
+        return dx, dw, db
+
+
+def linear(x, lin):
+    """lin(x) on the dtupd.h kernels (linear_applicable)."""
+    return _UpdLinear.apply(x, lin.weight, lin.bias)

@@ -199,3 +199,31 @@ def test_chain_rejects_bad_handoff(gpu):
                                   x.data_ptr(), 0.01, x.data_ptr(), x.data_ptr(),
                                   ctypes.byref(parts), None) != 0
     assert L.dt_upd_bn_finish(1, 0, x.data_ptr(), ctypes.byref(b), x.data_ptr(), None) != 0
+
+
+@pytest.mark.parametrize('m,n,k', [(64, 256, 4032), (5, 256, 4032), (33, 64, 1024)])
+def test_linear_matches_f64(gpu, m, n, k):
+    """The split-K linear kernels (dt_upd_linear_*) against float64 torch:
+    forward with bias, dx, dw and db (the trunk's 4032 -> 256 layer at batch
+    64, a ragged batch, another shape)."""
+    from aido1_amd import train_ops
+    g = torch.Generator().manual_seed(m + n)
+    x = torch.randn(m, k, generator=g, dtype=torch.float64)
+    w = torch.randn(n, k, generator=g, dtype=torch.float64) / k ** 0.5
+    b = torch.randn(n, generator=g, dtype=torch.float64)
+    dy = torch.randn(m, n, generator=g, dtype=torch.float64)
+    xg = x.float().to(gpu).requires_grad_()
+    lin = torch.nn.Linear(k, n).to(gpu)
+    with torch.no_grad():
+        lin.weight.copy_(w)
+        lin.bias.copy_(b)
+    assert train_ops.linear_applicable(xg, lin)
+    y = train_ops.linear(xg, lin)
+    y.backward(dy.float().to(gpu))
+    ref = x @ w.T + b
+    assert (y.detach().double().cpu() - ref).abs().max().item() <= _bound((x.abs() @ w.abs().T).max().item())
+    assert (xg.grad.double().cpu() - dy @ w).abs().max().item() <= _bound((dy.abs() @ w.abs()).max().item())
+    assert (lin.weight.grad.double().cpu() - dy.T @ x).abs().max().item() <= \
+        _bound((dy.abs().T @ x.abs()).max().item())
+    assert (lin.bias.grad.double().cpu() - dy.sum(0)).abs().max().item() <= \
+        _bound(dy.abs().sum(0).max().item())

@@ -6,6 +6,7 @@ timeout -k 10 200 python tools/upd_micro.py > gpurun_out/upd_micro.txt 2>&1 || {
 grep -v Warn gpurun_out/upd_micro.txt | head -4
 timeout -k 10 200 python tools/update_only.py > gpurun_out/update_only.txt 2>&1 || { tail -5 gpurun_out/update_only.txt; exit 1; }
 grep update gpurun_out/update_only.txt
+TORCH_BLAS_PREFER_HIPBLASLT=0 timeout -k 10 200 python tools/update_only.py > gpurun_out/update_only_rocblas.txt 2>&1 && echo "rocBLAS: $(grep update gpurun_out/update_only_rocblas.txt)"
 rm -rf /tmp/prof_upd
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d /tmp/prof_upd -o run --output-format csv -- python3 tools/update_only.py > gpurun_out/update_only_prof.log 2>&1 || { tail -20 gpurun_out/update_only_prof.log; exit 1; }
 f=$(find /tmp/prof_upd -name '*kernel_stats.csv' | head -1)
