@@ -200,9 +200,12 @@ def lib():
             'dt_upd_conv_wgrad_bn': (ctypes.c_int, [i32, i32, i32, i32, i32, i32, vp,
                                                     ctypes.POINTER(DtUpdBn), vp, vp, vp, vp]),
             'dt_upd_linear_work_floats': (i64, [i32, i32, i32]),
-            'dt_upd_linear_fwd': (ctypes.c_int, [i32, i32, i32, vp, vp, vp, vp, vp, vp]),
-            'dt_upd_linear_dgrad': (ctypes.c_int, [i32, i32, i32, vp, vp, vp, vp]),
-            'dt_upd_linear_wgrad': (ctypes.c_int, [i32, i32, i32, vp, vp, vp, vp, vp]),
+            'dt_upd_linear_fwd': (ctypes.c_int, [i32, i32, i32, vp, vp, vp, i32, ctypes.c_float,
+                                                 vp, vp, vp]),
+            'dt_upd_linear_dgrad': (ctypes.c_int, [i32, i32, i32, vp, vp, vp, ctypes.c_float, vp,
+                                                   vp]),
+            'dt_upd_linear_wgrad': (ctypes.c_int, [i32, i32, i32, vp, vp, vp, ctypes.c_float, vp,
+                                                   vp, vp]),
             'dt_soft_update': (ctypes.c_int, [i32, vp, vp, f64, vp]),
             # dtactor.h
             'dt_sample_norm': (ctypes.c_int, [vp, vp, i32, i32, i32, vp, vp, ctypes.c_float,

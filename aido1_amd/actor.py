@@ -81,10 +81,6 @@ class _Lin(nn.Module):       # LinearWrapper: parameter path ".linear"
         _init_weight(self.linear.weight, weight_init, conv=False)
 
     def forward(self, x):
-        if x.is_cuda and _Seq.fused_tail:
-            from aido1_amd import train_ops
-            if train_ops.linear_applicable(x, self.linear):
-                return train_ops.linear(x, self.linear)
         return self.linear(x)
 
 
@@ -136,6 +132,17 @@ class _Seq(nn.Module):       # MetaNet: ".internal_modules.<i>"
                 if train_ops.applicable(x, m.kernel, mods[i + 1], mods[i + 2]):
                     x = train_ops.conv_leaky_bn(x, m.kernel, mods[i + 1], mods[i + 2])
                     i += 3
+                    continue
+            if self.fused_tail and isinstance(m, _Lin) and x.is_cuda:
+                from aido1_amd import train_ops
+                if train_ops.linear_applicable(x, m.linear):
+                    act = mods[i + 1] if i + 1 < k else None
+                    if isinstance(act, nn.LeakyReLU):       # linear -> leaky_relu in one
+                        x = train_ops.linear(x, m.linear, float(act.negative_slope))
+                        i += 2
+                    else:
+                        x = train_ops.linear(x, m.linear)
+                        i += 1
                     continue
             if isinstance(m, nn.BatchNorm2d) and getattr(m, '_dt_updates', 1) != 1:
                 raise NotImplementedError('repeated running-statistics updates need the fused '

@@ -813,6 +813,12 @@ dgrad_kernel(int n, const float* __restrict__ dz, const float* __restrict__ w,
 // lin_reduce_kernel adds the partials in index order plus the bias.
 constexpr int kLinWaves = 4;
 
+// torch's leaky_relu backward on the output (same sign as the input for slope > 0)
+__device__ __forceinline__ float4 leaky_grad4(float4 g, float4 y, float slope) {
+  return make_float4(y.x > 0.0f ? g.x : g.x * slope, y.y > 0.0f ? g.y : g.y * slope,
+                     y.z > 0.0f ? g.z : g.z * slope, y.w > 0.0f ? g.w : g.w * slope);
+}
+
 __global__ void __launch_bounds__(64 * kLinWaves)
 lin_fwd_kernel(int m, int n, int k, int chunk, const float* __restrict__ x,
                const float* __restrict__ w, float* __restrict__ part) {
@@ -858,7 +864,7 @@ lin_fwd_kernel(int m, int n, int k, int chunk, const float* __restrict__ x,
 
 __global__ void __launch_bounds__(256)
 lin_reduce_kernel(int mn, int n, int splits, const float* __restrict__ part,
-                  const float* __restrict__ bias, float* __restrict__ y) {
+                  const float* __restrict__ bias, int act, float slope, float* __restrict__ y) {
   const int i = blockIdx.x * 256 + threadIdx.x;
   if (i >= mn) return;
   float s = 0.0f;
@@ -871,14 +877,16 @@ lin_reduce_kernel(int mn, int n, int splits, const float* __restrict__ part,
     for (int j = 0; j < 8; ++j) s += v[j];
   }
   for (; p < splits; ++p) s += part[(size_t)p * mn + i];
-  y[i] = bias ? s + bias[i % n] : s;
+  float v = bias ? s + bias[i % n] : s;
+  if (act) v = v > 0.0f ? v : v * slope;        // a following LeakyReLU, as torch computes it
+  y[i] = v;
 }
 
 // dx[m][k] = sum_n dy[m][n] W[n][k]: a workgroup a 32 x 32 tile of dx, its
 // four waves a quarter of n each, summed through LDS
 __global__ void __launch_bounds__(64 * kLinWaves)
 lin_dgrad_kernel(int m, int n, int k, const float* __restrict__ dy, const float* __restrict__ w,
-                 float* __restrict__ dx) {
+                 const float* __restrict__ yact, float slope, float* __restrict__ dx) {
   __shared__ float red[kLinWaves - 1][16][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 31, kk = lane >> 5;
@@ -895,6 +903,7 @@ lin_dgrad_kernel(int m, int n, int k, const float* __restrict__ dy, const float*
 #pragma unroll 2
   for (int st = s0; st < s1; ++st) {
     float4 a = *reinterpret_cast<const float4*>(dyr + 8 * st);
+    if (yact) a = leaky_grad4(a, *reinterpret_cast<const float4*>(yact + (dyr - dy) + 8 * st), slope);
     if (!mok) a = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     const float* wp = wc + (size_t)(8 * st) * k;
     const float4 b = make_float4(wp[0], wp[k], wp[2 * (size_t)k], wp[3 * (size_t)k]);
@@ -918,10 +927,16 @@ lin_dgrad_kernel(int m, int n, int k, const float* __restrict__ dy, const float*
 }
 
 // dW[n][k] = sum_m dy[m][n] x[m][k] (a wave a 32 x 32 tile, all m) and
-// db[n] = sum_m dy[m][n] (the k0 = 0 tiles, m in order)
+// db[n] = sum_m dy[m][n] (the k0 = 0 tiles, from the same loads)
 __global__ void __launch_bounds__(64 * kLinWaves)
 lin_wgrad_kernel(int m, int n, int k, const float* __restrict__ dy, const float* __restrict__ x,
-                 float* __restrict__ dw, float* __restrict__ db) {
+                 const float* __restrict__ yact, float slope, float* __restrict__ dw,
+                 float* __restrict__ db) {
+  // dy through a fused LeakyReLU (yact: its output, the same sign as its input)
+  auto gy = [&](size_t i) __attribute__((always_inline)) {
+    const float g = dy[i];
+    return yact ? (yact[i] > 0.0f ? g : g * slope) : g;
+  };
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 31, kk = lane >> 5;
   const int ktile = k / 32, tiles = (n / 32) * ktile;
@@ -932,32 +947,35 @@ lin_wgrad_kernel(int m, int n, int k, const float* __restrict__ dy, const float*
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
   const int steps = (m + 7) / 8;
-  for (int st = 0; st < steps; ++st) {
-    float av[4], bv[4];
+  float sb = 0.0f;
+  constexpr int kBatch = 8;                 // steps whose loads go out together (m <= 64: all)
+  for (int s0 = 0; s0 < steps; s0 += kBatch) {
+    float av[kBatch][4], bv[kBatch][4];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      const int mm = 8 * st + 4 * kk + e;
-      const bool ok = mm < m;
-      av[e] = ok ? dy[(size_t)mm * n + n0 + col] : 0.0f;
-      bv[e] = ok ? x[(size_t)mm * k + k0 + col] : 0.0f;
-    }
-    acc = mfma4(make_float4(av[0], av[1], av[2], av[3]), make_float4(bv[0], bv[1], bv[2], bv[3]),
-                acc);
+    for (int j = 0; j < kBatch; ++j)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int mm = 8 * (s0 + j) + 4 * kk + e;
+        const bool ok = s0 + j < steps && mm < m;
+        av[j][e] = ok ? gy((size_t)mm * n + n0 + col) : 0.0f;
+        bv[j][e] = ok ? x[(size_t)mm * k + k0 + col] : 0.0f;
+      }
+#pragma unroll
+    for (int j = 0; j < kBatch; ++j)
+      if (s0 + j < steps)
+        acc = mfma4(make_float4(av[j][0], av[j][1], av[j][2], av[j][3]),
+                    make_float4(bv[j][0], bv[j][1], bv[j][2], bv[j][3]), acc);
+    if (k0 == 0)   // db from the same loads: this lane's half of m, in order
+#pragma unroll
+      for (int j = 0; j < kBatch; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) sb += av[j][e];
   }
 #pragma unroll
   for (int r = 0; r < 16; ++r) dw[(size_t)(n0 + acc_row(r, kk)) * k + k0 + col] = acc[r];
-  if (db && k0 == 0 && kk == 0) {      // eight loads in flight, summed in m order
-    float sb = 0.0f;
-    int mm = 0;
-    for (; mm + 8 <= m; mm += 8) {
-      float v[8];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) v[j] = dy[(size_t)(mm + j) * n + n0 + col];
-#pragma unroll
-      for (int j = 0; j < 8; ++j) sb += v[j];
-    }
-    for (; mm < m; ++mm) sb += dy[(size_t)mm * n + n0 + col];
-    db[n0 + col] = sb;
+  if (k0 == 0) {                          // the two halves of m (lane pairs l, l ^ 32)
+    const float other = __shfl_xor(sb, 32);
+    if (db && kk == 0) db[n0 + col] = sb + other;
   }
 }
 
@@ -1145,7 +1163,8 @@ int64_t dt_upd_linear_work_floats(int32_t m, int32_t n, int32_t k) {
 }
 
 int dt_upd_linear_fwd(int32_t m, int32_t n, int32_t k, const float* x, const float* w,
-                      const float* b, float* y, float* work, void* stream) {
+                      const float* b, int32_t leaky, float slope, float* y, float* work,
+                      void* stream) {
   if (!lin_shape_ok(m, n, k) || !x || !w || !y || !work || !aligned16(x) || !aligned16(w))
     return DT_E_ARG;
   hipStream_t s = (hipStream_t)stream;
@@ -1156,25 +1175,27 @@ int dt_upd_linear_fwd(int32_t m, int32_t n, int32_t k, const float* x, const flo
                      chunk, x, w, work);
   const int mn = m * n;
   hipLaunchKernelGGL(lin_reduce_kernel, dim3((mn + 255) / 256), dim3(256), 0, s, mn, n, splits,
-                     work, b, y);
+                     work, b, (int)(leaky != 0), slope, y);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 
 int dt_upd_linear_dgrad(int32_t m, int32_t n, int32_t k, const float* dy, const float* w,
-                        float* dx, void* stream) {
-  if (!lin_shape_ok(m, n, k) || !dy || !w || !dx || !aligned16(dy)) return DT_E_ARG;
+                        const float* yact, float slope, float* dx, void* stream) {
+  if (!lin_shape_ok(m, n, k) || !dy || !w || !dx || !aligned16(dy) || (yact && !aligned16(yact)))
+    return DT_E_ARG;
   const int grid = ((m + 31) / 32) * (k / 32);
   hipLaunchKernelGGL(lin_dgrad_kernel, dim3(grid), dim3(64 * kLinWaves), 0, (hipStream_t)stream,
-                     m, n, k, dy, w, dx);
+                     m, n, k, dy, w, yact, slope, dx);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 
 int dt_upd_linear_wgrad(int32_t m, int32_t n, int32_t k, const float* dy, const float* x,
-                        float* dw, float* db, void* stream) {
+                        const float* yact, float slope, float* dw, float* db, void* stream) {
   if (!lin_shape_ok(m, n, k) || !dy || !x || !dw) return DT_E_ARG;
   const int tiles = (n / 32) * (k / 32);
   hipLaunchKernelGGL(lin_wgrad_kernel, dim3((tiles + kLinWaves - 1) / kLinWaves),
-                     dim3(64 * kLinWaves), 0, (hipStream_t)stream, m, n, k, dy, x, dw, db);
+                     dim3(64 * kLinWaves), 0, (hipStream_t)stream, m, n, k, dy, x, yact, slope,
+                     dw, db);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 

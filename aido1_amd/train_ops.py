@@ -468,13 +468,14 @@ def linear_applicable(x, lin):
 
 
 class _UpdLinear(torch.autograd.Function):
-    """y = x w^T + b (torch.nn.Linear) with K split over waves and summed in a
-    fixed order; backward dx and dw / db on their own MFMA kernels
-    (include/dtupd.h).  Where the library GEMM took one tile a workgroup
-    over all of K at batch 64."""
+    """y = x w^T + b (torch.nn.Linear), optionally through the following
+    LeakyReLU (slope not None), with K split over waves and summed in a fixed
+    order; backward dx and dw / db on their own MFMA kernels, the LeakyReLU's
+    gradient taken from the saved output (include/dtupd.h).  Where the library
+    GEMM took one tile a workgroup over all of K at batch 64."""
 
     @staticmethod
-    def forward(ctx, x, w, b):
+    def forward(ctx, x, w, b, slope):
         x = x.contiguous()
         w = w.contiguous()
         m, k = x.shape
@@ -482,16 +483,25 @@ class _UpdLinear(torch.autograd.Function):
         L = _lib.lib()
         y = torch.empty(m, n, device=x.device, dtype=x.dtype)
         work = torch.empty(int(L.dt_upd_linear_work_floats(m, n, k)), device=x.device)
-        rc = L.dt_upd_linear_fwd(m, n, k, x.data_ptr(), w.data_ptr(), b.data_ptr(), y.data_ptr(),
-                                 work.data_ptr(), _stream(x.device))
+        act = slope is not None
+        rc = L.dt_upd_linear_fwd(m, n, k, x.data_ptr(), w.data_ptr(), b.data_ptr(), int(act),
+                                 float(slope) if act else 0.0, y.data_ptr(), work.data_ptr(),
+                                 _stream(x.device))
         if rc != 0:
             raise _lib.DtError('dt_upd_linear_fwd failed (%d)' % rc)
-        ctx.save_for_backward(x, w)
+        if act:
+            ctx.save_for_backward(x, w, y)
+        else:
+            ctx.save_for_backward(x, w)
+        ctx.slope = slope
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, w = ctx.saved_tensors
+        saved = ctx.saved_tensors
+        x, w = saved[0], saved[1]
+        yact = saved[2].data_ptr() if ctx.slope is not None else None
+        slope = float(ctx.slope) if ctx.slope is not None else 0.0
         dy = dy.contiguous()
         m, k = x.shape
         n = w.shape[0]
@@ -500,19 +510,21 @@ class _UpdLinear(torch.autograd.Function):
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
             dx = torch.empty_like(x)
-            rc = L.dt_upd_linear_dgrad(m, n, k, dy.data_ptr(), w.data_ptr(), dx.data_ptr(), s)
+            rc = L.dt_upd_linear_dgrad(m, n, k, dy.data_ptr(), w.data_ptr(), yact, slope,
+                                       dx.data_ptr(), s)
             if rc != 0:
                 raise _lib.DtError('dt_upd_linear_dgrad failed (%d)' % rc)
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
             dw = torch.empty_like(w)
             db = torch.empty(n, device=x.device, dtype=x.dtype)
-            rc = L.dt_upd_linear_wgrad(m, n, k, dy.data_ptr(), x.data_ptr(), dw.data_ptr(),
-                                       db.data_ptr(), s)
+            rc = L.dt_upd_linear_wgrad(m, n, k, dy.data_ptr(), x.data_ptr(), yact, slope,
+                                       dw.data_ptr(), db.data_ptr(), s)
             if rc != 0:
                 raise _lib.DtError('dt_upd_linear_wgrad failed (%d)' % rc)
-        return dx, dw, db
+        return dx, dw, db, None
 
 
-def linear(x, lin):
-    """lin(x) on the dtupd.h kernels (linear_applicable)."""
-    return _UpdLinear.apply(x, lin.weight, lin.bias)
+def linear(x, lin, slope=None):
+    """lin(x), then LeakyReLU(slope) if slope is not None, on the dtupd.h
+    kernels (linear_applicable)."""
+    return _UpdLinear.apply(x, lin.weight, lin.bias, slope)

@@ -124,20 +124,24 @@ int dt_upd_conv_dgrad(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih
                       const float* dz, const float* w, float* dx, void* stream);
 
 /* ---- the linear layer after the trunk -------------------------------------------------
- * y[m][n] = b[n] + sum_k x[m][k] w[n][k] (torch.nn.Linear: x [M, K], w [N, K]
- * row-major), K split over waves and the slices summed in a fixed order
- * (deterministic); for config.json's flatten -> dropout -> linear 4032 -> 256,
- * where the batch M is small and K long.  N % 32 == 0, K % 32 == 0.
+ * y[m][n] = act(b[n] + sum_k x[m][k] w[n][k]) (torch.nn.Linear: x [M, K],
+ * w [N, K] row-major; act = the following LeakyReLU(slope) when leaky != 0,
+ * else none), K split over waves and the slices summed in a fixed order
+ * (deterministic); for config.json's flatten -> dropout -> linear 4032 -> 256
+ * -> leaky_relu, where the batch M is small and K long.  N % 32 == 0,
+ * K % 32 == 0.
  *   work  dt_upd_linear_work_floats(m, n, k) floats;  b may be NULL */
 int64_t dt_upd_linear_work_floats(int32_t m, int32_t n, int32_t k);
 int dt_upd_linear_fwd(int32_t m, int32_t n, int32_t k, const float* x, const float* w,
-                      const float* b, float* y, float* work, void* stream);
-/* dx[m][k] = sum_n dy[m][n] w[n][k] */
+                      const float* b, int32_t leaky, float slope, float* y, float* work,
+                      void* stream);
+/* dx[m][k] = sum_n g[m][n] w[n][k], g = dy through the fused LeakyReLU when
+ * yact (the forward's output y) is given, else dy */
 int dt_upd_linear_dgrad(int32_t m, int32_t n, int32_t k, const float* dy, const float* w,
-                        float* dx, void* stream);
-/* dw[n][k] = sum_m dy[m][n] x[m][k]; db[n] = sum_m dy[m][n] (db may be NULL) */
+                        const float* yact, float slope, float* dx, void* stream);
+/* dw[n][k] = sum_m g[m][n] x[m][k]; db[n] = sum_m g[m][n] (db may be NULL) */
 int dt_upd_linear_wgrad(int32_t m, int32_t n, int32_t k, const float* dy, const float* x,
-                        float* dw, float* db, void* stream);
+                        const float* yact, float slope, float* dw, float* db, void* stream);
 
 #ifdef __cplusplus
 }

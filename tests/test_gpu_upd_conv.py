@@ -201,11 +201,13 @@ def test_chain_rejects_bad_handoff(gpu):
     assert L.dt_upd_bn_finish(1, 0, x.data_ptr(), ctypes.byref(b), x.data_ptr(), None) != 0
 
 
+@pytest.mark.parametrize('slope', [None, 0.01])
 @pytest.mark.parametrize('m,n,k', [(64, 256, 4032), (5, 256, 4032), (33, 64, 1024)])
-def test_linear_matches_f64(gpu, m, n, k):
+def test_linear_matches_f64(gpu, m, n, k, slope):
     """The split-K linear kernels (dt_upd_linear_*) against float64 torch:
     forward with bias, dx, dw and db (the trunk's 4032 -> 256 layer at batch
-    64, a ragged batch, another shape)."""
+    64, a ragged batch, another shape), alone and with the LeakyReLU after it
+    fused (its gradient from the output)."""
     from aido1_amd import train_ops
     g = torch.Generator().manual_seed(m + n)
     x = torch.randn(m, k, generator=g, dtype=torch.float64)
@@ -218,9 +220,14 @@ def test_linear_matches_f64(gpu, m, n, k):
         lin.weight.copy_(w)
         lin.bias.copy_(b)
     assert train_ops.linear_applicable(xg, lin)
-    y = train_ops.linear(xg, lin)
+    y = train_ops.linear(xg, lin, slope)
     y.backward(dy.float().to(gpu))
     ref = x @ w.T + b
+    if slope is not None:
+        ref = torch.where(ref > 0, ref, ref * slope)
+        # the gradient's mask is the f32 output's sign (a pre-activation within
+        # rounding of zero may fall either side; its value is then ~0 anyway)
+        dy = torch.where(y.detach().double().cpu() > 0, dy, dy * slope)
     assert (y.detach().double().cpu() - ref).abs().max().item() <= _bound((x.abs() @ w.abs().T).max().item())
     assert (xg.grad.double().cpu() - dy @ w).abs().max().item() <= _bound((dy.abs() @ w.abs()).max().item())
     assert (lin.weight.grad.double().cpu() - dy.T @ x).abs().max().item() <= \
