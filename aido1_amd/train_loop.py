@@ -135,6 +135,18 @@ class TrainLoop:
                 self._refresh()
                 self.refresh_due = False
 
+    def save(self, directory, episode, reward):
+        """The exploiters' checkpoint (training/explorers.py:142-152): the
+        target networks the exploiting envs act with, in the reference's
+        layout (aido1_amd/checkpoint.py).  Returns the episode directory."""
+        return self.trainer.save(directory, episode, reward, target=True)
+
+    def load(self, directory):
+        """Start from a checkpoint (the reference's or save()'s): online and
+        target networks, then the acting copies."""
+        self.trainer.load(directory)
+        self._refresh()
+
     def check(self):
         """Synchronise and raise if anything went wrong since the last check:
         guard.NonFiniteError naming the first stages that produced NaN / Inf

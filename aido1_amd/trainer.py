@@ -207,6 +207,24 @@ class DDPGTrainer:
         opt.step()
         self.guard.scan(param_stage, *[p.data for p in params])
 
+    def save(self, directory, episode, reward, target=True):
+        """A checkpoint in the reference's layout (models/ddpg/model.py:130-140,
+        aido1_amd/checkpoint.py).  target=True saves the target networks: the
+        weights the reference's exploiters act with and save
+        (training/explorers.py:104-105, 142-152); False the online ones."""
+        from aido1_amd import checkpoint
+        actor, critic = ((self.target_actor, self.target_critic) if target
+                         else (self.actor, self.critic))
+        return checkpoint.save(self.config, directory, episode, reward, actor, critic)
+
+    def load(self, directory):
+        """Load a checkpoint directory (the reference's or save()'s) into the
+        online and the target networks (DDPG.load, then the hard copy the
+        trainer starts from)."""
+        from aido1_amd import checkpoint
+        checkpoint.load(directory, self.actor, self.critic)
+        checkpoint.load(directory, self.target_actor, self.target_critic)
+
     def check(self):
         """Raise guard.NonFiniteError naming the stages of the updates since the
         last check that produced NaN / Inf (synchronises)."""
