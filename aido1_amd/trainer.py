@@ -271,13 +271,19 @@ class DDPGTrainer:
     def _stage_actor(self):
         x = self._in
         self._opt_step(self.critic_optim, self.critic, 'critic_grad', 'critic_param')
-        pred_actions = self.actor(x['obs'])
         if self._shared_trunk():
             from aido1_amd import train_ops
-            with torch.no_grad(), train_ops.running_updates(self.critic, 2):
+            # the (stepped) critic's trunk and the actor's forward are
+            # independent until the head: two streams, two graph branches
+            side = self._fork()
+            with torch.cuda.stream(side), torch.no_grad(), \
+                    train_ops.running_updates(self.critic, 2):
                 self._trunk = self.critic.trunk(x['obs'])
+            pred_actions = self.actor(x['obs'])
+            self._join(side, self._trunk)
             q = self.critic.head(self._trunk, pred_actions)
         else:
+            pred_actions = self.actor(x['obs'])
             q = self.critic(x['obs'], pred_actions)
         actor_loss = -1.0 * torch.mean(q)
         self._grads(actor_loss, self.actor)
