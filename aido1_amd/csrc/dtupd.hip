@@ -33,6 +33,16 @@
 #ifndef DTUPD_SKIP
 #define DTUPD_SKIP 0
 #endif
+// input-gradient waves a workgroup per layer (tools/upd_micro.py variants)
+#ifndef DTUPD_DG2_NW
+#define DTUPD_DG2_NW 8
+#endif
+#ifndef DTUPD_DG3_NW
+#define DTUPD_DG3_NW 4
+#endif
+#ifndef DTUPD_DG4_NW
+#define DTUPD_DG4_NW 4
+#endif
 
 namespace {
 
@@ -1235,9 +1245,9 @@ int dt_upd_conv_dgrad(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih
   if (n == 0) return DT_OK;
   hipStream_t s = (hipStream_t)stream;
   switch (l) {
-    case 2: return launch_dgrad<L2, 4>(n, dz, w, dx, s);
-    case 3: return launch_dgrad<L3, 16>(n, dz, w, dx, s);
-    default: return launch_dgrad<L4, 4>(n, dz, w, dx, s);
+    case 2: return launch_dgrad<L2, DTUPD_DG2_NW>(n, dz, w, dx, s);
+    case 3: return launch_dgrad<L3, DTUPD_DG3_NW>(n, dz, w, dx, s);
+    default: return launch_dgrad<L4, DTUPD_DG4_NW>(n, dz, w, dx, s);
   }
 }
 

@@ -13,6 +13,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, 'tools', 'variants')
 SKIPS = {'full': 0, 'no_a_loads': 1, 'no_w_stage': 2, 'no_merge': 4, 'no_ksum': 8, 'bare': 15,
          'no_part_loads': 16, 'no_chain_merge': 32, 'no_chain_both': 48}
+# other variants: extra -D flags (dgrad waves per layer)
+EXTRA = {'dg_8_8_2': ['-DDTUPD_DG2_NW=8', '-DDTUPD_DG3_NW=8', '-DDTUPD_DG4_NW=2'],
+         'dg_16_4_8': ['-DDTUPD_DG2_NW=16', '-DDTUPD_DG3_NW=4', '-DDTUPD_DG4_NW=8'],
+         'dg_2_16_1': ['-DDTUPD_DG2_NW=2', '-DDTUPD_DG3_NW=16', '-DDTUPD_DG4_NW=1']}
 LAYERS = {1: (3, 8, 2, 120, 160), 2: (32, 4, 2, 57, 77), 3: (32, 4, 2, 27, 37),
           4: (32, 4, 1, 12, 17)}
 
@@ -26,6 +30,10 @@ def build():
         so = os.path.join(OUT, 'libupd_%s.so' % name)
         subprocess.check_call([_lib.HIPCC] + _lib.HIP_FLAGS + ['-DDTUPD_SKIP=%d' % bits,
                                                                 '-o', so, src])
+        print('built', so)
+    for name, flags in EXTRA.items():
+        so = os.path.join(OUT, 'libupd_%s.so' % name)
+        subprocess.check_call([_lib.HIPCC] + _lib.HIP_FLAGS + flags + ['-o', so, src])
         print('built', so)
 
 
@@ -72,7 +80,7 @@ def run(n, reps):
     dev = torch.device('cuda', 0)
     torch.manual_seed(0)
     s = torch.cuda.current_stream().cuda_stream
-    for name in SKIPS:
+    for name in list(SKIPS) + list(EXTRA):
         L = load(name)
         row = []
         for layer, (cin, ks, st, ih, iw) in LAYERS.items():
@@ -125,7 +133,7 @@ def run(n, reps):
                         assert L.dt_upd_bn_finish(z.numel() // 32, 0, z.data_ptr(),
                                                   ctypes.byref(hand), y.data_ptr(), s) == 0
                     t['finish'] = timeit(torch, finish, reps)
-            if name == 'full':
+            if name == 'full' or name in EXTRA:
                 ww = torch.empty(int(L.dt_upd_wgrad_work_floats(*a)), device=dev)
                 dw = torch.empty_like(w)
 
