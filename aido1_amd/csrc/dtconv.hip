@@ -601,9 +601,14 @@ __device__ __forceinline__ int ring_off(int px, int c) {
   return 64 * pos + 16 * (c ^ ((pos >> 2) & 3));
 }
 
-// conv4 (NW 4) waves per SIMD: 1 holds its 317 registers; 2 spills ~60 (diagnostic)
+// conv4 (NW 4): its weights in LDS (32 KB) rather than 128 registers a lane,
+// so two of its latency-bound workgroups share a CU (2 waves a SIMD, <= 256
+// registers each); DTCONV4_WLDS 0 / DTCONV4_OCC 1 is round 3's register form
+#ifndef DTCONV4_WLDS
+#define DTCONV4_WLDS 1
+#endif
 #ifndef DTCONV4_OCC
-#define DTCONV4_OCC 1
+#define DTCONV4_OCC (DTCONV4_WLDS ? 2 : 1)
 #endif
 template <int IH, int IW, int OH, int OW, int ST, int NW, int kIn, int kOut>
 __global__ void __launch_bounds__(64 * NW, NW == 4 ? DTCONV4_OCC : 1)   // 1: one wave per SIMD, the full register file
@@ -711,10 +716,17 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
     }
   };
 
-  // weights and bias for the whole launch (row = out channel = lane & 31)
-  half8 wa[32];
+  // weights and bias for the whole launch (row = out channel = lane & 31): in
+  // registers, or for conv4 in LDS (kWL), read per MFMA
+  constexpr bool kWL = NW == 4 && DTCONV4_WLDS;
+  __shared__ __attribute__((aligned(16))) half8 wl[kWL ? 32 * 64 : 1];
+  half8 wa[kWL ? 1 : 32];
+  if constexpr (kWL) {
+    for (int i = tid; i < 32 * 64; i += kThreads) wl[i] = wfrag[i];
+  } else {
 #pragma unroll
-  for (int s = 0; s < 32; ++s) wa[s] = wfrag[s * 64 + lane];
+    for (int s = 0; s < 32; ++s) wa[s] = wfrag[s * 64 + lane];
+  }
   if (tid < CO) s_bias[tid] = bias[tid];
   float w_cnt = 0.0f, w_mean[16], w_m2[16];
 #pragma unroll
@@ -759,7 +771,9 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
     auto mm = [&](half8 (&b)[8], int gy) __attribute__((always_inline)) {
 #pragma unroll
       for (int i = 0; i < 8; ++i)   // the ring rows are already normalised (commit)
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wa[8 * gy + i], b[i], acc, 0, 0, 0);
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kWL ? wl[(8 * gy + i) * 64 + lane]
+                                                         : wa[kWL ? 0 : 8 * gy + i],
+                                                     b[i], acc, 0, 0, 0);
     };
     if (!(DTCONV_SKIP & 2)) ld(bq[0], 0);
 #pragma unroll
