@@ -1,19 +1,25 @@
-"""The fused conv-block tail of the DDPG update (include/dttrain.h).
+"""The DDPG update's train-mode layers on the GPU kernels (include/dttrain.h,
+include/dtupd.h).
 
 Every conv block of config.json's actor and critic is conv_2d -> leaky_relu
 -> batch_norm_2d (models/ddpg/modules.py MetaNet), and the trainer runs all
 four networks in train mode (training/trainers.py:143-237).  On the GPU in
-float32 with channels_last activations, ``conv_leaky_bn`` runs the
-convolution without its bias (include/dtupd.h's f32 MFMA kernels for
-config.json's layers; MIOpen for any other shape) and then dt_bn_leaky_fwd: bias,
-LeakyReLU, the batch statistics, the running-statistics update and
-num_batches_tracked in one kernel, the normalisation in a second; its
-backward is dt_bn_leaky_bwd (two kernels for BatchNorm's, LeakyReLU's and the
-bias's gradients).  The activation leaky(z + bias) is never stored: every
-kernel recomputes it from the convolution output z (one f32 add and one
-select), which saves writing a second full-size tensor per block.  torch runs eight kernels for the forward tail and five for
-the backward.  The modules, parameters and state_dict are the unchanged
-torch ones; ``applicable`` says when the fused tail replaces them.
+float32 with channels_last activations:
+* ``conv_trunk``: a run of such blocks on config.json's four layers as ONE
+  chain (dtupd.h): each convolution merges the previous block's BatchNorm
+  partials itself and normalises while it loads, so no normalised activation
+  is stored; the last block writes the trunk's output in NCHW (the flatten
+  after it is a view).  Backward: dt_bn_leaky_bwd per block, the weight
+  gradient normalising its input rows again while staging them, the input
+  gradient.
+* ``conv_leaky_bn``: one block (dt_upd_conv_fwd_bn + dt_bn_leaky_apply on
+  dtupd.h's layers; MIOpen + dt_bn_leaky_fwd for any other shape).
+* ``linear``: the long-K linear after the trunk (4032 -> 256) with its
+  LeakyReLU, split-K MFMA kernels.
+The activation leaky(z + bias) is never stored: every kernel recomputes it
+from the convolution output z.  The modules, parameters and state_dict are
+the unchanged torch ones; ``applicable`` / ``trunk_len`` /
+``linear_applicable`` say when the kernels replace them.
 """
 import contextlib
 import ctypes
