@@ -814,7 +814,7 @@ dgrad_kernel(int n, const float* __restrict__ dz, const float* __restrict__ w,
   }
 }
 
-// ---- the linear layer after the trunk (flatten -> dropout -> linear 4032 -> 256) ----------
+// ---- the linear layer after the trunk (flatten -> dropout -> linear 4032 -> 256 / 512) ----
 // y[m][n] = b[n] + sum_k x[m][k] W[n][k] with M (the batch) small and K long:
 // library GEMMs pick one tile a workgroup over all of K (latency-bound, 20 us
 // at batch 64).  Here K is split: each wave takes a slice of k-steps of a

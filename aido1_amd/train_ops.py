@@ -14,7 +14,7 @@ float32 with channels_last activations:
   gradient.
 * ``conv_leaky_bn``: one block (dt_upd_conv_fwd_bn + dt_bn_leaky_apply on
   dtupd.h's layers; MIOpen + dt_bn_leaky_fwd for any other shape).
-* ``linear``: the long-K linear after the trunk (4032 -> 256) with its
+* ``linear``: the long-K linear after the trunk (4032 -> 256 / 512) with its
   LeakyReLU, split-K MFMA kernels.
 The activation leaky(z + bias) is never stored: every kernel recomputes it
 from the convolution output z.  The modules, parameters and state_dict are

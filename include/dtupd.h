@@ -127,9 +127,9 @@ int dt_upd_conv_dgrad(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih
  * y[m][n] = act(b[n] + sum_k x[m][k] w[n][k]) (torch.nn.Linear: x [M, K],
  * w [N, K] row-major; act = the following LeakyReLU(slope) when leaky != 0,
  * else none), K split over waves and the slices summed in a fixed order
- * (deterministic); for config.json's flatten -> dropout -> linear 4032 -> 256
- * -> leaky_relu, where the batch M is small and K long.  N % 32 == 0,
- * K % 32 == 0.
+ * (deterministic); for config.json's flatten -> dropout -> linear 4032 ->
+ * 256 (critic) or 512 (actor) -> leaky_relu, where the batch M is small and
+ * K long.  N % 32 == 0, K % 32 == 0.
  *   work  dt_upd_linear_work_floats(m, n, k) floats;  b may be NULL */
 int64_t dt_upd_linear_work_floats(int32_t m, int32_t n, int32_t k);
 int dt_upd_linear_fwd(int32_t m, int32_t n, int32_t k, const float* x, const float* w,

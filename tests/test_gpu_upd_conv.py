@@ -205,7 +205,7 @@ def test_chain_rejects_bad_handoff(gpu):
 @pytest.mark.parametrize('m,n,k', [(64, 256, 4032), (5, 256, 4032), (33, 64, 1024)])
 def test_linear_matches_f64(gpu, m, n, k, slope):
     """The split-K linear kernels (dt_upd_linear_*) against float64 torch:
-    forward with bias, dx, dw and db (the trunk's 4032 -> 256 layer at batch
+    forward with bias, dx, dw and db (the critic's 4032 -> 256 layer at batch
     64, a ragged batch, another shape), alone and with the LeakyReLU after it
     fused (its gradient from the output)."""
     from aido1_amd import train_ops
