@@ -86,3 +86,40 @@ def test_render_io_layout_matches_header(tmp_path):
     assert vals[:len(fields)] == [getattr(RenderIO, f).offset for f in fields]
     assert vals[len(fields)] == ctypes.sizeof(RenderIO)
     assert vals[len(fields) + 1] == ctypes.sizeof(LineParams)
+
+
+def test_upd_bn_layout_matches_header(tmp_path):
+    """include/dtupd.h DtUpdBn against its ctypes mirror (_lib.DtUpdBn)."""
+    from aido1_amd._lib import DtUpdBn
+    fields = [f[0] for f in DtUpdBn._fields_]
+    src = tmp_path / 'updbn.c'
+    body = '\n'.join('printf("%%zu ", offsetof(DtUpdBn, %s));' % f for f in fields)
+    src.write_text('#include <stdio.h>\n#include <stddef.h>\n#include "dtupd.h"\nint main(){'
+                   + body + 'printf("%zu\\n", sizeof(DtUpdBn)); return 0;}')
+    exe = tmp_path / 'updbn'
+    subprocess.run(['gcc', '-I', os.path.join(REPO, 'include'), '-o', str(exe), str(src)],
+                   check=True)
+    vals = [int(v) for v in subprocess.run([str(exe)], capture_output=True, text=True,
+                                           check=True).stdout.split()]
+    assert vals[:-1] == [getattr(DtUpdBn, f).offset for f in fields]
+    assert vals[-1] == ctypes.sizeof(DtUpdBn)
+
+
+def test_upd_entry_points_check_arguments(libpath):
+    """dtupd.h's host-side argument checks (no GPU work is issued): other
+    geometries, bad linear shapes and an empty hand-off are refused."""
+    from aido1_amd import _lib
+    L = _lib.lib()
+    parts = ctypes.c_int32(0)
+    assert L.dt_upd_part_floats() == 256 * 32 * 3
+    assert L.dt_upd_conv_fwd_part(16, 4, 2, 1, 57, 77, 1, None, 1, 1, 0.01, 1, 1,
+                                  ctypes.byref(parts), None) != 0
+    empty = _lib.DtUpdBn()
+    assert L.dt_upd_conv_fwd_part(32, 4, 2, 1, 57, 77, 1, ctypes.byref(empty), 1, 1, 0.01, 1, 1,
+                                  ctypes.byref(parts), None) != 0
+    assert L.dt_upd_bn_finish(126, 7, 16, ctypes.byref(empty), 16, None) != 0   # m % hw
+    assert L.dt_upd_linear_work_floats(64, 250, 4032) == -1                    # n % 32
+    assert L.dt_upd_linear_work_floats(64, 256, 4030) == -1                    # k % 32
+    assert L.dt_upd_linear_work_floats(64, 256, 4032) % (64 * 256) == 0
+    assert L.dt_upd_linear_fwd(64, 256, 4032, None, 16, 16, 0, 0.0, 16, 16, None) != 0
+    assert L.dt_upd_wgrad_work_floats(3, 8, 2, 64, 120, 160) == 512 * 32 * 192
