@@ -414,12 +414,13 @@ __device__ inline int sobel_swar(uint32_t a00, uint32_t a01, uint32_t a02, uint3
 // b (< 256) in all four bytes: one v_perm, not a 32-bit multiply
 __device__ inline uint32_t splat_byte(uint32_t b) { return __builtin_amdgcn_perm(0u, b, 0u); }
 
-// bytes of 0 / 1 -> 0 / 255 (= m * 255 mod 2^32: no byte borrows), shift and
-// subtract instead of a quarter-rate v_mul_lo_u32 (asm: the compiler folds the
-// two back into the multiply)
+// bytes of 0 / 1 -> 0 / 255: each 16-bit half (b0 + 256 b1) times 255 is
+// b0 * 0xFF + b1 * 0xFF00 (no carry past the half), one full-rate packed
+// 16-bit multiply (the constant in an SGPR: VOP3P takes no literal here),
+// where shift + subtract took two instructions
 __device__ inline uint32_t bytes01_to_ff(uint32_t m) {
   uint32_t r;
-  asm("v_lshlrev_b32 %0, 8, %1\n\tv_sub_u32 %0, %0, %1" : "=&v"(r) : "v"(m));
+  asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(r) : "v"(m), "s"(0x00FF00FFu));
   return r;
 }
 
@@ -1194,16 +1195,16 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, in
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const uint32_t mid = m[1][j];
-        const uint32_t b = mid & 255u;
-        const uint32_t rep = splat_byte(b);
-        const uint32_t l0 = j > 0 ? m[0][j - 1] : lw[0], l1 = j > 0 ? m[1][j - 1] : lw[1],
-                       l2 = j > 0 ? m[2][j - 1] : lw[2];
-        const uint32_t r0 = j < 3 ? m[0][j + 1] : rw[0], r1 = j < 3 ? m[1][j + 1] : rw[1],
-                       r2 = j < 3 ? m[2][j + 1] : rw[2];
-        const uint32_t diff = (mid ^ rep) | (m[0][j] ^ rep) | (m[2][j] ^ rep) |
-                              (((l0 >> 24) ^ b) | ((l1 >> 24) ^ b) | ((l2 >> 24) ^ b)) |
-                              (((r0 ^ b) | (r1 ^ b) | (r2 ^ b)) & 255u);
+        const uint32_t rep = splat_byte(m[1][j] & 255u);
+        // per row the word's 6-pixel span as two byte-shifted words (v_alignbyte):
+        // pixels 4j-1 .. 4j+2 and 4j+1 .. 4j+4, each compared with the splat
+        uint32_t diff = 0u;
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+          const uint32_t lft = j > 0 ? m[i][j - 1] : lw[i], rgt = j < 3 ? m[i][j + 1] : rw[i];
+          diff |= (__builtin_amdgcn_alignbyte(m[i][j], lft, 3u) ^ rep) |
+                  (__builtin_amdgcn_alignbyte(rgt, m[i][j], 1u) ^ rep);
+        }
         non[4 * k + j] = act && diff != 0u;
       }
     }
