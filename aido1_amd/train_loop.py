@@ -99,7 +99,10 @@ class TrainLoop:
         self.rollout.reset()
         self.obs = self.rollout.stack()
 
-    def step(self, timing=None):
+    def step(self, timing=None, update_timing=None):
+        """One decision: rollout, add, and the update(s).  timing: an event
+        pair around the actor forward (ActorRollout.step); update_timing: one
+        around this decision's updates (recorded on the stream they run on)."""
         r, rm, done = self.rollout.step(timing)
         rew = rm if self.reward_modified else r        # explorers.py:205-206
         if self.pending:   # the previous update (side stream) precedes this add
@@ -118,12 +121,20 @@ class TrainLoop:
             if self.side is not None:
                 self.side.wait_stream(torch.cuda.current_stream(self.device))
                 with torch.cuda.stream(self.side):
+                    if update_timing is not None:
+                        update_timing[0].record()
                     for _ in range(self.updates_per_step):
                         self._update()
+                    if update_timing is not None:
+                        update_timing[1].record()
                 self.pending = True
             else:
+                if update_timing is not None:
+                    update_timing[0].record()
                 for _ in range(self.updates_per_step):
                     self._update()
+                if update_timing is not None:
+                    update_timing[1].record()
         return r, rm, done
 
     def flush(self):

@@ -1003,17 +1003,23 @@ def train_record(args, ctx, K, W, parity=True):
     u0 = loop.updates
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for _ in range(K)]
+    uev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+           for _ in range(K)]
     ctx.barrier()
     ctx.sync()
     t0 = time.perf_counter()
     for k in range(K):
-        loop.step(timing=ev[k])
+        loop.step(timing=ev[k], update_timing=uev[k])
     loop.flush()
     ctx.sync()
     ctx.barrier()
     elapsed = time.perf_counter() - t0
     st = loop.rollout.stats()
     actor_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    try:   # a decision without an update (buffer below a batch) records no events
+        update_ms = float(np.mean([a.elapsed_time(b) for a, b in uev]))
+    except RuntimeError:
+        update_ms = None
     tot, tmax, per = rank_report(ctx, [st['sim_steps'], st['decisions'], st['resets'],
                                        loop.updates - u0], elapsed)
     sim_steps, decisions, resets, updates = tot
@@ -1068,6 +1074,9 @@ def train_record(args, ctx, K, W, parity=True):
                    'updates_all_ranks': updates, 'elapsed_s': tmax,
                    'synchronous_updates_per_s': K / tmax,
                    'samples_per_s': batch * updates / tmax},
+        'phases_ms': {'actor': actor_ms, 'update': update_ms,
+                      'timing': 'HIP events around the actor forward and around the '
+                                'update(s) of every timed decision (rank 0)'},
         'per_rank': per,
         'parity': par,
         'roofline': {'bound': 'mfma', 'kernel': 'actor forward (fp16 MFMA convs + linears)',
