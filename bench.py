@@ -85,7 +85,7 @@ def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument('--gpus', type=int, default=1)
     p.add_argument('--steps', type=int, default=100)
-    p.add_argument('--warmup', type=int, default=10)
+    p.add_argument('--warmup', type=int, default=30)
     p.add_argument('--envs', type=int, default=4096)
     p.add_argument('--map', default='loop_empty')
     p.add_argument('--config', default='render', choices=['render', 'lane', 'actor', 'train'])
