@@ -22,7 +22,7 @@ SOURCES = ['dtsim.hip', 'dtrender.hip', 'dtreplay.hip', 'dtactor.hip', 'dtconv.h
 HEADERS = ['dtsim_common.h', 'dtrender.h', 'dtsync.h']
 PUBLIC_HEADERS = ['dtsim.h', 'dtreplay.h', 'dtactor.h', 'dttrain.h', 'dtupd.h']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
-ABI_VERSION = 8
+ABI_VERSION = 9
 
 HIP_FLAGS = ['--offload-arch=gfx950', '-O3', '-fPIC', '-shared', '-std=c++17',
              '-ffp-contract=off', '-munsafe-fp-atomics']
@@ -55,6 +55,14 @@ class DtUpdBn(ctypes.Structure):
                 ('running_mean', ctypes.c_void_p), ('running_var', ctypes.c_void_p),
                 ('num_batches_tracked', ctypes.c_void_p), ('updates', ctypes.c_int32),
                 ('mean_invstd', ctypes.c_void_p), ('guard', ctypes.c_void_p)]
+
+
+class DtEpisodeState(ctypes.Structure):
+    """include/dtactor.h DtEpisodeState: the episode accumulators and ring."""
+    _fields_ = [('reward', ctypes.c_void_p), ('reward_modified', ctypes.c_void_p),
+                ('tick', ctypes.c_void_p), ('episode', ctypes.c_void_p),
+                ('decisions', ctypes.c_void_p), ('count', ctypes.c_void_p),
+                ('ring', ctypes.c_void_p), ('capacity', ctypes.c_int64)]
 
 
 class DtExploreParams(ctypes.Structure):
@@ -224,6 +232,8 @@ def lib():
             'dt_explore': (ctypes.c_int, [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                           ctypes.POINTER(DtExploreParams), vp, vp]),
             'dt_explore_done': (ctypes.c_int, [i32, vp, vp, vp, vp, i32, vp]),
+            'dt_episode_account': (ctypes.c_int, [i32, i32, vp, vp, vp,
+                                                  ctypes.POINTER(DtEpisodeState), vp]),
             'dt_actor_head': (ctypes.c_int, [i32, i32, i32, vp, i32, vp, vp, vp, vp, i32,
                                              ctypes.c_float, vp, vp]),
         }

@@ -137,7 +137,10 @@ class _Seq(nn.Module):       # MetaNet: ".internal_modules.<i>"
                 from aido1_amd import train_ops
                 if train_ops.linear_applicable(x, m.linear):
                     act = mods[i + 1] if i + 1 < k else None
-                    if isinstance(act, nn.LeakyReLU):       # linear -> leaky_relu in one
+                    # linear -> leaky_relu in one; its backward reads the
+                    # gradient off the sign of the saved output, which is only
+                    # the input's sign for a non-negative slope
+                    if isinstance(act, nn.LeakyReLU) and act.negative_slope >= 0:
                         x = train_ops.linear(x, m.linear, float(act.negative_slope))
                         i += 2
                     else:

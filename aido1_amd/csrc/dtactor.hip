@@ -296,6 +296,69 @@ extern "C" int dt_explore_done(int32_t n, const uint8_t* done, double* ou_x, int
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 
+// ---- dt_episode_account: the explorers' episode sums and finished-episode ring -------------
+// One lane per env walks its k decisions in order (the f64 sums are the
+// explorer's `episode_metrics[...] += ...` in the same order); a finished
+// episode takes a ring slot from one device-wide counter.  Finished episodes
+// are ~10 % of the envs a decision, so the per-lane atomic is not contended
+// enough to aggregate.
+namespace {
+
+__global__ void __launch_bounds__(256)
+episode_account_kernel(int n, int k, const double* __restrict__ reward,
+                       const double* __restrict__ reward_mod, const uint8_t* __restrict__ done,
+                       DtEpisodeState st) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  double r = st.reward[i], m = st.reward_modified[i];
+  int64_t tick = st.tick[i], ep = st.episode[i];
+  int32_t len = st.decisions[i];
+  for (int d = 0; d < k; ++d) {
+    const size_t o = (size_t)d * n + i;
+    r = r + reward[o];
+    m = m + reward_mod[o];
+    tick += 1;
+    len += 1;
+    if (done[o]) {
+      const unsigned long long slot =
+          atomicAdd(reinterpret_cast<unsigned long long*>(st.count), 1ull);
+      DtEpisodeRecord rec;
+      rec.reward = r;
+      rec.reward_modified = m;
+      rec.tick = tick;
+      rec.episode = ep;
+      rec.env = i;
+      rec.decisions = len;
+      st.ring[slot % (unsigned long long)st.capacity] = rec;
+      r = 0.0;
+      m = 0.0;
+      len = 0;
+      ep += 1;
+    }
+  }
+  st.reward[i] = r;
+  st.reward_modified[i] = m;
+  st.tick[i] = tick;
+  st.episode[i] = ep;
+  st.decisions[i] = len;
+}
+
+}  // namespace
+
+extern "C" int dt_episode_account(int32_t n, int32_t k, const double* reward,
+                                  const double* reward_mod, const uint8_t* done,
+                                  const DtEpisodeState* state, void* stream) {
+  if (n < 0 || k < 1 || !state) return DT_E_ARG;
+  if (n == 0) return DT_OK;
+  if (!reward || !reward_mod || !done || !state->reward || !state->reward_modified ||
+      !state->tick || !state->episode || !state->decisions || !state->count || !state->ring ||
+      state->capacity < 1)
+    return DT_E_ARG;
+  episode_account_kernel<<<(n + 255) / 256, 256, 0, (hipStream_t)stream>>>(
+      n, k, reward, reward_mod, done, *state);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
 // ---- the actor head after the first linear: LeakyReLU -> lin2 -> output ---------------
 // (config.json actor output branch: linear 512 -> 2, tanh; ddpg.py:58-62).  One
 // wave a sample: each lane takes 8 of the K inputs (16-B loads), LeakyReLU in

@@ -38,21 +38,33 @@ def reduce_run(counts, elapsed, device='cpu'):
 
 
 def gather_returns(returns):
-    """All ranks' 1-D float tensors of finished-episode returns, concatenated in
-    rank order (padded transfer: all_gather needs equal sizes)."""
+    """All ranks' finished-episode returns, concatenated in rank order: 1-D
+    tensors, or [m, c] tables of per-episode records (TrainLoop.poll_episodes:
+    rank, env, tick, returns, steps), m varying by rank (padded transfer:
+    all_gather needs equal sizes).  The tensors must live where the backend
+    can reach them (GPU for nccl, CPU for gloo)."""
     rank, ws = world()
     if ws == 1:
         return returns.clone()
     dev = returns.device
-    n = torch.tensor([returns.numel()], dtype=torch.int64, device=dev)
+    n = torch.tensor([returns.shape[0]], dtype=torch.int64, device=dev)
     sizes = [torch.zeros_like(n) for _ in range(ws)]
     dist.all_gather(sizes, n)
     m = int(max(s.item() for s in sizes))
-    buf = torch.full((m,), float('nan'), dtype=returns.dtype, device=dev)
-    buf[:returns.numel()] = returns
+    buf = torch.full((max(m, 1),) + tuple(returns.shape[1:]), float('nan'), dtype=returns.dtype,
+                     device=dev)
+    buf[:returns.shape[0]] = returns
     parts = [torch.empty_like(buf) for _ in range(ws)]
     dist.all_gather(parts, buf)
     return torch.cat([p[:int(s.item())] for p, s in zip(parts, sizes)])
+
+
+def collective_device(device):
+    """Where a collective's tensors must live: the rank's GPU under nccl (RCCL),
+    the host under gloo."""
+    if world()[1] > 1 and dist.get_backend() == 'nccl':
+        return torch.device(device)
+    return torch.device('cpu')
 
 
 class GradAllReduce:

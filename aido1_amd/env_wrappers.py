@@ -19,6 +19,8 @@ EnvironmentWrapper.step (utils/env_wrappers.py:213-253) semantics kept:
 Finished envs respawn inside the same launch (VectorEnv auto-reset); their
 stack restarts with three copies of the first frame (Transformer.reset) and
 ``terminal`` in the info holds the lane pose they finished in.
+``total_reward`` holds a finished env's episode return until its next step
+(the reference's sum lives until reset(), env_wrappers.py:197,251).
 """
 import torch
 
@@ -61,6 +63,7 @@ class EnvironmentWrapper:
         self.render = RenderOutput(n_envs, self.env.device, slots=3) if obs == 'render' else None
         self.seed = None
         self.total_reward = torch.zeros(n_envs, dtype=torch.float64, device=self.env.device)
+        self._restart = torch.zeros(n_envs, dtype=torch.bool, device=self.env.device)
         self.observation_transformed = None
 
     # ---- reference API -----------------------------------------------------------
@@ -77,6 +80,7 @@ class EnvironmentWrapper:
     def reset(self):
         obs = self.env.reset()
         self.total_reward.zero_()
+        self._restart.zero_()
         if self.render is not None:
             self.render.restart()
             self.env.render_into(self.render)
@@ -93,8 +97,13 @@ class EnvironmentWrapper:
             obs = self.render.stack_view()
         else:
             obs = out.obs
+        # the reference keeps total_reward until the next reset()
+        # (utils/env_wrappers.py:197,251); a finished env's auto-reset is
+        # that reset, so its sum restarts at the env's next step and the
+        # finished episode's return stays readable until then
+        self.total_reward.masked_fill_(self._restart, 0.0)
         self.total_reward += out.reward
-        self.total_reward.masked_fill_(out.done.bool(), 0.0)
+        self._restart = out.done.bool()
         self.observation_transformed = obs
         info = {'terminal': out.lanepos, 'tile': out.tile}
         return obs, (out.reward, out.reward_mod), out.done.bool(), info

@@ -135,16 +135,32 @@ class DeviceAdam(torch.optim.Adam):
         """Adam's, then the one shared float64 step tensor again (torch restores
         a float32 step per parameter, which would send every later step down
         the torch fallback) and the moments in their parameter's memory format
-        (the dt_adam table needs equal strides)."""
+        (the dt_adam table needs equal strides).  Each group keeps its own
+        float64 device lr tensor, filled with the loaded value: torch would
+        put a deep copy there (a host tensor after map_location='cpu'), which
+        dt_adam cannot read and which HIP graphs captured earlier and
+        TrainingDecay's fill_ never see.  Likewise the moments are copied into
+        the tensors they replace, so a captured dt_adam keeps reading them."""
+        lrs = [g['lr'] for g in self.param_groups]
+        old = {p: (st.get('exp_avg'), st.get('exp_avg_sq')) for p, st in self.state.items()}
         super().load_state_dict(state_dict)
+        for g, lr in zip(self.param_groups, lrs):
+            loaded = g['lr']
+            if torch.is_tensor(lr):
+                lr.fill_(float(loaded.item() if torch.is_tensor(loaded) else loaded))
+                g['lr'] = lr
         step = None
         for group in self.param_groups:
             for p in group['params']:
                 st = self.state[p]
                 if 'step' in st and step is None:
                     step = st['step']
-                for k in ('exp_avg', 'exp_avg_sq'):
-                    if k in st and st[k].stride() != p.stride():
+                for k, prev in zip(('exp_avg', 'exp_avg_sq'), old.get(p, (None, None))):
+                    if k not in st:
+                        continue
+                    if prev is not None and prev.shape == st[k].shape:
+                        st[k] = prev.copy_(st[k])
+                    elif st[k].stride() != p.stride() or st[k].device != p.device:
                         st[k] = torch.empty_like(p).copy_(st[k])
         if step is not None:
             self._step_t.copy_(torch.as_tensor(step, dtype=torch.float64))

@@ -28,6 +28,7 @@ import torch
 
 from aido1_amd.actor import ConfigActor, FusedActor
 from aido1_amd.config import EnvConfig
+from aido1_amd.episodes import EpisodeTracker
 from aido1_amd.env_wrappers import map_tanh_in_place
 from aido1_amd.explore import FusedExplore, OUNoise, act, explore_actions
 from aido1_amd.render import H, W, RenderOutput
@@ -120,6 +121,9 @@ class ActorRollout:
         # restatement (explore.py), which draws the same numbers
         self.fx = FusedExplore(config, self.ou, self.eps, self.explorer_id, head=head) \
             if fused_explore else None
+        # the explorers' episode sums and finished-episode records
+        # (explorers.py:118-123, 202-204; aido1_amd/episodes.py)
+        self.episodes = EpisodeTracker(n_envs, self.device)
 
     def reset(self):
         for env, ro in zip(self.envs, self.renders):
@@ -128,6 +132,7 @@ class ActorRollout:
             env.render_into(ro)
         self.ou.reset_states()
         self.episode.zero_()
+        self.episodes.reset()       # every env starts a new episode
 
     def order(self):
         return self.renders[0].order()
@@ -202,6 +207,7 @@ class ActorRollout:
         self._step_envs()
         if self.guard is not None:
             self.guard.scan('env', self.reward, self.reward_mod)
+        self.episodes.account(self.reward, self.reward_mod, self.done)
         if self.fx is not None:   # tanh map, OU reset and episode count in one kernel
             self.fx.done(self.done, self.episode, self.actions)
             return self.reward, self.reward_mod, self.done

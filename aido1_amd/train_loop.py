@@ -33,13 +33,25 @@ reference's explorers act with whatever the asynchronous trainer last
 published (training/managers.py:113-124), so a lag of one update is within
 its semantics.  overlap=False keeps the strictly sequential order.
 
-Nothing in the loop synchronises with the host.  Transition semantics: the
+Episodes (training/explorers.py:118-154, 215-240): the rollout keeps every
+env's episode sums on the device (episodes.EpisodeTracker);
+poll_episodes() drains the finished episodes, gathers them from every rank
+(distributed.gather_returns), feeds the exploiting envs' ones to the
+exploiter checkpoint rule (save() under save_dir) and logs the explorers'
+scalars to log_dir (episodes.EpisodeBook).  step() calls it every
+`poll_every` decisions and check() every `check_every` (0: the caller does;
+both synchronise with the host).
+
+Nothing else in the loop synchronises with the host.  Transition semantics: the
 stored next_obs of a finished env is its respawn stack (auto-reset), harmless
 because notdone = 0 removes Q(s') from its target.
 """
+import os
+
 import torch
 
 from aido1_amd.actor import ConfigActor, ConfigCritic
+from aido1_amd.episodes import EpisodeBook
 from aido1_amd.guard import Guard
 from aido1_amd.replay import PrioritizedReplayBuffer, ReplayBuffer
 from aido1_amd.rollout import ActorRollout
@@ -52,7 +64,8 @@ class TrainLoop:
     def __init__(self, config, n_envs=4096, maps=('small_loop', 'zigzag'), device=0, seed=1234,
                  env_id_base=0, buffer_size=None, prioritized=True, batch_size=None,
                  updates_per_step=1, refresh_every=1, obs_dtype=None, actor_dtype=torch.float16,
-                 actor_mode='reference', masks=False, graph=True, overlap=False, n_exploit=None):
+                 actor_mode='reference', masks=False, graph=True, overlap=False, n_exploit=None,
+                 save_dir=None, log_dir=None, poll_every=0, check_every=0):
         t = config['training']
         self.config = config
         self.device = torch.device('cuda', device)
@@ -94,6 +107,11 @@ class TrainLoop:
         self.side = torch.cuda.Stream(self.device) if overlap else None
         self.pending = False        # an update is in flight on self.side
         self.refresh_due = False
+        # episode accounting (explorers.py:118-154, 215-240)
+        self.save_dir = save_dir
+        self.book = EpisodeBook(config, self.device, self.rollout.n_explore,
+                                save=self._save_exploiter if save_dir else None, log_dir=log_dir)
+        self.poll_every, self.check_every = int(poll_every), int(check_every)
 
     def reset(self):
         self.rollout.reset()
@@ -135,16 +153,27 @@ class TrainLoop:
                     self._update()
                 if update_timing is not None:
                     update_timing[1].record()
+        if self.poll_every and self.decisions % self.poll_every == 0:
+            self.poll_episodes()
+        if self.check_every and self.decisions % self.check_every == 0:
+            self.check()
         return r, rm, done
 
-    def flush(self):
-        """Join an in-flight update (overlap=True) and apply its refresh."""
-        if self.pending:
-            torch.cuda.current_stream(self.device).wait_stream(self.side)
-            self.pending = False
-            if self.refresh_due:
-                self._refresh()
-                self.refresh_due = False
+    # ---- episodes -------------------------------------------------------------------
+    def poll_episodes(self):
+        """Drain this rank's finished episodes and hand them to the episode book
+        (gather over ranks, exploiter checkpoints, scalars; episodes.EpisodeBook).
+        Returns the gathered table.  Every rank must call it (a collective)."""
+        return self.book.poll(self.rollout.episodes.drain())
+
+    def _save_exploiter(self, counter, reward):
+        """explorers.py:75,150-152: the exploiters' model under
+        save_dir/exploiting_virtual_thread_<p_id>, p_id the first virtual
+        exploiter's (training/managers.py:243-253)."""
+        t = self.config['training']
+        p_id = t.get('num_threads_exploring_virtual', 0) + t.get('num_threads_exploiting', 0)
+        return self.save(os.path.join(self.save_dir, 'exploiting_virtual_thread_%d' % p_id),
+                         counter, reward)
 
     def save(self, directory, episode, reward):
         """The exploiters' checkpoint (training/explorers.py:142-152): the

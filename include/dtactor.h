@@ -143,6 +143,45 @@ int dt_explore(int32_t n, const float* actor_out, const double* normals, const d
 int dt_explore_done(int32_t n, const uint8_t* done, double* ou_x, int64_t* episode,
                     float* actions, int32_t tanh_map, void* stream);
 
+/* dt_episode_account: the explorers' per-episode accounting for n envs, after
+ * each decision (training/explorers.py:118-123 start an episode at zero,
+ * :202-204 add every decision's (reward, reward_modified) and one step, the
+ * episode ends with done; utils/env_wrappers.py:251 keeps total_reward).
+ * Replaces the Python float sums of one SingleThreadExplorer per env.
+ *   reward, reward_mod  device f64 [k, n]: dt_step's outputs (k = 1), or
+ *                       dt_step_many's k decisions (decision d at [d * n])
+ *   done                device u8 [k, n]
+ * Per env, in decision order: sums += (reward, reward_mod) in f64, decisions
+ * += 1, tick += 1; on done one record (below) is written to the ring at slot
+ * count % capacity (count += 1, a device atomic), and the sums restart.  An
+ * env that finishes several episodes inside one k-chunk writes one record
+ * for each.  Records of one call are in no particular order: (tick, env)
+ * orders them.  The caller owns and zero-initialises every array.  The
+ * reference's episode reward divides by reward_scale and multiplies steps by
+ * repeat_actions (explorers.py:135-140); the host does that, in f64. */
+typedef struct DtEpisodeRecord {
+  double reward;            /* sum of the episode's decision rewards */
+  double reward_modified;   /* sum of its reward_mod */
+  int64_t tick;             /* the env's decisions so far, this one included */
+  int64_t episode;          /* the env's episode index (0-based) */
+  int32_t env;              /* env index in [0, n) */
+  int32_t decisions;        /* decisions in the episode */
+} DtEpisodeRecord;
+
+typedef struct DtEpisodeState {
+  double* reward;               /* [n] running sums of the current episode */
+  double* reward_modified;      /* [n] */
+  int64_t* tick;                /* [n] */
+  int64_t* episode;             /* [n] finished episodes */
+  int32_t* decisions;           /* [n] */
+  uint64_t* count;              /* [1] records written since creation */
+  DtEpisodeRecord* ring;        /* [capacity] */
+  int64_t capacity;             /* >= 1 */
+} DtEpisodeState;
+
+int dt_episode_account(int32_t n, int32_t k, const double* reward, const double* reward_mod,
+                       const uint8_t* done, const DtEpisodeState* state, void* stream);
+
 /* dt_actor_head: the actor's output branch after its first linear
  * (config.json actor: leaky_relu -> linear(512 -> 2) -> tanh;
  * duckietown_rl/ddpg.py:58-62) for n samples in one launch, one wave each:

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DT_ABI_VERSION 8  /* 2: curves per tile vary (curve_start), intersections;
+#define DT_ABI_VERSION 9  /* 2: curves per tile vary (curve_start), intersections;
                              3: static objects in dt_map, safety_rad_mult;
                              4: dt_render_io.pose / list_cap, dt_copy_pose,
                                 dt_step_many pose output;
@@ -45,7 +45,9 @@ extern "C" {
                                 dtactor.h reference-mode partials [n, 32, 3]
                                 (mean, M2, centre) with centred activations;
                                 dtupd.h (the update's convolutions and the
-                                conv trunk's BatchNorm hand-off) */
+                                conv trunk's BatchNorm hand-off);
+                             9: dtactor.h dt_episode_account (episode sums and
+                                the finished-episode ring) */
 
 /* error codes */
 #define DT_OK 0

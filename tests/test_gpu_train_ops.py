@@ -127,6 +127,64 @@ def test_device_adam_matches_torch_adam(gpu):
     assert opt._table is not None          # the fused path ran
 
 
+def test_device_adam_load_state_dict_cpu_map_eager_and_graph(gpu, tmp_path):
+    """DeviceAdam.load_state_dict from torch.save + torch.load(map_location='cpu',
+    weights_only=True): the lr stays the group's float64 device tensor (filled
+    with the loaded value), the moments land in the tensors they replace, so
+    both an eager step and a HIP graph captured BEFORE the load continue the
+    saved optimiser bit for bit."""
+    from aido1_amd.optim import DeviceAdam
+    torch.manual_seed(10)
+    src = nn.Sequential(nn.Linear(64, 32), nn.Linear(32, 8)).to(gpu)
+    opt = DeviceAdam(src.parameters(), gpu)
+    for lr in (1e-3, 5e-4):
+        opt.param_groups[0]['lr'].fill_(lr)
+        for p in src.parameters():
+            p.grad = torch.randn_like(p)
+        opt.step()
+    path = tmp_path / 'adam.pt'
+    torch.save(opt.state_dict(), path)
+    net_e, net_g = copy.deepcopy(src), copy.deepcopy(src)
+    grads = [torch.randn_like(p) for p in src.parameters()]
+    for p, g in zip(src.parameters(), grads):
+        p.grad.copy_(g)
+    opt.param_groups[0]['lr'].fill_(2e-4)
+    opt.step()
+    # eager
+    opt_e = DeviceAdam(net_e.parameters(), gpu)
+    lr_e = opt_e.param_groups[0]['lr']
+    opt_e.load_state_dict(torch.load(path, map_location='cpu', weights_only=True))
+    assert opt_e.param_groups[0]['lr'] is lr_e and lr_e.device.type == 'cuda'
+    assert lr_e.dtype == torch.float64 and float(lr_e) == 5e-4
+    lr_e.fill_(2e-4)
+    for p, g in zip(net_e.parameters(), grads):
+        p.grad = g.clone()
+    opt_e.step()
+    assert opt_e._table is not None
+    # graph captured before the load
+    opt_g = DeviceAdam(net_g.parameters(), gpu)
+    lr_g = opt_g.param_groups[0]['lr']
+    for p in net_g.parameters():
+        p.grad = torch.zeros_like(p)
+    opt_g.step()                      # lr 0, zero grads: builds the dt_adam table
+    torch.cuda.synchronize()
+    graph = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(graph):
+        opt_g.step()
+    opt_g.load_state_dict(torch.load(path, map_location='cpu', weights_only=True))
+    assert opt_g.param_groups[0]['lr'] is lr_g and float(lr_g) == 5e-4
+    lr_g.fill_(2e-4)
+    for p, g in zip(net_g.parameters(), grads):
+        p.grad.copy_(g)
+    graph.replay()
+    torch.cuda.synchronize()
+    for a, b, c in zip(src.parameters(), net_e.parameters(), net_g.parameters()):
+        assert torch.equal(a, b) and torch.equal(a, c)
+    for p, q in zip(src.parameters(), net_g.parameters()):
+        assert torch.equal(opt.state[p]['exp_avg'], opt_g.state[q]['exp_avg'])
+        assert float(opt_g.state[q]['step']) == 3.0
+
+
 def test_soft_update_gpu_bit_exact(gpu):
     """dt_soft_update = torch's t * (1 - tau) + p * tau, bit for bit."""
     from aido1_amd.trainer import soft_update
