@@ -159,6 +159,15 @@ class TrainLoop:
             self.check()
         return r, rm, done
 
+    def flush(self):
+        """Join an in-flight update (overlap=True) and apply its refresh."""
+        if self.pending:
+            torch.cuda.current_stream(self.device).wait_stream(self.side)
+            self.pending = False
+            if self.refresh_due:
+                self._refresh()
+                self.refresh_due = False
+
     # ---- episodes -------------------------------------------------------------------
     def poll_episodes(self):
         """Drain this rank's finished episodes and hand them to the episode book
