@@ -65,6 +65,7 @@ METRIC = 'env-steps/sec (whole node) at 4096 envs/GPU; pose/reward max-abs-err v
 HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
 FP64_VECTOR_PEAK_TFLOPS = 78.6   # MI355X spec: fp64 vector = 1/2 of fp32 vector 157.3 TF
 BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16/fp16 MFMA (spec)
+F32_MFMA_PEAK_TFLOPS = 157.3     # MI355X spec: f32 matrix (MFMA) dense
 
 # algorithmic HBM bytes per env-step of config 2 = action 8 +
 # state read 28 + state write 28 + reward 4 + done 1 + dist/angle 8 + tile 4.
@@ -92,6 +93,9 @@ def parse(argv=None):
     p.add_argument('--actor-mode', default='reference', choices=['reference', 'eval'],
                    help="actor/train: 'reference' = train-mode batch-of-one BatchNorm + live "
                         "dropout as the reference's explorers act; 'eval' = BN folded")
+    p.add_argument('--actor-dtype', default='float16', choices=['float16', 'float32'],
+                   help='actor/train: the acting actor\'s arithmetic (float16 = the fast '
+                        'mode; float32 = the reference\'s precision)')
     p.add_argument('--batch-size', type=int, default=0, help='train: 0 = config.json (64)')
     p.add_argument('--buffer-size', type=int, default=131072)
     p.add_argument('--updates-per-step', type=int, default=1)
@@ -128,6 +132,10 @@ def parse(argv=None):
                         'steps (BASELINE.md §3); 0 = skip every CPU baseline')
     p.add_argument('--cpu-decisions', type=int, default=1000,
                    help='config-3 CPU baseline: timed decisions (step + render) per process')
+    p.add_argument('--cpu-actor-decisions', type=int, default=3000,
+                   help='configs 4 / 5 CPU baselines: timed decisions per explorer process')
+    p.add_argument('--cpu-updates', type=int, default=10,
+                   help='config-5 CPU baseline: timed updates of the trainer process')
     p.add_argument('--cpu-procs', type=int, default=0,
                    help='CPU baseline processes (0 = the box CPU share: min(16, affinity))')
     p.add_argument('--dry-run', action='store_true',
@@ -223,6 +231,123 @@ def _cpu_obs_worker(args):
     t0 = time.perf_counter()
     steps = run(decisions)
     return steps, time.perf_counter() - t0
+
+
+def _reference_config():
+    with open(os.path.join(REPO, 'aido1_amd', 'configs', 'reference_config.json')) as f:
+        return json.load(f)
+
+
+def _cpu_actor_worker(args):
+    """configs[3] / [4] on the host, the reference's way: one explorer per
+    process acting on ONE observation at a time (training/explorers.py:164-211,
+    models/ddpg/model.py:74-102: a batch-of-one float32 forward of the
+    train-mode ConfigActor on torch's CPU, one thread), OU noise, the numpy
+    step restatement x repeat 3 with the tanh head's mapping, the C render +
+    line filter and the 3-frame stack.  role 'train': a DDPG trainer process
+    instead (training/trainers.py:143-237 on torch's CPU, batch 64, one
+    thread), `decisions` updates on synthetic batches."""
+    idx, warm, decisions, map_name, role = args
+    import torch
+    torch.set_num_threads(1)
+    from aido1_amd.actor import ConfigActor, ConfigCritic
+    cfg = _reference_config()
+    torch.manual_seed(idx)
+    if role == 'train':
+        from aido1_amd.trainer import DDPGTrainer
+        tr = DDPGTrainer(cfg, ConfigActor(cfg['model']['actor']),
+                         ConfigCritic(cfg['model']['critic']), device='cpu')
+        b = int(cfg['training']['batch_size'])
+        g = torch.Generator().manual_seed(idx)
+        batch = (torch.rand(b, 3, 120, 160, generator=g), torch.rand(b, 2, generator=g),
+                 torch.randn(b, generator=g).double(), torch.rand(b, 3, 120, 160, generator=g),
+                 (torch.rand(b, generator=g) < 0.05))
+        tr.update(batch)
+        t0 = time.perf_counter()
+        for _ in range(decisions):
+            tr.update(batch)
+        return 0, time.perf_counter() - t0, decisions
+    from oracle import dtsim_ref as R
+    from oracle import oracle_c as OC
+    rows = _map_rows(map_name)
+    env = R.EnvironmentWrapperRef(R.SimulatorRef(rows, seed=1234, env_id=idx,
+                                                 cfg=R.SimConfig(action_mode='tanh')))
+    rend = OC.OracleRender(rows)
+    actor = ConfigActor(cfg['model']['actor'])
+    actor.train()                           # the explorers' models are in train mode
+    t = cfg['training']
+    rng = np.random.default_rng(1234 + idx)
+    ou = np.zeros(2)
+    stack = np.zeros((3, 120, 160), np.float32)
+
+    def frame(fresh):
+        p = env.sim.cur_pos
+        g, _, _ = rend.render((p[0],), (p[2],), (env.sim.cur_angle,))
+        if fresh:
+            stack[:] = g[0]
+        else:
+            stack[:2] = stack[1:]
+            stack[2] = g[0]
+
+    env.reset()
+    frame(True)
+
+    def run(k):
+        nonlocal ou
+        steps = 0
+        for _ in range(k):
+            with torch.no_grad():
+                a = actor(torch.from_numpy(stack[None])).numpy()[0]
+            ou = ou + t['rp_theta'] * (t['rp_mu'] - ou) * 1e-2 + \
+                t['rp_sigma'] * np.sqrt(1e-2) * rng.standard_normal(2)
+            a = np.clip(a + 2 * 0.5 * ou, -1.0, 1.0).astype(np.float32)   # tanh head, eps 0.5
+            before = env.sim.step_count
+            _, _, d = env.step(a)
+            steps += env.sim.step_count - before
+            if d:
+                env.reset()
+                ou = np.zeros(2)
+            frame(d)
+        return steps
+    run(warm)
+    t0 = time.perf_counter()
+    steps = run(decisions)
+    return steps, time.perf_counter() - t0, decisions
+
+
+def cpu_actor_baseline(decisions, procs, train=False, updates=3):
+    """configs[3] (train=False) / configs[4] (train=True) on the host cores: P
+    explorer processes of the reference's per-observation act path on the
+    config-4 maps (alternating small_loop / zigzag); with train, one of the P
+    processes is a DDPG trainer instead (the reference's TrainManager runs
+    explorers and trainers as separate processes side by side), timed
+    concurrently.  value = the explorers' env-steps / the slowest explorer."""
+    procs, avail, model = _cpu_info(procs)
+    items = [(i, 3, decisions, ('small_loop', 'zigzag')[i % 2], 'explore')
+             for i in range(procs - (1 if train else 0))]
+    if train:
+        items.append((procs, 0, updates, None, 'train'))
+    res = _cpu_pool(_cpu_actor_worker, items, procs)
+    ex = [r for r, it in zip(res, items) if it[4] == 'explore']
+    total = sum(r[0] for r in ex)
+    wall = max(r[1] for r in ex)
+    out = {'value': total / wall, 'unit': 'env-steps/s', 'cores': procs, 'kind': 'port',
+           'procs': procs, 'host_cores': os.cpu_count(), 'affinity_cores': avail,
+           'deviation': DEVIATION % (procs, os.cpu_count()),
+           'sample': '%d explorer processes x (3 warm-up + %d timed decisions), one env each: '
+                     'per decision a batch-of-one float32 forward of the train-mode ConfigActor '
+                     '(torch CPU, 1 thread; models/ddpg/model.py:74-102), OU noise, '
+                     'oracle/dtsim_ref.py numpy-float64 step x repeat 3 (tanh head mapping), '
+                     'oracle/render_oracle.c render + line filter, 3-frame stack; small_loop / '
+                     'zigzag alternating; %d timed env-steps in %.1f s; host CPU: %s'
+                     % (len(ex), decisions, total, wall, model)}
+    if train:
+        tr = [r for r, it in zip(res, items) if it[4] == 'train'][0]
+        out['trainer'] = {'updates': tr[2], 'seconds': tr[1], 'updates_per_s': tr[2] / tr[1],
+                          'what': 'one process: DDPGTrainer.update (critic + actor + soft '
+                                  'targets) on torch CPU, batch %d, 1 thread, beside the '
+                                  'explorers' % int(_reference_config()['training']['batch_size'])}
+    return out
 
 
 def _cpu_pool(worker, items, procs):
@@ -592,10 +717,14 @@ def bench_obs(args, ctx):
     lane = None if args.no_lane else lane_record(args, ctx, args.lane_steps, args.lane_warmup,
                                                  cpu=True)
     # configs 4 and 5 as sub-records of the same line (not the headline)
-    c4 = c5 = None
+    c4 = c4f = c5 = None
     if not args.no_sub:
-        c4 = actor_record(args, ctx, args.sub_steps, args.sub_warmup, parity=not args.no_parity)
-        c5 = train_record(args, ctx, args.sub_steps, args.sub_warmup, parity=not args.no_parity)
+        c4 = actor_record(args, ctx, args.sub_steps, args.sub_warmup, parity=not args.no_parity,
+                          cpu=True)
+        c4f = actor_record(args, ctx, args.sub_steps, args.sub_warmup,
+                           parity=not args.no_parity, dtype=torch.float32)
+        c5 = train_record(args, ctx, args.sub_steps, args.sub_warmup, parity=not args.no_parity,
+                          cpu=True)
     if rank == 0:
         kms = float(np.mean(rend_ms))
         fresh_per_launch = st['resets'] / K
@@ -655,6 +784,7 @@ def bench_obs(args, ctx):
             'host_enqueue_ms_per_step': t_host / K * 1e3,
             'config2': lane,
             'config4': c4,
+            'config4_f32': c4f,
             'config5': c5,
         }
         line['cpu_baseline'] = (cpu_obs_baseline(args.cpu_decisions, args.cpu_procs, args.map)
@@ -890,20 +1020,49 @@ def step_parity(env, start, actions, out, rank, args, frames=None, m=64):
 
 
 # ---- configs 4 and 5 -----------------------------------------------------------------------
-def actor_record(args, ctx, K, W, parity=True):
+def actor_f64(actor, x):
+    """The actor in float64 on the host (torch CPU): the reference-mode forward
+    (train-mode batch-of-one BatchNorm = per-sample statistics, dropout off),
+    the precision yardstick of configs 4 / 5 (tools/actor_precision.py)."""
+    import torch
+    import torch.nn.functional as F
+    from aido1_amd.actor import apply_head
+    convs, bns, l1, l2 = actor.layers()
+    d = lambda t: t.detach().double().cpu()   # noqa: E731
+    h = x.double().cpu()
+    for c, b in zip(convs, bns):
+        h = F.leaky_relu(F.conv2d(h, d(c.weight), d(c.bias), stride=c.stride))
+        m = h.mean((2, 3), keepdim=True)
+        v = (h - m).square().mean((2, 3), keepdim=True)
+        h = (h - m) / torch.sqrt(v + b.eps) * d(b.weight).view(1, -1, 1, 1) + \
+            d(b.bias).view(1, -1, 1, 1)
+    h = F.leaky_relu(F.linear(h.flatten(1), d(l1.weight), d(l1.bias)))
+    return apply_head(F.linear(h, d(l2.weight), d(l2.bias)), actor.head)
+
+
+# fp16 fast mode: the action bound against the float64 forward (DESIGN §3.6:
+# measured max 6e-3 .. 1.0e-2 over 8192 actions, p99 3.4e-3 .. 3.9e-3; the
+# per-sample BatchNorm of nearly flat channels amplifies fp16 rounding)
+FP16_ACTION_TOL = 1.5e-2
+F32_ACTION_TOL = 1e-4
+
+
+def actor_record(args, ctx, K, W, parity=True, dtype=None, cpu=False):
     """BASELINE configs[3]: 4096 envs/GPU, mixed small_loop/zigzag, actor in the
     loop (the explorers' loop body, training/explorers.py:164-213).  Returns
-    the line (rank 0) or None.  parity: the fp16 HIP chain against the f32 GPU
-    path on the live frame ring, every env, dropout off in both."""
+    the line (rank 0) or None.  dtype: the actor's arithmetic (float16: the
+    hand-written MFMA chain, the fast mode; float32: the reference's
+    precision).  parity: every env's actions against the other-precision GPU
+    path, and 64 envs' against a float64 host forward (actor_f64), dropout off."""
     torch = ctx.torch
     from aido1_amd.actor import FusedActor, flops_per_sample
     from aido1_amd.rollout import ActorRollout
-    with open(os.path.join(REPO, 'aido1_amd', 'configs', 'reference_config.json')) as f:
-        cfg = json.load(f)
+    cfg = _reference_config()
+    dtype = dtype or torch.float16
     dev, rank, n = ctx.dev, ctx.rank, args.envs
     torch.manual_seed(args.seed)
     roll = ActorRollout(cfg, n, maps=('small_loop', 'zigzag'), device=dev.index, seed=args.seed,
-                        env_id_base=rank * n, actor_mode=args.actor_mode)
+                        env_id_base=rank * n, actor_mode=args.actor_mode, dtype=dtype)
     roll.reset()
     for _ in range(W):
         roll.step()
@@ -924,33 +1083,49 @@ def actor_record(args, ctx, K, W, parity=True):
     tot, tmax, per = rank_report(ctx, [st['sim_steps'], st['decisions'], st['resets']], elapsed)
     par = None
     if parity:
-        # the timed actor's weights, dropout off, fp16 chain vs f32 path (MIOpen
-        # convolutions + the per-sample norm, tests/test_gpu_actor.py)
+        other = torch.float32 if dtype == torch.float16 else torch.float16
         drop = roll.actor.p_drop
         roll.actor.p_drop = 0.0
         with torch.no_grad():
-            ref = FusedActor(roll.actor_src, dtype=torch.float32, mode=roll.actor.mode)
-            ref.p_drop = 0.0
+            alt = FusedActor(roll.actor_src, dtype=other, mode=roll.actor.mode)
+            alt.p_drop = 0.0
             got = roll.actor(roll.ring, roll.order()).float()
-            want = ref(roll.stack()).float()
+            want = alt(roll.ring, roll.order()).float()
+            m = 64
+            ref64 = actor_f64(roll.actor_src, roll.stack()[:m])
         roll.actor.p_drop = drop
         d = torch.abs(got - want)
-        par = {'vs': 'f32 GPU path (same weights, live ring, dropout off)', 'envs_checked': n,
-               'max_abs_err': d.max().item(),
-               'p99_abs_err': torch.quantile(d.flatten(), 0.99).item(),
-               'frac_above_1e-2': (d > 1e-2).float().mean().item()}
-        par['ok'] = bool(torch.isfinite(got).all()) and par['max_abs_err'] <= 1e-2
-        par = worst_over_ranks(ctx, par, ['max_abs_err', 'p99_abs_err', 'frac_above_1e-2'])
+        e64 = (got[:m].double().cpu() - ref64).abs()
+        a64 = (want[:m].double().cpu() - ref64).abs()
+        tol = FP16_ACTION_TOL if dtype == torch.float16 else F32_ACTION_TOL
+        par = {'vs': 'float64 host forward (actor_f64, same weights, live frames, dropout off) '
+                     'on %d envs; and the %s GPU path on every env' % (m, other),
+               'tolerance_vs_f64': tol, 'envs_checked': n, 'envs_checked_f64': m,
+               'max_abs_err_vs_f64': e64.max().item(),
+               'other_path_max_abs_err_vs_f64': a64.max().item(),
+               'max_abs_err_vs_other': d.max().item(),
+               'p99_abs_err_vs_other': torch.quantile(d.flatten(), 0.99).item()}
+        par['ok'] = bool(torch.isfinite(got).all()) and par['max_abs_err_vs_f64'] <= tol
+        par = worst_over_ranks(ctx, par, ['max_abs_err_vs_f64', 'max_abs_err_vs_other',
+                                          'p99_abs_err_vs_other'])
     roll.close()
+    base = None
+    if cpu and ctx.world == 1 and args.cpu_steps > 0 and rank == 0:
+        base = cpu_actor_baseline(args.cpu_actor_decisions, args.cpu_procs)
     if rank != 0:
         return None
     tflops = n * flops_per_sample() / (actor_ms * 1e-3) / 1e12
+    name = str(dtype).replace('torch.', '')
+    peak = BF16_DENSE_PEAK_TFLOPS if dtype == torch.float16 else F32_MFMA_PEAK_TFLOPS
     return {
         'metric': METRIC, 'value': tot[0] / tmax, 'unit': 'env-steps/s',
         'n_gpus': ctx.world, 'steps': K, 'warmup': W,
         'ms_per_step': tmax / K * 1e3,
         'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
-        'dtype': 'f64 env / %s actor' % str(roll.actor.dtype).replace('torch.', ''),
+        'dtype': 'f64 env / %s actor' % name,
+        'precision': ('fast mode: fp16 MFMA operands, f32 accumulation (narrower than the '
+                      'reference\'s float32)' if dtype == torch.float16 else
+                      'the reference\'s float32 (models/ddpg/model.py:74-88)'),
         'data': 'synthetic',
         'config': {'workload': 'config4: %d envs/GPU, actor in the loop (ConfigActor, '
                                'config.json), mixed small_loop/zigzag' % n,
@@ -962,23 +1137,29 @@ def actor_record(args, ctx, K, W, parity=True):
                    'elapsed_s': tmax},
         'per_rank': per,
         'parity': par,
-        'roofline': {'bound': 'mfma', 'kernel': 'actor forward (fp16 MFMA convs + linears)',
-                     'achieved': tflops, 'peak': BF16_DENSE_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                     'frac': tflops / BF16_DENSE_PEAK_TFLOPS, 'traffic': None,
+        'roofline': {'bound': 'mfma', 'kernel': ('actor forward (fp16 MFMA convs + linears)'
+                                                 if dtype == torch.float16 else
+                                                 'actor forward (f32: MIOpen convs, '
+                                                 'dt_sample_norm, linears)'),
+                     'achieved': tflops, 'peak': peak, 'unit': 'TFLOP/s',
+                     'frac': tflops / peak, 'traffic': None,
                      'avg_kernel_ms': actor_ms,
                      'timing': 'HIP events around the actor forward of every timed decision',
                      'algorithmic_flops_per_launch': n * flops_per_sample()},
-        'cpu_baseline': None}
+        'cpu_baseline': base}
 
 
 def bench_actor(args, ctx):
-    line = actor_record(args, ctx, args.steps, args.warmup, parity=not args.no_parity)
+    torch = ctx.torch
+    line = actor_record(args, ctx, args.steps, args.warmup, parity=not args.no_parity,
+                        dtype=torch.float32 if args.actor_dtype == 'float32' else torch.float16,
+                        cpu=True)
     if line is not None:
         print(json.dumps(line), flush=True)
     ctx.close()
 
 
-def train_record(args, ctx, K, W, parity=True):
+def train_record(args, ctx, K, W, parity=True, cpu=False):
     """BASELINE configs[4]: full DDPG on every GPU -- actor-in-loop rollout of
     4096 envs, GPU prioritized replay, one update per decision
     (training/trainers.py:143-237), gradients all-reduced over RCCL (world >
@@ -988,13 +1169,13 @@ def train_record(args, ctx, K, W, parity=True):
     torch = ctx.torch
     from aido1_amd.actor import flops_per_sample
     from aido1_amd.train_loop import TrainLoop
-    with open(os.path.join(REPO, 'aido1_amd', 'configs', 'reference_config.json')) as f:
-        cfg = json.load(f)
+    cfg = _reference_config()
     dev, rank, n = ctx.dev, ctx.rank, args.envs
     loop = TrainLoop(cfg, n, device=dev.index, seed=args.seed, env_id_base=rank * n,
                      buffer_size=args.buffer_size, batch_size=args.batch_size or None,
                      updates_per_step=args.updates_per_step, actor_mode=args.actor_mode,
-                     overlap=args.overlap)
+                     overlap=args.overlap,
+                     actor_dtype=torch.float32 if args.actor_dtype == 'float32' else torch.float16)
     loop.reset()
     for _ in range(max(W, 2)):
         loop.step()
@@ -1027,9 +1208,11 @@ def train_record(args, ctx, K, W, parity=True):
     if parity:
         par = {'losses_finite': bool(torch.isfinite(loop.metrics['critic_loss']).item()
                                      and torch.isfinite(loop.metrics['actor_loss']).item())}
+        guard_ok = False
         try:
             rec = loop.check()
             par['guard'] = 'clean: no stage reported NaN / Inf over %d updates' % rec['tick']
+            guard_ok = True
         except Exception as e:  # noqa: BLE001 -- reported in the line
             par['guard'] = str(e)
         if loop.prioritized:
@@ -1042,11 +1225,24 @@ def train_record(args, ctx, K, W, parity=True):
             par['stored'] = len(loop.replay)
         par['critic_loss'] = loop.metrics['critic_loss'].item()
         par['actor_loss'] = loop.metrics['actor_loss'].item()
+        # the finished episodes of the run, gathered over the ranks (explorers.py:134-140)
+        eps = loop.poll_episodes()
+        par['episodes'] = {'finished': int(len(eps['reward'])),
+                           'mean_reward': float(eps['reward'].mean()) if len(eps['reward'])
+                           else None,
+                           'mean_step': float(eps['step'].mean()) if len(eps['step']) else None,
+                           'exploiter_best_reward': loop.book.exploiter.best}
+        par['ok'] = bool(guard_ok and par['losses_finite'] and
+                         par.get('tree_root_vs_leaf_sum_rel', 0.0) <= 1e-9)
     nparams = sum(p.numel() for p in loop.trainer.actor.parameters()) + \
         sum(p.numel() for p in loop.trainer.critic.parameters())
     dtype = str(loop.rollout.actor.dtype).replace('torch.', '')
     batch = loop.batch_size
     loop.rollout.close()
+    base = None
+    if cpu and ctx.world == 1 and args.cpu_steps > 0 and rank == 0:
+        base = cpu_actor_baseline(args.cpu_actor_decisions, args.cpu_procs, train=True,
+                                  updates=args.cpu_updates)
     if rank != 0:
         return None
     tflops = n * flops_per_sample() / (actor_ms * 1e-3) / 1e12
@@ -1085,7 +1281,7 @@ def train_record(args, ctx, K, W, parity=True):
                      'avg_kernel_ms': actor_ms,
                      'timing': 'HIP events around the actor forward of every timed decision',
                      'algorithmic_flops_per_launch': n * flops_per_sample()},
-        'cpu_baseline': None}
+        'cpu_baseline': base}
 
 
 def bench_train(args, ctx):

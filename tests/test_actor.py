@@ -126,3 +126,23 @@ def test_refresh_fragments_match_fragment_builders(mode):
             assert torch.equal(f.bf[i], convs[i].bias.detach())
     else:
         assert torch.allclose(f.bf, torch.stack([b.float() for b in f.b]), rtol=1e-3, atol=1e-3)
+
+
+def test_bench_actor_f64_is_batch_of_one_train_mode():
+    """bench.actor_f64 (configs 4 / 5's precision yardstick) = the reference's
+    act: the train-mode ConfigActor on ONE observation at a time, in float64,
+    dropout off (models/ddpg/model.py:74-88)."""
+    import bench
+    from aido1_amd.actor import ConfigActor
+    from test_trainer import no_dropout
+    cfg = golden('reference_config.json')
+    torch.manual_seed(3)
+    a = ConfigActor(no_dropout(cfg['model']['actor']))
+    x = torch.rand(3, 3, 120, 160)
+    got = bench.actor_f64(a, x)
+    a64 = ConfigActor(no_dropout(cfg['model']['actor']))
+    a64.load_state_dict(a.state_dict())
+    a64.double().train()
+    with torch.no_grad():
+        want = torch.cat([a64(x[i:i + 1].double()) for i in range(3)])
+    torch.testing.assert_close(got, want, rtol=1e-12, atol=1e-12)

@@ -28,23 +28,29 @@ def _no_dropout_cfg():
     return cfg
 
 
-def test_config4_actor_rollout_at_size(gpu):
-    from aido1_amd.actor import ConfigActor
+@pytest.mark.parametrize('wseed', [11, 1234])
+def test_config4_actor_rollout_at_size(gpu, wseed):
+    """The fp16 fast mode and the float32 reference-precision mode against a
+    float64 host forward of the same weights (bench.actor_f64) on live frames,
+    two weight seeds.  Bounds (tools/actor_layer_error.py): the
+    fp16 chain's error is spread over the layers -- conv1's fp16 weights the
+    largest single term -- and amplified by the per-sample BatchNorm of nearly
+    flat channels (conv1 output std down to 3e-5 of a frame): measured max
+    6e-3 .. 1.0e-2 over 8192 actions, p99 3.4e-3 .. 3.9e-3.  So the fast mode
+    is held to p99 <= 5e-3 over every env and max <= 1.5e-2; float32 to 1e-4."""
+    import bench
+    from aido1_amd.actor import ConfigActor, FusedActor
     from aido1_amd.rollout import ActorRollout
     cfg = _no_dropout_cfg()
-    torch.manual_seed(11)
+    torch.manual_seed(wseed)
     actor = ConfigActor(cfg['model']['actor'])
-    ref_actor = ConfigActor(cfg['model']['actor'])
-    ref_actor.load_state_dict(actor.state_dict())
     n = 4096
     roll = ActorRollout(cfg, n, maps=('small_loop', 'zigzag'), device=0, seed=1234, actor=actor,
                         actor_mode='reference')
     assert [e.n for e in roll.envs] == [2048, 2048]
     roll.reset()
-    done_total = 0
     for _ in range(6):
         r, rm, d = roll.step()
-        done_total += int(d.sum())
     torch.cuda.synchronize()
     st = roll.stats()
     assert st['decisions'] == n * 6
@@ -56,38 +62,24 @@ def test_config4_actor_rollout_at_size(gpu):
     assert ((a >= 0.0) & (a <= 1.0)).all()          # tanh head mapped a/2 + 0.5 in place
     for env in roll.envs:
         env.check()
-    # the fp16 HIP conv chain on the live ring vs the fp32 per-sample reference
-    idx = torch.linspace(0, n - 1, 64).long()
-    out = roll.actor(roll.ring, roll.order())[idx].float().cpu()
-    frames = roll.stack()[idx].cpu()
-    ref_actor.train()
-    with torch.no_grad():
-        ref = torch.cat([ref_actor(frames[i:i + 1]) for i in range(64)])
-    err = torch.max(torch.abs(out - ref)).item()
-    print('config4 fp16 actor vs fp32 per-sample CPU reference, 64 envs: max %.3g' % err)
-    assert err < 1e-2, err
-    # every env: against the float32 GPU path (MIOpen convolutions + the
-    # batched per-sample norm, 1e-5 from a float64 restatement,
-    # tests/test_gpu_actor.py), the same weights and live ring
-    from aido1_amd.actor import FusedActor
-    f32 = FusedActor(ref_actor.to(gpu), dtype=torch.float32, mode='reference')
+    f32 = FusedActor(roll.actor_src, dtype=torch.float32, mode='reference')
     f32.p_drop = 0.0
-    full = roll.actor(roll.ring, roll.order()).float()
-    full_ref = f32(roll.stack()).float()
+    with torch.no_grad():
+        full = roll.actor(roll.ring, roll.order()).float()
+        full_ref = f32(roll.ring, roll.order()).float()
+    idx = torch.linspace(0, n - 1, 96).long().to(gpu)
+    ref64 = bench.actor_f64(roll.actor_src, roll.stack()[idx])
+    e16 = (full[idx].double().cpu() - ref64).abs().max().item()
+    e32 = (full_ref[idx].double().cpu() - ref64).abs().max().item()
     diff = torch.abs(full - full_ref)
-    err_all = diff.max().item()
     q = torch.quantile(diff.flatten(), torch.tensor([0.5, 0.99, 0.999], device=gpu)).tolist()
-    frac = (diff > 1e-2).float().mean().item()
-    print('config4 fp16 actor vs f32 GPU path, all %d envs: max %.3g, median %.3g, p99 %.3g, '
-          'p99.9 %.3g, outputs > 1e-2: %.4f' % (n, err_all, q[0], q[1], q[2], frac))
-    # fp16 under per-sample (batch-of-one) BatchNorm: a channel that is
-    # nearly flat over a frame is divided by a tiny standard deviation.  Stored
-    # uncentred, its fp16 rounding (~2^-11 |v|) was amplified by that 1 / std
-    # (max 6.8e-2 over these 4096 live envs in round 3); the kernels now store
-    # each sample's activations centred on its pixel 0 (include/dtactor.h), so
-    # the rounding is of |v - c|, the channel's own spread
-    assert err_all <= 1e-2, err_all
-    assert frac == 0.0, frac
+    print('config4 seed %d: fp16 vs f64 (96 envs) max %.3g; f32 vs f64 max %.3g; fp16 vs f32 '
+          'all %d envs: max %.3g median %.3g p99 %.3g p99.9 %.3g'
+          % (wseed, e16, e32, n, diff.max().item(), q[0], q[1], q[2]))
+    assert e32 <= bench.F32_ACTION_TOL, e32
+    assert e16 <= bench.FP16_ACTION_TOL, e16
+    assert diff.max().item() <= bench.FP16_ACTION_TOL
+    assert q[1] <= 5e-3, q[1]
     roll.close()
 
 
