@@ -150,6 +150,7 @@ def lib():
             'dt_lane_pos': (ctypes.c_int, [vp, vp, vp, vp]),
             'dt_render': (ctypes.c_int, [vp, vp, vp]),
             'dt_copy_pose': (ctypes.c_int, [vp, vp, vp]),
+            'dt_render_order': (ctypes.c_int, [vp, ctypes.POINTER(u32), vp, vp]),
             'dt_default_line_params': (ctypes.c_int, [vp]),
             'dt_set_line_params': (ctypes.c_int, [vp, vp]),
             'dt_line_detect': (ctypes.c_int, [vp, vp, i32, i32, i32, vp, vp, vp]),

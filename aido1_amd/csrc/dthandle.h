@@ -30,6 +30,7 @@ struct dt_handle {
   void* mark_buf = nullptr;   // float4 segments (x0, z0, x1, z1): yellow then white
   int32_t n_yellow = 0, n_white = 0;
   void* render_spill = nullptr;  // per env: listed words past the LDS list (dtrender.hip)
+  void* render_sched = nullptr;  // render_kernel's dispatch order state (dtrender.hip)
   std::string err;
 };
 

@@ -301,6 +301,7 @@ struct RenderArgs {
   int32_t list_cap;  // listed words kept in LDS (<= kListCap)
   LineDev line;
   int32_t n;
+  uint32_t* sched;   // dispatch order state (kSchedHead + cost[n] + perm[2][n]), or null
 };
 
 // ---- fused render kernel ----------------------------------------------------------
@@ -376,6 +377,10 @@ struct RenderLds {
   uint32_t bits_lo, bits_hi;  // colour bits of raster bytes 0-3 / 4-7 (one byte each)
   View view;
   int32_t cnt[kNCnt];
+  int32_t env;          // this workgroup's env (the dispatch order's entry)
+  uint32_t launch;      // the dispatch order state's launch count at entry
+  uint32_t arrival;     // this workgroup's finishing rank in the launch
+  unsigned long long t0;  // shader clock at entry (the env's recorded cost)
   int8_t kind[dt::kMaxLdsTiles];
 };
 static_assert(sizeof(RenderLds) <= 163840 / 4, "four render workgroups per CU");
@@ -998,6 +1003,102 @@ __device__ __forceinline__ void write_outputs(const RenderArgs& a, RenderLds& S,
   }
 }
 
+// ---- dispatch order: longest measured renders first ---------------------------------
+// A launch's time is its drain: once the last workgroups are dispatched (~80 %
+// of the launch) the CUs finish between 0.77 and 1.0 of it,
+// because a frame with many listed words or markings takes up to twice the
+// median.  Greedy dispatch in blockIdx order is list scheduling; with the
+// longest jobs first (LPT) the tail holds only short ones.  Each workgroup
+// records its env's cost (shader cycles from entry to exit), and when 512
+// workgroups of the launch remain, the one finishing then (its CU is idling
+// into the drain anyway) counting-sorts the envs by cost, descending, into the
+// order the NEXT launch dispatches in (the last one of a launch of <= 512
+// workgroups; poses move 3 sim steps a decision, so
+// a frame's cost predicts the next one's; respawned envs' guesses are stale).
+// Block b renders env perm[launch & 1][b]; the order is only a schedule:
+// every env is rendered exactly once a launch and its outputs do not depend
+// on it.  State (per handle, dt_render_init): [0] launches, [1] arrivals,
+// then cost[n] (u32 cycles), perm[2][n] (i32, both the identity at first).
+constexpr int kSchedHead = 16;
+constexpr int kSchedTail = 512;      // workgroups still running when the order is built
+constexpr int kSchedBuckets = 1024;  // cost >> 8 (256-cycle buckets), clamped
+constexpr int kSchedMaxN = (int)(sizeof(((RenderLds*)0)->u) / sizeof(uint16_t));
+
+__device__ __forceinline__ uint32_t* sched_cost(const RenderArgs& a) { return a.sched + kSchedHead; }
+__device__ __forceinline__ int32_t* sched_perm(const RenderArgs& a, uint32_t launch) {
+  return (int32_t*)(a.sched + kSchedHead) + (size_t)a.n * (1 + (launch & 1u));
+}
+
+// the whole workgroup: envs sorted by recorded cost, descending, into the
+// next launch's order (a permutation whatever the costs read: each is read
+// once, its bucket kept in LDS for both passes)
+__device__ __forceinline__ void sched_build(const RenderArgs& a, RenderLds& S, uint32_t launch) {
+  const int tid = threadIdx.x;
+  constexpr int T = kRenderThreads;
+  const int n = a.n;
+  uint32_t* hist = S.img;                       // [kSchedBuckets] (the image is written out)
+  uint16_t* key = (uint16_t*)&S.u;              // [n] bucket of env i
+  const uint32_t* cost = sched_cost(a);
+  for (int i = tid; i < kSchedBuckets; i += T) hist[i] = 0u;
+  __syncthreads();
+  for (int i = tid; i < n; i += T) {
+    const uint32_t c = __hip_atomic_load(const_cast<uint32_t*>(cost + i), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    const uint32_t b = (kSchedBuckets - 1) - min(c >> 8, (uint32_t)(kSchedBuckets - 1));
+    key[i] = (uint16_t)b;                        // ascending bucket = descending cost
+    atomicAdd(&hist[b], 1u);
+  }
+  __syncthreads();
+  if (tid < 64) {   // exclusive scan, one wave: 16 buckets a lane
+    constexpr int P = kSchedBuckets / 64;
+    uint32_t v[P], sum = 0;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      v[k] = hist[P * tid + k];
+      sum += v[k];
+    }
+    uint32_t inc = sum;
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+      const uint32_t t = __shfl_up(inc, d, 64);
+      if (tid >= d) inc += t;
+    }
+    uint32_t base = inc - sum;
+#pragma unroll
+    for (int k = 0; k < P; ++k) {
+      hist[P * tid + k] = base;
+      base += v[k];
+    }
+  }
+  __syncthreads();
+  int32_t* next = sched_perm(a, launch + 1u);
+  for (int i = tid; i < n; i += T) next[atomicAdd(&hist[key[i]], 1u)] = i;
+}
+
+// exit of a workgroup: its cost; the order builder and the launch's last
+// arriver (which advances the launch count and resets the arrivals)
+__device__ __forceinline__ void sched_exit(const RenderArgs& a, RenderLds& S, int e) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long dt = __builtin_amdgcn_s_memtime() - S.t0;
+    __hip_atomic_store(sched_cost(a) + e, dt > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)dt,
+                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the cost lands before the arrival
+    S.arrival = __hip_atomic_fetch_add(a.sched + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  const uint32_t arr = S.arrival;
+  // the builder: the workgroup finishing when kSchedTail remain (the drain);
+  // in a smaller launch the last one, which sees every cost of this launch
+  const uint32_t at = (uint32_t)(a.n > kSchedTail ? a.n - kSchedTail : a.n - 1);
+  if (arr == at && a.n <= kSchedMaxN) sched_build(a, S, S.launch);
+  if (arr == (uint32_t)(a.n - 1) && threadIdx.x == 0) {
+    __hip_atomic_store(a.sched + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(a.sched, S.launch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // One env of render_kernel.
 __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, int e
 #ifdef DTSIM_EARLY_MARKS
@@ -1288,8 +1389,9 @@ render_kernel(RenderArgs a) {
     for (int i = 0; i < kNCnt; ++i) S.cnt[i] = 0;
   }
   for (int i = tid; i < a.width * a.height; i += kRenderThreads) S.kind[i] = a.kind[i];
-  // the camera frame, once per workgroup (wave 1; wave 0 has the palette)
-  const int e = blockIdx.x;
+  // the camera frame, once per workgroup (wave 1; wave 0 has the palette), of
+  // the env the dispatch order gives this block
+  int e = blockIdx.x;
 #ifdef DTSIM_EARLY_MARKS
   float4 mq[4];
   {
@@ -1302,13 +1404,26 @@ render_kernel(RenderArgs a) {
     }
   }
 #endif
-  if (tid == 64) S.view = view_of(a.x[e], a.z[e], a.angle[e], a.cam_fwd);
+  if (tid == 64) {
+    if (a.sched) {
+      const uint32_t launch =
+          __hip_atomic_load(a.sched, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int p = sched_perm(a, launch)[blockIdx.x];
+      e = (unsigned)p < (unsigned)a.n ? p : (int)blockIdx.x;   // (always a permutation)
+      S.launch = launch;
+    }
+    S.env = e;
+    S.t0 = __builtin_amdgcn_s_memtime();
+    S.view = view_of(a.x[e], a.z[e], a.angle[e], a.cam_fwd);
+  }
   __syncthreads();
+  e = __builtin_amdgcn_readfirstlane(S.env);   // uniform: kept in an SGPR, as blockIdx was
   render_env(a, S, e
 #ifdef DTSIM_EARLY_MARKS
              , mq
 #endif
   );
+  if (a.sched) sched_exit(a, S, e);
 }
 
 // LineDetectorHSV on caller BGR images (one workgroup per image, <= 19200 px).
@@ -1656,6 +1771,16 @@ int dt_render_init(dt_handle* h, const dt_map* map) {
     h->err = "hipMalloc(render spill) failed";
     return DT_E_HIP;
   }
+  // dispatch order state (render_kernel: longest measured renders first)
+  std::vector<uint32_t> sch((size_t)kSchedHead + 3 * (size_t)h->n, 0u);
+  for (int k = 0; k < 2; ++k)
+    for (int i = 0; i < h->n; ++i) sch[kSchedHead + (size_t)h->n * (1 + k) + i] = (uint32_t)i;
+  if (hipMalloc(&h->render_sched, sch.size() * sizeof(uint32_t)) != hipSuccess ||
+      hipMemcpy(h->render_sched, sch.data(), sch.size() * sizeof(uint32_t),
+                hipMemcpyHostToDevice) != hipSuccess) {
+    h->err = "render dispatch order state: hipMalloc / hipMemcpy failed";
+    return DT_E_HIP;
+  }
   return DT_OK;
 }
 
@@ -1664,6 +1789,8 @@ void dt_render_free(dt_handle* h) {
   h->mark_buf = nullptr;
   if (h->render_spill) (void)hipFree(h->render_spill);
   h->render_spill = nullptr;
+  if (h->render_sched) (void)hipFree(h->render_sched);
+  h->render_sched = nullptr;
 }
 
 extern "C" {
@@ -1737,6 +1864,9 @@ int dt_render(dt_handle* h, const dt_render_io* io, void* stream) {
   a.line = h->line;
   a.n = h->n;
   a.spill = (uint16_t*)h->render_spill;
+#ifndef DTSIM_NO_SCHED   // diagnostic builds only (A/B of the dispatch order)
+  a.sched = (uint32_t*)h->render_sched;
+#endif
   a.list_cap = io->list_cap > 0 && io->list_cap < kListCap ? io->list_cap : kListCap;
   hipLaunchKernelGGL(render_kernel, dim3(h->n), dim3(kRenderThreads), 0, (hipStream_t)stream, a);
   const hipError_t e = hipGetLastError();
@@ -1744,6 +1874,23 @@ int dt_render(dt_handle* h, const dt_render_io* io, void* stream) {
     h->err = std::string("dt_render launch: ") + hipGetErrorString(e);
     return DT_E_HIP;
   }
+  return DT_OK;
+}
+
+int dt_render_order(dt_handle* h, uint32_t* launches, uint32_t* cost, int32_t* order) {
+  if (!h || !h->render_sched) return DT_E_ARG;
+  DevGuard dg(h->device);
+  HIP_OR_FAIL(h, hipDeviceSynchronize());
+  uint32_t head[kSchedHead];
+  const uint32_t* base = (const uint32_t*)h->render_sched;
+  HIP_OR_FAIL(h, hipMemcpy(head, base, sizeof(head), hipMemcpyDeviceToHost));
+  if (launches) *launches = head[0];
+  const size_t n = (size_t)h->n;
+  if (cost)
+    HIP_OR_FAIL(h, hipMemcpy(cost, base + kSchedHead, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
+  if (order)
+    HIP_OR_FAIL(h, hipMemcpy(order, base + kSchedHead + n * (1 + (head[0] & 1u)),
+                             n * sizeof(int32_t), hipMemcpyDeviceToHost));
   return DT_OK;
 }
 

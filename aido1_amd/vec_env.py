@@ -284,6 +284,18 @@ class VecEnv:
         self._check(self._L.dt_copy_pose(self._h, _ptr(pose), self._stream()), 'dt_copy_pose')
         return pose
 
+    def render_order(self):
+        """(launches, cost [n] u32 shader cycles, order [n] i32): dt_render's
+        dispatch order state (diagnostics; synchronises)."""
+        launches = ctypes.c_uint32(0)
+        cost = np.zeros(self.n, np.uint32)
+        order = np.zeros(self.n, np.int32)
+        self._check(self._L.dt_render_order(self._h, ctypes.byref(launches),
+                                            cost.ctypes.data_as(ctypes.c_void_p),
+                                            order.ctypes.data_as(ctypes.c_void_p)),
+                    'dt_render_order')
+        return launches.value, cost, order
+
     def set_line_params(self, params):
         self._check(self._L.dt_set_line_params(self._h, ctypes.byref(params)),
                     'dt_set_line_params')

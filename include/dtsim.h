@@ -47,7 +47,7 @@ extern "C" {
                                 dtupd.h (the update's convolutions and the
                                 conv trunk's BatchNorm hand-off);
                              9: dtactor.h dt_episode_account (episode sums and
-                                the finished-episode ring) */
+                                the finished-episode ring); dt_render_order */
 
 /* error codes */
 #define DT_OK 0
@@ -273,8 +273,15 @@ typedef struct dt_render_io {
  * (utils/reward_shaping/env_utils.py:48-51) and LineDetectorHSV.setImage +
  * _colorFilter (features/line_detector1.py:134-141, :36-57): HSV inRange,
  * ellipse dilation, Canny(bgr, lo, hi, 3).  Renders the CURRENT pose (call it
- * after dt_step), or io->pose. */
+ * after dt_step), or io->pose.  The envs are dispatched longest measured
+ * render first (each launch records every env's cost and orders the next
+ * launch's workgroups by it); the order never changes an output. */
 int dt_render(dt_handle* h, const dt_render_io* io, void* stream);
+
+/* Diagnostics of that dispatch order (synchronises): launches so far, each
+ * env's last recorded cost (shader cycles) and the order the next launch
+ * dispatches in (a permutation of 0..n-1).  cost / order: host [n] or NULL. */
+int dt_render_order(dt_handle* h, uint32_t* launches, uint32_t* cost, int32_t* order);
 
 /* Enqueue a copy of every env's current pose into pose (device [3, n] f64:
  * x, z, angle planes) on `stream`: the render of decision d can then read the

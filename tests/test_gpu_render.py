@@ -166,3 +166,38 @@ def test_render_pose_snapshot(gpu):
     g, m, _ = OC.OracleRender(map_rows('loop_empty')).render(x, z, a)
     assert np.array_equal(out.masks.cpu().numpy(), m)
     assert np.array_equal(out.ring[:, 0].cpu().numpy(), g)
+
+
+def test_render_dispatch_order(gpu):
+    """dt_render dispatches the envs longest recorded render first: after each
+    launch the next order is a permutation of the envs sorted by the recorded
+    costs (descending, 256-cycle buckets), and over launches in that order the
+    outputs stay the oracle's bit for bit (n = 4096: the order is built while
+    512 workgroups still run, so late envs' costs may be the previous
+    launch's; n = 100: by the last one, from this launch's costs)."""
+    from aido1_amd.render import RenderOutput
+    from aido1_amd.vec_env import VecEnv
+    orend = OC.OracleRender(map_rows('loop_empty'))
+    for n in (4096, 100):
+        env = VecEnv(n, seed=9)
+        env.reset()
+        out = RenderOutput(n, gpu, slots=1)
+        rng = np.random.default_rng(n)
+        l0, _, order0 = env.render_order()
+        assert l0 == 0 and np.array_equal(order0, np.arange(n))
+        for k in range(4):
+            x, z, a = poses(n, rng)
+            env.set_state(x=x, z=z, angle=a)
+            env.render_into(out)
+            launches, cost, order = env.render_order()
+            assert launches == k + 1
+            assert np.array_equal(np.sort(order), np.arange(n))          # a permutation
+            assert (cost > 0).all()
+            b = np.minimum(cost[order] >> 8, 1023)
+            if n <= 512:        # built after every workgroup's cost of this launch
+                assert (np.diff(b.astype(np.int64)) <= 0).all()
+            g, m, _ = orend.render(x, z, a)
+            assert np.array_equal(out.masks.cpu().numpy(), m)
+            assert np.array_equal(out.ring[:, 0].cpu().numpy(), g)
+        if n > 512:   # the later launches really ran in another order
+            assert not np.array_equal(order, np.arange(n))
