@@ -18,9 +18,9 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_PATH = os.path.join(PKG_DIR, 'libdtsim.so')
 CSRC = os.path.join(PKG_DIR, 'csrc')
 SOURCES = ['dtsim.hip', 'dtrender.hip', 'dtreplay.hip', 'dtactor.hip', 'dtconv.hip',
-           'dttrain.hip', 'dtupd.hip']
+           'dttrain.hip', 'dtupd.hip', 'dthead.hip']
 HEADERS = ['dtsim_common.h', 'dtrender.h', 'dtsync.h']
-PUBLIC_HEADERS = ['dtsim.h', 'dtreplay.h', 'dtactor.h', 'dttrain.h', 'dtupd.h']
+PUBLIC_HEADERS = ['dtsim.h', 'dtreplay.h', 'dtactor.h', 'dttrain.h', 'dtupd.h', 'dthead.h']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
 ABI_VERSION = 9
 
@@ -63,6 +63,12 @@ class DtEpisodeState(ctypes.Structure):
                 ('tick', ctypes.c_void_p), ('episode', ctypes.c_void_p),
                 ('decisions', ctypes.c_void_p), ('count', ctypes.c_void_p),
                 ('ring', ctypes.c_void_p), ('capacity', ctypes.c_int64)]
+
+
+class DtMlp(ctypes.Structure):
+    """include/dthead.h DtMlp: a small fully connected tail."""
+    _fields_ = [(k, ctypes.c_int32) for k in ('m', 'k0', 'k1', 'n1', 'n2', 'act1', 'act2')] + \
+        [('slope', ctypes.c_float)] + [(k, ctypes.c_void_p) for k in ('w1', 'b1', 'w2', 'b2')]
 
 
 class DtExploreParams(ctypes.Structure):
@@ -216,6 +222,10 @@ def lib():
             'dt_upd_linear_wgrad': (ctypes.c_int, [i32, i32, i32, vp, vp, vp, ctypes.c_float, vp,
                                                    vp, vp]),
             'dt_soft_update': (ctypes.c_int, [i32, vp, vp, f64, vp]),
+            # dthead.h
+            'dt_mlp_fwd': (ctypes.c_int, [ctypes.POINTER(DtMlp), vp, vp, vp, vp, vp]),
+            'dt_mlp_bwd': (ctypes.c_int, [ctypes.POINTER(DtMlp), vp, vp, vp, vp, vp, vp, vp, vp,
+                                          vp, vp, vp, vp]),
             # dtactor.h
             'dt_sample_norm': (ctypes.c_int, [vp, vp, i32, i32, i32, vp, vp, ctypes.c_float,
                                               ctypes.c_float, i32, vp]),

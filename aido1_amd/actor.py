@@ -162,7 +162,20 @@ class _Net(nn.Module):       # Net: input_nets / output_nets (modules.py:86-109)
         self.output_nets = nn.ModuleList(outputs)
 
     def forward(self, *inputs):
-        x = torch.cat([net(v) for net, v in zip(self.input_nets, inputs)], dim=1)
+        return self.out([net(v) for net, v in zip(self.input_nets, inputs)])
+
+    def out(self, parts):
+        """The output branches on the concatenated input branches.  On the GPU
+        in float32 a single small output branch (linear [-> act] [-> linear
+        [-> act]]) runs as one dt_mlp_fwd launch reading the parts in place
+        (train_ops.mlp, include/dthead.h) instead of torch.cat + two library
+        GEMMs + activations."""
+        if len(self.output_nets) == 1 and self.output_nets[0].fused_tail and parts[0].is_cuda:
+            from aido1_amd import train_ops
+            plan = train_ops.mlp_plan(self.output_nets[0], parts)
+            if plan is not None:
+                return [train_ops.mlp(parts, plan)]
+        x = torch.cat(parts, dim=1)
         return [net(x) for net in self.output_nets]
 
 
@@ -273,8 +286,7 @@ class ConfigCritic(ConfigNet):
     def head(self, t, *rest):
         seq = self.net.input_nets[0]
         x0 = seq.run(t, self._cut(), len(seq.internal_modules))
-        x = torch.cat([x0] + [net(v) for net, v in zip(self.net.input_nets[1:], rest)], dim=1)
-        return self.net.output_nets[0](x)
+        return self.net.out([x0] + [net(v) for net, v in zip(self.net.input_nets[1:], rest)])[0]
 
 
 def apply_head(x, head, max_action=1.0):

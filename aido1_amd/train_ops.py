@@ -20,6 +20,13 @@ The activation leaky(z + bias) is never stored: every kernel recomputes it
 from the convolution output z.  The modules, parameters and state_dict are
 the unchanged torch ones; ``applicable`` / ``trunk_len`` /
 ``linear_applicable`` say when the kernels replace them.
+
+Streams: every BatchNorm module owns its kernels' scratch (the partials and
+work buffers, ``_dt_part`` / ``_dt_work``), so ONE module must not be
+forwarded on two streams at once.  The trainer's two-stream stages
+(trainer._fork) forward different modules on each branch;
+tests/test_gpu_trainer.py checks them against the one-stream order bit for
+bit, eager and captured.
 """
 import contextlib
 import ctypes
@@ -534,3 +541,116 @@ def linear(x, lin, slope=None):
     """lin(x), then LeakyReLU(slope) if slope is not None, on the dtupd.h
     kernels (linear_applicable)."""
     return _UpdLinear.apply(x, lin.weight, lin.bias, slope)
+
+
+# ---- the small fully connected tails after the trunk's linear (include/dthead.h) --------
+MLP_ACT = {'none': 0, 'leaky': 1, 'tanh': 2, 'sigmoid': 3}
+
+
+def _act_code(m):
+    if m is None:
+        return 0, None
+    if isinstance(m, nn.LeakyReLU):
+        return (1, float(m.negative_slope)) if m.negative_slope >= 0 else (None, None)
+    if isinstance(m, nn.Tanh):
+        return 2, None
+    if isinstance(m, nn.Sigmoid):
+        return 3, None
+    return None, None
+
+
+def mlp_plan(seq, parts):
+    """(w1, b1, act1, w2, b2, act2, slope) when the output branch `seq`
+    (config.json's output MetaNet: linear [-> act] [-> linear [-> act]]) on the
+    concatenation of `parts` fits dt_mlp_fwd; None otherwise (torch runs it)."""
+    mods = list(seq.internal_modules)
+    if not mods or not all(p.is_cuda and p.dtype == torch.float32 and p.dim() == 2 for p in parts):
+        return None
+    if len(parts) not in (1, 2) or any(p.shape[0] != parts[0].shape[0] for p in parts):
+        return None
+    lins, acts, i = [], [], 0
+    while i < len(mods):
+        lin = getattr(mods[i], 'linear', None)
+        if lin is None or len(lins) == 2:
+            return None
+        act = mods[i + 1] if i + 1 < len(mods) and getattr(mods[i + 1], 'linear', None) is None \
+            else None
+        code, slope = _act_code(act)
+        if code is None:
+            return None
+        lins.append(lin)
+        acts.append((code, slope))
+        i += 2 if act is not None else 1
+    slopes = {s for _, s in acts if s is not None}
+    if len(slopes) > 1:
+        return None
+    m, k = parts[0].shape[0], sum(p.shape[1] for p in parts)
+    n1 = lins[0].out_features
+    n2 = lins[1].out_features if len(lins) == 2 else 0
+    if (lins[0].in_features != k or (n2 and lins[1].in_features != n1) or m > 256 or k > 1024
+            or n1 > (512 if n2 else 1024) or n2 > 64 or m * n1 > 8192 or m * n2 > 2048
+            or any(l.weight.dtype != torch.float32 or not l.weight.is_cuda for l in lins)):
+        return None
+    slope = slopes.pop() if slopes else 0.0
+    w2, b2 = (lins[1].weight, lins[1].bias) if n2 else (None, None)
+    return (lins[0].weight, lins[0].bias, acts[0][0], w2, b2, acts[1][0] if n2 else 0, slope)
+
+
+def _mlp_struct(x0, x1, w1, b1, w2, b2, act1, act2, slope):
+    ptr = (lambda t: t.data_ptr() if t is not None else None)
+    return _lib.DtMlp(x0.shape[0], x0.shape[1], x1.shape[1] if x1 is not None else 0,
+                      w1.shape[0], w2.shape[0] if w2 is not None else 0, act1, act2, slope,
+                      w1.data_ptr(), ptr(b1), ptr(w2), ptr(b2))
+
+
+class _Mlp(torch.autograd.Function):
+    """The output branch on [x0 | x1] in one dt_mlp_fwd launch; backward in one
+    dt_mlp_bwd launch (only the gradients autograd asks for)."""
+
+    @staticmethod
+    def forward(ctx, x0, x1, w1, b1, w2, b2, meta):
+        act1, act2, slope = meta
+        x0 = x0.contiguous()
+        x1 = x1.contiguous() if x1 is not None else None
+        w1 = w1.contiguous()
+        w2 = w2.contiguous() if w2 is not None else None
+        p = _mlp_struct(x0, x1, w1, b1, w2, b2, act1, act2, slope)
+        h = torch.empty(p.m, p.n1, device=x0.device)
+        y = torch.empty(p.m, p.n2, device=x0.device) if p.n2 else None
+        rc = _lib.lib().dt_mlp_fwd(ctypes.byref(p), x0.data_ptr(),
+                                   x1.data_ptr() if x1 is not None else None, h.data_ptr(),
+                                   y.data_ptr() if y is not None else None,
+                                   torch.cuda.current_stream(x0.device).cuda_stream)
+        if rc != 0:
+            raise _lib.DtError('dt_mlp_fwd failed (%d)' % rc)
+        ctx.meta = meta
+        ctx.has = (x1 is not None, b1 is not None, w2 is not None, b2 is not None)
+        ctx.save_for_backward(x0, x1, w1, b1, w2, b2, h, y)
+        return y if y is not None else h
+
+    @staticmethod
+    def backward(ctx, dy):
+        x0, x1, w1, b1, w2, b2, h, y = ctx.saved_tensors
+        act1, act2, slope = ctx.meta
+        need = ctx.needs_input_grad
+        dy = dy.contiguous()
+        new = (lambda t, want: torch.empty_like(t) if (want and t is not None) else None)
+        dx0, dx1 = new(x0, need[0]), new(x1, need[1])
+        dw1, db1 = new(w1, need[2]), new(b1, need[3])
+        dw2, db2 = new(w2, need[4]), new(b2, need[5])
+        p = _mlp_struct(x0, x1, w1, b1, w2, b2, act1, act2, slope)
+        ptr = (lambda t: t.data_ptr() if t is not None else None)
+        rc = _lib.lib().dt_mlp_bwd(ctypes.byref(p), x0.data_ptr(), ptr(x1), h.data_ptr(), ptr(y),
+                                   dy.data_ptr(), ptr(dx0), ptr(dx1), ptr(dw1), ptr(db1),
+                                   ptr(dw2), ptr(db2),
+                                   torch.cuda.current_stream(dy.device).cuda_stream)
+        if rc != 0:
+            raise _lib.DtError('dt_mlp_bwd failed (%d)' % rc)
+        return dx0, dx1, dw1, db1, dw2, db2, None
+
+
+def mlp(parts, plan):
+    """The output branch of mlp_plan on `parts` (1 or 2 [m, k] tensors)."""
+    w1, b1, act1, w2, b2, act2, slope = plan
+    x1 = parts[1] if len(parts) == 2 else None
+    return _Mlp.apply(parts[0], x1, w1, b1, w2, b2, (act1, act2, slope))

@@ -230,3 +230,86 @@ def test_shared_critic_trunk_equals_two_forwards(gpu):
     with pytest.raises(NotImplementedError):   # the torch BatchNorm path cannot repeat
         with running_updates(b.cpu().double(), 2):
             b.trunk(obs.cpu().double())
+
+
+@pytest.mark.parametrize('slope', [0.01, -0.2])
+def test_linear_leaky_fusion_only_for_nonnegative_slope(gpu, slope):
+    """_Seq fuses linear -> LeakyReLU into the split-K kernel (its backward
+    takes the gradient from the sign of the saved output) only for a slope
+    >= 0; a negative slope runs the unfused linear and torch's leaky_relu.
+    Either way: output and gradients as torch's modules (float32 tolerance)."""
+    from aido1_amd.actor import _Lin, _Seq
+    torch.manual_seed(12)
+    seq = _Seq([_Lin(1024, 64), nn.LeakyReLU(slope)]).to(gpu)
+    ref = copy.deepcopy(seq)
+    ref.fused_tail = False
+    x = torch.randn(8, 1024, device=gpu, requires_grad=True)
+    xr = x.detach().clone().requires_grad_(True)
+    y, yr = seq(x), ref(xr)
+    g = torch.randn_like(y)
+    y.backward(g)
+    yr.backward(g)
+    torch.testing.assert_close(y, yr, rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(x.grad, xr.grad, rtol=1e-5, atol=1e-5)
+    for p, q in zip(seq.parameters(), ref.parameters()):
+        torch.testing.assert_close(p.grad, q.grad, rtol=1e-4, atol=1e-5)
+
+
+@pytest.mark.parametrize('m,k0,k1,n1,n2,acts', [
+    (64, 256, 2, 128, 1, ('leaky', 'none')),      # config.json's critic tail
+    (64, 512, 0, 2, 0, ('tanh', None)),           # config.json's actor tail
+    (1, 40, 3, 17, 5, ('sigmoid', 'tanh')),
+    (37, 1024, 0, 64, 2, ('leaky', 'sigmoid')),
+    (256, 8, 8, 32, 0, ('none', None))])
+def test_mlp_tail_matches_float64(gpu, m, k0, k1, n1, n2, acts):
+    """dt_mlp_fwd / dt_mlp_bwd (include/dthead.h) through train_ops.mlp against
+    float64 torch: the output and every input / parameter gradient, also with
+    only some gradients asked for."""
+    from aido1_amd import train_ops
+    torch.manual_seed(m + k0 + n1)
+    mods = [nn.Linear(k0 + k1, n1)]
+    act = {'leaky': nn.LeakyReLU(0.01), 'tanh': nn.Tanh(), 'sigmoid': nn.Sigmoid(), 'none': None}
+    if act[acts[0]] is not None:
+        mods.append(act[acts[0]])
+    if n2:
+        mods.append(nn.Linear(n1, n2))
+        if act[acts[1]] is not None:
+            mods.append(act[acts[1]])
+
+    class _L(nn.Module):   # the config MetaNet's '.linear' wrapper
+        def __init__(self, lin):
+            super().__init__()
+            self.linear = lin
+
+    class _S(nn.Module):
+        def __init__(self, ms):
+            super().__init__()
+            self.internal_modules = nn.ModuleList(
+                [_L(x) if isinstance(x, nn.Linear) else x for x in ms])
+
+    seq = _S(mods).to(gpu)
+    x0 = torch.randn(m, k0, device=gpu, requires_grad=True)
+    x1 = torch.randn(m, k1, device=gpu, requires_grad=True) if k1 else None
+    parts = [x0] + ([x1] if k1 else [])
+    plan = train_ops.mlp_plan(seq, parts)
+    assert plan is not None
+    y = train_ops.mlp(parts, plan)
+    ref = copy.deepcopy(nn.Sequential(*mods)).double()
+    x64 = torch.cat([p.detach().double() for p in parts], 1).requires_grad_(True)
+    y64 = ref(x64)
+    torch.testing.assert_close(y.double(), y64, rtol=1e-5, atol=1e-6)
+    g = torch.randn_like(y)
+    y.backward(g)
+    y64.backward(g.double())
+    gx = torch.cat([p.grad for p in parts], 1)
+    torch.testing.assert_close(gx.double(), x64.grad, rtol=1e-5, atol=1e-6)
+    for a, b in zip([x for x in seq.parameters()], ref.parameters()):
+        torch.testing.assert_close(a.grad.double(), b.grad, rtol=1e-5, atol=1e-5)
+    # only the first input's gradient
+    for p in seq.parameters():
+        p.grad = None
+        p.requires_grad_(False)
+    x0.grad = None
+    y2 = train_ops.mlp(parts, train_ops.mlp_plan(seq, parts))
+    (gx0,) = torch.autograd.grad(y2, [x0], g)
+    torch.testing.assert_close(gx0, gx[:, :k0], rtol=1e-6, atol=1e-7)

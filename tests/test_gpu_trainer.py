@@ -77,3 +77,34 @@ def test_train_loop_runs(gpu, prioritized, graph, size):
         _, _, mp = loop.replay.trees()
         assert mp.item() >= 1.0
     assert loop.rollout.stats()['decisions'] == 128 * 12
+
+
+@pytest.mark.parametrize('graph', [False, True])
+def test_two_stream_stages_equal_one_stream(gpu, graph):
+    """The update's side-stream branches (trainer._fork: the targets' forward
+    beside the critic's, the stepped critic's trunk beside the actor's
+    forward, the TD forward beside the actor step and soft updates) against
+    the same update with every stage on one stream: losses, TD errors and
+    every state_dict entry (weights, BatchNorm running statistics) bit for
+    bit over three updates, eager and captured as HIP graphs (two graph
+    branches vs a chain).  Holds because no BatchNorm module is forwarded on
+    both branches (its kernels' scratch is per module, train_ops)."""
+    torch.backends.cudnn.allow_tf32 = False
+    two = make_trainer(gpu, graph=graph, warmup=1)
+    one = make_trainer(gpu, graph=graph, warmup=1)
+    one._fork = lambda: None
+    batch = formula_batch(16)
+    for _ in range(3):
+        m2, i2 = two.update(batch)
+        m1, i1 = one.update(batch)
+        torch.cuda.synchronize()
+        for k in ('critic_loss', 'actor_loss'):
+            assert torch.equal(m1[k], m2[k]), k
+        assert torch.equal(i1['td_error'], i2['td_error'])
+    for a, b in ((two.actor, one.actor), (two.critic, one.critic),
+                 (two.target_actor, one.target_actor), (two.target_critic, one.target_critic)):
+        sa, sb = a.state_dict(), b.state_dict()
+        for k in sa:
+            assert torch.equal(sa[k], sb[k]), k
+    if graph:
+        assert two._graphs is not None and one._graphs is not None
