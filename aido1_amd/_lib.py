@@ -185,6 +185,8 @@ def lib():
             'dt_per_read': (ctypes.c_int, [vp, vp, vp, vp, vp]),
             'dt_per_check': (ctypes.c_int, [vp]),
             'dt_frame_add': (ctypes.c_int, [i32, i64, vp, i64, vp, i32, vp, vp, i32, vp, vp, vp]),
+            'dt_frame_gather': (ctypes.c_int, [i32, vp, vp, i64, i32, vp, vp, vp, vp, vp, vp, vp,
+                                               vp, vp, vp, vp]),
             # dttrain.h
             'dt_train_work_floats': (i64, [i64]),
             'dt_bn_leaky_fwd': (ctypes.c_int, [i64, vp, vp, ctypes.c_float, vp, vp, ctypes.c_float,

@@ -213,6 +213,31 @@ sample_kernel(const double* sum, const double* mn, int64_t cap, int64_t len, int
 // marks a respawned env (the renderer refilled every slot of its stack).
 constexpr int kFrameThreads = 256;
 
+// dt_frame_gather: block (x, b) covers pixels [x * threads, ...) of sample b;
+// a thread reads its pixel from the k frames of obs and of next_obs (each
+// plane read coalesced) and writes the k-float NHWC pixel of each
+__global__ void __launch_bounds__(kFrameThreads)
+frame_gather_kernel(const int64_t* __restrict__ idx, const float* __restrict__ frames, int64_t hw,
+                    int k, const int32_t* __restrict__ obs_ptr,
+                    const int32_t* __restrict__ next_ptr, const float* __restrict__ action,
+                    const double* __restrict__ reward, const uint8_t* __restrict__ done,
+                    float* __restrict__ obs, float* __restrict__ nxt, float* __restrict__ act,
+                    float* __restrict__ rew, float* __restrict__ notdone) {
+  const int b = blockIdx.y;
+  const int64_t i = idx[b];
+  const int64_t px = (int64_t)blockIdx.x * kFrameThreads + threadIdx.x;
+  if (blockIdx.x == 0 && threadIdx.x < 2) act[2 * b + threadIdx.x] = action[2 * i + threadIdx.x];
+  if (blockIdx.x == 0 && threadIdx.x == 2) rew[b] = (float)reward[i];
+  if (blockIdx.x == 0 && threadIdx.x == 3) notdone[b] = done[i] ? 0.0f : 1.0f;
+  if (px >= hw) return;
+  float* o = obs + ((int64_t)b * hw + px) * k;
+  float* q = nxt + ((int64_t)b * hw + px) * k;
+  for (int c = 0; c < k; ++c) {
+    o[c] = frames[(int64_t)obs_ptr[i * k + c] * hw + px];
+    q[c] = frames[(int64_t)next_ptr[i * k + c] * hw + px];
+  }
+}
+
 __global__ void __launch_bounds__(kFrameThreads)
 frame_add_kernel(int64_t frame4, const float4* __restrict__ src, int64_t src_stride4,
                  float4* __restrict__ dst, int k, int32_t* __restrict__ stack,
@@ -379,6 +404,23 @@ int dt_frame_add(int32_t n, int64_t frame_elems, const float* src, int64_t src_e
   frame_add_kernel<<<n, kFrameThreads, 0, (hipStream_t)stream>>>(
       frame_elems / 4, reinterpret_cast<const float4*>(src), src_env_stride / 4,
       reinterpret_cast<float4*>(dst), k, stack, done, base_row, obs_ptr, next_ptr);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
+int dt_frame_gather(int32_t batch, const int64_t* idx, const float* frames, int64_t hw,
+                    int32_t k, const int32_t* obs_ptr, const int32_t* next_ptr,
+                    const float* action, const double* reward, const uint8_t* done, float* obs,
+                    float* nxt, float* act, float* rew, float* notdone, void* stream) {
+  if (batch < 0 || hw < 1 || k < 1 || k > 4) return DT_E_ARG;
+  if (batch == 0) return DT_OK;
+  if (!idx || !frames || !obs_ptr || !next_ptr || !action || !reward || !done || !obs || !nxt ||
+      !act || !rew || !notdone)
+    return DT_E_ARG;
+  const int64_t per = (hw + kFrameThreads - 1) / kFrameThreads;
+  if (per > 65535) return DT_E_ARG;
+  frame_gather_kernel<<<dim3((unsigned)per, (unsigned)batch), kFrameThreads, 0,
+                        (hipStream_t)stream>>>(idx, frames, hw, k, obs_ptr, next_ptr, action,
+                                               reward, done, obs, nxt, act, rew, notdone);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 

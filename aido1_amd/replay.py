@@ -264,6 +264,38 @@ class ReplayBuffer:
                     st['done'].index_select(0, idxes))
         return tuple(st[name].index_select(0, idxes) for name in FIELDS)
 
+    def gather_into(self, idxes, out):
+        """_encode_sample(idxes) written straight into a trainer's inputs `out`
+        (DDPGTrainer.static_inputs: obs / nxt float32 channels_last [b, k, h, w],
+        act [b, 2], rew [b, 1], notdone [b, 1]): one dt_frame_gather launch with
+        the frame store on the GPU (include/dtreplay.h), torch copies otherwise."""
+        st = self.storage
+        b = idxes.shape[0]
+        if (self.frames is not None and self.frames.is_cuda and out['obs'].dtype == torch.float32
+                and out['obs'].is_contiguous(memory_format=torch.channels_last)
+                and out['nxt'].is_contiguous(memory_format=torch.channels_last)
+                and st['action'].dtype == torch.float32 and st['reward'].dtype == torch.float64
+                and st['done'].dtype == torch.bool and idxes.dtype == torch.int64):
+            k = st['obs_ptr'].shape[1]
+            hw = self.frames[0].numel()
+            idxes = idxes.contiguous()
+            rc = _lib.lib().dt_frame_gather(
+                b, idxes.data_ptr(), self.frames.data_ptr(), hw, k, st['obs_ptr'].data_ptr(),
+                st['next_ptr'].data_ptr(), st['action'].data_ptr(), st['reward'].data_ptr(),
+                st['done'].data_ptr(), out['obs'].data_ptr(), out['nxt'].data_ptr(),
+                out['act'].data_ptr(), out['rew'].data_ptr(), out['notdone'].data_ptr(),
+                ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream))
+            if rc != 0:
+                raise _lib.DtError('dt_frame_gather failed (%d)' % rc)
+            return out
+        obs, act, rew, nxt, done = self._encode_sample(idxes)
+        out['obs'].copy_(obs)
+        out['nxt'].copy_(nxt)
+        out['act'].copy_(act)
+        out['rew'].copy_(rew.reshape(-1, 1))
+        out['notdone'].copy_((~done.bool()).reshape(-1, 1))
+        return out
+
     def uniforms(self, batch_size):
         return torch.rand(batch_size, dtype=torch.float64, device=self.device, generator=self.gen)
 
@@ -318,6 +350,11 @@ class PrioritizedReplayBuffer(ReplayBuffer):
 
     def sample(self, batch_size, beta=0.5, u=None):
         """buffers.py:185-235 -> (obs, act, rew, next_obs, done, weights, idxes)."""
+        idxes, weights = self.sample_indices(batch_size, beta, u)
+        return self._encode_sample(idxes) + (weights, idxes)
+
+    def sample_indices(self, batch_size, beta=0.5, u=None):
+        """sample()'s (idxes, weights) without encoding the rows."""
         if not beta > 0:
             raise ValueError('beta must be > 0')     # buffers.py:221
         u = self.uniforms(batch_size) if u is None else torch.as_tensor(
@@ -329,7 +366,7 @@ class PrioritizedReplayBuffer(ReplayBuffer):
                                               float(beta), ctypes.c_void_p(idxes.data_ptr()),
                                               ctypes.c_void_p(weights.data_ptr()),
                                               self._stream()), 'dt_per_sample')
-        return self._encode_sample(idxes) + (weights, idxes)
+        return idxes, weights
 
     def update_priorities(self, idxes, priorities):
         """buffers.py:237-259.  Invalid entries (the reference's asserts) are

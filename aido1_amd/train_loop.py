@@ -214,11 +214,18 @@ class TrainLoop:
         self.rollout.load_exploit_actor(self.trainer.target_actor)
 
     def _update(self):
-        if self.prioritized:
+        if self.prioritized and self.trainer.dtype == torch.float32:
+            # the sampled rows gathered straight into the update's inputs
+            # (one dt_frame_gather launch, replay.gather_into)
+            idx, _w = self.replay.sample_indices(self.batch_size, self.beta)
+            self.replay.gather_into(idx, self.trainer.static_inputs(self.batch_size))
+            self.metrics, info = self.trainer.update_prepared()
+        elif self.prioritized:
             obs, act, rew, nxt, done, _w, idx = self.replay.sample(self.batch_size, self.beta)
+            self.metrics, info = self.trainer.update((obs, act, rew, nxt, done))
         else:
             obs, act, rew, nxt, done = self.replay.sample(self.batch_size)
-        self.metrics, info = self.trainer.update((obs, act, rew, nxt, done))
+            self.metrics, info = self.trainer.update((obs, act, rew, nxt, done))
         if self.prioritized:
             pr = info['td_error'].detach().abs().reshape(-1).double() + PRIORITY_EPS
             self.replay.update_priorities(idx, pr)

@@ -163,6 +163,20 @@ class DDPGTrainer:
                     raise ValueError('graph mode needs a fixed batch shape')
                 self._in[k].copy_(v)
 
+    def static_inputs(self, batch, obs_shape=(3, 120, 160)):
+        """The inputs an update reads (graph mode: the captured graphs' static
+        tensors), for a producer that writes them in place (TrainLoop: the
+        replay's dt_frame_gather); then update_prepared()."""
+        if self._in is None:
+            cl = torch.channels_last
+            z = (lambda *s: torch.zeros(*s, device=self.device, dtype=self.dtype))
+            self._in = {'obs': z(batch, *obs_shape).contiguous(memory_format=cl),
+                        'nxt': z(batch, *obs_shape).contiguous(memory_format=cl),
+                        'act': z(batch, 2), 'rew': z(batch, 1), 'notdone': z(batch, 1)}
+        if self._in['obs'].shape[0] != batch:
+            raise ValueError('graph mode needs a fixed batch shape')
+        return self._in
+
     def _grads(self, loss, module):
         """zero_grad + loss.backward() for `module`'s parameters
         (trainers.py:178-179, 197-198) as torch.autograd.grad: the same
@@ -327,6 +341,11 @@ class DDPGTrainer:
         reference; metric values are 0-dim device tensors (valid until the
         next update in graph mode)."""
         self._inputs(train_data)
+        return self.update_prepared()
+
+    def update_prepared(self):
+        """update() on the inputs already in static_inputs() (written in place
+        by the caller on the current stream)."""
         self.critic_decay.update_step(self.global_update_step)
         self.actor_decay.update_step(self.global_update_step)
         for group in self.critic_optim.param_groups:

@@ -90,6 +90,24 @@ int dt_frame_add(int32_t n, int64_t frame_elems, const float* src, int64_t src_e
                  float* dst, int32_t k, int32_t* stack, const uint8_t* done, int32_t base_row,
                  int32_t* obs_ptr, int32_t* next_ptr, void* stream);
 
+/* dt_frame_gather: a sampled batch of the frame store straight into the
+ * update's inputs (ReplayBuffer._encode_sample, buffers.py:38-52, then
+ * DDPGTrainer's float32 channels_last inputs, trainers.py:156-163), one
+ * launch instead of the index_selects, the layout change, the casts and the
+ * copies into the captured graph's static inputs.  For b < batch, i = idx[b]:
+ *   obs[b][y][x][c] = frames[obs_ptr[i][c]][y * w + x]   (c < k; NHWC: the
+ *   nxt[b][y][x][c] = frames[next_ptr[i][c]][...]         channels_last memory
+ *                                                          of [batch, k, h, w])
+ *   act[b][j] = action[i][j] (j < 2), rew[b] = (float)reward[i],
+ *   notdone[b] = done[i] ? 0 : 1
+ *   idx device i64 [batch] in [0, size) (unchecked: dt_per_sample's output);
+ *   frames f32 [rows, hw]; obs_ptr / next_ptr i32 [size, k]; action f32
+ *   [size, 2]; reward f64 [size]; done u8 [size] (torch bool); k <= 4 */
+int dt_frame_gather(int32_t batch, const int64_t* idx, const float* frames, int64_t hw,
+                    int32_t k, const int32_t* obs_ptr, const int32_t* next_ptr,
+                    const float* action, const double* reward, const uint8_t* done, float* obs,
+                    float* nxt, float* act, float* rew, float* notdone, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -141,3 +141,32 @@ def test_frame_store_gpu_equals_stacked_per(gpu):
     idx = torch.arange(size, device=gpu)
     for x, y in zip(a._encode_sample(idx), b._encode_sample(idx)):
         assert torch.equal(x, y)
+
+
+def test_frame_gather_equals_encode_and_trainer_inputs(gpu):
+    """dt_frame_gather (replay.gather_into) writes exactly what _encode_sample
+    followed by DDPGTrainer._inputs makes of the same indices: channels_last
+    float32 obs / next_obs, actions, float32 rewards, notdone; also for the
+    stacked storage (torch fallback) and indices of every row."""
+    import sys
+    sys.path.insert(0, __import__('os').path.dirname(__file__))
+    from test_replay import _frame_steps
+    from test_trainer import make_trainer
+    from aido1_amd.replay import PrioritizedReplayBuffer
+    g = torch.Generator().manual_seed(4)
+    n, size = 256, 1024
+    a = PrioritizedReplayBuffer(size, 0.6, device=gpu, frame_envs=n)
+    b = PrioritizedReplayBuffer(size, 0.6, device=gpu)
+    for _ in _frame_steps(a, b, n, 7, g):
+        pass
+    tr = make_trainer(gpu)
+    for buf in (a, b):
+        for idx in (torch.arange(size, device=gpu), torch.randint(0, size, (64,), device=gpu)):
+            tr._in = None
+            tr._inputs(buf._encode_sample(idx))
+            want = {k: v.clone() for k, v in tr._in.items()}
+            tr._in = None
+            got = buf.gather_into(idx, tr.static_inputs(idx.shape[0]))
+            for k in want:
+                assert torch.equal(got[k], want[k]), k
+            assert got['obs'].is_contiguous(memory_format=torch.channels_last)
