@@ -123,6 +123,9 @@ def parse(argv=None):
                         '(the roofline\'s average kernel duration is over those launches); '
                         'an event pair around every launch adds ~6 us a decision of stream '
                         'packets to the wall time (measured: 0.1805 vs 0.1745 ms per step)')
+    p.add_argument('--roofline-launches', type=int, default=60,
+                   help='render: dt_render launches of the event-only pass after the timed '
+                        'region that the roofline averages (at least --steps)')
     p.add_argument('--lane-steps', type=int, default=320,
                    help='render: decisions timed by the config-2 sub-record')
     p.add_argument('--lane-warmup', type=int, default=20)
@@ -713,6 +716,21 @@ def bench_obs(args, ctx):
         parity = step_parity(env, start, actions[W:], out, rank, args, frames=ro)
     parity = worst_over_ranks(ctx, parity, STEP_PARITY_KEYS + ['gray_mismatches',
                                                                'mask_mismatches'])
+    # the roofline's kernel time: an event-only pass after the timed region
+    # with HIP events around EVERY dt_render (in the timed region they wrap
+    # every --event-stride-th launch only: an event pair per launch adds ~6 us
+    # a decision of stream packets to the wall time)
+    KE = max(K, args.roofline_launches)
+    ev_loop = ObsLoop(env, ro, torch, args.obs_mode, args.many, 1)
+    ev_act = torch.rand(KE, n, 2, generator=g, device=dev, dtype=torch.float32)
+    ev_out = StepOutput(KE * n, dev, lanepos=False, tile=False)
+    env.stats(reset=True)
+    ev_all = ev_loop.events(KE)
+    if ev_loop.run(ev_loop.bind(ev_act, ev_out), ev_all):
+        raise RuntimeError('a call of the roofline pass failed')
+    ctx.sync()
+    ev_st = env.stats()
+    rend_all = [a.elapsed_time(b) for a, b in ev_all[1]]
     env.close()
     lane = None if args.no_lane else lane_record(args, ctx, args.lane_steps, args.lane_warmup,
                                                  cpu=True)
@@ -726,8 +744,8 @@ def bench_obs(args, ctx):
         c5 = train_record(args, ctx, args.sub_steps, args.sub_warmup, parity=not args.no_parity,
                           cpu=True)
     if rank == 0:
-        kms = float(np.mean(rend_ms))
-        fresh_per_launch = st['resets'] / K
+        kms = float(np.mean(rend_all))
+        fresh_per_launch = ev_st['resets'] / KE
         bpl = RENDER_BYTES_PER_ENV * n + RENDER_BYTES_PER_FRESH * fresh_per_launch
         achieved = bpl / (kms * 1e-3) / 1e9
         pmc = load_pmc('render_kernel') or {}
@@ -768,17 +786,21 @@ def bench_obs(args, ctx):
                          'peak': HBM_PEAK_GBS, 'unit': 'GB/s', 'frac': achieved / HBM_PEAK_GBS,
                          'traffic': pmc.get('hbm_bytes_per_launch'),
                          'traffic_round': pmc.get('round'),
-                         'avg_kernel_ms': kms, 'min_kernel_ms': float(np.min(rend_ms)),
-                         'max_kernel_ms': float(np.max(rend_ms)),
+                         'avg_kernel_ms': kms, 'min_kernel_ms': float(np.min(rend_all)),
+                         'max_kernel_ms': float(np.max(rend_all)),
+                         'timed_region_sampled_ms': float(np.mean(rend_ms)),
                          'algorithmic_bytes_per_launch': bpl,
                          'algorithmic_basis': 'per env: grey f32 76,800 + 4 u8 masks 76,800 '
                                               'written + pose 24 read (SURVEY §8d config 3 '
                                               'without the step\'s 81 B); plus 153,600 B of '
                                               'ring refill per respawned env (%.1f per launch)'
                                               % fresh_per_launch,
-                         'timing': 'HIP events on the render stream around every %d-th '
-                                   'dt_render of the timed region (%d launches averaged)'
-                                   % (loop.event_stride, len(rend_ms))},
+                         'timing': 'HIP events on the render stream around every dt_render of '
+                                   'a %d-decision pass right after the timed region (same '
+                                   'envs, launches and streams; %d launches averaged); '
+                                   'timed_region_sampled_ms: events around every %d-th '
+                                   'dt_render inside the timed region (%d launches)'
+                                   % (KE, len(rend_all), loop.event_stride, len(rend_ms))},
             'step_launch_ms': float(np.mean(step_ms)),
             'step_launches': len(starts),
             'host_enqueue_ms_per_step': t_host / K * 1e3,
