@@ -81,6 +81,18 @@ class MultiTensorTable:
         self.tensors = torch.from_numpy(tab.view(np.uint8).copy()).to(device)
         self.chunks = torch.tensor(chunks, dtype=torch.int32, device=device).reshape(-1)
         self.n_chunks = len(chunks)
+        self.sizes = [r[0].numel() for r in rows]
+
+    def refill(self, rows):
+        """New pointers for rows of the same sizes, written into the same
+        device table (a captured launch that reads it sees them)."""
+        if [r[0].numel() for r in rows] != self.sizes:
+            raise ValueError('refill needs rows of the same sizes')
+        tab = np.zeros(len(rows), self.ROW)
+        for i, r in enumerate(rows):
+            tab[i] = tuple([t.data_ptr() for t in r] + [0] * (4 - len(r))) + (r[0].numel(),)
+        self.tensors.copy_(torch.from_numpy(tab.view(np.uint8).copy()))
+        self.key = self.key_of(rows)
 
     @staticmethod
     def key_of(rows):
@@ -169,19 +181,45 @@ class DeviceAdam(torch.optim.Adam):
                 self.state[p]['step'] = self._step_t
         self._table = None
 
-    def _rows(self):
+    def _rows(self, grads=None):
         rows = []
-        for group in self.param_groups:
-            for p in group['params']:
-                if p.grad is not None:
-                    st = self.state[p]
-                    rows.append((p, p.grad, st['exp_avg'], st['exp_avg_sq']))
+        params = [p for group in self.param_groups for p in group['params']]
+        if grads is not None:
+            if len(grads) != len(params):
+                raise ValueError('one gradient per parameter')
+            for p, gr in zip(params, grads):
+                st = self.state[p]
+                rows.append((p, gr, st['exp_avg'], st['exp_avg_sq']))
+            return rows
+        for p in params:
+            if p.grad is not None:
+                st = self.state[p]
+                rows.append((p, p.grad, st['exp_avg'], st['exp_avg_sq']))
         return rows
 
+    def finish_capture(self):
+        """After a HIP graph captured step(grads=...): write the captured
+        gradients' addresses into the table the captured dt_adam reads."""
+        if getattr(self, '_deferred', None) is not None:
+            self._table.refill(self._deferred)
+            self._deferred = None
+
     @torch.no_grad()
-    def step(self, closure=None):
+    def step(self, closure=None, grads=None):
+        """grads: the gradients as a list in parameter order (the trainer's
+        torch.autograd.grad outputs) instead of .grad, so nothing is copied
+        into .grad; inside a graph capture with new addresses the table is
+        refilled by finish_capture() (its launch reads the table then)."""
         g = self.param_groups[0]
-        rows = self._rows()
+        rows = self._rows(grads)
+        if grads is not None and not (MultiTensorTable.fits(rows) and len(self.param_groups) == 1
+                                       and not g['weight_decay'] and not g['amsgrad']
+                                       and not g['maximize'] and torch.is_tensor(g['lr'])):
+            for p, gr in zip([p for gp in self.param_groups for p in gp['params']], grads):
+                if p.grad is None:     # .grad in the parameter's own memory format
+                    p.grad = torch.empty_like(p)
+                p.grad.copy_(gr)
+            grads, rows = None, self._rows()
         if (len(self.param_groups) != 1 or g['weight_decay'] or g['amsgrad'] or g['maximize']
                 or not torch.is_tensor(g['lr']) or not rows or not MultiTensorTable.fits(rows)
                 or any(self.state[r[0]]['step'] is not self._step_t for r in rows)):
@@ -198,7 +236,11 @@ class DeviceAdam(torch.optim.Adam):
                 self.guard.scan(self.param_bit, *[r[0] for r in rows])
             return out
         if self._table is None or self._table.key != MultiTensorTable.key_of(rows):
-            self._table = MultiTensorTable(rows, self._step_t.device)
+            if (torch.cuda.is_current_stream_capturing() and self._table is not None
+                    and self._table.sizes == [r[0].numel() for r in rows]):
+                self._deferred = rows          # finish_capture() writes them
+            else:
+                self._table = MultiTensorTable(rows, self._step_t.device)
         from aido1_amd import _lib
         t = self._table
         b1, b2 = g['betas']

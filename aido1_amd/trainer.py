@@ -130,6 +130,7 @@ class DDPGTrainer:
             if isinstance(opt, DeviceAdam):
                 opt.set_guard(self.guard, *stages)
         self.warmup = warmup
+        self._pending_grads = {}      # module id -> its autograd gradients (_grads -> _opt_step)
         self.conv_search = bool(conv_search)
         self._graphs = None
         self._in = None
@@ -187,6 +188,15 @@ class DDPGTrainer:
         conv trunk (independent of the actor) is not differentiated at all."""
         params = [p for p in module.parameters() if p.requires_grad]
         grads = torch.autograd.grad(loss, params, allow_unused=True, materialize_grads=True)
+        opt = self.actor_optim if module is self.actor else self.critic_optim
+        if (self.graph and isinstance(opt, DeviceAdam) and len(params) == len(list(
+                module.parameters())) and (self.sync_actor if module is self.actor
+                                            else self.sync_critic) is None):
+            # graph mode, one rank: dt_adam reads the autograd outputs
+            # themselves (their addresses are fixed in the graph's pool), so
+            # no copy into .grad (two multi-tensor kernels an update)
+            self._pending_grads[id(module)] = list(grads)
+            return
         if all(p.grad is not None for p in params):
             torch._foreach_copy_([p.grad for p in params], list(grads))
         else:   # .grad in the parameter's own memory format (DeviceAdam's layout)
@@ -214,7 +224,7 @@ class DDPGTrainer:
         """opt.step() with its gradients and results guarded: DeviceAdam reports
         from inside dt_adam, any other optimiser is scanned around."""
         if isinstance(opt, DeviceAdam):
-            opt.step()
+            opt.step(grads=self._pending_grads.pop(id(module), None))
             return
         params = [p for p in module.parameters() if p.grad is not None]
         self.guard.scan(grad_stage, *[p.grad for p in params])
@@ -334,6 +344,9 @@ class DDPGTrainer:
                 for st in group:
                     st()
             self._graphs.append(g)
+        for opt in (self.actor_optim, self.critic_optim):
+            if isinstance(opt, DeviceAdam):
+                opt.finish_capture()
 
     def update(self, train_data):
         """train_data = (obs, actions, rewards, next_obs, dones), leading batch

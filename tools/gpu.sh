@@ -7,7 +7,7 @@
 #   bench:<args>          bench.py with <args> (commas become spaces)
 #   prof:<config>         rocprofv3 --kernel-trace --stats of bench.py --config <config>
 #   py:<script>[,args]    a tools/ python script
-#   ab:<diag .so>[,R]     tools/render_ab.sh: the render bench, product vs a diagnostic build
+#   ab:<diag .so>,R[,bench args]  tools/ab.sh: bench.py, product vs a diagnostic build
 # Each step has its own time limit; the first failure ends the call (no retries).
 # Logs: gpurun_out/<TAG>_<n>_<step>.log
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
@@ -57,7 +57,7 @@ for st in "$@"; do
           f=$(find "/tmp/prof_$arg" -name '*kernel_stats.csv' | head -1)
           cp "$f" "gpurun_out/${TAG}_${arg}_kernel_stats.csv"
           python3 tools/kstats.py "gpurun_out/${TAG}_${arg}_kernel_stats.csv" 25 ;;
-    ab) run ab 900 bash tools/render_ab.sh $args ;;
+    ab) run ab 900 bash tools/ab.sh $args ;;
     py) set -- $args; s=$1; shift
         run "py_$(basename "$s" .py)" 600 python -u "tools/$s" "$@" ;;
     *) echo "unknown step $st"; exit 2 ;;
