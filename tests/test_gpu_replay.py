@@ -166,7 +166,8 @@ def test_frame_gather_equals_encode_and_trainer_inputs(gpu):
             tr._inputs(buf._encode_sample(idx))
             want = {k: v.clone() for k, v in tr._in.items()}
             tr._in = None
-            got = buf.gather_into(idx, tr.static_inputs(idx.shape[0]))
+            got = buf.gather_into(idx, tr.static_inputs(idx.shape[0],
+                                                        tuple(want['obs'].shape[1:])))
             for k in want:
                 assert torch.equal(got[k], want[k]), k
             assert got['obs'].is_contiguous(memory_format=torch.channels_last)
