@@ -28,9 +28,6 @@
 #endif
 // conv1s_kernel's reduction layout: 1 = K 192 (3-channel pixels, 12 MFMAs a
 // tile), 0 = K 256 (4-channel pixels with a zero channel, 16 MFMAs a tile)
-#ifndef DTCONV2_KS_GROUP
-#define DTCONV2_KS_GROUP 2   // B fragments a group in conv2's K-split form
-#endif
 #ifndef DTCONV1_K192
 #define DTCONV1_K192 1
 #endif
@@ -84,34 +81,6 @@ __device__ __forceinline__ void store_px32(__half* sample, int px, const float (
     const u32x4 d = {u[2 * m][0], u[2 * m][1], u[2 * m + 1][0], u[2 * m + 1][1]};
     __builtin_amdgcn_raw_buffer_store_b128(d, rsrc, off + 32 * m, 0, 0);
   }
-}
-
-// store_px32 for one 16-channel half of the pixel (K-split conv2: registers
-// 8 half .. 8 half + 7 of the tile = channels 16 half .. 16 half + 15): one
-// 16-B store a lane at byte 32 half + 16 h.
-template <int kPix>
-__device__ __forceinline__ void store_px16(__half* sample, int px, const float (&v)[8], int h,
-                                           int half, bool valid) {
-  constexpr int kBytes = kPix * 32 * 2;
-  uint32_t u[2][2];
-#pragma unroll
-  for (int q = 0; q < 2; ++q) {
-    const __half2 v0 = __floats2half2_rn(v[4 * q + 0], v[4 * q + 1]);
-    const __half2 v1 = __floats2half2_rn(v[4 * q + 2], v[4 * q + 3]);
-    u[q][0] = *reinterpret_cast<const uint32_t*>(&v0);
-    u[q][1] = *reinterpret_cast<const uint32_t*>(&v1);
-  }
-#pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    const auto r = __builtin_amdgcn_permlane32_swap(u[0][e], u[1][e], false, false);
-    u[0][e] = r[0];
-    u[1][e] = r[1];
-  }
-  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(reinterpret_cast<void*>(sample), 0, kBytes,
-                                                      0x00020000);
-  const int off = valid ? px * 64 + 32 * half + 16 * h : kBytes;
-  const u32x4 d = {u[0][0], u[0][1], u[1][0], u[1][1]};
-  __builtin_amdgcn_raw_buffer_store_b128(d, rsrc, off, 0, 0);
 }
 
 // Reference mode keeps each sample's activations CENTRED in fp16: the stored
@@ -641,13 +610,7 @@ __device__ __forceinline__ int ring_off(int px, int c) {
 #ifndef DTCONV4_OCC
 #define DTCONV4_OCC (DTCONV4_WLDS ? 2 : 1)
 #endif
-// KS 2 (conv2): each step tile is computed by TWO waves, one per half of the
-// kernel rows (ky 0-1 / 2-3: 16 MFMAs and 16 weight fragments each); the
-// second half's accumulators reach the first through LDS, which runs the
-// epilogue.  Half the weights a lane (64 registers) lets two workgroups of
-// four waves share a CU (two waves a SIMD), so one workgroup's epilogue,
-// commit and barrier overlap the other's MFMAs.
-template <int IH, int IW, int OH, int OW, int ST, int NW, int kIn, int kOut, int KS = 1>
+template <int IH, int IW, int OH, int OW, int ST, int NW, int kIn, int kOut>
 __global__ void __launch_bounds__(64 * NW, NW == 4 ? DTCONV4_OCC : 1)   // 1: one wave per SIMD, the full register file
 conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfrag,
               const float* __restrict__ bias, const float* __restrict__ prev_part,
@@ -655,9 +618,7 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
               __half* __restrict__ y, float* __restrict__ part,
               const float* __restrict__ out_gamma, const float* __restrict__ out_beta,
               float out_eps, float slope, WeightSplit ws) {
-  static_assert(KS == 1 || (KS == 2 && kOut < 2), "K split: conv2 / conv3 forms only");
-  constexpr int NT = NW / KS;                     // tiles a step
-  using G = ConvGeom<IH, IW, OH, OW, ST, NT>;
+  using G = ConvGeom<IH, IW, OH, OW, ST, NW>;
   constexpr int kRing = G::ring();
   constexpr int kRowU4 = IW * 4;                  // 16-B chunks per input row
   constexpr int kRowBytes = IW * 64;
@@ -671,10 +632,7 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
   __shared__ float s_c[CO];   // the sample's centre (kOut 0): its pixel-0 outputs
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 31, h = lane >> 5;
-  const int tw = KS > 1 ? wave % NT : wave;    // the wave's tile in a step
-  const int half = KS > 1 ? wave / NT : 0;      // its K half
   unsigned char* rb = reinterpret_cast<unsigned char*>(ring);
-  __shared__ float xch[KS > 1 ? NT * 16 * 64 : 1];   // K half 1's accumulators
 
   const SplitPart sp = split_part(ws, n);
   if (sp.set2) {
@@ -697,9 +655,8 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
   float gam = 0.0f, bet = 0.0f;
   auto stats_load = [&](int k) __attribute__((always_inline)) {
     // every thread, every step, sample clamped: a fixed count of loads on
-    // every path keeps the compiler's vmcnt waits exact (KS 2: loaded by
-    // stats_merge itself, four registers fewer across the step)
-    if (kIn == 1 && KS == 1) {
+    // every path keeps the compiler's vmcnt waits exact
+    if (kIn == 1) {
       const int ns = sample(k) < send ? sample(k) : send - 1;
       const int c = tid & (CO - 1);
       const float* pp = prev_part + ((size_t)ns * CO + c) * 3;
@@ -711,14 +668,6 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
   };
   auto stats_merge = [&](int k) __attribute__((always_inline)) {
     if (kIn == 1 && tid < CO) {
-      if (KS > 1) {
-        const int ns = sample(k) < send ? sample(k) : send - 1;
-        const float* pp = prev_part + ((size_t)ns * CO + tid) * 3;
-        st[0] = pp[0];
-        st[1] = pp[1];
-        gam = in_gamma[tid];
-        bet = in_beta[tid];
-      }
       const float mean = st[0], m2 = st[1], cnt = (float)(IH * IW);
       const float sc = gam / sqrtf(m2 / cnt + in_eps);
       s_sc[k % 3][tid] = sc;
@@ -769,20 +718,19 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
 
   // weights and bias for the whole launch (row = out channel = lane & 31): in
   // registers, or for conv4 in LDS (kWL), read per MFMA
-  constexpr bool kWL = NT == 4 && DTCONV4_WLDS;
-  constexpr int kMW = 32 / KS;                    // MFMAs (weight fragments) a wave a tile
+  constexpr bool kWL = NW == 4 && DTCONV4_WLDS;
   __shared__ __attribute__((aligned(16))) half8 wl[kWL ? 32 * 64 : 1];
-  half8 wa[kWL ? 1 : kMW];
+  half8 wa[kWL ? 1 : 32];
   if constexpr (kWL) {
     for (int i = tid; i < 32 * 64; i += kThreads) wl[i] = wfrag[i];
   } else {
 #pragma unroll
-    for (int s = 0; s < kMW; ++s) wa[s] = wfrag[(kMW * half + s) * 64 + lane];
+    for (int s = 0; s < 32; ++s) wa[s] = wfrag[s * 64 + lane];
   }
   if (tid < CO) s_bias[tid] = bias[tid];
-  float w_cnt = 0.0f, w_mean[16 / KS], w_m2[16 / KS];
+  float w_cnt = 0.0f, w_mean[16], w_m2[16];
 #pragma unroll
-  for (int r = 0; r < 16 / KS; ++r) w_mean[r] = w_m2[r] = 0.0f;
+  for (int r = 0; r < 16; ++r) w_mean[r] = w_m2[r] = 0.0f;
 
   // One step.  At its start the ring holds step g's rows and registers `cur`
   // the rows of step g+1 (loaded during step g-1); it loads step g+2's new
@@ -798,113 +746,57 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
     stats_load(k2);
     if (!(DTCONV_SKIP & 1)) issue(nxt, k2, G::first_new(j1), G::last_new(j1));
 
-    // this wave's tile (KS 2: with the other K half's wave)
-    const int t = NT * j + tw;
+    // this wave's tile
+    const int t = NW * j + wave;
     const int p = 32 * t + col;
     const bool valid = p < G::kPix;
     const int pc = valid ? p : 0;
     const int oy = pc / OW, ox = pc - oy * OW;
-    // the wave's kernel rows' ring offsets: all four, or its K half's two
-    int row[4 / KS];
+    int row[4];
 #pragma unroll
-    for (int q = 0; q < 4 / KS; ++q)
-      row[q] = ((k * IH + ST * oy + (4 / KS) * half + q) % kRing) * kRowBytes;
+    for (int ky = 0; ky < 4; ++ky) row[ky] = ((k * IH + ST * oy + ky) % kRing) * kRowBytes;
     int off[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) off[q] = ring_off<IW, ST>(ST * ox + (q >> 1), 2 * (q & 1) + h);
     // 4 groups (ky) of 8 B fragments: group g+1's LDS reads are in flight
     // while group g's MFMAs run
-    f32x16 acc;   // starts at the bias (KS 2: K half 1 at 0)
+    f32x16 acc;   // starts at the bias
 #pragma unroll
-    for (int r = 0; r < 16; ++r) acc[r] = half == 0 ? s_bias[(r & 3) + 8 * (r >> 2) + 4 * h] : 0.0f;
-    // groups of kGS B fragments (a kernel row ky is 8): KS 1 whole rows, KS 2
-    // half rows (fewer registers in flight); the wave's groups cover all four
-    // rows, or its K half's two
-    constexpr int kGS = KS > 1 ? DTCONV2_KS_GROUP : 8, kNG = kMW / kGS;
-    half8 bq[2][kGS];
-    auto ld = [&](half8 (&b)[kGS], int g) __attribute__((always_inline)) {   // g: the wave's group
-      const int f = kGS * g;                    // the wave's fragment index (8 a kernel row)
+    for (int r = 0; r < 16; ++r) acc[r] = s_bias[(r & 3) + 8 * (r >> 2) + 4 * h];
+    half8 bq[2][8];
+    auto ld = [&](half8 (&b)[8], int gy) __attribute__((always_inline)) {
 #pragma unroll
-      for (int i = 0; i < kGS; ++i)
-        b[i] = *reinterpret_cast<const half8*>(rb + row[f / 8] + off[f % 8 + i]);
+      for (int i = 0; i < 8; ++i) b[i] = *reinterpret_cast<const half8*>(rb + row[gy] + off[i]);
     };
-    auto mm = [&](half8 (&b)[kGS], int g) __attribute__((always_inline)) {
+    auto mm = [&](half8 (&b)[8], int gy) __attribute__((always_inline)) {
 #pragma unroll
-      for (int i = 0; i < kGS; ++i)   // the ring rows are already normalised (commit)
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kWL ? wl[(kGS * g + i) * 64 + lane]
-                                                         : wa[kWL ? 0 : kGS * g + i],
+      for (int i = 0; i < 8; ++i)   // the ring rows are already normalised (commit)
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(kWL ? wl[(8 * gy + i) * 64 + lane]
+                                                         : wa[kWL ? 0 : 8 * gy + i],
                                                      b[i], acc, 0, 0, 0);
     };
     if (!(DTCONV_SKIP & 2)) ld(bq[0], 0);
 #pragma unroll
-    for (int g = 0; g < kNG && !(DTCONV_SKIP & 2); ++g) {
-      if (g + 1 < kNG) ld(bq[(g + 1) & 1], g + 1);
+    for (int gy = 0; gy < 4 && !(DTCONV_SKIP & 2); ++gy) {
+      if (gy < 3) ld(bq[(gy + 1) & 1], gy + 1);
       __builtin_amdgcn_sched_barrier(0);
-      mm(bq[g & 1], g);
+      mm(bq[gy & 1], gy);
       __builtin_amdgcn_sched_barrier(0);
     }
-    // the epilogue's registers: all 16 (KS 1), or 8 a K half (KS 2: half 0
-    // finishes registers 0-7 = channels 0-15, half 1 registers 8-15 =
-    // channels 16-31; each half first adds the other half's partial sums of
-    // them, exchanged through LDS).  Register i of the wave is the tile's
-    // register rb0 + i: channel (i & 3) + 8 (i >> 2) + 4 h + 16 half.
-    constexpr int kR = 16 / KS;
-    float v[kR];
-    if constexpr (KS > 1) {
-      float* xo = xch + (tw * 2 + (1 - half)) * 8 * 64 + lane;   // the other half's registers
-      const float* xi = xch + (tw * 2 + half) * 8 * 64 + lane;   // mine, from the other half
-      if (half) {   // wave-uniform branches: registers picked at compile time
-#pragma unroll
-        for (int i = 0; i < 8; ++i) xo[64 * i] = acc[i];
-      } else {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) xo[64 * i] = acc[8 + i];
-      }
-      __syncthreads();
-      if (half) {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = acc[8 + i] + xi[64 * i];
-      } else {
-#pragma unroll
-        for (int i = 0; i < 8; ++i) v[i] = acc[i] + xi[64 * i];
-      }
-    } else {
-#pragma unroll
-      for (int r = 0; r < 16; ++r) v[r] = acc[r];
-    }
-    auto chan = [&](int i) __attribute__((always_inline)) {
-      return (i & 3) + 8 * (i >> 2) + 4 * h + 16 * half;
-    };
     if (stats2) stats_merge(k2);   // read by step g+2, after two barriers
+    float v[16];
 #pragma unroll
-    for (int r = 0; r < kR; ++r) v[r] = lrelu2(v[r], slope);
+    for (int r = 0; r < 16; ++r) v[r] = lrelu2(acc[r], slope);
 
     // epilogue
     if (kOut <= 1) {
-      if (kOut == 0) {
-        if constexpr (KS == 1) {
-          centre_px32(v, s_c, j == 0 && wave == 0 && col == 0, j == 0, h);
-        } else {   // each half's tile-0 wave publishes its channels' centre
-          if (j == 0 && tw == 0 && col == 0)
-#pragma unroll
-            for (int i = 0; i < kR; ++i) s_c[chan(i)] = v[i];
-          if (j == 0) __syncthreads();
-#pragma unroll
-          for (int i = 0; i < kR; ++i) v[i] -= s_c[chan(i)];
-        }
-      }
-      if (!(DTCONV_SKIP & 4)) {
-        if constexpr (KS == 1)
-          store_px32<G::kPix>(y + (size_t)ns * G::kPix * CO, pc, v, h, valid);
-        else
-          store_px16<G::kPix>(y + (size_t)ns * G::kPix * CO, pc, v, h, half, valid);
-      }
+      if (kOut == 0) centre_px32(v, s_c, j == 0 && wave == 0 && col == 0, j == 0, h);
+      if (!(DTCONV_SKIP & 4)) store_px32<G::kPix>(y + (size_t)ns * G::kPix * CO, pc, v, h, valid);
       if (kOut == 0 && valid && !(DTCONV_SKIP & 8)) {   // Welford over this lane's pixels
         w_cnt += 1.0f;
-        // (KS 2: the hardware reciprocal, as conv1's: 1 ulp of the weight)
-        const float inv = KS > 1 ? __builtin_amdgcn_rcpf(w_cnt) : 1.0f / w_cnt;
+        const float inv = 1.0f / w_cnt;
 #pragma unroll
-        for (int r = 0; r < kR; ++r) {
+        for (int r = 0; r < 16; ++r) {
           const float d = v[r] - w_mean[r];
           w_mean[r] += d * inv;
           w_m2[r] += d * (v[r] - w_mean[r]);
@@ -918,7 +810,7 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
           const float tot = w_cnt + nb;
           const float fa = tot > 0.0f ? nb / tot : 0.0f, fb = tot > 0.0f ? w_cnt * nb / tot : 0.0f;
 #pragma unroll
-          for (int r = 0; r < kR; ++r) {
+          for (int r = 0; r < 16; ++r) {
             const float mb = __shfl_xor(w_mean[r], o, 32), m2b = __shfl_xor(w_m2[r], o, 32);
             const float d = mb - w_mean[r];
             w_mean[r] += d * fa;
@@ -926,18 +818,14 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
           }
           w_cnt = tot;
         }
-        if (col == 0) {
+        if (col == 0)
 #pragma unroll
-          for (int r = 0; r < kR; ++r) {
-            const int c = chan(r);
+          for (int r = 0; r < 16; ++r) {
+            const int c = (r & 3) + 8 * (r >> 2) + 4 * h;
             red[wave][c][0] = w_cnt;
             red[wave][c][1] = w_mean[r];
             red[wave][c][2] = w_m2[r];
           }
-          if (KS > 1)   // no count for the other half's channels
-#pragma unroll
-            for (int r = 0; r < kR; ++r) red[wave][(chan(r) + 16) & 31][0] = 0.0f;
-        }
         __syncthreads();
         if (tid < CO) {
           float cnt = 0.0f, mean = 0.0f, m2 = 0.0f;
@@ -956,7 +844,7 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
         }
         w_cnt = 0.0f;
 #pragma unroll
-        for (int r = 0; r < kR; ++r) w_mean[r] = w_m2[r] = 0.0f;
+        for (int r = 0; r < 16; ++r) w_mean[r] = w_m2[r] = 0.0f;
       }
     } else {   // the whole sample is in this step: BatchNorm of a batch of one, flatten
       if (kOut == 2) {
@@ -1048,12 +936,12 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
   }
 }
 
-template <int IH, int IW, int OH, int OW, int ST, int NW, int kIn, int kOut, int KS = 1>
+template <int IH, int IW, int OH, int OW, int ST, int NW, int kIn, int kOut>
 int launch_conv32(int n, const void* x, const void* wfrag, const float* bias,
                   const float* prev_part, const float* ig, const float* ibt,
                   float ieps, void* y, float* part, const float* og, const float* obt, float oeps,
                   float slope, hipStream_t s, WeightSplit ws, int n0) {
-  auto kern = conv32_kernel<IH, IW, OH, OW, ST, NW, kIn, kOut, KS>;
+  auto kern = conv32_kernel<IH, IW, OH, OW, ST, NW, kIn, kOut>;
   static int grid = 0;   // resident workgroups: one wave of them, persistent
   if (!grid) {
     int dev = 0, cus = 256, per = 1;
@@ -1074,11 +962,6 @@ int launch_conv32(int n, const void* x, const void* wfrag, const float* bias,
 // waves (tiles per step) per layer: conv2 / conv3 two (2-3 rings per CU), conv4
 // four (its 4 tiles in one step for the in-kernel norm)
 constexpr int kConv2Waves = 2, kConv3Waves = 2, kConv4Waves = 4;
-// conv2 with the K split (KS 2): four waves, two tiles a step
-#ifndef DTCONV2_KSPLIT
-#define DTCONV2_KSPLIT 1
-#endif
-constexpr int kConv2KS = DTCONV2_KSPLIT ? 2 : 1;
 
 }  // namespace
 
@@ -1174,10 +1057,10 @@ extern "C" int dt_conv32_split(int32_t layer, int32_t n, const void* x, const vo
   switch (layer) {
     case 2:   // 57x77 -> 27x37, stride 2; input norm from conv1's per-sample statistics
       if (in != (part != nullptr)) return DT_E_ARG;
-      return in ? launch_conv32<57, 77, 27, 37, 2, kConv2Waves * kConv2KS, 1, 0, kConv2KS>(
+      return in ? launch_conv32<57, 77, 27, 37, 2, kConv2Waves, 1, 0>(
                       n, x, wfrag, bias, prev_part, in_gamma, in_beta, in_eps, y, part,
                       nullptr, nullptr, 0.f, slope, s, ws, n0)
-                : launch_conv32<57, 77, 27, 37, 2, kConv2Waves * kConv2KS, 0, 1, kConv2KS>(
+                : launch_conv32<57, 77, 27, 37, 2, kConv2Waves, 0, 1>(
                       n, x, wfrag, bias, nullptr, nullptr, nullptr, 0.f, y, nullptr, nullptr,
                       nullptr, 0.f, slope, s, ws, n0);
     case 3:   // 27x37 -> 12x17, stride 2; input norm from conv2's per-sample statistics

@@ -379,7 +379,7 @@ struct RenderLds {
   int32_t cnt[kNCnt];
   int32_t env;          // this workgroup's env (the dispatch order's entry)
   uint32_t launch;      // the dispatch order state's launch count at entry
-  uint32_t arrival;     // this workgroup's finishing rank in the launch
+  uint32_t arrival;     // this workgroup's ticket (start order) in the launch
   unsigned long long t0;  // shader clock at entry (the env's recorded cost)
   int8_t kind[dt::kMaxLdsTiles];
 };
@@ -1009,18 +1009,22 @@ __device__ __forceinline__ void write_outputs(const RenderArgs& a, RenderLds& S,
 // because a frame with many listed words or markings takes up to twice the
 // median.  Greedy dispatch in blockIdx order is list scheduling; with the
 // longest jobs first (LPT) the tail holds only short ones.  Each workgroup
-// records its env's cost (shader cycles from entry to exit), and when 512
-// workgroups of the launch remain, the one finishing then (its CU is idling
-// into the drain anyway) counting-sorts the envs by cost, descending, into the
-// order the NEXT launch dispatches in (the last one of a launch of <= 512
-// workgroups; poses move 3 sim steps a decision, so
-// a frame's cost predicts the next one's; respawned envs' guesses are stale).
+// records its env's cost (shader cycles from entry to exit) and takes a
+// ticket (its start order) when it starts; the workgroup with ticket n - 512
+// (it finishes in the drain, when its CU idles anyway; ticket n - 1 in a
+// launch of <= 512 workgroups) counting-sorts the envs by recorded cost,
+// descending, into the order the NEXT launch dispatches in (poses move 3 sim
+// steps a decision, so a frame's cost predicts the next one's; respawned
+// envs' guesses are stale, and costs not yet recorded are the last launch's).
 // Block b renders env perm[launch & 1][b]; the order is only a schedule:
 // every env is rendered exactly once a launch and its outputs do not depend
-// on it.  State (per handle, dt_render_init): [0] launches, [1] arrivals,
-// then cost[n] (u32 cycles), perm[2][n] (i32, both the identity at first).
+// on it.  Nothing here waits on the workgroup's output stores: the ticket is
+// taken at entry, the cost stored without a wait, and only the builder
+// synchronises its waves.  State (per handle, dt_render_init): [0] launches,
+// [1] tickets, then cost[n] (u32 cycles), perm[2][n] (i32, both the identity
+// at first).
 constexpr int kSchedHead = 16;
-constexpr int kSchedTail = 512;      // workgroups still running when the order is built
+constexpr int kSchedTail = 512;      // workgroups started after the builder
 constexpr int kSchedBuckets = 1024;  // cost >> 8 (256-cycle buckets), clamped
 constexpr int kSchedMaxN = (int)(sizeof(((RenderLds*)0)->u) / sizeof(uint16_t));
 
@@ -1075,27 +1079,21 @@ __device__ __forceinline__ void sched_build(const RenderArgs& a, RenderLds& S, u
   for (int i = tid; i < n; i += T) next[atomicAdd(&hist[key[i]], 1u)] = i;
 }
 
-// exit of a workgroup: its cost; the order builder and the launch's last
-// arriver (which advances the launch count and resets the arrivals)
+// the builder's ticket
+__device__ __forceinline__ uint32_t sched_builder(const RenderArgs& a) {
+  return (uint32_t)(a.n > kSchedTail ? a.n - kSchedTail : a.n - 1);
+}
+
+// exit of a workgroup: its cost (thread 0, no wait); the builder sorts
 __device__ __forceinline__ void sched_exit(const RenderArgs& a, RenderLds& S, int e) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
   if (threadIdx.x == 0) {
     const unsigned long long dt = __builtin_amdgcn_s_memtime() - S.t0;
     __hip_atomic_store(sched_cost(a) + e, dt > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)dt,
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the cost lands before the arrival
-    S.arrival = __hip_atomic_fetch_add(a.sched + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  __syncthreads();
-  const uint32_t arr = S.arrival;
-  // the builder: the workgroup finishing when kSchedTail remain (the drain);
-  // in a smaller launch the last one, which sees every cost of this launch
-  const uint32_t at = (uint32_t)(a.n > kSchedTail ? a.n - kSchedTail : a.n - 1);
-  if (arr == at && a.n <= kSchedMaxN) sched_build(a, S, S.launch);
-  if (arr == (uint32_t)(a.n - 1) && threadIdx.x == 0) {
-    __hip_atomic_store(a.sched + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __hip_atomic_store(a.sched, S.launch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (S.arrival == sched_builder(a) && a.n <= kSchedMaxN) {   // workgroup-uniform
+    __syncthreads();                      // every wave past its outputs: LDS is free
+    sched_build(a, S, S.launch);
   }
 }
 
@@ -1411,6 +1409,16 @@ render_kernel(RenderArgs a) {
       const int p = sched_perm(a, launch)[blockIdx.x];
       e = (unsigned)p < (unsigned)a.n ? p : (int)blockIdx.x;   // (always a permutation)
       S.launch = launch;
+      // the ticket, taken after the launch count was read: so when the last
+      // ticket's holder advances the count, every workgroup has read it
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      const uint32_t ticket =
+          __hip_atomic_fetch_add(a.sched + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      S.arrival = ticket;
+      if (ticket == (uint32_t)(a.n - 1)) {
+        __hip_atomic_store(a.sched + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(a.sched, launch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
     }
     S.env = e;
     S.t0 = __builtin_amdgcn_s_memtime();
