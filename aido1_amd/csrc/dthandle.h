@@ -31,6 +31,7 @@ struct dt_handle {
   int32_t n_yellow = 0, n_white = 0;
   void* render_spill = nullptr;  // per env: listed words past the LDS list (dtrender.hip)
   void* render_sched = nullptr;  // render_kernel's dispatch order state (dtrender.hip)
+  uint32_t render_launches = 0;  // dt_render launches (the order's double-buffer parity)
   std::string err;
 };
 

@@ -302,6 +302,7 @@ struct RenderArgs {
   LineDev line;
   int32_t n;
   uint32_t* sched;   // dispatch order state (kSchedHead + cost[n] + perm[2][n]), or null
+  uint32_t launch;   // the handle's render launch count (host side): perm[launch & 1] is read
 };
 
 // ---- fused render kernel ----------------------------------------------------------
@@ -378,8 +379,6 @@ struct RenderLds {
   View view;
   int32_t cnt[kNCnt];
   int32_t env;          // this workgroup's env (the dispatch order's entry)
-  uint32_t launch;      // the dispatch order state's launch count at entry
-  uint32_t arrival;     // this workgroup's ticket (start order) in the launch
   unsigned long long t0;  // shader clock at entry (the env's recorded cost)
   int8_t kind[dt::kMaxLdsTiles];
 };
@@ -1009,20 +1008,23 @@ __device__ __forceinline__ void write_outputs(const RenderArgs& a, RenderLds& S,
 // because a frame with many listed words or markings takes up to twice the
 // median.  Greedy dispatch in blockIdx order is list scheduling; with the
 // longest jobs first (LPT) the tail holds only short ones.  Each workgroup
-// records its env's cost (shader cycles from entry to exit) and takes a
-// ticket (its start order) when it starts; the workgroup with ticket n - 512
-// (it finishes in the drain, when its CU idles anyway; ticket n - 1 in a
-// launch of <= 512 workgroups) counting-sorts the envs by recorded cost,
-// descending, into the order the NEXT launch dispatches in (poses move 3 sim
-// steps a decision, so a frame's cost predicts the next one's; respawned
-// envs' guesses are stale, and costs not yet recorded are the last launch's).
-// Block b renders env perm[launch & 1][b]; the order is only a schedule:
+// records its env's cost (shader cycles from entry to exit); block n - 512
+// (dispatched about 512 workgroups before the end, so it finishes in the
+// drain, when its CU idles anyway; launches of <= 512 workgroups run at once
+// and keep the identity order)
+// counting-sorts the envs by recorded cost, descending, into the order the
+// NEXT launch dispatches in (poses move 3 sim steps a decision, so a frame's
+// cost predicts the next one's; respawned envs' guesses are stale, and costs
+// not yet recorded are the last launch's).  Block b renders env
+// perm[launch & 1][b], launch the handle's host-side launch count passed as an
+// argument (a launch baked into a HIP graph keeps its parity: an odd graph
+// length re-reads an older order, still a permutation).  No device-wide
+// counter: an agent-scope atomic on one address from every workgroup
+// serialises at memory across the 8 XCDs (a start ticket taken that way cost
+// 0.15 ms a 4096-env launch).  The order is only a schedule:
 // every env is rendered exactly once a launch and its outputs do not depend
-// on it.  Nothing here waits on the workgroup's output stores: the ticket is
-// taken at entry, the cost stored without a wait, and only the builder
-// synchronises its waves.  State (per handle, dt_render_init): [0] launches,
-// [1] tickets, then cost[n] (u32 cycles), perm[2][n] (i32, both the identity
-// at first).
+// on it.  State (per handle, dt_render_init): kSchedHead unused words, then
+// cost[n] (u32 cycles), perm[2][n] (i32, both the identity at first).
 constexpr int kSchedHead = 16;
 constexpr int kSchedTail = 512;      // workgroups started after the builder
 constexpr int kSchedBuckets = 1024;  // cost >> 8 (256-cycle buckets), clamped
@@ -1043,6 +1045,10 @@ __device__ __forceinline__ void sched_build(const RenderArgs& a, RenderLds& S, u
   uint32_t* hist = S.img;                       // [kSchedBuckets] (the image is written out)
   uint16_t* key = (uint16_t*)&S.u;              // [n] bucket of env i
   const uint32_t* cost = sched_cost(a);
+#ifdef DTSIM_SCHED_IDENTITY   // diagnostic: the mechanism without the reordering
+  for (int i = tid; i < n; i += T) sched_perm(a, launch + 1u)[i] = i;
+  return;
+#endif
   for (int i = tid; i < kSchedBuckets; i += T) hist[i] = 0u;
   __syncthreads();
   for (int i = tid; i < n; i += T) {
@@ -1081,7 +1087,7 @@ __device__ __forceinline__ void sched_build(const RenderArgs& a, RenderLds& S, u
 
 // the builder's ticket
 __device__ __forceinline__ uint32_t sched_builder(const RenderArgs& a) {
-  return (uint32_t)(a.n > kSchedTail ? a.n - kSchedTail : a.n - 1);
+  return (uint32_t)(a.n - kSchedTail);   // dt_render: n > kSchedTail
 }
 
 // exit of a workgroup: its cost (thread 0, no wait); the builder sorts
@@ -1091,9 +1097,9 @@ __device__ __forceinline__ void sched_exit(const RenderArgs& a, RenderLds& S, in
     __hip_atomic_store(sched_cost(a) + e, dt > 0xFFFFFFFFull ? 0xFFFFFFFFu : (uint32_t)dt,
                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
-  if (S.arrival == sched_builder(a) && a.n <= kSchedMaxN) {   // workgroup-uniform
+  if (blockIdx.x == sched_builder(a) && a.n <= kSchedMaxN) {
     __syncthreads();                      // every wave past its outputs: LDS is free
-    sched_build(a, S, S.launch);
+    sched_build(a, S, a.launch);
   }
 }
 
@@ -1404,21 +1410,8 @@ render_kernel(RenderArgs a) {
 #endif
   if (tid == 64) {
     if (a.sched) {
-      const uint32_t launch =
-          __hip_atomic_load(a.sched, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      const int p = sched_perm(a, launch)[blockIdx.x];
+      const int p = sched_perm(a, a.launch)[blockIdx.x];
       e = (unsigned)p < (unsigned)a.n ? p : (int)blockIdx.x;   // (always a permutation)
-      S.launch = launch;
-      // the ticket, taken after the launch count was read: so when the last
-      // ticket's holder advances the count, every workgroup has read it
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      const uint32_t ticket =
-          __hip_atomic_fetch_add(a.sched + 1, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      S.arrival = ticket;
-      if (ticket == (uint32_t)(a.n - 1)) {
-        __hip_atomic_store(a.sched + 1, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(a.sched, launch + 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
     }
     S.env = e;
     S.t0 = __builtin_amdgcn_s_memtime();
@@ -1873,7 +1866,9 @@ int dt_render(dt_handle* h, const dt_render_io* io, void* stream) {
   a.n = h->n;
   a.spill = (uint16_t*)h->render_spill;
 #ifndef DTSIM_NO_SCHED   // diagnostic builds only (A/B of the dispatch order)
-  a.sched = (uint32_t*)h->render_sched;
+  // a launch of <= kSchedTail workgroups runs all at once: no drain to order
+  a.sched = h->n > kSchedTail ? (uint32_t*)h->render_sched : nullptr;
+  a.launch = h->render_launches++;
 #endif
   a.list_cap = io->list_cap > 0 && io->list_cap < kListCap ? io->list_cap : kListCap;
   hipLaunchKernelGGL(render_kernel, dim3(h->n), dim3(kRenderThreads), 0, (hipStream_t)stream, a);
@@ -1889,15 +1884,13 @@ int dt_render_order(dt_handle* h, uint32_t* launches, uint32_t* cost, int32_t* o
   if (!h || !h->render_sched) return DT_E_ARG;
   DevGuard dg(h->device);
   HIP_OR_FAIL(h, hipDeviceSynchronize());
-  uint32_t head[kSchedHead];
   const uint32_t* base = (const uint32_t*)h->render_sched;
-  HIP_OR_FAIL(h, hipMemcpy(head, base, sizeof(head), hipMemcpyDeviceToHost));
-  if (launches) *launches = head[0];
+  if (launches) *launches = h->render_launches;
   const size_t n = (size_t)h->n;
   if (cost)
     HIP_OR_FAIL(h, hipMemcpy(cost, base + kSchedHead, n * sizeof(uint32_t), hipMemcpyDeviceToHost));
   if (order)
-    HIP_OR_FAIL(h, hipMemcpy(order, base + kSchedHead + n * (1 + (head[0] & 1u)),
+    HIP_OR_FAIL(h, hipMemcpy(order, base + kSchedHead + n * (1 + (h->render_launches & 1u)),
                              n * sizeof(int32_t), hipMemcpyDeviceToHost));
   return DT_OK;
 }

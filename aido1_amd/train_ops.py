@@ -589,6 +589,7 @@ def mlp_plan(seq, parts):
     n2 = lins[1].out_features if len(lins) == 2 else 0
     if (lins[0].in_features != k or (n2 and lins[1].in_features != n1) or m > 256 or k > 1024
             or n1 > (512 if n2 else 1024) or n2 > 64 or m * n1 > 8192 or m * n2 > 2048
+            or n2 * n1 > 4096
             or any(l.weight.dtype != torch.float32 or not l.weight.is_cuda for l in lins)):
         return None
     slope = slopes.pop() if slopes else 0.0

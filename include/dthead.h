@@ -17,7 +17,7 @@
  * chain per element over the rows (dw) or the outputs (dx).  Deterministic;
  * the order differs from a library GEMM's.
  * Limits: m <= 256, k0 + k1 <= 1024, n1 <= 1024 (<= 512 with a second layer),
- * n2 <= 64, m * n1 <= 8192, m * n2 <= 2048; DT_E_ARG otherwise.
+ * n2 <= 64, m * n1 <= 8192, m * n2 <= 2048, n2 * n1 <= 4096; DT_E_ARG otherwise.
  * leaky_relu with slope >= 0 only (its derivative is read from the sign of
  * the saved output).
  * Conventions as dtsim.h: 0 or a negative DT_E_* code; device pointers; work

@@ -173,7 +173,7 @@ def test_render_dispatch_order(gpu):
     launch the next order is a permutation of the envs, sorted by the costs
     recorded when it was built (the last launch's for envs still running
     then), and over launches in that order the outputs stay the oracle's bit
-    for bit."""
+    for bit.  A launch of <= 512 envs runs at once and keeps the identity."""
     from aido1_amd.render import RenderOutput
     from aido1_amd.vec_env import VecEnv
     orend = OC.OracleRender(map_rows('loop_empty'))
@@ -191,8 +191,11 @@ def test_render_dispatch_order(gpu):
             launches, cost, order = env.render_order()
             assert launches == k + 1
             assert np.array_equal(np.sort(order), np.arange(n))          # a permutation
-            assert (cost > 0).all()
-            if k >= 1:   # built mostly from this launch's costs: the longest first, roughly
+            if n <= 512:
+                assert np.array_equal(order, np.arange(n))
+            else:
+                assert (cost > 0).all()
+            if k >= 1 and n > 512:   # built mostly from this launch's costs: the longest first, roughly
                 top = cost[order[:n // 4]].astype(np.float64).mean()
                 assert top >= np.median(cost), (top, np.median(cost))
             g, m, _ = orend.render(x, z, a)

@@ -7,6 +7,7 @@
 #   bench:<args>          bench.py with <args> (commas become spaces)
 #   prof:<config>         rocprofv3 --kernel-trace --stats of bench.py --config <config>
 #   py:<script>[,args]    a tools/ python script
+#   profpy:<script>[,args]  the same under rocprofv3 --kernel-trace --stats (stats + trace kept)
 #   ab:<diag .so>,R[,bench args]  tools/ab.sh: bench.py, product vs a diagnostic build
 # Each step has its own time limit; the first failure ends the call (no retries).
 # Logs: gpurun_out/<TAG>_<n>_<step>.log
@@ -56,7 +57,15 @@ for st in "$@"; do
             --steps 20 --warmup 5 --cpu-steps 0 --no-parity
           f=$(find "/tmp/prof_$arg" -name '*kernel_stats.csv' | head -1)
           cp "$f" "gpurun_out/${TAG}_${arg}_kernel_stats.csv"
+          cp "${f%_kernel_stats.csv}_kernel_trace.csv" "gpurun_out/${TAG}_${arg}_kernel_trace.csv"
           python3 tools/kstats.py "gpurun_out/${TAG}_${arg}_kernel_stats.csv" 25 ;;
+    profpy) set -- $args; s=$1; shift; rm -rf "/tmp/prof_py"
+          run "profpy_$(basename "$s" .py)" 600 rocprofv3 --kernel-trace --stats \
+            --output-format csv -d /tmp/prof_py -o run -- python3 "$ROOT/tools/$s" "$@"
+          f=$(find /tmp/prof_py -name '*kernel_stats.csv' | head -1)
+          cp "$f" "gpurun_out/${TAG}_$(basename "$s" .py)_kernel_stats.csv"
+          cp "${f%_kernel_stats.csv}_kernel_trace.csv" "gpurun_out/${TAG}_$(basename "$s" .py)_kernel_trace.csv"
+          python3 tools/kstats.py "gpurun_out/${TAG}_$(basename "$s" .py)_kernel_stats.csv" 40 ;;
     ab) run ab 900 bash tools/ab.sh $args ;;
     py) set -- $args; s=$1; shift
         run "py_$(basename "$s" .py)" 600 python -u "tools/$s" "$@" ;;
