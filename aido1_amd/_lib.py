@@ -22,7 +22,7 @@ SOURCES = ['dtsim.hip', 'dtrender.hip', 'dtreplay.hip', 'dtactor.hip', 'dtconv.h
 HEADERS = ['dtsim_common.h', 'dtrender.h', 'dtsync.h']
 PUBLIC_HEADERS = ['dtsim.h', 'dtreplay.h', 'dtactor.h', 'dttrain.h', 'dtupd.h', 'dthead.h']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
-ABI_VERSION = 9
+ABI_VERSION = 10
 
 HIP_FLAGS = ['--offload-arch=gfx950', '-O3', '-fPIC', '-shared', '-std=c++17',
              '-ffp-contract=off', '-munsafe-fp-atomics']
@@ -157,6 +157,7 @@ def lib():
             'dt_render': (ctypes.c_int, [vp, vp, vp]),
             'dt_copy_pose': (ctypes.c_int, [vp, vp, vp]),
             'dt_render_order': (ctypes.c_int, [vp, ctypes.POINTER(u32), vp, vp]),
+            'dt_palette_gray': (ctypes.c_int, [ctypes.POINTER(ctypes.c_float)]),
             'dt_default_line_params': (ctypes.c_int, [vp]),
             'dt_set_line_params': (ctypes.c_int, [vp, vp]),
             'dt_line_detect': (ctypes.c_int, [vp, vp, i32, i32, i32, vp, vp, vp]),
@@ -185,8 +186,8 @@ def lib():
             'dt_per_read': (ctypes.c_int, [vp, vp, vp, vp, vp]),
             'dt_per_check': (ctypes.c_int, [vp]),
             'dt_frame_add': (ctypes.c_int, [i32, i64, vp, i64, vp, i32, vp, vp, i32, vp, vp, vp]),
-            'dt_frame_gather': (ctypes.c_int, [i32, vp, vp, i64, i32, vp, vp, vp, vp, vp, vp, vp,
-                                               vp, vp, vp, vp]),
+            'dt_frame_gather': (ctypes.c_int, [i32, vp, vp, i32, i64, i32, vp, vp, vp, vp, vp,
+                                               vp, vp, vp, vp, vp, vp]),
             # dttrain.h
             'dt_train_work_floats': (i64, [i64]),
             'dt_bn_leaky_fwd': (ctypes.c_int, [i64, vp, vp, ctypes.c_float, vp, vp, ctypes.c_float,
@@ -236,6 +237,9 @@ def lib():
             'dt_conv1_split': (ctypes.c_int, [vp, i32, i32, ctypes.POINTER(i32), vp, vp,
                                               ctypes.POINTER(DtConvSet), vp, vp, ctypes.c_float,
                                               vp]),
+            'dt_conv1_index_split': (ctypes.c_int, [vp, i32, i32, ctypes.POINTER(i32), vp, vp,
+                                                    ctypes.POINTER(DtConvSet), vp, vp,
+                                                    ctypes.c_float, vp]),
             'dt_conv1_norm': (ctypes.c_int, [vp, i32, vp, vp, vp, ctypes.c_float, vp]),
             'dt_conv32': (ctypes.c_int, [i32, i32, vp, vp, vp, vp, vp, vp, ctypes.c_float, vp,
                                          vp, vp, vp, ctypes.c_float, ctypes.c_float, vp]),

@@ -435,7 +435,8 @@ class FusedActor(nn.Module):
 
     def _convs_hip(self, ring, order):
         """The four convolutions by the hand-written MFMA kernels (include/dtactor.h):
-        dt_conv1 straight from the f32 ring, then dt_conv32 x3; in reference
+        dt_conv1 straight from the ring (grey f32, or palette-index u8 through
+        dt_conv1_index_split), then dt_conv32 x3; in reference
         mode every per-sample BatchNorm is applied by the next kernel while it
         stages its input (the last one in conv4's epilogue).  Returns the
         flattened [N, 4032] fp16 activation in NCHW order."""
@@ -474,8 +475,9 @@ class FusedActor(nn.Module):
         stream = torch.cuda.current_stream(ring.device).cuda_stream
         ptr = (lambda t: t.data_ptr() if t is not None else None)
         o = (ctypes.c_int32 * 3)(*[int(v) for v in order])
-        rc = L.dt_conv1(ring.data_ptr(), n, slots, o, self.w0frag.data_ptr(),
-                        self.bf[0].data_ptr(), B['y1'].data_ptr(), ptr(B['p1']), 0.01, stream)
+        conv1 = L.dt_conv1_index_split if ring.dtype == torch.uint8 else L.dt_conv1_split
+        rc = conv1(ring.data_ptr(), n, slots, o, self.w0frag.data_ptr(), self.bf[0].data_ptr(),
+                   None, B['y1'].data_ptr(), ptr(B['p1']), 0.01, stream)
         ins = [(B['y1'], B['p1']), (B['y2'], B['p2']), (B['y3'], B['p3'])]
         outs = [(B['y2'], B['p2']), (B['y3'], B['p3']), (flat, None)]
         for layer in range(3):
@@ -498,7 +500,7 @@ class FusedActor(nn.Module):
     def _pairable(self, other, x):
         return (other is not None and other.mode == self.mode and x.is_cuda and
                 self.dtype == torch.float16 and other.dtype == torch.float16 and
-                x.dtype == torch.float32 and x.is_contiguous() and
+                x.dtype in (torch.float32, torch.uint8) and x.is_contiguous() and
                 tuple(x.shape[2:]) == (120, 160) and x.shape[1] >= 3 and
                 self.w[0].shape == (32, 3, 8, 8) and other.w[0].shape == (32, 3, 8, 8))
 
@@ -539,9 +541,9 @@ class FusedActor(nn.Module):
         ptr = (lambda t: t.data_ptr() if t is not None else None)
         o = (ctypes.c_int32 * 3)(*[int(v) for v in order])
         s1 = _lib.DtConvSet(n0, other.w0frag.data_ptr(), other.bf[0].data_ptr())
-        rc = L.dt_conv1_split(x.data_ptr(), n, x.shape[1], o, self.w0frag.data_ptr(),
-                              self.bf[0].data_ptr(), ctypes.byref(s1), B['y1'].data_ptr(),
-                              ptr(B['p1']), 0.01, stream)
+        conv1 = L.dt_conv1_index_split if x.dtype == torch.uint8 else L.dt_conv1_split
+        rc = conv1(x.data_ptr(), n, x.shape[1], o, self.w0frag.data_ptr(), self.bf[0].data_ptr(),
+                   ctypes.byref(s1), B['y1'].data_ptr(), ptr(B['p1']), 0.01, stream)
         ins = [(B['y1'], B['p1']), (B['y2'], B['p2']), (B['y3'], B['p3'])]
         outs = [(B['y2'], B['p2']), (B['y3'], B['p3']), (flat, None)]
         for layer in range(3):
@@ -611,7 +613,8 @@ class FusedActor(nn.Module):
     @torch.no_grad()
     def forward(self, x, order=None):
         """x: [N,3,120,160] stack (oldest first), or the frame ring with
-        `order` = ring slots oldest->newest (RenderOutput.order())."""
+        `order` = ring slots oldest->newest (RenderOutput.order()); grey
+        float32 or palette-index uint8 frames (render.py)."""
         # MIOpen's heuristic choice for conv2 at these shapes is a 2.5 ms CK
         # kernel; its benchmark-mode search finds a 0.57 ms one (once per shape)
         with torch.backends.cudnn.flags(enabled=True, benchmark=True,
@@ -620,7 +623,8 @@ class FusedActor(nn.Module):
 
     def _forward(self, x, order):
         ref = self.mode == 'reference'
-        if (x.is_cuda and self.dtype == torch.float16 and x.dtype == torch.float32 and
+        if (x.is_cuda and self.dtype == torch.float16 and
+                x.dtype in (torch.float32, torch.uint8) and
                 x.is_contiguous() and tuple(x.shape[2:]) == (120, 160) and x.shape[1] >= 3 and
                 self.w[0].shape == (32, 3, 8, 8)):
             # the fp16 product path: all four convs are the hand-written MFMA kernels
@@ -629,6 +633,8 @@ class FusedActor(nn.Module):
                 out = torch.empty(x.shape[0], 2, dtype=torch.float32, device=x.device)
                 return self._heads(None, x, x.shape[0], out)
         else:
+            from aido1_amd.render import as_gray
+            x = as_gray(x)
             w0 = self.w[0]
             if order is not None:
                 inv = sorted(range(len(order)), key=lambda c: order[c])

@@ -13,8 +13,10 @@
 
 #include <cstdint>
 #include <cstdlib>
+#include <type_traits>
 
 #include "../../include/dtactor.h"
+#include "dtrender.h"   // dr::kPalGray: the grey levels of palette-index frames
 
 // diagnostic builds only (tools/conv32_micro.py): bit 0 skips the prefetch
 // loads, 1 the MFMA section, 2 the output stores, 3 the statistics, 4 the ring
@@ -208,7 +210,7 @@ constexpr int kSPre = (s_max_new() * kSQuads + kSThreads - 1) / kSThreads;
 __device__ unsigned int g_conv1_oob;
 #define CONV1_CHECK(p)                                                          \
   do {                                                                          \
-    const size_t e_ = (size_t)((p) - ring);                                     \
+    const size_t e_ = (size_t)((p) - ringT);                                    \
     if (e_ + 4 > (size_t)n * (size_t)slots * plane) atomicOr(&g_conv1_oob, 1u); \
   } while (0)
 #else
@@ -217,12 +219,20 @@ __device__ unsigned int g_conv1_oob;
   } while (0)
 #endif
 
-template <bool kStats>
+// kIdx: the ring holds palette-index frames (u8, dt_render_io.index): a load
+// item is one 32-bit word of 4 pixels a frame instead of a float4, decoded to
+// the same grey floats (dr::kPalGray) at the commit, so every fp16 value and
+// every output equals the grey ring's.
+template <bool kStats, bool kIdx>
 __global__ void __launch_bounds__(kSThreads, 2)   // 2 waves / SIMD: <= 256 registers
-conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, int s2,
+conv1s_kernel(int n, const void* __restrict__ ring, int slots, int s0, int s1, int s2,
               const half8* __restrict__ wfrag, const float* __restrict__ bias,
               __half* __restrict__ y, float* __restrict__ partials, float slope, WeightSplit ws) {
+  using Elem = typename std::conditional<kIdx, uint8_t, float>::type;
+  using Item = typename std::conditional<kIdx, uint32_t, float4>::type;
+  const Elem* __restrict__ ringT = static_cast<const Elem*>(ring);
   __shared__ __attribute__((aligned(16))) unsigned char rb[kSRing * kSRowB];
+  __shared__ float s_gray[8];
   __shared__ float red[kSW][CO][3];
   __shared__ float s_bias[CO];
   __shared__ float s_c[CO];   // the sample's centre (kStats): its pixel-0 outputs
@@ -254,35 +264,48 @@ conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, 
   // range's first quad, the sample is clamped), so the compiler's vmcnt waits
   // stay exact.  A step may add no rows (r0 = r1 + 1, up to IH at the end of a
   // sample): its loads then read the sample's row 0, never past the plane.
-  auto issue = [&](float4 (&pre)[kSPre][3], int k, int r0, int r1) __attribute__((always_inline)) {
+  auto issue = [&](Item (&pre)[kSPre][3], int k, int r0, int r1) __attribute__((always_inline)) {
     const int rows = r1 - r0 + 1;
     const int ns = sample(k) < send ? sample(k) : send - 1;
-    const float* base = ring + (size_t)ns * slots * plane + (size_t)(rows > 0 ? r0 : 0) * IW;
-    const float* p0 = base + (size_t)s0 * plane;
-    const float* p1 = base + (size_t)s1 * plane;
-    const float* p2 = base + (size_t)s2 * plane;
+    const Elem* base = ringT + (size_t)ns * slots * plane + (size_t)(rows > 0 ? r0 : 0) * IW;
+    const Elem* p0 = base + (size_t)s0 * plane;
+    const Elem* p1 = base + (size_t)s1 * plane;
+    const Elem* p2 = base + (size_t)s2 * plane;
 #pragma unroll
     for (int i = 0; i < kSPre; ++i) {
       const int off = it_r[i] < rows ? it_off[i] : 0;
       CONV1_CHECK(p0 + off);
       CONV1_CHECK(p1 + off);
       CONV1_CHECK(p2 + off);
-      pre[i][0] = *reinterpret_cast<const float4*>(p0 + off);
-      pre[i][1] = *reinterpret_cast<const float4*>(p1 + off);
-      pre[i][2] = *reinterpret_cast<const float4*>(p2 + off);
+      pre[i][0] = *reinterpret_cast<const Item*>(p0 + off);
+      pre[i][1] = *reinterpret_cast<const Item*>(p1 + off);
+      pre[i][2] = *reinterpret_cast<const Item*>(p2 + off);
+    }
+  };
+  // a load item's 4 pixels of one frame as grey floats
+  auto px4 = [&](const Item& it, float (&o)[4]) __attribute__((always_inline)) {
+    if constexpr (kIdx) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = s_gray[(it >> (8 * e)) & 7u];
+    } else {
+      o[0] = it.x;
+      o[1] = it.y;
+      o[2] = it.z;
+      o[3] = it.w;
     }
   };
   // fp16 4-channel pixels (channel 3 = 0) into the ring: row R of the stream
   // (k * IH + r) sits in slot R % kSRing
-  auto commit = [&](const float4 (&pre)[kSPre][3], int k, int r0, int r1) __attribute__((always_inline)) {
+  auto commit = [&](const Item (&pre)[kSPre][3], int k, int r0, int r1) __attribute__((always_inline)) {
     const int rows = r1 - r0 + 1;
 #pragma unroll
     for (int i = 0; i < kSPre; ++i) {
       if (it_r[i] >= rows) continue;
       const int slot = (k * IH + r0 + it_r[i]) & (kSRing - 1);
-      const float av[4] = {pre[i][0].x, pre[i][0].y, pre[i][0].z, pre[i][0].w};
-      const float bv[4] = {pre[i][1].x, pre[i][1].y, pre[i][1].z, pre[i][1].w};
-      const float cv[4] = {pre[i][2].x, pre[i][2].y, pre[i][2].z, pre[i][2].w};
+      float av[4], bv[4], cv[4];
+      px4(pre[i][0], av);
+      px4(pre[i][1], bv);
+      px4(pre[i][2], cv);
       if constexpr (kK192) {
         // 4 pixels x 3 channels, pixel-major: (a0 b0)(c0 a1)(b1 c1)(a2 b2)(c2 a3)(b3 c3)
         const float f[12] = {av[0], bv[0], cv[0], av[1], bv[1], cv[1],
@@ -334,11 +357,12 @@ conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, 
     for (int s = 0; s < kSMfma; ++s) wa[s] = wfrag[s * 64 + lane];
   }
   if (tid < CO) s_bias[tid] = bias[tid];
+  if (kIdx && tid < 8) s_gray[tid] = dr::kPalGray[tid];
   float w_cnt = 0.0f, w_mean[16], w_m2[16];
 #pragma unroll
   for (int r = 0; r < 16; ++r) w_mean[r] = w_m2[r] = 0.0f;
 
-  auto step = [&](int g, int k, int j, float4 (&nxt)[kSPre][3], const float4 (&cur)[kSPre][3]) __attribute__((always_inline)) {
+  auto step = [&](int g, int k, int j, Item (&nxt)[kSPre][3], const Item (&cur)[kSPre][3]) __attribute__((always_inline)) {
     const int ns = sample(k);
     const bool last_j = j + 1 == kSSteps;
     const int k1 = last_j ? k + 1 : k, j1 = last_j ? 0 : j + 1;   // step g+1
@@ -459,8 +483,9 @@ conv1s_kernel(int n, const float* __restrict__ ring, int slots, int s0, int s1, 
   };
 
   // prologue: step 0's rows into the ring, step 1's into registers
-  float4 pa[kSPre][3], pb[kSPre][3];
+  Item pa[kSPre][3], pb[kSPre][3];
   issue(pa, 0, 0, s_hi(0));
+  if (kIdx) __syncthreads();   // s_gray
   commit(pa, 0, 0, s_hi(0));
   if (total > 1) issue(pb, kSSteps == 1 ? 1 : 0, s_first_new(0), s_last_new(0));
   __syncthreads();
@@ -965,9 +990,11 @@ constexpr int kConv2Waves = 2, kConv3Waves = 2, kConv4Waves = 4;
 
 }  // namespace
 
-extern "C" int dt_conv1_split(const float* ring, int32_t n, int32_t slots, const int32_t* order,
-                              const void* wfrag, const float* bias, const dt_conv_set* set2,
-                              void* y, float* partials, float slope, void* stream) {
+namespace {
+template <bool kIdx>
+int conv1_launch(const void* ring, int32_t n, int32_t slots, const int32_t* order,
+                 const void* wfrag, const float* bias, const dt_conv_set* set2, void* y,
+                 float* partials, float slope, void* stream) {
   if (!ring || !wfrag || !bias || !y || !order || n < 0 || slots < 3) return DT_E_ARG;
   for (int i = 0; i < 3; ++i)
     if (order[i] < 0 || order[i] >= slots) return DT_E_ARG;
@@ -978,8 +1005,9 @@ extern "C" int dt_conv1_split(const float* ring, int32_t n, int32_t slots, const
     int dev = 0, cus = 256, per = 2;
     if (hipGetDevice(&dev) == hipSuccess)
       (void)hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev);
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, conv1s_kernel<true>, kSThreads, 0) !=
-            hipSuccess || per < 1)
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per, conv1s_kernel<true, kIdx>, kSThreads,
+                                                     0) != hipSuccess ||
+        per < 1)
       per = 1;
     grid = per * cus;
   }
@@ -990,14 +1018,28 @@ extern "C" int dt_conv1_split(const float* ring, int32_t n, int32_t slots, const
   }
   const int g = split_grid(ws, n, set2 ? set2->n0 : n, grid);
   if (partials)
-    hipLaunchKernelGGL(conv1s_kernel<true>, dim3(g), dim3(kSThreads), 0, (hipStream_t)stream, n,
-                       ring, slots, order[0], order[1], order[2], (const half8*)wfrag, bias,
-                       (__half*)y, partials, slope, ws);
+    hipLaunchKernelGGL((conv1s_kernel<true, kIdx>), dim3(g), dim3(kSThreads), 0,
+                       (hipStream_t)stream, n, ring, slots, order[0], order[1], order[2],
+                       (const half8*)wfrag, bias, (__half*)y, partials, slope, ws);
   else
-    hipLaunchKernelGGL(conv1s_kernel<false>, dim3(g), dim3(kSThreads), 0, (hipStream_t)stream, n,
-                       ring, slots, order[0], order[1], order[2], (const half8*)wfrag, bias,
-                       (__half*)y, nullptr, slope, ws);
+    hipLaunchKernelGGL((conv1s_kernel<false, kIdx>), dim3(g), dim3(kSThreads), 0,
+                       (hipStream_t)stream, n, ring, slots, order[0], order[1], order[2],
+                       (const half8*)wfrag, bias, (__half*)y, nullptr, slope, ws);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+}  // namespace
+
+extern "C" int dt_conv1_split(const float* ring, int32_t n, int32_t slots, const int32_t* order,
+                              const void* wfrag, const float* bias, const dt_conv_set* set2,
+                              void* y, float* partials, float slope, void* stream) {
+  return conv1_launch<false>(ring, n, slots, order, wfrag, bias, set2, y, partials, slope, stream);
+}
+
+extern "C" int dt_conv1_index_split(const uint8_t* ring, int32_t n, int32_t slots,
+                                    const int32_t* order, const void* wfrag, const float* bias,
+                                    const dt_conv_set* set2, void* y, float* partials, float slope,
+                                    void* stream) {
+  return conv1_launch<true>(ring, n, slots, order, wfrag, bias, set2, y, partials, slope, stream);
 }
 
 extern "C" int dt_conv1(const float* ring, int32_t n, int32_t slots, const int32_t* order,

@@ -38,6 +38,21 @@ constexpr uint32_t kPalette[PAL_N] = {
     kYellowRgb,
     kYellowRgb,
     rgb_pack(250, 250, 250)};  // white edge line
+// The grey level of a palette byte: PreliminaryTransformer's rgb2gray of its
+// colour (0.2125 R + 0.7154 G + 0.0721 B on [0, 1] channels in float64, then
+// float32; utils/reward_shaping/env_utils.py:48-51).  A grey frame is this
+// table applied to the frame's palette bytes, so a palette-index frame (u8)
+// decodes to the grey frame bit for bit (dt_palette_gray, dt_conv1_index_split,
+// dt_frame_gather).
+__host__ __device__ constexpr float pal_gray_of(uint32_t p) {
+  return (float)(((double)((p >> 16) & 255) * (1.0 / 255.0) * 0.2125 +
+                  (double)((p >> 8) & 255) * (1.0 / 255.0) * 0.7154) +
+                 (double)(p & 255) * (1.0 / 255.0) * 0.0721);
+}
+constexpr float kPalGray[PAL_N] = {pal_gray_of(kPalette[0]), pal_gray_of(kPalette[1]),
+                                   pal_gray_of(kPalette[2]), pal_gray_of(kPalette[3]),
+                                   pal_gray_of(kPalette[4]), pal_gray_of(kPalette[5]),
+                                   pal_gray_of(kPalette[6]), pal_gray_of(kPalette[7])};
 
 // OpenCV RGB2HSV_b fixed-point tables (hsv_shift = 12):
 //   sdiv[i] = round((255 << 12) / i), hdiv180[i] = round((180 << 12) / (6 i)).

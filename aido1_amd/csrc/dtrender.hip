@@ -293,6 +293,7 @@ struct RenderArgs {
   const float4* marks;
   int32_t n_yellow, n_white;
   float* gray;
+  uint8_t* index;   // [n, slots, 120, 160] palette bytes (dt_render_io.index), or null
   int32_t slots, slot;
   const uint8_t* fresh;
   uint8_t* masks;
@@ -927,11 +928,28 @@ __device__ __forceinline__ void write_outputs(const RenderArgs& a, RenderLds& S,
                          a.spill + (size_t)e * kSpillHalves + 4 * NW, a.list_cap};
   const bool fresh = a.fresh != nullptr && a.fresh[e] != 0;
   float* gbase = a.gray ? a.gray + (size_t)e * a.slots * NPIX : nullptr;
+  uint8_t* ibase = a.index ? a.index + (size_t)e * a.slots * NPIX : nullptr;
   const uint32_t blo = S.bits_lo, bhi = S.bits_hi;
   const bool quick_masks = L.dil_r <= 1;
   const int lane = tid & 63;
   for (int q0 = 0; q0 < NQ; q0 += T) {
     const int wbase = 4 * (q0 + (tid - lane));
+    if (ibase) {   // the palette bytes themselves (4 pixels a word)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int w = wbase + 64 * j + lane;
+        if (w < NW) {
+          const uint32_t v = S.img[w] & kPalMask;
+          if (fresh) {
+#pragma clang loop vectorize(disable) interleave(disable)
+            for (int k = 0; k < a.slots; ++k)
+              *reinterpret_cast<uint32_t*>(ibase + k * NPIX + 4 * w) = v;
+          } else {
+            *reinterpret_cast<uint32_t*>(ibase + a.slot * NPIX + 4 * w) = v;
+          }
+        }
+      }
+    }
     if (gbase) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -1381,10 +1399,7 @@ render_kernel(RenderArgs a) {
   if (tid < PAL_N) {
     const uint32_t p = kPalette[tid];
     S.pal_swar[tid] = swar_of(p);
-    const double inv = 1.0 / 255.0;
-    const double rr = (double)((p >> 16) & 255) * inv, gg = (double)((p >> 8) & 255) * inv,
-                 bb = (double)(p & 255) * inv;
-    S.pal_gray[tid] = (float)((rr * 0.2125 + gg * 0.7154) + bb * 0.0721);
+    S.pal_gray[tid] = kPalGray[tid];
   }
   if (tid == 0) {
     S.bits_lo = L.pal_bits[0];
@@ -1834,7 +1849,8 @@ int dt_set_line_params(dt_handle* h, const dt_line_params* p) {
 
 int dt_render(dt_handle* h, const dt_render_io* io, void* stream) {
   if (!h || !io) return DT_E_ARG;
-  if (io->gray && (io->gray_slots < 1 || io->gray_slot < 0 || io->gray_slot >= io->gray_slots)) {
+  if ((io->gray || io->index) &&
+      (io->gray_slots < 1 || io->gray_slot < 0 || io->gray_slot >= io->gray_slots)) {
     h->err = "dt_render: gray_slot out of range";
     return DT_E_ARG;
   }
@@ -1857,6 +1873,7 @@ int dt_render(dt_handle* h, const dt_render_io* io, void* stream) {
   a.n_yellow = h->n_yellow;
   a.n_white = h->n_white;
   a.gray = io->gray;
+  a.index = io->index;
   a.slots = io->gray_slots < 1 ? 1 : io->gray_slots;
   a.slot = io->gray_slot;
   a.fresh = io->fresh;
@@ -1877,6 +1894,12 @@ int dt_render(dt_handle* h, const dt_render_io* io, void* stream) {
     h->err = std::string("dt_render launch: ") + hipGetErrorString(e);
     return DT_E_HIP;
   }
+  return DT_OK;
+}
+
+int dt_palette_gray(float* gray8) {
+  if (!gray8) return DT_E_ARG;
+  for (int i = 0; i < PAL_N; ++i) gray8[i] = kPalGray[i];
   return DT_OK;
 }
 

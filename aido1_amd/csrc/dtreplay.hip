@@ -16,6 +16,7 @@
 #include <string>
 
 #include "../../include/dtreplay.h"
+#include "dtrender.h"   // dr::kPalGray (palette-index frames)
 
 struct dt_per {
   int device = 0;
@@ -216,8 +217,17 @@ constexpr int kFrameThreads = 256;
 // dt_frame_gather: block (x, b) covers pixels [x * threads, ...) of sample b;
 // a thread reads its pixel from the k frames of obs and of next_obs (each
 // plane read coalesced) and writes the k-float NHWC pixel of each
+template <typename F>
+__device__ __forceinline__ float frame_px(const F* frames, int64_t i) {
+  if constexpr (sizeof(F) == 1)
+    return dr::kPalGray[frames[i] & 7u];
+  else
+    return frames[i];
+}
+
+template <typename F>
 __global__ void __launch_bounds__(kFrameThreads)
-frame_gather_kernel(const int64_t* __restrict__ idx, const float* __restrict__ frames, int64_t hw,
+frame_gather_kernel(const int64_t* __restrict__ idx, const F* __restrict__ frames, int64_t hw,
                     int k, const int32_t* __restrict__ obs_ptr,
                     const int32_t* __restrict__ next_ptr, const float* __restrict__ action,
                     const double* __restrict__ reward, const uint8_t* __restrict__ done,
@@ -233,8 +243,8 @@ frame_gather_kernel(const int64_t* __restrict__ idx, const float* __restrict__ f
   float* o = obs + ((int64_t)b * hw + px) * k;
   float* q = nxt + ((int64_t)b * hw + px) * k;
   for (int c = 0; c < k; ++c) {
-    o[c] = frames[(int64_t)obs_ptr[i * k + c] * hw + px];
-    q[c] = frames[(int64_t)next_ptr[i * k + c] * hw + px];
+    o[c] = frame_px(frames, (int64_t)obs_ptr[i * k + c] * hw + px);
+    q[c] = frame_px(frames, (int64_t)next_ptr[i * k + c] * hw + px);
   }
 }
 
@@ -394,8 +404,8 @@ int dt_per_read(dt_per* h, double* sum_dev, double* min_dev, double* max_priorit
   return DT_OK;
 }
 
-int dt_frame_add(int32_t n, int64_t frame_elems, const float* src, int64_t src_env_stride,
-                 float* dst, int32_t k, int32_t* stack, const uint8_t* done, int32_t base_row,
+int dt_frame_add(int32_t n, int64_t frame_elems, const void* src, int64_t src_env_stride,
+                 void* dst, int32_t k, int32_t* stack, const uint8_t* done, int32_t base_row,
                  int32_t* obs_ptr, int32_t* next_ptr, void* stream) {
   if (n < 0 || k < 1 || frame_elems < 4 || frame_elems % 4 || src_env_stride % 4) return DT_E_ARG;
   if (n == 0) return DT_OK;
@@ -407,20 +417,26 @@ int dt_frame_add(int32_t n, int64_t frame_elems, const float* src, int64_t src_e
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 
-int dt_frame_gather(int32_t batch, const int64_t* idx, const float* frames, int64_t hw,
-                    int32_t k, const int32_t* obs_ptr, const int32_t* next_ptr,
+int dt_frame_gather(int32_t batch, const int64_t* idx, const void* frames, int32_t frame_kind,
+                    int64_t hw, int32_t k, const int32_t* obs_ptr, const int32_t* next_ptr,
                     const float* action, const double* reward, const uint8_t* done, float* obs,
                     float* nxt, float* act, float* rew, float* notdone, void* stream) {
-  if (batch < 0 || hw < 1 || k < 1 || k > 4) return DT_E_ARG;
+  if (batch < 0 || hw < 1 || k < 1 || k > 4 || frame_kind < 0 || frame_kind > 1) return DT_E_ARG;
   if (batch == 0) return DT_OK;
   if (!idx || !frames || !obs_ptr || !next_ptr || !action || !reward || !done || !obs || !nxt ||
       !act || !rew || !notdone)
     return DT_E_ARG;
   const int64_t per = (hw + kFrameThreads - 1) / kFrameThreads;
   if (per > 65535) return DT_E_ARG;
-  frame_gather_kernel<<<dim3((unsigned)per, (unsigned)batch), kFrameThreads, 0,
-                        (hipStream_t)stream>>>(idx, frames, hw, k, obs_ptr, next_ptr, action,
-                                               reward, done, obs, nxt, act, rew, notdone);
+  const dim3 grid((unsigned)per, (unsigned)batch);
+  if (frame_kind == 1)
+    frame_gather_kernel<<<grid, kFrameThreads, 0, (hipStream_t)stream>>>(
+        idx, static_cast<const uint8_t*>(frames), hw, k, obs_ptr, next_ptr, action, reward, done,
+        obs, nxt, act, rew, notdone);
+  else
+    frame_gather_kernel<<<grid, kFrameThreads, 0, (hipStream_t)stream>>>(
+        idx, static_cast<const float*>(frames), hw, k, obs_ptr, next_ptr, action, reward, done,
+        obs, nxt, act, rew, notdone);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 

@@ -9,6 +9,11 @@
 - ``line_detect``: LineDetectorHSV (setImage + _colorFilter for white, yellow,
   red + the Canny edge map) on caller-supplied BGR images.
 - ``stack_view``: the Transformer's oldest-first [N,3,120,160] view of the ring.
+- Palette-index frames (``RenderOutput(frames='index')``): the ring holds each
+  frame's palette bytes (u8, a quarter of the grey frame) instead of its grey
+  floats; ``decode_index`` / ``palette_gray`` give the grey frame bit for bit
+  (the renderer's grey IS the palette's grey table applied to those bytes),
+  and the actor's first conv and the replay's gather decode them on the fly.
 - ``hough_lines`` / ``find_normals`` / ``detect_lines``: LineDetectorHSV's
   _HoughLine, _findNormal and detectLines on those masks.
 """
@@ -29,6 +34,35 @@ RENDER_BYTES_PER_ENV = 4 * NPIX + 4 * NPIX + 24
 # ring's other two slots (Transformer.reset stacks three copies,
 # utils/reward_shaping/env_utils.py:60-63)
 RENDER_BYTES_PER_FRESH = 2 * 4 * NPIX
+# the same with palette-index frames (1 byte a pixel instead of 4)
+RENDER_INDEX_BYTES_PER_ENV = NPIX + 4 * NPIX + 24
+RENDER_INDEX_BYTES_PER_FRESH = 2 * NPIX
+
+_GRAY = {}
+
+
+def palette_gray(device):
+    """The renderer's 8 grey levels (dt_palette_gray) as a float32 tensor on
+    `device`: grey frame = palette_gray[index frame]."""
+    key = str(torch.device(device))
+    if key not in _GRAY:
+        buf = (ctypes.c_float * 8)()
+        if _lib.lib().dt_palette_gray(buf) != 0:
+            raise _lib.DtError('dt_palette_gray failed')
+        _GRAY[key] = torch.tensor(list(buf), dtype=torch.float32, device=device)
+    return _GRAY[key]
+
+
+def decode_index(frames):
+    """Grey frames (float32, same shape) from palette-index frames (uint8)."""
+    if frames.dtype != torch.uint8:
+        raise ValueError('decode_index: uint8 palette-index frames expected')
+    return palette_gray(frames.device)[frames.long()]
+
+
+def as_gray(frames):
+    """frames as grey float32: decoded if they are palette-index frames."""
+    return decode_index(frames) if frames.dtype == torch.uint8 else frames
 
 
 class LineParams(ctypes.Structure):
@@ -65,24 +99,31 @@ class RenderIO(ctypes.Structure):
     _fields_ = [('gray', ctypes.c_void_p), ('gray_slots', ctypes.c_int32),
                 ('gray_slot', ctypes.c_int32), ('fresh', ctypes.c_void_p),
                 ('masks', ctypes.c_void_p), ('rgb', ctypes.c_void_p),
-                ('pose', ctypes.c_void_p), ('list_cap', ctypes.c_int32)]
+                ('pose', ctypes.c_void_p), ('list_cap', ctypes.c_int32),
+                ('index', ctypes.c_void_p)]
+
+
+FRAME_DTYPES = {'gray': torch.float32, 'index': torch.uint8}
 
 
 class RenderOutput:
-    """Device buffers of the observation path for n envs: a 3-slot grey frame
-    ring (the Transformer's stack, see stack_view), the 4 line masks of the
-    latest frame, optionally the RGB raster."""
+    """Device buffers of the observation path for n envs: a 3-slot frame
+    ring (the Transformer's stack, see stack_view) of grey floats
+    (frames='gray') or palette-index bytes (frames='index'), the 4 line masks
+    of the latest frame, optionally the RGB raster."""
 
-    def __init__(self, n, device, slots=3, rgb=False, masks=True, ring=None):
+    def __init__(self, n, device, slots=3, rgb=False, masks=True, ring=None, frames='gray'):
         self.n = n
         self.slots = slots
         self.slot = -1  # slot of the newest frame
+        self.frames = frames
+        dt = FRAME_DTYPES[frames]
         self._all = torch.ones(n, dtype=torch.uint8, device=device)
-        if ring is not None:  # a contiguous [n, slots, 120, 160] f32 view (e.g. a slice)
+        if ring is not None:  # a contiguous [n, slots, 120, 160] view (e.g. a slice)
             assert ring.is_contiguous() and tuple(ring.shape) == (n, slots, H, W)
-            assert ring.dtype == torch.float32
-        self.ring = ring if ring is not None else torch.zeros(n, slots, H, W,
-                                                              dtype=torch.float32, device=device)
+            assert ring.dtype == dt
+        self.ring = ring if ring is not None else torch.zeros(n, slots, H, W, dtype=dt,
+                                                              device=device)
         self.masks = torch.zeros(n, 4, H, W, dtype=torch.uint8, device=device) if masks else None
         self.rgb = torch.zeros(n, H, W, 3, dtype=torch.uint8, device=device) if rgb else None
 
@@ -98,10 +139,12 @@ class RenderOutput:
         """Ring slots oldest -> newest (the Transformer's concatenation order)."""
         return [(self.slot + 1 + k) % self.slots for k in range(self.slots)]
 
-    def stack_view(self):
-        """[n, 3, 120, 160] oldest-first stack (a gather copy; the actor consumes the
-        ring zero-copy by permuting its first conv's input channels instead)."""
-        return self.ring[:, self.order()]
+    def stack_view(self, raw=False):
+        """[n, 3, 120, 160] oldest-first grey stack (a gather copy; the actor
+        consumes the ring zero-copy by permuting its first conv's input channels
+        instead); raw=True keeps the ring's own dtype (index frames as bytes)."""
+        st = self.ring[:, self.order()]
+        return st if raw else as_gray(st)
 
 
 def _render_io(env, out, fresh, pose, list_cap):
@@ -112,12 +155,14 @@ def _render_io(env, out, fresh, pose, list_cap):
                              tuple(pose.shape) != (3, env.n) or pose.device != env.device):
         raise ValueError('pose must be a contiguous float64 [3, %d] tensor on %s'
                          % (env.n, env.device))
-    return RenderIO(ctypes.c_void_p(out.ring.data_ptr()), out.slots, slot,
+    idx = out.ring.dtype == torch.uint8
+    ring = ctypes.c_void_p(out.ring.data_ptr())
+    return RenderIO(None if idx else ring, out.slots, slot,
                     ctypes.c_void_p(fresh.data_ptr()) if fresh is not None else None,
                     ctypes.c_void_p(out.masks.data_ptr()) if out.masks is not None else None,
                     ctypes.c_void_p(out.rgb.data_ptr()) if out.rgb is not None else None,
                     ctypes.c_void_p(pose.data_ptr()) if pose is not None else None,
-                    int(list_cap))
+                    int(list_cap), ring if idx else None)
 
 
 def render_into(env, out, fresh=None, pose=None, list_cap=0):

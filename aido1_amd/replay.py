@@ -25,7 +25,11 @@ decision's ONE new frame per env in a ring of frame blocks (n rows a block,
 frame indices, written by dt_frame_add (include/dtreplay.h) in one kernel
 with the frame copy.  ``sample`` gathers the stacks through them, so it
 returns what the stacked storage returns.  Needs ``size % n == 0`` and
-float32 observations; only ``add_batch_ring`` adds to it.
+float32 observations; only ``add_batch_ring`` adds to it.  The frames keep the
+ring's dtype: a ring of palette-index frames (u8, render.py) is stored as
+such -- a quarter of the grey bytes, 4x the transitions per GiB of HBM -- and
+decoded to the grey float32 observations by ``sample`` / ``gather_into``
+(bit for bit the grey ring's).
 """
 import collections
 import ctypes
@@ -33,6 +37,7 @@ import ctypes
 import torch
 
 from aido1_amd import _lib
+from aido1_amd.render import as_gray
 
 FIELDS = ('obs', 'action', 'reward', 'next_obs', 'done')
 
@@ -142,7 +147,7 @@ class ReplayBuffer:
         n = ring.shape[0]
         p = self._next_idx
         if self.storage is None or p + n > self._maxsize or 2 * n > self._maxsize:
-            nxt = ring[:, list(order)]
+            nxt = as_gray(ring[:, list(order)])
             self.add_batch(obs_t, action, reward, nxt, done)
             return nxt
         self._reserve(n)
@@ -151,7 +156,7 @@ class ReplayBuffer:
         st['action'][p:p + n].copy_(torch.as_tensor(action, device=self.device))
         st['reward'][p:p + n].copy_(torch.as_tensor(reward, device=self.device))
         for k, sl in enumerate(order):
-            st['next_obs'][p:p + n, k].copy_(ring[:, sl])
+            st['next_obs'][p:p + n, k].copy_(as_gray(ring[:, sl]))
         st['done'][p:p + n].copy_(torch.as_tensor(done, device=self.device).to(torch.bool))
         self._advance(n)
         return st['next_obs'][p:p + n]
@@ -173,7 +178,7 @@ class ReplayBuffer:
                              % (n, ring.shape[0]))
         if self.frames is None:
             blocks = self._maxsize // n + 2 * k
-            self.frames = torch.zeros((blocks * n,) + tuple(ring.shape[2:]), dtype=torch.float32,
+            self.frames = torch.zeros((blocks * n,) + tuple(ring.shape[2:]), dtype=ring.dtype,
                                       device=self.device)
             self._stack = torch.zeros(n, k, dtype=torch.int32, device=self.device)
             self.storage = {
@@ -198,6 +203,9 @@ class ReplayBuffer:
             # a new chain (the first add, or a rollout reset): obs_t's k frames
             # become k frame blocks
             obs_t = torch.as_tensor(obs_t, device=self.device)
+            if obs_t.dtype != self.frames.dtype:
+                raise ValueError('frame store: obs_t must be in the ring\'s frame dtype (%s)'
+                                 % self.frames.dtype)
             ar = torch.arange(n, dtype=torch.int32, device=self.device)
             self._stack_lo = self._fblock
             for j in range(k):
@@ -220,11 +228,15 @@ class ReplayBuffer:
         dn = fields[4]
         if self.device.type == 'cuda':
             L = _lib.lib()
-            if not newest[0].is_contiguous() or ring.dtype != torch.float32:
-                raise ValueError('frame store: the ring must be float32 with contiguous frames')
-            fe = newest[0].numel()
+            if (not newest[0].is_contiguous() or ring.dtype != self.frames.dtype
+                    or ring.dtype not in (torch.float32, torch.uint8)):
+                raise ValueError('frame store: the ring must hold float32 or uint8 frames, '
+                                 'contiguous')
+            # dt_frame_add copies 4-byte words
+            sz = ring.element_size()
+            fe, stride = newest[0].numel() * sz // 4, newest.stride(0) * sz // 4
             with torch.cuda.device(self.device):
-                rc = L.dt_frame_add(n, fe, newest.data_ptr(), newest.stride(0),
+                rc = L.dt_frame_add(n, fe, newest.data_ptr(), stride,
                                     self.frames[b * n].data_ptr(), k, self._stack.data_ptr(),
                                     dn.view(torch.uint8).data_ptr(), b * n,
                                     st['obs_ptr'][p].data_ptr(), st['next_ptr'][p].data_ptr(),
@@ -257,8 +269,10 @@ class ReplayBuffer:
         st = self.storage
         if self.frames is not None:
             shp = (idxes.shape[0], st['obs_ptr'].shape[1]) + tuple(self.frames.shape[1:])
-            obs = self.frames.index_select(0, st['obs_ptr'].index_select(0, idxes).reshape(-1))
-            nxt = self.frames.index_select(0, st['next_ptr'].index_select(0, idxes).reshape(-1))
+            obs = as_gray(self.frames.index_select(
+                0, st['obs_ptr'].index_select(0, idxes).reshape(-1)))
+            nxt = as_gray(self.frames.index_select(
+                0, st['next_ptr'].index_select(0, idxes).reshape(-1)))
             return (obs.view(shp), st['action'].index_select(0, idxes),
                     st['reward'].index_select(0, idxes), nxt.view(shp),
                     st['done'].index_select(0, idxes))
@@ -279,8 +293,9 @@ class ReplayBuffer:
             k = st['obs_ptr'].shape[1]
             hw = self.frames[0].numel()
             idxes = idxes.contiguous()
+            kind = 1 if self.frames.dtype == torch.uint8 else 0
             rc = _lib.lib().dt_frame_gather(
-                b, idxes.data_ptr(), self.frames.data_ptr(), hw, k, st['obs_ptr'].data_ptr(),
+                b, idxes.data_ptr(), self.frames.data_ptr(), kind, hw, k, st['obs_ptr'].data_ptr(),
                 st['next_ptr'].data_ptr(), st['action'].data_ptr(), st['reward'].data_ptr(),
                 st['done'].data_ptr(), out['obs'].data_ptr(), out['nxt'].data_ptr(),
                 out['act'].data_ptr(), out['rew'].data_ptr(), out['notdone'].data_ptr(),

@@ -20,6 +20,12 @@ TrainLoop gives it the target actor, which the reference's exploiters
 hard-copy, explorers.py:104-105) with epsilon 0: no noise, no random actions,
 the action the clipped actor output (explorers.py:116, 182-184).  The OU
 process still advances for them, as the reference samples it every step.
+
+frames='index' (the default) keeps the ring as palette-index frames (u8,
+render.py): the renderer writes a quarter of the bytes, the actor's first conv
+reads a quarter (dt_conv1_index_split), the replay's frame store keeps u8
+frames, and every consumer sees the same grey values bit for bit
+(stack() decodes; frames='gray' keeps float32 grey frames).
 """
 import math
 
@@ -31,7 +37,7 @@ from aido1_amd.config import EnvConfig
 from aido1_amd.episodes import EpisodeTracker
 from aido1_amd.env_wrappers import map_tanh_in_place
 from aido1_amd.explore import FusedExplore, OUNoise, act, explore_actions
-from aido1_amd.render import H, W, RenderOutput
+from aido1_amd.render import FRAME_DTYPES, H, W, RenderOutput, as_gray
 from aido1_amd.vec_env import StepOutput, VecEnv
 
 
@@ -57,14 +63,16 @@ class CycleEpsilon:
 class ActorRollout:
     def __init__(self, config, n_envs=4096, maps=('small_loop', 'zigzag'), device=0, seed=1234,
                  env_id_base=0, actor=None, dtype=torch.float16, masks=True,
-                 actor_mode='reference', fused_explore=True, n_exploit=None, guard=None):
+                 actor_mode='reference', fused_explore=True, n_exploit=None, guard=None,
+                 frames='index'):
         self.config = config
         self.guard = guard      # non-finite guard (guard.py): actor outputs, rewards
         self.device = torch.device('cuda', device)
         self.n = n_envs
         k = len(maps)
         sizes = [n_envs // k + (1 if i < n_envs % k else 0) for i in range(k)]
-        self.ring = torch.zeros(n_envs, 3, H, W, dtype=torch.float32, device=self.device)
+        self.frames = frames
+        self.ring = torch.zeros(n_envs, 3, H, W, dtype=FRAME_DTYPES[frames], device=self.device)
         self.masks = torch.zeros(n_envs, 4, H, W, dtype=torch.uint8, device=self.device) \
             if masks else None
         self.actions = torch.zeros(n_envs, 2, dtype=torch.float32, device=self.device)
@@ -83,7 +91,7 @@ class ActorRollout:
             out.reward, out.reward_mod, out.done = self.reward[sl], self.reward_mod[sl], \
                 self.done[sl]
             ro = RenderOutput(sz, self.device, slots=3, ring=self.ring[sl],
-                              masks=False)
+                              masks=False, frames=frames)
             if masks:
                 ro.masks = self.masks[sl]
             self.envs.append(env)
@@ -137,9 +145,15 @@ class ActorRollout:
     def order(self):
         return self.renders[0].order()
 
-    def stack(self):
-        """[n, 3, 120, 160] oldest-first observation (a copy of the ring)."""
-        return self.ring[:, self.order()]
+    def stack(self, raw=False):
+        """[n, 3, 120, 160] oldest-first observation (a copy of the ring), grey
+        float32; raw=True keeps the ring's dtype (palette-index bytes)."""
+        st = self.ring[:, self.order()]
+        return st if raw else as_gray(st)
+
+    def gray_ring(self):
+        """The ring as grey float32 frames (decoded: a copy for index frames)."""
+        return as_gray(self.ring)
 
     def load_actor(self, actor):
         """The exploring envs act with `actor`'s current weights from the next

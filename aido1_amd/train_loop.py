@@ -65,7 +65,7 @@ class TrainLoop:
                  env_id_base=0, buffer_size=None, prioritized=True, batch_size=None,
                  updates_per_step=1, refresh_every=1, obs_dtype=None, actor_dtype=torch.float16,
                  actor_mode='reference', masks=False, graph=True, overlap=False, n_exploit=None,
-                 save_dir=None, log_dir=None, poll_every=0, check_every=0):
+                 save_dir=None, log_dir=None, poll_every=0, check_every=0, frames='index'):
         t = config['training']
         self.config = config
         self.device = torch.device('cuda', device)
@@ -84,7 +84,7 @@ class TrainLoop:
         self.rollout = ActorRollout(config, n_envs, maps=maps, device=device, seed=seed,
                                     env_id_base=env_id_base, actor=self.trainer.actor,
                                     dtype=actor_dtype, masks=masks, actor_mode=actor_mode,
-                                    n_exploit=n_exploit, guard=self.guard)
+                                    n_exploit=n_exploit, guard=self.guard, frames=frames)
         self.rollout.load_exploit_actor(self.trainer.target_actor)
         size = int(buffer_size or t['buffer_size'])
         gen = torch.Generator(device=self.device)
@@ -115,7 +115,8 @@ class TrainLoop:
 
     def reset(self):
         self.rollout.reset()
-        self.obs = self.rollout.stack()
+        # the frame store keeps the ring's own frames (index bytes or grey)
+        self.obs = self.rollout.stack(raw=self.replay.frame_envs is not None)
 
     def step(self, timing=None, update_timing=None):
         """One decision: rollout, add, and the update(s).  timing: an event

@@ -96,6 +96,9 @@ def parse(argv=None):
     p.add_argument('--actor-dtype', default='float16', choices=['float16', 'float32'],
                    help='actor/train: the acting actor\'s arithmetic (float16 = the fast '
                         'mode; float32 = the reference\'s precision)')
+    p.add_argument('--frames', default='index', choices=['index', 'gray'],
+                   help="actor/train: the frame ring's format: 'index' = palette-index u8 frames "
+                        "(lossless, a quarter of the bytes; render.py), 'gray' = float32 grey")
     p.add_argument('--batch-size', type=int, default=0, help='train: 0 = config.json (64)')
     p.add_argument('--buffer-size', type=int, default=131072)
     p.add_argument('--updates-per-step', type=int, default=1)
@@ -1084,7 +1087,8 @@ def actor_record(args, ctx, K, W, parity=True, dtype=None, cpu=False):
     dev, rank, n = ctx.dev, ctx.rank, args.envs
     torch.manual_seed(args.seed)
     roll = ActorRollout(cfg, n, maps=('small_loop', 'zigzag'), device=dev.index, seed=args.seed,
-                        env_id_base=rank * n, actor_mode=args.actor_mode, dtype=dtype)
+                        env_id_base=rank * n, actor_mode=args.actor_mode, dtype=dtype,
+                        frames=args.frames)
     roll.reset()
     for _ in range(W):
         roll.step()
@@ -1151,7 +1155,7 @@ def actor_record(args, ctx, K, W, parity=True, dtype=None, cpu=False):
         'data': 'synthetic',
         'config': {'workload': 'config4: %d envs/GPU, actor in the loop (ConfigActor, '
                                'config.json), mixed small_loop/zigzag' % n,
-                   'actor_mode': args.actor_mode, 'envs_per_gpu': n,
+                   'actor_mode': args.actor_mode, 'frames': args.frames, 'envs_per_gpu': n,
                    'global_envs': n * ctx.world, 'repeat_actions': 3,
                    'weights': 'random init (no checkpoint offline)',
                    'parallelism': 'env shards (%d x %d), no collective' % (ctx.world, n)},
@@ -1196,7 +1200,7 @@ def train_record(args, ctx, K, W, parity=True, cpu=False):
     loop = TrainLoop(cfg, n, device=dev.index, seed=args.seed, env_id_base=rank * n,
                      buffer_size=args.buffer_size, batch_size=args.batch_size or None,
                      updates_per_step=args.updates_per_step, actor_mode=args.actor_mode,
-                     overlap=args.overlap,
+                     overlap=args.overlap, frames=args.frames,
                      actor_dtype=torch.float32 if args.actor_dtype == 'float32' else torch.float16)
     loop.reset()
     for _ in range(max(W, 2)):
@@ -1276,7 +1280,7 @@ def train_record(args, ctx, K, W, parity=True, cpu=False):
         'dtype': 'f64 env / %s actor / f32 update' % dtype, 'data': 'synthetic',
         'config': {'workload': 'config5: %d envs/GPU full DDPG (rollout + GPU prioritized '
                                'replay + update + grad all-reduce)' % n,
-                   'actor_mode': args.actor_mode, 'envs_per_gpu': n,
+                   'actor_mode': args.actor_mode, 'frames': args.frames, 'envs_per_gpu': n,
                    'global_envs': n * ctx.world, 'batch_size_per_gpu': batch,
                    'buffer_size_per_gpu': args.buffer_size,
                    'updates_per_step': args.updates_per_step,

@@ -102,6 +102,15 @@ int dt_conv1_split(const float* ring, int32_t n, int32_t slots, const int32_t* o
                    const void* wfrag, const float* bias, const dt_conv_set* set2, void* y,
                    float* partials, float slope, void* stream);
 
+/* dt_conv1_split on a ring of palette-index frames (u8 [n, slots, 120, 160],
+ * dt_render_io.index): each byte is decoded to its grey level
+ * (dt_palette_gray) as the rows are staged, so y and partials equal
+ * dt_conv1_split's on the grey ring of the same frames bit for bit, from a
+ * quarter of its input bytes. */
+int dt_conv1_index_split(const uint8_t* ring, int32_t n, int32_t slots, const int32_t* order,
+                         const void* wfrag, const float* bias, const dt_conv_set* set2, void* y,
+                         float* partials, float slope, void* stream);
+
 /* dt_conv32 with an optional second weight set (set2 NULL = dt_conv32). */
 int dt_conv32_split(int32_t layer, int32_t n, const void* x, const void* wfrag,
                     const float* bias, const float* prev_part, const float* in_gamma,

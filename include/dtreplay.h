@@ -76,18 +76,20 @@ int dt_per_check(dt_per* h);
  * two stacked observation copies buffers.py:29-36 stores per transition
  * (obs_t, obs_tp1; the Transformer stack of 3 frames each): a decision adds
  * ONE frame per env, and a transition keeps frame-row indices instead.
- *   src        device f32, env e's newest frame at src + e * src_env_stride
- *              (the rollout ring's newest slot); frame_elems floats a frame,
- *              a multiple of 4, src and dst 16-B aligned
- *   dst        device f32 [n, frame_elems]: frame rows base_row .. base_row + n - 1
+ *   src        device, env e's newest frame at src + e * src_env_stride
+ *              4-byte words (the rollout ring's newest slot); frames are copied
+ *              as opaque words: f32 grey, or 4 u8 palette-index pixels a word
+ *              (dt_render_io.index); frame_elems words a frame, a multiple of
+ *              4, src and dst 16-B aligned
+ *   dst        device [n, frame_elems] words: frame rows base_row .. base_row + n - 1
  *   stack      device int32 [n, k]: each env's current stack as frame rows
  *              (oldest first), advanced in place
  *   done       device uint8 [n] or NULL: respawned envs, whose whole stack
  *              becomes the new row (the renderer refilled every slot)
  *   obs_ptr    device int32 [n, k] out: the stack before (the transition's obs)
  *   next_ptr   device int32 [n, k] out: the stack after (its next_obs) */
-int dt_frame_add(int32_t n, int64_t frame_elems, const float* src, int64_t src_env_stride,
-                 float* dst, int32_t k, int32_t* stack, const uint8_t* done, int32_t base_row,
+int dt_frame_add(int32_t n, int64_t frame_elems, const void* src, int64_t src_env_stride,
+                 void* dst, int32_t k, int32_t* stack, const uint8_t* done, int32_t base_row,
                  int32_t* obs_ptr, int32_t* next_ptr, void* stream);
 
 /* dt_frame_gather: a sampled batch of the frame store straight into the
@@ -101,10 +103,13 @@ int dt_frame_add(int32_t n, int64_t frame_elems, const float* src, int64_t src_e
  *   act[b][j] = action[i][j] (j < 2), rew[b] = (float)reward[i],
  *   notdone[b] = done[i] ? 0 : 1
  *   idx device i64 [batch] in [0, size) (unchecked: dt_per_sample's output);
- *   frames f32 [rows, hw]; obs_ptr / next_ptr i32 [size, k]; action f32
- *   [size, 2]; reward f64 [size]; done u8 [size] (torch bool); k <= 4 */
-int dt_frame_gather(int32_t batch, const int64_t* idx, const float* frames, int64_t hw,
-                    int32_t k, const int32_t* obs_ptr, const int32_t* next_ptr,
+ *   frames [rows, hw]: frame_kind 0 f32 grey, 1 u8 palette-index frames
+ *   (dt_render_io.index), decoded through dt_palette_gray's table (so the
+ *   output equals kind 0's on the grey frames bit for bit); obs_ptr /
+ *   next_ptr i32 [size, k]; action f32 [size, 2]; reward f64 [size]; done u8
+ *   [size] (torch bool); k <= 4 */
+int dt_frame_gather(int32_t batch, const int64_t* idx, const void* frames, int32_t frame_kind,
+                    int64_t hw, int32_t k, const int32_t* obs_ptr, const int32_t* next_ptr,
                     const float* action, const double* reward, const uint8_t* done, float* obs,
                     float* nxt, float* act, float* rew, float* notdone, void* stream);
 

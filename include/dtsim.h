@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DT_ABI_VERSION 9  /* 2: curves per tile vary (curve_start), intersections;
+#define DT_ABI_VERSION 10 /* 2: curves per tile vary (curve_start), intersections;
                              3: static objects in dt_map, safety_rad_mult;
                              4: dt_render_io.pose / list_cap, dt_copy_pose,
                                 dt_step_many pose output;
@@ -47,7 +47,10 @@ extern "C" {
                                 dtupd.h (the update's convolutions and the
                                 conv trunk's BatchNorm hand-off);
                              9: dtactor.h dt_episode_account (episode sums and
-                                the finished-episode ring); dt_render_order */
+                                the finished-episode ring); dt_render_order;
+                            10: palette-index frames: dt_render_io.index,
+                                dt_palette_gray, dt_conv1_index_split,
+                                dt_frame_gather frame_kind */
 
 /* error codes */
 #define DT_OK 0
@@ -264,7 +267,18 @@ typedef struct dt_render_io {
   int32_t list_cap;     /* 0 in production.  > 0 lowers the number of non-uniform words
                            the kernel keeps in LDS, so tests exercise the global-memory
                            overflow path (results are identical either way) */
+  uint8_t* index;       /* device [n, gray_slots, 120, 160] u8 palette-index frames, or
+                           NULL: the frame's palette bytes (0..7), same slots / fresh
+                           rules as `gray`.  A quarter of the grey frame's bytes and
+                           lossless: gray = dt_palette_gray's table[index] bit for bit
+                           (the actor's dt_conv1_index_split and dt_frame_gather read
+                           such frames directly) */
 } dt_render_io;
+
+/* The 8 grey levels of the renderer's palette bytes (PreliminaryTransformer's
+ * rgb2gray of each colour, float64 then float32): gray8[b] is the grey frame's
+ * value wherever the index frame holds b.  Host memory. */
+int dt_palette_gray(float* gray8);
 
 /* Replaces, per env and fused in one launch (one workgroup per env, the frame
  * kept in LDS): Simulator.render_obs (build-defined 120x160 ego-centric

@@ -275,6 +275,15 @@ for slots, order, n in ((4, [1, 2, 3], 1100), (3, [2, 0, 1], 37), (3, [0, 1, 2],
     assert L.dt_diag_conv1_oob(ctypes.byref(flag)) == 0
     print(n, flag.value)
     assert flag.value == 0, 'conv1s_kernel read past the ring (n=%%d)' %% n
+    # the palette-index ring (u8, its own exact-size allocation)
+    del ring
+    iring = torch.randint(0, 8, (n, slots, 120, 160), dtype=torch.uint8, device=dev)
+    assert L.dt_conv1_index_split(iring.data_ptr(), n, slots, o, wf.data_ptr(), b.data_ptr(),
+                                  None, y.data_ptr(), part.data_ptr(), 0.01,
+                                  torch.cuda.current_stream().cuda_stream) == 0
+    flag = ctypes.c_uint(7)
+    assert L.dt_diag_conv1_oob(ctypes.byref(flag)) == 0
+    assert flag.value == 0, 'conv1s_kernel read past the index ring (n=%%d)' %% n
 ''' % (os.path.dirname(os.path.dirname(os.path.abspath(__file__))),)
     env = dict(os.environ, DTSIM_DIAG_LIB=_lib.CHECK_LIB_PATH)
     r = subprocess.run([sys.executable, '-c', code], env=env, capture_output=True, text=True,
@@ -317,6 +326,29 @@ def test_split_launch_matches_separate_actors(gpu, mode, n, n0):
     out = fa.forward_pair(fb, ring, order, n0)
     ref = torch.cat([fa(ring[:n0].contiguous(), order), fb(ring[n0:].contiguous(), order)])
     assert torch.allclose(out, ref, atol=1e-3), (out - ref).abs().max()
+
+
+@pytest.mark.parametrize('mode', ['reference', 'eval'])
+@pytest.mark.parametrize('n,n0,slots,order', [(1100, 1100, 4, [1, 2, 3]), (600, 525, 3, [2, 0, 1]),
+                                              (37, 36, 3, [0, 1, 2])])
+def test_index_ring_equals_grey_ring(gpu, mode, n, n0, slots, order):
+    """dt_conv1_index_split on palette-index frames (u8) gives bit for bit
+    what dt_conv1_split gives on their grey frames (render.decode_index), for
+    one weight set and for the exploring / exploiting split, through the whole
+    conv chain; n = 1100 streams several samples per workgroup."""
+    from aido1_amd.actor import ConfigActor, FusedActor
+    from aido1_amd.render import decode_index
+    cfg = golden('reference_config.json')['model']['actor']
+    torch.manual_seed(n)
+    fa = FusedActor(ConfigActor(cfg).to(gpu), dtype=torch.float16, mode=mode)
+    fb = FusedActor(ConfigActor(cfg).to(gpu), dtype=torch.float16, mode=mode)
+    g = torch.Generator(device=gpu).manual_seed(n + 1)
+    idx = torch.randint(0, 8, (n, slots, 120, 160), dtype=torch.uint8, device=gpu, generator=g)
+    grey = decode_index(idx)
+    assert torch.equal(fa._convs_hip(idx, order), fa._convs_hip(grey, order))
+    if n0 < n:
+        assert torch.equal(fa._convs_pair(fb, idx, order, n0).clone(),
+                           fa._convs_pair(fb, grey, order, n0))
 
 
 @pytest.mark.parametrize('n,n0', [(300, 300), (300, 257), (64, 1)])

@@ -73,6 +73,36 @@ def test_ring_and_fresh(gpu):
         assert torch.equal(r[:, 0], r[:, 1]) and torch.equal(r[:, 2], r[:, 1])
 
 
+@pytest.mark.parametrize('map_name', ['loop_empty', 'zigzag'])
+def test_index_frames_decode_to_grey(gpu, map_name):
+    """Palette-index frames (dt_render_io.index): over launches with respawns
+    (fresh refills) the index ring decoded through dt_palette_gray equals the
+    grey ring of the same envs bit for bit, slot by slot, and the newest grey
+    frame is the oracle's."""
+    from aido1_amd.config import EnvConfig
+    from aido1_amd.render import RenderOutput, decode_index
+    from aido1_amd.vec_env import VecEnv
+    n = 300
+    envs = [VecEnv(n, seed=11, config=EnvConfig(map_name=map_name)) for _ in range(2)]
+    outs = [RenderOutput(n, gpu, slots=3, masks=False, frames=f) for f in ('gray', 'index')]
+    for env, out in zip(envs, outs):
+        env.reset()
+        env.render_into(out)
+    g = torch.Generator(device=gpu).manual_seed(1)
+    orend = OC.OracleRender(map_rows(map_name))
+    for t in range(6):
+        acts = torch.rand(n, 2, device=gpu, generator=g) * 2 - 1
+        for env, out in zip(envs, outs):
+            o = env.step_into(acts)
+            env.render_into(out, fresh=o.done)
+        assert outs[1].ring.dtype == torch.uint8 and int(outs[1].ring.max()) <= 7
+        assert torch.equal(decode_index(outs[1].ring), outs[0].ring)
+        assert torch.equal(outs[1].stack_view(), outs[0].stack_view())
+    s = envs[0].get_state()
+    gr, _, _ = orend.render(s['x'], s['z'], s['angle'])
+    assert np.array_equal(outs[0].ring[:, outs[0].slot].cpu().numpy(), gr)
+
+
 # (150, 200) and (480, 640) are past the LDS image (19,200 px): the workspace
 # kernel (dt_line_detect_ws); 480 x 640 is duckietown_rl/env.py:12-16's frame
 @pytest.mark.parametrize('shape', [(120, 160), (37, 53), (1, 1), (96, 200), (150, 200),

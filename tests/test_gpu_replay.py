@@ -118,10 +118,12 @@ def test_per_rejects_like_reference_asserts(gpu):
         one.sample(4, beta=0.4)
 
 
-def test_frame_store_gpu_equals_stacked_per(gpu):
+@pytest.mark.parametrize('index', [False, True])
+def test_frame_store_gpu_equals_stacked_per(gpu, index):
     """dt_frame_add (include/dtreplay.h) behind PrioritizedReplayBuffer's frame
     store: the same sampled indices, weights and stacks as the stacked
-    storage, across wraps and respawns."""
+    storage, across wraps and respawns; index=True stores palette-index
+    frames (u8, copied as 4-byte words) and samples their grey frames."""
     import sys
     sys.path.insert(0, __import__('os').path.dirname(__file__))
     from test_replay import _frame_steps
@@ -130,7 +132,7 @@ def test_frame_store_gpu_equals_stacked_per(gpu):
     n, size = 256, 1024
     a = PrioritizedReplayBuffer(size, 0.6, device=gpu, frame_envs=n)
     b = PrioritizedReplayBuffer(size, 0.6, device=gpu)
-    for t in _frame_steps(a, b, n, 9, g):
+    for t in _frame_steps(a, b, n, 9, g, index=index):
         u = torch.rand(64, generator=g, dtype=torch.float64)
         ra, rb = a.sample(64, 0.4, u=u), b.sample(64, 0.4, u=u)
         for x, y in zip(ra, rb):
@@ -143,11 +145,13 @@ def test_frame_store_gpu_equals_stacked_per(gpu):
         assert torch.equal(x, y)
 
 
-def test_frame_gather_equals_encode_and_trainer_inputs(gpu):
+@pytest.mark.parametrize('index', [False, True])
+def test_frame_gather_equals_encode_and_trainer_inputs(gpu, index):
     """dt_frame_gather (replay.gather_into) writes exactly what _encode_sample
     followed by DDPGTrainer._inputs makes of the same indices: channels_last
     float32 obs / next_obs, actions, float32 rewards, notdone; also for the
-    stacked storage (torch fallback) and indices of every row."""
+    stacked storage (torch fallback) and indices of every row.  index=True:
+    palette-index frames, decoded in the gather (frame_kind 1)."""
     import sys
     sys.path.insert(0, __import__('os').path.dirname(__file__))
     from test_replay import _frame_steps
@@ -157,8 +161,9 @@ def test_frame_gather_equals_encode_and_trainer_inputs(gpu):
     n, size = 256, 1024
     a = PrioritizedReplayBuffer(size, 0.6, device=gpu, frame_envs=n)
     b = PrioritizedReplayBuffer(size, 0.6, device=gpu)
-    for _ in _frame_steps(a, b, n, 7, g):
+    for _ in _frame_steps(a, b, n, 7, g, index=index):
         pass
+    assert a.frames.dtype == (torch.uint8 if index else torch.float32)
     tr = make_trainer(gpu)
     for buf in (a, b):
         for idx in (torch.arange(size, device=gpu), torch.randint(0, size, (64,), device=gpu)):

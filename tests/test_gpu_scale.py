@@ -55,8 +55,9 @@ def test_config4_actor_rollout_at_size(gpu, wseed):
     st = roll.stats()
     assert st['decisions'] == n * 6
     assert n * 6 <= st['sim_steps'] <= n * 18
-    assert torch.isfinite(roll.ring).all()
-    assert float(roll.ring.min()) >= 0.0 and float(roll.ring.max()) <= 1.0
+    assert roll.ring.dtype == torch.uint8 and int(roll.ring.max()) <= 7   # palette-index frames
+    grey = roll.gray_ring()
+    assert float(grey.min()) >= 0.0 and float(grey.max()) <= 1.0
     assert torch.isfinite(r).all() and torch.isfinite(rm).all()
     a = roll.actions
     assert ((a >= 0.0) & (a <= 1.0)).all()          # tanh head mapped a/2 + 0.5 in place

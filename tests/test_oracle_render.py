@@ -99,3 +99,30 @@ def test_render_on_lane(orc):
 def test_render_off_map(orc):
     gray, masks, rgb = orc.render(np.array([-50.0]), np.array([-50.0]), np.array([0.0]))
     assert not rgb.any() and not masks.any() and not gray.any()
+
+
+def test_palette_gray_table_is_the_oracle_grey(orc):
+    """dt_palette_gray (the library's 8 grey levels, which decode palette-index
+    frames): every grey value of oracle frames is the table's entry for that
+    pixel's colour, bit for bit -- so decoding an index frame gives the grey
+    frame.  Host call only (no GPU)."""
+    import ctypes
+    from aido1_amd import _lib
+    buf = (ctypes.c_float * 8)()
+    assert _lib.lib().dt_palette_gray(buf) == 0
+    table = np.array(list(buf), dtype=np.float32)
+    rng = np.random.default_rng(2)
+    n = 16
+    x, z = rng.uniform(0, 3 * 0.61, n), rng.uniform(0, 3 * 0.61, n)
+    a = rng.uniform(-math.pi, math.pi, n)
+    gray, _, rgb = orc.render(x, z, a)
+    cols = {}
+    for c, g in zip(rgb.reshape(-1, 3), gray.reshape(-1)):
+        cols.setdefault(tuple(int(v) for v in c), set()).add(float(g))
+    assert len(cols) >= 4                      # floor / grass / road / markings seen
+    for c, gs in cols.items():
+        assert len(gs) == 1, c                 # one grey per colour
+        g = np.float32(next(iter(gs)))
+        r8, g8, b8 = (v / 255.0 for v in c)
+        assert g == np.float32((r8 * 0.2125 + g8 * 0.7154) + b8 * 0.0721)
+        assert (table == g).any(), (c, g, table)

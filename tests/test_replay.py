@@ -80,23 +80,33 @@ def test_add_batch_ring_equals_add_batch():
         assert torch.equal(a.storage[k], b.storage[k]), k
 
 
-def _frame_steps(a, b, n, steps, g, per=False):
+def _frame_steps(a, b, n, steps, g, per=False, index=False):
     """Feed a (frame store) and b (stacked storage) the same decisions of a
     frame ring with the rollout's semantics: one new frame a decision in the
     slot order advances, and a respawned env's whole stack is its new frame
-    (the renderer's fresh refill).  Yields after every decision."""
+    (the renderer's fresh refill).  index=True: a ring of palette-index
+    frames (u8 [4, 8]; b gets their grey frames).  Yields after every
+    decision."""
+    from aido1_amd.render import as_gray
     dev = a.device
-    ring = torch.rand(n, 3, 2, 4, generator=g).to(dev)
-    obs_a = obs_b = ring[:, [0, 1, 2]].clone()
+    shape = (4, 8) if index else (2, 4)
+
+    def frames(*lead):
+        if index:
+            return torch.randint(0, 8, lead + shape, generator=g, dtype=torch.uint8)
+        return torch.rand(lead + shape, generator=g)
+    ring = frames(n, 3).to(dev)
+    obs_a = ring[:, [0, 1, 2]].clone()
+    obs_b = as_gray(obs_a)
     for t in range(steps):
         order = [(t + 1 + k) % 3 for k in range(3)]
         done = (torch.rand(n, generator=g) < 0.3).to(dev)
-        new = torch.rand(n, 2, 4, generator=g).to(dev)
+        new = frames(n).to(dev)
         ring[:, order[-1]] = new
         ring[done] = new[done, None]
         act = torch.rand(n, 2, generator=g).to(dev)
         rew = torch.rand(n, generator=g, dtype=torch.float64).to(dev)
-        nxt = ring[:, order].clone()
+        nxt = as_gray(ring[:, order].clone())
         b.add_batch(obs_b, act, rew, nxt, done)
         obs_b = nxt
         obs_a = a.add_batch_ring(obs_a, act, rew, ring, order, done)
@@ -104,16 +114,18 @@ def _frame_steps(a, b, n, steps, g, per=False):
         yield t
 
 
-def test_frame_store_samples_equal_stacked_storage():
+@pytest.mark.parametrize('index', [False, True])
+def test_frame_store_samples_equal_stacked_storage(index):
     """The frame store (frame_envs: one frame per env a decision plus frame
     indices) returns the stacks the stacked storage (buffers.py:29-52) returns
-    for the same indices, across many wraps of the buffer and respawns."""
+    for the same indices, across many wraps of the buffer and respawns; a
+    palette-index ring is stored as bytes and sampled as its grey frames."""
     from aido1_amd.replay import ReplayBuffer
     g = torch.Generator().manual_seed(1)
     n, size = 3, 9
     a = ReplayBuffer(size, device='cpu', frame_envs=n)
     b = ReplayBuffer(size, device='cpu')
-    for _ in _frame_steps(a, b, n, 13, g):
+    for _ in _frame_steps(a, b, n, 13, g, index=index):
         assert len(a) == len(b) and a._next_idx == b._next_idx
         u = torch.rand(32, generator=g, dtype=torch.float64)
         for x, y in zip(a.sample(32, u=u), b.sample(32, u=u)):
