@@ -355,10 +355,41 @@ class FusedActor(nn.Module):
         self.register_buffer('w0frag', torch.zeros(16, 64, 8, dtype=torch.float16, device=dev))
         self.register_buffer('wfrag', torch.zeros(3, 32, 64, 8, dtype=torch.float16, device=dev))
         self.register_buffer('bf', torch.zeros(4, 32, device=dev))
-        self.refresh(actor)
+        self.refresh(actor, graph=False)
 
     @torch.no_grad()
-    def refresh(self, actor):
+    def refresh(self, actor, graph=None):
+        """Re-derive the acting weights from `actor`'s current ones, in place.
+        On the GPU the ~12 copy / gather kernels of a refresh are captured into
+        a HIP graph at the first refresh from a given source (its parameters'
+        addresses) and replayed afterwards: the training loop refreshes both
+        acting copies after every update, and issued one by one from Python
+        the kernels left the GPU idle ~0.4 ms a decision (launch gaps).
+        graph=False forces the eager path."""
+        dev = self.w0frag.device
+        if graph is None:
+            graph = dev.type == 'cuda'
+        if not graph:
+            return self._refresh(actor)
+        # the source's tensors are listed once per source module (walking the
+        # module tree costs ~80 us of host time a call); their addresses are
+        # checked on every call, so a source whose storage moved is recaptured
+        srcs = self.__dict__.setdefault('_refresh_srcs', {})
+        ts = srcs.get(id(actor))
+        if ts is None or ts[0] is not actor:
+            ts = srcs[id(actor)] = (actor, list(actor.parameters()) + list(actor.buffers()))
+        key = (id(actor),) + tuple(t.data_ptr() for t in ts[1])
+        cache = self.__dict__.setdefault('_refresh_graphs', {})
+        g = cache.get(key)
+        if g is None:
+            self._refresh(actor)                 # eager once: lazily built index maps, pools
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._refresh(actor)
+            cache[key] = g
+        g.replay()
+
+    def _refresh(self, actor):
         convs, bns, lin1, lin2 = actor.layers()
         if self.mode == 'reference':
             ws = [c.weight for c in convs]

@@ -80,14 +80,16 @@ class ReplayBuffer:
             self.storage[name] = torch.zeros((self._maxsize,) + tuple(t.shape[1:]), dtype=dt,
                                              device=self.device)
 
+    def _field(self, name, x):
+        t = torch.as_tensor(x, device=self.device)
+        if name == 'done':
+            return t.to(torch.bool)
+        return t if t.is_floating_point() else t.to(torch.float32)
+
     def _fields(self, obs_t, action, reward, obs_tp1, done, batched):
         out = []
         for name, x in zip(FIELDS, (obs_t, action, reward, obs_tp1, done)):
-            t = torch.as_tensor(x, device=self.device)
-            if name == 'done':
-                t = t.to(torch.bool)
-            elif not t.is_floating_point():
-                t = t.to(torch.float32)
+            t = self._field(name, x)
             out.append(t if batched else t.unsqueeze(0))
         n = out[0].shape[0]
         if any(t.shape[0] != n for t in out):
@@ -214,18 +216,22 @@ class ReplayBuffer:
         p = self._next_idx
         self._reserve(n)
         st = self.storage
-        fields = self._fields(torch.zeros(n, 1), action, reward, torch.zeros(n, 1), done, True)
+        # device tensors only: a host tensor here would be a blocking copy
+        # that drains the stream every decision
+        fields = {name: self._field(name, x)
+                  for name, x in (('action', action), ('reward', reward), ('done', done))}
+        if any(f.shape[0] != n for f in fields.values()):
+            raise ValueError('add_batch_ring: fields disagree on the batch size')
         if 'action' not in st:
-            for name, f in zip(FIELDS, fields):
-                if name not in ('obs', 'next_obs'):
-                    st[name] = torch.zeros((self._maxsize,) + tuple(f.shape[1:]), dtype=f.dtype,
-                                           device=self.device)
-        st['action'][p:p + n].copy_(fields[1])
-        st['reward'][p:p + n].copy_(fields[2])
-        st['done'][p:p + n].copy_(fields[4])
+            for name, f in fields.items():
+                st[name] = torch.zeros((self._maxsize,) + tuple(f.shape[1:]), dtype=f.dtype,
+                                       device=self.device)
+        st['action'][p:p + n].copy_(fields['action'])
+        st['reward'][p:p + n].copy_(fields['reward'])
+        st['done'][p:p + n].copy_(fields['done'])
         newest = ring[:, order[-1]]
         b = self._fblock % (self.frames.shape[0] // n)
-        dn = fields[4]
+        dn = fields['done']
         if self.device.type == 'cuda':
             L = _lib.lib()
             if (not newest[0].is_contiguous() or ring.dtype != self.frames.dtype

@@ -399,3 +399,29 @@ def test_refresh_copies_every_parameter_exactly(gpu, channels_last):
     for mine, src in ((f.w1, lin1.weight), (f.b1, lin1.bias), (f.w2, lin2.weight),
                       (f.b2, lin2.bias)):
         assert torch.equal(mine.float(), src.detach().half().float())
+
+
+@pytest.mark.parametrize('mode', ['reference', 'eval'])
+def test_graph_refresh_follows_in_place_updates(gpu, mode):
+    """FusedActor.refresh replays a HIP graph captured at the first refresh
+    from a source: after in-place updates of the source's weights (what Adam
+    and the soft update do) every acting tensor equals an eager refresh's."""
+    from aido1_amd.actor import ConfigActor, FusedActor
+    torch.manual_seed(13)
+    a = ConfigActor(golden('reference_config.json')['model']['actor']).to(gpu)
+    f = FusedActor(a, dtype=torch.float16, mode=mode)
+    for k in range(3):
+        with torch.no_grad():
+            for p in a.parameters():
+                p.add_(torch.randn_like(p) * 0.05)
+            for bn in [m for m in a.modules() if isinstance(m, torch.nn.BatchNorm2d)]:
+                bn.running_mean.uniform_(-0.2, 0.2)
+                bn.running_var.uniform_(0.5, 2.0)
+        f.refresh(a)
+        ref = FusedActor(a, dtype=torch.float16, mode=mode)
+        torch.cuda.synchronize()
+        for (name, x), (_, y) in zip(f.state_dict().items(), ref.state_dict().items()):
+            if mode == 'eval' and name.startswith(('gamma', 'beta')):
+                continue            # folded into the weights: unused (never written) in eval mode
+            assert torch.equal(x, y), (k, name)
+    assert len(f._refresh_graphs) == 1
