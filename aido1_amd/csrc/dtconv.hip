@@ -33,6 +33,11 @@
 #ifndef DTCONV1_K192
 #define DTCONV1_K192 1
 #endif
+// conv1s_kernel: resident workgroups a CU of the persistent grid; 0 = as many
+// as the occupancy allows (diagnostic builds fix it)
+#ifndef DTCONV1_PER
+#define DTCONV1_PER 0
+#endif
 
 namespace {
 
@@ -1009,6 +1014,7 @@ int conv1_launch(const void* ring, int32_t n, int32_t slots, const int32_t* orde
                                                      0) != hipSuccess ||
         per < 1)
       per = 1;
+    if (DTCONV1_PER > 0 && DTCONV1_PER < per) per = DTCONV1_PER;
     grid = per * cus;
   }
   WeightSplit ws{};

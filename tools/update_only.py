@@ -46,9 +46,19 @@ def main():
     t_full = timed(lambda: tr.update(batch))
     # the inputs already in the static buffers (TrainLoop: dt_frame_gather)
     t_prep = timed(tr.update_prepared)
+    # back to back, as the training loop issues them (the host runs ahead of
+    # the GPU, so its launch latency is hidden): mean over n_up updates
+    a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(n_up):
+        tr.update_prepared()
+    e.record()
+    torch.cuda.synchronize()
+    t_b2b = a.elapsed_time(e) / n_up
     tr.check()
     print('update %.3f ms with the input conversion + copies, %.3f ms on prepared inputs '
-          '(medians of %d)' % (t_full, t_prep, n_up))
+          '(medians of %d, each synchronised); %.3f ms back to back (mean of %d, host ahead)'
+          % (t_full, t_prep, n_up, t_b2b, n_up))
 
 
 if __name__ == '__main__':
