@@ -229,6 +229,10 @@ def lib():
             'dt_mlp_fwd': (ctypes.c_int, [ctypes.POINTER(DtMlp), vp, vp, vp, vp, vp]),
             'dt_mlp_bwd': (ctypes.c_int, [ctypes.POINTER(DtMlp), vp, vp, vp, vp, vp, vp, vp, vp,
                                           vp, vp, vp, vp]),
+            'dt_mlp_fwd_td': (ctypes.c_int, [ctypes.POINTER(DtMlp), vp, vp, vp, vp, vp, vp,
+                                             ctypes.c_float, vp, vp]),
+            'dt_loss': (ctypes.c_int, [i32, i32, vp, vp, vp, vp]),
+            'dt_loss_bwd': (ctypes.c_int, [i32, i32, vp, vp, vp, vp, vp]),
             # dtactor.h
             'dt_sample_norm': (ctypes.c_int, [vp, vp, i32, i32, i32, vp, vp, ctypes.c_float,
                                               ctypes.c_float, i32, vp]),

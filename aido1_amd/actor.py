@@ -178,6 +178,18 @@ class _Net(nn.Module):       # Net: input_nets / output_nets (modules.py:86-109)
         x = torch.cat(parts, dim=1)
         return [net(x) for net in self.output_nets]
 
+    def td_target(self, inputs, rew, notdone, gamma):
+        """rew + notdone * gamma * forward(*inputs) (training/trainers.py:166-170)
+        without gradients; on the GPU in float32 the output branch and the
+        target are one dt_mlp_fwd_td launch (include/dthead.h)."""
+        parts = [net(v) for net, v in zip(self.input_nets, inputs)]
+        if len(self.output_nets) == 1 and self.output_nets[0].fused_tail and parts[0].is_cuda:
+            from aido1_amd import train_ops
+            plan = train_ops.mlp_plan(self.output_nets[0], parts)
+            if plan is not None and train_ops.td_applicable(parts, rew, notdone):
+                return train_ops.mlp_td(parts, plan, rew, notdone, gamma)
+        return rew + notdone * gamma * self.out(parts)[0]
+
 
 def _build_branch(spec):
     """One branch of config.json's module list -> list of modules (index-aligned
@@ -287,6 +299,11 @@ class ConfigCritic(ConfigNet):
         seq = self.net.input_nets[0]
         x0 = seq.run(t, self._cut(), len(seq.internal_modules))
         return self.net.out([x0] + [net(v) for net, v in zip(self.net.input_nets[1:], rest)])[0]
+
+    def td_target(self, obs, action, rew, notdone, gamma):
+        """rew + notdone * gamma * forward(obs, action), no gradients (the
+        trainer's target y; _Net.td_target)."""
+        return self.net.td_target([obs, action], rew, notdone, gamma)
 
 
 def apply_head(x, head, max_action=1.0):

@@ -87,6 +87,17 @@ __device__ __forceinline__ void load_w(float (&wv)[KW], const float* __restrict_
   }
 }
 
+// The TD target epilogue (dt_mlp_fwd_td): out[r][n] = rew[r] + (notdone[r] *
+// gamma) * y[r][n], the trainer's y = r + notdone * gamma * Q'(s', a') in its
+// operation order (training/trainers.py:166-170); pointers at the workgroup's
+// first row.
+struct Td {
+  const float* rew;
+  const float* notdone;
+  float gamma;
+  float* out;
+};
+
 // out[r][n] = act(b[n] + sum_k in[r][k] w[n][k]) for the workgroup's rows:
 // lane group (kGrp lanes) per output n, kRows accumulators a lane.  wa holds
 // the lane's weights of its first output (load_w); the next output's are in
@@ -95,7 +106,7 @@ template <int KW, int NT>
 __device__ __forceinline__ void layer_fwd(float (&wa)[KW], const float* in, int K,
                                           const float* __restrict__ w, const float* __restrict__ b,
                                           int N, int act, float s, int rows, float* out_lds,
-                                          float* out, int ldo) {
+                                          float* out, int ldo, const Td* td = nullptr) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int grp = lane / kGrp, gl = lane % kGrp;
   constexpr int kPerWave = 64 / kGrp;
@@ -127,6 +138,7 @@ __device__ __forceinline__ void layer_fwd(float (&wa)[KW], const float* in, int 
           const float v = act_fwd(act, acc[r] + bias, s);
           if (out_lds) out_lds[r * N + n] = v;
           if (out) out[(size_t)r * ldo + n] = v;
+          if (td) td->out[(size_t)r * N + n] = td->rew[r] + (td->notdone[r] * td->gamma) * v;
         }
       }
     }
@@ -140,7 +152,7 @@ template <int KW1, int KW2, int NT>
 __global__ void __launch_bounds__(NT) mlp_fwd_kernel(DtMlp p, const float* __restrict__ x0,
                                                      const float* __restrict__ x1,
                                                      float* __restrict__ h,
-                                                     float* __restrict__ y) {
+                                                     float* __restrict__ y, Td td) {
   __shared__ float xs[kRows * kMaxK];
   __shared__ float hs[kRows * kMaxH];
   const int r0 = blockIdx.x * kRows;
@@ -156,14 +168,18 @@ __global__ void __launch_bounds__(NT) mlp_fwd_kernel(DtMlp p, const float* __res
     return k < p.k0 ? x0[(size_t)(r0 + r) * p.k0 + k] : x1[(size_t)(r0 + r) * p.k1 + (k - p.k0)];
   });
   __syncthreads();
+  const int nout = p.n2 > 0 ? p.n2 : p.n1;
+  const Td tdr{td.rew + r0, td.notdone + r0, td.gamma, td.out + (size_t)r0 * nout};
+  const Td* tdp = td.out ? &tdr : nullptr;
   layer_fwd<KW1, NT>(wa, xs, K, p.w1, p.b1, p.n1, p.act1, p.slope, rows,
-                     p.n2 > 0 ? hs : nullptr, h + (size_t)r0 * p.n1, p.n1);
+                     p.n2 > 0 ? hs : nullptr, h + (size_t)r0 * p.n1, p.n1,
+                     p.n2 > 0 ? nullptr : tdp);
   if (p.n2 > 0) {
     float w2[KW2];
     load_w<KW2>(w2, p.w2, p.n1, p.n2, wave * (64 / kGrp) + lane / kGrp, lane % kGrp);
     __syncthreads();
     layer_fwd<KW2, NT>(w2, hs, p.n1, p.w2, p.b2, p.n2, p.act2, p.slope, rows, nullptr,
-                       y + (size_t)r0 * p.n2, p.n2);
+                       y + (size_t)r0 * p.n2, p.n2, tdp);
   }
 }
 
@@ -293,24 +309,90 @@ bool mlp_ok(const DtMlp* p) {
          p->act2 <= 3 && p->slope >= 0.0f && p->w1 && (p->n2 == 0 || p->w2);
 }
 
-}  // namespace
-
-extern "C" {
-
-int dt_mlp_fwd(const DtMlp* p, const float* x0, const float* x1, float* h, float* y,
-               void* stream) {
+int mlp_fwd(const DtMlp* p, const float* x0, const float* x1, float* h, float* y, Td td,
+            void* stream) {
   if (!mlp_ok(p) || !x0 || (p->k1 > 0 && !x1) || !h || (p->n2 > 0 && !y)) return DT_E_ARG;
   const int kw1 = (p->k0 + p->k1 + kGrp - 1) / kGrp, kw2 = (p->n1 + kGrp - 1) / kGrp;
   const dim3 grid((p->m + kRows - 1) / kRows);
   hipStream_t s = (hipStream_t)stream;
   auto go = [&](auto kern, int nt) {
-    hipLaunchKernelGGL(kern, grid, dim3(nt), 0, s, *p, x0, x1, h, y);
+    hipLaunchKernelGGL(kern, grid, dim3(nt), 0, s, *p, x0, x1, h, y, td);
   };
   const bool two = p->n2 > 0;
   if (kw1 <= 16 && (!two || kw2 <= 8)) go(mlp_fwd_kernel<16, 8, 1024>, 1024);
   else if (kw1 <= 32 && (!two || kw2 <= 8)) go(mlp_fwd_kernel<32, 8, 1024>, 1024);
   else if (kw1 <= 32) go(mlp_fwd_kernel<32, 32, 1024>, 1024);
   else go(mlp_fwd_kernel<64, 32, 512>, 512);   // 64 weights a lane: half the lanes
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
+// ---- the two DDPG losses (training/trainers.py:174-177, 193-196) -------------------
+// One workgroup: the f64 sum of the m terms in a fixed tree order, then / m.
+constexpr int kLossThreads = 256;
+
+__device__ double block_sum(double v) {
+  __shared__ double part[kLossThreads / 64];
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = v;
+  __syncthreads();
+  double t = 0.0;
+  for (int w = 0; w < kLossThreads / 64; ++w) t += part[w];
+  return t;
+}
+
+// kind 0: mean((a - b)^2) (F.mse_loss); kind 1: -mean(a) (the actor loss)
+__global__ void __launch_bounds__(kLossThreads) loss_kernel(int kind, int m, const float* a,
+                                                            const float* b, float* loss) {
+  double acc = 0.0;
+  for (int i = threadIdx.x; i < m; i += kLossThreads) {
+    const float d = kind == 0 ? a[i] - b[i] : a[i];
+    acc += kind == 0 ? (double)(d * d) : (double)d;
+  }
+  const double t = block_sum(acc);
+  if (threadIdx.x == 0) *loss = kind == 0 ? (float)(t / m) : (float)(-(t / m));
+}
+
+// d loss / d a for a scalar upstream gradient *g: kind 0: g * 2 (a - b) / m;
+// kind 1: -g / m (both as torch's backward formulas order them)
+__global__ void __launch_bounds__(kLossThreads) loss_bwd_kernel(int kind, int m, const float* a,
+                                                                const float* b, const float* g,
+                                                                float* da) {
+  const float gv = *g;
+  const float norm = 2.0f / (float)m;
+  for (int i = blockIdx.x * kLossThreads + threadIdx.x; i < m; i += gridDim.x * kLossThreads)
+    da[i] = kind == 0 ? norm * (a[i] - b[i]) * gv : -(gv / (float)m);
+}
+
+}  // namespace
+
+extern "C" {
+
+
+int dt_mlp_fwd(const DtMlp* p, const float* x0, const float* x1, float* h, float* y,
+               void* stream) {
+  return mlp_fwd(p, x0, x1, h, y, Td{nullptr, nullptr, 0.0f, nullptr}, stream);
+}
+
+int dt_mlp_fwd_td(const DtMlp* p, const float* x0, const float* x1, float* h, float* y,
+                  const float* rew, const float* notdone, float gamma, float* target,
+                  void* stream) {
+  if (!rew || !notdone || !target) return DT_E_ARG;
+  return mlp_fwd(p, x0, x1, h, y, Td{rew, notdone, gamma, target}, stream);
+}
+
+int dt_loss(int32_t kind, int32_t m, const float* a, const float* b, float* loss, void* stream) {
+  if (kind < 0 || kind > 1 || m < 1 || !a || (kind == 0 && !b) || !loss) return DT_E_ARG;
+  hipLaunchKernelGGL(loss_kernel, dim3(1), dim3(kLossThreads), 0, (hipStream_t)stream, kind, m,
+                     a, b, loss);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
+int dt_loss_bwd(int32_t kind, int32_t m, const float* a, const float* b, const float* g,
+                float* da, void* stream) {
+  if (kind < 0 || kind > 1 || m < 1 || !a || (kind == 0 && !b) || !g || !da) return DT_E_ARG;
+  const int grid = (m + kLossThreads - 1) / kLossThreads;
+  hipLaunchKernelGGL(loss_bwd_kernel, dim3(grid < 64 ? grid : 64), dim3(kLossThreads), 0,
+                     (hipStream_t)stream, kind, m, a, b, g, da);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 

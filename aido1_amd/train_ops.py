@@ -655,3 +655,84 @@ def mlp(parts, plan):
     w1, b1, act1, w2, b2, act2, slope = plan
     x1 = parts[1] if len(parts) == 2 else None
     return _Mlp.apply(parts[0], x1, w1, b1, w2, b2, (act1, act2, slope))
+
+
+def td_applicable(parts, rew, notdone):
+    m = parts[0].shape[0]
+    return all(t.is_cuda and t.dtype == torch.float32 and t.is_contiguous() and t.numel() == m
+               for t in (rew, notdone))
+
+
+@torch.no_grad()
+def mlp_td(parts, plan, rew, notdone, gamma):
+    """The output branch of mlp_plan on `parts` and the TD target
+    rew + (notdone * gamma) * y in one dt_mlp_fwd_td launch; returns the
+    target [m, n_out] (no autograd: the target networks' pass)."""
+    w1, b1, act1, w2, b2, act2, slope = plan
+    x0 = parts[0].contiguous()
+    x1 = parts[1].contiguous() if len(parts) == 2 else None
+    p = _mlp_struct(x0, x1, w1.contiguous(), b1, w2.contiguous() if w2 is not None else None, b2,
+                    act1, act2, slope)
+    dev = x0.device
+    h = torch.empty(p.m, p.n1, device=dev)
+    y = torch.empty(p.m, p.n2, device=dev) if p.n2 else None
+    target = torch.empty(p.m, p.n2 or p.n1, device=dev)
+    rc = _lib.lib().dt_mlp_fwd_td(ctypes.byref(p), x0.data_ptr(),
+                                  x1.data_ptr() if x1 is not None else None, h.data_ptr(),
+                                  y.data_ptr() if y is not None else None, rew.data_ptr(),
+                                  notdone.data_ptr(), float(gamma), target.data_ptr(),
+                                  torch.cuda.current_stream(dev).cuda_stream)
+    if rc != 0:
+        raise _lib.DtError('dt_mlp_fwd_td failed (%d)' % rc)
+    return target
+
+
+# ---- the DDPG losses (include/dthead.h dt_loss) ------------------------------------------
+class _Loss(torch.autograd.Function):
+    """kind 0: F.mse_loss(a, b) (mean); kind 1: -mean(a).  One launch forward,
+    one backward (gradient for `a` only: b is the detached target)."""
+
+    @staticmethod
+    def forward(ctx, a, b, kind):
+        a = a.contiguous()
+        b = b.contiguous() if b is not None else None
+        loss = torch.empty((), device=a.device)
+        rc = _lib.lib().dt_loss(kind, a.numel(), a.data_ptr(),
+                                b.data_ptr() if b is not None else None, loss.data_ptr(),
+                                torch.cuda.current_stream(a.device).cuda_stream)
+        if rc != 0:
+            raise _lib.DtError('dt_loss failed (%d)' % rc)
+        ctx.kind = kind
+        ctx.save_for_backward(a, b)
+        return loss
+
+    @staticmethod
+    def backward(ctx, g):
+        a, b = ctx.saved_tensors
+        g = g.contiguous()
+        da = torch.empty_like(a)
+        rc = _lib.lib().dt_loss_bwd(ctx.kind, a.numel(), a.data_ptr(),
+                                    b.data_ptr() if b is not None else None, g.data_ptr(),
+                                    da.data_ptr(), torch.cuda.current_stream(a.device).cuda_stream)
+        if rc != 0:
+            raise _lib.DtError('dt_loss_bwd failed (%d)' % rc)
+        return da, None, None
+
+
+def _loss_applicable(*ts):
+    return all(t.is_cuda and t.dtype == torch.float32 for t in ts) and \
+        len({t.numel() for t in ts}) == 1
+
+
+def mse_loss(a, b):
+    """F.mse_loss(a, b) (b without gradient) in one launch each way on the GPU."""
+    if _loss_applicable(a, b) and not b.requires_grad:
+        return _Loss.apply(a, b.detach(), 0)
+    return F.mse_loss(a, b)
+
+
+def neg_mean(a):
+    """-1.0 * torch.mean(a) (the actor loss) in one launch each way on the GPU."""
+    if _loss_applicable(a):
+        return _Loss.apply(a, None, 1)
+    return -1.0 * torch.mean(a)

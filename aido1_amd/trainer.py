@@ -48,6 +48,7 @@ from aido1_amd.distributed import GradAllReduce, world
 from aido1_amd.explore import create_decay_fn
 from aido1_amd.guard import Guard
 from aido1_amd.optim import DeviceAdam, SoftUpdate, make_optimizer
+from aido1_amd import train_ops
 
 
 class TrainingDecay:
@@ -122,7 +123,6 @@ class DDPGTrainer:
         # block, read only by check()
         self.guard = guard if guard is not None else Guard(self.device)
         if self.device.type == 'cuda':
-            from aido1_amd import train_ops
             for m in (self.actor, self.critic, self.target_actor, self.target_critic):
                 train_ops.attach_guard(m, self.guard)
         for opt, stages in ((self.actor_optim, ('actor_grad', 'actor_param')),
@@ -130,6 +130,9 @@ class DDPGTrainer:
             if isinstance(opt, DeviceAdam):
                 opt.set_guard(self.guard, *stages)
         self.warmup = warmup
+        # stream layout of the stages (A/B: tools/update_only.py AB_ATTR=...)
+        self.multi_stream = True      # independent forwards on a side stream (_fork)
+        self.split_target = False     # + the target critic trunk on a third (measured slower)
         self._pending_grads = {}      # module id -> its autograd gradients (_grads -> _opt_step)
         self.conv_search = bool(conv_search)
         self._graphs = None
@@ -187,7 +190,12 @@ class DDPGTrainer:
         its next critic_optim.zero_grad() discards unread; here the critic's
         conv trunk (independent of the actor) is not differentiated at all."""
         params = [p for p in module.parameters() if p.requires_grad]
-        grads = torch.autograd.grad(loss, params, allow_unused=True, materialize_grads=True)
+        # a persistent 1 as the seed: no fill kernel a backward
+        one = getattr(self, '_one', None)
+        if one is None or one.device != loss.device or one.dtype != loss.dtype:
+            one = self._one = torch.ones((), device=loss.device, dtype=loss.dtype)
+        grads = torch.autograd.grad(loss, params, grad_outputs=one, allow_unused=True,
+                                    materialize_grads=True)
         opt = self.actor_optim if module is self.actor else self.critic_optim
         if (self.graph and isinstance(opt, DeviceAdam) and len(params) == len(list(
                 module.parameters())) and (self.sync_actor if module is self.actor
@@ -206,12 +214,26 @@ class DDPGTrainer:
     # ---- the three stages (trainers.py:156-229) ------------------------------------
     def _fork(self):
         """A side stream joined to the current one (GPU), or None (CPU)."""
-        if self.device.type != 'cuda':
+        if self.device.type != 'cuda' or not self.multi_stream:
             return None
         if getattr(self, '_side', None) is None:
             self._side = torch.cuda.Stream(self.device)
         self._side.wait_stream(torch.cuda.current_stream(self.device))
         return self._side
+
+    def _fork2(self):
+        """A second side stream joined to the current one (GPU)."""
+        if getattr(self, '_side2', None) is None:
+            self._side2 = torch.cuda.Stream(self.device)
+        self._side2.wait_stream(torch.cuda.current_stream(self.device))
+        return self._side2
+
+    @staticmethod
+    def _join_on(stream, other, *tensors):
+        """`stream` waits for `other`; tensors made on `other` are used on it."""
+        stream.wait_stream(other)
+        for t in tensors:
+            t.record_stream(stream)
 
     def _join(self, side, *tensors):
         if side is not None:
@@ -263,16 +285,33 @@ class DDPGTrainer:
         # batch-64 kernels (a few CUs each) run side by side -- in a HIP graph
         # two branches of the captured DAG
         side = self._fork()
+        # the target critic's conv trunk does not depend on the target actor's
+        # action: a third stream, so the target branch is one trunk deep
+        # instead of two (the trunk draws no dropout, so the RNG order holds)
+        side2 = self._fork2() if (side is not None and self.split_target and
+                                  hasattr(self.target_critic, 'trunk')) else None
+        if side2 is not None:
+            with torch.cuda.stream(side2), torch.no_grad():
+                t_next = self.target_critic.trunk(x['nxt'])
         with torch.cuda.stream(side) if side is not None else _nullctx():
             with torch.no_grad():
                 next_actions = self.target_actor(x['nxt'])
-                next_v = self.target_critic(x['nxt'], next_actions)
-                self._y = x['rew'] + x['notdone'] * self.gamma * next_v
+                if side2 is not None:
+                    self._join_on(side, side2, t_next)
+                    next_v = self.target_critic.head(t_next, next_actions)
+                    self._y = x['rew'] + x['notdone'] * self.gamma * next_v
+                elif hasattr(self.target_critic, 'td_target'):
+                    # the head and the target in one launch on the GPU
+                    self._y = self.target_critic.td_target(x['nxt'], next_actions, x['rew'],
+                                                           x['notdone'], self.gamma)
+                else:
+                    next_v = self.target_critic(x['nxt'], next_actions)
+                    self._y = x['rew'] + x['notdone'] * self.gamma * next_v
                 self.guard.scan('target', self._y)
         y_predicted = self.critic(x['obs'], x['act'])
         self._join(side, self._y)
         if self.critic_loss_kind == 'mse_loss':
-            critic_loss = F.mse_loss(y_predicted, self._y)
+            critic_loss = train_ops.mse_loss(y_predicted, self._y)
         else:
             critic_loss = F.smooth_l1_loss(y_predicted, self._y)
         self._grads(critic_loss, self.critic)
@@ -296,7 +335,6 @@ class DDPGTrainer:
         x = self._in
         self._opt_step(self.critic_optim, self.critic, 'critic_grad', 'critic_param')
         if self._shared_trunk():
-            from aido1_amd import train_ops
             # the (stepped) critic's trunk and the actor's forward are
             # independent until the head: two streams, two graph branches
             side = self._fork()
@@ -309,7 +347,7 @@ class DDPGTrainer:
         else:
             pred_actions = self.actor(x['obs'])
             q = self.critic(x['obs'], pred_actions)
-        actor_loss = -1.0 * torch.mean(q)
+        actor_loss = train_ops.neg_mean(q)
         self._grads(actor_loss, self.actor)
         self._actor_loss = actor_loss.detach()
         self.guard.scan('actor_loss', self._actor_loss)

@@ -46,6 +46,23 @@ typedef struct DtMlp {
 /* h [m, n1] (kept for the backward), y [m, n2] (two layers; NULL for one). */
 int dt_mlp_fwd(const DtMlp* p, const float* x0, const float* x1, float* h, float* y, void* stream);
 
+/* dt_mlp_fwd plus the TD target of the DDPG critic loss (training/trainers.py:
+ * 166-170) in the same launch: target[r][j] = rew[r] + (notdone[r] * gamma) *
+ * y[r][j] (y = h for one layer), rew / notdone [m] device f32, target [m, n_out]. */
+int dt_mlp_fwd_td(const DtMlp* p, const float* x0, const float* x1, float* h, float* y,
+                  const float* rew, const float* notdone, float gamma, float* target,
+                  void* stream);
+
+/* The DDPG losses in one launch each (training/trainers.py:174-177, 193-196),
+ * one workgroup, a float64 sum in a fixed order:
+ *   kind 0: loss = mean((a - b)^2)  (F.mse_loss, mean reduction)
+ *   kind 1: loss = -mean(a)         (the actor loss, b unused)
+ * dt_loss_bwd: da = (2 / m) (a - b) g (kind 0), -(g / m) (kind 1), g the
+ * scalar upstream gradient (device).  m >= 1. */
+int dt_loss(int32_t kind, int32_t m, const float* a, const float* b, float* loss, void* stream);
+int dt_loss_bwd(int32_t kind, int32_t m, const float* a, const float* b, const float* g,
+                float* da, void* stream);
+
 /* The tail's backward from dy (= dL/dy [m, n2], or dL/dh [m, n1] for one
  * layer) and the forward's h and y: any output may be NULL (not wanted).
  *   dx0 [m, k0], dx1 [m, k1], dw1 [n1, k0 + k1], db1 [n1], dw2 [n2, n1], db2 [n2] */

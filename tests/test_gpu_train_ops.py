@@ -313,3 +313,47 @@ def test_mlp_tail_matches_float64(gpu, m, k0, k1, n1, n2, acts):
     y2 = train_ops.mlp(parts, train_ops.mlp_plan(seq, parts))
     (gx0,) = torch.autograd.grad(y2, [x0], g)
     torch.testing.assert_close(gx0, gx[:, :k0], rtol=1e-6, atol=1e-7)
+
+
+@pytest.mark.parametrize('m', [1, 64, 300])
+def test_fused_losses_match_torch(gpu, m):
+    """dt_loss / dt_loss_bwd (train_ops.mse_loss, neg_mean): the DDPG critic
+    and actor losses and their input gradients against float64 torch."""
+    from aido1_amd import train_ops
+    torch.manual_seed(m)
+    a = torch.randn(m, 1, device=gpu, requires_grad=True)
+    b = torch.randn(m, 1, device=gpu)
+    loss = train_ops.mse_loss(a, b)
+    a64 = a.detach().double().requires_grad_(True)
+    ref = torch.nn.functional.mse_loss(a64, b.double())
+    torch.testing.assert_close(loss.double(), ref, rtol=1e-6, atol=1e-7)
+    loss.backward()
+    ref.backward()
+    torch.testing.assert_close(a.grad.double(), a64.grad, rtol=1e-6, atol=1e-8)
+    q = torch.randn(m, 1, device=gpu, requires_grad=True)
+    lq = train_ops.neg_mean(q)
+    q64 = q.detach().double().requires_grad_(True)
+    rq = -1.0 * torch.mean(q64)
+    torch.testing.assert_close(lq.double(), rq, rtol=1e-6, atol=1e-7)
+    lq.backward(torch.tensor(0.5, device=gpu))
+    rq.backward(torch.tensor(0.5, dtype=torch.float64, device=gpu))
+    torch.testing.assert_close(q.grad.double(), q64.grad, rtol=1e-6, atol=1e-9)
+
+
+def test_td_target_in_the_critic_head(gpu):
+    """ConfigCritic.td_target (dt_mlp_fwd_td: the output branch and
+    rew + (notdone * gamma) * Q in one launch) equals the torch expression on
+    the critic's forward, with dropout off."""
+    from aido1_amd.actor import ConfigCritic
+    from test_trainer import no_dropout
+    cfg = no_dropout(golden('reference_config.json')['model']['critic'])
+    torch.manual_seed(3)
+    c = ConfigCritic(cfg).to(gpu).to(memory_format=torch.channels_last).eval()
+    obs = torch.rand(64, 3, 120, 160, device=gpu).contiguous(memory_format=torch.channels_last)
+    act = torch.rand(64, 2, device=gpu)
+    rew = torch.randn(64, 1, device=gpu)
+    notdone = (torch.rand(64, 1, device=gpu) > 0.2).float()
+    with torch.no_grad():
+        got = c.td_target(obs, act, rew, notdone, 0.99)
+        want = rew + notdone * 0.99 * c(obs, act)
+    torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-5)

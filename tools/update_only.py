@@ -43,21 +43,46 @@ def main():
             torch.cuda.synchronize()
             times.append(a.elapsed_time(e))
         return float(np.median(times))
+    ab = os.environ.get('AB_ATTR')       # e.g. split_target: A/B of a trainer switch, one box
+    if ab:
+        tr2 = DDPGTrainer(cfg, ConfigActor(cfg['model']['actor']),
+                          ConfigCritic(cfg['model']['critic']), device=dev, graph=True)
+        setattr(tr2, ab, not getattr(tr, ab))
+        for _ in range(5):
+            tr2.update(batch)
+        res = {True: [], False: []}
+        for _ in range(5):
+            for t in (tr, tr2):
+                a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                a.record()
+                for _ in range(n_up):
+                    t.update_prepared()
+                e.record()
+                torch.cuda.synchronize()
+                res[bool(getattr(t, ab))].append(a.elapsed_time(e) / n_up)
+        for v in (True, False):
+            print('%s=%s back to back: %s ms (median %.3f)'
+                  % (ab, v, ' '.join('%.3f' % x for x in res[v]), float(np.median(res[v]))))
     t_full = timed(lambda: tr.update(batch))
     # the inputs already in the static buffers (TrainLoop: dt_frame_gather)
     t_prep = timed(tr.update_prepared)
     # back to back, as the training loop issues them (the host runs ahead of
     # the GPU, so its launch latency is hidden): mean over n_up updates
-    a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record()
-    for _ in range(n_up):
-        tr.update_prepared()
-    e.record()
-    torch.cuda.synchronize()
-    t_b2b = a.elapsed_time(e) / n_up
+    b2b = []
+    for _ in range(5):
+        a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(n_up):
+            tr.update_prepared()
+        e.record()
+        torch.cuda.synchronize()
+        b2b.append(a.elapsed_time(e) / n_up)
+    t_b2b = float(np.median(b2b))
+    print('back to back, 5 runs of %d: %s ms' % (n_up, ' '.join('%.3f' % v for v in b2b)))
     tr.check()
     print('update %.3f ms with the input conversion + copies, %.3f ms on prepared inputs '
-          '(medians of %d, each synchronised); %.3f ms back to back (mean of %d, host ahead)'
+          '(medians of %d, each synchronised); %.3f ms back to back (median of 5 means of %d, '
+          'host ahead)'
           % (t_full, t_prep, n_up, t_b2b, n_up))
 
 
