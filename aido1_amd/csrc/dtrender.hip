@@ -918,7 +918,9 @@ __device__ __forceinline__ void canny(const RenderArgs& a, RenderLds& S, int e,
 // pieces of each plane, so every line of a plane is written whole by one
 // instruction: a quad without a listed word (and radius <= 1) takes its own
 // colour bits, the others the dilation + edge path.
-template <bool kSpill>
+// kIdx: the frame goes out as palette bytes (a.index) instead of grey floats
+// (a.gray): two instantiations, so the grey path keeps its register budget.
+template <bool kSpill, bool kIdx>
 __device__ __forceinline__ void write_outputs(const RenderArgs& a, RenderLds& S, int e,
                                               uint8_t* mbase) {
   const int tid = threadIdx.x;
@@ -927,46 +929,41 @@ __device__ __forceinline__ void write_outputs(const RenderArgs& a, RenderLds& S,
   const Slots<kSpill> sl{S, a.spill + (size_t)e * kSpillHalves,
                          a.spill + (size_t)e * kSpillHalves + 4 * NW, a.list_cap};
   const bool fresh = a.fresh != nullptr && a.fresh[e] != 0;
-  float* gbase = a.gray ? a.gray + (size_t)e * a.slots * NPIX : nullptr;
-  uint8_t* ibase = a.index ? a.index + (size_t)e * a.slots * NPIX : nullptr;
+  float* gbase = !kIdx && a.gray ? a.gray + (size_t)e * a.slots * NPIX : nullptr;
+  uint8_t* ibase = kIdx ? a.index + (size_t)e * a.slots * NPIX : nullptr;
   const uint32_t blo = S.bits_lo, bhi = S.bits_hi;
   const bool quick_masks = L.dil_r <= 1;
   const int lane = tid & 63;
   for (int q0 = 0; q0 < NQ; q0 += T) {
     const int wbase = 4 * (q0 + (tid - lane));
-    if (ibase) {   // the palette bytes themselves (4 pixels a word)
+    if (gbase || ibase) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int w = wbase + 64 * j + lane;
         if (w < NW) {
           const uint32_t v = S.img[w] & kPalMask;
-          if (fresh) {
+          if (kIdx) {   // the palette bytes themselves (4 pixels a word)
+            if (fresh) {
 #pragma clang loop vectorize(disable) interleave(disable)
-            for (int k = 0; k < a.slots; ++k)
-              *reinterpret_cast<uint32_t*>(ibase + k * NPIX + 4 * w) = v;
-          } else {
-            *reinterpret_cast<uint32_t*>(ibase + a.slot * NPIX + 4 * w) = v;
+              for (int k = 0; k < a.slots; ++k)
+                *reinterpret_cast<uint32_t*>(ibase + k * NPIX + 4 * w) = v;
+            } else {
+              *reinterpret_cast<uint32_t*>(ibase + a.slot * NPIX + 4 * w) = v;
+            }
           }
-        }
-      }
-    }
-    if (gbase) {
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int w = wbase + 64 * j + lane;
-        if (w < NW) {
-          const uint32_t v = S.img[w] & kPalMask;
-          float4 g;
-          g.x = S.pal_gray[v & 255u];
-          g.y = S.pal_gray[(v >> 8) & 255u];
-          g.z = S.pal_gray[(v >> 16) & 255u];
-          g.w = S.pal_gray[v >> 24];
-          if (fresh) {
+          if (!kIdx) {
+            float4 g;
+            g.x = S.pal_gray[v & 255u];
+            g.y = S.pal_gray[(v >> 8) & 255u];
+            g.z = S.pal_gray[(v >> 16) & 255u];
+            g.w = S.pal_gray[v >> 24];
+            if (fresh) {
 #pragma clang loop vectorize(disable) interleave(disable)
-            for (int k = 0; k < a.slots; ++k)
-              *reinterpret_cast<float4*>(gbase + k * NPIX + 4 * w) = g;
-          } else {
-            *reinterpret_cast<float4*>(gbase + a.slot * NPIX + 4 * w) = g;
+              for (int k = 0; k < a.slots; ++k)
+                *reinterpret_cast<float4*>(gbase + k * NPIX + 4 * w) = g;
+            } else {
+              *reinterpret_cast<float4*>(gbase + a.slot * NPIX + 4 * w) = g;
+            }
           }
         }
       }
@@ -1364,12 +1361,14 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, in
     if (mbase) canny<false>(a, S, e, nlist);
     RENT(13);
     RENDER_STOP(4);
-    write_outputs<false>(a, S, e, mbase);
+    if (a.index) write_outputs<false, true>(a, S, e, mbase);
+    else write_outputs<false, false>(a, S, e, mbase);
   } else {
     if (mbase) canny<true>(a, S, e, nlist);
     RENT(13);
     RENDER_STOP(4);
-    write_outputs<true>(a, S, e, mbase);
+    if (a.index) write_outputs<true, true>(a, S, e, mbase);
+    else write_outputs<true, false>(a, S, e, mbase);
   }
 #ifdef DTSIM_STAMPS
   RENSTAMP(12, (unsigned long long)C[kNList] | ((unsigned long long)C[kNWeak] << 32));
@@ -1849,6 +1848,10 @@ int dt_set_line_params(dt_handle* h, const dt_line_params* p) {
 
 int dt_render(dt_handle* h, const dt_render_io* io, void* stream) {
   if (!h || !io) return DT_E_ARG;
+  if (io->gray && io->index) {
+    h->err = "dt_render: gray and index are two formats of one frame ring: give one";
+    return DT_E_ARG;
+  }
   if ((io->gray || io->index) &&
       (io->gray_slots < 1 || io->gray_slot < 0 || io->gray_slot >= io->gray_slots)) {
     h->err = "dt_render: gray_slot out of range";

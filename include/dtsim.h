@@ -268,8 +268,8 @@ typedef struct dt_render_io {
                            the kernel keeps in LDS, so tests exercise the global-memory
                            overflow path (results are identical either way) */
   uint8_t* index;       /* device [n, gray_slots, 120, 160] u8 palette-index frames, or
-                           NULL: the frame's palette bytes (0..7), same slots / fresh
-                           rules as `gray`.  A quarter of the grey frame's bytes and
+                           NULL (not both `gray` and `index`: DT_E_ARG): the frame's
+                           palette bytes (0..7), same slots / fresh rules as `gray`.  A quarter of the grey frame's bytes and
                            lossless: gray = dt_palette_gray's table[index] bit for bit
                            (the actor's dt_conv1_index_split and dt_frame_gather read
                            such frames directly) */
