@@ -56,19 +56,96 @@ __global__ void fill_kernel(double* sum, double* mn, double* maxp, int32_t* winn
   if (blockIdx.x == 0 && threadIdx.x == 0) *maxp = 1.0;
 }
 
-// n adds starting at slot `next`; one workgroup walks the touched leaf ranges
-// (at most two: the batch may wrap at `size`) up to the root level by level.
+// n adds starting at slot `next`; one workgroup.  Every new leaf gets the same
+// value v, so a touched node whose leaf span lies inside the written range
+// [L, H) holds exactly v * 2^level (sum: sums of equal halves double exactly)
+// and v (min): those are written in parallel, with no level-by-level
+// dependency.  The <= 2 nodes a level whose spans cross L or H are recomputed
+// by one lane from their children -- closed-form, the previous level's
+// crossing node, or an untouched node, all untouched ones loaded into LDS at
+// once first -- so the walk to the root is one load latency, not one a level.
+// The same values as recomputing every touched node level by level.  A batch
+// that wraps at `size` (two ranges) takes the level-by-level walk.
+constexpr int kAddMaxLevels = 40;
+
 __global__ void __launch_bounds__(kTreeThreads)
 add_kernel(double* sum, double* mn, const double* maxp, int64_t cap, int log2cap, int64_t size,
            int64_t next, int64_t n, double alpha, int64_t* slots) {
+  __shared__ double pre_s[kAddMaxLevels * 4], pre_m[kAddMaxLevels * 4];
   const double v = pow(*maxp, alpha);  // buffers.py:173-174
   for (int64_t k = threadIdx.x; k < n; k += blockDim.x) {
     const int64_t s = (next + k) % size;
     if (slots) slots[k] = s;
   }
   const int64_t m = n < size ? n : size;  // distinct slots written
-  int64_t lo[2], hi[2];
   const int64_t end = next + m;
+  if (end <= size) {
+    const int64_t L = cap + next, H = cap + end;   // leaf-node range [L, H)
+    auto interior = [&](int64_t p, int l) { return (p << l) >= L && ((p + 1) << l) <= H; };
+    auto untouched = [&](int64_t p, int l) { return ((p + 1) << l) <= L || (p << l) >= H; };
+    // the untouched children of the crossing nodes, every level at once
+    for (int it = threadIdx.x; it < 4 * log2cap; it += blockDim.x) {
+      const int l = it / 4 + 1, side = (it >> 1) & 1, ch = it & 1;
+      const int64_t p = side ? (H - 1) >> l : L >> l;
+      const int64_t c = 2 * p + ch;
+      if (!interior(p, l) && untouched(c, l - 1)) {
+        pre_s[it] = sum[c];
+        pre_m[it] = mn[c];
+      }
+    }
+    // the interior nodes (leaves included)
+    for (int l = 0; l <= log2cap; ++l) {
+      const int64_t first = ((L + (int64_t(1) << l) - 1) >> l), last = (H >> l) - 1;
+      const double sv = ldexp(v, l);
+      for (int64_t p = first + threadIdx.x; p <= last; p += blockDim.x) {
+        sum[p] = sv;
+        mn[p] = v;
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int64_t prev_p[2] = {-1, -1};
+      double prev_s[2] = {0.0, 0.0}, prev_m[2] = {0.0, 0.0};
+      for (int l = 1; l <= log2cap; ++l) {
+        int64_t cur_p[2] = {-1, -1};
+        double cur_s[2] = {0.0, 0.0}, cur_m[2] = {0.0, 0.0};
+        for (int side = 0; side < 2; ++side) {
+          const int64_t p = side ? (H - 1) >> l : L >> l;
+          if (interior(p, l) || (side == 1 && p == cur_p[0])) continue;
+          double cs[2], cm[2];
+          for (int ch = 0; ch < 2; ++ch) {
+            const int64_t c = 2 * p + ch;
+            if (interior(c, l - 1)) {
+              cs[ch] = ldexp(v, l - 1);
+              cm[ch] = v;
+            } else if (c == prev_p[0]) {
+              cs[ch] = prev_s[0];
+              cm[ch] = prev_m[0];
+            } else if (c == prev_p[1]) {
+              cs[ch] = prev_s[1];
+              cm[ch] = prev_m[1];
+            } else {   // untouched: prefetched
+              const int it = 4 * (l - 1) + 2 * side + ch;
+              cs[ch] = pre_s[it];
+              cm[ch] = pre_m[it];
+            }
+          }
+          cur_p[side] = p;
+          cur_s[side] = cs[0] + cs[1];
+          cur_m[side] = py_min(cm[0], cm[1]);
+          sum[p] = cur_s[side];
+          mn[p] = cur_m[side];
+        }
+        for (int q = 0; q < 2; ++q) {
+          prev_p[q] = cur_p[q];
+          prev_s[q] = cur_s[q];
+          prev_m[q] = cur_m[q];
+        }
+      }
+    }
+    return;
+  }
+  int64_t lo[2], hi[2];
   lo[0] = cap + next;
   hi[0] = cap + (end < size ? end : size);
   lo[1] = cap;
@@ -103,6 +180,9 @@ __device__ double block_max(double v, double* scratch) {
   return scratch[0];
 }
 
+constexpr int kUpdMax = 128;        // entries of the LDS ancestor walk
+constexpr int kUpdMaxLevels = 24;   // tree levels of the LDS ancestor walk
+
 __global__ void __launch_bounds__(kTreeThreads)
 update_kernel(double* sum, double* mn, double* maxp, int32_t* winner, int32_t* err, int64_t cap,
               int log2cap, int64_t len, int32_t n, const int64_t* idx, const double* prio,
@@ -136,6 +216,65 @@ update_kernel(double* sum, double* mn, double* maxp, int32_t* winner, int32_t* e
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
     const int64_t j = idx[i];
     if (j >= 0 && j < len) winner[j] = -1;
+  }
+  if (n <= kUpdMax && log2cap <= kUpdMaxLevels) {
+    // Every written leaf's ancestors as one chain per entry, computed in LDS:
+    // at level l, entry i's node has one child on its own chain and a
+    // sibling that is either on some entry's chain (its value from LDS) or
+    // untouched by this call -- those are loaded for every level at once
+    // first, so the walk to the root is LDS-speed instead of a memory
+    // round trip a level.  The same operands as recomputing level by level.
+    __shared__ double pre_s[kUpdMaxLevels][kUpdMax], pre_m[kUpdMaxLevels][kUpdMax];
+    __shared__ int16_t from[kUpdMaxLevels][kUpdMax];
+    __shared__ double vs[2][kUpdMax], vm[2][kUpdMax];
+    __shared__ int64_t leaf[kUpdMax];   // cap + j, or -1 for a rejected entry
+    for (int i = threadIdx.x; i < n; i += blockDim.x) {
+      const int64_t j = idx[i];
+      leaf[i] = (j >= 0 && j < len && prio[i] > 0.0) ? cap + j : -1;
+    }
+    __syncthreads();
+    for (int it = threadIdx.x; it < n * log2cap; it += blockDim.x) {
+      const int i = it % n, l = it / n + 1;
+      if (leaf[i] < 0) continue;
+      const int64_t sib = (leaf[i] >> (l - 1)) ^ 1;
+      int k = -1;
+      for (int q = 0; q < n; ++q)
+        if (leaf[q] >= 0 && (leaf[q] >> (l - 1)) == sib) {
+          k = q;
+          break;
+        }
+      from[l - 1][i] = (int16_t)k;
+      if (k < 0) {
+        pre_s[l - 1][i] = sum[sib];
+        pre_m[l - 1][i] = mn[sib];
+      }
+    }
+    for (int i = threadIdx.x; i < n; i += blockDim.x)
+      if (leaf[i] >= 0) {
+        vs[0][i] = sum[leaf[i]];   // the winner's leaf (written above)
+        vm[0][i] = mn[leaf[i]];
+      }
+    __syncthreads();
+    for (int l = 1; l <= log2cap; ++l) {
+      const int a = (l - 1) & 1, b = l & 1;
+      for (int i = threadIdx.x; i < n; i += blockDim.x) {
+        if (leaf[i] < 0) continue;
+        const int k = from[l - 1][i];
+        const double os = vs[a][i], om = vm[a][i];
+        const double ss = k >= 0 ? vs[a][k] : pre_s[l - 1][i];
+        const double sm = k >= 0 ? vm[a][k] : pre_m[l - 1][i];
+        const bool left = ((leaf[i] >> (l - 1)) & 1) == 0;
+        const double ns = left ? os + ss : ss + os;
+        const double nm = left ? py_min(om, sm) : py_min(sm, om);
+        vs[b][i] = ns;
+        vm[b][i] = nm;
+        const int64_t node = leaf[i] >> l;
+        sum[node] = ns;
+        mn[node] = nm;
+      }
+      __syncthreads();
+    }
+    return;
   }
   // the ancestors of every written leaf, level by level; a node shared by
   // several leaves is recomputed redundantly to the same value

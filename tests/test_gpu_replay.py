@@ -94,6 +94,45 @@ def test_per_full_size_against_oracle(gpu):
     rb.close()
 
 
+@pytest.mark.parametrize('size,n,batch', [(131072, 4096, 64), (1000, 96, 128), (4096, 300, 7)])
+def test_per_fast_paths_against_oracle(gpu, size, n, batch):
+    """The config-5 shapes of add / sample / update: whole-block adds (the
+    closed-form add walk; 1000 and 4096 also wrap mid-batch: the level walk),
+    batch-64 updates with duplicate indices (the LDS ancestor walk; 128 its
+    largest batch), samples through the LDS-staged top levels -- the trees bit
+    for bit against the reference's restatement."""
+    from aido1_amd.replay import PrioritizedReplayBuffer
+    alpha, beta = 0.6, 0.4
+    rb = PrioritizedReplayBuffer(size, alpha, device=gpu)
+    ref = PrioritizedReplayRef(size, alpha)
+    rng = np.random.default_rng(size + n)
+    obs = torch.zeros(n, 1, device=gpu)
+    act = torch.zeros(n, 2, device=gpu)
+    rew = torch.zeros(n, dtype=torch.float64, device=gpu)
+    done = torch.zeros(n, dtype=torch.bool, device=gpu)
+    for it in range(40):
+        rb.add_batch(obs, act, rew, obs, done)
+        ref.add(n)
+        u = rng.random(batch)
+        *_, w, idx = rb.sample(batch, beta=beta, u=u)
+        ridx, rw = ref.sample(u.tolist(), beta)
+        assert idx.tolist() == ridx, it
+        np.testing.assert_allclose(w.cpu().numpy(), rw, rtol=1e-13)
+        upd = idx[torch.from_numpy(rng.integers(0, batch, batch)).to(gpu)]   # duplicates
+        pr = rng.random(batch) * (2.0 + it) + 1e-6
+        rb.update_priorities(upd, pr)
+        ref.update_priorities(upd.tolist(), pr.tolist())
+        if it % 13 == 12:
+            st, mt, mp = rb.trees()
+            assert mp.item() == ref.max_priority
+            assert_trees(st, mt, ref.it_sum.value,
+                         [None if v == math.inf else v for v in ref.it_min.value])
+    rb.check()
+    st, mt, mp = rb.trees()
+    assert_trees(st, mt, ref.it_sum.value, [None if v == math.inf else v for v in ref.it_min.value])
+    rb.close()
+
+
 def test_per_rejects_like_reference_asserts(gpu):
     from aido1_amd._lib import DtError
     from aido1_amd.replay import PrioritizedReplayBuffer
