@@ -1045,10 +1045,12 @@ def step_parity(env, start, actions, out, rank, args, frames=None, m=64):
 
 
 # ---- configs 4 and 5 -----------------------------------------------------------------------
-def actor_f64(actor, x):
-    """The actor in float64 on the host (torch CPU): the reference-mode forward
-    (train-mode batch-of-one BatchNorm = per-sample statistics, dropout off),
-    the precision yardstick of configs 4 / 5 (tools/actor_precision.py)."""
+def actor_f64(actor, x, mode='reference'):
+    """The actor in float64 on the host (torch CPU), dropout off: mode
+    'reference' = train-mode batch-of-one BatchNorm (per-sample statistics,
+    the explorers' forward), 'eval' = the running statistics (the folded-BN
+    policy); the precision yardstick of configs 4 / 5
+    (tools/actor_precision.py)."""
     import torch
     import torch.nn.functional as F
     from aido1_amd.actor import apply_head
@@ -1057,8 +1059,12 @@ def actor_f64(actor, x):
     h = x.double().cpu()
     for c, b in zip(convs, bns):
         h = F.leaky_relu(F.conv2d(h, d(c.weight), d(c.bias), stride=c.stride))
-        m = h.mean((2, 3), keepdim=True)
-        v = (h - m).square().mean((2, 3), keepdim=True)
+        if mode == 'eval':
+            m = d(b.running_mean).view(1, -1, 1, 1)
+            v = d(b.running_var).view(1, -1, 1, 1)
+        else:
+            m = h.mean((2, 3), keepdim=True)
+            v = (h - m).square().mean((2, 3), keepdim=True)
         h = (h - m) / torch.sqrt(v + b.eps) * d(b.weight).view(1, -1, 1, 1) + \
             d(b.bias).view(1, -1, 1, 1)
     h = F.leaky_relu(F.linear(h.flatten(1), d(l1.weight), d(l1.bias)))
@@ -1118,7 +1124,7 @@ def actor_record(args, ctx, K, W, parity=True, dtype=None, cpu=False):
             got = roll.actor(roll.ring, roll.order()).float()
             want = alt(roll.ring, roll.order()).float()
             m = 64
-            ref64 = actor_f64(roll.actor_src, roll.stack()[:m])
+            ref64 = actor_f64(roll.actor_src, roll.stack()[:m], roll.actor.mode)
         roll.actor.p_drop = drop
         d = torch.abs(got - want)
         e64 = (got[:m].double().cpu() - ref64).abs()

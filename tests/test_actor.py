@@ -146,3 +146,25 @@ def test_bench_actor_f64_is_batch_of_one_train_mode():
     with torch.no_grad():
         want = torch.cat([a64(x[i:i + 1].double()) for i in range(3)])
     torch.testing.assert_close(got, want, rtol=1e-12, atol=1e-12)
+
+
+def test_bench_actor_f64_eval_mode_uses_running_statistics():
+    """bench.actor_f64(mode='eval') = the eval-mode ConfigActor in float64
+    (the running statistics: the folded-BN policy's reference)."""
+    import bench
+    from aido1_amd.actor import ConfigActor
+    from test_trainer import no_dropout
+    cfg = golden('reference_config.json')
+    torch.manual_seed(4)
+    a = ConfigActor(no_dropout(cfg['model']['actor']))
+    for bn in [m for m in a.modules() if isinstance(m, torch.nn.BatchNorm2d)]:
+        bn.running_mean.uniform_(-0.2, 0.2)
+        bn.running_var.uniform_(0.5, 2.0)
+    x = torch.rand(3, 3, 120, 160)
+    got = bench.actor_f64(a, x, 'eval')
+    a64 = ConfigActor(no_dropout(cfg['model']['actor']))
+    a64.load_state_dict(a.state_dict())
+    a64.double().eval()
+    with torch.no_grad():
+        want = a64(x.double())
+    torch.testing.assert_close(got, want, rtol=1e-12, atol=1e-12)
