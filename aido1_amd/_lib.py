@@ -183,6 +183,7 @@ def lib():
             'dt_per_add': (ctypes.c_int, [vp, i64, vp, vp]),
             'dt_per_sample': (ctypes.c_int, [vp, i32, vp, f64, vp, vp, vp]),
             'dt_per_update': (ctypes.c_int, [vp, i32, vp, vp, vp]),
+            'dt_per_update_td': (ctypes.c_int, [vp, i32, vp, vp, f64, vp]),
             'dt_per_read': (ctypes.c_int, [vp, vp, vp, vp, vp]),
             'dt_per_check': (ctypes.c_int, [vp]),
             'dt_frame_add': (ctypes.c_int, [i32, i64, vp, i64, vp, i32, vp, vp, i32, vp, vp, vp]),

@@ -180,13 +180,26 @@ __device__ double block_max(double v, double* scratch) {
   return scratch[0];
 }
 
+// the priorities of an update: given (dt_per_update), or |td| + eps from the
+// trainer's float32 TD errors (dt_per_update_td: the loop's abs -> float64 ->
+// + eps in one pass, the same values)
+struct PrioD {
+  const double* p;
+  __device__ double operator[](int i) const { return p[i]; }
+};
+struct PrioTd {
+  const float* td;
+  double eps;
+  __device__ double operator[](int i) const { return (double)fabsf(td[i]) + eps; }
+};
+
 constexpr int kUpdMax = 128;        // entries of the LDS ancestor walk
 constexpr int kUpdMaxLevels = 24;   // tree levels of the LDS ancestor walk
 
+template <class P>
 __global__ void __launch_bounds__(kTreeThreads)
 update_kernel(double* sum, double* mn, double* maxp, int32_t* winner, int32_t* err, int64_t cap,
-              int log2cap, int64_t len, int32_t n, const int64_t* idx, const double* prio,
-              double alpha) {
+              int log2cap, int64_t len, int32_t n, const int64_t* idx, P prio, double alpha) {
   __shared__ double scratch[kTreeThreads / 64];
   double pmax = 0.0;
   for (int i = threadIdx.x; i < n; i += blockDim.x) {
@@ -523,9 +536,21 @@ int dt_per_update(dt_per* h, int32_t n, const int64_t* idx_dev, const double* pr
   if (!h || n < 0 || (n > 0 && (!idx_dev || !priorities_dev))) return DT_E_ARG;
   if (n == 0) return DT_OK;
   PER_HIP(h, hipSetDevice(h->device));
-  update_kernel<<<1, kTreeThreads, 0, (hipStream_t)stream>>>(h->sum, h->mn, h->maxp, h->winner,
-                                                             h->err, h->cap, h->log2cap, h->len, n,
-                                                             idx_dev, priorities_dev, h->alpha);
+  update_kernel<<<1, kTreeThreads, 0, (hipStream_t)stream>>>(
+      h->sum, h->mn, h->maxp, h->winner, h->err, h->cap, h->log2cap, h->len, n, idx_dev,
+      PrioD{priorities_dev}, h->alpha);
+  PER_HIP(h, hipGetLastError());
+  return DT_OK;
+}
+
+int dt_per_update_td(dt_per* h, int32_t n, const int64_t* idx_dev, const float* td_dev,
+                     double eps, void* stream) {
+  if (!h || n < 0 || (n > 0 && (!idx_dev || !td_dev))) return DT_E_ARG;
+  if (n == 0) return DT_OK;
+  PER_HIP(h, hipSetDevice(h->device));
+  update_kernel<<<1, kTreeThreads, 0, (hipStream_t)stream>>>(
+      h->sum, h->mn, h->maxp, h->winner, h->err, h->cap, h->log2cap, h->len, n, idx_dev,
+      PrioTd{td_dev, eps}, h->alpha);
   PER_HIP(h, hipGetLastError());
   return DT_OK;
 }

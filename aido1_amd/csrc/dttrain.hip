@@ -518,7 +518,9 @@ int dt_guard_scan(int32_t n, const dt_guard_tensor* tensors, int32_t* guard, voi
     most = t.count > most ? t.count : most;
   }
   if (most == 0) return DT_OK;
-  int64_t g = (most / 4 + kGuardThreads * 4 - 1) / (kGuardThreads * 4);
+  // ~4 elements a thread (a float4 or four doubles): a 4096-double reward
+  // scan takes 4 workgroups, not one walking 16 strided loads a thread
+  int64_t g = (most + kGuardThreads * 4 - 1) / (kGuardThreads * 4);
   g = g < 1 ? 1 : (g > 1024 ? 1024 : g);
   hipLaunchKernelGGL(guard_scan_kernel, dim3((unsigned)g), dim3(kGuardThreads), 0,
                      (hipStream_t)stream, set, guard);

@@ -402,6 +402,19 @@ class PrioritizedReplayBuffer(ReplayBuffer):
                                               ctypes.c_void_p(pr.data_ptr()), self._stream()),
                         'dt_per_update')
 
+    def update_priorities_td(self, idxes, td, eps):
+        """update_priorities(idxes, |td| + eps) for float32 TD errors on the
+        device, the priorities formed inside the tree kernel (one launch)."""
+        idx = torch.as_tensor(idxes, dtype=torch.int64, device=self.device).reshape(-1).contiguous()
+        td = td.detach().reshape(-1).contiguous()
+        if td.dtype != torch.float32 or td.device != self.device or td.numel() != idx.numel():
+            return self.update_priorities(idx, td.abs().double() + eps)
+        with torch.cuda.device(self.device):
+            self._check(self._L.dt_per_update_td(self._h, idx.numel(),
+                                                 ctypes.c_void_p(idx.data_ptr()),
+                                                 ctypes.c_void_p(td.data_ptr()), float(eps),
+                                                 self._stream()), 'dt_per_update_td')
+
     def check(self):
         """Synchronise and raise if an update held an entry the reference rejects."""
         with torch.cuda.device(self.device):

@@ -227,9 +227,8 @@ class TrainLoop:
         else:
             obs, act, rew, nxt, done = self.replay.sample(self.batch_size)
             self.metrics, info = self.trainer.update((obs, act, rew, nxt, done))
-        if self.prioritized:
-            pr = info['td_error'].detach().abs().reshape(-1).double() + PRIORITY_EPS
-            self.replay.update_priorities(idx, pr)
+        if self.prioritized:   # |td| + eps formed in the tree kernel (dt_per_update_td)
+            self.replay.update_priorities_td(idx, info['td_error'], PRIORITY_EPS)
         self.updates += 1
         if self.updates % self.refresh_every == 0:
             if self.side is not None:

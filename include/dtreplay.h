@@ -61,6 +61,12 @@ int dt_per_sample(dt_per* h, int32_t batch, const double* u_dev, double beta, in
 int dt_per_update(dt_per* h, int32_t n, const int64_t* idx_dev, const double* priorities_dev,
                   void* stream);
 
+/* dt_per_update with priorities |td[i]| + eps (td device float32 [n], the
+ * trainer's TD errors; the float32 absolute value widened to float64, then
+ * + eps: what update_priorities(idx, abs(td) + eps) stores). */
+int dt_per_update_td(dt_per* h, int32_t n, const int64_t* idx, const float* td, double eps,
+                     void* stream);
+
 /* Copy out the trees (float64[2*capacity] each; NULL to skip) and the max
  * priority (float64[1]) — tests and checkpointing. */
 int dt_per_read(dt_per* h, double* sum_dev, double* min_dev, double* max_priority_dev,

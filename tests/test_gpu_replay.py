@@ -215,3 +215,29 @@ def test_frame_gather_equals_encode_and_trainer_inputs(gpu, index):
             for k in want:
                 assert torch.equal(got[k], want[k]), k
             assert got['obs'].is_contiguous(memory_format=torch.channels_last)
+
+
+def test_update_priorities_td_equals_explicit_priorities(gpu):
+    """dt_per_update_td (|td| + eps formed in the tree kernel, what TrainLoop
+    uses) leaves the trees bit for bit as update_priorities(abs(td) + eps)."""
+    from aido1_amd.replay import PrioritizedReplayBuffer
+    size, n = 4096, 1024
+    bufs = [PrioritizedReplayBuffer(size, 0.6, device=gpu) for _ in range(2)]
+    obs = torch.zeros(n, 1, device=gpu)
+    act = torch.zeros(n, 2, device=gpu)
+    rew = torch.zeros(n, dtype=torch.float64, device=gpu)
+    done = torch.zeros(n, dtype=torch.bool, device=gpu)
+    g = torch.Generator(device=gpu).manual_seed(7)
+    for _ in range(3):
+        for b in bufs:
+            b.add_batch(obs, act, rew, obs, done)
+        idx = torch.randint(0, n, (64,), device=gpu, generator=g)
+        td = torch.randn(64, 1, device=gpu, generator=g)
+        bufs[0].update_priorities_td(idx, td, 1e-6)
+        bufs[1].update_priorities(idx, td.detach().abs().reshape(-1).double() + 1e-6)
+    ta, tb = bufs[0].trees(), bufs[1].trees()
+    for x, y in zip(ta, tb):
+        assert torch.equal(x, y)
+    for b in bufs:
+        b.check()
+        b.close()
