@@ -65,6 +65,12 @@ class DtEpisodeState(ctypes.Structure):
                 ('ring', ctypes.c_void_p), ('capacity', ctypes.c_int64)]
 
 
+class DtCopyEntry(ctypes.Structure):
+    """Mirror of DtCopyEntry (include/dtactor.h)."""
+    _fields_ = [('src', ctypes.c_void_p), ('dst', ctypes.c_void_p), ('map', ctypes.c_void_p),
+                ('count', ctypes.c_int64), ('dst_dtype', ctypes.c_int32), ('pad', ctypes.c_int32)]
+
+
 class DtMlp(ctypes.Structure):
     """include/dthead.h DtMlp: a small fully connected tail."""
     _fields_ = [(k, ctypes.c_int32) for k in ('m', 'k0', 'k1', 'n1', 'n2', 'act1', 'act2')] + \
@@ -256,6 +262,7 @@ def lib():
             'dt_explore_done': (ctypes.c_int, [i32, vp, vp, vp, vp, i32, vp]),
             'dt_episode_account': (ctypes.c_int, [i32, i32, vp, vp, vp,
                                                   ctypes.POINTER(DtEpisodeState), vp]),
+            'dt_refresh_copy': (ctypes.c_int, [i32, vp, i64, vp]),
             'dt_actor_head': (ctypes.c_int, [i32, i32, i32, vp, i32, vp, vp, vp, vp, i32,
                                              ctypes.c_float, vp, vp]),
         }

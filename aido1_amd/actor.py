@@ -388,6 +388,8 @@ class FusedActor(nn.Module):
             graph = dev.type == 'cuda'
         if not graph:
             return self._refresh(actor)
+        if self.mode == 'reference' and self.dtype == torch.float16:
+            return self._refresh_gather(actor)
         # the source's tensors are listed once per source module (walking the
         # module tree costs ~80 us of host time a call); their addresses are
         # checked on every call, so a source whose storage moved is recaptured
@@ -405,6 +407,87 @@ class FusedActor(nn.Module):
                 self._refresh(actor)
             cache[key] = g
         g.replay()
+
+    def _refresh_pairs(self, actor):
+        """(destination, source, logical index map or None) of a reference-mode
+        refresh: what _refresh copies, with the fragment gathers' index maps."""
+        convs, bns, lin1, lin2 = actor.layers()
+        pairs = [(d, sp, None) for d, sp in zip(
+            list(self.w) + list(self.b) + list(self.gamma) + list(self.beta) +
+            [self.w1, self.b1, self.w2, self.b2],
+            [c.weight for c in convs] + [c.bias for c in convs] + [bn.weight for bn in bns] +
+            [bn.bias for bn in bns] + [lin1.weight, lin1.bias, lin2.weight, lin2.bias])]
+        dev = self.w0frag.device
+        if getattr(self, '_fidx', None) is None or self._fidx[0].device != dev:
+            self._fidx = (conv1_fragment_index(dev), conv32_fragment_index(dev))
+            self._w0pad = torch.zeros(32 * 3 * 64 + 1, device=dev)
+        n0 = convs[0].weight.numel()
+        f0 = self._fidx[0].reshape(-1)
+        pairs.append((self.w0frag, convs[0].weight, torch.where(f0 < n0, f0, torch.full_like(f0, -1))))
+        for i in range(1, 4):
+            pairs.append((self.wfrag[i - 1], convs[i].weight, self._fidx[1].reshape(-1)))
+        for i in range(4):
+            pairs.append((self.bf[i], convs[i].bias, None))
+        return pairs
+
+    @staticmethod
+    def _phys_map(dst, src, logical=None):
+        """For every element of dst in its physical order, the physical offset
+        in src of the element copied there (src's logical element, or
+        src.flatten()[logical[...]] with -1 kept); None for a plain copy."""
+        n = src.numel()
+        dev = src.device
+        ar = torch.arange(n, device=dev, dtype=torch.int64)
+        src_phys = ar.as_strided(tuple(src.shape), tuple(src.stride())).reshape(-1)
+        if logical is None:
+            lg = torch.empty_strided(tuple(dst.shape), tuple(dst.stride()), dtype=torch.int64,
+                                     device=dev)
+            lg.copy_(torch.arange(dst.numel(), device=dev, dtype=torch.int64).view(dst.shape))
+            lg = lg.as_strided((dst.numel(),), (1,))
+            m = src_phys[lg]
+            return None if torch.equal(m, torch.arange(dst.numel(), device=dev)) else m
+        if not dst.is_contiguous():
+            raise ValueError('refresh: a gathered destination must be contiguous')
+        lg = logical.reshape(-1).to(dev)
+        return torch.where(lg >= 0, src_phys[lg.clamp(min=0)], lg)
+
+    def _refresh_gather(self, actor):
+        """A reference-mode fp16 refresh as ONE dt_refresh_copy launch
+        (include/dtactor.h): every acting tensor gathered and converted from
+        the source's float32 parameters through index maps built at the first
+        refresh from a source (its tensors' addresses are checked every call).
+        Issued as ~28 small kernels (or their graph) it cost ~0.19 ms of GPU
+        time a decision in the training loop."""
+        import ctypes
+        from aido1_amd import _lib
+        srcs = self.__dict__.setdefault('_refresh_srcs', {})
+        ts = srcs.get(id(actor))
+        if ts is None or ts[0] is not actor:
+            ts = srcs[id(actor)] = (actor, list(actor.parameters()) + list(actor.buffers()))
+        key = (id(actor),) + tuple(t.data_ptr() for t in ts[1])
+        cache = self.__dict__.setdefault('_refresh_tables', {})
+        ent = cache.get(key)
+        if ent is None:
+            pairs = self._refresh_pairs(actor)
+            keep, rows = [], []
+            for dst, src, lg in pairs:
+                if src.dtype != torch.float32 or dst.dtype not in (torch.float16, torch.float32):
+                    raise ValueError('refresh: float32 sources, fp16 / f32 destinations')
+                m = self._phys_map(dst, src.detach(), lg)
+                if m is not None:
+                    keep.append(m)
+                rows.append(_lib.DtCopyEntry(src.data_ptr(), dst.data_ptr(),
+                                             m.data_ptr() if m is not None else None,
+                                             dst.numel(), 1 if dst.dtype == torch.float16 else 0, 0))
+            arr = (_lib.DtCopyEntry * len(rows))(*rows)
+            table = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(
+                self.w0frag.device)
+            ent = cache[key] = (table, keep, len(rows), max(r.count for r in rows))
+        table, _keep, n, most = ent
+        rc = _lib.lib().dt_refresh_copy(n, table.data_ptr(), most,
+                                        torch.cuda.current_stream(table.device).cuda_stream)
+        if rc != 0:
+            raise _lib.DtError('dt_refresh_copy failed (%d)' % rc)
 
     def _refresh(self, actor):
         convs, bns, lin1, lin2 = actor.layers()

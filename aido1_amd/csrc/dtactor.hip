@@ -427,3 +427,43 @@ extern "C" int dt_actor_head(int32_t n, int32_t n0, int32_t k, const void* h, in
                      (const __half*)w2b, (const __half*)b2b, head, slope, out);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
+
+// ---- the acting copies' refresh in one launch (dt_refresh_copy) --------------------
+namespace {
+
+constexpr int kCopyThreads = 256;
+
+// entry e of the table, element i: dst[i] = cast(src[map ? map[i] : i]), 0 where
+// map[i] < 0; blockIdx.y = entry, x-blocks stride over its elements
+__global__ void __launch_bounds__(kCopyThreads)
+refresh_copy_kernel(int32_t n, const DtCopyEntry* __restrict__ table) {
+  const DtCopyEntry t = table[blockIdx.y];
+  const float* src = static_cast<const float*>(t.src);
+  for (int64_t i = (int64_t)blockIdx.x * kCopyThreads + threadIdx.x; i < t.count;
+       i += (int64_t)gridDim.x * kCopyThreads) {
+    float v;
+    if (t.map) {
+      const int64_t j = t.map[i];
+      v = j >= 0 ? src[j] : 0.0f;
+    } else {
+      v = src[i];
+    }
+    if (t.dst_dtype == 1)
+      static_cast<__half*>(t.dst)[i] = __float2half(v);   // round to nearest, as .half()
+    else
+      static_cast<float*>(t.dst)[i] = v;
+  }
+}
+
+}  // namespace
+
+extern "C" int dt_refresh_copy(int32_t n, const DtCopyEntry* table, int64_t max_count,
+                               void* stream) {
+  if (n < 0 || n > 65535 || (n > 0 && !table) || max_count < 0) return DT_E_ARG;
+  if (n == 0 || max_count == 0) return DT_OK;
+  int64_t gx = (max_count + kCopyThreads * 4 - 1) / (kCopyThreads * 4);
+  gx = gx < 1 ? 1 : (gx > 2048 ? 2048 : gx);
+  hipLaunchKernelGGL(refresh_copy_kernel, dim3((unsigned)gx, (unsigned)n), dim3(kCopyThreads), 0,
+                     (hipStream_t)stream, n, table);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}

@@ -191,6 +191,25 @@ typedef struct DtEpisodeState {
 int dt_episode_account(int32_t n, int32_t k, const double* reward, const double* reward_mod,
                        const uint8_t* done, const DtEpisodeState* state, void* stream);
 
+/* dt_refresh_copy: FusedActor.refresh (reference mode) in one launch: every
+ * acting tensor (the MFMA weight fragments, biases, BatchNorm affine
+ * parameters, the linears in fp16) gathered and converted from the source
+ * actor's float32 parameters.  table: device [n] entries; entry e writes
+ * count elements of dst (in its physical order) from src (float32): element
+ * i = src[map[i]] (map device int64 [count], -1 = 0.0), or src[i] with map
+ * NULL; dst_dtype 0 float32, 1 fp16 (round to nearest).  max_count: the
+ * largest count (the grid's width). */
+typedef struct DtCopyEntry {
+  const void* src;
+  void* dst;
+  const int64_t* map;
+  int64_t count;
+  int32_t dst_dtype;
+  int32_t pad;
+} DtCopyEntry;
+
+int dt_refresh_copy(int32_t n, const DtCopyEntry* table, int64_t max_count, void* stream);
+
 /* dt_actor_head: the actor's output branch after its first linear
  * (config.json actor: leaky_relu -> linear(512 -> 2) -> tanh;
  * duckietown_rl/ddpg.py:58-62) for n samples in one launch, one wave each:

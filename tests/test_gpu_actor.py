@@ -403,9 +403,11 @@ def test_refresh_copies_every_parameter_exactly(gpu, channels_last):
 
 @pytest.mark.parametrize('mode', ['reference', 'eval'])
 def test_graph_refresh_follows_in_place_updates(gpu, mode):
-    """FusedActor.refresh replays a HIP graph captured at the first refresh
-    from a source: after in-place updates of the source's weights (what Adam
-    and the soft update do) every acting tensor equals an eager refresh's."""
+    """FusedActor.refresh on the GPU: one dt_refresh_copy launch through index
+    maps built at the first refresh from a source (reference mode), or a HIP
+    graph captured then (eval mode): after in-place updates of the source's
+    weights (what Adam and the soft update do) every acting tensor equals an
+    eager refresh's bit for bit."""
     from aido1_amd.actor import ConfigActor, FusedActor
     torch.manual_seed(13)
     a = ConfigActor(golden('reference_config.json')['model']['actor']).to(gpu)
@@ -424,4 +426,5 @@ def test_graph_refresh_follows_in_place_updates(gpu, mode):
             if mode == 'eval' and name.startswith(('gamma', 'beta')):
                 continue            # folded into the weights: unused (never written) in eval mode
             assert torch.equal(x, y), (k, name)
-    assert len(f._refresh_graphs) == 1
+    # one capture per source: reference mode's gather table, eval mode's graph
+    assert len(f._refresh_tables if mode == 'reference' else f._refresh_graphs) == 1
