@@ -920,7 +920,7 @@ __device__ __forceinline__ void canny(const RenderArgs& a, RenderLds& S, int e,
 // colour bits, the others the dilation + edge path.
 // kIdx: the frame goes out as palette bytes (a.index) instead of grey floats
 // (a.gray): two instantiations, so the grey path keeps its register budget.
-template <bool kSpill, bool kIdx>
+template <bool kSpill, bool kIdx, bool kBigR>
 __device__ __forceinline__ void write_outputs(const RenderArgs& a, RenderLds& S, int e,
                                               uint8_t* mbase) {
   const int tid = threadIdx.x;
@@ -994,11 +994,14 @@ __device__ __forceinline__ void write_outputs(const RenderArgs& a, RenderLds& S,
                 make_uint4(o[k][0], o[k][1], o[k][2], o[k][3]);
           *reinterpret_cast<uint4*>(mbase + 3 * NPIX + 16 * q) = make_uint4(0u, 0u, 0u, 0u);
         } else {
-          switch (L.dil_r) {
-            case 0: quad_masks<0>(S, sl, L, mbase, q); break;
-            case 1: quad_masks<1>(S, sl, L, mbase, q); break;
-            case 2: quad_masks<2>(S, sl, L, mbase, q); break;
-            default: quad_masks<3>(S, sl, L, mbase, q); break;
+          // radius 2-3 (kernel sizes 5, 7) in their own kernel: their
+          // unrolled ellipses held 450 SGPR spills in every instantiation
+          if (kBigR) {
+            if (L.dil_r == 2) quad_masks<2>(S, sl, L, mbase, q);
+            else quad_masks<3>(S, sl, L, mbase, q);
+          } else {
+            if (L.dil_r == 0) quad_masks<0>(S, sl, L, mbase, q);
+            else quad_masks<1>(S, sl, L, mbase, q);
           }
         }
       }
@@ -1119,6 +1122,7 @@ __device__ __forceinline__ void sched_exit(const RenderArgs& a, RenderLds& S, in
 }
 
 // One env of render_kernel.
+template <bool kIdx, bool kBigR>
 __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, int e
 #ifdef DTSIM_EARLY_MARKS
                                            , const float4 (&mq)[4]
@@ -1361,14 +1365,12 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, in
     if (mbase) canny<false>(a, S, e, nlist);
     RENT(13);
     RENDER_STOP(4);
-    if (a.index) write_outputs<false, true>(a, S, e, mbase);
-    else write_outputs<false, false>(a, S, e, mbase);
+    write_outputs<false, kIdx, kBigR>(a, S, e, mbase);
   } else {
     if (mbase) canny<true>(a, S, e, nlist);
     RENT(13);
     RENDER_STOP(4);
-    if (a.index) write_outputs<true, true>(a, S, e, mbase);
-    else write_outputs<true, false>(a, S, e, mbase);
+    write_outputs<true, kIdx, kBigR>(a, S, e, mbase);
   }
 #ifdef DTSIM_STAMPS
   RENSTAMP(12, (unsigned long long)C[kNList] | ((unsigned long long)C[kNWeak] << 32));
@@ -1383,6 +1385,9 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, in
 #ifndef DTSIM_RENDER_WPE
 #define DTSIM_RENDER_WPE 8
 #endif
+// kIdx: palette-byte frames (a.index) instead of grey floats; kBigR: a
+// dilation radius of 2-3.  Both are fixed for a launch: the host picks.
+template <bool kIdx, bool kBigR>
 __global__ __launch_bounds__(kRenderThreads) __attribute__((amdgpu_waves_per_eu(DTSIM_RENDER_WPE))) void
 render_kernel(RenderArgs a) {
   __shared__ __attribute__((aligned(16))) RenderLds S;
@@ -1433,7 +1438,7 @@ render_kernel(RenderArgs a) {
   }
   __syncthreads();
   e = __builtin_amdgcn_readfirstlane(S.env);   // uniform: kept in an SGPR, as blockIdx was
-  render_env(a, S, e
+  render_env<kIdx, kBigR>(a, S, e
 #ifdef DTSIM_EARLY_MARKS
              , mq
 #endif
@@ -1891,7 +1896,11 @@ int dt_render(dt_handle* h, const dt_render_io* io, void* stream) {
   a.launch = h->render_launches++;
 #endif
   a.list_cap = io->list_cap > 0 && io->list_cap < kListCap ? io->list_cap : kListCap;
-  hipLaunchKernelGGL(render_kernel, dim3(h->n), dim3(kRenderThreads), 0, (hipStream_t)stream, a);
+  const int grid = h->n;
+  const bool big_r = a.line.dil_r >= 2;
+  auto* kern = a.index ? (big_r ? render_kernel<true, true> : render_kernel<true, false>)
+                       : (big_r ? render_kernel<false, true> : render_kernel<false, false>);
+  hipLaunchKernelGGL(kern, dim3(grid), dim3(kRenderThreads), 0, (hipStream_t)stream, a);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) {
     h->err = std::string("dt_render launch: ") + hipGetErrorString(e);
