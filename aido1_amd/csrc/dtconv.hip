@@ -21,6 +21,19 @@
 // diagnostic builds only (tools/conv32_micro.py): bit 0 skips the prefetch
 // loads, 1 the MFMA section, 2 the output stores, 3 the statistics, 4 the ring
 // commit; the product build is 0
+#ifdef DTCONV_STAMPS   // diagnostic: shader-clock stamps inside conv2's steps
+__device__ unsigned long long g_cstamps[8 * 2 * 48 * 8];
+#define CSTAMP(i)                                                                          \
+  do {                                                                                     \
+    if (IH == 57 && (threadIdx.x & 63) == 0 && blockIdx.x < 8 && g < 48)                   \
+      g_cstamps[((blockIdx.x * 2 + (threadIdx.x >> 6)) * 48 + g) * 8 + (i)] =              \
+          __builtin_amdgcn_s_memtime();                                                    \
+  } while (0)
+#else
+#define CSTAMP(i) \
+  do {            \
+  } while (0)
+#endif
 #ifndef DTCONV_SKIP
 #define DTCONV_SKIP 0
 #endif
@@ -707,15 +720,16 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
   // new rows r0..r1 of the k-th sample: chunk q = tid + i*kThreads of the
   // contiguous range into registers, later into the ring as they are
   auto issue = [&](u32x4 (&pre)[kPre], int k, int r0, int r1) __attribute__((always_inline)) {
-    // unconditional (clamped chunk and sample): see stats_load
+    // unconditional (clamped sample; chunks past the rows are buffer loads
+    // out of range, zeros the commit skips): see stats_load.  The chunk
+    // offset is the lane's 16 tid plus a constant: no address VALU a load
     const int cnt = (r1 - r0 + 1) * kRowU4;
     const int ns = sample(k) < send ? sample(k) : send - 1;
-    const u32x4* src = reinterpret_cast<const u32x4*>(x + ((size_t)ns * IH + r0) * IW * CO);
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<__half*>(x + ((size_t)ns * IH + r0) * IW * CO), 0, cnt * 16, 0x00020000);
 #pragma unroll
-    for (int i = 0; i < kPre; ++i) {
-      const int q = tid + i * kThreads;
-      pre[i] = src[q < cnt ? q : cnt - 1];
-    }
+    for (int i = 0; i < kPre; ++i)
+      pre[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, 16 * tid, 16 * i * kThreads, 0);
   };
   // kIn 1: the previous layer's BatchNorm is applied here, once per input
   // element (a thread's chunks all hold channels 8*(tid&3)..+7: kThreads and
@@ -737,7 +751,7 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
       const int r = q / kRowU4, qq = q - r * kRowU4;
       const int slot = (k * IH + r0 + r) % kRing;
       u32x4 u = pre[i];
-      if (kIn == 1) {
+      if (kIn == 1 && !(DTCONV_SKIP & 64)) {   // (64: diagnostic, no norm)
 #pragma unroll
         for (int e = 0; e < 4; ++e)
           u[e] = norm_pair(u[e], csc[2 * e], csh[2 * e], csc[2 * e + 1], csh[2 * e + 1]);
@@ -773,6 +787,7 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
     const bool last_j1 = j1 + 1 == G::kSteps;
     const int k2 = last_j1 ? k1 + 1 : k1;                         // step g+2
     const bool stats2 = g + 2 < total && last_j1;   // step g+2 starts sample k2
+    CSTAMP(0);
     stats_load(k2);
     if (!(DTCONV_SKIP & 1)) issue(nxt, k2, G::first_new(j1), G::last_new(j1));
 
@@ -813,10 +828,12 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
       mm(bq[gy & 1], gy);
       __builtin_amdgcn_sched_barrier(0);
     }
+    CSTAMP(1);
     if (stats2) stats_merge(k2);   // read by step g+2, after two barriers
     float v[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = lrelu2(acc[r], slope);
+    CSTAMP(2);
 
     // epilogue
     if (kOut <= 1) {
@@ -936,8 +953,11 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
 
     // step g+1's rows into the ring: their slots held rows no wave reads in
     // this step; the barrier publishes them for the next
+    CSTAMP(3);
     if (g + 1 < total && !(DTCONV_SKIP & 16)) commit(cur, k1, G::first_new(j), G::last_new(j));
+    CSTAMP(4);
     __syncthreads();
+    CSTAMP(5);
   };
 
   // prologue: step 0's rows into the ring, step 1's into registers
@@ -1054,6 +1074,11 @@ extern "C" int dt_conv1(const float* ring, int32_t n, int32_t slots, const int32
   return dt_conv1_split(ring, n, slots, order, wfrag, bias, nullptr, y, partials, slope, stream);
 }
 
+#ifdef DTCONV_STAMPS
+extern "C" int dt_diag_convstamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cstamps), sizeof(g_cstamps)) == hipSuccess ? 0 : -1;
+}
+#endif
 #ifdef DTCONV_CHECK
 // diagnostic build only: the out-of-bounds word of conv1s_kernel (synchronous;
 // clears it)
