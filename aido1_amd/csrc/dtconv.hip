@@ -21,11 +21,12 @@
 // diagnostic builds only (tools/conv32_micro.py): bit 0 skips the prefetch
 // loads, 1 the MFMA section, 2 the output stores, 3 the statistics, 4 the ring
 // commit; the product build is 0
-#ifdef DTCONV_STAMPS   // diagnostic: shader-clock stamps inside conv2's steps
+#ifdef DTCONV_STAMPS   // diagnostic: shader-clock stamps inside the steps of the layer whose input height is DTCONV_STAMPS (57: conv2, 27: conv3, 12: conv4)
 __device__ unsigned long long g_cstamps[8 * 2 * 48 * 8];
 #define CSTAMP(i)                                                                          \
   do {                                                                                     \
-    if (IH == 57 && (threadIdx.x & 63) == 0 && blockIdx.x < 8 && g < 48)                   \
+    if (IH == DTCONV_STAMPS && (threadIdx.x & 63) == 0 && threadIdx.x < 128 && blockIdx.x < 8 && \
+        g < 48)                                                                            \
       g_cstamps[((blockIdx.x * 2 + (threadIdx.x >> 6)) * 48 + g) * 8 + (i)] =              \
           __builtin_amdgcn_s_memtime();                                                    \
   } while (0)
@@ -898,25 +899,37 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
         // per wave, two passes over its own 32 pixels (shuffles only: exact
         // mean, then M2 about it); the waves' (n, mean, M2) merged with
         // Chan's formula by threads < CO: two barriers a sample, not four
+        // level by level over the 16 channels: each level's 16 shuffles are
+        // in flight together (channel by channel, every shuffle waited for the
+        // one before it: 160 dependent LDS round trips, 16k cycles a sample);
+        // each channel's sums keep their order, so the bits are unchanged
         float nw = valid ? 1.0f : 0.0f;
 #pragma unroll
         for (int o = 16; o > 0; o >>= 1) nw += __shfl_xor(nw, o, 32);
         const float inw = nw > 0.0f ? 1.0f / nw : 0.0f;
+        float sum[16], m2[16];
+#pragma unroll
+        for (int r = 0; r < 16; ++r) sum[r] = valid ? v[r] : 0.0f;
+#pragma unroll
+        for (int o = 16; o > 0; o >>= 1)
+#pragma unroll
+          for (int r = 0; r < 16; ++r) sum[r] += __shfl_xor(sum[r], o, 32);
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
-          float sum = valid ? v[r] : 0.0f;
+          const float d = valid ? v[r] - sum[r] * inw : 0.0f;
+          m2[r] = d * d;
+        }
 #pragma unroll
-          for (int o = 16; o > 0; o >>= 1) sum += __shfl_xor(sum, o, 32);
-          const float mw = sum * inw;
-          const float d = valid ? v[r] - mw : 0.0f;
-          float m2 = d * d;
+        for (int o = 16; o > 0; o >>= 1)
 #pragma unroll
-          for (int o = 16; o > 0; o >>= 1) m2 += __shfl_xor(m2, o, 32);
-          if (col == 0) {
+          for (int r = 0; r < 16; ++r) m2[r] += __shfl_xor(m2[r], o, 32);
+        if (col == 0) {
+#pragma unroll
+          for (int r = 0; r < 16; ++r) {
             const int c = (r & 3) + 8 * (r >> 2) + 4 * h;
             red[wave][c][0] = nw;
-            red[wave][c][1] = mw;
-            red[wave][c][2] = m2;
+            red[wave][c][1] = sum[r] * inw;
+            red[wave][c][2] = m2[r];
           }
         }
         __syncthreads();
