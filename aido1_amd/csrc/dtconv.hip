@@ -35,6 +35,19 @@ __device__ unsigned long long g_cstamps[8 * 2 * 48 * 8];
   do {            \
   } while (0)
 #endif
+#ifdef DTCONV1_STAMPS   // diagnostic: the same stamps inside conv1s_kernel's steps
+__device__ unsigned long long g_c1stamps[8 * 2 * 48 * 8];
+#define C1STAMP(i)                                                                         \
+  do {                                                                                     \
+    if ((threadIdx.x & 63) == 0 && threadIdx.x < 128 && blockIdx.x < 8 && g < 48)         \
+      g_c1stamps[((blockIdx.x * 2 + (threadIdx.x >> 6)) * 48 + g) * 8 + (i)] =             \
+          __builtin_amdgcn_s_memtime();                                                    \
+  } while (0)
+#else
+#define C1STAMP(i) \
+  do {             \
+  } while (0)
+#endif
 #ifndef DTCONV_SKIP
 #define DTCONV_SKIP 0
 #endif
@@ -386,6 +399,7 @@ conv1s_kernel(int n, const void* __restrict__ ring, int slots, int s0, int s1, i
     const bool last_j = j + 1 == kSSteps;
     const int k1 = last_j ? k + 1 : k, j1 = last_j ? 0 : j + 1;   // step g+1
     const int k2 = (j1 + 1 == kSSteps) ? k1 + 1 : k1;             // step g+2
+    C1STAMP(0);
     if (!(DTCONV_SKIP & 1)) issue(nxt, k2, s_first_new(j1), s_last_new(j1));
 
     const int t = kSW * j + wave;
@@ -435,9 +449,11 @@ conv1s_kernel(int n, const void* __restrict__ ring, int slots, int s0, int s1, i
         acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(wa[kSGrp * gy + i], bq[gy % kBD][i], acc, 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);
     }
+    C1STAMP(1);
     float v[16];
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = lrelu2(acc[r], slope);
+    C1STAMP(2);
     if (kStats) centre_px32(v, s_c, j == 0 && wave == 0 && col == 0, j == 0, h);
     if (!(DTCONV_SKIP & 4)) store_px32<kSPix>(y + (size_t)ns * kSPix * CO, pc, v, h, valid);
     if (kStats && !(DTCONV_SKIP & 8)) {
@@ -497,8 +513,11 @@ conv1s_kernel(int n, const void* __restrict__ ring, int slots, int s0, int s1, i
     }
     // step g+1's rows into the ring: their slots hold rows no wave reads in
     // this step; the barrier publishes them for the next
+    C1STAMP(3);
     if (g + 1 < total && !(DTCONV_SKIP & 16)) commit(cur, k1, s_first_new(j), s_last_new(j));
+    C1STAMP(4);
     __syncthreads();
+    C1STAMP(5);
   };
 
   // prologue: step 0's rows into the ring, step 1's into registers
@@ -1090,6 +1109,12 @@ extern "C" int dt_conv1(const float* ring, int32_t n, int32_t slots, const int32
 #ifdef DTCONV_STAMPS
 extern "C" int dt_diag_convstamps(unsigned long long* out) {
   return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_cstamps), sizeof(g_cstamps)) == hipSuccess ? 0 : -1;
+}
+#endif
+#ifdef DTCONV1_STAMPS
+extern "C" int dt_diag_convstamps(unsigned long long* out) {
+  return hipMemcpyFromSymbol(out, HIP_SYMBOL(g_c1stamps), sizeof(g_c1stamps)) == hipSuccess ? 0
+                                                                                          : -1;
 }
 #endif
 #ifdef DTCONV_CHECK
