@@ -26,6 +26,10 @@ ABI_VERSION = 10
 
 HIP_FLAGS = ['--offload-arch=gfx950', '-O3', '-fPIC', '-shared', '-std=c++17',
              '-ffp-contract=off', '-munsafe-fp-atomics']
+# per-source extra flags.  dtrender.hip: no SLP vectorisation -- packed f32
+# VALU (v_pk_*) measured slower in render_kernel: 0.1634 -> 0.1618 ms, nine
+# paired runs; the other sources are neutral or slower with it.
+FILE_FLAGS = {'dtrender.hip': ['-fno-slp-vectorize']}
 
 
 class DtError(RuntimeError):
@@ -105,17 +109,44 @@ CHECK_LIB_PATH = os.path.join(PKG_DIR, 'libdtsim_check.so')
 
 def build(force=False, verbose=False, path=LIB_PATH, defines=()):
     """Compile libdtsim.so (or a diagnostic variant at `path` with -D defines)
-    for gfx950 in-tree."""
+    for gfx950 in-tree: each source to an object (its FILE_FLAGS added),
+    in parallel, then one shared link."""
     if not force and path == LIB_PATH and not _stale():
         return LIB_PATH
+    import shutil
+    import tempfile
+    from concurrent.futures import ThreadPoolExecutor
     tmp = path + '.tmp%d' % os.getpid()
-    cmd = [HIPCC] + HIP_FLAGS + ['-D' + d for d in defines] + ['-o', tmp] + _sources()
-    if verbose:
-        print(' '.join(cmd))
-    r = subprocess.run(cmd, capture_output=True, text=True)
-    if r.returncode != 0:
-        raise DtError('hipcc failed building %s:\n' % os.path.basename(path) + r.stderr[-4000:])
-    os.replace(tmp, path)
+    objdir = tempfile.mkdtemp(prefix='dtsim_build_')
+    try:
+        cflags = [f for f in HIP_FLAGS if f != '-shared'] + ['-D' + d for d in defines]
+        jobs = []
+        for src in _sources():
+            obj = os.path.join(objdir, os.path.basename(src) + '.o')
+            extra = FILE_FLAGS.get(os.path.basename(src), [])
+            jobs.append(([HIPCC] + cflags + extra + ['-c', src, '-o', obj], obj))
+        if verbose:
+            for cmd, _ in jobs:
+                print(' '.join(cmd))
+
+        def run(cmd):
+            return subprocess.run(cmd, capture_output=True, text=True)
+        with ThreadPoolExecutor(max_workers=min(8, len(jobs))) as ex:
+            results = list(ex.map(run, [c for c, _ in jobs]))
+        for (cmd, _), r in zip(jobs, results):
+            if r.returncode != 0:
+                raise DtError('hipcc failed building %s (%s):\n' % (
+                    os.path.basename(path), os.path.basename(cmd[-3])) + r.stderr[-4000:])
+        link = [HIPCC, '--offload-arch=gfx950', '-shared', '-fPIC', '-o', tmp] + \
+            [o for _, o in jobs]
+        if verbose:
+            print(' '.join(link))
+        r = subprocess.run(link, capture_output=True, text=True)
+        if r.returncode != 0:
+            raise DtError('hipcc failed linking %s:\n' % os.path.basename(path) + r.stderr[-4000:])
+        os.replace(tmp, path)
+    finally:
+        shutil.rmtree(objdir, ignore_errors=True)
     return path
 
 
