@@ -1373,6 +1373,9 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, in
     write_outputs<true, kIdx, kBigR>(a, S, e, mbase);
   }
 #ifdef DTSIM_STAMPS
+  // every wave's end (real time): [19 + w/2] for waves 1,3,5,7 -> [19..22]
+  if ((threadIdx.x & 63) == 0 && (threadIdx.x >> 6) & 1 && e < 4096)
+    g_renstamps[e * 24 + 19 + (threadIdx.x >> 7)] = __builtin_amdgcn_s_memrealtime();
   RENSTAMP(12, (unsigned long long)C[kNList] | ((unsigned long long)C[kNWeak] << 32));
   RENSTAMP(15, (unsigned long long)C[kNSeg]);
   RENSTAMP(14, __builtin_amdgcn_s_memtime());
@@ -1393,11 +1396,9 @@ render_kernel(RenderArgs a) {
   __shared__ __attribute__((aligned(16))) RenderLds S;
   const int tid = threadIdx.x;
 #ifdef DTSIM_STAMPS
-  {
-    const int e = blockIdx.x;
-    RENSTAMP(16, __builtin_amdgcn_s_memtime());
-    RENSTAMP(17, __builtin_amdgcn_s_memrealtime());
-  }
+  // the entry times, stored under the env this block renders (known after
+  // the dispatch-order lookup below), like every other stamp
+  const unsigned long long t16 = __builtin_amdgcn_s_memtime(), t17 = __builtin_amdgcn_s_memrealtime();
 #endif
   const LineDev& L = a.line;
   if (tid < PAL_N) {
@@ -1438,6 +1439,10 @@ render_kernel(RenderArgs a) {
   }
   __syncthreads();
   e = __builtin_amdgcn_readfirstlane(S.env);   // uniform: kept in an SGPR, as blockIdx was
+#ifdef DTSIM_STAMPS
+  RENSTAMP(16, t16);
+  RENSTAMP(17, t17);
+#endif
   render_env<kIdx, kBigR>(a, S, e
 #ifdef DTSIM_EARLY_MARKS
              , mq

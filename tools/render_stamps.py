@@ -137,6 +137,16 @@ def main():
         g = np.array(gaps)
         print('end -> next start on a CU: median %.2f us, p90 %.2f us, max %.2f us'
               % (np.median(g), np.percentile(g, 90), g.max()))
+    # the waves' ends: thread 0's [1] against waves 1, 3, 5, 7 ([19..22])
+    wend = b[..., 19:23]
+    ok = (wend > 0).all(-1)
+    if ok.any():
+        lastw = np.maximum(wend.max(-1), b[..., 1])[ok]
+        print('wave ends after thread 0\'s: median %.2f us, p90 %.2f us; the last wave is '
+              'wave 0 in %.0f %% of the workgroups'
+              % (np.median((lastw - b[..., 1][ok]) / 100.0),
+                 np.percentile((lastw - b[..., 1][ok]) / 100.0, 90),
+                 100 * np.mean(b[..., 1][ok] >= wend.max(-1)[ok])))
     hist = np.histogram(t_start, bins=10, range=(0, span))[0]
     print('workgroup starts per tenth of the span:', hist.tolist())
     env.close()
