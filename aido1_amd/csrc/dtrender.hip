@@ -304,6 +304,13 @@ struct RenderArgs {
   int32_t n;
   uint32_t* sched;   // dispatch order state (kSchedHead + cost[n] + perm[2][n]), or null
   uint32_t launch;   // the handle's render launch count (host side): perm[launch & 1] is read
+  // dt_render2: a second decision in the same grid (block 2b + 1 renders env
+  // perm[b] of it; its pose, ring slot, fresh flags and masks), pair = 1
+  int32_t pair;
+  int32_t slot2;
+  const double* pose2;      // [3, n]
+  const uint8_t* fresh2;
+  uint8_t* masks2;
 };
 
 // ---- fused render kernel ----------------------------------------------------------
@@ -922,15 +929,22 @@ __device__ __forceinline__ void canny(const RenderArgs& a, RenderLds& S, int e,
 // (a.gray): two instantiations, so the grey path keeps its register budget.
 template <bool kSpill, bool kIdx, bool kBigR>
 __device__ __forceinline__ void write_outputs(const RenderArgs& a, RenderLds& S, int e,
-                                              uint8_t* mbase) {
+                                              uint8_t* mbase, int half) {
   const int tid = threadIdx.x;
   constexpr int T = kRenderThreads;
   const LineDev& L = a.line;
   const Slots<kSpill> sl{S, a.spill + (size_t)e * kSpillHalves,
                          a.spill + (size_t)e * kSpillHalves + 4 * NW, a.list_cap};
-  const bool fresh = a.fresh != nullptr && a.fresh[e] != 0;
-  float* gbase = !kIdx && a.gray ? a.gray + (size_t)e * a.slots * NPIX : nullptr;
-  uint8_t* ibase = kIdx ? a.index + (size_t)e * a.slots * NPIX : nullptr;
+  const uint8_t* fr = half ? a.fresh2 : a.fresh;
+  const bool fresh = fr != nullptr && fr[e] != 0;
+  const int slot = half ? a.slot2 : a.slot;
+  // a pair's first decision never writes the second's slot (the second
+  // writes it for every env, so such a store is dead and would race), and
+  // writes no frame for an env the second decision refills
+  const int skip = a.pair && !half ? a.slot2 : -1;
+  const bool dead = a.pair && !half && a.fresh2 != nullptr && a.fresh2[e] != 0;
+  float* gbase = !kIdx && a.gray && !dead ? a.gray + (size_t)e * a.slots * NPIX : nullptr;
+  uint8_t* ibase = kIdx && !dead ? a.index + (size_t)e * a.slots * NPIX : nullptr;
   const uint32_t blo = S.bits_lo, bhi = S.bits_hi;
   const bool quick_masks = L.dil_r <= 1;
   const int lane = tid & 63;
@@ -946,9 +960,9 @@ __device__ __forceinline__ void write_outputs(const RenderArgs& a, RenderLds& S,
             if (fresh) {
 #pragma clang loop vectorize(disable) interleave(disable)
               for (int k = 0; k < a.slots; ++k)
-                *reinterpret_cast<uint32_t*>(ibase + k * NPIX + 4 * w) = v;
+                if (k != skip) *reinterpret_cast<uint32_t*>(ibase + k * NPIX + 4 * w) = v;
             } else {
-              *reinterpret_cast<uint32_t*>(ibase + a.slot * NPIX + 4 * w) = v;
+              *reinterpret_cast<uint32_t*>(ibase + slot * NPIX + 4 * w) = v;
             }
           }
           if (!kIdx) {
@@ -960,9 +974,9 @@ __device__ __forceinline__ void write_outputs(const RenderArgs& a, RenderLds& S,
             if (fresh) {
 #pragma clang loop vectorize(disable) interleave(disable)
               for (int k = 0; k < a.slots; ++k)
-                *reinterpret_cast<float4*>(gbase + k * NPIX + 4 * w) = g;
+                if (k != skip) *reinterpret_cast<float4*>(gbase + k * NPIX + 4 * w) = g;
             } else {
-              *reinterpret_cast<float4*>(gbase + a.slot * NPIX + 4 * w) = g;
+              *reinterpret_cast<float4*>(gbase + slot * NPIX + 4 * w) = g;
             }
           }
         }
@@ -1105,7 +1119,7 @@ __device__ __forceinline__ void sched_build(const RenderArgs& a, RenderLds& S, u
 
 // the builder's ticket
 __device__ __forceinline__ uint32_t sched_builder(const RenderArgs& a) {
-  return (uint32_t)(a.n - kSchedTail);   // dt_render: n > kSchedTail
+  return (uint32_t)((a.pair ? 2 : 1) * a.n - kSchedTail);   // dt_render: n > kSchedTail
 }
 
 // exit of a workgroup: its cost (thread 0, no wait); the builder sorts
@@ -1123,7 +1137,7 @@ __device__ __forceinline__ void sched_exit(const RenderArgs& a, RenderLds& S, in
 
 // One env of render_kernel.
 template <bool kIdx, bool kBigR>
-__device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, int e
+__device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, int e, int half
 #ifdef DTSIM_EARLY_MARKS
                                            , const float4 (&mq)[4]
 #endif
@@ -1289,7 +1303,8 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, in
   // byte).  Non-uniform words get a slot (the list); a quad with one takes
   // the dilation path of the output phase (every quad does when the dilation
   // radius is >= 2: uniformity only covers +-1 pixel).
-  uint8_t* mbase = a.masks ? a.masks + (size_t)e * 4 * NPIX : nullptr;
+  uint8_t* const mb0 = half ? a.masks2 : a.masks;
+  uint8_t* mbase = mb0 ? mb0 + (size_t)e * 4 * NPIX : nullptr;
   constexpr int kQuadPer = (NQ + T - 1) / T;  // quads per lane (3 at 512 threads)
   if (mbase) {
     bool non[4 * kQuadPer];
@@ -1365,12 +1380,12 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, in
     if (mbase) canny<false>(a, S, e, nlist);
     RENT(13);
     RENDER_STOP(4);
-    write_outputs<false, kIdx, kBigR>(a, S, e, mbase);
+    write_outputs<false, kIdx, kBigR>(a, S, e, mbase, half);
   } else {
     if (mbase) canny<true>(a, S, e, nlist);
     RENT(13);
     RENDER_STOP(4);
-    write_outputs<true, kIdx, kBigR>(a, S, e, mbase);
+    write_outputs<true, kIdx, kBigR>(a, S, e, mbase, half);
   }
 #ifdef DTSIM_STAMPS
   // every wave's end (real time): [19 + w/2] for waves 1,3,5,7 -> [19..22]
@@ -1415,7 +1430,10 @@ render_kernel(RenderArgs a) {
   for (int i = tid; i < a.width * a.height; i += kRenderThreads) S.kind[i] = a.kind[i];
   // the camera frame, once per workgroup (wave 1; wave 0 has the palette), of
   // the env the dispatch order gives this block
-  int e = blockIdx.x;
+  // dt_render2: blocks 2b and 2b + 1 render env perm[b] of the two decisions
+  const int half = a.pair ? (int)(blockIdx.x & 1u) : 0;
+  const int blk = a.pair ? (int)(blockIdx.x >> 1) : (int)blockIdx.x;
+  int e = blk;
 #ifdef DTSIM_EARLY_MARKS
   float4 mq[4];
   {
@@ -1430,12 +1448,17 @@ render_kernel(RenderArgs a) {
 #endif
   if (tid == 64) {
     if (a.sched) {
-      const int p = sched_perm(a, a.launch)[blockIdx.x];
-      e = (unsigned)p < (unsigned)a.n ? p : (int)blockIdx.x;   // (always a permutation)
+      const int p = sched_perm(a, a.launch)[blk];
+      e = (unsigned)p < (unsigned)a.n ? p : blk;   // (always a permutation)
     }
     S.env = e;
     S.t0 = __builtin_amdgcn_s_memtime();
-    S.view = view_of(a.x[e], a.z[e], a.angle[e], a.cam_fwd);
+    if (half) {
+      const size_t n = (size_t)a.n;
+      S.view = view_of(a.pose2[e], a.pose2[n + e], a.pose2[2 * n + e], a.cam_fwd);
+    } else {
+      S.view = view_of(a.x[e], a.z[e], a.angle[e], a.cam_fwd);
+    }
   }
   __syncthreads();
   e = __builtin_amdgcn_readfirstlane(S.env);   // uniform: kept in an SGPR, as blockIdx was
@@ -1443,7 +1466,7 @@ render_kernel(RenderArgs a) {
   RENSTAMP(16, t16);
   RENSTAMP(17, t17);
 #endif
-  render_env<kIdx, kBigR>(a, S, e
+  render_env<kIdx, kBigR>(a, S, e, half
 #ifdef DTSIM_EARLY_MARKS
              , mq
 #endif
@@ -1856,8 +1879,34 @@ int dt_set_line_params(dt_handle* h, const dt_line_params* p) {
   return DT_OK;
 }
 
+static int render_launch(dt_handle* h, const dt_render_io* io, const dt_render_io* io2,
+                         void* stream);
+
 int dt_render(dt_handle* h, const dt_render_io* io, void* stream) {
+  return render_launch(h, io, nullptr, stream);
+}
+
+int dt_render2(dt_handle* h, const dt_render_io* io_a, const dt_render_io* io_b, void* stream) {
+  if (!h || !io_a || !io_b) return DT_E_ARG;
+  if (!io_a->pose || !io_b->pose || io_a->rgb || io_b->rgb || io_a->gray != io_b->gray ||
+      io_a->index != io_b->index || io_a->gray_slots != io_b->gray_slots ||
+      io_a->list_cap != io_b->list_cap || (io_a->masks == nullptr) != (io_b->masks == nullptr) ||
+      (io_a->masks && io_a->masks == io_b->masks) ||
+      ((io_a->gray || io_a->index) && io_a->gray_slot == io_b->gray_slot)) {
+    h->err = "dt_render2: two decisions of one ring: both poses given, the same ring, "
+             "different slots, separate masks, no rgb";
+    return DT_E_ARG;
+  }
+  return render_launch(h, io_a, io_b, stream);
+}
+
+static int render_launch(dt_handle* h, const dt_render_io* io, const dt_render_io* io2,
+                         void* stream) {
   if (!h || !io) return DT_E_ARG;
+  if (io2 && (io2->gray_slots < 1 || io2->gray_slot < 0 || io2->gray_slot >= io2->gray_slots)) {
+    h->err = "dt_render2: gray_slot out of range";
+    return DT_E_ARG;
+  }
   if (io->gray && io->index) {
     h->err = "dt_render: gray and index are two formats of one frame ring: give one";
     return DT_E_ARG;
@@ -1901,7 +1950,14 @@ int dt_render(dt_handle* h, const dt_render_io* io, void* stream) {
   a.launch = h->render_launches++;
 #endif
   a.list_cap = io->list_cap > 0 && io->list_cap < kListCap ? io->list_cap : kListCap;
-  const int grid = h->n;
+  if (io2) {
+    a.pair = 1;
+    a.slot2 = io2->gray_slot;
+    a.pose2 = io2->pose;
+    a.fresh2 = io2->fresh;
+    a.masks2 = io2->masks;
+  }
+  const int grid = (io2 ? 2 : 1) * h->n;
   const bool big_r = a.line.dil_r >= 2;
   auto* kern = a.index ? (big_r ? render_kernel<true, true> : render_kernel<true, false>)
                        : (big_r ? render_kernel<false, true> : render_kernel<false, false>);

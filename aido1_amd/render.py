@@ -195,6 +195,42 @@ def bind_render(env, out, stream, fresh=None, pose=None):
     return launch
 
 
+def _render2_ios(env, out, masks_b, fresh_a, pose_a, fresh_b, pose_b):
+    if out.masks is None or masks_b is None or masks_b.shape != out.masks.shape or \
+            masks_b.data_ptr() == out.masks.data_ptr() or out.rgb is not None:
+        raise ValueError('render2: a second masks buffer of out.masks\' shape, no rgb')
+    if pose_a is None or pose_b is None:
+        raise ValueError('render2: both decisions\' pose snapshots')
+    io_a = _render_io(env, out, fresh_a, pose_a, 0)
+    io_b = _render_io(env, out, fresh_b, pose_b, 0)
+    io_b.masks = ctypes.c_void_p(masks_b.data_ptr())
+    return io_a, io_b
+
+
+def render2_into(env, out, masks_b, fresh_a, pose_a, fresh_b, pose_b):
+    """Two consecutive decisions' renders in ONE launch (dt_render2): the
+    earlier (pose_a, fresh_a) into out.masks and the ring slot after the
+    newest, the later (pose_b, fresh_b) into masks_b and the slot after that.
+    Every output equals render_into(a) then render_into(b)."""
+    io_a, io_b = _render2_ios(env, out, masks_b, fresh_a, pose_a, fresh_b, pose_b)
+    rc = env._L.dt_render2(env._h, ctypes.byref(io_a), ctypes.byref(io_b), env._stream())
+    env._check(rc, 'dt_render2')
+    return out
+
+
+def bind_render2(env, out, stream, masks_b, fresh_a, pose_a, fresh_b, pose_b):
+    """bind_render for render2_into (two decisions, one launch)."""
+    io_a, io_b = _render2_ios(env, out, masks_b, fresh_a, pose_a, fresh_b, pose_b)
+    fn, h, st = env._L.dt_render2, env._h, ctypes.c_void_p(stream.cuda_stream)
+    ra, rb = ctypes.byref(io_a), ctypes.byref(io_b)
+    keep = (out, masks_b, fresh_a, pose_a, fresh_b, pose_b, io_a, io_b, stream)
+
+    def launch():
+        keep  # noqa: B018
+        return fn(h, ra, rb, st)
+    return launch
+
+
 def line_detect(bgr, params=None, hsv=False, stream=None):
     """LineDetectorHSV.setImage + _colorFilter (features/line_detector1.py
     :134-141, :36-57) on a [n, h, w, 3] uint8 BGR CUDA tensor of any size.

@@ -105,6 +105,9 @@ def parse(argv=None):
     p.add_argument('--overlap', action='store_true',
                    help='train: run each update beside the next rollout (side stream); a '
                         'different schedule (acting one update behind), DESIGN 3.8')
+    p.add_argument('--no-pair', action='store_true',
+                   help='config 3 many modes: one decision a render launch (dt_render) '
+                        'instead of two (dt_render2)')
     p.add_argument('--many', type=int, default=20,
                    help='most decisions per dt_step_many launch (lane config, and the render '
                         'config\'s many mode); K decisions are split into ceil(K / many) '
@@ -594,8 +597,14 @@ class ObsLoop:
                the snapshot on another: step d + 1 beside render d.
     Every mode computes the same frames, masks and step outputs."""
 
-    def __init__(self, env, ro, torch, mode='many', chunk=20, event_stride=1):
+    def __init__(self, env, ro, torch, mode='many', chunk=20, event_stride=1, pair=True):
         self.env, self.ro, self.torch, self.mode = env, ro, torch, mode
+        # 'many' / 'many2': two consecutive decisions' renders a launch
+        # (dt_render2, one drain for both), their masks in two buffers
+        self.pair = bool(pair) and mode in ('many', 'many2') and ro.masks is not None
+        self.masks_b = torch.zeros_like(ro.masks) if self.pair else None
+        self.last_masks = ro.masks
+        self.launches = []    # per render launch: the decisions it renders
         # pipe mode orders the step stream on the render end events: all recorded
         self.event_stride = 1 if mode == 'pipe' else max(1, int(event_stride))
         lo, hi = torch.cuda.Stream.priority_range()
@@ -617,9 +626,10 @@ class ObsLoop:
         """The foreign calls of len(actions) decisions writing `out` (a
         StepOutput of k * n entries), built and checked before the timed region
         (the ring slots are taken here, in decision order)."""
-        from aido1_amd.render import bind_render
+        from aido1_amd.render import bind_render, bind_render2
         env, n, k = self.env, self.env.n, int(actions.shape[0])
         groups = []
+        self.launches = []
         if self.mode in ('many', 'many2'):
             for c, (a, b) in enumerate(_bounds(split_even(k, self.chunk))):
                 # many2: chunk c's poses in half c % 2 (its renders overlap step c + 1)
@@ -627,12 +637,28 @@ class ObsLoop:
                 pose = self.pose[h:h + b - a]
                 step = env.bind_step_many(actions[a:b], _Slice(out, a, b, n), pose=pose,
                                           stream=self.s_step)
-                rend = [bind_render(env, self.ro, self.s_rend, fresh=out.done[d * n:(d + 1) * n],
-                                    pose=pose[d - a]) for d in range(a, b)]
+                rend = []
+                d = a
+                while d < b:
+                    fr = out.done[d * n:(d + 1) * n]
+                    if self.pair and d + 1 < b:
+                        rend.append(bind_render2(env, self.ro, self.s_rend, self.masks_b, fr,
+                                                 pose[d - a], out.done[(d + 1) * n:(d + 2) * n],
+                                                 pose[d + 1 - a]))
+                        self.launches.append((d, d + 1))
+                        self.last_masks = self.masks_b
+                        d += 2
+                    else:
+                        rend.append(bind_render(env, self.ro, self.s_rend, fresh=fr,
+                                                pose=pose[d - a]))
+                        self.launches.append((d,))
+                        self.last_masks = self.ro.masks
+                        d += 1
                 groups.append((a, step, None, rend))
             return groups
         serial = self.mode == 'serial'
         for d in range(k):
+            self.launches.append((d,))
             o = _Slice(out, d, d + 1, n)
             pose = None if serial else self.pose[d % 2]
             groups.append((d, env.bind_step(actions[d], o, self.s_step),
@@ -647,6 +673,7 @@ class ObsLoop:
         ss, sr = self.s_step, self.s_rend
         ss.wait_stream(torch.cuda.current_stream(env.device))
         rcs = 0
+        li = 0    # render launch index (events are per launch)
         for c, (d0, step, copy, rends) in enumerate(groups):
             if self.mode == 'pipe' and d0 >= 2:
                 ss.wait_event(t_rend[d0 - 2][1])
@@ -660,13 +687,14 @@ class ObsLoop:
             if sr is not ss:
                 ev_step[d0].record(ss)
                 sr.wait_event(ev_step[d0])
-            for i, rend in enumerate(rends):
-                timed = (d0 + i) % self.event_stride == 0
+            for rend in rends:
+                timed = li % self.event_stride == 0
                 if timed:
-                    t_rend[d0 + i][0].record(sr)
+                    t_rend[li][0].record(sr)
                 rcs |= rend()
                 if timed:
-                    t_rend[d0 + i][1].record(sr)
+                    t_rend[li][1].record(sr)
+                li += 1
             if self.mode == 'many2':
                 ev_done[d0].record(sr)
         torch.cuda.current_stream(env.device).wait_stream(sr)
@@ -686,7 +714,8 @@ def bench_obs(args, ctx):
     g.manual_seed(args.seed + 7919 * rank)
     actions = torch.rand(W + K, n, 2, generator=g, device=dev, dtype=torch.float32)
     ro = RenderOutput(n, dev)          # 3-slot grey ring (Transformer stack) + 4 masks
-    loop = ObsLoop(env, ro, torch, args.obs_mode, args.many, args.event_stride)
+    loop = ObsLoop(env, ro, torch, args.obs_mode, args.many, args.event_stride,
+                   pair=not args.no_pair)
     env.reset()
     wout = StepOutput(max(W, 1) * n, dev, lanepos=False, tile=False)
     if W and loop.run(loop.bind(actions[:W], wout), loop.events(W)):
@@ -710,13 +739,18 @@ def bench_obs(args, ctx):
     st = env.stats()
     env.check()
     tot, tmax, per = rank_report(ctx, [st['sim_steps'], st['decisions'], st['resets']], elapsed)
-    rend_ms = [a.elapsed_time(b) for d, (a, b) in enumerate(ev[1]) if d % loop.event_stride == 0]
+    rend_ms = [ev[1][li][0].elapsed_time(ev[1][li][1]) for li in range(len(loop.launches))
+               if li % loop.event_stride == 0]
     starts = [g[0] for g in calls]
     step_ms = [ev[2][d][0].elapsed_time(ev[2][d][1]) for d in starts]
 
     parity = None
     if not args.no_parity:
-        parity = step_parity(env, start, actions[W:], out, rank, args, frames=ro)
+        # the last decision's masks: its own buffer when it closed a render pair
+        import types
+        frames = types.SimpleNamespace(slots=ro.slots, stack_view=ro.stack_view,
+                                       masks=loop.last_masks)
+        parity = step_parity(env, start, actions[W:], out, rank, args, frames=frames)
     parity = worst_over_ranks(ctx, parity, STEP_PARITY_KEYS + ['gray_mismatches',
                                                                'mask_mismatches'])
     # the roofline's kernel time: an event-only pass after the timed region
@@ -724,7 +758,7 @@ def bench_obs(args, ctx):
     # every --event-stride-th launch only: an event pair per launch adds ~6 us
     # a decision of stream packets to the wall time)
     KE = max(K, args.roofline_launches)
-    ev_loop = ObsLoop(env, ro, torch, args.obs_mode, args.many, 1)
+    ev_loop = ObsLoop(env, ro, torch, args.obs_mode, args.many, 1, pair=not args.no_pair)
     ev_act = torch.rand(KE, n, 2, generator=g, device=dev, dtype=torch.float32)
     ev_out = StepOutput(KE * n, dev, lanepos=False, tile=False)
     env.stats(reset=True)
@@ -733,7 +767,20 @@ def bench_obs(args, ctx):
         raise RuntimeError('a call of the roofline pass failed')
     ctx.sync()
     ev_st = env.stats()
-    rend_all = [a.elapsed_time(b) for a, b in ev_all[1]]
+    nl = len(ev_loop.launches)
+    rend_all = [ev_all[1][li][0].elapsed_time(ev_all[1][li][1]) for li in range(nl)]
+    # the pass's algorithmic bytes, exactly: every decision's grey frame +
+    # masks + pose, the refill of respawned envs' other slots, less the stores
+    # a render pair does not make (dt_render2: the earlier decision's frame
+    # store into the later one's slot, and its whole frame for envs the later
+    # decision refills)
+    dn = ev_out.done.view(KE, n).to(torch.int64)
+    frame_b = RENDER_BYTES_PER_FRESH // 2
+    pass_bytes = KE * RENDER_BYTES_PER_ENV * n + RENDER_BYTES_PER_FRESH * int(dn.sum())
+    for la in ev_loop.launches:
+        if len(la) == 2:
+            fa, fb = dn[la[0]], dn[la[1]]
+            pass_bytes -= frame_b * int((fb * (1 + fa) + (1 - fb) * fa).sum())
     env.close()
     lane = None if args.no_lane else lane_record(args, ctx, args.lane_steps, args.lane_warmup,
                                                  cpu=True)
@@ -749,7 +796,8 @@ def bench_obs(args, ctx):
     if rank == 0:
         kms = float(np.mean(rend_all))
         fresh_per_launch = ev_st['resets'] / KE
-        bpl = RENDER_BYTES_PER_ENV * n + RENDER_BYTES_PER_FRESH * fresh_per_launch
+        bpl = pass_bytes / nl
+        per_launch_dec = KE / nl
         achieved = bpl / (kms * 1e-3) / 1e9
         pmc = load_pmc('render_kernel') or {}
         line = {
@@ -766,9 +814,12 @@ def bench_obs(args, ctx):
                        'actions': 'U[0,1)^2 wheel velocities, resident in HBM',
                        'launch': {
                            'many': 'dt_step_many over chunks of <= %d decisions (each '
-                                   'decision\'s end pose written), then each decision\'s '
-                                   'dt_render of that pose with its done flags as fresh; one '
-                                   'stream, prebound calls' % args.many,
+                                   'decision\'s end pose written), then the chunk\'s renders, '
+                                   'each of its decision\'s pose with its done flags as fresh, '
+                                   '%s; one stream, prebound calls'
+                                   % (args.many, 'two consecutive decisions a launch '
+                                      '(dt_render2, each decision its own masks buffer)'
+                                      if loop.pair else 'one decision a launch (dt_render)'),
                            'many2': 'dt_step_many over chunks of <= %d decisions on a step '
                                     'stream (each decision\'s end pose written, two pose '
                                     'buffers), each decision\'s dt_render of that pose on a '
@@ -793,11 +844,16 @@ def bench_obs(args, ctx):
                          'max_kernel_ms': float(np.max(rend_all)),
                          'timed_region_sampled_ms': float(np.mean(rend_ms)),
                          'algorithmic_bytes_per_launch': bpl,
+                         'decisions_per_launch': per_launch_dec,
                          'algorithmic_basis': 'per env: grey f32 76,800 + 4 u8 masks 76,800 '
                                               'written + pose 24 read (SURVEY §8d config 3 '
                                               'without the step\'s 81 B); plus 153,600 B of '
-                                              'ring refill per respawned env (%.1f per launch)'
-                                              % fresh_per_launch,
+                                              'ring refill per respawned env (%.1f per '
+                                              'decision), per decision; a dt_render2 launch '
+                                              'holds two decisions, less the stores it does not '
+                                              'make (the earlier decision\'s frame where the '
+                                              'later one writes or refills), counted from the '
+                                              'done flags' % fresh_per_launch,
                          'timing': 'HIP events on the render stream around every dt_render of '
                                    'a %d-decision pass right after the timed region (same '
                                    'envs, launches and streams; %d launches averaged); '

@@ -292,6 +292,15 @@ int dt_palette_gray(float* gray8);
  * launch's workgroups by it); the order never changes an output. */
 int dt_render(dt_handle* h, const dt_render_io* io, void* stream);
 
+/* Two consecutive decisions' renders in one launch (one drain for both):
+ * io_a the earlier decision, io_b the later, each with its pose snapshot
+ * (dt_step_many's per-decision poses), its ring slot (different slots of one
+ * ring), its fresh flags and its own masks buffer; no rgb.  Every output
+ * equals dt_render(io_a) followed by dt_render(io_b): io_a's stores that
+ * io_b overwrites are not made (io_a never writes io_b's slot; an env io_b
+ * refills gets no io_a frame), so the two halves never write one byte. */
+int dt_render2(dt_handle* h, const dt_render_io* io_a, const dt_render_io* io_b, void* stream);
+
 /* Diagnostics of that dispatch order (synchronises): launches so far, each
  * env's last recorded cost (shader cycles) and the order the next launch
  * dispatches in (a permutation of 0..n-1).  cost / order: host [n] or NULL. */

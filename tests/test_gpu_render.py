@@ -233,3 +233,38 @@ def test_render_dispatch_order(gpu):
             assert np.array_equal(out.ring[:, 0].cpu().numpy(), g)
         if n > 512:   # the later launches really ran in another order
             assert not np.array_equal(order, np.arange(n))
+
+
+@pytest.mark.parametrize('frames', ['gray', 'index'])
+@pytest.mark.parametrize('n', [1024, 300])
+def test_render2_matches_two_renders(gpu, frames, n):
+    """dt_render2 (two consecutive decisions in one launch) leaves the frame
+    ring and both decisions' masks exactly as dt_render of the first then of
+    the second: with fresh flags in either, both or neither decision, over
+    several pairs (the first pair right after the ring's creation)."""
+    from aido1_amd.render import RenderOutput, render2_into
+    from aido1_amd.vec_env import VecEnv
+    env = VecEnv(n, seed=21)
+    env.reset()
+    ref = RenderOutput(n, gpu, frames=frames)
+    pair = RenderOutput(n, gpu, frames=frames)
+    masks_b = torch.zeros_like(pair.masks)
+    g = torch.Generator(device=gpu)
+    g.manual_seed(5)
+    for it in range(4):
+        poses, fresh = [], []
+        for _ in range(2):
+            env.step_into(torch.rand(n, 2, generator=g, device=gpu))
+            p = torch.empty(3, n, dtype=torch.float64, device=gpu)
+            env.copy_pose(p)
+            poses.append(p)
+            fresh.append((torch.rand(n, generator=g, device=gpu) < 0.3).to(torch.uint8))
+        env.render_into(ref, fresh=fresh[0], pose=poses[0])
+        masks_a_ref = ref.masks.clone()
+        env.render_into(ref, fresh=fresh[1], pose=poses[1])
+        render2_into(env, pair, masks_b, fresh[0], poses[0], fresh[1], poses[1])
+        torch.cuda.synchronize()
+        assert pair.slot == ref.slot
+        assert torch.equal(pair.masks, masks_a_ref), it
+        assert torch.equal(masks_b, ref.masks), it
+        assert torch.equal(pair.ring, ref.ring), it
