@@ -193,6 +193,7 @@ def lib():
             'dt_lane_pos': (ctypes.c_int, [vp, vp, vp, vp]),
             'dt_render': (ctypes.c_int, [vp, vp, vp]),
             'dt_render2': (ctypes.c_int, [vp, vp, vp, vp]),
+            'dt_render3': (ctypes.c_int, [vp, vp, vp, vp, vp]),
             'dt_copy_pose': (ctypes.c_int, [vp, vp, vp]),
             'dt_render_order': (ctypes.c_int, [vp, ctypes.POINTER(u32), vp, vp]),
             'dt_palette_gray': (ctypes.c_int, [ctypes.POINTER(ctypes.c_float)]),

@@ -304,13 +304,17 @@ struct RenderArgs {
   int32_t n;
   uint32_t* sched;   // dispatch order state (kSchedHead + cost[n] + perm[2][n]), or null
   uint32_t launch;   // the handle's render launch count (host side): perm[launch & 1] is read
-  // dt_render2: a second decision in the same grid (block 2b + 1 renders env
-  // perm[b] of it; its pose, ring slot, fresh flags and masks), pair = 1
-  int32_t pair;
-  int32_t slot2;
+  // dt_render2 / dt_render3: parts = 2 or 3 consecutive decisions in the
+  // same grid (block P b + p renders env perm[b] of decision p; decision 0 is
+  // the fields above, 1 and 2 these: pose, ring slot, fresh flags, masks)
+  int32_t parts;
+  int32_t slot2, slot3;
   const double* pose2;      // [3, n]
+  const double* pose3;
   const uint8_t* fresh2;
+  const uint8_t* fresh3;
   uint8_t* masks2;
+  uint8_t* masks3;
 };
 
 // ---- fused render kernel ----------------------------------------------------------
@@ -935,14 +939,16 @@ __device__ __forceinline__ void write_outputs(const RenderArgs& a, RenderLds& S,
   const LineDev& L = a.line;
   const Slots<kSpill> sl{S, a.spill + (size_t)e * kSpillHalves,
                          a.spill + (size_t)e * kSpillHalves + 4 * NW, a.list_cap};
-  const uint8_t* fr = half ? a.fresh2 : a.fresh;
+  const uint8_t* fr = half == 0 ? a.fresh : (half == 1 ? a.fresh2 : a.fresh3);
   const bool fresh = fr != nullptr && fr[e] != 0;
-  const int slot = half ? a.slot2 : a.slot;
-  // a pair's first decision never writes the second's slot (the second
-  // writes it for every env, so such a store is dead and would race), and
-  // writes no frame for an env the second decision refills
-  const int skip = a.pair && !half ? a.slot2 : -1;
-  const bool dead = a.pair && !half && a.fresh2 != nullptr && a.fresh2[e] != 0;
+  const int slot = half == 0 ? a.slot : (half == 1 ? a.slot2 : a.slot3);
+  // a decision of a group never writes a later decision's slot (the later
+  // one writes it for every env, so such a store is dead and would race),
+  // and writes no frame for an env a later decision refills
+  const int skip = half < a.parts - 1 ? (half == 0 ? a.slot2 : a.slot3) : -1;
+  const int skip2 = half == 0 && a.parts == 3 ? a.slot3 : -1;
+  const bool dead = (half < 1 && a.parts >= 2 && a.fresh2 != nullptr && a.fresh2[e] != 0) ||
+                    (half < 2 && a.parts == 3 && a.fresh3 != nullptr && a.fresh3[e] != 0);
   float* gbase = !kIdx && a.gray && !dead ? a.gray + (size_t)e * a.slots * NPIX : nullptr;
   uint8_t* ibase = kIdx && !dead ? a.index + (size_t)e * a.slots * NPIX : nullptr;
   const uint32_t blo = S.bits_lo, bhi = S.bits_hi;
@@ -960,7 +966,7 @@ __device__ __forceinline__ void write_outputs(const RenderArgs& a, RenderLds& S,
             if (fresh) {
 #pragma clang loop vectorize(disable) interleave(disable)
               for (int k = 0; k < a.slots; ++k)
-                if (k != skip) *reinterpret_cast<uint32_t*>(ibase + k * NPIX + 4 * w) = v;
+                if (k != skip && k != skip2) *reinterpret_cast<uint32_t*>(ibase + k * NPIX + 4 * w) = v;
             } else {
               *reinterpret_cast<uint32_t*>(ibase + slot * NPIX + 4 * w) = v;
             }
@@ -974,7 +980,7 @@ __device__ __forceinline__ void write_outputs(const RenderArgs& a, RenderLds& S,
             if (fresh) {
 #pragma clang loop vectorize(disable) interleave(disable)
               for (int k = 0; k < a.slots; ++k)
-                if (k != skip) *reinterpret_cast<float4*>(gbase + k * NPIX + 4 * w) = g;
+                if (k != skip && k != skip2) *reinterpret_cast<float4*>(gbase + k * NPIX + 4 * w) = g;
             } else {
               *reinterpret_cast<float4*>(gbase + slot * NPIX + 4 * w) = g;
             }
@@ -1119,7 +1125,7 @@ __device__ __forceinline__ void sched_build(const RenderArgs& a, RenderLds& S, u
 
 // the builder's ticket
 __device__ __forceinline__ uint32_t sched_builder(const RenderArgs& a) {
-  return (uint32_t)((a.pair ? 2 : 1) * a.n - kSchedTail);   // dt_render: n > kSchedTail
+  return (uint32_t)(a.parts * a.n - kSchedTail);   // dt_render: n > kSchedTail
 }
 
 // exit of a workgroup: its cost (thread 0, no wait); the builder sorts
@@ -1303,7 +1309,7 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, in
   // byte).  Non-uniform words get a slot (the list); a quad with one takes
   // the dilation path of the output phase (every quad does when the dilation
   // radius is >= 2: uniformity only covers +-1 pixel).
-  uint8_t* const mb0 = half ? a.masks2 : a.masks;
+  uint8_t* const mb0 = half == 0 ? a.masks : (half == 1 ? a.masks2 : a.masks3);
   uint8_t* mbase = mb0 ? mb0 + (size_t)e * 4 * NPIX : nullptr;
   constexpr int kQuadPer = (NQ + T - 1) / T;  // quads per lane (3 at 512 threads)
   if (mbase) {
@@ -1431,8 +1437,8 @@ render_kernel(RenderArgs a) {
   // the camera frame, once per workgroup (wave 1; wave 0 has the palette), of
   // the env the dispatch order gives this block
   // dt_render2: blocks 2b and 2b + 1 render env perm[b] of the two decisions
-  const int half = a.pair ? (int)(blockIdx.x & 1u) : 0;
-  const int blk = a.pair ? (int)(blockIdx.x >> 1) : (int)blockIdx.x;
+  const int blk = (int)blockIdx.x / a.parts;
+  const int half = (int)blockIdx.x - blk * a.parts;
   int e = blk;
 #ifdef DTSIM_EARLY_MARKS
   float4 mq[4];
@@ -1455,7 +1461,8 @@ render_kernel(RenderArgs a) {
     S.t0 = __builtin_amdgcn_s_memtime();
     if (half) {
       const size_t n = (size_t)a.n;
-      S.view = view_of(a.pose2[e], a.pose2[n + e], a.pose2[2 * n + e], a.cam_fwd);
+      const double* ps = half == 1 ? a.pose2 : a.pose3;
+      S.view = view_of(ps[e], ps[n + e], ps[2 * n + e], a.cam_fwd);
     } else {
       S.view = view_of(a.x[e], a.z[e], a.angle[e], a.cam_fwd);
     }
@@ -1880,33 +1887,46 @@ int dt_set_line_params(dt_handle* h, const dt_line_params* p) {
 }
 
 static int render_launch(dt_handle* h, const dt_render_io* io, const dt_render_io* io2,
-                         void* stream);
+                         const dt_render_io* io3, void* stream);
 
 int dt_render(dt_handle* h, const dt_render_io* io, void* stream) {
-  return render_launch(h, io, nullptr, stream);
+  return render_launch(h, io, nullptr, nullptr, stream);
+}
+
+// a later decision of a group against the first: the same ring, its own slot
+// and masks, a pose snapshot, no rgb
+static bool group_ok(const dt_render_io* a, const dt_render_io* b) {
+  return a->pose && b->pose && !a->rgb && !b->rgb && a->gray == b->gray && a->index == b->index &&
+         a->gray_slots == b->gray_slots && a->list_cap == b->list_cap &&
+         (a->masks == nullptr) == (b->masks == nullptr) && (!a->masks || a->masks != b->masks) &&
+         (!(a->gray || a->index) || a->gray_slot != b->gray_slot) && b->gray_slot >= 0 &&
+         b->gray_slot < (b->gray_slots < 1 ? 1 : b->gray_slots);
 }
 
 int dt_render2(dt_handle* h, const dt_render_io* io_a, const dt_render_io* io_b, void* stream) {
   if (!h || !io_a || !io_b) return DT_E_ARG;
-  if (!io_a->pose || !io_b->pose || io_a->rgb || io_b->rgb || io_a->gray != io_b->gray ||
-      io_a->index != io_b->index || io_a->gray_slots != io_b->gray_slots ||
-      io_a->list_cap != io_b->list_cap || (io_a->masks == nullptr) != (io_b->masks == nullptr) ||
-      (io_a->masks && io_a->masks == io_b->masks) ||
-      ((io_a->gray || io_a->index) && io_a->gray_slot == io_b->gray_slot)) {
-    h->err = "dt_render2: two decisions of one ring: both poses given, the same ring, "
+  if (!group_ok(io_a, io_b)) {
+    h->err = "dt_render2: two decisions of one ring: poses given, the same ring, "
              "different slots, separate masks, no rgb";
     return DT_E_ARG;
   }
-  return render_launch(h, io_a, io_b, stream);
+  return render_launch(h, io_a, io_b, nullptr, stream);
+}
+
+int dt_render3(dt_handle* h, const dt_render_io* io_a, const dt_render_io* io_b,
+               const dt_render_io* io_c, void* stream) {
+  if (!h || !io_a || !io_b || !io_c) return DT_E_ARG;
+  if (!group_ok(io_a, io_b) || !group_ok(io_a, io_c) || !group_ok(io_b, io_c)) {
+    h->err = "dt_render3: three decisions of one ring: poses given, the same ring, "
+             "different slots, separate masks, no rgb";
+    return DT_E_ARG;
+  }
+  return render_launch(h, io_a, io_b, io_c, stream);
 }
 
 static int render_launch(dt_handle* h, const dt_render_io* io, const dt_render_io* io2,
-                         void* stream) {
+                         const dt_render_io* io3, void* stream) {
   if (!h || !io) return DT_E_ARG;
-  if (io2 && (io2->gray_slots < 1 || io2->gray_slot < 0 || io2->gray_slot >= io2->gray_slots)) {
-    h->err = "dt_render2: gray_slot out of range";
-    return DT_E_ARG;
-  }
   if (io->gray && io->index) {
     h->err = "dt_render: gray and index are two formats of one frame ring: give one";
     return DT_E_ARG;
@@ -1950,14 +1970,22 @@ static int render_launch(dt_handle* h, const dt_render_io* io, const dt_render_i
   a.launch = h->render_launches++;
 #endif
   a.list_cap = io->list_cap > 0 && io->list_cap < kListCap ? io->list_cap : kListCap;
+  a.parts = 1;
   if (io2) {
-    a.pair = 1;
+    a.parts = 2;
     a.slot2 = io2->gray_slot;
     a.pose2 = io2->pose;
     a.fresh2 = io2->fresh;
     a.masks2 = io2->masks;
   }
-  const int grid = (io2 ? 2 : 1) * h->n;
+  if (io3) {
+    a.parts = 3;
+    a.slot3 = io3->gray_slot;
+    a.pose3 = io3->pose;
+    a.fresh3 = io3->fresh;
+    a.masks3 = io3->masks;
+  }
+  const int grid = a.parts * h->n;
   const bool big_r = a.line.dil_r >= 2;
   auto* kern = a.index ? (big_r ? render_kernel<true, true> : render_kernel<true, false>)
                        : (big_r ? render_kernel<false, true> : render_kernel<false, false>);

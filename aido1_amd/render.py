@@ -195,40 +195,58 @@ def bind_render(env, out, stream, fresh=None, pose=None):
     return launch
 
 
-def _render2_ios(env, out, masks_b, fresh_a, pose_a, fresh_b, pose_b):
-    if out.masks is None or masks_b is None or masks_b.shape != out.masks.shape or \
-            masks_b.data_ptr() == out.masks.data_ptr() or out.rgb is not None:
-        raise ValueError('render2: a second masks buffer of out.masks\' shape, no rgb')
-    if pose_a is None or pose_b is None:
-        raise ValueError('render2: both decisions\' pose snapshots')
-    io_a = _render_io(env, out, fresh_a, pose_a, 0)
-    io_b = _render_io(env, out, fresh_b, pose_b, 0)
-    io_b.masks = ctypes.c_void_p(masks_b.data_ptr())
-    return io_a, io_b
+def _group_ios(env, out, masks, fresh, pose):
+    """The dt_render_io of 2 or 3 consecutive decisions of one ring: decision
+    0 writes out.masks, decision i > 0 masks[i - 1]."""
+    k = len(pose)
+    if k not in (2, 3) or len(fresh) != k or len(masks) != k - 1:
+        raise ValueError('a render group is 2 or 3 decisions (k - 1 extra masks buffers)')
+    if out.masks is None or out.rgb is not None or any(
+            m is None or m.shape != out.masks.shape or m.data_ptr() == out.masks.data_ptr()
+            for m in masks) or len({m.data_ptr() for m in masks}) != len(masks):
+        raise ValueError('render group: separate masks buffers of out.masks\' shape, no rgb')
+    if any(p is None for p in pose):
+        raise ValueError('render group: every decision\'s pose snapshot')
+    ios = [_render_io(env, out, f, p, 0) for f, p in zip(fresh, pose)]
+    for io, m in zip(ios[1:], masks):
+        io.masks = ctypes.c_void_p(m.data_ptr())
+    return ios
 
 
-def render2_into(env, out, masks_b, fresh_a, pose_a, fresh_b, pose_b):
-    """Two consecutive decisions' renders in ONE launch (dt_render2): the
-    earlier (pose_a, fresh_a) into out.masks and the ring slot after the
-    newest, the later (pose_b, fresh_b) into masks_b and the slot after that.
-    Every output equals render_into(a) then render_into(b)."""
-    io_a, io_b = _render2_ios(env, out, masks_b, fresh_a, pose_a, fresh_b, pose_b)
-    rc = env._L.dt_render2(env._h, ctypes.byref(io_a), ctypes.byref(io_b), env._stream())
-    env._check(rc, 'dt_render2')
+def render_group_into(env, out, masks, fresh, pose):
+    """2 or 3 consecutive decisions' renders in ONE launch (dt_render2 /
+    dt_render3): decision i of the lists (fresh[i], pose[i]) into ring slot
+    after the newest + i, its masks into out.masks (i = 0) or masks[i - 1].
+    Every output equals render_into of each decision in order."""
+    ios = _group_ios(env, out, masks, fresh, pose)
+    fn = env._L.dt_render2 if len(ios) == 2 else env._L.dt_render3
+    rc = fn(env._h, *[ctypes.byref(io) for io in ios], env._stream())
+    env._check(rc, 'dt_render%d' % len(ios))
     return out
 
 
-def bind_render2(env, out, stream, masks_b, fresh_a, pose_a, fresh_b, pose_b):
-    """bind_render for render2_into (two decisions, one launch)."""
-    io_a, io_b = _render2_ios(env, out, masks_b, fresh_a, pose_a, fresh_b, pose_b)
-    fn, h, st = env._L.dt_render2, env._h, ctypes.c_void_p(stream.cuda_stream)
-    ra, rb = ctypes.byref(io_a), ctypes.byref(io_b)
-    keep = (out, masks_b, fresh_a, pose_a, fresh_b, pose_b, io_a, io_b, stream)
+def render2_into(env, out, masks_b, fresh_a, pose_a, fresh_b, pose_b):
+    """render_group_into of two decisions."""
+    return render_group_into(env, out, [masks_b], [fresh_a, fresh_b], [pose_a, pose_b])
+
+
+def bind_render_group(env, out, stream, masks, fresh, pose):
+    """bind_render for render_group_into (2 or 3 decisions, one launch)."""
+    ios = _group_ios(env, out, masks, fresh, pose)
+    fn = env._L.dt_render2 if len(ios) == 2 else env._L.dt_render3
+    refs = [ctypes.byref(io) for io in ios]
+    h, st = env._h, ctypes.c_void_p(stream.cuda_stream)
+    keep = (out, masks, fresh, pose, ios, stream)
 
     def launch():
         keep  # noqa: B018
-        return fn(h, ra, rb, st)
+        return fn(h, *refs, st)
     return launch
+
+
+def bind_render2(env, out, stream, masks_b, fresh_a, pose_a, fresh_b, pose_b):
+    """bind_render_group of two decisions."""
+    return bind_render_group(env, out, stream, [masks_b], [fresh_a, fresh_b], [pose_a, pose_b])
 
 
 def line_detect(bgr, params=None, hsv=False, stream=None):

@@ -105,9 +105,10 @@ def parse(argv=None):
     p.add_argument('--overlap', action='store_true',
                    help='train: run each update beside the next rollout (side stream); a '
                         'different schedule (acting one update behind), DESIGN 3.8')
-    p.add_argument('--no-pair', action='store_true',
-                   help='config 3 many modes: one decision a render launch (dt_render) '
-                        'instead of two (dt_render2)')
+    p.add_argument('--render-group', type=int, default=3,
+                   help='config 3 many modes: consecutive decisions a render launch '
+                        '(1 dt_render, 2 dt_render2, 3 dt_render3: the ring\'s slots)')
+    p.add_argument('--no-pair', action='store_true', help='= --render-group 1')
     p.add_argument('--many', type=int, default=20,
                    help='most decisions per dt_step_many launch (lane config, and the render '
                         'config\'s many mode); K decisions are split into ceil(K / many) '
@@ -597,12 +598,14 @@ class ObsLoop:
                the snapshot on another: step d + 1 beside render d.
     Every mode computes the same frames, masks and step outputs."""
 
-    def __init__(self, env, ro, torch, mode='many', chunk=20, event_stride=1, pair=True):
+    def __init__(self, env, ro, torch, mode='many', chunk=20, event_stride=1, group=3):
         self.env, self.ro, self.torch, self.mode = env, ro, torch, mode
-        # 'many' / 'many2': two consecutive decisions' renders a launch
-        # (dt_render2, one drain for both), their masks in two buffers
-        self.pair = bool(pair) and mode in ('many', 'many2') and ro.masks is not None
-        self.masks_b = torch.zeros_like(ro.masks) if self.pair else None
+        # 'many' / 'many2': up to `group` (<= 3, the ring's slots) consecutive
+        # decisions' renders a launch (dt_render2 / dt_render3, one drain for
+        # the group), each decision's masks in its own buffer
+        self.group = max(1, min(3, int(group))) if mode in ('many', 'many2') and \
+            ro.masks is not None else 1
+        self.extra = [torch.zeros_like(ro.masks) for _ in range(self.group - 1)]
         self.last_masks = ro.masks
         self.launches = []    # per render launch: the decisions it renders
         # pipe mode orders the step stream on the render end events: all recorded
@@ -626,7 +629,7 @@ class ObsLoop:
         """The foreign calls of len(actions) decisions writing `out` (a
         StepOutput of k * n entries), built and checked before the timed region
         (the ring slots are taken here, in decision order)."""
-        from aido1_amd.render import bind_render, bind_render2
+        from aido1_amd.render import bind_render, bind_render_group
         env, n, k = self.env, self.env.n, int(actions.shape[0])
         groups = []
         self.launches = []
@@ -640,20 +643,19 @@ class ObsLoop:
                 rend = []
                 d = a
                 while d < b:
-                    fr = out.done[d * n:(d + 1) * n]
-                    if self.pair and d + 1 < b:
-                        rend.append(bind_render2(env, self.ro, self.s_rend, self.masks_b, fr,
-                                                 pose[d - a], out.done[(d + 1) * n:(d + 2) * n],
-                                                 pose[d + 1 - a]))
-                        self.launches.append((d, d + 1))
-                        self.last_masks = self.masks_b
-                        d += 2
+                    gk = min(self.group, b - d)
+                    fr = [out.done[e * n:(e + 1) * n] for e in range(d, d + gk)]
+                    if gk > 1:
+                        rend.append(bind_render_group(env, self.ro, self.s_rend,
+                                                      self.extra[:gk - 1], fr,
+                                                      [pose[e - a] for e in range(d, d + gk)]))
+                        self.last_masks = self.extra[gk - 2]
                     else:
-                        rend.append(bind_render(env, self.ro, self.s_rend, fresh=fr,
+                        rend.append(bind_render(env, self.ro, self.s_rend, fresh=fr[0],
                                                 pose=pose[d - a]))
-                        self.launches.append((d,))
                         self.last_masks = self.ro.masks
-                        d += 1
+                    self.launches.append(tuple(range(d, d + gk)))
+                    d += gk
                 groups.append((a, step, None, rend))
             return groups
         serial = self.mode == 'serial'
@@ -715,7 +717,7 @@ def bench_obs(args, ctx):
     actions = torch.rand(W + K, n, 2, generator=g, device=dev, dtype=torch.float32)
     ro = RenderOutput(n, dev)          # 3-slot grey ring (Transformer stack) + 4 masks
     loop = ObsLoop(env, ro, torch, args.obs_mode, args.many, args.event_stride,
-                   pair=not args.no_pair)
+                   group=1 if args.no_pair else args.render_group)
     env.reset()
     wout = StepOutput(max(W, 1) * n, dev, lanepos=False, tile=False)
     if W and loop.run(loop.bind(actions[:W], wout), loop.events(W)):
@@ -758,7 +760,8 @@ def bench_obs(args, ctx):
     # every --event-stride-th launch only: an event pair per launch adds ~6 us
     # a decision of stream packets to the wall time)
     KE = max(K, args.roofline_launches)
-    ev_loop = ObsLoop(env, ro, torch, args.obs_mode, args.many, 1, pair=not args.no_pair)
+    ev_loop = ObsLoop(env, ro, torch, args.obs_mode, args.many, 1,
+                      group=1 if args.no_pair else args.render_group)
     ev_act = torch.rand(KE, n, 2, generator=g, device=dev, dtype=torch.float32)
     ev_out = StepOutput(KE * n, dev, lanepos=False, tile=False)
     env.stats(reset=True)
@@ -778,9 +781,15 @@ def bench_obs(args, ctx):
     frame_b = RENDER_BYTES_PER_FRESH // 2
     pass_bytes = KE * RENDER_BYTES_PER_ENV * n + RENDER_BYTES_PER_FRESH * int(dn.sum())
     for la in ev_loop.launches:
-        if len(la) == 2:
-            fa, fb = dn[la[0]], dn[la[1]]
-            pass_bytes -= frame_b * int((fb * (1 + fa) + (1 - fb) * fa).sum())
+        # decision i of a group against its sequential frame stores (3 slots
+        # on a refill, else 1): none if a later decision refills the env,
+        # else all but the later decisions' slots on a refill, else its slot
+        g = len(la)
+        for i in range(g - 1):
+            fi = dn[la[i]]
+            later = dn[list(la[i + 1:])].amax(0)
+            written = (1 - later) * (fi * (3 - (g - 1 - i)) + (1 - fi))
+            pass_bytes -= frame_b * int(((1 + 2 * fi) - written).sum())
     env.close()
     lane = None if args.no_lane else lane_record(args, ctx, args.lane_steps, args.lane_warmup,
                                                  cpu=True)
@@ -817,9 +826,10 @@ def bench_obs(args, ctx):
                                    'decision\'s end pose written), then the chunk\'s renders, '
                                    'each of its decision\'s pose with its done flags as fresh, '
                                    '%s; one stream, prebound calls'
-                                   % (args.many, 'two consecutive decisions a launch '
-                                      '(dt_render2, each decision its own masks buffer)'
-                                      if loop.pair else 'one decision a launch (dt_render)'),
+                                   % (args.many, '%d consecutive decisions a launch '
+                                      '(dt_render%d, each decision its own masks buffer)'
+                                      % (loop.group, loop.group) if loop.group > 1
+                                      else 'one decision a launch (dt_render)'),
                            'many2': 'dt_step_many over chunks of <= %d decisions on a step '
                                     'stream (each decision\'s end pose written, two pose '
                                     'buffers), each decision\'s dt_render of that pose on a '
@@ -849,10 +859,10 @@ def bench_obs(args, ctx):
                                               'written + pose 24 read (SURVEY §8d config 3 '
                                               'without the step\'s 81 B); plus 153,600 B of '
                                               'ring refill per respawned env (%.1f per '
-                                              'decision), per decision; a dt_render2 launch '
-                                              'holds two decisions, less the stores it does not '
-                                              'make (the earlier decision\'s frame where the '
-                                              'later one writes or refills), counted from the '
+                                              'decision), per decision; a dt_render2/3 launch '
+                                              'holds two or three decisions, less the stores it '
+                                              'does not make (an earlier decision\'s frame where '
+                                              'a later one writes or refills), counted from the '
                                               'done flags' % fresh_per_launch,
                          'timing': 'HIP events on the render stream around every dt_render of '
                                    'a %d-decision pass right after the timed region (same '

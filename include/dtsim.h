@@ -301,6 +301,11 @@ int dt_render(dt_handle* h, const dt_render_io* io, void* stream);
  * refills gets no io_a frame), so the two halves never write one byte. */
 int dt_render2(dt_handle* h, const dt_render_io* io_a, const dt_render_io* io_b, void* stream);
 
+/* dt_render2 for three consecutive decisions (three slots of the ring):
+ * equals dt_render(io_a), dt_render(io_b), dt_render(io_c) in that order. */
+int dt_render3(dt_handle* h, const dt_render_io* io_a, const dt_render_io* io_b,
+               const dt_render_io* io_c, void* stream);
+
 /* Diagnostics of that dispatch order (synchronises): launches so far, each
  * env's last recorded cost (shader cycles) and the order the next launch
  * dispatches in (a permutation of 0..n-1).  cost / order: host [n] or NULL. */

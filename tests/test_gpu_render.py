@@ -268,3 +268,37 @@ def test_render2_matches_two_renders(gpu, frames, n):
         assert torch.equal(pair.masks, masks_a_ref), it
         assert torch.equal(masks_b, ref.masks), it
         assert torch.equal(pair.ring, ref.ring), it
+
+
+@pytest.mark.parametrize('frames', ['gray', 'index'])
+def test_render3_matches_three_renders(gpu, frames):
+    """dt_render3 (three consecutive decisions, the ring's three slots, in one
+    launch) equals dt_render of each in order: the ring and all three
+    decisions' masks, fresh flags anywhere, over several groups."""
+    from aido1_amd.render import RenderOutput, render_group_into
+    from aido1_amd.vec_env import VecEnv
+    n = 1024
+    env = VecEnv(n, seed=23)
+    env.reset()
+    ref = RenderOutput(n, gpu, frames=frames)
+    grp = RenderOutput(n, gpu, frames=frames)
+    extra = [torch.zeros_like(grp.masks) for _ in range(2)]
+    g = torch.Generator(device=gpu)
+    g.manual_seed(7)
+    for it in range(4):
+        poses, fresh, want = [], [], []
+        for _ in range(3):
+            env.step_into(torch.rand(n, 2, generator=g, device=gpu))
+            p = torch.empty(3, n, dtype=torch.float64, device=gpu)
+            env.copy_pose(p)
+            poses.append(p)
+            fresh.append((torch.rand(n, generator=g, device=gpu) < 0.3).to(torch.uint8))
+        for f, p in zip(fresh, poses):
+            env.render_into(ref, fresh=f, pose=p)
+            want.append(ref.masks.clone())
+        render_group_into(env, grp, extra, fresh, poses)
+        torch.cuda.synchronize()
+        assert grp.slot == ref.slot
+        for got, w in zip([grp.masks] + extra, want):
+            assert torch.equal(got, w), it
+        assert torch.equal(grp.ring, ref.ring), it
