@@ -18,11 +18,11 @@ REPO_DIR = os.path.dirname(PKG_DIR)
 LIB_PATH = os.path.join(PKG_DIR, 'libdtsim.so')
 CSRC = os.path.join(PKG_DIR, 'csrc')
 SOURCES = ['dtsim.hip', 'dtrender.hip', 'dtreplay.hip', 'dtactor.hip', 'dtconv.hip',
-           'dttrain.hip', 'dtupd.hip', 'dthead.hip']
-HEADERS = ['dtsim_common.h', 'dtrender.h', 'dtsync.h']
+           'dtconvx.hip', 'dttrain.hip', 'dtupd.hip', 'dthead.hip']
+HEADERS = ['dtsim_common.h', 'dtrender.h', 'dtsync.h', 'dtconv_common.h']
 PUBLIC_HEADERS = ['dtsim.h', 'dtreplay.h', 'dtactor.h', 'dttrain.h', 'dtupd.h', 'dthead.h']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
-ABI_VERSION = 10
+ABI_VERSION = 11
 
 HIP_FLAGS = ['--offload-arch=gfx950', '-O3', '-fPIC', '-shared', '-std=c++17',
              '-ffp-contract=off', '-munsafe-fp-atomics']
@@ -290,6 +290,12 @@ def lib():
             'dt_conv32_split': (ctypes.c_int, [i32, i32, vp, vp, vp, vp, vp, vp, ctypes.c_float,
                                                vp, vp, vp, vp, ctypes.c_float, ctypes.c_float,
                                                ctypes.POINTER(DtConvSet), vp]),
+            'dt_conv1x_split': (ctypes.c_int, [vp, i32, i32, i32, ctypes.POINTER(i32), vp, vp,
+                                               ctypes.POINTER(DtConvSet), vp, vp,
+                                               ctypes.c_float, vp]),
+            'dt_conv32x_split': (ctypes.c_int, [i32, i32, vp, vp, vp, vp, vp, vp, ctypes.c_float,
+                                                vp, vp, vp, vp, ctypes.c_float, ctypes.c_float,
+                                                ctypes.POINTER(DtConvSet), vp]),
             'dt_explore': (ctypes.c_int, [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                           ctypes.POINTER(DtExploreParams), vp, vp]),
             'dt_explore_done': (ctypes.c_int, [i32, vp, vp, vp, vp, i32, vp]),

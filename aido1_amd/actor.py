@@ -372,6 +372,13 @@ class FusedActor(nn.Module):
         self.register_buffer('w0frag', torch.zeros(16, 64, 8, dtype=torch.float16, device=dev))
         self.register_buffer('wfrag', torch.zeros(3, 32, 64, 8, dtype=torch.float16, device=dev))
         self.register_buffer('bf', torch.zeros(4, 32, device=dev))
+        # the float32-accurate chain (dt_conv1x_split / dt_conv32x_split,
+        # reference mode in float32): conv1's fragments as (hi, lo) fp16
+        # halves, conv2..4's in float32
+        self.x3 = dtype == torch.float32 and mode == 'reference'
+        if self.x3:
+            self.register_buffer('w0x', torch.zeros(2, 16, 64, 8, dtype=torch.float16, device=dev))
+            self.register_buffer('wx32', torch.zeros(3, 32, 64, 8, device=dev))
         self.refresh(actor, graph=False)
 
     @torch.no_grad()
@@ -539,6 +546,10 @@ class FusedActor(nn.Module):
         for i in range(1, 4):
             self.wfrag[i - 1].view(-1).copy_(torch.take(ws[i], self._fidx[1]))
         torch._foreach_copy_(list(self.bf.unbind(0)), list(bs))
+        if self.x3:
+            self.w0x.view(2, -1).copy_(split_hl(torch.take(self._w0pad, self._fidx[0])))
+            for i in range(1, 4):
+                self.wx32[i - 1].view(-1).copy_(torch.take(ws[i], self._fidx[1]))
 
     def _lrelu_sample_norm(self, x, i):
         """LeakyReLU then BatchNorm2d in train mode on a batch of one, for every
@@ -628,9 +639,81 @@ class FusedActor(nn.Module):
                 self.eps[3] if ref else 0.0, 0.01, stream)
         return rc
 
+    def _x3_input(self, x):
+        """x is a frame ring the float32-accurate HIP chain takes."""
+        return (self.x3 and x.is_cuda and x.dtype in (torch.float32, torch.uint8) and
+                x.is_contiguous() and tuple(x.shape[2:]) == (120, 160) and x.shape[1] >= 3 and
+                self.w[0].shape == (32, 3, 8, 8))
+
+    def _x3_buffers(self, n, dev):
+        """The HL activations ((hi, lo) fp16 pairs, include/dtactor.h) of
+        conv1..conv3, their per-sample statistics [n, 32, 3] and the f32
+        flattened conv4 output."""
+        key = (n, dev)
+        if getattr(self, '_xbufs_key', None) != key:
+            f16 = torch.float16
+            self._xbufs = {
+                'y1': torch.empty(n, 57, 77, 64, dtype=f16, device=dev),
+                'y2': torch.empty(n, 27, 37, 64, dtype=f16, device=dev),
+                'y3': torch.empty(n, 12, 17, 64, dtype=f16, device=dev),
+                'p1': torch.empty(n, 32, 3, device=dev),
+                'p2': torch.empty(n, 32, 3, device=dev),
+                'p3': torch.empty(n, 32, 3, device=dev),
+                'flat': torch.empty(n, FLAT, device=dev)}
+            self._xbufs_key = key
+        return self._xbufs
+
+    def _convs_x3(self, ring, order, other=None, n0=None):
+        """The four convolutions at float32 accuracy (dt_conv1x_split, then
+        dt_conv32x_split x3; include/dtactor.h): every per-sample BatchNorm is
+        folded into the next layer's weights, the last one applied in conv4's
+        epilogue.  With `other`, samples [n0, n) use its weights in the same
+        launches.  Returns the flattened [N, 4032] float32 activation (NCHW
+        order); it is the buffers' own memory, valid until the next call."""
+        import ctypes
+        from aido1_amd import _lib
+        L = _lib.lib()
+        n, slots = ring.shape[0], ring.shape[1]
+        B = self._x3_buffers(n, ring.device)
+        stream = torch.cuda.current_stream(ring.device).cuda_stream
+        o = (ctypes.c_int32 * 3)(*[int(v) for v in order])
+        s1 = None if other is None else ctypes.byref(_lib.DtConvSet(
+            n0, other.w0x.data_ptr(), other.bf[0].data_ptr()))
+        rc = L.dt_conv1x_split(ring.data_ptr(), 1 if ring.dtype == torch.uint8 else 0, n, slots,
+                               o, self.w0x.data_ptr(), self.bf[0].data_ptr(), s1,
+                               B['y1'].data_ptr(), B['p1'].data_ptr(), 0.01, stream)
+        ins = [(B['y1'], B['p1']), (B['y2'], B['p2']), (B['y3'], B['p3'])]
+        outs = [(B['y2'], B['p2']), (B['y3'], B['p3']), (B['flat'], None)]
+        for layer in range(3):
+            if rc != 0:
+                break
+            x, pp = ins[layer]
+            y, po = outs[layer]
+            last = layer == 2
+            s2 = None
+            if other is not None:
+                s2 = ctypes.byref(_lib.DtConvSet(
+                    n0, other.wx32[layer].data_ptr(), other.bf[layer + 1].data_ptr(),
+                    other.gamma[layer].data_ptr(), other.beta[layer].data_ptr(),
+                    other.gamma[3].data_ptr() if last else None,
+                    other.beta[3].data_ptr() if last else None))
+            rc = L.dt_conv32x_split(
+                layer + 2, n, x.data_ptr(), self.wx32[layer].data_ptr(),
+                self.bf[layer + 1].data_ptr(), pp.data_ptr(), self.gamma[layer].data_ptr(),
+                self.beta[layer].data_ptr(), self.eps[layer], y.data_ptr(),
+                po.data_ptr() if po is not None else None,
+                self.gamma[3].data_ptr() if last else None,
+                self.beta[3].data_ptr() if last else None, self.eps[3], 0.01, s2, stream)
+        if rc != 0:
+            raise _lib.DtError('dt_conv1x_split / dt_conv32x_split failed (%d)' % rc)
+        return B['flat']
+
     def _pairable(self, other, x):
-        return (other is not None and other.mode == self.mode and x.is_cuda and
-                self.dtype == torch.float16 and other.dtype == torch.float16 and
+        if other is None or other.mode != self.mode or not x.is_cuda:
+            return False
+        if self.x3 and other.x3:
+            return self._x3_input(x) and other.w[0].shape == (32, 3, 8, 8)
+        return (self.dtype == torch.float16 and other.dtype == torch.float16 and
                 x.dtype in (torch.float32, torch.uint8) and x.is_contiguous() and
                 tuple(x.shape[2:]) == (120, 160) and x.shape[1] >= 3 and
                 self.w[0].shape == (32, 3, 8, 8) and other.w[0].shape == (32, 3, 8, 8))
@@ -649,6 +732,11 @@ class FusedActor(nn.Module):
         if not self._pairable(other, x) or not 0 < n0 < n:
             out[:n0] = self(x[:n0], order)
             out[n0:] = other(x[n0:], order)
+            return out
+        if self.x3:
+            flat = self._convs_x3(x, order, other, n0)
+            out[:n0] = self._head(flat[:n0])
+            out[n0:] = other._head(flat[n0:])
             return out
         flat = self._convs_pair(other, x, order, n0)
         if self._head_fusable(other):
@@ -754,6 +842,9 @@ class FusedActor(nn.Module):
 
     def _forward(self, x, order):
         ref = self.mode == 'reference'
+        if self._x3_input(x):
+            # the reference-precision product path: the float32-accurate HIP convs
+            return self._head(self._convs_x3(x, order if order is not None else [0, 1, 2]))
         if (x.is_cuda and self.dtype == torch.float16 and
                 x.dtype in (torch.float32, torch.uint8) and
                 x.is_contiguous() and tuple(x.shape[2:]) == (120, 160) and x.shape[1] >= 3 and
@@ -796,28 +887,36 @@ def copy_grouped(dsts, srcs):
         torch._foreach_copy_(ds, ss)
 
 
-def conv1_fragments(w):
+def split_hl(t):
+    """A float32 tensor as its (hi, lo) fp16 halves stacked in a new first
+    dim: hi = fp16(t), lo = fp16((t - hi) * 2^11) (the x3 operands of
+    include/dtactor.h's dt_conv1x_split)."""
+    hi = t.half()
+    return torch.stack([hi, ((t - hi.float()) * 2048.0).half()])
+
+
+def conv1_fragments(w, dtype=torch.float16):
     """conv1 weights [32, 3, 8, 8] -> dt_conv1's MFMA A fragments [16, 64, 8]
-    fp16: element [s][l][j] = w[l % 32][j % 4][s // 2][4 (s % 2) + 2 (l // 32)
-    + j // 4], zero for the padding channel j % 4 == 3."""
+    (fp16, or `dtype`): element [s][l][j] = w[l % 32][j % 4][s // 2][4 (s % 2)
+    + 2 (l // 32) + j // 4], zero for the padding channel j % 4 == 3."""
     dev = w.device
     s = torch.arange(16, device=dev).view(16, 1, 1)
     ln = torch.arange(64, device=dev).view(1, 64, 1)
     j = torch.arange(8, device=dev).view(1, 1, 8)
     wp = torch.cat([w.float(), torch.zeros(w.shape[0], 1, 8, 8, device=dev)], 1)
-    return wp[ln % 32, j % 4, s // 2, 4 * (s % 2) + 2 * (ln // 32) + j // 4].to(torch.float16)
+    return wp[ln % 32, j % 4, s // 2, 4 * (s % 2) + 2 * (ln // 32) + j // 4].to(dtype)
 
 
-def conv32_fragments(w):
+def conv32_fragments(w, dtype=torch.float16):
     """A 32 -> 32 4x4 conv's weights [32, 32, 4, 4] -> dt_conv32's MFMA A
-    fragments [32, 64, 8] fp16: element [s][l][j] = w[l % 32][16 (s % 2) +
-    8 (l // 32) + j][(s // 2) // 4][(s // 2) % 4]."""
+    fragments [32, 64, 8] (fp16, or `dtype`): element [s][l][j] = w[l % 32][16
+    (s % 2) + 8 (l // 32) + j][(s // 2) // 4][(s // 2) % 4]."""
     dev = w.device
     s = torch.arange(32, device=dev).view(32, 1, 1)
     ln = torch.arange(64, device=dev).view(1, 64, 1)
     j = torch.arange(8, device=dev).view(1, 1, 8)
     return w.float()[ln % 32, 16 * (s % 2) + 8 * (ln // 32) + j, (s // 2) // 4,
-                     (s // 2) % 4].to(torch.float16)
+                     (s // 2) % 4].to(dtype)
 
 
 def conv1_fragment_index(dev):

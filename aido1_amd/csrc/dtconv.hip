@@ -16,6 +16,7 @@
 #include <type_traits>
 
 #include "../../include/dtactor.h"
+#include "dtconv_common.h"
 #include "dtrender.h"   // dr::kPalGray: the grey levels of palette-index frames
 
 // diagnostic builds only (tools/conv32_micro.py): bit 0 skips the prefetch
@@ -68,14 +69,8 @@ __device__ unsigned long long g_c1stamps[8 * 2 * 48 * 8];
 
 namespace {
 
-constexpr int IH = 120, IW = 160, OH = 57, OW = 77, CO = 32;
-
-using half8 = __attribute__((ext_vector_type(8))) _Float16;
-using f32x16 = __attribute__((ext_vector_type(16))) float;
-using u32x4 = __attribute__((ext_vector_type(4))) uint32_t;
-
-// LeakyReLU for 0 <= s <= 1 as two instructions (a multiply and a max)
-__device__ __forceinline__ float lrelu2(float v, float s) { return fmaxf(v, v * s); }
+using namespace dtconv;
+using namespace dtconv::c1;
 
 // One pixel's 32 channels as fp16 NHWC from a 32x32x16 MFMA tile (lane = pixel
 // column, register r = channel (r&3) + 8*(r>>2) + 4h): v_permlane32_swap pairs
@@ -117,68 +112,6 @@ __device__ __forceinline__ void store_px32(__half* sample, int px, const float (
   }
 }
 
-// Reference mode keeps each sample's activations CENTRED in fp16: the stored
-// value is v - c with c the sample's pixel-0 output of the channel, and the
-// statistics are those of the stored values (M2 does not change, the mean
-// moves by c), so the next layer's norm (x - mean) * invstd is unchanged.  A
-// channel that is nearly flat over a frame is divided by a tiny standard
-// deviation; stored uncentred its fp16 rounding (~2^-11 |v|) is amplified by
-// that 1 / std, centred the rounding is of |v - c| ~ the channel's own spread.
-// The sample's first step publishes c (wave 0, pixel 0 = lanes 0 and 32) and
-// a barrier makes it visible; later steps read it (rewritten only after the
-// step barrier that ends the sample).  `first` is workgroup-uniform.
-__device__ __forceinline__ void centre_px32(float (&v)[16], float* s_c, bool publish, bool first,
-                                            int h) {
-  if (publish)
-#pragma unroll
-    for (int r = 0; r < 16; ++r) s_c[(r & 3) + 8 * (r >> 2) + 4 * h] = v[r];
-  if (first) __syncthreads();
-#pragma unroll
-  for (int r = 0; r < 16; ++r) v[r] -= s_c[(r & 3) + 8 * (r >> 2) + 4 * h];
-}
-
-// ---- two weight sets in one launch -----------------------------------------------
-// Samples [0, n0) use the launch's weights, [n0, n) a second set (the exploiting
-// explorers' actor): the persistent workgroups split in proportion, g0 for the
-// first set, the rest for the second, and each loads only its own set.  One set:
-// n0 = n, g0 = gridDim.x.
-struct WeightSplit {
-  int n0, g0;
-  const void* wfrag;
-  const float *bias, *in_gamma, *in_beta, *out_gamma, *out_beta;
-};
-struct SplitPart {
-  bool set2;
-  int bid, gdim, sbeg, send, my;   // this WG's index / count in its part, its samples
-};
-__device__ __forceinline__ SplitPart split_part(const WeightSplit& ws, int n) {
-  SplitPart p;
-  p.set2 = (int)blockIdx.x >= ws.g0;
-  p.bid = p.set2 ? (int)blockIdx.x - ws.g0 : (int)blockIdx.x;
-  p.gdim = p.set2 ? (int)gridDim.x - ws.g0 : ws.g0;
-  p.sbeg = p.set2 ? ws.n0 : 0;
-  p.send = p.set2 ? n : ws.n0;
-  const int nloc = p.send - p.sbeg;
-  p.my = nloc > p.bid ? (nloc - p.bid + p.gdim - 1) / p.gdim : 0;
-  return p;
-}
-// host: the grid of a launch over n samples (n0 of them with the first set) on
-// `grid` resident workgroups; fills ws.n0 / ws.g0
-inline int split_grid(WeightSplit& ws, int n, int n0, int grid) {
-  if (n0 <= 0 || n0 >= n) {   // one set
-    ws.n0 = n;
-    ws.g0 = n < grid ? n : grid;
-    return ws.g0;
-  }
-  int g0 = (int)(((long long)grid * n0 + n / 2) / n);
-  g0 = g0 < 1 ? 1 : (g0 > grid - 1 ? grid - 1 : g0);
-  const int g1raw = grid - g0;
-  ws.n0 = n0;
-  ws.g0 = n0 < g0 ? n0 : g0;
-  const int g1 = (n - n0) < g1raw ? (n - n0) : g1raw;
-  return ws.g0 + g1;
-}
-
 // ---- conv1 ----------------------------------------------------------------------
 // A persistent workgroup of kSW waves streams whole samples (n = blockIdx.x,
 // + gridDim.x, ...).  The input rows go through a ring of kSRing rows in LDS
@@ -190,50 +123,11 @@ inline int split_grid(WeightSplit& ws, int n, int n0, int grid) {
 // per CU, so one's barrier leaves the other's MFMAs running.  Reference mode:
 // per-lane Welford statistics over the sample, merged (Chan) into ONE
 // (mean, M2) per sample and channel.
-constexpr int kSW = 4;
-constexpr int kSThreads = 64 * kSW;
-constexpr int kSPix = OH * OW;                          // 4389
-constexpr int kSTiles = (kSPix + 31) / 32;              // 138
-constexpr int kSSteps = (kSTiles + kSW - 1) / kSW;      // 35
-constexpr int kSStepPix = 32 * kSW;
-constexpr int kSRing = 32;                              // rows (a power of two)
 constexpr bool kK192 = DTCONV1_K192 != 0;
 constexpr int kSPxB = kK192 ? 6 : 8;                    // bytes a ring pixel: fp16 x 3 (x 4)
 constexpr int kSRowB = IW * kSPxB;                      // 960 (1280) B
 constexpr int kSMfma = kK192 ? 12 : 16;                 // MFMAs a tile
 constexpr int kSGrp = kK192 ? 3 : 4;                    // MFMAs a B-fragment group
-constexpr int kSQuads = IW / 4;                         // 4-pixel load items per row
-__host__ __device__ constexpr int s_lo(int j) { return 2 * ((kSStepPix * j) / OW); }
-__host__ __device__ constexpr int s_hi(int j) {
-  const int end = kSStepPix * (j + 1) < kSPix ? kSStepPix * (j + 1) : kSPix;
-  const int r = 2 * ((end - 1) / OW) + 7;
-  return r < IH - 1 ? r : IH - 1;
-}
-__host__ __device__ constexpr int s_first_new(int j) {
-  return (j + 1 == kSSteps) ? 0 : (s_hi(j) + 1 > s_lo(j + 1) ? s_hi(j) + 1 : s_lo(j + 1));
-}
-__host__ __device__ constexpr int s_last_new(int j) {
-  return (j + 1 == kSSteps) ? s_hi(0) : s_hi(j + 1);
-}
-constexpr int s_span() {   // rows one step reads plus the rows its successor adds
-  int m = 0;
-  for (int j = 0; j < kSSteps; ++j) {
-    const int span = (j + 1 < kSSteps) ? s_hi(j + 1) - s_lo(j) + 1 : (IH - s_lo(j)) + s_hi(0) + 1;
-    m = span > m ? span : m;
-  }
-  return m;
-}
-constexpr int s_max_new() {
-  int m = s_hi(0) + 1;
-  for (int j = 0; j < kSSteps; ++j) {
-    const int r = s_last_new(j) - s_first_new(j) + 1;
-    m = r > m ? r : m;
-  }
-  return m;
-}
-static_assert(s_span() <= kSRing, "conv1 stream ring");
-constexpr int kSPre = (s_max_new() * kSQuads + kSThreads - 1) / kSThreads;
-
 #ifdef DTCONV_CHECK
 // Bounds-checked diagnostic build (tests/test_gpu_actor.py): every frame-ring
 // load of conv1s_kernel checks its float4 against the n x slots x 120 x 160
@@ -741,15 +635,18 @@ conv32_kernel(int n, const __half* __restrict__ x, const half8* __restrict__ wfr
   // contiguous range into registers, later into the ring as they are
   auto issue = [&](u32x4 (&pre)[kPre], int k, int r0, int r1) __attribute__((always_inline)) {
     // unconditional (clamped sample; chunks past the rows are buffer loads
-    // out of range, zeros the commit skips): see stats_load.  The chunk
-    // offset is the lane's 16 tid plus a constant: no address VALU a load
+    // out of range, zeros the commit skips): see stats_load.  The whole chunk
+    // offset is the VGPR offset: the raw-buffer range check covers the VGPR
+    // and instruction offsets, not the SGPR one, so a chunk past `cnt` reads
+    // zeros instead of the memory after the rows (the compiler folds the
+    // constant part into the instruction offset: no address VALU a load)
     const int cnt = (r1 - r0 + 1) * kRowU4;
     const int ns = sample(k) < send ? sample(k) : send - 1;
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<__half*>(x + ((size_t)ns * IH + r0) * IW * CO), 0, cnt * 16, 0x00020000);
 #pragma unroll
     for (int i = 0; i < kPre; ++i)
-      pre[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, 16 * tid, 16 * i * kThreads, 0);
+      pre[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, 16 * (tid + i * kThreads), 0, 0);
   };
   // kIn 1: the previous layer's BatchNorm is applied here, once per input
   // element (a thread's chunks all hold channels 8*(tid&3)..+7: kThreads and

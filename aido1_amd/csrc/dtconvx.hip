@@ -1,0 +1,714 @@
+// The actor's four convolutions at float32 accuracy on fp16 MFMA: the
+// reference-precision acting path (the reference acts in float32:
+// models/ddpg/model.py:79-88, duckietown_rl/ddpg.py:44-62) -- see
+// include/dtactor.h (dt_conv1x_split, dt_conv32x_split).
+//
+// "x3": every f32 operand x is carried as an fp16 pair (hi, lo),
+//   hi = fp16(x),  lo = fp16((x - hi) * 2^11),  x = hi + 2^-11 lo  (|error| <= 2^-24 |x|),
+// and a product as three fp16 MFMA products accumulated in f32,
+//   a * b ~ ah*bh + 2^-11 (ah*bl + al*bh)        (the dropped al*bl is ~2^-24 |a b|),
+// the ah*bh products in one accumulator and the cross products in a second, so
+// every operand is a normal fp16 number (an unscaled low part, ~2^-12 |w| for a
+// typical weight, would sit in fp16's subnormal range).  fp16 x fp16 products
+// are exact in f32, so the operands carry f32's rounding and the sums are f32
+// sums: the same accuracy class as the reference's float32 convolutions, at
+// 3/16 of the MFMA cycles an f32-input MFMA (v_mfma_f32_32x32x2_f32) needs.
+//
+// Activations between the layers are stored as such pairs ("HL" layout: a
+// pixel is 32 hi then 32 lo fp16 values, 128 B, the bytes of f32), centred on
+// the sample's pixel 0 as in the fp16 chain (dtconv_common.h centre_px32).
+//
+// conv1x_kernel: conv1s_kernel's row stream (dtconv.hip) with a hi ring and a
+//   lo ring in LDS, both weight halves in registers, three MFMAs a k step.
+// conv32x_kernel: conv2..conv4.  The previous layer's per-sample BatchNorm is
+//   folded into the weights once per sample (w' = w * sc[c], bias' = bias +
+//   sum_k w * sh[c]) and split into hi / lo fragments in LDS (64 KB); the B
+//   operand (the input's HL pairs) is read straight from global memory
+//   (L2-served im2col, no LDS ring: an f32-sized ring of conv2's 77-pixel rows
+//   would leave one workgroup a CU).  Four waves, one 32-pixel tile each a
+//   round; the next (round, kernel row) unit's 16 loads in flight while a
+//   unit's 24 MFMAs run.
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <type_traits>
+
+#include "../../include/dtactor.h"
+#include "dtconv_common.h"
+#include "dtrender.h"   // dr::kPalGray: the grey levels of palette-index frames
+
+namespace {
+
+using namespace dtconv;
+using namespace dtconv::c1;
+
+constexpr float kLo = 2048.0f, kLoInv = 1.0f / 2048.0f;
+
+// x as an (hi, lo) fp16 pair in one word: hi in the low half
+__device__ __forceinline__ uint32_t hl16(float x) {
+  const _Float16 h = (_Float16)x;
+  const _Float16 l = (_Float16)((x - (float)h) * kLo);
+  return (uint32_t)__builtin_bit_cast(uint16_t, h) |
+         ((uint32_t)__builtin_bit_cast(uint16_t, l) << 16);
+}
+// two (hi, lo) words -> their hi halves / their lo halves as fp16 pairs
+__device__ __forceinline__ uint32_t hi_pair(uint32_t a, uint32_t b) {
+  return (a & 0xffffu) | (b << 16);
+}
+__device__ __forceinline__ uint32_t lo_pair(uint32_t a, uint32_t b) {
+  return (a >> 16) | (b & 0xffff0000u);
+}
+
+// One pixel's 32 channels in the HL layout from a 32x32 MFMA tile (lane =
+// pixel column, register r = channel (r&3) + 8*(r>>2) + 4h): as store_px32
+// (dtconv.hip), v_permlane32_swap pairs the two half-waves' 4-channel groups
+// so a lane stores 16-B chunks, two of hi (byte 32m + 16h) and two of lo
+// (64 + 32m + 16h).  Branch-free: an invalid lane's offset lies past the
+// sample and the buffer store is dropped.
+template <int kPix>
+__device__ __forceinline__ void store_hl32(unsigned char* sample, int px, const float (&v)[16],
+                                           int h, bool valid) {
+  constexpr int kBytes = kPix * 128;
+  uint32_t uh[4][2], ul[4][2];
+#pragma unroll
+  for (int q = 0; q < 4; ++q)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const uint32_t a = hl16(v[4 * q + 2 * e]), b = hl16(v[4 * q + 2 * e + 1]);
+      uh[q][e] = hi_pair(a, b);
+      ul[q][e] = lo_pair(a, b);
+    }
+#pragma unroll
+  for (int m = 0; m < 2; ++m)
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      auto r = __builtin_amdgcn_permlane32_swap(uh[2 * m][e], uh[2 * m + 1][e], false, false);
+      uh[2 * m][e] = r[0];
+      uh[2 * m + 1][e] = r[1];
+      r = __builtin_amdgcn_permlane32_swap(ul[2 * m][e], ul[2 * m + 1][e], false, false);
+      ul[2 * m][e] = r[0];
+      ul[2 * m + 1][e] = r[1];
+    }
+  const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(sample, 0, kBytes, 0x00020000);
+  const int off = valid ? px * 128 + 16 * h : kBytes;
+#pragma unroll
+  for (int m = 0; m < 2; ++m) {
+    const u32x4 dh = {uh[2 * m][0], uh[2 * m][1], uh[2 * m + 1][0], uh[2 * m + 1][1]};
+    const u32x4 dl = {ul[2 * m][0], ul[2 * m][1], ul[2 * m + 1][0], ul[2 * m + 1][1]};
+    __builtin_amdgcn_raw_buffer_store_b128(dh, rsrc, off + 32 * m, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(dl, rsrc, off + 64 + 32 * m, 0, 0);
+  }
+}
+
+// Per-lane Welford statistics of a 32x32 tile's 16 channels merged over the
+// sample: the lanes of each half (shuffles), then the waves (red, one
+// barrier), written as (mean, M2, c) per channel by threads < CO.
+template <int NW>
+__device__ __forceinline__ void stats_flush(float& w_cnt, float (&w_mean)[16], float (&w_m2)[16],
+                                            float (*red)[CO][3], const float* s_c, float* out,
+                                            int tid, int wave, int col, int h) {
+#pragma unroll
+  for (int o = 1; o < 32; o <<= 1) {
+    const float nb = __shfl_xor(w_cnt, o, 32);
+    const float tot = w_cnt + nb;
+    const float fa = tot > 0.0f ? nb / tot : 0.0f, fb = tot > 0.0f ? w_cnt * nb / tot : 0.0f;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const float mb = __shfl_xor(w_mean[r], o, 32), m2b = __shfl_xor(w_m2[r], o, 32);
+      const float d = mb - w_mean[r];
+      w_mean[r] += d * fa;
+      w_m2[r] += m2b + d * d * fb;
+    }
+    w_cnt = tot;
+  }
+  if (col == 0)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int c = (r & 3) + 8 * (r >> 2) + 4 * h;
+      red[wave][c][0] = w_cnt;
+      red[wave][c][1] = w_mean[r];
+      red[wave][c][2] = w_m2[r];
+    }
+  __syncthreads();
+  if (tid < CO) {
+    float cnt = 0.0f, mean = 0.0f, m2 = 0.0f;
+    for (int w = 0; w < NW; ++w) {
+      const float nb = red[w][tid][0];
+      if (nb <= 0.0f) continue;
+      const float tot = cnt + nb, d = red[w][tid][1] - mean;
+      mean += d * (nb / tot);
+      m2 += red[w][tid][2] + d * d * (cnt * nb / tot);
+      cnt = tot;
+    }
+    float* pp = out + tid * 3;
+    pp[0] = mean;
+    pp[1] = m2;
+    pp[2] = s_c[tid];
+  }
+  w_cnt = 0.0f;
+#pragma unroll
+  for (int r = 0; r < 16; ++r) w_mean[r] = w_m2[r] = 0.0f;
+}
+
+// ---- conv1 -------------------------------------------------------------------------
+constexpr int kXPxB = 6;                  // bytes a ring pixel: 3 fp16 channels (hi or lo)
+constexpr int kXRowB = IW * kXPxB;        // 960 B a ring row
+constexpr int kXMfma = 12, kXGrp = 3;     // k steps a tile (K 192), a B-fragment group
+
+// kIdx: palette-index frames (u8), decoded through an 8-entry (hi, lo) table
+template <bool kIdx>
+__global__ void __launch_bounds__(kSThreads, 2)   // 2 waves / SIMD: <= 256 registers
+conv1x_kernel(int n, const void* __restrict__ ring, int slots, int s0, int s1, int s2,
+              const half8* __restrict__ wfrag, const float* __restrict__ bias,
+              unsigned char* __restrict__ y, float* __restrict__ partials, float slope,
+              WeightSplit ws) {
+  using Elem = typename std::conditional<kIdx, uint8_t, float>::type;
+  using Item = typename std::conditional<kIdx, uint32_t, float4>::type;
+  const Elem* __restrict__ ringT = static_cast<const Elem*>(ring);
+  __shared__ __attribute__((aligned(16))) unsigned char rbh[kSRing * kXRowB];
+  __shared__ __attribute__((aligned(16))) unsigned char rbl[kSRing * kXRowB];
+  __shared__ uint32_t s_hl[8];
+  __shared__ float red[kSW][CO][3];
+  __shared__ float s_bias[CO];
+  __shared__ float s_c[CO];   // the sample's centre: its pixel-0 outputs
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 31, h = lane >> 5;
+  const SplitPart sp = split_part(ws, n);
+  if (sp.set2) {
+    wfrag = static_cast<const half8*>(ws.wfrag);
+    bias = ws.bias;
+  }
+  const int send = sp.send;
+  const int total = sp.my * kSSteps;
+  if (total == 0) return;
+  auto sample = [&](int k) __attribute__((always_inline)) { return sp.sbeg + sp.bid + k * sp.gdim; };
+  const size_t plane = (size_t)IH * IW;
+
+  int it_r[kSPre], it_off[kSPre], it_lds[kSPre];
+#pragma unroll
+  for (int i = 0; i < kSPre; ++i) {
+    const int q = tid + i * kSThreads;
+    it_r[i] = q / kSQuads;
+    it_off[i] = it_r[i] * IW + 4 * (q - it_r[i] * kSQuads);
+    it_lds[i] = 4 * kXPxB * (q - it_r[i] * kSQuads);
+  }
+  // rows r0..r1 of the k-th sample into registers (conv1s_kernel's issue:
+  // every load on every path, sample clamped, row-free steps read row 0)
+  auto issue = [&](Item (&pre)[kSPre][3], int k, int r0, int r1) __attribute__((always_inline)) {
+    const int rows = r1 - r0 + 1;
+    const int ns = sample(k) < send ? sample(k) : send - 1;
+    const Elem* base = ringT + (size_t)ns * slots * plane + (size_t)(rows > 0 ? r0 : 0) * IW;
+    const Elem* p0 = base + (size_t)s0 * plane;
+    const Elem* p1 = base + (size_t)s1 * plane;
+    const Elem* p2 = base + (size_t)s2 * plane;
+#pragma unroll
+    for (int i = 0; i < kSPre; ++i) {
+      const int off = it_r[i] < rows ? it_off[i] : 0;
+      pre[i][0] = *reinterpret_cast<const Item*>(p0 + off);
+      pre[i][1] = *reinterpret_cast<const Item*>(p1 + off);
+      pre[i][2] = *reinterpret_cast<const Item*>(p2 + off);
+    }
+  };
+  // a load item's 4 pixels of one frame as (hi, lo) words
+  auto px4 = [&](const Item& it, uint32_t (&o)[4]) __attribute__((always_inline)) {
+    if constexpr (kIdx) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = s_hl[(it >> (8 * e)) & 7u];
+    } else {
+      o[0] = hl16(it.x);
+      o[1] = hl16(it.y);
+      o[2] = hl16(it.z);
+      o[3] = hl16(it.w);
+    }
+  };
+  // the rows into the hi and lo rings: 4 pixels x 3 channels pixel-major a
+  // ring, row R of the stream (k * IH + r) in slot R % kSRing
+  auto commit = [&](const Item (&pre)[kSPre][3], int k, int r0, int r1) __attribute__((always_inline)) {
+    const int rows = r1 - r0 + 1;
+#pragma unroll
+    for (int i = 0; i < kSPre; ++i) {
+      if (it_r[i] >= rows) continue;
+      const int slot = (k * IH + r0 + it_r[i]) & (kSRing - 1);
+      uint32_t av[4], bv[4], cv[4];
+      px4(pre[i][0], av);
+      px4(pre[i][1], bv);
+      px4(pre[i][2], cv);
+      const uint32_t f[12] = {av[0], bv[0], cv[0], av[1], bv[1], cv[1],
+                              av[2], bv[2], cv[2], av[3], bv[3], cv[3]};
+      uint2* dh = reinterpret_cast<uint2*>(rbh + slot * kXRowB + it_lds[i]);   // 8-B aligned
+      uint2* dl = reinterpret_cast<uint2*>(rbl + slot * kXRowB + it_lds[i]);
+#pragma unroll
+      for (int e = 0; e < 3; ++e) {
+        dh[e] = make_uint2(hi_pair(f[4 * e], f[4 * e + 1]), hi_pair(f[4 * e + 2], f[4 * e + 3]));
+        dl[e] = make_uint2(lo_pair(f[4 * e], f[4 * e + 1]), lo_pair(f[4 * e + 2], f[4 * e + 3]));
+      }
+    }
+  };
+
+  // A fragments, hi and lo halves (K 192 as conv1s_kernel: step s covers
+  // kernel row 2(s/3) + h and 8 of its 24 (kx, c) values, t = 8(s%3) + j),
+  // gathered once from dt_conv1's fragment layout
+  half8 wah[kXMfma], wal[kXMfma];
+  {
+    const _Float16* wh = reinterpret_cast<const _Float16*>(wfrag);
+    const _Float16* wl = wh + 16 * 64 * 8;
+    const int co = lane & 31, hh = lane >> 5;
+#pragma unroll
+    for (int s = 0; s < kXMfma; ++s)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const int ky = 2 * (s / 3) + hh, t = 8 * (s % 3) + e, kx = t / 3, c = t % 3;
+        const int s1 = 2 * ky + kx / 4, l1 = co + 32 * ((kx & 3) >> 1), j1 = 4 * (kx & 1) + c;
+        wah[s][e] = wh[(s1 * 64 + l1) * 8 + j1];
+        wal[s][e] = wl[(s1 * 64 + l1) * 8 + j1];
+      }
+  }
+  if (tid < CO) s_bias[tid] = bias[tid];
+  if (kIdx && tid < 8) s_hl[tid] = hl16(dr::kPalGray[tid]);
+  float w_cnt = 0.0f, w_mean[16], w_m2[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) w_mean[r] = w_m2[r] = 0.0f;
+
+  auto step = [&](int g, int k, int j, Item (&nxt)[kSPre][3], const Item (&cur)[kSPre][3]) __attribute__((always_inline)) {
+    const int ns = sample(k);
+    const bool last_j = j + 1 == kSSteps;
+    const int k1 = last_j ? k + 1 : k, j1 = last_j ? 0 : j + 1;   // step g+1
+    const int k2 = (j1 + 1 == kSSteps) ? k1 + 1 : k1;             // step g+2
+    issue(nxt, k2, s_first_new(j1), s_last_new(j1));
+
+    const int t = kSW * j + wave;
+    const int p = 32 * t + col;
+    const bool valid = p < kSPix;
+    const int pc = valid ? p : 0;
+    const int oy = pc / OW, ox = pc - oy * OW;
+    const int rbase = k * IH + 2 * oy;
+    const int cx = 12 * ox;
+    f32x16 acc0, acc1;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      acc0[r] = s_bias[(r & 3) + 8 * (r >> 2) + 4 * h];
+      acc1[r] = 0.0f;
+    }
+    half8 bqh[2][kXGrp], bql[2][kXGrp];
+    auto ld = [&](half8 (&bh)[kXGrp], half8 (&bl)[kXGrp], int gy) __attribute__((always_inline)) {
+      using u32x4a = __attribute__((ext_vector_type(4), aligned(4))) uint32_t;
+#pragma unroll
+      for (int i = 0; i < kXGrp; ++i) {   // row 2gy + h, bytes 12 ox + 16 i: 4-B aligned
+        const int off = ((rbase + 2 * gy + h) & (kSRing - 1)) * kXRowB + cx + 16 * i;
+        bh[i] = __builtin_bit_cast(half8, *reinterpret_cast<const u32x4a*>(rbh + off));
+        bl[i] = __builtin_bit_cast(half8, *reinterpret_cast<const u32x4a*>(rbl + off));
+      }
+    };
+    ld(bqh[0], bql[0], 0);
+#pragma unroll
+    for (int gy = 0; gy < 4; ++gy) {
+      if (gy < 3) ld(bqh[(gy + 1) & 1], bql[(gy + 1) & 1], gy + 1);
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < kXGrp; ++i) {
+        const int s = kXGrp * gy + i;
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(wah[s], bqh[gy & 1][i], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(wah[s], bql[gy & 1][i], acc1, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(wal[s], bqh[gy & 1][i], acc1, 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    float v[16];
+#pragma unroll
+    for (int r = 0; r < 16; ++r) v[r] = lrelu2(acc0[r] + acc1[r] * kLoInv, slope);
+    centre_px32(v, s_c, j == 0 && wave == 0 && col == 0, j == 0, h);
+    store_hl32<kSPix>(y + (size_t)ns * kSPix * 128, pc, v, h, valid);
+    if (valid) {   // Welford over this lane's pixels
+      w_cnt += 1.0f;
+      const float inv = 1.0f / w_cnt;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) {
+        const float d = v[r] - w_mean[r];
+        w_mean[r] += d * inv;
+        w_m2[r] += d * (v[r] - w_mean[r]);
+      }
+    }
+    if (last_j)
+      stats_flush<kSW>(w_cnt, w_mean, w_m2, red, s_c, partials + (size_t)ns * CO * 3, tid, wave,
+                       col, h);
+    // step g+1's rows into the rings (slots no wave reads in this step); the
+    // barrier publishes them
+    if (g + 1 < total) commit(cur, k1, s_first_new(j), s_last_new(j));
+    __syncthreads();
+  };
+
+  Item pa[kSPre][3], pb[kSPre][3];
+  issue(pa, 0, 0, s_hi(0));
+  if (kIdx) __syncthreads();   // s_hl
+  commit(pa, 0, 0, s_hi(0));
+  if (total > 1) issue(pb, kSSteps == 1 ? 1 : 0, s_first_new(0), s_last_new(0));
+  __syncthreads();
+  __builtin_amdgcn_s_waitcnt(0);   // see conv1s_kernel: keeps the loop's vmcnt waits exact
+  int k = 0, j = 0;
+  for (int g = 0; g < total; g += 2) {
+    step(g, k, j, pa, pb);
+    if (++j == kSSteps) { j = 0; ++k; }
+    if (g + 1 < total) {
+      step(g + 1, k, j, pb, pa);
+      if (++j == kSSteps) { j = 0; ++k; }
+    }
+  }
+}
+
+// ---- conv2..conv4 --------------------------------------------------------------------
+// conv_2d(32 -> 32, 4x4, stride ST) on an HL input [IH, IW] a sample.  k step
+// s (0..31) of a tile covers input pixel (ky, kx) = (s / 8, (s / 2) % 4),
+// channels 16 (s % 2) + 8 h .. +7 (dt_conv32's order); a unit is one kernel
+// row (8 steps, 24 MFMAs) of one round's tile.  kLast (conv4): the round holds
+// the whole sample; its own BatchNorm in-kernel (exact two-pass statistics),
+// written f32 flattened in NCHW order for the first linear.
+template <int IH_, int IW_, int OH_, int OW_, int ST, bool kLast>
+__global__ void __launch_bounds__(256, 2)   // 2 waves / SIMD: <= 256 registers
+conv32x_kernel(int n, const unsigned char* __restrict__ x, const float* __restrict__ wsrc,
+               const float* __restrict__ bias, const float* __restrict__ prev_part,
+               const float* __restrict__ in_gamma, const float* __restrict__ in_beta,
+               float in_eps, void* __restrict__ y, float* __restrict__ part,
+               const float* __restrict__ out_gamma, const float* __restrict__ out_beta,
+               float out_eps, float slope, WeightSplit ws) {
+  constexpr int kPix = OH_ * OW_, kTiles = (kPix + 31) / 32, kRounds = (kTiles + 3) / 4;
+  constexpr int kInBytes = IH_ * IW_ * 128;
+  static_assert(!kLast || kRounds == 1, "the in-kernel norm needs the sample in one round");
+  __shared__ half8 s_wh[32 * 64], s_wl[32 * 64];   // folded weights, hi / lo fragments
+  __shared__ float s_sc[CO], s_sh[CO], s_b2[CO], s_c[CO], s_bred[8][CO], red[4][CO][3];
+  __shared__ float s_omean[CO], s_osc[CO], s_obeta[CO];
+  __shared__ float s_wexp[2];   // 2^-e (the folded weights' scale), 2^e
+  __shared__ unsigned int s_wmax;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 31, h = lane >> 5;
+  const SplitPart sp = split_part(ws, n);
+  if (sp.set2) {
+    wsrc = static_cast<const float*>(ws.wfrag);
+    bias = ws.bias;
+    in_gamma = ws.in_gamma;
+    in_beta = ws.in_beta;
+    out_gamma = ws.out_gamma;
+    out_beta = ws.out_beta;
+  }
+  if (sp.my == 0) return;
+  const int send = sp.send;
+  auto sample = [&](int k) __attribute__((always_inline)) {
+    const int s = sp.sbeg + sp.bid + k * sp.gdim;
+    return s < send ? s : send - 1;
+  };
+
+  // max |w| of the set, once a launch: with the largest |sc| of a sample it
+  // bounds the folded weights, scaled by 2^-e into fp16's range when needed
+  if (tid == 0) s_wmax = 0u;
+  __syncthreads();
+  {
+    float m = 0.0f;
+    const float4* w4 = reinterpret_cast<const float4*>(wsrc);
+#pragma unroll 4
+    for (int i = 0; i < 16; ++i) {
+      const float4 q = w4[tid + 256 * i];
+      m = fmaxf(m, fmaxf(fmaxf(fabsf(q.x), fabsf(q.y)), fmaxf(fabsf(q.z), fabsf(q.w))));
+    }
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    if (lane == 0) atomicMax(&s_wmax, __float_as_uint(m));
+  }
+  __syncthreads();
+
+  // a unit's B operand: 8 k steps x (hi, lo) 16-B chunks of the lane's pixel
+  // (every load issued, pixel and sample clamped: the offsets stay inside the
+  // sample and the vmcnt waits stay exact)
+  auto unit_load = [&](u32x4 (&bh)[8], u32x4 (&bl)[8], int k, int u) __attribute__((always_inline)) {
+    const int r = u >> 2, gy = u & 3;
+    const int t = 4 * r + wave;
+    const int p = 32 * (t < kTiles ? t : 0) + col;
+    const int pc = p < kPix ? p : 0;
+    const int oy = pc / OW_, ox = pc - oy * OW_;
+    const int vb = ((ST * oy + gy) * IW_ + ST * ox) * 128 + 16 * h;
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+        const_cast<unsigned char*>(x + (size_t)sample(k) * kInBytes), 0, kInBytes, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int off = vb + (i >> 1) * 128 + 32 * (i & 1);
+      bh[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
+      bl[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 64, 0, 0);
+    }
+  };
+
+  float w_cnt = 0.0f, w_mean[16], w_m2[16];
+#pragma unroll
+  for (int r = 0; r < 16; ++r) w_mean[r] = w_m2[r] = 0.0f;
+  f32x16 acc0, acc1;
+  u32x4 ba[8], bb[8], ca[8], cb[8];   // two units' B operands: (ba, ca) and (bb, cb)
+
+  // one unit: issue the next unit's loads into (nh, nl), run this one's MFMAs
+  // on (bh, bl); the tile's epilogue after its last kernel row
+  auto unit = [&](int k, int u, u32x4 (&bh)[8], u32x4 (&bl)[8], u32x4 (&nh)[8],
+                  u32x4 (&nl)[8]) __attribute__((always_inline)) {
+    constexpr int kUnits = 4 * kRounds;
+    const bool lastu = u + 1 == kUnits;
+    unit_load(nh, nl, lastu ? k + 1 : k, lastu ? 0 : u + 1);
+    const int r = u >> 2, gy = u & 3;
+    const int t = 4 * r + wave;
+    if (gy == 0) {
+#pragma unroll
+      for (int q = 0; q < 16; ++q) acc0[q] = acc1[q] = 0.0f;
+    }
+    if (t < kTiles) {   // wave-uniform
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        const int s = 8 * gy + i;
+        const half8 ah = s_wh[s * 64 + lane], al = s_wl[s * 64 + lane];
+        const half8 xh = __builtin_bit_cast(half8, bh[i]), xl = __builtin_bit_cast(half8, bl[i]);
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, xh, acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, xl, acc1, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, xh, acc1, 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (gy != 3) return;
+    // epilogue of round r's tile
+    const int ns = sample(k);
+    if (r == 0) __syncthreads();   // s_b2 (threads < CO, after the weight barrier)
+    const float isc = s_wexp[1];
+    const int p = 32 * t + col;
+    const bool valid = t < kTiles && p < kPix;
+    float v[16];
+#pragma unroll
+    for (int q = 0; q < 16; ++q)
+      v[q] = lrelu2((acc0[q] + acc1[q] * kLoInv) * isc + s_b2[(q & 3) + 8 * (q >> 2) + 4 * h],
+                    slope);
+    if constexpr (!kLast) {
+      centre_px32(v, s_c, r == 0 && wave == 0 && col == 0, r == 0, h);
+      store_hl32<kPix>(static_cast<unsigned char*>(y) + (size_t)ns * kPix * 128, valid ? p : 0, v, h,
+                       valid);
+      if (valid) {
+        w_cnt += 1.0f;
+        const float inv = 1.0f / w_cnt;
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const float d = v[q] - w_mean[q];
+          w_mean[q] += d * inv;
+          w_m2[q] += d * (v[q] - w_mean[q]);
+        }
+      }
+      if (r + 1 == kRounds)
+        stats_flush<4>(w_cnt, w_mean, w_m2, red, s_c, part + (size_t)ns * CO * 3, tid, wave, col,
+                       h);
+    } else {
+      // exact two-pass statistics: per wave over its 32 pixels (shuffles),
+      // the waves merged with Chan's formula by threads < CO
+      float nw = valid ? 1.0f : 0.0f;
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) nw += __shfl_xor(nw, o, 32);
+      const float inw = nw > 0.0f ? 1.0f / nw : 0.0f;
+      float sum[16], m2[16];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) sum[q] = valid ? v[q] : 0.0f;
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) sum[q] += __shfl_xor(sum[q], o, 32);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const float d = valid ? v[q] - sum[q] * inw : 0.0f;
+        m2[q] = d * d;
+      }
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) m2[q] += __shfl_xor(m2[q], o, 32);
+      if (col == 0)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+          const int c = (q & 3) + 8 * (q >> 2) + 4 * h;
+          red[wave][c][0] = nw;
+          red[wave][c][1] = sum[q] * inw;
+          red[wave][c][2] = m2[q];
+        }
+      __syncthreads();
+      if (tid < CO) {
+        float cnt = 0.0f, mean = 0.0f, mm = 0.0f;
+        for (int w = 0; w < 4; ++w) {
+          const float nb = red[w][tid][0];
+          if (nb <= 0.0f) continue;
+          const float tot = cnt + nb, d = red[w][tid][1] - mean;
+          mean += d * (nb / tot);
+          mm += red[w][tid][2] + d * d * (cnt * nb / tot);
+          cnt = tot;
+        }
+        s_omean[tid] = mean;
+        s_osc[tid] = out_gamma[tid] / sqrtf(mm / (float)kPix + out_eps);
+        s_obeta[tid] = out_beta[tid];
+      }
+      __syncthreads();
+      constexpr int kBytes = kPix * CO * 4;
+      const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
+          static_cast<float*>(y) + (size_t)ns * CO * kPix, 0, kBytes, 0x00020000);
+#pragma unroll
+      for (int q = 0; q < 16; ++q) {
+        const int c = (q & 3) + 8 * (q >> 2) + 4 * h;
+        const float o = (v[q] - s_omean[c]) * s_osc[c] + s_obeta[c];
+        __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o), rsrc,
+                                              valid ? (c * kPix + p) * 4 : kBytes, 0, 0);
+      }
+    }
+  };
+
+  unit_load(ba, ca, 0, 0);
+  for (int k = 0; k < sp.my; ++k) {
+    const int ns = sample(k);
+    // (a) the input's BatchNorm (per sample, batch of one) and the weight scale
+    if (tid < CO) {
+      const float* pp = prev_part + ((size_t)ns * CO + tid) * 3;
+      const float mean = pp[0], m2 = pp[1];
+      const float sc = in_gamma[tid] / sqrtf(m2 / (float)(IH_ * IW_) + in_eps);
+      s_sc[tid] = sc;
+      s_sh[tid] = in_beta[tid] - mean * sc;
+      float a = fabsf(sc);
+#pragma unroll
+      for (int o = 16; o > 0; o >>= 1) a = fmaxf(a, __shfl_xor(a, o, 32));
+      if (tid == 0) {
+        const float bound = a * __uint_as_float(s_wmax);
+        int e = 0;
+        if (bound > 16384.0f && bound < __builtin_inff()) (void)frexpf(bound * (1.0f / 16384.0f), &e);
+        s_wexp[0] = ldexpf(1.0f, -e);
+        s_wexp[1] = ldexpf(1.0f, e);
+      }
+    }
+    __syncthreads();
+    // (b) the folded weights: A fragment (s, l) holds w[l % 32][16 (s % 2) +
+    // 8 (l / 32) + j][(s / 2) / 4][(s / 2) % 4]; thread tid folds fragments
+    // tid + 256 i, all of output channel tid % 32, and sums its share of
+    // sum_k w * sh for bias'
+    {
+      const float wsc = s_wexp[0];
+      float bacc = 0.0f;
+#pragma unroll 2
+      for (int i = 0; i < 8; ++i) {
+        const int pidx = tid + 256 * i, s = pidx >> 6, l = pidx & 63;
+        const float4* src = reinterpret_cast<const float4*>(wsrc) + 2 * pidx;
+        const float4 q0 = src[0], q1 = src[1];
+        const float wv[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+        const int ci0 = 16 * (s & 1) + 8 * (l >> 5);
+        half8 hh, ll;
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const float t = wv[j] * s_sc[ci0 + j] * wsc;
+          const _Float16 th = (_Float16)t;
+          hh[j] = th;
+          ll[j] = (_Float16)((t - (float)th) * kLo);
+          bacc += wv[j] * s_sh[ci0 + j];
+        }
+        s_wh[pidx] = hh;
+        s_wl[pidx] = ll;
+      }
+      s_bred[tid >> 5][tid & 31] = bacc;
+    }
+    __syncthreads();
+    if (tid < CO) {
+      float b2 = bias[tid];
+#pragma unroll
+      for (int m = 0; m < 8; ++m) b2 += s_bred[m][tid];
+      s_b2[tid] = b2;
+    }
+    // (c) the rounds: units alternate between the two register sets
+#pragma unroll 1
+    for (int r = 0; r < kRounds; ++r) {
+      unit(k, 4 * r + 0, ba, ca, bb, cb);
+      unit(k, 4 * r + 1, bb, cb, ba, ca);
+      unit(k, 4 * r + 2, ba, ca, bb, cb);
+      unit(k, 4 * r + 3, bb, cb, ba, ca);
+    }
+  }
+}
+
+template <int IH_, int IW_, int OH_, int OW_, int ST, bool kLast>
+int launch_conv32x(int n, const void* x, const float* w, const float* bias, const float* pp,
+                   const float* ig, const float* ib, float ieps, void* y, float* part,
+                   const float* og, const float* ob, float oeps, float slope, hipStream_t s,
+                   WeightSplit ws, int n0) {
+  auto kern = conv32x_kernel<IH_, IW_, OH_, OW_, ST, kLast>;
+  static int grid = 0;   // resident workgroups, persistent
+  if (!grid) grid = resident_grid(kern, 256, 0);
+  const int g = split_grid(ws, n, n0, grid);
+  hipLaunchKernelGGL(kern, dim3(g), dim3(256), 0, s, n, (const unsigned char*)x, w, bias, pp, ig,
+                     ib, ieps, y, part, og, ob, oeps, slope, ws);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
+template <bool kIdx>
+int conv1x_launch(const void* ring, int32_t n, int32_t slots, const int32_t* order,
+                  const void* wfrag, const float* bias, const dt_conv_set* set2, void* y,
+                  float* partials, float slope, void* stream) {
+  if (!ring || !wfrag || !bias || !y || !partials || !order || n < 0 || slots < 3) return DT_E_ARG;
+  for (int i = 0; i < 3; ++i)
+    if (order[i] < 0 || order[i] >= slots) return DT_E_ARG;
+  if (set2 && (set2->n0 < 0 || set2->n0 > n || !set2->wfrag || !set2->bias)) return DT_E_ARG;
+  if (n == 0) return DT_OK;
+  static int grid = 0;
+  if (!grid) grid = resident_grid(conv1x_kernel<kIdx>, kSThreads, 0);
+  WeightSplit ws{};
+  if (set2) {
+    ws.wfrag = set2->wfrag;
+    ws.bias = set2->bias;
+  }
+  const int g = split_grid(ws, n, set2 ? set2->n0 : n, grid);
+  hipLaunchKernelGGL((conv1x_kernel<kIdx>), dim3(g), dim3(kSThreads), 0, (hipStream_t)stream, n,
+                     ring, slots, order[0], order[1], order[2], (const half8*)wfrag, bias,
+                     (unsigned char*)y, partials, slope, ws);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
+}  // namespace
+
+extern "C" int dt_conv1x_split(const void* ring, int32_t index, int32_t n, int32_t slots,
+                               const int32_t* order, const void* wfrag, const float* bias,
+                               const dt_conv_set* set2, void* y, float* partials, float slope,
+                               void* stream) {
+  return index ? conv1x_launch<true>(ring, n, slots, order, wfrag, bias, set2, y, partials, slope,
+                                     stream)
+               : conv1x_launch<false>(ring, n, slots, order, wfrag, bias, set2, y, partials,
+                                      slope, stream);
+}
+
+extern "C" int dt_conv32x_split(int32_t layer, int32_t n, const void* x, const float* wfrag,
+                                const float* bias, const float* prev_part, const float* in_gamma,
+                                const float* in_beta, float in_eps, void* y, float* part,
+                                const float* out_gamma, const float* out_beta, float out_eps,
+                                float slope, const dt_conv_set* set2, void* stream) {
+  if (!x || !wfrag || !bias || !y || !prev_part || !in_gamma || !in_beta || n < 0) return DT_E_ARG;
+  const bool last = layer == 4;
+  if (last ? (!out_gamma || !out_beta) : !part) return DT_E_ARG;
+  if (set2 && (set2->n0 < 0 || set2->n0 > n || !set2->wfrag || !set2->bias || !set2->in_gamma ||
+               !set2->in_beta || (last && (!set2->out_gamma || !set2->out_beta))))
+    return DT_E_ARG;
+  if (n == 0) return DT_OK;
+  WeightSplit ws{};
+  if (set2) {
+    ws.wfrag = set2->wfrag;
+    ws.bias = set2->bias;
+    ws.in_gamma = set2->in_gamma;
+    ws.in_beta = set2->in_beta;
+    ws.out_gamma = set2->out_gamma;
+    ws.out_beta = set2->out_beta;
+  }
+  const int n0 = set2 ? set2->n0 : n;
+  hipStream_t s = (hipStream_t)stream;
+  switch (layer) {
+    case 2:
+      return launch_conv32x<57, 77, 27, 37, 2, false>(n, x, wfrag, bias, prev_part, in_gamma,
+                                                      in_beta, in_eps, y, part, nullptr, nullptr,
+                                                      0.f, slope, s, ws, n0);
+    case 3:
+      return launch_conv32x<27, 37, 12, 17, 2, false>(n, x, wfrag, bias, prev_part, in_gamma,
+                                                      in_beta, in_eps, y, part, nullptr, nullptr,
+                                                      0.f, slope, s, ws, n0);
+    case 4:
+      return launch_conv32x<12, 17, 9, 14, 1, true>(n, x, wfrag, bias, prev_part, in_gamma,
+                                                    in_beta, in_eps, y, nullptr, out_gamma,
+                                                    out_beta, out_eps, slope, s, ws, n0);
+    default:
+      return DT_E_ARG;
+  }
+}

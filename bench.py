@@ -1111,18 +1111,20 @@ def step_parity(env, start, actions, out, rank, args, frames=None, m=64):
 
 
 # ---- configs 4 and 5 -----------------------------------------------------------------------
-def actor_f64(actor, x, mode='reference'):
-    """The actor in float64 on the host (torch CPU), dropout off: mode
-    'reference' = train-mode batch-of-one BatchNorm (per-sample statistics,
-    the explorers' forward), 'eval' = the running statistics (the folded-BN
-    policy); the precision yardstick of configs 4 / 5
-    (tools/actor_precision.py)."""
+def actor_f64(actor, x, mode='reference', device='cpu'):
+    """The actor in float64 (torch on `device`: the host by default, or the
+    GPU's f64 units for large samples), dropout off: mode 'reference' =
+    train-mode batch-of-one BatchNorm (per-sample statistics, the explorers'
+    forward), 'eval' = the running statistics (the folded-BN policy); the
+    precision yardstick of configs 4 / 5 (tools/actor_precision.py).
+    Returns a CPU tensor."""
     import torch
     import torch.nn.functional as F
     from aido1_amd.actor import apply_head
+    from aido1_amd.render import as_gray
     convs, bns, l1, l2 = actor.layers()
-    d = lambda t: t.detach().double().cpu()   # noqa: E731
-    h = x.double().cpu()
+    d = lambda t: t.detach().double().to(device)   # noqa: E731
+    h = as_gray(x.to(device)).double()
     for c, b in zip(convs, bns):
         h = F.leaky_relu(F.conv2d(h, d(c.weight), d(c.bias), stride=c.stride))
         if mode == 'eval':
@@ -1134,7 +1136,7 @@ def actor_f64(actor, x, mode='reference'):
         h = (h - m) / torch.sqrt(v + b.eps) * d(b.weight).view(1, -1, 1, 1) + \
             d(b.bias).view(1, -1, 1, 1)
     h = F.leaky_relu(F.linear(h.flatten(1), d(l1.weight), d(l1.bias)))
-    return apply_head(F.linear(h, d(l2.weight), d(l2.bias)), actor.head)
+    return apply_head(F.linear(h, d(l2.weight), d(l2.bias)), actor.head).cpu()
 
 
 # fp16 fast mode: the action bound against the float64 forward (DESIGN §3.6:

@@ -118,6 +118,46 @@ int dt_conv32_split(int32_t layer, int32_t n, const void* x, const void* wfrag,
                     const float* out_gamma, const float* out_beta, float out_eps, float slope,
                     const dt_conv_set* set2, void* stream);
 
+/* dt_conv1x_split / dt_conv32x_split: the same four convolutions at the
+ * reference's float32 accuracy (models/ddpg/model.py:79-88 acts in float32;
+ * duckietown_rl/ddpg.py:44-62), reference mode only (train-mode batch-of-one
+ * BatchNorms), on fp16 MFMA (aido1_amd/csrc/dtconvx.hip).  Every f32 operand x
+ * is an fp16 pair hi = fp16(x), lo = fp16((x - hi) * 2^11) (x = hi + 2^-11 lo
+ * to 2^-24 |x|) and every product three fp16 MFMA products accumulated in f32:
+ * ah*bh + 2^-11 (ah*bl + al*bh).  Activations between layers use the "HL"
+ * layout: fp16 [n, H, W, 64], a pixel's 32 hi values then its 32 lo values
+ * (the bytes of f32), centred on the sample's pixel 0 as dt_conv1's.
+ *
+ * dt_conv1x_split: conv1 + bias + LeakyReLU from the frame ring, as
+ * dt_conv1_split / dt_conv1_index_split (index != 0: palette-index u8 frames,
+ * else grey f32).
+ *   wfrag     device fp16 [2, 16, 64, 8]: dt_conv1's fragment layout, first
+ *             the hi halves of the f32 weights, then the lo halves
+ *   y         device fp16 [n, 57, 77, 64] (HL), centred
+ *   partials  device f32 [n, 32, 3] (required): (mean, M2, c) as dt_conv1's
+ *   set2      the second weight set (wfrag in this layout) or NULL.
+ * Assumes |w| < 65504 (an fp16 hi of a larger weight overflows). */
+int dt_conv1x_split(const void* ring, int32_t index, int32_t n, int32_t slots,
+                    const int32_t* order, const void* wfrag, const float* bias,
+                    const dt_conv_set* set2, void* y, float* partials, float slope, void* stream);
+
+/* dt_conv32x_split: conv2 / conv3 / conv4 (layer 2, 3, 4) as dt_conv32_split
+ * in reference mode.  The previous layer's BatchNorm (prev_part, in_gamma,
+ * in_beta, in_eps; all required) is folded per sample into the weights: w' =
+ * w * sc[c] (scaled by a power of two when the sample's largest |w'| would
+ * leave fp16's range), bias' = bias + sum_k w * sh[c].
+ *   x      device fp16 HL [n, IH, IW, 64] (dt_conv1x_split's y, or this call's
+ *          y of layer 2 / 3)
+ *   wfrag  device f32 [32, 64, 8]: dt_conv32's fragment layout in float32
+ *   y, part  layers 2, 3: HL [n, OH, OW, 64] centred, and (mean, M2, c)
+ *          [n, 32, 3]; layer 4: f32 [n, 32*9*14] flattened in NCHW order,
+ *          normalised by (out_gamma, out_beta, out_eps) (required), part NULL */
+int dt_conv32x_split(int32_t layer, int32_t n, const void* x, const float* wfrag,
+                     const float* bias, const float* prev_part, const float* in_gamma,
+                     const float* in_beta, float in_eps, void* y, float* part,
+                     const float* out_gamma, const float* out_beta, float out_eps, float slope,
+                     const dt_conv_set* set2, void* stream);
+
 /* dt_explore: SingleThreadExplorer's action choice for n explorers at once,
  * one fused pass replacing the torch restatement's ~25 element-wise kernels
  * (aido1_amd/explore.py explore_actions + rollout.CycleEpsilon; the same

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DT_ABI_VERSION 10 /* 2: curves per tile vary (curve_start), intersections;
+#define DT_ABI_VERSION 11 /* 2: curves per tile vary (curve_start), intersections;
                              3: static objects in dt_map, safety_rad_mult;
                              4: dt_render_io.pose / list_cap, dt_copy_pose,
                                 dt_step_many pose output;
@@ -50,7 +50,9 @@ extern "C" {
                                 the finished-episode ring); dt_render_order;
                             10: palette-index frames: dt_render_io.index,
                                 dt_palette_gray, dt_conv1_index_split,
-                                dt_frame_gather frame_kind */
+                                dt_frame_gather frame_kind
+                            11: dtactor.h dt_conv1x_split / dt_conv32x_split
+                                (the float32-accurate convolutions) */
 
 /* error codes */
 #define DT_OK 0
