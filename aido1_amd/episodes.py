@@ -151,9 +151,12 @@ class ExploiterSaver:
       (then saving_best_reward = reward)
       save if counter % save_every_episode == 0 or saving_best_cond.
     The exploiters of one poll act with the same weights, so one poll saves
-    at most once, under the last triggering episode's (counter, reward): the
-    reference's per-episode saves of identical weights would differ only in
-    the directory name."""
+    at most once per trigger kind: under the last best-reward episode's
+    (counter, reward) and under the last periodic one's (one save when they
+    are the same episode), so the directory names are ones the reference
+    writes.  save(counter, reward, best) is told whether the save is a
+    best-reward one (the reference logs 'best reward' only then,
+    explorers.py:220-221)."""
 
     def __init__(self, config, save):
         t = config['training']
@@ -161,23 +164,25 @@ class ExploiterSaver:
         self.every = int(t.get('save_every_episode', 0) or 0)
         self.best = -np.inf
         self.counter = 0
-        self.save = save           # save(episode_counter, reward) -> directory
+        self.save = save           # save(episode_counter, reward, best) -> directory
         self.saved = []            # (counter, reward, directory or None)
 
     def __call__(self, rewards):
-        trigger = None
+        """Feed one poll's rewards; returns the directories saved to."""
+        best_t = per_t = None
         for r in np.asarray(rewards, np.float64):
             self.counter += 1
-            cond = r > self.best + self.tolerance
-            if cond:
+            if r > self.best + self.tolerance:
                 self.best = float(r)
-            if cond or (self.every and self.counter % self.every == 0):
-                trigger = (self.counter, float(r))
-        if trigger is None:
-            return None
-        d = self.save(*trigger)
-        self.saved.append(trigger + (d,))
-        return d
+                best_t = (self.counter, float(r))
+            if self.every and self.counter % self.every == 0:
+                per_t = (self.counter, float(r))
+        out = []
+        for trig in sorted({t for t in (best_t, per_t) if t is not None}):
+            d = self.save(trig[0], trig[1], trig == best_t)
+            self.saved.append(trig + (d,))
+            out.append(d)
+        return out
 
 
 COLUMNS = ('rank', 'env', 'tick', 'episode', 'reward', 'reward_modified', 'step')
@@ -208,11 +213,12 @@ class EpisodeBook:
         self.best_reward = -np.inf      # explorers.py:217-218 (the shared best_reward)
         self.start_time = time.time()
 
-    def _save(self, counter, reward):
+    def _save(self, counter, reward, best):
         if self._save_fn is None:
             return None
         d = self._save_fn(counter, reward)
-        self.log.scalar_summary('best reward', self.exploiter.best, counter)
+        if best:   # explorers.py:220-221: the new saving_best_reward
+            self.log.scalar_summary('best reward', reward, counter)
         return d
 
     def table(self, recs):

@@ -179,9 +179,12 @@ class TrainLoop:
     def _save_exploiter(self, counter, reward):
         """explorers.py:75,150-152: the exploiters' model under
         save_dir/exploiting_virtual_thread_<p_id>, p_id the first virtual
-        exploiter's (training/managers.py:243-253)."""
-        t = self.config['training']
-        p_id = t.get('num_threads_exploring_virtual', 0) + t.get('num_threads_exploiting', 0)
+        exploiter's: its index 0 plus num_threads_exploiting
+        (training/managers.py:238-255; num_threads_exploring_virtual only
+        shifts its TCP port), so exploiting_virtual_thread_0 under
+        config.json, the directory the reference's submit and afterlearn
+        configs load from."""
+        p_id = self.config['training'].get('num_threads_exploiting', 0)
         return self.save(os.path.join(self.save_dir, 'exploiting_virtual_thread_%d' % p_id),
                          counter, reward)
 

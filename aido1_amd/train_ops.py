@@ -720,8 +720,11 @@ class _Loss(torch.autograd.Function):
 
 
 def _loss_applicable(*ts):
+    """The fused loss kernels take float32 GPU tensors of ONE shape: F.mse_loss
+    broadcasts [m] against [m, 1] to [m, m], which an element-wise kernel over
+    equal numel would silently not do."""
     return all(t.is_cuda and t.dtype == torch.float32 for t in ts) and \
-        len({t.numel() for t in ts}) == 1
+        len({tuple(t.shape) for t in ts}) == 1
 
 
 def mse_loss(a, b):

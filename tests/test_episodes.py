@@ -69,21 +69,39 @@ def test_exploiter_saver_follows_explorer_rule():
     rewards = np.cumsum(rng.normal(0.2, 2.0, 400))
     cfg = {'training': {'saving_reward_tolerance': 1, 'save_every_episode': 50}}
     got = []
-    sv = ExploiterSaver(cfg, lambda c, r: got.append((c, r)) or 'dir')
+    sv = ExploiterSaver(cfg, lambda c, r, best: got.append((c, r, best)) or 'dir')
     polls = np.split(rewards, [7, 8, 60, 61, 150, 333])
     for p in polls:
         sv(p)
     saves, best = _explorer_saves(rewards, 1, 50)
     assert sv.counter == 400 and sv.best == best
-    # one save a poll: the last triggering episode of each poll that had one
+    # a poll saves once per trigger kind: its last best-reward episode and its
+    # last periodic one, each a (counter, reward) the reference saves under
     expect = []
     bounds = np.cumsum([0] + [len(p) for p in polls])
     for lo, hi in zip(bounds[:-1], bounds[1:]):
-        inside = [s for s in saves if lo < s[0] <= hi]
-        if inside:
-            expect.append(inside[-1])
+        b = [s for s in saves if lo < s[0] <= hi and _is_best(rewards, s[0], 1)]
+        e = [s for s in saves if lo < s[0] <= hi and s[0] % 50 == 0]
+        trig = sorted({t for t in (b[-1:] + e[-1:])})
+        expect += [t + (bool(b) and t == b[-1],) for t in trig]
     assert got == expect
-    assert [s[:2] for s in sv.saved] == expect
+    assert [s[:2] for s in sv.saved] == [t[:2] for t in expect]
+    assert all(s in saves for s in [t[:2] for t in expect])
+    assert sum(t[2] for t in expect) >= 2 and any(not t[2] for t in expect)
+
+
+def _is_best(rewards, c, tol):
+    """Episode c (1-based) meets explorers.py:142's saving_best_cond."""
+    return rewards[c - 1] > max([-np.inf] + list(_running_best(rewards[:c - 1], tol))) + tol \
+        if c > 1 else True
+
+
+def _running_best(rewards, tol):
+    best = -np.inf
+    for r in rewards:
+        if r > best + tol:
+            best = r
+        yield best
 
 
 def test_episode_book_single_rank(tmp_path):
@@ -104,8 +122,12 @@ def test_episode_book_single_rank(tmp_path):
     assert np.array_equal(out['reward'], recs['reward'] / 2.0)
     assert np.array_equal(out['step'], recs['decisions'] * 3)
     assert np.array_equal(out['exploiting'], recs['env'] >= 12)
-    saves, best = _explorer_saves(out['reward'][out['exploiting']], 0.5, 5)
-    assert saved == [saves[-1]] and book.exploiter.best == best
+    rew = out['reward'][out['exploiting']]
+    saves, best = _explorer_saves(rew, 0.5, 5)
+    b = [s for s in saves if _is_best(rew, s[0], 0.5)]
+    e = [s for s in saves if s[0] % 5 == 0]
+    assert saved == sorted({t for t in (b[-1:] + e[-1:])}) and book.exploiter.best == best
+    assert [r['value'] for r in book.log.rows if r['tag'] == 'best reward'] == [b[-1][1]]
     tags = {r['tag'] for r in book.log.rows}
     assert {'exploring/reward', 'exploiting/reward', 'step per second', 'episode per minute',
             'best reward'} <= tags

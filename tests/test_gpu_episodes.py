@@ -149,7 +149,7 @@ def test_train_loop_episodes_and_exploiter_checkpoints(gpu, tmp_path):
     # the first exploiter episode beats -inf: at least one save, each in the
     # reference's layout and loadable
     assert book.exploiter.saved
-    base = os.path.join(str(tmp_path / 'saved'), 'exploiting_virtual_thread_7')
+    base = os.path.join(str(tmp_path / 'saved'), 'exploiting_virtual_thread_0')
     for c, r, d in book.exploiter.saved:
         assert d == os.path.join(base, 'episode_{}_reward_{:.2f}'.format(c, r))
         for f in ('config.json', 'actor_state_dict.pth', 'critic_state_dict.pth'):
