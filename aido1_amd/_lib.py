@@ -156,6 +156,151 @@ _lib = None
 _lock = threading.Lock()
 
 
+def bind(L):
+    """Declare the C-ABI signatures (include/*.h) on a loaded libdtsim (the
+    product library, a diagnostic build, or the host-only sanitizer build of
+    `make asan`); returns L."""
+    vp, i32, u32, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64
+    i64, f64 = ctypes.c_int64, ctypes.c_double
+    sig = {
+        'dt_abi_version': (i32, []),
+        'dt_create': (ctypes.c_int, [ctypes.POINTER(DtConfig), ctypes.POINTER(DtMap), u64, i32,
+                                     i32, ctypes.POINTER(vp)]),
+        'dt_destroy': (ctypes.c_int, [vp]),
+        'dt_n_envs': (i32, [vp]),
+        'dt_last_error': (ctypes.c_char_p, [vp]),
+        'dt_seed': (ctypes.c_int, [vp, vp, u64, u32]),
+        'dt_reset': (ctypes.c_int, [vp, vp, vp]),
+        'dt_step': (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+        'dt_step_masked': (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
+        'dt_step_many': (ctypes.c_int, [vp, i32, vp, vp, vp, vp, vp, vp, vp]),
+        'dt_seed_env': (ctypes.c_int, [vp, i32, u64]),
+        'dt_lane_pos': (ctypes.c_int, [vp, vp, vp, vp]),
+        'dt_render': (ctypes.c_int, [vp, vp, vp]),
+        'dt_render2': (ctypes.c_int, [vp, vp, vp, vp]),
+        'dt_render3': (ctypes.c_int, [vp, vp, vp, vp, vp]),
+        'dt_copy_pose': (ctypes.c_int, [vp, vp, vp]),
+        'dt_render_order': (ctypes.c_int, [vp, ctypes.POINTER(u32), vp, vp]),
+        'dt_palette_gray': (ctypes.c_int, [ctypes.POINTER(ctypes.c_float)]),
+        'dt_default_line_params': (ctypes.c_int, [vp]),
+        'dt_set_line_params': (ctypes.c_int, [vp, vp]),
+        'dt_line_detect': (ctypes.c_int, [vp, vp, i32, i32, i32, vp, vp, vp]),
+        'dt_hough_lines': (ctypes.c_int, [vp, i32, i32, i32, i32, i32, i32, i32, vp, vp,
+                                          vp]),
+        'dt_line_detect_workspace': (ctypes.c_size_t, [i32, i32, i32]),
+        'dt_line_detect_ws': (ctypes.c_int, [vp, vp, i32, i32, i32, vp, vp, vp,
+                                             ctypes.c_size_t, vp]),
+        'dt_hough_workspace': (ctypes.c_size_t, [i32, i32, i32]),
+        'dt_hough_lines_ws': (ctypes.c_int, [vp, i32, i32, i32, i32, i32, i32, i32, vp, vp,
+                                             vp, ctypes.c_size_t, vp]),
+        'dt_get_state': (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp]),
+        'dt_set_state': (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp]),
+        'dt_check': (ctypes.c_int, [vp, ctypes.POINTER(u32)]),
+        'dt_stats': (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), i32]),
+        # dtreplay.h
+        'dt_per_create': (ctypes.c_int, [i64, f64, i32, ctypes.POINTER(vp)]),
+        'dt_per_destroy': (None, [vp]),
+        'dt_per_last_error': (ctypes.c_char_p, [vp]),
+        'dt_per_capacity': (i64, [vp]),
+        'dt_per_len': (i64, [vp]),
+        'dt_per_next_idx': (i64, [vp]),
+        'dt_per_add': (ctypes.c_int, [vp, i64, vp, vp]),
+        'dt_per_sample': (ctypes.c_int, [vp, i32, vp, f64, vp, vp, vp]),
+        'dt_per_update': (ctypes.c_int, [vp, i32, vp, vp, vp]),
+        'dt_per_update_td': (ctypes.c_int, [vp, i32, vp, vp, f64, vp]),
+        'dt_per_read': (ctypes.c_int, [vp, vp, vp, vp, vp]),
+        'dt_per_check': (ctypes.c_int, [vp]),
+        'dt_frame_add': (ctypes.c_int, [i32, i64, vp, i64, vp, i32, vp, vp, i32, vp, vp, vp]),
+        'dt_frame_gather': (ctypes.c_int, [i32, vp, vp, i32, i64, i32, vp, vp, vp, vp, vp,
+                                           vp, vp, vp, vp, vp, vp]),
+        # dttrain.h
+        'dt_train_work_floats': (i64, [i64]),
+        'dt_bn_leaky_fwd': (ctypes.c_int, [i64, vp, vp, ctypes.c_float, vp, vp, ctypes.c_float,
+                                           ctypes.c_float, vp, vp, vp, i32, vp, vp, vp, vp,
+                                           vp, vp]),
+        'dt_bn_leaky_bwd': (ctypes.c_int, [i64, vp, vp, vp, vp, vp, ctypes.c_float, vp, vp, vp,
+                                           vp, vp, vp, vp]),
+        'dt_adam': (ctypes.c_int, [i32, vp, vp, vp, vp, f64, f64, f64, vp, vp, i32, i32, vp]),
+        'dt_guard_scan': (ctypes.c_int, [i32, vp, vp, vp]),
+        # dtupd.h
+        'dt_upd_conv_fwd': (ctypes.c_int, [i32, i32, i32, i32, i32, i32, vp, vp, vp, vp]),
+        'dt_upd_conv_fwd_bn': (ctypes.c_int, [i32, i32, i32, i32, i32, i32, vp, vp, vp,
+                                              ctypes.c_float, ctypes.c_float, ctypes.c_float,
+                                              vp, vp, vp, i32, vp, vp, vp, vp, vp]),
+        'dt_bn_leaky_apply': (ctypes.c_int, [i64, vp, vp, ctypes.c_float, vp, vp, vp, vp,
+                                             vp]),
+        'dt_upd_wgrad_work_floats': (i64, [i32, i32, i32, i32, i32, i32]),
+        'dt_upd_bn_work_floats': (i64, []),
+        'dt_upd_conv_wgrad': (ctypes.c_int, [i32, i32, i32, i32, i32, i32, vp, vp, vp, vp,
+                                             vp]),
+        'dt_upd_conv_dgrad': (ctypes.c_int, [i32, i32, i32, i32, i32, i32, vp, vp, vp, vp]),
+        'dt_upd_part_floats': (i64, []),
+        'dt_upd_conv_fwd_part': (ctypes.c_int, [i32, i32, i32, i32, i32, i32, vp,
+                                                ctypes.POINTER(DtUpdBn), vp, vp,
+                                                ctypes.c_float, vp, vp,
+                                                ctypes.POINTER(i32), vp]),
+        'dt_upd_bn_finish': (ctypes.c_int, [i64, i32, vp, ctypes.POINTER(DtUpdBn), vp, vp]),
+        'dt_upd_conv_wgrad_bn': (ctypes.c_int, [i32, i32, i32, i32, i32, i32, vp,
+                                                ctypes.POINTER(DtUpdBn), vp, vp, vp, vp]),
+        'dt_upd_linear_work_floats': (i64, [i32, i32, i32]),
+        'dt_upd_linear_fwd': (ctypes.c_int, [i32, i32, i32, vp, vp, vp, i32, ctypes.c_float,
+                                             vp, vp, vp]),
+        'dt_upd_linear_dgrad': (ctypes.c_int, [i32, i32, i32, vp, vp, vp, ctypes.c_float, vp,
+                                               vp]),
+        'dt_upd_linear_wgrad': (ctypes.c_int, [i32, i32, i32, vp, vp, vp, ctypes.c_float, vp,
+                                               vp, vp]),
+        'dt_soft_update': (ctypes.c_int, [i32, vp, vp, f64, vp]),
+        # dthead.h
+        'dt_mlp_fwd': (ctypes.c_int, [ctypes.POINTER(DtMlp), vp, vp, vp, vp, vp]),
+        'dt_mlp_bwd': (ctypes.c_int, [ctypes.POINTER(DtMlp), vp, vp, vp, vp, vp, vp, vp, vp,
+                                      vp, vp, vp, vp]),
+        'dt_mlp_fwd_td': (ctypes.c_int, [ctypes.POINTER(DtMlp), vp, vp, vp, vp, vp, vp,
+                                         ctypes.c_float, vp, vp]),
+        'dt_loss': (ctypes.c_int, [i32, i32, vp, vp, vp, vp]),
+        'dt_loss_bwd': (ctypes.c_int, [i32, i32, vp, vp, vp, vp, vp]),
+        # dtactor.h
+        'dt_sample_norm': (ctypes.c_int, [vp, vp, i32, i32, i32, vp, vp, ctypes.c_float,
+                                          ctypes.c_float, i32, vp]),
+        'dt_conv1': (ctypes.c_int, [vp, i32, i32, ctypes.POINTER(i32), vp, vp, vp, vp,
+                                    ctypes.c_float, vp]),
+        'dt_conv1_split': (ctypes.c_int, [vp, i32, i32, ctypes.POINTER(i32), vp, vp,
+                                          ctypes.POINTER(DtConvSet), vp, vp, ctypes.c_float,
+                                          vp]),
+        'dt_conv1_index_split': (ctypes.c_int, [vp, i32, i32, ctypes.POINTER(i32), vp, vp,
+                                                ctypes.POINTER(DtConvSet), vp, vp,
+                                                ctypes.c_float, vp]),
+        'dt_conv1_norm': (ctypes.c_int, [vp, i32, vp, vp, vp, ctypes.c_float, vp]),
+        'dt_conv32': (ctypes.c_int, [i32, i32, vp, vp, vp, vp, vp, vp, ctypes.c_float, vp,
+                                     vp, vp, vp, ctypes.c_float, ctypes.c_float, vp]),
+        'dt_conv32_split': (ctypes.c_int, [i32, i32, vp, vp, vp, vp, vp, vp, ctypes.c_float,
+                                           vp, vp, vp, vp, ctypes.c_float, ctypes.c_float,
+                                           ctypes.POINTER(DtConvSet), vp]),
+        'dt_conv1x_split': (ctypes.c_int, [vp, i32, i32, i32, ctypes.POINTER(i32), vp, vp,
+                                           ctypes.POINTER(DtConvSet), vp, vp,
+                                           ctypes.c_float, vp]),
+        'dt_conv32x_split': (ctypes.c_int, [i32, i32, vp, vp, vp, vp, vp, vp, ctypes.c_float,
+                                            vp, vp, vp, vp, ctypes.c_float, ctypes.c_float,
+                                            ctypes.POINTER(DtConvSet), vp]),
+        'dt_explore': (ctypes.c_int, [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
+                                      ctypes.POINTER(DtExploreParams), vp, vp]),
+        'dt_explore_done': (ctypes.c_int, [i32, vp, vp, vp, vp, i32, vp]),
+        'dt_episode_account': (ctypes.c_int, [i32, i32, vp, vp, vp,
+                                              ctypes.POINTER(DtEpisodeState), vp]),
+        'dt_refresh_copy': (ctypes.c_int, [i32, vp, i64, vp]),
+        'dt_actor_head': (ctypes.c_int, [i32, i32, i32, vp, i32, vp, vp, vp, vp, i32,
+                                         ctypes.c_float, vp, vp]),
+    }
+    for name, (res, args) in sig.items():
+        if not hasattr(L, name):
+            if name in _OPTIONAL:
+                continue
+            raise DtError('libdtsim.so lacks %s (stale build?)' % name)
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    return L
+
+
 def lib():
     """Load (building first if needed) libdtsim.so; raises DtError if impossible."""
     global _lib
@@ -174,145 +319,7 @@ def lib():
             path = LIB_PATH
             if _stale():
                 build()
-        L = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
-        vp, i32, u32, u64 = ctypes.c_void_p, ctypes.c_int32, ctypes.c_uint32, ctypes.c_uint64
-        i64, f64 = ctypes.c_int64, ctypes.c_double
-        sig = {
-            'dt_abi_version': (i32, []),
-            'dt_create': (ctypes.c_int, [ctypes.POINTER(DtConfig), ctypes.POINTER(DtMap), u64, i32,
-                                         i32, ctypes.POINTER(vp)]),
-            'dt_destroy': (ctypes.c_int, [vp]),
-            'dt_n_envs': (i32, [vp]),
-            'dt_last_error': (ctypes.c_char_p, [vp]),
-            'dt_seed': (ctypes.c_int, [vp, vp, u64, u32]),
-            'dt_reset': (ctypes.c_int, [vp, vp, vp]),
-            'dt_step': (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp]),
-            'dt_step_masked': (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp, vp, vp, vp]),
-            'dt_step_many': (ctypes.c_int, [vp, i32, vp, vp, vp, vp, vp, vp, vp]),
-            'dt_seed_env': (ctypes.c_int, [vp, i32, u64]),
-            'dt_lane_pos': (ctypes.c_int, [vp, vp, vp, vp]),
-            'dt_render': (ctypes.c_int, [vp, vp, vp]),
-            'dt_render2': (ctypes.c_int, [vp, vp, vp, vp]),
-            'dt_render3': (ctypes.c_int, [vp, vp, vp, vp, vp]),
-            'dt_copy_pose': (ctypes.c_int, [vp, vp, vp]),
-            'dt_render_order': (ctypes.c_int, [vp, ctypes.POINTER(u32), vp, vp]),
-            'dt_palette_gray': (ctypes.c_int, [ctypes.POINTER(ctypes.c_float)]),
-            'dt_default_line_params': (ctypes.c_int, [vp]),
-            'dt_set_line_params': (ctypes.c_int, [vp, vp]),
-            'dt_line_detect': (ctypes.c_int, [vp, vp, i32, i32, i32, vp, vp, vp]),
-            'dt_hough_lines': (ctypes.c_int, [vp, i32, i32, i32, i32, i32, i32, i32, vp, vp,
-                                              vp]),
-            'dt_line_detect_workspace': (ctypes.c_size_t, [i32, i32, i32]),
-            'dt_line_detect_ws': (ctypes.c_int, [vp, vp, i32, i32, i32, vp, vp, vp,
-                                                 ctypes.c_size_t, vp]),
-            'dt_hough_workspace': (ctypes.c_size_t, [i32, i32, i32]),
-            'dt_hough_lines_ws': (ctypes.c_int, [vp, i32, i32, i32, i32, i32, i32, i32, vp, vp,
-                                                 vp, ctypes.c_size_t, vp]),
-            'dt_get_state': (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp]),
-            'dt_set_state': (ctypes.c_int, [vp, vp, vp, vp, vp, vp, vp]),
-            'dt_check': (ctypes.c_int, [vp, ctypes.POINTER(u32)]),
-            'dt_stats': (ctypes.c_int, [vp, ctypes.POINTER(ctypes.c_uint64), i32]),
-            # dtreplay.h
-            'dt_per_create': (ctypes.c_int, [i64, f64, i32, ctypes.POINTER(vp)]),
-            'dt_per_destroy': (None, [vp]),
-            'dt_per_last_error': (ctypes.c_char_p, [vp]),
-            'dt_per_capacity': (i64, [vp]),
-            'dt_per_len': (i64, [vp]),
-            'dt_per_next_idx': (i64, [vp]),
-            'dt_per_add': (ctypes.c_int, [vp, i64, vp, vp]),
-            'dt_per_sample': (ctypes.c_int, [vp, i32, vp, f64, vp, vp, vp]),
-            'dt_per_update': (ctypes.c_int, [vp, i32, vp, vp, vp]),
-            'dt_per_update_td': (ctypes.c_int, [vp, i32, vp, vp, f64, vp]),
-            'dt_per_read': (ctypes.c_int, [vp, vp, vp, vp, vp]),
-            'dt_per_check': (ctypes.c_int, [vp]),
-            'dt_frame_add': (ctypes.c_int, [i32, i64, vp, i64, vp, i32, vp, vp, i32, vp, vp, vp]),
-            'dt_frame_gather': (ctypes.c_int, [i32, vp, vp, i32, i64, i32, vp, vp, vp, vp, vp,
-                                               vp, vp, vp, vp, vp, vp]),
-            # dttrain.h
-            'dt_train_work_floats': (i64, [i64]),
-            'dt_bn_leaky_fwd': (ctypes.c_int, [i64, vp, vp, ctypes.c_float, vp, vp, ctypes.c_float,
-                                               ctypes.c_float, vp, vp, vp, i32, vp, vp, vp, vp,
-                                               vp, vp]),
-            'dt_bn_leaky_bwd': (ctypes.c_int, [i64, vp, vp, vp, vp, vp, ctypes.c_float, vp, vp, vp,
-                                               vp, vp, vp, vp]),
-            'dt_adam': (ctypes.c_int, [i32, vp, vp, vp, vp, f64, f64, f64, vp, vp, i32, i32, vp]),
-            'dt_guard_scan': (ctypes.c_int, [i32, vp, vp, vp]),
-            # dtupd.h
-            'dt_upd_conv_fwd': (ctypes.c_int, [i32, i32, i32, i32, i32, i32, vp, vp, vp, vp]),
-            'dt_upd_conv_fwd_bn': (ctypes.c_int, [i32, i32, i32, i32, i32, i32, vp, vp, vp,
-                                                  ctypes.c_float, ctypes.c_float, ctypes.c_float,
-                                                  vp, vp, vp, i32, vp, vp, vp, vp, vp]),
-            'dt_bn_leaky_apply': (ctypes.c_int, [i64, vp, vp, ctypes.c_float, vp, vp, vp, vp,
-                                                 vp]),
-            'dt_upd_wgrad_work_floats': (i64, [i32, i32, i32, i32, i32, i32]),
-            'dt_upd_bn_work_floats': (i64, []),
-            'dt_upd_conv_wgrad': (ctypes.c_int, [i32, i32, i32, i32, i32, i32, vp, vp, vp, vp,
-                                                 vp]),
-            'dt_upd_conv_dgrad': (ctypes.c_int, [i32, i32, i32, i32, i32, i32, vp, vp, vp, vp]),
-            'dt_upd_part_floats': (i64, []),
-            'dt_upd_conv_fwd_part': (ctypes.c_int, [i32, i32, i32, i32, i32, i32, vp,
-                                                    ctypes.POINTER(DtUpdBn), vp, vp,
-                                                    ctypes.c_float, vp, vp,
-                                                    ctypes.POINTER(i32), vp]),
-            'dt_upd_bn_finish': (ctypes.c_int, [i64, i32, vp, ctypes.POINTER(DtUpdBn), vp, vp]),
-            'dt_upd_conv_wgrad_bn': (ctypes.c_int, [i32, i32, i32, i32, i32, i32, vp,
-                                                    ctypes.POINTER(DtUpdBn), vp, vp, vp, vp]),
-            'dt_upd_linear_work_floats': (i64, [i32, i32, i32]),
-            'dt_upd_linear_fwd': (ctypes.c_int, [i32, i32, i32, vp, vp, vp, i32, ctypes.c_float,
-                                                 vp, vp, vp]),
-            'dt_upd_linear_dgrad': (ctypes.c_int, [i32, i32, i32, vp, vp, vp, ctypes.c_float, vp,
-                                                   vp]),
-            'dt_upd_linear_wgrad': (ctypes.c_int, [i32, i32, i32, vp, vp, vp, ctypes.c_float, vp,
-                                                   vp, vp]),
-            'dt_soft_update': (ctypes.c_int, [i32, vp, vp, f64, vp]),
-            # dthead.h
-            'dt_mlp_fwd': (ctypes.c_int, [ctypes.POINTER(DtMlp), vp, vp, vp, vp, vp]),
-            'dt_mlp_bwd': (ctypes.c_int, [ctypes.POINTER(DtMlp), vp, vp, vp, vp, vp, vp, vp, vp,
-                                          vp, vp, vp, vp]),
-            'dt_mlp_fwd_td': (ctypes.c_int, [ctypes.POINTER(DtMlp), vp, vp, vp, vp, vp, vp,
-                                             ctypes.c_float, vp, vp]),
-            'dt_loss': (ctypes.c_int, [i32, i32, vp, vp, vp, vp]),
-            'dt_loss_bwd': (ctypes.c_int, [i32, i32, vp, vp, vp, vp, vp]),
-            # dtactor.h
-            'dt_sample_norm': (ctypes.c_int, [vp, vp, i32, i32, i32, vp, vp, ctypes.c_float,
-                                              ctypes.c_float, i32, vp]),
-            'dt_conv1': (ctypes.c_int, [vp, i32, i32, ctypes.POINTER(i32), vp, vp, vp, vp,
-                                        ctypes.c_float, vp]),
-            'dt_conv1_split': (ctypes.c_int, [vp, i32, i32, ctypes.POINTER(i32), vp, vp,
-                                              ctypes.POINTER(DtConvSet), vp, vp, ctypes.c_float,
-                                              vp]),
-            'dt_conv1_index_split': (ctypes.c_int, [vp, i32, i32, ctypes.POINTER(i32), vp, vp,
-                                                    ctypes.POINTER(DtConvSet), vp, vp,
-                                                    ctypes.c_float, vp]),
-            'dt_conv1_norm': (ctypes.c_int, [vp, i32, vp, vp, vp, ctypes.c_float, vp]),
-            'dt_conv32': (ctypes.c_int, [i32, i32, vp, vp, vp, vp, vp, vp, ctypes.c_float, vp,
-                                         vp, vp, vp, ctypes.c_float, ctypes.c_float, vp]),
-            'dt_conv32_split': (ctypes.c_int, [i32, i32, vp, vp, vp, vp, vp, vp, ctypes.c_float,
-                                               vp, vp, vp, vp, ctypes.c_float, ctypes.c_float,
-                                               ctypes.POINTER(DtConvSet), vp]),
-            'dt_conv1x_split': (ctypes.c_int, [vp, i32, i32, i32, ctypes.POINTER(i32), vp, vp,
-                                               ctypes.POINTER(DtConvSet), vp, vp,
-                                               ctypes.c_float, vp]),
-            'dt_conv32x_split': (ctypes.c_int, [i32, i32, vp, vp, vp, vp, vp, vp, ctypes.c_float,
-                                                vp, vp, vp, vp, ctypes.c_float, ctypes.c_float,
-                                                ctypes.POINTER(DtConvSet), vp]),
-            'dt_explore': (ctypes.c_int, [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
-                                          ctypes.POINTER(DtExploreParams), vp, vp]),
-            'dt_explore_done': (ctypes.c_int, [i32, vp, vp, vp, vp, i32, vp]),
-            'dt_episode_account': (ctypes.c_int, [i32, i32, vp, vp, vp,
-                                                  ctypes.POINTER(DtEpisodeState), vp]),
-            'dt_refresh_copy': (ctypes.c_int, [i32, vp, i64, vp]),
-            'dt_actor_head': (ctypes.c_int, [i32, i32, i32, vp, i32, vp, vp, vp, vp, i32,
-                                             ctypes.c_float, vp, vp]),
-        }
-        for name, (res, args) in sig.items():
-            if not hasattr(L, name):
-                if name in _OPTIONAL:
-                    continue
-                raise DtError('libdtsim.so lacks %s (stale build?)' % name)
-            f = getattr(L, name)
-            f.restype = res
-            f.argtypes = args
+        L = bind(ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL))
         v = L.dt_abi_version()
         if v != ABI_VERSION:
             raise DtError('libdtsim ABI %d != expected %d (rebuild)' % (v, ABI_VERSION))

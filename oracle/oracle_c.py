@@ -16,7 +16,9 @@ import numpy as np
 from oracle import dtsim_ref as R
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-SO = os.path.join(HERE, '_build', 'liboracle.so')
+# DTSIM_ORACLE_LIB: another build of the same sources, loaded as is (the
+# sanitizer build of `make asan`, tests/test_asan.py)
+SO = os.environ.get('DTSIM_ORACLE_LIB') or os.path.join(HERE, '_build', 'liboracle.so')
 
 
 def build():
