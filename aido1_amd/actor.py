@@ -946,6 +946,18 @@ def flops_per_sample():
     return f + 2 * FLAT * 512 + 2 * 512 * 2
 
 
+def x3_bytes_per_sample(frame_bytes=1):
+    """HBM bytes one sample moves through the float32-accurate chain
+    (dt_conv1x_split, dt_conv32x_split x3, the first linear): the three
+    stacked frames read (palette index: 1 B a pixel), each layer's HL
+    activations (4 B an element) written once and read once, the f32
+    flattened conv4 output written and read by lin1.  Weights and
+    statistics are per launch, not per sample, and left out."""
+    frames = 3 * 120 * 160 * frame_bytes
+    hl = sum(h * w * 32 * 4 for h, w in ((57, 77), (27, 37), (12, 17)))
+    return frames + 2 * hl + 2 * FLAT * 4
+
+
 def clone_eval(actor):
     a = copy.deepcopy(actor)
     a.eval()

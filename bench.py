@@ -14,20 +14,25 @@ repeat_actions (3) Simulator steps each, plus the render of the pose it ends
 in; the unit counted is the Simulator step (env-step), read back exactly from
 the device counters.
 
-Timed region: per decision, dt_step on the step stream, a dt_copy_pose
-snapshot of the poses, and dt_render of that snapshot on a second stream, so
-the step of decision d + 1 runs beside the render of decision d (the render of
-d reads only d's snapshot and d's done flags; the snapshot buffer of d is
-reused by d + 2 only after render d finished).  After it, outside the timed
-region:
+Timed region (default --obs-mode many): the actions are i.i.d. and resident,
+so the K decisions are stepped in chunks of up to --many (20) decisions, one
+dt_step_many launch a chunk writing every decision's end pose, then the
+chunk's renders --render-group (3) consecutive decisions a launch (dt_render3,
+a trailing pair by dt_render2), each decision rendered from its own pose with
+its own done flags, its frame into the ring and its masks into its own buffer;
+one stream, every foreign call bound before the region (ObsLoop).  The other
+modes ('serial', 'pipe': dt_step + dt_copy_pose + dt_render of the snapshot
+on a second stream, the form an actor-in-the-loop consumer uses; 'many2')
+compute the same outputs.  After it, outside the timed region:
   * parity: the C oracle (oracle/dtsim_oracle.c, test infrastructure) re-runs
     every env of this rank from the saved start state through the same actions;
     reward/reward_mod/obs/done of every decision and the end pose/counters are
     compared with the timed launches' outputs, and a second GPU pass (dt_step,
-    tile index asked for) checks tile indices; 64 envs' whole frame stacks
-    (the last three decisions' frames, as the ring holds them) and masks are
-    compared bit for bit with oracle/render_oracle.c renders of the oracle's
-    poses;
+    tile index asked for) checks tile indices; 256 envs' masks of EVERY timed
+    decision and their final frame stacks (the last three decisions' frames,
+    as the ring holds them) are compared bit for bit with
+    oracle/render_oracle.c renders of the oracle's poses (a process pool on
+    the host);
   * roofline: render_kernel's algorithmic bytes (grey + masks + pose, plus the
     ring refill of respawned envs) / its mean duration from HIP events on the
     render stream;
@@ -66,6 +71,9 @@ HBM_PEAK_GBS = 8000.0   # MI355X_MICROARCH.md chip table: HBM3E 8.0 TB/s spec
 FP64_VECTOR_PEAK_TFLOPS = 78.6   # MI355X spec: fp64 vector = 1/2 of fp32 vector 157.3 TF
 BF16_DENSE_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: ~2.5 PF dense bf16/fp16 MFMA (spec)
 F32_MFMA_PEAK_TFLOPS = 157.3     # MI355X spec: f32 matrix (MFMA) dense
+# the float32-accurate actor (include/dtactor.h dt_conv1x_split): three fp16
+# MFMA products per f32 product, so its arithmetic ceiling is the fp16 peak / 3
+X3_PEAK_TFLOPS = BF16_DENSE_PEAK_TFLOPS / 3.0
 
 # algorithmic HBM bytes per env-step of config 2 = action 8 +
 # state read 28 + state write 28 + reward 4 + done 1 + dist/angle 8 + tile 4.
@@ -122,6 +130,9 @@ def parse(argv=None):
     p.add_argument('--no-lane', action='store_true', help='render: skip the config-2 sub-record')
     p.add_argument('--no-sub', action='store_true',
                    help='render: skip the config-4 / config-5 sub-records')
+    p.add_argument('--f64-envs', type=int, default=1024,
+                   help='configs 4 / 5: envs whose actions are checked against the float64 '
+                        'actor (actor_f64 on the GPU)')
     p.add_argument('--sub-steps', type=int, default=20,
                    help='timed decisions of the config-4 / config-5 sub-records')
     p.add_argument('--sub-warmup', type=int, default=5)
@@ -598,8 +609,15 @@ class ObsLoop:
                the snapshot on another: step d + 1 beside render d.
     Every mode computes the same frames, masks and step outputs."""
 
-    def __init__(self, env, ro, torch, mode='many', chunk=20, event_stride=1, group=3):
+    def __init__(self, env, ro, torch, mode='many', chunk=20, event_stride=1, group=3,
+                 keep_masks=0):
         self.env, self.ro, self.torch, self.mode = env, ro, torch, mode
+        # keep_masks = K: a bind of <= K decisions writes decision d's masks
+        # into dmasks[d] (its own buffer, kept for the post-run check of every
+        # decision) instead of the buffers a render group reuses
+        self.dmasks = torch.empty((keep_masks,) + tuple(ro.masks.shape), dtype=torch.uint8,
+                                  device=env.device) if keep_masks and ro.masks is not None \
+            else None
         # 'many' / 'many2': up to `group` (<= 3, the ring's slots) consecutive
         # decisions' renders a launch (dt_render2 / dt_render3, one drain for
         # the group), each decision's masks in its own buffer
@@ -629,10 +647,19 @@ class ObsLoop:
         """The foreign calls of len(actions) decisions writing `out` (a
         StepOutput of k * n entries), built and checked before the timed region
         (the ring slots are taken here, in decision order)."""
-        from aido1_amd.render import bind_render, bind_render_group
         env, n, k = self.env, self.env.n, int(actions.shape[0])
         groups = []
         self.launches = []
+        keep = self.dmasks is not None and k <= self.dmasks.shape[0]
+        self.kept = keep
+        own = self.ro.masks
+        try:
+            return self._bind(actions, out, env, n, k, groups, keep)
+        finally:
+            self.ro.masks = own
+
+    def _bind(self, actions, out, env, n, k, groups, keep):
+        from aido1_amd.render import bind_render, bind_render_group
         if self.mode in ('many', 'many2'):
             for c, (a, b) in enumerate(_bounds(split_even(k, self.chunk))):
                 # many2: chunk c's poses in half c % 2 (its renders overlap step c + 1)
@@ -645,11 +672,14 @@ class ObsLoop:
                 while d < b:
                     gk = min(self.group, b - d)
                     fr = [out.done[e * n:(e + 1) * n] for e in range(d, d + gk)]
+                    extra = self.extra[:gk - 1]
+                    if keep:   # the io structs take the buffers' addresses at bind time
+                        self.ro.masks = self.dmasks[d]
+                        extra = [self.dmasks[e] for e in range(d + 1, d + gk)]
                     if gk > 1:
-                        rend.append(bind_render_group(env, self.ro, self.s_rend,
-                                                      self.extra[:gk - 1], fr,
+                        rend.append(bind_render_group(env, self.ro, self.s_rend, extra, fr,
                                                       [pose[e - a] for e in range(d, d + gk)]))
-                        self.last_masks = self.extra[gk - 2]
+                        self.last_masks = extra[gk - 2]
                     else:
                         rend.append(bind_render(env, self.ro, self.s_rend, fresh=fr[0],
                                                 pose=pose[d - a]))
@@ -663,6 +693,8 @@ class ObsLoop:
             self.launches.append((d,))
             o = _Slice(out, d, d + 1, n)
             pose = None if serial else self.pose[d % 2]
+            if keep:
+                self.ro.masks = self.last_masks = self.dmasks[d]
             groups.append((d, env.bind_step(actions[d], o, self.s_step),
                            None if serial else env.bind_copy_pose(pose, self.s_step),
                            [bind_render(env, self.ro, self.s_rend, fresh=o.done, pose=pose)]))
@@ -717,7 +749,8 @@ def bench_obs(args, ctx):
     actions = torch.rand(W + K, n, 2, generator=g, device=dev, dtype=torch.float32)
     ro = RenderOutput(n, dev)          # 3-slot grey ring (Transformer stack) + 4 masks
     loop = ObsLoop(env, ro, torch, args.obs_mode, args.many, args.event_stride,
-                   group=1 if args.no_pair else args.render_group)
+                   group=1 if args.no_pair else args.render_group,
+                   keep_masks=0 if args.no_parity else K)
     env.reset()
     wout = StepOutput(max(W, 1) * n, dev, lanepos=False, tile=False)
     if W and loop.run(loop.bind(actions[:W], wout), loop.events(W)):
@@ -748,10 +781,11 @@ def bench_obs(args, ctx):
 
     parity = None
     if not args.no_parity:
-        # the last decision's masks: its own buffer when it closed a render pair
+        # every timed decision's masks (each its own buffer), or the last one's
         import types
         frames = types.SimpleNamespace(slots=ro.slots, stack_view=ro.stack_view,
-                                       masks=loop.last_masks)
+                                       masks=loop.last_masks,
+                                       dmasks=loop.dmasks if loop.kept else None)
         parity = step_parity(env, start, actions[W:], out, rank, args, frames=frames)
     parity = worst_over_ranks(ctx, parity, STEP_PARITY_KEYS + ['gray_mismatches',
                                                                'mask_mismatches'])
@@ -794,7 +828,7 @@ def bench_obs(args, ctx):
     lane = None if args.no_lane else lane_record(args, ctx, args.lane_steps, args.lane_warmup,
                                                  cpu=True)
     # configs 4 and 5 as sub-records of the same line (not the headline)
-    c4 = c4f = c5 = None
+    c4 = c4f = c5 = c5f = None
     if not args.no_sub:
         c4 = actor_record(args, ctx, args.sub_steps, args.sub_warmup, parity=not args.no_parity,
                           cpu=True)
@@ -802,6 +836,8 @@ def bench_obs(args, ctx):
                            parity=not args.no_parity, dtype=torch.float32)
         c5 = train_record(args, ctx, args.sub_steps, args.sub_warmup, parity=not args.no_parity,
                           cpu=True)
+        c5f = train_record(args, ctx, args.sub_steps, args.sub_warmup,
+                           parity=not args.no_parity, dtype=torch.float32)
     if rank == 0:
         kms = float(np.mean(rend_all))
         fresh_per_launch = ev_st['resets'] / KE
@@ -877,6 +913,7 @@ def bench_obs(args, ctx):
             'config4': c4,
             'config4_f32': c4f,
             'config5': c5,
+            'config5_f32': c5f,
         }
         line['cpu_baseline'] = (cpu_obs_baseline(args.cpu_decisions, args.cpu_procs, args.map)
                                 if ctx.world == 1 and args.cpu_steps > 0 else None)
@@ -1022,14 +1059,47 @@ def step_bound_record(kms, dec_per_launch, n, pmc):
     return rec
 
 
-def step_parity(env, start, actions, out, rank, args, frames=None, m=64):
+def _render_items(item):
+    """Pool worker of oracle_frames: oracle/render_oracle.c renders of a chunk
+    of poses; returns each render's masks digest and the grey frames of the
+    rows flagged in `keep`."""
+    import hashlib
+    rows, x, z, a, keep = item
+    from oracle import oracle_c as OC
+    gr, masks, _ = OC.OracleRender(rows).render(x, z, a)
+    return [hashlib.blake2b(masks[i].tobytes(), digest_size=16).digest()
+            for i in range(len(x))], gr[keep]
+
+
+def oracle_frames(rows, x, z, a, keep, procs):
+    """The oracle renders of poses (x, z, a) over `procs` processes: the 4
+    masks of each as a digest, the grey frames of the rows with keep set."""
+    parts = [p for p in np.array_split(np.arange(len(x)), max(1, procs)) if len(p)]
+    items = [(rows, x[p], z[p], a[p], keep[p]) for p in parts]
+    res = _cpu_pool(_render_items, items, len(items)) if len(items) > 1 else \
+        [_render_items(items[0])]
+    return [d for r in res for d in r[0]], np.concatenate([r[1] for r in res])
+
+
+def mask_digests(masks):
+    """Digests of [m, 4, H, W] u8 masks (as _render_items computes them)."""
+    import hashlib
+    a = masks.cpu().numpy()
+    return [hashlib.blake2b(a[i].tobytes(), digest_size=16).digest() for i in range(len(a))]
+
+
+def step_parity(env, start, actions, out, rank, args, frames=None, m=256):
     """Every env of this rank re-run by the C oracle (test infrastructure, used
     here as the checker only) from `start` through the timed decisions'
     actions, compared with the timed launches' outputs; then a dt_step check
     pass from the same start state with tile indices asked for.  With `frames`
     (the RenderOutput of the timed decisions), m envs' frame stacks (oldest
-    first, as the Transformer concatenates them) and masks are compared with
-    oracle/render_oracle.c renders of the oracle's poses."""
+    first, as the Transformer concatenates them) are compared with
+    oracle/render_oracle.c renders of the oracle's poses, and their masks: of
+    EVERY timed decision when frames.dmasks holds each decision's masks (the
+    launch form of the timed region, render groups included), else of the
+    last one.  The oracle renders run on the host's CPU share (a process
+    pool)."""
     import torch
     from aido1_amd.vec_env import StepOutput
     from oracle import oracle_c as OC
@@ -1053,9 +1123,10 @@ def step_parity(env, start, actions, out, rank, args, frames=None, m=64):
         for k in err:
             err[k] = max(err[k], float(np.max(np.abs(g[k][d] - r[k]))))
         done_mm += int(np.count_nonzero(g['done'][d] != r['done']))
-        if frames is not None and d >= K - frames.slots:
+        every = frames is not None and getattr(frames, 'dmasks', None) is not None
+        if frames is not None and (every or d >= K - frames.slots):
             o = ob.state()
-            track.append((o['x'][idx].copy(), o['z'][idx].copy(), o['angle'][idx].copy(),
+            track.append((d, o['x'][idx].copy(), o['z'][idx].copy(), o['angle'][idx].copy(),
                           r['done'][idx].copy()))
     o = ob.state()
     pose_err = max(float(np.max(np.abs(end[k] - o[k]))) for k in ('x', 'z', 'angle'))
@@ -1063,25 +1134,38 @@ def step_parity(env, start, actions, out, rank, args, frames=None, m=64):
                  for k in ('step_count', 'env_step', 'episode'))
     rec = {'envs_checked': n, 'decisions': K, 'oracle': 'oracle/dtsim_oracle.c (C restatement)'}
     if frames is not None:
+        # the oracle renders of the tracked decisions' poses: every decision's
+        # masks (digests), the grey frames of the last `slots` decisions
+        tail = [t for t in track if t[0] >= K - frames.slots]
+        cat = lambda i: np.concatenate([t[i] for t in track])   # noqa: E731
+        keep_rows = np.concatenate([np.full(m, t[0] >= K - frames.slots) for t in track])
+        procs = _cpu_info(getattr(args, 'cpu_procs', 0))[0]
+        dig, grey = oracle_frames(rows, cat(1), cat(2), cat(3), keep_rows, procs)
+        grey = grey.reshape(len(tail), m, *grey.shape[1:])
         # the ring as the Transformer holds it after the last decisions: a
         # respawn refills every slot with its frame, otherwise append + drop
-        R = OC.OracleRender(rows)
         stack = None
-        masks = None
-        for x, z, a, dn in track:
-            gr, masks, _ = R.render(x, z, a)
+        for t, gr in zip(tail, grey):
+            dn = t[4]
             if stack is None:
                 stack = np.repeat(gr[:, None], frames.slots, 1)
             else:
                 stack = np.where(dn[:, None, None, None] != 0, gr[:, None],
                                  np.concatenate([stack[:, 1:], gr[:, None]], 1))
         got = frames.stack_view()[idx.tolist()].cpu().numpy()
-        keep = frames.slots - len(track) if len(track) < frames.slots else 0
+        keep = frames.slots - len(tail) if len(tail) < frames.slots else 0
+        sel = torch.as_tensor(idx, device=env.device)
+        if every:
+            mine = [h for d in range(K) for h in mask_digests(frames.dmasks[d].index_select(0, sel))]
+        else:
+            mine = mask_digests(frames.masks.index_select(0, sel))
+            dig = dig[-m:]
         rec.update({'frame_envs_checked': m, 'frame_oracle': 'oracle/render_oracle.c',
                     'frames_per_env': frames.slots - keep,
+                    'mask_decisions_checked': K if every else 1,
                     'gray_mismatches': int(np.count_nonzero(got[:, keep:] != stack[:, keep:])),
-                    'mask_mismatches': int(np.count_nonzero(
-                        frames.masks[idx.tolist()].cpu().numpy() != masks))})
+                    'mask_mismatches': int(sum(a != b for a, b in zip(mine, dig))),
+                    'mask_mismatches_unit': '(decision, env) pairs whose 4 masks differ'})
     # check pass: dt_step from the same start, tile + lane pose produced
     env.set_state(**start)
     full = StepOutput(n, env.device)
@@ -1154,7 +1238,7 @@ def actor_record(args, ctx, K, W, parity=True, dtype=None, cpu=False):
     precision).  parity: every env's actions against the other-precision GPU
     path, and 64 envs' against a float64 host forward (actor_f64), dropout off."""
     torch = ctx.torch
-    from aido1_amd.actor import FusedActor, flops_per_sample
+    from aido1_amd.actor import FusedActor
     from aido1_amd.rollout import ActorRollout
     cfg = _reference_config()
     dtype = dtype or torch.float16
@@ -1191,15 +1275,16 @@ def actor_record(args, ctx, K, W, parity=True, dtype=None, cpu=False):
             alt.p_drop = 0.0
             got = roll.actor(roll.ring, roll.order()).float()
             want = alt(roll.ring, roll.order()).float()
-            m = 64
-            ref64 = actor_f64(roll.actor_src, roll.stack()[:m], roll.actor.mode)
+            m = min(n, args.f64_envs)
+            ref64 = actor_f64(roll.actor_src, roll.stack()[:m], roll.actor.mode, device=dev)
         roll.actor.p_drop = drop
         d = torch.abs(got - want)
         e64 = (got[:m].double().cpu() - ref64).abs()
         a64 = (want[:m].double().cpu() - ref64).abs()
         tol = FP16_ACTION_TOL if dtype == torch.float16 else F32_ACTION_TOL
-        par = {'vs': 'float64 host forward (actor_f64, same weights, live frames, dropout off) '
-                     'on %d envs; and the %s GPU path on every env' % (m, other),
+        par = {'vs': 'float64 forward (actor_f64 on the GPU\'s f64 units, same weights, live '
+                     'frames, dropout off) on %d envs; and the %s GPU path on every env'
+                     % (m, other),
                'tolerance_vs_f64': tol, 'envs_checked': n, 'envs_checked_f64': m,
                'max_abs_err_vs_f64': e64.max().item(),
                'other_path_max_abs_err_vs_f64': a64.max().item(),
@@ -1214,9 +1299,8 @@ def actor_record(args, ctx, K, W, parity=True, dtype=None, cpu=False):
         base = cpu_actor_baseline(args.cpu_actor_decisions, args.cpu_procs)
     if rank != 0:
         return None
-    tflops = n * flops_per_sample() / (actor_ms * 1e-3) / 1e12
     name = str(dtype).replace('torch.', '')
-    peak = BF16_DENSE_PEAK_TFLOPS if dtype == torch.float16 else F32_MFMA_PEAK_TFLOPS
+    frame_b = 1 if args.frames == 'index' else 4
     return {
         'metric': METRIC, 'value': tot[0] / tmax, 'unit': 'env-steps/s',
         'n_gpus': ctx.world, 'steps': K, 'warmup': W,
@@ -1237,16 +1321,42 @@ def actor_record(args, ctx, K, W, parity=True, dtype=None, cpu=False):
                    'elapsed_s': tmax},
         'per_rank': per,
         'parity': par,
-        'roofline': {'bound': 'mfma', 'kernel': ('actor forward (fp16 MFMA convs + linears)'
-                                                 if dtype == torch.float16 else
-                                                 'actor forward (f32: MIOpen convs, '
-                                                 'dt_sample_norm, linears)'),
-                     'achieved': tflops, 'peak': peak, 'unit': 'TFLOP/s',
-                     'frac': tflops / peak, 'traffic': None,
-                     'avg_kernel_ms': actor_ms,
-                     'timing': 'HIP events around the actor forward of every timed decision',
-                     'algorithmic_flops_per_launch': n * flops_per_sample()},
+        'roofline': actor_roofline(torch, dtype, n, actor_ms, frame_b),
         'cpu_baseline': base}
+
+
+def actor_roofline(torch, dtype, n, actor_ms, frame_b):
+    """The roofline object of the actor forward (configs 4 / 5).  fp16 fast
+    mode: MFMA-bound against the fp16 dense peak.  float32 (the x3 chain,
+    include/dtactor.h): its HBM bytes (actor.x3_bytes_per_sample: the HL
+    activations written and read) bound it before its arithmetic (three fp16
+    MFMA products per f32 product: a ceiling of the fp16 peak / 3), so the
+    bound is HBM, the MFMA figures beside it."""
+    from aido1_amd.actor import flops_per_sample, x3_bytes_per_sample
+    flops = n * flops_per_sample()
+    tflops = flops / (actor_ms * 1e-3) / 1e12
+    common = {'avg_kernel_ms': actor_ms, 'traffic': None,
+              'timing': 'HIP events around the actor forward of every timed decision',
+              'algorithmic_flops_per_launch': flops}
+    if dtype == torch.float16:
+        return dict(common, bound='mfma', kernel='actor forward (fp16 MFMA convs + linears)',
+                    achieved=tflops, peak=BF16_DENSE_PEAK_TFLOPS, unit='TFLOP/s',
+                    frac=tflops / BF16_DENSE_PEAK_TFLOPS)
+    nbytes = n * x3_bytes_per_sample(frame_b)
+    gbs = nbytes / (actor_ms * 1e-3) / 1e9
+    return dict(common, bound='hbm',
+                kernel='actor forward at float32 accuracy (dt_conv1x_split + dt_conv32x_split '
+                       'x3 on fp16 MFMA, float32 linears)',
+                achieved=gbs, peak=HBM_PEAK_GBS, unit='GB/s', frac=gbs / HBM_PEAK_GBS,
+                algorithmic_bytes_per_launch=nbytes,
+                algorithmic_basis='per sample: the 3 stacked frames read, each HL activation '
+                                  '(conv1..conv3 outputs, 4 B an element) written and read, '
+                                  'the f32 flattened conv4 output written and read',
+                mfma={'achieved': tflops, 'unit': 'TFLOP/s', 'peak_x3': X3_PEAK_TFLOPS,
+                      'frac_x3': tflops / X3_PEAK_TFLOPS,
+                      'f32_mfma_peak': F32_MFMA_PEAK_TFLOPS,
+                      'note': 'algorithmic f32 FLOP; x3 runs three fp16 MFMA products per '
+                              'f32 product'})
 
 
 def bench_actor(args, ctx):
@@ -1259,7 +1369,7 @@ def bench_actor(args, ctx):
     ctx.close()
 
 
-def train_record(args, ctx, K, W, parity=True, cpu=False):
+def train_record(args, ctx, K, W, parity=True, cpu=False, dtype=None):
     """BASELINE configs[4]: full DDPG on every GPU -- actor-in-loop rollout of
     4096 envs, GPU prioritized replay, one update per decision
     (training/trainers.py:143-237), gradients all-reduced over RCCL (world >
@@ -1267,15 +1377,15 @@ def train_record(args, ctx, K, W, parity=True, cpu=False):
     of every stage (TrainLoop.check), the replay's rejected priorities and the
     sum tree's invariants after the timed run."""
     torch = ctx.torch
-    from aido1_amd.actor import flops_per_sample
     from aido1_amd.train_loop import TrainLoop
     cfg = _reference_config()
     dev, rank, n = ctx.dev, ctx.rank, args.envs
+    if dtype is None:
+        dtype = torch.float32 if args.actor_dtype == 'float32' else torch.float16
     loop = TrainLoop(cfg, n, device=dev.index, seed=args.seed, env_id_base=rank * n,
                      buffer_size=args.buffer_size, batch_size=args.batch_size or None,
                      updates_per_step=args.updates_per_step, actor_mode=args.actor_mode,
-                     overlap=args.overlap, frames=args.frames,
-                     actor_dtype=torch.float32 if args.actor_dtype == 'float32' else torch.float16)
+                     overlap=args.overlap, frames=args.frames, actor_dtype=dtype)
     loop.reset()
     for _ in range(max(W, 2)):
         loop.step()
@@ -1336,7 +1446,7 @@ def train_record(args, ctx, K, W, parity=True, cpu=False):
                          par.get('tree_root_vs_leaf_sum_rel', 0.0) <= 1e-9)
     nparams = sum(p.numel() for p in loop.trainer.actor.parameters()) + \
         sum(p.numel() for p in loop.trainer.critic.parameters())
-    dtype = str(loop.rollout.actor.dtype).replace('torch.', '')
+    dtype_name = str(loop.rollout.actor.dtype).replace('torch.', '')
     batch = loop.batch_size
     loop.rollout.close()
     base = None
@@ -1345,13 +1455,16 @@ def train_record(args, ctx, K, W, parity=True, cpu=False):
                                   updates=args.cpu_updates)
     if rank != 0:
         return None
-    tflops = n * flops_per_sample() / (actor_ms * 1e-3) / 1e12
     return {
         'metric': METRIC, 'value': sim_steps / tmax, 'unit': 'env-steps/s',
         'n_gpus': ctx.world, 'steps': K, 'warmup': W,
         'ms_per_step': tmax / K * 1e3,
         'higher_is_better': True, 'scaling': 'weak', 'vs_baseline': None,
-        'dtype': 'f64 env / %s actor / f32 update' % dtype, 'data': 'synthetic',
+        'dtype': 'f64 env / %s actor / f32 update' % dtype_name,
+        'precision': ('fast mode: fp16 MFMA actor operands (narrower than the reference\'s '
+                      'float32)' if dtype == torch.float16 else
+                      'the reference\'s float32 acting (models/ddpg/model.py:74-88)'),
+        'data': 'synthetic',
         'config': {'workload': 'config5: %d envs/GPU full DDPG (rollout + GPU prioritized '
                                'replay + update + grad all-reduce)' % n,
                    'actor_mode': args.actor_mode, 'frames': args.frames, 'envs_per_gpu': n,
@@ -1375,12 +1488,8 @@ def train_record(args, ctx, K, W, parity=True, cpu=False):
                                 'update(s) of every timed decision (rank 0)'},
         'per_rank': per,
         'parity': par,
-        'roofline': {'bound': 'mfma', 'kernel': 'actor forward (fp16 MFMA convs + linears)',
-                     'achieved': tflops, 'peak': BF16_DENSE_PEAK_TFLOPS, 'unit': 'TFLOP/s',
-                     'frac': tflops / BF16_DENSE_PEAK_TFLOPS, 'traffic': None,
-                     'avg_kernel_ms': actor_ms,
-                     'timing': 'HIP events around the actor forward of every timed decision',
-                     'algorithmic_flops_per_launch': n * flops_per_sample()},
+        'roofline': actor_roofline(torch, dtype, n, actor_ms,
+                                   1 if args.frames == 'index' else 4),
         'cpu_baseline': base}
 
 
