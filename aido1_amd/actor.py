@@ -646,16 +646,16 @@ class FusedActor(nn.Module):
                 self.w[0].shape == (32, 3, 8, 8))
 
     def _x3_buffers(self, n, dev):
-        """The HL activations ((hi, lo) fp16 pairs, include/dtactor.h) of
+        """The HLB activations ((hi, lo) fp16 pairs, include/dtactor.h) of
         conv1..conv3, their per-sample statistics [n, 32, 3] and the f32
         flattened conv4 output."""
         key = (n, dev)
         if getattr(self, '_xbufs_key', None) != key:
             f16 = torch.float16
-            self._xbufs = {
-                'y1': torch.empty(n, 57, 77, 64, dtype=f16, device=dev),
-                'y2': torch.empty(n, 27, 37, 64, dtype=f16, device=dev),
-                'y3': torch.empty(n, 12, 17, 64, dtype=f16, device=dev),
+            self._xbufs = {   # each in the layout its consumer reads (stride 2, 2, 1)
+                'y1': torch.empty(hlb_shape(n, 57, 77, 2), dtype=f16, device=dev),
+                'y2': torch.empty(hlb_shape(n, 27, 37, 2), dtype=f16, device=dev),
+                'y3': torch.empty(hlb_shape(n, 12, 17, 1), dtype=f16, device=dev),
                 'p1': torch.empty(n, 32, 3, device=dev),
                 'p2': torch.empty(n, 32, 3, device=dev),
                 'p3': torch.empty(n, 32, 3, device=dev),
@@ -893,6 +893,38 @@ def split_hl(t):
     include/dtactor.h's dt_conv1x_split)."""
     hi = t.half()
     return torch.stack([hi, ((t - hi.float()) * 2048.0).half()])
+
+
+def hlb_geometry(w, stride):
+    """The HLB layout of a w-wide image read at `stride` by its consumer
+    (include/dtactor.h): the chunks a segment holds, and pixel x's chunk."""
+    half = (w + 1) // 2
+    if stride == 2:
+        return 2 * half, [(half + x // 2) if x % 2 else x // 2 for x in range(w)]
+    return w, list(range(w))
+
+
+def hlb_shape(n, h, w, stride):
+    """fp16 shape of n HLB images: [n, h, 4 blocks, {hi, lo}, chunks, 8]."""
+    return (n, h, 4, 2, hlb_geometry(w, stride)[0], 8)
+
+
+def hlb_decode(y, h, w, stride):
+    """n HLB images -> float64 [n, h, w, 32]: hi + 2^-11 lo (test helper)."""
+    segpx, pos = hlb_geometry(w, stride)
+    t = y.reshape(-1, h, 4, 2, segpx, 8)[:, :, :, :, pos, :]
+    v = t[:, :, :, 0].double() + t[:, :, :, 1].double() / 2048.0     # [n, h, 4, w, 8]
+    return v.permute(0, 1, 3, 2, 4).reshape(-1, h, w, 32)
+
+
+def hlb_encode(x, stride):
+    """float32 [n, h, w, 32] -> its HLB images (test helper)."""
+    n, h, w, _ = x.shape
+    segpx, pos = hlb_geometry(w, stride)
+    out = torch.zeros(hlb_shape(n, h, w, stride), dtype=torch.float16, device=x.device)
+    out[:, :, :, :, pos, :] = split_hl(x.float()).reshape(2, n, h, w, 4, 8).permute(
+        1, 2, 4, 0, 3, 5)
+    return out
 
 
 def conv1_fragments(w, dtype=torch.float16):

@@ -14,9 +14,14 @@
 // sums: the same accuracy class as the reference's float32 convolutions, at
 // 3/16 of the MFMA cycles an f32-input MFMA (v_mfma_f32_32x32x2_f32) needs.
 //
-// Activations between the layers are stored as such pairs ("HL" layout: a
-// pixel is 32 hi then 32 lo fp16 values, 128 B, the bytes of f32), centred on
-// the sample's pixel 0 as in the fp16 chain (dtconv_common.h centre_px32).
+// Activations between the layers are stored as such pairs in the "HLB"
+// layout (struct Hlb below: per image row, 4 blocks of 8 channels x {hi, lo}
+// segments, each segment the row's pixels as 16-B chunks in the CONSUMER's
+// read order -- even then odd columns for a stride-2 consumer), 4 B an
+// element like f32, centred on the sample's pixel 0 as in the fp16 chain
+// (dtconv_common.h centre_px32).  A consumer's B-operand load is then 32
+// lanes reading 512 contiguous bytes, not 32 pixels 256 B apart: the L1 tag
+// lookups a load costs fell 4x (measured on the pixel-major form first).
 //
 // conv1x_kernel: conv1s_kernel's row stream (dtconv.hip) with a hi ring and a
 //   lo ring in LDS, both weight halves in registers, three MFMAs a k step.
@@ -36,6 +41,16 @@
 #include "../../include/dtactor.h"
 #include "dtconv_common.h"
 #include "dtrender.h"   // dr::kPalGray: the grey levels of palette-index frames
+
+// conv2 / conv3 workgroup shape: waves a workgroup (4: two workgroups a CU;
+// 8: one) and units of B-operand loads in flight a wave (1: two waves a
+// SIMD; 3: one wave a SIMD, 512 registers)
+#ifndef DTCONVX_NW
+#define DTCONVX_NW 4
+#endif
+#ifndef DTCONVX_DEPTH
+#define DTCONVX_DEPTH 1
+#endif
 
 namespace {
 
@@ -58,26 +73,53 @@ __device__ __forceinline__ uint32_t hi_pair(uint32_t a, uint32_t b) {
 __device__ __forceinline__ uint32_t lo_pair(uint32_t a, uint32_t b) {
   return (a >> 16) | (b & 0xffff0000u);
 }
+// (a, b) -> the fp16 pairs (hi(a), hi(b)) and (lo(a), lo(b)): packed
+// conversions (v_cvt_pk_f16_f32, round to nearest even), 3 VALU a value
+using f32x2 = __attribute__((ext_vector_type(2))) float;
+using f16x2 = __attribute__((ext_vector_type(2))) _Float16;
+__device__ __forceinline__ void split2(float a, float b, uint32_t& hi, uint32_t& lo) {
+  const f32x2 x = {a, b};
+  const f16x2 h = __builtin_convertvector(x, f16x2);
+  const f32x2 r = (x - __builtin_convertvector(h, f32x2)) * kLo;
+  hi = __builtin_bit_cast(uint32_t, h);
+  lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, f16x2));
+}
 
-// One pixel's 32 channels in the HL layout from a 32x32 MFMA tile (lane =
-// pixel column, register r = channel (r&3) + 8*(r>>2) + 4h): as store_px32
-// (dtconv.hip), v_permlane32_swap pairs the two half-waves' 4-channel groups
-// so a lane stores 16-B chunks, two of hi (byte 32m + 16h) and two of lo
-// (64 + 32m + 16h).  Branch-free: an invalid lane's offset lies past the
-// sample and the buffer store is dropped.
-template <int kPix>
-__device__ __forceinline__ void store_hl32(unsigned char* sample, int px, const float (&v)[16],
-                                           int h, bool valid) {
-  constexpr int kBytes = kPix * 128;
+// The HLB layout of a W-wide image whose consumer reads it at stride S: a
+// row is 4 channel blocks x {hi, lo} segments of kSegPx 16-B chunks (8
+// channels' fp16 values); pixel x sits at chunk pos(x) of each segment, the
+// even columns first, then the odd ones, when S = 2.  Row y, block cb, half
+// hl (0 hi, 1 lo), pixel x: byte off(y, cb, hl, x).
+template <int W_, int S>
+struct Hlb {
+  static constexpr int kHalf = (W_ + 1) / 2;
+  static constexpr int kSegPx = S == 2 ? 2 * kHalf : W_;
+  static constexpr int kSeg = kSegPx * 16;
+  static constexpr int kRow = 8 * kSeg;
+  __host__ __device__ static constexpr int pos(int x) {
+    return S == 2 ? ((x & 1) ? kHalf + (x >> 1) : (x >> 1)) : x;
+  }
+  __host__ __device__ static constexpr int off(int y, int cb, int hl, int x) {
+    return y * kRow + (2 * cb + hl) * kSeg + 16 * pos(x);
+  }
+};
+
+// One output pixel's 32 channels into an HLB image (OW_ wide, its consumer's
+// stride SN) from a 32x32 MFMA tile (lane = pixel column, register r =
+// channel (r&3) + 8*(r>>2) + 4h): v_permlane32_swap pairs the two half-waves'
+// 4-channel groups, so a lane holds channels 16m + 8h .. +7 = block 2m + h
+// and stores it as one 16-B chunk of hi and one of lo.  Branch-free: an
+// invalid lane's offset lies past the sample and the buffer store is dropped.
+template <int OH_, int OW_, int SN>
+__device__ __forceinline__ void store_hlb(unsigned char* sample, int oy, int ox,
+                                          const float (&v)[16], int h, bool valid) {
+  using L = Hlb<OW_, SN>;
+  constexpr int kBytes = OH_ * L::kRow;
   uint32_t uh[4][2], ul[4][2];
 #pragma unroll
   for (int q = 0; q < 4; ++q)
 #pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      const uint32_t a = hl16(v[4 * q + 2 * e]), b = hl16(v[4 * q + 2 * e + 1]);
-      uh[q][e] = hi_pair(a, b);
-      ul[q][e] = lo_pair(a, b);
-    }
+    for (int e = 0; e < 2; ++e) split2(v[4 * q + 2 * e], v[4 * q + 2 * e + 1], uh[q][e], ul[q][e]);
 #pragma unroll
   for (int m = 0; m < 2; ++m)
 #pragma unroll
@@ -90,13 +132,13 @@ __device__ __forceinline__ void store_hl32(unsigned char* sample, int px, const 
       ul[2 * m + 1][e] = r[1];
     }
   const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(sample, 0, kBytes, 0x00020000);
-  const int off = valid ? px * 128 + 16 * h : kBytes;
+  const int base = valid ? L::off(oy, h, 0, ox) : kBytes;
 #pragma unroll
-  for (int m = 0; m < 2; ++m) {
+  for (int m = 0; m < 2; ++m) {   // block 2m + h: base + 2m segments-pairs on
     const u32x4 dh = {uh[2 * m][0], uh[2 * m][1], uh[2 * m + 1][0], uh[2 * m + 1][1]};
     const u32x4 dl = {ul[2 * m][0], ul[2 * m][1], ul[2 * m + 1][0], ul[2 * m + 1][1]};
-    __builtin_amdgcn_raw_buffer_store_b128(dh, rsrc, off + 32 * m, 0, 0);
-    __builtin_amdgcn_raw_buffer_store_b128(dl, rsrc, off + 64 + 32 * m, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(dh, rsrc, base + 4 * m * L::kSeg, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(dl, rsrc, base + (4 * m + 1) * L::kSeg, 0, 0);
   }
 }
 
@@ -317,7 +359,7 @@ conv1x_kernel(int n, const void* __restrict__ ring, int slots, int s0, int s1, i
 #pragma unroll
     for (int r = 0; r < 16; ++r) v[r] = lrelu2(acc0[r] + acc1[r] * kLoInv, slope);
     centre_px32(v, s_c, j == 0 && wave == 0 && col == 0, j == 0, h);
-    store_hl32<kSPix>(y + (size_t)ns * kSPix * 128, pc, v, h, valid);
+    store_hlb<OH, OW, 2>(y + (size_t)ns * OH * Hlb<OW, 2>::kRow, oy, ox, v, h, valid);
     if (valid) {   // Welford over this lane's pixels
       w_cnt += 1.0f;
       const float inv = 1.0f / w_cnt;
@@ -362,19 +404,26 @@ conv1x_kernel(int n, const void* __restrict__ ring, int slots, int s0, int s1, i
 // row (8 steps, 24 MFMAs) of one round's tile.  kLast (conv4): the round holds
 // the whole sample; its own BatchNorm in-kernel (exact two-pass statistics),
 // written f32 flattened in NCHW order for the first linear.
-template <int IH_, int IW_, int OH_, int OW_, int ST, bool kLast>
-__global__ void __launch_bounds__(256, 2)   // 2 waves / SIMD: <= 256 registers
+template <int IH_, int IW_, int OH_, int OW_, int ST, int SN, int NW, int DEPTH, bool kLast>
+__global__ void __launch_bounds__(64 * NW, (NW == 8 || DEPTH == 1) ? 2 : 1)
 conv32x_kernel(int n, const unsigned char* __restrict__ x, const float* __restrict__ wsrc,
                const float* __restrict__ bias, const float* __restrict__ prev_part,
                const float* __restrict__ in_gamma, const float* __restrict__ in_beta,
                float in_eps, void* __restrict__ y, float* __restrict__ part,
                const float* __restrict__ out_gamma, const float* __restrict__ out_beta,
                float out_eps, float slope, WeightSplit ws) {
-  constexpr int kPix = OH_ * OW_, kTiles = (kPix + 31) / 32, kRounds = (kTiles + 3) / 4;
-  constexpr int kInBytes = IH_ * IW_ * 128;
+  constexpr int kPix = OH_ * OW_, kTiles = (kPix + 31) / 32, kRounds = (kTiles + NW - 1) / NW;
+  constexpr int kThreads = 64 * NW;
+  constexpr int kSets = DEPTH + 1;   // B-operand register sets: DEPTH units of loads in flight
+  static_assert(NW == 4 || NW == 8, "4 or 8 waves");
+  static_assert(kSets == 2 || kSets == 4, "the sets cycle within a round's 4 units");
+  static_assert(NW == 4 || DEPTH == 1, "8 waves share a SIMD by two: <= 256 registers");
+  using In = Hlb<IW_, ST>;           // the input as this layer reads it
+  constexpr int kInBytes = IH_ * In::kRow;
   static_assert(!kLast || kRounds == 1, "the in-kernel norm needs the sample in one round");
   __shared__ half8 s_wh[32 * 64], s_wl[32 * 64];   // folded weights, hi / lo fragments
-  __shared__ float s_sc[CO], s_sh[CO], s_b2[CO], s_c[CO], s_bred[8][CO], red[4][CO][3];
+  __shared__ float s_sc[CO], s_sh[CO], s_b2[CO], s_c[CO], s_bred[kThreads / 32][CO];
+  __shared__ float red[NW][CO][3];
   __shared__ float s_omean[CO], s_osc[CO], s_obeta[CO];
   __shared__ float s_wexp[2];   // 2^-e (the folded weights' scale), 2^e
   __shared__ unsigned int s_wmax;
@@ -404,8 +453,8 @@ conv32x_kernel(int n, const unsigned char* __restrict__ x, const float* __restri
     float m = 0.0f;
     const float4* w4 = reinterpret_cast<const float4*>(wsrc);
 #pragma unroll 4
-    for (int i = 0; i < 16; ++i) {
-      const float4 q = w4[tid + 256 * i];
+    for (int i = 0; i < 4096 / kThreads; ++i) {   // the 4096 float4 of the set
+      const float4 q = w4[tid + kThreads * i];
       m = fmaxf(m, fmaxf(fmaxf(fabsf(q.x), fabsf(q.y)), fmaxf(fabsf(q.z), fabsf(q.w))));
     }
 #pragma unroll
@@ -415,22 +464,26 @@ conv32x_kernel(int n, const unsigned char* __restrict__ x, const float* __restri
   __syncthreads();
 
   // a unit's B operand: 8 k steps x (hi, lo) 16-B chunks of the lane's pixel
-  // (every load issued, pixel and sample clamped: the offsets stay inside the
-  // sample and the vmcnt waits stay exact)
+  // (ST ox + kx, row ST oy + ky), block 2 hf + h: In::off, its lane part in
+  // the VGPR offset and the step's constant part in the SGPR offset.  Every
+  // load issued, pixel and sample clamped, so every offset lies inside the
+  // sample (the raw-buffer range check, which does not cover the SGPR
+  // offset, is never relied on) and the vmcnt waits stay exact.
   auto unit_load = [&](u32x4 (&bh)[8], u32x4 (&bl)[8], int k, int u) __attribute__((always_inline)) {
     const int r = u >> 2, gy = u & 3;
-    const int t = 4 * r + wave;
+    const int t = NW * r + wave;
     const int p = 32 * (t < kTiles ? t : 0) + col;
     const int pc = p < kPix ? p : 0;
     const int oy = pc / OW_, ox = pc - oy * OW_;
-    const int vb = ((ST * oy + gy) * IW_ + ST * ox) * 128 + 16 * h;
+    const int vb = In::off(ST * oy + gy, h, 0, 0) + 16 * ox;
     const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(
         const_cast<unsigned char*>(x + (size_t)sample(k) * kInBytes), 0, kInBytes, 0x00020000);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      const int off = vb + (i >> 1) * 128 + 32 * (i & 1);
-      bh[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off, 0, 0);
-      bl[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, off + 64, 0, 0);
+      const int kx = i >> 1, hf = i & 1;
+      const int c = 4 * hf * In::kSeg + 16 * (ST == 2 ? In::pos(kx) : kx);
+      bh[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, vb, c, 0);
+      bl[i] = __builtin_amdgcn_raw_buffer_load_b128(rsrc, vb, c + In::kSeg, 0);
     }
   };
 
@@ -438,17 +491,18 @@ conv32x_kernel(int n, const unsigned char* __restrict__ x, const float* __restri
 #pragma unroll
   for (int r = 0; r < 16; ++r) w_mean[r] = w_m2[r] = 0.0f;
   f32x16 acc0, acc1;
-  u32x4 ba[8], bb[8], ca[8], cb[8];   // two units' B operands: (ba, ca) and (bb, cb)
+  u32x4 bh[kSets][8], bl[kSets][8];   // the B operands of kSets units (hi, lo)
+  constexpr int kUnits = 4 * kRounds;
 
-  // one unit: issue the next unit's loads into (nh, nl), run this one's MFMAs
-  // on (bh, bl); the tile's epilogue after its last kernel row
-  auto unit = [&](int k, int u, u32x4 (&bh)[8], u32x4 (&bl)[8], u32x4 (&nh)[8],
+  // one unit: issue unit u + DEPTH's loads into its set, run this one's MFMAs
+  // on set u % kSets; the tile's epilogue after its last kernel row.  `cur`
+  // and `nxt` are compile-time set indices (the rounds are unrolled by 4).
+  auto unit = [&](int k, int u, u32x4 (&ch)[8], u32x4 (&cl)[8], u32x4 (&nh)[8],
                   u32x4 (&nl)[8]) __attribute__((always_inline)) {
-    constexpr int kUnits = 4 * kRounds;
-    const bool lastu = u + 1 == kUnits;
-    unit_load(nh, nl, lastu ? k + 1 : k, lastu ? 0 : u + 1);
+    const int un = u + DEPTH;
+    unit_load(nh, nl, un >= kUnits ? k + 1 : k, un >= kUnits ? un - kUnits : un);
     const int r = u >> 2, gy = u & 3;
-    const int t = 4 * r + wave;
+    const int t = NW * r + wave;
     if (gy == 0) {
 #pragma unroll
       for (int q = 0; q < 16; ++q) acc0[q] = acc1[q] = 0.0f;
@@ -459,7 +513,7 @@ conv32x_kernel(int n, const unsigned char* __restrict__ x, const float* __restri
       for (int i = 0; i < 8; ++i) {
         const int s = 8 * gy + i;
         const half8 ah = s_wh[s * 64 + lane], al = s_wl[s * 64 + lane];
-        const half8 xh = __builtin_bit_cast(half8, bh[i]), xl = __builtin_bit_cast(half8, bl[i]);
+        const half8 xh = __builtin_bit_cast(half8, ch[i]), xl = __builtin_bit_cast(half8, cl[i]);
         acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, xh, acc0, 0, 0, 0);
         acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, xl, acc1, 0, 0, 0);
         acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, xh, acc1, 0, 0, 0);
@@ -480,8 +534,9 @@ conv32x_kernel(int n, const unsigned char* __restrict__ x, const float* __restri
                     slope);
     if constexpr (!kLast) {
       centre_px32(v, s_c, r == 0 && wave == 0 && col == 0, r == 0, h);
-      store_hl32<kPix>(static_cast<unsigned char*>(y) + (size_t)ns * kPix * 128, valid ? p : 0, v, h,
-                       valid);
+      const int pc = valid ? p : 0, oy = pc / OW_;
+      store_hlb<OH_, OW_, SN>(static_cast<unsigned char*>(y) + (size_t)ns * OH_ * Hlb<OW_, SN>::kRow,
+                              oy, pc - oy * OW_, v, h, valid);
       if (valid) {
         w_cnt += 1.0f;
         const float inv = 1.0f / w_cnt;
@@ -493,7 +548,7 @@ conv32x_kernel(int n, const unsigned char* __restrict__ x, const float* __restri
         }
       }
       if (r + 1 == kRounds)
-        stats_flush<4>(w_cnt, w_mean, w_m2, red, s_c, part + (size_t)ns * CO * 3, tid, wave, col,
+        stats_flush<NW>(w_cnt, w_mean, w_m2, red, s_c, part + (size_t)ns * CO * 3, tid, wave, col,
                        h);
     } else {
       // exact two-pass statistics: per wave over its 32 pixels (shuffles),
@@ -529,7 +584,7 @@ conv32x_kernel(int n, const unsigned char* __restrict__ x, const float* __restri
       __syncthreads();
       if (tid < CO) {
         float cnt = 0.0f, mean = 0.0f, mm = 0.0f;
-        for (int w = 0; w < 4; ++w) {
+        for (int w = 0; w < NW; ++w) {
           const float nb = red[w][tid][0];
           if (nb <= 0.0f) continue;
           const float tot = cnt + nb, d = red[w][tid][1] - mean;
@@ -555,7 +610,8 @@ conv32x_kernel(int n, const unsigned char* __restrict__ x, const float* __restri
     }
   };
 
-  unit_load(ba, ca, 0, 0);
+#pragma unroll
+  for (int d = 0; d < DEPTH; ++d) unit_load(bh[d], bl[d], d >= kUnits ? 1 : 0, d % kUnits);
   for (int k = 0; k < sp.my; ++k) {
     const int ns = sample(k);
     // (a) the input's BatchNorm (per sample, batch of one) and the weight scale
@@ -579,14 +635,14 @@ conv32x_kernel(int n, const unsigned char* __restrict__ x, const float* __restri
     __syncthreads();
     // (b) the folded weights: A fragment (s, l) holds w[l % 32][16 (s % 2) +
     // 8 (l / 32) + j][(s / 2) / 4][(s / 2) % 4]; thread tid folds fragments
-    // tid + 256 i, all of output channel tid % 32, and sums its share of
+    // tid + kThreads i, all of output channel tid % 32, and sums its share of
     // sum_k w * sh for bias'
     {
       const float wsc = s_wexp[0];
       float bacc = 0.0f;
 #pragma unroll 2
-      for (int i = 0; i < 8; ++i) {
-        const int pidx = tid + 256 * i, s = pidx >> 6, l = pidx & 63;
+      for (int i = 0; i < 2048 / kThreads; ++i) {
+        const int pidx = tid + kThreads * i, s = pidx >> 6, l = pidx & 63;
         const float4* src = reinterpret_cast<const float4*>(wsrc) + 2 * pidx;
         const float4 q0 = src[0], q1 = src[1];
         const float wv[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
@@ -609,30 +665,30 @@ conv32x_kernel(int n, const unsigned char* __restrict__ x, const float* __restri
     if (tid < CO) {
       float b2 = bias[tid];
 #pragma unroll
-      for (int m = 0; m < 8; ++m) b2 += s_bred[m][tid];
+      for (int m = 0; m < kThreads / 32; ++m) b2 += s_bred[m][tid];
       s_b2[tid] = b2;
     }
     // (c) the rounds: units alternate between the two register sets
 #pragma unroll 1
     for (int r = 0; r < kRounds; ++r) {
-      unit(k, 4 * r + 0, ba, ca, bb, cb);
-      unit(k, 4 * r + 1, bb, cb, ba, ca);
-      unit(k, 4 * r + 2, ba, ca, bb, cb);
-      unit(k, 4 * r + 3, bb, cb, ba, ca);
+#pragma unroll
+      for (int gy = 0; gy < 4; ++gy)
+        unit(k, 4 * r + gy, bh[gy % kSets], bl[gy % kSets], bh[(gy + DEPTH) % kSets],
+             bl[(gy + DEPTH) % kSets]);
     }
   }
 }
 
-template <int IH_, int IW_, int OH_, int OW_, int ST, bool kLast>
+template <int IH_, int IW_, int OH_, int OW_, int ST, int SN, int NW, int DEPTH, bool kLast>
 int launch_conv32x(int n, const void* x, const float* w, const float* bias, const float* pp,
                    const float* ig, const float* ib, float ieps, void* y, float* part,
                    const float* og, const float* ob, float oeps, float slope, hipStream_t s,
                    WeightSplit ws, int n0) {
-  auto kern = conv32x_kernel<IH_, IW_, OH_, OW_, ST, kLast>;
+  auto kern = conv32x_kernel<IH_, IW_, OH_, OW_, ST, SN, NW, DEPTH, kLast>;
   static int grid = 0;   // resident workgroups, persistent
-  if (!grid) grid = resident_grid(kern, 256, 0);
+  if (!grid) grid = resident_grid(kern, 64 * NW, 0);
   const int g = split_grid(ws, n, n0, grid);
-  hipLaunchKernelGGL(kern, dim3(g), dim3(256), 0, s, n, (const unsigned char*)x, w, bias, pp, ig,
+  hipLaunchKernelGGL(kern, dim3(g), dim3(64 * NW), 0, s, n, (const unsigned char*)x, w, bias, pp, ig,
                      ib, ieps, y, part, og, ob, oeps, slope, ws);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
@@ -697,15 +753,15 @@ extern "C" int dt_conv32x_split(int32_t layer, int32_t n, const void* x, const f
   hipStream_t s = (hipStream_t)stream;
   switch (layer) {
     case 2:
-      return launch_conv32x<57, 77, 27, 37, 2, false>(n, x, wfrag, bias, prev_part, in_gamma,
+      return launch_conv32x<57, 77, 27, 37, 2, 2, DTCONVX_NW, DTCONVX_DEPTH, false>(n, x, wfrag, bias, prev_part, in_gamma,
                                                       in_beta, in_eps, y, part, nullptr, nullptr,
                                                       0.f, slope, s, ws, n0);
     case 3:
-      return launch_conv32x<27, 37, 12, 17, 2, false>(n, x, wfrag, bias, prev_part, in_gamma,
+      return launch_conv32x<27, 37, 12, 17, 2, 1, DTCONVX_NW, DTCONVX_DEPTH, false>(n, x, wfrag, bias, prev_part, in_gamma,
                                                       in_beta, in_eps, y, part, nullptr, nullptr,
                                                       0.f, slope, s, ws, n0);
     case 4:
-      return launch_conv32x<12, 17, 9, 14, 1, true>(n, x, wfrag, bias, prev_part, in_gamma,
+      return launch_conv32x<12, 17, 9, 14, 1, 1, 4, DTCONVX_DEPTH, true>(n, x, wfrag, bias, prev_part, in_gamma,
                                                     in_beta, in_eps, y, nullptr, out_gamma,
                                                     out_beta, out_eps, slope, s, ws, n0);
     default:

@@ -124,16 +124,20 @@ int dt_conv32_split(int32_t layer, int32_t n, const void* x, const void* wfrag,
  * BatchNorms), on fp16 MFMA (aido1_amd/csrc/dtconvx.hip).  Every f32 operand x
  * is an fp16 pair hi = fp16(x), lo = fp16((x - hi) * 2^11) (x = hi + 2^-11 lo
  * to 2^-24 |x|) and every product three fp16 MFMA products accumulated in f32:
- * ah*bh + 2^-11 (ah*bl + al*bh).  Activations between layers use the "HL"
- * layout: fp16 [n, H, W, 64], a pixel's 32 hi values then its 32 lo values
- * (the bytes of f32), centred on the sample's pixel 0 as dt_conv1's.
+ * ah*bh + 2^-11 (ah*bl + al*bh).  Activations between layers use the "HLB"
+ * layout, 4 B an element like f32: fp16 [n, H, 4, 2, P, 8], for each image row
+ * 4 blocks of 8 channels, each a hi segment and a lo segment of P 8-channel
+ * chunks; pixel x is chunk x of a segment when the consumer reads the image
+ * at stride 1 (P = W), and chunk x / 2 (even x) or (W + 1) / 2 + x / 2 (odd x)
+ * at stride 2 (P = 2 ((W + 1) / 2)), so a wave's 32 pixels of one k step are
+ * contiguous.  Values are centred on the sample's pixel 0 as dt_conv1's.
  *
  * dt_conv1x_split: conv1 + bias + LeakyReLU from the frame ring, as
  * dt_conv1_split / dt_conv1_index_split (index != 0: palette-index u8 frames,
  * else grey f32).
  *   wfrag     device fp16 [2, 16, 64, 8]: dt_conv1's fragment layout, first
  *             the hi halves of the f32 weights, then the lo halves
- *   y         device fp16 [n, 57, 77, 64] (HL), centred
+ *   y         device fp16 HLB [n, 57, 4, 2, 78, 8] (read at stride 2), centred
  *   partials  device f32 [n, 32, 3] (required): (mean, M2, c) as dt_conv1's
  *   set2      the second weight set (wfrag in this layout) or NULL.
  * Assumes |w| < 65504 (an fp16 hi of a larger weight overflows). */
@@ -146,10 +150,11 @@ int dt_conv1x_split(const void* ring, int32_t index, int32_t n, int32_t slots,
  * in_beta, in_eps; all required) is folded per sample into the weights: w' =
  * w * sc[c] (scaled by a power of two when the sample's largest |w'| would
  * leave fp16's range), bias' = bias + sum_k w * sh[c].
- *   x      device fp16 HL [n, IH, IW, 64] (dt_conv1x_split's y, or this call's
- *          y of layer 2 / 3)
+ *   x      device fp16 HLB (dt_conv1x_split's y, or this call's y of layer
+ *          2 / 3)
  *   wfrag  device f32 [32, 64, 8]: dt_conv32's fragment layout in float32
- *   y, part  layers 2, 3: HL [n, OH, OW, 64] centred, and (mean, M2, c)
+ *   y, part  layers 2, 3: HLB [n, 27, 4, 2, 38, 8] (read at stride 2) /
+ *          [n, 12, 4, 2, 17, 8] (stride 1), centred, and (mean, M2, c)
  *          [n, 32, 3]; layer 4: f32 [n, 32*9*14] flattened in NCHW order,
  *          normalised by (out_gamma, out_beta, out_eps) (required), part NULL */
 int dt_conv32x_split(int32_t layer, int32_t n, const void* x, const float* wfrag,

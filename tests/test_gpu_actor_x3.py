@@ -19,18 +19,6 @@ from formulas import formula_state_dict  # noqa: E402
 pytestmark = pytest.mark.gpu
 
 
-def decode_hl(y):
-    """HL activations [..., 64] fp16 -> float64 [..., 32]: hi + 2^-11 lo."""
-    return y[..., :32].double() + y[..., 32:].double() / 2048.0
-
-
-def encode_hl(x):
-    """float32 [..., 32] -> HL [..., 64] fp16."""
-    from aido1_amd.actor import split_hl
-    s = split_hl(x.float())
-    return torch.cat([s[0], s[1]], dim=-1).contiguous()
-
-
 def stream():
     return torch.cuda.current_stream().cuda_stream
 
@@ -43,7 +31,7 @@ def test_conv1x_matches_float64(gpu, index, slots, order, n):
     plus the centre carry the f64 result to f32 rounding; the per-sample
     statistics (mean of the centred values, M2) likewise."""
     from aido1_amd import _lib
-    from aido1_amd.actor import conv1_fragments, split_hl
+    from aido1_amd.actor import conv1_fragments, hlb_decode, hlb_shape, split_hl
     from aido1_amd.render import decode_index
     L = _lib.lib()
     torch.manual_seed(n + slots)
@@ -56,7 +44,7 @@ def test_conv1x_matches_float64(gpu, index, slots, order, n):
     b = torch.randn(32, device=gpu) * 0.2
     ref = F.leaky_relu(F.conv2d(grey[:, order].double(), w.double(), b.double(), stride=2))
     wf = split_hl(conv1_fragments(w, torch.float32)).contiguous()
-    y = torch.empty(n, 57, 77, 64, dtype=torch.float16, device=gpu)
+    y = torch.empty(hlb_shape(n, 57, 77, 2), dtype=torch.float16, device=gpu)
     part = torch.empty(n, 32, 3, device=gpu)
     o = (ctypes.c_int32 * 3)(*order)
     assert L.dt_conv1x_split(ring.data_ptr(), int(index), n, slots, o, wf.data_ptr(),
@@ -65,7 +53,7 @@ def test_conv1x_matches_float64(gpu, index, slots, order, n):
     c = part[..., 2].double()
     scale = max(1.0, ref.abs().max().item())
     assert (c - ref[:, :, 0, 0]).abs().max().item() < 2e-6 * scale
-    got = decode_hl(y).permute(0, 3, 1, 2) + c[:, :, None, None]
+    got = hlb_decode(y, 57, 77, 2).permute(0, 3, 1, 2) + c[:, :, None, None]
     err = (got - ref).abs().max().item()
     assert err < 2e-6 * scale, err
     mean = ref.mean((2, 3))
@@ -75,9 +63,10 @@ def test_conv1x_matches_float64(gpu, index, slots, order, n):
 
 
 def _layer_case(gpu, layer, n, seed):
-    """A conv2..4 case: HL input (centred-like values) with its exact
+    """A conv2..4 case: HLB input (centred-like values) with its exact
     per-sample statistics, BatchNorm parameters, weights; the float64
     reference of the BatchNorm'd input's conv + LeakyReLU."""
+    from aido1_amd.actor import hlb_decode, hlb_encode
     shape, stride = {2: ((57, 77), 2), 3: ((27, 37), 2), 4: ((12, 17), 1)}[layer]
     g = torch.Generator(device=gpu).manual_seed(seed)
     ih, iw = shape
@@ -85,8 +74,8 @@ def _layer_case(gpu, layer, n, seed):
     spread = torch.exp(torch.randn(n, 1, 1, 32, device=gpu, generator=g) * 2.0)
     x = torch.randn(n, ih, iw, 32, device=gpu, generator=g) * spread + \
         torch.randn(n, 1, 1, 32, device=gpu, generator=g) * spread
-    xh = encode_hl(x)
-    xt = decode_hl(xh)                                   # the values the kernel sees
+    xh = hlb_encode(x, stride)
+    xt = hlb_decode(xh, ih, iw, stride)                  # the values the kernel sees
     mean = xt.mean((1, 2))
     m2 = ((xt - mean[:, None, None, :]) ** 2).sum((1, 2))
     prev = torch.stack([mean.float(), m2.float(), torch.zeros_like(mean).float()], -1).contiguous()
@@ -105,12 +94,12 @@ def _layer_case(gpu, layer, n, seed):
 @pytest.mark.parametrize('layer', [2, 3, 4])
 def test_conv32x_layers_match_float64(gpu, layer, n):
     """conv2..conv4 with the previous per-sample BatchNorm folded into the
-    weights vs float64: layers 2 / 3 write centred HL pairs and their
+    weights vs float64: layers 2 / 3 write centred HLB pairs and their
     statistics, layer 4 its own BatchNorm's output flattened NCHW in f32.
     Some input channels are nearly flat (spreads e^(2 N(0,1))), the case the
     per-sample norm amplifies.  n = 700 exceeds the resident grid."""
     from aido1_amd import _lib
-    from aido1_amd.actor import conv32_fragments
+    from aido1_amd.actor import conv32_fragments, hlb_decode, hlb_shape
     L = _lib.lib()
     xh, prev, gamma, beta, w, b, ref = _layer_case(gpu, layer, n, 10 * layer + n)
     oh, ow = ref.shape[2:]
@@ -121,7 +110,8 @@ def test_conv32x_layers_match_float64(gpu, layer, n):
         y = torch.empty(n, 32 * oh * ow, device=gpu)
         part = None
     else:
-        y = torch.empty(n, oh, ow, 64, dtype=torch.float16, device=gpu)
+        y = torch.empty(hlb_shape(n, oh, ow, 2 if layer == 2 else 1), dtype=torch.float16,
+                        device=gpu)
         part = torch.empty(n, 32, 3, device=gpu)
     ptr = (lambda t: t.data_ptr() if t is not None else None)
     assert L.dt_conv32x_split(layer, n, xh.data_ptr(), wf.data_ptr(), b.data_ptr(),
@@ -138,7 +128,8 @@ def test_conv32x_layers_match_float64(gpu, layer, n):
         return
     c = part[..., 2].double()
     scale = max(1.0, ref.abs().max().item())
-    got = decode_hl(y).permute(0, 3, 1, 2) + c[:, :, None, None]
+    got = hlb_decode(y, oh, ow, 2 if layer == 2 else 1).permute(0, 3, 1, 2) + \
+        c[:, :, None, None]
     err = (got - ref).abs().max().item()
     assert err < 1e-5 * scale, err
     mean = ref.mean((2, 3))
