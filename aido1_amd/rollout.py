@@ -62,7 +62,7 @@ class CycleEpsilon:
 
 class ActorRollout:
     def __init__(self, config, n_envs=4096, maps=('small_loop', 'zigzag'), device=0, seed=1234,
-                 env_id_base=0, actor=None, dtype=torch.float16, masks=True,
+                 env_id_base=0, actor=None, dtype=torch.float32, masks=True,
                  actor_mode='reference', fused_explore=True, n_exploit=None, guard=None,
                  frames='index'):
         self.config = config

@@ -63,7 +63,7 @@ PRIORITY_EPS = 1e-6
 class TrainLoop:
     def __init__(self, config, n_envs=4096, maps=('small_loop', 'zigzag'), device=0, seed=1234,
                  env_id_base=0, buffer_size=None, prioritized=True, batch_size=None,
-                 updates_per_step=1, refresh_every=1, obs_dtype=None, actor_dtype=torch.float16,
+                 updates_per_step=1, refresh_every=1, obs_dtype=None, actor_dtype=torch.float32,
                  actor_mode='reference', masks=False, graph=True, overlap=False, n_exploit=None,
                  save_dir=None, log_dir=None, poll_every=0, check_every=0, frames='index'):
         t = config['training']

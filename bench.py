@@ -101,9 +101,9 @@ def parse(argv=None):
     p.add_argument('--actor-mode', default='reference', choices=['reference', 'eval'],
                    help="actor/train: 'reference' = train-mode batch-of-one BatchNorm + live "
                         "dropout as the reference's explorers act; 'eval' = BN folded")
-    p.add_argument('--actor-dtype', default='float16', choices=['float16', 'float32'],
-                   help='actor/train: the acting actor\'s arithmetic (float16 = the fast '
-                        'mode; float32 = the reference\'s precision)')
+    p.add_argument('--actor-dtype', default='float32', choices=['float16', 'float32'],
+                   help='actor/train: the acting actor\'s arithmetic (float32 = the '
+                        'reference\'s precision, the x3 chain; float16 = the fast mode)')
     p.add_argument('--frames', default='index', choices=['index', 'gray'],
                    help="actor/train: the frame ring's format: 'index' = palette-index u8 frames "
                         "(lossless, a quarter of the bytes; render.py), 'gray' = float32 grey")
@@ -828,16 +828,17 @@ def bench_obs(args, ctx):
     lane = None if args.no_lane else lane_record(args, ctx, args.lane_steps, args.lane_warmup,
                                                  cpu=True)
     # configs 4 and 5 as sub-records of the same line (not the headline)
-    c4 = c4f = c5 = c5f = None
+    # (at the reference's float32 acting precision; the fp16 fast mode beside)
+    c4 = c4h = c5 = c5h = None
     if not args.no_sub:
         c4 = actor_record(args, ctx, args.sub_steps, args.sub_warmup, parity=not args.no_parity,
-                          cpu=True)
-        c4f = actor_record(args, ctx, args.sub_steps, args.sub_warmup,
-                           parity=not args.no_parity, dtype=torch.float32)
+                          cpu=True, dtype=torch.float32)
+        c4h = actor_record(args, ctx, args.sub_steps, args.sub_warmup,
+                           parity=not args.no_parity, dtype=torch.float16)
         c5 = train_record(args, ctx, args.sub_steps, args.sub_warmup, parity=not args.no_parity,
-                          cpu=True)
-        c5f = train_record(args, ctx, args.sub_steps, args.sub_warmup,
-                           parity=not args.no_parity, dtype=torch.float32)
+                          cpu=True, dtype=torch.float32)
+        c5h = train_record(args, ctx, args.sub_steps, args.sub_warmup,
+                           parity=not args.no_parity, dtype=torch.float16)
     if rank == 0:
         kms = float(np.mean(rend_all))
         fresh_per_launch = ev_st['resets'] / KE
@@ -911,9 +912,9 @@ def bench_obs(args, ctx):
             'host_enqueue_ms_per_step': t_host / K * 1e3,
             'config2': lane,
             'config4': c4,
-            'config4_f32': c4f,
+            'config4_fp16': c4h,
             'config5': c5,
-            'config5_f32': c5f,
+            'config5_fp16': c5h,
         }
         line['cpu_baseline'] = (cpu_obs_baseline(args.cpu_decisions, args.cpu_procs, args.map)
                                 if ctx.world == 1 and args.cpu_steps > 0 else None)
@@ -1233,15 +1234,16 @@ F32_ACTION_TOL = 1e-4
 def actor_record(args, ctx, K, W, parity=True, dtype=None, cpu=False):
     """BASELINE configs[3]: 4096 envs/GPU, mixed small_loop/zigzag, actor in the
     loop (the explorers' loop body, training/explorers.py:164-213).  Returns
-    the line (rank 0) or None.  dtype: the actor's arithmetic (float16: the
-    hand-written MFMA chain, the fast mode; float32: the reference's
-    precision).  parity: every env's actions against the other-precision GPU
-    path, and 64 envs' against a float64 host forward (actor_f64), dropout off."""
+    the line (rank 0) or None.  dtype: the actor's arithmetic (float32, the
+    default: the reference's precision, the x3 chain; float16: the fast
+    mode).  parity: every env's actions against the other-precision GPU path,
+    and --f64-envs envs' against a float64 forward (actor_f64 on the GPU),
+    dropout off."""
     torch = ctx.torch
     from aido1_amd.actor import FusedActor
     from aido1_amd.rollout import ActorRollout
     cfg = _reference_config()
-    dtype = dtype or torch.float16
+    dtype = dtype or torch.float32
     dev, rank, n = ctx.dev, ctx.rank, args.envs
     torch.manual_seed(args.seed)
     roll = ActorRollout(cfg, n, maps=('small_loop', 'zigzag'), device=dev.index, seed=args.seed,

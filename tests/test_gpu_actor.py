@@ -218,7 +218,7 @@ def test_rollout_exploiter_block(gpu):
     from aido1_amd.actor import ConfigActor, FusedActor
     from aido1_amd.rollout import ActorRollout
     cfg = golden('reference_config.json')
-    roll = ActorRollout(cfg, 512, device=0, seed=5, actor_mode='eval')
+    roll = ActorRollout(cfg, 512, device=0, seed=5, actor_mode='eval', dtype=torch.float16)
     assert roll.n_exploit == 64 and roll.n_explore == 448
     torch.manual_seed(21)
     other = ConfigActor(cfg['model']['actor']).to(gpu)

@@ -46,7 +46,7 @@ def test_config4_actor_rollout_at_size(gpu, wseed):
     actor = ConfigActor(cfg['model']['actor'])
     n = 4096
     roll = ActorRollout(cfg, n, maps=('small_loop', 'zigzag'), device=0, seed=1234, actor=actor,
-                        actor_mode='reference')
+                        actor_mode='reference', dtype=torch.float16)
     assert [e.n for e in roll.envs] == [2048, 2048]
     roll.reset()
     for _ in range(6):

@@ -17,7 +17,8 @@ from aido1_amd.rollout import ActorRollout  # noqa: E402
 dev = torch.device('cuda', 0)
 cfg = golden('reference_config.json')
 seeds = [int(s) for s in sys.argv[1:]] or [11, 1234]
-roll = ActorRollout(cfg, 4096, device=0, seed=1234, actor_mode='reference')
+roll = ActorRollout(cfg, 4096, device=0, seed=1234, actor_mode='reference',
+                    dtype=torch.float16)
 roll.reset()
 for _ in range(12):
     roll.step()

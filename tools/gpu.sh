@@ -34,7 +34,7 @@ for line in open(sys.argv[1]):
     r = d.get('roofline') or {}
     s = '%s %.4gM ms/step %.4f frac %s' % (d['config'].get('workload'), d['value'] / 1e6,
                                           d['ms_per_step'], r.get('frac'))
-    for k in ('config4', 'config4_f32', 'config5'):
+    for k in ('config4', 'config4_fp16', 'config5', 'config5_fp16'):
         if isinstance(d.get(k), dict) and d[k].get('value'):
             s += ' | %s %.3gM' % (k, d[k]['value'] / 1e6)
     print(s, 'parity', (d.get('parity') or {}).get('ok'))
