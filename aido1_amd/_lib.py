@@ -281,6 +281,9 @@ def bind(L):
         'dt_conv32x_split': (ctypes.c_int, [i32, i32, vp, vp, vp, vp, vp, vp, ctypes.c_float,
                                             vp, vp, vp, vp, ctypes.c_float, ctypes.c_float,
                                             ctypes.POINTER(DtConvSet), vp]),
+        'dt_actor_head_x3': (ctypes.c_int, [i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp,
+                                            i32, ctypes.c_float, vp, vp, vp]),
+        'dt_actor_head_x3_work_floats': (i64, [i32]),
         'dt_explore': (ctypes.c_int, [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                       ctypes.POINTER(DtExploreParams), vp, vp]),
         'dt_explore_done': (ctypes.c_int, [i32, vp, vp, vp, vp, i32, vp]),

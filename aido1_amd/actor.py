@@ -379,6 +379,9 @@ class FusedActor(nn.Module):
         if self.x3:
             self.register_buffer('w0x', torch.zeros(2, 16, 64, 8, dtype=torch.float16, device=dev))
             self.register_buffer('wx32', torch.zeros(3, 32, 64, 8, device=dev))
+            if tuple(lin1.weight.shape) == (512, FLAT):   # dt_actor_head_x3's lin1 fragments
+                self.register_buffer('w1x', torch.zeros(2, 16, 252, 64, 8, dtype=torch.float16,
+                                                        device=dev))
         self.refresh(actor, graph=False)
 
     @torch.no_grad()
@@ -506,6 +509,10 @@ class FusedActor(nn.Module):
                 [self.w1, self.b1, self.w2, self.b2],
                 ws + bs + [bn.weight for bn in bns] + [bn.bias for bn in bns] +
                 [lin1.weight, lin1.bias, lin2.weight, lin2.bias])
+            if hasattr(self, 'w1x'):
+                if getattr(self, '_h1idx', None) is None or self._h1idx.device != self.w1.device:
+                    self._h1idx = head_fragment_index(self.w1.device)
+                self.w1x.view(2, -1).copy_(split_hl(torch.take(self.w1, self._h1idx)))
         else:
             scale = shift = None
             ws, bs = [], []
@@ -735,6 +742,8 @@ class FusedActor(nn.Module):
             return out
         if self.x3:
             flat = self._convs_x3(x, order, other, n0)
+            if self._head_x3_ok(flat, other):
+                return self._heads_x3(other, flat, n0, out)
             out[:n0] = self._head(flat[:n0])
             out[n0:] = other._head(flat[n0:])
             return out
@@ -821,8 +830,43 @@ class FusedActor(nn.Module):
             raise _lib.DtError('dt_actor_head failed (%d)' % rc)
         return out
 
+    def _head_x3_ok(self, x, other=None):
+        nets = [self] if other is None else [self, other]
+        return (x.is_cuda and x.dtype == torch.float32 and x.is_contiguous() and
+                tuple(x.shape[1:]) == (FLAT,) and
+                all(hasattr(a, 'w1x') and a.head in self._HEAD_CODES and
+                    tuple(a.w2.shape) == (2, 512) for a in nets))
+
+    def _heads_x3(self, other, x, n0, out):
+        """dropout (reference mode) -> lin1 -> LeakyReLU -> lin2 -> head at
+        float32 accuracy in ONE dt_actor_head_x3 launch (include/dtactor.h):
+        rows [0, n0) with this actor's weights, [n0, n) with `other`'s."""
+        import ctypes
+        from aido1_amd import _lib
+        if self.mode == 'reference' and self.p_drop > 0:
+            x = F.dropout(x, self.p_drop, training=True)
+        o = other if other is not None else self
+        L = _lib.lib()
+        n = x.shape[0]
+        work = getattr(self, '_hwork', None)
+        if work is None or work.numel() < L.dt_actor_head_x3_work_floats(n) or \
+                work.device != x.device:
+            work = self._hwork = torch.empty(int(L.dt_actor_head_x3_work_floats(n)),
+                                             device=x.device)
+        rc = L.dt_actor_head_x3(
+            n, n0, FLAT, x.data_ptr(), self.w1x.data_ptr(), self.b1.data_ptr(),
+            self.w2.data_ptr(), self.b2.data_ptr(), o.w1x.data_ptr(), o.b1.data_ptr(),
+            o.w2.data_ptr(), o.b2.data_ptr(), self._HEAD_CODES[self.head], 0.01, work.data_ptr(),
+            out.data_ptr(), ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream))
+        if rc != 0:
+            raise _lib.DtError('dt_actor_head_x3 failed (%d)' % rc)
+        return out
+
     def _head(self, x):
         """dropout (reference mode) -> lin1 -> LeakyReLU -> lin2 -> head."""
+        if self._head_x3_ok(x) and x.shape[0] > 0:
+            out = torch.empty(x.shape[0], 2, dtype=torch.float32, device=x.device)
+            return self._heads_x3(None, x, x.shape[0], out)
         if self.mode == 'reference' and self.p_drop > 0:
             x = F.dropout(x, self.p_drop, training=True)
         x = F.leaky_relu(F.linear(x, self.w1, self.b1))
@@ -949,6 +993,17 @@ def conv32_fragments(w, dtype=torch.float16):
     j = torch.arange(8, device=dev).view(1, 1, 8)
     return w.float()[ln % 32, 16 * (s % 2) + 8 * (ln // 32) + j, (s // 2) // 4,
                      (s // 2) % 4].to(dtype)
+
+
+def head_fragment_index(dev):
+    """dt_actor_head_x3's lin1 fragment layout as flat indices into lin1's
+    weights [512, 4032]: element [t][s][l][j] = w1[32 t + l % 32][16 s + 8
+    (l // 32) + j]."""
+    t = torch.arange(16, device=dev).view(16, 1, 1, 1)
+    s = torch.arange(252, device=dev).view(1, 252, 1, 1)
+    ln = torch.arange(64, device=dev).view(1, 1, 64, 1)
+    j = torch.arange(8, device=dev).view(1, 1, 1, 8)
+    return ((32 * t + ln % 32) * FLAT + 16 * s + 8 * (ln // 32) + j).reshape(-1)
 
 
 def conv1_fragment_index(dev):

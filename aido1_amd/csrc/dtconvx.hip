@@ -693,6 +693,180 @@ int launch_conv32x(int n, const void* x, const float* w, const float* bias, cons
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 
+// ---- the output branch: lin1 (4032 -> 512) + LeakyReLU + lin2 (512 -> 2) + head --------
+// x3 like the convolutions: C[feature][sample] = W1 . x^T on fp16 MFMA with
+// A = lin1's weights as pre-split (hi, lo) fragments (feature rows), B = the
+// samples' flattened activations (f32, split as they are loaded).
+// head_lin1_x3_kernel: a workgroup owns 64 samples, all 512 features and a
+//   quarter of K (8 waves, 2 feature tiles x 2 sample tiles each), so lin1's
+//   8 MB of fragments are streamed once per 64 samples rather than per 32
+//   (a one-pass form with 32 samples a workgroup took 213 us at 4096
+//   samples, streaming them); it writes its partial sums [part][feature][row].
+// head_finish_kernel: the four partials + bias, LeakyReLU, lin2, the head;
+//   four lanes a sample, 128 features each.  Summation order is fixed:
+//   deterministic.
+constexpr int kHFeat = 512, kHK = 4032, kHSteps = kHK / 16;   // 252 k steps
+constexpr int kHWaves = 8, kHParts = 4, kHPartSteps = kHSteps / kHParts;   // 63
+constexpr int kHRows = 64;                                                 // samples a workgroup
+static_assert(kHSteps % kHParts == 0, "K split");
+
+__device__ __forceinline__ float head_act(float v, int head) {
+  if (head == 1) return tanhf(v);
+  if (head == 2) return 1.0f / (1.0f + expf(-v));
+  return v;
+}
+
+// the workgroup's rows: tiles of kHRows, the first set's [0, n0) then the second's
+struct HeadTile {
+  bool set2;
+  int rbeg, rend;
+};
+__device__ __forceinline__ HeadTile head_tile(int b, int n, int n0) {
+  const int t1 = (n0 + kHRows - 1) / kHRows;
+  HeadTile t;
+  t.set2 = b >= t1;
+  t.rbeg = t.set2 ? n0 + kHRows * (b - t1) : kHRows * b;
+  t.rend = t.set2 ? n : n0;
+  return t;
+}
+
+// XCD-aware order (blocks are dealt round-robin over the 8 XCDs, so b and
+// b + 8 share one): block b works K quarter (b % 8) / 2, so each XCD's L2
+// holds one quarter of lin1's fragments (2 MB) for all its workgroups; the
+// grid is padded to a multiple of 8, the spare blocks exit
+__global__ void __launch_bounds__(64 * kHWaves, 2)
+head_lin1_x3_kernel(int n, int n0, int ldp, int tiles, const float* __restrict__ x,
+                    const half8* __restrict__ w1a, const half8* __restrict__ w1b,
+                    float* __restrict__ part) {
+  const int b = blockIdx.x, xcd = b & 7;
+  const int kp = xcd >> 1;                        // the K quarter
+  const int tile = (b >> 3) * 2 + (xcd & 1);
+  if (tile >= tiles) return;
+  const HeadTile ht = head_tile(tile, n, n0);
+  const half8* __restrict__ w1 = ht.set2 ? w1b : w1a;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 31, h = lane >> 5;
+  const float4* xr[2];
+#pragma unroll
+  for (int st = 0; st < 2; ++st) {
+    const int row = ht.rbeg + 32 * st + col;
+    xr[st] = reinterpret_cast<const float4*>(x + (size_t)(row < ht.rend ? row : ht.rbeg) * kHK +
+                                             8 * h) + 4 * kHPartSteps * kp;
+  }
+  // w1 fragments: [2 (hi, lo)][16 feature tiles][252 k steps][64 lanes]
+  constexpr int kHalfFrag = 16 * kHSteps * 64;
+  const half8* wt[2];
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+    wt[c] = w1 + ((size_t)(2 * wave + c) * kHSteps + kHPartSteps * kp) * 64 + lane;
+  f32x16 acc0[2][2], acc1[2][2];   // [feature tile][sample tile]
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int st = 0; st < 2; ++st)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc0[c][st][r] = acc1[c][st][r] = 0.0f;
+  float4 xq[2][2][2];              // [buffer][sample tile][half]
+  half8 ah[2][2], al[2][2];        // [buffer][feature tile]
+  auto load = [&](int b, int s) __attribute__((always_inline)) {
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      xq[b][st][0] = xr[st][4 * s];
+      xq[b][st][1] = xr[st][4 * s + 1];
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      ah[b][c] = wt[c][s * 64];
+      al[b][c] = wt[c][kHalfFrag + s * 64];
+    }
+  };
+  auto step = [&](int b) __attribute__((always_inline)) {
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const float4 q0 = xq[b][st][0], q1 = xq[b][st][1];
+      uint32_t hi[4], lo[4];
+      split2(q0.x, q0.y, hi[0], lo[0]);
+      split2(q0.z, q0.w, hi[1], lo[1]);
+      split2(q1.x, q1.y, hi[2], lo[2]);
+      split2(q1.z, q1.w, hi[3], lo[3]);
+      const half8 xh = __builtin_bit_cast(half8, u32x4{hi[0], hi[1], hi[2], hi[3]});
+      const half8 xl = __builtin_bit_cast(half8, u32x4{lo[0], lo[1], lo[2], lo[3]});
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        acc0[c][st] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[b][c], xh, acc0[c][st], 0, 0, 0);
+        acc1[c][st] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[b][c], xl, acc1[c][st], 0, 0, 0);
+        acc1[c][st] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[b][c], xh, acc1[c][st], 0, 0, 0);
+      }
+    }
+  };
+  load(0, 0);
+  for (int s = 0; s + 1 < kHPartSteps; s += 2) {   // 63 steps: 31 pairs, then the last
+    load(1, s + 1);
+    step(0);
+    load(0, s + 2);
+    step(1);
+  }
+  step(0);
+  // partial sums [part][feature][row]: lanes of a half-wave are 32 consecutive rows
+  float* pp = part + (size_t)kp * kHFeat * ldp;
+#pragma unroll
+  for (int c = 0; c < 2; ++c)
+#pragma unroll
+    for (int st = 0; st < 2; ++st) {
+      const int row = ht.rbeg + 32 * st + col;
+      if (row < ht.rend)
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+          const int f = 32 * (2 * wave + c) + (r & 3) + 8 * (r >> 2) + 4 * h;
+          pp[(size_t)f * ldp + row] = acc0[c][st][r] + acc1[c][st][r] * kLoInv;
+        }
+    }
+}
+
+// 16 rows a workgroup, 16 lanes a row (consecutive lanes: consecutive rows,
+// so a load is 16 consecutive floats of one feature); lane g of a row sums
+// features g, g + 16, ... (32), the 16 partial dot products of a row reduced
+// in LDS in a fixed order
+__global__ void __launch_bounds__(256)
+head_finish_kernel(int n, int n0, int ldp, const float* __restrict__ part,
+                   const float* __restrict__ b1a, const float* __restrict__ w2a,
+                   const float* __restrict__ b2a, const float* __restrict__ b1b,
+                   const float* __restrict__ w2b, const float* __restrict__ b2b, int head,
+                   float slope, float* __restrict__ out) {
+  __shared__ float red[16][16][2];
+  const int tid = threadIdx.x, g = tid >> 4, rr = tid & 15;
+  const int row = 16 * blockIdx.x + rr;
+  const bool valid = row < n;
+  const int rc = valid ? row : 0;
+  const bool set2 = rc >= n0;
+  const float* __restrict__ b1 = set2 ? b1b : b1a;
+  const float* __restrict__ w2 = set2 ? w2b : w2a;
+  float p0 = 0.0f, p1 = 0.0f;
+#pragma unroll 4
+  for (int f = g; f < kHFeat; f += 16) {
+    float a = 0.0f;
+#pragma unroll
+    for (int k = 0; k < kHParts; ++k) a += part[((size_t)k * kHFeat + f) * ldp + rc];
+    const float v = lrelu2(a + b1[f], slope);
+    p0 = fmaf(v, w2[f], p0);
+    p1 = fmaf(v, w2[kHFeat + f], p1);
+  }
+  red[rr][g][0] = p0;
+  red[rr][g][1] = p1;
+  __syncthreads();
+  if (tid < 32) {
+    const int r2 = tid >> 1, j = tid & 1;
+    const int orow = 16 * blockIdx.x + r2;
+    if (orow < n) {
+      const float* __restrict__ b2 = orow >= n0 ? b2b : b2a;
+      float a = b2[j];
+#pragma unroll
+      for (int q = 0; q < 16; ++q) a += red[r2][q][j];
+      out[(size_t)orow * 2 + j] = head_act(a, head);
+    }
+  }
+}
+
 template <bool kIdx>
 int conv1x_launch(const void* ring, int32_t n, int32_t slots, const int32_t* order,
                   const void* wfrag, const float* bias, const dt_conv_set* set2, void* y,
@@ -726,6 +900,31 @@ extern "C" int dt_conv1x_split(const void* ring, int32_t index, int32_t n, int32
                                      stream)
                : conv1x_launch<false>(ring, n, slots, order, wfrag, bias, set2, y, partials,
                                       slope, stream);
+}
+
+extern "C" int64_t dt_actor_head_x3_work_floats(int32_t n) {
+  return n < 0 ? -1 : (int64_t)kHParts * kHFeat * n;
+}
+
+extern "C" int dt_actor_head_x3(int32_t n, int32_t n0, int32_t k, const float* x,
+                                const void* w1a, const float* b1a, const float* w2a,
+                                const float* b2a, const void* w1b, const float* b1b,
+                                const float* w2b, const float* b2b, int32_t head, float slope,
+                                float* work, float* out, void* stream) {
+  if (!x || !w1a || !b1a || !w2a || !b2a || !work || !out || n < 0 || n0 < 0 || n0 > n ||
+      k != kHK || head < 0 || head > 2)
+    return DT_E_ARG;
+  if (n0 < n && (!w1b || !b1b || !w2b || !b2b)) return DT_E_ARG;
+  if (n == 0) return DT_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int tiles = (n0 + kHRows - 1) / kHRows + (n - n0 + kHRows - 1) / kHRows;
+  const int blocks = 8 * ((tiles + 1) / 2);   // two tiles of each quarter an 8-block round
+  hipLaunchKernelGGL(head_lin1_x3_kernel, dim3(blocks), dim3(64 * kHWaves), 0, s, n, n0, n, tiles,
+                     x, (const half8*)w1a, (const half8*)(w1b ? w1b : w1a), work);
+  hipLaunchKernelGGL(head_finish_kernel, dim3((n + 15) / 16), dim3(256), 0, s, n, n0, n,
+                     work, b1a, w2a, b2a, b1b ? b1b : b1a, w2b ? w2b : w2a, b2b ? b2b : b2a,
+                     head, slope, out);
+  return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 
 extern "C" int dt_conv32x_split(int32_t layer, int32_t n, const void* x, const float* wfrag,

@@ -163,6 +163,26 @@ int dt_conv32x_split(int32_t layer, int32_t n, const void* x, const float* wfrag
                      const float* out_gamma, const float* out_beta, float out_eps, float slope,
                      const dt_conv_set* set2, void* stream);
 
+/* dt_actor_head_x3: the actor's output branch at float32 accuracy, for n
+ * samples in one launch (config.json actor: flatten -> dropout -> linear(4032
+ * -> 512) -> leaky_relu -> linear(512 -> 2) -> tanh; duckietown_rl/ddpg.py:
+ * 56-62):  out[i] = head(lrelu(x[i] . w1^T + b1) . w2^T + b2), rows [0, n0)
+ * with the first weight set, [n0, n) with the second.  lin1 on fp16 MFMA as
+ * dt_conv1x_split's products (x3), lin2 and the head in f32.
+ *   x      device f32 [n, k], k = 4032 (dropout already applied)
+ *   w1*    device fp16 [2, 16, 252, 64, 8]: lin1's weights [512, 4032] as
+ *          (hi, lo) MFMA A fragments, element [q][t][s][l][j] = half q of
+ *          w1[32 t + l % 32][16 s + 8 (l / 32) + j] (aido1_amd/actor.py)
+ *   b1*    device f32 [512]; w2* device f32 [2, 512]; b2* device f32 [2]
+ *   head   0 none, 1 tanh, 2 sigmoid; out device f32 [n, 2]
+ *   work   device f32 [dt_actor_head_x3_work_floats(n)]: lin1's partial sums
+ *          (four K quarters) between the two launches it makes */
+int dt_actor_head_x3(int32_t n, int32_t n0, int32_t k, const float* x, const void* w1a,
+                     const float* b1a, const float* w2a, const float* b2a, const void* w1b,
+                     const float* b1b, const float* w2b, const float* b2b, int32_t head,
+                     float slope, float* work, float* out, void* stream);
+int64_t dt_actor_head_x3_work_floats(int32_t n);
+
 /* dt_explore: SingleThreadExplorer's action choice for n explorers at once,
  * one fused pass replacing the torch restatement's ~25 element-wise kernels
  * (aido1_amd/explore.py explore_actions + rollout.CycleEpsilon; the same

@@ -218,3 +218,28 @@ def test_f32_actor_matches_formula_weights_per_sample(gpu):
     f = FusedActor(a.float().to(gpu), dtype=torch.float32, mode='reference')
     got = f(x.to(gpu).contiguous()).double().cpu()
     assert (got - ref).abs().max().item() < 1e-4
+
+
+@pytest.mark.parametrize('n,n0', [(300, 300), (300, 257), (4096, 3584), (33, 1)])
+def test_head_x3_matches_float64(gpu, n, n0):
+    """dt_actor_head_x3 (lin1 on x3 MFMA, LeakyReLU, lin2, tanh in one launch
+    over both weight sets) vs float64 on the same inputs, dropout off."""
+    from aido1_amd.actor import FLAT, ConfigActor, FusedActor
+    from test_trainer import no_dropout
+    cfg = no_dropout(golden('reference_config.json')['model']['actor'])
+    torch.manual_seed(n + n0)
+    a, b = ConfigActor(cfg).to(gpu), ConfigActor(cfg).to(gpu)
+    fa = FusedActor(a, dtype=torch.float32, mode='reference')
+    fb = FusedActor(b, dtype=torch.float32, mode='reference')
+    assert fa._head_x3_ok(torch.zeros(1, FLAT, device=gpu), fb)
+    x = torch.randn(n, FLAT, device=gpu) * 0.7
+    out = torch.full((n, 2), float('nan'), device=gpu)
+    fa._heads_x3(fb, x, n0, out)
+    want = []
+    for net, sl in ((a, slice(0, n0)), (b, slice(n0, n))):
+        _, _, l1, l2 = net.layers()
+        h = F.leaky_relu(x[sl].double() @ l1.weight.double().t() + l1.bias.double())
+        want.append(torch.tanh(h @ l2.weight.double().t() + l2.bias.double()))
+    want = torch.cat(want)
+    assert torch.isfinite(out).all()
+    assert (out.double() - want).abs().max().item() < 2e-6
