@@ -398,7 +398,7 @@ class FusedActor(nn.Module):
             graph = dev.type == 'cuda'
         if not graph:
             return self._refresh(actor)
-        if self.mode == 'reference' and self.dtype == torch.float16:
+        if self.mode == 'reference' and (self.dtype == torch.float16 or self.x3):
             return self._refresh_gather(actor)
         # the source's tensors are listed once per source module (walking the
         # module tree costs ~80 us of host time a call); their addresses are
@@ -419,10 +419,12 @@ class FusedActor(nn.Module):
         g.replay()
 
     def _refresh_pairs(self, actor):
-        """(destination, source, logical index map or None) of a reference-mode
-        refresh: what _refresh copies, with the fragment gathers' index maps."""
+        """(destination, source, logical index map or None, kind) of a
+        reference-mode refresh: what _refresh copies, with the fragment
+        gathers' index maps; kind 2 = the x3 (hi, lo) pair into dst[0], dst[1]
+        (dt_refresh_copy), None = by the destination's dtype."""
         convs, bns, lin1, lin2 = actor.layers()
-        pairs = [(d, sp, None) for d, sp in zip(
+        pairs = [(d, sp, None, None) for d, sp in zip(
             list(self.w) + list(self.b) + list(self.gamma) + list(self.beta) +
             [self.w1, self.b1, self.w2, self.b2],
             [c.weight for c in convs] + [c.bias for c in convs] + [bn.weight for bn in bns] +
@@ -433,11 +435,20 @@ class FusedActor(nn.Module):
             self._w0pad = torch.zeros(32 * 3 * 64 + 1, device=dev)
         n0 = convs[0].weight.numel()
         f0 = self._fidx[0].reshape(-1)
-        pairs.append((self.w0frag, convs[0].weight, torch.where(f0 < n0, f0, torch.full_like(f0, -1))))
+        f0 = torch.where(f0 < n0, f0, torch.full_like(f0, -1))
+        pairs.append((self.w0frag, convs[0].weight, f0, None))
         for i in range(1, 4):
-            pairs.append((self.wfrag[i - 1], convs[i].weight, self._fidx[1].reshape(-1)))
+            pairs.append((self.wfrag[i - 1], convs[i].weight, self._fidx[1].reshape(-1), None))
+        if self.x3:   # the x3 chain's fragments
+            pairs.append((self.w0x, convs[0].weight, f0, 2))
+            for i in range(1, 4):
+                pairs.append((self.wx32[i - 1], convs[i].weight, self._fidx[1].reshape(-1), None))
+            if hasattr(self, 'w1x'):
+                if getattr(self, '_h1idx', None) is None or self._h1idx.device != dev:
+                    self._h1idx = head_fragment_index(dev)
+                pairs.append((self.w1x, lin1.weight, self._h1idx, 2))
         for i in range(4):
-            pairs.append((self.bf[i], convs[i].bias, None))
+            pairs.append((self.bf[i], convs[i].bias, None, None))
         return pairs
 
     @staticmethod
@@ -480,15 +491,20 @@ class FusedActor(nn.Module):
         if ent is None:
             pairs = self._refresh_pairs(actor)
             keep, rows = [], []
-            for dst, src, lg in pairs:
+            for dst, src, lg, kind in pairs:
                 if src.dtype != torch.float32 or dst.dtype not in (torch.float16, torch.float32):
                     raise ValueError('refresh: float32 sources, fp16 / f32 destinations')
-                m = self._phys_map(dst, src.detach(), lg)
+                if kind == 2 and not (dst.is_contiguous() and dst.dtype == torch.float16):
+                    raise ValueError('refresh: an x3 pair is a contiguous fp16 [2, ...]')
+                half = dst[0] if kind == 2 else dst      # an x3 pair: the map of its hi half
+                m = self._phys_map(half, src.detach(), lg)
                 if m is not None:
                     keep.append(m)
+                if kind is None:
+                    kind = 1 if dst.dtype == torch.float16 else 0
                 rows.append(_lib.DtCopyEntry(src.data_ptr(), dst.data_ptr(),
                                              m.data_ptr() if m is not None else None,
-                                             dst.numel(), 1 if dst.dtype == torch.float16 else 0, 0))
+                                             half.numel(), kind, 0))
             arr = (_lib.DtCopyEntry * len(rows))(*rows)
             table = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).to(
                 self.w0frag.device)

@@ -434,7 +434,9 @@ namespace {
 constexpr int kCopyThreads = 256;
 
 // entry e of the table, element i: dst[i] = cast(src[map ? map[i] : i]), 0 where
-// map[i] < 0; blockIdx.y = entry, x-blocks stride over its elements
+// map[i] < 0; blockIdx.y = entry, x-blocks stride over its elements.  dst_dtype
+// 0 f32, 1 fp16, 2 the x3 pair (include/dtactor.h dt_conv1x_split): fp16 hi =
+// fp16(v) at dst[i], lo = fp16((v - hi) * 2^11) at dst[count + i]
 __global__ void __launch_bounds__(kCopyThreads)
 refresh_copy_kernel(int32_t n, const DtCopyEntry* __restrict__ table) {
   const DtCopyEntry t = table[blockIdx.y];
@@ -448,10 +450,15 @@ refresh_copy_kernel(int32_t n, const DtCopyEntry* __restrict__ table) {
     } else {
       v = src[i];
     }
-    if (t.dst_dtype == 1)
+    if (t.dst_dtype == 1) {
       static_cast<__half*>(t.dst)[i] = __float2half(v);   // round to nearest, as .half()
-    else
+    } else if (t.dst_dtype == 2) {
+      const __half h = __float2half(v);
+      static_cast<__half*>(t.dst)[i] = h;
+      static_cast<__half*>(t.dst)[t.count + i] = __float2half((v - __half2float(h)) * 2048.0f);
+    } else {
       static_cast<float*>(t.dst)[i] = v;
+    }
   }
 }
 

@@ -262,8 +262,10 @@ int dt_episode_account(int32_t n, int32_t k, const double* reward, const double*
  * actor's float32 parameters.  table: device [n] entries; entry e writes
  * count elements of dst (in its physical order) from src (float32): element
  * i = src[map[i]] (map device int64 [count], -1 = 0.0), or src[i] with map
- * NULL; dst_dtype 0 float32, 1 fp16 (round to nearest).  max_count: the
- * largest count (the grid's width). */
+ * NULL; dst_dtype 0 float32, 1 fp16 (round to nearest), 2 the x3 pair of
+ * dt_conv1x_split (fp16 hi = fp16(v) at dst[i], lo = fp16((v - hi) * 2^11)
+ * at dst[count + i]: dst holds 2 * count fp16).  max_count: the largest
+ * count (the grid's width). */
 typedef struct DtCopyEntry {
   const void* src;
   void* dst;

@@ -401,8 +401,9 @@ def test_refresh_copies_every_parameter_exactly(gpu, channels_last):
         assert torch.equal(mine.float(), src.detach().half().float())
 
 
-@pytest.mark.parametrize('mode', ['reference', 'eval'])
-def test_graph_refresh_follows_in_place_updates(gpu, mode):
+@pytest.mark.parametrize('mode,dtype', [('reference', torch.float16), ('eval', torch.float16),
+                                        ('reference', torch.float32)])
+def test_graph_refresh_follows_in_place_updates(gpu, mode, dtype):
     """FusedActor.refresh on the GPU: one dt_refresh_copy launch through index
     maps built at the first refresh from a source (reference mode), or a HIP
     graph captured then (eval mode): after in-place updates of the source's
@@ -411,7 +412,7 @@ def test_graph_refresh_follows_in_place_updates(gpu, mode):
     from aido1_amd.actor import ConfigActor, FusedActor
     torch.manual_seed(13)
     a = ConfigActor(golden('reference_config.json')['model']['actor']).to(gpu)
-    f = FusedActor(a, dtype=torch.float16, mode=mode)
+    f = FusedActor(a, dtype=dtype, mode=mode)
     for k in range(3):
         with torch.no_grad():
             for p in a.parameters():
@@ -420,7 +421,7 @@ def test_graph_refresh_follows_in_place_updates(gpu, mode):
                 bn.running_mean.uniform_(-0.2, 0.2)
                 bn.running_var.uniform_(0.5, 2.0)
         f.refresh(a)
-        ref = FusedActor(a, dtype=torch.float16, mode=mode)
+        ref = FusedActor(a, dtype=dtype, mode=mode)
         torch.cuda.synchronize()
         for (name, x), (_, y) in zip(f.state_dict().items(), ref.state_dict().items()):
             if mode == 'eval' and name.startswith(('gamma', 'beta')):
