@@ -32,6 +32,11 @@ struct dt_handle {
   void* render_spill = nullptr;  // per env: listed words past the LDS list (dtrender.hip)
   void* render_sched = nullptr;  // render_kernel's dispatch order state (dtrender.hip)
   uint32_t render_launches = 0;  // dt_render launches (the order's double-buffer parity)
+  // the last render launch that used the dispatch-order state: its stream and
+  // an event recorded after it (a render on another stream waits for it)
+  hipEvent_t render_done = nullptr;
+  hipStream_t render_stream = nullptr;
+  bool render_pending = false;
   std::string err;
 };
 

@@ -1055,8 +1055,11 @@ __device__ __forceinline__ void write_outputs(const RenderArgs& a, RenderLds& S,
 // cost predicts the next one's; respawned envs' guesses are stale, and costs
 // not yet recorded are the last launch's).  Block b renders env
 // perm[launch & 1][b], launch the handle's host-side launch count passed as an
-// argument (a launch baked into a HIP graph keeps its parity: an odd graph
-// length re-reads an older order, still a permutation).  No device-wide
+// argument.  One state a handle, so its launches run one after another: a
+// launch captured into a HIP graph (replayed later, perhaps beside eager ones)
+// uses the identity order and does not touch the state, and an eager launch
+// on another stream than the last one's waits for that launch (an event,
+// dt_render_launch).  No device-wide
 // counter: an agent-scope atomic on one address from every workgroup
 // serialises at memory across the 8 XCDs (a start ticket taken that way cost
 // 0.15 ms a 4096-env launch).  The order is only a schedule:
@@ -1846,6 +1849,8 @@ void dt_render_free(dt_handle* h) {
   h->render_spill = nullptr;
   if (h->render_sched) (void)hipFree(h->render_sched);
   h->render_sched = nullptr;
+  if (h->render_done) (void)hipEventDestroy(h->render_done);
+  h->render_done = nullptr;
 }
 
 extern "C" {
@@ -1965,8 +1970,23 @@ static int render_launch(dt_handle* h, const dt_render_io* io, const dt_render_i
   a.n = h->n;
   a.spill = (uint16_t*)h->render_spill;
 #ifndef DTSIM_NO_SCHED   // diagnostic builds only (A/B of the dispatch order)
-  // a launch of <= kSchedTail workgroups runs all at once: no drain to order
-  a.sched = h->n > kSchedTail ? (uint32_t*)h->render_sched : nullptr;
+  // a launch of <= kSchedTail workgroups runs all at once: no drain to order.
+  // The order state is one per handle, double-buffered by the host's launch
+  // count, so its launches must run one after another: a launch being
+  // captured into a graph (replayed later, beside anything) keeps the
+  // identity order and leaves the state alone, and an eager launch on a
+  // stream other than the previous one's waits for that launch first.
+  hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+  if (hipStreamIsCapturing((hipStream_t)stream, &cap) != hipSuccess)
+    cap = hipStreamCaptureStatusNone;
+  a.sched = h->n > kSchedTail && cap == hipStreamCaptureStatusNone
+                ? (uint32_t*)h->render_sched : nullptr;
+  if (a.sched) {
+    if (!h->render_done)
+      HIP_OR_FAIL(h, hipEventCreateWithFlags(&h->render_done, hipEventDisableTiming));
+    if (h->render_pending && (hipStream_t)stream != h->render_stream)
+      HIP_OR_FAIL(h, hipStreamWaitEvent((hipStream_t)stream, h->render_done, 0));
+  }
   a.launch = h->render_launches++;
 #endif
   a.list_cap = io->list_cap > 0 && io->list_cap < kListCap ? io->list_cap : kListCap;
@@ -1994,6 +2014,11 @@ static int render_launch(dt_handle* h, const dt_render_io* io, const dt_render_i
   if (e != hipSuccess) {
     h->err = std::string("dt_render launch: ") + hipGetErrorString(e);
     return DT_E_HIP;
+  }
+  if (a.sched) {
+    HIP_OR_FAIL(h, hipEventRecord(h->render_done, (hipStream_t)stream));
+    h->render_stream = (hipStream_t)stream;
+    h->render_pending = true;
   }
   return DT_OK;
 }
