@@ -1,7 +1,8 @@
 // The DDPG update's convolutions (include/dtupd.h): config.json's conv_2d
-// layers of the actor and critic in f32 on v_mfma_f32_32x32x2_f32, forward,
-// weight gradient and input gradient, replacing MIOpen in the train-mode
-// networks of training/trainers.py:143-237.
+// layers of the actor and critic in f32, forward (x3: f32 operands as fp16
+// hi / lo pairs on v_mfma_f32_32x32x16_f16, DTUPD_X3 below), weight gradient
+// and input gradient (v_mfma_f32_32x32x2_f32), replacing MIOpen in the
+// train-mode networks of training/trainers.py:143-237.
 //
 // Every layer is C_out = 32 and NHWC, so each pass is a GEMM whose N or M is
 // the 32 channels:
@@ -34,6 +35,19 @@
 #define DTUPD_SKIP 0
 #endif
 // input-gradient waves a workgroup per layer (tools/upd_micro.py variants)
+// the forward's K slices (waves a tile) per layer (tools/upd_micro.py variants)
+#ifndef DTUPD_KS1
+#define DTUPD_KS1 2
+#endif
+#ifndef DTUPD_KS2
+#define DTUPD_KS2 2
+#endif
+#ifndef DTUPD_KS3
+#define DTUPD_KS3 8
+#endif
+#ifndef DTUPD_KS4
+#define DTUPD_KS4 16
+#endif
 #ifndef DTUPD_DG2_NW
 #define DTUPD_DG2_NW 8
 #endif
@@ -83,6 +97,41 @@ __device__ __forceinline__ float4 ld4(const float* p) {
     const float2 b = *reinterpret_cast<const float2*>(p + 2);
     return make_float4(a.x, a.y, b.x, b.y);
   }
+}
+
+// The forward's x3 form (DTUPD_X3, the library default): each f32 operand
+// as an fp16 pair hi = fp16(v), lo = fp16((v - hi) * 2^11), and a 16-k unit
+// as three v_mfma_f32_32x32x16_f16 into two f32 accumulators,
+//   acc0 += Xh Wh,   acc1 += Xh Wl + Xl Wh,   z = acc0 + acc1 / 2^11
+// (the dropped Xl Wl and the split's rounding: ~2^-21 of each product, the
+// actor's conv chain, csrc/dtconvx.hip), 3/16 of the f32 MFMA cycles.
+// Operands past fp16's range (|v| >= 65520) become inf: the guard reports
+// them.  0 keeps the f32 MFMA chain (tools/upd_micro.py variants).
+#ifndef DTUPD_X3
+#define DTUPD_X3 1
+#endif
+using half8 = __attribute__((ext_vector_type(8))) _Float16;
+using f32x2 = __attribute__((ext_vector_type(2))) float;
+using f16x2 = __attribute__((ext_vector_type(2))) _Float16;
+using u32x4v = __attribute__((ext_vector_type(4))) uint32_t;
+constexpr float kLo = 2048.0f, kLoInv = 1.0f / 2048.0f;
+
+__device__ __forceinline__ void split2(float a, float b, uint32_t& hi, uint32_t& lo) {
+  const f32x2 x = {a, b};
+  const f16x2 h = __builtin_convertvector(x, f16x2);
+  const f32x2 r = (x - __builtin_convertvector(h, f32x2)) * kLo;
+  hi = __builtin_bit_cast(uint32_t, h);
+  lo = __builtin_bit_cast(uint32_t, __builtin_convertvector(r, f16x2));
+}
+// eight consecutive k (two float4s) -> their hi and lo fragments
+__device__ __forceinline__ void split8(float4 a, float4 b, half8& h, half8& l) {
+  uint32_t uh[4], ul[4];
+  split2(a.x, a.y, uh[0], ul[0]);
+  split2(a.z, a.w, uh[1], ul[1]);
+  split2(b.x, b.y, uh[2], ul[2]);
+  split2(b.z, b.w, uh[3], ul[3]);
+  h = __builtin_bit_cast(half8, u32x4v{uh[0], uh[1], uh[2], uh[3]});
+  l = __builtin_bit_cast(half8, u32x4v{ul[0], ul[1], ul[2], ul[3]});
 }
 
 __device__ __forceinline__ f32x16 mfma4(float4 a, float4 b, f32x16 c) {
@@ -443,12 +492,19 @@ template <class G, int KSPLIT, int STATS, bool NORM>
 __global__ void __launch_bounds__(kFwdThreads)
 fwd_kernel(int n, const float* __restrict__ x, const float* __restrict__ w, float* __restrict__ z,
            FwdBn fb, DtUpdBn in) {
+  constexpr bool X3 = DTUPD_X3 != 0;
   constexpr int WST = G::K + 4;
   constexpr int NW = kFwdThreads / 64;
   constexpr int GP = NW / KSPLIT;                // tiles a workgroup round
-  constexpr int SPW = G::KSTEPS / KSPLIT;        // k-steps a wave
+  constexpr int SPW = G::KSTEPS / KSPLIT;        // k-steps a wave (f32)
+  constexpr int KU = G::K / 16;                  // 16-k units (x3)
+  constexpr int UPW = KU / KSPLIT;               // units a wave (x3)
   static_assert(G::KSTEPS % KSPLIT == 0 && NW % KSPLIT == 0, "even K slices");
-  __shared__ __attribute__((aligned(16))) float ws[32 * WST];
+  static_assert(!X3 || (G::K % 16 == 0 && KU % KSPLIT == 0 && G::KROW % 8 == 0),
+                "x3: whole 16-k units a slice, 8 k inside a kernel row");
+  // W: f32 rows [32][K + 4], or (x3) its B fragments, unit u lane l at u * 64 + l
+  __shared__ __attribute__((aligned(16))) float ws[X3 ? 1 : 32 * WST];
+  __shared__ half8 wsh[X3 ? KU * 64 : 1], wsl[X3 ? KU * 64 : 1];
   __shared__ float red[KSPLIT > 1 ? GP * (KSPLIT - 1) * 16 * 64 : 1];
   __shared__ __attribute__((aligned(16))) float tab[NORM ? 4 : 1][32];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -458,9 +514,18 @@ fwd_kernel(int n, const float* __restrict__ x, const float* __restrict__ w, floa
     static_assert(G::CIN == 32, "the chain's inputs are 32-channel activations");
     nr = norm_loads<kFwdThreads>(in, blockIdx.x == 0);
   }
-  for (int q = tid; q < ((DTUPD_SKIP & 2) ? 0 : 32 * G::K / 4); q += kFwdThreads) {
-    const int co = q / (G::K / 4), k4 = q - co * (G::K / 4);
-    *reinterpret_cast<float4*>(ws + co * WST + 4 * k4) = reinterpret_cast<const float4*>(w)[q];
+  if constexpr (X3) {
+    // B fragment of unit u, lane l: W[co = l & 31][16 u + 8 (l >> 5) + 0 .. 7]
+    for (int q = tid; q < ((DTUPD_SKIP & 2) ? 0 : KU * 64); q += kFwdThreads) {
+      const int u = q >> 6, l = q & 63;
+      const float4* src = reinterpret_cast<const float4*>(w + (l & 31) * G::K + 16 * u + 8 * (l >> 5));
+      split8(src[0], src[1], wsh[q], wsl[q]);
+    }
+  } else {
+    for (int q = tid; q < ((DTUPD_SKIP & 2) ? 0 : 32 * G::K / 4); q += kFwdThreads) {
+      const int co = q / (G::K / 4), k4 = q - co * (G::K / 4);
+      *reinterpret_cast<float4*>(ws + co * WST + 4 * k4) = reinterpret_cast<const float4*>(w)[q];
+    }
   }
   if constexpr (NORM) norm_build<kFwdThreads>(in, nr, tab, blockIdx.x == 0);   // ends in a barrier
   else __syncthreads();
@@ -476,10 +541,58 @@ fwd_kernel(int n, const float* __restrict__ x, const float* __restrict__ w, floa
     const int s = tc / G::TPS, tb = tc - s * G::TPS;
     const int p = tb * 32 + col;
     const int pc = p < G::OPIX ? p : 0;          // an invalid row reads pixel 0, unused
-    const float* xl = x + G::xbase(s, pc) + 4 * kk;
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
+    if constexpr (X3) {
+      // unit u: A = this lane's pixel, k = 16 u + 8 kk + 0 .. 7 (two float4s
+      // of one kernel row), normalised for NORM, split; B from LDS
+      const float* xp = x + G::xbase(s, pc);
+      const int u0 = ks * UPW;
+      f32x16 acc1;
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc1[r] = 0.0f;
+      struct A8 { float4 a, b; };
+      auto load = [&](int uu) -> A8 {
+        const int kc = 16 * (u0 + uu) + 8 * kk;
+        if (DTUPD_SKIP & 1) return A8{make_float4(xp[0], kc, uu, 1.0f), make_float4(1.0f, kc, 0.5f, 2.0f)};
+        const float* q = xp + G::koff(kc);
+        return A8{ld4<G::CIN>(q), ld4<G::CIN>(q + 4)};
+      };
+      auto unit = [&](int uu, A8 v) {
+        const int u = u0 + uu;
+        if constexpr (NORM) {
+          asm volatile("" ::: "memory");
+          const int c0 = (16 * u + 8 * kk) & 31;
+          const float4* t0 = reinterpret_cast<const float4*>(&tab[0][c0]);
+          const float4* t1 = reinterpret_cast<const float4*>(&tab[1][c0]);
+          const float4* t2 = reinterpret_cast<const float4*>(&tab[2][c0]);
+          const float4* t3 = reinterpret_cast<const float4*>(&tab[3][c0]);
+          v.a = norm4(v.a, t0[0], t1[0], t2[0], t3[0], in.slope);
+          v.b = norm4(v.b, t0[1], t1[1], t2[1], t3[1], in.slope);
+        }
+        half8 xh, xl;
+        split8(v.a, v.b, xh, xl);
+        const half8 bh = wsh[u * 64 + lane], bl = wsl[u * 64 + lane];
+        acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, bh, acc, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, bl, acc1, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, bh, acc1, 0, 0, 0);
+      };
+      if constexpr (UPW <= kFwdAllLoads / 2) {
+        A8 av[UPW];
+#pragma unroll
+        for (int uu = 0; uu < UPW; ++uu) av[uu] = load(uu);
+        asm volatile("" ::: "memory");
+#pragma unroll
+        for (int uu = 0; uu < UPW; ++uu) unit(uu, av[uu]);
+      } else {
+#pragma unroll 2
+        for (int uu = 0; uu < UPW; ++uu) unit(uu, load(uu));
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] += acc1[r] * kLoInv;
+    } else {
+    const float* xl = x + G::xbase(s, pc) + 4 * kk;
     const int s0 = ks * SPW;
     // one step: A (normalised for NORM: channels c0 .. c0 + 3 of the previous
     // block) times W's float4 from LDS, four MFMAs
@@ -515,6 +628,7 @@ fwd_kernel(int n, const float* __restrict__ x, const float* __restrict__ w, floa
       constexpr int kUnroll = NORM ? 2 : 4;   // NORM: its table reads need the registers
 #pragma unroll kUnroll
       for (int st = 0; st < SPW; ++st) step(st, load(st));
+    }
     }
     if constexpr (KSPLIT > 1 && !(DTUPD_SKIP & 8)) {   // slice ks > 0 of tile g at slot g * (KSPLIT - 1) + ks - 1
       float* rs = red + (size_t)g * (KSPLIT - 1) * 16 * 64 + lane;
@@ -1037,10 +1151,10 @@ int dispatch_fwd(int l, int n, const float* x, const float* w, float* z, const F
   switch (l) {
     case 1:
       if constexpr (NORM) return DT_E_ARG;
-      else return launch_fwd<L1, 2, STATS, false>(n, x, w, z, fb, in, s, grid_out);
-    case 2: return launch_fwd<L2, 2, STATS, NORM>(n, x, w, z, fb, in, s, grid_out);
-    case 3: return launch_fwd<L3, 8, STATS, NORM>(n, x, w, z, fb, in, s, grid_out);
-    default: return launch_fwd<L4, 16, STATS, NORM>(n, x, w, z, fb, in, s, grid_out);
+      else return launch_fwd<L1, DTUPD_KS1, STATS, false>(n, x, w, z, fb, in, s, grid_out);
+    case 2: return launch_fwd<L2, DTUPD_KS2, STATS, NORM>(n, x, w, z, fb, in, s, grid_out);
+    case 3: return launch_fwd<L3, DTUPD_KS3, STATS, NORM>(n, x, w, z, fb, in, s, grid_out);
+    default: return launch_fwd<L4, DTUPD_KS4, STATS, NORM>(n, x, w, z, fb, in, s, grid_out);
   }
 }
 

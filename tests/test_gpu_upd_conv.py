@@ -2,10 +2,12 @@
 weight gradient and input gradient of config.json's four conv_2d layers
 against a float64 CPU restatement (torch's conv2d and torch.nn.grad), for
 batch sizes from 1 to past the persistent grid, and the train-mode conv
-blocks through autograd against the MIOpen path.  Tolerance: the kernels are
-an exact f32 fma chain per output (v_mfma_f32_32x32x2_f32) summed in another
-order, so |err| <= 2e-5 * (sum of |products|) is the bound written below
-(relative to the f64 result's scale)."""
+blocks through autograd against the MIOpen path.  Tolerance: the gradients
+are an exact f32 fma chain per output (v_mfma_f32_32x32x2_f32) summed in
+another order; the forward's x3 products (fp16 hi / lo pairs, dtupd.hip
+DTUPD_X3) carry ~2^-21 of each product besides, so |err| <= 2e-5 * (sum of
+|products|) is the bound written below for both (relative to the f64
+result's scale)."""
 import pytest
 import torch
 import torch.nn.functional as F

@@ -13,25 +13,30 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 OUT = os.path.join(ROOT, 'tools', 'variants')
 SKIPS = {'full': 0, 'no_a_loads': 1, 'no_w_stage': 2, 'no_merge': 4, 'no_ksum': 8, 'bare': 15,
          'no_part_loads': 16, 'no_chain_merge': 32, 'no_chain_both': 48}
-# other variants: extra -D flags (dgrad waves per layer)
-EXTRA = {'dg_8_8_2': ['-DDTUPD_DG2_NW=8', '-DDTUPD_DG3_NW=8', '-DDTUPD_DG4_NW=2'],
-         'dg_16_4_8': ['-DDTUPD_DG2_NW=16', '-DDTUPD_DG3_NW=4', '-DDTUPD_DG4_NW=8'],
-         'dg_2_16_1': ['-DDTUPD_DG2_NW=2', '-DDTUPD_DG3_NW=16', '-DDTUPD_DG4_NW=1']}
+# other variants: extra -D flags (the f32 MFMA forward, forward K slices)
+EXTRA = {'f32': ['-DDTUPD_X3=0'], 'f32_bare': ['-DDTUPD_X3=0', '-DDTUPD_SKIP=15'],
+         'ks_4_4_4_8': ['-DDTUPD_KS1=4', '-DDTUPD_KS2=4', '-DDTUPD_KS3=4', '-DDTUPD_KS4=8'],
+         'ks_1_1_2_4': ['-DDTUPD_KS1=1', '-DDTUPD_KS2=1', '-DDTUPD_KS3=2', '-DDTUPD_KS4=4']}
 LAYERS = {1: (3, 8, 2, 120, 160), 2: (32, 4, 2, 57, 77), 3: (32, 4, 2, 27, 37),
           4: (32, 4, 1, 12, 17)}
 
 
-def build():
+def build(variants=''):
     sys.path.insert(0, ROOT)
     from aido1_amd import _lib
     os.makedirs(OUT, exist_ok=True)
     src = os.path.join(ROOT, 'aido1_amd', 'csrc', 'dtupd.hip')
+    want = set(variants.split(',')) if variants else None
     for name, bits in SKIPS.items():
+        if want is not None and name not in want:
+            continue
         so = os.path.join(OUT, 'libupd_%s.so' % name)
         subprocess.check_call([_lib.HIPCC] + _lib.HIP_FLAGS + ['-DDTUPD_SKIP=%d' % bits,
                                                                 '-o', so, src])
         print('built', so)
     for name, flags in EXTRA.items():
+        if want is not None and name not in want:
+            continue
         so = os.path.join(OUT, 'libupd_%s.so' % name)
         subprocess.check_call([_lib.HIPCC] + _lib.HIP_FLAGS + flags + ['-o', so, src])
         print('built', so)
@@ -75,12 +80,13 @@ def timeit(torch, fn, reps):
     return a.elapsed_time(b) * 1e3 / reps
 
 
-def run(n, reps):
+def run(n, reps, variants=''):
     import torch
     dev = torch.device('cuda', 0)
     torch.manual_seed(0)
     s = torch.cuda.current_stream().cuda_stream
-    for name in list(SKIPS) + list(EXTRA):
+    names = variants.split(',') if variants else list(SKIPS) + list(EXTRA)
+    for name in names:
         L = load(name)
         row = []
         for layer, (cin, ks, st, ih, iw) in LAYERS.items():
@@ -133,7 +139,7 @@ def run(n, reps):
                         assert L.dt_upd_bn_finish(z.numel() // 32, 0, z.data_ptr(),
                                                   ctypes.byref(hand), y.data_ptr(), s) == 0
                     t['finish'] = timeit(torch, finish, reps)
-            if name == 'full' or name in EXTRA:
+            if name in ('full', 'f32'):
                 ww = torch.empty(int(L.dt_upd_wgrad_work_floats(*a)), device=dev)
                 dw = torch.empty_like(w)
 
@@ -157,8 +163,9 @@ if __name__ == '__main__':
     ap.add_argument('--build', action='store_true')
     ap.add_argument('--n', type=int, default=64)
     ap.add_argument('--reps', type=int, default=200)
+    ap.add_argument('--variants', default='', help='comma-separated names (default: all)')
     args = ap.parse_args()
     if args.build:
-        build()
+        build(args.variants)
     else:
-        run(args.n, args.reps)
+        run(args.n, args.reps, args.variants)
