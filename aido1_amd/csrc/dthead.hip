@@ -23,7 +23,11 @@
 
 namespace {
 
-constexpr int kRows = 8;          // rows a forward workgroup
+// rows a forward workgroup (tools/ab.sh variants)
+#ifndef DTHEAD_ROWS
+#define DTHEAD_ROWS 1
+#endif
+constexpr int kRows = DTHEAD_ROWS;
 constexpr int kGrp = 16;          // lanes per output (forward)
 constexpr int kMaxM = 256, kMaxK = 1024, kMaxN1 = 1024, kMaxN2 = 64;
 constexpr int kMaxH = 512;        // n1 of a two-layer tail (its outputs stay in LDS)

@@ -35,6 +35,15 @@
 #define DTUPD_SKIP 0
 #endif
 // input-gradient waves a workgroup per layer (tools/upd_micro.py variants)
+// weight gradient: double-buffered row staging for conv2-4 (the x3 MFMAs
+// left the row loads exposed: conv2 32.5 -> 27.9 us at batch 64) and conv1
+// (tools/upd_micro.py variants)
+#ifndef DTUPD_WG_DB
+#define DTUPD_WG_DB 1
+#endif
+#ifndef DTUPD_WG_DB1
+#define DTUPD_WG_DB1 0
+#endif
 // the forward's K slices (waves a tile) per layer (tools/upd_micro.py variants)
 #ifndef DTUPD_KS1
 #define DTUPD_KS1 2
@@ -132,6 +141,27 @@ __device__ __forceinline__ void split8(float4 a, float4 b, half8& h, half8& l) {
   split2(b.z, b.w, uh[3], ul[3]);
   h = __builtin_bit_cast(half8, u32x4v{uh[0], uh[1], uh[2], uh[3]});
   l = __builtin_bit_cast(half8, u32x4v{ul[0], ul[1], ul[2], ul[3]});
+}
+
+// four values as (hi, lo) words: hi in the low half
+__device__ __forceinline__ uint4 hl4(float4 v) {
+  uint32_t h0, l0, h1, l1;
+  split2(v.x, v.y, h0, l0);
+  split2(v.z, v.w, h1, l1);
+  return make_uint4((h0 & 0xffffu) | (l0 << 16), (h0 >> 16) | (l0 & 0xffff0000u),
+                    (h1 & 0xffffu) | (l1 << 16), (h1 >> 16) | (l1 & 0xffff0000u));
+}
+// eight (hi, lo) words -> the hi and lo fragments
+__device__ __forceinline__ void hl_frag(const uint32_t (&w)[8], half8& h, half8& l) {
+  u32x4v uh, ul;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t a = w[2 * i], b = w[2 * i + 1];
+    uh[i] = (a & 0xffffu) | (b << 16);
+    ul[i] = (a >> 16) | (b & 0xffff0000u);
+  }
+  h = __builtin_bit_cast(half8, uh);
+  l = __builtin_bit_cast(half8, ul);
 }
 
 __device__ __forceinline__ f32x16 mfma4(float4 a, float4 b, f32x16 c) {
@@ -726,11 +756,20 @@ wgrad_kernel(int n, const float* __restrict__ x, const float* __restrict__ dz,
     const int k = (wave * NBW + b) * 32 + col;
     kr[b] = (k / G::KROW) * XROW + k % G::KROW;
   }
-  f32x16 acc[NBW];
+  // x3 where a row fills >= 60 % of its 16-pixel units: conv3's 17-pixel
+  // rows would leave 47 % of the slots empty (measured at batch 64: 18.8 us
+  // f32 against 20.2 x3)
+  constexpr bool X3 = DTUPD_X3 != 0 && 10 * G::OW >= 6 * 16 * ((G::OW + 15) / 16);
+  f32x16 acc[NBW], acc1[X3 ? NBW : 1];
 #pragma unroll
   for (int b = 0; b < NBW; ++b)
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[b][r] = 0.0f;
+  if constexpr (X3)
+#pragma unroll
+    for (int b = 0; b < NBW; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc1[b][r] = 0.0f;
   const int rows = n * G::OH;
   // a row's staging as loads into registers (fetch) and LDS stores (commit):
   // DB fetches row i + 1 before row i's MFMAs and commits it after them
@@ -752,9 +791,16 @@ wgrad_kernel(int n, const float* __restrict__ x, const float* __restrict__ dz,
     if (0 < PD && tid + 0 * NT < DT / 4) rd0 = dsrc_[0 * NT];                                     \
     if (1 < PD && tid + 1 * NT < DT / 4) rd1 = dsrc_[1 * NT];                                     \
   } while (0)
+  // x3: the staged values as (hi, lo) fp16 words (hl4), split once a stage
+  // instead of once a use
   auto put = [&](int buf, int i, float4 v) __attribute__((always_inline)) {
     if constexpr (NORM) v = norm4(v, nb, nm, ns, nt, in.slope);
-    reinterpret_cast<float4*>(xs[buf])[tid + i * NT] = v;
+    if constexpr (X3) reinterpret_cast<uint4*>(xs[buf])[tid + i * NT] = hl4(v);
+    else reinterpret_cast<float4*>(xs[buf])[tid + i * NT] = v;
+  };
+  auto putd = [&](int buf, int i, float4 v) __attribute__((always_inline)) {
+    if constexpr (X3) reinterpret_cast<uint4*>(ds[buf])[tid + i * NT] = hl4(v);
+    else reinterpret_cast<float4*>(ds[buf])[tid + i * NT] = v;
   };
   auto commit = [&](int buf) __attribute__((always_inline)) {
     if (0 < PX && tid + 0 * NT < XT / 4) put(buf, 0, rx0);
@@ -763,10 +809,40 @@ wgrad_kernel(int n, const float* __restrict__ x, const float* __restrict__ dz,
     if (3 < PX && tid + 3 * NT < XT / 4) put(buf, 3, rx3);
     if (4 < PX && tid + 4 * NT < XT / 4) put(buf, 4, rx4);
     if (5 < PX && tid + 5 * NT < XT / 4) put(buf, 5, rx5);
-    if (0 < PD && tid + 0 * NT < DT / 4) reinterpret_cast<float4*>(ds[buf])[tid] = rd0;
-    if (1 < PD && tid + 1 * NT < DT / 4) reinterpret_cast<float4*>(ds[buf])[tid + NT] = rd1;
+    if (0 < PD && tid + 0 * NT < DT / 4) putd(buf, 0, rd0);
+    if (1 < PD && tid + 1 * NT < DT / 4) putd(buf, 1, rd1);
   };
   auto compute = [&](int buf) __attribute__((always_inline)) {
+    if constexpr (X3) {
+      // 16 pixels a unit: A = dZ[ox0 + 8 kk + j][co], B = X[ox0 + 8 kk + j][k]
+      // (pixels past the row: A zero, B pixel 0's)
+      const uint32_t* xb = reinterpret_cast<const uint32_t*>(xs[buf]);
+      const uint32_t* db = reinterpret_cast<const uint32_t*>(ds[buf]);
+#pragma unroll 1
+      for (int ox0 = 0; ox0 < G::OW; ox0 += 16) {
+        uint32_t aw[8], xw[NBW][8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          const int ox = ox0 + 8 * kk + j;
+          const bool ok = ox < G::OW;
+          aw[j] = ok ? db[ox * 32 + col] : 0u;
+          const int xo = (ok ? ox : 0) * G::ST * G::CIN;
+#pragma unroll
+          for (int b = 0; b < NBW; ++b) xw[b][j] = xb[xo + kr[b]];
+        }
+        half8 ah, al;
+        hl_frag(aw, ah, al);
+#pragma unroll
+        for (int b = 0; b < NBW; ++b) {
+          half8 xh, xl;
+          hl_frag(xw[b], xh, xl);
+          acc[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, xh, acc[b], 0, 0, 0);
+          acc1[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah, xl, acc1[b], 0, 0, 0);
+          acc1[b] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al, xh, acc1[b], 0, 0, 0);
+        }
+      }
+      return;
+    }
     const float* xb = xs[buf];
     const float* db = ds[buf];
 #pragma unroll 2
@@ -805,6 +881,11 @@ wgrad_kernel(int n, const float* __restrict__ x, const float* __restrict__ dz,
     }
   }
 #undef DTUPD_FETCH
+  if constexpr (X3)
+#pragma unroll
+    for (int b = 0; b < NBW; ++b)
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[b][r] += acc1[b][r] * kLoInv;
   // D[co][k]: lane (k = block * 32 + col), rows co
   float* pp = part + (size_t)blockIdx.x * 32 * G::K;
 #pragma unroll
@@ -814,31 +895,54 @@ wgrad_kernel(int n, const float* __restrict__ x, const float* __restrict__ dz,
       pp[acc_row(r, kk) * G::K + (wave * NBW + b) * 32 + col] = acc[b][r];
 }
 
-// dw[i] = sum of the chunks' partials: a workgroup takes 32 outputs, eight
-// threads an output each summing every eighth chunk, then the eight sums in
-// a fixed order (deterministic)
-constexpr int kRedOut = 32, kRedWays = 8;
-__global__ void __launch_bounds__(kRedOut * kRedWays)
+// dw[i] = sum of the chunks' partials: a workgroup takes kRedCols float4
+// columns (4 outputs each), kRedWays threads a column each summing every
+// kRedWays-th chunk (two accumulators), then the ways in a fixed two-level
+// order (deterministic).  Few loads a thread, all of a column's chunks in
+// flight at once: the reduce is one memory round trip (round 6; the former
+// 8-way scalar form ran the conv1 partials at 1 TB/s).
+constexpr int kRedCols = 16, kRedWays = 64, kRedThreads = kRedCols * kRedWays;
+__global__ void __launch_bounds__(kRedThreads)
 wgrad_reduce_kernel(int chunks, int len, const float* __restrict__ part, float* __restrict__ dw) {
-  __shared__ float red[kRedWays][kRedOut];
-  const int o = threadIdx.x & (kRedOut - 1), w = threadIdx.x / kRedOut;
-  const int i = blockIdx.x * kRedOut + o;
-  float s0 = 0.0f, s1 = 0.0f;
-  if (i < len) {
+  __shared__ float4 red[kRedWays][kRedCols];
+  __shared__ float4 red2[8][kRedCols];
+  const int o = threadIdx.x & (kRedCols - 1), w = threadIdx.x / kRedCols;
+  const int len4 = len >> 2;
+  const int i4 = blockIdx.x * kRedCols + o;
+  float4 s0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f), s1 = s0;
+  if (i4 < len4) {
+    const float4* p = reinterpret_cast<const float4*>(part) + i4;
     int c = w;
     for (; c + kRedWays < chunks; c += 2 * kRedWays) {
-      s0 += part[(size_t)c * len + i];
-      s1 += part[(size_t)(c + kRedWays) * len + i];
+      const float4 a = p[(size_t)c * len4], b = p[(size_t)(c + kRedWays) * len4];
+      s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
+      s1.x += b.x; s1.y += b.y; s1.z += b.z; s1.w += b.w;
     }
-    if (c < chunks) s0 += part[(size_t)c * len + i];
+    if (c < chunks) {
+      const float4 a = p[(size_t)c * len4];
+      s0.x += a.x; s0.y += a.y; s0.z += a.z; s0.w += a.w;
+    }
   }
-  red[w][o] = s0 + s1;
+  red[w][o] = make_float4(s0.x + s1.x, s0.y + s1.y, s0.z + s1.z, s0.w + s1.w);
   __syncthreads();
-  if (w == 0 && i < len) {
-    float t = 0.0f;
+  if (w < 8) {
+    float4 t = red[8 * w][o];
 #pragma unroll
-    for (int k = 0; k < kRedWays; ++k) t += red[k][o];
-    dw[i] = t;
+    for (int k = 1; k < 8; ++k) {
+      const float4 v = red[8 * w + k][o];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    red2[w][o] = t;
+  }
+  __syncthreads();
+  if (w == 0 && i4 < len4) {
+    float4 t = red2[0][o];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) {
+      const float4 v = red2[k][o];
+      t.x += v.x; t.y += v.y; t.z += v.z; t.w += v.w;
+    }
+    reinterpret_cast<float4*>(dw)[i4] = t;
   }
 }
 
@@ -872,15 +976,31 @@ dgrad_kernel(int n, const float* __restrict__ dz, const float* __restrict__ w,
              float* __restrict__ dx) {
   using D = DGeom<G>;
   static_assert(G::CIN == 32, "dgrad for 32-channel inputs");
+  constexpr bool X3 = DTUPD_X3 != 0;
+  constexpr int KK = G::KS * G::KS;               // taps of W
   constexpr int CST = 36;                         // co stride of a W^T row
-  __shared__ __attribute__((aligned(16))) float wt[G::KS * G::KS * 32 * CST];
+  // f32: W^T as [tap][ci][co + 4]; x3: its B fragments, tap t, unit u (co
+  // 16 u ..), lane l at (t * 2 + u) * 64 + l, hi and lo
+  __shared__ __attribute__((aligned(16))) float wt[X3 ? 1 : KK * 32 * CST];
+  __shared__ half8 wth[X3 ? KK * 128 : 1], wtl[X3 ? KK * 128 : 1];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 31, kk = lane >> 5;
-  // W [co][kh][kw][ci] -> wt[kh * KS + kw][ci][co]
-  for (int i = tid; i < 32 * G::K; i += 64 * NW) {
-    const int co = i / G::K, r = i - co * G::K;
-    const int tap = r / 32, ci = r - tap * 32;
-    wt[(tap * 32 + ci) * CST + co] = w[i];
+  if constexpr (X3) {
+    // fragment (t, u, l): W[co = 16 u + 8 (l >> 5) + j][t][ci = l & 31], j < 8
+    for (int q = tid; q < KK * 128; q += 64 * NW) {
+      const int t = q >> 7, u = (q >> 6) & 1, l = q & 63;
+      const float* src = w + (size_t)(16 * u + 8 * (l >> 5)) * G::K + t * 32 + (l & 31);
+      const float4 a = make_float4(src[0], src[G::K], src[2 * G::K], src[3 * G::K]);
+      const float4 b = make_float4(src[4 * G::K], src[5 * G::K], src[6 * G::K], src[7 * G::K]);
+      split8(a, b, wth[q], wtl[q]);
+    }
+  } else {
+    // W [co][kh][kw][ci] -> wt[kh * KS + kw][ci][co]
+    for (int i = tid; i < 32 * G::K; i += 64 * NW) {
+      const int co = i / G::K, r = i - co * G::K;
+      const int tap = r / 32, ci = r - tap * 32;
+      wt[(tap * 32 + ci) * CST + co] = w[i];
+    }
   }
   __syncthreads();
   const int tiles = n * D::TPS;
@@ -896,24 +1016,57 @@ dgrad_kernel(int n, const float* __restrict__ dz, const float* __restrict__ w,
     const int idx = t * 32 + col;
     const int ic = idx < np ? idx : 0;
     const int a = ic / bcn, b = ic - a * bcn;
-    const float* dzs = dz + (size_t)s * G::OPIX * 32 + 4 * kk;
     f32x16 acc;
 #pragma unroll
     for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
-#pragma unroll 4
-    for (int tap = 0; tap < D::TAPS; ++tap) {
-      const int th = tap / D::T1, tw = tap - th * D::T1;
-      const int oy = a - th, ox = b - tw;
-      const bool ok = idx < np && oy >= 0 && oy < G::OH && ox >= 0 && ox < G::OW;
-      const float* src = dzs + (ok ? (oy * G::OW + ox) * 32 : 0);
-      const int kh = ph + D::ST * th, kw = pw + D::ST * tw;
-      const float* wrow = wt + ((kh * G::KS + kw) * 32 + col) * CST + 4 * kk;
+    if constexpr (X3) {
+      // unit u of a tap: A = dZ[o][16 u + 8 kk + 0 .. 7] (zero off the output)
+      const float* dzs = dz + (size_t)s * G::OPIX * 32 + 8 * kk;
+      f32x16 acc1;
 #pragma unroll
-      for (int c8 = 0; c8 < 4; ++c8) {
-        float4 av = *reinterpret_cast<const float4*>(src + 8 * c8);
-        if (!ok) av = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-        const float4 bv = *reinterpret_cast<const float4*>(wrow + 8 * c8);
-        acc = mfma4(av, bv, acc);
+      for (int r = 0; r < 16; ++r) acc1[r] = 0.0f;
+#pragma unroll 2
+      for (int tap = 0; tap < D::TAPS; ++tap) {
+        const int th = tap / D::T1, tw = tap - th * D::T1;
+        const int oy = a - th, ox = b - tw;
+        const bool ok = idx < np && oy >= 0 && oy < G::OH && ox >= 0 && ox < G::OW;
+        const float4* src = reinterpret_cast<const float4*>(dzs + (ok ? (oy * G::OW + ox) * 32 : 0));
+        const int wtap = (ph + D::ST * th) * G::KS + pw + D::ST * tw;
+        float4 av[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+          av[i] = src[(i >> 1) * 4 + (i & 1)];
+          if (!ok) av[i] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+        }
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          half8 xh, xl;
+          split8(av[2 * u], av[2 * u + 1], xh, xl);
+          const half8 bh = wth[(wtap * 2 + u) * 64 + lane], bl = wtl[(wtap * 2 + u) * 64 + lane];
+          acc = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, bh, acc, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(xh, bl, acc1, 0, 0, 0);
+          acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(xl, bh, acc1, 0, 0, 0);
+        }
+      }
+#pragma unroll
+      for (int r = 0; r < 16; ++r) acc[r] += acc1[r] * kLoInv;
+    } else {
+      const float* dzs = dz + (size_t)s * G::OPIX * 32 + 4 * kk;
+#pragma unroll 4
+      for (int tap = 0; tap < D::TAPS; ++tap) {
+        const int th = tap / D::T1, tw = tap - th * D::T1;
+        const int oy = a - th, ox = b - tw;
+        const bool ok = idx < np && oy >= 0 && oy < G::OH && ox >= 0 && ox < G::OW;
+        const float* src = dzs + (ok ? (oy * G::OW + ox) * 32 : 0);
+        const int kh = ph + D::ST * th, kw = pw + D::ST * tw;
+        const float* wrow = wt + ((kh * G::KS + kw) * 32 + col) * CST + 4 * kk;
+#pragma unroll
+        for (int c8 = 0; c8 < 4; ++c8) {
+          float4 av = *reinterpret_cast<const float4*>(src + 8 * c8);
+          if (!ok) av = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+          const float4 bv = *reinterpret_cast<const float4*>(wrow + 8 * c8);
+          acc = mfma4(av, bv, acc);
+        }
       }
     }
     float* dxs = dx + (size_t)s * G::IH * G::IW * 32;
@@ -1165,15 +1318,16 @@ int wgrad_chunks(int n) {
   return rows < wgrad_max_grid<G>() ? rows : wgrad_max_grid<G>();
 }
 
-template <class G, int NBW, int WAVES, bool NORM, bool DB = false>
+template <class G, int NBW, int WAVES, bool NORM, bool DB = (DTUPD_WG_DB != 0)>
 int launch_wgrad(int n, const float* x, const DtUpdBn& in, const float* dz, float* dw, float* work,
                  hipStream_t s) {
   const int chunks = wgrad_chunks<G>(n);
   hipLaunchKernelGGL((wgrad_kernel<G, NBW, WAVES, NORM, DB>), dim3(chunks), dim3(64 * WAVES), 0, s,
                      n, x, dz, work, in);
-  const int len = 32 * G::K;
-  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((len + kRedOut - 1) / kRedOut),
-                     dim3(kRedOut * kRedWays), 0, s, chunks, len, work, dw);
+  constexpr int len = 32 * G::K;
+  static_assert(len % 4 == 0, "float4 columns");
+  hipLaunchKernelGGL(wgrad_reduce_kernel, dim3((len / 4 + kRedCols - 1) / kRedCols),
+                     dim3(kRedThreads), 0, s, chunks, len, work, dw);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 
@@ -1249,7 +1403,7 @@ int dt_upd_conv_wgrad_bn(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t
                          const float* x, const DtUpdBn* in, const float* dz, float* dw,
                          float* work, void* stream) {
   const int l = layer_of(cin, ks, st, ih, iw);
-  if (!l || n < 1 || !x || !dz || !dw || !work) return DT_E_ARG;
+  if (!l || n < 1 || !x || !dz || !dw || !work || !aligned16(dw) || !aligned16(work)) return DT_E_ARG;
   if (in && (l == 1 || !in->mean_invstd || !in->bias || !in->gamma || !in->beta ||
              !aligned16(in->mean_invstd) || !aligned16(in->bias) || !aligned16(in->gamma) ||
              !aligned16(in->beta)))
@@ -1257,7 +1411,7 @@ int dt_upd_conv_wgrad_bn(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t
   hipStream_t s = (hipStream_t)stream;
   const DtUpdBn b = in ? *in : DtUpdBn{};
   switch (l) {
-    case 1: return launch_wgrad<L1, 1, 6, false, false>(n, x, b, dz, dw, work, s);
+    case 1: return launch_wgrad<L1, 1, 6, false, DTUPD_WG_DB1 != 0>(n, x, b, dz, dw, work, s);
     case 2:
       return in ? launch_wgrad<L2, 2, 8, true>(n, x, b, dz, dw, work, s)
                 : launch_wgrad<L2, 2, 8, false>(n, x, b, dz, dw, work, s);

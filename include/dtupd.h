@@ -110,8 +110,8 @@ int64_t dt_upd_wgrad_work_floats(int32_t cin, int32_t ks, int32_t st, int32_t n,
 
 /* dw[co][k] = sum over the n * OH * OW output pixels of dz[pixel][co] * the
  * pixel's input patch x[...][k] (torch.nn.grad.conv2d_weight).
- *   dz device f32 [n, OH, OW, 32];  dw device f32 [32, K] out;
- *   work device f32 [dt_upd_wgrad_work_floats(...)] */
+ *   dz device f32 [n, OH, OW, 32];  dw device f32 [32, K] out, 16-B aligned;
+ *   work device f32 [dt_upd_wgrad_work_floats(...)], 16-B aligned */
 int dt_upd_conv_wgrad(int32_t cin, int32_t ks, int32_t st, int32_t n, int32_t ih, int32_t iw,
                       const float* x, const float* dz, float* dw, float* work, void* stream);
 

@@ -16,6 +16,7 @@ for i in $(seq 1 "$R"); do
     python3 -c "
 import json; d=json.load(open('gpurun_out/ab_${v}_${i}.json'))
 r=d['roofline']
-print('$v', 'value %.4gM' % (d['value']/1e6), 'ms/step %.4f' % d['ms_per_step'], 'kernel ms %.4f' % r['avg_kernel_ms'], 'frac %.3f' % r['frac'])"
+ph=d.get('phases_ms') or {}
+print('$v', 'value %.4gM' % (d['value']/1e6), 'ms/step %.4f' % d['ms_per_step'], 'kernel ms %.4f' % r['avg_kernel_ms'], 'frac %.3f' % r['frac'], ('update ms %.4f' % ph['update']) if 'update' in ph else '')"
   done
 done

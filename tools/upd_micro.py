@@ -14,7 +14,7 @@ OUT = os.path.join(ROOT, 'tools', 'variants')
 SKIPS = {'full': 0, 'no_a_loads': 1, 'no_w_stage': 2, 'no_merge': 4, 'no_ksum': 8, 'bare': 15,
          'no_part_loads': 16, 'no_chain_merge': 32, 'no_chain_both': 48}
 # other variants: extra -D flags (the f32 MFMA forward, forward K slices)
-EXTRA = {'f32': ['-DDTUPD_X3=0'], 'f32_bare': ['-DDTUPD_X3=0', '-DDTUPD_SKIP=15'],
+EXTRA = {'f32': ['-DDTUPD_X3=0'], 'wg_nodb': ['-DDTUPD_WG_DB=0'], 'wg_db1': ['-DDTUPD_WG_DB1=1'], 'f32_bare': ['-DDTUPD_X3=0', '-DDTUPD_SKIP=15'],
          'ks_4_4_4_8': ['-DDTUPD_KS1=4', '-DDTUPD_KS2=4', '-DDTUPD_KS3=4', '-DDTUPD_KS4=8'],
          'ks_1_1_2_4': ['-DDTUPD_KS1=1', '-DDTUPD_KS2=1', '-DDTUPD_KS3=2', '-DDTUPD_KS4=4']}
 LAYERS = {1: (3, 8, 2, 120, 160), 2: (32, 4, 2, 57, 77), 3: (32, 4, 2, 27, 37),
@@ -139,7 +139,7 @@ def run(n, reps, variants=''):
                         assert L.dt_upd_bn_finish(z.numel() // 32, 0, z.data_ptr(),
                                                   ctypes.byref(hand), y.data_ptr(), s) == 0
                     t['finish'] = timeit(torch, finish, reps)
-            if name in ('full', 'f32'):
+            if name in ('full', 'f32', 'wg_nodb', 'wg_db1'):
                 ww = torch.empty(int(L.dt_upd_wgrad_work_floats(*a)), device=dev)
                 dw = torch.empty_like(w)
 
