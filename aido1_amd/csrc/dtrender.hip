@@ -1983,7 +1983,10 @@ static int render_launch(dt_handle* h, const dt_render_io* io, const dt_render_i
                 ? (uint32_t*)h->render_sched : nullptr;
   if (a.sched) {
     if (!h->render_done)
-      HIP_OR_FAIL(h, hipEventCreateWithFlags(&h->render_done, hipEventDisableTiming));
+      // ordering on this device only: no system-scope fence (with one, the
+      // record after every launch cost the config-3 bench 2 % of its rate)
+      HIP_OR_FAIL(h, hipEventCreateWithFlags(&h->render_done,
+                                             hipEventDisableTiming | hipEventDisableSystemFence));
     if (h->render_pending && (hipStream_t)stream != h->render_stream)
       HIP_OR_FAIL(h, hipStreamWaitEvent((hipStream_t)stream, h->render_done, 0));
   }
