@@ -22,7 +22,7 @@ SOURCES = ['dtsim.hip', 'dtrender.hip', 'dtreplay.hip', 'dtactor.hip', 'dtconv.h
 HEADERS = ['dtsim_common.h', 'dtrender.h', 'dtsync.h', 'dtconv_common.h']
 PUBLIC_HEADERS = ['dtsim.h', 'dtreplay.h', 'dtactor.h', 'dttrain.h', 'dtupd.h', 'dthead.h']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
-ABI_VERSION = 11
+ABI_VERSION = 12
 
 HIP_FLAGS = ['--offload-arch=gfx950', '-O3', '-fPIC', '-shared', '-std=c++17',
              '-ffp-contract=off', '-munsafe-fp-atomics']
@@ -249,6 +249,10 @@ def bind(L):
                                                vp]),
         'dt_upd_linear_wgrad': (ctypes.c_int, [i32, i32, i32, vp, vp, vp, ctypes.c_float, vp,
                                                vp, vp]),
+        'dt_upd_linear_fwd_drop': (ctypes.c_int, [i32, i32, i32, vp, vp, ctypes.c_float, vp, vp,
+                                                  vp, i32, ctypes.c_float, vp, vp, vp]),
+        'dt_upd_linear_dgrad_drop': (ctypes.c_int, [i32, i32, i32, vp, vp, vp, ctypes.c_float,
+                                                    vp, ctypes.c_float, vp, vp]),
         'dt_soft_update': (ctypes.c_int, [i32, vp, vp, f64, vp]),
         # dthead.h
         'dt_mlp_fwd': (ctypes.c_int, [ctypes.POINTER(DtMlp), vp, vp, vp, vp, vp]),

@@ -133,6 +133,15 @@ class _Seq(nn.Module):       # MetaNet: ".internal_modules.<i>"
                     x = train_ops.conv_leaky_bn(x, m.kernel, mods[i + 1], mods[i + 2])
                     i += 3
                     continue
+            drop = 0.0
+            if (self.fused_tail and isinstance(m, nn.Dropout) and i + 1 < k
+                    and isinstance(mods[i + 1], _Lin) and x.is_cuda):
+                from aido1_amd import train_ops
+                if train_ops.FOLD_DROPOUT and train_ops.linear_applicable(x, mods[i + 1].linear):
+                    # the dropout folded into the linear's kernels (dtupd.h *_drop)
+                    drop = float(m.p) if m.training else 0.0
+                    i += 1
+                    m = mods[i]
             if self.fused_tail and isinstance(m, _Lin) and x.is_cuda:
                 from aido1_amd import train_ops
                 if train_ops.linear_applicable(x, m.linear):
@@ -141,10 +150,10 @@ class _Seq(nn.Module):       # MetaNet: ".internal_modules.<i>"
                     # gradient off the sign of the saved output, which is only
                     # the input's sign for a non-negative slope
                     if isinstance(act, nn.LeakyReLU) and act.negative_slope >= 0:
-                        x = train_ops.linear(x, m.linear, float(act.negative_slope))
+                        x = train_ops.linear(x, m.linear, float(act.negative_slope), drop=drop)
                         i += 2
                     else:
-                        x = train_ops.linear(x, m.linear)
+                        x = train_ops.linear(x, m.linear, drop=drop)
                         i += 1
                     continue
             if isinstance(m, nn.BatchNorm2d) and getattr(m, '_dt_updates', 1) != 1:

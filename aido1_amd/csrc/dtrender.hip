@@ -282,6 +282,23 @@ struct View {  // f32 camera frame of one env
   float cx, cz, dirx, dirz, rx, rz;
 };
 
+// the thread index, opaque to the compiler: with several decisions a
+// workgroup (DTSIM_RENDER_SEQ) it would otherwise hoist tid-derived addresses
+// out of the decision loop and spill them
+__device__ __forceinline__ int opaque_tid() {
+  int t = (int)threadIdx.x;
+#if DTSIM_RENDER_SEQ
+  asm volatile("" : "+v"(t));
+#endif
+  return t;
+}
+
+// DTSIM_RENDER_SEQ: a dt_render2/3 workgroup renders its env's decisions one
+// after the other (one prologue and one dispatch for the group) instead of
+// one workgroup an (env, decision)
+#ifndef DTSIM_RENDER_SEQ
+#define DTSIM_RENDER_SEQ 0
+#endif
 struct RenderArgs {
   const double* x;
   const double* z;
@@ -388,7 +405,7 @@ struct RenderLds {
   uint32_t pal_swar[PAL_N];
   float pal_gray[PAL_N];
   uint32_t bits_lo, bits_hi;  // colour bits of raster bytes 0-3 / 4-7 (one byte each)
-  View view;
+  View view[3];         // the camera of each decision the workgroup renders
   int32_t cnt[kNCnt];
   int32_t env;          // this workgroup's env (the dispatch order's entry)
   unsigned long long t0;  // shader clock at entry (the env's recorded cost)
@@ -754,7 +771,7 @@ __device__ __forceinline__ void quad_masks(const RenderLds& S, const Slots<kSpil
 template <bool kSpill>
 __device__ __forceinline__ void canny(const RenderArgs& a, RenderLds& S, int e,
                                                 int nlist) {
-  const int tid = threadIdx.x;
+  const int tid = opaque_tid();
   constexpr int T = kRenderThreads;
   const LineDev& L = a.line;
   Slots<kSpill> sl{S, a.spill + (size_t)e * kSpillHalves, a.spill + (size_t)e * kSpillHalves + 4 * NW,
@@ -934,7 +951,7 @@ __device__ __forceinline__ void canny(const RenderArgs& a, RenderLds& S, int e,
 template <bool kSpill, bool kIdx, bool kBigR>
 __device__ __forceinline__ void write_outputs(const RenderArgs& a, RenderLds& S, int e,
                                               uint8_t* mbase, int half) {
-  const int tid = threadIdx.x;
+  const int tid = opaque_tid();
   constexpr int T = kRenderThreads;
   const LineDev& L = a.line;
   const Slots<kSpill> sl{S, a.spill + (size_t)e * kSpillHalves,
@@ -1128,7 +1145,11 @@ __device__ __forceinline__ void sched_build(const RenderArgs& a, RenderLds& S, u
 
 // the builder's ticket
 __device__ __forceinline__ uint32_t sched_builder(const RenderArgs& a) {
+#if DTSIM_RENDER_SEQ
+  return (uint32_t)(a.n - kSchedTail);             // one block an env: n > kSchedTail
+#else
   return (uint32_t)(a.parts * a.n - kSchedTail);   // dt_render: n > kSchedTail
+#endif
 }
 
 // exit of a workgroup: its cost (thread 0, no wait); the builder sorts
@@ -1146,12 +1167,13 @@ __device__ __forceinline__ void sched_exit(const RenderArgs& a, RenderLds& S, in
 
 // One env of render_kernel.
 template <bool kIdx, bool kBigR>
-__device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, int e, int half
+__device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, int e, int half,
+                                           int vi
 #ifdef DTSIM_EARLY_MARKS
                                            , const float4 (&mq)[4]
 #endif
 ) {
-  const int tid = threadIdx.x;
+  const int tid = opaque_tid();
   constexpr int T = kRenderThreads;
   const LineDev& L = a.line;
   const int nmark = a.n_yellow + a.n_white;
@@ -1163,7 +1185,7 @@ __device__ __forceinline__ void render_env(const RenderArgs& a, RenderLds& S, in
 #endif
   RENT(4);
   int32_t* const C = S.cnt;
-  const View V = S.view;
+  const View V = S.view[vi];
   lds_u32* const img = (lds_u32*)S.img;
 #ifndef DTSIM_EARLY_MARKS
   // the marking segments' loads (L2-resident), first used after the background
@@ -1439,9 +1461,15 @@ render_kernel(RenderArgs a) {
   for (int i = tid; i < a.width * a.height; i += kRenderThreads) S.kind[i] = a.kind[i];
   // the camera frame, once per workgroup (wave 1; wave 0 has the palette), of
   // the env the dispatch order gives this block
-  // dt_render2: blocks 2b and 2b + 1 render env perm[b] of the two decisions
+  // dt_render2: blocks 2b and 2b + 1 render env perm[b] of the two decisions;
+  // DTSIM_RENDER_SEQ: block b renders env perm[b] of every decision in turn
+#if DTSIM_RENDER_SEQ
+  const int nseq = a.parts, blk = (int)blockIdx.x, half0 = 0;
+#else
+  const int nseq = 1;
   const int blk = (int)blockIdx.x / a.parts;
-  const int half = (int)blockIdx.x - blk * a.parts;
+  const int half0 = (int)blockIdx.x - blk * a.parts;
+#endif
   int e = blk;
 #ifdef DTSIM_EARLY_MARKS
   float4 mq[4];
@@ -1455,19 +1483,22 @@ render_kernel(RenderArgs a) {
     }
   }
 #endif
-  if (tid == 64) {
+  if (tid >= 64 && tid < 64 + nseq) {
+    const int vi = tid - 64, half = half0 + vi;
     if (a.sched) {
       const int p = sched_perm(a, a.launch)[blk];
       e = (unsigned)p < (unsigned)a.n ? p : blk;   // (always a permutation)
     }
-    S.env = e;
-    S.t0 = __builtin_amdgcn_s_memtime();
+    if (vi == 0) {
+      S.env = e;
+      S.t0 = __builtin_amdgcn_s_memtime();
+    }
     if (half) {
       const size_t n = (size_t)a.n;
       const double* ps = half == 1 ? a.pose2 : a.pose3;
-      S.view = view_of(ps[e], ps[n + e], ps[2 * n + e], a.cam_fwd);
+      S.view[vi] = view_of(ps[e], ps[n + e], ps[2 * n + e], a.cam_fwd);
     } else {
-      S.view = view_of(a.x[e], a.z[e], a.angle[e], a.cam_fwd);
+      S.view[vi] = view_of(a.x[e], a.z[e], a.angle[e], a.cam_fwd);
     }
   }
   __syncthreads();
@@ -1476,11 +1507,18 @@ render_kernel(RenderArgs a) {
   RENSTAMP(16, t16);
   RENSTAMP(17, t17);
 #endif
-  render_env<kIdx, kBigR>(a, S, e, half
+  for (int vi = 0; vi < nseq; ++vi) {
+    if (vi > 0) {   // the previous decision's outputs are read out of LDS: reset
+      __syncthreads();
+      if (tid < kNCnt) S.cnt[tid] = 0;
+      __syncthreads();
+    }
+    render_env<kIdx, kBigR>(a, S, e, half0 + vi, vi
 #ifdef DTSIM_EARLY_MARKS
-             , mq
+               , mq
 #endif
-  );
+    );
+  }
   if (a.sched) sched_exit(a, S, e);
 }
 
@@ -2008,7 +2046,7 @@ static int render_launch(dt_handle* h, const dt_render_io* io, const dt_render_i
     a.fresh3 = io3->fresh;
     a.masks3 = io3->masks;
   }
-  const int grid = a.parts * h->n;
+  const int grid = DTSIM_RENDER_SEQ ? h->n : a.parts * h->n;
   const bool big_r = a.line.dil_r >= 2;
   auto* kern = a.index ? (big_r ? render_kernel<true, true> : render_kernel<true, false>)
                        : (big_r ? render_kernel<false, true> : render_kernel<false, false>);

@@ -303,38 +303,75 @@ update_kernel(double* sum, double* mn, double* maxp, int32_t* winner, int32_t* e
 // reduce(0, len - 1) of segment_tree.py:37-74 for the sum tree: the recursion
 // with start == node_start peels exact left children, combined right-nested:
 // a1 + (a2 + (... + ak)).
+// The node addresses depend only on `end` (cap a power of two: at depth d the
+// path's node covers 2^(lg - d) leaves; `end` is its last leaf -> take it and
+// stop; `end` in its right half -> take its left child), so every load is
+// issued before the first is used: one memory latency, not one a level, and
+// the same values summed in the same order.
 __device__ double prefix_range_sum(const double* sum, int64_t cap, int64_t end) {
+  const int lg = 63 - __builtin_clzll((unsigned long long)cap);
   double vals[kMaxDepth];
-  int k = 0;
-  int64_t node = 1, ns = 0, ne = cap - 1;
-  while (true) {
-    if (end == ne) {
-      vals[k++] = sum[node];
-      break;
+  bool on[kMaxDepth];
+  bool done = false;
+#pragma unroll
+  for (int d = 0; d < kMaxDepth; ++d) {
+    const int rem = lg - d;
+    bool take = false;
+    int64_t at = 0;
+    if (!done && rem >= 0) {
+      const int64_t node = (cap + end) >> rem;
+      const int64_t ones = (int64_t(1) << rem) - 1;
+      if ((end & ones) == ones) {
+        take = true;
+        at = node;
+        done = true;
+      } else if ((end >> (rem - 1)) & 1) {
+        take = true;
+        at = 2 * node;
+      }
     }
-    const int64_t mid = (ns + ne) / 2;
-    if (end <= mid) {
-      node = 2 * node;
-      ne = mid;
-    } else {
-      vals[k++] = sum[2 * node];
-      node = 2 * node + 1;
-      ns = mid + 1;
-    }
+    on[d] = take;
+    vals[d] = take ? sum[at] : 0.0;
   }
-  double acc = vals[k - 1];
-  for (int q = k - 2; q >= 0; --q) acc = vals[q] + acc;
+  double acc = 0.0;
+  bool first = true;
+#pragma unroll
+  for (int d = kMaxDepth - 1; d >= 0; --d)
+    if (on[d]) {
+      acc = first ? vals[d] : vals[d] + acc;
+      first = false;
+    }
   return acc;
 }
+
+// The top levels of the sum tree (nodes [1, kTopNodes)) are staged in LDS by
+// the whole workgroup, all loads in flight at once, while thread 0 forms the
+// range sum; the descent then walks those levels in LDS and only the deeper
+// ones in global memory (segment_tree.py:125-131's comparisons and order).
+constexpr int kTopNodes = 2048;
 
 __global__ void __launch_bounds__(kSampleThreads)
 sample_kernel(const double* sum, const double* mn, int64_t cap, int64_t len, int32_t batch,
               const double* u, double beta, int64_t* idx_out, double* w_out) {
   __shared__ double s_range, s_total, s_maxw;
+  __shared__ double s_top[kTopNodes];
+  const int64_t top = 2 * cap < kTopNodes ? 2 * cap : kTopNodes;
+  {
+    constexpr int kPer = kTopNodes / kSampleThreads;
+    double v[kPer];
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) {
+      const int64_t nd = threadIdx.x + q * kSampleThreads;
+      v[q] = nd >= 1 && nd < top ? sum[nd] : 0.0;
+    }
+#pragma unroll
+    for (int q = 0; q < kPer; ++q) s_top[threadIdx.x + q * kSampleThreads] = v[q];
+  }
   if (threadIdx.x == 0) {
+    const double total = sum[1], mn1 = mn[1];
     s_range = prefix_range_sum(sum, cap, len - 2);
-    s_total = sum[1];
-    const double p_min = mn[1] / s_total;                         // buffers.py:226
+    s_total = total;
+    const double p_min = mn1 / total;                               // buffers.py:226
     s_maxw = pow(p_min * (double)len, -beta);                      // :227
   }
   __syncthreads();
@@ -343,7 +380,7 @@ sample_kernel(const double* sum, const double* mn, int64_t cap, int64_t len, int
   double mass = u[i] * s_range;                                    // :180
   int64_t node = 1;
   while (node < cap) {                                             // segment_tree.py:125-131
-    const double l = sum[2 * node];
+    const double l = 2 * node < top ? s_top[2 * node] : sum[2 * node];
     if (l > mass) {
       node = 2 * node;
     } else {

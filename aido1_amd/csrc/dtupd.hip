@@ -1090,6 +1090,23 @@ dgrad_kernel(int n, const float* __restrict__ dz, const float* __restrict__ w,
 // lin_reduce_kernel adds the partials in index order plus the bias.
 constexpr int kLinWaves = 4;
 
+// The dropout before the linear (flatten -> dropout -> linear, config.json),
+// folded into its three kernels: u [m, k] uniforms in [0, 1) (or null: no
+// dropout), an element kept where u >= p and then scaled by 1 / (1 - p), as
+// F.dropout's bernoulli(1 - p) mask; the same u in the forward (on x's
+// loads), the input gradient (on its stores) and the weight gradient (on x's
+// loads).
+struct Drop {
+  const float* u;
+  float p, scale;
+  float* xd;   // forward: the dropped input written out (the n0 = 0 tiles), or null
+};
+__device__ __forceinline__ float4 drop4(float4 v, const float* u, float p, float scale) {
+  const float4 q = *reinterpret_cast<const float4*>(u);
+  return make_float4(q.x >= p ? v.x * scale : 0.0f, q.y >= p ? v.y * scale : 0.0f,
+                     q.z >= p ? v.z * scale : 0.0f, q.w >= p ? v.w * scale : 0.0f);
+}
+
 // torch's leaky_relu backward on the output (same sign as the input for slope > 0)
 __device__ __forceinline__ float4 leaky_grad4(float4 g, float4 y, float slope) {
   return make_float4(y.x > 0.0f ? g.x : g.x * slope, y.y > 0.0f ? g.y : g.y * slope,
@@ -1098,7 +1115,7 @@ __device__ __forceinline__ float4 leaky_grad4(float4 g, float4 y, float slope) {
 
 __global__ void __launch_bounds__(64 * kLinWaves)
 lin_fwd_kernel(int m, int n, int k, int chunk, const float* __restrict__ x,
-               const float* __restrict__ w, float* __restrict__ part) {
+               const float* __restrict__ w, float* __restrict__ part, Drop dr) {
   __shared__ float red[kLinWaves - 1][16][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 31, kk = lane >> 5;
@@ -1117,6 +1134,10 @@ lin_fwd_kernel(int m, int n, int k, int chunk, const float* __restrict__ x,
 #pragma unroll 4
   for (int st = s0; st < s1; ++st) {
     float4 a = *reinterpret_cast<const float4*>(xr + 8 * st);
+    if (dr.u) {
+      a = drop4(a, dr.u + (xr - x) + 8 * st, dr.p, dr.scale);
+      if (dr.xd && n0 == 0 && mok) *reinterpret_cast<float4*>(dr.xd + (xr - x) + 8 * st) = a;
+    }
     if (!mok) a = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
     const float4 b = *reinterpret_cast<const float4*>(wr + 8 * st);
     acc = mfma4(a, b, acc);
@@ -1163,7 +1184,7 @@ lin_reduce_kernel(int mn, int n, int splits, const float* __restrict__ part,
 // four waves a quarter of n each, summed through LDS
 __global__ void __launch_bounds__(64 * kLinWaves)
 lin_dgrad_kernel(int m, int n, int k, const float* __restrict__ dy, const float* __restrict__ w,
-                 const float* __restrict__ yact, float slope, float* __restrict__ dx) {
+                 const float* __restrict__ yact, float slope, float* __restrict__ dx, Drop dr) {
   __shared__ float red[kLinWaves - 1][16][64];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 31, kk = lane >> 5;
@@ -1174,6 +1195,13 @@ lin_dgrad_kernel(int m, int n, int k, const float* __restrict__ dy, const float*
   const bool mok = m0 + col < m;
   const float* dyr = dy + (size_t)(mok ? m0 + col : 0) * n + 4 * kk;
   const float* wc = w + (size_t)(4 * kk) * k + k0 + col;   // W[n][k0 + col], n = 8 st + 4 kk + e
+  float um[16];   // the dropout uniforms of this lane's dx elements, loaded up front
+  if (dr.u)
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int mm = m0 + acc_row(r, kk);
+      um[r] = mm < m ? dr.u[(size_t)mm * k + k0 + col] : 0.0f;
+    }
   f32x16 acc;
 #pragma unroll
   for (int r = 0; r < 16; ++r) acc[r] = 0.0f;
@@ -1198,7 +1226,10 @@ lin_dgrad_kernel(int m, int n, int k, const float* __restrict__ dy, const float*
 #pragma unroll
     for (int r = 0; r < 16; ++r) {
       const int mm = m0 + acc_row(r, kk);
-      if (mm < m) dx[(size_t)mm * k + k0 + col] = acc[r];
+      if (mm < m) {
+        const size_t at = (size_t)mm * k + k0 + col;
+        dx[at] = dr.u ? (um[r] >= dr.p ? acc[r] * dr.scale : 0.0f) : acc[r];
+      }
     }
   }
 }
@@ -1440,31 +1471,53 @@ int64_t dt_upd_linear_work_floats(int32_t m, int32_t n, int32_t k) {
   return (int64_t)lin_splits(m, n, k) * m * n;
 }
 
-int dt_upd_linear_fwd(int32_t m, int32_t n, int32_t k, const float* x, const float* w,
-                      const float* b, int32_t leaky, float slope, float* y, float* work,
-                      void* stream) {
-  if (!lin_shape_ok(m, n, k) || !x || !w || !y || !work || !aligned16(x) || !aligned16(w))
+static bool drop_ok(const float* u, float p) {
+  return !u || (aligned16(u) && p >= 0.0f && p < 1.0f);
+}
+static Drop drop_of(const float* u, float p, float* xd = nullptr) {
+  return Drop{u, p, u ? 1.0f / (1.0f - p) : 1.0f, u ? xd : nullptr};
+}
+
+int dt_upd_linear_fwd_drop(int32_t m, int32_t n, int32_t k, const float* x, const float* u,
+                           float p, float* xd, const float* w, const float* b, int32_t leaky,
+                           float slope, float* y, float* work, void* stream) {
+  if (!lin_shape_ok(m, n, k) || !x || !w || !y || !work || !aligned16(x) || !aligned16(w) ||
+      !drop_ok(u, p) || (xd && !aligned16(xd)))
     return DT_E_ARG;
   hipStream_t s = (hipStream_t)stream;
   const int splits = lin_splits(m, n, k);
   const int tiles = (n / 32) * ((m + 31) / 32);
   const int steps = k / 8, chunk = (steps + splits * kLinWaves - 1) / (splits * kLinWaves);
   hipLaunchKernelGGL(lin_fwd_kernel, dim3(tiles * splits), dim3(64 * kLinWaves), 0, s, m, n, k,
-                     chunk, x, w, work);
+                     chunk, x, w, work, drop_of(u, p, xd));
   const int mn = m * n;
   hipLaunchKernelGGL(lin_reduce_kernel, dim3((mn + 255) / 256), dim3(256), 0, s, mn, n, splits,
                      work, b, (int)(leaky != 0), slope, y);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
 }
 
-int dt_upd_linear_dgrad(int32_t m, int32_t n, int32_t k, const float* dy, const float* w,
-                        const float* yact, float slope, float* dx, void* stream) {
-  if (!lin_shape_ok(m, n, k) || !dy || !w || !dx || !aligned16(dy) || (yact && !aligned16(yact)))
+int dt_upd_linear_fwd(int32_t m, int32_t n, int32_t k, const float* x, const float* w,
+                      const float* b, int32_t leaky, float slope, float* y, float* work,
+                      void* stream) {
+  return dt_upd_linear_fwd_drop(m, n, k, x, nullptr, 0.0f, nullptr, w, b, leaky, slope, y, work,
+                                stream);
+}
+
+int dt_upd_linear_dgrad_drop(int32_t m, int32_t n, int32_t k, const float* dy, const float* w,
+                             const float* yact, float slope, const float* u, float p, float* dx,
+                             void* stream) {
+  if (!lin_shape_ok(m, n, k) || !dy || !w || !dx || !aligned16(dy) || (yact && !aligned16(yact)) ||
+      !drop_ok(u, p))
     return DT_E_ARG;
   const int grid = ((m + 31) / 32) * (k / 32);
   hipLaunchKernelGGL(lin_dgrad_kernel, dim3(grid), dim3(64 * kLinWaves), 0, (hipStream_t)stream,
-                     m, n, k, dy, w, yact, slope, dx);
+                     m, n, k, dy, w, yact, slope, dx, drop_of(u, p));
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
+int dt_upd_linear_dgrad(int32_t m, int32_t n, int32_t k, const float* dy, const float* w,
+                        const float* yact, float slope, float* dx, void* stream) {
+  return dt_upd_linear_dgrad_drop(m, n, k, dy, w, yact, slope, nullptr, 0.0f, dx, stream);
 }
 
 int dt_upd_linear_wgrad(int32_t m, int32_t n, int32_t k, const float* dy, const float* x,

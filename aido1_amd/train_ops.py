@@ -482,13 +482,15 @@ def linear_applicable(x, lin):
 
 class _UpdLinear(torch.autograd.Function):
     """y = x w^T + b (torch.nn.Linear), optionally through the following
-    LeakyReLU (slope not None), with K split over waves and summed in a fixed
-    order; backward dx and dw / db on their own MFMA kernels, the LeakyReLU's
-    gradient taken from the saved output (include/dtupd.h).  Where the library
-    GEMM took one tile a workgroup over all of K at batch 64."""
+    LeakyReLU (slope not None) and after a dropout folded in (u: uniforms,
+    p: the rate; include/dtupd.h *_drop), with K split over waves and summed
+    in a fixed order; backward dx and dw / db on their own MFMA kernels, the
+    LeakyReLU's gradient taken from the saved output, the dropout mask
+    re-read from u.  Where the library GEMM took one tile a workgroup over all
+    of K at batch 64."""
 
     @staticmethod
-    def forward(ctx, x, w, b, slope):
+    def forward(ctx, x, w, b, slope, u, p, grads):
         x = x.contiguous()
         w = w.contiguous()
         m, k = x.shape
@@ -497,50 +499,86 @@ class _UpdLinear(torch.autograd.Function):
         y = torch.empty(m, n, device=x.device, dtype=x.dtype)
         work = torch.empty(int(L.dt_upd_linear_work_floats(m, n, k)), device=x.device)
         act = slope is not None
-        rc = L.dt_upd_linear_fwd(m, n, k, x.data_ptr(), w.data_ptr(), b.data_ptr(), int(act),
-                                 float(slope) if act else 0.0, y.data_ptr(), work.data_ptr(),
-                                 _stream(x.device))
+        # the dropped input for the weight gradient (written by the forward)
+        # (grads: autograd is recording -- Function.forward itself runs with it off)
+        want = grads and (ctx.needs_input_grad[1] or ctx.needs_input_grad[2])
+        xd = torch.empty_like(x) if (u is not None and want) else None
+        rc = L.dt_upd_linear_fwd_drop(m, n, k, x.data_ptr(), u.data_ptr() if u is not None else None,
+                                      float(p), xd.data_ptr() if xd is not None else None,
+                                      w.data_ptr(), b.data_ptr(), int(act),
+                                      float(slope) if act else 0.0, y.data_ptr(), work.data_ptr(),
+                                      _stream(x.device))
         if rc != 0:
-            raise _lib.DtError('dt_upd_linear_fwd failed (%d)' % rc)
-        if act:
-            ctx.save_for_backward(x, w, y)
-        else:
-            ctx.save_for_backward(x, w)
-        ctx.slope = slope
+            raise _lib.DtError('dt_upd_linear_fwd_drop failed (%d)' % rc)
+        ctx.save_for_backward(x if u is None else xd, w, y if act else None, u)
+        ctx.slope, ctx.p = slope, float(p)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        saved = ctx.saved_tensors
-        x, w = saved[0], saved[1]
-        yact = saved[2].data_ptr() if ctx.slope is not None else None
+        xs, w, yv, u = ctx.saved_tensors
+        yact = yv.data_ptr() if yv is not None else None
+        up = u.data_ptr() if u is not None else None
         slope = float(ctx.slope) if ctx.slope is not None else 0.0
         dy = dy.contiguous()
-        m, k = x.shape
+        m, k = dy.shape[0], w.shape[1]
         n = w.shape[0]
         L = _lib.lib()
-        s = _stream(x.device)
+        s = _stream(dy.device)
         dx = dw = db = None
         if ctx.needs_input_grad[0]:
-            dx = torch.empty_like(x)
-            rc = L.dt_upd_linear_dgrad(m, n, k, dy.data_ptr(), w.data_ptr(), yact, slope,
-                                       dx.data_ptr(), s)
+            dx = torch.empty(m, k, device=dy.device, dtype=dy.dtype)
+            rc = L.dt_upd_linear_dgrad_drop(m, n, k, dy.data_ptr(), w.data_ptr(), yact, slope, up,
+                                            ctx.p, dx.data_ptr(), s)
             if rc != 0:
-                raise _lib.DtError('dt_upd_linear_dgrad failed (%d)' % rc)
+                raise _lib.DtError('dt_upd_linear_dgrad_drop failed (%d)' % rc)
         if ctx.needs_input_grad[1] or ctx.needs_input_grad[2]:
             dw = torch.empty_like(w)
-            db = torch.empty(n, device=x.device, dtype=x.dtype)
-            rc = L.dt_upd_linear_wgrad(m, n, k, dy.data_ptr(), x.data_ptr(), yact, slope,
+            db = torch.empty(n, device=dy.device, dtype=dy.dtype)
+            # xs: the input, or with a dropout the dropped input the forward wrote
+            rc = L.dt_upd_linear_wgrad(m, n, k, dy.data_ptr(), xs.data_ptr(), yact, slope,
                                        dw.data_ptr(), db.data_ptr(), s)
             if rc != 0:
                 raise _lib.DtError('dt_upd_linear_wgrad failed (%d)' % rc)
-        return dx, dw, db, None
+        return dx, dw, db, None, None, None, None
 
 
-def linear(x, lin, slope=None):
+# The dropout uniforms of one update drawn in ONE launch: the trainer opens a
+# pool of `sites` [m, k] slices (drop_pool) before its stages and every folded
+# dropout takes the next slice; outside a pool (or past its end) a site draws
+# its own torch.rand.  The slices are static tensors, so a captured graph
+# replays the single draw (graph-safe Philox offsets) and the sites read it.
+_DROP = {'pool': None, 'next': 0}
+FOLD_DROPOUT = True   # fold a dropout into the linear after it (A/B switch, tools/update_only.py)
+
+
+@contextlib.contextmanager
+def drop_pool(sites, m, k, device):
+    pool = torch.rand(sites, m, k, device=device)
+    saved = dict(_DROP)
+    _DROP['pool'], _DROP['next'] = pool, 0
+    try:
+        yield pool
+    finally:
+        _DROP.update(saved)
+
+
+def drop_uniforms(x):
+    pool, i = _DROP['pool'], _DROP['next']
+    if (pool is not None and i < pool.shape[0] and tuple(pool.shape[1:]) == tuple(x.shape)
+            and pool.device == x.device):
+        _DROP['next'] = i + 1
+        return pool[i]
+    return torch.rand(x.shape, device=x.device, dtype=torch.float32)
+
+
+def linear(x, lin, slope=None, drop=0.0):
     """lin(x), then LeakyReLU(slope) if slope is not None, on the dtupd.h
-    kernels (linear_applicable)."""
-    return _UpdLinear.apply(x, lin.weight, lin.bias, slope)
+    kernels (linear_applicable); drop > 0: F.dropout(x, drop) folded in
+    (uniforms from drop_uniforms)."""
+    u = drop_uniforms(x) if drop > 0.0 else None
+    return _UpdLinear.apply(x, lin.weight, lin.bias, slope, u, float(drop) if drop > 0.0 else 0.0,
+                            torch.is_grad_enabled())
 
 
 # ---- the small fully connected tails after the trunk's linear (include/dthead.h) --------

@@ -133,6 +133,7 @@ class DDPGTrainer:
         # stream layout of the stages (A/B: tools/update_only.py AB_ATTR=...)
         self.multi_stream = True      # independent forwards on a side stream (_fork)
         self.split_target = False     # + the target critic trunk on a third (measured slower)
+        self.fold_dropout = True      # dropouts folded into the linears after them (train_ops)
         self._pending_grads = {}      # module id -> its autograd gradients (_grads -> _opt_step)
         self.conv_search = bool(conv_search)
         self._graphs = None
@@ -276,9 +277,45 @@ class DDPGTrainer:
         last check that produced NaN / Inf (synchronises)."""
         return self.guard.check('DDPG update')
 
+    # folded dropouts an update draws (train_ops.drop_pool): the target actor,
+    # the target critic, the critic, the actor and the critic's head twice
+    DROP_SITES = 6
+
+    def _drop_width(self):
+        """The flatten width every folded dropout of the two networks sees
+        (the input of a linear right after a dropout), or None."""
+        ks = set()
+        for net in (self.actor, self.critic):
+            for seq in getattr(getattr(net, 'net', None), 'input_nets', []):
+                mods = list(seq.internal_modules)
+                for j in range(len(mods) - 1):
+                    if (isinstance(mods[j], torch.nn.Dropout) and mods[j].p > 0
+                            and hasattr(mods[j + 1], 'linear')):
+                        ks.add(mods[j + 1].linear.in_features)
+        return ks.pop() if len(ks) == 1 else None
+
+    def _drop_open(self):
+        """One launch draws every folded dropout's uniforms of the update
+        (instead of one dropout kernel a site); closed by _drop_close."""
+        train_ops.FOLD_DROPOUT = self.fold_dropout
+        k = self._drop_width() if (self.device.type == 'cuda' and self.dtype == torch.float32
+                                   and self.fold_dropout) else None
+        if k is None:
+            return
+        self._drop_ctx = train_ops.drop_pool(self.DROP_SITES, self._in['obs'].shape[0], k,
+                                             self.device)
+        self._drop_buf = self._drop_ctx.__enter__()
+
+    def _drop_close(self):
+        ctx = getattr(self, '_drop_ctx', None)
+        if ctx is not None:
+            ctx.__exit__(None, None, None)
+            self._drop_ctx = None
+
     def _stage_critic(self):
         x = self._in
         self.guard.tick()
+        self._drop_open()
         self.guard.scan('batch', x['obs'], x['act'], x['rew'], x['nxt'])
         # the targets' forward (target actor -> target critic on next_obs) and
         # the critic's forward on obs are independent: two streams, so their
@@ -369,6 +406,7 @@ class DDPGTrainer:
         soft_update(self.target_actor, self.actor, self.tau)       # trainers.py:215-216
         soft_update(self.target_critic, self.critic, self.tau)
         self._join(side, self._td)
+        self._drop_close()
         with torch.no_grad():
             self._metrics = (torch.sqrt(self._critic_loss), self._actor_loss)
 

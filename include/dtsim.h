@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DT_ABI_VERSION 11 /* 2: curves per tile vary (curve_start), intersections;
+#define DT_ABI_VERSION 12 /* 2: curves per tile vary (curve_start), intersections;
                              3: static objects in dt_map, safety_rad_mult;
                              4: dt_render_io.pose / list_cap, dt_copy_pose,
                                 dt_step_many pose output;
@@ -52,7 +52,9 @@ extern "C" {
                                 dt_palette_gray, dt_conv1_index_split,
                                 dt_frame_gather frame_kind
                             11: dtactor.h dt_conv1x_split / dt_conv32x_split
-                                (the float32-accurate convolutions) */
+                                (the float32-accurate convolutions);
+                            12: dtupd.h dt_upd_linear_fwd_drop / _dgrad_drop
+                                (dropout folded into the linears) */
 
 /* error codes */
 #define DT_OK 0

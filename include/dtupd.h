@@ -143,6 +143,25 @@ int dt_upd_linear_dgrad(int32_t m, int32_t n, int32_t k, const float* dy, const 
 int dt_upd_linear_wgrad(int32_t m, int32_t n, int32_t k, const float* dy, const float* x,
                         const float* yact, float slope, float* dw, float* db, void* stream);
 
+/* The forward and the input gradient with the dropout before the linear
+ * folded in (config.json's flatten -> dropout(p) -> linear; ABI 12).
+ *   u   device f32 [m, k] uniforms in [0, 1), 16-B aligned, or NULL (no
+ *       dropout): element (i, j) of x is kept where u[i][j] >= p and then
+ *       scaled by 1 / (1 - p) -- torch's F.dropout with the bernoulli(1 - p)
+ *       mask {u >= p} -- on x's loads in the forward and on dx's stores in
+ *       the input gradient.  0 <= p < 1.
+ *   xd  device f32 [m, k] out or NULL: the dropped input, written by the
+ *       forward for the weight gradient (dt_upd_linear_wgrad with x = xd).
+ * Replaces the dropout + nn.Linear pair of the reference's MetaNet
+ * (models/ddpg/modules.py) as training/trainers.py runs it: no separate
+ * dropout kernel, no dropout backward. */
+int dt_upd_linear_fwd_drop(int32_t m, int32_t n, int32_t k, const float* x, const float* u,
+                           float p, float* xd, const float* w, const float* b, int32_t leaky,
+                           float slope, float* y, float* work, void* stream);
+int dt_upd_linear_dgrad_drop(int32_t m, int32_t n, int32_t k, const float* dy, const float* w,
+                             const float* yact, float slope, const float* u, float p, float* dx,
+                             void* stream);
+
 #ifdef __cplusplus
 }
 #endif

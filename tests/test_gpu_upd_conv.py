@@ -236,3 +236,60 @@ def test_linear_matches_f64(gpu, m, n, k, slope):
         _bound((dy.abs().T @ x.abs()).max().item())
     assert (lin.bias.grad.double().cpu() - dy.sum(0)).abs().max().item() <= \
         _bound(dy.abs().sum(0).max().item())
+
+
+@pytest.mark.parametrize('m,slope,p', [(64, 0.01, 0.5), (37, None, 0.25)])
+def test_linear_dropout_folded_matches_f64(gpu, m, slope, p):
+    """Dropout folded into the split-K linear (dt_upd_linear_*_drop): the
+    forward, dx, dw and db against float64 torch of x * {u >= p} / (1 - p)
+    through the same linear (F.dropout's bernoulli(1 - p) mask made from the
+    same uniforms u), at the config's flatten width."""
+    from aido1_amd import train_ops
+    n, k = 256, 4032
+    g = torch.Generator().manual_seed(m)
+    x = torch.randn(m, k, generator=g, dtype=torch.float64)
+    w = torch.randn(n, k, generator=g, dtype=torch.float64) / k ** 0.5
+    b = torch.randn(n, generator=g, dtype=torch.float64)
+    dy = torch.randn(m, n, generator=g, dtype=torch.float64)
+    u = torch.rand(m, k, generator=g, dtype=torch.float32)
+    keep = (u >= p).double() / (1.0 - p)
+    xg = x.float().to(gpu).requires_grad_()
+    lin = torch.nn.Linear(k, n).to(gpu)
+    with torch.no_grad():
+        lin.weight.copy_(w)
+        lin.bias.copy_(b)
+    with train_ops.drop_pool(1, m, k, gpu) as pool:
+        pool.copy_(u.to(gpu).unsqueeze(0))
+        y = train_ops.linear(xg, lin, slope, drop=p)
+    y.backward(dy.float().to(gpu))
+    xd = x * keep
+    ref = xd @ w.T + b
+    if slope is not None:
+        ref = torch.where(ref > 0, ref, ref * slope)
+        dy = torch.where(y.detach().double().cpu() > 0, dy, dy * slope)
+    assert (y.detach().double().cpu() - ref).abs().max().item() <= \
+        _bound((xd.abs() @ w.abs().T).max().item())
+    assert (xg.grad.double().cpu() - (dy @ w) * keep).abs().max().item() <= \
+        _bound((dy.abs() @ w.abs()).max().item() * 2.0)
+    assert (lin.weight.grad.double().cpu() - dy.T @ xd).abs().max().item() <= \
+        _bound((dy.abs().T @ xd.abs()).max().item())
+    assert (lin.bias.grad.double().cpu() - dy.sum(0)).abs().max().item() <= \
+        _bound(dy.abs().sum(0).max().item())
+    # the dropped elements' gradient is exactly zero, the kept ones scaled
+    dx = xg.grad.cpu()
+    assert torch.all(dx[u < p] == 0)
+
+
+def test_linear_dropout_site_draws_fresh_uniforms(gpu):
+    """Outside a pool every folded dropout draws its own uniforms; inside one
+    the sites take consecutive slices and a site past its end draws its own."""
+    from aido1_amd import train_ops
+    x = torch.ones(8, 1024, device=gpu)
+    a = train_ops.drop_uniforms(x)
+    bb = train_ops.drop_uniforms(x)
+    assert a.shape == x.shape and not torch.equal(a, bb)
+    with train_ops.drop_pool(2, 8, 1024, gpu) as pool:
+        s0, s1, s2 = (train_ops.drop_uniforms(x) for _ in range(3))
+        assert s0.data_ptr() == pool[0].data_ptr() and s1.data_ptr() == pool[1].data_ptr()
+        assert s2.data_ptr() not in (pool[0].data_ptr(), pool[1].data_ptr())
+    assert train_ops._DROP['pool'] is None
