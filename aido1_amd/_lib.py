@@ -22,7 +22,7 @@ SOURCES = ['dtsim.hip', 'dtrender.hip', 'dtreplay.hip', 'dtactor.hip', 'dtconv.h
 HEADERS = ['dtsim_common.h', 'dtrender.h', 'dtsync.h', 'dtconv_common.h']
 PUBLIC_HEADERS = ['dtsim.h', 'dtreplay.h', 'dtactor.h', 'dttrain.h', 'dtupd.h', 'dthead.h']
 HIPCC = os.environ.get('HIPCC', '/opt/rocm/bin/hipcc')
-ABI_VERSION = 12
+ABI_VERSION = 13
 
 HIP_FLAGS = ['--offload-arch=gfx950', '-O3', '-fPIC', '-shared', '-std=c++17',
              '-ffp-contract=off', '-munsafe-fp-atomics']
@@ -93,10 +93,13 @@ def _sources():
     return [os.path.join(CSRC, s) for s in SOURCES if os.path.exists(os.path.join(CSRC, s))]
 
 
-def _stale():
-    if not os.path.exists(LIB_PATH):
+def _stale(path=None):
+    """True when the library at `path` (the product library by default) is
+    missing or older than any source or header it is built from."""
+    path = path or LIB_PATH
+    if not os.path.exists(path):
         return True
-    t = os.path.getmtime(LIB_PATH)
+    t = os.path.getmtime(path)
     deps = _sources() + [os.path.join(CSRC, h) for h in HEADERS] + \
         [os.path.join(REPO_DIR, 'include', h) for h in PUBLIC_HEADERS]
     return any(os.path.exists(d) and os.path.getmtime(d) > t for d in deps)
@@ -288,6 +291,9 @@ def bind(L):
         'dt_actor_head_x3': (ctypes.c_int, [i32, i32, i32, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                             i32, ctypes.c_float, vp, vp, vp]),
         'dt_actor_head_x3_work_floats': (i64, [i32]),
+        'dt_actor_head_x3_drop': (ctypes.c_int, [i32, i32, i32, vp, ctypes.c_float, ctypes.c_uint32,
+                                                 vp, vp, vp, vp, vp, vp, vp, vp, i32,
+                                                 ctypes.c_float, vp, vp, vp]),
         'dt_explore': (ctypes.c_int, [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                       ctypes.POINTER(DtExploreParams), vp, vp]),
         'dt_explore_done': (ctypes.c_int, [i32, vp, vp, vp, vp, i32, vp]),

@@ -864,13 +864,24 @@ class FusedActor(nn.Module):
 
     def _heads_x3(self, other, x, n0, out):
         """dropout (reference mode) -> lin1 -> LeakyReLU -> lin2 -> head at
-        float32 accuracy in ONE dt_actor_head_x3 launch (include/dtactor.h):
-        rows [0, n0) with this actor's weights, [n0, n) with `other`'s."""
+        float32 accuracy in ONE dt_actor_head_x3_drop launch pair
+        (include/dtactor.h; the dropout folded into lin1's staging): rows
+        [0, n0) with this actor's weights, [n0, n) with `other`'s."""
         import ctypes
         from aido1_amd import _lib
-        if self.mode == 'reference' and self.p_drop > 0:
-            x = F.dropout(x, self.p_drop, training=True)
         o = other if other is not None else self
+        p = self.p_drop if self.mode == 'reference' else 0.0
+        if p > 0 and o.p_drop != self.p_drop:     # one rate a launch: torch's dropout
+            x = F.dropout(x, p, training=True)
+            p = 0.0
+        # the dropout folded into lin1's staging (dt_actor_head_x3_drop): a
+        # fresh counter-based key a call, drawn from torch's generator once
+        seed = 0
+        if p > 0:
+            if getattr(self, '_drop_key', None) is None:
+                self._drop_key = [int(torch.randint(0, 2 ** 31, (1,)).item()), 0]
+            self._drop_key[1] += 1
+            seed = (self._drop_key[0] + 0x9E3779B9 * self._drop_key[1]) & 0xFFFFFFFF
         L = _lib.lib()
         n = x.shape[0]
         work = getattr(self, '_hwork', None)
@@ -878,8 +889,8 @@ class FusedActor(nn.Module):
                 work.device != x.device:
             work = self._hwork = torch.empty(int(L.dt_actor_head_x3_work_floats(n)),
                                              device=x.device)
-        rc = L.dt_actor_head_x3(
-            n, n0, FLAT, x.data_ptr(), self.w1x.data_ptr(), self.b1.data_ptr(),
+        rc = L.dt_actor_head_x3_drop(
+            n, n0, FLAT, x.data_ptr(), float(p), seed, self.w1x.data_ptr(), self.b1.data_ptr(),
             self.w2.data_ptr(), self.b2.data_ptr(), o.w1x.data_ptr(), o.b1.data_ptr(),
             o.w2.data_ptr(), o.b2.data_ptr(), self._HEAD_CODES[self.head], 0.01, work.data_ptr(),
             out.data_ptr(), ctypes.c_void_p(torch.cuda.current_stream(x.device).cuda_stream))

@@ -730,14 +730,46 @@ __device__ __forceinline__ HeadTile head_tile(int b, int n, int n0) {
   return t;
 }
 
+// The head's dropout (reference mode: F.dropout(flatten, p) before lin1),
+// folded into lin1's staging: element (row, k) is kept where u >= p, u a
+// 16-bit uniform in [0, 1) from a counter-based hash of (seed, row * K + k)
+// (lowbias32, two rounds keyed by the seed; one hash a pair of elements),
+// then scaled by 1 / (1 - p) -- F.dropout's bernoulli(1 - p) mask and scale
+// with its own generator instead of torch's stream.
+__device__ __forceinline__ uint32_t drop_hash(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7feb352du;
+  x ^= x >> 15;
+  x *= 0x846ca68bu;
+  x ^= x >> 16;
+  return x;
+}
+struct HeadDrop {
+  float p, scale;   // p == 0: no dropout
+  uint32_t seed;
+};
+
 // XCD-aware order (blocks are dealt round-robin over the 8 XCDs, so b and
 // b + 8 share one): block b works K quarter (b % 8) / 2, so each XCD's L2
 // holds one quarter of lin1's fragments (2 MB) for all its workgroups; the
-// grid is padded to a multiple of 8, the spare blocks exit
+// grid is padded to a multiple of 8, the spare blocks exit.
+// The workgroup's 64 x-rows are staged through LDS a stage of kHStage k steps
+// at a time -- loaded from HBM once, dropped out and split into (hi, lo) once,
+// instead of by each of the 8 waves (which read the same rows: 8x the L1
+// traffic and the split VALU) -- double-buffered, one barrier a stage.
+constexpr int kHStage = 3;                         // k steps a stage (63 = 21 x 3)
+constexpr int kHStages = kHPartSteps / kHStage;
+constexpr int kHStageK = 16 * kHStage;             // 48 k
+constexpr int kHRowH = kHStageK + 8;               // halves a staged row (112 B: conflict-free b128 reads)
+constexpr int kHChunks = kHStageK / 8;             // 8-k chunks a row
+static_assert(kHPartSteps % kHStage == 0, "whole stages");
+static_assert(kHRows * kHChunks <= 64 * kHWaves, "a chunk a thread");
+
 __global__ void __launch_bounds__(64 * kHWaves, 2)
 head_lin1_x3_kernel(int n, int n0, int ldp, int tiles, const float* __restrict__ x,
                     const half8* __restrict__ w1a, const half8* __restrict__ w1b,
-                    float* __restrict__ part) {
+                    float* __restrict__ part, HeadDrop dr) {
+  __shared__ __attribute__((aligned(16))) _Float16 xs[2][2][kHRows * kHRowH];   // [buf][hi, lo]
   const int b = blockIdx.x, xcd = b & 7;
   const int kp = xcd >> 1;                        // the K quarter
   const int tile = (b >> 3) * 2 + (xcd & 1);
@@ -746,13 +778,44 @@ head_lin1_x3_kernel(int n, int n0, int ldp, int tiles, const float* __restrict__
   const half8* __restrict__ w1 = ht.set2 ? w1b : w1a;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int col = lane & 31, h = lane >> 5;
-  const float4* xr[2];
+  // staging: thread tid < 64 * 6 owns row tid / 6, chunk tid % 6 of a stage
+  const bool stager = tid < kHRows * kHChunks;
+  const int srow = tid / kHChunks, schunk = tid - srow * kHChunks;
+  const int grow = ht.rbeg + srow;                 // the global sample row
+  const bool rvalid = stager && grow < ht.rend;
+  const float4* xsrc = reinterpret_cast<const float4*>(
+      x + (size_t)(rvalid ? grow : ht.rbeg) * kHK + 16 * kHPartSteps * kp + 8 * schunk);
+  float4 xq[2];
+  auto stage_load = [&](int g) __attribute__((always_inline)) {
+    if (stager) {
+      xq[0] = xsrc[(kHStageK / 4) * g];
+      xq[1] = xsrc[(kHStageK / 4) * g + 1];
+    }
+  };
+  auto stage_store = [&](int g, int buf) __attribute__((always_inline)) {
+    if (!stager) return;
+    float v[8] = {xq[0].x, xq[0].y, xq[0].z, xq[0].w, xq[1].x, xq[1].y, xq[1].z, xq[1].w};
+    if (dr.p > 0.0f) {
+      // one hash a pair of elements, 16 bits each: u = h16 / 2^16
+      const uint32_t k0 = 16 * kHPartSteps * kp + kHStageK * g + 8 * schunk;
+      const uint32_t base = (uint32_t)grow * (uint32_t)kHK + k0;
+      const uint32_t mix = drop_hash(dr.seed ^ 0x9e3779b9u);
 #pragma unroll
-  for (int st = 0; st < 2; ++st) {
-    const int row = ht.rbeg + 32 * st + col;
-    xr[st] = reinterpret_cast<const float4*>(x + (size_t)(row < ht.rend ? row : ht.rbeg) * kHK +
-                                             8 * h) + 4 * kHPartSteps * kp;
-  }
+      for (int j = 0; j < 8; j += 2) {
+        const uint32_t hh = drop_hash(drop_hash((base + j) ^ mix) + dr.seed);
+        const float u0 = (float)(hh & 0xffffu) * (1.0f / 65536.0f);
+        const float u1 = (float)(hh >> 16) * (1.0f / 65536.0f);
+        v[j] = u0 >= dr.p ? v[j] * dr.scale : 0.0f;
+        v[j + 1] = u1 >= dr.p ? v[j + 1] * dr.scale : 0.0f;
+      }
+    }
+    uint32_t hi[4], lo[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) split2(v[2 * e], v[2 * e + 1], hi[e], lo[e]);
+    const int at = srow * kHRowH + 8 * schunk;
+    *reinterpret_cast<u32x4*>(&xs[buf][0][at]) = u32x4{hi[0], hi[1], hi[2], hi[3]};
+    *reinterpret_cast<u32x4*>(&xs[buf][1][at]) = u32x4{lo[0], lo[1], lo[2], lo[3]};
+  };
   // w1 fragments: [2 (hi, lo)][16 feature tiles][252 k steps][64 lanes]
   constexpr int kHalfFrag = 16 * kHSteps * 64;
   const half8* wt[2];
@@ -766,47 +829,46 @@ head_lin1_x3_kernel(int n, int n0, int ldp, int tiles, const float* __restrict__
     for (int st = 0; st < 2; ++st)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc0[c][st][r] = acc1[c][st][r] = 0.0f;
-  float4 xq[2][2][2];              // [buffer][sample tile][half]
-  half8 ah[2][2], al[2][2];        // [buffer][feature tile]
-  auto load = [&](int b, int s) __attribute__((always_inline)) {
-#pragma unroll
-    for (int st = 0; st < 2; ++st) {
-      xq[b][st][0] = xr[st][4 * s];
-      xq[b][st][1] = xr[st][4 * s + 1];
-    }
+  half8 ah[kHStage][2], al[kHStage][2];   // [buffer = step in stage][feature tile]
+  auto wload = [&](int bb, int s) __attribute__((always_inline)) {
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
-      ah[b][c] = wt[c][s * 64];
-      al[b][c] = wt[c][kHalfFrag + s * 64];
+      ah[bb][c] = wt[c][s * 64];
+      al[bb][c] = wt[c][kHalfFrag + s * 64];
     }
   };
-  auto step = [&](int b) __attribute__((always_inline)) {
+  // step ss of stage buffer `buf` on weight buffer bb: B = the staged rows
+  // (lane: sample col of each tile, k 16 ss + 8 h .. + 7)
+  auto step = [&](int buf, int ss, int bb) __attribute__((always_inline)) {
 #pragma unroll
     for (int st = 0; st < 2; ++st) {
-      const float4 q0 = xq[b][st][0], q1 = xq[b][st][1];
-      uint32_t hi[4], lo[4];
-      split2(q0.x, q0.y, hi[0], lo[0]);
-      split2(q0.z, q0.w, hi[1], lo[1]);
-      split2(q1.x, q1.y, hi[2], lo[2]);
-      split2(q1.z, q1.w, hi[3], lo[3]);
-      const half8 xh = __builtin_bit_cast(half8, u32x4{hi[0], hi[1], hi[2], hi[3]});
-      const half8 xl = __builtin_bit_cast(half8, u32x4{lo[0], lo[1], lo[2], lo[3]});
+      const int at = (32 * st + col) * kHRowH + 16 * ss + 8 * h;
+      const half8 xh = *reinterpret_cast<const half8*>(&xs[buf][0][at]);
+      const half8 xl = *reinterpret_cast<const half8*>(&xs[buf][1][at]);
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
-        acc0[c][st] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[b][c], xh, acc0[c][st], 0, 0, 0);
-        acc1[c][st] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[b][c], xl, acc1[c][st], 0, 0, 0);
-        acc1[c][st] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[b][c], xh, acc1[c][st], 0, 0, 0);
+        acc0[c][st] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[bb][c], xh, acc0[c][st], 0, 0, 0);
+        acc1[c][st] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[bb][c], xl, acc1[c][st], 0, 0, 0);
+        acc1[c][st] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[bb][c], xh, acc1[c][st], 0, 0, 0);
       }
     }
   };
-  load(0, 0);
-  for (int s = 0; s + 1 < kHPartSteps; s += 2) {   // 63 steps: 31 pairs, then the last
-    load(1, s + 1);
-    step(0);
-    load(0, s + 2);
-    step(1);
+  stage_load(0);
+  wload(0, 0);
+  stage_store(0, 0);
+  __syncthreads();
+  for (int g = 0; g < kHStages; ++g) {
+    const int buf = g & 1;
+    if (g + 1 < kHStages) stage_load(g + 1);      // in flight during this stage's MFMAs
+#pragma unroll
+    for (int ss = 0; ss < kHStage; ++ss) {
+      const int s = kHStage * g + ss;              // the quarter's k step
+      if (s + 1 < kHPartSteps) wload((ss + 1) % kHStage, s + 1);
+      step(buf, ss, ss);
+    }
+    if (g + 1 < kHStages) stage_store(g + 1, buf ^ 1);
+    __syncthreads();
   }
-  step(0);
   // partial sums [part][feature][row]: lanes of a half-wave are 32 consecutive rows
   float* pp = part + (size_t)kp * kHFeat * ldp;
 #pragma unroll
@@ -906,25 +968,36 @@ extern "C" int64_t dt_actor_head_x3_work_floats(int32_t n) {
   return n < 0 ? -1 : (int64_t)kHParts * kHFeat * n;
 }
 
-extern "C" int dt_actor_head_x3(int32_t n, int32_t n0, int32_t k, const float* x,
-                                const void* w1a, const float* b1a, const float* w2a,
-                                const float* b2a, const void* w1b, const float* b1b,
-                                const float* w2b, const float* b2b, int32_t head, float slope,
-                                float* work, float* out, void* stream) {
+extern "C" int dt_actor_head_x3_drop(int32_t n, int32_t n0, int32_t k, const float* x,
+                                     float p, uint32_t seed, const void* w1a, const float* b1a,
+                                     const float* w2a, const float* b2a, const void* w1b,
+                                     const float* b1b, const float* w2b, const float* b2b,
+                                     int32_t head, float slope, float* work, float* out,
+                                     void* stream) {
   if (!x || !w1a || !b1a || !w2a || !b2a || !work || !out || n < 0 || n0 < 0 || n0 > n ||
-      k != kHK || head < 0 || head > 2)
+      k != kHK || head < 0 || head > 2 || !(p >= 0.0f && p < 1.0f))
     return DT_E_ARG;
   if (n0 < n && (!w1b || !b1b || !w2b || !b2b)) return DT_E_ARG;
   if (n == 0) return DT_OK;
   hipStream_t s = (hipStream_t)stream;
   const int tiles = (n0 + kHRows - 1) / kHRows + (n - n0 + kHRows - 1) / kHRows;
   const int blocks = 8 * ((tiles + 1) / 2);   // two tiles of each quarter an 8-block round
+  const HeadDrop dr{p, p > 0.0f ? 1.0f / (1.0f - p) : 1.0f, seed};
   hipLaunchKernelGGL(head_lin1_x3_kernel, dim3(blocks), dim3(64 * kHWaves), 0, s, n, n0, n, tiles,
-                     x, (const half8*)w1a, (const half8*)(w1b ? w1b : w1a), work);
+                     x, (const half8*)w1a, (const half8*)(w1b ? w1b : w1a), work, dr);
   hipLaunchKernelGGL(head_finish_kernel, dim3((n + 15) / 16), dim3(256), 0, s, n, n0, n,
                      work, b1a, w2a, b2a, b1b ? b1b : b1a, w2b ? w2b : w2a, b2b ? b2b : b2a,
                      head, slope, out);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+
+extern "C" int dt_actor_head_x3(int32_t n, int32_t n0, int32_t k, const float* x,
+                                const void* w1a, const float* b1a, const float* w2a,
+                                const float* b2a, const void* w1b, const float* b1b,
+                                const float* w2b, const float* b2b, int32_t head, float slope,
+                                float* work, float* out, void* stream) {
+  return dt_actor_head_x3_drop(n, n0, k, x, 0.0f, 0u, w1a, b1a, w2a, b2a, w1b, b1b, w2b, b2b,
+                               head, slope, work, out, stream);
 }
 
 extern "C" int dt_conv32x_split(int32_t layer, int32_t n, const void* x, const float* wfrag,

@@ -182,6 +182,17 @@ int dt_actor_head_x3(int32_t n, int32_t n0, int32_t k, const float* x, const voi
                      const float* b1b, const float* w2b, const float* b2b, int32_t head,
                      float slope, float* work, float* out, void* stream);
 int64_t dt_actor_head_x3_work_floats(int32_t n);
+/* dt_actor_head_x3 with reference mode's dropout before lin1 folded in (ABI
+ * 13): x[i][j] is kept where u >= p and scaled by 1 / (1 - p), u a 16-bit
+ * uniform from a counter-based hash of (seed, i * k + j) -- F.dropout(x, p)'s
+ * bernoulli(1 - p) mask and scale (duckietown_rl/ddpg.py:56-62 in train mode),
+ * with its own generator.  0 <= p < 1 (0: no dropout).  x is read in place,
+ * the dropped rows never written. */
+int dt_actor_head_x3_drop(int32_t n, int32_t n0, int32_t k, const float* x, float p,
+                          uint32_t seed, const void* w1a, const float* b1a, const float* w2a,
+                          const float* b2a, const void* w1b, const float* b1b, const float* w2b,
+                          const float* b2b, int32_t head, float slope, float* work, float* out,
+                          void* stream);
 
 /* dt_explore: SingleThreadExplorer's action choice for n explorers at once,
  * one fused pass replacing the torch restatement's ~25 element-wise kernels

@@ -29,7 +29,7 @@
 extern "C" {
 #endif
 
-#define DT_ABI_VERSION 12 /* 2: curves per tile vary (curve_start), intersections;
+#define DT_ABI_VERSION 13 /* 2: curves per tile vary (curve_start), intersections;
                              3: static objects in dt_map, safety_rad_mult;
                              4: dt_render_io.pose / list_cap, dt_copy_pose,
                                 dt_step_many pose output;
@@ -54,7 +54,8 @@ extern "C" {
                             11: dtactor.h dt_conv1x_split / dt_conv32x_split
                                 (the float32-accurate convolutions);
                             12: dtupd.h dt_upd_linear_fwd_drop / _dgrad_drop
-                                (dropout folded into the linears) */
+                                (dropout folded into the linears);
+                            13: dtactor.h dt_actor_head_x3_drop */
 
 /* error codes */
 #define DT_OK 0

@@ -123,3 +123,12 @@ def test_upd_entry_points_check_arguments(libpath):
     assert L.dt_upd_linear_work_floats(64, 256, 4032) % (64 * 256) == 0
     assert L.dt_upd_linear_fwd(64, 256, 4032, None, 16, 16, 0, 0.0, 16, 16, None) != 0
     assert L.dt_upd_wgrad_work_floats(3, 8, 2, 64, 120, 160) == 512 * 32 * 192
+
+
+def test_diagnostic_check_library_is_current():
+    """The bounds-checked build (libdtsim_check.so, made by
+    __graft_entry__.build() for tests/test_gpu_actor.py) is no older than the
+    sources: a stale one lacks the current entry points and fails on the GPU."""
+    from aido1_amd import _lib
+    if os.path.exists(_lib.CHECK_LIB_PATH):
+        assert not _lib._stale(_lib.CHECK_LIB_PATH), 'rebuild: python -c "import __graft_entry__ as g; g.build()"'

@@ -7,6 +7,7 @@ duckietown_rl/ddpg.py:44-62), and the bar is |da| <= 1e-4."""
 import ctypes
 import sys
 
+import numpy as np
 import pytest
 import torch
 import torch.nn.functional as F
@@ -243,3 +244,63 @@ def test_head_x3_matches_float64(gpu, n, n0):
     want = torch.cat(want)
     assert torch.isfinite(out).all()
     assert (out.double() - want).abs().max().item() < 2e-6
+
+
+def _drop_hash(x):
+    x = x.astype(np.uint64) & 0xFFFFFFFF
+    x ^= x >> 16
+    x = (x * 0x7FEB352D) & 0xFFFFFFFF
+    x ^= x >> 15
+    x = (x * 0x846CA68B) & 0xFFFFFFFF
+    x ^= x >> 16
+    return x
+
+
+def _drop_uniforms(n, k, seed):
+    """dt_actor_head_x3_drop's uniforms restated: one two-round hash a pair of
+    elements keyed by the seed, 16 bits each (csrc/dtconvx.hip drop_hash)."""
+    idx = np.arange(n * k, dtype=np.uint64).reshape(n, k)
+    pair = idx[:, 0::2]
+    mix = _drop_hash(np.array([seed ^ 0x9E3779B9], dtype=np.uint64))[0]
+    hh = _drop_hash((_drop_hash(pair ^ mix) + seed) & 0xFFFFFFFF)
+    u = np.empty((n, k))
+    u[:, 0::2] = (hh & 0xFFFF) / 65536.0
+    u[:, 1::2] = (hh >> 16) / 65536.0
+    return u
+
+
+@pytest.mark.parametrize('n,n0,p,seed', [(300, 257, 0.5, 12345), (64, 64, 0.25, 7)])
+def test_head_x3_dropout_folded(gpu, n, n0, p, seed):
+    """The dropout folded into lin1's staging (dt_actor_head_x3_drop) against
+    float64 of F.dropout with the kernel's mask restated in numpy: every
+    element kept where u >= p, scaled by 1 / (1 - p); about 1 - p of them."""
+    import ctypes
+
+    from aido1_amd import _lib
+    from aido1_amd.actor import FLAT, ConfigActor, FusedActor
+    cfg = golden('reference_config.json')['model']['actor']
+    torch.manual_seed(n + seed)
+    a, b = ConfigActor(cfg).to(gpu), ConfigActor(cfg).to(gpu)
+    fa = FusedActor(a, dtype=torch.float32, mode='reference')
+    fb = FusedActor(b, dtype=torch.float32, mode='reference')
+    x = torch.randn(n, FLAT, device=gpu) * 0.7
+    out = torch.full((n, 2), float('nan'), device=gpu)
+    L = _lib.lib()
+    work = torch.empty(int(L.dt_actor_head_x3_work_floats(n)), device=gpu)
+    rc = L.dt_actor_head_x3_drop(
+        n, n0, FLAT, x.data_ptr(), p, seed, fa.w1x.data_ptr(), fa.b1.data_ptr(),
+        fa.w2.data_ptr(), fa.b2.data_ptr(), fb.w1x.data_ptr(), fb.b1.data_ptr(),
+        fb.w2.data_ptr(), fb.b2.data_ptr(), fa._HEAD_CODES[fa.head], 0.01, work.data_ptr(),
+        out.data_ptr(), ctypes.c_void_p(torch.cuda.current_stream(gpu).cuda_stream))
+    assert rc == 0
+    keep = torch.from_numpy(_drop_uniforms(n, FLAT, seed) >= p)
+    assert abs(keep.double().mean().item() - (1 - p)) < 0.01
+    xd = x.double().cpu() * keep / (1.0 - p)
+    want = []
+    for net, sl in ((a, slice(0, n0)), (b, slice(n0, n))):
+        _, _, l1, l2 = net.layers()
+        h = F.leaky_relu(xd[sl] @ l1.weight.double().cpu().t() + l1.bias.double().cpu())
+        want.append(torch.tanh(h @ l2.weight.double().cpu().t() + l2.bias.double().cpu()))
+    want = torch.cat(want)
+    assert torch.isfinite(out).all()
+    assert (out.double().cpu() - want).abs().max().item() < 4e-6
