@@ -265,7 +265,14 @@ class SoftUpdate:
 
     @torch.no_grad()
     def __call__(self, target, source, tau):
-        rows = [(t.data, s.data) for t, s in zip(target.parameters(), source.parameters())]
+        self.many([(target, source)], tau)
+
+    @torch.no_grad()
+    def many(self, pairs, tau):
+        """Every (target, source) pair of `pairs` in ONE dt_soft_update launch
+        (the trainer's target actor and target critic together)."""
+        rows = [(t.data, s.data) for target, source in pairs
+                for t, s in zip(target.parameters(), source.parameters())]
         if not rows or not MultiTensorTable.fits(rows):
             tp = [r[0] for r in rows]
             a = torch._foreach_mul(tp, 1.0 - tau)
@@ -273,7 +280,7 @@ class SoftUpdate:
             torch._foreach_add_(a, b)
             torch._foreach_copy_(tp, a)
             return
-        key = (id(target), id(source))
+        key = tuple((id(target), id(source)) for target, source in pairs)
         t = self._tables.get(key)
         if t is None or t.key != MultiTensorTable.key_of(rows):
             t = self._tables[key] = MultiTensorTable(rows, rows[0][0].device)

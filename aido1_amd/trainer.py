@@ -403,8 +403,8 @@ class DDPGTrainer:
                 self._td = self._y - q
                 self.guard.scan('td', self._td)
         self._opt_step(self.actor_optim, self.actor, 'actor_grad', 'actor_param')
-        soft_update(self.target_actor, self.actor, self.tau)       # trainers.py:215-216
-        soft_update(self.target_critic, self.critic, self.tau)
+        # trainers.py:215-216, both pairs in one launch
+        _SOFT.many([(self.target_actor, self.actor), (self.target_critic, self.critic)], self.tau)
         self._join(side, self._td)
         self._drop_close()
         with torch.no_grad():
