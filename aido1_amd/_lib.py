@@ -294,6 +294,9 @@ def bind(L):
         'dt_actor_head_x3_drop': (ctypes.c_int, [i32, i32, i32, vp, ctypes.c_float, ctypes.c_uint32,
                                                  vp, vp, vp, vp, vp, vp, vp, vp, i32,
                                                  ctypes.c_float, vp, vp, vp]),
+        'dt_actor_head_f16_drop': (ctypes.c_int, [i32, i32, i32, vp, ctypes.c_float,
+                                                  ctypes.c_uint32, vp, vp, vp, vp, vp, vp, vp, vp,
+                                                  i32, ctypes.c_float, vp, vp, vp]),
         'dt_explore': (ctypes.c_int, [i32, vp, vp, vp, vp, vp, vp, vp, vp, vp, vp,
                                       ctypes.POINTER(DtExploreParams), vp, vp]),
         'dt_explore_done': (ctypes.c_int, [i32, vp, vp, vp, vp, i32, vp]),

@@ -385,6 +385,11 @@ class FusedActor(nn.Module):
         # reference mode in float32): conv1's fragments as (hi, lo) fp16
         # halves, conv2..4's in float32
         self.x3 = dtype == torch.float32 and mode == 'reference'
+        if dtype == torch.float16 and tuple(lin1.weight.shape) == (512, FLAT):
+            # the fast mode's head (dt_actor_head_f16_drop): lin1's fp16
+            # weights in the head fragment layout
+            self.register_buffer('w1f', torch.zeros(16, 252, 64, 8, dtype=torch.float16,
+                                                    device=dev))
         if self.x3:
             self.register_buffer('w0x', torch.zeros(2, 16, 64, 8, dtype=torch.float16, device=dev))
             self.register_buffer('wx32', torch.zeros(3, 32, 64, 8, device=dev))
@@ -456,6 +461,10 @@ class FusedActor(nn.Module):
                 if getattr(self, '_h1idx', None) is None or self._h1idx.device != dev:
                     self._h1idx = head_fragment_index(dev)
                 pairs.append((self.w1x, lin1.weight, self._h1idx, 2))
+        if hasattr(self, 'w1f'):   # the fp16 head's fragments (from float32: fp16 rounding)
+            if getattr(self, '_h1idx', None) is None or self._h1idx.device != dev:
+                self._h1idx = head_fragment_index(dev)
+            pairs.append((self.w1f, lin1.weight, self._h1idx, None))
         for i in range(4):
             pairs.append((self.bf[i], convs[i].bias, None, None))
         return pairs
@@ -562,6 +571,10 @@ class FusedActor(nn.Module):
             self.b1.copy_(b1 + w1 @ t_flat)
             self.w2.copy_(lin2.weight)
             self.b2.copy_(lin2.bias)
+        if hasattr(self, 'w1f'):   # from the acting w1 (folded in eval mode)
+            if getattr(self, '_h1idx', None) is None or self._h1idx.device != self.w1.device:
+                self._h1idx = head_fragment_index(self.w1.device)
+            self.w1f.view(-1).copy_(torch.take(self.w1, self._h1idx))
         self._fragments(ws, bs)
 
     def _fragments(self, ws, bs):
@@ -838,9 +851,13 @@ class FusedActor(nn.Module):
         launch (include/dtactor.h), written into out [n, 2] f32."""
         import ctypes
         from aido1_amd import _lib
+        o = other if other is not None else self
+        if (hasattr(self, 'w1f') and hasattr(o, 'w1f') and flat.dtype == torch.float16
+                and flat.is_contiguous() and tuple(flat.shape[1:]) == (FLAT,)
+                and o.p_drop == self.p_drop and o.mode == self.mode):
+            return self._heads_f16(o, flat, n0, out)
         n, k = flat.shape[0], self.w1.shape[0]
         h = torch.empty(n, k, dtype=torch.float16, device=flat.device)
-        o = other if other is not None else self
         for a, sl in ((self, slice(0, n0)), (o, slice(n0, n))):
             if sl.stop > sl.start:
                 x = flat[sl]
@@ -853,6 +870,41 @@ class FusedActor(nn.Module):
             ctypes.c_void_p(torch.cuda.current_stream(flat.device).cuda_stream))
         if rc != 0:
             raise _lib.DtError('dt_actor_head failed (%d)' % rc)
+        return out
+
+    def _drop_seed(self, p):
+        """A fresh key for the head's folded dropout (one a call), from a
+        base drawn once from torch's generator."""
+        if p <= 0:
+            return 0
+        if getattr(self, '_drop_key', None) is None:
+            self._drop_key = [int(torch.randint(0, 2 ** 31, (1,)).item()), 0]
+        self._drop_key[1] += 1
+        return (self._drop_key[0] + 0x9E3779B9 * self._drop_key[1]) & 0xFFFFFFFF
+
+    def _heads_f16(self, o, flat, n0, out):
+        """The fast mode's head (dropout -> lin1 -> LeakyReLU -> lin2 -> head)
+        for both weight sets in one dt_actor_head_f16_drop launch pair: lin1
+        on fp16 MFMA with f32 accumulation, the dropout folded into its
+        staging (include/dtactor.h)."""
+        import ctypes
+        from aido1_amd import _lib
+        p = self.p_drop if self.mode == 'reference' else 0.0
+        L = _lib.lib()
+        n = flat.shape[0]
+        work = getattr(self, '_hwork', None)
+        if work is None or work.numel() < L.dt_actor_head_x3_work_floats(n) or \
+                work.device != flat.device:
+            work = self._hwork = torch.empty(int(L.dt_actor_head_x3_work_floats(n)),
+                                             device=flat.device)
+        rc = L.dt_actor_head_f16_drop(
+            n, n0, FLAT, flat.data_ptr(), float(p), self._drop_seed(p), self.w1f.data_ptr(),
+            self.b1.data_ptr(), self.w2.data_ptr(), self.b2.data_ptr(), o.w1f.data_ptr(),
+            o.b1.data_ptr(), o.w2.data_ptr(), o.b2.data_ptr(), self._HEAD_CODES[self.head], 0.01,
+            work.data_ptr(), out.data_ptr(),
+            ctypes.c_void_p(torch.cuda.current_stream(flat.device).cuda_stream))
+        if rc != 0:
+            raise _lib.DtError('dt_actor_head_f16_drop failed (%d)' % rc)
         return out
 
     def _head_x3_ok(self, x, other=None):
@@ -876,12 +928,7 @@ class FusedActor(nn.Module):
             p = 0.0
         # the dropout folded into lin1's staging (dt_actor_head_x3_drop): a
         # fresh counter-based key a call, drawn from torch's generator once
-        seed = 0
-        if p > 0:
-            if getattr(self, '_drop_key', None) is None:
-                self._drop_key = [int(torch.randint(0, 2 ** 31, (1,)).item()), 0]
-            self._drop_key[1] += 1
-            seed = (self._drop_key[0] + 0x9E3779B9 * self._drop_key[1]) & 0xFFFFFFFF
+        seed = self._drop_seed(p)
         L = _lib.lib()
         n = x.shape[0]
         work = getattr(self, '_hwork', None)

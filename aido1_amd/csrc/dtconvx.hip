@@ -697,7 +697,7 @@ int launch_conv32x(int n, const void* x, const float* w, const float* bias, cons
 // x3 like the convolutions: C[feature][sample] = W1 . x^T on fp16 MFMA with
 // A = lin1's weights as pre-split (hi, lo) fragments (feature rows), B = the
 // samples' flattened activations (f32, split as they are loaded).
-// head_lin1_x3_kernel: a workgroup owns 64 samples, all 512 features and a
+// head_lin1_kernel: a workgroup owns 64 samples, all 512 features and a
 //   quarter of K (8 waves, 2 feature tiles x 2 sample tiles each), so lin1's
 //   8 MB of fragments are streamed once per 64 samples rather than per 32
 //   (a one-pass form with 32 samples a workgroup took 213 us at 4096
@@ -765,10 +765,13 @@ constexpr int kHChunks = kHStageK / 8;             // 8-k chunks a row
 static_assert(kHPartSteps % kHStage == 0, "whole stages");
 static_assert(kHRows * kHChunks <= 64 * kHWaves, "a chunk a thread");
 
+// kX3: x f32, its products as three fp16 MFMAs on (hi, lo) pairs; else the
+// fp16 fast mode: x fp16, one MFMA a product (the fragments' hi half only)
+template <bool kX3>
 __global__ void __launch_bounds__(64 * kHWaves, 2)
-head_lin1_x3_kernel(int n, int n0, int ldp, int tiles, const float* __restrict__ x,
-                    const half8* __restrict__ w1a, const half8* __restrict__ w1b,
-                    float* __restrict__ part, HeadDrop dr) {
+head_lin1_kernel(int n, int n0, int ldp, int tiles, const void* __restrict__ xv,
+                 const half8* __restrict__ w1a, const half8* __restrict__ w1b,
+                 float* __restrict__ part, HeadDrop dr) {
   __shared__ __attribute__((aligned(16))) _Float16 xs[2][2][kHRows * kHRowH];   // [buf][hi, lo]
   const int b = blockIdx.x, xcd = b & 7;
   const int kp = xcd >> 1;                        // the K quarter
@@ -783,18 +786,31 @@ head_lin1_x3_kernel(int n, int n0, int ldp, int tiles, const float* __restrict__
   const int srow = tid / kHChunks, schunk = tid - srow * kHChunks;
   const int grow = ht.rbeg + srow;                 // the global sample row
   const bool rvalid = stager && grow < ht.rend;
-  const float4* xsrc = reinterpret_cast<const float4*>(
-      x + (size_t)(rvalid ? grow : ht.rbeg) * kHK + 16 * kHPartSteps * kp + 8 * schunk);
-  float4 xq[2];
+  const size_t xoff = (size_t)(rvalid ? grow : ht.rbeg) * kHK + 16 * kHPartSteps * kp + 8 * schunk;
+  float4 xq[2];   // kX3: 8 floats; fp16: 8 halves in xq[0]
   auto stage_load = [&](int g) __attribute__((always_inline)) {
-    if (stager) {
+    if (!stager) return;
+    if constexpr (kX3) {
+      const float4* xsrc = reinterpret_cast<const float4*>(static_cast<const float*>(xv) + xoff);
       xq[0] = xsrc[(kHStageK / 4) * g];
       xq[1] = xsrc[(kHStageK / 4) * g + 1];
+    } else {
+      const float4* xsrc =
+          reinterpret_cast<const float4*>(static_cast<const _Float16*>(xv) + xoff);
+      xq[0] = xsrc[(kHStageK / 8) * g];
     }
   };
   auto stage_store = [&](int g, int buf) __attribute__((always_inline)) {
     if (!stager) return;
-    float v[8] = {xq[0].x, xq[0].y, xq[0].z, xq[0].w, xq[1].x, xq[1].y, xq[1].z, xq[1].w};
+    float v[8];
+    if constexpr (kX3) {
+      v[0] = xq[0].x, v[1] = xq[0].y, v[2] = xq[0].z, v[3] = xq[0].w;
+      v[4] = xq[1].x, v[5] = xq[1].y, v[6] = xq[1].z, v[7] = xq[1].w;
+    } else {
+      const half8 hv = __builtin_bit_cast(half8, xq[0]);
+#pragma unroll
+      for (int j = 0; j < 8; ++j) v[j] = (float)hv[j];
+    }
     if (dr.p > 0.0f) {
       // one hash a pair of elements, 16 bits each: u = h16 / 2^16
       const uint32_t k0 = 16 * kHPartSteps * kp + kHStageK * g + 8 * schunk;
@@ -809,12 +825,19 @@ head_lin1_x3_kernel(int n, int n0, int ldp, int tiles, const float* __restrict__
         v[j + 1] = u1 >= dr.p ? v[j + 1] * dr.scale : 0.0f;
       }
     }
-    uint32_t hi[4], lo[4];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) split2(v[2 * e], v[2 * e + 1], hi[e], lo[e]);
     const int at = srow * kHRowH + 8 * schunk;
-    *reinterpret_cast<u32x4*>(&xs[buf][0][at]) = u32x4{hi[0], hi[1], hi[2], hi[3]};
-    *reinterpret_cast<u32x4*>(&xs[buf][1][at]) = u32x4{lo[0], lo[1], lo[2], lo[3]};
+    if constexpr (kX3) {
+      uint32_t hi[4], lo[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) split2(v[2 * e], v[2 * e + 1], hi[e], lo[e]);
+      *reinterpret_cast<u32x4*>(&xs[buf][0][at]) = u32x4{hi[0], hi[1], hi[2], hi[3]};
+      *reinterpret_cast<u32x4*>(&xs[buf][1][at]) = u32x4{lo[0], lo[1], lo[2], lo[3]};
+    } else {
+      half8 hv;
+#pragma unroll
+      for (int j = 0; j < 8; ++j) hv[j] = (_Float16)v[j];
+      *reinterpret_cast<half8*>(&xs[buf][0][at]) = hv;
+    }
   };
   // w1 fragments: [2 (hi, lo)][16 feature tiles][252 k steps][64 lanes]
   constexpr int kHalfFrag = 16 * kHSteps * 64;
@@ -834,7 +857,7 @@ head_lin1_x3_kernel(int n, int n0, int ldp, int tiles, const float* __restrict__
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       ah[bb][c] = wt[c][s * 64];
-      al[bb][c] = wt[c][kHalfFrag + s * 64];
+      if constexpr (kX3) al[bb][c] = wt[c][kHalfFrag + s * 64];
     }
   };
   // step ss of stage buffer `buf` on weight buffer bb: B = the staged rows
@@ -844,12 +867,16 @@ head_lin1_x3_kernel(int n, int n0, int ldp, int tiles, const float* __restrict__
     for (int st = 0; st < 2; ++st) {
       const int at = (32 * st + col) * kHRowH + 16 * ss + 8 * h;
       const half8 xh = *reinterpret_cast<const half8*>(&xs[buf][0][at]);
-      const half8 xl = *reinterpret_cast<const half8*>(&xs[buf][1][at]);
 #pragma unroll
-      for (int c = 0; c < 2; ++c) {
+      for (int c = 0; c < 2; ++c)
         acc0[c][st] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[bb][c], xh, acc0[c][st], 0, 0, 0);
-        acc1[c][st] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[bb][c], xl, acc1[c][st], 0, 0, 0);
-        acc1[c][st] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[bb][c], xh, acc1[c][st], 0, 0, 0);
+      if constexpr (kX3) {
+        const half8 xl = *reinterpret_cast<const half8*>(&xs[buf][1][at]);
+#pragma unroll
+        for (int c = 0; c < 2; ++c) {
+          acc1[c][st] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[bb][c], xl, acc1[c][st], 0, 0, 0);
+          acc1[c][st] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[bb][c], xh, acc1[c][st], 0, 0, 0);
+        }
       }
     }
   };
@@ -880,7 +907,7 @@ head_lin1_x3_kernel(int n, int n0, int ldp, int tiles, const float* __restrict__
 #pragma unroll
         for (int r = 0; r < 16; ++r) {
           const int f = 32 * (2 * wave + c) + (r & 3) + 8 * (r >> 2) + 4 * h;
-          pp[(size_t)f * ldp + row] = acc0[c][st][r] + acc1[c][st][r] * kLoInv;
+          pp[(size_t)f * ldp + row] = kX3 ? acc0[c][st][r] + acc1[c][st][r] * kLoInv : acc0[c][st][r];
         }
     }
 }
@@ -889,11 +916,13 @@ head_lin1_x3_kernel(int n, int n0, int ldp, int tiles, const float* __restrict__
 // so a load is 16 consecutive floats of one feature); lane g of a row sums
 // features g, g + 16, ... (32), the 16 partial dot products of a row reduced
 // in LDS in a fixed order
+// T: the head's parameters as the actor keeps them (f32, or fp16 in fast mode)
+template <typename T>
 __global__ void __launch_bounds__(256)
 head_finish_kernel(int n, int n0, int ldp, const float* __restrict__ part,
-                   const float* __restrict__ b1a, const float* __restrict__ w2a,
-                   const float* __restrict__ b2a, const float* __restrict__ b1b,
-                   const float* __restrict__ w2b, const float* __restrict__ b2b, int head,
+                   const T* __restrict__ b1a, const T* __restrict__ w2a,
+                   const T* __restrict__ b2a, const T* __restrict__ b1b,
+                   const T* __restrict__ w2b, const T* __restrict__ b2b, int head,
                    float slope, float* __restrict__ out) {
   __shared__ float red[16][16][2];
   const int tid = threadIdx.x, g = tid >> 4, rr = tid & 15;
@@ -901,17 +930,17 @@ head_finish_kernel(int n, int n0, int ldp, const float* __restrict__ part,
   const bool valid = row < n;
   const int rc = valid ? row : 0;
   const bool set2 = rc >= n0;
-  const float* __restrict__ b1 = set2 ? b1b : b1a;
-  const float* __restrict__ w2 = set2 ? w2b : w2a;
+  const T* __restrict__ b1 = set2 ? b1b : b1a;
+  const T* __restrict__ w2 = set2 ? w2b : w2a;
   float p0 = 0.0f, p1 = 0.0f;
 #pragma unroll 4
   for (int f = g; f < kHFeat; f += 16) {
     float a = 0.0f;
 #pragma unroll
     for (int k = 0; k < kHParts; ++k) a += part[((size_t)k * kHFeat + f) * ldp + rc];
-    const float v = lrelu2(a + b1[f], slope);
-    p0 = fmaf(v, w2[f], p0);
-    p1 = fmaf(v, w2[kHFeat + f], p1);
+    const float v = lrelu2(a + (float)b1[f], slope);
+    p0 = fmaf(v, (float)w2[f], p0);
+    p1 = fmaf(v, (float)w2[kHFeat + f], p1);
   }
   red[rr][g][0] = p0;
   red[rr][g][1] = p1;
@@ -920,8 +949,8 @@ head_finish_kernel(int n, int n0, int ldp, const float* __restrict__ part,
     const int r2 = tid >> 1, j = tid & 1;
     const int orow = 16 * blockIdx.x + r2;
     if (orow < n) {
-      const float* __restrict__ b2 = orow >= n0 ? b2b : b2a;
-      float a = b2[j];
+      const T* __restrict__ b2 = orow >= n0 ? b2b : b2a;
+      float a = (float)b2[j];
 #pragma unroll
       for (int q = 0; q < 16; ++q) a += red[r2][q][j];
       out[(size_t)orow * 2 + j] = head_act(a, head);
@@ -968,12 +997,12 @@ extern "C" int64_t dt_actor_head_x3_work_floats(int32_t n) {
   return n < 0 ? -1 : (int64_t)kHParts * kHFeat * n;
 }
 
-extern "C" int dt_actor_head_x3_drop(int32_t n, int32_t n0, int32_t k, const float* x,
-                                     float p, uint32_t seed, const void* w1a, const float* b1a,
-                                     const float* w2a, const float* b2a, const void* w1b,
-                                     const float* b1b, const float* w2b, const float* b2b,
-                                     int32_t head, float slope, float* work, float* out,
-                                     void* stream) {
+namespace {
+template <bool kX3, typename T>
+int head_launch(int32_t n, int32_t n0, int32_t k, const void* x, float p, uint32_t seed,
+                const void* w1a, const T* b1a, const T* w2a, const T* b2a, const void* w1b,
+                const T* b1b, const T* w2b, const T* b2b, int32_t head, float slope, float* work,
+                float* out, void* stream) {
   if (!x || !w1a || !b1a || !w2a || !b2a || !work || !out || n < 0 || n0 < 0 || n0 > n ||
       k != kHK || head < 0 || head > 2 || !(p >= 0.0f && p < 1.0f))
     return DT_E_ARG;
@@ -983,12 +1012,35 @@ extern "C" int dt_actor_head_x3_drop(int32_t n, int32_t n0, int32_t k, const flo
   const int tiles = (n0 + kHRows - 1) / kHRows + (n - n0 + kHRows - 1) / kHRows;
   const int blocks = 8 * ((tiles + 1) / 2);   // two tiles of each quarter an 8-block round
   const HeadDrop dr{p, p > 0.0f ? 1.0f / (1.0f - p) : 1.0f, seed};
-  hipLaunchKernelGGL(head_lin1_x3_kernel, dim3(blocks), dim3(64 * kHWaves), 0, s, n, n0, n, tiles,
-                     x, (const half8*)w1a, (const half8*)(w1b ? w1b : w1a), work, dr);
-  hipLaunchKernelGGL(head_finish_kernel, dim3((n + 15) / 16), dim3(256), 0, s, n, n0, n,
+  hipLaunchKernelGGL(head_lin1_kernel<kX3>, dim3(blocks), dim3(64 * kHWaves), 0, s, n, n0, n,
+                     tiles, x, (const half8*)w1a, (const half8*)(w1b ? w1b : w1a), work, dr);
+  hipLaunchKernelGGL(head_finish_kernel<T>, dim3((n + 15) / 16), dim3(256), 0, s, n, n0, n,
                      work, b1a, w2a, b2a, b1b ? b1b : b1a, w2b ? w2b : w2a, b2b ? b2b : b2a,
                      head, slope, out);
   return hipGetLastError() == hipSuccess ? DT_OK : DT_E_HIP;
+}
+}  // namespace
+
+extern "C" int dt_actor_head_x3_drop(int32_t n, int32_t n0, int32_t k, const float* x,
+                                     float p, uint32_t seed, const void* w1a, const float* b1a,
+                                     const float* w2a, const float* b2a, const void* w1b,
+                                     const float* b1b, const float* w2b, const float* b2b,
+                                     int32_t head, float slope, float* work, float* out,
+                                     void* stream) {
+  return head_launch<true, float>(n, n0, k, x, p, seed, w1a, b1a, w2a, b2a, w1b, b1b, w2b, b2b,
+                                  head, slope, work, out, stream);
+}
+
+extern "C" int dt_actor_head_f16_drop(int32_t n, int32_t n0, int32_t k, const void* x, float p,
+                                      uint32_t seed, const void* w1a, const void* b1a,
+                                      const void* w2a, const void* b2a, const void* w1b,
+                                      const void* b1b, const void* w2b, const void* b2b,
+                                      int32_t head, float slope, float* work, float* out,
+                                      void* stream) {
+  using H = _Float16;
+  return head_launch<false, H>(n, n0, k, x, p, seed, w1a, (const H*)b1a, (const H*)w2a,
+                               (const H*)b2a, w1b, (const H*)b1b, (const H*)w2b, (const H*)b2b,
+                               head, slope, work, out, stream);
 }
 
 extern "C" int dt_actor_head_x3(int32_t n, int32_t n0, int32_t k, const float* x,

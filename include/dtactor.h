@@ -193,6 +193,17 @@ int dt_actor_head_x3_drop(int32_t n, int32_t n0, int32_t k, const float* x, floa
                           const float* b2a, const void* w1b, const float* b1b, const float* w2b,
                           const float* b2b, int32_t head, float slope, float* work, float* out,
                           void* stream);
+/* The fp16 fast mode's head in the same two launches (ABI 13): x device fp16
+ * [n, k]; w1* the hi half of dt_actor_head_x3's fragment layout ([16, 252,
+ * 64, 8] fp16 from the fp16 lin1 weights); b1*, w2*, b2* device fp16; one
+ * fp16 MFMA a product with f32 accumulation, the same folded dropout; the
+ * lin1 output kept in f32 (the library-GEMM path it replaces rounded it to
+ * fp16).  work: dt_actor_head_x3_work_floats(n). */
+int dt_actor_head_f16_drop(int32_t n, int32_t n0, int32_t k, const void* x, float p,
+                           uint32_t seed, const void* w1a, const void* b1a, const void* w2a,
+                           const void* b2a, const void* w1b, const void* b1b, const void* w2b,
+                           const void* b2b, int32_t head, float slope, float* work, float* out,
+                           void* stream);
 
 /* dt_explore: SingleThreadExplorer's action choice for n explorers at once,
  * one fused pass replacing the torch restatement's ~25 element-wise kernels

@@ -55,7 +55,8 @@ extern "C" {
                                 (the float32-accurate convolutions);
                             12: dtupd.h dt_upd_linear_fwd_drop / _dgrad_drop
                                 (dropout folded into the linears);
-                            13: dtactor.h dt_actor_head_x3_drop */
+                            13: dtactor.h dt_actor_head_x3_drop,
+                                dt_actor_head_f16_drop */
 
 /* error codes */
 #define DT_OK 0

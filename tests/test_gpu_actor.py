@@ -351,11 +351,14 @@ def test_index_ring_equals_grey_ring(gpu, mode, n, n0, slots, order):
                            fa._convs_pair(fb, grey, order, n0))
 
 
-@pytest.mark.parametrize('n,n0', [(300, 300), (300, 257), (64, 1)])
-def test_fused_head_matches_torch_head(gpu, n, n0):
-    """dt_actor_head (LeakyReLU -> lin2 -> tanh in one launch over both weight
-    sets) against FusedActor._head (torch ops, hipBLASLt lin2) on the same
-    lin1 inputs: within the fp16 rounding of the pre-tanh value (1e-3)."""
+@pytest.mark.parametrize('n,n0', [(300, 300), (300, 257), (64, 1), (4096, 3584)])
+def test_fused_head_matches_float64(gpu, n, n0):
+    """The fast mode's head (dt_actor_head_f16_drop: lin1 on fp16 MFMA with
+    f32 accumulation, LeakyReLU, lin2, tanh for both weight sets in one
+    launch pair) against float64 of the same fp16 operands (its lin1 weights,
+    biases and inputs): the products are exact, the sums f32 (2e-6); and
+    against FusedActor._head's torch fp16 ops, which round lin1's output and
+    the pre-tanh value to fp16 (2e-3)."""
     from aido1_amd.actor import FLAT, ConfigActor, FusedActor
     from test_trainer import no_dropout
     cfg = golden('reference_config.json')['model']['actor']
@@ -366,9 +369,38 @@ def test_fused_head_matches_torch_head(gpu, n, n0):
     flat = (torch.randn(n, FLAT, device=gpu) * 0.5).half()
     out = torch.full((n, 2), float('nan'), device=gpu)
     fa._heads(fb, flat, n0, out)
-    ref = torch.cat([fa._head(flat[:n0]), fb._head(flat[n0:])])
     assert torch.isfinite(out).all()
-    assert torch.allclose(out, ref, rtol=0, atol=1e-3), (out - ref).abs().max()
+    want = []
+    for a, sl in ((fa, slice(0, n0)), (fb, slice(n0, n))):
+        h = torch.nn.functional.leaky_relu(flat[sl].double() @ a.w1.double().t() + a.b1.double())
+        want.append(torch.tanh(h @ a.w2.double().t() + a.b2.double()))
+    want = torch.cat(want)
+    assert (out.double() - want).abs().max().item() < 2e-6
+    ref = torch.cat([fa._head(flat[:n0]), fb._head(flat[n0:])])
+    assert torch.allclose(out, ref, rtol=0, atol=2e-3), (out - ref).abs().max()
+
+
+def test_fused_head_dropout_keeps_the_rate(gpu):
+    """Reference mode's dropout folded into the fast-mode head: two calls use
+    fresh masks (different outputs), and each differs from the no-dropout
+    output (the same folded hash as dt_actor_head_x3_drop, whose mask
+    tests/test_gpu_actor_x3.py restates bit for bit)."""
+    from aido1_amd.actor import FLAT, ConfigActor, FusedActor
+    cfg = golden('reference_config.json')['model']['actor']
+    torch.manual_seed(3)
+    fa = FusedActor(ConfigActor(cfg).to(gpu), dtype=torch.float16, mode='reference')
+    assert fa.p_drop == 0.5 and hasattr(fa, 'w1f')
+    flat = (torch.randn(256, FLAT, device=gpu) * 0.5).half()
+    outs = []
+    for _ in range(2):
+        out = torch.empty(256, 2, device=gpu)
+        fa._heads(None, flat, 256, out)
+        outs.append(out)
+    fa.p_drop = 0.0
+    plain = torch.empty(256, 2, device=gpu)
+    fa._heads(None, flat, 256, plain)
+    assert not torch.equal(outs[0], outs[1])
+    assert not torch.equal(outs[0], plain)
 
 
 @pytest.mark.parametrize('channels_last', [False, True])
