@@ -8,7 +8,12 @@ run() {
   env "$@" UPDATES=50 timeout -k 10 120 python -u tools/update_only.py > gpurun_out/genv_$tag.txt 2>&1 \
     || { echo "$tag failed"; tail -5 gpurun_out/genv_$tag.txt; return 1; }
   echo "$tag $(grep 'back to back, 5' gpurun_out/genv_$tag.txt)"
+  echo "$tag $(grep 'host time' gpurun_out/genv_$tag.txt)"
 }
+if [ $# -gt 0 ]; then
+  for kv in "$@"; do run "${kv%%=*}" "$kv"; done
+  exit 0
+fi
 run default X=1
 run batch256 DEBUG_HIP_GRAPH_BATCH_SIZE=256
 run batch8 DEBUG_HIP_GRAPH_BATCH_SIZE=8

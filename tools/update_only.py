@@ -5,6 +5,7 @@ Prints the median update time over the timed updates."""
 import json
 import os
 import sys
+import time
 
 import numpy as np
 import torch
@@ -23,6 +24,9 @@ def main():
     dev = torch.device('cuda', 0)
     tr = DDPGTrainer(cfg, ConfigActor(cfg['model']['actor']), ConfigCritic(cfg['model']['critic']),
                      device=dev, graph=True)
+    for kv in filter(None, os.environ.get('TR_SET', '').split(',')):   # attr=0/1 on the trainer
+        k, v = kv.split('=')
+        setattr(tr, k, bool(int(v)))
     b = 64
     g = torch.Generator(device=dev).manual_seed(1)
     batch = (torch.rand(b, 3, 120, 160, device=dev, generator=g),
@@ -68,17 +72,21 @@ def main():
     t_prep = timed(tr.update_prepared)
     # back to back, as the training loop issues them (the host runs ahead of
     # the GPU, so its launch latency is hidden): mean over n_up updates
-    b2b = []
+    b2b, host = [], []
     for _ in range(5):
         a, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         a.record()
+        h0 = time.perf_counter()
         for _ in range(n_up):
             tr.update_prepared()
+        host.append((time.perf_counter() - h0) * 1e3 / n_up)
         e.record()
         torch.cuda.synchronize()
         b2b.append(a.elapsed_time(e) / n_up)
     t_b2b = float(np.median(b2b))
     print('back to back, 5 runs of %d: %s ms' % (n_up, ' '.join('%.3f' % v for v in b2b)))
+    print('host time a call (graph replay enqueue), same runs: %s ms'
+          % ' '.join('%.3f' % v for v in host))
     tr.check()
     print('update %.3f ms with the input conversion + copies, %.3f ms on prepared inputs '
           '(medians of %d, each synchronised); %.3f ms back to back (median of 5 means of %d, '
