@@ -512,7 +512,10 @@ bn_finish_kernel(int64_t m, int hw, const float* __restrict__ z, DtUpdBn b, floa
 // tile, each a slice of K, summed through LDS (the small layers: more waves
 // than tiles).
 constexpr int kFwdThreads = 1024;
-constexpr int kFwdAllLoads = 8;     // slices of up to this many k-steps load all A first
+#ifndef DTUPD_ALL_LOADS
+#define DTUPD_ALL_LOADS 8
+#endif
+constexpr int kFwdAllLoads = DTUPD_ALL_LOADS;   // slices of up to this many k-steps load all A first
 
 
 // STATS: 0 none, 1 merged by the last workgroup (dt_upd_conv_fwd_bn), 2

@@ -16,7 +16,10 @@ SKIPS = {'full': 0, 'no_a_loads': 1, 'no_w_stage': 2, 'no_merge': 4, 'no_ksum': 
 # other variants: extra -D flags (the f32 MFMA forward, forward K slices)
 EXTRA = {'f32': ['-DDTUPD_X3=0'], 'wg_nodb': ['-DDTUPD_WG_DB=0'], 'wg_db1': ['-DDTUPD_WG_DB1=1'], 'f32_bare': ['-DDTUPD_X3=0', '-DDTUPD_SKIP=15'],
          'ks_4_4_4_8': ['-DDTUPD_KS1=4', '-DDTUPD_KS2=4', '-DDTUPD_KS3=4', '-DDTUPD_KS4=8'],
-         'ks_1_1_2_4': ['-DDTUPD_KS1=1', '-DDTUPD_KS2=1', '-DDTUPD_KS3=2', '-DDTUPD_KS4=4']}
+         'ks_1_1_2_4': ['-DDTUPD_KS1=1', '-DDTUPD_KS2=1', '-DDTUPD_KS3=2', '-DDTUPD_KS4=4'],
+         'all12': ['-DDTUPD_ALL_LOADS=12'],
+         'all16_ks2_4': ['-DDTUPD_ALL_LOADS=16', '-DDTUPD_KS2=4'],
+         'all32': ['-DDTUPD_ALL_LOADS=32']}
 LAYERS = {1: (3, 8, 2, 120, 160), 2: (32, 4, 2, 57, 77), 3: (32, 4, 2, 27, 37),
           4: (32, 4, 1, 12, 17)}
 
