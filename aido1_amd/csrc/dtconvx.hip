@@ -764,6 +764,20 @@ constexpr int kHRowH = kHStageK + 8;               // halves a staged row (112 B
 constexpr int kHChunks = kHStageK / 8;             // 8-k chunks a row
 static_assert(kHPartSteps % kHStage == 0, "whole stages");
 static_assert(kHRows * kHChunks <= 64 * kHWaves, "a chunk a thread");
+// lin1's weight fragments are loaded kHWpf k steps ahead of their MFMAs into
+// kHNB register buffers, step s in buffer s % kHNB (static: the stage loop
+// runs two stages an iteration).  x3 holds hi and lo fragments: 3 buffers.
+#ifndef DTHEAD_WPF
+#define DTHEAD_WPF 2
+#endif
+#ifndef DTHEAD_WPF16
+#define DTHEAD_WPF16 5
+#endif
+template <bool kX3> struct HeadPf {
+  static constexpr int kNB = kX3 ? kHStage : 2 * kHStage;
+  static constexpr int kWpf = kX3 ? DTHEAD_WPF : DTHEAD_WPF16;
+  static_assert(kWpf >= 1 && kWpf < kNB, "a free buffer per step in flight");
+};
 
 // kX3: x f32, its products as three fp16 MFMAs on (hi, lo) pairs; else the
 // fp16 fast mode: x fp16, one MFMA a product (the fragments' hi half only)
@@ -852,12 +866,13 @@ head_lin1_kernel(int n, int n0, int ldp, int tiles, const void* __restrict__ xv,
     for (int st = 0; st < 2; ++st)
 #pragma unroll
       for (int r = 0; r < 16; ++r) acc0[c][st][r] = acc1[c][st][r] = 0.0f;
-  half8 ah[kHStage][2], al[kHStage][2];   // [buffer = step in stage][feature tile]
+  constexpr int kNB = HeadPf<kX3>::kNB, kWpf = HeadPf<kX3>::kWpf;
+  half8 ah[kNB][2], al[kX3 ? kNB : 1][2];   // [buffer = step % kNB][feature tile]
   auto wload = [&](int bb, int s) __attribute__((always_inline)) {
 #pragma unroll
     for (int c = 0; c < 2; ++c) {
       ah[bb][c] = wt[c][s * 64];
-      if constexpr (kX3) al[bb][c] = wt[c][kHalfFrag + s * 64];
+      if constexpr (kX3) al[kX3 ? bb : 0][c] = wt[c][kHalfFrag + s * 64];
     }
   };
   // step ss of stage buffer `buf` on weight buffer bb: B = the staged rows
@@ -875,27 +890,36 @@ head_lin1_kernel(int n, int n0, int ldp, int tiles, const void* __restrict__ xv,
 #pragma unroll
         for (int c = 0; c < 2; ++c) {
           acc1[c][st] = __builtin_amdgcn_mfma_f32_32x32x16_f16(ah[bb][c], xl, acc1[c][st], 0, 0, 0);
-          acc1[c][st] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[bb][c], xh, acc1[c][st], 0, 0, 0);
+          acc1[c][st] = __builtin_amdgcn_mfma_f32_32x32x16_f16(al[kX3 ? bb : 0][c], xh, acc1[c][st], 0, 0, 0);
         }
       }
     }
   };
   stage_load(0);
-  wload(0, 0);
+#pragma unroll
+  for (int s = 0; s < kWpf; ++s) wload(s % kNB, s);
   stage_store(0, 0);
   __syncthreads();
-  for (int g = 0; g < kHStages; ++g) {
-    const int buf = g & 1;
+  // stage g (parity PAR: g & 1, so step s = 3 g + ss sits in buffer
+  // (3 PAR + ss) % kNB, known at compile time)
+  auto stage = [&](int g, auto par) __attribute__((always_inline)) {
+    constexpr int PAR = decltype(par)::value;
     if (g + 1 < kHStages) stage_load(g + 1);      // in flight during this stage's MFMAs
 #pragma unroll
     for (int ss = 0; ss < kHStage; ++ss) {
       const int s = kHStage * g + ss;              // the quarter's k step
-      if (s + 1 < kHPartSteps) wload((ss + 1) % kHStage, s + 1);
-      step(buf, ss, ss);
+      if (s + kWpf < kHPartSteps) wload((kHStage * PAR + ss + kWpf) % kNB, s + kWpf);
+      step(PAR, ss, (kHStage * PAR + ss) % kNB);
     }
-    if (g + 1 < kHStages) stage_store(g + 1, buf ^ 1);
+    if (g + 1 < kHStages) stage_store(g + 1, PAR ^ 1);
     __syncthreads();
+  };
+  int g = 0;
+  for (; g + 1 < kHStages; g += 2) {
+    stage(g, std::integral_constant<int, 0>{});
+    stage(g + 1, std::integral_constant<int, 1>{});
   }
+  if (g < kHStages) stage(g, std::integral_constant<int, 0>{});
   // partial sums [part][feature][row]: lanes of a half-wave are 32 consecutive rows
   float* pp = part + (size_t)kp * kHFeat * ldp;
 #pragma unroll
