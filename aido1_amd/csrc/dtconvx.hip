@@ -37,6 +37,7 @@
 
 #include <cstdint>
 #include <type_traits>
+#include <utility>
 
 #include "../../include/dtactor.h"
 #include "dtconv_common.h"
@@ -764,20 +765,27 @@ constexpr int kHRowH = kHStageK + 8;               // halves a staged row (112 B
 constexpr int kHChunks = kHStageK / 8;             // 8-k chunks a row
 static_assert(kHPartSteps % kHStage == 0, "whole stages");
 static_assert(kHRows * kHChunks <= 64 * kHWaves, "a chunk a thread");
-// lin1's weight fragments are loaded kHWpf k steps ahead of their MFMAs into
-// kHNB register buffers, step s in buffer s % kHNB (static: the stage loop
-// runs two stages an iteration).  x3 holds hi and lo fragments: 3 buffers.
-#ifndef DTHEAD_WPF
-#define DTHEAD_WPF 2
+// lin1's weight fragments are loaded kNB - 1 k steps ahead of their MFMAs
+// into kNB register buffers, step s in buffer s % kNB; the stage loop runs
+// kU stages an iteration so that index is a compile-time constant.  x3 holds
+// hi and lo fragments (16 registers a buffer): 4 buffers fit its 256.
+#ifndef DTHEAD_NB
+#define DTHEAD_NB 4
 #endif
-#ifndef DTHEAD_WPF16
-#define DTHEAD_WPF16 5
+#ifndef DTHEAD_NB16
+#define DTHEAD_NB16 6
 #endif
+__host__ __device__ constexpr int head_gcd(int a, int b) { return b ? head_gcd(b, a % b) : a; }
 template <bool kX3> struct HeadPf {
-  static constexpr int kNB = kX3 ? kHStage : 2 * kHStage;
-  static constexpr int kWpf = kX3 ? DTHEAD_WPF : DTHEAD_WPF16;
-  static_assert(kWpf >= 1 && kWpf < kNB, "a free buffer per step in flight");
+  static constexpr int kNB = kX3 ? DTHEAD_NB : DTHEAD_NB16;
+  static constexpr int kWpf = kNB - 1;
+  static constexpr int kU = kNB / head_gcd(kNB, kHStage);   // stages an iteration
+  static_assert(kNB >= 2 && kNB <= 12, "register buffers");
 };
+template <typename F, int... J>
+__device__ __forceinline__ void head_stages(F&& f, int g, std::integer_sequence<int, J...>) {
+  (f(g + J, std::integral_constant<int, J>{}), ...);
+}
 
 // kX3: x f32, its products as three fp16 MFMAs on (hi, lo) pairs; else the
 // fp16 fast mode: x fp16, one MFMA a product (the fragments' hi half only)
@@ -900,8 +908,10 @@ head_lin1_kernel(int n, int n0, int ldp, int tiles, const void* __restrict__ xv,
   for (int s = 0; s < kWpf; ++s) wload(s % kNB, s);
   stage_store(0, 0);
   __syncthreads();
-  // stage g (parity PAR: g & 1, so step s = 3 g + ss sits in buffer
-  // (3 PAR + ss) % kNB, known at compile time)
+  // stage g = kU i + PAR: step s = 3 g + ss sits in register buffer
+  // (3 PAR + ss) % kNB (kU stages are a multiple of kNB steps), its rows in
+  // LDS buffer g & 1
+  constexpr int kU = HeadPf<kX3>::kU;
   auto stage = [&](int g, auto par) __attribute__((always_inline)) {
     constexpr int PAR = decltype(par)::value;
     if (g + 1 < kHStages) stage_load(g + 1);      // in flight during this stage's MFMAs
@@ -909,17 +919,14 @@ head_lin1_kernel(int n, int n0, int ldp, int tiles, const void* __restrict__ xv,
     for (int ss = 0; ss < kHStage; ++ss) {
       const int s = kHStage * g + ss;              // the quarter's k step
       if (s + kWpf < kHPartSteps) wload((kHStage * PAR + ss + kWpf) % kNB, s + kWpf);
-      step(PAR, ss, (kHStage * PAR + ss) % kNB);
+      step(g & 1, ss, (kHStage * PAR + ss) % kNB);
     }
-    if (g + 1 < kHStages) stage_store(g + 1, PAR ^ 1);
+    if (g + 1 < kHStages) stage_store(g + 1, (g & 1) ^ 1);
     __syncthreads();
   };
   int g = 0;
-  for (; g + 1 < kHStages; g += 2) {
-    stage(g, std::integral_constant<int, 0>{});
-    stage(g + 1, std::integral_constant<int, 1>{});
-  }
-  if (g < kHStages) stage(g, std::integral_constant<int, 0>{});
+  for (; g + kU <= kHStages; g += kU) head_stages(stage, g, std::make_integer_sequence<int, kU>{});
+  head_stages(stage, g, std::make_integer_sequence<int, kHStages % kU>{});
   // partial sums [part][feature][row]: lanes of a half-wave are 32 consecutive rows
   float* pp = part + (size_t)kp * kHFeat * ldp;
 #pragma unroll
